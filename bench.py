@@ -1,0 +1,184 @@
+#!/usr/bin/env python
+"""bench.py — MI355X in-loop-filter hot path throughput (BASELINE.json metric).
+
+A "step" = one 4K 10-bit 4:2:0 frame through the device-resident CDEF pipeline of the reference's
+CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
+strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
+(svt_av1_cdef_frame).  Inputs are synthetic and resident in HBM before timing.
+
+N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the frame is tiled into
+bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and skip flags
+are all-reduce-summed over RCCL (zeros outside each band), every rank runs the (replicated,
+deterministic) pick and applies its band — strong scaling of one frame per step.
+
+Prints ONE JSON line on rank 0 (contract in the task description): value = luma Mpixels/s of the
+whole job, plus `roofline` for the dominant kernel (timed with HIP events on the stream it runs
+on) and `cpu_baseline` (the repo's C restatement on this host, rank 0, N = 1, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
+
+import svtgpu  # noqa: E402
+import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--bit-depth", type=int, default=10)
+    ap.add_argument("--cdef-level", type=int, default=1)
+    ap.add_argument("--base-q-idx", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
+    return ap.parse_args()
+
+
+def cpu_baseline(src, rec, bd, level, q, lam, sample):
+    """The repo's scalar C restatement (oracle/) on one host core over a crop of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: used here only as the reported CPU baseline
+    sw, sh = (int(x) for x in sample.split("x"))
+    crop = [rec[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in rec[1:]]
+    cs = [src[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in src[1:]]
+    crop = [np.ascontiguousarray(a) for a in crop]
+    cs = [np.ascontiguousarray(a) for a in cs]
+    ctrls = oracle.controls(level)
+    t0 = time.perf_counter()
+    mse, skip, d, v = oracle.cdef_search_frame(crop, cs, bd, ctrls, q)
+    prm, fbs = oracle.cdef_pick(sw, sh, mse, skip, ctrls, q, lam)
+    oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
+    dt = time.perf_counter() - t0
+    return {"value": round(sw * sh / dt / 1e6, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": "%dx%d crop of the same %d-bit frame, CDEF search+pick+apply, cdef_level %d, scalar C "
+                      "restatement (oracle/cdef_oracle.c), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n = world
+    W, H, bd = a.width, a.height, a.bit_depth
+    q, lam = a.base_q_idx, 60000
+
+    ctx = svtgpu.Context(local)
+    # a non-default torch stream: the library launches on it, torch events time it, RCCL orders on it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    src, rec = synth.frame_pair(W, H, bd, seed=0x5EED0003)
+    R, S, O = (svtgpu.Frame(ctx, W, H, bd) for _ in range(3))
+    R.upload(rec, sp)
+    S.upload(src, sp)
+    ctrls = svtgpu.cdef_controls(a.cdef_level)
+    st = svtgpu.CdefState(ctx, W, H)
+    nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
+    if n > 1:
+        rows = np.linspace(0, nvfb, n + 1).round().astype(int)
+        st.set_fb_rows(int(rows[rank]), int(rows[rank + 1]))
+        mse_t = torch.zeros((2, st.nfb, 64), dtype=torch.int64, device="cuda")
+        skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
+        st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+
+    ev = []  # (start, end) around the dominant kernel, on the stream it is launched on
+
+    def step(timed):
+        if n > 1:
+            st.clear_tables(sp)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        st.search(R, S, ctrls, q, sp)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if n > 1:
+            dist.all_reduce(mse_t)   # zero-padded band tables -> full frame table (RCCL over xGMI)
+            dist.all_reduce(skip_t)
+        prm, _ = st.pick(ctrls, q, lam, sp)
+        st.apply(R, O, prm, sp)
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if n > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    search_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+
+    ms_per_step = dt * 1e3 / a.steps
+    value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
+    # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
+    # recon + source read once (2*S*B) + per-FB outputs (mse 2x64 u64, dir 64 u8, var 64 i32, skip)
+    S_samples = 1.5 * W * H
+    B = 2 if bd > 8 else 1
+    nfb_band = st.nfb if n == 1 else (int(rows[rank + 1]) - int(rows[rank])) * nhfb
+    alg_bytes = 2 * S_samples * B / n + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
+    achieved = alg_bytes / (search_ms * 1e-3) / 1e9
+    evals = nfb_band * 6144 * ctrls.strengths().__len__()  # (sample, strength) filter evaluations
+    out = {
+        "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
+        "value": round(value, 3),
+        "unit": "Mpixels/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u16" if bd > 8 else "u8",
+        "data": "synthetic",
+        "config": {"workload": "cdef_search+pick+apply %dx%d %d-bit 4:2:0, cdef_level %d (%d strengths); "
+                               "DLF/LR/SAD not yet in the step" % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
+                   "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
+                   "parallelism": "fb_row_bands%d" % n if n > 1 else "single"},
+        "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": None, "avg_launch_ms": round(search_ms, 4),
+                     "note": "VALU-bound kernel (64 strengths per sample read); HBM fraction is low by "
+                             "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))},
+    }
+    if rank == 0 and n == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(src, rec, bd, a.cdef_level, q, lam, a.cpu_sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

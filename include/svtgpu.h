@@ -1,0 +1,201 @@
+/*
+ * svtgpu.h — C ABI of the MI355X (gfx950) in-loop-filter / distortion library.
+ *
+ * Drop-in boundary for SVT-AV1 v2.1.0 (reference: GabrielGao0310/SVT-av1_pro-anchor-v2.1.0-).
+ * Two layers, both plain C (no HIP or torch types in any signature):
+ *
+ *  1. RTCD-compatible per-block entry points.  Each has EXACTLY the signature of the reference's
+ *     RTCD function pointer it can be assigned to after svt_aom_setup_common_rtcd_internal /
+ *     svt_aom_setup_rtcd_internal (Source/Lib/Encoder/Globals/EbEncHandle.c:1530-1531).  They take
+ *     host pointers, run the HIP kernel on the library's default device and return the result
+ *     synchronously.  They exist for unit parity (the reference's own gtests call these pointers);
+ *     they are far too fine-grained to be fast.
+ *
+ *  2. Frame-level entry points (the real GPU boundary).  They replace the reference's C loops over
+ *     64x64 filter blocks (cdef_seg_search, finish_cdef_search, svt_av1_cdef_frame, ...) and run on
+ *     device-resident frames.  Every call takes a `void *stream` (a hipStream_t; NULL = the
+ *     context's own stream) and is asynchronous with respect to the host unless stated otherwise.
+ *
+ * Error convention: functions returning int return SVTGPU_OK (0) or a negative SVTGPU_ERR_* code;
+ * nothing throws or longjmps across this ABI.  Per-block shims cannot report errors through their
+ * reference signature; they abort() with a message if the device is missing (the encoder must not
+ * install them without a device — see svtgpu_device_available()).
+ */
+#ifndef SVTGPU_H
+#define SVTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVTGPU_OK 0
+#define SVTGPU_ERR_INVALID_ARG (-1)
+#define SVTGPU_ERR_HIP (-2)
+#define SVTGPU_ERR_UNSUPPORTED (-3)
+#define SVTGPU_ERR_NO_DEVICE (-4)
+#define SVTGPU_ERR_OOM (-5)
+
+/* Block-size codes used by the per-block CDEF shims; values equal the reference's BlockSize enum
+ * (Source/Lib/Common/Codec/EbDefinitions.h:769-772). */
+#define SVTGPU_BLOCK_4X4 0
+#define SVTGPU_BLOCK_4X8 1
+#define SVTGPU_BLOCK_8X4 2
+#define SVTGPU_BLOCK_8X8 3
+
+/* Layout-identical to the reference's CdefList (EbDefinitions.h:253-256). */
+typedef struct SvtGpuCdefList {
+    uint8_t by;
+    uint8_t bx;
+} SvtGpuCdefList;
+
+/* ---------------------------------------------------------------------------------------------
+ * Library / device
+ * ------------------------------------------------------------------------------------------- */
+/* 1 when a gfx950 device is visible and the kernels are loadable, else 0. Never aborts. */
+int         svtgpu_device_available(void);
+const char *svtgpu_version(void);
+const char *svtgpu_error_string(int code);
+
+typedef struct SvtGpuContext SvtGpuContext;
+/* One context per (process, device). Owns a HIP stream and the scratch of the frame-level calls. */
+int   svtgpu_context_create(int device, SvtGpuContext **out);
+void  svtgpu_context_destroy(SvtGpuContext *ctx);
+void *svtgpu_context_stream(SvtGpuContext *ctx); /* the context's hipStream_t */
+int   svtgpu_synchronize(SvtGpuContext *ctx, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device-resident 4:2:0 pictures
+ *   Samples are uint8 when bit_depth == 8 and uint16 when bit_depth == 10 (the reference's
+ *   "16-bit pipeline", EbEncHandle.c:4534).  width/height are luma sizes, multiples of 8.
+ *   Plane p (0=Y,1=U,2=V) is stored with stride svtgpu_frame_stride(f, p) samples and no padding
+ *   requirement on the caller side.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct SvtGpuFrame SvtGpuFrame;
+int      svtgpu_frame_create(SvtGpuContext *ctx, int32_t width, int32_t height, int32_t bit_depth,
+                             SvtGpuFrame **out);
+void     svtgpu_frame_destroy(SvtGpuFrame *f);
+int32_t  svtgpu_frame_stride(const SvtGpuFrame *f, int plane);
+void    *svtgpu_frame_plane_ptr(SvtGpuFrame *f, int plane); /* device pointer */
+/* host <-> device copies of one plane; host_stride in samples. Asynchronous on `stream` unless the
+ * host buffer is pageable (then HIP makes it synchronous). */
+int svtgpu_frame_upload(SvtGpuFrame *f, int plane, const void *host, int32_t host_stride, void *stream);
+int svtgpu_frame_download(const SvtGpuFrame *f, int plane, void *host, int32_t host_stride, void *stream);
+int svtgpu_frame_copy(SvtGpuFrame *dst, const SvtGpuFrame *src, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * CDEF — per-block RTCD shims (host pointers, synchronous)
+ * ------------------------------------------------------------------------------------------- */
+/* replaces svt_aom_cdef_find_dir (common_dsp_rtcd.h:1017); C: EbCdef.c:150 */
+uint8_t svtgpu_cdef_find_dir(const uint16_t *img, int32_t stride, int32_t *var, int32_t coeff_shift);
+/* replaces svt_aom_cdef_find_dir_dual (common_dsp_rtcd.h:1096); C: EbCdef.c:212 */
+void svtgpu_cdef_find_dir_dual(const uint16_t *img1, const uint16_t *img2, int stride, int32_t *var1,
+                               int32_t *var2, int32_t coeff_shift, uint8_t *out1, uint8_t *out2);
+/* replaces svt_cdef_filter_block (common_dsp_rtcd.h:1099); C: EbCdef.c:253.
+ * `in` points into a CDEF_BSTRIDE(=144)-stride buffer; rows -2..h+1 and cols -2..w+1 are read. */
+void svtgpu_cdef_filter_block(uint8_t *dst8, uint16_t *dst16, int32_t dstride, const uint16_t *in,
+                              int32_t pri_strength, int32_t sec_strength, int32_t dir, int32_t pri_damping,
+                              int32_t sec_damping, int32_t bsize, int32_t coeff_shift,
+                              uint8_t subsampling_factor);
+/* replaces svt_compute_cdef_dist_16bit / _8bit (aom_dsp_rtcd.h:62-64); C: EbEncCdef.c:129/175 */
+uint64_t svtgpu_compute_cdef_dist_16bit(const uint16_t *dst, int32_t dstride, const uint16_t *src,
+                                        const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                        int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+uint64_t svtgpu_compute_cdef_dist_8bit(const uint8_t *dst8, int32_t dstride, const uint8_t *src8,
+                                       const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                       int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+/* replaces svt_search_one_dual (aom_dsp_rtcd.h:239); C: EbEncCdef.c:627 */
+uint64_t svtgpu_search_one_dual(int *lev0, int *lev1, int nb_strengths, uint64_t **mse[2], int sb_count,
+                                int start_gi, int end_gi);
+
+/* ---------------------------------------------------------------------------------------------
+ * CDEF — frame level (device-resident)
+ * ------------------------------------------------------------------------------------------- */
+#define SVTGPU_CDEF_TOTAL_STRENGTHS 64
+#define SVTGPU_CDEF_MAX_STRENGTHS 16
+
+/* Subset of the reference's CdefControls (EbPictureControlSet.h:592-628) that the search and pick
+ * read.  Strength codes are pri*4 + sec (sec code 3 means strength 4), as in
+ * EncModeConfig.c:860-1330. */
+typedef struct SvtGpuCdefControls {
+    uint8_t  first_pass_fs_num;
+    uint8_t  default_second_pass_fs_num;
+    uint8_t  default_first_pass_fs[SVTGPU_CDEF_TOTAL_STRENGTHS];
+    uint8_t  default_second_pass_fs[SVTGPU_CDEF_TOTAL_STRENGTHS];
+    int8_t   default_first_pass_fs_uv[SVTGPU_CDEF_TOTAL_STRENGTHS];  /* -1 = chroma not tested */
+    int8_t   default_second_pass_fs_uv[SVTGPU_CDEF_TOTAL_STRENGTHS]; /* -1 = chroma not tested */
+    uint8_t  subsampling_factor;                                     /* 1, 2 or 4 */
+    uint16_t zero_fs_cost_bias;                                      /* 0 = off, else x/64 */
+} SvtGpuCdefControls;
+
+/* Fill `c` exactly as set_cdef_controls(cdef_level) does (EncModeConfig.c:860-1330) for the
+ * levels this library supports (1..17 minus use_reference_cdef_fs levels). Returns
+ * SVTGPU_ERR_UNSUPPORTED for level 0 or reference-fs levels. fast_decode/resolution tweaks of the
+ * zero_fs_cost_bias are applied by the caller. */
+int svtgpu_cdef_controls_for_level(int cdef_level, SvtGpuCdefControls *c);
+
+/* Frame parameters chosen by the pick; layout mirrors CdefParams (EbAv1Structs.h:359-369). */
+typedef struct SvtGpuCdefParams {
+    uint8_t cdef_damping;
+    uint8_t cdef_bits;
+    uint8_t cdef_y_strength[SVTGPU_CDEF_MAX_STRENGTHS];
+    uint8_t cdef_uv_strength[SVTGPU_CDEF_MAX_STRENGTHS];
+} SvtGpuCdefParams;
+
+/* Device-resident search state for one frame (mse_seg, skip_cdef_seg and cdef_dir_data of the
+ * reference's PictureControlSet, EbPictureControlSet.h:268-270). */
+typedef struct SvtGpuCdefFrameState SvtGpuCdefFrameState;
+int  svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuCdefFrameState **out);
+void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s);
+int32_t svtgpu_cdef_state_nfb(const SvtGpuCdefFrameState *s); /* nvfb*nhfb */
+
+/* Per-8x8 "filter this block" mask, row-major, ((h+7)/8) x ((w+7)/8) bytes; an 8x8 block is
+ * listed iff any of its four 4x4 mode-info units is non-skip (svt_sb_compute_cdef_list,
+ * EbEncCdef.c:238).  Upload once per frame; NULL mask = every block listed. */
+int svtgpu_cdef_set_block_mask(SvtGpuCdefFrameState *s, const uint8_t *host_mask, void *stream);
+
+/* ≙ all segments of cdef_seg_search (EbCdefProcess.c:114-357) for SB64 frames.
+ * recon = DLF output, source = input picture (same geometry/bit depth). */
+int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                             const SvtGpuCdefControls *ctrls, int32_t base_q_idx, void *stream);
+
+/* ≙ finish_cdef_search (EbEncCdef.c:728-926) with svt_search_one_dual on the device.
+ * lambda = full_lambda of the frame (computed by the encoder's lambda function table).
+ * Writes params and the per-FB strength index (int8 per FB, host array of nfb entries) and keeps
+ * the per-FB index on the device for svtgpu_cdef_apply_frame.  Synchronous (returns host data). */
+int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                     uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream);
+
+/* Optional override of the per-FB strength index used by apply (host array of nfb entries). */
+int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream);
+
+/* ≙ svt_av1_cdef_frame (EbEncCdef.c:284-610): apply params to `recon` (DLF output) and write the
+ * filtered picture to `out` (out-of-place; the reference's in-place result with its saved
+ * unfiltered line/column buffers is identical).  Uses dir/var of the last search. */
+int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
+                            const SvtGpuCdefParams *params, void *stream);
+
+/* Frame tiling across GPUs (BASELINE config 4): restrict search and apply to filter-block rows
+ * [fb_row_begin, fb_row_end).  Samples outside the band are still read as filter context (apron), so
+ * the picture passed in must hold valid samples for the band +-3 rows.  Default: all rows. */
+int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32_t fb_row_end);
+/* Use caller-owned device memory for the search tables: mse [2][nfb][64] uint64 and skip [nfb] uint8
+ * (e.g. buffers all-reduced with RCCL between the search and the pick).  NULL, NULL restores the
+ * state's own buffers.  svtgpu_cdef_clear_tables zeroes both (a band search then leaves zeros —
+ * the identity of an all-reduce-sum — outside its rows). */
+int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, void *skip_dev);
+int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream);
+
+/* Host views of the search results (synchronous). mse: [2][nfb][64] uint64, skip: [nfb] uint8,
+ * dir: [nfb][64] uint8 and var: [nfb][64] int32 (8x8 blocks of the FB, row-major). Any may be NULL. */
+int svtgpu_cdef_read_state(SvtGpuCdefFrameState *s, uint64_t *mse, uint8_t *skip, uint8_t *dir, int32_t *var,
+                           void *stream);
+/* Device pointer of the [2][nfb][64] uint64 mse table (for RCCL gathers across tiles). */
+void *svtgpu_cdef_mse_device_ptr(SvtGpuCdefFrameState *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVTGPU_H */

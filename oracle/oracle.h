@@ -1,0 +1,62 @@
+/*
+ * oracle.h — CPU restatement of the reference's CDEF hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code, and
+ * only as the checker / CPU baseline — never as the product path.  Each function cites the
+ * reference file:line it restates (paths relative to Source/Lib/ of
+ * GabrielGao0310/SVT-av1_pro-anchor-v2.1.0-).  Pinned against golden vectors produced by the
+ * reference's own C functions (oracle/ref.mk → tests/golden/).
+ */
+#ifndef SVTGPU_ORACLE_H
+#define SVTGPU_ORACLE_H
+#include <stdint.h>
+#include "../include/svtgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OR_CDEF_BSTRIDE 144 /* ALIGN_POWER_OF_TWO(128 + 2*8, 3), EbCdef.h:35 */
+#define OR_CDEF_VBORDER 3
+#define OR_CDEF_HBORDER 8
+#define OR_CDEF_VERY_LARGE 0x7F7F
+#define OR_CDEF_INBUF_SIZE (OR_CDEF_BSTRIDE * (128 + 2 * OR_CDEF_VBORDER))
+
+/* host-side picture view (plane pointers at the visible origin, strides in samples) */
+typedef struct OracleFrame {
+    int32_t width, height, bit_depth;
+    void   *plane[3];
+    int32_t stride[3];
+} OracleFrame;
+
+/* ---- kernel level (same signatures/semantics as the reference C functions) ---- */
+uint8_t  oracle_cdef_find_dir(const uint16_t *img, int32_t stride, int32_t *var, int32_t coeff_shift);
+void     oracle_cdef_filter_block(uint8_t *dst8, uint16_t *dst16, int32_t dstride, const uint16_t *in,
+                                  int32_t pri_strength, int32_t sec_strength, int32_t dir, int32_t pri_damping,
+                                  int32_t sec_damping, int32_t bsize, int32_t coeff_shift, uint8_t subsampling_factor);
+uint64_t oracle_compute_cdef_dist_16bit(const uint16_t *dst, int32_t dstride, const uint16_t *src,
+                                        const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                        int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+uint64_t oracle_compute_cdef_dist_8bit(const uint8_t *dst, int32_t dstride, const uint8_t *src,
+                                       const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                       int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+uint64_t oracle_search_one_dual(int *lev0, int *lev1, int nb_strengths, uint64_t **mse[2], int sb_count,
+                                int start_gi, int end_gi);
+
+/* ---- frame level ---- */
+int oracle_cdef_controls_for_level(int cdef_level, SvtGpuCdefControls *c);
+/* mse: [2][nfb][64], skip: [nfb], dir: [nfb][64], var: [nfb][64]; block_mask as in svtgpu.h (NULL=all) */
+int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
+                             const SvtGpuCdefControls *ctrls, int32_t base_q_idx, uint64_t *mse, uint8_t *skip,
+                             uint8_t *dir, int32_t *var);
+int oracle_cdef_pick(int32_t width, int32_t height, const uint64_t *mse, const uint8_t *skip,
+                     const SvtGpuCdefControls *ctrls, int32_t base_q_idx, uint64_t lambda,
+                     SvtGpuCdefParams *params, int8_t *fb_strength);
+int oracle_cdef_apply_frame(const OracleFrame *recon, OracleFrame *out, const uint8_t *block_mask,
+                            const uint8_t *dir, const int32_t *var, const SvtGpuCdefParams *params,
+                            const int8_t *fb_strength);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,41 @@
+# oracle/ref.mk — builds the REFERENCE's own C (and AVX2) hot-path sources, straight from
+# /root/reference with gcc, into oracle/_ref/ (git-ignored, shipped to the GPU box by gpurun).
+# Test infrastructure only: the golden-vector generators and the reference CPU baseline.
+# The reference's cmake build system is NOT used; only its source files are compiled directly.
+#
+#   make -f oracle/ref.mk            # from the repo root
+REF      ?= /root/reference
+OUT      ?= oracle/_ref
+S        := $(REF)/Source
+CC       ?= gcc
+INC      := -I$(S)/API -I$(S)/Lib/Common/Codec -I$(S)/Lib/Common/C_DEFAULT -I$(S)/Lib/Encoder/Codec \
+            -I$(S)/Lib/Encoder/C_DEFAULT -I$(S)/Lib/Encoder/Globals -I$(S)/Lib/Common/ASM_AVX2 \
+            -I$(S)/Lib/Encoder/ASM_AVX2 -I$(S)/Lib/Common/ASM_SSE2 -I$(S)/Lib/Common/ASM_SSE4_1 \
+            -I$(REF)/third_party/aom/inc -I$(REF)/third_party/cpuinfo/include -Ioracle/ref_harness
+CFLAGS   := -O2 -fPIC -ffunction-sections -fdata-sections -DARCH_X86_64=1 -w $(INC)
+
+# reference C sources (semantic definitions of the kernels)
+REF_C    := Lib/Common/Codec/EbCdef.c Lib/Encoder/Codec/EbEncCdef.c Lib/Common/Codec/common_dsp_rtcd.c \
+            Lib/Encoder/Codec/aom_dsp_rtcd.c Lib/Common/Codec/EbUtility.c
+# reference AVX2 sources (the CPU baseline the north star names)
+REF_AVX2 := Lib/Common/ASM_AVX2/cdef_block_avx2.c Lib/Encoder/ASM_AVX2/EbCdef_AVX2.c
+
+C_OBJ    := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_C))
+AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
+
+all: $(OUT)/gen_golden_cdef
+
+$(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
+$(OUT)/obj/%.o: $(S)/%.c
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/gen_golden_cdef: oracle/ref_harness/gen_golden_cdef.c $(C_OBJ)
+	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
+
+$(OUT)/ref_cdef_bench: oracle/ref_harness/ref_cdef_bench.c $(C_OBJ) $(AVX2_OBJ)
+	$(CC) $(CFLAGS) -mavx2 $^ -o $@ -Wl,--gc-sections -lm -lpthread
+
+clean:
+	rm -rf $(OUT)
+.PHONY: all clean

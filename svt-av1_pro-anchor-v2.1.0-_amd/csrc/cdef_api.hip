@@ -1,0 +1,238 @@
+// cdef_api.hip — frame-level CDEF entry points of the C ABI (include/svtgpu.h).
+#include <algorithm>
+#include <cstring>
+
+#include "svtgpu_internal.h"
+
+int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                          uint64_t lambda, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st);
+
+// set_cdef_controls (Source/Lib/Encoder/Codec/EncModeConfig.c:860-1330), searched levels only.
+extern "C" int svtgpu_cdef_controls_for_level(int level, SvtGpuCdefControls *c) {
+    if (!c)
+        return SVTGPU_ERR_INVALID_ARG;
+    static const uint8_t pf_gi[16] = {0, 4, 8, 12, 16, 20, 24, 28, 32, 36, 40, 44, 48, 52, 56, 60}; // :12
+    struct Level {
+        int         nfirst;
+        uint8_t     first[16]; // indices into pf_gi
+        int         nsec;      // secondary strengths per primary
+        uint8_t     sec[3];    // secondary codes added to the primary code
+        bool        sec_uv;    // second-pass chroma tested
+        uint8_t     ss;
+        uint16_t    bias;
+    };
+    Level L{};
+    switch (level) {
+    case 1: L = {16, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, 3, {1, 2, 3}, true, 1, 0}; break;
+    case 2: L = {12, {0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14}, 3, {1, 2, 3}, false, 1, 0}; break;
+    case 3: L = {8, {0, 2, 4, 6, 8, 10, 12, 14}, 3, {1, 2, 3}, true, 1, 0}; break;
+    case 4: L = {5, {0, 4, 8, 12, 15}, 3, {1, 2, 3}, false, 1, 0}; break;
+    case 5: L = {4, {0, 5, 10, 15}, 3, {1, 2, 3}, true, 1, 0}; break;
+    case 6: L = {3, {0, 7, 15}, 3, {1, 2, 3}, false, 1, 0}; break;
+    case 7: L = {3, {0, 7, 15}, 2, {1, 2}, true, 1, 0}; break;
+    case 8: L = {3, {0, 7, 15}, 1, {2}, false, 1, 0}; break;
+    case 9:
+    case 10: L = {2, {0, 15}, 1, {2}, false, 4, 0}; break;
+    case 12:
+    case 13:
+    case 16: L = {2, {0, 15}, 1, {2}, false, 4, 62}; break;
+    default: return SVTGPU_ERR_UNSUPPORTED; // 0: off; 11/14/15/17: use_reference_cdef_fs
+    }
+    memset(c, 0, sizeof(*c));
+    c->first_pass_fs_num          = (uint8_t)L.nfirst;
+    c->default_second_pass_fs_num = (uint8_t)(L.nfirst * L.nsec);
+    c->subsampling_factor         = L.ss;
+    c->zero_fs_cost_bias          = L.bias;
+    for (int i = 0, sf = 0; i < L.nfirst; i++) {
+        const uint8_t p              = pf_gi[L.first[i]];
+        c->default_first_pass_fs[i]    = p;
+        c->default_first_pass_fs_uv[i] = (int8_t)p;
+        for (int j = 0; j < L.nsec; j++, sf++) {
+            c->default_second_pass_fs[sf]    = (uint8_t)(p + L.sec[j]);
+            c->default_second_pass_fs_uv[sf] = L.sec_uv ? (int8_t)(p + L.sec[j]) : (int8_t)-1;
+        }
+    }
+    return SVTGPU_OK;
+}
+
+static int valid_controls(const SvtGpuCdefControls *c) {
+    const int n = c->first_pass_fs_num + c->default_second_pass_fs_num;
+    if (n <= 0 || n > 64)
+        return 0;
+    if (c->subsampling_factor != 1 && c->subsampling_factor != 2 && c->subsampling_factor != 4)
+        return 0;
+    for (int i = 0; i < n; i++) {
+        const int code = i < c->first_pass_fs_num ? c->default_first_pass_fs[i]
+                                                  : c->default_second_pass_fs[i - c->first_pass_fs_num];
+        if (code > 63)
+            return 0;
+    }
+    return 1;
+}
+
+static void build_table(const SvtGpuCdefControls *c, CdefStrengthTable *t) {
+    memset(t, 0, sizeof(*t));
+    const int nf = c->first_pass_fs_num;
+    t->nstr      = nf + c->default_second_pass_fs_num;
+    for (int gi = 0; gi < t->nstr; gi++) {
+        const bool first = gi < nf;
+        const int  code  = first ? c->default_first_pass_fs[gi] : c->default_second_pass_fs[gi - nf];
+        const bool uv    = first ? c->default_first_pass_fs_uv[gi] != -1 : c->default_second_pass_fs_uv[gi - nf] != -1;
+        t->code[gi]      = (uint8_t)code;
+        t->uv_on[gi]     = uv;
+        if ((code >> 2) == 0)
+            t->luma_a[t->n_luma_a++] = (int8_t)gi;
+        else
+            t->luma_b[t->n_luma_b++] = (int8_t)gi;
+        if (uv) {
+            if ((code >> 2) == 0)
+                t->chroma_a[t->n_chroma_a++] = (int8_t)gi;
+            else
+                t->chroma_b[t->n_chroma_b++] = (int8_t)gi;
+        }
+    }
+}
+
+extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuCdefFrameState **out) {
+    if (!ctx || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7))
+        return SVTGPU_ERR_INVALID_ARG;
+    auto *s      = new SvtGpuCdefFrameState{};
+    s->ctx       = ctx;
+    s->width     = width;
+    s->height    = height;
+    s->geo       = frame_geo(width, height);
+    s->nfb       = s->geo.nvfb * s->geo.nhfb;
+    s->mask_all  = 1;
+    s->pick_parts = 32;
+    const size_t nfb = s->nfb;
+    bool ok = hipMalloc(&s->d_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols) == hipSuccess &&
+              hipMalloc(&s->d_mse, nfb * 2 * 64 * 8) == hipSuccess && hipMalloc(&s->d_skip, nfb) == hipSuccess &&
+              hipMalloc(&s->d_dir, nfb * 64) == hipSuccess && hipMalloc(&s->d_var, nfb * 64 * 4) == hipSuccess &&
+              hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
+              hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)4 * s->pick_parts * 4096) * 8) == hipSuccess &&
+              hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, 4 * 256) == hipSuccess &&
+              hipMalloc(&s->d_fb_list, (nfb + 1) * 4) == hipSuccess;
+    if (!ok) {
+        svtgpu_cdef_state_destroy(s);
+        return SVTGPU_ERR_OOM;
+    }
+    HIP_TRY(hipMemset(s->d_fb_strength, 0, nfb));
+    HIP_TRY(hipMemset(s->d_skip, 1, nfb));
+    s->own_mse      = s->d_mse;
+    s->own_skip     = s->d_skip;
+    s->fb_row_begin = 0;
+    s->fb_row_end   = s->geo.nvfb;
+    *out = s;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
+    if (!s)
+        return;
+    void *bufs[] = {s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip, s->d_dir, s->d_var, s->d_fb_strength, s->d_pick_part,
+                    s->d_pick_out, s->d_pick_lev, s->d_fb_list};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    delete s;
+}
+
+extern "C" int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32_t fb_row_end) {
+    if (!s || fb_row_begin < 0 || fb_row_end > s->geo.nvfb || fb_row_begin >= fb_row_end)
+        return SVTGPU_ERR_INVALID_ARG;
+    s->fb_row_begin = fb_row_begin;
+    s->fb_row_end   = fb_row_end;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, void *skip_dev) {
+    if (!s || (!mse_dev) != (!skip_dev))
+        return SVTGPU_ERR_INVALID_ARG;
+    s->d_mse  = mse_dev ? (uint64_t *)mse_dev : s->own_mse;
+    s->d_skip = skip_dev ? (uint8_t *)skip_dev : s->own_skip;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream) {
+    if (!s)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    HIP_TRY(hipMemsetAsync(s->d_mse, 0, (size_t)s->nfb * 2 * 64 * 8, st));
+    HIP_TRY(hipMemsetAsync(s->d_skip, 0, (size_t)s->nfb, st));
+    return SVTGPU_OK;
+}
+
+extern "C" int32_t svtgpu_cdef_state_nfb(const SvtGpuCdefFrameState *s) { return s ? s->nfb : -1; }
+
+extern "C" int svtgpu_cdef_set_block_mask(SvtGpuCdefFrameState *s, const uint8_t *host_mask, void *stream) {
+    if (!s)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (!host_mask) {
+        s->mask_all = 1;
+        return SVTGPU_OK;
+    }
+    s->mask_all = 0;
+    HIP_TRY(hipMemcpyAsync(s->d_mask, host_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols, hipMemcpyHostToDevice,
+                           pick_stream(s->ctx, stream)));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                        const SvtGpuCdefControls *ctrls, int32_t base_q_idx, void *stream) {
+    if (!s || !recon || !source || !ctrls || !valid_controls(ctrls))
+        return SVTGPU_ERR_INVALID_ARG;
+    if (recon->width != s->width || recon->height != s->height || source->width != s->width ||
+        source->height != s->height || recon->bit_depth != source->bit_depth)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (base_q_idx < 0 || base_q_idx > 255)
+        return SVTGPU_ERR_INVALID_ARG;
+    CdefStrengthTable tab;
+    build_table(ctrls, &tab);
+    return svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6),
+                                     pick_stream(s->ctx, stream));
+}
+
+extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                                uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream) {
+    if (!s || !ctrls || !params_out || !valid_controls(ctrls))
+        return SVTGPU_ERR_INVALID_ARG;
+    return svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out,
+                                 pick_stream(s->ctx, stream));
+}
+
+extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream) {
+    if (!s || !fb_strength)
+        return SVTGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipMemcpyAsync(s->d_fb_strength, fb_strength, s->nfb, hipMemcpyHostToDevice, pick_stream(s->ctx, stream)));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
+                                       const SvtGpuCdefParams *params, void *stream) {
+    if (!s || !recon || !out || !params || recon == out)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (recon->width != s->width || recon->height != s->height || out->width != s->width ||
+        out->height != s->height || out->bit_depth != recon->bit_depth)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (params->cdef_bits > 3)
+        return SVTGPU_ERR_INVALID_ARG;
+    for (int i = 0; i < (1 << params->cdef_bits); i++)
+        if (params->cdef_y_strength[i] > 63 || params->cdef_uv_strength[i] > 63)
+            return SVTGPU_ERR_INVALID_ARG;
+    return svtgpu_launch_cdef_apply(s, recon, out, params, pick_stream(s->ctx, stream));
+}
+
+extern "C" int svtgpu_cdef_read_state(SvtGpuCdefFrameState *s, uint64_t *mse, uint8_t *skip, uint8_t *dir,
+                                      int32_t *var, void *stream) {
+    if (!s)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t  st  = pick_stream(s->ctx, stream);
+    const size_t nfb = s->nfb;
+    if (mse) HIP_TRY(hipMemcpyAsync(mse, s->d_mse, nfb * 2 * 64 * 8, hipMemcpyDeviceToHost, st));
+    if (skip) HIP_TRY(hipMemcpyAsync(skip, s->d_skip, nfb, hipMemcpyDeviceToHost, st));
+    if (dir) HIP_TRY(hipMemcpyAsync(dir, s->d_dir, nfb * 64, hipMemcpyDeviceToHost, st));
+    if (var) HIP_TRY(hipMemcpyAsync(var, s->d_var, nfb * 64 * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}
+
+extern "C" void *svtgpu_cdef_mse_device_ptr(SvtGpuCdefFrameState *s) { return s ? (void *)s->d_mse : nullptr; }

@@ -1,0 +1,173 @@
+// runtime.hip — device/context/frame management of the C ABI (include/svtgpu.h).
+#include <cstring>
+#include <mutex>
+
+#include "svtgpu_internal.h"
+
+static thread_local char g_last_err[512];
+
+void svtgpu_set_last_hip_error(hipError_t e, const char *what, const char *file, int line) {
+    snprintf(g_last_err, sizeof g_last_err, "%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+}
+
+void svtgpu_fatal(const char *what) {
+    fprintf(stderr, "svtgpu: fatal: %s: %s\n", what, g_last_err[0] ? g_last_err : "(no detail)");
+    abort();
+}
+
+extern "C" const char *svtgpu_version(void) { return SVTGPU_VERSION_STR; }
+
+extern "C" const char *svtgpu_error_string(int code) {
+    switch (code) {
+    case SVTGPU_OK: return "ok";
+    case SVTGPU_ERR_INVALID_ARG: return "invalid argument";
+    case SVTGPU_ERR_HIP: return g_last_err[0] ? g_last_err : "HIP error";
+    case SVTGPU_ERR_UNSUPPORTED: return "unsupported configuration";
+    case SVTGPU_ERR_NO_DEVICE: return "no gfx950 device";
+    case SVTGPU_ERR_OOM: return "out of device memory";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int svtgpu_device_available(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return 0;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, 0) != hipSuccess)
+        return 0;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+extern "C" int svtgpu_context_create(int device, SvtGpuContext **out) {
+    if (!out)
+        return SVTGPU_ERR_INVALID_ARG;
+    *out  = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return SVTGPU_ERR_NO_DEVICE;
+    HIP_TRY(hipSetDevice(device));
+    auto *c   = new SvtGpuContext;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SVTGPU_ERR_HIP;
+    }
+    *out = c;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_context_destroy(SvtGpuContext *ctx) {
+    if (!ctx)
+        return;
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" void *svtgpu_context_stream(SvtGpuContext *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+extern "C" int svtgpu_synchronize(SvtGpuContext *ctx, void *stream) {
+    if (!ctx)
+        return SVTGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipStreamSynchronize(pick_stream(ctx, stream)));
+    return SVTGPU_OK;
+}
+
+// process-wide context used by the per-block RTCD shims (they have no context argument)
+static std::once_flag g_default_once;
+static SvtGpuContext *g_default_ctx = nullptr;
+SvtGpuContext        *svtgpu_default_context() {
+    std::call_once(g_default_once, [] {
+        if (!svtgpu_device_available()) {
+            snprintf(g_last_err, sizeof g_last_err, "no gfx950 device visible");
+            return;
+        }
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (svtgpu_context_create(dev, &g_default_ctx) != SVTGPU_OK)
+            g_default_ctx = nullptr;
+    });
+    if (!g_default_ctx)
+        svtgpu_fatal("svtgpu per-block shim called without a usable gfx950 device");
+    return g_default_ctx;
+}
+hipStream_t svtgpu_default_stream() { return svtgpu_default_context()->stream; }
+
+// ---------------------------------------------------------------------------------------------
+// frames
+// ---------------------------------------------------------------------------------------------
+extern "C" int svtgpu_frame_create(SvtGpuContext *ctx, int32_t width, int32_t height, int32_t bit_depth,
+                                   SvtGpuFrame **out) {
+    if (!ctx || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7))
+        return SVTGPU_ERR_INVALID_ARG;
+    if (bit_depth != 8 && bit_depth != 10)
+        return SVTGPU_ERR_UNSUPPORTED;
+    auto *f             = new SvtGpuFrame;
+    f->ctx              = ctx;
+    f->width            = width;
+    f->height           = height;
+    f->bit_depth        = bit_depth;
+    f->bytes_per_sample = bit_depth > 8 ? 2 : 1;
+    size_t off[3], total = 0;
+    for (int p = 0; p < 3; p++) {
+        f->pw[p] = p ? width / 2 : width;
+        f->ph[p] = p ? height / 2 : height;
+        // rows padded to 256 B so every row starts 256-B aligned (coalesced 16-B lane loads)
+        const size_t row_bytes = ((size_t)f->pw[p] * f->bytes_per_sample + 255) & ~(size_t)255;
+        f->stride[p]           = (int32_t)(row_bytes / f->bytes_per_sample);
+        off[p]                 = total;
+        total += row_bytes * f->ph[p];
+    }
+    if (hipMalloc(&f->base, total) != hipSuccess) {
+        delete f;
+        return SVTGPU_ERR_OOM;
+    }
+    for (int p = 0; p < 3; p++) f->plane[p] = (char *)f->base + off[p];
+    *out = f;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_frame_destroy(SvtGpuFrame *f) {
+    if (!f)
+        return;
+    (void)hipFree(f->base);
+    delete f;
+}
+
+extern "C" int32_t svtgpu_frame_stride(const SvtGpuFrame *f, int plane) {
+    return (f && plane >= 0 && plane < 3) ? f->stride[plane] : -1;
+}
+extern "C" void *svtgpu_frame_plane_ptr(SvtGpuFrame *f, int plane) {
+    return (f && plane >= 0 && plane < 3) ? f->plane[plane] : nullptr;
+}
+
+extern "C" int svtgpu_frame_upload(SvtGpuFrame *f, int plane, const void *host, int32_t host_stride, void *stream) {
+    if (!f || !host || plane < 0 || plane > 2 || host_stride < f->pw[plane])
+        return SVTGPU_ERR_INVALID_ARG;
+    const size_t b = f->bytes_per_sample;
+    HIP_TRY(hipMemcpy2DAsync(f->plane[plane], f->stride[plane] * b, host, host_stride * b, f->pw[plane] * b,
+                             f->ph[plane], hipMemcpyHostToDevice, pick_stream(f->ctx, stream)));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_frame_download(const SvtGpuFrame *f, int plane, void *host, int32_t host_stride, void *stream) {
+    if (!f || !host || plane < 0 || plane > 2 || host_stride < f->pw[plane])
+        return SVTGPU_ERR_INVALID_ARG;
+    const size_t b  = f->bytes_per_sample;
+    hipStream_t  st = pick_stream(f->ctx, stream);
+    HIP_TRY(hipMemcpy2DAsync(host, host_stride * b, f->plane[plane], f->stride[plane] * b, f->pw[plane] * b,
+                             f->ph[plane], hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_frame_copy(SvtGpuFrame *dst, const SvtGpuFrame *src, void *stream) {
+    if (!dst || !src || dst->width != src->width || dst->height != src->height || dst->bit_depth != src->bit_depth)
+        return SVTGPU_ERR_INVALID_ARG;
+    const size_t b = src->bytes_per_sample;
+    for (int p = 0; p < 3; p++)
+        HIP_TRY(hipMemcpy2DAsync(dst->plane[p], dst->stride[p] * b, src->plane[p], src->stride[p] * b, src->pw[p] * b,
+                                 src->ph[p], hipMemcpyDeviceToDevice, pick_stream(dst->ctx, stream)));
+    return SVTGPU_OK;
+}

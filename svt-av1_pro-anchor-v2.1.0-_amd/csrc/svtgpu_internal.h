@@ -1,0 +1,118 @@
+// svtgpu_internal.h — shared host/device definitions of the MI355X in-loop-filter library.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../../include/svtgpu.h"
+
+#define SVTGPU_VERSION_STR "svtgpu 0.1.0 (gfx950)"
+
+// ---------------------------------------------------------------------------------------------
+// error plumbing (never throws across the C ABI)
+// ---------------------------------------------------------------------------------------------
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            svtgpu_set_last_hip_error(e_, #expr, __FILE__, __LINE__);                         \
+            return SVTGPU_ERR_HIP;                                                            \
+        }                                                                                     \
+    } while (0)
+
+void svtgpu_set_last_hip_error(hipError_t e, const char *what, const char *file, int line);
+// Per-block RTCD shims cannot return an error through their reference signature: abort loudly.
+[[noreturn]] void svtgpu_fatal(const char *what);
+#define HIP_OR_DIE(expr)                                                                      \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            svtgpu_set_last_hip_error(e_, #expr, __FILE__, __LINE__);                         \
+            svtgpu_fatal(#expr);                                                              \
+        }                                                                                     \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// objects
+// ---------------------------------------------------------------------------------------------
+struct SvtGpuContext {
+    int         device;
+    hipStream_t stream;
+};
+
+struct SvtGpuFrame {
+    SvtGpuContext *ctx;
+    int32_t        width, height, bit_depth;
+    int32_t        bytes_per_sample;
+    int32_t        pw[3], ph[3]; // plane sizes
+    int32_t        stride[3];    // samples
+    void          *plane[3];     // device pointers (one allocation)
+    void          *base;
+};
+
+// frame geometry in 4x4 mode-info units (SB64 CDEF filter blocks of 16x16 mi)
+struct FrameGeo {
+    int32_t mi_rows, mi_cols, nvfb, nhfb, b8_rows, b8_cols;
+};
+static inline FrameGeo frame_geo(int32_t w, int32_t h) {
+    FrameGeo g;
+    g.mi_cols = ((w + 7) & ~7) >> 2;
+    g.mi_rows = ((h + 7) & ~7) >> 2;
+    g.nhfb    = (g.mi_cols + 15) / 16;
+    g.nvfb    = (g.mi_rows + 15) / 16;
+    g.b8_cols = g.mi_cols / 2;
+    g.b8_rows = g.mi_rows / 2;
+    return g;
+}
+
+struct SvtGpuCdefFrameState {
+    SvtGpuContext *ctx;
+    int32_t        width, height;
+    FrameGeo       geo;
+    int32_t        nfb;
+    uint8_t       *d_mask;        // [b8_rows][b8_cols] 1 = filter block
+    uint64_t      *d_mse;         // [2][nfb][64]
+    uint8_t       *d_skip;        // [nfb]
+    uint8_t       *d_dir;         // [nfb][64]
+    int32_t       *d_var;         // [nfb][64]
+    int8_t        *d_fb_strength; // [nfb]
+    // pick scratch
+    uint64_t      *d_pick_part;   // partial tot_mse tables
+    uint64_t      *d_pick_out;    // [chains][4] (best, j, k)
+    int32_t       *d_pick_lev;    // [chains][2][16]
+    int32_t       *d_fb_list;     // compacted non-skip FB indices
+    int32_t        pick_parts;
+    int32_t        mask_all;      // mask == every block
+    int32_t        fb_row_begin, fb_row_end; // band of FB rows searched/applied (tiling)
+    uint64_t      *own_mse;       // state-owned tables (d_mse/d_skip may point at caller memory)
+    uint8_t       *own_skip;
+};
+
+// device-side views of the search strength lists (built on the host from SvtGpuCdefControls)
+struct CdefStrengthTable {
+    int32_t nstr;          // total strengths searched (first + second pass)
+    int32_t n_luma_a;      // luma strengths with pri level 0 (direction 0 taps)
+    int32_t n_luma_b;      // luma strengths with pri level != 0 (block direction taps)
+    int32_t n_chroma_a, n_chroma_b;
+    int8_t  luma_a[64], luma_b[64];     // gi lists
+    int8_t  chroma_a[64], chroma_b[64]; // gi lists (chroma-enabled strengths only)
+    uint8_t code[64];                   // gi -> pri*4+sec strength code
+    uint8_t uv_on[64];                  // gi -> chroma tested
+};
+
+// ---------------------------------------------------------------------------------------------
+// launchers (defined in the .hip translation units)
+// ---------------------------------------------------------------------------------------------
+int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src,
+                              const CdefStrengthTable *tab, int32_t subsampling, int32_t damping,
+                              hipStream_t st);
+int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
+                             const SvtGpuCdefParams *p, hipStream_t st);
+
+hipStream_t svtgpu_default_stream();
+SvtGpuContext *svtgpu_default_context();
+static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
+    return stream ? (hipStream_t)stream : ctx->stream;
+}

@@ -1,0 +1,284 @@
+"""ctypes binding of libsvtgpu (the MI355X C ABI declared in include/svtgpu.h).
+
+Host-side mirror of the reference's CDEF frame pipeline surface (EbCdefProcess.c /
+EbEncCdef.c): search -> pick -> apply on device-resident 4:2:0 frames.  This module is what
+tests/ and bench.py call; it never falls back to a CPU path — if the HIP library is missing or no
+gfx950 device is visible, it raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsvtgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "svtgpu.h")
+
+SVTGPU_OK = 0
+TOTAL_STRENGTHS = 64
+MAX_STRENGTHS = 16
+
+
+class CdefList(ctypes.Structure):
+    _fields_ = [("by", ctypes.c_uint8), ("bx", ctypes.c_uint8)]
+
+
+class CdefControls(ctypes.Structure):
+    """SvtGpuCdefControls (mirror of CdefControls, EbPictureControlSet.h:592-628)."""
+    _fields_ = [
+        ("first_pass_fs_num", ctypes.c_uint8),
+        ("default_second_pass_fs_num", ctypes.c_uint8),
+        ("default_first_pass_fs", ctypes.c_uint8 * TOTAL_STRENGTHS),
+        ("default_second_pass_fs", ctypes.c_uint8 * TOTAL_STRENGTHS),
+        ("default_first_pass_fs_uv", ctypes.c_int8 * TOTAL_STRENGTHS),
+        ("default_second_pass_fs_uv", ctypes.c_int8 * TOTAL_STRENGTHS),
+        ("subsampling_factor", ctypes.c_uint8),
+        ("zero_fs_cost_bias", ctypes.c_uint16),
+    ]
+
+    def strengths(self):
+        n1, n2 = self.first_pass_fs_num, self.default_second_pass_fs_num
+        return list(self.default_first_pass_fs[:n1]) + list(self.default_second_pass_fs[:n2])
+
+
+class CdefParams(ctypes.Structure):
+    """SvtGpuCdefParams (mirror of CdefParams, EbAv1Structs.h:359-369)."""
+    _fields_ = [
+        ("cdef_damping", ctypes.c_uint8),
+        ("cdef_bits", ctypes.c_uint8),
+        ("cdef_y_strength", ctypes.c_uint8 * MAX_STRENGTHS),
+        ("cdef_uv_strength", ctypes.c_uint8 * MAX_STRENGTHS),
+    ]
+
+    def as_tuple(self):
+        nb = 1 << self.cdef_bits
+        return (self.cdef_damping, self.cdef_bits, tuple(self.cdef_y_strength[:nb]),
+                tuple(self.cdef_uv_strength[:nb]))
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_U64 = ctypes.c_uint64
+_SIGS = {
+    "svtgpu_device_available": (ctypes.c_int, []),
+    "svtgpu_version": (ctypes.c_char_p, []),
+    "svtgpu_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "svtgpu_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "svtgpu_context_destroy": (None, [_P]),
+    "svtgpu_context_stream": (_P, [_P]),
+    "svtgpu_synchronize": (ctypes.c_int, [_P, _P]),
+    "svtgpu_frame_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_frame_destroy": (None, [_P]),
+    "svtgpu_frame_stride": (_I32, [_P, ctypes.c_int]),
+    "svtgpu_frame_plane_ptr": (_P, [_P, ctypes.c_int]),
+    "svtgpu_frame_upload": (ctypes.c_int, [_P, ctypes.c_int, _P, _I32, _P]),
+    "svtgpu_frame_download": (ctypes.c_int, [_P, ctypes.c_int, _P, _I32, _P]),
+    "svtgpu_frame_copy": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_find_dir": (ctypes.c_uint8, [_P, _I32, ctypes.POINTER(_I32), _I32]),
+    "svtgpu_cdef_find_dir_dual": (None, [_P, _P, ctypes.c_int, ctypes.POINTER(_I32), ctypes.POINTER(_I32), _I32,
+                                         ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8)]),
+    "svtgpu_cdef_filter_block": (None, [_P, _P, _I32, _P, _I32, _I32, _I32, _I32, _I32, _I32, _I32, ctypes.c_uint8]),
+    "svtgpu_compute_cdef_dist_16bit": (_U64, [_P, _I32, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_uint8]),
+    "svtgpu_compute_cdef_dist_8bit": (_U64, [_P, _I32, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_uint8]),
+    "svtgpu_search_one_dual": (_U64, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                      ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(_U64))), ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int]),
+    "svtgpu_cdef_controls_for_level": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(CdefControls)]),
+    "svtgpu_cdef_state_create": (ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_cdef_state_destroy": (None, [_P]),
+    "svtgpu_cdef_state_nfb": (_I32, [_P]),
+    "svtgpu_cdef_set_block_mask": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_search_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(CdefControls), _I32, _P]),
+    "svtgpu_cdef_pick": (ctypes.c_int, [_P, ctypes.POINTER(CdefControls), _I32, _U64, ctypes.POINTER(CdefParams),
+                                        _P, _P]),
+    "svtgpu_cdef_set_fb_strength": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_apply_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(CdefParams), _P]),
+    "svtgpu_cdef_set_fb_rows": (ctypes.c_int, [_P, _I32, _I32]),
+    "svtgpu_cdef_bind_tables": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_clear_tables": (ctypes.c_int, [_P, _P]),
+    "svtgpu_cdef_read_state": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "svtgpu_cdef_mse_device_ptr": (_P, [_P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libsvtgpu.so (in-tree build).  Raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libsvtgpu.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class SvtGpuError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != SVTGPU_OK:
+        raise SvtGpuError("svtgpu error %d: %s" % (rc, lib().svtgpu_error_string(rc).decode()))
+    return rc
+
+
+def require_device():
+    if not lib().svtgpu_device_available():
+        raise SvtGpuError("no gfx950 device visible: the HIP path is required (no CPU fallback)")
+
+
+def ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Context:
+    def __init__(self, device=0):
+        require_device()
+        h = _P()
+        check(lib().svtgpu_context_create(device, ctypes.byref(h)))
+        self.h = h
+
+    @property
+    def stream(self):
+        return lib().svtgpu_context_stream(self.h)
+
+    def synchronize(self, stream=None):
+        check(lib().svtgpu_synchronize(self.h, stream))
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Frame:
+    """Device-resident 4:2:0 picture (uint8 for 8-bit, uint16 for 10-bit samples)."""
+
+    def __init__(self, ctx, width, height, bit_depth):
+        self.ctx, self.width, self.height, self.bit_depth = ctx, width, height, bit_depth
+        self.dtype = np.uint16 if bit_depth > 8 else np.uint8
+        h = _P()
+        check(lib().svtgpu_frame_create(ctx.h, width, height, bit_depth, ctypes.byref(h)))
+        self.h = h
+
+    def plane_shape(self, p):
+        return (self.height, self.width) if p == 0 else (self.height // 2, self.width // 2)
+
+    def upload(self, planes, stream=None):
+        keep = []
+        for p, a in enumerate(planes):
+            a = np.ascontiguousarray(a, dtype=self.dtype)
+            assert a.shape == self.plane_shape(p), (a.shape, self.plane_shape(p))
+            keep.append(a)
+            check(lib().svtgpu_frame_upload(self.h, p, ptr(a), a.shape[1], stream))
+        self.ctx.synchronize(stream)  # host buffers must outlive the copies
+
+    def download(self, stream=None):
+        out = []
+        for p in range(3):
+            a = np.empty(self.plane_shape(p), dtype=self.dtype)
+            check(lib().svtgpu_frame_download(self.h, p, ptr(a), a.shape[1], stream))
+            out.append(a)
+        return out
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_frame_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def cdef_controls(level):
+    c = CdefControls()
+    check(lib().svtgpu_cdef_controls_for_level(level, ctypes.byref(c)))
+    return c
+
+
+class CdefState:
+    """Device search state of one frame (mse_seg / skip_cdef_seg / cdef_dir_data)."""
+
+    def __init__(self, ctx, width, height):
+        self.ctx, self.width, self.height = ctx, width, height
+        h = _P()
+        check(lib().svtgpu_cdef_state_create(ctx.h, width, height, ctypes.byref(h)))
+        self.h = h
+        self.nfb = lib().svtgpu_cdef_state_nfb(h)
+
+    def set_block_mask(self, mask, stream=None):
+        if mask is None:
+            check(lib().svtgpu_cdef_set_block_mask(self.h, None, stream))
+        else:
+            self._mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            check(lib().svtgpu_cdef_set_block_mask(self.h, ptr(self._mask), stream))
+
+    def search(self, recon, source, ctrls, base_q_idx, stream=None):
+        check(lib().svtgpu_cdef_search_frame(self.h, recon.h, source.h, ctypes.byref(ctrls), base_q_idx, stream))
+
+    def pick(self, ctrls, base_q_idx, lam, stream=None):
+        prm = CdefParams()
+        fbs = np.zeros(self.nfb, dtype=np.int8)
+        check(lib().svtgpu_cdef_pick(self.h, ctypes.byref(ctrls), base_q_idx, lam, ctypes.byref(prm), ptr(fbs), stream))
+        return prm, fbs
+
+    def set_fb_strength(self, fbs, stream=None):
+        self._fbs = np.ascontiguousarray(fbs, dtype=np.int8)
+        check(lib().svtgpu_cdef_set_fb_strength(self.h, ptr(self._fbs), stream))
+
+    def apply(self, recon, out, params, stream=None):
+        check(lib().svtgpu_cdef_apply_frame(self.h, recon.h, out.h, ctypes.byref(params), stream))
+
+    def read(self, stream=None):
+        mse = np.empty((2, self.nfb, 64), dtype=np.uint64)
+        skip = np.empty(self.nfb, dtype=np.uint8)
+        d = np.empty((self.nfb, 64), dtype=np.uint8)
+        v = np.empty((self.nfb, 64), dtype=np.int32)
+        check(lib().svtgpu_cdef_read_state(self.h, ptr(mse), ptr(skip), ptr(d), ptr(v), stream))
+        return mse, skip, d, v
+
+    def set_fb_rows(self, begin, end):
+        check(lib().svtgpu_cdef_set_fb_rows(self.h, begin, end))
+
+    def bind_tables(self, mse_dev_ptr, skip_dev_ptr):
+        check(lib().svtgpu_cdef_bind_tables(self.h, mse_dev_ptr, skip_dev_ptr))
+
+    def clear_tables(self, stream=None):
+        check(lib().svtgpu_cdef_clear_tables(self.h, stream))
+
+    def mse_device_ptr(self):
+        return lib().svtgpu_cdef_mse_device_ptr(self.h)
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_cdef_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def declared_symbols(header=HEADER_PATH):
+    """Function names declared in include/svtgpu.h (for the ABI export test)."""
+    import re
+    txt = open(header).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(svtgpu_[a-z0-9_]+)\s*\(", txt)))

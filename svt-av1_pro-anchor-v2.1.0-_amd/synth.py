@@ -1,0 +1,56 @@
+"""Deterministic synthetic 4:2:0 inputs (BASELINE.md §3 / SURVEY.md §8d).
+
+source = clip(smooth 2-D gradient + oriented sinusoid texture (random angle per 64x64 block, so
+CDEF directions vary) + Gaussian noise sigma = 3*2^(bd-8));
+recon  = clip(source + per-8x8 DC offset U(-q/2, q/2) + ringing noise U(-q, q)), q = 6*2^(bd-8).
+Values in [0, 2^bd - 1]; uint8 for 8-bit, uint16 for 10-bit.  Chroma uses the same generator at half
+resolution.  seed = 0x5EED0000 + config number by convention.
+"""
+import numpy as np
+
+
+def _plane(rng, h, w, bd):
+    maxv = (1 << bd) - 1
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    base = (0.25 + 0.5 * (xx / max(w, 1)) * 0.6 + 0.5 * (yy / max(h, 1)) * 0.4) * maxv
+    nbh, nbw = (h + 63) // 64, (w + 63) // 64
+    ang = rng.uniform(0, np.pi, size=(nbh, nbw)).astype(np.float32)
+    freq = rng.uniform(0.15, 0.6, size=(nbh, nbw)).astype(np.float32)
+    amp = rng.uniform(0.02, 0.12, size=(nbh, nbw)).astype(np.float32) * maxv
+    A = np.repeat(np.repeat(ang, 64, 0), 64, 1)[:h, :w]
+    F = np.repeat(np.repeat(freq, 64, 0), 64, 1)[:h, :w]
+    M = np.repeat(np.repeat(amp, 64, 0), 64, 1)[:h, :w]
+    tex = M * np.sin(F * (xx * np.cos(A) + yy * np.sin(A)))
+    noise = rng.normal(0.0, 3.0 * (1 << (bd - 8)), size=(h, w)).astype(np.float32)
+    return np.clip(np.rint(base + tex + noise), 0, maxv)
+
+
+def _coded(rng, src, bd):
+    h, w = src.shape
+    maxv = (1 << bd) - 1
+    q = 6.0 * (1 << (bd - 8))
+    dc = rng.uniform(-q / 2, q / 2, size=((h + 7) // 8, (w + 7) // 8)).astype(np.float32)
+    DC = np.repeat(np.repeat(dc, 8, 0), 8, 1)[:h, :w]
+    ring = rng.uniform(-q, q, size=(h, w)).astype(np.float32)
+    return np.clip(np.rint(src + DC + ring), 0, maxv)
+
+
+def frame_pair(width, height, bit_depth, seed):
+    """Returns (source_planes, recon_planes), each a list [Y, U, V] of 2-D arrays."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dt = np.uint16 if bit_depth > 8 else np.uint8
+    src, rec = [], []
+    for p in range(3):
+        h, w = (height, width) if p == 0 else (height // 2, width // 2)
+        s = _plane(rng, h, w, bit_depth)
+        r = _coded(rng, s, bit_depth)
+        src.append(s.astype(dt))
+        rec.append(r.astype(dt))
+    return src, rec
+
+
+def block_mask(width, height, seed, p_skip=0.0):
+    """Per-8x8 'filter this block' mask (1 = listed); p_skip = probability a block is skipped."""
+    rng = np.random.Generator(np.random.PCG64(seed ^ 0xB10C))
+    m = (rng.random(((height + 7) // 8, (width + 7) // 8)) >= p_skip).astype(np.uint8)
+    return m

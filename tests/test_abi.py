@@ -1,0 +1,58 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol include/svtgpu.h declares,
+host-only entry points agree with the oracle, and device entry points fail loudly without a device."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import oracle
+import svtgpu
+
+
+def test_library_exports_every_declared_symbol():
+    L = svtgpu.lib()
+    names = svtgpu.declared_symbols()
+    assert len(names) >= 30
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # the ctypes signature table covers the whole header
+    assert sorted(svtgpu._SIGS) == names
+
+
+def test_exports_are_plain_c_symbols():
+    out = subprocess.run(["nm", "-D", "--defined-only", svtgpu.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    for n in svtgpu.declared_symbols():
+        assert n in exported, n  # extern "C": no C++ mangling
+
+
+@pytest.mark.parametrize("level", list(range(0, 18)))
+def test_controls_for_level_matches_oracle(level):
+    L = svtgpu.lib()
+    c = svtgpu.CdefControls()
+    rc = L.svtgpu_cdef_controls_for_level(level, ctypes.byref(c))
+    try:
+        o = oracle.controls(level)
+    except ValueError:
+        assert rc == -3
+        return
+    assert rc == 0
+    assert bytes(c) == bytes(o)
+
+
+def test_version_and_errors():
+    L = svtgpu.lib()
+    assert b"gfx950" in L.svtgpu_version()
+    assert L.svtgpu_error_string(-1) == b"invalid argument"
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and svtgpu.lib().svtgpu_device_available(),
+                    reason="a device is present")
+def test_no_device_fails_loudly():
+    L = svtgpu.lib()
+    assert L.svtgpu_device_available() == 0
+    h = ctypes.c_void_p()
+    assert L.svtgpu_context_create(0, ctypes.byref(h)) == -4
+    with pytest.raises(svtgpu.SvtGpuError):
+        svtgpu.Context()
