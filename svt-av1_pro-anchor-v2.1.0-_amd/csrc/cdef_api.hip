@@ -72,24 +72,31 @@ static int valid_controls(const SvtGpuCdefControls *c) {
 
 static void build_table(const SvtGpuCdefControls *c, CdefStrengthTable *t) {
     memset(t, 0, sizeof(*t));
+    for (int g = 0; g < 2; g++)
+        for (int i = 0; i < 16; i++)
+            for (int q = 0; q < 4; q++) t->luma[g].gi[i][q] = t->chroma[g].gi[i][q] = -1;
     const int nf = c->first_pass_fs_num;
     t->nstr      = nf + c->default_second_pass_fs_num;
+    int first_of[64];
+    for (int i = 0; i < 64; i++) first_of[i] = -1;
+    auto add = [](CdefGroupTable &G, int level, int sc, int gi) {
+        int li = 0;
+        while (li < G.nlv && G.lv[li] != level) li++;
+        if (li == G.nlv) G.lv[G.nlv++] = level;
+        G.gi[li][sc] = gi;
+        if (sc) G.sec_used |= 1 << sc;
+    };
     for (int gi = 0; gi < t->nstr; gi++) {
         const bool first = gi < nf;
         const int  code  = first ? c->default_first_pass_fs[gi] : c->default_second_pass_fs[gi - nf];
         const bool uv    = first ? c->default_first_pass_fs_uv[gi] != -1 : c->default_second_pass_fs_uv[gi - nf] != -1;
-        t->code[gi]      = (uint8_t)code;
         t->uv_on[gi]     = uv;
-        if ((code >> 2) == 0)
-            t->luma_a[t->n_luma_a++] = (int8_t)gi;
-        else
-            t->luma_b[t->n_luma_b++] = (int8_t)gi;
-        if (uv) {
-            if ((code >> 2) == 0)
-                t->chroma_a[t->n_chroma_a++] = (int8_t)gi;
-            else
-                t->chroma_b[t->n_chroma_b++] = (int8_t)gi;
-        }
+        t->alias[gi]     = (int8_t)first_of[code];
+        if (first_of[code] >= 0) continue; // same code searched twice: copy its result
+        first_of[code] = gi;
+        const int level = code >> 2, sc = code & 3, g = level != 0;
+        add(t->luma[g], level, sc, gi);
+        if (uv) add(t->chroma[g], level, sc, gi);
     }
 }
 
@@ -103,14 +110,14 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
     s->geo       = frame_geo(width, height);
     s->nfb       = s->geo.nvfb * s->geo.nhfb;
     s->mask_all  = 1;
-    s->pick_parts = 32;
+    s->pick_parts = 64;
     const size_t nfb = s->nfb;
     bool ok = hipMalloc(&s->d_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols) == hipSuccess &&
               hipMalloc(&s->d_mse, nfb * 2 * 64 * 8) == hipSuccess && hipMalloc(&s->d_skip, nfb) == hipSuccess &&
               hipMalloc(&s->d_dir, nfb * 64) == hipSuccess && hipMalloc(&s->d_var, nfb * 64 * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
-              hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)4 * s->pick_parts * 4096) * 8) == hipSuccess &&
-              hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, 4 * 256) == hipSuccess &&
+              hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096) * 8) == hipSuccess &&
+              hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, (size_t)(41 * 4 * 32 + 4 * 32 + 64) * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_list, (nfb + 1) * 4) == hipSuccess;
     if (!ok) {
         svtgpu_cdef_state_destroy(s);

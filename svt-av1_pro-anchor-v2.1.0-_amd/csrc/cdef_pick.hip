@@ -15,20 +15,23 @@
 
 #define NT 256
 #define MAX_CHAINS 4
-#define FB_BATCH 8
+#define NSTEPS 40            // longest chain: nb = 8 → 8 + 32 calls (EbEncCdef.c:714-726)
+#define PICK_CHUNK 48        // max FBs per workgroup (staged in LDS: <= 48.4 KB)
 
 struct StepChain {
-    int32_t chain;     // 0..3 (nb = 1 << chain)
-    int32_t nb_sel;    // number of already-selected pairs for this call
-    int32_t shift_after;
+    int32_t chain;       // 0..3 (nb = 1 << chain)
     int32_t nb;
+    int32_t nb_sel;      // selection size of this call (-1: finalize only)
+    int32_t prev_nb_sel; // selection size of the previous call (-1: none)
+    int32_t prev_shift;  // the previous call's result is followed by a refinement shift
 };
 struct StepArgs {
-    const uint64_t *wmse; // [sb_count][2][64] compacted, bias applied
-    int32_t         sb_count, chunk, parts, start_gi, end_gi;
-    int32_t        *lev;  // [4][2][16]
-    uint64_t       *part; // [4][parts][4096]
-    uint64_t       *best; // [4]
+    const uint64_t *wmse;   // [sb_count][2][64] compacted, bias applied
+    int32_t         sb_count, chunk, start_gi, end_gi, step;
+    uint64_t       *tot;    // [3][4][4096] rotating tot_mse accumulators
+    int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
+    int32_t        *fin;    // [4][32] final list per chain
+    uint64_t       *best;   // [4] value returned by each chain's last call
     StepChain       ch[MAX_CHAINS];
 };
 
@@ -67,85 +70,111 @@ __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *
     wmse[((size_t)i * 2 + p) * 64 + g] = v;
 }
 
-// ---- one svt_search_one_dual call per active chain, partial over an FB chunk ----
-__global__ void __launch_bounds__(NT) sod_partial_kernel(const StepArgs A) {
-    __shared__ uint64_t m[FB_BATCH][2][64];
-    __shared__ int32_t  sel[2][16];
-    const StepChain C = A.ch[blockIdx.y];
-    const int       t = threadIdx.x, j = t >> 2, k0 = (t & 3) * 16;
-    if (t < 32) sel[t >> 4][t & 15] = A.lev[(C.chain * 2 + (t >> 4)) * 16 + (t & 15)];
-    uint64_t tot[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) tot[u] = 0;
-    const int f0 = blockIdx.x * A.chunk, f1 = min(A.sb_count, f0 + A.chunk);
-    for (int fb = f0; fb < f1; fb += FB_BATCH) {
-        const int nb = min(FB_BATCH, f1 - fb);
-        __syncthreads();
-        for (int i = t; i < nb * 128; i += NT) (&m[0][0][0])[i] = A.wmse[(size_t)fb * 128 + i];
-        __syncthreads();
-        for (int b = 0; b < nb; b++) {
-            uint64_t best = (uint64_t)1 << 63;
-            for (int g = 0; g < C.nb_sel; g++) {
-                const uint64_t c = m[b][0][sel[0][g]] + m[b][1][sel[1][g]];
-                best = c < best ? c : best;
-            }
-            const uint64_t mj = m[b][0][j];
-#pragma unroll
-            for (int u = 0; u < 16; u++) {
-                const uint64_t c = mj + m[b][1][k0 + u];
-                tot[u] += c < best ? c : best;
-            }
-        }
-    }
-    uint64_t *out = A.part + ((size_t)C.chain * A.parts + blockIdx.x) * 4096;
-#pragma unroll
-    for (int u = 0; u < 16; u++) out[j * 64 + k0 + u] = tot[u];
-}
-
-// ---- sum partials, first argmin over [start, end)^2, append the pick, pre-shift for refinement ----
-__global__ void __launch_bounds__(NT) sod_reduce_kernel(const StepArgs A) {
-    __shared__ uint64_t bv[NT];
-    __shared__ int32_t  bi[NT];
-    const StepChain C = A.ch[blockIdx.x];
-    const int       t = threadIdx.x;
-    uint64_t        best = (uint64_t)1 << 63; // best_tot_mse initial value (EbEncCdef.c:632)
-    int             bidx = 1 << 30;
-    for (int u = 0; u < 16; u++) {
-        const int e = t * 16 + u, j = e >> 6, k = e & 63;
-        uint64_t  s = 0;
-        for (int p = 0; p < A.parts; p++) s += A.part[((size_t)C.chain * A.parts + p) * 4096 + e];
-        if (j >= A.start_gi && j < A.end_gi && k >= A.start_gi && k < A.end_gi && s < best) {
-            best = s;
-            bidx = e;
+// First minimum of tot over [start, end)^2 (svt_search_one_dual's final loop, EbEncCdef.c:670-679),
+// computed by every workgroup that needs it.  Returns (best, e = j*64 + k) through LDS.
+__device__ void tot_argmin(const uint64_t *tot, int start, int end, uint64_t *bv, int32_t *bi) {
+    const int t    = threadIdx.x;
+    uint64_t  best = (uint64_t)1 << 63; // best_tot_mse initial value (EbEncCdef.c:632)
+    int       idx  = 1 << 30;
+    for (int u = 0; u < 4096 / NT; u++) { // ascending e per lane keeps the first minimum
+        const int      e = u * NT + t, j = e >> 6, k = e & 63;
+        const uint64_t v = tot[e];
+        if (j >= start && j < end && k >= start && k < end && v < best) {
+            best = v;
+            idx  = e;
         }
     }
     bv[t] = best;
-    bi[t] = bidx;
+    bi[t] = idx;
     __syncthreads();
     for (int w = NT / 2; w > 0; w >>= 1) {
-        if (t < w) {
-            const uint64_t ov = bv[t + w];
-            const int      oi = bi[t + w];
-            if (ov < bv[t] || (ov == bv[t] && oi < bi[t])) {
-                bv[t] = ov;
-                bi[t] = oi;
-            }
+        if (t < w && (bv[t + w] < bv[t] || (bv[t + w] == bv[t] && bi[t + w] < bi[t]))) {
+            bv[t] = bv[t + w];
+            bi[t] = bi[t + w];
         }
         __syncthreads();
     }
-    if (t == 0) {
-        int32_t  *l0 = A.lev + C.chain * 32, *l1 = l0 + 16;
-        // a search with no candidate returns (1<<63, 0, 0) like the reference's initial values
-        const bool any = bi[0] < (1 << 30);
-        l0[C.nb_sel] = any ? bi[0] >> 6 : 0;
-        l1[C.nb_sel] = any ? bi[0] & 63 : 0;
-        A.best[C.chain] = any ? bv[0] : ((uint64_t)1 << 63);
-        if (C.shift_after)
-            for (int q = 0; q < C.nb - 1; q++) {
-                l0[q] = l0[q + 1];
-                l1[q] = l1[q + 1];
-            }
+}
+
+// One launch per greedy step: every active chain finishes its previous svt_search_one_dual call
+// (argmin of the previous tot), forms the selection entering this call (append + refinement shift,
+// EbEncCdef.c:714-726) and accumulates this call's tot[j][k] = sum_fb min(best_fb, m0[j] + m1[k]).
+// grid (4 tiles of 16 rows j, FB chunks, chains).  The chunk's mse rows are staged in LDS; lane
+// k = t & 63, wave q owns rows 16*tile + 4*q + {0..3}; partials meet through u64 atomics.
+__global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn[]; // [chunk][128] mse rows + [chunk] best
+    uint64_t (*m)[128] = (uint64_t(*)[128])dyn;
+    __shared__ uint64_t bv[NT];
+    __shared__ int32_t  bi[NT];
+    __shared__ int32_t  sl[32];
+    const StepChain C = A.ch[blockIdx.z];
+    const int t = threadIdx.x, c = C.chain;
+    const int lead = blockIdx.x == 0 && blockIdx.y == 0;
+    if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
+    const int f0 = blockIdx.y * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(A.sb_count - f0, A.chunk);
+    uint64_t *sbest = dyn + (size_t)A.chunk * 128;
+    // 0. start staging this workgroup's FB chunk (independent of the previous call's result)
+    if (nfb > 0) {
+        const uint4 *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
+        uint4       *dst = (uint4 *)dyn;
+        for (int i = t; i < nfb * 64; i += NT) dst[i] = src[i];
     }
+    // 1. selection entering this call
+    if (t < 32) sl[t] = A.step ? A.lev[((size_t)(A.step - 1) * MAX_CHAINS + c) * 32 + t] : 0;
+    if (C.prev_nb_sel >= 0) {
+        tot_argmin(A.tot + ((size_t)((A.step + 2) % 3) * MAX_CHAINS + c) * 4096, A.start_gi, A.end_gi, bv, bi);
+        if (t == 0) {
+            const bool any = bi[0] < (1 << 30); // no candidate: (1 << 63, 0, 0) like the reference
+            sl[C.prev_nb_sel]      = any ? bi[0] >> 6 : 0;
+            sl[16 + C.prev_nb_sel] = any ? bi[0] & 63 : 0;
+            if (C.prev_shift)
+                for (int q = 0; q < C.nb - 1; q++) {
+                    sl[q]      = sl[q + 1];
+                    sl[16 + q] = sl[16 + q + 1];
+                }
+            if (lead && C.nb_sel < 0) A.best[c] = any ? bv[0] : ((uint64_t)1 << 63);
+        }
+    }
+    __syncthreads();
+    if (C.nb_sel < 0) { // the chain's last call has finished: publish its list
+        if (t < 32) A.fin[c * 32 + t] = sl[t];
+        return;
+    }
+    if (lead && t < 32) A.lev[((size_t)A.step * MAX_CHAINS + c) * 32 + t] = sl[t];
+    // 2. zero this workgroup's slice of the accumulator used by the next step
+    {
+        uint64_t *nxt = A.tot + ((size_t)((A.step + 1) % 3) * MAX_CHAINS + c) * 4096;
+        const int nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+        for (int e = wg * NT + t; e < 4096; e += nwg * NT) nxt[e] = 0;
+    }
+    if (nfb <= 0) return;
+    // 3. per-FB best over the selection (EbEncCdef.c:645-651)
+    if (t < nfb) {
+        uint64_t b = (uint64_t)1 << 63;
+        for (int g = 0; g < C.nb_sel; g++) {
+            const uint64_t v = m[t][sl[g]] + m[t][64 + sl[16 + g]];
+            b = v < b ? v : b;
+        }
+        sbest[t] = b;
+    }
+    __syncthreads();
+    // 4. accumulate
+    const int k = t & 63, j0 = 16 * blockIdx.x + 4 * (t >> 6);
+    uint64_t  acc[4] = {0, 0, 0, 0};
+    for (int f = 0; f < nfb; f++) {
+        const uint64_t b = sbest[f], m1k = m[f][64 + k];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t v = m[f][j0 + u] + m1k;
+            acc[u] += v < b ? v : b;
+        }
+    }
+    uint64_t *cur = A.tot + ((size_t)(A.step % 3) * MAX_CHAINS + c) * 4096;
+    if (k >= A.start_gi && k < A.end_gi)
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (j0 + u >= A.start_gi && j0 + u < A.end_gi)
+                atomicAdd((unsigned long long *)&cur[(j0 + u) * 64 + k], (unsigned long long)acc[u]);
 }
 
 // ---- per-FB strength index (EbEncCdef.c:866-890) ----
@@ -185,33 +214,38 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     StepArgs A;
     A.wmse     = wmse;
     A.sb_count = sb_count;
-    A.parts    = std::max(1, std::min(s->pick_parts, (sb_count + 63) / 64));
-    A.chunk    = (sb_count + A.parts - 1) / A.parts;
-    if (A.chunk == 0) A.chunk = 1;
     A.start_gi = 0;
     A.end_gi   = end;
-    A.lev      = s->d_pick_lev;
-    A.part     = wmse + wmse_elems;
+    A.tot      = wmse + wmse_elems;                            // [3][4][4096]
+    A.lev      = s->d_pick_lev;                                // [NSTEPS+1][4][32]
+    A.fin      = s->d_pick_lev + (NSTEPS + 1) * MAX_CHAINS * 32; // [4][32]
     A.best     = s->d_pick_out;
-    HIP_TRY(hipMemsetAsync(s->d_pick_lev, 0, sizeof(int32_t) * MAX_CHAINS * 32, st));
-    for (int step = 0; step < 40; step++) {
+    HIP_TRY(hipMemsetAsync(A.lev, 0, sizeof(int32_t) * (NSTEPS + 2) * MAX_CHAINS * 32, st));
+    HIP_TRY(hipMemsetAsync(A.tot, 0, sizeof(uint64_t) * MAX_CHAINS * 4096, st)); // tot[0]
+    for (int step = 0; step <= NSTEPS; step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {
-            const int nb = 1 << c, len = 5 * nb;
-            if (step >= len) continue;
-            StepChain &C  = A.ch[na++];
-            C.chain       = c;
-            C.nb          = nb;
-            C.nb_sel      = step < nb ? step : nb - 1;
-            C.shift_after = (step + 1 < len) && (step + 1 >= nb);
+            const int nb = 1 << c, len = 5 * nb; // nb calls + 4*nb refinements
+            if (step > len) continue;
+            StepChain &C   = A.ch[na++];
+            C.chain        = c;
+            C.nb           = nb;
+            C.nb_sel       = step < len ? (step < nb ? step : nb - 1) : -1;
+            C.prev_nb_sel  = step == 0 ? -1 : (step - 1 < nb ? step - 1 : nb - 1);
+            C.prev_shift   = step >= 1 && step < len && step >= nb; // shift before calls nb.. (refinements)
         }
-        hipLaunchKernelGGL(sod_partial_kernel, dim3(A.parts, na), dim3(NT), 0, st, A);
-        hipLaunchKernelGGL(sod_reduce_kernel, dim3(na), dim3(NT), 0, st, A);
+        A.step = step;
+        // ~1024 workgroups per step whatever the number of live chains; chunk <= PICK_CHUNK FBs
+        const int want  = std::max(1, 256 / std::max(na, 1));
+        A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_count + want - 1) / std::max(want, 1)));
+        const int parts = std::max(1, (sb_count + A.chunk - 1) / A.chunk);
+        const size_t lds = (size_t)A.chunk * 129 * 8;
+        hipLaunchKernelGGL(sod_step_kernel, dim3(4, parts, na), dim3(NT), lds, st, A);
     }
     HIP_TRY(hipGetLastError());
     int32_t  lev[MAX_CHAINS][2][16];
     uint64_t best[MAX_CHAINS];
-    HIP_TRY(hipMemcpyAsync(lev, s->d_pick_lev, sizeof lev, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(lev, A.fin, sizeof lev, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(best, s->d_pick_out, sizeof best, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 
@@ -240,7 +274,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         gis[j]      = params->cdef_y_strength[j];
         gis[16 + j] = params->cdef_uv_strength[j];
     }
-    int32_t *d_gis = s->d_pick_lev + MAX_CHAINS * 32;
+    int32_t *d_gis = A.fin + MAX_CHAINS * 32;
     HIP_TRY(hipMemcpyAsync(d_gis, gis, sizeof gis, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, nfb, st));
     hipLaunchKernelGGL(pick_assign_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, wmse, s->d_fb_list, d_count, nb,

@@ -5,15 +5,20 @@
 // 8x8 (luma) / 4x4 (chroma) blocks (svt_cdef_filter_fb, EbCdef.c:339) and measure the distortion
 // against the source (compute_cdef_dist, EbCdefProcess.c:87 → EbEncCdef.c:129/175).
 //
-// One workgroup (256 lanes, 4 waves) per FB.  The DLF output tile (+-2 px context, 0x7F7F outside
-// the frame, exactly the samples the reference stages, EbCdefProcess.c:206-236) lives in LDS.
-// Each lane owns two horizontally adjacent pixel PAIRS (4 px).  For a fixed direction the 12 tap
-// differences |p - x| and their signs are strength-independent, so they are computed once per
-// pass and kept in registers as packed int16 pairs; the strength loop is then pure packed-int16
-// VALU (v_pk_lshrrev/sub/max/min/mad: 5 ops per tap pair) — no LDS traffic per strength.
-// Per-8x8 luma statistics (sum d, sum d^2, sum (d-s)^2) reduce over the block's 16 lanes with DPP;
-// the double-precision SSIM-like distortion (EbEncCdef.c:42-47) is evaluated once per
-// (strength, block) in a lane-parallel epilogue.  Chroma SSE reduces through LDS atomics.
+// One workgroup (256 lanes) per FB; the DLF-output tile (+-2 px context, 0x7F7F outside the frame —
+// exactly the samples the reference stages, EbCdefProcess.c:206-236) lives in LDS.
+//
+// Work decomposition (the reason this is fast): the filter output is
+//     y = clamp(x + round(P(pri) + S(sec)), lo, hi)
+// where P sums the 4 primary taps (depends only on the primary strength, adjusted per block) and S
+// the 8 secondary taps (depends only on the secondary strength); lo/hi depend on neither (EbCdef.c:
+// 263-297; int16 sums never wrap for 8/10-bit input).  So per tap-direction set each lane evaluates
+// S once per secondary strength (3) and P once per primary level (<= 16) — 16x4 + 3x8 tap
+// constraints instead of 64x12 — and each of the 64 strengths costs only the rounding, clamp and
+// distortion statistics.  Everything is packed int16 (two samples per VGPR).
+// Lanes own whole rows of 8 samples (4 pairs): a luma 8x8 block is 8 lanes, so its per-strength
+// statistics (sum d, sum d^2, sum (d-s)^2) reduce with 3 DPP steps; the double-precision SSIM-like
+// distortion (EbEncCdef.c:42-47) runs once per (strength, block) in a lane-parallel epilogue.
 #include "cdef_common.h"
 
 #define NT 256
@@ -21,25 +26,25 @@
 #define CT 36 // chroma tile: rows/cols -2..33
 
 struct SearchArgs {
-    const void *rec[3];
-    const void *src[3];
-    int32_t     rstride[3], sstride[3];
-    int32_t     width, height;
-    int32_t     b8_cols, nhfb;
+    const void    *rec[3];
+    const void    *src[3];
+    int32_t        rstride[3], sstride[3];
+    int32_t        width, height;
+    int32_t        b8_cols, nhfb;
     const uint8_t *mask;
-    uint64_t   *mse;   // [2][nfb][64]
-    uint8_t    *skip;  // [nfb]
-    uint8_t    *dir;   // [nfb][64]
-    int32_t    *var;   // [nfb][64]
-    int32_t     nfb, fb0;
-    int32_t     cs, ss, damping;
+    uint64_t      *mse;  // [2][nfb][64]
+    uint8_t       *skip; // [nfb]
+    uint8_t       *dir;  // [nfb][64]
+    int32_t       *var;  // [nfb][64]
+    int32_t        nfb, fb0;
+    int32_t        cs, ss, damping;
     CdefStrengthTable tab;
 };
 
-struct PxPair { // two horizontally adjacent samples, packed int16 (lo = left, hi = right)
+struct PriPair { // two horizontally adjacent samples, packed int16 (lo half = left sample)
     s16x2 x, lo, hi;
-    s16x2 ad[12]; // |tap - x|: [0..1] pri k0 (+,-), [2..3] pri k1, [4..7] sec k0, [8..11] sec k1
-    s16x2 sg[12]; // sign(tap - x) as +-1
+    s16x2 ad[4]; // |p - x| of the primary taps: (k0,+), (k0,-), (k1,+), (k1,-)
+    s16x2 sg[4]; // sign(p - x) as +-1
 };
 
 template <typename T>
@@ -62,17 +67,31 @@ __device__ void stage_tile(uint16_t *tile, int ts, int n, const void *plane, int
     }
 }
 
-// Neighbourhood of the pair at tile position (r, c), (r, c+1) for direction `dir`.
-__device__ __forceinline__ void load_pair(PxPair &P, const uint16_t *tile, int ts, int r, int c, int dir) {
+__device__ __forceinline__ s16x2 splat16(int v) { return (s16x2){(short)v, (short)v}; }
+__device__ __forceinline__ u16x2 splatu16(int v) { return (u16x2){(unsigned short)v, (unsigned short)v}; }
+
+// sign(d) * min(|d|, max(0, thr - (|d| >> shift))) == constrain(d, thr, damping) (EbCdef.c:85-91)
+__device__ __forceinline__ s16x2 constrain2(s16x2 ad, s16x2 sg, s16x2 thr, u16x2 sh) {
+    const s16x2 a = (s16x2)(((u16x2)ad) >> sh);
+    const s16x2 c = __builtin_elementwise_max(thr - a, (s16x2){0, 0});
+    return __builtin_elementwise_min(ad, c) * sg;
+}
+
+// Neighbourhood of the pair at tile (r, c), (r, c+1) for direction `dir`: keeps the primary taps
+// and the clamp range, and returns the secondary sums S[1..3] for the secondary codes in `sec_used`.
+__device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t *tile, int ts, int r, int c,
+                                          int dir, int sec_used, int sdamp, int cs) {
     const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + CDEF_BORDER);
-    const int        xa = (int16_t)p0[0], xb = (int16_t)p0[1];
-    int              loa = xa, hia = xa, lob = xb, hib = xb;
-    const int        ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
+    const int       xa = (int16_t)p0[0], xb = (int16_t)p0[1];
+    int             loa = xa, hia = xa, lob = xb, hib = xb;
+    const int       ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
+    s16x2           sad[8], ssg[8];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        const int o[6] = {cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k), -(cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k)),
-                          cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k), -(cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k)),
-                          cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k), -(cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k))};
+        const int op = cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k);
+        const int o0 = cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k);
+        const int o1 = cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k);
+        const int o[6] = {op, -op, o0, -o0, o1, -o1};
 #pragma unroll
         for (int t = 0; t < 6; t++) {
             const int va = (int16_t)p0[o[t]], vb = (int16_t)p0[o[t] + 1];
@@ -80,65 +99,87 @@ __device__ __forceinline__ void load_pair(PxPair &P, const uint16_t *tile, int t
             if (vb != CDEF_VERY_LARGE_V) hib = max(hib, vb);
             loa = min(loa, va);
             lob = min(lob, vb);
-            const int da = va - xa, db = vb - xb;
-            // slot: pri taps (t<2) -> 2k + t ; sec taps -> 4 + 4k + (t-2)
-            const int slot = t < 2 ? 2 * k + t : 4 + 4 * k + (t - 2);
-            P.ad[slot] = (s16x2){(short)abs(da), (short)abs(db)};
-            P.sg[slot] = (s16x2){(short)(da < 0 ? -1 : 1), (short)(db < 0 ? -1 : 1)};
+            const int   da = va - xa, db = vb - xb;
+            const s16x2 ad = {(short)abs(da), (short)abs(db)};
+            const s16x2 sg = {(short)(da < 0 ? -1 : 1), (short)(db < 0 ? -1 : 1)};
+            if (t < 2) {
+                P.ad[2 * k + t] = ad;
+                P.sg[2 * k + t] = sg;
+            } else {
+                sad[4 * k + t - 2] = ad;
+                ssg[4 * k + t - 2] = sg;
+            }
         }
     }
     P.x  = (s16x2){(short)xa, (short)xb};
     P.lo = (s16x2){(short)loa, (short)lob};
     P.hi = (s16x2){(short)hia, (short)hib};
-}
-
-// Filter one pair with thresholds/shifts broadcast in both halves (EbCdef.c:253-300 in packed form:
-// constrain(d) * tap == sign(d) * min(|d|, max(0, thr - (|d| >> shift))) * tap).
-__device__ __forceinline__ s16x2 filter_pair(const PxPair &P, s16x2 pthr, u16x2 psh, s16x2 sthr, u16x2 ssh, short w0,
-                                             short w1) {
-    const s16x2 z = {0, 0};
-    s16x2       acc[4] = {z, z, z, z};
+    S[0] = (s16x2){0, 0};
 #pragma unroll
-    for (int t = 0; t < 12; t++) {
-        const bool  pri = t < 4;
-        const s16x2 thr = pri ? pthr : sthr;
-        const u16x2 sh  = pri ? psh : ssh;
-        const s16x2 a   = (s16x2)(((u16x2)P.ad[t]) >> sh);
-        const s16x2 c   = __builtin_elementwise_max(thr - a, z);
-        const s16x2 e   = __builtin_elementwise_min(P.ad[t], c);
-        const int   cls = t < 2 ? 0 : t < 4 ? 1 : t < 8 ? 2 : 3;
-        acc[cls]        = acc[cls] + e * P.sg[t];
+    for (int sc = 1; sc < 4; sc++) {
+        S[sc] = (s16x2){0, 0};
+        if (!(sec_used & (1 << sc))) continue; // workgroup-uniform
+        const int   sec = (sc == 3 ? 4 : sc) << cs;
+        const s16x2 thr = splat16(sec);
+        const u16x2 sh  = splatu16(max(0, sdamp - msb32_dev((uint32_t)sec)));
+        s16x2       a0 = {0, 0}, a1 = {0, 0};
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            a0 = a0 + constrain2(sad[t], ssg[t], thr, sh);         // k = 0, tap weight 2
+            a1 = a1 + constrain2(sad[4 + t], ssg[4 + t], thr, sh); // k = 1, tap weight 1
+        }
+        S[sc] = (a0 << (s16x2){1, 1}) + a1;
     }
-    const s16x2 sum = acc[0] * (s16x2){w0, w0} + acc[1] * (s16x2){w1, w1} + (acc[2] << (s16x2){1, 1}) + acc[3];
-    const s16x2 rnd = (sum + (s16x2){8, 8} + (sum >> (s16x2){15, 15})) >> (s16x2){4, 4};
-    const s16x2 y   = P.x + rnd;
-    return __builtin_elementwise_max(__builtin_elementwise_min(y, P.hi), P.lo);
 }
 
-__device__ __forceinline__ s16x2 splat16(int v) { return (s16x2){(short)v, (short)v}; }
-__device__ __forceinline__ u16x2 splatu16(int v) { return (u16x2){(unsigned short)v, (unsigned short)v}; }
+// primary sum for threshold `thr` (already strength-adjusted), weights {4,2} or {3,3}
+__device__ __forceinline__ s16x2 pri_sum(const PriPair &P, s16x2 thr, u16x2 sh, s16x2 w0, s16x2 w1) {
+    const s16x2 k0 = constrain2(P.ad[0], P.sg[0], thr, sh) + constrain2(P.ad[1], P.sg[1], thr, sh);
+    const s16x2 k1 = constrain2(P.ad[2], P.sg[2], thr, sh) + constrain2(P.ad[3], P.sg[3], thr, sh);
+    return k0 * w0 + k1 * w1;
+}
+
+// y = clamp(x + ((8 + sum - (sum < 0)) >> 4), lo, hi)   (EbCdef.c:298)
+__device__ __forceinline__ s16x2 finish(const PriPair &P, s16x2 sum) {
+    const s16x2 rnd = (sum + (s16x2){8, 8} + (sum >> (s16x2){15, 15})) >> (s16x2){4, 4};
+    return __builtin_elementwise_max(__builtin_elementwise_min(P.x + rnd, P.hi), P.lo);
+}
+
+// sum over the 8 lanes of each aligned octet (quad xor1, quad xor2, row_half_mirror)
+__device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return v;
+}
 
 template <typename T>
 __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     __shared__ uint16_t ltile[LT * LT];
     __shared__ uint16_t ctile[2][CT * CT];
-    __shared__ uint32_t stats[64][16][3];  // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
-    __shared__ uint32_t sstat[64][2];      // per block source sum, sum^2 (luma)
-    __shared__ uint64_t acc_l[64];         // per gi luma distortion
-    __shared__ uint32_t acc_c[2][64];      // per gi chroma SSE per plane
+    __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
+    __shared__ uint32_t sstat[64][2];     // per block source sum, sum^2 (luma)
+    __shared__ uint64_t acc_l[64];        // per gi luma distortion
+    __shared__ uint32_t acc_c[2][64];     // per gi chroma SSE per plane
     __shared__ int32_t  dcost[64][8];
     __shared__ uint8_t  sdir[64];
     __shared__ int32_t  svar[64];
     __shared__ uint8_t  slisted[64];
     __shared__ int32_t  nlisted;
+    __shared__ CdefGroupTable grp[4]; // luma A, luma B, chroma A, chroma B
 
     const int fb = A.fb0 + blockIdx.x;
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cs = A.cs;
 
-    // ---- block list (svt_sb_compute_cdef_list, EbEncCdef.c:238-282) ----
+    // ---- block list (svt_sb_compute_cdef_list, EbEncCdef.c:238-282) + strength tables ----
     if (tid == 0) nlisted = 0;
+    {
+        const int32_t *src = (const int32_t *)&A.tab.luma[0];
+        int32_t       *dst = (int32_t *)&grp[0];
+        for (int i = tid; i < (int)(sizeof(grp) / 4); i += NT) dst[i] = src[i];
+    }
     __syncthreads();
     if (tid < 64) {
         const int by = tid >> 3, bx = tid & 7;
@@ -155,10 +196,10 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     if (nlisted == 0) { // EbCdefProcess.c:209-212
         if (tid == 0) A.skip[fb] = 1;
         if (tid < 64) {
-            A.mse[(size_t)fb * 64 + tid]         = 0;
+            A.mse[(size_t)fb * 64 + tid]           = 0;
             A.mse[((size_t)A.nfb + fb) * 64 + tid] = 0;
-            A.dir[(size_t)fb * 64 + tid]         = 0;
-            A.var[(size_t)fb * 64 + tid]         = 0;
+            A.dir[(size_t)fb * 64 + tid]           = 0;
+            A.var[(size_t)fb * 64 + tid]           = 0;
         }
         return;
     }
@@ -237,90 +278,91 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
 
     const int ldamp = A.damping + cs, cdamp = A.damping + cs - 1;
     const int ss    = A.ss;
-    const CdefStrengthTable &tab = A.tab;
+    const int nstr  = A.tab.nstr;
 
-    // ================= luma: 4 passes of 16 blocks =================
-    for (int pass = 0; pass < 4; pass++) {
-        const int bip = 4 * wave + (lane >> 4); // block in pass
-        const int b = 16 * pass + bip, by = b >> 3, bx = b & 7;
-        const int q = lane & 15, row = q >> 1, col0 = (q & 1) * 4;
-        const int r = 8 * by + row, c = 8 * bx + col0;
-        const bool listed = slisted[b];
-        const bool valid = listed && (row % ss == 0);
-        const uint32_t vmask = valid ? 0xFFFFFFFFu : 0u;
-        // source samples (registers), zeroed outside the measured set
-        s16x2 sp[2] = {{0, 0}, {0, 0}};
+    // ================= luma: 2 passes of 32 blocks; lane = one 8-sample row =================
+    for (int pass = 0; pass < 2; pass++) {
+        const int bip = tid >> 3, row = tid & 7; // block in pass, row in block
+        const int b = 32 * pass + bip, by = b >> 3, bx = b & 7;
+        const int r = 8 * by + row, c0 = 8 * bx;
+        const bool valid = slisted[b] && (row % ss == 0);
+        const unsigned short vm = valid ? 0xFFFF : 0;
+        // source row (registers), zeroed outside the measured set
+        s16x2 sp[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         if (valid) {
-            const long o = (long)(64 * fbr + r) * A.sstride[0] + 64 * fbc + c;
-            sp[0] = (s16x2){(short)ld_px<T>(A.src[0], o), (short)ld_px<T>(A.src[0], o + 1)};
-            sp[1] = (s16x2){(short)ld_px<T>(A.src[0], o + 2), (short)ld_px<T>(A.src[0], o + 3)};
+            const long o = (long)(64 * fbr + r) * A.sstride[0] + 64 * fbc + c0;
+#pragma unroll
+            for (int h = 0; h < 4; h++)
+                sp[h] = (s16x2){(short)ld_px<T>(A.src[0], o + 2 * h), (short)ld_px<T>(A.src[0], o + 2 * h + 1)};
         }
         {
             uint32_t s1 = 0, s2 = 0;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
+            for (int h = 0; h < 4; h++) {
                 s1 = __builtin_amdgcn_udot2((u16x2)sp[h], (u16x2){1, 1}, s1, false);
                 s2 = __builtin_amdgcn_udot2((u16x2)sp[h], (u16x2)sp[h], s2, false);
             }
-            s1 = row16_sum(s1);
-            s2 = row16_sum(s2);
-            if (q == 0) {
+            s1 = oct_sum(s1);
+            s2 = oct_sum(s2);
+            if (row == 0) {
                 sstat[b][0] = s1;
                 sstat[b][1] = s2;
             }
         }
-        const int   vb = svar[b];
-        const int   ib = (vb >> 6) ? min(msb32_dev((uint32_t)(vb >> 6)), 12) : 0;
-        PxPair P[2];
-        for (int grp = 0; grp < 2; grp++) {
-            const int     n   = grp ? tab.n_luma_b : tab.n_luma_a;
-            const int8_t *lst = grp ? tab.luma_b : tab.luma_a;
-            if (n == 0) continue;
-            const int d = grp ? sdir[b] : 0;
-            load_pair(P[0], ltile, LT, r, c, d);
-            load_pair(P[1], ltile, LT, r, c + 2, d);
-            for (int k = 0; k < n; k++) {
-                const int gi = lst[k];
-                const int code = tab.code[gi];
-                const int level = code >> 2;
-                int       sec = code & 3;
-                sec += sec == 3;
-                const int pri  = level << cs;
-                const int t    = vb ? (pri * (4 + ib) + 8) >> 4 : 0; // adjust_strength
-                const int secs = sec << cs;
-                const int psh  = max(0, ldamp - msb32_dev((uint32_t)t));
-                const int ssh  = max(0, ldamp - msb32_dev((uint32_t)secs));
-                const int odd  = (t >> cs) & 1;
-                uint32_t sd = 0, sd2 = 0, sse = 0;
+        const int vb = svar[b];
+        const int ib = (vb >> 6) ? min(msb32_dev((uint32_t)(vb >> 6)), 12) : 0;
+        for (int g = 0; g < 2; g++) {
+            const CdefGroupTable &G = grp[g];
+            if (G.nlv == 0) continue;
+            const int d = g ? sdir[b] : 0; // pri_strength ? dir : 0 (EbCdef.c:404)
+            PriPair   P[4];
+            s16x2     S[4][4];
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    s16x2 y = filter_pair(P[h], splat16(t), splatu16(psh), splat16(secs), splatu16(ssh),
-                                          (short)(odd ? 3 : 4), (short)(odd ? 3 : 2));
-                    y                = (s16x2)((u16x2)y & (u16x2){(unsigned short)vmask, (unsigned short)vmask});
-                    const s16x2 diff = y - sp[h];
-                    sd  = __builtin_amdgcn_udot2((u16x2)y, (u16x2){1, 1}, sd, false);
-                    sd2 = __builtin_amdgcn_udot2((u16x2)y, (u16x2)y, sd2, false);
-                    sse = (uint32_t)__builtin_amdgcn_sdot2(diff, diff, (int)sse, false);
-                }
-                sd  = row16_sum(sd);
-                sd2 = row16_sum(sd2);
-                sse = row16_sum(sse);
-                if (q == 0) {
-                    stats[gi][bip][0] = sd;
-                    stats[gi][bip][1] = sd2;
-                    stats[gi][bip][2] = sse;
+            for (int h = 0; h < 4; h++) load_pair(P[h], S[h], ltile, LT, r, c0 + 2 * h, d, G.sec_used, ldamp, cs);
+            for (int li = 0; li < G.nlv; li++) {
+                const int pri = G.lv[li] << cs;
+                const int t   = vb ? (pri * (4 + ib) + 8) >> 4 : 0; // adjust_strength (EbCdef.c:130-135)
+                const int odd = (t >> cs) & 1;
+                const s16x2 thr = splat16(t);
+                const u16x2 sh  = splatu16(max(0, ldamp - msb32_dev((uint32_t)t)));
+                const s16x2 w0 = splat16(odd ? 3 : 4), w1 = splat16(odd ? 3 : 2);
+                s16x2 Pv[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) Pv[h] = pri_sum(P[h], thr, sh, w0, w1);
+#pragma unroll
+                for (int sc = 0; sc < 4; sc++) {
+                    const int gi = G.gi[li][sc];
+                    if (gi < 0) continue; // workgroup-uniform
+                    uint32_t sd = 0, sd2 = 0, sse = 0;
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        s16x2 y = finish(P[h], Pv[h] + S[h][sc]);
+                        y       = (s16x2)((u16x2)y & (u16x2){vm, vm});
+                        const s16x2 df = y - sp[h];
+                        sd  = __builtin_amdgcn_udot2((u16x2)y, (u16x2){1, 1}, sd, false);
+                        sd2 = __builtin_amdgcn_udot2((u16x2)y, (u16x2)y, sd2, false);
+                        sse = (uint32_t)__builtin_amdgcn_sdot2(df, df, (int)sse, false);
+                    }
+                    sd  = oct_sum(sd);
+                    sd2 = oct_sum(sd2);
+                    sse = oct_sum(sse);
+                    if (row == 0) {
+                        stats[gi][bip][0] = sd;
+                        stats[gi][bip][1] = sd2;
+                        stats[gi][bip][2] = sse;
+                    }
                 }
             }
         }
         __syncthreads();
-        // double-precision distortion per (gi, block): 4 lanes per gi, 4 blocks per lane
+        // double-precision distortion per (gi, block): 4 lanes per gi, 8 blocks per lane
         {
             const int gi = tid >> 2, sub = tid & 3;
             unsigned long long acc = 0;
-            if (gi < tab.nstr) {
+            if (gi < nstr && A.tab.alias[gi] < 0) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int bb = 4 * sub + u, bg = 16 * pass + bb;
+                for (int u = 0; u < 8; u++) {
+                    const int bb = 8 * sub + u, bg = 32 * pass + bb;
                     if (!slisted[bg]) continue;
                     acc += cdef_luma_dist(stats[gi][bb][0], sstat[bg][0], stats[gi][bb][1], sstat[bg][1],
                                           stats[gi][bb][2], cs);
@@ -328,52 +370,61 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
             }
             acc += __shfl_xor(acc, 1);
             acc += __shfl_xor(acc, 2);
-            if (sub == 0 && gi < tab.nstr) acc_l[gi] += acc;
+            if (sub == 0 && gi < nstr) acc_l[gi] += acc;
         }
         __syncthreads();
     }
 
-    // ================= chroma: one pass per plane =================
-    for (int pl = 0; pl < 2; pl++) {
-        const int cb = tid >> 2, by = cb >> 3, bx = cb & 7, row = tid & 3;
-        const int r = 4 * by + row, c = 4 * bx;
-        const bool valid = slisted[cb];
-        s16x2 sp[2] = {{0, 0}, {0, 0}};
-        if (valid) {
-            const long o = (long)(32 * fbr + r) * A.sstride[1 + pl] + 32 * fbc + c;
-            sp[0] = (s16x2){(short)ld_px<T>(A.src[1 + pl], o), (short)ld_px<T>(A.src[1 + pl], o + 1)};
-            sp[1] = (s16x2){(short)ld_px<T>(A.src[1 + pl], o + 2), (short)ld_px<T>(A.src[1 + pl], o + 3)};
-        }
-        const uint32_t vmask = valid ? 0xFFFFFFFFu : 0u;
-        PxPair P[2];
-        for (int grp = 0; grp < 2; grp++) {
-            const int     n   = grp ? tab.n_chroma_b : tab.n_chroma_a;
-            const int8_t *lst = grp ? tab.chroma_b : tab.chroma_a;
-            if (n == 0) continue;
-            const int d = grp ? sdir[cb] : 0;
-            load_pair(P[0], ctile[pl], CT, r, c, d);
-            load_pair(P[1], ctile[pl], CT, r, c + 2, d);
-            for (int k = 0; k < n; k++) {
-                const int gi = lst[k];
-                const int code = tab.code[gi];
-                int       sec = code & 3;
-                sec += sec == 3;
-                const int pri  = (code >> 2) << cs;
-                const int secs = sec << cs;
-                const int psh  = max(0, cdamp - msb32_dev((uint32_t)pri));
-                const int ssh  = max(0, cdamp - msb32_dev((uint32_t)secs));
-                const int odd  = (pri >> cs) & 1;
-                uint32_t sse = 0;
+    // ================= chroma: both planes in one pass; lane = one 8-sample row =================
+    {
+        const int pl = tid >> 7, q = tid & 127, r = q >> 2, c0 = (q & 3) * 8;
+        const int by = r >> 2;
+        const uint16_t *tile = ctile[pl];
+        s16x2 sp[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+        unsigned short vm[4];
+        int  dirb[4];
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    s16x2 y = filter_pair(P[h], splat16(pri), splatu16(psh), splat16(secs), splatu16(ssh),
-                                          (short)(odd ? 3 : 4), (short)(odd ? 3 : 2));
-                    y                = (s16x2)((u16x2)y & (u16x2){(unsigned short)vmask, (unsigned short)vmask});
-                    const s16x2 diff = y - sp[h];
-                    sse = (uint32_t)__builtin_amdgcn_sdot2(diff, diff, (int)sse, false);
+        for (int h = 0; h < 4; h++) {
+            const int cb = by * 8 + ((c0 + 2 * h) >> 2);
+            vm[h]   = slisted[cb] ? 0xFFFF : 0;
+            dirb[h] = sdir[cb];
+            if (slisted[cb]) {
+                const long o = (long)(32 * fbr + r) * A.sstride[1 + pl] + 32 * fbc + c0 + 2 * h;
+                sp[h] = (s16x2){(short)ld_px<T>(A.src[1 + pl], o), (short)ld_px<T>(A.src[1 + pl], o + 1)};
+            }
+        }
+        for (int g = 0; g < 2; g++) {
+            const CdefGroupTable &G = grp[2 + g];
+            if (G.nlv == 0) continue;
+            PriPair P[4];
+            s16x2   S[4][4];
+#pragma unroll
+            for (int h = 0; h < 4; h++)
+                load_pair(P[h], S[h], tile, CT, r, c0 + 2 * h, g ? dirb[h] : 0, G.sec_used, cdamp, cs);
+            for (int li = 0; li < G.nlv; li++) {
+                const int pri = G.lv[li] << cs; // no strength adjustment for chroma (EbCdef.c:401)
+                const int odd = (pri >> cs) & 1;
+                const s16x2 thr = splat16(pri);
+                const u16x2 sh  = splatu16(max(0, cdamp - msb32_dev((uint32_t)pri)));
+                const s16x2 w0 = splat16(odd ? 3 : 4), w1 = splat16(odd ? 3 : 2);
+                s16x2 Pv[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) Pv[h] = pri_sum(P[h], thr, sh, w0, w1);
+#pragma unroll
+                for (int sc = 0; sc < 4; sc++) {
+                    const int gi = G.gi[li][sc];
+                    if (gi < 0) continue;
+                    uint32_t sse = 0;
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        s16x2 y = finish(P[h], Pv[h] + S[h][sc]);
+                        y       = (s16x2)((u16x2)y & (u16x2){vm[h], vm[h]});
+                        const s16x2 df = y - sp[h];
+                        sse = (uint32_t)__builtin_amdgcn_sdot2(df, df, (int)sse, false);
+                    }
+                    sse = row16_sum(sse);
+                    if ((lane & 15) == 0) atomicAdd(&acc_c[pl][gi], sse);
                 }
-                sse = row16_sum(sse);
-                if ((lane & 15) == 0) atomicAdd(&acc_c[pl][gi], sse);
             }
         }
     }
@@ -383,13 +434,14 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     if (tid < 64) {
         const int gi = tid;
         uint64_t  m0 = 0, m1 = 0;
-        if (gi < tab.nstr) {
-            m0 = (acc_l[gi] >> (2 * cs)) * (uint64_t)ss;
-            m1 = tab.uv_on[gi] ? ((uint64_t)(acc_c[0][gi] >> (2 * cs)) + (uint64_t)(acc_c[1][gi] >> (2 * cs)))
-                               : 1040400ull * 64; // default_mse_uv * 64
+        if (gi < nstr) {
+            const int src = A.tab.alias[gi] < 0 ? gi : A.tab.alias[gi];
+            m0 = (acc_l[src] >> (2 * cs)) * (uint64_t)ss;
+            m1 = A.tab.uv_on[gi] ? ((uint64_t)(acc_c[0][src] >> (2 * cs)) + (uint64_t)(acc_c[1][src] >> (2 * cs)))
+                                 : 1040400ull * 64; // default_mse_uv * 64
         }
-        A.mse[(size_t)fb * 64 + gi]             = m0;
-        A.mse[((size_t)A.nfb + fb) * 64 + gi]   = m1;
+        A.mse[(size_t)fb * 64 + gi]           = m0;
+        A.mse[((size_t)A.nfb + fb) * 64 + gi] = m1;
         if (tid == 0) A.skip[fb] = 0;
     }
 }
@@ -418,10 +470,11 @@ int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon,
     A.ss      = subsampling;
     A.damping = damping;
     A.tab     = *tab;
+    const dim3 grid((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb);
     if (recon->bit_depth > 8)
-        hipLaunchKernelGGL(cdef_search_kernel<uint16_t>, dim3((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb), dim3(NT), 0, st, A);
+        hipLaunchKernelGGL(cdef_search_kernel<uint16_t>, grid, dim3(NT), 0, st, A);
     else
-        hipLaunchKernelGGL(cdef_search_kernel<uint8_t>, dim3((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb), dim3(NT), 0, st, A);
+        hipLaunchKernelGGL(cdef_search_kernel<uint8_t>, grid, dim3(NT), 0, st, A);
     HIP_TRY(hipGetLastError());
     return SVTGPU_OK;
 }

@@ -90,16 +90,22 @@ struct SvtGpuCdefFrameState {
     uint8_t       *own_skip;
 };
 
-// device-side views of the search strength lists (built on the host from SvtGpuCdefControls)
+// Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
+// The CDEF tap sum splits into a primary part that depends only on the primary strength and a
+// secondary part that depends only on the secondary strength (EbCdef.c:263-297), so strengths are
+// grouped by (tap direction set, primary level) and the secondary sums are shared.
+struct CdefGroupTable {  // strengths evaluated with one tap-direction set
+    int32_t nlv;         // number of primary levels in the group
+    int32_t sec_used;    // bitmask of secondary codes (1..3) used by the group
+    int32_t lv[16];      // primary levels
+    int32_t gi[16][4];   // gi of (level idx, secondary code) or -1
+};
 struct CdefStrengthTable {
-    int32_t nstr;          // total strengths searched (first + second pass)
-    int32_t n_luma_a;      // luma strengths with pri level 0 (direction 0 taps)
-    int32_t n_luma_b;      // luma strengths with pri level != 0 (block direction taps)
-    int32_t n_chroma_a, n_chroma_b;
-    int8_t  luma_a[64], luma_b[64];     // gi lists
-    int8_t  chroma_a[64], chroma_b[64]; // gi lists (chroma-enabled strengths only)
-    uint8_t code[64];                   // gi -> pri*4+sec strength code
-    uint8_t uv_on[64];                  // gi -> chroma tested
+    int32_t        nstr;      // total strengths searched (first + second pass)
+    CdefGroupTable luma[2];   // [0]: primary level 0 (direction-0 taps), [1]: block direction
+    CdefGroupTable chroma[2]; // same, chroma-tested strengths only
+    uint8_t        uv_on[64]; // gi -> chroma tested
+    int8_t         alias[64]; // gi -> earlier gi with the same strength code (or -1)
 };
 
 // ---------------------------------------------------------------------------------------------
