@@ -195,6 +195,100 @@ int svtgpu_cdef_read_state(SvtGpuCdefFrameState *s, uint64_t *mse, uint8_t *skip
 /* Device pointer of the [2][nfb][64] uint64 mse table (for RCCL gathers across tiles). */
 void *svtgpu_cdef_mse_device_ptr(SvtGpuCdefFrameState *s);
 
+/* ---------------------------------------------------------------------------------------------
+ * Deblocking loop filter — per-segment RTCD shims (host pointers, synchronous).
+ * Each filters one 4-sample edge segment exactly like the reference C (EbDeblockingCommon.c).
+ * ------------------------------------------------------------------------------------------- */
+/* replace svt_aom_lpf_{horizontal,vertical}_{4,6,8,14} (common_dsp_rtcd.h:1116-1131) */
+void svtgpu_lpf_horizontal_4(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                             const uint8_t *thresh);
+void svtgpu_lpf_horizontal_6(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                             const uint8_t *thresh);
+void svtgpu_lpf_horizontal_8(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                             const uint8_t *thresh);
+void svtgpu_lpf_horizontal_14(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                              const uint8_t *thresh);
+void svtgpu_lpf_vertical_4(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                           const uint8_t *thresh);
+void svtgpu_lpf_vertical_6(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                           const uint8_t *thresh);
+void svtgpu_lpf_vertical_8(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                           const uint8_t *thresh);
+void svtgpu_lpf_vertical_14(uint8_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                            const uint8_t *thresh);
+/* replace svt_aom_highbd_lpf_{horizontal,vertical}_{4,6,8,14} (common_dsp_rtcd.h:1132-1146) */
+void svtgpu_highbd_lpf_horizontal_4(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                    const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_horizontal_6(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                    const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_horizontal_8(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                    const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_horizontal_14(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                     const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_vertical_4(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                  const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_vertical_6(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                  const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_vertical_8(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                  const uint8_t *thresh, int32_t bd);
+void svtgpu_highbd_lpf_vertical_14(uint16_t *s, int32_t pitch, const uint8_t *blimit, const uint8_t *limit,
+                                   const uint8_t *thresh, int32_t bd);
+
+/* ---------------------------------------------------------------------------------------------
+ * Deblocking loop filter — frame level (device-resident, in place)
+ * ------------------------------------------------------------------------------------------- */
+/* One record per 4x4 mode-info unit (mi), raster order, mi_rows x mi_cols (mi = 4 luma samples;
+ * frame dimensions rounded up to 8).  The MbModeInfo fields set_lpf_parameters reads
+ * (EbDeblockingFilter.c:162-282); values are the reference's enums (BlockSize, PredictionMode,
+ * MvReferenceFrame with INTRA_FRAME = 0). */
+typedef struct SvtGpuLfMi {
+    uint8_t bsize;      /* block_mi.bsize */
+    uint8_t tx_depth;   /* block_mi.tx_depth (0..2) */
+    uint8_t skip;       /* block_mi.skip */
+    int8_t  ref_frame0; /* block_mi.ref_frame[0] */
+    uint8_t mode;       /* block_mi.mode */
+    uint8_t segment_id; /* block_mi.segment_id */
+    uint8_t pad[2];
+} SvtGpuLfMi;
+
+/* Frame loop-filter parameters: struct LoopFilter (EbDefinitions.h:1903-1920) + the segmentation
+ * feature arrays (EbSegmentationParams.h:49-53) the level table depends on.  delta_lf is not
+ * supported (delta_lf_present = 0). */
+typedef struct SvtGpuLfParams {
+    int32_t filter_level[2]; /* luma: [0] vertical edges, [1] horizontal edges */
+    int32_t filter_level_u;
+    int32_t filter_level_v;
+    int32_t sharpness_level;
+    uint8_t mode_ref_delta_enabled;
+    int8_t  ref_deltas[8];
+    int8_t  mode_deltas[2];
+    uint8_t segmentation_enabled;
+    int16_t seg_feature_data[8][8];    /* [segment][SEG_LVL_*] */
+    int16_t seg_feature_enabled[8][8]; /* [segment][SEG_LVL_*] */
+} SvtGpuLfParams;
+
+typedef struct SvtGpuDlfState SvtGpuDlfState;
+int  svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuDlfState **out);
+void svtgpu_dlf_state_destroy(SvtGpuDlfState *s);
+/* upload the mi grid ((h+7)/8*2 rows x (w+7)/8*2 cols records) */
+int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream);
+/* ≙ svt_av1_loop_filter_frame(frame, pcs, plane_start, plane_end) (EbDeblockingFilter.c:624-653):
+ * all vertical edges of each plane, then all horizontal edges (equivalent to the reference's
+ * SB-lagged order with combine_vert_horz_lf = 1, :41, :580-605), in place on `frame`. */
+int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params, int32_t plane_start,
+                     int32_t plane_end, void *stream);
+/* ≙ svt_av1_pick_filter_level(LPF_PICK_FROM_FULL_IMAGE) (EbDeblockingFilter.c:1129-1252): bisection
+ * on the filter level per plane with a device trial per level (filter + SSE vs `source` + restore).
+ * `params` carries the previous levels in and the picked levels out; `recon` is left unfiltered.
+ * dlf_avg_uv/temporal_layer_index select the reference's "use averaged chroma levels" shortcut.
+ * Synchronous. */
+int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source, SvtGpuLfParams *params,
+                    int32_t dlf_avg, int32_t dlf_avg_uv, int32_t temporal_layer_index,
+                    int32_t early_exit_convergence, int32_t tx_mode_only_4x4, void *stream);
+/* Σ (a - b)^2 over one plane (svt_spatial_full_distortion_kernel / svt_full_distortion_kernel16_bits
+ * over the frame, EbDeblockingFilter.c:716-838). Synchronous. */
+int svtgpu_plane_sse(const SvtGpuFrame *a, const SvtGpuFrame *b, int32_t plane, uint64_t *sse, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

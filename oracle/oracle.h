@@ -1,5 +1,5 @@
 /*
- * oracle.h — CPU restatement of the reference's CDEF hot path.  TEST INFRASTRUCTURE ONLY.
+ * oracle.h — CPU restatement of the reference's CDEF + deblocking hot path.  TEST INFRASTRUCTURE ONLY.
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this code, and
  * only as the checker / CPU baseline — never as the product path.  Each function cites the
@@ -55,6 +55,18 @@ int oracle_cdef_pick(int32_t width, int32_t height, const uint64_t *mse, const u
 int oracle_cdef_apply_frame(const OracleFrame *recon, OracleFrame *out, const uint8_t *block_mask,
                             const uint8_t *dir, const int32_t *var, const SvtGpuCdefParams *params,
                             const int8_t *fb_strength);
+
+/* ---- deblocking (dlf_oracle.c) ---- */
+/* one 4-sample edge segment: vertical = filter across a vertical edge; len in {4, 6, 8, 14} */
+void oracle_lpf(uint8_t *s, int32_t pitch, int vertical, int len, const uint8_t *blimit, const uint8_t *limit,
+                const uint8_t *thresh);
+void oracle_highbd_lpf(uint16_t *s, int32_t pitch, int vertical, int len, const uint8_t *blimit,
+                       const uint8_t *limit, const uint8_t *thresh, int32_t bd);
+/* mi: [mi_rows][mi_cols] with mi_cols = ((w+7)&~7)/4; filters planes [plane_start, plane_end) in place */
+int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end);
+/* level search; p in = last-frame levels (already averaged when dlf_avg), out = picked levels */
+int oracle_dlf_pick(OracleFrame *recon, const OracleFrame *src, const SvtGpuLfMi *mi, SvtGpuLfParams *p, int dlf_avg,
+                    int dlf_avg_uv, int temporal_layer_index, int early_exit, int only4x4);
 
 #ifdef __cplusplus
 }

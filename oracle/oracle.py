@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
-from svtgpu import CdefControls, CdefParams, CdefList  # noqa: E402  (shared C struct layouts)
+from svtgpu import CdefControls, CdefParams, CdefList, LfParams, LF_MI_DTYPE  # noqa: E402  (shared C struct layouts)
 
 
 class OracleFrame(ctypes.Structure):
@@ -42,6 +42,13 @@ _SIGS = {
                                         ctypes.POINTER(CdefParams), _P]),
     "oracle_cdef_apply_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P, _P, _P,
                                                ctypes.POINTER(CdefParams), _P]),
+    "oracle_lpf": (None, [_P, _I32, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
+    "oracle_highbd_lpf": (None, [_P, _I32, ctypes.c_int, ctypes.c_int, _P, _P, _P, _I32]),
+    "oracle_dlf_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), _P, ctypes.POINTER(LfParams), ctypes.c_int,
+                                        ctypes.c_int]),
+    "oracle_dlf_pick": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
+                                       ctypes.POINTER(LfParams), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int]),
 }
 _lib = None
 
@@ -122,3 +129,56 @@ def cdef_apply_frame(rec, bd, mask, d, v, params, fbs):
                                   ptr(np.ascontiguousarray(v)), ctypes.byref(params),
                                   ptr(np.ascontiguousarray(fbs, np.int8)))
     return outp
+
+
+def _mi(mi, h, w):
+    a = np.ascontiguousarray(mi)
+    if a.dtype != LF_MI_DTYPE:
+        a = np.ascontiguousarray(a.astype(np.uint8))
+    assert a.nbytes == (((h + 7) & ~7) >> 2) * (((w + 7) & ~7) >> 2) * 8
+    return a
+
+
+def lpf_lines(lines, bd, fn, blimit, limit, thresh, lowbd=False):
+    """Apply one edge filter to 4 sample lines of 16 (edge between 7 and 8).  fn: 0..3 horizontal
+    4/6/8/14, 4..7 vertical.  Returns the filtered lines (the C is run on a 16x16 window)."""
+    vertical = fn >= 4
+    n = (4, 6, 8, 14)[fn & 3]
+    win = np.zeros((16, 16), np.uint8 if lowbd else np.uint16)
+    for i in range(4):
+        if vertical:
+            win[8 + i, :] = lines[i]
+        else:
+            win[:, 8 + i] = lines[i]
+    th = [np.full(16, v, np.uint8) for v in (blimit, limit, thresh)]
+    base = win.ctypes.data + (8 * 16 + 8) * win.itemsize
+    if lowbd:
+        lib().oracle_lpf(base, 16, int(vertical), n, *[ptr(t) for t in th])
+    else:
+        lib().oracle_highbd_lpf(base, 16, int(vertical), n, *[ptr(t) for t in th], bd)
+    return np.stack([win[8 + i, :] if vertical else win[:, 8 + i] for i in range(4)]).astype(np.uint16)
+
+
+def dlf_frame(planes, bd, mi, params, plane_start=0, plane_end=3):
+    """svt_av1_loop_filter_frame restatement; returns filtered copies of the planes."""
+    keep = []
+    out = [np.array(p, copy=True) for p in planes]
+    F = _frame(out, bd, keep)
+    m = _mi(mi, *planes[0].shape)
+    rc = lib().oracle_dlf_frame(ctypes.byref(F), ptr(m), ctypes.byref(params), plane_start, plane_end)
+    assert rc == 0
+    return out
+
+
+def dlf_pick(rec, src, bd, mi, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=2, only_4x4=0):
+    """svt_av1_pick_filter_level (full image) restatement; returns the picked LfParams."""
+    keep = []
+    work = [np.array(p, copy=True) for p in rec]
+    R, S = _frame(work, bd, keep), _frame(src, bd, keep)
+    p = LfParams()
+    ctypes.pointer(p)[0] = params
+    m = _mi(mi, *rec[0].shape)
+    rc = lib().oracle_dlf_pick(ctypes.byref(R), ctypes.byref(S), ptr(m), ctypes.byref(p), dlf_avg, dlf_avg_uv,
+                               temporal_layer_index, early_exit, only_4x4)
+    assert rc == 0
+    return p

@@ -17,13 +17,15 @@ CFLAGS   := -O2 -fPIC -ffunction-sections -fdata-sections -DARCH_X86_64=1 -w $(I
 # reference C sources (semantic definitions of the kernels)
 REF_C    := Lib/Common/Codec/EbCdef.c Lib/Encoder/Codec/EbEncCdef.c Lib/Common/Codec/common_dsp_rtcd.c \
             Lib/Encoder/Codec/aom_dsp_rtcd.c Lib/Common/Codec/EbUtility.c
+DLF_C    := Lib/Common/Codec/EbDeblockingCommon.c Lib/Encoder/Codec/EbDeblockingFilter.c
 # reference AVX2 sources (the CPU baseline the north star names)
 REF_AVX2 := Lib/Common/ASM_AVX2/cdef_block_avx2.c Lib/Encoder/ASM_AVX2/EbCdef_AVX2.c
 
 C_OBJ    := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_C))
+DLF_OBJ  := $(patsubst %.c,$(OUT)/obj/%.o,$(DLF_C))
 AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
 
-all: $(OUT)/gen_golden_cdef
+all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/%.o: $(S)/%.c
@@ -31,6 +33,9 @@ $(OUT)/obj/%.o: $(S)/%.c
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(OUT)/gen_golden_cdef: oracle/ref_harness/gen_golden_cdef.c $(C_OBJ)
+	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
+
+$(OUT)/gen_golden_dlf: oracle/ref_harness/gen_golden_dlf.c $(DLF_OBJ) $(C_OBJ)
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
 
 $(OUT)/ref_cdef_bench: oracle/ref_harness/ref_cdef_bench.c $(C_OBJ) $(AVX2_OBJ)

@@ -1,0 +1,719 @@
+// dlf.hip — AV1 deblocking loop filter on gfx950: frame apply and full-image level search.
+//
+// Reference path (GabrielGao0310/SVT-av1_pro-anchor-v2.1.0-, Source/Lib/):
+//   edge filters       Common/Codec/EbDeblockingCommon.c:141-373, 436-865 (lpf 4/6/8/14, 8-bit + highbd)
+//   edge parameters    Encoder/Codec/EbDeblockingFilter.c:143-282 (get_transform_size, set_lpf_parameters)
+//   level tables       Common/Codec/EbDeblockingCommon.c:76-139, 554-572; EbDeblockingFilter.c:35-47
+//   frame passes       Encoder/Codec/EbDeblockingFilter.c:287-653 (SB-lagged vert/horz, combine_vert_horz_lf)
+//   level search       Encoder/Codec/EbDeblockingFilter.c:716-991, 1129-1252 (FULL_IMAGE bisection)
+//
+// Design (MI355X):
+//  * The mode-info grid is uploaded once per frame and turned into per-4x4 *edge records* per plane
+//    type and direction: the filter length the transform/prediction geometry allows (0/4/6/8/14) and
+//    the (segment, ref, mode) level classes of the two sides.  Everything that does not depend on
+//    the filter level is resolved once; a level trial then only looks a level up in a 128-entry table.
+//  * Within one direction no two edge segments touch the same samples (4-tap: p1..q1, 8-tap needs
+//    8-wide transforms on both sides, 14-tap 16-wide), so the reference's SB-lagged order equals
+//    "all vertical edges, then all horizontal edges" (the AV1 normative order).
+//  * One workgroup per 64x64 tile: the tile plus a 12-sample apron is staged in LDS, the vertical
+//    edges that reach the tile are filtered over the tile's rows and the apron rows, then the
+//    horizontal edges over the tile's columns; the tile is either written out (apply) or compared with
+//    the source for the SSE of a level trial — recon is never modified by a trial, so the search
+//    needs no backup/restore copies, and a trial reads each sample once.
+#include <cstring>
+#include <vector>
+
+#include "svtgpu_internal.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// AV1 size tables (BlockSize / TxSize enum order of EbDefinitions.h)
+// ---------------------------------------------------------------------------------------------
+constexpr int kNumBsize = 22;
+// log2 of the transform width/height of tx_depth_to_tx_size[depth][bsize] (EbDefinitions.h:885-906)
+__constant__ uint8_t c_tx_lw[3][kNumBsize] = {
+    {2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6, 6, 6, 2, 4, 3, 5, 4, 6},
+    {2, 2, 3, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6, 2, 3, 3, 4, 4, 5},
+    {2, 2, 3, 3, 2, 2, 2, 3, 3, 3, 4, 4, 4, 6, 6, 6, 2, 2, 3, 3, 4, 4}};
+__constant__ uint8_t c_tx_lh[3][kNumBsize] = {
+    {2, 3, 2, 3, 4, 3, 4, 5, 4, 5, 6, 5, 6, 6, 6, 6, 4, 2, 5, 3, 6, 4},
+    {2, 3, 2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6, 3, 2, 4, 3, 5, 4},
+    {2, 3, 2, 3, 2, 2, 2, 3, 3, 3, 4, 4, 4, 6, 6, 6, 2, 2, 3, 3, 4, 4}};
+// 4:2:0 chroma: av1_get_max_uv_txsize (EbUtility.h:117-123, 64 -> 32) and the plane block size
+// ss_size_lookup[bsize][1][1] (EbUtility.h:86-110), as log2 width / height
+__constant__ uint8_t c_uvtx_lw[kNumBsize] = {2, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 5, 5, 2, 3, 2, 4, 3, 5};
+__constant__ uint8_t c_uvtx_lh[kNumBsize] = {2, 2, 2, 2, 3, 2, 3, 4, 3, 4, 5, 4, 5, 5, 5, 5, 3, 2, 4, 2, 5, 3};
+__constant__ uint8_t c_bs_lw[kNumBsize]   = {2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6, 7, 7, 2, 4, 3, 5, 4, 6};
+__constant__ uint8_t c_bs_lh[kNumBsize]   = {2, 3, 2, 3, 4, 3, 4, 5, 4, 5, 6, 5, 6, 7, 6, 7, 4, 2, 5, 3, 6, 4};
+__constant__ uint8_t c_uvbs_lw[kNumBsize] = {2, 2, 2, 2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 2, 3, 2, 4, 3, 5};
+__constant__ uint8_t c_uvbs_lh[kNumBsize] = {2, 2, 2, 2, 3, 2, 3, 4, 3, 4, 5, 4, 5, 6, 5, 6, 3, 2, 4, 2, 5, 3};
+// mode_lf_lut (EbDeblockingCommon.h:62-66): GLOBALMV (15) and GLOBAL_GLOBALMV (23) map to 0
+__device__ __forceinline__ int mode_lf(int mode) { return mode >= 13 && mode != 15 && mode != 23; }
+
+// Edge record (one per 4x4 unit per plane type and direction):
+//   bits 0..3  filter length allowed by geometry (0, 4, 6, 8, 14)
+//   bits 8..14 level class of the current block  (segment*16 + ref*2 + mode_lf)
+//   bits 16..22 level class of the previous block
+__device__ __forceinline__ int lf_class(const SvtGpuLfMi &m) {
+    return m.segment_id * 16 + m.ref_frame0 * 2 + mode_lf(m.mode);
+}
+
+// log2 of the transform extent across the edge (get_transform_size + txsize_{horz,vert}_map)
+__device__ __forceinline__ int tx_log2(const SvtGpuLfMi &m, int vert, int chroma) {
+    const int skipped = m.skip && m.ref_frame0 > 0;
+    if (chroma) return vert ? c_uvtx_lw[m.bsize] : c_uvtx_lh[m.bsize];
+    const int d = skipped ? 0 : m.tx_depth;
+    return vert ? c_tx_lw[d][m.bsize] : c_tx_lh[d][m.bsize];
+}
+
+__global__ void dlf_edge_records_kernel(const SvtGpuLfMi *__restrict__ mi, int mi_cols, int units_w, int units_h,
+                                        int chroma, int vert, uint32_t *__restrict__ rec) {
+    const int ux = blockIdx.x * blockDim.x + threadIdx.x;
+    const int uy = blockIdx.y;
+    if (ux >= units_w || uy >= units_h) return;
+    const int ss     = chroma;
+    const int x      = ux * 4, y = uy * 4;
+    const int mi_row = ss | ((y << ss) >> 2), mi_col = ss | ((x << ss) >> 2);
+    const SvtGpuLfMi m = mi[mi_row * mi_cols + mi_col];
+    const int coord    = vert ? x : y;
+    uint32_t  r        = 0;
+    const int lt       = tx_log2(m, vert, chroma);
+    if (coord && !(coord & ((1 << lt) - 1))) { // a transform edge with a block on the other side
+        const SvtGpuLfMi p = vert ? mi[mi_row * mi_cols + mi_col - (1 << ss)]
+                                  : mi[(mi_row - (1 << ss)) * mi_cols + mi_col];
+        const int cur_skip = m.skip && m.ref_frame0 > 0;
+        const int pv_skip  = p.skip && p.ref_frame0 > 0;
+        const int lpb      = chroma ? (vert ? c_uvbs_lw[m.bsize] : c_uvbs_lh[m.bsize])
+                                    : (vert ? c_bs_lw[m.bsize] : c_bs_lh[m.bsize]);
+        const int pu_edge  = !(coord & ((1 << lpb) - 1));
+        if (!pv_skip || !cur_skip || pu_edge) {
+            const int mlt = min(lt, tx_log2(p, vert, chroma));
+            const int len = mlt == 2 ? 4 : chroma ? 6 : mlt == 3 ? 8 : 14;
+            r = (uint32_t)len | ((uint32_t)lf_class(m) << 8) | ((uint32_t)lf_class(p) << 16);
+        }
+    }
+    rec[(size_t)uy * units_w + ux] = r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// one sample line across an edge: F[k] = sample at offset k-7 from the edge (p6 = F[0], q0 = F[7])
+// AV1 narrow filter / wide filters (filter4/6/8/14 of EbDeblockingCommon.c)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int sclamp(int v, int lo, int hi) { return min(max(v, lo), hi); }
+
+// wide filter with n taps per side (n = 2: 6-tap, 3: 8-tap, 6: 14-tap); outputs F[7-n .. 7+n-1]
+template <int N, int LOG2>
+__device__ __forceinline__ void wide_filter(int *F) {
+    int out[2 * N];
+#pragma unroll
+    for (int i = -N; i < N; i++) {
+        int t = 0;
+#pragma unroll
+        for (int j = -N; j <= N; j++) {
+            const int p   = min(max(i + j, -(N + 1)), N);
+            const int tap = (N == 3 ? j == 0 : (j >= -1 && j <= 1)) ? 2 : 1;
+            t += F[p + 7] * tap;
+        }
+        out[i + N] = (t + (1 << (LOG2 - 1))) >> LOG2;
+    }
+#pragma unroll
+    for (int i = -N; i < N; i++) F[i + 7] = out[i + N];
+}
+
+__device__ __forceinline__ void filter_line(int *F, int len, int blimit, int limit, int thresh, int bd) {
+    const int sh = bd - 8, one = 1 << sh;
+    const int p3 = F[3], p2 = F[4], p1 = F[5], p0 = F[6], q0 = F[7], q1 = F[8], q2 = F[9], q3 = F[10];
+    const int lim = limit << sh;
+    if (abs(p0 - q0) * 2 + abs(p1 - q1) / 2 > (blimit << sh)) return;
+    int m = max(abs(p1 - p0), abs(q1 - q0));
+    int flat = 0;
+    if (len >= 6) {
+        m = max(m, max(abs(p2 - p1), abs(q2 - q1)));
+        flat = max(max(abs(p1 - p0), abs(q1 - q0)), max(abs(p2 - p0), abs(q2 - q0)));
+    }
+    if (len >= 8) {
+        m    = max(m, max(abs(p3 - p2), abs(q3 - q2)));
+        flat = max(flat, max(abs(p3 - p0), abs(q3 - q0)));
+    }
+    if (m > lim) return;
+    if (len >= 6 && flat <= one) {
+        if (len == 14) {
+            const int flat2 = max(max(max(abs(F[2] - p0), abs(F[11] - q0)), max(abs(F[1] - p0), abs(F[12] - q0))),
+                                  max(abs(F[0] - p0), abs(F[13] - q0)));
+            if (flat2 <= one) {
+                wide_filter<6, 4>(F);
+                return;
+            }
+        }
+        if (len == 6)
+            wide_filter<2, 3>(F);
+        else
+            wide_filter<3, 3>(F);
+        return;
+    }
+    // narrow filter (filter4)
+    const int off = 0x80 << sh, lo = -(128 << sh), hi = (128 << sh) - 1;
+    const bool hev = max(abs(p1 - p0), abs(q1 - q0)) > (thresh << sh);
+    const int ps1 = p1 - off, ps0 = p0 - off, qs0 = q0 - off, qs1 = q1 - off;
+    int f = hev ? sclamp(ps1 - qs1, lo, hi) : 0;
+    f            = sclamp(f + 3 * (qs0 - ps0), lo, hi);
+    const int f1 = sclamp(f + 4, lo, hi) >> 3;
+    const int f2 = sclamp(f + 3, lo, hi) >> 3;
+    F[7]         = sclamp(qs0 - f1, lo, hi) + off;
+    F[6]         = sclamp(ps0 + f2, lo, hi) + off;
+    if (!hev) {
+        const int f3 = (f1 + 1) >> 1;
+        F[8]         = sclamp(qs1 - f3, lo, hi) + off;
+        F[5]         = sclamp(ps1 + f3, lo, hi) + off;
+    }
+}
+
+__device__ __forceinline__ int half_taps(int len) { return len == 14 ? 7 : len == 8 ? 4 : len == 6 ? 3 : 2; }
+
+// ---------------------------------------------------------------------------------------------
+// tile kernel: apply (write) or level trial (SSE)
+// ---------------------------------------------------------------------------------------------
+constexpr int TILE  = 64;
+constexpr int APRON = 12;
+constexpr int LW    = TILE + 2 * APRON; // 88 samples per LDS row
+constexpr int NTHR  = 256;
+constexpr int MAX_TRIALS = 2;
+
+struct DlfTileArgs {
+    const void     *src;      // recon plane (apply: a copy of it)
+    int32_t         src_stride;
+    void           *dst;      // apply output
+    int32_t         dst_stride;
+    const void     *ref;      // source picture plane (trial)
+    int32_t         ref_stride;
+    const uint32_t *rec_v, *rec_h; // edge records of this plane type
+    int32_t         units_w;  // records per row (= pw / 4)
+    int32_t         pw, ph, bd, tiles_x;
+    int32_t         ntrial;
+    uint8_t         lvl[MAX_TRIALS][2][128]; // [trial][dir][class] filter level
+    uint8_t         mblim[64], lim[64], hev[64];
+    unsigned long long *sse; // [ntrial] (trial mode)
+};
+
+template <typename T, bool TRIAL>
+__global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
+    __shared__ uint16_t t[LW * LW];
+    __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
+    __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
+    __shared__ unsigned long long red[NTHR / 64];
+    const int tid = threadIdx.x;
+    const int x0 = (blockIdx.x % a.tiles_x) * TILE, y0 = (blockIdx.x / a.tiles_x) * TILE;
+    const int gx = x0 - APRON, gy = y0 - APRON;
+    const T  *src = (const T *)a.src;
+
+    // edge records reaching the tile (no records outside the plane: length 0)
+    constexpr int RV_R = LW / 4, RV_C = TILE / 4 + 3, RH_R = TILE / 4 + 3, RH_C = TILE / 4;
+    for (int i = tid; i < RV_R * RV_C; i += NTHR) {
+        const int ur = gy / 4 + i / RV_C, uc = (x0 - 4) / 4 + i % RV_C;
+        rv[i] = (ur >= 0 && uc >= 0 && ur * 4 < a.ph && uc * 4 < a.pw) ? a.rec_v[(size_t)ur * a.units_w + uc] : 0u;
+    }
+    for (int i = tid; i < RH_R * RH_C; i += NTHR) {
+        const int ur = (y0 - 4) / 4 + i / RH_C, uc = x0 / 4 + i % RH_C;
+        rh[i] = (ur >= 0 && ur * 4 < a.ph && uc * 4 < a.pw) ? a.rec_h[(size_t)ur * a.units_w + uc] : 0u;
+    }
+
+    for (int tr = 0; tr < (TRIAL ? a.ntrial : 1); tr++) {
+        // stage the tile + apron (samples outside the plane are never read by an active edge)
+        for (int i = tid; i < LW * LW; i += NTHR) {
+            const int r = gy + i / LW, c = gx + i % LW;
+            t[i] = (r >= 0 && c >= 0 && r < a.ph && c < a.pw) ? (uint16_t)src[(size_t)r * a.src_stride + c] : 0;
+        }
+        __syncthreads();
+        // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
+        for (int i = tid; i < RV_R * RV_C * 4; i += NTHR) {
+            const int line = i & 3, e = (i >> 2) % RV_C, sr = (i >> 2) / RV_C;
+            const uint32_t r = rv[sr * RV_C + e];
+            const int len = r & 15;
+            if (!len) continue;
+            const int cur = a.lvl[tr][0][(r >> 8) & 127], prv = a.lvl[tr][0][(r >> 16) & 127];
+            if (!cur && !prv) continue;
+            const int lvl = cur ? cur : prv;
+            uint16_t *row = &t[(sr * 4 + line) * LW + (APRON - 4 + e * 4)];
+            const int h = half_taps(len);
+            int F[14];
+#pragma unroll
+            for (int k = 0; k < 14; k++) F[k] = (k >= 7 - h && k < 7 + h) ? row[k - 7] : 0;
+            filter_line(F, len, a.mblim[lvl], a.lim[lvl], a.hev[lvl], a.bd);
+#pragma unroll
+            for (int k = 0; k < 14; k++)
+                if (k >= 7 - h && k < 7 + h) row[k - 7] = (uint16_t)F[k];
+        }
+        __syncthreads();
+        // horizontal edges y0-4 .. y0+64 over the tile's 64 columns
+        for (int i = tid; i < RH_R * RH_C * 4; i += NTHR) {
+            const int col = i % TILE, e = i / TILE;
+            const uint32_t r = rh[e * RH_C + col / 4];
+            const int len = r & 15;
+            if (!len) continue;
+            const int cur = a.lvl[tr][1][(r >> 8) & 127], prv = a.lvl[tr][1][(r >> 16) & 127];
+            if (!cur && !prv) continue;
+            const int lvl = cur ? cur : prv;
+            uint16_t *c = &t[(APRON - 4 + e * 4) * LW + APRON + col];
+            const int h = half_taps(len);
+            int F[14];
+#pragma unroll
+            for (int k = 0; k < 14; k++) F[k] = (k >= 7 - h && k < 7 + h) ? c[(k - 7) * LW] : 0;
+            filter_line(F, len, a.mblim[lvl], a.lim[lvl], a.hev[lvl], a.bd);
+#pragma unroll
+            for (int k = 0; k < 14; k++)
+                if (k >= 7 - h && k < 7 + h) c[(k - 7) * LW] = (uint16_t)F[k];
+        }
+        __syncthreads();
+        // emit the tile
+        const int tw = min(TILE, a.pw - x0), th = min(TILE, a.ph - y0);
+        if (TRIAL) {
+            const T *ref = (const T *)a.ref;
+            unsigned long long s = 0;
+            for (int i = tid; i < TILE * TILE; i += NTHR) {
+                const int r = i / TILE, c = i % TILE;
+                if (r < th && c < tw) {
+                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)ref[(size_t)(y0 + r) * a.ref_stride + x0 + c];
+                    s += (unsigned long long)(d * d);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+            if ((tid & 63) == 0) red[tid >> 6] = s;
+            __syncthreads();
+            if (tid == 0) {
+                unsigned long long tot = 0;
+                for (int w = 0; w < NTHR / 64; w++) tot += red[w];
+                atomicAdd(&a.sse[tr], tot);
+            }
+            __syncthreads();
+        } else {
+            T *dst = (T *)a.dst;
+            for (int i = tid; i < TILE * TILE; i += NTHR) {
+                const int r = i / TILE, c = i % TILE;
+                if (r < th && c < tw) dst[(size_t)(y0 + r) * a.dst_stride + x0 + c] = (T)t[(APRON + r) * LW + APRON + c];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// plane SSE (svt_spatial_full_distortion_kernel / svt_full_distortion_kernel16_bits)
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void plane_sse_kernel(const T *a, int as, const T *b, int bs, int w, int h,
+                                                        unsigned long long *out) {
+    __shared__ unsigned long long red[4];
+    unsigned long long s = 0;
+    for (int r = blockIdx.x; r < h; r += gridDim.x)
+        for (int c = threadIdx.x; c < w; c += 256) {
+            const int d = (int)a[(size_t)r * as + c] - (int)b[(size_t)r * bs + c];
+            s += (unsigned long long)(d * d);
+        }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-segment shim kernel: 4 lines of one edge, staged as [4][16] with the edge between 7 and 8
+// ---------------------------------------------------------------------------------------------
+__global__ void lpf_lines_kernel(uint16_t *lines, int len, int blimit, int limit, int thresh, int bd) {
+    const int l = threadIdx.x;
+    if (l >= 4) return;
+    int F[14];
+    for (int k = 0; k < 14; k++) F[k] = lines[l * 16 + 1 + k];
+    filter_line(F, len, blimit, limit, thresh, bd);
+    for (int k = 0; k < 14; k++) lines[l * 16 + 1 + k] = (uint16_t)F[k];
+}
+
+} // namespace
+
+// =============================================================================================
+// host side
+// =============================================================================================
+struct SvtGpuDlfState {
+    SvtGpuContext *ctx;
+    int32_t        width, height, mi_rows, mi_cols;
+    SvtGpuLfMi    *d_mi;
+    uint32_t      *d_rec[2][2]; // [chroma][dir]
+    int32_t        uw[2], uh[2]; // record grid per plane type
+    void          *d_scratch;    // plane copy for in-place apply
+    unsigned long long *d_sse;   // trial results
+    unsigned long long *h_sse;   // pinned
+    int32_t        have_mi;
+};
+
+namespace {
+
+// level tables: svt_av1_loop_filter_frame_init + svt_aom_update_sharpness (EbDeblockingCommon.c:76-139, 554-572)
+struct LevelTables {
+    uint8_t lvl[3][2][128]; // [plane][dir][segment*16 + ref*2 + mode_lf]
+    uint8_t mblim[64], lim[64], hev[64];
+};
+
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+void build_level_tables(const SvtGpuLfParams &p, LevelTables &L) {
+    std::memset(&L, 0, sizeof L);
+    const int sh = p.sharpness_level;
+    for (int l = 0; l < 64; l++) {
+        int inside = l >> ((sh > 0) + (sh > 4));
+        if (sh > 0) inside = std::min(inside, 9 - sh);
+        inside     = std::max(inside, 1);
+        L.lim[l]   = (uint8_t)inside;
+        L.mblim[l] = (uint8_t)(2 * (l + 2) + inside);
+        L.hev[l]   = (uint8_t)(l >> 4);
+    }
+    const int base[3][2] = {{p.filter_level[0], p.filter_level[1]},
+                            {p.filter_level_u, p.filter_level_u},
+                            {p.filter_level_v, p.filter_level_v}};
+    const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
+    for (int pl = 0; pl < 3; pl++)
+        for (int seg = 0; seg < 8; seg++)
+            for (int dir = 0; dir < 2; dir++) {
+                int lv = base[pl][dir];
+                if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
+                    lv = clampi(lv + p.seg_feature_data[seg][feat[pl][dir]], 0, 63);
+                for (int ref = 0; ref < 8; ref++)
+                    for (int mode = 0; mode < 2; mode++) {
+                        int v = lv;
+                        if (p.mode_ref_delta_enabled) {
+                            const int scale = 1 << (lv >> 5);
+                            v = lv + p.ref_deltas[ref] * scale + (ref > 0 ? p.mode_deltas[mode] * scale : 0);
+                            v = clampi(v, 0, 63);
+                        }
+                        L.lvl[pl][dir][seg * 16 + ref * 2 + mode] = (uint8_t)v;
+                    }
+            }
+}
+
+// is the plane filtered at all with these levels (svt_aom_loop_filter_sb :575-582)
+bool plane_active(const SvtGpuLfParams &p, int plane) {
+    if (plane == 0) return p.filter_level[0] || p.filter_level[1];
+    return plane == 1 ? p.filter_level_u != 0 : p.filter_level_v != 0;
+}
+
+DlfTileArgs base_args(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane, const LevelTables &L) {
+    DlfTileArgs a;
+    std::memset(&a, 0, sizeof a);
+    const int ch = plane > 0;
+    a.rec_v   = s->d_rec[ch][0];
+    a.rec_h   = s->d_rec[ch][1];
+    a.units_w = s->uw[ch];
+    a.pw      = f->pw[plane];
+    a.ph      = f->ph[plane];
+    a.bd      = f->bit_depth;
+    a.tiles_x = (a.pw + TILE - 1) / TILE;
+    std::memcpy(a.mblim, L.mblim, 64);
+    std::memcpy(a.lim, L.lim, 64);
+    std::memcpy(a.hev, L.hev, 64);
+    return a;
+}
+
+int launch_tile(const DlfTileArgs &a, int bps, bool trial, hipStream_t st) {
+    const int tiles = a.tiles_x * ((a.ph + TILE - 1) / TILE);
+    if (bps == 2) {
+        if (trial) hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, true>), dim3(tiles), dim3(NTHR), 0, st, a);
+        else       hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);
+    } else {
+        if (trial) hipLaunchKernelGGL((dlf_tile_kernel<uint8_t, true>), dim3(tiles), dim3(NTHR), 0, st, a);
+        else       hipLaunchKernelGGL((dlf_tile_kernel<uint8_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
+bool frame_matches(const SvtGpuDlfState *s, const SvtGpuFrame *f) {
+    return f && f->width == s->width && f->height == s->height && (f->bit_depth == 8 || f->bit_depth == 10);
+}
+
+// level trial: SSE(source, filtered plane) for up to MAX_TRIALS parameter sets, recon untouched
+int trial_sse(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, int plane,
+              const SvtGpuLfParams *prm, int n, uint64_t *out, hipStream_t st) {
+    LevelTables L;
+    build_level_tables(prm[0], L);
+    DlfTileArgs a = base_args(s, recon, plane, L);
+    a.src        = recon->plane[plane];
+    a.src_stride = recon->stride[plane];
+    a.ref        = src->plane[plane];
+    a.ref_stride = src->stride[plane];
+    a.ntrial     = n;
+    a.sse        = s->d_sse;
+    for (int k = 0; k < n; k++) {
+        if (k) build_level_tables(prm[k], L);
+        const bool on = plane_active(prm[k], plane);
+        for (int dir = 0; dir < 2; dir++)
+            if (on) std::memcpy(a.lvl[k][dir], L.lvl[plane][dir], 128);
+    }
+    HIP_TRY(hipMemsetAsync(s->d_sse, 0, sizeof(unsigned long long) * MAX_TRIALS, st));
+    int rc = launch_tile(a, recon->bytes_per_sample, true, st);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(s->h_sse, s->d_sse, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int k = 0; k < n; k++) out[k] = s->h_sse[k];
+    return SVTGPU_OK;
+}
+
+void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_filter_frame (:841-883)
+    if (plane == 0) {
+        if (dir != 1) p.filter_level[0] = lvl;
+        if (dir != 0) p.filter_level[1] = lvl;
+    } else if (plane == 1)
+        p.filter_level_u = lvl;
+    else
+        p.filter_level_v = lvl;
+}
+
+// search_filter_level (EbDeblockingFilter.c:886-991)
+int search_level(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, SvtGpuLfParams &p,
+                 const int last[4], int dlf_avg, int early_exit, int only4x4, int plane, int dir, hipStream_t st,
+                 int *best_out) {
+    const int start = plane == 0 ? (dlf_avg ? last[0] : last[dir]) : last[plane + 1];
+    int       mid = clampi(start, 0, 63), step = mid < 16 ? 4 : mid / 4, direction = 0, conv = 0;
+    int64_t   err[64];
+    for (int i = 0; i < 64; i++) err[i] = -1;
+    auto eval = [&](const int *lv, int n) -> int { // evaluate the not-yet-known levels in one launch
+        SvtGpuLfParams q[MAX_TRIALS];
+        int            idx[MAX_TRIALS], m = 0;
+        for (int k = 0; k < n; k++)
+            if (err[lv[k]] < 0 && (m == 0 || idx[0] != lv[k])) {
+                q[m] = p;
+                set_trial_level(q[m], plane, dir, lv[k]);
+                idx[m++] = lv[k];
+            }
+        if (!m) return SVTGPU_OK;
+        uint64_t r[MAX_TRIALS];
+        int      rc = trial_sse(s, recon, src, plane, q, m, r, st);
+        if (rc) return rc;
+        for (int k = 0; k < m; k++) err[idx[k]] = (int64_t)r[k];
+        return SVTGPU_OK;
+    };
+    int rc = eval(&mid, 1);
+    if (rc) return rc;
+    int64_t best_err = err[mid];
+    int     best     = mid;
+    while (step > 0) {
+        const int hi = std::min(mid + step, 63), lo = std::max(mid - step, 0);
+        int64_t   bias = (best_err >> (15 - (mid / 8))) * step;
+        if (!only4x4) bias >>= 1;
+        const bool try_lo = direction <= 0 && lo != mid, try_hi = direction >= 0 && hi != mid;
+        int        lv[2], n = 0;
+        if (try_lo) lv[n++] = lo;
+        if (try_hi) lv[n++] = hi;
+        if ((rc = eval(lv, n))) return rc;
+        if (try_lo && err[lo] < best_err + bias) {
+            if (err[lo] < best_err) best_err = err[lo];
+            best = lo;
+        }
+        if (try_hi && err[hi] < best_err - bias) {
+            best_err = err[hi];
+            best     = hi;
+        }
+        if (best == mid) {
+            conv++;
+            step      = conv == early_exit ? 0 : step / 2;
+            direction = 0;
+        } else {
+            direction = best < mid ? -1 : 1;
+            mid       = best;
+        }
+    }
+    *best_out = best;
+    return SVTGPU_OK;
+}
+
+bool valid_params(const SvtGpuLfParams *p) {
+    if (!p) return false;
+    const int lv[4] = {p->filter_level[0], p->filter_level[1], p->filter_level_u, p->filter_level_v};
+    for (int v : lv)
+        if (v < 0 || v > 63) return false;
+    return p->sharpness_level >= 0 && p->sharpness_level <= 7;
+}
+
+} // namespace
+
+extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuDlfState **out) {
+    if (!ctx || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7)) return SVTGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    SvtGpuDlfState *s = new SvtGpuDlfState();
+    s->ctx     = ctx;
+    s->width   = width;
+    s->height  = height;
+    s->mi_cols = width >> 2;
+    s->mi_rows = height >> 2;
+    s->uw[0]   = width / 4, s->uh[0] = height / 4;
+    s->uw[1]   = width / 8, s->uh[1] = height / 8;
+    hipError_t e = hipMalloc(&s->d_mi, sizeof(SvtGpuLfMi) * s->mi_rows * s->mi_cols);
+    for (int c = 0; c < 2 && e == hipSuccess; c++)
+        for (int d = 0; d < 2 && e == hipSuccess; d++)
+            e = hipMalloc(&s->d_rec[c][d], sizeof(uint32_t) * s->uw[c] * s->uh[c]);
+    if (e == hipSuccess) e = hipMalloc(&s->d_scratch, (size_t)width * height * 2);
+    if (e == hipSuccess) e = hipMalloc(&s->d_sse, sizeof(unsigned long long) * MAX_TRIALS);
+    if (e == hipSuccess) e = hipHostMalloc(&s->h_sse, sizeof(unsigned long long) * MAX_TRIALS, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        svtgpu_dlf_state_destroy(s);
+        svtgpu_set_last_hip_error(e, "dlf state alloc", __FILE__, __LINE__);
+        return e == hipErrorOutOfMemory ? SVTGPU_ERR_OOM : SVTGPU_ERR_HIP;
+    }
+    *out = s;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
+    if (!s) return;
+    (void)hipFree(s->d_mi);
+    for (int c = 0; c < 2; c++)
+        for (int d = 0; d < 2; d++) (void)hipFree(s->d_rec[c][d]);
+    (void)hipFree(s->d_scratch);
+    (void)hipFree(s->d_sse);
+    if (s->h_sse) (void)hipHostFree(s->h_sse);
+    delete s;
+}
+
+extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream) {
+    if (!s || !mi) return SVTGPU_ERR_INVALID_ARG;
+    const size_t n = (size_t)s->mi_rows * s->mi_cols;
+    for (size_t i = 0; i < n; i++) { // the device tables are indexed by these fields
+        const SvtGpuLfMi &m = mi[i];
+        if (m.bsize >= kNumBsize || m.tx_depth > 2 || m.ref_frame0 < 0 || m.ref_frame0 > 7 || m.mode > 24 ||
+            m.segment_id > 7)
+            return SVTGPU_ERR_INVALID_ARG;
+    }
+    hipStream_t st = pick_stream(s->ctx, stream);
+    HIP_TRY(hipMemcpyAsync(s->d_mi, mi, n * sizeof(SvtGpuLfMi), hipMemcpyHostToDevice, st));
+    for (int c = 0; c < 2; c++)
+        for (int d = 0; d < 2; d++) {
+            hipLaunchKernelGGL(dlf_edge_records_kernel, dim3((s->uw[c] + 127) / 128, s->uh[c]), dim3(128), 0, st,
+                               s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->d_rec[c][d]);
+            HIP_TRY(hipGetLastError());
+        }
+    HIP_TRY(hipStreamSynchronize(st)); // the caller's mi buffer may be reused after return
+    s->have_mi = 1;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params,
+                                int32_t plane_start, int32_t plane_end, void *stream) {
+    if (!s || !frame_matches(s, frame) || !valid_params(params) || plane_start < 0 || plane_end > 3 ||
+        plane_start > plane_end || !s->have_mi)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    LevelTables L;
+    build_level_tables(*params, L);
+    for (int pl = plane_start; pl < plane_end; pl++) {
+        if (pl == 0 && !plane_active(*params, 0)) break; // luma off: no plane is filtered (:575-577)
+        if (!plane_active(*params, pl)) continue;
+        const size_t bps = frame->bytes_per_sample;
+        HIP_TRY(hipMemcpy2DAsync(s->d_scratch, frame->pw[pl] * bps, frame->plane[pl], frame->stride[pl] * bps,
+                                 frame->pw[pl] * bps, frame->ph[pl], hipMemcpyDeviceToDevice, st));
+        DlfTileArgs a = base_args(s, frame, pl, L);
+        a.src        = s->d_scratch;
+        a.src_stride = frame->pw[pl];
+        a.dst        = frame->plane[pl];
+        a.dst_stride = frame->stride[pl];
+        a.ntrial     = 1;
+        for (int dir = 0; dir < 2; dir++) std::memcpy(a.lvl[0][dir], L.lvl[pl][dir], 128);
+        int rc = launch_tile(a, (int)bps, false, st);
+        if (rc) return rc;
+    }
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source,
+                               SvtGpuLfParams *params, int32_t dlf_avg, int32_t dlf_avg_uv,
+                               int32_t temporal_layer_index, int32_t early_exit_convergence,
+                               int32_t tx_mode_only_4x4, void *stream) {
+    if (!s || !frame_matches(s, recon) || !frame_matches(s, source) || source->bit_depth != recon->bit_depth ||
+        !valid_params(params) || !s->have_mi)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t    st = pick_stream(s->ctx, stream);
+    SvtGpuLfParams p  = *params;
+    p.sharpness_level = 0;
+    const int last[4] = {p.filter_level[0], p.filter_level[1], p.filter_level_u, p.filter_level_v};
+    int       y = 0, u = 0, v = 0, rc;
+    if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 0, 2, st, &y)))
+        return rc;
+    p.filter_level[0] = p.filter_level[1] = y;
+    if (dlf_avg_uv && temporal_layer_index > 0) {
+        u = last[2];
+        v = last[3];
+    } else {
+        if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0, st, &u)))
+            return rc;
+        p.filter_level_u = u;
+        if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0, st, &v)))
+            return rc;
+    }
+    p.filter_level_u = u;
+    p.filter_level_v = v;
+    *params          = p;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_plane_sse(const SvtGpuFrame *a, const SvtGpuFrame *b, int32_t plane, uint64_t *sse,
+                                void *stream) {
+    if (!a || !b || !sse || plane < 0 || plane > 2 || a->width != b->width || a->height != b->height ||
+        a->bytes_per_sample != b->bytes_per_sample)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(a->ctx, stream);
+    static thread_local unsigned long long *d = nullptr; // per-thread result slot
+    if (!d) HIP_TRY(hipMalloc((void **)&d, sizeof *d));
+    HIP_TRY(hipMemsetAsync(d, 0, sizeof *d, st));
+    const int rows = a->ph[plane], blocks = std::min(rows, 1024);
+    if (a->bytes_per_sample == 2)
+        hipLaunchKernelGGL(plane_sse_kernel<uint16_t>, dim3(blocks), dim3(256), 0, st, (const uint16_t *)a->plane[plane],
+                           a->stride[plane], (const uint16_t *)b->plane[plane], b->stride[plane], a->pw[plane], rows, d);
+    else
+        hipLaunchKernelGGL(plane_sse_kernel<uint8_t>, dim3(blocks), dim3(256), 0, st, (const uint8_t *)a->plane[plane],
+                           a->stride[plane], (const uint8_t *)b->plane[plane], b->stride[plane], a->pw[plane], rows, d);
+    HIP_TRY(hipGetLastError());
+    unsigned long long h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *sse = h;
+    return SVTGPU_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RTCD-compatible per-segment shims (common_dsp_rtcd.h:1115-1146): synchronous, for unit parity
+// ---------------------------------------------------------------------------------------------
+namespace {
+template <typename T>
+void lpf_shim(T *s, int32_t pitch, int vertical, int len, const uint8_t *blimit, const uint8_t *limit,
+              const uint8_t *thresh, int bd) {
+    const long step = vertical ? 1 : pitch, adv = vertical ? pitch : 1;
+    const int  h    = len == 14 ? 7 : len == 8 ? 4 : len == 6 ? 3 : 2;
+    uint16_t   lines[4 * 16] = {0};
+    for (int l = 0; l < 4; l++) // only the samples the reference function touches
+        for (int k = -h; k < h; k++) lines[l * 16 + 8 + k] = s[l * adv + k * step];
+    hipStream_t st = svtgpu_default_stream();
+    static thread_local uint16_t *d = nullptr;
+    if (!d) HIP_OR_DIE(hipMalloc(&d, sizeof lines));
+    HIP_OR_DIE(hipMemcpyAsync(d, lines, sizeof lines, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lpf_lines_kernel, dim3(1), dim3(64), 0, st, d, len, (int)*blimit, (int)*limit, (int)*thresh, bd);
+    HIP_OR_DIE(hipGetLastError());
+    HIP_OR_DIE(hipMemcpyAsync(lines, d, sizeof lines, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int l = 0; l < 4; l++)
+        for (int k = -h; k < h; k++) s[l * adv + k * step] = (T)lines[l * 16 + 8 + k];
+}
+} // namespace
+
+#define LPF_SHIMS(DIR, VERT, N)                                                                           \
+    extern "C" void svtgpu_lpf_##DIR##_##N(uint8_t *s, int32_t pitch, const uint8_t *blimit,               \
+                                           const uint8_t *limit, const uint8_t *thresh) {                  \
+        lpf_shim<uint8_t>(s, pitch, VERT, N, blimit, limit, thresh, 8);                                    \
+    }                                                                                                      \
+    extern "C" void svtgpu_highbd_lpf_##DIR##_##N(uint16_t *s, int32_t pitch, const uint8_t *blimit,       \
+                                                  const uint8_t *limit, const uint8_t *thresh, int32_t bd) { \
+        lpf_shim<uint16_t>(s, pitch, VERT, N, blimit, limit, thresh, bd);                                  \
+    }
+LPF_SHIMS(horizontal, 0, 4)
+LPF_SHIMS(horizontal, 0, 6)
+LPF_SHIMS(horizontal, 0, 8)
+LPF_SHIMS(horizontal, 0, 14)
+LPF_SHIMS(vertical, 1, 4)
+LPF_SHIMS(vertical, 1, 6)
+LPF_SHIMS(vertical, 1, 8)
+LPF_SHIMS(vertical, 1, 14)

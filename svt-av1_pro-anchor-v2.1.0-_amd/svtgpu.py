@@ -56,9 +56,63 @@ class CdefParams(ctypes.Structure):
                 tuple(self.cdef_uv_strength[:nb]))
 
 
+class LfMi(ctypes.Structure):
+    """SvtGpuLfMi: the MbModeInfo.block_mi fields the deblocking filter reads (one per 4x4 mi)."""
+    _fields_ = [("bsize", ctypes.c_uint8), ("tx_depth", ctypes.c_uint8), ("skip", ctypes.c_uint8),
+                ("ref_frame0", ctypes.c_int8), ("mode", ctypes.c_uint8), ("segment_id", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 2)]
+
+
+LF_MI_DTYPE = np.dtype([("bsize", np.uint8), ("tx_depth", np.uint8), ("skip", np.uint8), ("ref_frame0", np.int8),
+                        ("mode", np.uint8), ("segment_id", np.uint8), ("pad", np.uint8, 2)])
+
+
+class LfParams(ctypes.Structure):
+    """SvtGpuLfParams (struct LoopFilter, EbDefinitions.h:1903-1920, + segmentation features)."""
+    _fields_ = [
+        ("filter_level", ctypes.c_int32 * 2),
+        ("filter_level_u", ctypes.c_int32),
+        ("filter_level_v", ctypes.c_int32),
+        ("sharpness_level", ctypes.c_int32),
+        ("mode_ref_delta_enabled", ctypes.c_uint8),
+        ("ref_deltas", ctypes.c_int8 * 8),
+        ("mode_deltas", ctypes.c_int8 * 2),
+        ("segmentation_enabled", ctypes.c_uint8),
+        ("seg_feature_data", (ctypes.c_int16 * 8) * 8),
+        ("seg_feature_enabled", (ctypes.c_int16 * 8) * 8),
+    ]
+
+    def levels(self):
+        return (self.filter_level[0], self.filter_level[1], self.filter_level_u, self.filter_level_v)
+
+    @classmethod
+    def make(cls, fl0, fl1, flu, flv, sharpness=0, ref_deltas=None, mode_deltas=None, seg_enabled=None,
+             seg_data=None):
+        """Build from plain values; ref_deltas/mode_deltas given => mode_ref_delta_enabled."""
+        p = cls()
+        p.filter_level[0], p.filter_level[1], p.filter_level_u, p.filter_level_v = fl0, fl1, flu, flv
+        p.sharpness_level = sharpness
+        if ref_deltas is not None:
+            p.mode_ref_delta_enabled = 1
+            for i, v in enumerate(ref_deltas):
+                p.ref_deltas[i] = int(v)
+            for i, v in enumerate(mode_deltas if mode_deltas is not None else (0, 0)):
+                p.mode_deltas[i] = int(v)
+        if seg_enabled is not None:
+            p.segmentation_enabled = 1
+            for s in range(8):
+                for f in range(8):
+                    p.seg_feature_enabled[s][f] = int(seg_enabled[s][f])
+                    p.seg_feature_data[s][f] = int(seg_data[s][f])
+        return p
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _U64 = ctypes.c_uint64
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_LPF8 = (None, [_P, _I32, _P, _P, _P])
+_LPF16 = (None, [_P, _I32, _P, _P, _P, _I32])
 _SIGS = {
     "svtgpu_device_available": (ctypes.c_int, []),
     "svtgpu_version": (ctypes.c_char_p, []),
@@ -98,6 +152,14 @@ _SIGS = {
     "svtgpu_cdef_clear_tables": (ctypes.c_int, [_P, _P]),
     "svtgpu_cdef_read_state": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "svtgpu_cdef_mse_device_ptr": (_P, [_P]),
+    **{"svtgpu_lpf_%s_%d" % (d, n): _LPF8 for d in ("horizontal", "vertical") for n in (4, 6, 8, 14)},
+    **{"svtgpu_highbd_lpf_%s_%d" % (d, n): _LPF16 for d in ("horizontal", "vertical") for n in (4, 6, 8, 14)},
+    "svtgpu_dlf_state_create": (ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_dlf_state_destroy": (None, [_P]),
+    "svtgpu_dlf_set_mode_info": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_dlf_frame": (ctypes.c_int, [_P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
+    "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
 }
 
 _lib = None
@@ -274,6 +336,55 @@ class CdefState:
             self.close()
         except Exception:
             pass
+
+
+class DlfState:
+    """Deblocking state of one picture size: the device mode-info grid and the level tables."""
+
+    def __init__(self, ctx, width, height):
+        self.ctx, self.width, self.height = ctx, width, height
+        self.mi_rows, self.mi_cols = ((height + 7) & ~7) >> 2, ((width + 7) & ~7) >> 2
+        h = _P()
+        check(lib().svtgpu_dlf_state_create(ctx.h, width, height, ctypes.byref(h)))
+        self.h = h
+
+    def set_mode_info(self, mi, stream=None):
+        """mi: structured array (LF_MI_DTYPE) or uint8 [mi_rows, mi_cols, 8]."""
+        a = np.ascontiguousarray(mi)
+        if a.dtype != LF_MI_DTYPE:
+            a = np.ascontiguousarray(a.astype(np.uint8).reshape(self.mi_rows, self.mi_cols, 8))
+        assert a.nbytes == self.mi_rows * self.mi_cols * 8, (a.shape, self.mi_rows, self.mi_cols)
+        check(lib().svtgpu_dlf_set_mode_info(self.h, ptr(a), stream))
+        self.ctx.synchronize(stream)
+
+    def filter(self, frame, params, plane_start=0, plane_end=3, stream=None):
+        check(lib().svtgpu_dlf_frame(self.h, frame.h, ctypes.byref(params), plane_start, plane_end, stream))
+
+    def pick(self, recon, source, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=2,
+             only_4x4=0, stream=None):
+        """Level search; `params` carries the previous levels in; returns the picked LfParams."""
+        p = LfParams()
+        ctypes.pointer(p)[0] = params
+        check(lib().svtgpu_dlf_pick(self.h, recon.h, source.h, ctypes.byref(p), dlf_avg, dlf_avg_uv,
+                                    temporal_layer_index, early_exit, only_4x4, stream))
+        return p
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_dlf_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def plane_sse(a, b, plane, stream=None):
+    v = _U64()
+    check(lib().svtgpu_plane_sse(a.h, b.h, plane, ctypes.byref(v), stream))
+    return v.value
 
 
 def declared_symbols(header=HEADER_PATH):

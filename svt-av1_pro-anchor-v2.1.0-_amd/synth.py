@@ -54,3 +54,21 @@ def block_mask(width, height, seed, p_skip=0.0):
     rng = np.random.Generator(np.random.PCG64(seed ^ 0xB10C))
     m = (rng.random(((height + 7) // 8, (width + 7) // 8)) >= p_skip).astype(np.uint8)
     return m
+
+
+def mode_info(width, height, seed):
+    """Deblocking mode-info grid for the benchmark: 16x16 non-skip inter blocks
+    (LAST_FRAME, NEWMV), transform size hashed per block from {16, 8, 4} (tx_depth 0/1/2).
+    Returns a structured array [mi_rows][mi_cols] with svtgpu.LF_MI_DTYPE."""
+    from svtgpu import LF_MI_DTYPE
+    mr, mc = ((height + 7) & ~7) >> 2, ((width + 7) & ~7) >> 2
+    mi = np.zeros((mr, mc), LF_MI_DTYPE)
+    by, bx = np.mgrid[0:mr, 0:mc] // 4
+    h = (by * 0x9E3779B1 + bx * 0x85EBCA77 + seed) & 0xFFFFFFFF
+    h = ((h ^ (h >> 15)) * 0x2C1B3C6D) & 0xFFFFFFFF
+    mi["bsize"] = 6           # BLOCK_16X16
+    mi["tx_depth"] = (h >> 7) % 3
+    mi["skip"] = 0
+    mi["ref_frame0"] = 1      # LAST_FRAME
+    mi["mode"] = 16           # NEWMV
+    return mi

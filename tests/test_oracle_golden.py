@@ -59,3 +59,32 @@ def test_controls_level1_match_encmodeconfig():
     for lvl in (0, 11, 14, 15, 17):
         with pytest.raises(ValueError):
             oracle.controls(lvl)
+
+
+# ---------------------------------------------------------------- deblocking (gen_golden_dlf.c)
+def test_lpf_golden():
+    import dlf_cases as dc
+    g = cc.load("dlf_lpf.bin")
+    meta, inp, out = g["meta"], g["in"], g["out"]
+    bad = []
+    for n in range(len(meta)):
+        kind, fn, bl, li, th = (int(x) for x in meta[n])
+        bd = 8 if kind == 108 else kind
+        got = oracle.lpf_lines(inp[n], bd, fn, bl, li, th, lowbd=(kind == 8))
+        if not np.array_equal(got, out[n]):
+            bad.append((n, kind, dc.LPF_NAMES[fn]))
+    assert not bad, bad[:10]
+    # the sweep exercises the flat (6/8/14-tap) paths, not only filter4
+    changed_far = sum(int(np.any(inp[n][:, [1, 2, 13, 14]] != out[n][:, [1, 2, 13, 14]])) for n in range(len(meta)))
+    assert changed_far > 50
+
+
+def test_dlf_frame_golden():
+    import dlf_cases as dc
+    n = 0
+    for c in dc.frame_cases():
+        got = oracle.dlf_frame(c["inp"], c["bd"], c["mi"], c["params"], c["plane_start"], c["plane_end"])
+        for p in range(3):
+            assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
+        n += 1
+    assert n >= 8
