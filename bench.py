@@ -1,15 +1,20 @@
 #!/usr/bin/env python
 """bench.py — MI355X in-loop-filter hot path throughput (BASELINE.json metric).
 
-A "step" = one 4K 10-bit 4:2:0 frame through the device-resident CDEF pipeline of the reference's
-CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
-strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
-(svt_av1_cdef_frame).  Inputs are synthetic and resident in HBM before timing.
+A "step" = one 4K 10-bit 4:2:0 frame through the device-resident in-loop filter pipeline:
+  DLF stage (EbDlfProcess.c, dlf level 1): full-image level search (svt_av1_pick_filter_level) and
+      the frame filter (svt_av1_loop_filter_frame) into the DLF output frame;
+  CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
+      strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
+      (svt_av1_cdef_frame).
+Inputs are synthetic (recon = source + blocking/ringing, 16x16 non-skip inter blocks
+with hashed 4/8/16 transforms) and resident in HBM before timing.
 
-N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the frame is tiled into
-bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and skip flags
-are all-reduce-summed over RCCL (zeros outside each band), every rank runs the (replicated,
-deterministic) pick and applies its band — strong scaling of one frame per step.
+N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the DLF stage is replicated
+(every rank deblocks the whole frame: its level search needs whole-frame SSEs); the CDEF frame is
+tiled into bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and
+skip flags are all-reduce-summed over RCCL (zeros outside each band), every rank runs the
+(replicated, deterministic) pick and applies its band — strong scaling of one frame per step.
 
 Prints ONE JSON line on rank 0 (contract in the task description): value = luma Mpixels/s of the
 whole job, plus `roofline` for the dominant kernel (timed with HIP events on the stream it runs
@@ -47,24 +52,27 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(src, rec, bd, level, q, lam, sample):
+def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, sample):
     """The repo's scalar C restatement (oracle/) on one host core over a crop of the same frame."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: used here only as the reported CPU baseline
     sw, sh = (int(x) for x in sample.split("x"))
+    mi_c = np.ascontiguousarray(mi[:sh // 4, :sw // 4])
     crop = [rec[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in rec[1:]]
     cs = [src[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in src[1:]]
     crop = [np.ascontiguousarray(a) for a in crop]
     cs = [np.ascontiguousarray(a) for a in cs]
     ctrls = oracle.controls(level)
     t0 = time.perf_counter()
+    lfp = oracle.dlf_pick(crop, cs, bd, mi_c, lf_start, 0, 0, 0, 0, 0)
+    crop = oracle.dlf_frame(crop, bd, mi_c, lfp)
     mse, skip, d, v = oracle.cdef_search_frame(crop, cs, bd, ctrls, q)
     prm, fbs = oracle.cdef_pick(sw, sh, mse, skip, ctrls, q, lam)
     oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
     dt = time.perf_counter() - t0
     return {"value": round(sw * sh / dt / 1e6, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%dx%d crop of the same %d-bit frame, CDEF search+pick+apply, cdef_level %d, scalar C "
-                      "restatement (oracle/cdef_oracle.c), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
+            "sample": "%dx%d crop of the same %d-bit frame, DLF pick+filter then CDEF search+pick+apply, cdef_level %d, scalar C "
+                      "restatement (oracle/), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
 
 
 def main():
@@ -87,9 +95,13 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
     src, rec = synth.frame_pair(W, H, bd, seed=0x5EED0003)
-    R, S, O = (svtgpu.Frame(ctx, W, H, bd) for _ in range(3))
+    R, S, D, O = (svtgpu.Frame(ctx, W, H, bd) for _ in range(4))
     R.upload(rec, sp)
     S.upload(src, sp)
+    mi = synth.mode_info(W, H, 3)
+    dl = svtgpu.DlfState(ctx, W, H)
+    dl.set_mode_info(mi, sp)
+    lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
     ctrls = svtgpu.cdef_controls(a.cdef_level)
     st = svtgpu.CdefState(ctx, W, H)
     nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
@@ -100,24 +112,33 @@ def main():
         skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
         st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
 
-    ev = []  # (start, end) around the dominant kernel, on the stream it is launched on
+    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply)
+    lf_levels = []
 
     def step(timed):
+        es = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if timed:
+            es[0].record(stream)
+        # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
+        lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
+        dl.filter_to(R, D, lfp, 0, 3, sp)
+        if timed:
+            es[1].record(stream)
+            lf_levels.append(lfp.levels())
+        # CDEF stage on the deblocked frame
         if n > 1:
             st.clear_tables(sp)
+        st.search(D, S, ctrls, q, sp)
         if timed:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        st.search(R, S, ctrls, q, sp)
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
+            es[2].record(stream)
         if n > 1:
             dist.all_reduce(mse_t)   # zero-padded band tables -> full frame table (RCCL over xGMI)
             dist.all_reduce(skip_t)
         prm, _ = st.pick(ctrls, q, lam, sp)
-        st.apply(R, O, prm, sp)
+        st.apply(D, O, prm, sp)
+        if timed:
+            es[3].record(stream)
+            ev.append(es)
 
     for _ in range(a.warmup):
         step(False)
@@ -137,7 +158,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    search_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(3)] for es in ev], axis=0)
+    dlf_ms, search_ms, cdef_rest_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
     value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
@@ -162,10 +184,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u16" if bd > 8 else "u8",
         "data": "synthetic",
-        "config": {"workload": "cdef_search+pick+apply %dx%d %d-bit 4:2:0, cdef_level %d (%d strengths); "
-                               "DLF/LR/SAD not yet in the step" % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
+        "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply %dx%d %d-bit 4:2:0, dlf level 1 "
+                               "(full-image search), cdef_level %d (%d strengths); LR/SAD not yet in the step"
+                               % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
-                   "parallelism": "fb_row_bands%d" % n if n > 1 else "single"},
+                   "parallelism": "fb_row_bands%d" % n if n > 1 else "single",
+                   "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
+                                "cdef_pick_apply": round(cdef_rest_ms, 4)},
+                   "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
         "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": None, "avg_launch_ms": round(search_ms, 4),
@@ -173,7 +199,7 @@ def main():
                              "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))},
     }
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(src, rec, bd, a.cdef_level, q, lam, a.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(src, rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if n > 1:

@@ -277,6 +277,10 @@ int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stre
  * SB-lagged order with combine_vert_horz_lf = 1, :41, :580-605), in place on `frame`. */
 int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params, int32_t plane_start,
                      int32_t plane_end, void *stream);
+/* Out-of-place form of svtgpu_dlf_frame: reads `in`, writes every sample of planes
+ * [plane_start, plane_end) of `out` (filtered, or copied when the plane is not filtered). */
+int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
+                        int32_t plane_start, int32_t plane_end, void *stream);
 /* ≙ svt_av1_pick_filter_level(LPF_PICK_FROM_FULL_IMAGE) (EbDeblockingFilter.c:1129-1252): bisection
  * on the filter level per plane with a device trial per level (filter + SSE vs `source` + restore).
  * `params` carries the previous levels in and the picked levels out; `recon` is left unfiltered.

@@ -593,31 +593,59 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
     return SVTGPU_OK;
 }
 
-extern "C" int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params,
-                                int32_t plane_start, int32_t plane_end, void *stream) {
-    if (!s || !frame_matches(s, frame) || !valid_params(params) || plane_start < 0 || plane_end > 3 ||
-        plane_start > plane_end || !s->have_mi)
-        return SVTGPU_ERR_INVALID_ARG;
-    hipStream_t st = pick_stream(s->ctx, stream);
+namespace {
+// filter planes [ps, pe) of `in` into `out`; in == out is allowed (the plane is staged in scratch)
+int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
+                   int32_t ps, int32_t pe, hipStream_t st) {
     LevelTables L;
     build_level_tables(*params, L);
-    for (int pl = plane_start; pl < plane_end; pl++) {
-        if (pl == 0 && !plane_active(*params, 0)) break; // luma off: no plane is filtered (:575-577)
-        if (!plane_active(*params, pl)) continue;
-        const size_t bps = frame->bytes_per_sample;
-        HIP_TRY(hipMemcpy2DAsync(s->d_scratch, frame->pw[pl] * bps, frame->plane[pl], frame->stride[pl] * bps,
-                                 frame->pw[pl] * bps, frame->ph[pl], hipMemcpyDeviceToDevice, st));
-        DlfTileArgs a = base_args(s, frame, pl, L);
-        a.src        = s->d_scratch;
-        a.src_stride = frame->pw[pl];
-        a.dst        = frame->plane[pl];
-        a.dst_stride = frame->stride[pl];
+    bool luma_off = false;
+    for (int pl = ps; pl < pe; pl++) {
+        if (pl == 0 && !plane_active(*params, 0)) luma_off = true; // no plane is filtered (:575-577)
+        const size_t bps = in->bytes_per_sample;
+        const bool   on  = !luma_off && plane_active(*params, pl);
+        if (!on) {
+            if (in != out)
+                HIP_TRY(hipMemcpy2DAsync(out->plane[pl], out->stride[pl] * bps, in->plane[pl], in->stride[pl] * bps,
+                                         in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
+            continue;
+        }
+        DlfTileArgs a = base_args(s, in, pl, L);
+        if (in == out) {
+            HIP_TRY(hipMemcpy2DAsync(s->d_scratch, in->pw[pl] * bps, in->plane[pl], in->stride[pl] * bps,
+                                     in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
+            a.src        = s->d_scratch;
+            a.src_stride = in->pw[pl];
+        } else {
+            a.src        = in->plane[pl];
+            a.src_stride = in->stride[pl];
+        }
+        a.dst        = out->plane[pl];
+        a.dst_stride = out->stride[pl];
         a.ntrial     = 1;
         for (int dir = 0; dir < 2; dir++) std::memcpy(a.lvl[0][dir], L.lvl[pl][dir], 128);
         int rc = launch_tile(a, (int)bps, false, st);
         if (rc) return rc;
     }
     return SVTGPU_OK;
+}
+} // namespace
+
+extern "C" int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params,
+                                int32_t plane_start, int32_t plane_end, void *stream) {
+    if (!s || !frame_matches(s, frame) || !valid_params(params) || plane_start < 0 || plane_end > 3 ||
+        plane_start > plane_end || !s->have_mi)
+        return SVTGPU_ERR_INVALID_ARG;
+    return dlf_frame_impl(s, frame, frame, params, plane_start, plane_end, pick_stream(s->ctx, stream));
+}
+
+extern "C" int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out,
+                                   const SvtGpuLfParams *params, int32_t plane_start, int32_t plane_end,
+                                   void *stream) {
+    if (!s || !frame_matches(s, in) || !frame_matches(s, out) || in->bit_depth != out->bit_depth ||
+        !valid_params(params) || plane_start < 0 || plane_end > 3 || plane_start > plane_end || !s->have_mi)
+        return SVTGPU_ERR_INVALID_ARG;
+    return dlf_frame_impl(s, in, out, params, plane_start, plane_end, pick_stream(s->ctx, stream));
 }
 
 extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source,

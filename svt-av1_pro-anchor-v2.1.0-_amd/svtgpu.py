@@ -158,6 +158,7 @@ _SIGS = {
     "svtgpu_dlf_state_destroy": (None, [_P]),
     "svtgpu_dlf_set_mode_info": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_dlf_frame": (ctypes.c_int, [_P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
+    "svtgpu_dlf_frame_to": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
 }
@@ -359,6 +360,9 @@ class DlfState:
 
     def filter(self, frame, params, plane_start=0, plane_end=3, stream=None):
         check(lib().svtgpu_dlf_frame(self.h, frame.h, ctypes.byref(params), plane_start, plane_end, stream))
+
+    def filter_to(self, src, out, params, plane_start=0, plane_end=3, stream=None):
+        check(lib().svtgpu_dlf_frame_to(self.h, src.h, out.h, ctypes.byref(params), plane_start, plane_end, stream))
 
     def pick(self, recon, source, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=2,
              only_4x4=0, stream=None):

@@ -97,6 +97,15 @@ def test_dlf_frame_vs_oracle(ctx, w, h, bd, seed, pk, mk):
     for p in range(3):
         assert np.array_equal(got[p], want[p]), p
     assert any(not np.array_equal(want[p], rec[p]) for p in range(3))
+    # out-of-place form
+    A, B = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+    A.upload(rec)
+    st = svtgpu.DlfState(ctx, w, h)
+    st.set_mode_info(mi)
+    st.filter_to(A, B, prm)
+    got2, back = B.download(), A.download()
+    for p in range(3):
+        assert np.array_equal(got2[p], want[p]) and np.array_equal(back[p], rec[p]), p
 
 
 def test_dlf_frame_4k10_vs_oracle(ctx):
@@ -113,7 +122,8 @@ def test_dlf_frame_4k10_vs_oracle(ctx):
 # ------------------------------------------------------------------ level search vs oracle
 PICK_CASES = [
     # w, h, bd, seed, start levels, dlf_avg, dlf_avg_uv, tl, early_exit, only4x4
-    (320, 192, 10, 11, (20, 20, 8, 8), 0, 0, 0, 2, 0),
+    (320, 192, 10, 11, (20, 20, 8, 8), 0, 0, 0, 0, 0),   # dlf level 1 (EncModeConfig.c:1569-1576)
+    (320, 192, 10, 15, (32, 32, 16, 16), 0, 0, 0, 2, 0),
     (256, 128, 8, 12, (0, 0, 0, 0), 0, 0, 0, 1, 0),
     (384, 200, 10, 13, (40, 36, 12, 30), 1, 1, 1, 2, 1),
     (192, 192, 8, 14, (63, 5, 63, 0), 0, 1, 0, 3, 0),
