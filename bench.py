@@ -7,6 +7,8 @@ A "step" = one 4K 10-bit 4:2:0 frame through the device-resident in-loop filter 
   CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
       strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
       (svt_av1_cdef_frame).
+  MD distortion stage: SAD / SSE / variance of every AV1 block shape of every SB against 7 reference
+      frames at one full-pel motion vector per (SB, reference) (SURVEY.md §8d config 5 workload at 4K).
 Inputs are synthetic (recon = source + blocking/ringing, 16x16 non-skip inter blocks
 with hashed 4/8/16 transforms) and resident in HBM before timing.
 
@@ -102,6 +104,15 @@ def main():
     dl = svtgpu.DlfState(ctx, W, H)
     dl.set_mode_info(mi, sp)
     lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
+    NREF = 7
+    md_refs = []
+    for r in range(NREF):
+        rs, _ = synth.frame_pair(W, H, bd, seed=0x5EED0005 + 17 * (r + 1))
+        f = svtgpu.Frame(ctx, W, H, bd)
+        f.upload(rs, sp)
+        md_refs.append(f)
+    md = svtgpu.MdBatch(ctx, W, H, NREF)
+    md.set_mvs(np.random.default_rng(5).integers(-16, 17, size=(md.nsb, NREF, 2)), sp)
     ctrls = svtgpu.cdef_controls(a.cdef_level)
     st = svtgpu.CdefState(ctx, W, H)
     nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
@@ -112,11 +123,16 @@ def main():
         skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
         st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
 
-    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply)
+    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | md)
+    if n > 1:  # MD batch: SB row bands, no collective
+        sbr = np.linspace(0, md.nsb, n + 1).round().astype(int)
+        md_range = (int(sbr[rank]), int(sbr[rank + 1]))
+    else:
+        md_range = (0, md.nsb)
     lf_levels = []
 
     def step(timed):
-        es = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        es = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
         if timed:
             es[0].record(stream)
         # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
@@ -138,6 +154,10 @@ def main():
         st.apply(D, O, prm, sp)
         if timed:
             es[3].record(stream)
+        # MD distortion batch (source vs 7 references, every block shape)
+        md.run(S, md_refs, md_range[0], md_range[1], sp)
+        if timed:
+            es[4].record(stream)
             ev.append(es)
 
     for _ in range(a.warmup):
@@ -158,8 +178,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(3)] for es in ev], axis=0)
-    dlf_ms, search_ms, cdef_rest_ms = (float(x) for x in stage_ms)
+    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] for es in ev], axis=0)
+    dlf_ms, search_ms, cdef_rest_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
     value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
@@ -185,12 +205,13 @@ def main():
         "dtype": "u16" if bd > 8 else "u8",
         "data": "synthetic",
         "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply %dx%d %d-bit 4:2:0, dlf level 1 "
-                               "(full-image search), cdef_level %d (%d strengths); LR/SAD not yet in the step"
+                               "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
+                               "LR not yet in the step"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
                    "parallelism": "fb_row_bands%d" % n if n > 1 else "single",
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
-                                "cdef_pick_apply": round(cdef_rest_ms, 4)},
+                                "cdef_pick_apply": round(cdef_rest_ms, 4), "md_sad_sse_var": round(md_ms, 4)},
                    "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
         "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

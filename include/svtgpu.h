@@ -293,6 +293,142 @@ int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *so
  * over the frame, EbDeblockingFilter.c:716-838). Synchronous. */
 int svtgpu_plane_sse(const SvtGpuFrame *a, const SvtGpuFrame *b, int32_t plane, uint64_t *sse, void *stream);
 
+
+/* =========================================================================================
+ * Mode-decision distortion: SAD / SSE / variance
+ * ========================================================================================= */
+/* RTCD-compatible per-block shims, one per AV1 block size (BlockSize order).  Synchronous.
+ *   svtgpu_aom_sad{W}x{H}              ≙ svt_aom_sad{W}x{H}            (aom_dsp_rtcd.h:264-350, C EbComputeSAD_C.c:117-206)
+ *   svtgpu_aom_sad{W}x{H}x4d           ≙ svt_aom_sad{W}x{H}x4d
+ *   svtgpu_aom_variance{W}x{H}         ≙ svt_aom_variance{W}x{H}       (aom_dsp_rtcd.h:480-540, C variance.c:300-345)
+ *   svtgpu_aom_highbd_10_variance{W}x{H} ≙ svt_aom_highbd_10_variance{W}x{H} (aom_dsp_rtcd.h:544-570, C EbPsnr.c:174-214);
+ *       its pointers are CONVERT_TO_BYTEPTR-encoded uint16_t planes, as in the reference (EbDefinitions.h:950-951). */
+uint32_t     svtgpu_aom_sad4x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad4x4x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance4x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance4x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad4x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad4x8x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance4x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance4x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad8x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad8x4x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance8x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance8x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad8x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad8x8x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance8x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance8x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad8x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad8x16x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance8x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance8x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad16x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad16x8x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance16x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance16x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad16x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad16x16x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance16x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance16x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad16x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad16x32x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance16x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance16x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad32x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad32x16x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance32x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance32x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad32x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad32x32x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance32x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance32x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad32x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad32x64x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance32x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance32x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad64x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad64x32x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance64x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance64x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad64x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad64x64x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance64x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance64x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad64x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad64x128x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance64x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance64x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad128x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad128x64x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance128x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance128x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad128x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad128x128x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance128x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance128x128(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad4x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad4x16x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance4x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance4x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad16x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad16x4x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance16x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance16x4(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad8x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad8x32x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance8x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance8x32(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad32x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad32x8x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance32x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance32x8(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad16x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad16x64x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance16x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance16x64(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+uint32_t     svtgpu_aom_sad64x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride);
+void         svtgpu_aom_sad64x16x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[], int ref_stride, uint32_t *sad_array);
+unsigned int svtgpu_aom_variance64x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+unsigned int svtgpu_aom_highbd_10_variance64x16(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, unsigned int *sse);
+/* ≙ sad_16b_kernel (aom_dsp_rtcd.h:861, C svt_aom_sad_16b_kernel_c EbComputeSAD_C.c:39) */
+uint32_t svtgpu_sad_16b_kernel(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride, uint32_t height,
+                               uint32_t width);
+/* ≙ svt_aom_sse / svt_aom_highbd_sse (aom_dsp_rtcd.h:54-56, C EbEncInterPrediction.c:562-590; highbd takes plain
+ * uint16_t planes cast to uint8_t*) */
+int64_t svtgpu_aom_sse(const uint8_t *a, int a_stride, const uint8_t *b, int b_stride, int width, int height);
+int64_t svtgpu_aom_highbd_sse(const uint8_t *a8, int a_stride, const uint8_t *b8, int b_stride, int width, int height);
+/* ≙ svt_spatial_full_distortion_kernel / svt_full_distortion_kernel16_bits (common_dsp_rtcd.h:169-171) */
+uint64_t svtgpu_spatial_full_distortion_kernel(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
+                                               uint8_t *recon, int32_t recon_offset, uint32_t recon_stride,
+                                               uint32_t area_width, uint32_t area_height);
+uint64_t svtgpu_full_distortion_kernel16_bits(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
+                                              uint8_t *recon, int32_t recon_offset, uint32_t recon_stride,
+                                              uint32_t area_width, uint32_t area_height);
+
+/* Batched MD distortion (the frame-level GPU boundary; no single reference equivalent: it evaluates what
+ * the MD candidate loops evaluate block by block through svt_aom_mefn_ptr, av1me.c:29-174).
+ * For every 64x64 SB of `source` and every reference frame r at the SB's full-pel motion vector
+ * mv[sb][r] = {x, y}, it computes for every block of every AV1 shape <= 64x64 tiling the SB:
+ *   q = 0: SAD (sad{W}x{H} / sad_16b_kernel), q = 1: the *sse the variance function reports,
+ *   q = 2: the variance (8-bit: svt_aom_variance{W}x{H}; 10-bit: svt_aom_highbd_10_variance{W}x{H}).
+ * Samples outside the frame read the nearest edge sample (the encoder's padded pictures).
+ * Output layout: out[sb][r][q][SVTGPU_MD_BLOCKS]; shapes in BlockSize order without the 128 shapes,
+ * blocks of one shape in raster order (svtgpu_md_layout). */
+#define SVTGPU_MD_SHAPES 19
+#define SVTGPU_MD_BLOCKS 849
+typedef struct SvtGpuMdBatch SvtGpuMdBatch;
+int     svtgpu_md_batch_create(SvtGpuContext *ctx, int32_t width, int32_t height, int32_t nref, SvtGpuMdBatch **out);
+void    svtgpu_md_batch_destroy(SvtGpuMdBatch *b);
+int32_t svtgpu_md_batch_nsb(const SvtGpuMdBatch *b);
+int     svtgpu_md_set_mvs(SvtGpuMdBatch *b, const int16_t *mv, void *stream); /* host [nsb][nref][2] */
+int     svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source, const SvtGpuFrame *const *refs,
+                             int32_t sb_begin, int32_t sb_end, void *stream);
+int     svtgpu_md_read(SvtGpuMdBatch *b, uint32_t *out, int32_t sb_begin, int32_t sb_end, void *stream);
+void   *svtgpu_md_out_device_ptr(SvtGpuMdBatch *b);
+/* shape_w/shape_h/shape_offset: [SVTGPU_MD_SHAPES] block dims and first output index of each shape */
+void    svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offset);
+
 #ifdef __cplusplus
 }
 #endif

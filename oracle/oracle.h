@@ -68,6 +68,17 @@ int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams 
 int oracle_dlf_pick(OracleFrame *recon, const OracleFrame *src, const SvtGpuLfMi *mi, SvtGpuLfParams *p, int dlf_avg,
                     int dlf_avg_uv, int temporal_layer_index, int early_exit, int only4x4);
 
+/* ---- mode-decision distortion (md_oracle.c) ---- */
+uint32_t oracle_sad(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h);
+uint32_t oracle_sad16(const uint16_t *a, int as, const uint16_t *b, int bs, int w, int h);
+uint32_t oracle_variance(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h, uint32_t *sse);
+uint32_t oracle_highbd_10_variance(const uint16_t *a, int as, const uint16_t *b, int bs, int w, int h, uint32_t *sse);
+int64_t  oracle_sse(const uint8_t *a, int as, const uint8_t *b, int bs, int w, int h);
+int64_t  oracle_sse16(const uint16_t *a, int as, const uint16_t *b, int bs, int w, int h);
+/* out: [nsb][nref][3][SVTGPU_MD_BLOCKS]; mv: [nsb][nref][2] */
+int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs, int nref, const int16_t *mv,
+                         uint32_t *out);
+
 #ifdef __cplusplus
 }
 #endif

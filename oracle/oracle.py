@@ -44,6 +44,16 @@ _SIGS = {
                                                ctypes.POINTER(CdefParams), _P]),
     "oracle_lpf": (None, [_P, _I32, ctypes.c_int, ctypes.c_int, _P, _P, _P]),
     "oracle_highbd_lpf": (None, [_P, _I32, ctypes.c_int, ctypes.c_int, _P, _P, _P, _I32]),
+    "oracle_sad": (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_sad16": (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_variance": (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_uint32)]),
+    "oracle_highbd_10_variance": (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.POINTER(ctypes.c_uint32)]),
+    "oracle_sse": (ctypes.c_int64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_sse16": (ctypes.c_int64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_md_dist_batch": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(ctypes.POINTER(OracleFrame)),
+                                            ctypes.c_int, _P, _P]),
     "oracle_dlf_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), _P, ctypes.POINTER(LfParams), ctypes.c_int,
                                         ctypes.c_int]),
     "oracle_dlf_pick": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
@@ -182,3 +192,41 @@ def dlf_pick(rec, src, bd, mi, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_i
                                temporal_layer_index, early_exit, only_4x4)
     assert rc == 0
     return p
+
+
+MD_SHAPES = [(4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 8), (16, 16), (16, 32), (32, 16), (32, 32), (32, 64),
+             (64, 32), (64, 64), (4, 16), (16, 4), (8, 32), (32, 8), (16, 64), (64, 16)]
+MD_BLOCKS = 849
+
+
+def block_dist(src, ref, w, h, bd):
+    """(sad, sse, var) of one block with the reference's per-bit-depth kernels (arrays 2-D, any stride)."""
+    L = lib()
+    s = np.ascontiguousarray(src)
+    r = np.ascontiguousarray(ref)
+    sse = ctypes.c_uint32()
+    if bd > 8:
+        s, r = s.astype(np.uint16), r.astype(np.uint16)
+        sad = L.oracle_sad16(ptr(s), s.shape[1], ptr(r), r.shape[1], w, h)
+        var = L.oracle_highbd_10_variance(ptr(s), s.shape[1], ptr(r), r.shape[1], w, h, ctypes.byref(sse))
+    else:
+        s, r = s.astype(np.uint8), r.astype(np.uint8)
+        sad = L.oracle_sad(ptr(s), s.shape[1], ptr(r), r.shape[1], w, h)
+        var = L.oracle_variance(ptr(s), s.shape[1], ptr(r), r.shape[1], w, h, ctypes.byref(sse))
+    return sad, sse.value, var
+
+
+def md_dist_batch(src_y, ref_ys, bd, mv):
+    """Batched MD distortion over all SBs / refs / shapes; returns uint32 [nsb][nref][3][849]."""
+    keep = []
+    h, w = src_y.shape
+    dummy = [np.zeros((h // 2, w // 2), src_y.dtype)] * 2
+    S = _frame([src_y] + dummy, bd, keep)
+    Rs = [_frame([r] + dummy, bd, keep) for r in ref_ys]
+    arr = (ctypes.POINTER(OracleFrame) * len(Rs))(*[ctypes.pointer(x) for x in Rs])
+    nsb = ((w + 63) // 64) * ((h + 63) // 64)
+    mv = np.ascontiguousarray(mv, np.int16)
+    assert mv.shape == (nsb, len(ref_ys), 2)
+    out = np.zeros((nsb, len(ref_ys), 3, MD_BLOCKS), np.uint32)
+    lib().oracle_md_dist_batch(ctypes.byref(S), arr, len(Rs), ptr(mv), ptr(out))
+    return out

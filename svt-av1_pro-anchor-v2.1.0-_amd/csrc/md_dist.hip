@@ -1,0 +1,421 @@
+// md_dist.hip — mode-decision distortion on gfx950: SAD / SSE / variance for every AV1 block shape.
+//
+// Reference kernels (Source/Lib/): Encoder/C_DEFAULT/EbComputeSAD_C.c:39-206 (sad, sad_16b_kernel, x4d),
+// Encoder/C_DEFAULT/variance.c:256-345 (variance{W}x{H}), Encoder/Codec/EbPsnr.c:146-214
+// (highbd_10_variance{W}x{H}), Encoder/Codec/EbEncInterPrediction.c:562-590 (sse / highbd_sse),
+// Common/C_DEFAULT/EbPictureOperators_C.c:62 and Common/Codec/EbPictureOperators.c:174 (full distortion).
+//
+// Batch design (svtgpu_md_dist_batch): one 256-lane workgroup per 64x64 SB stages the source SB in LDS
+// once and loops over the reference frames.  Each lane owns one 4x4 cell (lanes 0-15 of a cell row read
+// 64 consecutive samples of a picture row, so each load instruction covers 4 rows x 128 B); the cell's
+// SAD, SSE and signed sum are additive, so every larger shape is reduced from two halves of a smaller
+// one in 8 LDS passes (no sample is read twice), and the per-bit-depth variance formula of the
+// reference is applied per block at the end.  Output rows [q][849] per (SB, ref) are written coalesced.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "svtgpu_internal.h"
+
+namespace {
+
+constexpr int kShapes = SVTGPU_MD_SHAPES;
+constexpr int kBlocks = SVTGPU_MD_BLOCKS;
+// BlockSize order without the 128 shapes (EbDefinitions.h BlockSize enum); offsets of each shape's blocks
+#define MD_W {4, 4, 8, 8, 8, 16, 16, 16, 32, 32, 32, 64, 64, 4, 16, 8, 32, 16, 64}
+#define MD_H {4, 8, 4, 8, 16, 8, 16, 32, 16, 32, 64, 32, 64, 16, 4, 32, 8, 64, 16}
+#define MD_OFF {0, 256, 384, 512, 576, 608, 640, 656, 664, 672, 676, 678, 680, 681, 745, 809, 825, 841, 845, 849}
+constexpr int    h_w[kShapes] = MD_W, h_h[kShapes] = MD_H, h_off[kShapes + 1] = MD_OFF;
+__constant__ int c_w[kShapes] = MD_W, c_h[kShapes] = MD_H, c_off[kShapes + 1] = MD_OFF;
+
+// reduction steps: shape s = two halves of child shape c (horizontally or vertically adjacent);
+// steps [c_pass_end[p-1], c_pass_end[p]) depend only on earlier passes
+struct Step {
+    int s, c, horiz;
+};
+__constant__ int  c_pass_end[8] = {2, 5, 7, 10, 12, 15, 17, 18};
+__constant__ Step c_steps[18]   = {
+    {2, 0, 1}, {1, 0, 0},               // 8x4, 4x8 from 4x4
+    {3, 2, 0}, {14, 2, 1}, {13, 1, 0},  // 8x8, 16x4, 4x16
+    {5, 3, 1}, {4, 3, 0},               // 16x8, 8x16
+    {6, 5, 0}, {16, 5, 1}, {15, 4, 0},  // 16x16, 32x8, 8x32
+    {8, 6, 1}, {7, 6, 0},               // 32x16, 16x32
+    {9, 8, 0}, {18, 8, 1}, {17, 7, 0},  // 32x32, 64x16, 16x64
+    {11, 9, 1}, {10, 9, 0},             // 64x32, 32x64
+    {12, 11, 0},                        // 64x64
+};
+
+struct MdArgs {
+    const void    *src;
+    int32_t        src_stride;
+    const void    *ref[8];
+    int32_t        ref_stride[8];
+    const int16_t *mv; // [nsb][nref][2]
+    uint32_t      *out; // [nsb][nref][3][849]
+    int32_t        nref, width, height, nsbx, sb_begin, highbd;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
+    __shared__ uint16_t s_src[64 * 64];
+    __shared__ uint32_t s_sad[kBlocks], s_sse[kBlocks];
+    __shared__ int32_t  s_sum[kBlocks];
+    const int tid = threadIdx.x;
+    const int sb  = a.sb_begin + blockIdx.x;
+    const int ox = (sb % a.nsbx) * 64, oy = (sb / a.nsbx) * 64;
+    const int W = a.width, H = a.height;
+    const T  *src = (const T *)a.src;
+    const bool inside = ox + 64 <= W && oy + 64 <= H;
+    for (int i = tid; i < 64 * 64; i += 256) {
+        int y = oy + i / 64, x = ox + i % 64;
+        if (!inside) y = min(y, H - 1), x = min(x, W - 1);
+        s_src[i] = src[(size_t)y * a.src_stride + x];
+    }
+    const int cy = tid >> 4, cx = tid & 15;
+    for (int r = 0; r < a.nref; r++) {
+        const int mx = a.mv[((size_t)sb * a.nref + r) * 2], my = a.mv[((size_t)sb * a.nref + r) * 2 + 1];
+        const T  *ref = (const T *)a.ref[r];
+        const int rs  = a.ref_stride[r];
+        const int rx = ox + mx, ry = oy + my;
+        const bool rin = rx >= 0 && ry >= 0 && rx + 64 <= W && ry + 64 <= H;
+        __syncthreads(); // s_src staged / previous reference's outputs written
+        uint32_t sad = 0, sse = 0;
+        int32_t  sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            int y = ry + cy * 4 + i;
+            if (!rin) y = min(max(y, 0), H - 1);
+            const T *row = ref + (size_t)y * rs;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                int x = rx + cx * 4 + j;
+                if (!rin) x = min(max(x, 0), W - 1);
+                const int d = (int)s_src[(cy * 4 + i) * 64 + cx * 4 + j] - (int)row[x];
+                sad += (uint32_t)abs(d);
+                sse += (uint32_t)(d * d);
+                sum += d;
+            }
+        }
+        s_sad[tid] = sad, s_sse[tid] = sse, s_sum[tid] = sum;
+        // hierarchical reduction: 8 passes, each shape from two halves of an already reduced shape
+        int st = 0;
+        for (int p = 0; p < 8; p++) {
+            __syncthreads();
+            for (; st < c_pass_end[p]; st++) {
+                const Step q    = c_steps[st];
+                const int  ncol = 64 / c_w[q.s], n = 4096 / (c_w[q.s] * c_h[q.s]);
+                const int  ccol = 64 / c_w[q.c];
+                for (int b = tid; b < n; b += 256) {
+                    const int bi = b / ncol, bj = b % ncol;
+                    const int c0 = q.horiz ? bi * ccol + 2 * bj : 2 * bi * ccol + bj;
+                    const int c1 = q.horiz ? c0 + 1 : c0 + ccol;
+                    const int dst = c_off[q.s] + b, x0 = c_off[q.c] + c0, x1 = c_off[q.c] + c1;
+                    s_sad[dst] = s_sad[x0] + s_sad[x1];
+                    s_sse[dst] = s_sse[x0] + s_sse[x1];
+                    s_sum[dst] = s_sum[x0] + s_sum[x1];
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t *out = a.out + ((size_t)sb * a.nref + r) * 3 * kBlocks;
+        for (int k = tid; k < kBlocks; k += 256) {
+            int s = 0;
+            while (k >= c_off[s + 1]) s++;
+            const int n = c_w[s] * c_h[s];
+            uint32_t  e, v;
+            if (a.highbd) { // highbd_10_variance: sse rounded >> 4, sum rounded >> 2, clamped at 0
+                e                = (s_sse[k] + 8u) >> 4;
+                const int64_t rs2 = ((int64_t)s_sum[k] + 2) >> 2;
+                const int64_t var = (int64_t)e - (rs2 * rs2) / n;
+                v                = var >= 0 ? (uint32_t)var : 0u;
+            } else {
+                e = s_sse[k];
+                v = e - (uint32_t)(((int64_t)s_sum[k] * s_sum[k]) / n);
+            }
+            out[k]               = s_sad[k];
+            out[kBlocks + k]     = e;
+            out[2 * kBlocks + k] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// per-block shims: Σ|d|, Σd², Σd over nblk compact uint16 blocks (block i of a at a + i*w*h)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void block_stats_kernel(const uint16_t *a, const uint16_t *b, int n,
+                                                          unsigned long long *out) {
+    __shared__ long long red[3][4];
+    const uint16_t *pa = a + (size_t)blockIdx.x * n, *pb = b + (size_t)blockIdx.x * n;
+    unsigned long long sad = 0, sse = 0;
+    long long          sum = 0;
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const int d = (int)pa[i] - (int)pb[i];
+        sad += (unsigned)abs(d);
+        sse += (unsigned long long)((long long)d * d);
+        sum += d;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sad += __shfl_down(sad, o, 64);
+        sse += __shfl_down(sse, o, 64);
+        sum += __shfl_down(sum, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = (long long)sad;
+        red[1][threadIdx.x >> 6] = (long long)sse;
+        red[2][threadIdx.x >> 6] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int q = threadIdx.x;
+        out[blockIdx.x * 3 + q] = (unsigned long long)(red[q][0] + red[q][1] + red[q][2] + red[q][3]);
+    }
+}
+
+struct Stats {
+    uint64_t sad, sse;
+    int64_t  sum;
+};
+
+// stage nblk (w x h) blocks (a: 1 block, broadcast; b: nblk blocks) and reduce them on the device
+template <typename T>
+void block_stats(const T *a, int as, const T *const *b, int bs, int nblk, int w, int h, Stats *out) {
+    const int             n = w * h;
+    std::vector<uint16_t> ha((size_t)n * nblk), hb((size_t)n * nblk);
+    for (int k = 0; k < nblk; k++)
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                ha[(size_t)k * n + y * w + x] = a[(size_t)y * as + x];
+                hb[(size_t)k * n + y * w + x] = b[k][(size_t)y * bs + x];
+            }
+    static thread_local uint16_t *d = nullptr;
+    static thread_local size_t    cap = 0;
+    static thread_local unsigned long long *dr = nullptr;
+    const size_t need = (size_t)2 * n * nblk * sizeof(uint16_t);
+    if (need > cap) {
+        if (d) (void)hipFree(d);
+        HIP_OR_DIE(hipMalloc(&d, need));
+        cap = need;
+    }
+    if (!dr) HIP_OR_DIE(hipMalloc(&dr, sizeof(unsigned long long) * 3 * 4));
+    hipStream_t st = svtgpu_default_stream();
+    HIP_OR_DIE(hipMemcpyAsync(d, ha.data(), need / 2, hipMemcpyHostToDevice, st));
+    HIP_OR_DIE(hipMemcpyAsync(d + (size_t)n * nblk, hb.data(), need / 2, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(block_stats_kernel, dim3(nblk), dim3(256), 0, st, d, d + (size_t)n * nblk, n, dr);
+    HIP_OR_DIE(hipGetLastError());
+    unsigned long long r[12];
+    HIP_OR_DIE(hipMemcpyAsync(r, dr, sizeof(unsigned long long) * 3 * nblk, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int k = 0; k < nblk; k++) out[k] = {r[3 * k], r[3 * k + 1], (int64_t)r[3 * k + 2]};
+}
+
+uint32_t var8(const Stats &s, int n, unsigned int *sse) { // svt_aom_variance{W}x{H}_c
+    *sse = (uint32_t)s.sse;
+    return *sse - (uint32_t)((s.sum * s.sum) / n);
+}
+uint32_t var10(const Stats &s, int n, unsigned int *sse) { // svt_aom_highbd_10_variance{W}x{H}_c
+    *sse                = (uint32_t)((s.sse + 8) >> 4);
+    const int     rsum  = (int)((s.sum + 2) >> 2);
+    const int64_t v     = (int64_t)*sse - ((int64_t)rsum * rsum) / n;
+    return v >= 0 ? (uint32_t)v : 0u;
+}
+inline const uint16_t *short_ptr(const uint8_t *p) { return (const uint16_t *)((uintptr_t)p << 1); }
+
+} // namespace
+
+#define MD_SIZE_SHIMS(W, H)                                                                                        \
+    extern "C" uint32_t svtgpu_aom_sad##W##x##H(const uint8_t *src, int src_stride, const uint8_t *ref,          \
+                                                int ref_stride) {                                                \
+        Stats s;                                                                                                 \
+        block_stats<uint8_t>(src, src_stride, &ref, ref_stride, 1, W, H, &s);                                     \
+        return (uint32_t)s.sad;                                                                                  \
+    }                                                                                                            \
+    extern "C" void svtgpu_aom_sad##W##x##H##x4d(const uint8_t *src, int src_stride, const uint8_t *const ref[],  \
+                                                 int ref_stride, uint32_t *sad_array) {                          \
+        Stats s[4];                                                                                              \
+        block_stats<uint8_t>(src, src_stride, ref, ref_stride, 4, W, H, s);                                       \
+        for (int i = 0; i < 4; i++) sad_array[i] = (uint32_t)s[i].sad;                                           \
+    }                                                                                                            \
+    extern "C" unsigned int svtgpu_aom_variance##W##x##H(const uint8_t *src, int src_stride, const uint8_t *ref, \
+                                                         int ref_stride, unsigned int *sse) {                    \
+        Stats s;                                                                                                 \
+        block_stats<uint8_t>(src, src_stride, &ref, ref_stride, 1, W, H, &s);                                     \
+        return var8(s, W * H, sse);                                                                              \
+    }                                                                                                            \
+    extern "C" unsigned int svtgpu_aom_highbd_10_variance##W##x##H(const uint8_t *src, int src_stride,           \
+                                                                   const uint8_t *ref, int ref_stride,           \
+                                                                   unsigned int *sse) {                          \
+        Stats           s;                                                                                       \
+        const uint16_t *r = short_ptr(ref);                                                                      \
+        block_stats<uint16_t>(short_ptr(src), src_stride, &r, ref_stride, 1, W, H, &s);                           \
+        return var10(s, W * H, sse);                                                                             \
+    }
+MD_SIZE_SHIMS(4, 4)
+MD_SIZE_SHIMS(4, 8)
+MD_SIZE_SHIMS(8, 4)
+MD_SIZE_SHIMS(8, 8)
+MD_SIZE_SHIMS(8, 16)
+MD_SIZE_SHIMS(16, 8)
+MD_SIZE_SHIMS(16, 16)
+MD_SIZE_SHIMS(16, 32)
+MD_SIZE_SHIMS(32, 16)
+MD_SIZE_SHIMS(32, 32)
+MD_SIZE_SHIMS(32, 64)
+MD_SIZE_SHIMS(64, 32)
+MD_SIZE_SHIMS(64, 64)
+MD_SIZE_SHIMS(64, 128)
+MD_SIZE_SHIMS(128, 64)
+MD_SIZE_SHIMS(128, 128)
+MD_SIZE_SHIMS(4, 16)
+MD_SIZE_SHIMS(16, 4)
+MD_SIZE_SHIMS(8, 32)
+MD_SIZE_SHIMS(32, 8)
+MD_SIZE_SHIMS(16, 64)
+MD_SIZE_SHIMS(64, 16)
+
+extern "C" uint32_t svtgpu_sad_16b_kernel(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride,
+                                          uint32_t height, uint32_t width) {
+    Stats           s;
+    const uint16_t *r = ref;
+    block_stats<uint16_t>(src, (int)src_stride, &r, (int)ref_stride, 1, (int)width, (int)height, &s);
+    return (uint32_t)s.sad;
+}
+extern "C" int64_t svtgpu_aom_sse(const uint8_t *a, int a_stride, const uint8_t *b, int b_stride, int width,
+                                  int height) {
+    Stats s;
+    block_stats<uint8_t>(a, a_stride, &b, b_stride, 1, width, height, &s);
+    return (int64_t)s.sse;
+}
+extern "C" int64_t svtgpu_aom_highbd_sse(const uint8_t *a8, int a_stride, const uint8_t *b8, int b_stride, int width,
+                                         int height) {
+    Stats           s;
+    const uint16_t *b = (const uint16_t *)b8;
+    block_stats<uint16_t>((const uint16_t *)a8, a_stride, &b, b_stride, 1, width, height, &s);
+    return (int64_t)s.sse;
+}
+extern "C" uint64_t svtgpu_spatial_full_distortion_kernel(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
+                                                          uint8_t *recon, int32_t recon_offset, uint32_t recon_stride,
+                                                          uint32_t area_width, uint32_t area_height) {
+    Stats          s;
+    const uint8_t *r = recon + recon_offset;
+    block_stats<uint8_t>(input + input_offset, (int)input_stride, &r, (int)recon_stride, 1, (int)area_width,
+                         (int)area_height, &s);
+    return s.sse;
+}
+extern "C" uint64_t svtgpu_full_distortion_kernel16_bits(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
+                                                         uint8_t *recon, int32_t recon_offset, uint32_t recon_stride,
+                                                         uint32_t area_width, uint32_t area_height) {
+    Stats           s;
+    const uint16_t *r = (const uint16_t *)recon + recon_offset;
+    block_stats<uint16_t>((const uint16_t *)input + input_offset, (int)input_stride, &r, (int)recon_stride, 1,
+                          (int)area_width, (int)area_height, &s);
+    return s.sse;
+}
+
+// ---------------------------------------------------------------------------------------------
+// batch object
+// ---------------------------------------------------------------------------------------------
+struct SvtGpuMdBatch {
+    SvtGpuContext *ctx;
+    int32_t        width, height, nref, nsbx, nsby;
+    int16_t       *d_mv;
+    uint32_t      *d_out;
+};
+
+extern "C" void svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offset) {
+    for (int s = 0; s < kShapes; s++) {
+        if (shape_w) shape_w[s] = h_w[s];
+        if (shape_h) shape_h[s] = h_h[s];
+        if (shape_offset) shape_offset[s] = h_off[s];
+    }
+}
+
+extern "C" int svtgpu_md_batch_create(SvtGpuContext *ctx, int32_t width, int32_t height, int32_t nref,
+                                      SvtGpuMdBatch **out) {
+    if (!ctx || !out || width <= 0 || height <= 0 || nref < 1 || nref > 8) return SVTGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    SvtGpuMdBatch *b = new SvtGpuMdBatch();
+    b->ctx           = ctx;
+    b->width         = width;
+    b->height        = height;
+    b->nref          = nref;
+    b->nsbx          = (width + 63) / 64;
+    b->nsby          = (height + 63) / 64;
+    const size_t nsb = (size_t)b->nsbx * b->nsby;
+    hipError_t   e   = hipMalloc(&b->d_mv, nsb * nref * 2 * sizeof(int16_t));
+    if (e == hipSuccess) e = hipMalloc(&b->d_out, nsb * nref * 3 * kBlocks * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(b->d_mv, 0, nsb * nref * 2 * sizeof(int16_t));
+    if (e != hipSuccess) {
+        svtgpu_md_batch_destroy(b);
+        svtgpu_set_last_hip_error(e, "md batch alloc", __FILE__, __LINE__);
+        return e == hipErrorOutOfMemory ? SVTGPU_ERR_OOM : SVTGPU_ERR_HIP;
+    }
+    *out = b;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_md_batch_destroy(SvtGpuMdBatch *b) {
+    if (!b) return;
+    (void)hipFree(b->d_mv);
+    (void)hipFree(b->d_out);
+    delete b;
+}
+
+extern "C" int32_t svtgpu_md_batch_nsb(const SvtGpuMdBatch *b) { return b ? b->nsbx * b->nsby : 0; }
+
+extern "C" void *svtgpu_md_out_device_ptr(SvtGpuMdBatch *b) { return b ? b->d_out : nullptr; }
+
+extern "C" int svtgpu_md_set_mvs(SvtGpuMdBatch *b, const int16_t *mv, void *stream) {
+    if (!b || !mv) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(b->ctx, stream);
+    HIP_TRY(hipMemcpyAsync(b->d_mv, mv, (size_t)b->nsbx * b->nsby * b->nref * 2 * sizeof(int16_t),
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source, const SvtGpuFrame *const *refs,
+                                    int32_t sb_begin, int32_t sb_end, void *stream) {
+    const int nsb = b ? b->nsbx * b->nsby : 0;
+    if (!b || !source || !refs || source->width != b->width || source->height != b->height || sb_begin < 0 ||
+        sb_end > nsb || sb_begin > sb_end)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (source->bit_depth != 8 && source->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
+    MdArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.src        = source->plane[0];
+    a.src_stride = source->stride[0];
+    for (int r = 0; r < b->nref; r++) {
+        const SvtGpuFrame *f = refs[r];
+        if (!f || f->width != b->width || f->height != b->height || f->bit_depth != source->bit_depth)
+            return SVTGPU_ERR_INVALID_ARG;
+        a.ref[r]        = f->plane[0];
+        a.ref_stride[r] = f->stride[0];
+    }
+    a.mv       = b->d_mv;
+    a.out      = b->d_out;
+    a.nref     = b->nref;
+    a.width    = b->width;
+    a.height   = b->height;
+    a.nsbx     = b->nsbx;
+    a.sb_begin = sb_begin;
+    a.highbd   = source->bit_depth > 8;
+    if (sb_end == sb_begin) return SVTGPU_OK;
+    hipStream_t st = pick_stream(b->ctx, stream);
+    if (a.highbd)
+        hipLaunchKernelGGL(md_dist_kernel<uint16_t>, dim3(sb_end - sb_begin), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(md_dist_kernel<uint8_t>, dim3(sb_end - sb_begin), dim3(256), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_md_read(SvtGpuMdBatch *b, uint32_t *out, int32_t sb_begin, int32_t sb_end, void *stream) {
+    const int nsb = b ? b->nsbx * b->nsby : 0;
+    if (!b || !out || sb_begin < 0 || sb_end > nsb || sb_begin > sb_end) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t  st  = pick_stream(b->ctx, stream);
+    const size_t row = (size_t)b->nref * 3 * kBlocks;
+    HIP_TRY(hipMemcpyAsync(out, b->d_out + sb_begin * row, (sb_end - sb_begin) * row * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}

@@ -107,6 +107,11 @@ class LfParams(ctypes.Structure):
         return p
 
 
+MD_SIZES = [(4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 8), (16, 16), (16, 32), (32, 16), (32, 32), (32, 64),
+            (64, 32), (64, 64), (64, 128), (128, 64), (128, 128), (4, 16), (16, 4), (8, 32), (32, 8), (16, 64),
+            (64, 16)]
+MD_BLOCKS = 849
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _U64 = ctypes.c_uint64
@@ -161,6 +166,29 @@ _SIGS = {
     "svtgpu_dlf_frame_to": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
+    **{"svtgpu_aom_sad%dx%d" % s: (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int]) for s in MD_SIZES},
+    **{"svtgpu_aom_sad%dx%dx4d" % s: (None, [_P, ctypes.c_int, _P, ctypes.c_int, _P]) for s in MD_SIZES},
+    **{"svtgpu_aom_variance%dx%d" % s: (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int,
+                                                          ctypes.POINTER(ctypes.c_uint32)]) for s in MD_SIZES},
+    **{"svtgpu_aom_highbd_10_variance%dx%d" % s: (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int,
+                                                                    ctypes.POINTER(ctypes.c_uint32)])
+       for s in MD_SIZES},
+    "svtgpu_sad_16b_kernel": (ctypes.c_uint32, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32]),
+    "svtgpu_aom_sse": (ctypes.c_int64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "svtgpu_aom_highbd_sse": (ctypes.c_int64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "svtgpu_spatial_full_distortion_kernel": (_U64, [_P, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_full_distortion_kernel16_bits": (_U64, [_P, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_md_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_md_batch_destroy": (None, [_P]),
+    "svtgpu_md_batch_nsb": (_I32, [_P]),
+    "svtgpu_md_set_mvs": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_md_dist_batch": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P]),
+    "svtgpu_md_read": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
+    "svtgpu_md_out_device_ptr": (_P, [_P]),
+    "svtgpu_md_layout": (None, [_P, _P, _P]),
 }
 
 _lib = None
@@ -383,6 +411,54 @@ class DlfState:
             self.close()
         except Exception:
             pass
+
+
+class MdBatch:
+    """Batched MD distortion: every SB x reference x AV1 block shape (SAD, sse, variance)."""
+
+    def __init__(self, ctx, width, height, nref):
+        self.ctx, self.width, self.height, self.nref = ctx, width, height, nref
+        h = _P()
+        check(lib().svtgpu_md_batch_create(ctx.h, width, height, nref, ctypes.byref(h)))
+        self.h = h
+        self.nsb = lib().svtgpu_md_batch_nsb(h)
+
+    def set_mvs(self, mv, stream=None):
+        a = np.ascontiguousarray(mv, dtype=np.int16)
+        assert a.shape == (self.nsb, self.nref, 2), a.shape
+        check(lib().svtgpu_md_set_mvs(self.h, ptr(a), stream))
+
+    def run(self, source, refs, sb_begin=0, sb_end=None, stream=None):
+        assert len(refs) == self.nref
+        arr = (_P * self.nref)(*[r.h for r in refs])
+        end = self.nsb if sb_end is None else sb_end
+        check(lib().svtgpu_md_dist_batch(self.h, source.h, arr, sb_begin, end, stream))
+
+    def read(self, sb_begin=0, sb_end=None, stream=None):
+        end = self.nsb if sb_end is None else sb_end
+        out = np.empty((end - sb_begin, self.nref, 3, MD_BLOCKS), np.uint32)
+        check(lib().svtgpu_md_read(self.h, ptr(out), sb_begin, end, stream))
+        return out
+
+    def out_device_ptr(self):
+        return lib().svtgpu_md_out_device_ptr(self.h)
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_md_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def md_layout():
+    w, h, o = (np.zeros(19, np.int32) for _ in range(3))
+    lib().svtgpu_md_layout(ptr(w), ptr(h), ptr(o))
+    return w, h, o
 
 
 def plane_sse(a, b, plane, stream=None):

@@ -88,3 +88,71 @@ def test_dlf_frame_golden():
             assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
         n += 1
     assert n >= 8
+
+
+# ---------------------------------------------------------------- MD distortion (gen_golden_md.c)
+MD_SIZES = [(4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 8), (16, 16), (16, 32), (32, 16), (32, 32), (32, 64),
+            (64, 32), (64, 64), (64, 128), (128, 64), (128, 128), (4, 16), (16, 4), (8, 32), (32, 8), (16, 64),
+            (64, 16)]
+
+
+def md_case(g, si, c):
+    """(src16, ref16, src8, ref8) views of golden case c of size si (the 8-bit kernels saw the low byte;
+    case 1 is the maximum-difference pattern 255/0)."""
+    s16, r16 = g["s%d_src" % si][c], g["s%d_ref" % si][c]
+    if c == 1:
+        return s16, r16, np.full(s16.shape, 255, np.uint8), np.zeros(r16.shape, np.uint8)
+    return s16, r16, (s16 & 255).astype(np.uint8), (r16 & 255).astype(np.uint8)
+
+
+def test_md_dist_golden():
+    L = oracle.lib()
+    import ctypes
+    g = cc.load("md_dist.bin")
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)
+    for si, (w, h) in enumerate(MD_SIZES):
+        res = g["s%d_res" % si]
+        for c in range(res.shape[0]):
+            s16, r16, s8, r8 = (np.ascontiguousarray(a) for a in md_case(g, si, c))
+            st = s16.shape[1]
+            sse = ctypes.c_uint32()
+            assert L.oracle_sad(P(s8), st, P(r8), st, w, h) == res[c][0], (w, h, c)
+            assert L.oracle_variance(P(s8), st, P(r8), st, w, h, ctypes.byref(sse)) == res[c][1], (w, h, c)
+            assert sse.value == res[c][2]
+            assert L.oracle_highbd_10_variance(P(s16), st, P(r16), st, w, h, ctypes.byref(sse)) == res[c][3], (w, h, c)
+            assert sse.value == res[c][4]
+            assert L.oracle_sad16(P(s16), st, P(r16), st, w, h) == res[c][5]
+            for k, off in enumerate((0, 1, st, 3 * st + 2)):
+                rr = np.ascontiguousarray(r8.reshape(-1)[off:])
+                assert L.oracle_sad(P(s8), st, P(rr), st, w, h) == res[c][6 + k]
+            assert L.oracle_sse(P(s8), st, P(r8), st, w, h) & 0xFFFFFFFF == res[c][10]
+            assert (L.oracle_sse16(P(s16), st, P(r16), st, w, h) >> 4) & 0xFFFFFFFF == res[c][11]
+    # known answers: zero difference -> 0, maximum difference -> var 0 with full sse
+    assert g["s12_res"][0][0] == 0 and g["s12_res"][1][0] == 255 * 4096 and g["s12_res"][1][1] == 0
+
+
+def test_md_batch_oracle_consistent():
+    """The oracle batch = the pinned per-block kernels on the gathered (edge-clamped) blocks."""
+    import md_cases as mc
+    import synth
+    w, h, bd, nref = 136, 72, 10, 2
+    src, _ = synth.frame_pair(w, h, bd, seed=7)
+    refs = mc.ref_frames(w, h, bd, nref, 7)
+    mv = mc.mvs(w, h, nref, 7, rng_max=40)
+    out = oracle.md_dist_batch(src[0], refs, bd, mv)
+    rng = np.random.default_rng(0)
+    offs = np.cumsum([0] + [4096 // (sw * sh) for sw, sh in oracle.MD_SHAPES])
+    nsbx = (w + 63) // 64
+    for _ in range(60):
+        sb, r, s = rng.integers(0, out.shape[0]), rng.integers(0, nref), rng.integers(0, 19)
+        sw, sh = oracle.MD_SHAPES[s]
+        b = rng.integers(0, 4096 // (sw * sh))
+        by, bx = (b // (64 // sw)) * sh, (b % (64 // sw)) * sw
+        oy, ox = (sb // nsbx) * 64 + by, (sb % nsbx) * 64 + bx
+        ys, xs = np.clip(np.arange(oy, oy + sh), 0, h - 1), np.clip(np.arange(ox, ox + sw), 0, w - 1)
+        yr = np.clip(np.arange(oy, oy + sh) + mv[sb, r, 1], 0, h - 1)
+        xr = np.clip(np.arange(ox, ox + sw) + mv[sb, r, 0], 0, w - 1)
+        a, c = src[0][np.ix_(ys, xs)], refs[r][np.ix_(yr, xr)]
+        want = oracle.block_dist(a, c, sw, sh, bd)
+        k = offs[s] + b
+        assert tuple(int(x) for x in out[sb, r, :, k]) == want
