@@ -429,6 +429,63 @@ void   *svtgpu_md_out_device_ptr(SvtGpuMdBatch *b);
 /* shape_w/shape_h/shape_offset: [SVTGPU_MD_SHAPES] block dims and first output index of each shape */
 void    svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offset);
 
+
+/* =========================================================================================
+ * Loop restoration
+ * ========================================================================================= */
+/* RTCD-compatible per-block shims (common_dsp_rtcd.h:174-185).  SvtGpuConvolveParams mirrors the fields
+ * of ConvolveParams the Wiener convolve reads (round_0, round_1); 16-bit planes are passed
+ * CONVERT_TO_BYTEPTR-encoded (EbDefinitions.h:950-951), as in the reference. */
+typedef struct SvtGpuConvolveParams {
+    int32_t round_0, round_1;
+} SvtGpuConvolveParams;
+/* ≙ svt_av1_wiener_convolve_add_src (C convolve.c:109-151): 8-tap separable, src row/col -3..+4 */
+void svtgpu_av1_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst, ptrdiff_t dst_stride,
+                                        const int16_t *filter_x, const int16_t *filter_y, int32_t w, int32_t h,
+                                        const SvtGpuConvolveParams *conv_params);
+/* ≙ svt_av1_highbd_wiener_convolve_add_src (C convolve.c:194-232) */
+void svtgpu_av1_highbd_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst,
+                                               ptrdiff_t dst_stride, const int16_t *filter_x,
+                                               const int16_t *filter_y, int32_t w, int32_t h,
+                                               const SvtGpuConvolveParams *conv_params, int32_t bd);
+/* ≙ svt_av1_selfguided_restoration (C EbRestoration.c:923-955): flt0/flt1 of one processing unit, input read
+ * with a 3-sample border */
+void svtgpu_av1_selfguided_restoration(const uint8_t *dgd8, int32_t width, int32_t height, int32_t dgd_stride,
+                                       int32_t *flt0, int32_t *flt1, int32_t flt_stride, int32_t sgr_params_idx,
+                                       int32_t bit_depth, int32_t highbd);
+/* ≙ svt_apply_selfguided_restoration (C EbRestoration.c:957-991) */
+void svtgpu_apply_selfguided_restoration(const uint8_t *dat8, int32_t width, int32_t height, int32_t stride,
+                                         int32_t eps, const int32_t *xqd, uint8_t *dst8, int32_t dst_stride,
+                                         int32_t *tmpbuf, int32_t bit_depth, int32_t highbd);
+
+/* Per restoration unit parameters (RestorationUnitInfo, EbRestoration.h:169-188). */
+#define SVTGPU_RESTORE_NONE 0
+#define SVTGPU_RESTORE_WIENER 1
+#define SVTGPU_RESTORE_SGRPROJ 2
+typedef struct SvtGpuRestUnit {
+    int32_t type;       /* SVTGPU_RESTORE_* */
+    int16_t vfilter[8]; /* WienerInfo */
+    int16_t hfilter[8];
+    int32_t ep;         /* SgrprojInfo */
+    int32_t xqd[2];
+} SvtGpuRestUnit;
+
+typedef struct SvtGpuLrState SvtGpuLrState;
+/* unit_size[plane]: restoration_unit_size (64/128/256 luma; chroma usually luma >> 1) */
+int  svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, const int32_t unit_size[3],
+                            SvtGpuLrState **out);
+void svtgpu_lr_state_destroy(SvtGpuLrState *s);
+/* number of units of a plane: horz/vert units (count_units_in_tile, EbRestoration.c:122-124) */
+int  svtgpu_lr_units(const SvtGpuLrState *s, int32_t plane, int32_t *hunits, int32_t *vunits);
+int  svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpuRestUnit *units, void *stream);
+/* ≙ svt_av1_loop_restoration_filter_frame(rst_tmpbuf, frame, cm, 0) (EbRestoration.c:1179-1255) with the
+ * stripe boundary lines of svt_av1_loop_restoration_save_boundary_lines (EbRestoration.c:1682): rows above /
+ * below each 64-row processing stripe come from `deblocked` (the DLF output) inside the frame and from
+ * `cdef_out` at the frame top/bottom.  Writes every sample of `out` (planes whose frame_type is NONE are
+ * copied).  frame_type[plane]: SVTGPU_RESTORE_NONE or any other value (= per-unit types apply). */
+int  svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *deblocked, const SvtGpuFrame *cdef_out,
+                           SvtGpuFrame *out, const int32_t frame_type[3], void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,21 @@ int64_t  oracle_sse16(const uint16_t *a, int as, const uint16_t *b, int bs, int 
 int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs, int nref, const int16_t *mv,
                          uint32_t *out);
 
+/* ---- loop restoration (lr_oracle.c) ---- */
+void oracle_wiener_round(int bd, int *round0, int *round1);
+/* src/dst at the output origin; src readable at rows -3..h+3, cols -3..w+4 */
+void oracle_wiener_convolve(const uint16_t *src, int sstride, uint16_t *dst, int dstride, const int16_t *fx,
+                            const int16_t *fy, int w, int h, int round0, int round1, int bd);
+/* dgd readable at rows -3..h+2, cols -3..w+2 */
+void oracle_sgr_filter(const int32_t *dgd, int stride, int w, int h, int eps, int bd, int32_t *flt0, int32_t *flt1,
+                       int fstride);
+void oracle_decode_xq(const int32_t *xqd, int32_t *xq, int eps);
+void oracle_sgr_apply(const uint16_t *dat, int stride, int w, int h, int eps, const int32_t *xqd, uint16_t *dst,
+                      int dstride, int bd);
+int  oracle_lr_units(int size, int extent);
+int  oracle_lr_apply_frame(const OracleFrame *dlf, const OracleFrame *cdef, OracleFrame *out, const int *frame_type,
+                           const int *unit_size, const SvtGpuRestUnit *const *units);
+
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,10 @@ CFLAGS   := -O2 -fPIC -ffunction-sections -fdata-sections -DARCH_X86_64=1 -w $(I
 REF_C    := Lib/Common/Codec/EbCdef.c Lib/Encoder/Codec/EbEncCdef.c Lib/Common/Codec/common_dsp_rtcd.c \
             Lib/Encoder/Codec/aom_dsp_rtcd.c Lib/Common/Codec/EbUtility.c
 DLF_C    := Lib/Common/Codec/EbDeblockingCommon.c Lib/Encoder/Codec/EbDeblockingFilter.c
+LR_C     := Lib/Common/Codec/convolve.c Lib/Common/Codec/EbRestoration.c Lib/Common/Codec/EbPictureBufferDesc.c \
+            Lib/Common/Codec/EbMalloc.c Lib/Common/Codec/EbLog.c Lib/Common/Codec/EbSuperRes.c Lib/Common/C_DEFAULT/EbPictureOperators_C.c \
+            Lib/Common/Codec/EbThreads.c Lib/Common/Codec/EbBlockStructures.c \
+            Lib/Common/Codec/EbPictureOperators.c
 MD_C     := Lib/Encoder/C_DEFAULT/EbComputeSAD_C.c Lib/Encoder/C_DEFAULT/variance.c Lib/Encoder/Codec/EbPsnr.c \
             Lib/Encoder/Codec/EbEncInterPrediction.c Lib/Common/C_DEFAULT/EbPictureOperators_C.c \
             Lib/Common/Codec/EbPictureOperators.c
@@ -27,9 +31,10 @@ REF_AVX2 := Lib/Common/ASM_AVX2/cdef_block_avx2.c Lib/Encoder/ASM_AVX2/EbCdef_AV
 C_OBJ    := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_C))
 DLF_OBJ  := $(patsubst %.c,$(OUT)/obj/%.o,$(DLF_C))
 MD_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(MD_C))
+LR_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(LR_C))
 AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
 
-all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md
+all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/%.o: $(S)/%.c
@@ -43,6 +48,9 @@ $(OUT)/gen_golden_dlf: oracle/ref_harness/gen_golden_dlf.c $(DLF_OBJ) $(C_OBJ)
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
 
 $(OUT)/gen_golden_md: oracle/ref_harness/gen_golden_md.c $(MD_OBJ) $(C_OBJ)
+	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
+
+$(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(LR_OBJ) $(C_OBJ)
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
 
 $(OUT)/ref_cdef_bench: oracle/ref_harness/ref_cdef_bench.c $(C_OBJ) $(AVX2_OBJ)

@@ -107,6 +107,32 @@ class LfParams(ctypes.Structure):
         return p
 
 
+class RestUnit(ctypes.Structure):
+    """SvtGpuRestUnit (RestorationUnitInfo, EbRestoration.h:169-188)."""
+    _fields_ = [("type", ctypes.c_int32), ("vfilter", ctypes.c_int16 * 8), ("hfilter", ctypes.c_int16 * 8),
+                ("ep", ctypes.c_int32), ("xqd", ctypes.c_int32 * 2)]
+
+
+REST_UNIT_DTYPE = np.dtype([("type", np.int32), ("vfilter", np.int16, 8), ("hfilter", np.int16, 8), ("ep", np.int32),
+                            ("xqd", np.int32, 2)])
+
+
+def rest_units_from_rows(rows):
+    """[n][20] int32 rows {type, vfilter[8], hfilter[8], ep, xqd0, xqd1} -> REST_UNIT_DTYPE array."""
+    rows = np.asarray(rows)
+    u = np.zeros(len(rows), REST_UNIT_DTYPE)
+    u["type"] = rows[:, 0]
+    u["vfilter"] = rows[:, 1:9]
+    u["hfilter"] = rows[:, 9:17]
+    u["ep"] = rows[:, 17]
+    u["xqd"] = rows[:, 18:20]
+    return u
+
+
+class ConvolveParams(ctypes.Structure):
+    _fields_ = [("round_0", ctypes.c_int32), ("round_1", ctypes.c_int32)]
+
+
 MD_SIZES = [(4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 8), (16, 16), (16, 32), (32, 16), (32, 32), (32, 64),
             (64, 32), (64, 64), (64, 128), (128, 64), (128, 128), (4, 16), (16, 4), (8, 32), (32, 8), (16, 64),
             (64, 16)]

@@ -156,3 +156,38 @@ def test_md_batch_oracle_consistent():
         want = oracle.block_dist(a, c, sw, sh, bd)
         k = offs[s] + b
         assert tuple(int(x) for x in out[sb, r, :, k]) == want
+
+
+# ---------------------------------------------------------------- loop restoration (gen_golden_lr.c)
+def test_wiener_golden():
+    g = cc.load("lr_wiener.bin")
+    for n in range(len(g["meta"])):
+        bd, w, h = (int(x) for x in g["meta"][n])
+        got = oracle.wiener_convolve(g["in%d" % n], w, h, g["taps"][n][:8], g["taps"][n][8:], bd)
+        assert np.array_equal(got, g["out%d" % n]), (n, bd, w, h)
+
+
+def test_sgr_golden():
+    g = cc.load("lr_sgr.bin")
+    eps_seen = set()
+    for n in range(len(g["meta"])):
+        bd, w, h, eps, x0, x1 = (int(x) for x in g["meta"][n])
+        f0, f1 = oracle.sgr_filter(g["in%d" % n], w, h, eps, bd)
+        if eps < 10 or eps >= 14:
+            assert np.array_equal(f0, g["flt0_%d" % n]), (n, eps)
+        if eps < 14:
+            assert np.array_equal(f1, g["flt1_%d" % n]), (n, eps)
+        assert np.array_equal(oracle.sgr_apply(g["in%d" % n], w, h, eps, (x0, x1), bd), g["out%d" % n]), (n, eps)
+        eps_seen.add(eps)
+    assert eps_seen == set(range(16))
+
+
+def test_lr_frame_golden():
+    import lr_cases as lc
+    n = 0
+    for c in lc.frame_cases():
+        got = oracle.lr_apply_frame(c["dlf"], c["cdef"], c["bd"], c["frame_type"], c["unit_size"], c["units"])
+        for p in range(3):
+            assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
+        n += 1
+    assert n >= 6
