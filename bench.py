@@ -7,6 +7,9 @@ A "step" = one 4K 10-bit 4:2:0 frame through the device-resident in-loop filter 
   CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
       strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
       (svt_av1_cdef_frame).
+  LR stage (EbRestProcess.c): loop-restoration apply (svt_av1_loop_restoration_filter_frame) of the CDEF
+      output with per-unit Wiener / self-guided parameters (RU 256 luma / 128 chroma; stripe boundary lines
+      from the DLF output);
   MD distortion stage: SAD / SSE / variance of every AV1 block shape of every SB against 7 reference
       frames at one full-pel motion vector per (SB, reference) (SURVEY.md §8d config 5 workload at 4K).
 Inputs are synthetic (recon = source + blocking/ringing, 16x16 non-skip inter blocks
@@ -104,6 +107,22 @@ def main():
     dl = svtgpu.DlfState(ctx, W, H)
     dl.set_mode_info(mi, sp)
     lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
+    # loop restoration: unit parameters (the LR search is not yet in the step: fixed mixed Wiener/SGR units)
+    lr_us = [256, 128, 128]
+    lr = svtgpu.LrState(ctx, W, H, lr_us)
+    rng_lr = np.random.default_rng(7)
+    for p in range(3):
+        hu, vu = lr.units[p]
+        rows = np.zeros((hu * vu, 20), np.int32)
+        for k in range(hu * vu):
+            t = [int(rng_lr.integers(-5, 11)), int(rng_lr.integers(-23, 9)), int(rng_lr.integers(-17, 47))]
+            if p:
+                t[0] = 0
+            taps = [t[0], t[1], t[2], -2 * sum(t), t[2], t[1], t[0], 0]
+            rows[k] = [1 + (k % 2)] + taps + taps + [int(rng_lr.integers(0, 16)), int(rng_lr.integers(-96, 32)),
+                                                      int(rng_lr.integers(-32, 96))]
+        lr.set_units(p, svtgpu.rest_units_from_rows(rows), sp)
+    L = svtgpu.Frame(ctx, W, H, bd)
     NREF = 7
     md_refs = []
     for r in range(NREF):
@@ -123,7 +142,7 @@ def main():
         skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
         st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
 
-    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | md)
+    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | lr | md)
     if n > 1:  # MD batch: SB row bands, no collective
         sbr = np.linspace(0, md.nsb, n + 1).round().astype(int)
         md_range = (int(sbr[rank]), int(sbr[rank + 1]))
@@ -132,7 +151,7 @@ def main():
     lf_levels = []
 
     def step(timed):
-        es = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if timed else None
+        es = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
         if timed:
             es[0].record(stream)
         # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
@@ -154,10 +173,14 @@ def main():
         st.apply(D, O, prm, sp)
         if timed:
             es[3].record(stream)
+        # LR apply on the CDEF output (boundary lines from the DLF output)
+        lr.apply(D, O, L, [1, 1, 1], sp)
+        if timed:
+            es[4].record(stream)
         # MD distortion batch (source vs 7 references, every block shape)
         md.run(S, md_refs, md_range[0], md_range[1], sp)
         if timed:
-            es[4].record(stream)
+            es[5].record(stream)
             ev.append(es)
 
     for _ in range(a.warmup):
@@ -178,8 +201,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] for es in ev], axis=0)
-    dlf_ms, search_ms, cdef_rest_ms, md_ms = (float(x) for x in stage_ms)
+    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(5)] for es in ev], axis=0)
+    dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
     value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
@@ -206,12 +229,13 @@ def main():
         "data": "synthetic",
         "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply %dx%d %d-bit 4:2:0, dlf level 1 "
                                "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
-                               "LR not yet in the step"
+                               "LR apply (RU 256/128, mixed Wiener/SGR units; LR search not yet in the step)"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
                    "parallelism": "fb_row_bands%d" % n if n > 1 else "single",
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
-                                "cdef_pick_apply": round(cdef_rest_ms, 4), "md_sad_sse_var": round(md_ms, 4)},
+                                "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_apply": round(lr_ms, 4),
+                                "md_sad_sse_var": round(md_ms, 4)},
                    "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
         "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

@@ -1,0 +1,558 @@
+// lr.hip — AV1 loop restoration (Wiener / self-guided) on gfx950: frame apply and RTCD shims.
+//
+// Reference (Source/Lib/): Common/Codec/convolve.c:109-232 (Wiener convolve add src),
+// Common/Codec/EbRestoration.c:466-991 (box sums, self-guided filters, decode_xq, projection),
+// :222-435 + :1067-1139 (processing stripes, boundary substitution), :1179-1296 (units of the frame),
+// :1522-1680 (stripe boundary lines saved after deblocking / CDEF).
+//
+// Design (MI355X): a restoration unit's output at a pixel depends only on a 7x7 (Wiener) / 5x5+3x3
+// (self-guided) window of its processing stripe's *virtual input*: the CDEF output rows of the stripe, the
+// three rows above/below replaced by the saved deblocked lines (L0 L0 L1 / B0 B1 B1) inside the frame and by
+// the replicated edge row at the frame top/bottom, and edge-replicated columns.  So the frame is processed
+// as independent tiles of one stripe x 64 (luma) / 32 (chroma) columns — which never straddle a unit — one
+// workgroup each: the virtual tile is staged in LDS straight from the resident DLF and CDEF frames (no line
+// buffers, no frame extension pass), then the unit's filter runs from LDS and the tile is written once.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "svtgpu_internal.h"
+
+namespace {
+
+constexpr int NTHR = 256;
+// self-guided parameter sets svt_aom_eb_sgr_params (EbRestoration.c:85-103): radii and s values
+__constant__ int c_sgr_r[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
+                                   {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
+__constant__ int c_sgr_s[16][2] = {{140, 3236}, {112, 2158}, {93, 1618}, {80, 1438}, {70, 1295}, {58, 1177},
+                                   {47, 1079},  {37, 996},   {30, 925},  {25, 863},  {-1, 2589}, {-1, 1618},
+                                   {-1, 1177},  {-1, 925},   {56, -1},   {22, -1}};
+// svt_aom_eb_x_by_xplus1 (EbRestoration.c:647-662): round(256 x / (x + 1)), 0 -> 1, 255 -> 256
+__constant__ int c_x_by_xplus1[256] = {
+    1,   128, 171, 192, 205, 213, 219, 224, 228, 230, 233, 235, 236, 238, 239, 240, 241, 242, 243, 243, 244, 244,
+    245, 245, 246, 246, 247, 247, 247, 247, 248, 248, 248, 248, 249, 249, 249, 249, 249, 250, 250, 250, 250, 250,
+    250, 250, 251, 251, 251, 251, 251, 251, 251, 251, 251, 251, 252, 252, 252, 252, 252, 252, 252, 252, 252, 252,
+    252, 252, 252, 252, 252, 252, 252, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253,
+    253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 256};
+// svt_aom_eb_one_by_x (EbRestoration.c:664-667): round(4096 / n)
+__constant__ int c_one_by_x[25] = {4096, 2048, 1365, 1024, 819, 683, 585, 512, 455, 410, 372, 341, 315,
+                                   293,  273,  256,  241,  228, 216, 205, 195, 186, 178, 171, 164};
+
+struct WienerRound {
+    int r0, r1;
+};
+// get_conv_params_wiener (EbRestoration.c:49-72)
+__host__ __device__ inline WienerRound wiener_round(int bd) {
+    WienerRound r{3, 11};
+    const int   over = bd + 7 - 3 + 2 - 16;
+    if (over > 0) r.r0 += over, r.r1 -= over;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// tile filters over an LDS image `v` (u16, row stride vs) whose (0,0) is the tile's first output
+// ---------------------------------------------------------------------------------------------
+// Wiener: horizontal 8-tap pass into t (rows -3..h+3 -> t rows 0..h+6), vertical pass into out.
+template <typename T>
+__device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int w, int h, const int16_t *fx,
+                            const int16_t *fy, int bd, T *out, size_t os) {
+    const WienerRound rr  = wiener_round(bd);
+    const int         lim = (1 << (bd + 1 + 7 - rr.r0)) - 1;
+    int16_t           hx[8], vy[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) hx[k] = fx[k], vy[k] = fy[k];
+    for (int i = threadIdx.x; i < (h + 7) * w; i += NTHR) {
+        const int       y = i / w - 3, x = i % w;
+        const uint16_t *s = v + y * vs + x - 3;
+        int             sum = ((int)s[3] << 7) + (1 << (bd + 6));
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += (int)s[k] * hx[k];
+        t[(y + 3) * ts + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
+    }
+    __syncthreads();
+    const int maxv = (1 << bd) - 1;
+    for (int i = threadIdx.x; i < h * w; i += NTHR) {
+        const int       y = i / w, x = i % w;
+        const uint16_t *c = t + y * ts + x; // rows y-3 .. y+4 of the intermediate
+        int             sum = ((int)c[3 * ts] << 7) - (1 << (bd + rr.r1 - 1));
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += (int)c[k * ts] * vy[k];
+        out[y * os + x] = (T)min(max((sum + (1 << (rr.r1 - 1))) >> rr.r1, 0), maxv);
+    }
+}
+
+// A, B of one self-guided pass at (i, j) (selfguided_restoration_*_internal, EbRestoration.c:693-760)
+__device__ inline void sgr_ab(const uint16_t *v, int vs, int i, int j, int r, int s, int bd, int *A, int *B) {
+    int sum = 0, sq = 0;
+    for (int y = -r; y <= r; y++)
+        for (int x = -r; x <= r; x++) {
+            const int p = v[(i + y) * vs + j + x];
+            sum += p;
+            sq += p * p;
+        }
+    const int      n = (2 * r + 1) * (2 * r + 1);
+    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
+    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
+    const uint32_t p = (a * n < b * b) ? 0u : a * n - b * b;
+    const uint32_t z = (p * (uint32_t)s + (1u << 19)) >> 20;
+    *A               = c_x_by_xplus1[min(z, 255u)];
+    *B = (int)(((uint32_t)(256 - *A) * (uint32_t)sum * (uint32_t)c_one_by_x[n - 1] + (1u << 11)) >> 12);
+}
+
+// self-guided filter + projection (svt_apply_selfguided_restoration_c) of a w x h tile; AB holds 2 int arrays of
+// (h+2) x (w+2); flt0 is kept per thread between the passes (px k of thread = threadIdx.x + k * NTHR)
+constexpr int SGR_MAXPX = 64 * 64 / NTHR;
+template <typename T>
+__device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h, int eps, const int32_t *xqd,
+                         int bd, T *out, size_t os) {
+    const int bw = w + 2;
+    int       f0[SGR_MAXPX];
+    const int r0 = c_sgr_r[eps][0], r1 = c_sgr_r[eps][1];
+    if (r0 > 0) { // r = 2 on odd rows -1, 1, 3, ...
+        const int nrow = (h + 3) / 2;
+        for (int i = threadIdx.x; i < nrow * bw; i += NTHR) {
+            const int y = 2 * (i / bw) - 1, x = i % bw - 1;
+            sgr_ab(v, vs, y, x, 2, c_sgr_s[eps][0], bd, &A[(y + 1) * bw + x + 1], &B[(y + 1) * bw + x + 1]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SGR_MAXPX; k++) {
+            const int i = threadIdx.x + k * NTHR;
+            if (i >= w * h) break;
+            const int y = i / w, x = i % w;
+            const int *a = A + (y + 1) * bw + x + 1, *b = B + (y + 1) * bw + x + 1;
+            int        aa, bb, nb;
+            if (!(y & 1)) {
+                aa = (a[-bw] + a[bw]) * 6 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 5;
+                bb = (b[-bw] + b[bw]) * 6 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 5;
+                nb = 5;
+            } else {
+                aa = a[0] * 6 + (a[-1] + a[1]) * 5;
+                bb = b[0] * 6 + (b[-1] + b[1]) * 5;
+                nb = 4;
+            }
+            const int sh = 8 + nb - 4;
+            f0[k]        = (aa * (int)v[y * vs + x] + bb + (1 << (sh - 1))) >> sh;
+        }
+        __syncthreads();
+    }
+    if (r1 > 0) {
+        for (int i = threadIdx.x; i < (h + 2) * bw; i += NTHR) {
+            const int y = i / bw - 1, x = i % bw - 1;
+            sgr_ab(v, vs, y, x, 1, c_sgr_s[eps][1], bd, &A[i], &B[i]);
+        }
+        __syncthreads();
+    }
+    // projection: xq from xqd (svt_decode_xq, EbRestoration.c:634-646)
+    int xq0, xq1;
+    if (r0 == 0)
+        xq0 = 0, xq1 = 128 - xqd[1];
+    else if (r1 == 0)
+        xq0 = xqd[0], xq1 = 0;
+    else
+        xq0 = xqd[0], xq1 = 128 - xqd[0] - xqd[1];
+    const int maxv = (1 << bd) - 1;
+#pragma unroll
+    for (int k = 0; k < SGR_MAXPX; k++) {
+        const int i = threadIdx.x + k * NTHR;
+        if (i >= w * h) break;
+        const int y = i / w, x = i % w;
+        const int u = (int)v[y * vs + x] << 4;
+        int       val = u << 7;
+        if (r0 > 0) val += xq0 * (f0[k] - u);
+        if (r1 > 0) {
+            const int *a = A + (y + 1) * bw + x + 1, *b = B + (y + 1) * bw + x + 1;
+            const int  aa = (a[0] + a[-1] + a[1] + a[-bw] + a[bw]) * 4 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 3;
+            const int  bb = (b[0] + b[-1] + b[1] + b[-bw] + b[bw]) * 4 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 3;
+            const int  f1 = (aa * (int)v[y * vs + x] + bb + (1 << 8)) >> 9;
+            val += xq1 * (f1 - u);
+        }
+        const int16_t o = (int16_t)((val + (1 << 10)) >> 11);
+        out[y * os + x] = (T)min(max((int)o, 0), maxv);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// frame apply: one workgroup per (stripe, column chunk) of a plane
+// ---------------------------------------------------------------------------------------------
+constexpr int TW = 64, TH = 64;
+constexpr int VS = TW + 8;            // virtual tile columns -3 .. TW+4
+constexpr int VR = TH + 7;            // virtual tile rows -3 .. TH+3
+struct LrPlaneArgs {
+    const void           *dlf, *cdef;
+    void                 *out;
+    int32_t               dlf_stride, cdef_stride, out_stride;
+    int32_t               W, H, ss, unit_size, hunits, vunits, nchunks, bd;
+    const SvtGpuRestUnit *units;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrPlaneArgs a) {
+    __shared__ uint16_t v[VR * VS];
+    __shared__ uint16_t t[VR * TW];        // Wiener intermediate
+    __shared__ int      AB[2][(TH + 2) * (TW + 2)];
+    const int S = 64 >> a.ss, off = 8 >> a.ss, cwmax = 64 >> a.ss;
+    const int k = blockIdx.x / a.nchunks, c = blockIdx.x % a.nchunks;
+    const int y0 = max(0, k * S - off), y1 = min((k + 1) * S - off, a.H);
+    const int x0 = c * cwmax, w = min(cwmax, a.W - x0), h = y1 - y0;
+    if (h <= 0 || w <= 0) return;
+    const int ur = min((y0 + off) / a.unit_size, a.vunits - 1), uc = min(x0 / a.unit_size, a.hunits - 1);
+    const SvtGpuRestUnit u = a.units[ur * a.hunits + uc];
+    const T *cdef = (const T *)a.cdef, *dlf = (const T *)a.dlf;
+    T       *out  = (T *)a.out;
+    if (u.type == SVTGPU_RESTORE_NONE) {
+        for (int i = threadIdx.x; i < w * h; i += NTHR) {
+            const int y = i / w, x = i % w;
+            out[(size_t)(y0 + y) * a.out_stride + x0 + x] = cdef[(size_t)(y0 + y) * a.cdef_stride + x0 + x];
+        }
+        return;
+    }
+    // virtual stripe input (svt_aom_setup_processing_stripe_boundary with saved lines, EbRestoration.c:271-352)
+    const int copy_above = y0 != 0;
+    const int copy_below = !(y0 + S - (y0 == 0 ? off : 0) >= a.H);
+    const int vw         = w + 8;
+    for (int i = threadIdx.x; i < (h + 7) * vw; i += NTHR) {
+        const int r = i / vw - 3, cc = i % vw - 3;
+        const int x = min(max(x0 + cc, 0), a.W - 1);
+        int       val;
+        if (r < 0 && copy_above)
+            val = dlf[(size_t)(y0 + (r == -1 ? -1 : -2)) * a.dlf_stride + x];
+        else if (r >= h && r < h + 3 && copy_below)
+            val = dlf[(size_t)min(y1 + (r == h ? 0 : 1), a.H - 1) * a.dlf_stride + x];
+        else
+            val = cdef[(size_t)min(max(y0 + r, 0), a.H - 1) * a.cdef_stride + x];
+        v[(r + 3) * VS + cc + 3] = (uint16_t)val;
+    }
+    __syncthreads();
+    const uint16_t *v0 = v + 3 * VS + 3;
+    T              *o0 = out + (size_t)y0 * a.out_stride + x0;
+    if (u.type == SVTGPU_RESTORE_WIENER)
+        wiener_tile(v0, VS, t, TW, w, h, u.hfilter, u.vfilter, a.bd, o0, (size_t)a.out_stride);
+    else
+        sgr_tile(v0, VS, AB[0], AB[1], w, h, u.ep, u.xqd, a.bd, o0, (size_t)a.out_stride);
+}
+
+// ---------------------------------------------------------------------------------------------
+// RTCD shim kernels (one small block staged compactly)
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTHR) void wiener_shim_kernel(const uint16_t *in, int is, uint16_t *out, int w, int h,
+                                                           const int16_t *taps, int bd, int r0, int r1) {
+    __shared__ uint16_t t[(64 + 7) * 64];
+    __shared__ int16_t  f[16];
+    if (threadIdx.x < 16) f[threadIdx.x] = taps[threadIdx.x];
+    __syncthreads();
+    // custom rounding (the shim honours the caller's ConvolveParams)
+    const int lim = (1 << (bd + 1 + 7 - r0)) - 1;
+    for (int i = threadIdx.x; i < (h + 7) * w; i += NTHR) {
+        const int       y = i / w - 3, x = i % w;
+        const uint16_t *s = in + (y + 3) * is + x; // in holds rows/cols from -3
+        int             sum = ((int)s[3] << 7) + (1 << (bd + 6));
+        for (int k = 0; k < 8; k++) sum += (int)s[k] * f[k];
+        t[(y + 3) * w + x] = (uint16_t)min(max((sum + (1 << (r0 - 1))) >> r0, 0), lim);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < h * w; i += NTHR) {
+        const int       y = i / w, x = i % w;
+        const uint16_t *c = t + y * w + x;
+        int             sum = ((int)c[3 * w] << 7) - (1 << (bd + r1 - 1));
+        for (int k = 0; k < 8; k++) sum += (int)c[k * w] * f[8 + k];
+        out[y * w + x] = (uint16_t)min(max((sum + (1 << (r1 - 1))) >> r1, 0), (1 << bd) - 1);
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void sgr_shim_kernel(const uint16_t *in, int is, int w, int h, int eps, int bd,
+                                                        int32_t x0q, int32_t x1q, int mode, int32_t *flt0,
+                                                        int32_t *flt1, uint16_t *out) {
+    __shared__ uint16_t v[70 * 70];
+    __shared__ int      AB[2][66 * 66];
+    for (int i = threadIdx.x; i < (h + 6) * (w + 6); i += NTHR) v[(i / (w + 6)) * 70 + i % (w + 6)] = in[(i / (w + 6)) * is + i % (w + 6)];
+    __syncthreads();
+    const uint16_t *v0 = v + 3 * 70 + 3;
+    const int       bw = w + 2;
+    if (mode == 0) { // flt0 / flt1 (svt_av1_selfguided_restoration)
+        for (int pass = 0; pass < 2; pass++) {
+            const int r = c_sgr_r[eps][pass];
+            if (!r) continue;
+            for (int i = threadIdx.x; i < (h + 2) * bw; i += NTHR) {
+                const int y = i / bw - 1, x = i % bw - 1;
+                if (r == 2 && !(y & 1)) continue;
+                sgr_ab(v0, 70, y, x, r, c_sgr_s[eps][pass], bd, &AB[0][i], &AB[1][i]);
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i < w * h; i += NTHR) {
+                const int  y = i / w, x = i % w;
+                const int *a = AB[0] + (y + 1) * bw + x + 1, *b = AB[1] + (y + 1) * bw + x + 1;
+                int        aa, bb, nb;
+                if (r == 1) {
+                    aa = (a[0] + a[-1] + a[1] + a[-bw] + a[bw]) * 4 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 3;
+                    bb = (b[0] + b[-1] + b[1] + b[-bw] + b[bw]) * 4 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 3;
+                    nb = 5;
+                } else if (!(y & 1)) {
+                    aa = (a[-bw] + a[bw]) * 6 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 5;
+                    bb = (b[-bw] + b[bw]) * 6 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 5;
+                    nb = 5;
+                } else {
+                    aa = a[0] * 6 + (a[-1] + a[1]) * 5;
+                    bb = b[0] * 6 + (b[-1] + b[1]) * 5;
+                    nb = 4;
+                }
+                const int sh = 8 + nb - 4;
+                (pass ? flt1 : flt0)[i] = (aa * (int)v0[y * 70 + x] + bb + (1 << (sh - 1))) >> sh;
+            }
+            __syncthreads();
+        }
+    } else {
+        const int32_t xqd[2] = {x0q, x1q};
+        sgr_tile(v0, 70, AB[0], AB[1], w, h, eps, xqd, bd, out, (size_t)w);
+    }
+}
+
+} // namespace
+
+// =============================================================================================
+// host
+// =============================================================================================
+struct SvtGpuLrState {
+    SvtGpuContext  *ctx;
+    int32_t         width, height;
+    int32_t         unit_size[3], hunits[3], vunits[3];
+    SvtGpuRestUnit *d_units[3];
+};
+
+namespace {
+int count_units(int size, int extent) { return std::max((extent + (size >> 1)) / size, 1); }
+} // namespace
+
+extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, const int32_t unit_size[3],
+                                      SvtGpuLrState **out) {
+    if (!ctx || !out || !unit_size || width <= 0 || height <= 0 || (width & 7) || (height & 7))
+        return SVTGPU_ERR_INVALID_ARG;
+    for (int p = 0; p < 3; p++) {
+        const int u = unit_size[p], minu = p ? 32 : 64;
+        if (u < minu || u > 256 || (u & (u - 1))) return SVTGPU_ERR_INVALID_ARG;
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    SvtGpuLrState *s = new SvtGpuLrState();
+    s->ctx           = ctx;
+    s->width         = width;
+    s->height        = height;
+    hipError_t e     = hipSuccess;
+    for (int p = 0; p < 3 && e == hipSuccess; p++) {
+        const int pw = p ? width / 2 : width, ph = p ? height / 2 : height;
+        s->unit_size[p] = unit_size[p];
+        s->hunits[p]    = count_units(unit_size[p], pw);
+        s->vunits[p]    = count_units(unit_size[p], ph);
+        e = hipMalloc(&s->d_units[p], sizeof(SvtGpuRestUnit) * s->hunits[p] * s->vunits[p]);
+        if (e == hipSuccess) e = hipMemset(s->d_units[p], 0, sizeof(SvtGpuRestUnit) * s->hunits[p] * s->vunits[p]);
+    }
+    if (e != hipSuccess) {
+        svtgpu_lr_state_destroy(s);
+        svtgpu_set_last_hip_error(e, "lr state alloc", __FILE__, __LINE__);
+        return e == hipErrorOutOfMemory ? SVTGPU_ERR_OOM : SVTGPU_ERR_HIP;
+    }
+    *out = s;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
+    if (!s) return;
+    for (int p = 0; p < 3; p++) (void)hipFree(s->d_units[p]);
+    delete s;
+}
+
+extern "C" int svtgpu_lr_units(const SvtGpuLrState *s, int32_t plane, int32_t *hunits, int32_t *vunits) {
+    if (!s || plane < 0 || plane > 2) return SVTGPU_ERR_INVALID_ARG;
+    if (hunits) *hunits = s->hunits[plane];
+    if (vunits) *vunits = s->vunits[plane];
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpuRestUnit *units, void *stream) {
+    if (!s || !units || plane < 0 || plane > 2) return SVTGPU_ERR_INVALID_ARG;
+    const int n = s->hunits[plane] * s->vunits[plane];
+    for (int i = 0; i < n; i++) { // the kernels index tables with these fields
+        const SvtGpuRestUnit &u = units[i];
+        if (u.type < 0 || u.type > 2 || (u.type == SVTGPU_RESTORE_SGRPROJ && (u.ep < 0 || u.ep > 15)))
+            return SVTGPU_ERR_INVALID_ARG;
+    }
+    hipStream_t st = pick_stream(s->ctx, stream);
+    HIP_TRY(hipMemcpyAsync(s->d_units[plane], units, sizeof(SvtGpuRestUnit) * n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *deblocked, const SvtGpuFrame *cdef_out,
+                                     SvtGpuFrame *out, const int32_t frame_type[3], void *stream) {
+    auto ok = [&](const SvtGpuFrame *f) {
+        return f && f->width == s->width && f->height == s->height && f->bit_depth == cdef_out->bit_depth;
+    };
+    if (!s || !cdef_out || !ok(deblocked) || !ok(out) || !frame_type || out == cdef_out || out == deblocked)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (cdef_out->bit_depth != 8 && cdef_out->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
+    hipStream_t  st  = pick_stream(s->ctx, stream);
+    const size_t bps = cdef_out->bytes_per_sample;
+    for (int p = 0; p < 3; p++) {
+        if (frame_type[p] == SVTGPU_RESTORE_NONE) {
+            HIP_TRY(hipMemcpy2DAsync(out->plane[p], out->stride[p] * bps, cdef_out->plane[p], cdef_out->stride[p] * bps,
+                                     cdef_out->pw[p] * bps, cdef_out->ph[p], hipMemcpyDeviceToDevice, st));
+            continue;
+        }
+        LrPlaneArgs a;
+        a.dlf         = deblocked->plane[p];
+        a.cdef        = cdef_out->plane[p];
+        a.out         = out->plane[p];
+        a.dlf_stride  = deblocked->stride[p];
+        a.cdef_stride = cdef_out->stride[p];
+        a.out_stride  = out->stride[p];
+        a.W           = cdef_out->pw[p];
+        a.H           = cdef_out->ph[p];
+        a.ss          = p > 0;
+        a.unit_size   = s->unit_size[p];
+        a.hunits      = s->hunits[p];
+        a.vunits      = s->vunits[p];
+        a.bd          = cdef_out->bit_depth;
+        a.units       = s->d_units[p];
+        const int S = 64 >> a.ss, off = 8 >> a.ss;
+        a.nchunks     = (a.W + (64 >> a.ss) - 1) / (64 >> a.ss);
+        const int nstripes = (a.H + off + S - 1) / S;
+        const dim3 grid(nstripes * a.nchunks);
+        if (bps == 2)
+            hipLaunchKernelGGL(lr_apply_kernel<uint16_t>, grid, dim3(NTHR), 0, st, a);
+        else
+            hipLaunchKernelGGL(lr_apply_kernel<uint8_t>, grid, dim3(NTHR), 0, st, a);
+        HIP_TRY(hipGetLastError());
+    }
+    return SVTGPU_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// shims
+// ---------------------------------------------------------------------------------------------
+namespace {
+struct ShimBuf {
+    void  *p = nullptr;
+    size_t n = 0;
+    void  *get(size_t b) {
+        if (b > n) {
+            if (p) (void)hipFree(p);
+            HIP_OR_DIE(hipMalloc(&p, b));
+            n = b;
+        }
+        return p;
+    }
+};
+thread_local ShimBuf g_lr_buf;
+
+const int kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
+                              {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
+inline bool c_host_r0(int eps) { return kHostSgrR[eps][0] > 0; }
+inline bool c_host_r1(int eps) { return kHostSgrR[eps][1] > 0; }
+
+template <typename T>
+void wiener_shim(const T *src, ptrdiff_t ss, T *dst, ptrdiff_t ds, const int16_t *fx, const int16_t *fy, int w, int h,
+                 int r0, int r1, int bd) {
+    if (w <= 0 || h <= 0 || w > 64 || h > 64) svtgpu_fatal("wiener shim: block larger than 64x64");
+    const int             is = w + 8;
+    std::vector<uint16_t> in((size_t)(h + 8) * is);
+    for (int y = -3; y < h + 5; y++)
+        for (int x = -3; x < w + 5; x++) in[(size_t)(y + 3) * is + x + 3] = src[y * ss + x];
+    int16_t taps[16];
+    std::memcpy(taps, fx, 16);
+    std::memcpy(taps + 8, fy, 16);
+    uint8_t  *d    = (uint8_t *)g_lr_buf.get(in.size() * 2 + (size_t)w * h * 2 + 64);
+    uint16_t *di   = (uint16_t *)d, *dout = (uint16_t *)(d + in.size() * 2);
+    int16_t  *dt   = (int16_t *)(d + in.size() * 2 + (size_t)w * h * 2);
+    hipStream_t st = svtgpu_default_stream();
+    HIP_OR_DIE(hipMemcpyAsync(di, in.data(), in.size() * 2, hipMemcpyHostToDevice, st));
+    HIP_OR_DIE(hipMemcpyAsync(dt, taps, 32, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(wiener_shim_kernel, dim3(1), dim3(NTHR), 0, st, di, is, dout, w, h, dt, bd, r0, r1);
+    HIP_OR_DIE(hipGetLastError());
+    std::vector<uint16_t> res((size_t)w * h);
+    HIP_OR_DIE(hipMemcpyAsync(res.data(), dout, res.size() * 2, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) dst[y * ds + x] = (T)res[(size_t)y * w + x];
+}
+
+template <typename T>
+void sgr_shim(const T *src, int stride, int w, int h, int eps, const int32_t *xqd, int bd, int mode, int32_t *flt0,
+              int32_t *flt1, int fstride, T *dst, int dstride) {
+    if (w <= 0 || h <= 0 || w > 64 || h > 64 || eps < 0 || eps > 15) svtgpu_fatal("sgr shim: bad block");
+    const int             is = w + 6;
+    std::vector<uint16_t> in((size_t)(h + 6) * is);
+    for (int y = -3; y < h + 3; y++)
+        for (int x = -3; x < w + 3; x++) in[(size_t)(y + 3) * is + x + 3] = src[y * stride + x];
+    const size_t nb = in.size() * 2, no = (size_t)w * h;
+    uint8_t     *d  = (uint8_t *)g_lr_buf.get(nb + no * 10 + 64);
+    uint16_t    *di = (uint16_t *)d;
+    int32_t     *f0 = (int32_t *)(d + ((nb + 15) & ~15)), *f1 = f0 + no;
+    uint16_t    *dout = (uint16_t *)(f1 + no);
+    hipStream_t  st   = svtgpu_default_stream();
+    HIP_OR_DIE(hipMemcpyAsync(di, in.data(), nb, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(sgr_shim_kernel, dim3(1), dim3(NTHR), 0, st, di, is, w, h, eps, bd, xqd ? xqd[0] : 0,
+                       xqd ? xqd[1] : 0, mode, f0, f1, dout);
+    HIP_OR_DIE(hipGetLastError());
+    std::vector<int32_t>  r0(no), r1(no);
+    std::vector<uint16_t> ro(no);
+    if (mode == 0) {
+        HIP_OR_DIE(hipMemcpyAsync(r0.data(), f0, no * 4, hipMemcpyDeviceToHost, st));
+        HIP_OR_DIE(hipMemcpyAsync(r1.data(), f1, no * 4, hipMemcpyDeviceToHost, st));
+    } else
+        HIP_OR_DIE(hipMemcpyAsync(ro.data(), dout, no * 2, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            if (mode == 0) {
+                // the reference writes only the filters its radii enable
+                if (flt0 && c_host_r0(eps)) flt0[y * fstride + x] = r0[(size_t)y * w + x];
+                if (flt1 && c_host_r1(eps)) flt1[y * fstride + x] = r1[(size_t)y * w + x];
+            } else
+                dst[y * dstride + x] = (T)ro[(size_t)y * w + x];
+        }
+}
+} // namespace
+
+extern "C" void svtgpu_av1_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst,
+                                                   ptrdiff_t dst_stride, const int16_t *filter_x,
+                                                   const int16_t *filter_y, int32_t w, int32_t h,
+                                                   const SvtGpuConvolveParams *conv_params) {
+    wiener_shim<uint8_t>(src, src_stride, dst, dst_stride, filter_x, filter_y, w, h, conv_params->round_0,
+                         conv_params->round_1, 8);
+}
+
+extern "C" void svtgpu_av1_highbd_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst,
+                                                          ptrdiff_t dst_stride, const int16_t *filter_x,
+                                                          const int16_t *filter_y, int32_t w, int32_t h,
+                                                          const SvtGpuConvolveParams *conv_params, int32_t bd) {
+    wiener_shim<uint16_t>((const uint16_t *)((uintptr_t)src << 1), src_stride, (uint16_t *)((uintptr_t)dst << 1),
+                          dst_stride, filter_x, filter_y, w, h, conv_params->round_0, conv_params->round_1, bd);
+}
+
+extern "C" void svtgpu_av1_selfguided_restoration(const uint8_t *dgd8, int32_t width, int32_t height,
+                                                  int32_t dgd_stride, int32_t *flt0, int32_t *flt1, int32_t flt_stride,
+                                                  int32_t sgr_params_idx, int32_t bit_depth, int32_t highbd) {
+    if (highbd)
+        sgr_shim<uint16_t>((const uint16_t *)((uintptr_t)dgd8 << 1), dgd_stride, width, height, sgr_params_idx,
+                           nullptr, bit_depth, 0, flt0, flt1, flt_stride, nullptr, 0);
+    else
+        sgr_shim<uint8_t>(dgd8, dgd_stride, width, height, sgr_params_idx, nullptr, bit_depth, 0, flt0, flt1,
+                          flt_stride, nullptr, 0);
+}
+
+extern "C" void svtgpu_apply_selfguided_restoration(const uint8_t *dat8, int32_t width, int32_t height, int32_t stride,
+                                                    int32_t eps, const int32_t *xqd, uint8_t *dst8, int32_t dst_stride,
+                                                    int32_t *tmpbuf, int32_t bit_depth, int32_t highbd) {
+    (void)tmpbuf;
+    if (highbd)
+        sgr_shim<uint16_t>((const uint16_t *)((uintptr_t)dat8 << 1), stride, width, height, eps, xqd, bit_depth, 1,
+                           nullptr, nullptr, 0, (uint16_t *)((uintptr_t)dst8 << 1), dst_stride);
+    else
+        sgr_shim<uint8_t>(dat8, stride, width, height, eps, xqd, bit_depth, 1, nullptr, nullptr, 0, dst8, dst_stride);
+}

@@ -215,6 +215,17 @@ _SIGS = {
     "svtgpu_md_read": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     "svtgpu_md_out_device_ptr": (_P, [_P]),
     "svtgpu_md_layout": (None, [_P, _P, _P]),
+    "svtgpu_av1_wiener_convolve_add_src": (None, [_P, ctypes.c_ssize_t, _P, ctypes.c_ssize_t, _P, _P, _I32, _I32,
+                                                  ctypes.POINTER(ConvolveParams)]),
+    "svtgpu_av1_highbd_wiener_convolve_add_src": (None, [_P, ctypes.c_ssize_t, _P, ctypes.c_ssize_t, _P, _P, _I32,
+                                                         _I32, ctypes.POINTER(ConvolveParams), _I32]),
+    "svtgpu_av1_selfguided_restoration": (None, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _I32, _I32]),
+    "svtgpu_apply_selfguided_restoration": (None, [_P, _I32, _I32, _I32, _I32, _P, _P, _I32, _P, _I32, _I32]),
+    "svtgpu_lr_state_create": (ctypes.c_int, [_P, _I32, _I32, _P, ctypes.POINTER(_P)]),
+    "svtgpu_lr_state_destroy": (None, [_P]),
+    "svtgpu_lr_units": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "svtgpu_lr_set_units": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "svtgpu_lr_apply_frame": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
 }
 
 _lib = None
@@ -485,6 +496,43 @@ def md_layout():
     w, h, o = (np.zeros(19, np.int32) for _ in range(3))
     lib().svtgpu_md_layout(ptr(w), ptr(h), ptr(o))
     return w, h, o
+
+
+class LrState:
+    """Loop-restoration state of one picture size: unit grid and per-unit parameters per plane."""
+
+    def __init__(self, ctx, width, height, unit_size):
+        self.ctx, self.width, self.height = ctx, width, height
+        self.unit_size = list(unit_size)
+        us = np.ascontiguousarray(unit_size, np.int32)
+        h = _P()
+        check(lib().svtgpu_lr_state_create(ctx.h, width, height, ptr(us), ctypes.byref(h)))
+        self.h = h
+        self.units = []
+        for p in range(3):
+            hu, vu = _I32(), _I32()
+            check(lib().svtgpu_lr_units(h, p, ctypes.byref(hu), ctypes.byref(vu)))
+            self.units.append((hu.value, vu.value))
+
+    def set_units(self, plane, units, stream=None):
+        u = np.ascontiguousarray(units, REST_UNIT_DTYPE)
+        assert len(u) == self.units[plane][0] * self.units[plane][1], (len(u), self.units[plane])
+        check(lib().svtgpu_lr_set_units(self.h, plane, ptr(u), stream))
+
+    def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
+        ft = np.ascontiguousarray(frame_type, np.int32)
+        check(lib().svtgpu_lr_apply_frame(self.h, deblocked.h, cdef_out.h, out.h, ptr(ft), stream))
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_lr_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def plane_sse(a, b, plane, stream=None):

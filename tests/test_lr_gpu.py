@@ -1,0 +1,113 @@
+"""Loop-restoration parity on the MI355X: RTCD shims vs the reference's golden vectors, the frame apply
+vs the reference's whole-frame golden outputs and vs the CPU oracle.  Bit-exact."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import cdef_cases as cc
+import lr_cases as lc
+import oracle
+import svtgpu
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return svtgpu.Context(0)
+
+
+def _at(a, y, x, enc=False):
+    addr = a.ctypes.data + (y * a.shape[1] + x) * a.itemsize
+    return ctypes.c_void_p(addr >> 1 if enc else addr)
+
+
+def test_wiener_shims_golden(ctx):
+    L = svtgpu.lib()
+    g = cc.load("lr_wiener.bin")
+    for n in range(len(g["meta"])):
+        bd, w, h = (int(x) for x in g["meta"][n])
+        fx, fy = (np.ascontiguousarray(g["taps"][n][k * 8:(k + 1) * 8]).copy() for k in range(2))
+        inp = g["in%d" % n].copy()
+        r0, r1 = oracle.wiener_round(bd)
+        cp = svtgpu.ConvolveParams(r0, r1)
+        if bd == 8:
+            i8 = inp.astype(np.uint8)
+            o8 = np.zeros((h, w), np.uint8)
+            L.svtgpu_av1_wiener_convolve_add_src(_at(i8, 3, 3), i8.shape[1], ctypes.c_void_p(o8.ctypes.data), w,
+                                                 ctypes.c_void_p(fx.ctypes.data), ctypes.c_void_p(fy.ctypes.data),
+                                                 w, h, ctypes.byref(cp))
+            got = o8.astype(np.uint16)
+        else:
+            got = np.zeros((h, w), np.uint16)
+            L.svtgpu_av1_highbd_wiener_convolve_add_src(_at(inp, 3, 3, True), inp.shape[1], _at(got, 0, 0, True), w,
+                                                        ctypes.c_void_p(fx.ctypes.data),
+                                                        ctypes.c_void_p(fy.ctypes.data), w, h, ctypes.byref(cp), bd)
+        assert np.array_equal(got, g["out%d" % n]), (n, bd, w, h)
+
+
+def test_sgr_shims_golden(ctx):
+    L = svtgpu.lib()
+    g = cc.load("lr_sgr.bin")
+    for n in range(len(g["meta"])):
+        bd, w, h, eps, x0, x1 = (int(x) for x in g["meta"][n])
+        inp = g["in%d" % n].copy()
+        hb = bd > 8
+        src = inp if hb else inp.astype(np.uint8)
+        f0, f1 = np.zeros((h, w), np.int32), np.zeros((h, w), np.int32)
+        L.svtgpu_av1_selfguided_restoration(_at(src, 3, 3, hb), w, h, src.shape[1], ctypes.c_void_p(f0.ctypes.data),
+                                            ctypes.c_void_p(f1.ctypes.data), w, eps, bd, int(hb))
+        if eps < 10 or eps >= 14:
+            assert np.array_equal(f0, g["flt0_%d" % n]), (n, eps)
+        if eps < 14:
+            assert np.array_equal(f1, g["flt1_%d" % n]), (n, eps)
+        out = np.zeros((h, w), np.uint16 if hb else np.uint8)
+        xqd = np.array([x0, x1], np.int32)
+        L.svtgpu_apply_selfguided_restoration(_at(src, 3, 3, hb), w, h, src.shape[1], eps,
+                                              ctypes.c_void_p(xqd.ctypes.data), _at(out, 0, 0, hb), w, None, bd,
+                                              int(hb))
+        assert np.array_equal(out.astype(np.uint16), g["out%d" % n]), (n, eps)
+
+
+def _gpu_apply(ctx, dlf, cdef, bd, frame_type, unit_size, units):
+    h, w = cdef[0].shape
+    D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(3))
+    D.upload(dlf)
+    C.upload(cdef)
+    st = svtgpu.LrState(ctx, w, h, unit_size)
+    for p in range(3):
+        st.set_units(p, units[p])
+    st.apply(D, C, O, frame_type)
+    return O.download()
+
+
+@pytest.mark.parametrize("case", list(range(6)))
+def test_lr_frame_golden(ctx, case):
+    c = list(lc.frame_cases())[case]
+    got = _gpu_apply(ctx, c["dlf"], c["cdef"], c["bd"], c["frame_type"], c["unit_size"], c["units"])
+    for p in range(3):
+        assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
+
+
+LR_CASES = [(640, 360, 10, 64, 1), (1920, 1080, 8, 128, 2), (392, 232, 8, 256, 3), (3840, 2160, 10, 256, 4)]
+
+
+@pytest.mark.parametrize("w,h,bd,usize,seed", LR_CASES)
+def test_lr_frame_vs_oracle(ctx, w, h, bd, usize, seed):
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0700 + seed)
+    dlf = rec
+    cdef = [np.clip(p.astype(np.int32) + ((src[i].astype(np.int32) - p) >> 2), 0, (1 << bd) - 1).astype(p.dtype)
+            for i, p in enumerate(rec)]
+    unit_size = [usize, usize >> 1, usize >> 1]
+    units = []
+    for p in range(3):
+        pw, ph = (w, h) if p == 0 else (w // 2, h // 2)
+        n = oracle.lr_units(unit_size[p], pw) * oracle.lr_units(unit_size[p], ph)
+        units.append(lc.random_units(n, seed * 10 + p, chroma=p > 0))
+    ft = [1, 1, 1]
+    want = oracle.lr_apply_frame(dlf, cdef, bd, ft, unit_size, units)
+    got = _gpu_apply(ctx, dlf, cdef, bd, ft, unit_size, units)
+    for p in range(3):
+        assert np.array_equal(got[p], want[p]), p
