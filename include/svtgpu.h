@@ -486,6 +486,30 @@ int  svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpuRestUnit *
 int  svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *deblocked, const SvtGpuFrame *cdef_out,
                            SvtGpuFrame *out, const int32_t frame_type[3], void *stream);
 
+
+/* Loop-restoration search controls (WnFilterCtrls / SgFilterCtrls, EncModeConfig.c:1329-1445, fixed-range SGR
+ * search: step_range 16) and the encoder's rate inputs (Macroblock rdmult / restore costs). */
+typedef struct SvtGpuLrSearchControls {
+    int32_t wn_enabled, wn_use_chroma, wn_filter_tap_lvl, wn_use_refinement, wn_max_one_refinement_step;
+    int32_t sg_enabled, sg_use_chroma;
+    int32_t sg_start_ep[2], sg_end_ep[2], sg_ep_inc[2], sg_refine[2]; /* [luma, chroma] */
+    int32_t rdmult;
+    int32_t switchable_restore_cost[3], wiener_restore_cost[2], sgrproj_restore_cost[2];
+} SvtGpuLrSearchControls;
+/* Per-unit search record (RestUnitSearchInfo, EbRestoration.h:349-360). */
+typedef struct SvtGpuLrUnitSearch {
+    int64_t        sse[3];        /* NONE, WIENER (INT64_MAX = no filter), SGRPROJ */
+    SvtGpuRestUnit wiener, sgrproj; /* best parameters of each type */
+} SvtGpuLrUnitSearch;
+/* ≙ restoration_seg_search over every segment + rest_finish_search (EbRestorationPick.c:1471-1634) on the CDEF
+ * output `recon` against `source`; sets the units of `s` (frame types in frame_type_out[3]) and, if
+ * search_out[plane] is non-NULL, returns the per-unit records.  Synchronous. */
+int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                           const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
+                           SvtGpuLrUnitSearch *const search_out[3], void *stream);
+/* controls of wn_filter_lvl / sg_filter_lvl (EncModeConfig.c:1329-1445); rate fields are left zero */
+int svtgpu_lr_controls_for_level(int32_t wn_level, int32_t sg_level, SvtGpuLrSearchControls *c);
+
 #ifdef __cplusplus
 }
 #endif

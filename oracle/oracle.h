@@ -94,6 +94,12 @@ int  oracle_lr_units(int size, int extent);
 int  oracle_lr_apply_frame(const OracleFrame *dlf, const OracleFrame *cdef, OracleFrame *out, const int *frame_type,
                            const int *unit_size, const SvtGpuRestUnit *const *units);
 
+/* ---- loop-restoration search (lr_search_oracle.c) ---- */
+int oracle_lr_controls_for_level(int wn, int sg, SvtGpuLrSearchControls *c);
+int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, const int *unit_size,
+                           const SvtGpuLrSearchControls *c, int *frame_type_out, SvtGpuRestUnit *const *units_out,
+                           SvtGpuLrUnitSearch *const *search_out);
+
 #ifdef __cplusplus
 }
 #endif

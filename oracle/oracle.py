@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
-from svtgpu import CdefControls, CdefParams, CdefList, LfParams, LF_MI_DTYPE, REST_UNIT_DTYPE  # noqa: E402  (shared C struct layouts)
+from svtgpu import (CdefControls, CdefParams, CdefList, LfParams, LF_MI_DTYPE, REST_UNIT_DTYPE,  # noqa: E402
+                    LrSearchControls, LR_UNIT_SEARCH_DTYPE)  # (shared C struct layouts)
 
 
 class OracleFrame(ctypes.Structure):
@@ -64,6 +65,11 @@ _SIGS = {
     "oracle_lr_units": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "oracle_lr_apply_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame),
                                              ctypes.POINTER(OracleFrame), _P, _P, _P]),
+    "oracle_lr_controls_for_level": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(LrSearchControls)]),
+    "oracle_lr_search_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
+                                              ctypes.POINTER(LrSearchControls), _P, _P, _P]),
+    "oracle_compute_stats": (None, [ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
+                                    _P]),
     "oracle_dlf_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), _P, ctypes.POINTER(LfParams), ctypes.c_int,
                                         ctypes.c_int]),
     "oracle_dlf_pick": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
@@ -295,3 +301,37 @@ def lr_apply_frame(dlf, cdef, bd, frame_type, unit_size, units):
     ptrs = (ctypes.c_void_p * 3)(*[u.ctypes.data for u in ua])
     lib().oracle_lr_apply_frame(ctypes.byref(D), ctypes.byref(C), ctypes.byref(O), ptr(ft), ptr(us), ptrs)
     return out
+
+
+def lr_controls(wn, sg, rdmult=0, switchable=(0, 0, 0), wiener=(0, 0), sgrproj=(0, 0)):
+    c = LrSearchControls()
+    rc = lib().oracle_lr_controls_for_level(wn, sg, ctypes.byref(c))
+    if rc:
+        raise ValueError("unsupported lr levels %d/%d" % (wn, sg))
+    c.rdmult = rdmult
+    for i, v in enumerate(switchable):
+        c.switchable_restore_cost[i] = v
+    for i, v in enumerate(wiener):
+        c.wiener_restore_cost[i] = v
+    for i, v in enumerate(sgrproj):
+        c.sgrproj_restore_cost[i] = v
+    return c
+
+
+def lr_search_frame(rec, src, bd, unit_size, ctrls):
+    """restoration_seg_search + rest_finish_search restatement -> (frame types, units[3], records[3])."""
+    keep = []
+    R, S = _frame(rec, bd, keep), _frame(src, bd, keep)
+    us = np.ascontiguousarray(unit_size, np.int32)
+    ft = np.zeros(3, np.int32)
+    units, recs = [], []
+    for p in range(3):
+        h, w = rec[p].shape
+        n = lr_units(unit_size[p], w) * lr_units(unit_size[p], h)
+        units.append(np.zeros(n, REST_UNIT_DTYPE))
+        recs.append(np.zeros(n, LR_UNIT_SEARCH_DTYPE))
+    up = (ctypes.c_void_p * 3)(*[u.ctypes.data for u in units])
+    rp = (ctypes.c_void_p * 3)(*[r.ctypes.data for r in recs])
+    rc = lib().oracle_lr_search_frame(ctypes.byref(R), ctypes.byref(S), ptr(us), ctypes.byref(ctrls), ptr(ft), up, rp)
+    assert rc == 0
+    return [int(x) for x in ft], units, recs

@@ -11,7 +11,7 @@ CC       ?= gcc
 INC      := -I$(S)/API -I$(S)/Lib/Common/Codec -I$(S)/Lib/Common/C_DEFAULT -I$(S)/Lib/Encoder/Codec \
             -I$(S)/Lib/Encoder/C_DEFAULT -I$(S)/Lib/Encoder/Globals -I$(S)/Lib/Common/ASM_AVX2 \
             -I$(S)/Lib/Encoder/ASM_AVX2 -I$(S)/Lib/Common/ASM_SSE2 -I$(S)/Lib/Common/ASM_SSE4_1 \
-            -I$(REF)/third_party/aom/inc -I$(REF)/third_party/cpuinfo/include -Ioracle/ref_harness
+            -I$(REF)/third_party/aom/inc -I$(REF)/third_party/cpuinfo/include -I$(REF) -Ioracle/ref_harness
 CFLAGS   := -O2 -fPIC -ffunction-sections -fdata-sections -DARCH_X86_64=1 -w $(INC)
 
 # reference C sources (semantic definitions of the kernels)
@@ -21,7 +21,7 @@ DLF_C    := Lib/Common/Codec/EbDeblockingCommon.c Lib/Encoder/Codec/EbDeblocking
 LR_C     := Lib/Common/Codec/convolve.c Lib/Common/Codec/EbRestoration.c Lib/Common/Codec/EbPictureBufferDesc.c \
             Lib/Common/Codec/EbMalloc.c Lib/Common/Codec/EbLog.c Lib/Common/Codec/EbSuperRes.c Lib/Common/C_DEFAULT/EbPictureOperators_C.c \
             Lib/Common/Codec/EbThreads.c Lib/Common/Codec/EbBlockStructures.c \
-            Lib/Common/Codec/EbPictureOperators.c
+            Lib/Common/Codec/EbPictureOperators.c Lib/Encoder/Codec/EbRestorationPick.c Lib/Encoder/Codec/EbEntropyCoding.c
 MD_C     := Lib/Encoder/C_DEFAULT/EbComputeSAD_C.c Lib/Encoder/C_DEFAULT/variance.c Lib/Encoder/Codec/EbPsnr.c \
             Lib/Encoder/Codec/EbEncInterPrediction.c Lib/Common/C_DEFAULT/EbPictureOperators_C.c \
             Lib/Common/Codec/EbPictureOperators.c
@@ -37,6 +37,9 @@ AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
+# RunEmms (x86 `emms`, only reachable through aom_clear_system_state) lives in NASM sources this image cannot
+# assemble; the generic (non-x86) configuration of this file skips that call and computes the same values.
+$(OUT)/obj/Lib/Encoder/Codec/EbRestorationPick.o: CFLAGS += -UARCH_X86_64
 $(OUT)/obj/%.o: $(S)/%.c
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS) -c $< -o $@
@@ -50,8 +53,8 @@ $(OUT)/gen_golden_dlf: oracle/ref_harness/gen_golden_dlf.c $(DLF_OBJ) $(C_OBJ)
 $(OUT)/gen_golden_md: oracle/ref_harness/gen_golden_md.c $(MD_OBJ) $(C_OBJ)
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
 
-$(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(LR_OBJ) $(C_OBJ)
-	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
+$(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(sort $(LR_OBJ) $(MD_OBJ) $(C_OBJ))
+	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
 
 $(OUT)/ref_cdef_bench: oracle/ref_harness/ref_cdef_bench.c $(C_OBJ) $(AVX2_OBJ)
 	$(CC) $(CFLAGS) -mavx2 $^ -o $@ -Wl,--gc-sections -lm -lpthread

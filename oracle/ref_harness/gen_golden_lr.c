@@ -18,6 +18,9 @@
 #include "EbPictureControlSet.h"
 #include "Av1Common.h"
 #include "common_dsp_rtcd.h"
+#include "aom_dsp_rtcd.h"
+#include "EbCodingUnit.h"
+#include "EbThreads.h"
 #include "golden_io.h"
 
 void    svt_av1_loop_restoration_filter_frame(int32_t *rst_tmpbuf, Yv12BufferConfig *frame, Av1Common *cm,
@@ -27,6 +30,9 @@ int32_t svt_aom_realloc_frame_buffer(Yv12BufferConfig *ybf, int32_t width, int32
                                      int32_t use_highbitdepth, int32_t border, int32_t byte_alignment,
                                      AomCodecFrameBuffer *fb, AomGetFrameBufferCbFn cb, void *cb_priv);
 EbErrorType svt_av1_alloc_restoration_buffers(PictureControlSet *pcs, Av1Common *cm);
+void        restoration_seg_search(int32_t *rst_tmpbuf, Yv12BufferConfig *org_fts, const Yv12BufferConfig *src,
+                                   Yv12BufferConfig *trial_frame_rst, PictureControlSet *pcs, uint32_t segment_index);
+void        rest_finish_search(PictureControlSet *pcs);
 
 static void bind_c_kernels(void) {
     svt_av1_wiener_convolve_add_src        = svt_av1_wiener_convolve_add_src_c;
@@ -34,6 +40,13 @@ static void bind_c_kernels(void) {
     svt_av1_selfguided_restoration         = svt_av1_selfguided_restoration_c;
     svt_apply_selfguided_restoration       = svt_apply_selfguided_restoration_c;
     svt_memcpy                             = svt_memcpy_c;
+    svt_av1_compute_stats                  = svt_av1_compute_stats_c;
+    svt_av1_compute_stats_highbd           = svt_av1_compute_stats_highbd_c;
+    svt_get_proj_subspace                  = svt_get_proj_subspace_c;
+    svt_av1_lowbd_pixel_proj_error         = svt_av1_lowbd_pixel_proj_error_c;
+    svt_av1_highbd_pixel_proj_error        = svt_av1_highbd_pixel_proj_error_c;
+    svt_aom_mse16x16                       = svt_aom_mse16x16_c;
+    svt_aom_highbd_8_mse16x16              = svt_aom_highbd_8_mse16x16_c;
 }
 
 static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
@@ -294,6 +307,175 @@ static void gen_frames(const char *dir) {
     golden_close(&g);
 }
 
+/* ------------------------------------------------------------------------------------------- */
+/* whole-frame search: restoration_seg_search (one segment) + rest_finish_search                  */
+/* ------------------------------------------------------------------------------------------- */
+typedef struct SearchCase {
+    int w, h, bd, usize, wn, sg;
+} SearchCase;
+
+static void set_ctrls(Av1Common *cm, int wn, int sg) {
+    WnFilterCtrls *w = &cm->wn_filter_ctrls;
+    SgFilterCtrls *g = &cm->sg_filter_ctrls;
+    memset(w, 0, sizeof *w);
+    memset(g, 0, sizeof *g);
+    /* svt_aom_set_wn_filter_ctrls / svt_aom_set_sg_filter_ctrls (EncModeConfig.c:1329-1445) are static: the
+     * same values are written here */
+    if (wn) {
+        w->enabled = 1, w->use_chroma = wn <= 4, w->filter_tap_lvl = wn <= 2 ? 1 : 2;
+        w->use_refinement = wn <= 3, w->max_one_refinement_step = wn >= 2, w->use_prev_frame_coeffs = 0;
+    }
+    if (sg) {
+        g->enabled = 1, g->use_chroma = sg <= 3, g->step_range = 16;
+        g->start_ep[0] = 0, g->end_ep[0] = 16, g->ep_inc[0] = sg >= 3 ? 8 : 1;
+        g->start_ep[1] = sg == 1 ? 0 : 4, g->end_ep[1] = sg == 1 ? 16 : 5, g->ep_inc[1] = 1;
+        g->refine[0] = 1, g->refine[1] = sg == 1;
+    }
+}
+
+static void gen_search(const char *dir) {
+    static const SearchCase cases[] = {
+        {136, 72, 8, 64, 1, 1}, {200, 136, 10, 64, 1, 1}, {256, 144, 10, 128, 2, 2},
+        {160, 96, 8, 64, 3, 3}, {128, 128, 10, 64, 4, 4}, {96, 64, 8, 128, 1, 0},
+    };
+    const int ncase = (int)(sizeof(cases) / sizeof(cases[0]));
+    char      path[512];
+    snprintf(path, sizeof path, "%s/lr_search.bin", dir);
+    GoldenFile g  = golden_open(path);
+    Rng        r  = {0x4C52000000000004ull};
+    uint32_t   nc = (uint32_t)ncase;
+    golden_put1(&g, "ncase", 'I', 1, &nc);
+    int32_t *tmpbuf = malloc(RESTORATION_TMPBUF_SIZE);
+    for (int ci = 0; ci < ncase; ci++) {
+        const SearchCase *c  = &cases[ci];
+        const int         hb = c->bd > 8;
+        Av1Common               *cm   = calloc(1, sizeof(Av1Common));
+        PictureControlSet       *pcs  = calloc(1, sizeof(PictureControlSet));
+        PictureParentControlSet *ppcs = calloc(1, sizeof(PictureParentControlSet));
+        Macroblock              *x    = calloc(1, sizeof(Macroblock));
+        pcs->ppcs                     = ppcs;
+        ppcs->av1_cm                  = cm;
+        ppcs->av1x                    = x;
+        cm->child_pcs                 = pcs;
+        cm->frm_size.frame_width = cm->frm_size.superres_upscaled_width = c->w;
+        cm->frm_size.frame_height = cm->frm_size.superres_upscaled_height = c->h;
+        cm->subsampling_x = cm->subsampling_y = 1;
+        cm->use_highbitdepth                   = hb;
+        cm->bit_depth                          = c->bd;
+        cm->mi_rows                            = c->h >> 2;
+        cm->mi_cols                            = c->w >> 2;
+        set_ctrls(cm, c->wn, c->sg);
+        x->rdmult = 1000 + (int)rng_below(&r, 20000);
+        for (int k = 0; k < 3; k++) x->switchable_restore_cost[k] = 100 + (int)rng_below(&r, 2000);
+        for (int k = 0; k < 2; k++) x->wiener_restore_cost[k] = 100 + (int)rng_below(&r, 2000);
+        for (int k = 0; k < 2; k++) x->sgrproj_restore_cost[k] = 100 + (int)rng_below(&r, 2000);
+        const int usize[3] = {c->usize, c->usize >> 1, c->usize >> 1};
+        for (int p = 0; p < 3; p++) pcs->rst_info[p].restoration_unit_size = usize[p];
+        svt_av1_alloc_restoration_buffers(pcs, cm);
+        for (int p = 0; p < 3; p++) pcs->rusi_picture[p] = calloc(pcs->rst_info[p].units_per_tile, sizeof(RestUnitSearchInfo));
+        pcs->rest_search_mutex          = svt_create_mutex();
+        pcs->rest_segments_column_count = 1;
+        pcs->rest_segments_row_count    = 1;
+        Yv12BufferConfig rec, src, trial;
+        memset(&rec, 0, sizeof rec);
+        memset(&src, 0, sizeof src);
+        memset(&trial, 0, sizeof trial);
+        svt_aom_realloc_frame_buffer(&rec, c->w, c->h, 1, 1, hb, 32, 0, NULL, NULL, NULL);
+        svt_aom_realloc_frame_buffer(&src, c->w, c->h, 1, 1, hb, 32, 0, NULL, NULL, NULL);
+        svt_aom_realloc_frame_buffer(&trial, c->w, c->h, 1, 1, hb, 32, 0, NULL, NULL, NULL);
+        fill_frame(&src, c->bd, &r, NULL, 0);
+        fill_frame(&rec, c->bd, &r, &src, 6 << (c->bd - 8));
+        put_frame(&g, "src", ci, &src, c->bd);
+        put_frame(&g, "rec", ci, &rec, c->bd);
+        cm->frame_to_show = &rec; /* search_norestore_seg reads the unfiltered recon through it */
+        restoration_seg_search(tmpbuf, &rec, &src, &trial, pcs, 0);
+        rest_finish_search(pcs);
+        char    nm[64];
+        int32_t prm[16] = {c->w, c->h, c->bd, c->usize, c->wn, c->sg, x->rdmult, x->switchable_restore_cost[0],
+                           x->switchable_restore_cost[1], x->switchable_restore_cost[2], x->wiener_restore_cost[0],
+                           x->wiener_restore_cost[1], x->sgrproj_restore_cost[0], x->sgrproj_restore_cost[1], 0, 0};
+        snprintf(nm, sizeof nm, "c%d_params", ci);
+        golden_put1(&g, nm, 'i', 16, prm);
+        int32_t ft[3];
+        for (int p = 0; p < 3; p++) {
+            const RestorationInfo *rsi = &pcs->rst_info[p];
+            ft[p]                      = rsi->frame_restoration_type;
+            const int nu               = rsi->units_per_tile;
+            /* per unit: {type, vfilter[8], hfilter[8], ep, xqd0, xqd1} of the final unit info, and the search record
+             * {sse none, sse wiener (or -1 = INT64_MAX), sse sgr, wiener v[8] h[8], sgr ep xqd0 xqd1} */
+            int32_t *u  = calloc((size_t)nu, 20 * sizeof(int32_t));
+            int64_t *ss = calloc((size_t)nu, 3 * sizeof(int64_t));
+            int32_t *sp = calloc((size_t)nu, 19 * sizeof(int32_t));
+            for (int k = 0; k < nu; k++) {
+                const RestorationUnitInfo *ui = &rsi->unit_info[k];
+                int32_t                   *e  = u + 20 * k;
+                e[0]                          = ft[p] == RESTORE_NONE ? 0 : ui->restoration_type;
+                for (int q = 0; q < 8; q++) e[1 + q] = ui->wiener_info.vfilter[q], e[9 + q] = ui->wiener_info.hfilter[q];
+                e[17] = ui->sgrproj_info.ep, e[18] = ui->sgrproj_info.xqd[0], e[19] = ui->sgrproj_info.xqd[1];
+                const RestUnitSearchInfo *rs = &pcs->rusi_picture[p][k];
+                for (int q = 0; q < 3; q++) ss[3 * k + q] = rs->sse[q] == INT64_MAX ? -1 : rs->sse[q];
+                for (int q = 0; q < 8; q++) sp[19 * k + q] = rs->wiener.vfilter[q], sp[19 * k + 8 + q] = rs->wiener.hfilter[q];
+                sp[19 * k + 16] = rs->sgrproj.ep, sp[19 * k + 17] = rs->sgrproj.xqd[0], sp[19 * k + 18] = rs->sgrproj.xqd[1];
+            }
+            snprintf(nm, sizeof nm, "c%d_units%d", ci, p);
+            golden_put2(&g, nm, 'i', (uint32_t)nu, 20, u);
+            snprintf(nm, sizeof nm, "c%d_sse%d", ci, p);
+            golden_put2(&g, nm, 'q', (uint32_t)nu, 3, ss);
+            snprintf(nm, sizeof nm, "c%d_rec%d_params", ci, p);
+            golden_put2(&g, nm, 'i', (uint32_t)nu, 19, sp);
+            free(u), free(ss), free(sp);
+        }
+        snprintf(nm, sizeof nm, "c%d_ftype", ci);
+        golden_put1(&g, nm, 'i', 3, ft);
+        free(rec.buffer_alloc), free(src.buffer_alloc), free(trial.buffer_alloc);
+    }
+    free(tmpbuf);
+    golden_close(&g);
+}
+
+/* svt_av1_compute_stats(_highbd)_c on random units (win 7/5/3, bd 8/10/12) */
+static void gen_stats(const char *dir) {
+    char path[512];
+    snprintf(path, sizeof path, "%s/lr_stats.bin", dir);
+    GoldenFile g = golden_open(path);
+    Rng        r = {0x4C52000000000005ull};
+    const int  N = 18;
+    int32_t    meta[18 * 6];
+    for (int n = 0; n < N; n++) {
+        const int bd = n % 3 == 0 ? 8 : n % 3 == 1 ? 10 : 12, win = n % 9 < 3 ? 7 : n % 9 < 6 ? 5 : 3;
+        const int w = 16 + (int)rng_below(&r, 100), h = 16 + (int)rng_below(&r, 80), st = w + 8;
+        uint16_t *d = malloc(sizeof(uint16_t) * st * (h + 8)), *s = malloc(sizeof(uint16_t) * st * (h + 8));
+        const int base = (int)rng_below(&r, 1u << bd), kind = n & 1;
+        for (int k = 0; k < st * (h + 8); k++) {
+            d[k] = (uint16_t)rand_px(&r, bd, base, kind);
+            s[k] = (uint16_t)clampi(d[k] + (int)rng_below(&r, 9) - 4, 0, (1 << bd) - 1);
+        }
+        int64_t M[49], H[49 * 49];
+        if (bd == 8) {
+            uint8_t *d8 = malloc(st * (h + 8)), *s8 = malloc(st * (h + 8));
+            for (int k = 0; k < st * (h + 8); k++) d8[k] = (uint8_t)d[k], s8[k] = (uint8_t)s[k];
+            svt_av1_compute_stats_c(win, d8 + 4 * st + 4, s8 + 4 * st + 4, 0, w, 0, h, st, st, M, H);
+            free(d8), free(s8);
+        } else
+            svt_av1_compute_stats_highbd_c(win, CONVERT_TO_BYTEPTR(d + 4 * st + 4), CONVERT_TO_BYTEPTR(s + 4 * st + 4), 0, w,
+                                           0, h, st, st, M, H, (EbBitDepth)bd);
+        int32_t *m = meta + 6 * n;
+        m[0] = bd, m[1] = win, m[2] = w, m[3] = h, m[4] = st, m[5] = 0;
+        char nm[32];
+        snprintf(nm, sizeof nm, "dgd%d", n);
+        golden_put2(&g, nm, 'H', (uint32_t)(h + 8), (uint32_t)st, d);
+        snprintf(nm, sizeof nm, "src%d", n);
+        golden_put2(&g, nm, 'H', (uint32_t)(h + 8), (uint32_t)st, s);
+        snprintf(nm, sizeof nm, "M%d", n);
+        golden_put1(&g, nm, 'q', (uint32_t)(win * win), M);
+        snprintf(nm, sizeof nm, "H%d", n);
+        golden_put1(&g, nm, 'q', (uint32_t)(win * win * win * win), H);
+        free(d), free(s);
+    }
+    golden_put2(&g, "meta", 'i', N, 6, meta);
+    golden_close(&g);
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: %s <out_dir>\n", argv[0]);
@@ -303,6 +485,8 @@ int main(int argc, char **argv) {
     gen_wiener(argv[1]);
     gen_sgr(argv[1]);
     gen_frames(argv[1]);
+    gen_stats(argv[1]);
+    gen_search(argv[1]);
     printf("lr golden vectors written to %s\n", argv[1]);
     return 0;
 }

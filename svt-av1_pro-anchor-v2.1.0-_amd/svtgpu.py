@@ -129,6 +129,21 @@ def rest_units_from_rows(rows):
     return u
 
 
+class LrSearchControls(ctypes.Structure):
+    """SvtGpuLrSearchControls (WnFilterCtrls / SgFilterCtrls + Macroblock rate fields)."""
+    _fields_ = [("wn_enabled", ctypes.c_int32), ("wn_use_chroma", ctypes.c_int32), ("wn_filter_tap_lvl", ctypes.c_int32),
+                ("wn_use_refinement", ctypes.c_int32), ("wn_max_one_refinement_step", ctypes.c_int32),
+                ("sg_enabled", ctypes.c_int32), ("sg_use_chroma", ctypes.c_int32),
+                ("sg_start_ep", ctypes.c_int32 * 2), ("sg_end_ep", ctypes.c_int32 * 2),
+                ("sg_ep_inc", ctypes.c_int32 * 2), ("sg_refine", ctypes.c_int32 * 2), ("rdmult", ctypes.c_int32),
+                ("switchable_restore_cost", ctypes.c_int32 * 3), ("wiener_restore_cost", ctypes.c_int32 * 2),
+                ("sgrproj_restore_cost", ctypes.c_int32 * 2)]
+
+
+LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYPE), ("sgrproj", REST_UNIT_DTYPE)],
+                                align=True)
+
+
 class ConvolveParams(ctypes.Structure):
     _fields_ = [("round_0", ctypes.c_int32), ("round_1", ctypes.c_int32)]
 
@@ -226,6 +241,8 @@ _SIGS = {
     "svtgpu_lr_units": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "svtgpu_lr_set_units": (ctypes.c_int, [_P, _I32, _P, _P]),
     "svtgpu_lr_apply_frame": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "svtgpu_lr_search_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P, _P, _P]),
+    "svtgpu_lr_controls_for_level": (ctypes.c_int, [_I32, _I32, ctypes.POINTER(LrSearchControls)]),
 }
 
 _lib = None

@@ -191,3 +191,24 @@ def test_lr_frame_golden():
             assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
         n += 1
     assert n >= 6
+
+
+def test_lr_search_golden():
+    import lr_cases as lc
+    n = 0
+    for c in lc.search_cases():
+        ft, units, recs = oracle.lr_search_frame(c["rec"], c["src"], c["bd"], c["unit_size"], c["ctrls"])
+        lc.compare_search(ft, units, recs, c)
+        n += 1
+    assert n >= 6
+
+
+def test_compute_stats_golden():
+    g = cc.load("lr_stats.bin")
+    L = oracle.lib()
+    for n in range(len(g["meta"])):
+        bd, win, w, h, st, _ = (int(x) for x in g["meta"][n])
+        d, s = g["dgd%d" % n].copy(), g["src%d" % n].copy()
+        M, H = np.zeros(win * win, np.int64), np.zeros(win ** 4, np.int64)
+        L.oracle_compute_stats(win, oracle.ptr(d), oracle.ptr(s), st, w, h, bd, oracle.ptr(M), oracle.ptr(H))
+        assert np.array_equal(M, g["M%d" % n]) and np.array_equal(H, g["H%d" % n]), (n, bd, win)
