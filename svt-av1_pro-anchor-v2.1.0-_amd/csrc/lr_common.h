@@ -1,0 +1,105 @@
+// lr_common.h — device tables and per-pixel helpers shared by the loop-restoration apply (lr.hip) and
+// search (lr_search.hip) kernels.  Reference: Source/Lib/Common/Codec/EbRestoration.c:49-103, 647-760.
+#pragma once
+#include "svtgpu_internal.h"
+
+struct SvtGpuLrState {
+    SvtGpuContext  *ctx;
+    int32_t         width, height;
+    int32_t         unit_size[3], hunits[3], vunits[3];
+    SvtGpuRestUnit *d_units[3];
+    // search scratch (allocated on the first svtgpu_lr_search_frame)
+    int16_t        *d_flt;   // [16 eps][2][W*H] self-guided filter outputs of the plane being searched
+    void           *d_work;  // per-unit / per-tile accumulators
+    size_t          work_bytes;
+};
+
+namespace {
+
+constexpr int NTHR = 256;
+// self-guided parameter sets svt_aom_eb_sgr_params (EbRestoration.c:85-103): radii and s values
+__constant__ int c_sgr_r[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
+                                   {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
+__constant__ int c_sgr_s[16][2] = {{140, 3236}, {112, 2158}, {93, 1618}, {80, 1438}, {70, 1295}, {58, 1177},
+                                   {47, 1079},  {37, 996},   {30, 925},  {25, 863},  {-1, 2589}, {-1, 1618},
+                                   {-1, 1177},  {-1, 925},   {56, -1},   {22, -1}};
+// svt_aom_eb_x_by_xplus1 (EbRestoration.c:647-662): round(256 x / (x + 1)), 0 -> 1, 255 -> 256
+__constant__ int c_x_by_xplus1[256] = {
+    1,   128, 171, 192, 205, 213, 219, 224, 228, 230, 233, 235, 236, 238, 239, 240, 241, 242, 243, 243, 244, 244,
+    245, 245, 246, 246, 247, 247, 247, 247, 248, 248, 248, 248, 249, 249, 249, 249, 249, 250, 250, 250, 250, 250,
+    250, 250, 251, 251, 251, 251, 251, 251, 251, 251, 251, 251, 252, 252, 252, 252, 252, 252, 252, 252, 252, 252,
+    252, 252, 252, 252, 252, 252, 252, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253,
+    253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 253, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254,
+    254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 254, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
+    255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 256};
+// svt_aom_eb_one_by_x (EbRestoration.c:664-667): round(4096 / n)
+__constant__ int c_one_by_x[25] = {4096, 2048, 1365, 1024, 819, 683, 585, 512, 455, 410, 372, 341, 315,
+                                   293,  273,  256,  241,  228, 216, 205, 195, 186, 178, 171, 164};
+
+struct WienerRound {
+    int r0, r1;
+};
+// get_conv_params_wiener (EbRestoration.c:49-72)
+__host__ __device__ inline WienerRound wiener_round(int bd) {
+    WienerRound r{3, 11};
+    const int   over = bd + 7 - 3 + 2 - 16;
+    if (over > 0) r.r0 += over, r.r1 -= over;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
+// tile filters over an LDS image `v` (u16, row stride vs) whose (0,0) is the tile's first output
+// ---------------------------------------------------------------------------------------------
+// Wiener: horizontal 8-tap pass into t (rows -3..h+3 -> t rows 0..h+6), vertical pass into out.
+template <typename T>
+__device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int w, int h, const int16_t *fx,
+                            const int16_t *fy, int bd, T *out, size_t os) {
+    const WienerRound rr  = wiener_round(bd);
+    const int         lim = (1 << (bd + 1 + 7 - rr.r0)) - 1;
+    int16_t           hx[8], vy[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) hx[k] = fx[k], vy[k] = fy[k];
+    for (int i = threadIdx.x; i < (h + 7) * w; i += NTHR) {
+        const int       y = i / w - 3, x = i % w;
+        const uint16_t *s = v + y * vs + x - 3;
+        int             sum = ((int)s[3] << 7) + (1 << (bd + 6));
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += (int)s[k] * hx[k];
+        t[(y + 3) * ts + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
+    }
+    __syncthreads();
+    const int maxv = (1 << bd) - 1;
+    for (int i = threadIdx.x; i < h * w; i += NTHR) {
+        const int       y = i / w, x = i % w;
+        const uint16_t *c = t + y * ts + x; // rows y-3 .. y+4 of the intermediate
+        int             sum = ((int)c[3 * ts] << 7) - (1 << (bd + rr.r1 - 1));
+#pragma unroll
+        for (int k = 0; k < 8; k++) sum += (int)c[k * ts] * vy[k];
+        out[y * os + x] = (T)min(max((sum + (1 << (rr.r1 - 1))) >> rr.r1, 0), maxv);
+    }
+}
+
+// A, B of one self-guided pass at (i, j) (selfguided_restoration_*_internal, EbRestoration.c:693-760)
+__device__ inline void sgr_ab(const uint16_t *v, int vs, int i, int j, int r, int s, int bd, int *A, int *B) {
+    int sum = 0, sq = 0;
+    for (int y = -r; y <= r; y++)
+        for (int x = -r; x <= r; x++) {
+            const int p = v[(i + y) * vs + j + x];
+            sum += p;
+            sq += p * p;
+        }
+    const int      n = (2 * r + 1) * (2 * r + 1);
+    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
+    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
+    const uint32_t p = (a * n < b * b) ? 0u : a * n - b * b;
+    const uint32_t z = (p * (uint32_t)s + (1u << 19)) >> 20;
+    *A               = c_x_by_xplus1[min(z, 255u)];
+    *B = (int)(((uint32_t)(256 - *A) * (uint32_t)sum * (uint32_t)c_one_by_x[n - 1] + (1u << 11)) >> 12);
+}
+
+} // namespace

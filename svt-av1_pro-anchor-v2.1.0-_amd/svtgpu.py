@@ -536,6 +536,15 @@ class LrState:
         assert len(u) == self.units[plane][0] * self.units[plane][1], (len(u), self.units[plane])
         check(lib().svtgpu_lr_set_units(self.h, plane, ptr(u), stream))
 
+    def search(self, recon, source, ctrls, stream=None, records=False):
+        """svtgpu_lr_search_frame: picks frame types and unit parameters (kept on the device for apply).
+        Returns the frame types and, with records=True, the per-unit search records."""
+        ft = np.zeros(3, np.int32)
+        recs = [np.zeros(hu * vu, LR_UNIT_SEARCH_DTYPE) for hu, vu in self.units] if records else None
+        rp = (ctypes.c_void_p * 3)(*[r.ctypes.data for r in recs]) if records else None
+        check(lib().svtgpu_lr_search_frame(self.h, recon.h, source.h, ctypes.byref(ctrls), ptr(ft), rp, stream))
+        return ([int(x) for x in ft], recs) if records else [int(x) for x in ft]
+
     def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
         ft = np.ascontiguousarray(frame_type, np.int32)
         check(lib().svtgpu_lr_apply_frame(self.h, deblocked.h, cdef_out.h, out.h, ptr(ft), stream))

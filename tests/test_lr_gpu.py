@@ -111,3 +111,59 @@ def test_lr_frame_vs_oracle(ctx, w, h, bd, usize, seed):
     got = _gpu_apply(ctx, dlf, cdef, bd, ft, unit_size, units)
     for p in range(3):
         assert np.array_equal(got[p], want[p]), p
+
+
+# ------------------------------------------------------------------ search
+def _gpu_search(ctx, rec, src, bd, unit_size, ctrls):
+    h, w = rec[0].shape
+    R, S = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+    R.upload(rec)
+    S.upload(src)
+    st = svtgpu.LrState(ctx, w, h, unit_size)
+    ft, recs = st.search(R, S, ctrls, records=True)
+    return st, R, ft, recs
+
+
+@pytest.mark.parametrize("case", list(range(6)))
+def test_lr_search_golden(ctx, case):
+    c = list(lc.search_cases())[case]
+    st, R, ft, recs = _gpu_search(ctx, c["rec"], c["src"], c["bd"], c["unit_size"], c["ctrls"])
+    lc.compare_search(ft, c["units"], recs, c)  # frame types + per-unit records vs the reference
+    # the picked units stay in the state: applying them must equal applying the reference's picked units
+    h, w = c["rec"][0].shape
+    D, O = svtgpu.Frame(ctx, w, h, c["bd"]), svtgpu.Frame(ctx, w, h, c["bd"])
+    D.upload(c["rec"])
+    st.apply(D, R, O, ft)
+    want = oracle.lr_apply_frame(c["rec"], c["rec"], c["bd"], ft, c["unit_size"], c["units"])
+    got = O.download()
+    for p in range(3):
+        assert np.array_equal(got[p], want[p]), (c["name"], p)
+
+
+LR_SEARCH_CASES = [(320, 192, 10, 64, 1, 1, 5), (640, 360, 8, 128, 1, 1, 6), (1920, 1080, 10, 256, 1, 1, 7),
+                   (512, 288, 10, 128, 3, 2, 8)]
+
+
+@pytest.mark.parametrize("w,h,bd,usize,wn,sg,seed", LR_SEARCH_CASES)
+def test_lr_search_vs_oracle(ctx, w, h, bd, usize, wn, sg, seed):
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0800 + seed)
+    ctrls = oracle.lr_controls(wn, sg, rdmult=6000 + seed * 1000, switchable=(300, 700, 900), wiener=(250, 800),
+                               sgrproj=(250, 900))
+    unit_size = [usize, usize >> 1, usize >> 1]
+    want_ft, want_units, want_recs = oracle.lr_search_frame(rec, src, bd, unit_size, ctrls)
+    st, R, ft, recs = _gpu_search(ctx, rec, src, bd, unit_size, ctrls)
+    assert ft == want_ft
+    for p in range(3):
+        for k in ("sse",):
+            np.testing.assert_array_equal(recs[p][k], want_recs[p][k], err_msg="plane %d %s" % (p, k))
+        np.testing.assert_array_equal(recs[p]["sgrproj"], want_recs[p]["sgrproj"])
+        ok = recs[p]["sse"][:, 1] != np.iinfo(np.int64).max
+        np.testing.assert_array_equal(recs[p]["wiener"][ok], want_recs[p]["wiener"][ok])
+    # the searched units drive the apply: compare the restored frame with the oracle apply of the oracle's units
+    D, O = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+    D.upload(rec)
+    st.apply(D, R, O, ft)
+    want = oracle.lr_apply_frame(rec, rec, bd, ft, unit_size, want_units)
+    got = O.download()
+    for p in range(3):
+        assert np.array_equal(got[p], want[p]), p
