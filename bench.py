@@ -7,8 +7,9 @@ A "step" = one 4K 10-bit 4:2:0 frame through the device-resident in-loop filter 
   CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
       strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
       (svt_av1_cdef_frame).
-  LR stage (EbRestProcess.c): loop-restoration apply (svt_av1_loop_restoration_filter_frame) of the CDEF
-      output with per-unit Wiener / self-guided parameters (RU 256 luma / 128 chroma; stripe boundary lines
+  LR stage (EbRestProcess.c): loop-restoration search (restoration_seg_search + rest_finish_search,
+      wn/sg filter level 1: 7-tap Wiener with refinement, 16 SGR eps with refinement) on the CDEF output and
+      the apply (svt_av1_loop_restoration_filter_frame; RU 256 luma / 128 chroma; stripe boundary lines
       from the DLF output);
   MD distortion stage: SAD / SSE / variance of every AV1 block shape of every SB against 7 reference
       frames at one full-pel motion vector per (SB, reference) (SURVEY.md §8d config 5 workload at 4K).
@@ -107,21 +108,12 @@ def main():
     dl = svtgpu.DlfState(ctx, W, H)
     dl.set_mode_info(mi, sp)
     lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
-    # loop restoration: unit parameters (the LR search is not yet in the step: fixed mixed Wiener/SGR units)
+    # loop restoration: RU 256 / 128, wn_filter_lvl 1 + sg_filter_lvl 1 (maximum search work); the rate
+    # inputs (rdmult, restore-type costs) come from the encoder's entropy state: fixed representative values
     lr_us = [256, 128, 128]
     lr = svtgpu.LrState(ctx, W, H, lr_us)
-    rng_lr = np.random.default_rng(7)
-    for p in range(3):
-        hu, vu = lr.units[p]
-        rows = np.zeros((hu * vu, 20), np.int32)
-        for k in range(hu * vu):
-            t = [int(rng_lr.integers(-5, 11)), int(rng_lr.integers(-23, 9)), int(rng_lr.integers(-17, 47))]
-            if p:
-                t[0] = 0
-            taps = [t[0], t[1], t[2], -2 * sum(t), t[2], t[1], t[0], 0]
-            rows[k] = [1 + (k % 2)] + taps + taps + [int(rng_lr.integers(0, 16)), int(rng_lr.integers(-96, 32)),
-                                                      int(rng_lr.integers(-32, 96))]
-        lr.set_units(p, svtgpu.rest_units_from_rows(rows), sp)
+    lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=7000, switchable=(300, 700, 900), wiener=(250, 800),
+                                  sgrproj=(250, 900))
     L = svtgpu.Frame(ctx, W, H, bd)
     NREF = 7
     md_refs = []
@@ -173,8 +165,9 @@ def main():
         st.apply(D, O, prm, sp)
         if timed:
             es[3].record(stream)
-        # LR apply on the CDEF output (boundary lines from the DLF output)
-        lr.apply(D, O, L, [1, 1, 1], sp)
+        # LR search + apply on the CDEF output (boundary lines from the DLF output)
+        lr_ft = lr.search(O, S, lr_ctrls, sp)
+        lr.apply(D, O, L, lr_ft, sp)
         if timed:
             es[4].record(stream)
         # MD distortion batch (source vs 7 references, every block shape)
@@ -229,12 +222,12 @@ def main():
         "data": "synthetic",
         "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply %dx%d %d-bit 4:2:0, dlf level 1 "
                                "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
-                               "LR apply (RU 256/128, mixed Wiener/SGR units; LR search not yet in the step)"
+                               "LR search+apply (RU 256/128, wn/sg level 1)"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
                    "parallelism": "fb_row_bands%d" % n if n > 1 else "single",
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
-                                "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_apply": round(lr_ms, 4),
+                                "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_search_apply": round(lr_ms, 4),
                                 "md_sad_sse_var": round(md_ms, 4)},
                    "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
         "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),

@@ -561,6 +561,20 @@ class LrState:
             pass
 
 
+def lr_controls(wn_level, sg_level, rdmult=0, switchable=(0, 0, 0), wiener=(0, 0), sgrproj=(0, 0)):
+    """SvtGpuLrSearchControls of the reference's wn/sg filter levels plus the encoder's rate inputs."""
+    c = LrSearchControls()
+    check(lib().svtgpu_lr_controls_for_level(wn_level, sg_level, ctypes.byref(c)))
+    c.rdmult = rdmult
+    for i, v in enumerate(switchable):
+        c.switchable_restore_cost[i] = v
+    for i, v in enumerate(wiener):
+        c.wiener_restore_cost[i] = v
+    for i, v in enumerate(sgrproj):
+        c.sgrproj_restore_cost[i] = v
+    return c
+
+
 def plane_sse(a, b, plane, stream=None):
     v = _U64()
     check(lib().svtgpu_plane_sse(a.h, b.h, plane, ctypes.byref(v), stream))
