@@ -274,6 +274,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     for (int p = 0; p < 3; p++) (void)hipFree(s->d_units[p]);
     (void)hipFree(s->d_flt);
     (void)hipFree(s->d_work);
+    if (s->h_pin) (void)hipHostFree(s->h_pin);
     delete s;
 }
 

@@ -9,9 +9,12 @@ struct SvtGpuLrState {
     int32_t         unit_size[3], hunits[3], vunits[3];
     SvtGpuRestUnit *d_units[3];
     // search scratch (allocated on the first svtgpu_lr_search_frame)
-    int16_t        *d_flt;   // [16 eps][2][W*H] self-guided filter outputs of the plane being searched
-    void           *d_work;  // per-unit / per-tile accumulators
+    int16_t        *d_flt;   // per plane [eps][2][W*H] self-guided filter outputs of every searched ep
+    size_t          flt_bytes;
+    void           *d_work;  // per-unit / per-tile accumulators, descents, work lists
     size_t          work_bytes;
+    void           *h_pin;   // pinned host staging for the search's read-backs
+    size_t          pin_bytes;
 };
 
 namespace {
@@ -84,7 +87,19 @@ __device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int 
     }
 }
 
-// A, B of one self-guided pass at (i, j) (selfguided_restoration_*_internal, EbRestoration.c:693-760)
+// A, B of a self-guided pass from the box sum / sum of squares over n = (2r+1)^2 pixels
+// (selfguided_restoration_*_internal, EbRestoration.c:693-760); u32 arithmetic wraps like the reference's
+__device__ inline void sgr_ab_from_sums(int sum, int sq, int n, int s, int bd, const int *x_by_xplus1, int *A,
+                                        int *B) {
+    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
+    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
+    const uint32_t p = (a * n < b * b) ? 0u : a * n - b * b;
+    const uint32_t z = (p * (uint32_t)s + (1u << 19)) >> 20;
+    *A               = x_by_xplus1[min(z, 255u)];
+    *B = (int)(((uint32_t)(256 - *A) * (uint32_t)sum * (uint32_t)c_one_by_x[n - 1] + (1u << 11)) >> 12);
+}
+
+// A, B of one self-guided pass at (i, j) of an LDS image
 __device__ inline void sgr_ab(const uint16_t *v, int vs, int i, int j, int r, int s, int bd, int *A, int *B) {
     int sum = 0, sq = 0;
     for (int y = -r; y <= r; y++)
@@ -93,13 +108,7 @@ __device__ inline void sgr_ab(const uint16_t *v, int vs, int i, int j, int r, in
             sum += p;
             sq += p * p;
         }
-    const int      n = (2 * r + 1) * (2 * r + 1);
-    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
-    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
-    const uint32_t p = (a * n < b * b) ? 0u : a * n - b * b;
-    const uint32_t z = (p * (uint32_t)s + (1u << 19)) >> 20;
-    *A               = c_x_by_xplus1[min(z, 255u)];
-    *B = (int)(((uint32_t)(256 - *A) * (uint32_t)sum * (uint32_t)c_one_by_x[n - 1] + (1u << 11)) >> 12);
+    sgr_ab_from_sums(sum, sq, (2 * r + 1) * (2 * r + 1), s, bd, c_x_by_xplus1, A, B);
 }
 
 } // namespace

@@ -4,22 +4,28 @@
 // of Common/Codec/EbRestoration.c and convolve.c; the rate helpers of EbEntropyCoding.c:2876-3022.
 //
 // The search runs without stripe boundaries (use_boundaries_in_rest_search = 0, EbEncHandle.c:4162), so every
-// filter output is a per-pixel function of the edge-clamped CDEF output.  The data-parallel work runs on the
-// device over a tile list (<= 64x64 tiles aligned to each restoration unit):
+// filter output is a per-pixel function of the edge-clamped CDEF output.  All searched planes are processed
+// together over one tile list (<= 64x64 tiles aligned to each restoration unit, planes in order):
 //   unit_sums_kernel      Σ dgd (Wiener average) and the RESTORE_NONE SSE per unit
-//   wiener_stats_kernel   the 7x7 (5x5, 3x3) Wiener statistics M, H of svt_av1_compute_stats: each lane
-//                         accumulates a window-column pair block (49 MACs per 14 LDS reads) over a slice of the
-//                         tile; per-tile partials are reduced per unit without atomics
-//   wiener_trial_kernel   SSE of a unit filtered with candidate taps (one candidate per unit per launch)
-//   sgr_flt_kernel        the self-guided filters of every searched ep (flt kept in HBM as int16) and the 2x2
-//                         projection moments per (unit, ep) in exact int64
-//   proj_err_kernel       projection error of candidate xqd per (unit, ep)
-//   sgr_sse_kernel        SSE of the chosen self-guided unit output (with clipping)
-// The sequential parts — the int64 fixed-point Wiener solve, the coordinate-descent refinements (advanced in
-// lock-step rounds: all units / (unit, ep) pairs propose one candidate per launch) and the RD pass over the
-// units — run on the host exactly as the reference orders them.
+//   wiener_stats_kernel   the 7x7 (5x5, 3x3) Wiener statistics M, H of svt_av1_compute_stats: a lane group per
+//                         window-column pair accumulates its 7x7 block with v_dot2_i32_i16 over horizontal pixel
+//                         pairs (diagonal groups also form M); per-tile partials are reduced per unit
+//   sgr_flt_kernel        box sums of a tile once, then for every searched ep the A/B maps, both self-guided
+//                         filters (kept in HBM as int16) and the 2x2 projection moments in exact int64
+//   wiener_trial_kernel / proj_err_kernel
+//                         the SSE of one candidate per live descent (grid-stride over a device work list)
+//   *_advance_kernel      the coordinate descents of finer_tile_search_wiener_seg / finer_search_pixel_proj_error
+//                         run on the device: report the last error, propose the next candidate, rebuild the list
+//   sgr_best_kernel, sgr_sse_kernel
+//                         best ep per unit (strict <) and the SSE of its clipped output
+// The host does what is sequential in the reference and cheap: the int64 fixed-point Wiener decomposition, the
+// 2x2 projection solve in double, and the RD pass over the units.  A frame costs four host synchronisations plus
+// one per batch of descent rounds.
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -29,7 +35,7 @@
 namespace {
 
 struct Tile {
-    int32_t unit, x0, y0, w, h;
+    int32_t plane, unit, x0, y0, w, h; // unit: global index over the searched planes
 };
 struct URect {
     int32_t h_start, h_end, v_start, v_end;
@@ -39,6 +45,22 @@ constexpr int PRJ_MIN0 = -96, PRJ_MAX0 = 31, PRJ_MIN1 = -32, PRJ_MAX1 = 95;
 const int     kTapMin[3] = {-5, -23, -17}, kTapMax[3] = {10, 8, 46};
 const int     kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
                               {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
+
+struct PlaneArgs {
+    const void *dgd, *src;
+    int16_t    *flt; // [ne][2][W*H] self-guided outputs
+    int32_t     dstride, sstride, W, H, bd;
+    int32_t     unit_base, pair_base, ne; // SGR pair of (unit, k) = pair_base + (unit - unit_base) * ne + k
+    int32_t     eps[16];
+    int32_t     win, nval;                // Wiener window and statistics values per unit
+    int64_t     mh_off;                   // this plane's statistics in the M/H buffer (int64 elements)
+};
+struct SearchArgs {
+    PlaneArgs      pl[3];
+    const Tile    *tiles;
+    const URect   *units;
+    const int32_t *tile0; // first tile of every global unit, plus the end
+};
 
 template <typename T>
 __device__ inline int px(const T *p, int stride, int W, int H, int y, int x) {
@@ -52,23 +74,22 @@ __device__ inline unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
-struct PlaneArgs {
-    const void *dgd, *src;
-    int32_t     dstride, sstride, W, H, bd;
-    const Tile *tiles;
-    const URect *units;
-};
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+__device__ inline int dot2(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
+}
 
 // ---------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void unit_sums_kernel(const PlaneArgs a, unsigned long long *sum,
+__global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsigned long long *sum,
                                                         unsigned long long *sse) {
-    const Tile t = a.tiles[blockIdx.x];
-    const T   *d = (const T *)a.dgd, *s = (const T *)a.src;
+    const Tile       t = A.tiles[blockIdx.x];
+    const PlaneArgs &P = A.pl[t.plane];
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     unsigned long long ps = 0, pe = 0;
     for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
         const int y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-        const int dv = d[(size_t)y * a.dstride + x], sv = s[(size_t)y * a.sstride + x];
+        const int dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
         ps += (unsigned)dv;
         pe += (unsigned long long)((dv - sv) * (dv - sv));
     }
@@ -81,76 +102,125 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const PlaneArgs a, unsig
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wiener statistics: jobs = window-column pairs (c1 <= c2) + one M job; 8 lanes per job split the pixels
+// Wiener statistics.  Output per tile: [pair (c1 <= c2)][r1 * 7 + r2] H blocks, then [c * 7 + r] M.
+// Off-diagonal column pairs get LO lanes each in the first waves, the WIN diagonal pairs (whose blocks are
+// symmetric, and which also accumulate M) LD lanes each in the last wave(s); lanes stride over pixel pairs.
 // ---------------------------------------------------------------------------------------------
-constexpr int ST_APRON = 3, ST_W = 64 + 2 * ST_APRON;
-template <typename T>
-__global__ __launch_bounds__(256) void wiener_stats_kernel(const PlaneArgs a, int win, const unsigned long long *sum,
-                                                           long long *part) {
-    __shared__ int D[ST_W * ST_W];
-    __shared__ int S[64 * 64];
-    const Tile  t   = a.tiles[blockIdx.x];
-    const URect u   = a.units[t.unit];
-    const long long area = (long long)(u.h_end - u.h_start) * (u.v_end - u.v_start);
-    const int   avg  = (int)(sum[t.unit] / (unsigned long long)area);
-    const T    *d = (const T *)a.dgd, *s = (const T *)a.src;
-    for (int i = threadIdx.x; i < (t.h + 6) * (t.w + 6); i += 256) {
-        const int r = i / (t.w + 6), c = i % (t.w + 6);
-        D[r * ST_W + c] = px(d, a.dstride, a.W, a.H, t.y0 + r - 3, t.x0 + c - 3) - avg;
+constexpr int ST_W = 70, ST_SLOTS = 56;
+template <int WIN>
+struct StatsCfg {
+    static constexpr int HALF = WIN / 2, NPAIR = WIN * (WIN + 1) / 2, NOFF = WIN * (WIN - 1) / 2;
+    static constexpr int OFF_THR = WIN == 3 ? 128 : 192, LO = OFF_THR / NOFF, LD = (256 - OFF_THR) / WIN;
+};
+
+__device__ inline void off_pair(int win, int q, int *c1, int *c2) { // q-th (c1 < c2) pair
+    int a = 0;
+    while (q >= win - 1 - a) q -= win - 1 - a, a++;
+    *c1 = a, *c2 = a + 1 + q;
+}
+
+template <typename T, int WIN>
+__global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, int tile_begin,
+                                                           const unsigned long long *sum, long long *part) {
+    using C = StatsCfg<WIN>;
+    constexpr int NVAL = (C::NPAIR + 1) * 49;
+    __shared__ int lds[256 * ST_SLOTS]; // staging (D pairs, S pairs), then the lane partials
+    uint32_t      *D2 = (uint32_t *)lds, *S2 = D2 + ST_W * ST_W;
+    const Tile       t = A.tiles[tile_begin + blockIdx.x];
+    const PlaneArgs &P = A.pl[t.plane];
+    const URect      u = A.units[t.unit];
+    const long long  area = (long long)(u.h_end - u.h_start) * (u.v_end - u.v_start);
+    const int        avg  = (int)(sum[t.unit] / (unsigned long long)area);
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    const int        sw = t.w + 6, hw2 = (t.w + 1) >> 1;
+    // D2[r][c] = (D[r][c], D[r][c + 1]) as int16 pairs, D = dgd - avg over the tile plus a 3-pixel apron
+    for (int i = threadIdx.x; i < (t.h + 6) * sw; i += 256) {
+        const int r = i / sw, c = i % sw, y = t.y0 + r - 3, x = t.x0 + c - 3;
+        const int lo = px(d, P.dstride, P.W, P.H, y, x) - avg, hi = px(d, P.dstride, P.W, P.H, y, x + 1) - avg;
+        D2[r * ST_W + c] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16);
     }
-    for (int i = threadIdx.x; i < t.h * t.w; i += 256)
-        S[(i / t.w) * 64 + i % t.w] = (int)s[(size_t)(t.y0 + i / t.w) * a.sstride + t.x0 + i % t.w] - avg;
+    for (int i = threadIdx.x; i < t.h * hw2; i += 256) {
+        const int r = i / hw2, j = 2 * (i % hw2);
+        const T  *sp = s + (size_t)(t.y0 + r) * P.sstride + t.x0 + j;
+        const int lo = (int)sp[0] - avg, hi = j + 1 < t.w ? (int)sp[1] - avg : 0;
+        S2[r * 32 + (j >> 1)] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16);
+    }
     __syncthreads();
-    const int half = win >> 1, npair = win * (win + 1) / 2, njob = npair + 1;
-    const int job = threadIdx.x >> 3, g = threadIdx.x & 7;
-    long long *out = part + (size_t)blockIdx.x * (size_t)njob * 49;
-    int        acc[49];
+    const int tid = threadIdx.x, o = 3 - C::HALF, items = t.h * hw2;
+    int       acc[ST_SLOTS];
 #pragma unroll
-    for (int k = 0; k < 49; k++) acc[k] = 0;
-    if (job < npair) {
-        int c1 = 0, rem = job; // job -> (c1, c2), c1 <= c2
-        while (rem >= win - c1) rem -= win - c1, c1++;
-        const int c2 = c1 + rem;
-        for (int p = g; p < t.w * t.h; p += 8) {
-            const int i = p / t.w, j = p % t.w;
-            int       y1[7], y2[7];
+    for (int k = 0; k < ST_SLOTS; k++) acc[k] = 0;
+    if (tid < C::OFF_THR) {
+        const int q = tid / C::LO;
+        if (q < C::NOFF) {
+            int c1, c2;
+            off_pair(WIN, q, &c1, &c2);
+            for (int it = tid % C::LO; it < items; it += C::LO) {
+                const int       i = it / hw2, j = 2 * (it - i * hw2);
+                const uint32_t  m = j + 1 < t.w ? 0xFFFFFFFFu : 0xFFFFu; // odd-width tail: drop the phantom pixel
+                const uint32_t *b = D2 + (i + o) * ST_W + j + o;
+                uint32_t        y1[WIN], y2[WIN];
 #pragma unroll
-            for (int r = 0; r < 7; r++)
-                if (r < win) {
-                    y1[r] = D[(i + 3 + r - half) * ST_W + j + 3 + c1 - half];
-                    y2[r] = D[(i + 3 + r - half) * ST_W + j + 3 + c2 - half];
-                }
+                for (int r = 0; r < WIN; r++) y1[r] = b[r * ST_W + c1] & m, y2[r] = b[r * ST_W + c2];
 #pragma unroll
-            for (int r1 = 0; r1 < 7; r1++)
+                for (int r1 = 0; r1 < WIN; r1++)
 #pragma unroll
-                for (int r2 = 0; r2 < 7; r2++)
-                    if (r1 < win && r2 < win) acc[r1 * 7 + r2] += y1[r1] * y2[r2];
+                    for (int r2 = 0; r2 < WIN; r2++) acc[r1 * 7 + r2] = dot2(y1[r1], y2[r2], acc[r1 * 7 + r2]);
+            }
         }
-    } else if (job == npair) { // M: y_k * x with k = c * win + r
-        for (int p = g; p < t.w * t.h; p += 8) {
-            const int i = p / t.w, j = p % t.w, x = S[i * 64 + j];
+    } else {
+        const int c = (tid - C::OFF_THR) / C::LD;
+        if (c < WIN) {
+            for (int it = (tid - C::OFF_THR) % C::LD; it < items; it += C::LD) {
+                const int       i = it / hw2, j = 2 * (it - i * hw2);
+                const uint32_t  m = j + 1 < t.w ? 0xFFFFFFFFu : 0xFFFFu;
+                const uint32_t *b = D2 + (i + o) * ST_W + j + o;
+                const uint32_t  x = S2[i * 32 + (j >> 1)];
+                uint32_t        y[WIN];
 #pragma unroll
-            for (int c = 0; c < 7; c++)
+                for (int r = 0; r < WIN; r++) y[r] = b[r * ST_W + c] & m;
 #pragma unroll
-                for (int r = 0; r < 7; r++)
-                    if (c < win && r < win) acc[c * 7 + r] += D[(i + 3 + r - half) * ST_W + j + 3 + c - half] * x;
+                for (int r1 = 0; r1 < WIN; r1++) {
+#pragma unroll
+                    for (int r2 = r1; r2 < WIN; r2++) acc[r1 * 7 + r2] = dot2(y[r1], y[r2], acc[r1 * 7 + r2]);
+                    acc[49 + r1] = dot2(y[r1], x, acc[49 + r1]);
+                }
+            }
         }
     }
-    if (job <= npair) {
+    __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 49; k++) {
-            long long v = acc[k];
-            v += __shfl_xor(v, 1, 64);
-            v += __shfl_xor(v, 2, 64);
-            v += __shfl_xor(v, 4, 64);
-            if (g == 0) out[job * 49 + k] = v;
+    for (int k = 0; k < ST_SLOTS; k++) lds[k * 256 + tid] = acc[k];
+    __syncthreads();
+    long long *out = part + (size_t)blockIdx.x * NVAL;
+    for (int oi = tid; oi < NVAL; oi += 256) {
+        const int pair = oi / 49, k = oi % 49, r1 = k / 7, r2 = k % 7;
+        int       lane0 = 0, nl = 0, slot = 0;
+        if (r1 < WIN && r2 < WIN) {
+            if (pair < C::NPAIR) {
+                int c1 = 0, rem = pair; // pair -> (c1, c2), c1 <= c2
+                while (rem >= WIN - c1) rem -= WIN - c1, c1++;
+                const int c2 = c1 + rem;
+                if (c1 == c2) {
+                    lane0 = C::OFF_THR + c1 * C::LD, nl = C::LD, slot = min(r1, r2) * 7 + max(r1, r2);
+                } else {
+                    const int q = c1 * (2 * WIN - c1 - 1) / 2 + (c2 - c1 - 1);
+                    lane0 = q * C::LO, nl = C::LO, slot = k;
+                }
+            } else { // M: k = c * 7 + r
+                lane0 = C::OFF_THR + r1 * C::LD, nl = C::LD, slot = 49 + r2;
+            }
         }
+        long long v = 0;
+        for (int l = 0; l < nl; l++) v += lds[slot * 256 + lane0 + l];
+        out[oi] = v;
     }
 }
 
 // per unit: sum the tile partials (tiles of a unit are contiguous in the tile list)
-__global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_tile0, int nvals, long long *out) {
-    const int u = blockIdx.x, t0 = unit_tile0[u], t1 = unit_tile0[u + 1];
+__global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_tile0, int tile_begin, int nvals,
+                                    long long *out) {
+    const int u = blockIdx.x, t0 = unit_tile0[u] - tile_begin, t1 = unit_tile0[u + 1] - tile_begin;
     for (int k = threadIdx.x; k < nvals; k += blockDim.x) {
         long long s = 0;
         for (int t = t0; t < t1; t++) s += part[(size_t)t * nvals + k];
@@ -159,202 +229,261 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wiener trial: SSE of each active unit filtered with its candidate taps (hfilter[8], vfilter[8])
+// Wiener trial: SSE of a unit's tiles filtered with the unit's candidate taps (hfilter[8], vfilter[8]);
+// items[] lists the tiles of the units with a pending candidate, cnt[0] their number
 // ---------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void wiener_trial_kernel(const PlaneArgs a, const int16_t *taps,
-                                                           const int32_t *active, unsigned long long *err) {
+__global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
+                                                           const int32_t *items, const int32_t *cnt,
+                                                           int32_t *cnt_next, unsigned long long *err) {
     __shared__ uint16_t v[(64 + 7) * (64 + 8)];
     __shared__ uint16_t tmp[(64 + 7) * 64];
-    const Tile t = a.tiles[blockIdx.x];
-    if (!active[t.unit]) return;
-    const T  *d = (const T *)a.dgd, *s = (const T *)a.src;
-    const int vs = 64 + 8;
-    for (int i = threadIdx.x; i < (t.h + 7) * (t.w + 8); i += 256) {
-        const int r = i / (t.w + 8), c = i % (t.w + 8);
-        v[r * vs + c] = (uint16_t)px(d, a.dstride, a.W, a.H, t.y0 + r - 3, t.x0 + c - 3);
-    }
-    __syncthreads();
-    const int16_t *hf = taps + t.unit * 16, *vf = hf + 8;
-    const WienerRound rr  = wiener_round(a.bd);
-    const int         lim = (1 << (a.bd + 1 + 7 - rr.r0)) - 1;
-    for (int i = threadIdx.x; i < (t.h + 7) * t.w; i += 256) {
-        const int       y = i / t.w, x = i % t.w;
-        const uint16_t *p = v + y * vs + x;
-        int             sum = ((int)p[3] << 7) + (1 << (a.bd + 6));
+    const int n = cnt[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0; // the next advance counts there
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+        const Tile       t = A.tiles[items[it]];
+        const PlaneArgs &P = A.pl[t.plane];
+        const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+        const int        vs = 64 + 8;
+        __syncthreads(); // LDS reuse across items
+        for (int i = threadIdx.x; i < (t.h + 7) * (t.w + 8); i += 256) {
+            const int r = i / (t.w + 8), c = i % (t.w + 8);
+            v[r * vs + c] = (uint16_t)px(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 + c - 3);
+        }
+        __syncthreads();
+        int hf[8], vf[8]; // registers: the LDS stores below could alias a generic pointer
 #pragma unroll
-        for (int k = 0; k < 8; k++) sum += (int)p[k] * hf[k];
-        tmp[y * 64 + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
-    }
-    __syncthreads();
-    unsigned long long e = 0;
-    const int          maxv = (1 << a.bd) - 1;
-    for (int i = threadIdx.x; i < t.h * t.w; i += 256) {
-        const int       y = i / t.w, x = i % t.w;
-        const uint16_t *c = tmp + y * 64 + x;
-        int             sum = ((int)c[3 * 64] << 7) - (1 << (a.bd + rr.r1 - 1));
+        for (int k = 0; k < 8; k++) hf[k] = taps[t.unit * 16 + k], vf[k] = taps[t.unit * 16 + 8 + k];
+        const WienerRound rr = wiener_round(P.bd);
+        const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1;
+        for (int i = threadIdx.x; i < (t.h + 7) * t.w; i += 256) {
+            const int       y = i / t.w, x = i % t.w;
+            const uint16_t *p = v + y * vs + x;
+            int             sum = ((int)p[3] << 7) + (1 << (P.bd + 6));
 #pragma unroll
-        for (int k = 0; k < 8; k++) sum += (int)c[k * 64] * vf[k];
-        const int o  = min(max((sum + (1 << (rr.r1 - 1))) >> rr.r1, 0), maxv);
-        const int dd = o - (int)s[(size_t)(t.y0 + y) * a.sstride + t.x0 + x];
-        e += (unsigned long long)(dd * dd);
+            for (int k = 0; k < 8; k++) sum += (int)p[k] * hf[k];
+            tmp[y * 64 + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
+        }
+        __syncthreads();
+        unsigned long long e    = 0;
+        const int          maxv = (1 << P.bd) - 1;
+        for (int i = threadIdx.x; i < t.h * t.w; i += 256) {
+            const int       y = i / t.w, x = i % t.w;
+            const uint16_t *c = tmp + y * 64 + x;
+            int             sum = ((int)c[3 * 64] << 7) - (1 << (P.bd + rr.r1 - 1));
+#pragma unroll
+            for (int k = 0; k < 8; k++) sum += (int)c[k * 64] * vf[k];
+            const int o  = min(max((sum + (1 << (rr.r1 - 1))) >> rr.r1, 0), maxv);
+            const int dd = o - (int)s[(size_t)(t.y0 + y) * P.sstride + t.x0 + x];
+            e += (unsigned long long)(dd * dd);
+        }
+        e = wave_sum(e);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
     }
-    e = wave_sum(e);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
 }
 
 // ---------------------------------------------------------------------------------------------
-// self-guided: flt0/flt1 of every searched ep, stored as int16, plus the projection moments
-// mom[unit][ep] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} with u = x<<4, s = (src<<4) - u, g = flt - u
+// self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
+// registers; per ep the A/B maps (packed B << 9 | A) go to LDS, the filters to HBM, and the projection moments
+// mom[pair] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} (u = x<<4, s = (src<<4) - u, g = flt - u) to int64 atomics.
 // ---------------------------------------------------------------------------------------------
+constexpr int SG_V = 70, SG_B = 66, SG_NT = 512, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
 template <typename T>
-__global__ __launch_bounds__(256) void sgr_flt_kernel(const PlaneArgs a, const int32_t *eps, int16_t *flt,
-                                                      long long *mom, int nep_all) {
-    __shared__ uint16_t v[(64 + 6) * (64 + 6)];
-    __shared__ int      AB[2][66 * 66];
-    const Tile t   = a.tiles[blockIdx.x];
-    const int  ei  = blockIdx.y, ep = eps[ei];
-    const T   *d = (const T *)a.dgd, *s = (const T *)a.src;
-    const int  vs = 64 + 6, bw = t.w + 2;
-    for (int i = threadIdx.x; i < (t.h + 6) * (t.w + 6); i += 256) {
+__global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long long *mom) {
+    __shared__ uint16_t v[SG_V * SG_V];
+    __shared__ int      ab1[SG_B * SG_B], ab2[SG_B * SG_B];
+    __shared__ int      xby[256];
+    const Tile       t = A.tiles[blockIdx.x];
+    const PlaneArgs &P = A.pl[t.plane];
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    for (int i = threadIdx.x; i < (t.h + 6) * (t.w + 6); i += SG_NT) {
         const int r = i / (t.w + 6), c = i % (t.w + 6);
-        v[r * vs + c] = (uint16_t)px(d, a.dstride, a.W, a.H, t.y0 + r - 3, t.x0 + c - 3);
+        v[r * SG_V + c] = (uint16_t)px(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 + c - 3);
     }
+    if (threadIdx.x < 256) xby[threadIdx.x] = c_x_by_xplus1[threadIdx.x];
     __syncthreads();
-    const uint16_t *v0  = v + 3 * vs + 3;
-    const size_t    pn  = (size_t)a.W * a.H;
-    int16_t        *f0g = flt + (size_t)ei * 2 * pn, *f1g = f0g + pn;
-    const int       r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-    constexpr int   PX = 64 * 64 / 256;
-    int             f[2][PX]; // pixel k of this lane: threadIdx.x + k * 256
-    for (int pass = 0; pass < 2; pass++) {
-        const int r = pass ? r1 : r0;
-        if (!r) continue;
-        for (int i = threadIdx.x; i < (t.h + 2) * bw; i += 256) {
-            const int y = i / bw - 1, x = i % bw - 1;
-            if (r == 2 && !(y & 1)) continue;
-            sgr_ab(v0, vs, y, x, r, c_sgr_s[ep][pass], a.bd, &AB[0][i], &AB[1][i]);
-        }
-        __syncthreads();
+    const uint16_t *v0 = v + 3 * SG_V + 3;
+    const int       bw = t.w + 2, nq = (t.h + 2) * bw, npx = t.w * t.h;
+    int             s1[SG_NQ], q1[SG_NQ], s2[SG_NQ], q2[SG_NQ];
 #pragma unroll
-        for (int k = 0; k < PX; k++) {
-            const int i = threadIdx.x + k * 256;
-            if (i >= t.w * t.h) break;
-            const int  y = i / t.w, x = i % t.w;
-            const int *A = AB[0] + (y + 1) * bw + x + 1, *B = AB[1] + (y + 1) * bw + x + 1;
-            int        aa, bb, nb;
-            if (r == 1) {
-                aa = (A[0] + A[-1] + A[1] + A[-bw] + A[bw]) * 4 + (A[-bw - 1] + A[bw - 1] + A[-bw + 1] + A[bw + 1]) * 3;
-                bb = (B[0] + B[-1] + B[1] + B[-bw] + B[bw]) * 4 + (B[-bw - 1] + B[bw - 1] + B[-bw + 1] + B[bw + 1]) * 3;
-                nb = 5;
-            } else if (!(y & 1)) {
-                aa = (A[-bw] + A[bw]) * 6 + (A[-bw - 1] + A[bw - 1] + A[-bw + 1] + A[bw + 1]) * 5;
-                bb = (B[-bw] + B[bw]) * 6 + (B[-bw - 1] + B[bw - 1] + B[-bw + 1] + B[bw + 1]) * 5;
-                nb = 5;
-            } else {
-                aa = A[0] * 6 + (A[-1] + A[1]) * 5;
-                bb = B[0] * 6 + (B[-1] + B[1]) * 5;
-                nb = 4;
+    for (int k = 0; k < SG_NQ; k++) {
+        const int q = threadIdx.x + k * SG_NT;
+        s1[k] = q1[k] = s2[k] = q2[k] = 0;
+        if (q < nq) {
+            const int y = q / bw - 1, x = q % bw - 1;
+#pragma unroll
+            for (int dy = -2; dy <= 2; dy++)
+#pragma unroll
+                for (int dx = -2; dx <= 2; dx++) {
+                    const int p = v0[(y + dy) * SG_V + x + dx];
+                    s2[k] += p, q2[k] += p * p;
+                    if (dy >= -1 && dy <= 1 && dx >= -1 && dx <= 1) s1[k] += p, q1[k] += p * p;
+                }
+        }
+    }
+    int pix[SG_NP], sv[SG_NP]; // this lane's pixels: threadIdx.x + k * SG_NT
+#pragma unroll
+    for (int k = 0; k < SG_NP; k++) {
+        const int i = threadIdx.x + k * SG_NT;
+        pix[k] = sv[k] = 0;
+        if (i < npx) {
+            const int y = i / t.w, x = i % t.w;
+            pix[k]      = v0[y * SG_V + x];
+            sv[k]       = ((int)s[(size_t)(t.y0 + y) * P.sstride + t.x0 + x] << 4) - (pix[k] << 4);
+        }
+    }
+    const size_t pn = (size_t)P.W * P.H;
+    for (int e = 0; e < P.ne; e++) {
+        const int ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+#pragma unroll
+        for (int k = 0; k < SG_NQ; k++) {
+            const int q = threadIdx.x + k * SG_NT;
+            if (q >= nq) break;
+            int a, b;
+            if (r1) {
+                sgr_ab_from_sums(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
+                ab1[q] = (b << 9) | a;
             }
-            const int sh = 8 + nb - 4;
-            f[pass][k]   = (aa * (int)v0[y * vs + x] + bb + (1 << (sh - 1))) >> sh;
-            (pass ? f1g : f0g)[(size_t)(t.y0 + y) * a.W + t.x0 + x] = (int16_t)f[pass][k];
+            if (r0 && ((q / bw - 1) & 1)) {
+                sgr_ab_from_sums(s2[k], q2[k], 25, c_sgr_s[ep][0], P.bd, xby, &a, &b);
+                ab2[q] = (b << 9) | a;
+            }
         }
         __syncthreads();
-    }
-    // projection moments from the lane's own filter values
-    long long m[5] = {0, 0, 0, 0, 0};
+        int16_t  *f0g = P.flt + (size_t)e * 2 * pn, *f1g = f0g + pn;
+        long long m[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < PX; k++) {
-        const int i = threadIdx.x + k * 256;
-        if (i >= t.w * t.h) break;
-        const int y = i / t.w, x = i % t.w;
-        const int u  = (int)v0[y * vs + x] << 4;
-        const int sv = ((int)s[(size_t)(t.y0 + y) * a.sstride + t.x0 + x] << 4) - u;
-        const int g1 = r0 > 0 ? f[0][k] - u : 0, g2 = r1 > 0 ? f[1][k] - u : 0;
-        m[0] += (long long)g1 * g1;
-        m[1] += (long long)g2 * g2;
-        m[2] += (long long)g1 * g2;
-        m[3] += (long long)g1 * sv;
-        m[4] += (long long)g2 * sv;
-    }
+        for (int k = 0; k < SG_NP; k++) {
+            const int i = threadIdx.x + k * SG_NT;
+            if (i >= npx) break;
+            const int    y = i / t.w, x = i % t.w, c = (y + 1) * bw + x + 1, u = pix[k] << 4;
+            const size_t o = (size_t)(t.y0 + y) * P.W + t.x0 + x;
+            int          g1 = 0, g2 = 0;
+            if (r0) {
+                const int *Q = ab2 + c;
+                int        aa, bb, sh;
+                if (!(y & 1)) {
+                    const int c6 = Q[-bw] + Q[bw], c5 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
+                    const int a6 = (Q[-bw] & 511) + (Q[bw] & 511);
+                    const int a5 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
+                    aa = a6 * 6 + a5 * 5;
+                    bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5;
+                    sh = 9;
+                } else {
+                    const int a6 = Q[0] & 511, a5 = (Q[-1] & 511) + (Q[1] & 511);
+                    aa = a6 * 6 + a5 * 5;
+                    bb = (Q[0] >> 9) * 6 + ((Q[-1] >> 9) + (Q[1] >> 9)) * 5;
+                    sh = 8;
+                }
+                const int f = (aa * pix[k] + bb + (1 << (sh - 1))) >> sh;
+                f0g[o]      = (int16_t)f;
+                g1          = f - u;
+            }
+            if (r1) {
+                const int *Q  = ab1 + c;
+                const int  a4 = (Q[0] & 511) + (Q[-1] & 511) + (Q[1] & 511) + (Q[-bw] & 511) + (Q[bw] & 511);
+                const int  a3 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
+                const int  b4 = (Q[0] >> 9) + (Q[-1] >> 9) + (Q[1] >> 9) + (Q[-bw] >> 9) + (Q[bw] >> 9);
+                const int  b3 = (Q[-bw - 1] >> 9) + (Q[bw - 1] >> 9) + (Q[-bw + 1] >> 9) + (Q[bw + 1] >> 9);
+                const int  f  = ((a4 * 4 + a3 * 3) * pix[k] + b4 * 4 + b3 * 3 + (1 << 8)) >> 9;
+                f1g[o]        = (int16_t)f;
+                g2            = f - u;
+            }
+            m[0] += (long long)g1 * g1;
+            m[1] += (long long)g2 * g2;
+            m[2] += (long long)g1 * g2;
+            m[3] += (long long)g1 * sv[k];
+            m[4] += (long long)g2 * sv[k];
+        }
+        const int pair = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        const unsigned long long w = wave_sum((unsigned long long)m[k]);
-        if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&mom[((size_t)t.unit * nep_all + ei) * 5 + k], w);
+        for (int k = 0; k < 5; k++) {
+            const unsigned long long w = wave_sum((unsigned long long)m[k]);
+            if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&mom[(size_t)pair * 5 + k], w);
+        }
+        __syncthreads(); // the next ep rewrites the A/B maps
     }
 }
 
-// projection error of candidate xq[unit][ep] = {xq0, xq1, active}
+// projection error of the pending candidate of every listed (tile, ep): items[] = tile * 16 + ep index
 template <typename T>
-__global__ __launch_bounds__(256) void proj_err_kernel(const PlaneArgs a, const int32_t *eps, const int16_t *flt,
-                                                       const int32_t *cand, unsigned long long *err, int nep_all) {
-    const Tile t  = a.tiles[blockIdx.x];
-    const int  ei = blockIdx.y, ep = eps[ei];
-    const int *c  = cand + ((size_t)t.unit * nep_all + ei) * 3;
-    if (!c[2]) return;
-    const int      xq0 = c[0], xq1 = c[1], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-    const T       *d = (const T *)a.dgd, *s = (const T *)a.src;
-    const size_t   pn = (size_t)a.W * a.H;
-    const int16_t *f0 = flt + (size_t)ei * 2 * pn, *f1 = f0 + pn;
-    unsigned long long e = 0;
-    for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
-        const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-        const size_t o = (size_t)y * a.W + x;
-        const int    dv = d[(size_t)y * a.dstride + x], sv = s[(size_t)y * a.sstride + x];
-        const int    u = dv << 4;
-        int          v = 1 << 10;
-        if (r0 > 0) v += xq0 * (f0[o] - u);
-        if (r1 > 0) v += xq1 * (f1[o] - u);
-        const int ee = (v >> 11) + dv - sv;
-        e += (unsigned long long)((long long)ee * ee);
+__global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
+                                                       int32_t *cnt_next, const int32_t *cand, unsigned long long *err) {
+    const int n = cnt[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+        const int        item = items[it], e = item & 15;
+        const Tile       t = A.tiles[item >> 4];
+        const PlaneArgs &P = A.pl[t.plane];
+        const int        ep = P.eps[e], pair = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
+        const int        xq0 = cand[2 * pair], xq1 = cand[2 * pair + 1], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+        const size_t     pn = (size_t)P.W * P.H;
+        const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+        unsigned long long acc = 0;
+        for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
+            const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
+            const size_t o = (size_t)y * P.W + x;
+            const int    dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
+            const int    u = dv << 4;
+            int          v = 1 << 10;
+            if (r0 > 0) v += xq0 * (f0[o] - u);
+            if (r1 > 0) v += xq1 * (f1[o] - u);
+            const int ee = (v >> 11) + dv - sv;
+            acc += (unsigned long long)((long long)ee * ee);
+        }
+        acc = wave_sum(acc);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&err[pair], acc);
     }
-    e = wave_sum(e);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&err[(size_t)t.unit * nep_all + ei], e);
 }
 
 // SSE of the chosen self-guided output (apply_selfguided_restoration: projection, int16 wrap, clip)
 template <typename T>
-__global__ __launch_bounds__(256) void sgr_sse_kernel(const PlaneArgs a, const int16_t *flt, const int32_t *best,
-                                                      unsigned long long *err) {
-    const Tile t  = a.tiles[blockIdx.x];
-    const int *b  = best + t.unit * 4; // {ep index, ep, xq0, xq1}
-    const int  ei = b[0], ep = b[1], xq0 = b[2], xq1 = b[3], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-    const T   *d = (const T *)a.dgd, *s = (const T *)a.src;
-    const size_t   pn = (size_t)a.W * a.H;
-    const int16_t *f0 = flt + (size_t)ei * 2 * pn, *f1 = f0 + pn;
-    const int      maxv = (1 << a.bd) - 1;
-    unsigned long long e = 0;
+__global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const int32_t *best, unsigned long long *err) {
+    const Tile       t = A.tiles[blockIdx.x];
+    const PlaneArgs &P = A.pl[t.plane];
+    const int       *b = best + t.unit * 4; // {ep index, ep, xq0, xq1}
+    const int        e = b[0], ep = b[1], xq0 = b[2], xq1 = b[3], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    const size_t     pn = (size_t)P.W * P.H;
+    const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+    const int        maxv = (1 << P.bd) - 1;
+    unsigned long long acc = 0;
     for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
         const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-        const size_t o = (size_t)y * a.W + x;
-        const int    dv = d[(size_t)y * a.dstride + x], sv = s[(size_t)y * a.sstride + x];
+        const size_t o = (size_t)y * P.W + x;
+        const int    dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
         const int    u = dv << 4;
         int          v = u << 7;
         if (r0 > 0) v += xq0 * (f0[o] - u);
         if (r1 > 0) v += xq1 * (f1[o] - u);
         const int16_t w  = (int16_t)((v + (1 << 10)) >> 11);
         const int     ov = min(max((int)w, 0), maxv);
-        e += (unsigned long long)((ov - sv) * (ov - sv));
+        acc += (unsigned long long)((ov - sv) * (ov - sv));
     }
-    e = wave_sum(e);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], acc);
 }
 
 // =============================================================================================
-// host: the reference's sequential logic
+// the reference's sequential logic (host), and the coordinate descent (host and device)
 // =============================================================================================
 constexpr int64_t TAP_SCALE = (int64_t)1 << 16;
 constexpr int     FILT_STEP = 128;
 
-int wrap_index(int i, int win) { return i >= (win >> 1) + 1 ? win - 1 - i : i; }
+__host__ __device__ inline int wrap_index(int i, int win) { return i >= (win >> 1) + 1 ? win - 1 - i : i; }
+__host__ __device__ inline int64_t abs64(int64_t v) { return v < 0 ? -v : v; }
 
-int linsolve_wiener(int n, int64_t *A, int stride, int64_t *b, int32_t *x) { // EbRestorationPick.c:766-803
+__device__ int linsolve_wiener(int n, int64_t *A, int stride, int64_t *b, int32_t *x) { // EbRestorationPick.c:766-803
     for (int k = 0; k < n - 1; k++) {
         for (int i = n - 1; i > k; i--)
-            if (std::llabs(A[(i - 1) * stride + k]) < std::llabs(A[i * stride + k])) {
-                for (int j = 0; j < n; j++) std::swap(A[i * stride + j], A[(i - 1) * stride + j]);
-                std::swap(b[i], b[i - 1]);
+            if (abs64(A[(i - 1) * stride + k]) < abs64(A[i * stride + k])) {
+                for (int j = 0; j < n; j++) {
+                    const int64_t t = A[i * stride + j];
+                    A[i * stride + j] = A[(i - 1) * stride + j], A[(i - 1) * stride + j] = t;
+                }
+                const int64_t t = b[i];
+                b[i] = b[i - 1], b[i - 1] = t;
             }
         for (int i = k; i < n - 1; i++) {
             if (A[k * stride + k] == 0) return 0;
@@ -372,52 +501,72 @@ int linsolve_wiener(int n, int64_t *A, int stride, int64_t *b, int32_t *x) { // 
     return 1;
 }
 
-// update_a_sep_sym (solve_a) / update_b_sep_sym (EbRestorationPick.c:805-904); H viewed as hc[r][c]
-void update_sep_sym(bool solve_b, int win, const int64_t *M, const int64_t *H, int32_t *a, int32_t *b) {
-    const int win2 = win * win, h1 = (win >> 1) + 1;
-    int64_t   A[4] = {0, 0, 0, 0}, B[16] = {0};
-    int32_t   S[7];
-    auto      hc = [&](int r, int c) { return H[(r / win) * win * win2 + (r % win) * win + c]; };
-    if (!solve_b) {
-        for (int i = 0; i < win; i++)
-            for (int j = 0; j < win; j++) A[wrap_index(j, win)] += M[i * win + j] * b[i] / TAP_SCALE;
-        for (int i = 0; i < win; i++)
-            for (int j = 0; j < win; j++)
-                for (int k = 0; k < win; k++)
-                    for (int l = 0; l < win; l++)
-                        B[wrap_index(l, win) * h1 + wrap_index(k, win)] +=
-                            hc(j * win + i, k * win2 + l) * b[i] / TAP_SCALE * b[j] / TAP_SCALE;
-    } else {
-        for (int i = 0; i < win; i++)
-            for (int j = 0; j < win; j++) A[wrap_index(i, win)] += M[i * win + j] * a[j] / TAP_SCALE;
-        for (int i = 0; i < win; i++)
-            for (int j = 0; j < win; j++)
-                for (int k = 0; k < win; k++)
-                    for (int l = 0; l < win; l++)
-                        B[wrap_index(j, win) * h1 + wrap_index(i, win)] +=
-                            hc(i * win + j, k * win2 + l) * a[k] / TAP_SCALE * a[l] / TAP_SCALE;
+// Shared-memory workspace of the per-unit Wiener decomposition (one workgroup per unit)
+struct WienerSolveLds {
+    int64_t M[49], H[49 * 49];
+    int64_t accA[4], accB[16], accP, accQ;
+    int32_t a[7], b[7], ab[49];
+};
+
+// update_a_sep_sym (solve_b = false) / update_b_sep_sym (EbRestorationPick.c:805-904), H viewed as hc[r][c].
+// Every term of the reference's A / B sums is formed exactly as the reference forms it; the integer sums are
+// split over the lanes (5 lanes per B cell) and combined with LDS atomics, which is exact.
+__device__ void update_sep_sym(bool solve_b, int win, WienerSolveLds &L) {
+    const int win2 = win * win, h1 = (win >> 1) + 1, tid = threadIdx.x;
+    if (tid < 16) L.accB[tid] = 0;
+    if (tid < 4) L.accA[tid] = 0;
+    __syncthreads();
+    auto hc = [&](int r, int c) { return L.H[(r / win) * win * win2 + (r % win) * win + c]; };
+    if (tid < win2) {
+        const int     i = tid / win, j = tid % win;
+        const int64_t t = solve_b ? L.M[i * win + j] * L.a[j] / TAP_SCALE : L.M[i * win + j] * L.b[i] / TAP_SCALE;
+        atomicAdd((unsigned long long *)&L.accA[solve_b ? wrap_index(i, win) : wrap_index(j, win)], (unsigned long long)t);
     }
-    const int64_t last = A[h1 - 1];
-    for (int i = 0; i < h1 - 1; i++) A[i] -= last * 2 + B[i * h1 + h1 - 1] - 2 * B[(h1 - 1) * h1 + (h1 - 1)];
-    for (int i = 0; i < h1 - 1; i++)
-        for (int j = 0; j < h1 - 1; j++)
-            B[i * h1 + j] -= 2 * (B[i * h1 + (h1 - 1)] + B[(h1 - 1) * h1 + j] - 2 * B[(h1 - 1) * h1 + (h1 - 1)]);
-    if (linsolve_wiener(h1 - 1, B, h1, A, S)) {
-        S[h1 - 1] = (int32_t)TAP_SCALE;
-        for (int i = h1; i < win; i++) {
-            S[i] = S[win - 1 - i];
-            S[h1 - 1] -= 2 * S[i];
+    constexpr int SL = 5;
+    const int     cell = tid / SL;
+    if (cell < win2) {
+        const int c0 = cell / win, c1 = cell % win;
+        int64_t   sum = 0;
+        for (int q = tid % SL; q < win2; q += SL) {
+            const int o0 = q / win, o1 = q % win;
+            if (!solve_b) // cell (k, l), terms over (i, j)
+                sum += hc(o1 * win + o0, c0 * win2 + c1) * L.b[o0] / TAP_SCALE * L.b[o1] / TAP_SCALE;
+            else // cell (i, j), terms over (k, l)
+                sum += hc(c0 * win + c1, o0 * win2 + o1) * L.a[o0] / TAP_SCALE * L.a[o1] / TAP_SCALE;
         }
-        std::memcpy(solve_b ? b : a, S, win * sizeof(int32_t));
+        const int idx = wrap_index(c1, win) * h1 + wrap_index(c0, win); // (l, k) resp. (j, i)
+        atomicAdd((unsigned long long *)&L.accB[idx], (unsigned long long)sum);
     }
+    __syncthreads();
+    if (tid == 0) {
+        int64_t *A = L.accA, *B = L.accB;
+        int32_t  S[7];
+        const int64_t last = A[h1 - 1];
+        for (int i = 0; i < h1 - 1; i++) A[i] -= last * 2 + B[i * h1 + h1 - 1] - 2 * B[(h1 - 1) * h1 + (h1 - 1)];
+        for (int i = 0; i < h1 - 1; i++)
+            for (int j = 0; j < h1 - 1; j++)
+                B[i * h1 + j] -= 2 * (B[i * h1 + (h1 - 1)] + B[(h1 - 1) * h1 + j] - 2 * B[(h1 - 1) * h1 + (h1 - 1)]);
+        if (linsolve_wiener(h1 - 1, B, h1, A, S)) {
+            S[h1 - 1] = (int32_t)TAP_SCALE;
+            for (int i = h1; i < win; i++) {
+                S[i] = S[win - 1 - i];
+                S[h1 - 1] -= 2 * S[i];
+            }
+            int32_t *dst = solve_b ? L.b : L.a;
+            for (int i = 0; i < win; i++) dst[i] = S[i];
+        }
+    }
+    __syncthreads();
 }
 
-void finalize_sym_filter(int win, const int32_t *f, int16_t *fi) { // EbRestorationPick.c:977-1006
+__constant__ int c_tap_min[3] = {-5, -23, -17}, c_tap_max[3] = {10, 8, 46};
+
+__device__ void finalize_sym_filter(int win, const int32_t *f, int16_t *fi) { // EbRestorationPick.c:977-1006
     for (int i = 0; i < (win >> 1); i++) {
         const int64_t n = (int64_t)f[i] * FILT_STEP;
         fi[i]           = (int16_t)(n < 0 ? (n - TAP_SCALE / 2) / TAP_SCALE : (n + TAP_SCALE / 2) / TAP_SCALE);
     }
-    auto clip = [](int v, int t) { return (int16_t)std::min(std::max(v, kTapMin[t]), kTapMax[t]); };
+    auto clip = [](int v, int t) { return (int16_t)min(max(v, c_tap_min[t]), c_tap_max[t]); };
     if (win == 7) {
         fi[0] = clip(fi[0], 0), fi[1] = clip(fi[1], 1), fi[2] = clip(fi[2], 2);
     } else {
@@ -428,25 +577,32 @@ void finalize_sym_filter(int win, const int32_t *f, int16_t *fi) { // EbRestorat
     fi[7] = 0;
 }
 
-int64_t compute_score(int win, const int64_t *M, const int64_t *H, const int16_t *vf, const int16_t *hf) {
-    int32_t   ab[49];
-    int16_t   a[7], b[7];
-    const int off = (7 - win) >> 1, win2 = win * win;
-    a[3] = b[3] = FILT_STEP;
-    for (int i = 0; i < 3; i++) {
-        a[i] = a[6 - i] = vf[i];
-        b[i] = b[6 - i] = hf[i];
-        a[3] -= 2 * a[i];
-        b[3] -= 2 * b[i];
+// compute_score (EbRestorationPick.c:1008-1040): the P and Q sums split over the lanes
+__device__ int64_t compute_score(int win, WienerSolveLds &L, const int16_t *vf, const int16_t *hf) {
+    const int off = (7 - win) >> 1, win2 = win * win, tid = threadIdx.x;
+    if (tid == 0) {
+        int16_t a[7], b[7];
+        a[3] = b[3] = FILT_STEP;
+        for (int i = 0; i < 3; i++) {
+            a[i] = a[6 - i] = vf[i];
+            b[i] = b[6 - i] = hf[i];
+            a[3] -= 2 * a[i];
+            b[3] -= 2 * b[i];
+        }
+        for (int k = 0; k < win; k++)
+            for (int l = 0; l < win; l++) L.ab[k * win + l] = a[l + off] * b[k + off];
+        L.accP = 0, L.accQ = 0;
     }
-    for (int k = 0; k < win; k++)
-        for (int l = 0; l < win; l++) ab[k * win + l] = a[l + off] * b[k + off];
-    int64_t P = 0, Q = 0;
-    for (int k = 0; k < win2; k++) {
-        P += ab[k] * M[k] / FILT_STEP / FILT_STEP;
-        for (int l = 0; l < win2; l++) Q += ab[k] * H[k * win2 + l] * ab[l] / FILT_STEP / FILT_STEP / FILT_STEP / FILT_STEP;
+    __syncthreads();
+    if (tid < win2) atomicAdd((unsigned long long *)&L.accP, (unsigned long long)(L.ab[tid] * L.M[tid] / FILT_STEP / FILT_STEP));
+    int64_t q = 0;
+    for (int t = tid; t < win2 * win2; t += blockDim.x) {
+        const int k = t / win2, l = t % win2;
+        q += L.ab[k] * L.H[k * win2 + l] * L.ab[l] / FILT_STEP / FILT_STEP / FILT_STEP / FILT_STEP;
     }
-    return (Q - 2 * P) - (H[(win2 >> 1) * win2 + (win2 >> 1)] - 2 * M[win2 >> 1]);
+    atomicAdd((unsigned long long *)&L.accQ, (unsigned long long)q);
+    __syncthreads();
+    return (L.accQ - 2 * L.accP) - (L.H[(win2 >> 1) * win2 + (win2 >> 1)] - 2 * L.M[win2 >> 1]);
 }
 
 // rates (EbEntropyCoding.c:2876-3022, EbRestorationPick.c:655-668, 1008-1040)
@@ -498,6 +654,7 @@ double rdcost(int rdmult, int64_t bits, int64_t sse) { // RDCOST_DBL (EbRestorat
 // finer_search_pixel_proj_error (:320-413): coordinates (f, p) move by -s then +s; at the first step size a
 // successful move is repeated; a successful downward move ends the p loop of its filter.
 struct Descent {
+    int32_t unit = 0, k = 0, ep = 0;                       // owner: global unit, ep index, ep (self-guided)
     int     start = 0, end = 1, nf = 1, p_lo = 0, p_hi = 0; // p in [p_lo, p_hi]
     bool    cont = true, skip_p[3] = {false, false, false};
     int     lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
@@ -507,9 +664,9 @@ struct Descent {
     bool    skip = false, init = true, done = false;
     int64_t err = 0;
     int     mf = 0, mp = 0, md = 0;              // pending move
-    void    begin() { s = start, f = 0, p = p_lo, phase = 0, skip = false, init = true, done = false; }
+    __host__ __device__ void begin() { s = start, f = 0, p = p_lo, phase = 0, skip = false, init = true, done = false; }
     // proposes the next candidate (val holds it) or sets done; returns true when a candidate is pending
-    bool next() {
+    __host__ __device__ bool next() {
         if (init) return true;
         for (;;) {
             if (s < end) {
@@ -549,7 +706,7 @@ struct Descent {
             p++, phase = 0, skip = false;
         }
     }
-    void report(int64_t e2) {
+    __host__ __device__ void report(int64_t e2) {
         if (init) {
             err = e2, init = false;
             return;
@@ -572,7 +729,7 @@ struct Descent {
     }
 };
 
-void set_wiener_taps(int16_t *t, const int *v) { // symmetric 7-tap from taps 0..2
+__host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // symmetric 7-tap from taps 0..2
     t[0] = t[6] = (int16_t)v[0];
     t[1] = t[5] = (int16_t)v[1];
     t[2] = t[4] = (int16_t)v[2];
@@ -580,340 +737,215 @@ void set_wiener_taps(int16_t *t, const int *v) { // symmetric 7-tap from taps 0.
     t[7] = 0;
 }
 
-struct DevBuf {
-    void  *p = nullptr;
-    size_t n = 0;
-    int    get(size_t bytes) {
-        if (bytes <= n) return SVTGPU_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr, n = 0;
-        HIP_TRY(hipMalloc(&p, bytes));
-        n = bytes;
-        return SVTGPU_OK;
+// ---------------------------------------------------------------------------------------------
+// device-side descent rounds, one lane per descent.  A descent that is not done holds one pending candidate
+// whose error the trial kernel accumulated in err[].  cnt[0] = listed items, cnt[1] = descents with a pending
+// candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
+// the other one, the advance kernel fills it).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, const int32_t *tile0,
+                                                             unsigned long long *err, int16_t *taps, int32_t *items,
+                                                             int32_t *cnt, int first) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    Descent d = ds[u];
+    if (d.done) return;
+    if (!first) d.report((int64_t)err[u]);
+    err[u] = 0;
+    if (d.next()) {
+        set_wiener_taps(taps + 16 * u, d.val[0]); // f = 0: hfilter, f = 1: vfilter
+        set_wiener_taps(taps + 16 * u + 8, d.val[1]);
+        const int t0 = tile0[u], nt = tile0[u + 1] - t0, pos = atomicAdd(&cnt[0], nt);
+        for (int i = 0; i < nt; i++) items[pos + i] = t0 + i;
+        atomicAdd(&cnt[1], 1);
     }
-    ~DevBuf() {
-        if (p) (void)hipFree(p);
-    }
-};
-
-} // namespace
-
-extern "C" int svtgpu_lr_controls_for_level(int32_t wn, int32_t sg, SvtGpuLrSearchControls *c) {
-    if (!c) return SVTGPU_ERR_INVALID_ARG;
-    std::memset(c, 0, sizeof *c);
-    // svt_aom_set_wn_filter_ctrls (EncModeConfig.c:1329-1384); level 6 reuses the previous frame's taps
-    if (wn < 0 || wn > 5 || sg < 0 || sg > 4) return SVTGPU_ERR_UNSUPPORTED;
-    if (wn > 0) {
-        c->wn_enabled                 = 1;
-        c->wn_use_chroma              = wn <= 4;
-        c->wn_filter_tap_lvl          = wn <= 2 ? 1 : 2;
-        c->wn_use_refinement          = wn <= 3;
-        c->wn_max_one_refinement_step = wn >= 2;
-    }
-    // svt_aom_set_sg_filter_ctrls (EncModeConfig.c:1386-1445), fixed-range search (step_range 16)
-    if (sg > 0) {
-        c->sg_enabled     = 1;
-        c->sg_use_chroma  = sg <= 3;
-        c->sg_start_ep[0] = 0, c->sg_end_ep[0] = 16, c->sg_ep_inc[0] = sg >= 3 ? 8 : 1;
-        c->sg_start_ep[1] = sg == 1 ? 0 : 4, c->sg_end_ep[1] = sg == 1 ? 16 : 5, c->sg_ep_inc[1] = 1;
-        c->sg_refine[0] = 1, c->sg_refine[1] = sg == 1;
-    }
-    return SVTGPU_OK;
+    ds[u] = d;
 }
 
-namespace {
-template <typename T>
-int search_plane(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *src, int p,
-                 const SvtGpuLrSearchControls *c, int *frame_type, SvtGpuLrUnitSearch *rec_out, hipStream_t st) {
-    const int W = rec->pw[p], H = rec->ph[p], bd = rec->bit_depth;
-    const int usz = s->unit_size[p], hu = s->hunits[p], vu = s->vunits[p], n = hu * vu;
-    const int ext = usz * 3 / 2, off = 8 >> (p > 0);
-    // units (foreach_rest_unit_in_tile, EbRestoration.c:1257-1294) and their <= 64x64 tiles
-    std::vector<URect>   units;
-    std::vector<Tile>    tiles;
-    std::vector<int32_t> tile0;
-    for (int y0 = 0; y0 < H;) {
-        const int uh = (H - y0 < ext) ? H - y0 : usz;
-        int       vs = std::max(0, y0 - off), ve = y0 + uh;
-        if (ve < H) ve -= off;
-        for (int x0 = 0; x0 < W;) {
-            const int uw = (W - x0 < ext) ? W - x0 : usz;
-            tile0.push_back((int)tiles.size());
-            for (int y = vs; y < ve; y += 64)
-                for (int x = x0; x < x0 + uw; x += 64)
-                    tiles.push_back({(int)units.size(), x, y, std::min(64, x0 + uw - x), std::min(64, ve - y)});
-            units.push_back({x0, x0 + uw, vs, ve});
-            x0 += uw;
-        }
-        y0 += uh;
+__global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
+                                                          unsigned long long *err, int32_t *cand, int32_t *items,
+                                                          int32_t *cnt, int first) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Descent d = ds[i];
+    if (d.done) return;
+    if (!first) d.report((int64_t)err[i]);
+    err[i] = 0;
+    if (d.next()) {
+        // svt_decode_xq (EbRestoration.c:634-646)
+        const int x0 = d.val[0][0], x1 = d.val[0][1], r0 = c_sgr_r[d.ep][0], r1 = c_sgr_r[d.ep][1];
+        cand[2 * i]     = r0 == 0 ? 0 : x0;
+        cand[2 * i + 1] = r0 == 0 ? 128 - x1 : r1 == 0 ? 0 : 128 - x0 - x1;
+        const int t0 = tile0[d.unit], nt = tile0[d.unit + 1] - t0, pos = atomicAdd(&cnt[0], nt);
+        for (int j = 0; j < nt; j++) items[pos + j] = (t0 + j) * 16 + d.k;
+        atomicAdd(&cnt[1], 1);
     }
-    tile0.push_back((int)tiles.size());
-    if ((int)units.size() != n) return SVTGPU_ERR_INVALID_ARG;
-    const int nt = (int)tiles.size();
-    // plane-sized scratch: tiles, units, accumulators, Wiener partials and candidates
-    const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
-    const int win = p == 0 ? win_l : std::min(win_l, 5), nval = (win * (win + 1) / 2 + 1) * 49;
-    std::vector<int32_t> eps;
-    const int q = p > 0;
-    if (c->sg_enabled && (!p || c->sg_use_chroma))
-        for (int e = c->sg_start_ep[q]; e < c->sg_end_ep[q]; e += std::max(1, c->sg_ep_inc[q])) eps.push_back(e);
-    const int ne = std::max(1, (int)eps.size());
-    size_t    off_b = 0;
-    auto      carve = [&](size_t bytes) {
-        const size_t o = off_b;
-        off_b += (bytes + 255) & ~(size_t)255;
-        return o;
-    };
-    const size_t o_tiles = carve(sizeof(Tile) * nt), o_units = carve(sizeof(URect) * n), o_t0 = carve(4 * (n + 1));
-    const size_t o_sum = carve(8 * n), o_sse = carve(8 * n), o_part = carve(8 * (size_t)nt * nval),
-                 o_mh = carve(8 * (size_t)n * nval), o_taps = carve(2 * 16 * (size_t)n), o_act = carve(4 * (size_t)n),
-                 o_err = carve(8 * (size_t)n * ne), o_eps = carve(4 * ne), o_mom = carve(8 * 5 * (size_t)n * ne),
-                 o_cand = carve(4 * 3 * (size_t)n * ne), o_best = carve(4 * 4 * (size_t)n);
-    if (off_b > s->work_bytes) {
-        (void)hipFree(s->d_work);
-        s->d_work = nullptr, s->work_bytes = 0;
-        HIP_TRY(hipMalloc(&s->d_work, off_b));
-        s->work_bytes = off_b;
+    ds[i] = d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// descent seeds on the device
+// ---------------------------------------------------------------------------------------------
+struct SeedCfg {
+    int32_t wn_use_refinement, wn_max_one_step, sg_refine[2];
+};
+
+__device__ inline int unit_plane(const SearchArgs &A, int nplanes, int u) {
+    int p = 0;
+    while (p + 1 < nplanes && u >= A.pl[p + 1].unit_base) p++;
+    return p;
+}
+
+// wiener_decompose_sep_sym + finalize + compute_score (EbRestorationPick.c:906-1040, 1337-1419), one workgroup
+// per unit; the unit's descent starts from the finalized taps unless the score says the filter does not help
+__global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, int nplanes, const int64_t *mh,
+                                                           const SeedCfg cfg, Descent *ds, SvtGpuRestUnit *wu) {
+    __shared__ WienerSolveLds L;
+    const int        u = blockIdx.x, tid = threadIdx.x;
+    const PlaneArgs &P = A.pl[unit_plane(A, nplanes, u)];
+    const int        win = P.win, win2 = win * win, div = P.bd == 10 ? 4 : 1;
+    const int64_t   *blk = mh + P.mh_off + (size_t)(u - P.unit_base) * P.nval;
+    // assemble M[k] (k = col * win + row) and the full H from the column-pair blocks
+    for (int t = tid; t < win2 * win2; t += blockDim.x) {
+        const int k = t / win2, l = t % win2, ck = k / win, rk = k % win, cl = l / win, rl = l % win;
+        const int c1 = min(ck, cl), c2 = max(ck, cl), r1 = ck <= cl ? rk : rl, r2 = ck <= cl ? rl : rk;
+        const int pair = c1 * win - c1 * (c1 - 1) / 2 + (c2 - c1);
+        L.H[t] = blk[pair * 49 + r1 * 7 + r2] / div;
     }
-    if (!eps.empty() && !s->d_flt) HIP_TRY(hipMalloc(&s->d_flt, sizeof(int16_t) * 2 * 16 * (size_t)s->width * s->height));
-    uint8_t *wb = (uint8_t *)s->d_work;
-    auto     dp = [&](size_t o) { return (void *)(wb + o); };
-    HIP_TRY(hipMemcpyAsync(dp(o_tiles), tiles.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dp(o_units), units.data(), sizeof(URect) * n, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dp(o_t0), tile0.data(), 4 * (n + 1), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(dp(o_sum), 0, 8 * (size_t)n, st));
-    HIP_TRY(hipMemsetAsync(dp(o_sse), 0, 8 * (size_t)n, st));
-    PlaneArgs a;
-    a.dgd = rec->plane[p], a.src = src->plane[p], a.dstride = rec->stride[p], a.sstride = src->stride[p];
-    a.W = W, a.H = H, a.bd = bd, a.tiles = (const Tile *)dp(o_tiles), a.units = (const URect *)dp(o_units);
-    hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt), dim3(256), 0, st, a, (unsigned long long *)dp(o_sum),
-                       (unsigned long long *)dp(o_sse));
-    HIP_TRY(hipGetLastError());
-    std::vector<uint64_t> h_sse(n);
-    HIP_TRY(hipMemcpyAsync(h_sse.data(), dp(o_sse), 8 * n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    std::vector<SvtGpuLrUnitSearch> rs(n);
-    for (int u = 0; u < n; u++) {
-        std::memset(&rs[u], 0, sizeof rs[u]);
-        rs[u].sse[0] = (int64_t)h_sse[u];
-        rs[u].sse[1] = INT64_MAX;
+    const int npair = win * (win + 1) / 2;
+    if (tid < win2) L.M[tid] = blk[npair * 49 + (tid / win) * 7 + tid % win] / div;
+    if (tid < win) { // start from the mid taps (centre incl. the implicit step)
+        const int init[7] = {3, -7, 15, 128 - 2 * (3 - 7 + 15), 15, -7, 3}, poff = (7 - win) >> 1;
+        L.a[tid] = L.b[tid] = (int32_t)(TAP_SCALE / FILT_STEP * init[tid + poff]);
     }
-    // ---------------- Wiener (search_wiener_seg, EbRestorationPick.c:1337-1419) ----------------
-    if (c->wn_enabled && (!p || c->wn_use_chroma)) {
-        hipLaunchKernelGGL(wiener_stats_kernel<T>, dim3(nt), dim3(256), 0, st, a, win,
-                           (const unsigned long long *)dp(o_sum), (long long *)dp(o_part));
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(reduce_parts_kernel, dim3(n), dim3(256), 0, st, (const long long *)dp(o_part),
-                           (const int32_t *)dp(o_t0), nval, (long long *)dp(o_mh));
-        HIP_TRY(hipGetLastError());
-        std::vector<int64_t> mh((size_t)n * nval);
-        HIP_TRY(hipMemcpyAsync(mh.data(), dp(o_mh), 8 * mh.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        const int            win2 = win * win, div = bd == 10 ? 4 : 1, half = win >> 1;
-        std::vector<Descent> ds(n);
-        std::vector<bool>    live(n, false);
-        std::vector<SvtGpuRestUnit> wu(n);
-        for (int u = 0; u < n; u++) {
-            // assemble M[k] (k = col * win + row) and the full H from the column-pair blocks
-            const int64_t *blk = mh.data() + (size_t)u * nval;
-            int64_t        M[49], Hm[49 * 49];
-            int            pair = 0;
-            for (int c1 = 0; c1 < win; c1++)
-                for (int c2 = c1; c2 < win; c2++, pair++)
-                    for (int r1 = 0; r1 < win; r1++)
-                        for (int r2 = 0; r2 < win; r2++) {
-                            const int64_t v = blk[pair * 49 + r1 * 7 + r2] / div;
-                            const int     k = c1 * win + r1, l = c2 * win + r2;
-                            Hm[k * win2 + l] = v;
-                            Hm[l * win2 + k] = v;
-                        }
-            for (int cc = 0; cc < win; cc++)
-                for (int r = 0; r < win; r++) M[cc * win + r] = blk[pair * 49 + cc * 7 + r] / div;
-            (void)half;
-            // wiener_decompose_sep_sym (:906-935): start from the mid taps (centre incl. the implicit step)
-            static const int init[7] = {3, -7, 15, 128 - 2 * (3 - 7 + 15), 15, -7, 3};
-            const int        poff    = (7 - win) >> 1;
-            int32_t          va[7], hb[7];
-            for (int i = 0; i < win; i++) va[i] = hb[i] = (int32_t)(TAP_SCALE / FILT_STEP * init[i + poff]);
-            for (int it = 1; it < 5; it++) {
-                update_sep_sym(false, win, M, Hm, va, hb);
-                update_sep_sym(true, win, M, Hm, va, hb);
-            }
-            SvtGpuRestUnit w;
-            std::memset(&w, 0, sizeof w);
-            w.type = SVTGPU_RESTORE_WIENER;
-            finalize_sym_filter(win, va, w.vfilter);
-            finalize_sym_filter(win, hb, w.hfilter);
-            if (compute_score(win, M, Hm, w.vfilter, w.hfilter) > 0) continue; // sse stays INT64_MAX
-            wu[u]        = w;
-            Descent &d   = ds[u];
-            d.start      = 4;
-            d.end        = c->wn_use_refinement ? (c->wn_max_one_refinement_step ? 4 : 1) : 8; // 8: no refinement
-            d.cont       = !c->wn_max_one_refinement_step;
-            d.nf         = 2;
-            d.p_lo       = (7 - win) >> 1;
-            d.p_hi       = 2;
+    __syncthreads();
+    for (int it = 1; it < 5; it++) {
+        update_sep_sym(false, win, L);
+        update_sep_sym(true, win, L);
+    }
+    __shared__ SvtGpuRestUnit w;
+    if (tid == 0) {
+        for (int k = 0; k < 8; k++) w.vfilter[k] = w.hfilter[k] = 0;
+        w.type = SVTGPU_RESTORE_WIENER, w.ep = 0, w.xqd[0] = w.xqd[1] = 0;
+        finalize_sym_filter(win, L.a, w.vfilter);
+        finalize_sym_filter(win, L.b, w.hfilter);
+    }
+    __syncthreads();
+    const int64_t score = compute_score(win, L, w.vfilter, w.hfilter);
+    if (tid == 0) {
+        Descent d;
+        d.unit = u;
+        if (score > 0) { // the unit keeps sse = INT64_MAX
+            w.type = 0;
+            d.done = true;
+        } else {
+            d.start = 4;
+            d.end   = cfg.wn_use_refinement ? (cfg.wn_max_one_step ? 4 : 1) : 8; // 8: no refinement
+            d.cont  = !cfg.wn_max_one_step;
+            d.nf = 2, d.p_lo = (7 - win) >> 1, d.p_hi = 2;
             for (int t = 0; t < 3; t++) {
-                d.lo[t]     = kTapMin[t], d.hi[t] = kTapMax[t];
+                d.lo[t] = c_tap_min[t], d.hi[t] = c_tap_max[t];
                 d.val[0][t] = w.hfilter[t]; // f = 0: hfilter, f = 1: vfilter (the reference's order)
                 d.val[1][t] = w.vfilter[t];
             }
             d.begin();
-            live[u] = true;
         }
-        // refinement rounds: every live unit evaluates one candidate per launch
-        std::vector<int16_t> taps((size_t)16 * n);
-        std::vector<int32_t> act(n);
-        std::vector<uint64_t> e(n);
-        for (;;) {
-            int nact = 0;
-            for (int u = 0; u < n; u++) {
-                act[u] = 0;
-                if (!live[u]) continue;
-                if (!ds[u].next()) {
-                    live[u] = false;
-                    continue;
-                }
-                set_wiener_taps(&taps[16 * u], ds[u].val[0]);
-                set_wiener_taps(&taps[16 * u + 8], ds[u].val[1]);
-                act[u] = 1;
-                nact++;
-            }
-            if (!nact) break;
-            HIP_TRY(hipMemcpyAsync(dp(o_taps), taps.data(), 2 * taps.size(), hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(dp(o_act), act.data(), 4 * n, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemsetAsync(dp(o_err), 0, 8 * (size_t)n, st));
-            hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt), dim3(256), 0, st, a, (const int16_t *)dp(o_taps),
-                               (const int32_t *)dp(o_act), (unsigned long long *)dp(o_err));
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipMemcpyAsync(e.data(), dp(o_err), 8 * n, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            for (int u = 0; u < n; u++)
-                if (act[u]) ds[u].report((int64_t)e[u]);
-        }
-        for (int u = 0; u < n; u++) {
-            if (!wu[u].type) continue;
-            rs[u].sse[1] = ds[u].err;
-            rs[u].wiener = wu[u];
-            set_wiener_taps(rs[u].wiener.hfilter, ds[u].val[0]);
-            set_wiener_taps(rs[u].wiener.vfilter, ds[u].val[1]);
+        ds[u] = d;
+        wu[u] = w;
+    }
+}
+
+// svt_get_proj_subspace_c (:417-500) from the exact integer moments, encode_xq (:502-518), and the descent of
+// finer_search_pixel_proj_error (:320-413) seeded there; one lane per (unit, ep)
+__global__ void sgr_seed_kernel(const SearchArgs A, int nplanes, int npairs, const int64_t *mom, const SeedCfg cfg,
+                                Descent *ds) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    int p = 0;
+    while (p + 1 < nplanes && i >= A.pl[p + 1].pair_base) p++;
+    const PlaneArgs &P  = A.pl[p];
+    const int        ul = (i - P.pair_base) / P.ne, k = (i - P.pair_base) % P.ne, ep = P.eps[k];
+    const URect      ur = A.units[P.unit_base + ul];
+    const double     size = (double)((ur.h_end - ur.h_start) * (ur.v_end - ur.v_start));
+    const int64_t   *m    = mom + (size_t)i * 5;
+    double H00 = (double)m[0], H11 = (double)m[1], H01 = (double)m[2], C0 = (double)m[3], C1 = (double)m[4];
+    H00 /= size, H01 /= size, H11 /= size;
+    const double H10 = H01;
+    C0 /= size, C1 /= size;
+    const int r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+    int32_t   xq[2] = {0, 0};
+    if (r0 == 0) {
+        if (!(H11 < 1e-8)) xq[1] = (int32_t)rint(C1 / H11 * (1 << 7));
+    } else if (r1 == 0) {
+        if (!(H00 < 1e-8)) xq[0] = (int32_t)rint(C0 / H00 * (1 << 7));
+    } else {
+        const double det = H00 * H11 - H01 * H10;
+        if (!(det < 1e-8)) {
+            xq[0] = (int32_t)rint((H11 * C0 - H01 * C1) / det * (1 << 7));
+            xq[1] = (int32_t)rint((H00 * C1 - H10 * C0) / det * (1 << 7));
         }
     }
-    // ---------------- self-guided (search_sgrproj_seg / search_selfguided_restoration) ----------------
-    if (!eps.empty()) {
-        HIP_TRY(hipMemcpyAsync(dp(o_eps), eps.data(), 4 * ne, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(dp(o_mom), 0, 8 * 5 * (size_t)n * ne, st));
-        hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt, ne), dim3(256), 0, st, a, (const int32_t *)dp(o_eps), s->d_flt,
-                           (long long *)dp(o_mom), ne);
-        HIP_TRY(hipGetLastError());
-        std::vector<int64_t> mom((size_t)5 * n * ne);
-        HIP_TRY(hipMemcpyAsync(mom.data(), dp(o_mom), 8 * mom.size(), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        std::vector<Descent> ds((size_t)n * ne);
-        std::vector<int32_t> xqd0((size_t)2 * n * ne);
-        for (int u = 0; u < n; u++)
-            for (int k = 0; k < ne; k++) {
-                // svt_get_proj_subspace_c (:417-500): the integer moments are exact doubles
-                const int      ep = eps[k];
-                const int64_t *m  = mom.data() + ((size_t)u * ne + k) * 5;
-                const double   size = (double)((units[u].h_end - units[u].h_start) * (units[u].v_end - units[u].v_start));
-                double         H00 = (double)m[0], H11 = (double)m[1], H01 = (double)m[2], C0 = (double)m[3], C1 = (double)m[4];
-                H00 /= size, H01 /= size, H11 /= size;
-                const double H10 = H01;
-                C0 /= size, C1 /= size;
-                int32_t xq[2] = {0, 0};
-                if (kHostSgrR[ep][0] == 0) {
-                    if (!(H11 < 1e-8)) xq[1] = (int32_t)std::rint(C1 / H11 * (1 << 7));
-                } else if (kHostSgrR[ep][1] == 0) {
-                    if (!(H00 < 1e-8)) xq[0] = (int32_t)std::rint(C0 / H00 * (1 << 7));
-                } else {
-                    const double det = H00 * H11 - H01 * H10;
-                    if (!(det < 1e-8)) {
-                        xq[0] = (int32_t)std::rint((H11 * C0 - H01 * C1) / det * (1 << 7));
-                        xq[1] = (int32_t)std::rint((H00 * C1 - H10 * C0) / det * (1 << 7));
-                    }
-                }
-                // encode_xq (:502-518)
-                int xd[2];
-                if (kHostSgrR[ep][0] == 0) {
-                    xd[0] = 0;
-                    xd[1] = std::min(std::max(128 - xq[1], PRJ_MIN1), PRJ_MAX1);
-                } else if (kHostSgrR[ep][1] == 0) {
-                    xd[0] = std::min(std::max(xq[0], PRJ_MIN0), PRJ_MAX0);
-                    xd[1] = std::min(std::max(128 - xd[0], PRJ_MIN1), PRJ_MAX1);
-                } else {
-                    xd[0] = std::min(std::max(xq[0], PRJ_MIN0), PRJ_MAX0);
-                    xd[1] = std::min(std::max(128 - xd[0] - xq[1], PRJ_MIN1), PRJ_MAX1);
-                }
-                Descent &d = ds[(size_t)u * ne + k];
-                d.start = 2, d.end = c->sg_refine[q] ? 1 : 4, d.cont = true, d.nf = 1, d.p_lo = 0, d.p_hi = 1;
-                d.lo[0] = PRJ_MIN0, d.hi[0] = PRJ_MAX0, d.lo[1] = PRJ_MIN1, d.hi[1] = PRJ_MAX1;
-                d.skip_p[0] = kHostSgrR[ep][0] == 0;
-                d.skip_p[1] = kHostSgrR[ep][1] == 0;
-                d.val[0][0] = xd[0], d.val[0][1] = xd[1];
-                d.begin();
-            }
-        std::vector<int32_t>  cand((size_t)3 * n * ne);
-        std::vector<uint64_t> e((size_t)n * ne);
-        for (;;) {
-            int nact = 0;
-            for (size_t i = 0; i < ds.size(); i++) {
-                cand[3 * i + 2] = 0;
-                if (ds[i].done || !ds[i].next()) continue;
-                const int ep = eps[i % ne];
-                // svt_decode_xq (EbRestoration.c:634-646)
-                const int x0 = ds[i].val[0][0], x1 = ds[i].val[0][1];
-                cand[3 * i]     = kHostSgrR[ep][0] == 0 ? 0 : x0;
-                cand[3 * i + 1] = kHostSgrR[ep][0] == 0 ? 128 - x1 : kHostSgrR[ep][1] == 0 ? 0 : 128 - x0 - x1;
-                cand[3 * i + 2] = 1;
-                nact++;
-            }
-            if (!nact) break;
-            HIP_TRY(hipMemcpyAsync(dp(o_cand), cand.data(), 4 * cand.size(), hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemsetAsync(dp(o_err), 0, 8 * e.size(), st));
-            hipLaunchKernelGGL(proj_err_kernel<T>, dim3(nt, ne), dim3(256), 0, st, a, (const int32_t *)dp(o_eps),
-                               (const int16_t *)s->d_flt, (const int32_t *)dp(o_cand),
-                               (unsigned long long *)dp(o_err), ne);
-            HIP_TRY(hipGetLastError());
-            HIP_TRY(hipMemcpyAsync(e.data(), dp(o_err), 8 * e.size(), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            for (size_t i = 0; i < ds.size(); i++)
-                if (cand[3 * i + 2]) ds[i].report((int64_t)e[i]);
-        }
-        // best ep per unit (strict <, first), then the SSE of its clipped output
-        std::vector<int32_t> best((size_t)4 * n);
-        for (int u = 0; u < n; u++) {
-            int64_t be = -1;
-            int     bk = 0;
-            for (int k = 0; k < ne; k++) {
-                const int64_t err = ds[(size_t)u * ne + k].err;
-                if (be == -1 || err < be) be = err, bk = k;
-            }
-            const Descent &d  = ds[(size_t)u * ne + bk];
-            const int      ep = eps[bk];
-            SvtGpuRestUnit g;
-            std::memset(&g, 0, sizeof g);
-            g.type = SVTGPU_RESTORE_SGRPROJ, g.ep = ep, g.xqd[0] = d.val[0][0], g.xqd[1] = d.val[0][1];
-            rs[u].sgrproj  = g;
-            best[4 * u]     = bk;
-            best[4 * u + 1] = ep;
-            best[4 * u + 2] = kHostSgrR[ep][0] == 0 ? 0 : g.xqd[0];
-            best[4 * u + 3] = kHostSgrR[ep][0] == 0 ? 128 - g.xqd[1] : kHostSgrR[ep][1] == 0 ? 0 : 128 - g.xqd[0] - g.xqd[1];
-        }
-        HIP_TRY(hipMemcpyAsync(dp(o_best), best.data(), 4 * best.size(), hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(dp(o_err), 0, 8 * (size_t)n, st));
-        hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt), dim3(256), 0, st, a, (const int16_t *)s->d_flt,
-                           (const int32_t *)dp(o_best), (unsigned long long *)dp(o_err));
-        HIP_TRY(hipGetLastError());
-        std::vector<uint64_t> es(n);
-        HIP_TRY(hipMemcpyAsync(es.data(), dp(o_err), 8 * n, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        for (int u = 0; u < n; u++) rs[u].sse[2] = (int64_t)es[u];
+    int xd0, xd1;
+    if (r0 == 0) {
+        xd0 = 0;
+        xd1 = min(max(128 - xq[1], PRJ_MIN1), PRJ_MAX1);
+    } else if (r1 == 0) {
+        xd0 = min(max(xq[0], PRJ_MIN0), PRJ_MAX0);
+        xd1 = min(max(128 - xd0, PRJ_MIN1), PRJ_MAX1);
+    } else {
+        xd0 = min(max(xq[0], PRJ_MIN0), PRJ_MAX0);
+        xd1 = min(max(128 - xd0 - xq[1], PRJ_MIN1), PRJ_MAX1);
     }
-    // ---------------- rest_finish_search (EbRestorationPick.c:1555-1634) ----------------
-    const bool wn_on = c->wn_enabled && (!p || c->wn_use_chroma), sg_on = !eps.empty();
-    const int  force = c->wn_enabled ? (c->sg_enabled ? 4 : 1) : (c->sg_enabled ? 2 : 0);
-    const int  nrt   = n > 1 ? 4 : 3;
+    Descent d;
+    d.unit = P.unit_base + ul, d.k = k, d.ep = ep;
+    d.start = 2, d.end = cfg.sg_refine[p > 0] ? 1 : 4, d.cont = true, d.nf = 1, d.p_lo = 0, d.p_hi = 1;
+    d.lo[0] = PRJ_MIN0, d.hi[0] = PRJ_MAX0, d.lo[1] = PRJ_MIN1, d.hi[1] = PRJ_MAX1;
+    d.skip_p[0] = r0 == 0, d.skip_p[1] = r1 == 0;
+    d.val[0][0] = xd0, d.val[0][1] = xd1;
+    d.begin();
+    ds[i] = d;
+}
+
+// best ep per unit (strict <, first) -> best[unit] = {ep index, ep, xq0, xq1}
+__global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplanes, int n, int32_t *best) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n) return;
+    int p = 0;
+    while (p + 1 < nplanes && u >= A.pl[p + 1].unit_base) p++;
+    const PlaneArgs &P    = A.pl[p];
+    const Descent   *d    = ds + P.pair_base + (u - P.unit_base) * P.ne;
+    long long        be   = -1;
+    int              bk   = 0;
+    for (int k = 0; k < P.ne; k++)
+        if (be == -1 || d[k].err < be) be = d[k].err, bk = k;
+    const int ep = P.eps[bk], x0 = d[bk].val[0][0], x1 = d[bk].val[0][1];
+    best[4 * u]     = bk;
+    best[4 * u + 1] = ep;
+    best[4 * u + 2] = c_sgr_r[ep][0] == 0 ? 0 : x0;
+    best[4 * u + 3] = c_sgr_r[ep][0] == 0 ? 128 - x1 : c_sgr_r[ep][1] == 0 ? 0 : 128 - x0 - x1;
+}
+
+struct Carver {
+    size_t off = 0;
+    size_t operator()(size_t bytes) {
+        const size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    }
+};
+
+struct PlanePlan {
+    int                  n = 0, nt = 0, unit_base = 0, tile_base = 0, win = 7, nval = 0, ne = 0, pair_base = 0;
+    bool                 wn = false, sg = false;
+    size_t               part_off = 0, mh_off = 0; // element offsets (int64)
+    std::vector<int32_t> eps;
+};
+
+// rest_finish_search (EbRestorationPick.c:1555-1634) of one plane over its per-unit search results
+void finish_plane(const SvtGpuLrSearchControls *c, int p, int win, const SvtGpuLrUnitSearch *rs, int n,
+                  int32_t *frame_type, SvtGpuRestUnit *out) {
+    const int force = c->wn_enabled ? (c->sg_enabled ? 4 : 1) : (c->sg_enabled ? 2 : 0);
+    const int nrt   = n > 1 ? 4 : 3;
     std::vector<int>            brt((size_t)3 * n, 0);
     std::vector<SvtGpuRestUnit> uw(n), us(n);
     double                      best_cost = 0;
@@ -975,9 +1007,7 @@ int search_plane(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         const double cost = rdcost(c->rdmult, bits >> 4, sse);
         if (r == 0 || cost < best_cost) best_cost = cost, best_type = r;
     }
-    (void)wn_on, (void)sg_on;
     *frame_type = best_type;
-    std::vector<SvtGpuRestUnit> out(n);
     for (int u = 0; u < n; u++) { // copy_unit_info
         std::memset(&out[u], 0, sizeof out[u]);
         if (best_type) {
@@ -985,13 +1015,309 @@ int search_plane(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             out[u]      = t == 1 ? uw[u] : us[u];
             out[u].type = t;
         }
-        if (rec_out) rec_out[u] = rs[u];
     }
-    HIP_TRY(hipMemcpyAsync(s->d_units[p], out.data(), sizeof(SvtGpuRestUnit) * n, hipMemcpyHostToDevice, st));
+}
+
+template <typename Fn>
+void launch_stats(int win, Fn &&f) {
+    if (win == 7) f(std::integral_constant<int, 7>());
+    else if (win == 5) f(std::integral_constant<int, 5>());
+    else f(std::integral_constant<int, 3>());
+}
+
+constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
+
+template <typename T>
+int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *src, const SvtGpuLrSearchControls *c,
+                 int nplanes, int32_t *frame_type, SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
+    // SVTGPU_LR_TIMING=1 prints the host-side phase times (wall clock, including the waits) to stderr
+    static const bool timing = std::getenv("SVTGPU_LR_TIMING") != nullptr;
+    auto              clk    = [] { return std::chrono::steady_clock::now(); };
+    auto              t_last = clk();
+    double            t_ph[6] = {0, 0, 0, 0, 0, 0};
+    auto              mark   = [&](int i) {
+        const auto now = clk();
+        t_ph[i] += std::chrono::duration<double, std::milli>(now - t_last).count();
+        t_last = now;
+    };
+    // ---- plan: units (foreach_rest_unit_in_tile, EbRestoration.c:1257-1294), their <= 64x64 tiles, the eps ----
+    PlanePlan            pp[3];
+    std::vector<URect>   units;
+    std::vector<Tile>    tiles;
+    std::vector<int32_t> tile0;
+    const int            win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
+    int                  npairs = 0, n_wn = 0, nt_wn = 0, n_sg = 0, nt_sg = 0, sg_planes = 0;
+    size_t               flt_elems = 0, part_elems = 0, mh_elems = 0, n_sitems = 0;
+    for (int p = 0; p < nplanes; p++) {
+        PlanePlan &q = pp[p];
+        const int  W = rec->pw[p], H = rec->ph[p], usz = s->unit_size[p], ext = usz * 3 / 2, off = 8 >> (p > 0);
+        q.unit_base = (int)units.size(), q.tile_base = (int)tiles.size();
+        for (int y0 = 0; y0 < H;) {
+            const int uh = (H - y0 < ext) ? H - y0 : usz;
+            int       vs = std::max(0, y0 - off), ve = y0 + uh;
+            if (ve < H) ve -= off;
+            for (int x0 = 0; x0 < W;) {
+                const int uw = (W - x0 < ext) ? W - x0 : usz;
+                tile0.push_back((int)tiles.size());
+                for (int y = vs; y < ve; y += 64)
+                    for (int x = x0; x < x0 + uw; x += 64)
+                        tiles.push_back({p, (int)units.size(), x, y, std::min(64, x0 + uw - x), std::min(64, ve - y)});
+                units.push_back({x0, x0 + uw, vs, ve});
+                x0 += uw;
+            }
+            y0 += uh;
+        }
+        q.n = (int)units.size() - q.unit_base, q.nt = (int)tiles.size() - q.tile_base;
+        if (q.n != s->hunits[p] * s->vunits[p]) return SVTGPU_ERR_INVALID_ARG;
+        q.wn   = c->wn_enabled && (!p || c->wn_use_chroma);
+        q.win  = p == 0 ? win_l : std::min(win_l, 5);
+        q.nval = (q.win * (q.win + 1) / 2 + 1) * 49;
+        if (c->sg_enabled && (!p || c->sg_use_chroma))
+            for (int e = c->sg_start_ep[p > 0]; e < c->sg_end_ep[p > 0]; e += std::max(1, c->sg_ep_inc[p > 0]))
+                q.eps.push_back(e);
+        q.ne = (int)q.eps.size(), q.sg = q.ne > 0;
+        q.pair_base = npairs;
+        npairs += q.n * q.ne;
+        if (q.wn) {
+            n_wn += q.n, nt_wn += q.nt;
+            q.part_off = part_elems, q.mh_off = mh_elems;
+            part_elems += (size_t)q.nt * q.nval, mh_elems += (size_t)q.n * q.nval;
+        }
+        if (q.sg) {
+            n_sg += q.n, nt_sg += q.nt, sg_planes++;
+            flt_elems += (size_t)q.ne * 2 * W * H;
+            n_sitems += (size_t)q.nt * q.ne;
+        }
+    }
+    tile0.push_back((int)tiles.size());
+    const int n_all = (int)units.size(), nt_all = (int)tiles.size();
+    // ---- device scratch and pinned staging ----
+    Carver       dc;
+    const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1));
+    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
+    const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn);
+    const size_t o_wds = dc(sizeof(Descent) * n_wn), o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
+                 o_witems = dc(4 * (size_t)nt_wn);
+    const size_t o_mom = dc(40 * (size_t)npairs), o_sds = dc(sizeof(Descent) * npairs), o_cand = dc(8 * (size_t)npairs),
+                 o_serr = dc(8 * (size_t)npairs), o_sitems = dc(4 * n_sitems), o_best = dc(16 * (size_t)n_sg),
+                 o_sse2 = dc(8 * (size_t)n_sg), o_cnt = dc(32);
+    Carver       hc;
+    const size_t h_tiles = hc(sizeof(Tile) * nt_all), h_units = hc(sizeof(URect) * n_all), h_t0 = hc(4 * (n_all + 1));
+    const size_t h_sse = hc(8 * n_all), h_cnt = hc(16), h_wu = hc(sizeof(SvtGpuRestUnit) * n_wn);
+    const size_t h_wds = hc(sizeof(Descent) * n_wn), h_sds = hc(sizeof(Descent) * npairs), h_sse2 = hc(8 * (size_t)n_sg),
+                 h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
+    if (dc.off > s->work_bytes) {
+        (void)hipFree(s->d_work);
+        s->d_work = nullptr, s->work_bytes = 0;
+        HIP_TRY(hipMalloc(&s->d_work, dc.off));
+        s->work_bytes = dc.off;
+    }
+    if (hc.off > s->pin_bytes) {
+        if (s->h_pin) (void)hipHostFree(s->h_pin);
+        s->h_pin = nullptr, s->pin_bytes = 0;
+        HIP_TRY(hipHostMalloc(&s->h_pin, hc.off, hipHostMallocDefault));
+        s->pin_bytes = hc.off;
+    }
+    if (2 * flt_elems > s->flt_bytes) {
+        (void)hipFree(s->d_flt);
+        s->d_flt = nullptr, s->flt_bytes = 0;
+        HIP_TRY(hipMalloc(&s->d_flt, 2 * flt_elems));
+        s->flt_bytes = 2 * flt_elems;
+    }
+    uint8_t *wb = (uint8_t *)s->d_work, *hb = (uint8_t *)s->h_pin;
+    auto     dp = [&](size_t o) { return (void *)(wb + o); };
+    auto     hp = [&](size_t o) { return (void *)(hb + o); };
+    SearchArgs A;
+    std::memset(&A, 0, sizeof A);
+    size_t flt_off = 0;
+    for (int p = 0; p < nplanes; p++) {
+        PlaneArgs &P = A.pl[p];
+        P.dgd = rec->plane[p], P.src = src->plane[p], P.dstride = rec->stride[p], P.sstride = src->stride[p];
+        P.W = rec->pw[p], P.H = rec->ph[p], P.bd = rec->bit_depth;
+        P.flt       = s->d_flt + flt_off;
+        P.unit_base = pp[p].unit_base, P.pair_base = pp[p].pair_base, P.ne = pp[p].ne;
+        for (int k = 0; k < pp[p].ne; k++) P.eps[k] = pp[p].eps[k];
+        P.win = pp[p].win, P.nval = pp[p].nval, P.mh_off = (int64_t)pp[p].mh_off;
+        if (pp[p].sg) flt_off += (size_t)pp[p].ne * 2 * P.W * P.H;
+    }
+    A.tiles = (const Tile *)dp(o_tiles), A.units = (const URect *)dp(o_units), A.tile0 = (const int32_t *)dp(o_t0);
+    auto *d_t0 = (int32_t *)dp(o_t0);
+    // ---- phase 1: sums, Wiener statistics, self-guided filters and moments ----
+    std::memcpy(hp(h_tiles), tiles.data(), sizeof(Tile) * nt_all);
+    std::memcpy(hp(h_units), units.data(), sizeof(URect) * n_all);
+    std::memcpy(hp(h_t0), tile0.data(), 4 * (n_all + 1));
+    HIP_TRY(hipMemcpyAsync(dp(o_tiles), hp(h_tiles), sizeof(Tile) * nt_all, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dp(o_units), hp(h_units), sizeof(URect) * n_all, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(dp(o_t0), hp(h_t0), 4 * (n_all + 1), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(dp(o_sum), 0, 8 * (size_t)n_all, st));
+    HIP_TRY(hipMemsetAsync(dp(o_sse), 0, 8 * (size_t)n_all, st));
+    if (npairs) HIP_TRY(hipMemsetAsync(dp(o_mom), 0, 40 * (size_t)npairs, st));
+    hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
+                       (unsigned long long *)dp(o_sse));
+    HIP_TRY(hipGetLastError());
+    for (int p = 0; p < nplanes; p++) {
+        const PlanePlan &q = pp[p];
+        if (!q.wn) continue;
+        long long *part = (long long *)dp(o_part) + q.part_off, *mh = (long long *)dp(o_mh) + q.mh_off;
+        launch_stats(q.win, [&](auto wc) {
+            hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, st, A,
+                               q.tile_base, (const unsigned long long *)dp(o_sum), part);
+        });
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, st, (const long long *)part,
+                           (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh);
+        HIP_TRY(hipGetLastError());
+    }
+    if (nt_sg) {
+        hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, (long long *)dp(o_mom));
+        HIP_TRY(hipGetLastError());
+    }
+    mark(0);
+    // ---- phase 2: descent seeds (Wiener decomposition per unit, projection solve per (unit, ep)) ----
+    SeedCfg cfg;
+    cfg.wn_use_refinement = c->wn_use_refinement, cfg.wn_max_one_step = c->wn_max_one_refinement_step;
+    cfg.sg_refine[0] = c->sg_refine[0], cfg.sg_refine[1] = c->sg_refine[1];
+    if (n_wn) {
+        hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, st, A, nplanes, (const int64_t *)dp(o_mh), cfg,
+                           (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu));
+        HIP_TRY(hipGetLastError());
+    }
+    if (npairs) {
+        hipLaunchKernelGGL(sgr_seed_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, A, sg_planes, npairs,
+                           (const int64_t *)dp(o_mom), cfg, (Descent *)dp(o_sds));
+        HIP_TRY(hipGetLastError());
+    }
+    mark(1);
+    // ---- phase 3: descent rounds on the device ----
+    auto *cnt = (int32_t *)dp(o_cnt); // [parity][wn items, wn live, sg items, sg live]
+    HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
+    if (n_wn) {
+        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, st));
+        hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
+                           d_t0, (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_witems), cnt, 1);
+        HIP_TRY(hipGetLastError());
+    }
+    if (npairs) {
+        HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * (size_t)npairs, st));
+        hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
+                           npairs, d_t0, (unsigned long long *)dp(o_serr), (int32_t *)dp(o_cand),
+                           (int32_t *)dp(o_sitems), cnt + 2, 1);
+        HIP_TRY(hipGetLastError());
+    }
+    const int gw = std::max(1, std::min(nt_wn, 2048)), gs = (int)std::max<size_t>(1, std::min<size_t>(n_sitems, 4096));
+    bool      wl = n_wn > 0, sl = npairs > 0;
+    int32_t  *hcnt = (int32_t *)hp(h_cnt);
+    int       g    = 0; // global round index
+    while (wl || sl) {
+        for (int b = 0; b < ROUNDS_PER_BATCH; b++, g++) {
+            int32_t *cur = cnt + 4 * (g & 1), *nxt = cnt + 4 * ((g + 1) & 1);
+            if (wl) {
+                hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(gw), dim3(256), 0, st, A, (const int16_t *)dp(o_taps),
+                                   (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
+                                   (unsigned long long *)dp(o_werr));
+                hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
+                                   (Descent *)dp(o_wds), n_wn, d_t0, (unsigned long long *)dp(o_werr),
+                                   (int16_t *)dp(o_taps), (int32_t *)dp(o_witems), nxt, 0);
+            }
+            if (sl) {
+                hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
+                                   (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
+                                   (unsigned long long *)dp(o_serr));
+                hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
+                                   (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
+                                   (int32_t *)dp(o_cand), (int32_t *)dp(o_sitems), nxt + 2, 0);
+            }
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(hcnt, cnt + 4 * (g & 1), 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        wl = wl && hcnt[1] > 0;
+        sl = sl && hcnt[3] > 0;
+        if (g > MAX_ROUNDS) return SVTGPU_ERR_INVALID_ARG; // a descent always terminates; guard anyway
+    }
+    mark(2);
+    // ---- phase 4: best ep and its clipped SSE; read back the descents ----
+    if (n_sg) {
+        hipLaunchKernelGGL(sgr_best_kernel, dim3((n_sg + 255) / 256), dim3(256), 0, st, (const Descent *)dp(o_sds), A,
+                           sg_planes, n_sg, (int32_t *)dp(o_best));
+        HIP_TRY(hipMemsetAsync(dp(o_sse2), 0, 8 * (size_t)n_sg, st));
+        hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
+                           (unsigned long long *)dp(o_sse2));
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(hp(h_sse2), dp(o_sse2), 8 * (size_t)n_sg, hipMemcpyDeviceToHost, st));
+    }
+    Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
+    SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
+    HIP_TRY(hipMemcpyAsync(hp(h_sse), dp(o_sse), 8 * n_all, hipMemcpyDeviceToHost, st));
+    if (n_wn) HIP_TRY(hipMemcpyAsync(hw, dp(o_wds), sizeof(Descent) * n_wn, hipMemcpyDeviceToHost, st));
+    if (n_wn) HIP_TRY(hipMemcpyAsync(wu, dp(o_wu), sizeof(SvtGpuRestUnit) * n_wn, hipMemcpyDeviceToHost, st));
+    if (npairs) HIP_TRY(hipMemcpyAsync(hs, dp(o_sds), sizeof(Descent) * npairs, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    mark(3);
+    // ---- phase 5 (host): per-unit results and the RD finish ----
+    const uint64_t                 *sse0 = (const uint64_t *)hp(h_sse), *sse2 = (const uint64_t *)hp(h_sse2);
+    SvtGpuRestUnit                 *out  = (SvtGpuRestUnit *)hp(h_out);
+    std::vector<SvtGpuLrUnitSearch> rs(n_all);
+    for (int p = 0; p < nplanes; p++) {
+        const PlanePlan &q = pp[p];
+        for (int u = 0; u < q.n; u++) {
+            const int           gu = q.unit_base + u;
+            SvtGpuLrUnitSearch &R  = rs[gu];
+            std::memset(&R, 0, sizeof R);
+            R.sse[0] = (int64_t)sse0[gu];
+            R.sse[1] = INT64_MAX;
+            if (q.wn && wu[gu].type) {
+                R.sse[1] = hw[gu].err;
+                R.wiener = wu[gu];
+                set_wiener_taps(R.wiener.hfilter, hw[gu].val[0]);
+                set_wiener_taps(R.wiener.vfilter, hw[gu].val[1]);
+            }
+            if (q.sg) {
+                const Descent *d  = hs + q.pair_base + u * q.ne;
+                int64_t        be = -1;
+                int            bk = 0;
+                for (int k = 0; k < q.ne; k++)
+                    if (be == -1 || d[k].err < be) be = d[k].err, bk = k;
+                R.sgrproj.type = SVTGPU_RESTORE_SGRPROJ, R.sgrproj.ep = q.eps[bk];
+                R.sgrproj.xqd[0] = d[bk].val[0][0], R.sgrproj.xqd[1] = d[bk].val[0][1];
+                R.sse[2] = (int64_t)sse2[gu];
+            }
+        }
+        finish_plane(c, p, q.win, rs.data() + q.unit_base, q.n, &frame_type[p], out + q.unit_base);
+        HIP_TRY(hipMemcpyAsync(s->d_units[p], out + q.unit_base, sizeof(SvtGpuRestUnit) * q.n, hipMemcpyHostToDevice, st));
+        if (search_out && search_out[p]) std::memcpy(search_out[p], rs.data() + q.unit_base, sizeof(SvtGpuLrUnitSearch) * q.n);
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    mark(4);
+    if (timing)
+        std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d) %.3f  best %.3f  finish %.3f\n",
+                     t_ph[0], t_ph[1], g, t_ph[2], t_ph[3], t_ph[4]);
     return SVTGPU_OK;
 }
 } // namespace
+
+extern "C" int svtgpu_lr_controls_for_level(int32_t wn, int32_t sg, SvtGpuLrSearchControls *c) {
+    if (!c) return SVTGPU_ERR_INVALID_ARG;
+    std::memset(c, 0, sizeof *c);
+    // svt_aom_set_wn_filter_ctrls (EncModeConfig.c:1329-1384); level 6 reuses the previous frame's taps
+    if (wn < 0 || wn > 5 || sg < 0 || sg > 4) return SVTGPU_ERR_UNSUPPORTED;
+    if (wn > 0) {
+        c->wn_enabled                 = 1;
+        c->wn_use_chroma              = wn <= 4;
+        c->wn_filter_tap_lvl          = wn <= 2 ? 1 : 2;
+        c->wn_use_refinement          = wn <= 3;
+        c->wn_max_one_refinement_step = wn >= 2;
+    }
+    // svt_aom_set_sg_filter_ctrls (EncModeConfig.c:1386-1445), fixed-range search (step_range 16)
+    if (sg > 0) {
+        c->sg_enabled     = 1;
+        c->sg_use_chroma  = sg <= 3;
+        c->sg_start_ep[0] = 0, c->sg_end_ep[0] = 16, c->sg_ep_inc[0] = sg >= 3 ? 8 : 1;
+        c->sg_start_ep[1] = sg == 1 ? 0 : 4, c->sg_end_ep[1] = sg == 1 ? 16 : 5, c->sg_ep_inc[1] = 1;
+        c->sg_refine[0] = 1, c->sg_refine[1] = sg == 1;
+    }
+    return SVTGPU_OK;
+}
 
 extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                                       const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
@@ -1004,14 +1330,10 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
     for (int q = 0; q < 2; q++)
         if (ctrls->sg_enabled && (ctrls->sg_start_ep[q] < 0 || ctrls->sg_end_ep[q] > 16 || ctrls->sg_ep_inc[q] < 1))
             return SVTGPU_ERR_INVALID_ARG;
-    hipStream_t st        = pick_stream(s->ctx, stream);
-    const int   plane_end = ((ctrls->wn_enabled && ctrls->wn_use_chroma) || (ctrls->sg_enabled && ctrls->sg_use_chroma)) ? 2 : 0;
+    hipStream_t st      = pick_stream(s->ctx, stream);
+    const int   nplanes = ((ctrls->wn_enabled && ctrls->wn_use_chroma) || (ctrls->sg_enabled && ctrls->sg_use_chroma)) ? 3 : 1;
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
-    for (int p = 0; p <= plane_end; p++) {
-        int rc = recon->bytes_per_sample == 2
-            ? search_plane<uint16_t>(s, recon, source, p, ctrls, &frame_type_out[p], search_out ? search_out[p] : nullptr, st)
-            : search_plane<uint8_t>(s, recon, source, p, ctrls, &frame_type_out[p], search_out ? search_out[p] : nullptr, st);
-        if (rc) return rc;
-    }
-    return SVTGPU_OK;
+    return recon->bytes_per_sample == 2
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, frame_type_out, search_out, st)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, frame_type_out, search_out, st);
 }

@@ -141,7 +141,7 @@ def test_lr_search_golden(ctx, case):
 
 
 LR_SEARCH_CASES = [(320, 192, 10, 64, 1, 1, 5), (640, 360, 8, 128, 1, 1, 6), (1920, 1080, 10, 256, 1, 1, 7),
-                   (512, 288, 10, 128, 3, 2, 8)]
+                   (512, 288, 10, 128, 3, 2, 8), (328, 184, 10, 64, 1, 1, 9), (264, 152, 8, 64, 2, 3, 10)]
 
 
 @pytest.mark.parametrize("w,h,bd,usize,wn,sg,seed", LR_SEARCH_CASES)
