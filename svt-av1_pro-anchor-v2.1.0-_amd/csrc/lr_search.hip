@@ -40,7 +40,6 @@ struct Tile {
 struct URect {
     int32_t h_start, h_end, v_start, v_end;
 };
-
 constexpr int PRJ_MIN0 = -96, PRJ_MAX0 = 31, PRJ_MIN1 = -32, PRJ_MAX1 = 95;
 const int     kTapMin[3] = {-5, -23, -17}, kTapMax[3] = {10, 8, 46};
 const int     kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
@@ -48,8 +47,8 @@ const int     kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}
 
 struct PlaneArgs {
     const void *dgd, *src;
-    int16_t    *flt; // [ne][2][W*H] self-guided outputs
-    int32_t     dstride, sstride, W, H, bd;
+    int16_t    *flt; // [ne][2][H][fstride] self-guided outputs
+    int32_t     dstride, sstride, W, H, bd, fstride;
     int32_t     unit_base, pair_base, ne; // SGR pair of (unit, k) = pair_base + (unit - unit_base) * ne + k
     int32_t     eps[16];
     int32_t     win, nval;                // Wiener window and statistics values per unit
@@ -77,6 +76,21 @@ __device__ inline unsigned long long wave_sum(unsigned long long v) {
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 __device__ inline int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
+}
+
+template <typename T>
+__device__ inline void load4(const T *p, int *v) {
+    if constexpr (sizeof(T) == 2) {
+        const uint2 w = *(const uint2 *)p;
+        v[0] = w.x & 0xFFFF, v[1] = w.x >> 16, v[2] = w.y & 0xFFFF, v[3] = w.y >> 16;
+    } else {
+        const uint32_t w = *(const uint32_t *)p;
+        v[0] = w & 0xFF, v[1] = (w >> 8) & 0xFF, v[2] = (w >> 16) & 0xFF, v[3] = w >> 24;
+    }
+}
+__device__ inline void load4s(const int16_t *p, int *v) {
+    const int2 w = *(const int2 *)p;
+    v[0] = (int)(int16_t)(w.x & 0xFFFF), v[1] = w.x >> 16, v[2] = (int)(int16_t)(w.y & 0xFFFF), v[3] = w.y >> 16;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -107,6 +121,7 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
 // symmetric, and which also accumulate M) LD lanes each in the last wave(s); lanes stride over pixel pairs.
 // ---------------------------------------------------------------------------------------------
 constexpr int ST_W = 70, ST_SLOTS = 56;
+constexpr int SG_NC = 7; // candidates per self-guided descent pass (a depth-3 outcome tree)
 template <int WIN>
 struct StatsCfg {
     static constexpr int HALF = WIN / 2, NPAIR = WIN * (WIN + 1) / 2, NOFF = WIN * (WIN - 1) / 2;
@@ -229,57 +244,87 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wiener trial: SSE of a unit's tiles filtered with the unit's candidate taps (hfilter[8], vfilter[8]);
-// items[] lists the tiles of the units with a pending candidate, cnt[0] their number
+// Wiener trial: SSE of every tile of a unit with a pending candidate, filtered with the unit's candidate taps
+// (hfilter[8], vfilter[8]); one workgroup per Wiener tile, units without a pending candidate (wact = 0) exit at
+// once.  Both passes run on packed int16 pairs with v_dot2_i32_i16, two outputs per lane: the staged tile
+// (columns x0-4 .. x0+w+3, rows y0-3 .. y0+h+3) is read as aligned column pairs, the horizontal output is stored
+// as row pairs.  Fixed lane mappings (no runtime divisions): staging in 18 groups of 4 pixels per row, the
+// horizontal pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
 // ---------------------------------------------------------------------------------------------
+__device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16); }
+
 template <typename T>
 __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
-                                                           const int32_t *items, const int32_t *cnt,
-                                                           int32_t *cnt_next, unsigned long long *err) {
-    __shared__ uint16_t v[(64 + 7) * (64 + 8)];
-    __shared__ uint16_t tmp[(64 + 7) * 64];
-    const int n = cnt[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0; // the next advance counts there
-    for (int it = blockIdx.x; it < n; it += gridDim.x) {
-        const Tile       t = A.tiles[items[it]];
-        const PlaneArgs &P = A.pl[t.plane];
-        const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-        const int        vs = 64 + 8;
-        __syncthreads(); // LDS reuse across items
-        for (int i = threadIdx.x; i < (t.h + 7) * (t.w + 8); i += 256) {
-            const int r = i / (t.w + 8), c = i % (t.w + 8);
-            v[r * vs + c] = (uint16_t)px(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 + c - 3);
-        }
-        __syncthreads();
-        int hf[8], vf[8]; // registers: the LDS stores below could alias a generic pointer
+                                                           const int32_t *wact, int32_t *cnt_next,
+                                                           unsigned long long *err) {
+    constexpr int VS = 72;
+    __shared__ __align__(16) uint16_t v[71 * VS];
+    __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[1] = 0; // the next advance counts its live descents there
+    const Tile t = A.tiles[blockIdx.x];
+    if (!wact[t.unit]) return;
+    const PlaneArgs &P  = A.pl[t.plane];
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    const int16_t   *tp = taps + t.unit * 16;
+    int              h[8], w[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) hf[k] = taps[t.unit * 16 + k], vf[k] = taps[t.unit * 16 + 8 + k];
-        const WienerRound rr = wiener_round(P.bd);
-        const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1;
-        for (int i = threadIdx.x; i < (t.h + 7) * t.w; i += 256) {
-            const int       y = i / t.w, x = i % t.w;
-            const uint16_t *p = v + y * vs + x;
-            int             sum = ((int)p[3] << 7) + (1 << (P.bd + 6));
+    for (int k = 0; k < 8; k++) h[k] = tp[k], w[k] = tp[8 + k];
+    // pair weights: even output x (pairs at x, x+2, ...) and odd output x+1; the same for rows
+    const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
+    const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+    const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
+    const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
+    const int      rows = t.h + 7, ng = (t.w + 8) >> 2, nyp = (t.h + 1) >> 1;
 #pragma unroll
-            for (int k = 0; k < 8; k++) sum += (int)p[k] * hf[k];
-            tmp[y * 64 + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
-        }
-        __syncthreads();
-        unsigned long long e    = 0;
-        const int          maxv = (1 << P.bd) - 1;
-        for (int i = threadIdx.x; i < t.h * t.w; i += 256) {
-            const int       y = i / t.w, x = i % t.w;
-            const uint16_t *c = tmp + y * 64 + x;
-            int             sum = ((int)c[3 * 64] << 7) - (1 << (P.bd + rr.r1 - 1));
+    for (int k = 0; k < (71 * 18 + 255) / 256; k++) {
+        const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
+        if (r >= rows || g >= ng) continue;
+        const int yy = t.y0 + r - 3, xx = t.x0 - 4 + 4 * g;
+        int       q[4];
+        if (yy >= 0 && yy < P.H && xx >= 0 && xx + 4 <= P.W) {
+            load4(d + (size_t)yy * P.dstride + xx, q);
+        } else {
 #pragma unroll
-            for (int k = 0; k < 8; k++) sum += (int)c[k * 64] * vf[k];
-            const int o  = min(max((sum + (1 << (rr.r1 - 1))) >> rr.r1, 0), maxv);
-            const int dd = o - (int)s[(size_t)(t.y0 + y) * P.sstride + t.x0 + x];
-            e += (unsigned long long)(dd * dd);
+            for (int j = 0; j < 4; j++) q[j] = px(d, P.dstride, P.W, P.H, yy, xx + j);
         }
-        e = wave_sum(e);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
+        *(uint2 *)(v + r * VS + 4 * g) = make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
     }
+    __syncthreads();
+    const WienerRound rr  = wiener_round(P.bd);
+    const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
+    uint16_t         *tq16 = (uint16_t *)tq;
+    const int         xh   = 2 * (threadIdx.x & 31);
+    if (xh < t.w)
+        for (int r = threadIdx.x >> 5; r < rows; r += 8) {
+            const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
+            const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
+            const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
+            const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
+            const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
+            tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
+            tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
+        }
+    __syncthreads();
+    unsigned long long e    = 0;
+    const int          maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
+    const int          x    = threadIdx.x & 63;
+    if (x < t.w)
+        for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
+            const int       y  = 2 * yp;
+            const uint32_t *c  = tq + yp * 64 + x;
+            const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
+            const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
+            const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
+            const T  *sp = s + (size_t)(t.y0 + y) * P.sstride + t.x0 + x;
+            const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
+            e += (unsigned long long)(d0 * d0);
+            if (y + 1 < t.h) {
+                const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[P.sstride];
+                e += (unsigned long long)(d1 * d1);
+            }
+        }
+    e = wave_sum(e);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -332,7 +377,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
             sv[k]       = ((int)s[(size_t)(t.y0 + y) * P.sstride + t.x0 + x] << 4) - (pix[k] << 4);
         }
     }
-    const size_t pn = (size_t)P.W * P.H;
+    const size_t pn = (size_t)P.fstride * P.H;
     for (int e = 0; e < P.ne; e++) {
         const int ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
 #pragma unroll
@@ -357,7 +402,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
             const int i = threadIdx.x + k * SG_NT;
             if (i >= npx) break;
             const int    y = i / t.w, x = i % t.w, c = (y + 1) * bw + x + 1, u = pix[k] << 4;
-            const size_t o = (size_t)(t.y0 + y) * P.W + t.x0 + x;
+            const size_t o = (size_t)(t.y0 + y) * P.fstride + t.x0 + x;
             int          g1 = 0, g2 = 0;
             if (r0) {
                 const int *Q = ab2 + c;
@@ -405,35 +450,77 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
     }
 }
 
-// projection error of the pending candidate of every listed (tile, ep): items[] = tile * 16 + ep index
+// projection errors of the candidate trees of every listed tile: the tile's CDEF and source pixels are read once
+// (packed per pixel as (x, x - src) int16 pairs), then every ep of the unit with a pending tree (candm != 0) is
+// evaluated on them.  Per pixel the filter differences (g1, g2) = (flt0 - u, flt1 - u) fit int16 (|g| < 2^15),
+// as do the xq pairs, so a candidate costs one v_dot2_i32_i16 plus the error.  Tiles are read in 4-pixel chunks
+// (tile widths and x offsets are multiples of 4), 16 chunks per row.
 template <typename T>
 __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
-                                                       int32_t *cnt_next, const int32_t *cand, unsigned long long *err) {
+                                                       int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
+                                                       unsigned long long *err) {
     const int n = cnt[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
+    constexpr int NCH = 4; // chunks per lane (64 rows x 16 chunks / 256 lanes)
     for (int it = blockIdx.x; it < n; it += gridDim.x) {
-        const int        item = items[it], e = item & 15;
-        const Tile       t = A.tiles[item >> 4];
+        const Tile       t = A.tiles[items[it]];
         const PlaneArgs &P = A.pl[t.plane];
-        const int        ep = P.eps[e], pair = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
-        const int        xq0 = cand[2 * pair], xq1 = cand[2 * pair + 1], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne, cw = t.w >> 2;
         const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-        const size_t     pn = (size_t)P.W * P.H;
-        const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
-        unsigned long long acc = 0;
-        for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
-            const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-            const size_t o = (size_t)y * P.W + x;
-            const int    dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
-            const int    u = dv << 4;
-            int          v = 1 << 10;
-            if (r0 > 0) v += xq0 * (f0[o] - u);
-            if (r1 > 0) v += xq1 * (f1[o] - u);
-            const int ee = (v >> 11) + dv - sv;
-            acc += (unsigned long long)((long long)ee * ee);
+        const size_t     pn = (size_t)P.fstride * P.H;
+        uint32_t         px2[NCH][4]; // (x, x - src) per pixel
+        size_t           fo[NCH];
+        bool             on[NCH];
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            const int ch = threadIdx.x + k * 256, y = t.y0 + (ch >> 4), x = t.x0 + (ch & 15) * 4;
+            on[k]        = (ch >> 4) < t.h && (ch & 15) < cw;
+            fo[k]        = (size_t)y * P.fstride + x;
+            if (on[k]) {
+                int dv[4], sv[4];
+                load4(d + (size_t)y * P.dstride + x, dv);
+                load4(s + (size_t)y * P.sstride + x, sv);
+#pragma unroll
+                for (int j = 0; j < 4; j++) px2[k][j] = pack2(dv[j], dv[j] - sv[j]);
+            }
         }
-        acc = wave_sum(acc);
-        if ((threadIdx.x & 63) == 0) atomicAdd(&err[pair], acc);
+        for (int e = 0; e < P.ne; e++) {
+            const int      pair = pb + e;
+            const uint32_t mask = candm[pair];
+            if (!mask) continue;
+            uint32_t xq[SG_NC];
+#pragma unroll
+            for (int c = 0; c < SG_NC; c++)
+                xq[c] = (mask >> c & 1) ? pack2(cand[(pair * SG_NC + c) * 2], cand[(pair * SG_NC + c) * 2 + 1]) : 0u;
+            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+            uint32_t       acc[SG_NC];
+#pragma unroll
+            for (int c = 0; c < SG_NC; c++) acc[c] = 0;
+#pragma unroll
+            for (int k = 0; k < NCH; k++) {
+                if (!on[k]) continue;
+                int a0[4], a1[4];
+                load4s(f0 + fo[k], a0);
+                load4s(f1 + fo[k], a1);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    // floor((v + 1024) / 2^11) + (x - src) == (v + 1024 + (x - src) * 2^11) >> 11
+                    const int      u = (int)(px2[k][j] & 0xFFFF) << 4, c0 = 1024 + (((int)px2[k][j] >> 16) << 11);
+                    const uint32_t g = pack2(a0[j] - u, a1[j] - u);
+#pragma unroll
+                    for (int c = 0; c < SG_NC; c++) { // branch-free: candidates outside the tree have xq = 0
+                        const int ee = (dot2(g, xq[c], 0) + c0) >> 11;
+                        acc[c] += (uint32_t)(ee * ee);
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < SG_NC; c++) {
+                if (!(mask >> c & 1)) continue;
+                const unsigned long long w = wave_sum(acc[c]);
+                if ((threadIdx.x & 63) == 0) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
+            }
+        }
     }
 }
 
@@ -445,13 +532,13 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
     const int       *b = best + t.unit * 4; // {ep index, ep, xq0, xq1}
     const int        e = b[0], ep = b[1], xq0 = b[2], xq1 = b[3], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    const size_t     pn = (size_t)P.W * P.H;
+    const size_t     pn = (size_t)P.fstride * P.H;
     const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
     const int        maxv = (1 << P.bd) - 1;
     unsigned long long acc = 0;
     for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
         const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-        const size_t o = (size_t)y * P.W + x;
+        const size_t o = (size_t)y * P.fstride + x;
         const int    dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
         const int    u = dv << 4;
         int          v = u << 7;
@@ -656,9 +743,23 @@ double rdcost(int rdmult, int64_t bits, int64_t sse) { // RDCOST_DBL (EbRestorat
 struct Descent {
     int32_t unit = 0, k = 0, ep = 0;                       // owner: global unit, ep index, ep (self-guided)
     int     start = 0, end = 1, nf = 1, p_lo = 0, p_hi = 0; // p in [p_lo, p_hi]
-    bool    cont = true, skip_p[3] = {false, false, false};
-    int     lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-    int     val[2][3] = {{0, 0, 0}, {0, 0, 0}}; // coordinate values
+    bool    cont = true;
+    // coordinates and bounds packed as int8 fields (taps and xqd fit), so that the device keeps a descent in
+    // registers: value (f, p) at bits 8 * (3 f + p) of vals, bounds of p at bits 8 p of lo4 / hi4
+    uint64_t vals = 0;
+    uint32_t lo4 = 0, hi4 = 0, skipm = 0;
+    __host__ __device__ int  val(int f_, int p_) const { return (int8_t)(vals >> (8 * (3 * f_ + p_))); }
+    __host__ __device__ void set_val(int f_, int p_, int v) {
+        const int sh = 8 * (3 * f_ + p_);
+        vals         = (vals & ~(0xFFull << sh)) | ((uint64_t)(uint8_t)v << sh);
+    }
+    __host__ __device__ int  lo(int p_) const { return (int8_t)(lo4 >> (8 * p_)); }
+    __host__ __device__ int  hi(int p_) const { return (int8_t)(hi4 >> (8 * p_)); }
+    __host__ __device__ void set_bounds(int p_, int l, int h) {
+        lo4 = (lo4 & ~(0xFFu << (8 * p_))) | ((uint32_t)(uint8_t)l << (8 * p_));
+        hi4 = (hi4 & ~(0xFFu << (8 * p_))) | ((uint32_t)(uint8_t)h << (8 * p_));
+    }
+    __host__ __device__ void taps(int f_, int *v) const { v[0] = val(f_, 0), v[1] = val(f_, 1), v[2] = val(f_, 2); }
     // state
     int     s = 0, f = 0, p = 0, phase = 0;      // phase 0: minus, 1: after minus, 2: plus
     bool    skip = false, init = true, done = false;
@@ -681,13 +782,13 @@ struct Descent {
                 f++, p = p_lo, phase = 0, skip = false;
                 continue;
             }
-            if (skip_p[p]) {
+            if (skipm >> p & 1) {
                 p++;
                 continue;
             }
             if (phase == 0) {
-                if (val[f][p] - s >= lo[p]) {
-                    val[f][p] -= s, mf = f, mp = p, md = -s;
+                if (val(f, p) - s >= lo(p)) {
+                    set_val(f, p, val(f, p) - s), mf = f, mp = p, md = -s;
                     return true;
                 }
                 phase = 1;
@@ -699,20 +800,23 @@ struct Descent {
                 }
                 phase = 2;
             }
-            if (val[f][p] + s <= hi[p]) {
-                val[f][p] += s, mf = f, mp = p, md = s;
+            if (val(f, p) + s <= hi(p)) {
+                set_val(f, p, val(f, p) + s), mf = f, mp = p, md = s;
                 return true;
             }
             p++, phase = 0, skip = false;
         }
     }
-    __host__ __device__ void report(int64_t e2) {
+    __host__ __device__ void report(int64_t e2) { report_outcome(!init && e2 > err, e2); }
+    // the state change of report() for a known outcome; the candidate sequence depends only on the outcomes, so
+    // a speculative tree of candidates can be built before their errors are known
+    __host__ __device__ void report_outcome(bool worse, int64_t e2) {
         if (init) {
             err = e2, init = false;
             return;
         }
-        if (e2 > err) {
-            val[mf][mp] -= md;
+        if (worse) {
+            set_val(mf, mp, val(mf, mp) - md);
             if (md < 0)
                 phase = 1;
             else
@@ -743,42 +847,94 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
 // the other one, the advance kernel fills it).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, const int32_t *tile0,
-                                                             unsigned long long *err, int16_t *taps, int32_t *items,
-                                                             int32_t *cnt, int first) {
+__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
+                                                             int16_t *taps, int32_t *wact, int32_t *cnt, int first) {
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= n) return;
     Descent d = ds[u];
     if (d.done) return;
     if (!first) d.report((int64_t)err[u]);
-    err[u] = 0;
+    err[u]  = 0;
+    wact[u] = 0;
     if (d.next()) {
-        set_wiener_taps(taps + 16 * u, d.val[0]); // f = 0: hfilter, f = 1: vfilter
-        set_wiener_taps(taps + 16 * u + 8, d.val[1]);
-        const int t0 = tile0[u], nt = tile0[u + 1] - t0, pos = atomicAdd(&cnt[0], nt);
-        for (int i = 0; i < nt; i++) items[pos + i] = t0 + i;
+        int v[3];
+        d.taps(0, v), set_wiener_taps(taps + 16 * u, v); // f = 0: hfilter, f = 1: vfilter
+        d.taps(1, v), set_wiener_taps(taps + 16 * u + 8, v);
+        wact[u] = 1;
         atomicAdd(&cnt[1], 1);
     }
     ds[u] = d;
 }
 
+// svt_decode_xq (EbRestoration.c:634-646): xq of the ep's absent filter is 0
+__device__ inline void decode_xq(const Descent &d, int32_t *xq) {
+    const int x0 = d.val(0, 0), x1 = d.val(0, 1), r0 = c_sgr_r[d.ep][0], r1 = c_sgr_r[d.ep][1];
+    xq[0] = r0 == 0 ? 0 : x0;
+    xq[1] = r0 == 0 ? 128 - x1 : r1 == 0 ? 0 : 128 - x0 - x1;
+}
+
+// Self-guided descents evaluate a speculative tree per pass: node 0 is the pending candidate, node n's children
+// 2n+1 / 2n+2 are the candidates proposed after a worse / not-worse outcome of node n.  The walk replays the
+// outcomes against the measured errors (report() decides exactly as the reference does) and stops at the first
+// candidate outside the evaluated tree, which becomes the next root.
+// Self-guided descents evaluate a speculative tree per pass: node 0 is the pending candidate, node n's children
+// 2n+1 / 2n+2 are the candidates proposed after a worse / not-worse outcome of node n.  The walk replays the
+// outcomes against the measured errors (report() decides exactly as the reference does) and stops at the first
+// candidate that was not evaluated, which becomes the next root.  While many descents are live the rounds are
+// VALU-bound and a deeper tree amortizes the per-pixel work over more candidates: the tree is always depth 3
+// (SG_SPEC_LIVE >= 0 would keep single-node trees while more than that many descents are live).
+constexpr int SG_SPEC_LIVE = -1;
 __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
-                                                          unsigned long long *err, int32_t *cand, int32_t *items,
-                                                          int32_t *cnt, int first) {
+                                                          unsigned long long *err, int32_t *cand, uint32_t *candm,
+                                                          int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
+                                                          int32_t *cnt, int first, int stamp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Descent d = ds[i];
     if (d.done) return;
-    if (!first) d.report((int64_t)err[i]);
-    err[i] = 0;
-    if (d.next()) {
-        // svt_decode_xq (EbRestoration.c:634-646)
-        const int x0 = d.val[0][0], x1 = d.val[0][1], r0 = c_sgr_r[d.ep][0], r1 = c_sgr_r[d.ep][1];
-        cand[2 * i]     = r0 == 0 ? 0 : x0;
-        cand[2 * i + 1] = r0 == 0 ? 128 - x1 : r1 == 0 ? 0 : 128 - x0 - x1;
-        const int t0 = tile0[d.unit], nt = tile0[d.unit + 1] - t0, pos = atomicAdd(&cnt[0], nt);
-        for (int j = 0; j < nt; j++) items[pos + j] = (t0 + j) * 16 + d.k;
+    unsigned long long *e = err + (size_t)i * SG_NC;
+    if (first) {
+        d.next(); // the seed itself is the first candidate
+    } else {
+        const uint32_t evaluated = candm[i];
+        for (int node = 0;;) {
+            const int64_t v     = (int64_t)e[node];
+            const bool    worse = !d.init && v > d.err;
+            d.report(v);
+            if (!d.next()) break;
+            node = 2 * node + (worse ? 1 : 2);
+            if (node >= SG_NC || !(evaluated >> node & 1)) break;
+        }
+    }
+    for (int c = 0; c < SG_NC; c++) e[c] = 0;
+    if (!d.done) {
+        const int depth_nodes = (SG_SPEC_LIVE >= 0 && (first || cnt_cur[1] > SG_SPEC_LIVE)) ? 1 : SG_NC; // nodes
+        Descent   tree[SG_NC / 2];
+        uint32_t  mask = 1;
+        int32_t  *cd   = cand + (size_t)i * SG_NC * 2;
+        decode_xq(d, cd);
+        tree[0] = d;
+        for (int nd = 0; nd < SG_NC / 2; nd++) {
+            if (!(mask >> nd & 1) || 2 * nd + 1 >= depth_nodes) continue;
+            for (int w = 1; w >= 0; w--) {
+                if (w && tree[nd].init) continue; // the seed's outcome does not steer the descent
+                Descent c = tree[nd];
+                c.report_outcome(w != 0, 0);
+                if (!c.next()) continue;
+                const int ch = 2 * nd + (w ? 1 : 2);
+                decode_xq(c, cd + 2 * ch);
+                mask |= 1u << ch;
+                if (ch < SG_NC / 2) tree[ch] = c;
+            }
+        }
+        candm[i] = mask;
+        if (atomicExch(&ustamp[d.unit], stamp) != stamp) { // the unit's tiles are listed once per round
+            const int t0 = tile0[d.unit], nt = tile0[d.unit + 1] - t0, pos = atomicAdd(&cnt[0], nt);
+            for (int j = 0; j < nt; j++) items[pos + j] = t0 + j;
+        }
         atomicAdd(&cnt[1], 1);
+    } else {
+        candm[i] = 0;
     }
     ds[i] = d;
 }
@@ -844,9 +1000,9 @@ __global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, i
             d.cont  = !cfg.wn_max_one_step;
             d.nf = 2, d.p_lo = (7 - win) >> 1, d.p_hi = 2;
             for (int t = 0; t < 3; t++) {
-                d.lo[t] = c_tap_min[t], d.hi[t] = c_tap_max[t];
-                d.val[0][t] = w.hfilter[t]; // f = 0: hfilter, f = 1: vfilter (the reference's order)
-                d.val[1][t] = w.vfilter[t];
+                d.set_bounds(t, c_tap_min[t], c_tap_max[t]);
+                d.set_val(0, t, w.hfilter[t]); // f = 0: hfilter, f = 1: vfilter (the reference's order)
+                d.set_val(1, t, w.vfilter[t]);
             }
             d.begin();
         }
@@ -899,9 +1055,9 @@ __global__ void sgr_seed_kernel(const SearchArgs A, int nplanes, int npairs, con
     Descent d;
     d.unit = P.unit_base + ul, d.k = k, d.ep = ep;
     d.start = 2, d.end = cfg.sg_refine[p > 0] ? 1 : 4, d.cont = true, d.nf = 1, d.p_lo = 0, d.p_hi = 1;
-    d.lo[0] = PRJ_MIN0, d.hi[0] = PRJ_MAX0, d.lo[1] = PRJ_MIN1, d.hi[1] = PRJ_MAX1;
-    d.skip_p[0] = r0 == 0, d.skip_p[1] = r1 == 0;
-    d.val[0][0] = xd0, d.val[0][1] = xd1;
+    d.set_bounds(0, PRJ_MIN0, PRJ_MAX0), d.set_bounds(1, PRJ_MIN1, PRJ_MAX1);
+    d.skipm = (r0 == 0 ? 1u : 0u) | (r1 == 0 ? 2u : 0u);
+    d.set_val(0, 0, xd0), d.set_val(0, 1, xd1);
     d.begin();
     ds[i] = d;
 }
@@ -918,7 +1074,7 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
     int              bk   = 0;
     for (int k = 0; k < P.ne; k++)
         if (be == -1 || d[k].err < be) be = d[k].err, bk = k;
-    const int ep = P.eps[bk], x0 = d[bk].val[0][0], x1 = d[bk].val[0][1];
+    const int ep = P.eps[bk], x0 = d[bk].val(0, 0), x1 = d[bk].val(0, 1);
     best[4 * u]     = bk;
     best[4 * u + 1] = ep;
     best[4 * u + 2] = c_sgr_r[ep][0] == 0 ? 0 : x0;
@@ -1047,7 +1203,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     std::vector<int32_t> tile0;
     const int            win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
     int                  npairs = 0, n_wn = 0, nt_wn = 0, n_sg = 0, nt_sg = 0, sg_planes = 0;
-    size_t               flt_elems = 0, part_elems = 0, mh_elems = 0, n_sitems = 0;
+    size_t               flt_elems = 0, part_elems = 0, mh_elems = 0;
     for (int p = 0; p < nplanes; p++) {
         PlanePlan &q = pp[p];
         const int  W = rec->pw[p], H = rec->ph[p], usz = s->unit_size[p], ext = usz * 3 / 2, off = 8 >> (p > 0);
@@ -1085,11 +1241,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         if (q.sg) {
             n_sg += q.n, nt_sg += q.nt, sg_planes++;
-            flt_elems += (size_t)q.ne * 2 * W * H;
-            n_sitems += (size_t)q.nt * q.ne;
+            flt_elems += (size_t)q.ne * 2 * ((W + 63) & ~63) * H;
         }
     }
     tile0.push_back((int)tiles.size());
+    for (const Tile &t : tiles) // the projection kernel reads 4-pixel chunks
+        if ((t.x0 & 3) || (t.w & 3)) return SVTGPU_ERR_UNSUPPORTED;
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
     // ---- device scratch and pinned staging ----
     Carver       dc;
@@ -1097,9 +1254,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
     const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn);
     const size_t o_wds = dc(sizeof(Descent) * n_wn), o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
-                 o_witems = dc(4 * (size_t)nt_wn);
-    const size_t o_mom = dc(40 * (size_t)npairs), o_sds = dc(sizeof(Descent) * npairs), o_cand = dc(8 * (size_t)npairs),
-                 o_serr = dc(8 * (size_t)npairs), o_sitems = dc(4 * n_sitems), o_best = dc(16 * (size_t)n_sg),
+                 o_wact = dc(4 * (size_t)n_wn);
+    const size_t o_mom = dc(40 * (size_t)npairs), o_sds = dc(sizeof(Descent) * npairs),
+                 o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
+                 o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
                  o_sse2 = dc(8 * (size_t)n_sg), o_cnt = dc(32);
     Carver       hc;
     const size_t h_tiles = hc(sizeof(Tile) * nt_all), h_units = hc(sizeof(URect) * n_all), h_t0 = hc(4 * (n_all + 1));
@@ -1133,12 +1291,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     for (int p = 0; p < nplanes; p++) {
         PlaneArgs &P = A.pl[p];
         P.dgd = rec->plane[p], P.src = src->plane[p], P.dstride = rec->stride[p], P.sstride = src->stride[p];
-        P.W = rec->pw[p], P.H = rec->ph[p], P.bd = rec->bit_depth;
+        P.W = rec->pw[p], P.H = rec->ph[p], P.bd = rec->bit_depth, P.fstride = (P.W + 63) & ~63;
         P.flt       = s->d_flt + flt_off;
         P.unit_base = pp[p].unit_base, P.pair_base = pp[p].pair_base, P.ne = pp[p].ne;
         for (int k = 0; k < pp[p].ne; k++) P.eps[k] = pp[p].eps[k];
         P.win = pp[p].win, P.nval = pp[p].nval, P.mh_off = (int64_t)pp[p].mh_off;
-        if (pp[p].sg) flt_off += (size_t)pp[p].ne * 2 * P.W * P.H;
+        if (pp[p].sg) flt_off += (size_t)pp[p].ne * 2 * P.fstride * P.H;
     }
     A.tiles = (const Tile *)dp(o_tiles), A.units = (const URect *)dp(o_units), A.tile0 = (const int32_t *)dp(o_t0);
     auto *d_t0 = (int32_t *)dp(o_t0);
@@ -1189,22 +1347,24 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    auto *cnt = (int32_t *)dp(o_cnt); // [parity][wn items, wn live, sg items, sg live]
+    auto *cnt = (int32_t *)dp(o_cnt); // [parity][-, wn live, sg items, sg live]
     HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
     if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, st));
         hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
-                           d_t0, (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_witems), cnt, 1);
+                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), cnt, 1);
         HIP_TRY(hipGetLastError());
     }
     if (npairs) {
-        HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * (size_t)npairs, st));
+        HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * SG_NC * (size_t)npairs, st));
+        HIP_TRY(hipMemsetAsync(dp(o_ustamp), 0, 4 * (size_t)n_all, st));
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
                            npairs, d_t0, (unsigned long long *)dp(o_serr), (int32_t *)dp(o_cand),
-                           (int32_t *)dp(o_sitems), cnt + 2, 1);
+                           (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp), (int32_t *)dp(o_sitems),
+                           (const int32_t *)cnt + 6, cnt + 2, 1, 1);
         HIP_TRY(hipGetLastError());
     }
-    const int gw = std::max(1, std::min(nt_wn, 2048)), gs = (int)std::max<size_t>(1, std::min<size_t>(n_sitems, 4096));
+    const int gs = std::max(1, nt_sg);
     bool      wl = n_wn > 0, sl = npairs > 0;
     int32_t  *hcnt = (int32_t *)hp(h_cnt);
     int       g    = 0; // global round index
@@ -1212,20 +1372,20 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         for (int b = 0; b < ROUNDS_PER_BATCH; b++, g++) {
             int32_t *cur = cnt + 4 * (g & 1), *nxt = cnt + 4 * ((g + 1) & 1);
             if (wl) {
-                hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(gw), dim3(256), 0, st, A, (const int16_t *)dp(o_taps),
-                                   (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
-                                   (unsigned long long *)dp(o_werr));
+                hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt_wn), dim3(256), 0, st, A, (const int16_t *)dp(o_taps),
+                                   (const int32_t *)dp(o_wact), nxt, (unsigned long long *)dp(o_werr));
                 hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
-                                   (Descent *)dp(o_wds), n_wn, d_t0, (unsigned long long *)dp(o_werr),
-                                   (int16_t *)dp(o_taps), (int32_t *)dp(o_witems), nxt, 0);
+                                   (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps),
+                                   (int32_t *)dp(o_wact), nxt, 0);
             }
             if (sl) {
                 hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
                                    (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
-                                   (unsigned long long *)dp(o_serr));
+                                   (const uint32_t *)dp(o_candm), (unsigned long long *)dp(o_serr));
                 hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
                                    (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
-                                   (int32_t *)dp(o_cand), (int32_t *)dp(o_sitems), nxt + 2, 0);
+                                   (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
+                                   (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, g + 2);
             }
         }
         HIP_TRY(hipGetLastError());
@@ -1269,8 +1429,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             if (q.wn && wu[gu].type) {
                 R.sse[1] = hw[gu].err;
                 R.wiener = wu[gu];
-                set_wiener_taps(R.wiener.hfilter, hw[gu].val[0]);
-                set_wiener_taps(R.wiener.vfilter, hw[gu].val[1]);
+                int v[3];
+                hw[gu].taps(0, v), set_wiener_taps(R.wiener.hfilter, v);
+                hw[gu].taps(1, v), set_wiener_taps(R.wiener.vfilter, v);
             }
             if (q.sg) {
                 const Descent *d  = hs + q.pair_base + u * q.ne;
@@ -1279,7 +1440,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 for (int k = 0; k < q.ne; k++)
                     if (be == -1 || d[k].err < be) be = d[k].err, bk = k;
                 R.sgrproj.type = SVTGPU_RESTORE_SGRPROJ, R.sgrproj.ep = q.eps[bk];
-                R.sgrproj.xqd[0] = d[bk].val[0][0], R.sgrproj.xqd[1] = d[bk].val[0][1];
+                R.sgrproj.xqd[0] = d[bk].val(0, 0), R.sgrproj.xqd[1] = d[bk].val(0, 1);
                 R.sse[2] = (int64_t)sse2[gu];
             }
         }
