@@ -20,7 +20,10 @@ N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the DLF 
 (every rank deblocks the whole frame: its level search needs whole-frame SSEs); the CDEF frame is
 tiled into bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and
 skip flags are all-reduce-summed over RCCL (zeros outside each band), every rank runs the
-(replicated, deterministic) pick and applies its band — strong scaling of one frame per step.
+(replicated, deterministic) pick and applies its band; the LR search is split by unit rows (each rank
+searches its units, the per-unit records are all-gathered over RCCL and every rank runs the host RD
+finish, then the replicated apply); the MD batch is split by superblock ranges (no exchange) — strong
+scaling of one frame per step.
 
 Prints ONE JSON line on rank 0 (contract in the task description): value = luma Mpixels/s of the
 whole job, plus `roofline` for the dominant kernel (timed with HIP events on the stream it runs
@@ -54,12 +57,14 @@ def parse():
     ap.add_argument("--cdef-level", type=int, default=1)
     ap.add_argument("--base-q-idx", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="no HIP-event timing inside the LR search")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
     return ap.parse_args()
 
 
-def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, sample):
-    """The repo's scalar C restatement (oracle/) on one host core over a crop of the same frame."""
+def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, sample, lr_ctrls, lr_us, md_refs, md_mvs):
+    """The repo's scalar C restatement (oracle/) on one host core over a crop of the same frame: the same
+    stages as the GPU step (DLF pick + filter, CDEF search + pick + apply, LR search + apply, MD batch)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: used here only as the reported CPU baseline
     sw, sh = (int(x) for x in sample.split("x"))
@@ -74,11 +79,19 @@ def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, sample):
     crop = oracle.dlf_frame(crop, bd, mi_c, lfp)
     mse, skip, d, v = oracle.cdef_search_frame(crop, cs, bd, ctrls, q)
     prm, fbs = oracle.cdef_pick(sw, sh, mse, skip, ctrls, q, lam)
-    oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
+    cdef_out = oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
+    octrls = oracle.lr_controls(1, 1, rdmult=lr_ctrls.rdmult, switchable=tuple(lr_ctrls.switchable_restore_cost),
+                                wiener=tuple(lr_ctrls.wiener_restore_cost), sgrproj=tuple(lr_ctrls.sgrproj_restore_cost))
+    ft, units, _ = oracle.lr_search_frame(cdef_out, cs, bd, lr_us, octrls)
+    oracle.lr_apply_frame(crop, cdef_out, bd, ft, lr_us, units)
+    nsb = ((sw + 63) // 64) * ((sh + 63) // 64)
+    oracle.md_dist_batch(cs[0], [np.ascontiguousarray(r[:sh, :sw]) for r in md_refs],
+                         bd, np.ascontiguousarray(md_mvs[:nsb], np.int32))
     dt = time.perf_counter() - t0
     return {"value": round(sw * sh / dt / 1e6, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%dx%d crop of the same %d-bit frame, DLF pick+filter then CDEF search+pick+apply, cdef_level %d, scalar C "
-                      "restatement (oracle/), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
+            "sample": "%dx%d crop of the same %d-bit frame through the same stages (DLF pick+filter, CDEF "
+                      "search+pick+apply at cdef_level %d, LR search+apply at wn/sg level 1, MD batch 7 refs), scalar "
+                      "C restatement (oracle/), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
 
 
 def main():
@@ -116,14 +129,16 @@ def main():
                                   sgrproj=(250, 900))
     L = svtgpu.Frame(ctx, W, H, bd)
     NREF = 7
-    md_refs = []
+    md_refs, md_ref_y = [], []
     for r in range(NREF):
         rs, _ = synth.frame_pair(W, H, bd, seed=0x5EED0005 + 17 * (r + 1))
         f = svtgpu.Frame(ctx, W, H, bd)
         f.upload(rs, sp)
         md_refs.append(f)
+        md_ref_y.append(rs[0])
     md = svtgpu.MdBatch(ctx, W, H, NREF)
-    md.set_mvs(np.random.default_rng(5).integers(-16, 17, size=(md.nsb, NREF, 2)), sp)
+    md_mvs = np.random.default_rng(5).integers(-16, 17, size=(md.nsb, NREF, 2))
+    md.set_mvs(md_mvs, sp)
     ctrls = svtgpu.cdef_controls(a.cdef_level)
     st = svtgpu.CdefState(ctx, W, H)
     nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
@@ -135,12 +150,10 @@ def main():
         st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
 
     ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | lr | md)
-    if n > 1:  # MD batch: SB row bands, no collective
-        sbr = np.linspace(0, md.nsb, n + 1).round().astype(int)
-        md_range = (int(sbr[rank]), int(sbr[rank + 1]))
-    else:
-        md_range = (0, md.nsb)
+    md_range = svtgpu.band(md.nsb, n, rank)  # MD batch: SB ranges, no collective
+    lr_rb, lr_re = svtgpu.lr_unit_rows(lr.units, n, rank)  # LR search: unit-row bands, records all-gathered
     lf_levels = []
+    lr_prof = []  # per timed step: the LR search's per-kernel-class device times (HIP events on `stream`)
 
     def step(timed):
         es = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
@@ -166,7 +179,18 @@ def main():
         if timed:
             es[3].record(stream)
         # LR search + apply on the CDEF output (boundary lines from the DLF output)
-        lr_ft = lr.search(O, S, lr_ctrls, sp)
+        if n == 1:
+            lr_ft = lr.search(O, S, lr_ctrls, sp)
+        else:
+            recs = lr.search_units(O, S, lr_ctrls, lr_rb, lr_re, stream=sp)
+            recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, device="cuda")
+            lr_ft = []
+            for p in range(3):
+                ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])
+                lr.set_units(p, units_p, sp)
+                lr_ft.append(ftp)
+        if timed and not a.no_kernel_timing:
+            lr_prof.append(lr.profile(True))
         lr.apply(D, O, L, lr_ft, sp)
         if timed:
             es[4].record(stream)
@@ -178,6 +202,9 @@ def main():
 
     for _ in range(a.warmup):
         step(False)
+    # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
+    # of every launch; HIP-event packets around each of the ~100 launches per search cost ~20 us apiece)
+    lr.profile(not a.no_kernel_timing)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -199,6 +226,8 @@ def main():
 
     ms_per_step = dt * 1e3 / a.steps
     value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
+    lr_cls = {c: {k: float(np.mean([pr[c][k] for pr in lr_prof])) if lr_prof else 0.0
+                  for k in ("launches", "ms", "bytes")} for c in svtgpu.LrState.PROFILE_CLASSES}
     # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
     # recon + source read once (2*S*B) + per-FB outputs (mse 2x64 u64, dir 64 u8, var 64 i32, skip)
     S_samples = 1.5 * W * H
@@ -207,6 +236,25 @@ def main():
     alg_bytes = 2 * S_samples * B / n + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
     achieved = alg_bytes / (search_ms * 1e-3) / 1e9
     evals = nfb_band * 6144 * ctrls.strengths().__len__()  # (sample, strength) filter evaluations
+    roof = {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None, "avg_launch_ms": round(search_ms, 4),
+            "note": "VALU-bound kernel (64 strengths per sample read); HBM fraction is low by "
+                    "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))}
+    lr_names = {"stats": "wiener_stats_kernel (+unit sums)", "sgr_filters": "sgr_flt_kernel",
+                "wiener_trials": "wiener_trial_kernel", "projection": "proj_err_kernel", "other": "lr descent kernels"}
+    dom = max(lr_cls, key=lambda c: lr_cls[c]["ms"])
+    if lr_cls[dom]["ms"] > search_ms:
+        c = lr_cls[dom]
+        ach = c["bytes"] / (c["ms"] * 1e-3) / 1e9
+        roof = {"kernel": lr_names[dom], "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
+                "avg_launch_ms": round(c["ms"] / max(c["launches"], 1), 5), "launches_per_step": c["launches"],
+                "ms_per_step": round(c["ms"], 4),
+                "note": "largest device-time kernel class of the step; launch durations from the device's "
+                        "s_memrealtime clock (first workgroup start to last workgroup end, every launch of the timed "
+                        "steps); achieved = algorithmic bytes (samples + filter planes touched) / device time; the "
+                        "class is VALU-bound, so its HBM fraction is low by construction"}
     out = {
         "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
         "value": round(value, 3),
@@ -220,24 +268,22 @@ def main():
         "vs_baseline": None,
         "dtype": "u16" if bd > 8 else "u8",
         "data": "synthetic",
-        "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply %dx%d %d-bit 4:2:0, dlf level 1 "
+        "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply -> lr_search+apply, + md batch; %dx%d %d-bit 4:2:0, dlf level 1 "
                                "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
                                "LR search+apply (RU 256/128, wn/sg level 1)"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
-                   "parallelism": "fb_row_bands%d" % n if n > 1 else "single",
+                   "parallelism": "row_bands%d (CDEF FB rows, LR unit rows, MD SBs; DLF replicated)" % n if n > 1 else "single",
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
                                 "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_search_apply": round(lr_ms, 4),
                                 "md_sad_sse_var": round(md_ms, 4)},
+                   "lr_search_kernel_ms": {c: round(v["ms"], 4) for c, v in lr_cls.items()},
                    "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
-        "roofline": {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": None, "avg_launch_ms": round(search_ms, 4),
-                     "note": "VALU-bound kernel (64 strengths per sample read); HBM fraction is low by "
-                             "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))},
+        "roofline": roof,
     }
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(src, rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(src, rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample, lr_ctrls,
+                                           lr_us, md_ref_y, md_mvs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if n > 1:

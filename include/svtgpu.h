@@ -507,6 +507,34 @@ typedef struct SvtGpuLrUnitSearch {
 int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                            const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
                            SvtGpuLrUnitSearch *const search_out[3], void *stream);
+/* Per-unit part of the search for a band of unit rows: the units of unit rows [row_begin[p], row_end[p]) of each
+ * searched plane (restoration_seg_search restricted to those units; every unit's search is independent of the
+ * others).  Writes those units' records into search_out[p] (arrays of all units of the plane, row-major; other
+ * entries untouched); no RD finish and the state's units are not changed.  The multi-GPU split of the search:
+ * every rank searches a band, the records are gathered and svtgpu_lr_finish_plane picks on every rank.
+ * Synchronous. */
+int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                           const SvtGpuLrSearchControls *ctrls, const int32_t row_begin[3], const int32_t row_end[3],
+                           SvtGpuLrUnitSearch *const search_out[3], void *stream);
+/* ≙ rest_finish_search of one plane (EbRestorationPick.c:1555-1634): the frame restoration type and the units'
+ * types/parameters (copy_unit_info) from the records of all `nunits` units of the plane.  Host only (no device
+ * work, usable without a GPU); returns SVTGPU_OK with *frame_type_out = NONE for a plane that is not searched. */
+int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
+                           const SvtGpuLrUnitSearch *records, int32_t *frame_type_out, SvtGpuRestUnit *units_out);
+/* Device-time profile of the last search by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
+ * + moments, 2 Wiener trials, 3 projection errors, 4 Wiener decomposition, descent advance rounds, SGR SSE.  Each
+ * launch is timed from its first workgroup's start to its last workgroup's end on the device's 100 MHz
+ * s_memrealtime clock (per-launch HIP event packets would cost more than these launches); bytes = algorithmic
+ * HBM bytes of the class (compulsory reads/writes of the samples and filter planes the launches touch). */
+typedef struct SvtGpuLrProfile {
+    int32_t launches[5];
+    float   ms[5];
+    double  bytes[5];
+} SvtGpuLrProfile;
+/* enable != 0 turns timing of the following searches on (0 off): a bit mask of the classes to time (bit c =
+ * class c; -1 = all); `last` (nullable) receives the profile of the last search made with timing on (untimed
+ * classes read 0). */
+int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *last);
 /* controls of wn_filter_lvl / sg_filter_lvl (EncModeConfig.c:1329-1445); rate fields are left zero */
 int svtgpu_lr_controls_for_level(int32_t wn_level, int32_t sg_level, SvtGpuLrSearchControls *c);
 

@@ -275,6 +275,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     (void)hipFree(s->d_flt);
     (void)hipFree(s->d_work);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
+    lr_profiler_destroy(s->prof);
     delete s;
 }
 

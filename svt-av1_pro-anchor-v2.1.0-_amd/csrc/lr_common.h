@@ -15,7 +15,9 @@ struct SvtGpuLrState {
     size_t          work_bytes;
     void           *h_pin;   // pinned host staging for the search's read-backs
     size_t          pin_bytes;
+    void           *prof;    // per-kernel-class timing of the search (svtgpu_lr_profile), nullptr when off
 };
+void lr_profiler_destroy(void *prof);
 
 namespace {
 

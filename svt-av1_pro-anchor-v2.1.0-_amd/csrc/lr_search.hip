@@ -73,6 +73,22 @@ __device__ inline unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+// Kernel timing for svtgpu_lr_profile: with a slot `tk`, the earliest workgroup start (atomicMin) and the latest
+// workgroup end (atomicMax, at tk + PROF_NL * PROF_SP) of a launch on the 100 MHz s_memrealtime clock, spread over
+// PROF_SP addresses by workgroup index so that thousands of workgroups do not contend on one line -- the launch's
+// device duration without per-launch event packets (which cost far more than these launches).
+constexpr int PROF_NL = 512, PROF_SP = 64;
+#define PROF_BEGIN(tk)                                                                                      \
+    if ((tk) && threadIdx.x == 0)                                                                           \
+    atomicMin((tk) + (blockIdx.x & (PROF_SP - 1)), (unsigned long long)__builtin_amdgcn_s_memrealtime())
+#define PROF_END(tk)                                                                                        \
+    if (tk) {                                                                                               \
+        __syncthreads();                                                                                    \
+        if (threadIdx.x == 0)                                                                               \
+            atomicMax((tk) + PROF_NL * PROF_SP + (blockIdx.x & (PROF_SP - 1)),                              \
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());                                \
+    }
+
 typedef short v2i16 __attribute__((ext_vector_type(2)));
 __device__ inline int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
@@ -96,7 +112,8 @@ __device__ inline void load4s(const int16_t *p, int *v) {
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsigned long long *sum,
-                                                        unsigned long long *sse) {
+                                                        unsigned long long *sse, unsigned long long *tk) {
+    PROF_BEGIN(tk);
     const Tile       t = A.tiles[blockIdx.x];
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
@@ -113,6 +130,7 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
         atomicAdd(&sum[t.unit], ps);
         atomicAdd(&sse[t.unit], pe);
     }
+    PROF_END(tk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -136,7 +154,9 @@ __device__ inline void off_pair(int win, int q, int *c1, int *c2) { // q-th (c1 
 
 template <typename T, int WIN>
 __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, int tile_begin,
-                                                           const unsigned long long *sum, long long *part) {
+                                                           const unsigned long long *sum, long long *part,
+                                                           unsigned long long *tk) {
+    PROF_BEGIN(tk);
     using C = StatsCfg<WIN>;
     constexpr int NVAL = (C::NPAIR + 1) * 49;
     __shared__ int lds[256 * ST_SLOTS]; // staging (D pairs, S pairs), then the lane partials
@@ -230,17 +250,20 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
         for (int l = 0; l < nl; l++) v += lds[slot * 256 + lane0 + l];
         out[oi] = v;
     }
+    PROF_END(tk);
 }
 
 // per unit: sum the tile partials (tiles of a unit are contiguous in the tile list)
 __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_tile0, int tile_begin, int nvals,
-                                    long long *out) {
+                                    long long *out, unsigned long long *tk) {
+    PROF_BEGIN(tk);
     const int u = blockIdx.x, t0 = unit_tile0[u] - tile_begin, t1 = unit_tile0[u + 1] - tile_begin;
     for (int k = threadIdx.x; k < nvals; k += blockDim.x) {
         long long s = 0;
         for (int t = t0; t < t1; t++) s += part[(size_t)t * nvals + k];
         out[(size_t)u * nvals + k] = s;
     }
+    PROF_END(tk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -256,13 +279,17 @@ __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF
 template <typename T>
 __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
                                                            const int32_t *wact, int32_t *cnt_next,
-                                                           unsigned long long *err) {
+                                                           unsigned long long *err, unsigned long long *pc,
+                                                           unsigned long long *tk) {
+    PROF_BEGIN(tk);
     constexpr int VS = 72;
     __shared__ __align__(16) uint16_t v[71 * VS];
     __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[1] = 0; // the next advance counts its live descents there
     const Tile t = A.tiles[blockIdx.x];
     if (!wact[t.unit]) return;
+    if (pc && threadIdx.x == 0) // profiling: evaluated pixels (spread over PROF_SP counters)
+        atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), (unsigned long long)(t.w * t.h));
     const PlaneArgs &P  = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     const int16_t   *tp = taps + t.unit * 16;
@@ -325,6 +352,7 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
         }
     e = wave_sum(e);
     if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
+    PROF_END(tk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -334,7 +362,8 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
 // ---------------------------------------------------------------------------------------------
 constexpr int SG_V = 70, SG_B = 66, SG_NT = 512, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
 template <typename T>
-__global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long long *mom) {
+__global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long long *mom, unsigned long long *tk) {
+    PROF_BEGIN(tk);
     __shared__ uint16_t v[SG_V * SG_V];
     __shared__ int      ab1[SG_B * SG_B], ab2[SG_B * SG_B];
     __shared__ int      xby[256];
@@ -448,6 +477,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
         }
         __syncthreads(); // the next ep rewrites the A/B maps
     }
+    PROF_END(tk);
 }
 
 // projection errors of the candidate trees of every listed tile: the tile's CDEF and source pixels are read once
@@ -458,14 +488,18 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
 template <typename T>
 __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
                                                        int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
-                                                       unsigned long long *err) {
+                                                       unsigned long long *err, unsigned long long *pc,
+                                                       unsigned long long *tk) {
+    PROF_BEGIN(tk);
     const int n = cnt[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
-    constexpr int NCH = 4; // chunks per lane (64 rows x 16 chunks / 256 lanes)
+    constexpr int      NCH   = 4;
+    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated // chunks per lane (64 rows x 16 chunks / 256 lanes)
     for (int it = blockIdx.x; it < n; it += gridDim.x) {
         const Tile       t = A.tiles[items[it]];
         const PlaneArgs &P = A.pl[t.plane];
         const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne, cw = t.w >> 2;
+        npx_t += t.w * t.h; // profiling
         const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
         const size_t     pn = (size_t)P.fstride * P.H;
         uint32_t         px2[NCH][4]; // (x, x - src) per pixel
@@ -488,6 +522,7 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
             const int      pair = pb + e;
             const uint32_t mask = candm[pair];
             if (!mask) continue;
+            npx_e += t.w * t.h; // profiling
             uint32_t xq[SG_NC];
 #pragma unroll
             for (int c = 0; c < SG_NC; c++)
@@ -522,11 +557,18 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
             }
         }
     }
+    if (pc && threadIdx.x == 0 && npx_t) {
+        atomicAdd(pc + PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_e);
+        atomicAdd(pc + 2 * PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_t);
+    }
+    PROF_END(tk);
 }
 
 // SSE of the chosen self-guided output (apply_selfguided_restoration: projection, int16 wrap, clip)
 template <typename T>
-__global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const int32_t *best, unsigned long long *err) {
+__global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const int32_t *best, unsigned long long *err,
+                                                      unsigned long long *tk) {
+    PROF_BEGIN(tk);
     const Tile       t = A.tiles[blockIdx.x];
     const PlaneArgs &P = A.pl[t.plane];
     const int       *b = best + t.unit * 4; // {ep index, ep, xq0, xq1}
@@ -550,6 +592,7 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
     }
     acc = wave_sum(acc);
     if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], acc);
+    PROF_END(tk);
 }
 
 // =============================================================================================
@@ -847,10 +890,8 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
 // the other one, the advance kernel fills it).
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
-                                                             int16_t *taps, int32_t *wact, int32_t *cnt, int first) {
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n) return;
+__device__ void wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
+                                   int32_t *cnt, int first) {
     Descent d = ds[u];
     if (d.done) return;
     if (!first) d.report((int64_t)err[u]);
@@ -864,6 +905,15 @@ __global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n,
         atomicAdd(&cnt[1], 1);
     }
     ds[u] = d;
+}
+
+__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
+                                                             int16_t *taps, int32_t *wact, int32_t *cnt, int first,
+                                                             unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < n) wiener_advance_one(ds, u, err, taps, wact, cnt, first);
+    PROF_END(tk);
 }
 
 // svt_decode_xq (EbRestoration.c:634-646): xq of the ep's absent filter is 0
@@ -884,12 +934,9 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 // VALU-bound and a deeper tree amortizes the per-pixel work over more candidates: the tree is always depth 3
 // (SG_SPEC_LIVE >= 0 would keep single-node trees while more than that many descents are live).
 constexpr int SG_SPEC_LIVE = -1;
-__global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
-                                                          unsigned long long *err, int32_t *cand, uint32_t *candm,
-                                                          int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
-                                                          int32_t *cnt, int first, int stamp) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ void sgr_advance_one(Descent *ds, int i, const int32_t *tile0, unsigned long long *err, int32_t *cand,
+                                uint32_t *candm, int32_t *ustamp, int32_t *items, const int32_t *cnt_cur, int32_t *cnt,
+                                int first, int stamp) {
     Descent d = ds[i];
     if (d.done) return;
     unsigned long long *e = err + (size_t)i * SG_NC;
@@ -939,6 +986,16 @@ __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, co
     ds[i] = d;
 }
 
+__global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
+                                                          unsigned long long *err, int32_t *cand, uint32_t *candm,
+                                                          int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
+                                                          int32_t *cnt, int first, int stamp, unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) sgr_advance_one(ds, i, tile0, err, cand, candm, ustamp, items, cnt_cur, cnt, first, stamp);
+    PROF_END(tk);
+}
+
 // ---------------------------------------------------------------------------------------------
 // descent seeds on the device
 // ---------------------------------------------------------------------------------------------
@@ -955,7 +1012,9 @@ __device__ inline int unit_plane(const SearchArgs &A, int nplanes, int u) {
 // wiener_decompose_sep_sym + finalize + compute_score (EbRestorationPick.c:906-1040, 1337-1419), one workgroup
 // per unit; the unit's descent starts from the finalized taps unless the score says the filter does not help
 __global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, int nplanes, const int64_t *mh,
-                                                           const SeedCfg cfg, Descent *ds, SvtGpuRestUnit *wu) {
+                                                           const SeedCfg cfg, Descent *ds, SvtGpuRestUnit *wu,
+                                                           unsigned long long *tk) {
+    PROF_BEGIN(tk);
     __shared__ WienerSolveLds L;
     const int        u = blockIdx.x, tid = threadIdx.x;
     const PlaneArgs &P = A.pl[unit_plane(A, nplanes, u)];
@@ -1009,6 +1068,7 @@ __global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, i
         ds[u] = d;
         wu[u] = w;
     }
+    PROF_END(tk);
 }
 
 // svt_get_proj_subspace_c (:417-500) from the exact integer moments, encode_xq (:502-518), and the descent of
@@ -1087,6 +1147,48 @@ struct Carver {
         const size_t o = off;
         off += (bytes + 255) & ~(size_t)255;
         return o;
+    }
+};
+
+// device-clock timing of the search's launches by kernel class (svtgpu_lr_profile)
+struct LrProfiler {
+    unsigned long long *d_clk = nullptr; // [PROF_NL][PROF_SP] workgroup starts (min), then the same of ends (max)
+    unsigned long long *d_px  = nullptr; // [3][PROF_SP] evaluated pixels: trials, projection (pixel, ep), projection tiles
+    int                 nl = 0, cls[PROF_NL];
+    SvtGpuLrProfile     cur{}, last{};
+    bool                ok   = false;
+    int32_t             mask = 31; // classes timed (bit c)
+    LrProfiler() {
+        ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess;
+    }
+    ~LrProfiler() {
+        (void)hipFree(d_clk);
+        (void)hipFree(d_px);
+    }
+    void start(hipStream_t st) {
+        nl = 0;
+        std::memset(&cur, 0, sizeof cur);
+        (void)hipMemsetAsync(d_clk, 0xFF, 8 * PROF_NL * PROF_SP, st);
+        (void)hipMemsetAsync(d_clk + PROF_NL * PROF_SP, 0, 8 * PROF_NL * PROF_SP, st);
+        (void)hipMemsetAsync(d_px, 0, 24 * PROF_SP, st);
+    }
+    // the timing slot of one launch of class c (nullptr: not timed)
+    unsigned long long *slot(int c) {
+        if (!(mask >> c & 1) || nl >= PROF_NL) return nullptr;
+        cls[nl] = c;
+        cur.launches[c]++;
+        return d_clk + PROF_SP * nl++;
+    }
+    void finish() { // after the stream is synchronized
+        std::vector<unsigned long long> h(2 * PROF_NL * PROF_SP);
+        if (hipMemcpy(h.data(), d_clk, 16 * PROF_NL * PROF_SP, hipMemcpyDeviceToHost) == hipSuccess)
+            for (int i = 0; i < nl; i++) {
+                unsigned long long t0 = ~0ull, t1 = 0;
+                for (int k = 0; k < PROF_SP; k++)
+                    t0 = std::min(t0, h[i * PROF_SP + k]), t1 = std::max(t1, h[(PROF_NL + i) * PROF_SP + k]);
+                if (t0 != ~0ull && t1 >= t0) cur.ms[cls[i]] += (float)((t1 - t0) * 1e-5);
+            }
+        last = cur;
     }
 };
 
@@ -1183,9 +1285,18 @@ void launch_stats(int win, Fn &&f) {
 
 constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
 
+// plane p's Wiener window for the controls
+int plane_win(const SvtGpuLrSearchControls *c, int p) {
+    const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
+    return p == 0 ? win_l : std::min(win_l, 5);
+}
+
+// The search of the units in unit rows [rb[p], re[p]) of planes 0..nplanes-1.  frame_type != nullptr: the band
+// is the whole frame and the RD finish runs and sets the state's units.
 template <typename T>
 int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *src, const SvtGpuLrSearchControls *c,
-                 int nplanes, int32_t *frame_type, SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
+                 int nplanes, const int32_t *rb, const int32_t *re, int32_t *frame_type,
+                 SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
     // SVTGPU_LR_TIMING=1 prints the host-side phase times (wall clock, including the waits) to stderr
     static const bool timing = std::getenv("SVTGPU_LR_TIMING") != nullptr;
     auto              clk    = [] { return std::chrono::steady_clock::now(); };
@@ -1200,33 +1311,36 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     PlanePlan            pp[3];
     std::vector<URect>   units;
     std::vector<Tile>    tiles;
-    std::vector<int32_t> tile0;
-    const int            win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
+    std::vector<int32_t> tile0, uloc; // uloc: plane-local index of every global unit
     int                  npairs = 0, n_wn = 0, nt_wn = 0, n_sg = 0, nt_sg = 0, sg_planes = 0;
     size_t               flt_elems = 0, part_elems = 0, mh_elems = 0;
     for (int p = 0; p < nplanes; p++) {
         PlanePlan &q = pp[p];
         const int  W = rec->pw[p], H = rec->ph[p], usz = s->unit_size[p], ext = usz * 3 / 2, off = 8 >> (p > 0);
         q.unit_base = (int)units.size(), q.tile_base = (int)tiles.size();
-        for (int y0 = 0; y0 < H;) {
+        int urow = 0, uidx = 0;
+        for (int y0 = 0; y0 < H; urow++) {
             const int uh = (H - y0 < ext) ? H - y0 : usz;
             int       vs = std::max(0, y0 - off), ve = y0 + uh;
             if (ve < H) ve -= off;
-            for (int x0 = 0; x0 < W;) {
+            for (int x0 = 0; x0 < W; uidx++) {
                 const int uw = (W - x0 < ext) ? W - x0 : usz;
-                tile0.push_back((int)tiles.size());
-                for (int y = vs; y < ve; y += 64)
-                    for (int x = x0; x < x0 + uw; x += 64)
-                        tiles.push_back({p, (int)units.size(), x, y, std::min(64, x0 + uw - x), std::min(64, ve - y)});
-                units.push_back({x0, x0 + uw, vs, ve});
+                if (urow >= rb[p] && urow < re[p]) {
+                    tile0.push_back((int)tiles.size());
+                    for (int y = vs; y < ve; y += 64)
+                        for (int x = x0; x < x0 + uw; x += 64)
+                            tiles.push_back({p, (int)units.size(), x, y, std::min(64, x0 + uw - x), std::min(64, ve - y)});
+                    units.push_back({x0, x0 + uw, vs, ve});
+                    uloc.push_back(uidx);
+                }
                 x0 += uw;
             }
             y0 += uh;
         }
         q.n = (int)units.size() - q.unit_base, q.nt = (int)tiles.size() - q.tile_base;
-        if (q.n != s->hunits[p] * s->vunits[p]) return SVTGPU_ERR_INVALID_ARG;
+        if (urow != s->vunits[p] || uidx != s->hunits[p] * s->vunits[p]) return SVTGPU_ERR_INVALID_ARG;
         q.wn   = c->wn_enabled && (!p || c->wn_use_chroma);
-        q.win  = p == 0 ? win_l : std::min(win_l, 5);
+        q.win  = plane_win(c, p);
         q.nval = (q.win * (q.win + 1) / 2 + 1) * 49;
         if (c->sg_enabled && (!p || c->sg_use_chroma))
             for (int e = c->sg_start_ep[p > 0]; e < c->sg_end_ep[p > 0]; e += std::max(1, c->sg_ep_inc[p > 0]))
@@ -1248,6 +1362,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     for (const Tile &t : tiles) // the projection kernel reads 4-pixel chunks
         if ((t.x0 & 3) || (t.w & 3)) return SVTGPU_ERR_UNSUPPORTED;
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
+    if (n_all == 0) return SVTGPU_OK; // an empty band
     // ---- device scratch and pinned staging ----
     Carver       dc;
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1));
@@ -1301,6 +1416,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     A.tiles = (const Tile *)dp(o_tiles), A.units = (const URect *)dp(o_units), A.tile0 = (const int32_t *)dp(o_t0);
     auto *d_t0 = (int32_t *)dp(o_t0);
     // ---- phase 1: sums, Wiener statistics, self-guided filters and moments ----
+    LrProfiler         *prof = (LrProfiler *)s->prof;
+    unsigned long long *pc   = prof ? prof->d_px : nullptr;
+    auto                run  = [&](int c, auto &&launch) { launch(prof ? prof->slot(c) : nullptr); };
+    if (prof) prof->start(st);
     std::memcpy(hp(h_tiles), tiles.data(), sizeof(Tile) * nt_all);
     std::memcpy(hp(h_units), units.data(), sizeof(URect) * n_all);
     std::memcpy(hp(h_t0), tile0.data(), 4 * (n_all + 1));
@@ -1310,24 +1429,29 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipMemsetAsync(dp(o_sum), 0, 8 * (size_t)n_all, st));
     HIP_TRY(hipMemsetAsync(dp(o_sse), 0, 8 * (size_t)n_all, st));
     if (npairs) HIP_TRY(hipMemsetAsync(dp(o_mom), 0, 40 * (size_t)npairs, st));
-    hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
-                       (unsigned long long *)dp(o_sse));
+    run(0, [&](unsigned long long *tk) {
+        hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
+                           (unsigned long long *)dp(o_sse), tk);
+    });
     HIP_TRY(hipGetLastError());
     for (int p = 0; p < nplanes; p++) {
         const PlanePlan &q = pp[p];
         if (!q.wn) continue;
         long long *part = (long long *)dp(o_part) + q.part_off, *mh = (long long *)dp(o_mh) + q.mh_off;
-        launch_stats(q.win, [&](auto wc) {
-            hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, st, A,
-                               q.tile_base, (const unsigned long long *)dp(o_sum), part);
+        run(0, [&](unsigned long long *tk) {
+            launch_stats(q.win, [&](auto wc) {
+                hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, st, A,
+                                   q.tile_base, (const unsigned long long *)dp(o_sum), part, tk);
+            });
         });
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, st, (const long long *)part,
-                           (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh);
+        run(0, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, st, (const long long *)part,
+                               (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh, tk);
+        });
         HIP_TRY(hipGetLastError());
     }
     if (nt_sg) {
-        hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, (long long *)dp(o_mom));
+        run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, (long long *)dp(o_mom), tk); });
         HIP_TRY(hipGetLastError());
     }
     mark(0);
@@ -1336,13 +1460,17 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     cfg.wn_use_refinement = c->wn_use_refinement, cfg.wn_max_one_step = c->wn_max_one_refinement_step;
     cfg.sg_refine[0] = c->sg_refine[0], cfg.sg_refine[1] = c->sg_refine[1];
     if (n_wn) {
-        hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, st, A, nplanes, (const int64_t *)dp(o_mh), cfg,
-                           (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu));
+        run(4, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, st, A, nplanes, (const int64_t *)dp(o_mh),
+                               cfg, (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu), tk);
+        });
         HIP_TRY(hipGetLastError());
     }
     if (npairs) {
-        hipLaunchKernelGGL(sgr_seed_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, A, sg_planes, npairs,
-                           (const int64_t *)dp(o_mom), cfg, (Descent *)dp(o_sds));
+        run(4, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(sgr_seed_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, A, sg_planes, npairs,
+                               (const int64_t *)dp(o_mom), cfg, (Descent *)dp(o_sds));
+        });
         HIP_TRY(hipGetLastError());
     }
     mark(1);
@@ -1352,7 +1480,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, st));
         hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
-                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), cnt, 1);
+                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), cnt, 1,
+                           (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
     if (npairs) {
@@ -1361,7 +1490,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
                            npairs, d_t0, (unsigned long long *)dp(o_serr), (int32_t *)dp(o_cand),
                            (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp), (int32_t *)dp(o_sitems),
-                           (const int32_t *)cnt + 6, cnt + 2, 1, 1);
+                           (const int32_t *)cnt + 6, cnt + 2, 1, 1, (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
     const int gs = std::max(1, nt_sg);
@@ -1372,20 +1501,29 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         for (int b = 0; b < ROUNDS_PER_BATCH; b++, g++) {
             int32_t *cur = cnt + 4 * (g & 1), *nxt = cnt + 4 * ((g + 1) & 1);
             if (wl) {
-                hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt_wn), dim3(256), 0, st, A, (const int16_t *)dp(o_taps),
-                                   (const int32_t *)dp(o_wact), nxt, (unsigned long long *)dp(o_werr));
-                hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
-                                   (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps),
-                                   (int32_t *)dp(o_wact), nxt, 0);
+                run(2, [&](unsigned long long *tk) {
+                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt_wn), dim3(256), 0, st, A,
+                                       (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact), nxt,
+                                       (unsigned long long *)dp(o_werr), pc, tk);
+                });
+                run(4, [&](unsigned long long *tk) {
+                    hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
+                                       (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr),
+                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), nxt, 0, tk);
+                });
             }
             if (sl) {
-                hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
-                                   (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
-                                   (const uint32_t *)dp(o_candm), (unsigned long long *)dp(o_serr));
-                hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
-                                   (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
-                                   (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
-                                   (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, g + 2);
+                run(3, [&](unsigned long long *tk) {
+                    hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
+                                       (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
+                                       (const uint32_t *)dp(o_candm), (unsigned long long *)dp(o_serr), pc, tk);
+                });
+                run(4, [&](unsigned long long *tk) {
+                    hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
+                                       (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
+                                       (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
+                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, g + 2, tk);
+                });
             }
         }
         HIP_TRY(hipGetLastError());
@@ -1401,8 +1539,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         hipLaunchKernelGGL(sgr_best_kernel, dim3((n_sg + 255) / 256), dim3(256), 0, st, (const Descent *)dp(o_sds), A,
                            sg_planes, n_sg, (int32_t *)dp(o_best));
         HIP_TRY(hipMemsetAsync(dp(o_sse2), 0, 8 * (size_t)n_sg, st));
-        hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
-                           (unsigned long long *)dp(o_sse2));
+        run(4, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
+                               (unsigned long long *)dp(o_sse2), tk);
+        });
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(hp(h_sse2), dp(o_sse2), 8 * (size_t)n_sg, hipMemcpyDeviceToHost, st));
     }
@@ -1414,7 +1554,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     if (npairs) HIP_TRY(hipMemcpyAsync(hs, dp(o_sds), sizeof(Descent) * npairs, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     mark(3);
-    // ---- phase 5 (host): per-unit results and the RD finish ----
+    // ---- phase 5 (host): per-unit results and, for the whole frame, the RD finish ----
     const uint64_t                 *sse0 = (const uint64_t *)hp(h_sse), *sse2 = (const uint64_t *)hp(h_sse2);
     SvtGpuRestUnit                 *out  = (SvtGpuRestUnit *)hp(h_out);
     std::vector<SvtGpuLrUnitSearch> rs(n_all);
@@ -1443,12 +1583,35 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 R.sgrproj.xqd[0] = d[bk].val(0, 0), R.sgrproj.xqd[1] = d[bk].val(0, 1);
                 R.sse[2] = (int64_t)sse2[gu];
             }
+            if (search_out && search_out[p]) search_out[p][uloc[gu]] = R;
         }
-        finish_plane(c, p, q.win, rs.data() + q.unit_base, q.n, &frame_type[p], out + q.unit_base);
-        HIP_TRY(hipMemcpyAsync(s->d_units[p], out + q.unit_base, sizeof(SvtGpuRestUnit) * q.n, hipMemcpyHostToDevice, st));
-        if (search_out && search_out[p]) std::memcpy(search_out[p], rs.data() + q.unit_base, sizeof(SvtGpuLrUnitSearch) * q.n);
+        if (frame_type) { // whole frame: units are in plane order, uloc[gu] == u
+            finish_plane(c, p, q.win, rs.data() + q.unit_base, q.n, &frame_type[p], out + q.unit_base);
+            HIP_TRY(hipMemcpyAsync(s->d_units[p], out + q.unit_base, sizeof(SvtGpuRestUnit) * q.n,
+                                   hipMemcpyHostToDevice, st));
+        }
     }
     HIP_TRY(hipStreamSynchronize(st));
+    if (prof) { // algorithmic bytes per class (sample bytes bps, filter planes int16)
+        unsigned long long px[3] = {0, 0, 0}, pxs[3 * PROF_SP];
+        HIP_TRY(hipMemcpy(pxs, prof->d_px, sizeof pxs, hipMemcpyDeviceToHost));
+        for (int k = 0; k < 3 * PROF_SP; k++) px[k / PROF_SP] += pxs[k];
+        const double bps = (double)sizeof(T);
+        double       all = 0, wn = 0, sgb = 0, sgp = 0;
+        for (int p = 0; p < nplanes; p++) {
+            double area = 0;
+            for (int i = pp[p].tile_base; i < pp[p].tile_base + pp[p].nt; i++) area += (double)tiles[i].w * tiles[i].h;
+            all += area;
+            if (pp[p].wn) wn += area;
+            if (pp[p].sg) sgb += area, sgp += area * pp[p].ne;
+        }
+        prof->cur.bytes[0] = (all + wn) * 2 * bps;                       // unit sums, statistics: x and source
+        prof->cur.bytes[1] = sgb * 2 * bps + sgp * 4;                     // x and source in, flt0/flt1 out
+        prof->cur.bytes[2] = (double)px[0] * 2 * bps;                     // x and source per evaluated pixel
+        prof->cur.bytes[3] = (double)px[1] * 4 + (double)px[2] * 2 * bps; // flt per (pixel, ep), x/source per tile
+        prof->cur.bytes[4] = sgb * (4 + 2 * bps);                         // the chosen ep's SSE
+        prof->finish();
+    }
     mark(4);
     if (timing)
         std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d) %.3f  best %.3f  finish %.3f\n",
@@ -1480,21 +1643,95 @@ extern "C" int svtgpu_lr_controls_for_level(int32_t wn, int32_t sg, SvtGpuLrSear
     return SVTGPU_OK;
 }
 
-extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
-                                      const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
-                                      SvtGpuLrUnitSearch *const search_out[3], void *stream) {
-    if (!s || !recon || !source || !ctrls || !frame_type_out || recon->width != s->width ||
-        recon->height != s->height || source->width != s->width || source->height != s->height ||
-        recon->bit_depth != source->bit_depth)
+void lr_profiler_destroy(void *prof) { delete (LrProfiler *)prof; }
+
+extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *last) {
+    if (!s) return SVTGPU_ERR_INVALID_ARG;
+    LrProfiler *pr = (LrProfiler *)s->prof;
+    if (last) {
+        if (pr)
+            *last = pr->last;
+        else
+            std::memset(last, 0, sizeof *last);
+    }
+    if (enable && !pr) {
+        pr = new LrProfiler();
+        if (!pr->ok) {
+            delete pr;
+            return SVTGPU_ERR_HIP;
+        }
+        s->prof = pr;
+    }
+    if (enable) {
+        pr->mask = enable < 0 ? 31 : enable & 31;
+    } else if (pr) {
+        delete pr;
+        s->prof = nullptr;
+    }
+    return SVTGPU_OK;
+}
+
+namespace {
+int check_search_args(const SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                      const SvtGpuLrSearchControls *ctrls) {
+    if (!s || !recon || !source || !ctrls || recon->width != s->width || recon->height != s->height ||
+        source->width != s->width || source->height != s->height || recon->bit_depth != source->bit_depth)
         return SVTGPU_ERR_INVALID_ARG;
     if (recon->bit_depth != 8 && recon->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
     for (int q = 0; q < 2; q++)
         if (ctrls->sg_enabled && (ctrls->sg_start_ep[q] < 0 || ctrls->sg_end_ep[q] > 16 || ctrls->sg_ep_inc[q] < 1))
             return SVTGPU_ERR_INVALID_ARG;
+    return SVTGPU_OK;
+}
+int searched_planes(const SvtGpuLrSearchControls *c) {
+    return ((c->wn_enabled && c->wn_use_chroma) || (c->sg_enabled && c->sg_use_chroma)) ? 3 : 1;
+}
+} // namespace
+
+extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                      const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
+                                      SvtGpuLrUnitSearch *const search_out[3], void *stream) {
+    if (!frame_type_out) return SVTGPU_ERR_INVALID_ARG;
+    if (int rc = check_search_args(s, recon, source, ctrls)) return rc;
     hipStream_t st      = pick_stream(s->ctx, stream);
-    const int   nplanes = ((ctrls->wn_enabled && ctrls->wn_use_chroma) || (ctrls->sg_enabled && ctrls->sg_use_chroma)) ? 3 : 1;
+    const int   nplanes = searched_planes(ctrls);
+    int32_t     rb[3] = {0, 0, 0}, re[3] = {s->vunits[0], s->vunits[1], s->vunits[2]};
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
     return recon->bytes_per_sample == 2
-        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, frame_type_out, search_out, st)
-        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, frame_type_out, search_out, st);
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, frame_type_out, search_out, st)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, frame_type_out, search_out, st);
+}
+
+extern "C" int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                      const SvtGpuLrSearchControls *ctrls, const int32_t row_begin[3],
+                                      const int32_t row_end[3], SvtGpuLrUnitSearch *const search_out[3],
+                                      void *stream) {
+    if (!row_begin || !row_end || !search_out) return SVTGPU_ERR_INVALID_ARG;
+    if (int rc = check_search_args(s, recon, source, ctrls)) return rc;
+    const int nplanes = searched_planes(ctrls);
+    for (int p = 0; p < nplanes; p++)
+        if (row_begin[p] < 0 || row_end[p] > s->vunits[p] || row_begin[p] > row_end[p] || !search_out[p])
+            return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    return recon->bytes_per_sample == 2
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, nullptr, search_out, st)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, nullptr, search_out, st);
+}
+
+extern "C" int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
+                                      const SvtGpuLrUnitSearch *records, int32_t *frame_type_out,
+                                      SvtGpuRestUnit *units_out) {
+    if (!ctrls || plane < 0 || plane > 2 || nunits <= 0 || !records || !frame_type_out || !units_out)
+        return SVTGPU_ERR_INVALID_ARG;
+    for (int u = 0; u < nunits; u++) { // the rate helpers index tables with these fields
+        const SvtGpuRestUnit &g = records[u].sgrproj;
+        if (g.ep < 0 || g.ep > 15) return SVTGPU_ERR_INVALID_ARG;
+    }
+    if (plane >= searched_planes(ctrls)) {
+        *frame_type_out = SVTGPU_RESTORE_NONE;
+        std::memset(units_out, 0, sizeof(SvtGpuRestUnit) * nunits);
+        return SVTGPU_OK;
+    }
+    finish_plane(ctrls, plane, plane_win(ctrls, plane), records, nunits, frame_type_out, units_out);
+    return SVTGPU_OK;
 }

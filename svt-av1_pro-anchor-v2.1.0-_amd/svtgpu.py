@@ -140,6 +140,7 @@ class LrSearchControls(ctypes.Structure):
                 ("sgrproj_restore_cost", ctypes.c_int32 * 2)]
 
 
+LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 5), ("ms", np.float32, 5), ("bytes", np.float64, 5)], align=True)
 LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYPE), ("sgrproj", REST_UNIT_DTYPE)],
                                 align=True)
 
@@ -243,6 +244,9 @@ _SIGS = {
     "svtgpu_lr_apply_frame": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "svtgpu_lr_search_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P, _P, _P]),
     "svtgpu_lr_controls_for_level": (ctypes.c_int, [_I32, _I32, ctypes.POINTER(LrSearchControls)]),
+    "svtgpu_lr_search_units": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P, _P, _P, _P]),
+    "svtgpu_lr_finish_plane": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _I32, _I32, _P, _P, _P]),
+    "svtgpu_lr_profile": (ctypes.c_int, [_P, _I32, _P]),
 }
 
 _lib = None
@@ -545,6 +549,36 @@ class LrState:
         check(lib().svtgpu_lr_search_frame(self.h, recon.h, source.h, ctypes.byref(ctrls), ptr(ft), rp, stream))
         return ([int(x) for x in ft], recs) if records else [int(x) for x in ft]
 
+    def search_units(self, recon, source, ctrls, row_begin, row_end, records=None, stream=None):
+        """svtgpu_lr_search_units: per-unit records of the unit rows [row_begin[p], row_end[p]) of every plane,
+        written into `records` (per-plane arrays of all units; allocated zeroed when None).  No RD finish."""
+        if records is None:
+            records = [np.zeros(hu * vu, LR_UNIT_SEARCH_DTYPE) for hu, vu in self.units]
+        rb = np.ascontiguousarray(row_begin, np.int32)
+        re_ = np.ascontiguousarray(row_end, np.int32)
+        rp = (ctypes.c_void_p * 3)(*[r.ctypes.data for r in records])
+        check(lib().svtgpu_lr_search_units(self.h, recon.h, source.h, ctypes.byref(ctrls), ptr(rb), ptr(re_), rp,
+                                           stream))
+        return records
+
+    PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other")
+
+    def profile(self, enable=True):
+        """svtgpu_lr_profile: HIP-event timing of the searches (enable: True = every class, a class name or a
+        list of names = those classes, False = off); returns the last timed search's per-class
+        {launches, ms, bytes} (kernel classes of svtgpu.h; untimed classes read 0)."""
+        if enable is True:
+            mask = -1
+        elif not enable:
+            mask = 0
+        else:
+            names = [enable] if isinstance(enable, str) else list(enable)
+            mask = sum(1 << self.PROFILE_CLASSES.index(c) for c in names)
+        raw = np.zeros(1, LR_PROFILE_DTYPE)
+        check(lib().svtgpu_lr_profile(self.h, mask, ptr(raw)))
+        return {c: {"launches": int(raw["launches"][0][i]), "ms": float(raw["ms"][0][i]),
+                    "bytes": float(raw["bytes"][0][i])} for i, c in enumerate(self.PROFILE_CLASSES)}
+
     def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
         ft = np.ascontiguousarray(frame_type, np.int32)
         check(lib().svtgpu_lr_apply_frame(self.h, deblocked.h, cdef_out.h, out.h, ptr(ft), stream))
@@ -573,6 +607,53 @@ def lr_controls(wn_level, sg_level, rdmult=0, switchable=(0, 0, 0), wiener=(0, 0
     for i, v in enumerate(sgrproj):
         c.sgrproj_restore_cost[i] = v
     return c
+
+
+def lr_finish_plane(ctrls, plane, records):
+    """svtgpu_lr_finish_plane (host only): (frame restoration type, units) of a plane from all its records."""
+    r = np.ascontiguousarray(records, LR_UNIT_SEARCH_DTYPE)
+    units = np.zeros(len(r), REST_UNIT_DTYPE)
+    ft = _I32()
+    check(lib().svtgpu_lr_finish_plane(ctypes.byref(ctrls), plane, len(r), ptr(r), ctypes.byref(ft), ptr(units)))
+    return ft.value, units
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-GPU decomposition (one rank per GPU): balanced bands of rows; the only data-path exchanges are
+# the CDEF mse/skip table all-reduce and the LR record all-gather
+# ---------------------------------------------------------------------------------------------
+def band(count, n, rank):
+    """[begin, end) of `rank`'s share of `count` rows split into `n` balanced contiguous bands."""
+    edges = np.linspace(0, count, n + 1).round().astype(int)
+    return int(edges[rank]), int(edges[rank + 1])
+
+
+def lr_unit_rows(units, n, rank):
+    """Per-plane unit-row bands (row_begin[3], row_end[3]) of `rank` for an LrState.units list [(hu, vu)]."""
+    rb, re_ = zip(*(band(vu, n, rank) for _, vu in units))
+    return list(rb), list(re_)
+
+
+def gather_lr_records(records, units, n, rank, group=None, device=None):
+    """All-gather the per-unit LR search records of every rank's unit-row band (torch.distributed; RCCL with
+    device="cuda", gloo with device=None).  `records`: per-plane arrays of all units with this rank's band
+    filled.  Returns the merged per-plane arrays (every unit from the rank that searched it)."""
+    import torch
+    import torch.distributed as dist
+    merged = []
+    for p, (hu, vu) in enumerate(units):
+        raw = torch.from_numpy(np.ascontiguousarray(records[p]).view(np.uint8).copy())
+        if device is not None:
+            raw = raw.to(device)
+        parts = [torch.empty_like(raw) for _ in range(n)]
+        dist.all_gather(parts, raw, group=group)
+        out = np.zeros(hu * vu, LR_UNIT_SEARCH_DTYPE)
+        for r in range(n):
+            b, e = band(vu, n, r)
+            got = parts[r].cpu().numpy().view(LR_UNIT_SEARCH_DTYPE)
+            out[b * hu:e * hu] = got[b * hu:e * hu]
+        merged.append(out)
+    return merged
 
 
 def plane_sse(a, b, plane, stream=None):

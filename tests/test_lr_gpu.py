@@ -167,3 +167,26 @@ def test_lr_search_vs_oracle(ctx, w, h, bd, usize, wn, sg, seed):
     got = O.download()
     for p in range(3):
         assert np.array_equal(got[p], want[p]), p
+
+
+@pytest.mark.parametrize("nb", [2, 3])
+def test_lr_search_units_bands(ctx, nb):
+    """svtgpu_lr_search_units over unit-row bands + svtgpu_lr_finish_plane == the whole-frame search (the
+    multi-GPU split of bench.py, run as bands on one device)."""
+    w, h, bd, usize = 640, 360, 10, 64
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0A00 + nb)
+    ctrls = oracle.lr_controls(1, 1, rdmult=7000, switchable=(300, 700, 900), wiener=(250, 800), sgrproj=(250, 900))
+    unit_size = [usize, usize >> 1, usize >> 1]
+    st, R, ft, recs = _gpu_search(ctx, rec, src, bd, unit_size, ctrls)
+    S = svtgpu.Frame(ctx, w, h, bd)
+    S.upload(src)
+    merged = None
+    for r in range(nb):
+        rb, re_ = svtgpu.lr_unit_rows(st.units, nb, r)
+        merged = st.search_units(R, S, ctrls, rb, re_, merged)
+    want_ft, want_units, _ = oracle.lr_search_frame(rec, src, bd, unit_size, ctrls)
+    for p in range(3):
+        assert merged[p].tobytes() == recs[p].tobytes(), p
+        fin_ft, fin_units = svtgpu.lr_finish_plane(ctrls, p, merged[p])
+        assert fin_ft == ft[p] == want_ft[p]
+        assert fin_units.tobytes() == want_units[p].tobytes(), p
