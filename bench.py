@@ -19,8 +19,9 @@ with hashed 4/8/16 transforms) and resident in HBM before timing.
 N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the DLF stage is replicated
 (every rank deblocks the whole frame: its level search needs whole-frame SSEs); the CDEF frame is
 tiled into bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and
-skip flags are all-reduce-summed over RCCL (zeros outside each band), every rank runs the
-(replicated, deterministic) pick and applies its band; the LR search is split by unit rows (each rank
+skip flags and the per-8x8 dir/var tables are all-reduce-summed over RCCL (zeros outside each band),
+every rank runs the (replicated, deterministic) pick and applies the whole frame (0.12 ms; the LR search
+bands below read all of it); the LR search is split by unit rows (each rank
 searches its units, the per-unit records are all-gathered over RCCL and every rank runs the host RD
 finish, then the replicated apply); the MD batch is split by superblock ranges (no exchange) — strong
 scaling of one frame per step.
@@ -144,10 +145,14 @@ def main():
     nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
     if n > 1:
         rows = np.linspace(0, nvfb, n + 1).round().astype(int)
-        st.set_fb_rows(int(rows[rank]), int(rows[rank + 1]))
+        cdef_rows = (int(rows[rank]), int(rows[rank + 1]))
+        st.set_fb_rows(*cdef_rows)
         mse_t = torch.zeros((2, st.nfb, 64), dtype=torch.int64, device="cuda")
         skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
+        dir_t = torch.zeros((st.nfb, 64), dtype=torch.uint8, device="cuda")
+        var_t = torch.zeros((st.nfb, 64), dtype=torch.int32, device="cuda")
         st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+        st.bind_dir_tables(dir_t.data_ptr(), var_t.data_ptr())
 
     ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | lr | md)
     md_range = svtgpu.band(md.nsb, n, rank)  # MD batch: SB ranges, no collective
@@ -172,10 +177,15 @@ def main():
         if timed:
             es[2].record(stream)
         if n > 1:
-            dist.all_reduce(mse_t)   # zero-padded band tables -> full frame table (RCCL over xGMI)
+            dist.all_reduce(mse_t)   # zero-padded band tables -> full frame tables (RCCL over xGMI)
             dist.all_reduce(skip_t)
+            dist.all_reduce(dir_t)
+            dist.all_reduce(var_t)
+            st.set_fb_rows(0, nvfb)  # every rank applies the whole frame: the LR search bands read all of O
         prm, _ = st.pick(ctrls, q, lam, sp)
         st.apply(D, O, prm, sp)
+        if n > 1:
+            st.set_fb_rows(cdef_rows[0], cdef_rows[1])
         if timed:
             es[3].record(stream)
         # LR search + apply on the CDEF output (boundary lines from the DLF output)

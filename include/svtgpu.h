@@ -186,6 +186,11 @@ int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32
  * state's own buffers.  svtgpu_cdef_clear_tables zeroes both (a band search then leaves zeros —
  * the identity of an all-reduce-sum — outside its rows). */
 int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, void *skip_dev);
+/* The same for the per-8x8 direction/variance tables the apply reuses: dir [nfb][64] uint8, var [nfb][64]
+ * int32 (zero outside a band after svtgpu_cdef_clear_tables, so an all-reduce-sum completes them and every
+ * rank can apply the whole frame). */
+int svtgpu_cdef_bind_dir_tables(SvtGpuCdefFrameState *s, void *dir_dev, void *var_dev);
+/* zeroes mse, skip, dir and var */
 int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream);
 
 /* Host views of the search results (synchronous). mse: [2][nfb][64] uint64, skip: [nfb] uint8,

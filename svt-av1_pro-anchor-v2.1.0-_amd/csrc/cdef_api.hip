@@ -127,6 +127,8 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
     HIP_TRY(hipMemset(s->d_skip, 1, nfb));
     s->own_mse      = s->d_mse;
     s->own_skip     = s->d_skip;
+    s->own_dir      = s->d_dir;
+    s->own_var      = s->d_var;
     s->fb_row_begin = 0;
     s->fb_row_end   = s->geo.nvfb;
     *out = s;
@@ -136,7 +138,8 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
 extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     if (!s)
         return;
-    void *bufs[] = {s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip, s->d_dir, s->d_var, s->d_fb_strength, s->d_pick_part,
+    void *bufs[] = {s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip,
+                    s->own_dir ? s->own_dir : s->d_dir, s->own_var ? (void *)s->own_var : (void *)s->d_var, s->d_fb_strength, s->d_pick_part,
                     s->d_pick_out, s->d_pick_lev, s->d_fb_list};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -159,12 +162,22 @@ extern "C" int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, v
     return SVTGPU_OK;
 }
 
+extern "C" int svtgpu_cdef_bind_dir_tables(SvtGpuCdefFrameState *s, void *dir_dev, void *var_dev) {
+    if (!s || (!dir_dev) != (!var_dev))
+        return SVTGPU_ERR_INVALID_ARG;
+    s->d_dir = dir_dev ? (uint8_t *)dir_dev : s->own_dir;
+    s->d_var = var_dev ? (int32_t *)var_dev : s->own_var;
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream) {
     if (!s)
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
     HIP_TRY(hipMemsetAsync(s->d_mse, 0, (size_t)s->nfb * 2 * 64 * 8, st));
     HIP_TRY(hipMemsetAsync(s->d_skip, 0, (size_t)s->nfb, st));
+    HIP_TRY(hipMemsetAsync(s->d_dir, 0, (size_t)s->nfb * 64, st));
+    HIP_TRY(hipMemsetAsync(s->d_var, 0, (size_t)s->nfb * 64 * 4, st));
     return SVTGPU_OK;
 }
 

@@ -277,8 +277,8 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
                     s += (unsigned long long)(d * d);
                 }
             }
-            for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-            if ((tid & 63) == 0) red[tid >> 6] = s;
+            s = wave_sum_lane63(s);
+            if ((tid & 63) == 63) red[tid >> 6] = s;
             __syncthreads();
             if (tid == 0) {
                 unsigned long long tot = 0;
@@ -309,8 +309,8 @@ __global__ __launch_bounds__(256) void plane_sse_kernel(const T *a, int as, cons
             const int d = (int)a[(size_t)r * as + c] - (int)b[(size_t)r * bs + c];
             s += (unsigned long long)(d * d);
         }
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    s = wave_sum_lane63(s);
+    if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
 }

@@ -32,6 +32,10 @@
 
 #include "lr_common.h"
 
+#ifndef SGR_EXP
+#define SGR_EXP 0 // development experiments on sgr_flt_kernel (0 = the real kernel)
+#endif
+
 namespace {
 
 struct Tile {
@@ -68,10 +72,9 @@ __device__ inline int px(const T *p, int stride, int W, int H, int y, int x) {
     return p[(size_t)y * stride + x];
 }
 
-__device__ inline unsigned long long wave_sum(unsigned long long v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    return v;
-}
+// wave total in lane 63 (svtgpu_internal.h)
+__device__ inline unsigned long long wave_sum(unsigned long long v) { return wave_sum_lane63(v); }
+constexpr int WAVE_LAST = 63;
 
 // Kernel timing for svtgpu_lr_profile: with a slot `tk`, the earliest workgroup start (atomicMin) and the latest
 // workgroup end (atomicMax, at tk + PROF_NL * PROF_SP) of a launch on the 100 MHz s_memrealtime clock, spread over
@@ -117,18 +120,17 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
     const Tile       t = A.tiles[blockIdx.x];
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    unsigned long long ps = 0, pe = 0;
+    uint32_t ps = 0, pe = 0; // <= 16 samples per lane: fits 32 bits
     for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
         const int y = t.y0 + i / t.w, x = t.x0 + i % t.w;
         const int dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
         ps += (unsigned)dv;
-        pe += (unsigned long long)((dv - sv) * (dv - sv));
+        pe += (uint32_t)((dv - sv) * (dv - sv));
     }
-    ps = wave_sum(ps);
-    pe = wave_sum(pe);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&sum[t.unit], ps);
-        atomicAdd(&sse[t.unit], pe);
+    const unsigned long long tsum = wave_sum_u32_wide(ps), tsse = wave_sum_u32_wide(pe);
+    if ((threadIdx.x & 63) == WAVE_LAST) {
+        atomicAdd(&sum[t.unit], tsum);
+        atomicAdd(&sse[t.unit], tsse);
     }
     PROF_END(tk);
 }
@@ -276,18 +278,23 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 // ---------------------------------------------------------------------------------------------
 __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16); }
 
+// wact[unit]: 0 no pending candidate; 1 full evaluation; a vertical-filter move (the candidate's hfilter is the
+// unit's current one): 2 the horizontal pass of that hfilter is cached per tile (tcache) -- only the vertical pass
+// runs; 3 not cached yet -- full evaluation that also stores its horizontal pass.
 template <typename T>
 __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
-                                                           const int32_t *wact, int32_t *cnt_next,
-                                                           unsigned long long *err, unsigned long long *pc,
-                                                           unsigned long long *tk) {
+                                                                const int32_t *wact, int32_t *cnt_next,
+                                                                unsigned long long *err, unsigned long long *pc,
+                                                                unsigned long long *tk, uint32_t *tcache) {
     PROF_BEGIN(tk);
     constexpr int VS = 72;
     __shared__ __align__(16) uint16_t v[71 * VS];
     __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[1] = 0; // the next advance counts its live descents there
-    const Tile t = A.tiles[blockIdx.x];
-    if (!wact[t.unit]) return;
+    const Tile t    = A.tiles[blockIdx.x];
+    const int  mode = wact[t.unit];
+    if (!mode) return;
+    uint32_t *tc = tcache + (size_t)blockIdx.x * 36 * 64; // this tile's cached horizontal pass
     if (pc && threadIdx.x == 0) // profiling: evaluated pixels (spread over PROF_SP counters)
         atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), (unsigned long long)(t.w * t.h));
     const PlaneArgs &P  = A.pl[t.plane];
@@ -302,6 +309,11 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
     const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
     const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
     const int      rows = t.h + 7, ng = (t.w + 8) >> 2, nyp = (t.h + 1) >> 1;
+    const WienerRound rr = wiener_round(P.bd);
+    if (mode == 2) {
+        for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = ((const uint4 *)tc)[i];
+        __syncthreads();
+    } else {
 #pragma unroll
     for (int k = 0; k < (71 * 18 + 255) / 256; k++) {
         const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
@@ -317,7 +329,6 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
         *(uint2 *)(v + r * VS + 4 * g) = make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
     }
     __syncthreads();
-    const WienerRound rr  = wiener_round(P.bd);
     const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
     uint16_t         *tq16 = (uint16_t *)tq;
     const int         xh   = 2 * (threadIdx.x & 31);
@@ -332,7 +343,11 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
             tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
         }
     __syncthreads();
-    unsigned long long e    = 0;
+    if (mode == 3) {
+        for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
+    }
+    }
+    uint32_t           e    = 0; // <= 32 outputs per lane: fits 32 bits
     const int          maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
     const int          x    = threadIdx.x & 63;
     if (x < t.w)
@@ -344,14 +359,14 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
             const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
             const T  *sp = s + (size_t)(t.y0 + y) * P.sstride + t.x0 + x;
             const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
-            e += (unsigned long long)(d0 * d0);
+            e += (uint32_t)(d0 * d0);
             if (y + 1 < t.h) {
                 const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[P.sstride];
-                e += (unsigned long long)(d1 * d1);
+                e += (uint32_t)(d1 * d1);
             }
         }
-    e = wave_sum(e);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], e);
+    const unsigned long long et = wave_sum_u32_wide(e);
+    if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], et);
     PROF_END(tk);
 }
 
@@ -360,12 +375,32 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
 // registers; per ep the A/B maps (packed B << 9 | A) go to LDS, the filters to HBM, and the projection moments
 // mom[pair] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} (u = x<<4, s = (src<<4) - u, g = flt - u) to int64 atomics.
 // ---------------------------------------------------------------------------------------------
-constexpr int SG_V = 70, SG_B = 66, SG_NT = 512, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
+constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
+
+// A, B of a self-guided pass from its box sums with 24-bit multiplies where the operands provably fit:
+// b <= 25*1023 >> (bd-8) < 2^24; a*n <= 1.64e6*25 < 2^32 with a < 2^24; (256-A)*sum <= 255*25575 < 2^24 and
+// times one_by_x (<= 455) < 2^32.  Only p*s wraps like the reference's u32 product and keeps the full multiply.
+__device__ inline void sgr_ab_fast(int sum, int sq, int n, int s, int bd, const int *x_by_xplus1, int *A, int *B) {
+    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
+    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
+    const uint32_t an = __umul24(a, (uint32_t)n), bb = __umul24(b, b);
+    const uint32_t p  = an < bb ? 0u : an - bb;
+    const uint32_t z  = (p * (uint32_t)s + (1u << 19)) >> 20;
+    *A                = x_by_xplus1[min(z, 255u)];
+    *B = (int)((__umul24(__umul24((uint32_t)(256 - *A), (uint32_t)sum), (uint32_t)c_one_by_x[n - 1]) + (1u << 11)) >> 12);
+}
+
 template <typename T>
 __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long long *mom, unsigned long long *tk) {
     PROF_BEGIN(tk);
+    // the lane's moment partials stay 32-bit over groups of 4 pixels: f <= 32767 (the filter's weighted A/B
+    // sums are bounded by 32 * 256 * 1023 + 32 * 261111 < 2^24 before the >> 9), so |g| = |f - (x<<4)| <= 32767,
+    // g^2 * 4 < 2^32 (unsigned) and |g * s| * 4 < 2^31 with |s| = |(src - x) << 4| <= 16368
+    static_assert(SG_NP % 4 == 0, "moment partials are flushed every 4 pixels");
     __shared__ uint16_t v[SG_V * SG_V];
-    __shared__ int      ab1[SG_B * SG_B], ab2[SG_B * SG_B];
+    // packed B << 9 | A (A <= 256, B < 2^19) of the r = 1 and r = 2 passes, double-buffered over eps: the maps of
+    // ep e + 1 are built while ep e is filtered, one barrier per ep
+    __shared__ int ab1[2][SG_B * SG_B], ab2[2][SG_B * SG_B];
     __shared__ int      xby[256];
     const Tile       t = A.tiles[blockIdx.x];
     const PlaneArgs &P = A.pl[t.plane];
@@ -407,25 +442,39 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
         }
     }
     const size_t pn = (size_t)P.fstride * P.H;
-    for (int e = 0; e < P.ne; e++) {
+    auto build_ab = [&](int e) { // A/B maps of ep index e into buffer e & 1
         const int ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        int      *m1 = ab1[e & 1], *m2 = ab2[e & 1];
 #pragma unroll
         for (int k = 0; k < SG_NQ; k++) {
             const int q = threadIdx.x + k * SG_NT;
             if (q >= nq) break;
             int a, b;
+#if SGR_EXP == 3
+            a = s1[k] & 255, b = q1[k] & 0xFFFF;
+            m1[q] = (b << 9) | a, m2[q] = (b << 9) | a;
+            continue;
+#endif
             if (r1) {
-                sgr_ab_from_sums(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
-                ab1[q] = (b << 9) | a;
+                sgr_ab_fast(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
+                m1[q] = (b << 9) | a;
             }
             if (r0 && ((q / bw - 1) & 1)) {
-                sgr_ab_from_sums(s2[k], q2[k], 25, c_sgr_s[ep][0], P.bd, xby, &a, &b);
-                ab2[q] = (b << 9) | a;
+                sgr_ab_fast(s2[k], q2[k], 25, c_sgr_s[ep][0], P.bd, xby, &a, &b);
+                m2[q] = (b << 9) | a;
             }
         }
-        __syncthreads();
+    };
+    build_ab(0);
+    __syncthreads();
+    for (int e = 0; e < P.ne; e++) {
+        if (e + 1 < P.ne) build_ab(e + 1);
+        const int  ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const int *ab1e = ab1[e & 1], *ab2e = ab2[e & 1];
         int16_t  *f0g = P.flt + (size_t)e * 2 * pn, *f1g = f0g + pn;
-        long long m[5] = {0, 0, 0, 0, 0};
+        uint32_t  m0 = 0, m1 = 0;   // sum g1^2, g2^2 over the current 4 pixels
+        int       m3 = 0, m4 = 0;   // sum g1*s, g2*s over the current 4 pixels
+        long long m2 = 0, M[4] = {0, 0, 0, 0}; // sum g1*g2; flushed 64-bit totals of m0, m1, m3, m4
 #pragma unroll
         for (int k = 0; k < SG_NP; k++) {
             const int i = threadIdx.x + k * SG_NT;
@@ -434,14 +483,14 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
             const size_t o = (size_t)(t.y0 + y) * P.fstride + t.x0 + x;
             int          g1 = 0, g2 = 0;
             if (r0) {
-                const int *Q = ab2 + c;
+                const int *Q = ab2e + c;
                 int        aa, bb, sh;
                 if (!(y & 1)) {
                     const int c6 = Q[-bw] + Q[bw], c5 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
                     const int a6 = (Q[-bw] & 511) + (Q[bw] & 511);
                     const int a5 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
                     aa = a6 * 6 + a5 * 5;
-                    bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5;
+                    bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5; // sums of packed words: exact (no carry into B)
                     sh = 9;
                 } else {
                     const int a6 = Q[0] & 511, a5 = (Q[-1] & 511) + (Q[1] & 511);
@@ -449,33 +498,51 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
                     bb = (Q[0] >> 9) * 6 + ((Q[-1] >> 9) + (Q[1] >> 9)) * 5;
                     sh = 8;
                 }
-                const int f = (aa * pix[k] + bb + (1 << (sh - 1))) >> sh;
+                const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << (sh - 1))) >> sh;
+#if SGR_EXP != 1
                 f0g[o]      = (int16_t)f;
+#endif
                 g1          = f - u;
             }
             if (r1) {
-                const int *Q  = ab1 + c;
+                const int *Q  = ab1e + c;
+                const int  c4 = Q[0] + Q[-1] + Q[1] + Q[-bw] + Q[bw], c3 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
                 const int  a4 = (Q[0] & 511) + (Q[-1] & 511) + (Q[1] & 511) + (Q[-bw] & 511) + (Q[bw] & 511);
                 const int  a3 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
-                const int  b4 = (Q[0] >> 9) + (Q[-1] >> 9) + (Q[1] >> 9) + (Q[-bw] >> 9) + (Q[bw] >> 9);
-                const int  b3 = (Q[-bw - 1] >> 9) + (Q[bw - 1] >> 9) + (Q[-bw + 1] >> 9) + (Q[bw + 1] >> 9);
-                const int  f  = ((a4 * 4 + a3 * 3) * pix[k] + b4 * 4 + b3 * 3 + (1 << 8)) >> 9;
-                f1g[o]        = (int16_t)f;
-                g2            = f - u;
+                const int  aa = a4 * 4 + a3 * 3, bb = ((c4 - a4) >> 9) * 4 + ((c3 - a3) >> 9) * 3;
+                const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9;
+#if SGR_EXP != 1
+                f1g[o]      = (int16_t)f;
+#endif
+                g2          = f - u;
             }
-            m[0] += (long long)g1 * g1;
-            m[1] += (long long)g2 * g2;
-            m[2] += (long long)g1 * g2;
-            m[3] += (long long)g1 * sv[k];
-            m[4] += (long long)g2 * sv[k];
+            m0 += (uint32_t)__mul24(g1, g1);
+            m1 += (uint32_t)__mul24(g2, g2);
+            m2 += (long long)__mul24(g1, g2);
+            m3 += __mul24(g1, sv[k]);
+            m4 += __mul24(g2, sv[k]);
+            if (SG_NP > 4 && (k & 3) == 3) {
+                M[0] += m0, M[1] += m1, M[2] += m3, M[3] += m4;
+                m0 = m1 = 0, m3 = m4 = 0;
+            }
         }
-        const int pair = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
+        M[0] += m0, M[1] += m1, M[2] += m3, M[3] += m4;
+        const int       pair  = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
+        // wave totals on 32-bit DPP adds over limbs; the moments an ep's filters cannot produce stay zero
+        unsigned long long tot[5] = {0, 0, 0, 0, 0};
+        if (SG_NP == 4) { // the lane partials are the (un-flushed) 32-bit sums
+            if (r0) tot[0] = wave_sum_u32_wide(m0), tot[3] = (unsigned long long)wave_sum_i32_wide(m3);
+            if (r1) tot[1] = wave_sum_u32_wide(m1), tot[4] = (unsigned long long)wave_sum_i32_wide(m4);
+        } else {
+            if (r0) tot[0] = wave_sum_u64_limbs(M[0]), tot[3] = wave_sum_u64_limbs(M[2]);
+            if (r1) tot[1] = wave_sum_u64_limbs(M[1]), tot[4] = wave_sum_u64_limbs(M[3]);
+        }
+        if (r0 && r1) tot[2] = wave_sum_u64_limbs((unsigned long long)m2);
+        if ((threadIdx.x & 63) == WAVE_LAST)
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const unsigned long long w = wave_sum((unsigned long long)m[k]);
-            if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&mom[(size_t)pair * 5 + k], w);
-        }
-        __syncthreads(); // the next ep rewrites the A/B maps
+            for (int k = 0; k < 5; k++)
+                if (tot[k]) atomicAdd((unsigned long long *)&mom[(size_t)pair * 5 + k], tot[k]);
+        __syncthreads(); // ep e + 2 rewrites this ep's buffer; ep e + 1's maps are complete
     }
     PROF_END(tk);
 }
@@ -552,8 +619,8 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
 #pragma unroll
             for (int c = 0; c < SG_NC; c++) {
                 if (!(mask >> c & 1)) continue;
-                const unsigned long long w = wave_sum(acc[c]);
-                if ((threadIdx.x & 63) == 0) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
+                const unsigned long long w = wave_sum_u32_wide(acc[c]); // <= 16 pixels per lane: fits 32 bits
+                if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
             }
         }
     }
@@ -590,8 +657,8 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
         const int     ov = min(max((int)w, 0), maxv);
         acc += (unsigned long long)((ov - sv) * (ov - sv));
     }
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&err[t.unit], acc);
+    const unsigned long long at = wave_sum(acc);
+    if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], at);
     PROF_END(tk);
 }
 
@@ -890,10 +957,14 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
 // the other one, the advance kernel fills it).
 // ---------------------------------------------------------------------------------------------
+__device__ inline int32_t htag(const Descent &d) { return (int32_t)(d.vals & 0xFFFFFF); } // hfilter taps 0..2
+
 __device__ void wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
-                                   int32_t *cnt, int first) {
+                                   int32_t *ctag, int32_t *cnt, int first) {
     Descent d = ds[u];
     if (d.done) return;
+    // a mode-3 trial stored the horizontal pass of the candidate's hfilter (a vertical move leaves it unchanged)
+    if (!first && wact[u] == 3) ctag[u] = htag(d);
     if (!first) d.report((int64_t)err[u]);
     err[u]  = 0;
     wact[u] = 0;
@@ -901,18 +972,18 @@ __device__ void wiener_advance_one(Descent *ds, int u, unsigned long long *err, 
         int v[3];
         d.taps(0, v), set_wiener_taps(taps + 16 * u, v); // f = 0: hfilter, f = 1: vfilter
         d.taps(1, v), set_wiener_taps(taps + 16 * u + 8, v);
-        wact[u] = 1;
+        wact[u] = (d.init || d.mf != 1) ? 1 : (ctag[u] == htag(d) ? 2 : 3);
         atomicAdd(&cnt[1], 1);
     }
     ds[u] = d;
 }
 
 __global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
-                                                             int16_t *taps, int32_t *wact, int32_t *cnt, int first,
-                                                             unsigned long long *tk) {
+                                                             int16_t *taps, int32_t *wact, int32_t *ctag, int32_t *cnt,
+                                                             int first, unsigned long long *tk) {
     PROF_BEGIN(tk);
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < n) wiener_advance_one(ds, u, err, taps, wact, cnt, first);
+    if (u < n) wiener_advance_one(ds, u, err, taps, wact, ctag, cnt, first);
     PROF_END(tk);
 }
 
@@ -1369,7 +1440,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
     const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn);
     const size_t o_wds = dc(sizeof(Descent) * n_wn), o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
-                 o_wact = dc(4 * (size_t)n_wn);
+                 o_wact = dc(4 * (size_t)n_wn), o_ctag = dc(4 * (size_t)n_wn),
+                 o_tcache = dc((size_t)36 * 64 * 4 * nt_wn);
     const size_t o_mom = dc(40 * (size_t)npairs), o_sds = dc(sizeof(Descent) * npairs),
                  o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
                  o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
@@ -1479,9 +1551,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
     if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, st));
+        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, st)); // no cached horizontal pass
         hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
-                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), cnt, 1,
-                           (unsigned long long *)nullptr);
+                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
+                           (int32_t *)dp(o_ctag), cnt, 1, (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
     if (npairs) {
@@ -1504,12 +1577,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 run(2, [&](unsigned long long *tk) {
                     hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt_wn), dim3(256), 0, st, A,
                                        (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact), nxt,
-                                       (unsigned long long *)dp(o_werr), pc, tk);
+                                       (unsigned long long *)dp(o_werr), pc, tk, (uint32_t *)dp(o_tcache));
                 });
                 run(4, [&](unsigned long long *tk) {
                     hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
                                        (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr),
-                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), nxt, 0, tk);
+                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag), nxt, 0,
+                                       tk);
                 });
             }
             if (sl) {

@@ -88,6 +88,8 @@ struct SvtGpuCdefFrameState {
     int32_t        fb_row_begin, fb_row_end; // band of FB rows searched/applied (tiling)
     uint64_t      *own_mse;       // state-owned tables (d_mse/d_skip may point at caller memory)
     uint8_t       *own_skip;
+    uint8_t       *own_dir;       // state-owned dir/var (d_dir/d_var may point at caller memory)
+    int32_t       *own_var;
 };
 
 // Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
@@ -121,4 +123,48 @@ hipStream_t svtgpu_default_stream();
 SvtGpuContext *svtgpu_default_context();
 static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave64 reductions with DPP (VALU only; no ds_bpermute chains): row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast 15 / 31 across rows.  The total lands in lane 63 (the other lanes hold partial sums).
+// ---------------------------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ unsigned long long dpp_u64(unsigned long long v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, BANK_MASK, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, BANK_MASK, true);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ unsigned long long wave_sum_lane63(unsigned long long v) {
+    v += dpp_u64<0x111, 0xf, 0xf>(v); // row_shr:1
+    v += dpp_u64<0x112, 0xf, 0xf>(v); // row_shr:2
+    v += dpp_u64<0x114, 0xf, 0xe>(v); // row_shr:4, banks 1-3
+    v += dpp_u64<0x118, 0xf, 0xc>(v); // row_shr:8, banks 2-3
+    v += dpp_u64<0x142, 0xa, 0xf>(v); // row_bcast:15 into rows 1 and 3
+    v += dpp_u64<0x143, 0xc, 0xf>(v); // row_bcast:31 into rows 2 and 3
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32_lane63(uint32_t v) { // 32-bit DPP adds (mod 2^32)
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xe, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xc, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, true);
+    return v;
+}
+// exact 64-bit wave total (lane 63) of per-lane u32 values: two 16-bit limbs (each limb sum < 2^22)
+__device__ __forceinline__ unsigned long long wave_sum_u32_wide(uint32_t v) {
+    return (unsigned long long)wave_sum_u32_lane63(v & 0xFFFFu) +
+           ((unsigned long long)wave_sum_u32_lane63(v >> 16) << 16);
+}
+// exact wave total (lane 63) of per-lane int32 values, as int64
+__device__ __forceinline__ long long wave_sum_i32_wide(int v) {
+    return (long long)wave_sum_u32_wide((uint32_t)v ^ 0x80000000u) - 64ll * 0x80000000ll;
+}
+// exact wave total (lane 63) of per-lane 64-bit values mod 2^64: three 22-bit limbs (each limb sum < 2^28)
+__device__ __forceinline__ unsigned long long wave_sum_u64_limbs(unsigned long long v) {
+    const uint32_t l0 = (uint32_t)(v & 0x3FFFFF), l1 = (uint32_t)((v >> 22) & 0x3FFFFF), l2 = (uint32_t)(v >> 44);
+    return (unsigned long long)wave_sum_u32_lane63(l0) + ((unsigned long long)wave_sum_u32_lane63(l1) << 22) +
+           ((unsigned long long)wave_sum_u32_lane63(l2) << 44);
 }

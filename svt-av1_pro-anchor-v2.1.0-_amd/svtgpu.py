@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsvtgpu.so")
+LIB_PATH = os.environ.get("SVTGPU_LIB") or os.path.join(_HERE, "lib", "libsvtgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "svtgpu.h")
 
 SVTGPU_OK = 0
@@ -196,6 +196,7 @@ _SIGS = {
     "svtgpu_cdef_apply_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(CdefParams), _P]),
     "svtgpu_cdef_set_fb_rows": (ctypes.c_int, [_P, _I32, _I32]),
     "svtgpu_cdef_bind_tables": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_bind_dir_tables": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_cdef_clear_tables": (ctypes.c_int, [_P, _P]),
     "svtgpu_cdef_read_state": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "svtgpu_cdef_mse_device_ptr": (_P, [_P]),
@@ -406,6 +407,9 @@ class CdefState:
 
     def bind_tables(self, mse_dev_ptr, skip_dev_ptr):
         check(lib().svtgpu_cdef_bind_tables(self.h, mse_dev_ptr, skip_dev_ptr))
+
+    def bind_dir_tables(self, dir_dev_ptr, var_dev_ptr):
+        check(lib().svtgpu_cdef_bind_dir_tables(self.h, dir_dev_ptr, var_dev_ptr))
 
     def clear_tables(self, stream=None):
         check(lib().svtgpu_cdef_clear_tables(self.h, stream))

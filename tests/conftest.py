@@ -13,3 +13,17 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
     config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """torch bundles its own HIP runtime; it must initialize the device before libsvtgpu's runtime does (the
+    order bench.py uses), or torch reports no GPU.  Only when GPU tests are selected."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
+    yield

@@ -183,3 +183,45 @@ def test_cdef_4k_10bit_properties(ctx):
     # filtered output stays within the sample range and differs from the input somewhere
     assert max(int(p.max()) for p in out) <= 1023
     assert any((a != b).any() for a, b in zip(out, rec))
+
+
+@pytest.mark.parametrize("nb", [2, 3])
+def test_cdef_band_search_allreduce(ctx, nb):
+    """The multi-GPU split of bench.py on one device: each band's search into zeroed tables, the tables summed
+    (what the RCCL all-reduce does), then the pick and a whole-frame apply == the one-band pipeline."""
+    import torch
+    w, h, bd, q, lam = 512, 328, 10, 128, 60000
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0B00 + nb)
+    R, S, O1, O2 = (svtgpu.Frame(ctx, w, h, bd) for _ in range(4))
+    R.upload(rec)
+    S.upload(src)
+    ctrls = svtgpu.cdef_controls(1)
+    full = svtgpu.CdefState(ctx, w, h)
+    full.search(R, S, ctrls, q)
+    prm1, fbs1 = full.pick(ctrls, q, lam)
+    full.apply(R, O1, prm1)
+    st = svtgpu.CdefState(ctx, w, h)
+    nvfb = (h // 4 + 15) // 16
+    tabs = [torch.zeros((2, st.nfb, 64), dtype=torch.int64, device="cuda"),
+            torch.zeros(st.nfb, dtype=torch.uint8, device="cuda"),
+            torch.zeros((st.nfb, 64), dtype=torch.uint8, device="cuda"),
+            torch.zeros((st.nfb, 64), dtype=torch.int32, device="cuda")]
+    total = [torch.zeros_like(t) for t in tabs]
+    st.bind_tables(tabs[0].data_ptr(), tabs[1].data_ptr())
+    st.bind_dir_tables(tabs[2].data_ptr(), tabs[3].data_ptr())
+    for r in range(nb):
+        st.set_fb_rows(*svtgpu.band(nvfb, nb, r))
+        st.clear_tables()
+        st.search(R, S, ctrls, q)
+        torch.cuda.synchronize()
+        for a, b in zip(total, tabs):
+            a += b
+    for a, b in zip(tabs, total):
+        a.copy_(b)
+    torch.cuda.synchronize()
+    st.set_fb_rows(0, nvfb)
+    prm2, fbs2 = st.pick(ctrls, q, lam)
+    st.apply(R, O2, prm2)
+    assert prm1.as_tuple() == prm2.as_tuple() and np.array_equal(fbs1, fbs2)
+    for a, b in zip(O1.download(), O2.download()):
+        assert np.array_equal(a, b)
