@@ -25,6 +25,10 @@
 
 #include "svtgpu_internal.h"
 
+#ifndef DLF_EXP
+#define DLF_EXP 0 // development experiments (bit 0: no vertical pass, bit 1: no horizontal pass); 0 = real kernel
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------------------------------------
@@ -178,7 +182,7 @@ constexpr int TILE  = 64;
 constexpr int APRON = 12;
 constexpr int LW    = TILE + 2 * APRON; // 88 samples per LDS row
 constexpr int NTHR  = 256;
-constexpr int MAX_TRIALS = 2;
+constexpr int MAX_TRIALS = 2; // levels per trial launch (the bisection's lo and hi candidates)
 
 struct DlfTileArgs {
     const void     *src;      // recon plane (apply: a copy of it)
@@ -198,7 +202,9 @@ struct DlfTileArgs {
 
 template <typename T, bool TRIAL>
 __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
-    __shared__ uint16_t t[LW * LW];
+    __shared__ __align__(16) uint16_t t[LW * LW];
+    __shared__ __align__(16) uint16_t t0[TRIAL ? LW * LW : 8];       // the staged tile, kept for every trial
+    __shared__ __align__(16) uint16_t sref[TRIAL ? TILE * TILE : 8]; // the source tile (trial SSE)
     __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
@@ -218,15 +224,40 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         rh[i] = (ur >= 0 && ur * 4 < a.ph && uc * 4 < a.pw) ? a.rec_h[(size_t)ur * a.units_w + uc] : 0u;
     }
 
+    // stage the tile + apron once (samples outside the plane are never read by an active edge), 4 per item;
+    // gx is a multiple of 4, so interior groups are aligned
+    uint16_t *stage = TRIAL ? t0 : t;
+    for (int i = tid; i < LW * LW / 4; i += NTHR) {
+        const int r = gy + i / (LW / 4), c = gx + 4 * (i % (LW / 4));
+        uint16_t  q[4];
+        if (r >= 0 && r < a.ph && c >= 0 && c + 4 <= a.pw) {
+            const T *sp = src + (size_t)r * a.src_stride + c;
+#pragma unroll
+            for (int j = 0; j < 4; j++) q[j] = (uint16_t)sp[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                q[j] = (r >= 0 && c + j >= 0 && r < a.ph && c + j < a.pw) ? (uint16_t)src[(size_t)r * a.src_stride + c + j] : 0;
+        }
+        *(uint2 *)&stage[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
+    }
+    const int tw = min(TILE, a.pw - x0), th = min(TILE, a.ph - y0);
+    if (TRIAL) {
+        const T *ref = (const T *)a.ref;
+        for (int i = tid; i < TILE * TILE; i += NTHR) {
+            const int r = i / TILE, c = i % TILE;
+            sref[i]     = (r < th && c < tw) ? (uint16_t)ref[(size_t)(y0 + r) * a.ref_stride + x0 + c] : 0;
+        }
+    }
+
     for (int tr = 0; tr < (TRIAL ? a.ntrial : 1); tr++) {
-        // stage the tile + apron (samples outside the plane are never read by an active edge)
-        for (int i = tid; i < LW * LW; i += NTHR) {
-            const int r = gy + i / LW, c = gx + i % LW;
-            t[i] = (r >= 0 && c >= 0 && r < a.ph && c < a.pw) ? (uint16_t)src[(size_t)r * a.src_stride + c] : 0;
+        if (TRIAL) { // every trial starts from the staged samples
+            __syncthreads();
+            for (int i = tid; i < LW * LW / 8; i += NTHR) ((uint4 *)t)[i] = ((const uint4 *)t0)[i];
         }
         __syncthreads();
         // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
-        for (int i = tid; i < RV_R * RV_C * 4; i += NTHR) {
+        for (int i = tid; i < ((DLF_EXP & 1) ? 0 : RV_R * RV_C * 4); i += NTHR) {
             const int line = i & 3, e = (i >> 2) % RV_C, sr = (i >> 2) / RV_C;
             const uint32_t r = rv[sr * RV_C + e];
             const int len = r & 15;
@@ -246,7 +277,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         }
         __syncthreads();
         // horizontal edges y0-4 .. y0+64 over the tile's 64 columns
-        for (int i = tid; i < RH_R * RH_C * 4; i += NTHR) {
+        for (int i = tid; i < ((DLF_EXP & 2) ? 0 : RH_R * RH_C * 4); i += NTHR) {
             const int col = i % TILE, e = i / TILE;
             const uint32_t r = rh[e * RH_C + col / 4];
             const int len = r & 15;
@@ -266,26 +297,23 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         }
         __syncthreads();
         // emit the tile
-        const int tw = min(TILE, a.pw - x0), th = min(TILE, a.ph - y0);
         if (TRIAL) {
-            const T *ref = (const T *)a.ref;
-            unsigned long long s = 0;
+            uint32_t s = 0; // <= 16 samples per lane
             for (int i = tid; i < TILE * TILE; i += NTHR) {
                 const int r = i / TILE, c = i % TILE;
                 if (r < th && c < tw) {
-                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)ref[(size_t)(y0 + r) * a.ref_stride + x0 + c];
-                    s += (unsigned long long)(d * d);
+                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)sref[i];
+                    s += (uint32_t)(d * d);
                 }
             }
-            s = wave_sum_lane63(s);
-            if ((tid & 63) == 63) red[tid >> 6] = s;
+            const unsigned long long sw = wave_sum_u32_wide(s);
+            if ((tid & 63) == 63) red[tid >> 6] = sw;
             __syncthreads();
             if (tid == 0) {
                 unsigned long long tot = 0;
                 for (int w = 0; w < NTHR / 64; w++) tot += red[w];
                 atomicAdd(&a.sse[tr], tot);
             }
-            __syncthreads();
         } else {
             T *dst = (T *)a.dst;
             for (int i = tid; i < TILE * TILE; i += NTHR) {
@@ -476,12 +504,15 @@ int search_level(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
     auto eval = [&](const int *lv, int n) -> int { // evaluate the not-yet-known levels in one launch
         SvtGpuLfParams q[MAX_TRIALS];
         int            idx[MAX_TRIALS], m = 0;
-        for (int k = 0; k < n; k++)
-            if (err[lv[k]] < 0 && (m == 0 || idx[0] != lv[k])) {
+        for (int k = 0; k < n; k++) {
+            bool dup = err[lv[k]] >= 0;
+            for (int j = 0; j < m && !dup; j++) dup = idx[j] == lv[k];
+            if (!dup) {
                 q[m] = p;
                 set_trial_level(q[m], plane, dir, lv[k]);
                 idx[m++] = lv[k];
             }
+        }
         if (!m) return SVTGPU_OK;
         uint64_t r[MAX_TRIALS];
         int      rc = trial_sse(s, recon, src, plane, q, m, r, st);
@@ -498,9 +529,11 @@ int search_level(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
         int64_t   bias = (best_err >> (15 - (mid / 8))) * step;
         if (!only4x4) bias >>= 1;
         const bool try_lo = direction <= 0 && lo != mid, try_hi = direction >= 0 && hi != mid;
-        int        lv[2], n = 0;
+        int        lv[MAX_TRIALS], n = 0;
         if (try_lo) lv[n++] = lo;
         if (try_hi) lv[n++] = hi;
+        // (speculatively batching the next iteration's levels was measured slower: each extra luma level costs a
+        // ~45 us filter pass, more than the launch and read-back it saves)
         if ((rc = eval(lv, n))) return rc;
         if (try_lo && err[lo] < best_err + bias) {
             if (err[lo] < best_err) best_err = err[lo];
