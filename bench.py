@@ -44,6 +44,21 @@ sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
 import svtgpu  # noqa: E402
 import synth  # noqa: E402
 
+def measured_traffic(path, kernel, bd):
+    """HBM-side bytes per launch of `kernel` from the committed PMC summary (scripts/pmc_traffic.py): FETCH_SIZE and
+    WRITE_SIZE need their own rocprofv3 --pmc passes, so they are collected by a separate profiled run of this bench
+    and read back here.  None when no summary covers the kernel."""
+    try:
+        summary = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    name = kernel.split()[0] + ("<unsigned short>" if bd > 8 else "<unsigned char>")
+    k = summary.get("kernels", {}).get(name)
+    if not k:
+        return None, None
+    return k["traffic_bytes"], "%s (%s; %d launches)" % (os.path.relpath(path, ROOT), summary["method"], k["launches"])
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -59,6 +74,8 @@ def parse():
     ap.add_argument("--base-q-idx", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no HIP-event timing inside the LR search")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
+                    help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
     return ap.parse_args()
 
@@ -265,6 +282,7 @@ def main():
                         "s_memrealtime clock (first workgroup start to last workgroup end, every launch of the timed "
                         "steps); achieved = algorithmic bytes (samples + filter planes touched) / device time; the "
                         "class is VALU-bound, so its HBM fraction is low by construction"}
+    roof["traffic"], roof["traffic_source"] = measured_traffic(a.traffic_json, roof["kernel"], bd)
     out = {
         "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
         "value": round(value, 3),

@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     __shared__ uint16_t ctile[2][CT * CT];
     __shared__ uint8_t  slisted[64];
     __shared__ int32_t  nlisted;
-    const int fb = A.fb0 + blockIdx.x, fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
+    const int fb = A.fb0 + xcd_swizzle(blockIdx.x, gridDim.x), fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
     const int cs = A.cs;
     const int si = A.fb_strength[fb];
     int level = A.prm.cdef_y_strength[si] >> 2, sec = A.prm.cdef_y_strength[si] & 3;

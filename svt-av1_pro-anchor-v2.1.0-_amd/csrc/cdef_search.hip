@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     __shared__ int32_t  nlisted;
     __shared__ CdefGroupTable grp[4]; // luma A, luma B, chroma A, chroma B
 
-    const int fb = A.fb0 + blockIdx.x;
+    const int fb = A.fb0 + xcd_swizzle(blockIdx.x, gridDim.x);
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cs = A.cs;

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
     const int tid = threadIdx.x;
-    const int x0 = (blockIdx.x % a.tiles_x) * TILE, y0 = (blockIdx.x / a.tiles_x) * TILE;
+    const int tb = xcd_swizzle(blockIdx.x, gridDim.x), x0 = (tb % a.tiles_x) * TILE, y0 = (tb / a.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)a.src;
 

@@ -117,7 +117,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsigned long long *sum,
                                                         unsigned long long *sse, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    const Tile       t = A.tiles[blockIdx.x];
+    const Tile       t = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     uint32_t ps = 0, pe = 0; // <= 16 samples per lane: fits 32 bits
@@ -163,7 +163,8 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
     constexpr int NVAL = (C::NPAIR + 1) * 49;
     __shared__ int lds[256 * ST_SLOTS]; // staging (D pairs, S pairs), then the lane partials
     uint32_t      *D2 = (uint32_t *)lds, *S2 = D2 + ST_W * ST_W;
-    const Tile       t = A.tiles[tile_begin + blockIdx.x];
+    const int        tl = xcd_swizzle(blockIdx.x, gridDim.x);
+    const Tile       t = A.tiles[tile_begin + tl];
     const PlaneArgs &P = A.pl[t.plane];
     const URect      u = A.units[t.unit];
     const long long  area = (long long)(u.h_end - u.h_start) * (u.v_end - u.v_start);
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
 #pragma unroll
     for (int k = 0; k < ST_SLOTS; k++) lds[k * 256 + tid] = acc[k];
     __syncthreads();
-    long long *out = part + (size_t)blockIdx.x * NVAL;
+    long long *out = part + (size_t)tl * NVAL;
     for (int oi = tid; oi < NVAL; oi += 256) {
         const int pair = oi / 49, k = oi % 49, r1 = k / 7, r2 = k % 7;
         int       lane0 = 0, nl = 0, slot = 0;
@@ -291,10 +292,11 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
     __shared__ __align__(16) uint16_t v[71 * VS];
     __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[1] = 0; // the next advance counts its live descents there
-    const Tile t    = A.tiles[blockIdx.x];
+    const int  ti   = xcd_swizzle(blockIdx.x, gridDim.x);
+    const Tile t    = A.tiles[ti];
     const int  mode = wact[t.unit];
     if (!mode) return;
-    uint32_t *tc = tcache + (size_t)blockIdx.x * 36 * 64; // this tile's cached horizontal pass
+    uint32_t *tc = tcache + (size_t)ti * 36 * 64; // this tile's cached horizontal pass
     if (pc && threadIdx.x == 0) // profiling: evaluated pixels (spread over PROF_SP counters)
         atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), (unsigned long long)(t.w * t.h));
     const PlaneArgs &P  = A.pl[t.plane];
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
     // ep e + 1 are built while ep e is filtered, one barrier per ep
     __shared__ int ab1[2][SG_B * SG_B], ab2[2][SG_B * SG_B];
     __shared__ int      xby[256];
-    const Tile       t = A.tiles[blockIdx.x];
+    const Tile       t = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     for (int i = threadIdx.x; i < (t.h + 6) * (t.w + 6); i += SG_NT) {
@@ -636,7 +638,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const int32_t *best, unsigned long long *err,
                                                       unsigned long long *tk) {
     PROF_BEGIN(tk);
-    const Tile       t = A.tiles[blockIdx.x];
+    const Tile       t = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
     const PlaneArgs &P = A.pl[t.plane];
     const int       *b = best + t.unit * 4; // {ep index, ep, xq0, xq1}
     const int        e = b[0], ep = b[1], xq0 = b[2], xq1 = b[3], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];

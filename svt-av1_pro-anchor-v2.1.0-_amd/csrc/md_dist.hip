@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
     __shared__ uint32_t s_sad[kBlocks], s_sse[kBlocks];
     __shared__ int32_t  s_sum[kBlocks];
     const int tid = threadIdx.x;
-    const int sb  = a.sb_begin + blockIdx.x;
+    const int sb  = a.sb_begin + xcd_swizzle(blockIdx.x, gridDim.x);
     const int ox = (sb % a.nsbx) * 64, oy = (sb / a.nsbx) * 64;
     const int W = a.width, H = a.height;
     const T  *src = (const T *)a.src;

@@ -125,6 +125,14 @@ static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;
 }
 
+// XCD-aware block order (speed only, never correctness): workgroups are dealt round-robin over the 8 XCDs, so
+// blocks b, b + 8, ... share one XCD's L2.  Give each such group a contiguous range of logical indices so tiles that
+// share halo lines (the neighbours of a row-major tile list) are read through the same L2.  Bijective for any n.
+__device__ __forceinline__ int xcd_swizzle(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Wave64 reductions with DPP (VALU only; no ds_bpermute chains): row_shr 1/2/4/8 inside each 16-lane row,
 // then row_bcast 15 / 31 across rows.  The total lands in lane 63 (the other lanes hold partial sums).

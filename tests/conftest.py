@@ -13,6 +13,15 @@ for p in (ROOT, PKG, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    # torch bundles its own HIP runtime and must initialize the device before libsvtgpu's runtime does (the order
+    # bench.py uses), or torch reports no GPU: do it before collection, where a test module could touch the device
+    if os.path.exists("/dev/kfd"):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except ImportError:
+            pass
 
 
 @pytest.fixture(scope="session", autouse=True)

@@ -47,8 +47,8 @@ def test_version_and_errors():
     assert L.svtgpu_error_string(-1) == b"invalid argument"
 
 
-@pytest.mark.skipif(os.path.exists("/dev/kfd") and svtgpu.lib().svtgpu_device_available(),
-                    reason="a device is present")
+# decided without touching the device: probing it at collection would start libsvtgpu's HIP runtime before torch's
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a device may be present")
 def test_no_device_fails_loudly():
     L = svtgpu.lib()
     assert L.svtgpu_device_available() == 0
