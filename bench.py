@@ -175,7 +175,6 @@ def main():
     md_range = svtgpu.band(md.nsb, n, rank)  # MD batch: SB ranges, no collective
     lr_rb, lr_re = svtgpu.lr_unit_rows(lr.units, n, rank)  # LR search: unit-row bands, records all-gathered
     lf_levels = []
-    lr_prof = []  # per timed step: the LR search's per-kernel-class device times (HIP events on `stream`)
 
     def step(timed):
         es = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
@@ -216,8 +215,6 @@ def main():
                 ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])
                 lr.set_units(p, units_p, sp)
                 lr_ft.append(ftp)
-        if timed and not a.no_kernel_timing:
-            lr_prof.append(lr.profile(True))
         lr.apply(D, O, L, lr_ft, sp)
         if timed:
             es[4].record(stream)
@@ -230,7 +227,8 @@ def main():
     for _ in range(a.warmup):
         step(False)
     # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
-    # of every launch; HIP-event packets around each of the ~100 launches per search cost ~20 us apiece)
+    # of every launch, accumulated on the device and read once after the timed region; HIP-event packets around
+    # each of the ~100 launches per search would cost ~20 us apiece)
     lr.profile(not a.no_kernel_timing)
     torch.cuda.synchronize()
     if n > 1:
@@ -244,6 +242,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    lr_tot = lr.profile(False) if not a.no_kernel_timing else None
     if n > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -253,8 +252,8 @@ def main():
 
     ms_per_step = dt * 1e3 / a.steps
     value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
-    lr_cls = {c: {k: float(np.mean([pr[c][k] for pr in lr_prof])) if lr_prof else 0.0
-                  for k in ("launches", "ms", "bytes")} for c in svtgpu.LrState.PROFILE_CLASSES}
+    lr_cls = {c: {k: lr_tot[c][k] / max(lr_tot["searches"], 1) if lr_tot else 0.0 for k in ("launches", "ms", "bytes")}
+              for c in svtgpu.LrState.PROFILE_CLASSES}
     # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
     # recon + source read once (2*S*B) + per-FB outputs (mse 2x64 u64, dir 64 u8, var 64 i32, skip)
     S_samples = 1.5 * W * H

@@ -526,20 +526,22 @@ int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const Svt
  * work, usable without a GPU); returns SVTGPU_OK with *frame_type_out = NONE for a plane that is not searched. */
 int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
                            const SvtGpuLrUnitSearch *records, int32_t *frame_type_out, SvtGpuRestUnit *units_out);
-/* Device-time profile of the last search by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
+/* Device-time profile of the searches timed since the previous read, by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
  * + moments, 2 Wiener trials, 3 projection errors, 4 Wiener decomposition, descent advance rounds, SGR SSE.  Each
  * launch is timed from its first workgroup's start to its last workgroup's end on the device's 100 MHz
  * s_memrealtime clock (per-launch HIP event packets would cost more than these launches); bytes = algorithmic
  * HBM bytes of the class (compulsory reads/writes of the samples and filter planes the launches touch). */
 typedef struct SvtGpuLrProfile {
-    int32_t launches[5];
+    int32_t launches[5]; /* totals over `searches` searches */
     float   ms[5];
     double  bytes[5];
+    int32_t searches;
 } SvtGpuLrProfile;
 /* enable != 0 turns timing of the following searches on (0 off): a bit mask of the classes to time (bit c =
- * class c; -1 = all); `last` (nullable) receives the profile of the last search made with timing on (untimed
- * classes read 0). */
-int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *last);
+ * class c; -1 = all).  `totals` (nullable) first receives the sums over the searches timed since the previous read
+ * (untimed classes read 0), which are then reset; reading synchronizes the device.  The timings accumulate on the
+ * device: a timed search adds one small launch and no copies or host synchronization. */
+int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *totals);
 /* controls of wn_filter_lvl / sg_filter_lvl (EncModeConfig.c:1329-1445); rate fields are left zero */
 int svtgpu_lr_controls_for_level(int32_t wn_level, int32_t sg_level, SvtGpuLrSearchControls *c);
 

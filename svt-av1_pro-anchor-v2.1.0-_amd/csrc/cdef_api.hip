@@ -118,7 +118,9 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
               hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
               hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096) * 8) == hipSuccess &&
               hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, (size_t)(41 * 4 * 32 + 4 * 32 + 64) * 4) == hipSuccess &&
-              hipMalloc(&s->d_fb_list, (nfb + 1) * 4) == hipSuccess;
+              hipMalloc(&s->d_fb_list, (nfb + 1) * 4) == hipSuccess &&
+              hipHostMalloc((void **)&s->h_pick, 512 + nfb, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+              hipHostGetDevicePointer((void **)&s->h_pick_dev, s->h_pick, 0) == hipSuccess;
     if (!ok) {
         svtgpu_cdef_state_destroy(s);
         return SVTGPU_ERR_OOM;
@@ -143,6 +145,7 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
                     s->d_pick_out, s->d_pick_lev, s->d_fb_list};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (s->h_pick) (void)hipHostFree(s->h_pick);
     delete s;
 }
 

@@ -6,8 +6,10 @@
 // (nb = 1, 2, 4, 8 → 5, 10, 20, 40 dependent calls, :697-727) are independent, so each device step
 // advances every chain that is still running: step = one partial-sum kernel (FB chunks x chains)
 // + one reduce/argmin kernel per chain that also appends the pick and pre-shifts the selection list
-// for the next refinement call.  40 steps, all enqueued without host synchronisation.  The RD
-// choice over nb (:853-872) and the filter_map remap (:911-919) are a few scalar ops on the host.
+// for the next refinement call.  40 steps, all enqueued without host synchronisation (the grid is shaped
+// for every FB; workgroups past the non-skipped count read on the device find no work).  The RD choice over
+// nb (:853-872) and the per-FB assignment run on the device too and write the result straight into mapped
+// pinned memory: one host synchronisation per pick.  The filter_map remap (:911-919) stays on the host.
 #include <algorithm>
 #include <cstring>
 
@@ -27,7 +29,8 @@ struct StepChain {
 };
 struct StepArgs {
     const uint64_t *wmse;   // [sb_count][2][64] compacted, bias applied
-    int32_t         sb_count, chunk, start_gi, end_gi, step;
+    const int32_t  *count;  // sb_count, the number of non-skipped FBs (device)
+    int32_t         chunk, start_gi, end_gi, step;
     uint64_t       *tot;    // [3][4][4096] rotating tot_mse accumulators
     int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
     int32_t        *fin;    // [4][32] final list per chain
@@ -111,7 +114,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int t = threadIdx.x, c = C.chain;
     const int lead = blockIdx.x == 0 && blockIdx.y == 0;
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
-    const int f0 = blockIdx.y * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(A.sb_count - f0, A.chunk);
+    const int f0 = blockIdx.y * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
     // 0. start staging this workgroup's FB chunk (independent of the previous call's result)
     if (nfb > 0) {
@@ -177,11 +180,43 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
                 atomicAdd((unsigned long long *)&cur[(j0 + u) * 64 + k], (unsigned long long)acc[u]);
 }
 
-// ---- per-FB strength index (EbEncCdef.c:866-890) ----
-__global__ void pick_assign_kernel(const uint64_t *wmse, const int32_t *fb_list, const int32_t *count, int nb,
-                                   const int32_t *ygi, int8_t *fb_strength) {
+// ---- RD choice over the number of signalled strengths (EbEncCdef.c:853-872) ----
+struct PickOut {
+    int32_t  sb_count, nbits;
+    int32_t  gi[32]; // [0, 16) luma, [16, 32) chroma strength indices of the chosen list (zero past nb)
+    uint64_t best[MAX_CHAINS];
+};
+__global__ void pick_finish_kernel(const uint64_t *best, const int32_t *fin, const int32_t *count, uint64_t lambda,
+                                   int32_t *gis, int32_t *nb_out, PickOut *out) {
+    if (threadIdx.x != 0) return;
+    const int sb_count  = *count;
+    uint64_t  best_cost = (uint64_t)1 << 63;
+    int       nbits = 0, chosen = -1; // no list chosen: the strengths stay zero
+    for (int i = 0; i <= 3; i++) {
+        const int      nb   = 1 << i;
+        const int      bits = sb_count * i + nb * 6 * 2;
+        const int64_t  rate = (int64_t)bits << 9;                                                  // av1_cost_literal
+        const uint64_t cost = (uint64_t)(((rate * (int64_t)lambda + 256) >> 9) + ((int64_t)(best[i] * 16) << 7)); // RDCOST
+        if (cost < best_cost) best_cost = cost, nbits = i, chosen = i;
+    }
+    const int nb = 1 << nbits;
+    for (int j = 0; j < 16; j++) {
+        gis[j]      = chosen >= 0 && j < nb ? fin[chosen * 32 + j] : 0;
+        gis[16 + j] = chosen >= 0 && j < nb ? fin[chosen * 32 + 16 + j] : 0;
+        out->gi[j] = gis[j], out->gi[16 + j] = gis[16 + j];
+    }
+    *nb_out       = nb;
+    out->sb_count = sb_count;
+    out->nbits    = nbits;
+    for (int c = 0; c < MAX_CHAINS; c++) out->best[c] = best[c];
+}
+
+// ---- per-FB strength index (EbEncCdef.c:866-890); also into the host's copy ----
+__global__ void pick_assign_kernel(const uint64_t *wmse, const int32_t *fb_list, const int32_t *count, const int32_t *d_nb,
+                                   const int32_t *ygi, int8_t *fb_strength, int8_t *host_fbs) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *count) return;
+    const int nb = *d_nb;
     const uint64_t *m0 = wmse + (size_t)i * 128, *m1 = m0 + 64;
     uint64_t        best = (uint64_t)1 << 63;
     int             bg   = 0;
@@ -193,6 +228,12 @@ __global__ void pick_assign_kernel(const uint64_t *wmse, const int32_t *fb_list,
         }
     }
     fb_strength[fb_list[i]] = (int8_t)bg;
+    if (host_fbs) host_fbs[fb_list[i]] = (int8_t)bg;
+}
+
+__global__ void fill_i8_kernel(int8_t *p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
 }
 
 int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
@@ -207,13 +248,11 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count);
     hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
                        (int)ctrls->zero_fs_cost_bias, wmse);
-    int32_t sb_count = 0;
-    HIP_TRY(hipMemcpyAsync(&sb_count, d_count, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device
 
     StepArgs A;
     A.wmse     = wmse;
-    A.sb_count = sb_count;
+    A.count    = d_count;
     A.start_gi = 0;
     A.end_gi   = end;
     A.tot      = wmse + wmse_elems;                            // [3][4][4096]
@@ -237,52 +276,33 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         A.step = step;
         // ~1024 workgroups per step whatever the number of live chains; chunk <= PICK_CHUNK FBs
         const int want  = std::max(1, 256 / std::max(na, 1));
-        A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_count + want - 1) / std::max(want, 1)));
-        const int parts = std::max(1, (sb_count + A.chunk - 1) / A.chunk);
+        A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_max + want - 1) / std::max(want, 1)));
+        const int parts = std::max(1, (sb_max + A.chunk - 1) / A.chunk);
         const size_t lds = (size_t)A.chunk * 129 * 8;
         hipLaunchKernelGGL(sod_step_kernel, dim3(4, parts, na), dim3(NT), lds, st, A);
     }
     HIP_TRY(hipGetLastError());
-    int32_t  lev[MAX_CHAINS][2][16];
-    uint64_t best[MAX_CHAINS];
-    HIP_TRY(hipMemcpyAsync(lev, A.fin, sizeof lev, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(best, s->d_pick_out, sizeof best, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-
-    // RD choice over the number of signalled strengths (EbEncCdef.c:853-872)
-    memset(params, 0, sizeof(*params));
-    uint64_t best_cost = (uint64_t)1 << 63;
-    int      nbits     = 0;
-    for (int i = 0; i <= 3; i++) {
-        const int      nb   = 1 << i;
-        const int      bits = sb_count * i + nb * 6 * 2;
-        const int64_t  rate = (int64_t)bits << 9;                              // av1_cost_literal
-        const uint64_t cost = (uint64_t)(((rate * (int64_t)lambda + 256) >> 9) + ((int64_t)(best[i] * 16) << 7)); // RDCOST
-        if (cost < best_cost) {
-            best_cost = cost;
-            nbits     = i;
-            for (int j = 0; j < nb; j++) {
-                params->cdef_y_strength[j]  = (uint8_t)lev[i][0][j];
-                params->cdef_uv_strength[j] = (uint8_t)lev[i][1][j];
-            }
-        }
-    }
-    const int nb      = 1 << nbits;
-    params->cdef_bits = (uint8_t)nbits;
-    int32_t gis[32];
-    for (int j = 0; j < 16; j++) {
-        gis[j]      = params->cdef_y_strength[j];
-        gis[16 + j] = params->cdef_uv_strength[j];
-    }
-    int32_t *d_gis = A.fin + MAX_CHAINS * 32;
-    HIP_TRY(hipMemcpyAsync(d_gis, gis, sizeof gis, hipMemcpyHostToDevice, st));
+    int32_t *d_gis = A.fin + MAX_CHAINS * 32, *d_nb = d_gis + 32;
+    PickOut *h_out = (PickOut *)s->h_pick;
+    int8_t  *h_fbs = (int8_t *)(s->h_pick + 512);
+    static_assert(sizeof(PickOut) <= 512, "pick output slot");
+    hipLaunchKernelGGL(pick_finish_kernel, dim3(1), dim3(64), 0, st, (const uint64_t *)s->d_pick_out, (const int32_t *)A.fin,
+                       (const int32_t *)d_count, (uint64_t)lambda, d_gis, d_nb, (PickOut *)s->h_pick_dev);
     HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, nfb, st));
-    hipLaunchKernelGGL(pick_assign_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, wmse, s->d_fb_list, d_count, nb,
-                       d_gis, s->d_fb_strength);
+    int8_t *host_fbs = fb_strength_out ? (int8_t *)(s->h_pick_dev + 512) : nullptr;
+    if (host_fbs) hipLaunchKernelGGL(fill_i8_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, host_fbs, nfb);
+    hipLaunchKernelGGL(pick_assign_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, wmse, s->d_fb_list, d_count, d_nb,
+                       d_gis, s->d_fb_strength, host_fbs);
     HIP_TRY(hipGetLastError());
-    if (fb_strength_out) {
-        HIP_TRY(hipMemcpyAsync(fb_strength_out, s->d_fb_strength, nfb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st)); // the only wait of the pick
+    memset(params, 0, sizeof(*params));
+    const int nbits = h_out->nbits, nb = 1 << nbits;
+    params->cdef_bits = (uint8_t)nbits;
+    for (int j = 0; j < nb; j++) {
+        params->cdef_y_strength[j]  = (uint8_t)h_out->gi[j];
+        params->cdef_uv_strength[j] = (uint8_t)h_out->gi[16 + j];
     }
+    if (fb_strength_out) memcpy(fb_strength_out, h_fbs, nfb);
     // gi -> strength code (filter_map, EbEncCdef.c:911-919); damping (:921)
     const int nf = ctrls->first_pass_fs_num;
     for (int i = 0; i < nb; i++) {
@@ -291,6 +311,5 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         params->cdef_uv_strength[i] = uv < nf ? ctrls->default_first_pass_fs[uv] : ctrls->default_second_pass_fs[uv - nf];
     }
     params->cdef_damping = (uint8_t)(3 + (base_q_idx >> 6));
-    HIP_TRY(hipStreamSynchronize(st));
     return SVTGPU_OK;
 }

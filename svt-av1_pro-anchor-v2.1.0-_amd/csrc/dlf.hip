@@ -184,20 +184,31 @@ constexpr int LW    = TILE + 2 * APRON; // 88 samples per LDS row
 constexpr int NTHR  = 256;
 constexpr int MAX_TRIALS = 2; // levels per trial launch (the bisection's lo and hi candidates)
 
-struct DlfTileArgs {
+constexpr int MAX_JOBS   = 2; // planes per launch: the U and V level searches run side by side
+
+// one plane of a launch
+struct DlfPlaneJob {
     const void     *src;      // recon plane (apply: a copy of it)
-    int32_t         src_stride;
     void           *dst;      // apply output
-    int32_t         dst_stride;
     const void     *ref;      // source picture plane (trial)
-    int32_t         ref_stride;
     const uint32_t *rec_v, *rec_h; // edge records of this plane type
+    int32_t         src_stride, dst_stride, ref_stride;
     int32_t         units_w;  // records per row (= pw / 4)
-    int32_t         pw, ph, bd, tiles_x;
+    int32_t         pw, ph, tiles_x, tiles;
     int32_t         ntrial;
     uint8_t         lvl[MAX_TRIALS][2][128]; // [trial][dir][class] filter level
-    uint8_t         mblim[64], lim[64], hev[64];
-    unsigned long long *sse; // [ntrial] (trial mode)
+};
+
+struct DlfTileArgs {
+    DlfPlaneJob job[MAX_JOBS];
+    int32_t     njob, bd;
+    uint8_t     mblim[64], lim[64], hev[64];
+    // trial mode: per-(job, trial) SSE accumulators and the count of finished workgroups, both zero between
+    // launches (the last workgroup hands the sums to `out` -- mapped pinned host memory -- and re-zeroes them)
+    unsigned long long *sse;
+    unsigned int       *arrive;
+    unsigned long long *out; // [MAX_JOBS][MAX_TRIALS] sums, then the sequence word (svtgpu_wait_seq)
+    unsigned long long  seq;
 };
 
 template <typename T, bool TRIAL>
@@ -209,19 +220,21 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
     const int tid = threadIdx.x;
-    const int tb = xcd_swizzle(blockIdx.x, gridDim.x), x0 = (tb % a.tiles_x) * TILE, y0 = (tb / a.tiles_x) * TILE;
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x), jb = (a.njob > 1 && b >= a.job[0].tiles) ? 1 : 0;
+    const DlfPlaneJob &J = a.job[jb];
+    const int tb = b - (jb ? a.job[0].tiles : 0), x0 = (tb % J.tiles_x) * TILE, y0 = (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
-    const T  *src = (const T *)a.src;
+    const T  *src = (const T *)J.src;
 
     // edge records reaching the tile (no records outside the plane: length 0)
     constexpr int RV_R = LW / 4, RV_C = TILE / 4 + 3, RH_R = TILE / 4 + 3, RH_C = TILE / 4;
     for (int i = tid; i < RV_R * RV_C; i += NTHR) {
         const int ur = gy / 4 + i / RV_C, uc = (x0 - 4) / 4 + i % RV_C;
-        rv[i] = (ur >= 0 && uc >= 0 && ur * 4 < a.ph && uc * 4 < a.pw) ? a.rec_v[(size_t)ur * a.units_w + uc] : 0u;
+        rv[i] = (ur >= 0 && uc >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_v[(size_t)ur * J.units_w + uc] : 0u;
     }
     for (int i = tid; i < RH_R * RH_C; i += NTHR) {
         const int ur = (y0 - 4) / 4 + i / RH_C, uc = x0 / 4 + i % RH_C;
-        rh[i] = (ur >= 0 && ur * 4 < a.ph && uc * 4 < a.pw) ? a.rec_h[(size_t)ur * a.units_w + uc] : 0u;
+        rh[i] = (ur >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_h[(size_t)ur * J.units_w + uc] : 0u;
     }
 
     // stage the tile + apron once (samples outside the plane are never read by an active edge), 4 per item;
@@ -230,27 +243,27 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     for (int i = tid; i < LW * LW / 4; i += NTHR) {
         const int r = gy + i / (LW / 4), c = gx + 4 * (i % (LW / 4));
         uint16_t  q[4];
-        if (r >= 0 && r < a.ph && c >= 0 && c + 4 <= a.pw) {
-            const T *sp = src + (size_t)r * a.src_stride + c;
+        if (r >= 0 && r < J.ph && c >= 0 && c + 4 <= J.pw) {
+            const T *sp = src + (size_t)r * J.src_stride + c;
 #pragma unroll
             for (int j = 0; j < 4; j++) q[j] = (uint16_t)sp[j];
         } else {
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                q[j] = (r >= 0 && c + j >= 0 && r < a.ph && c + j < a.pw) ? (uint16_t)src[(size_t)r * a.src_stride + c + j] : 0;
+                q[j] = (r >= 0 && c + j >= 0 && r < J.ph && c + j < J.pw) ? (uint16_t)src[(size_t)r * J.src_stride + c + j] : 0;
         }
         *(uint2 *)&stage[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
     }
-    const int tw = min(TILE, a.pw - x0), th = min(TILE, a.ph - y0);
+    const int tw = min(TILE, J.pw - x0), th = min(TILE, J.ph - y0);
     if (TRIAL) {
-        const T *ref = (const T *)a.ref;
+        const T *ref = (const T *)J.ref;
         for (int i = tid; i < TILE * TILE; i += NTHR) {
             const int r = i / TILE, c = i % TILE;
-            sref[i]     = (r < th && c < tw) ? (uint16_t)ref[(size_t)(y0 + r) * a.ref_stride + x0 + c] : 0;
+            sref[i]     = (r < th && c < tw) ? (uint16_t)ref[(size_t)(y0 + r) * J.ref_stride + x0 + c] : 0;
         }
     }
 
-    for (int tr = 0; tr < (TRIAL ? a.ntrial : 1); tr++) {
+    for (int tr = 0; tr < (TRIAL ? J.ntrial : 1); tr++) {
         if (TRIAL) { // every trial starts from the staged samples
             __syncthreads();
             for (int i = tid; i < LW * LW / 8; i += NTHR) ((uint4 *)t)[i] = ((const uint4 *)t0)[i];
@@ -262,7 +275,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             const uint32_t r = rv[sr * RV_C + e];
             const int len = r & 15;
             if (!len) continue;
-            const int cur = a.lvl[tr][0][(r >> 8) & 127], prv = a.lvl[tr][0][(r >> 16) & 127];
+            const int cur = J.lvl[tr][0][(r >> 8) & 127], prv = J.lvl[tr][0][(r >> 16) & 127];
             if (!cur && !prv) continue;
             const int lvl = cur ? cur : prv;
             uint16_t *row = &t[(sr * 4 + line) * LW + (APRON - 4 + e * 4)];
@@ -282,7 +295,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             const uint32_t r = rh[e * RH_C + col / 4];
             const int len = r & 15;
             if (!len) continue;
-            const int cur = a.lvl[tr][1][(r >> 8) & 127], prv = a.lvl[tr][1][(r >> 16) & 127];
+            const int cur = J.lvl[tr][1][(r >> 8) & 127], prv = J.lvl[tr][1][(r >> 16) & 127];
             if (!cur && !prv) continue;
             const int lvl = cur ? cur : prv;
             uint16_t *c = &t[(APRON - 4 + e * 4) * LW + APRON + col];
@@ -312,14 +325,25 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             if (tid == 0) {
                 unsigned long long tot = 0;
                 for (int w = 0; w < NTHR / 64; w++) tot += red[w];
-                atomicAdd(&a.sse[tr], tot);
+                atomicAdd(&a.sse[jb * MAX_TRIALS + tr], tot);
             }
         } else {
-            T *dst = (T *)a.dst;
+            T *dst = (T *)J.dst;
             for (int i = tid; i < TILE * TILE; i += NTHR) {
                 const int r = i / TILE, c = i % TILE;
-                if (r < th && c < tw) dst[(size_t)(y0 + r) * a.dst_stride + x0 + c] = (T)t[(APRON + r) * LW + APRON + c];
+                if (r < th && c < tw) dst[(size_t)(y0 + r) * J.dst_stride + x0 + c] = (T)t[(APRON + r) * LW + APRON + c];
             }
+        }
+    }
+    // trial: the last workgroup to finish reads the sums (8-B agent atomics on both sides; this lane's SSE adds have
+    // completed before its arrival is counted) and re-arms the accumulators for the next launch
+    if (TRIAL && tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(a.arrive, 1u) == gridDim.x - 1) {
+            for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) a.out[q] = atomicExch(&a.sse[q], 0ull);
+            atomicExch(a.arrive, 0u);
+            __threadfence_system(); // the sums reach the host before the word that announces them
+            __hip_atomic_store(&a.out[MAX_JOBS * MAX_TRIALS], a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -367,8 +391,11 @@ struct SvtGpuDlfState {
     uint32_t      *d_rec[2][2]; // [chroma][dir]
     int32_t        uw[2], uh[2]; // record grid per plane type
     void          *d_scratch;    // plane copy for in-place apply
-    unsigned long long *d_sse;   // trial results
-    unsigned long long *h_sse;   // pinned
+    unsigned long long *d_sse;   // trial accumulators [MAX_JOBS][MAX_TRIALS], zero between launches
+    unsigned int       *d_arrive; // trial workgroup arrivals, zero between launches
+    unsigned long long *h_sse;   // pinned, mapped: the trial results written by the kernel's last workgroup
+    unsigned long long *h_sse_dev; // its device address
+    unsigned long long  seq;       // last trial launch's sequence number
     int32_t        have_mi;
 };
 
@@ -422,17 +449,24 @@ bool plane_active(const SvtGpuLfParams &p, int plane) {
     return plane == 1 ? p.filter_level_u != 0 : p.filter_level_v != 0;
 }
 
-DlfTileArgs base_args(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane, const LevelTables &L) {
+DlfPlaneJob plane_job(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane) {
+    DlfPlaneJob j;
+    std::memset(&j, 0, sizeof j);
+    const int ch = plane > 0;
+    j.rec_v   = s->d_rec[ch][0];
+    j.rec_h   = s->d_rec[ch][1];
+    j.units_w = s->uw[ch];
+    j.pw      = f->pw[plane];
+    j.ph      = f->ph[plane];
+    j.tiles_x = (j.pw + TILE - 1) / TILE;
+    j.tiles   = j.tiles_x * ((j.ph + TILE - 1) / TILE);
+    return j;
+}
+
+DlfTileArgs base_args(const SvtGpuFrame *f, const LevelTables &L) {
     DlfTileArgs a;
     std::memset(&a, 0, sizeof a);
-    const int ch = plane > 0;
-    a.rec_v   = s->d_rec[ch][0];
-    a.rec_h   = s->d_rec[ch][1];
-    a.units_w = s->uw[ch];
-    a.pw      = f->pw[plane];
-    a.ph      = f->ph[plane];
-    a.bd      = f->bit_depth;
-    a.tiles_x = (a.pw + TILE - 1) / TILE;
+    a.bd = f->bit_depth;
     std::memcpy(a.mblim, L.mblim, 64);
     std::memcpy(a.lim, L.lim, 64);
     std::memcpy(a.hev, L.hev, 64);
@@ -440,7 +474,8 @@ DlfTileArgs base_args(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane, const 
 }
 
 int launch_tile(const DlfTileArgs &a, int bps, bool trial, hipStream_t st) {
-    const int tiles = a.tiles_x * ((a.ph + TILE - 1) / TILE);
+    int tiles = 0;
+    for (int j = 0; j < a.njob; j++) tiles += a.job[j].tiles;
     if (bps == 2) {
         if (trial) hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, true>), dim3(tiles), dim3(NTHR), 0, st, a);
         else       hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);
@@ -456,33 +491,6 @@ bool frame_matches(const SvtGpuDlfState *s, const SvtGpuFrame *f) {
     return f && f->width == s->width && f->height == s->height && (f->bit_depth == 8 || f->bit_depth == 10);
 }
 
-// level trial: SSE(source, filtered plane) for up to MAX_TRIALS parameter sets, recon untouched
-int trial_sse(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, int plane,
-              const SvtGpuLfParams *prm, int n, uint64_t *out, hipStream_t st) {
-    LevelTables L;
-    build_level_tables(prm[0], L);
-    DlfTileArgs a = base_args(s, recon, plane, L);
-    a.src        = recon->plane[plane];
-    a.src_stride = recon->stride[plane];
-    a.ref        = src->plane[plane];
-    a.ref_stride = src->stride[plane];
-    a.ntrial     = n;
-    a.sse        = s->d_sse;
-    for (int k = 0; k < n; k++) {
-        if (k) build_level_tables(prm[k], L);
-        const bool on = plane_active(prm[k], plane);
-        for (int dir = 0; dir < 2; dir++)
-            if (on) std::memcpy(a.lvl[k][dir], L.lvl[plane][dir], 128);
-    }
-    HIP_TRY(hipMemsetAsync(s->d_sse, 0, sizeof(unsigned long long) * MAX_TRIALS, st));
-    int rc = launch_tile(a, recon->bytes_per_sample, true, st);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(s->h_sse, s->d_sse, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    for (int k = 0; k < n; k++) out[k] = s->h_sse[k];
-    return SVTGPU_OK;
-}
-
 void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_filter_frame (:841-883)
     if (plane == 0) {
         if (dir != 1) p.filter_level[0] = lvl;
@@ -493,67 +501,128 @@ void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_fi
         p.filter_level_v = lvl;
 }
 
-// search_filter_level (EbDeblockingFilter.c:886-991)
-int search_level(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, SvtGpuLfParams &p,
-                 const int last[4], int dlf_avg, int early_exit, int only4x4, int plane, int dir, hipStream_t st,
-                 int *best_out) {
-    const int start = plane == 0 ? (dlf_avg ? last[0] : last[dir]) : last[plane + 1];
-    int       mid = clampi(start, 0, 63), step = mid < 16 ? 4 : mid / 4, direction = 0, conv = 0;
-    int64_t   err[64];
-    for (int i = 0; i < 64; i++) err[i] = -1;
-    auto eval = [&](const int *lv, int n) -> int { // evaluate the not-yet-known levels in one launch
-        SvtGpuLfParams q[MAX_TRIALS];
-        int            idx[MAX_TRIALS], m = 0;
-        for (int k = 0; k < n; k++) {
-            bool dup = err[lv[k]] >= 0;
-            for (int j = 0; j < m && !dup; j++) dup = idx[j] == lv[k];
-            if (!dup) {
-                q[m] = p;
-                set_trial_level(q[m], plane, dir, lv[k]);
-                idx[m++] = lv[k];
+// search_filter_level (EbDeblockingFilter.c:886-991) as a resumable state machine: pending() names the levels the
+// next step needs (advancing over steps whose levels are already known), feed() records their SSE.  Independent
+// searches (U and V) then share launches.
+struct LevelSearch {
+    int     plane, dir, early_exit, only4x4;
+    int     mid, step, direction = 0, conv = 0, best;
+    int64_t best_err = 0, bias = 0, err[64];
+    int     phase = 0; // 0: the start level; 1: bisection steps; 2: done
+    int     lo = 0, hi = 0;
+    bool    try_lo = false, try_hi = false;
+    int     req[MAX_TRIALS], nreq = 0;
+
+    LevelSearch(const int last[4], int dlf_avg, int early_exit_, int only4x4_, int plane_, int dir_)
+        : plane(plane_), dir(dir_), early_exit(early_exit_), only4x4(only4x4_) {
+        const int start = plane == 0 ? (dlf_avg ? last[0] : last[dir]) : last[plane + 1];
+        mid  = clampi(start, 0, 63);
+        step = mid < 16 ? 4 : mid / 4;
+        best = mid;
+        for (int i = 0; i < 64; i++) err[i] = -1;
+        req[0] = mid, nreq = 1;
+    }
+    // the next bisection step's candidates (try lo / hi around mid), or done
+    void next_request() {
+        if (step <= 0) {
+            phase = 2, nreq = 0;
+            return;
+        }
+        hi   = std::min(mid + step, 63), lo = std::max(mid - step, 0);
+        bias = (best_err >> (15 - (mid / 8))) * step;
+        if (!only4x4) bias >>= 1;
+        try_lo = direction <= 0 && lo != mid, try_hi = direction >= 0 && hi != mid;
+        nreq   = 0;
+        if (try_lo) req[nreq++] = lo;
+        if (try_hi) req[nreq++] = hi;
+    }
+    void resolve() {
+        if (phase == 0) {
+            best_err = err[mid], best = mid, phase = 1;
+        } else {
+            if (try_lo && err[lo] < best_err + bias) {
+                if (err[lo] < best_err) best_err = err[lo];
+                best = lo;
+            }
+            if (try_hi && err[hi] < best_err - bias) {
+                best_err = err[hi];
+                best     = hi;
+            }
+            if (best == mid) {
+                conv++;
+                step      = conv == early_exit ? 0 : step / 2;
+                direction = 0;
+            } else {
+                direction = best < mid ? -1 : 1;
+                mid       = best;
             }
         }
-        if (!m) return SVTGPU_OK;
-        uint64_t r[MAX_TRIALS];
-        int      rc = trial_sse(s, recon, src, plane, q, m, r, st);
-        if (rc) return rc;
-        for (int k = 0; k < m; k++) err[idx[k]] = (int64_t)r[k];
-        return SVTGPU_OK;
-    };
-    int rc = eval(&mid, 1);
-    if (rc) return rc;
-    int64_t best_err = err[mid];
-    int     best     = mid;
-    while (step > 0) {
-        const int hi = std::min(mid + step, 63), lo = std::max(mid - step, 0);
-        int64_t   bias = (best_err >> (15 - (mid / 8))) * step;
-        if (!only4x4) bias >>= 1;
-        const bool try_lo = direction <= 0 && lo != mid, try_hi = direction >= 0 && hi != mid;
-        int        lv[MAX_TRIALS], n = 0;
-        if (try_lo) lv[n++] = lo;
-        if (try_hi) lv[n++] = hi;
-        // (speculatively batching the next iteration's levels was measured slower: each extra luma level costs a
-        // ~45 us filter pass, more than the launch and read-back it saves)
-        if ((rc = eval(lv, n))) return rc;
-        if (try_lo && err[lo] < best_err + bias) {
-            if (err[lo] < best_err) best_err = err[lo];
-            best = lo;
-        }
-        if (try_hi && err[hi] < best_err - bias) {
-            best_err = err[hi];
-            best     = hi;
-        }
-        if (best == mid) {
-            conv++;
-            step      = conv == early_exit ? 0 : step / 2;
-            direction = 0;
-        } else {
-            direction = best < mid ? -1 : 1;
-            mid       = best;
-        }
+        next_request();
     }
-    *best_out = best;
-    return SVTGPU_OK;
+    int pending(int *lv) {
+        while (phase != 2) {
+            int m = 0;
+            for (int k = 0; k < nreq; k++) {
+                bool dup = err[req[k]] >= 0;
+                for (int j = 0; j < m && !dup; j++) dup = lv[j] == req[k];
+                if (!dup) lv[m++] = req[k];
+            }
+            if (m) return m;
+            resolve();
+        }
+        return 0;
+    }
+    void feed(const int *lv, int m, const unsigned long long *sse) {
+        for (int k = 0; k < m; k++) err[lv[k]] = (int64_t)sse[k];
+    }
+};
+
+// run searches side by side: each launch evaluates the pending levels of every unfinished search (one plane job
+// each), the SSE of every (job, level) comes back through mapped pinned memory; recon is never modified
+int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, const SvtGpuLfParams &p,
+                 LevelSearch *const *srch, int ns, hipStream_t st) {
+    for (;;) {
+        DlfTileArgs a;
+        int         lv[MAX_JOBS][MAX_TRIALS], m[MAX_JOBS], who[MAX_JOBS];
+        bool        first = true;
+        for (int i = 0; i < ns; i++) {
+            const int mi = srch[i]->pending(lv[i]);
+            if (!mi) continue;
+            const int plane = srch[i]->plane;
+            LevelTables L;
+            if (first) {
+                build_level_tables(p, L);
+                a     = base_args(recon, L);
+                first = false;
+            }
+            DlfPlaneJob &J = a.job[a.njob];
+            J              = plane_job(s, recon, plane);
+            J.src          = recon->plane[plane];
+            J.src_stride   = recon->stride[plane];
+            J.ref          = src->plane[plane];
+            J.ref_stride   = src->stride[plane];
+            J.ntrial       = mi;
+            for (int k = 0; k < mi; k++) {
+                SvtGpuLfParams q = p;
+                set_trial_level(q, plane, srch[i]->dir, lv[i][k]);
+                build_level_tables(q, L);
+                const bool on = plane_active(q, plane);
+                for (int dir = 0; dir < 2; dir++)
+                    if (on) std::memcpy(J.lvl[k][dir], L.lvl[plane][dir], 128);
+            }
+            m[a.njob]   = mi;
+            who[a.njob] = i;
+            a.njob++;
+        }
+        if (first) return SVTGPU_OK; // every search has finished
+        a.sse    = s->d_sse;
+        a.arrive = s->d_arrive;
+        a.out    = s->h_sse_dev;
+        a.seq    = ++s->seq;
+        if (int rc = launch_tile(a, recon->bytes_per_sample, true, st)) return rc;
+        if (int rc = svtgpu_wait_seq(s->h_sse + MAX_JOBS * MAX_TRIALS, a.seq, st)) return rc;
+        for (int j = 0; j < a.njob; j++) srch[who[j]]->feed(lv[who[j]], m[j], s->h_sse + j * MAX_TRIALS);
+    }
 }
 
 bool valid_params(const SvtGpuLfParams *p) {
@@ -582,8 +651,16 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
         for (int d = 0; d < 2 && e == hipSuccess; d++)
             e = hipMalloc(&s->d_rec[c][d], sizeof(uint32_t) * s->uw[c] * s->uh[c]);
     if (e == hipSuccess) e = hipMalloc(&s->d_scratch, (size_t)width * height * 2);
-    if (e == hipSuccess) e = hipMalloc(&s->d_sse, sizeof(unsigned long long) * MAX_TRIALS);
-    if (e == hipSuccess) e = hipHostMalloc(&s->h_sse, sizeof(unsigned long long) * MAX_TRIALS, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&s->d_sse, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS);
+    if (e == hipSuccess) e = hipMalloc(&s->d_arrive, sizeof(unsigned int));
+    if (e == hipSuccess) e = hipMemset(s->d_sse, 0, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS);
+    if (e == hipSuccess) e = hipMemset(s->d_arrive, 0, sizeof(unsigned int));
+    if (e == hipSuccess)
+        e = hipHostMalloc(&s->h_sse, sizeof(unsigned long long) * (MAX_JOBS * MAX_TRIALS + 1),
+                          hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) s->h_sse[MAX_JOBS * MAX_TRIALS] = 0;
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&s->h_sse_dev, s->h_sse, 0);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         svtgpu_dlf_state_destroy(s);
         svtgpu_set_last_hip_error(e, "dlf state alloc", __FILE__, __LINE__);
@@ -600,6 +677,7 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
         for (int d = 0; d < 2; d++) (void)hipFree(s->d_rec[c][d]);
     (void)hipFree(s->d_scratch);
     (void)hipFree(s->d_sse);
+    (void)hipFree(s->d_arrive);
     if (s->h_sse) (void)hipHostFree(s->h_sse);
     delete s;
 }
@@ -643,20 +721,23 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
                                          in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
             continue;
         }
-        DlfTileArgs a = base_args(s, in, pl, L);
+        DlfTileArgs  a = base_args(in, L);
+        DlfPlaneJob &J = a.job[0];
+        J              = plane_job(s, in, pl);
+        a.njob         = 1;
         if (in == out) {
             HIP_TRY(hipMemcpy2DAsync(s->d_scratch, in->pw[pl] * bps, in->plane[pl], in->stride[pl] * bps,
                                      in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
-            a.src        = s->d_scratch;
-            a.src_stride = in->pw[pl];
+            J.src        = s->d_scratch;
+            J.src_stride = in->pw[pl];
         } else {
-            a.src        = in->plane[pl];
-            a.src_stride = in->stride[pl];
+            J.src        = in->plane[pl];
+            J.src_stride = in->stride[pl];
         }
-        a.dst        = out->plane[pl];
-        a.dst_stride = out->stride[pl];
-        a.ntrial     = 1;
-        for (int dir = 0; dir < 2; dir++) std::memcpy(a.lvl[0][dir], L.lvl[pl][dir], 128);
+        J.dst        = out->plane[pl];
+        J.dst_stride = out->stride[pl];
+        J.ntrial     = 1;
+        for (int dir = 0; dir < 2; dir++) std::memcpy(J.lvl[0][dir], L.lvl[pl][dir], 128);
         int rc = launch_tile(a, (int)bps, false, st);
         if (rc) return rc;
     }
@@ -692,19 +773,18 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     SvtGpuLfParams p  = *params;
     p.sharpness_level = 0;
     const int last[4] = {p.filter_level[0], p.filter_level[1], p.filter_level_u, p.filter_level_v};
-    int       y = 0, u = 0, v = 0, rc;
-    if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 0, 2, st, &y)))
-        return rc;
-    p.filter_level[0] = p.filter_level[1] = y;
-    if (dlf_avg_uv && temporal_layer_index > 0) {
-        u = last[2];
-        v = last[3];
-    } else {
-        if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0, st, &u)))
-            return rc;
-        p.filter_level_u = u;
-        if ((rc = search_level(s, recon, source, p, last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0, st, &v)))
-            return rc;
+    int       u = last[2], v = last[3], rc;
+    LevelSearch ys(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 0, 2);
+    LevelSearch *yl[1] = {&ys};
+    if ((rc = run_searches(s, recon, source, p, yl, 1, st))) return rc;
+    p.filter_level[0] = p.filter_level[1] = ys.best;
+    if (!(dlf_avg_uv && temporal_layer_index > 0)) { // else the chroma levels stay (EbDeblockingFilter.c:1221-1229)
+        // the U and V searches are independent (a chroma trial filters only its own plane): run them together
+        LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
+        LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
+        LevelSearch *uv[2] = {&us, &vs};
+        if ((rc = run_searches(s, recon, source, p, uv, 2, st))) return rc;
+        u = us.best, v = vs.best;
     }
     p.filter_level_u = u;
     p.filter_level_v = v;

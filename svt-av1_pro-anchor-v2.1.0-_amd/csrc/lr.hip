@@ -252,14 +252,18 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
     s->width         = width;
     s->height        = height;
     hipError_t e     = hipSuccess;
-    for (int p = 0; p < 3 && e == hipSuccess; p++) {
+    size_t     nu    = 0;
+    for (int p = 0; p < 3; p++) {
         const int pw = p ? width / 2 : width, ph = p ? height / 2 : height;
         s->unit_size[p] = unit_size[p];
         s->hunits[p]    = count_units(unit_size[p], pw);
         s->vunits[p]    = count_units(unit_size[p], ph);
-        e = hipMalloc(&s->d_units[p], sizeof(SvtGpuRestUnit) * s->hunits[p] * s->vunits[p]);
-        if (e == hipSuccess) e = hipMemset(s->d_units[p], 0, sizeof(SvtGpuRestUnit) * s->hunits[p] * s->vunits[p]);
+        nu += (size_t)s->hunits[p] * s->vunits[p];
     }
+    e = hipMalloc(&s->d_units[0], sizeof(SvtGpuRestUnit) * nu);
+    if (e == hipSuccess) e = hipMemset(s->d_units[0], 0, sizeof(SvtGpuRestUnit) * nu);
+    if (e != hipSuccess) s->d_units[0] = nullptr;
+    for (int p = 1; p < 3 && s->d_units[0]; p++) s->d_units[p] = s->d_units[p - 1] + s->hunits[p - 1] * s->vunits[p - 1];
     if (e != hipSuccess) {
         svtgpu_lr_state_destroy(s);
         svtgpu_set_last_hip_error(e, "lr state alloc", __FILE__, __LINE__);
@@ -271,9 +275,10 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
 
 extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     if (!s) return;
-    for (int p = 0; p < 3; p++) (void)hipFree(s->d_units[p]);
+    (void)hipFree(s->d_units[0]);
     (void)hipFree(s->d_flt);
     (void)hipFree(s->d_work);
+    if (s->pin_free) (void)hipEventSynchronize(s->pin_free), (void)hipEventDestroy(s->pin_free);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
     lr_profiler_destroy(s->prof);
     delete s;

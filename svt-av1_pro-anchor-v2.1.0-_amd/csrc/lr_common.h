@@ -3,11 +3,13 @@
 #pragma once
 #include "svtgpu_internal.h"
 
+#include <vector>
+
 struct SvtGpuLrState {
     SvtGpuContext  *ctx;
     int32_t         width, height;
     int32_t         unit_size[3], hunits[3], vunits[3];
-    SvtGpuRestUnit *d_units[3];
+    SvtGpuRestUnit *d_units[3]; // one allocation, planes in order (the search uploads all three in one copy)
     // search scratch (allocated on the first svtgpu_lr_search_frame)
     int16_t        *d_flt;   // per plane [eps][2][W*H] self-guided filter outputs of every searched ep
     size_t          flt_bytes;
@@ -16,6 +18,10 @@ struct SvtGpuLrState {
     void           *h_pin;   // pinned host staging for the search's read-backs
     size_t          pin_bytes;
     void           *prof;    // per-kernel-class timing of the search (svtgpu_lr_profile), nullptr when off
+    // the tile/unit plan last uploaded into d_work (re-sent only when it changes or d_work moves)
+    void                *plan_work;
+    std::vector<uint8_t> plan_bytes;
+    hipEvent_t           pin_free; // the last copy out of h_pin has run: the host may rewrite it
 };
 void lr_profiler_destroy(void *prof);
 

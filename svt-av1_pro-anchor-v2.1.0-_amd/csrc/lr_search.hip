@@ -76,6 +76,31 @@ __device__ inline int px(const T *p, int stride, int W, int H, int y, int x) {
 __device__ inline unsigned long long wave_sum(unsigned long long v) { return wave_sum_lane63(v); }
 constexpr int WAVE_LAST = 63;
 
+// Work lists and live counts filled by thousands of lanes: one atomic per wave instead of one per lane (a single
+// counter hit by every lane serializes).  Every lane of the wave must call these.
+__device__ inline int wave_prefix(int v, int &total) { // exclusive prefix over the wave, and the wave total
+    const int lane = threadIdx.x & 63;
+    int       x    = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+__device__ inline int wave_alloc(int32_t *counter, int v) { // this lane's first slot of v in the counted list
+    int       tot;
+    const int ex   = wave_prefix(v, tot);
+    int       base = 0;
+    if ((threadIdx.x & 63) == 0 && tot) base = atomicAdd(counter, tot);
+    return __shfl(base, 0, 64) + ex;
+}
+__device__ inline void wave_count(int32_t *counter, bool live) {
+    const unsigned long long b = __ballot(live);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(counter, (int)__popcll(b));
+}
+
 // Kernel timing for svtgpu_lr_profile: with a slot `tk`, the earliest workgroup start (atomicMin) and the latest
 // workgroup end (atomicMax, at tk + PROF_NL * PROF_SP) of a launch on the 100 MHz s_memrealtime clock, spread over
 // PROF_SP addresses by workgroup index so that thousands of workgroups do not contend on one line -- the launch's
@@ -271,104 +296,175 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 
 // ---------------------------------------------------------------------------------------------
 // Wiener trial: SSE of every tile of a unit with a pending candidate, filtered with the unit's candidate taps
-// (hfilter[8], vfilter[8]); one workgroup per Wiener tile, units without a pending candidate (wact = 0) exit at
-// once.  Both passes run on packed int16 pairs with v_dot2_i32_i16, two outputs per lane: the staged tile
-// (columns x0-4 .. x0+w+3, rows y0-3 .. y0+h+3) is read as aligned column pairs, the horizontal output is stored
-// as row pairs.  Fixed lane mappings (no runtime divisions): staging in 18 groups of 4 pixels per row, the
-// horizontal pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
+// (hfilter[8], vfilter[8]).  The advance kernel lists those tiles (items); a fixed grid of persistent workgroups
+// takes contiguous runs of the list (XCD-aware, so neighbouring tiles share an L2) and software-pipelines them:
+// the next tile's global loads (its tile record, mode, cached pass or CDEF pixels, source pixels) are issued into
+// registers right after the current tile is staged in LDS, and land while the current tile is filtered.  Both
+// passes run on packed int16 pairs with v_dot2_i32_i16, two outputs per lane: the staged tile (columns
+// x0-4 .. x0+w+3, rows y0-3 .. y0+h+3) is read as aligned column pairs, the horizontal output is stored as row
+// pairs.  Fixed lane mappings (no runtime divisions): staging in 18 groups of 4 pixels per row, the horizontal
+// pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
 // ---------------------------------------------------------------------------------------------
 __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16); }
+
+template <typename T>
+__device__ inline uint2 load_group(const T *d, int stride, int W, int H, int yy, int xx) {
+    int q[4];
+    if (yy >= 0 && yy < H && xx >= 0 && xx + 4 <= W) {
+        load4(d + (size_t)yy * stride + xx, q);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) q[j] = px(d, stride, W, H, yy, xx + j);
+    }
+    return make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
+}
+
+// one tile's inputs in flight: record index, mode, and this lane's share of the pixels
+struct TrialFetch {
+    int   ti, mode;
+    uint2 dg[5];  // CDEF pixel groups (modes 1, 3): 71 rows x 18 groups over 256 lanes
+    uint4 tcv[3]; // cached horizontal pass (mode 2): 36 x 64 u32 over 256 lanes
+    uint2 sg[4];  // source groups: 64 rows x 16 groups
+};
+
+template <typename T>
+__device__ inline void trial_fetch(const SearchArgs &A, const int32_t *wact, const uint32_t *tcache, int ti,
+                                   TrialFetch &f) {
+    const Tile       t = A.tiles[ti];
+    const PlaneArgs &P = A.pl[t.plane];
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    f.ti   = ti;
+    f.mode = wact[t.unit];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = threadIdx.x + k * 256, r = i >> 4, g = i & 15;
+        if (r < t.h && 4 * g < t.w) {
+            int q[4];
+            load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g, q);
+            f.sg[k] = make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
+        }
+    }
+    if (f.mode == 2) {
+        const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int i = threadIdx.x + k * 256;
+            if (i < 36 * 64 / 4) f.tcv[k] = tc[i];
+        }
+    } else {
+        const int rows = t.h + 7, ng = (t.w + 8) >> 2;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
+            if (i < 71 * 18 && r < rows && g < ng) f.dg[k] = load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * g);
+        }
+    }
+}
 
 // wact[unit]: 0 no pending candidate; 1 full evaluation; a vertical-filter move (the candidate's hfilter is the
 // unit's current one): 2 the horizontal pass of that hfilter is cached per tile (tcache) -- only the vertical pass
 // runs; 3 not cached yet -- full evaluation that also stores its horizontal pass.
 template <typename T>
 __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
-                                                                const int32_t *wact, int32_t *cnt_next,
+                                                                const int32_t *wact, const int32_t *items,
+                                                                const int32_t *cnt_cur, int32_t *cnt_next,
                                                                 unsigned long long *err, unsigned long long *pc,
                                                                 unsigned long long *tk, uint32_t *tcache) {
     PROF_BEGIN(tk);
     constexpr int VS = 72;
     __shared__ __align__(16) uint16_t v[71 * VS];
     __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[1] = 0; // the next advance counts its live descents there
-    const int  ti   = xcd_swizzle(blockIdx.x, gridDim.x);
-    const Tile t    = A.tiles[ti];
-    const int  mode = wact[t.unit];
-    if (!mode) return;
-    uint32_t *tc = tcache + (size_t)ti * 36 * 64; // this tile's cached horizontal pass
-    if (pc && threadIdx.x == 0) // profiling: evaluated pixels (spread over PROF_SP counters)
-        atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), (unsigned long long)(t.w * t.h));
-    const PlaneArgs &P  = A.pl[t.plane];
-    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    const int16_t   *tp = taps + t.unit * 16;
-    int              h[8], w[8];
+    __shared__ __align__(16) uint16_t sv[64 * 64]; // the source tile
+    // the next advance lists its tiles and counts its live descents there
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
+    const int n  = cnt_cur[0];
+    const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int i0 = (int)((long long)n * lb / gridDim.x), i1 = (int)((long long)n * (lb + 1) / gridDim.x);
+    unsigned long long npx = 0;
+    TrialFetch f;
+    if (i0 < i1) trial_fetch<T>(A, wact, tcache, items[i0], f);
+    for (int it = i0; it < i1; it++) {
+        const int        ti = f.ti, mode = f.mode;
+        const Tile       t  = A.tiles[ti];
+        const PlaneArgs &P  = A.pl[t.plane];
+        // stage the fetched tile
 #pragma unroll
-    for (int k = 0; k < 8; k++) h[k] = tp[k], w[k] = tp[8 + k];
-    // pair weights: even output x (pairs at x, x+2, ...) and odd output x+1; the same for rows
-    const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
-    const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
-    const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
-    const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
-    const int      rows = t.h + 7, ng = (t.w + 8) >> 2, nyp = (t.h + 1) >> 1;
-    const WienerRound rr = wiener_round(P.bd);
-    if (mode == 2) {
-        for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = ((const uint4 *)tc)[i];
-        __syncthreads();
-    } else {
+        for (int k = 0; k < 4; k++) {
+            const int i = threadIdx.x + k * 256, r = i >> 4, g = i & 15;
+            if (r < t.h && 4 * g < t.w) *(uint2 *)(sv + r * 64 + 4 * g) = f.sg[k];
+        }
+        if (mode == 2) {
 #pragma unroll
-    for (int k = 0; k < (71 * 18 + 255) / 256; k++) {
-        const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
-        if (r >= rows || g >= ng) continue;
-        const int yy = t.y0 + r - 3, xx = t.x0 - 4 + 4 * g;
-        int       q[4];
-        if (yy >= 0 && yy < P.H && xx >= 0 && xx + 4 <= P.W) {
-            load4(d + (size_t)yy * P.dstride + xx, q);
+            for (int k = 0; k < 3; k++) {
+                const int i = threadIdx.x + k * 256;
+                if (i < 36 * 64 / 4) ((uint4 *)tq)[i] = f.tcv[k];
+            }
         } else {
+            const int rows = t.h + 7, ng = (t.w + 8) >> 2;
 #pragma unroll
-            for (int j = 0; j < 4; j++) q[j] = px(d, P.dstride, P.W, P.H, yy, xx + j);
-        }
-        *(uint2 *)(v + r * VS + 4 * g) = make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
-    }
-    __syncthreads();
-    const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
-    uint16_t         *tq16 = (uint16_t *)tq;
-    const int         xh   = 2 * (threadIdx.x & 31);
-    if (xh < t.w)
-        for (int r = threadIdx.x >> 5; r < rows; r += 8) {
-            const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
-            const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
-            const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
-            const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
-            const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
-            tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
-            tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
-        }
-    __syncthreads();
-    if (mode == 3) {
-        for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
-    }
-    }
-    uint32_t           e    = 0; // <= 32 outputs per lane: fits 32 bits
-    const int          maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
-    const int          x    = threadIdx.x & 63;
-    if (x < t.w)
-        for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
-            const int       y  = 2 * yp;
-            const uint32_t *c  = tq + yp * 64 + x;
-            const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
-            const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
-            const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
-            const T  *sp = s + (size_t)(t.y0 + y) * P.sstride + t.x0 + x;
-            const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
-            e += (uint32_t)(d0 * d0);
-            if (y + 1 < t.h) {
-                const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[P.sstride];
-                e += (uint32_t)(d1 * d1);
+            for (int k = 0; k < 5; k++) {
+                const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
+                if (i < 71 * 18 && r < rows && g < ng) *(uint2 *)(v + r * VS + 4 * g) = f.dg[k];
             }
         }
-    const unsigned long long et = wave_sum_u32_wide(e);
-    if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], et);
+        __syncthreads();
+        if (it + 1 < i1) trial_fetch<T>(A, wact, tcache, items[it + 1], f); // in flight during the passes
+        const int16_t *tp = taps + t.unit * 16;
+        int            h[8], w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = tp[k], w[k] = tp[8 + k];
+        // pair weights: even output x (pairs at x, x+2, ...) and odd output x+1; the same for rows
+        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
+        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
+        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
+        const int      rows = t.h + 7, nyp = (t.h + 1) >> 1;
+        const WienerRound rr = wiener_round(P.bd);
+        if (mode != 2) {
+            const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
+            uint16_t *tq16 = (uint16_t *)tq;
+            const int xh   = 2 * (threadIdx.x & 31);
+            if (xh < t.w)
+                for (int r = threadIdx.x >> 5; r < rows; r += 8) {
+                    const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
+                    const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
+                    const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
+                    const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
+                    const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
+                    tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
+                    tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
+                }
+            __syncthreads();
+            if (mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
+                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
+                for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
+            }
+        }
+        uint32_t  e    = 0; // <= 32 outputs per lane: fits 32 bits
+        const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
+        const int x    = threadIdx.x & 63;
+        if (x < t.w)
+            for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
+                const int       y  = 2 * yp;
+                const uint32_t *c  = tq + yp * 64 + x;
+                const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
+                const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
+                const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
+                const uint16_t *sp = sv + y * 64 + x;
+                const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
+                e += (uint32_t)(d0 * d0);
+                if (y + 1 < t.h) {
+                    const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[64];
+                    e += (uint32_t)(d1 * d1);
+                }
+            }
+        const unsigned long long et = wave_sum_u32_wide(e);
+        if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], et);
+        npx += (unsigned long long)(t.w * t.h);
+        __syncthreads(); // the next tile overwrites the LDS images
+    }
+    if (pc && threadIdx.x == 0 && npx) // profiling: evaluated pixels (spread over PROF_SP counters)
+        atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
     PROF_END(tk);
 }
 
@@ -961,10 +1057,11 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // ---------------------------------------------------------------------------------------------
 __device__ inline int32_t htag(const Descent &d) { return (int32_t)(d.vals & 0xFFFFFF); } // hfilter taps 0..2
 
-__device__ void wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
-                                   int32_t *ctag, int32_t *cnt, int first) {
+// returns 1 when the unit has a pending candidate (its tiles go on the next trial's list)
+__device__ int wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
+                                  int32_t *ctag, int first) {
     Descent d = ds[u];
-    if (d.done) return;
+    if (d.done) return 0;
     // a mode-3 trial stored the horizontal pass of the candidate's hfilter (a vertical move leaves it unchanged)
     if (!first && wact[u] == 3) ctag[u] = htag(d);
     if (!first) d.report((int64_t)err[u]);
@@ -975,17 +1072,24 @@ __device__ void wiener_advance_one(Descent *ds, int u, unsigned long long *err, 
         d.taps(0, v), set_wiener_taps(taps + 16 * u, v); // f = 0: hfilter, f = 1: vfilter
         d.taps(1, v), set_wiener_taps(taps + 16 * u + 8, v);
         wact[u] = (d.init || d.mf != 1) ? 1 : (ctag[u] == htag(d) ? 2 : 3);
-        atomicAdd(&cnt[1], 1);
+        ds[u]   = d;
+        return 1;
     }
     ds[u] = d;
+    return 0;
 }
 
 __global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
-                                                             int16_t *taps, int32_t *wact, int32_t *ctag, int32_t *cnt,
+                                                             int16_t *taps, int32_t *wact, int32_t *ctag,
+                                                             const int32_t *tile0, int32_t *items, int32_t *cnt,
                                                              int first, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < n) wiener_advance_one(ds, u, err, taps, wact, ctag, cnt, first);
+    const int u    = blockIdx.x * blockDim.x + threadIdx.x;
+    const int live = u < n ? wiener_advance_one(ds, u, err, taps, wact, ctag, first) : 0;
+    wave_count(&cnt[1], live);
+    // list the unit's tiles for the next trial (Wiener units are the first units: global index u)
+    const int t0 = live ? tile0[u] : 0, nt = live ? tile0[u + 1] - t0 : 0, pos = wave_alloc(&cnt[0], nt);
+    for (int k = 0; k < nt; k++) items[pos + k] = t0 + k;
     PROF_END(tk);
 }
 
@@ -1007,11 +1111,11 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 // VALU-bound and a deeper tree amortizes the per-pixel work over more candidates: the tree is always depth 3
 // (SG_SPEC_LIVE >= 0 would keep single-node trees while more than that many descents are live).
 constexpr int SG_SPEC_LIVE = -1;
-__device__ void sgr_advance_one(Descent *ds, int i, const int32_t *tile0, unsigned long long *err, int32_t *cand,
-                                uint32_t *candm, int32_t *ustamp, int32_t *items, const int32_t *cnt_cur, int32_t *cnt,
-                                int first, int stamp) {
+// returns 1 when the descent stays live; *list_unit = its unit when this descent lists the unit's tiles
+__device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
+                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit) {
     Descent d = ds[i];
-    if (d.done) return;
+    if (d.done) return 0;
     unsigned long long *e = err + (size_t)i * SG_NC;
     if (first) {
         d.next(); // the seed itself is the first candidate
@@ -1048,15 +1152,13 @@ __device__ void sgr_advance_one(Descent *ds, int i, const int32_t *tile0, unsign
             }
         }
         candm[i] = mask;
-        if (atomicExch(&ustamp[d.unit], stamp) != stamp) { // the unit's tiles are listed once per round
-            const int t0 = tile0[d.unit], nt = tile0[d.unit + 1] - t0, pos = atomicAdd(&cnt[0], nt);
-            for (int j = 0; j < nt; j++) items[pos + j] = t0 + j;
-        }
-        atomicAdd(&cnt[1], 1);
-    } else {
-        candm[i] = 0;
+        if (atomicExch(&ustamp[d.unit], stamp) != stamp) *list_unit = d.unit; // listed once per round
+        ds[i] = d;
+        return 1;
     }
-    ds[i] = d;
+    candm[i] = 0;
+    ds[i]    = d;
+    return 0;
 }
 
 __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
@@ -1064,8 +1166,12 @@ __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, co
                                                           int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
                                                           int32_t *cnt, int first, int stamp, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) sgr_advance_one(ds, i, tile0, err, cand, candm, ustamp, items, cnt_cur, cnt, first, stamp);
+    const int i    = blockIdx.x * blockDim.x + threadIdx.x;
+    int       lu   = -1;
+    const int live = i < n ? sgr_advance_one(ds, i, err, cand, candm, ustamp, cnt_cur, first, stamp, &lu) : 0;
+    wave_count(&cnt[1], live);
+    const int t0 = lu >= 0 ? tile0[lu] : 0, nt = lu >= 0 ? tile0[lu + 1] - t0 : 0, pos = wave_alloc(&cnt[0], nt);
+    for (int j = 0; j < nt; j++) items[pos + j] = t0 + j;
     PROF_END(tk);
 }
 
@@ -1223,45 +1329,82 @@ struct Carver {
     }
 };
 
-// device-clock timing of the search's launches by kernel class (svtgpu_lr_profile)
+// device-clock timing of the search's launches by kernel class (svtgpu_lr_profile).  Everything accumulates on the
+// device: after a search one small kernel folds its launches' slots into per-class tick totals (and re-arms the
+// slots), so a timed search adds no copies or host synchronization; the totals are read back only when asked for.
+struct ProfClasses {
+    uint8_t c[PROF_NL];
+};
+__global__ __launch_bounds__(PROF_NL) void prof_fold_kernel(unsigned long long *clk, int nl, const ProfClasses cls,
+                                                            unsigned long long *acc) {
+    const int i = threadIdx.x;
+    if (i >= nl) return;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int k = 0; k < PROF_SP; k++) {
+        t0 = min(t0, clk[i * PROF_SP + k]), t1 = max(t1, clk[(PROF_NL + i) * PROF_SP + k]);
+        clk[i * PROF_SP + k] = ~0ull, clk[(PROF_NL + i) * PROF_SP + k] = 0;
+    }
+    if (t0 != ~0ull && t1 >= t0) atomicAdd(&acc[cls.c[i]], t1 - t0);
+}
+
 struct LrProfiler {
     unsigned long long *d_clk = nullptr; // [PROF_NL][PROF_SP] workgroup starts (min), then the same of ends (max)
     unsigned long long *d_px  = nullptr; // [3][PROF_SP] evaluated pixels: trials, projection (pixel, ep), projection tiles
-    int                 nl = 0, cls[PROF_NL];
-    SvtGpuLrProfile     cur{}, last{};
+    unsigned long long *d_acc = nullptr; // [5] ticks per class, over the searches since the last read
+    int                 nl = 0, searches = 0;
+    ProfClasses         cls{};
+    int32_t             launches[5] = {0, 0, 0, 0, 0};
+    double              static_bytes[5] = {0, 0, 0, 0, 0}, bps = 2;
     bool                ok   = false;
     int32_t             mask = 31; // classes timed (bit c)
     LrProfiler() {
-        ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess;
+        ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess &&
+             hipMalloc(&d_acc, 8 * 5) == hipSuccess && hipMemset(d_clk, 0xFF, 8 * PROF_NL * PROF_SP) == hipSuccess &&
+             hipMemset(d_clk + PROF_NL * PROF_SP, 0, 8 * PROF_NL * PROF_SP) == hipSuccess &&
+             hipMemset(d_px, 0, 24 * PROF_SP) == hipSuccess && hipMemset(d_acc, 0, 8 * 5) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
     }
     ~LrProfiler() {
         (void)hipFree(d_clk);
         (void)hipFree(d_px);
+        (void)hipFree(d_acc);
     }
-    void start(hipStream_t st) {
-        nl = 0;
-        std::memset(&cur, 0, sizeof cur);
-        (void)hipMemsetAsync(d_clk, 0xFF, 8 * PROF_NL * PROF_SP, st);
-        (void)hipMemsetAsync(d_clk + PROF_NL * PROF_SP, 0, 8 * PROF_NL * PROF_SP, st);
-        (void)hipMemsetAsync(d_px, 0, 24 * PROF_SP, st);
-    }
+    void start() { nl = 0; }
     // the timing slot of one launch of class c (nullptr: not timed)
     unsigned long long *slot(int c) {
         if (!(mask >> c & 1) || nl >= PROF_NL) return nullptr;
-        cls[nl] = c;
-        cur.launches[c]++;
+        cls.c[nl] = (uint8_t)c;
+        launches[c]++;
         return d_clk + PROF_SP * nl++;
     }
-    void finish() { // after the stream is synchronized
-        std::vector<unsigned long long> h(2 * PROF_NL * PROF_SP);
-        if (hipMemcpy(h.data(), d_clk, 16 * PROF_NL * PROF_SP, hipMemcpyDeviceToHost) == hipSuccess)
-            for (int i = 0; i < nl; i++) {
-                unsigned long long t0 = ~0ull, t1 = 0;
-                for (int k = 0; k < PROF_SP; k++)
-                    t0 = std::min(t0, h[i * PROF_SP + k]), t1 = std::max(t1, h[(PROF_NL + i) * PROF_SP + k]);
-                if (t0 != ~0ull && t1 >= t0) cur.ms[cls[i]] += (float)((t1 - t0) * 1e-5);
-            }
-        last = cur;
+    int finish(hipStream_t st) { // enqueued after the search's launches
+        searches++;
+        if (!nl) return SVTGPU_OK;
+        hipLaunchKernelGGL(prof_fold_kernel, dim3(1), dim3(PROF_NL), 0, st, d_clk, nl, cls, d_acc);
+        HIP_TRY(hipGetLastError());
+        return SVTGPU_OK;
+    }
+    int read(SvtGpuLrProfile *out) { // totals since the last read, then reset
+        unsigned long long acc[5], pxs[3 * PROF_SP], px[3] = {0, 0, 0};
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(acc, d_acc, sizeof acc, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(pxs, d_px, sizeof pxs, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(d_acc, 0, sizeof acc));
+        HIP_TRY(hipMemset(d_px, 0, sizeof pxs));
+        HIP_TRY(hipDeviceSynchronize());
+        for (int k = 0; k < 3 * PROF_SP; k++) px[k / PROF_SP] += pxs[k];
+        std::memset(out, 0, sizeof *out);
+        for (int c = 0; c < 5; c++) {
+            out->launches[c] = launches[c];
+            out->ms[c]       = (float)(acc[c] * 1e-5); // 100 MHz ticks
+            out->bytes[c]    = static_bytes[c];
+        }
+        out->bytes[2] += (double)px[0] * 2 * bps;                     // x and source per evaluated pixel
+        out->bytes[3] += (double)px[1] * 4 + (double)px[2] * 2 * bps; // flt per (pixel, ep), x/source per tile
+        out->searches = searches;
+        searches      = 0;
+        for (int c = 0; c < 5; c++) launches[c] = 0, static_bytes[c] = 0;
+        return SVTGPU_OK;
     }
 };
 
@@ -1357,6 +1500,7 @@ void launch_stats(int win, Fn &&f) {
 }
 
 constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
+constexpr int WN_TRIAL_GRID = 768; // persistent Wiener trial workgroups (3 per CU)
 
 // plane p's Wiener window for the controls
 int plane_win(const SvtGpuLrSearchControls *c, int p) {
@@ -1437,28 +1581,35 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
     if (n_all == 0) return SVTGPU_OK; // an empty band
     // ---- device scratch and pinned staging ----
+    // three contiguous spans keep the host traffic to one copy each: the plan (uploaded when it changes), the
+    // accumulators zeroed per search, the results read back (o_sse is the last zeroed and the first read)
     Carver       dc;
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1));
-    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn);
-    const size_t o_wds = dc(sizeof(Descent) * n_wn), o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
+    const size_t plan_span = dc.off;
+    const size_t o_sum = dc(8 * n_all), o_mom = dc(40 * (size_t)npairs), o_sse = dc(8 * n_all);
+    const size_t zero_span = dc.off - o_sum;
+    const size_t o_sse2 = dc(8 * (size_t)n_sg), o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
+                 o_sds = dc(sizeof(Descent) * npairs);
+    const size_t res_span = dc.off - o_sse;
+    const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
+    const size_t o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
                  o_wact = dc(4 * (size_t)n_wn), o_ctag = dc(4 * (size_t)n_wn),
                  o_tcache = dc((size_t)36 * 64 * 4 * nt_wn);
-    const size_t o_mom = dc(40 * (size_t)npairs), o_sds = dc(sizeof(Descent) * npairs),
-                 o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
+    const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
                  o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
-                 o_sse2 = dc(8 * (size_t)n_sg), o_cnt = dc(32);
-    Carver       hc;
-    const size_t h_tiles = hc(sizeof(Tile) * nt_all), h_units = hc(sizeof(URect) * n_all), h_t0 = hc(4 * (n_all + 1));
-    const size_t h_sse = hc(8 * n_all), h_cnt = hc(16), h_wu = hc(sizeof(SvtGpuRestUnit) * n_wn);
-    const size_t h_wds = hc(sizeof(Descent) * n_wn), h_sds = hc(sizeof(Descent) * npairs), h_sse2 = hc(8 * (size_t)n_sg),
-                 h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
+                 o_witems = dc(4 * (size_t)nt_wn), o_cnt = dc(32);
+    Carver       hc; // host mirrors of the plan and result spans keep the device layout
+    const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(16), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
+    const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
+                 h_wds = h_res + (o_wds - o_sse), h_sds = h_res + (o_sds - o_sse);
     if (dc.off > s->work_bytes) {
         (void)hipFree(s->d_work);
         s->d_work = nullptr, s->work_bytes = 0;
         HIP_TRY(hipMalloc(&s->d_work, dc.off));
         s->work_bytes = dc.off;
+        s->plan_bytes.clear(); // nothing uploaded into the new buffer yet
     }
+    if (s->pin_free) HIP_TRY(hipEventSynchronize(s->pin_free)); // the previous search's upload has read h_pin
     if (hc.off > s->pin_bytes) {
         if (s->h_pin) (void)hipHostFree(s->h_pin);
         s->h_pin = nullptr, s->pin_bytes = 0;
@@ -1493,16 +1644,21 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     LrProfiler         *prof = (LrProfiler *)s->prof;
     unsigned long long *pc   = prof ? prof->d_px : nullptr;
     auto                run  = [&](int c, auto &&launch) { launch(prof ? prof->slot(c) : nullptr); };
-    if (prof) prof->start(st);
-    std::memcpy(hp(h_tiles), tiles.data(), sizeof(Tile) * nt_all);
-    std::memcpy(hp(h_units), units.data(), sizeof(URect) * n_all);
-    std::memcpy(hp(h_t0), tile0.data(), 4 * (n_all + 1));
-    HIP_TRY(hipMemcpyAsync(dp(o_tiles), hp(h_tiles), sizeof(Tile) * nt_all, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dp(o_units), hp(h_units), sizeof(URect) * n_all, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(dp(o_t0), hp(h_t0), 4 * (n_all + 1), hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(dp(o_sum), 0, 8 * (size_t)n_all, st));
-    HIP_TRY(hipMemsetAsync(dp(o_sse), 0, 8 * (size_t)n_all, st));
-    if (npairs) HIP_TRY(hipMemsetAsync(dp(o_mom), 0, 40 * (size_t)npairs, st));
+    if (prof) prof->start();
+    {
+        uint8_t *pl = (uint8_t *)hp(h_plan);
+        std::memset(pl, 0, plan_span);
+        std::memcpy(pl + o_tiles, tiles.data(), sizeof(Tile) * nt_all);
+        std::memcpy(pl + o_units, units.data(), sizeof(URect) * n_all);
+        std::memcpy(pl + o_t0, tile0.data(), 4 * (n_all + 1));
+        if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
+            std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
+            HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
+            s->plan_bytes.assign(pl, pl + plan_span);
+            s->plan_work = s->d_work;
+        }
+    }
+    HIP_TRY(hipMemsetAsync(dp(o_sum), 0, zero_span, st));
     run(0, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
@@ -1556,7 +1712,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, st)); // no cached horizontal pass
         hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
                            (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
-                           (int32_t *)dp(o_ctag), cnt, 1, (unsigned long long *)nullptr);
+                           (int32_t *)dp(o_ctag), (const int32_t *)d_t0, (int32_t *)dp(o_witems), cnt, 1,
+                           (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
     if (npairs) {
@@ -1577,15 +1734,16 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             int32_t *cur = cnt + 4 * (g & 1), *nxt = cnt + 4 * ((g + 1) & 1);
             if (wl) {
                 run(2, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(nt_wn), dim3(256), 0, st, A,
-                                       (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact), nxt,
+                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, WN_TRIAL_GRID)), dim3(256), 0, st,
+                                       A, (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact),
+                                       (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
                                        (unsigned long long *)dp(o_werr), pc, tk, (uint32_t *)dp(o_tcache));
                 });
                 run(4, [&](unsigned long long *tk) {
                     hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
                                        (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr),
-                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag), nxt, 0,
-                                       tk);
+                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag),
+                                       (const int32_t *)d_t0, (int32_t *)dp(o_witems), nxt, 0, tk);
                 });
             }
             if (sl) {
@@ -1620,14 +1778,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                                (unsigned long long *)dp(o_sse2), tk);
         });
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(hp(h_sse2), dp(o_sse2), 8 * (size_t)n_sg, hipMemcpyDeviceToHost, st));
     }
+    if (prof)
+        if (int rc = prof->finish(st)) return rc; // fold the launch timings on the device, no read-back
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
-    HIP_TRY(hipMemcpyAsync(hp(h_sse), dp(o_sse), 8 * n_all, hipMemcpyDeviceToHost, st));
-    if (n_wn) HIP_TRY(hipMemcpyAsync(hw, dp(o_wds), sizeof(Descent) * n_wn, hipMemcpyDeviceToHost, st));
-    if (n_wn) HIP_TRY(hipMemcpyAsync(wu, dp(o_wu), sizeof(SvtGpuRestUnit) * n_wn, hipMemcpyDeviceToHost, st));
-    if (npairs) HIP_TRY(hipMemcpyAsync(hs, dp(o_sds), sizeof(Descent) * npairs, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
     HIP_TRY(hipStreamSynchronize(st));
     mark(3);
     // ---- phase 5 (host): per-unit results and, for the whole frame, the RD finish ----
@@ -1663,15 +1819,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         if (frame_type) { // whole frame: units are in plane order, uloc[gu] == u
             finish_plane(c, p, q.win, rs.data() + q.unit_base, q.n, &frame_type[p], out + q.unit_base);
-            HIP_TRY(hipMemcpyAsync(s->d_units[p], out + q.unit_base, sizeof(SvtGpuRestUnit) * q.n,
-                                   hipMemcpyHostToDevice, st));
         }
     }
-    HIP_TRY(hipStreamSynchronize(st));
-    if (prof) { // algorithmic bytes per class (sample bytes bps, filter planes int16)
-        unsigned long long px[3] = {0, 0, 0}, pxs[3 * PROF_SP];
-        HIP_TRY(hipMemcpy(pxs, prof->d_px, sizeof pxs, hipMemcpyDeviceToHost));
-        for (int k = 0; k < 3 * PROF_SP; k++) px[k / PROF_SP] += pxs[k];
+    if (frame_type) // d_units holds the planes back to back in the same order: one upload
+        HIP_TRY(hipMemcpyAsync(s->d_units[0], out, sizeof(SvtGpuRestUnit) * n_all, hipMemcpyHostToDevice, st));
+    if (prof) { // algorithmic bytes per class (sample bytes bps, filter planes int16); the pixel-count parts at read
         const double bps = (double)sizeof(T);
         double       all = 0, wn = 0, sgb = 0, sgp = 0;
         for (int p = 0; p < nplanes; p++) {
@@ -1681,13 +1833,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             if (pp[p].wn) wn += area;
             if (pp[p].sg) sgb += area, sgp += area * pp[p].ne;
         }
-        prof->cur.bytes[0] = (all + wn) * 2 * bps;                       // unit sums, statistics: x and source
-        prof->cur.bytes[1] = sgb * 2 * bps + sgp * 4;                     // x and source in, flt0/flt1 out
-        prof->cur.bytes[2] = (double)px[0] * 2 * bps;                     // x and source per evaluated pixel
-        prof->cur.bytes[3] = (double)px[1] * 4 + (double)px[2] * 2 * bps; // flt per (pixel, ep), x/source per tile
-        prof->cur.bytes[4] = sgb * (4 + 2 * bps);                         // the chosen ep's SSE
-        prof->finish();
+        prof->bps = bps;
+        prof->static_bytes[0] += (all + wn) * 2 * bps; // unit sums, statistics: x and source
+        prof->static_bytes[1] += sgb * 2 * bps + sgp * 4; // x and source in, flt0/flt1 out
+        prof->static_bytes[4] += sgb * (4 + 2 * bps);     // the chosen ep's SSE
     }
+    // no wait for the units upload: the next search waits for this event before it rewrites the pinned staging
+    if (!s->pin_free) HIP_TRY(hipEventCreateWithFlags(&s->pin_free, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s->pin_free, st));
     mark(4);
     if (timing)
         std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d) %.3f  best %.3f  finish %.3f\n",
@@ -1725,10 +1878,11 @@ extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfi
     if (!s) return SVTGPU_ERR_INVALID_ARG;
     LrProfiler *pr = (LrProfiler *)s->prof;
     if (last) {
-        if (pr)
-            *last = pr->last;
-        else
+        if (pr) {
+            if (int rc = pr->read(last)) return rc;
+        } else {
             std::memset(last, 0, sizeof *last);
+        }
     }
     if (enable && !pr) {
         pr = new LrProfiler();

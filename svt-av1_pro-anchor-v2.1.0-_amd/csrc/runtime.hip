@@ -1,4 +1,5 @@
 // runtime.hip — device/context/frame management of the C ABI (include/svtgpu.h).
+#include <chrono>
 #include <cstring>
 #include <mutex>
 
@@ -93,6 +94,22 @@ SvtGpuContext        *svtgpu_default_context() {
     return g_default_ctx;
 }
 hipStream_t svtgpu_default_stream() { return svtgpu_default_context()->stream; }
+
+int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; it++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return SVTGPU_OK;
+        // after ~2 ms of spinning (a long kernel, or a failed launch) hand over to the runtime's wait
+        if ((it & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "device result word missing after stream synchronize", __FILE__,
+                                  __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    return SVTGPU_OK;
+}
 
 // ---------------------------------------------------------------------------------------------
 // frames

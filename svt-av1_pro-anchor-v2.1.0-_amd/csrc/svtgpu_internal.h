@@ -83,6 +83,8 @@ struct SvtGpuCdefFrameState {
     uint64_t      *d_pick_out;    // [chains][4] (best, j, k)
     int32_t       *d_pick_lev;    // [chains][2][16]
     int32_t       *d_fb_list;     // compacted non-skip FB indices
+    uint8_t       *h_pick;        // pinned, mapped: the pick's result (PickOut) then the per-FB strengths [nfb]
+    uint8_t       *h_pick_dev;    // its device address
     int32_t        pick_parts;
     int32_t        mask_all;      // mask == every block
     int32_t        fb_row_begin, fb_row_end; // band of FB rows searched/applied (tiling)
@@ -120,6 +122,11 @@ int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
                              const SvtGpuCdefParams *p, hipStream_t st);
 
 hipStream_t svtgpu_default_stream();
+// Host wait for a small device result: the kernel's last workgroup writes the payload into mapped pinned memory,
+// then (after a system-scope fence) the sequence word `seq`.  Spinning on that word returns as soon as it lands;
+// the stream's own synchronize wakes the host up tens of microseconds later, once per host round trip.  Falls
+// back to synchronizing `st` (and fails if the word is still missing after it).
+int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st);
 SvtGpuContext *svtgpu_default_context();
 static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;

@@ -140,7 +140,8 @@ class LrSearchControls(ctypes.Structure):
                 ("sgrproj_restore_cost", ctypes.c_int32 * 2)]
 
 
-LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 5), ("ms", np.float32, 5), ("bytes", np.float64, 5)], align=True)
+LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 5), ("ms", np.float32, 5), ("bytes", np.float64, 5),
+                             ("searches", np.int32)], align=True)
 LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYPE), ("sgrproj", REST_UNIT_DTYPE)],
                                 align=True)
 
@@ -568,9 +569,10 @@ class LrState:
     PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other")
 
     def profile(self, enable=True):
-        """svtgpu_lr_profile: HIP-event timing of the searches (enable: True = every class, a class name or a
-        list of names = those classes, False = off); returns the last timed search's per-class
-        {launches, ms, bytes} (kernel classes of svtgpu.h; untimed classes read 0)."""
+        """svtgpu_lr_profile: device-clock timing of the searches (enable: True = every class, a class name or a
+        list of names = those classes, False = off).  Returns the per-class {launches, ms, bytes} totals of the
+        searches timed since the previous call (kernel classes of svtgpu.h; untimed classes read 0) plus
+        "searches", their count; reading synchronizes the device."""
         if enable is True:
             mask = -1
         elif not enable:
@@ -580,8 +582,10 @@ class LrState:
             mask = sum(1 << self.PROFILE_CLASSES.index(c) for c in names)
         raw = np.zeros(1, LR_PROFILE_DTYPE)
         check(lib().svtgpu_lr_profile(self.h, mask, ptr(raw)))
-        return {c: {"launches": int(raw["launches"][0][i]), "ms": float(raw["ms"][0][i]),
-                    "bytes": float(raw["bytes"][0][i])} for i, c in enumerate(self.PROFILE_CLASSES)}
+        out = {c: {"launches": int(raw["launches"][0][i]), "ms": float(raw["ms"][0][i]),
+                   "bytes": float(raw["bytes"][0][i])} for i, c in enumerate(self.PROFILE_CLASSES)}
+        out["searches"] = int(raw["searches"][0])
+        return out
 
     def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
         ft = np.ascontiguousarray(frame_type, np.int32)

@@ -127,6 +127,8 @@ PICK_CASES = [
     (256, 128, 8, 12, (0, 0, 0, 0), 0, 0, 0, 1, 0),
     (384, 200, 10, 13, (40, 36, 12, 30), 1, 1, 1, 2, 1),
     (192, 192, 8, 14, (63, 5, 63, 0), 0, 1, 0, 3, 0),
+    (320, 256, 10, 16, (24, 24, 4, 50), 0, 0, 0, 0, 0),  # U and V searches of different lengths share launches
+    (264, 136, 10, 17, (12, 40, 60, 2), 0, 0, 0, 0, 1),
 ]
 
 
