@@ -279,6 +279,11 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     (void)hipFree(s->d_flt);
     (void)hipFree(s->d_work);
     if (s->pin_free) (void)hipEventSynchronize(s->pin_free), (void)hipEventDestroy(s->pin_free);
+    if (s->wst) (void)hipStreamSynchronize(s->wst), (void)hipStreamDestroy(s->wst);
+    if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+    if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+    for (hipEvent_t e : s->ev_batch)
+        if (e) (void)hipEventDestroy(e);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
     lr_profiler_destroy(s->prof);
     delete s;

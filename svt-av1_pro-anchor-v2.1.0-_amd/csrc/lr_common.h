@@ -22,6 +22,9 @@ struct SvtGpuLrState {
     void                *plan_work;
     std::vector<uint8_t> plan_bytes;
     hipEvent_t           pin_free; // the last copy out of h_pin has run: the host may rewrite it
+    hipStream_t          wst;      // the search's Wiener chain (the caller's stream carries the self-guided one)
+    hipEvent_t           ev_fork, ev_join;
+    hipEvent_t           ev_batch[4]; // [chain][slot]: a batch of descent rounds and its live-count read-back
 };
 void lr_profiler_destroy(void *prof);
 

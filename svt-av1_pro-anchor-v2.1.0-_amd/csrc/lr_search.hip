@@ -1599,7 +1599,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                  o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
                  o_witems = dc(4 * (size_t)nt_wn), o_cnt = dc(32);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
-    const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(16), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
+    const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
                  h_wds = h_res + (o_wds - o_sse), h_sds = h_res + (o_sds - o_sse);
     if (dc.off > s->work_bytes) {
@@ -1659,23 +1659,36 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
     }
     HIP_TRY(hipMemsetAsync(dp(o_sum), 0, zero_span, st));
+    auto *cnt = (int32_t *)dp(o_cnt); // [parity][wn items, wn live, sg items, sg live]
+    HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
     run(0, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
     });
     HIP_TRY(hipGetLastError());
+    // The Wiener chain (statistics, decomposition, trial rounds) and the self-guided chain (filters, seeds,
+    // projection rounds) are independent until the RD finish: the Wiener chain runs on a second stream, so its
+    // latency-bound rounds fill the gaps of the self-guided work and the other way round.
+    if (!s->wst) {
+        HIP_TRY(hipStreamCreateWithFlags(&s->wst, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    }
+    hipStream_t sw = s->wst;
+    HIP_TRY(hipEventRecord(s->ev_fork, st));
+    HIP_TRY(hipStreamWaitEvent(sw, s->ev_fork, 0));
     for (int p = 0; p < nplanes; p++) {
         const PlanePlan &q = pp[p];
         if (!q.wn) continue;
         long long *part = (long long *)dp(o_part) + q.part_off, *mh = (long long *)dp(o_mh) + q.mh_off;
         run(0, [&](unsigned long long *tk) {
             launch_stats(q.win, [&](auto wc) {
-                hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, st, A,
+                hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, sw, A,
                                    q.tile_base, (const unsigned long long *)dp(o_sum), part, tk);
             });
         });
         run(0, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, st, (const long long *)part,
+            hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, sw, (const long long *)part,
                                (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh, tk);
         });
         HIP_TRY(hipGetLastError());
@@ -1691,7 +1704,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     cfg.sg_refine[0] = c->sg_refine[0], cfg.sg_refine[1] = c->sg_refine[1];
     if (n_wn) {
         run(4, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, st, A, nplanes, (const int64_t *)dp(o_mh),
+            hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, sw, A, nplanes, (const int64_t *)dp(o_mh),
                                cfg, (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu), tk);
         });
         HIP_TRY(hipGetLastError());
@@ -1705,12 +1718,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    auto *cnt = (int32_t *)dp(o_cnt); // [parity][-, wn live, sg items, sg live]
-    HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
     if (n_wn) {
-        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, st));
-        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, st)); // no cached horizontal pass
-        hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_wds), n_wn,
+        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
+        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
+        hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, sw, (Descent *)dp(o_wds), n_wn,
                            (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
                            (int32_t *)dp(o_ctag), (const int32_t *)d_t0, (int32_t *)dp(o_witems), cnt, 1,
                            (unsigned long long *)nullptr);
@@ -1725,28 +1736,38 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                            (const int32_t *)cnt + 6, cnt + 2, 1, 1, (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
+    // Each chain runs in batches of ROUNDS_PER_BATCH rounds with the next batch already queued behind the one the
+    // host is checking (a chain whose descents have all finished turns the queued rounds into no-op launches), so
+    // neither stream waits for the host between batches.
     const int gs = std::max(1, nt_sg);
-    bool      wl = n_wn > 0, sl = npairs > 0;
-    int32_t  *hcnt = (int32_t *)hp(h_cnt);
-    int       g    = 0; // global round index
-    while (wl || sl) {
-        for (int b = 0; b < ROUNDS_PER_BATCH; b++, g++) {
-            int32_t *cur = cnt + 4 * (g & 1), *nxt = cnt + 4 * ((g + 1) & 1);
-            if (wl) {
+    struct Chain {
+        bool        live;
+        int         g = 0, head = 0, inflight = 0; // round index; ring of two batches in flight
+        hipStream_t stream;
+    } ch[2];
+    ch[0].live = n_wn > 0, ch[0].stream = sw;
+    ch[1].live = npairs > 0, ch[1].stream = st;
+    int32_t *hcnt = (int32_t *)hp(h_cnt); // [chain][slot][2]
+    for (int k = 0; k < 4; k++)
+        if (!s->ev_batch[k]) HIP_TRY(hipEventCreateWithFlags(&s->ev_batch[k], hipEventDisableTiming));
+    auto enqueue_batch = [&](int c) -> int {
+        Chain &C = ch[c];
+        for (int b = 0; b < ROUNDS_PER_BATCH; b++, C.g++) {
+            int32_t *cur = cnt + 4 * (C.g & 1), *nxt = cnt + 4 * ((C.g + 1) & 1);
+            if (c == 0) {
                 run(2, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, WN_TRIAL_GRID)), dim3(256), 0, st,
+                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, WN_TRIAL_GRID)), dim3(256), 0, sw,
                                        A, (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact),
                                        (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
                                        (unsigned long long *)dp(o_werr), pc, tk, (uint32_t *)dp(o_tcache));
                 });
                 run(4, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, st,
+                    hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, sw,
                                        (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr),
                                        (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag),
                                        (const int32_t *)d_t0, (int32_t *)dp(o_witems), nxt, 0, tk);
                 });
-            }
-            if (sl) {
+            } else {
                 run(3, [&](unsigned long long *tk) {
                     hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
                                        (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
@@ -1756,16 +1777,34 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                     hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
                                        (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
                                        (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
-                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, g + 2, tk);
+                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, C.g + 2, tk);
                 });
             }
         }
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(hcnt, cnt + 4 * (g & 1), 16, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        wl = wl && hcnt[1] > 0;
-        sl = sl && hcnt[3] > 0;
-        if (g > MAX_ROUNDS) return SVTGPU_ERR_INVALID_ARG; // a descent always terminates; guard anyway
+        const int k = (C.head + C.inflight) & 1; // the batch's live count, read after its last advance
+        HIP_TRY(hipMemcpyAsync(hcnt + (c * 2 + k) * 2, cnt + 4 * (C.g & 1) + 2 * c, 8, hipMemcpyDeviceToHost, C.stream));
+        HIP_TRY(hipEventRecord(s->ev_batch[c * 2 + k], C.stream));
+        C.inflight++;
+        return SVTGPU_OK;
+    };
+    while (ch[0].live || ch[1].live) {
+        for (int c = 0; c < 2; c++)
+            while (ch[c].live && ch[c].inflight < 2)
+                if (int rc = enqueue_batch(c)) return rc;
+        bool consumed = false; // spin until the oldest batch of a live chain has landed
+        while (!consumed) {
+            for (int c = 0; c < 2 && !consumed; c++) {
+                Chain &C = ch[c];
+                if (!C.live || !C.inflight) continue;
+                const hipError_t q = hipEventQuery(s->ev_batch[c * 2 + C.head]);
+                if (q == hipErrorNotReady) continue;
+                HIP_TRY(q);
+                C.live = hcnt[(c * 2 + C.head) * 2 + 1] > 0;
+                C.head ^= 1, C.inflight--, consumed = true;
+                if (C.g > MAX_ROUNDS) return SVTGPU_ERR_INVALID_ARG; // a descent always terminates; guard anyway
+            }
+        }
     }
     mark(2);
     // ---- phase 4: best ep and its clipped SSE; read back the descents ----
@@ -1779,6 +1818,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
     }
+    HIP_TRY(hipEventRecord(s->ev_join, sw)); // the Wiener chain joins the caller's stream
+    HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
     if (prof)
         if (int rc = prof->finish(st)) return rc; // fold the launch timings on the device, no read-back
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
@@ -1843,8 +1884,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipEventRecord(s->pin_free, st));
     mark(4);
     if (timing)
-        std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d) %.3f  best %.3f  finish %.3f\n",
-                     t_ph[0], t_ph[1], g, t_ph[2], t_ph[3], t_ph[4]);
+        std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d wn, %d sg) %.3f  best %.3f  finish %.3f\n",
+                     t_ph[0], t_ph[1], ch[0].g, ch[1].g, t_ph[2], t_ph[3], t_ph[4]);
     return SVTGPU_OK;
 }
 } // namespace
