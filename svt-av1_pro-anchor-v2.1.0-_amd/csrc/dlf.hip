@@ -184,7 +184,7 @@ constexpr int LW    = TILE + 2 * APRON; // 88 samples per LDS row
 constexpr int NTHR  = 256;
 constexpr int MAX_TRIALS = 2; // levels per trial launch (the bisection's lo and hi candidates)
 
-constexpr int MAX_JOBS   = 2; // planes per launch: the U and V level searches run side by side
+constexpr int MAX_JOBS   = 3; // planes per launch: the Y, U and V level searches run side by side
 
 // one plane of a launch
 struct DlfPlaneJob {
@@ -220,9 +220,11 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
     const int tid = threadIdx.x;
-    const int b = xcd_swizzle(blockIdx.x, gridDim.x), jb = (a.njob > 1 && b >= a.job[0].tiles) ? 1 : 0;
+    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    int       jb = 0, tb = b;
+    while (jb + 1 < a.njob && tb >= a.job[jb].tiles) tb -= a.job[jb].tiles, jb++;
     const DlfPlaneJob &J = a.job[jb];
-    const int tb = b - (jb ? a.job[0].tiles : 0), x0 = (tb % J.tiles_x) * TILE, y0 = (tb / J.tiles_x) * TILE;
+    const int x0 = (tb % J.tiles_x) * TILE, y0 = (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
 
@@ -773,21 +775,19 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     SvtGpuLfParams p  = *params;
     p.sharpness_level = 0;
     const int last[4] = {p.filter_level[0], p.filter_level[1], p.filter_level_u, p.filter_level_v};
-    int       u = last[2], v = last[3], rc;
+    int       rc;
+    // The three searches are independent: a trial filters only its own plane with its own level (the luma levels
+    // gate only the luma plane, EbDeblockingFilter.c:571-577), so they share launches.  With dlf_avg_uv on a
+    // non-base layer the chroma levels stay (EbDeblockingFilter.c:1221-1229).
+    const bool  search_uv = !(dlf_avg_uv && temporal_layer_index > 0);
     LevelSearch ys(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 0, 2);
-    LevelSearch *yl[1] = {&ys};
-    if ((rc = run_searches(s, recon, source, p, yl, 1, st))) return rc;
+    LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
+    LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
+    LevelSearch *all[3] = {&ys, &us, &vs};
+    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st))) return rc;
     p.filter_level[0] = p.filter_level[1] = ys.best;
-    if (!(dlf_avg_uv && temporal_layer_index > 0)) { // else the chroma levels stay (EbDeblockingFilter.c:1221-1229)
-        // the U and V searches are independent (a chroma trial filters only its own plane): run them together
-        LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
-        LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
-        LevelSearch *uv[2] = {&us, &vs};
-        if ((rc = run_searches(s, recon, source, p, uv, 2, st))) return rc;
-        u = us.best, v = vs.best;
-    }
-    p.filter_level_u = u;
-    p.filter_level_v = v;
+    p.filter_level_u = search_uv ? us.best : last[2];
+    p.filter_level_v = search_uv ? vs.best : last[3];
     *params          = p;
     return SVTGPU_OK;
 }
