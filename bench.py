@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
                     help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (= RCCL over xGMI) for the real runs; gloo rehearses N > 1 ranks sharing one GPU")
     return ap.parse_args()
 
 
@@ -119,9 +121,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    local = local % max(1, torch.cuda.device_count())  # ranks > GPUs only in a gloo rehearsal on one GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     n = world
     W, H, bd = a.width, a.height, a.bit_depth
     q, lam = a.base_q_idx, 60000
@@ -219,7 +225,7 @@ def main():
             lr_ft = lr.search(O, S, lr_ctrls, sp)
         else:
             recs = lr.search_units(O, S, lr_ctrls, lr_rb, lr_re, stream=sp)
-            recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, device="cuda")
+            recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, device="cuda" if a.dist_backend == "nccl" else None)
             lr_ft = []
             for p in range(3):
                 ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])

@@ -30,6 +30,7 @@ struct StepChain {
 struct StepArgs {
     const uint64_t *wmse;   // [sb_count][2][64] compacted, bias applied
     const int32_t  *count;  // sb_count, the number of non-skipped FBs (device)
+    const int32_t  *wide;   // nonzero when some wmse entry is >= 2^31 (the 32-bit path would not be exact)
     int32_t         chunk, start_gi, end_gi, step;
     uint64_t       *tot;    // [3][4][4096] rotating tot_mse accumulators
     int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
@@ -63,7 +64,7 @@ __global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_li
 }
 
 __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *fb_list, const int32_t *count,
-                                   int bias, uint64_t *wmse) {
+                                   int bias, uint64_t *wmse, int32_t *wide) {
     const int i = blockIdx.x;
     if (i >= *count) return;
     const int fb = fb_list[i];
@@ -71,6 +72,8 @@ __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *
     uint64_t  v = mse[((size_t)p * nfb + fb) * 64 + g];
     if (bias && g == 0) v = ((uint64_t)bias * v) >> 6;
     wmse[((size_t)i * 2 + p) * 64 + g] = v;
+    if (__any(v >> 31)) // m0 + m1 may leave 32 bits: the step kernels keep the 64-bit arithmetic
+        if ((threadIdx.x & 63) == 0) atomicOr(wide, 1);
 }
 
 // First minimum of tot over [start, end)^2 (svt_search_one_dual's final loop, EbEncCdef.c:670-679),
@@ -87,16 +90,19 @@ __device__ void tot_argmin(const uint64_t *tot, int start, int end, uint64_t *bv
             idx  = e;
         }
     }
-    bv[t] = best;
-    bi[t] = idx;
-    __syncthreads();
-    for (int w = NT / 2; w > 0; w >>= 1) {
-        if (t < w && (bv[t + w] < bv[t] || (bv[t + w] == bv[t] && bi[t + w] < bi[t]))) {
-            bv[t] = bv[t + w];
-            bi[t] = bi[t + w];
-        }
-        __syncthreads();
+    // (value, index) minimum over the wave with cross-lane shuffles, then over the 4 waves: 2 barriers instead of 8
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t ov = __shfl_xor(best, o);
+        const int      oi = __shfl_xor(idx, o);
+        if (ov < best || (ov == best && oi < idx)) best = ov, idx = oi;
     }
+    if ((t & 63) == 0) bv[t >> 6] = best, bi[t >> 6] = idx;
+    __syncthreads();
+    if (t == 0)
+        for (int w = 1; w < NT / 64; w++)
+            if (bv[w] < bv[0] || (bv[w] == bv[0] && bi[w] < bi[0])) bv[0] = bv[w], bi[0] = bi[w];
+    __syncthreads();
 }
 
 // One launch per greedy step: every active chain finishes its previous svt_search_one_dual call
@@ -161,15 +167,29 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         sbest[t] = b;
     }
     __syncthreads();
-    // 4. accumulate
+    // 4. accumulate.  When every entry is < 2^31 (the usual case: the check is in pick_gather_kernel), m0 + m1
+    // and the min stay in 32 bits and only the running sum is 64-bit: 4 ALU ops per term instead of 7
     const int k = t & 63, j0 = 16 * blockIdx.x + 4 * (t >> 6);
     uint64_t  acc[4] = {0, 0, 0, 0};
-    for (int f = 0; f < nfb; f++) {
-        const uint64_t b = sbest[f], m1k = m[f][64 + k];
+    if (!*A.wide) {
+        const uint32_t *m32 = (const uint32_t *)dyn; // low words: entry e of the chunk at m32[2 * e]
+        for (int f = 0; f < nfb; f++) {
+            const uint64_t b64 = sbest[f];
+            const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[2 * (f * 128 + 64 + k)];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint64_t v = m[f][j0 + u] + m1k;
-            acc[u] += v < b ? v : b;
+            for (int u = 0; u < 4; u++) {
+                const uint32_t v = m32[2 * (f * 128 + j0 + u)] + m1k;
+                acc[u] += min(v, b);
+            }
+        }
+    } else {
+        for (int f = 0; f < nfb; f++) {
+            const uint64_t b = sbest[f], m1k = m[f][64 + k];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t v = m[f][j0 + u] + m1k;
+                acc[u] += v < b ? v : b;
+            }
         }
     }
     uint64_t *cur = A.tot + ((size_t)(A.step % 3) * MAX_CHAINS + c) * 4096;
@@ -246,8 +266,6 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     const size_t wmse_elems = (size_t)nfb * 128;
     int32_t  *d_count = s->d_fb_list + nfb;
     hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count);
-    hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
-                       (int)ctrls->zero_fs_cost_bias, wmse);
     const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device
 
     StepArgs A;
@@ -259,8 +277,11 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     A.lev      = s->d_pick_lev;                                // [NSTEPS+1][4][32]
     A.fin      = s->d_pick_lev + (NSTEPS + 1) * MAX_CHAINS * 32; // [4][32]
     A.best     = s->d_pick_out;
-    HIP_TRY(hipMemsetAsync(A.lev, 0, sizeof(int32_t) * (NSTEPS + 2) * MAX_CHAINS * 32, st));
+    A.wide     = A.fin + MAX_CHAINS * 32 + 33; // after the chosen list (32) and nb
+    HIP_TRY(hipMemsetAsync(A.lev, 0, sizeof(int32_t) * ((NSTEPS + 2) * MAX_CHAINS * 32 + 64), st));
     HIP_TRY(hipMemsetAsync(A.tot, 0, sizeof(uint64_t) * MAX_CHAINS * 4096, st)); // tot[0]
+    hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
+                       (int)ctrls->zero_fs_cost_bias, wmse, (int32_t *)A.wide);
     for (int step = 0; step <= NSTEPS; step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {

@@ -214,16 +214,19 @@ struct DlfTileArgs {
 template <typename T, bool TRIAL>
 __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ __align__(16) uint16_t t[LW * LW];
-    __shared__ __align__(16) uint16_t t0[TRIAL ? LW * LW : 8];       // the staged tile, kept for every trial
-    __shared__ __align__(16) uint16_t sref[TRIAL ? TILE * TILE : 8]; // the source tile (trial SSE)
     __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
     const int tid = threadIdx.x;
+    // one (plane job, tile, trial) per workgroup: the trials of a tile are neighbours after the XCD swizzle, so
+    // the second staging of a tile hits the L2; one working image in LDS (18 KB) keeps 8 waves per SIMD
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
     int       jb = 0, tb = b;
-    while (jb + 1 < a.njob && tb >= a.job[jb].tiles) tb -= a.job[jb].tiles, jb++;
+    while (jb + 1 < a.njob && tb >= a.job[jb].tiles * (TRIAL ? a.job[jb].ntrial : 1))
+        tb -= a.job[jb].tiles * (TRIAL ? a.job[jb].ntrial : 1), jb++;
     const DlfPlaneJob &J = a.job[jb];
+    const int tr = TRIAL ? tb % J.ntrial : 0;
+    if (TRIAL) tb /= J.ntrial;
     const int x0 = (tb % J.tiles_x) * TILE, y0 = (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
@@ -239,9 +242,8 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         rh[i] = (ur >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_h[(size_t)ur * J.units_w + uc] : 0u;
     }
 
-    // stage the tile + apron once (samples outside the plane are never read by an active edge), 4 per item;
+    // stage the tile + apron (samples outside the plane are never read by an active edge), 4 per item;
     // gx is a multiple of 4, so interior groups are aligned
-    uint16_t *stage = TRIAL ? t0 : t;
     for (int i = tid; i < LW * LW / 4; i += NTHR) {
         const int r = gy + i / (LW / 4), c = gx + 4 * (i % (LW / 4));
         uint16_t  q[4];
@@ -254,22 +256,10 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             for (int j = 0; j < 4; j++)
                 q[j] = (r >= 0 && c + j >= 0 && r < J.ph && c + j < J.pw) ? (uint16_t)src[(size_t)r * J.src_stride + c + j] : 0;
         }
-        *(uint2 *)&stage[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
+        *(uint2 *)&t[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
     }
     const int tw = min(TILE, J.pw - x0), th = min(TILE, J.ph - y0);
-    if (TRIAL) {
-        const T *ref = (const T *)J.ref;
-        for (int i = tid; i < TILE * TILE; i += NTHR) {
-            const int r = i / TILE, c = i % TILE;
-            sref[i]     = (r < th && c < tw) ? (uint16_t)ref[(size_t)(y0 + r) * J.ref_stride + x0 + c] : 0;
-        }
-    }
-
-    for (int tr = 0; tr < (TRIAL ? J.ntrial : 1); tr++) {
-        if (TRIAL) { // every trial starts from the staged samples
-            __syncthreads();
-            for (int i = tid; i < LW * LW / 8; i += NTHR) ((uint4 *)t)[i] = ((const uint4 *)t0)[i];
-        }
+    {
         __syncthreads();
         // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
         for (int i = tid; i < ((DLF_EXP & 1) ? 0 : RV_R * RV_C * 4); i += NTHR) {
@@ -313,14 +303,14 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         __syncthreads();
         // emit the tile
         if (TRIAL) {
-            uint32_t s = 0; // <= 16 samples per lane
-            for (int i = tid; i < TILE * TILE; i += NTHR) {
-                const int r = i / TILE, c = i % TILE;
-                if (r < th && c < tw) {
-                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)sref[i];
+            uint32_t  s = 0; // <= 16 samples per lane
+            const T  *ref = (const T *)J.ref;
+            const int c = tid % TILE;
+            if (c < tw)
+                for (int r = tid / TILE; r < th; r += NTHR / TILE) {
+                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)ref[(size_t)(y0 + r) * J.ref_stride + x0 + c];
                     s += (uint32_t)(d * d);
                 }
-            }
             const unsigned long long sw = wave_sum_u32_wide(s);
             if ((tid & 63) == 63) red[tid >> 6] = sw;
             __syncthreads();
@@ -476,8 +466,8 @@ DlfTileArgs base_args(const SvtGpuFrame *f, const LevelTables &L) {
 }
 
 int launch_tile(const DlfTileArgs &a, int bps, bool trial, hipStream_t st) {
-    int tiles = 0;
-    for (int j = 0; j < a.njob; j++) tiles += a.job[j].tiles;
+    int tiles = 0; // workgroups: one per tile (apply) or per (tile, trial)
+    for (int j = 0; j < a.njob; j++) tiles += a.job[j].tiles * (trial ? a.job[j].ntrial : 1);
     if (bps == 2) {
         if (trial) hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, true>), dim3(tiles), dim3(NTHR), 0, st, a);
         else       hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);

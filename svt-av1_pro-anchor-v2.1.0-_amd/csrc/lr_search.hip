@@ -1500,7 +1500,14 @@ void launch_stats(int win, Fn &&f) {
 }
 
 constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
-constexpr int WN_TRIAL_GRID = 768; // persistent Wiener trial workgroups (3 per CU)
+constexpr int WN_TRIAL_GRID = 768; // persistent Wiener trial workgroups (3 per CU); SVTGPU_WN_GRID overrides (sweeps)
+int wn_trial_grid() {
+    static const int g = [] {
+        const char *e = std::getenv("SVTGPU_WN_GRID");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : WN_TRIAL_GRID;
+    }();
+    return g;
+}
 
 // plane p's Wiener window for the controls
 int plane_win(const SvtGpuLrSearchControls *c, int p) {
@@ -1756,7 +1763,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             int32_t *cur = cnt + 4 * (C.g & 1), *nxt = cnt + 4 * ((C.g + 1) & 1);
             if (c == 0) {
                 run(2, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, WN_TRIAL_GRID)), dim3(256), 0, sw,
+                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, wn_trial_grid())), dim3(256), 0, sw,
                                        A, (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact),
                                        (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
                                        (unsigned long long *)dp(o_werr), pc, tk, (uint32_t *)dp(o_tcache));

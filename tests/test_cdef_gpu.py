@@ -225,3 +225,25 @@ def test_cdef_band_search_allreduce(ctx, nb):
     assert prm1.as_tuple() == prm2.as_tuple() and np.array_equal(fbs1, fbs2)
     for a, b in zip(O1.download(), O2.download()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("top", [1 << 31, 1 << 40])
+def test_cdef_pick_bound_tables_vs_oracle(ctx, top):
+    """The frame pick over arbitrary mse tables: entries just below 2^31 (the 32-bit accumulation path, sums of
+    two entries up to 2^32 - 2) and up to 2^40 (the 64-bit path), random skipped FBs; bit-exact vs the oracle."""
+    import torch
+    w, h, q, lam = 1024, 512, 128, 60000
+    ctrls = svtgpu.cdef_controls(1)
+    st = svtgpu.CdefState(ctx, w, h)
+    rng = np.random.default_rng(top % 1000003)
+    mse = (top - 1 - rng.integers(0, top // 64, size=(2, st.nfb, 64), dtype=np.int64)).astype(np.uint64)
+    mse[:, :, 0] = rng.integers(0, top // 2, size=(2, st.nfb)).astype(np.uint64)  # strength 0 often best
+    skip = (rng.random(st.nfb) < 0.1).astype(np.uint8)
+    mse_t = torch.from_numpy(mse.view(np.int64)).cuda()
+    skip_t = torch.from_numpy(skip).cuda()
+    st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+    torch.cuda.synchronize()
+    prm, fbs = st.pick(ctrls, q, lam)
+    oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
+    assert prm.as_tuple() == oprm.as_tuple()
+    assert np.array_equal(fbs, ofbs)
