@@ -34,9 +34,15 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
+
+# the frames in flight need more than HIP's default 4 hardware queues per process (each frame runs on 3 streams);
+# set before the HIP runtime starts
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
@@ -77,6 +83,9 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
                     help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
+    ap.add_argument("--frames-in-flight", type=int, default=2,
+                    help="frames pipelined per GPU, each on its own streams and host thread (the encoder's "
+                         "picture-level parallelism); a step processes one frame per slot")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for the real runs; gloo rehearses N > 1 ranks sharing one GPU")
     return ap.parse_args()
@@ -133,125 +142,155 @@ def main():
     q, lam = a.base_q_idx, 60000
 
     ctx = svtgpu.Context(local)
-    # a non-default torch stream: the library launches on it, torch events time it, RCCL orders on it
-    stream = torch.cuda.Stream()
-    torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
-    src, rec = synth.frame_pair(W, H, bd, seed=0x5EED0003)
-    R, S, D, O = (svtgpu.Frame(ctx, W, H, bd) for _ in range(4))
-    R.upload(rec, sp)
-    S.upload(src, sp)
+    ctrls = svtgpu.cdef_controls(a.cdef_level)
+    nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
+    rows = np.linspace(0, nvfb, n + 1).round().astype(int)
+    cdef_rows = (int(rows[rank]), int(rows[rank + 1]))
     mi = synth.mode_info(W, H, 3)
-    dl = svtgpu.DlfState(ctx, W, H)
-    dl.set_mode_info(mi, sp)
     lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
     # loop restoration: RU 256 / 128, wn_filter_lvl 1 + sg_filter_lvl 1 (maximum search work); the rate
     # inputs (rdmult, restore-type costs) come from the encoder's entropy state: fixed representative values
     lr_us = [256, 128, 128]
-    lr = svtgpu.LrState(ctx, W, H, lr_us)
     lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=7000, switchable=(300, 700, 900), wiener=(250, 800),
                                   sgrproj=(250, 900))
-    L = svtgpu.Frame(ctx, W, H, bd)
     NREF = 7
-    md_refs, md_ref_y = [], []
+    md_refs, md_ref_y = [], []  # reference frames of the MD batch, shared by the frames in flight
     for r in range(NREF):
         rs, _ = synth.frame_pair(W, H, bd, seed=0x5EED0005 + 17 * (r + 1))
         f = svtgpu.Frame(ctx, W, H, bd)
-        f.upload(rs, sp)
+        f.upload(rs)
         md_refs.append(f)
         md_ref_y.append(rs[0])
-    md = svtgpu.MdBatch(ctx, W, H, NREF)
-    md_mvs = np.random.default_rng(5).integers(-16, 17, size=(md.nsb, NREF, 2))
-    md.set_mvs(md_mvs, sp)
-    ctrls = svtgpu.cdef_controls(a.cdef_level)
-    st = svtgpu.CdefState(ctx, W, H)
-    nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
-    if n > 1:
-        rows = np.linspace(0, nvfb, n + 1).round().astype(int)
-        cdef_rows = (int(rows[rank]), int(rows[rank + 1]))
-        st.set_fb_rows(*cdef_rows)
-        mse_t = torch.zeros((2, st.nfb, 64), dtype=torch.int64, device="cuda")
-        skip_t = torch.zeros(st.nfb, dtype=torch.uint8, device="cuda")
-        dir_t = torch.zeros((st.nfb, 64), dtype=torch.uint8, device="cuda")
-        var_t = torch.zeros((st.nfb, 64), dtype=torch.int32, device="cuda")
-        st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
-        st.bind_dir_tables(dir_t.data_ptr(), var_t.data_ptr())
+    torch.cuda.synchronize()
 
-    ev = []  # per step: events on the stream the kernels run on (dlf | cdef search | cdef pick+apply | lr | md)
-    md_range = svtgpu.band(md.nsb, n, rank)  # MD batch: SB ranges, no collective
-    lr_rb, lr_re = svtgpu.lr_unit_rows(lr.units, n, rank)  # LR search: unit-row bands, records all-gathered
-    lf_levels = []
+    class Slot:
+        """One frame in flight: its own input frames, stage states, streams and (N > 1) process group."""
 
-    md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
+        def __init__(self, k):
+            self.k = k
+            # a non-default torch stream: the library launches on it, torch events time it, RCCL orders on it
+            self.stream = torch.cuda.Stream()
+            self.md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
+            sp = self.stream.cuda_stream
+            self.src, self.rec = synth.frame_pair(W, H, bd, seed=0x5EED0003 + 0x100 * k)
+            self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
+            self.R.upload(self.rec, sp)
+            self.S.upload(self.src, sp)
+            self.dl = svtgpu.DlfState(ctx, W, H)
+            self.dl.set_mode_info(mi, sp)
+            self.lr = svtgpu.LrState(ctx, W, H, lr_us)
+            self.md = svtgpu.MdBatch(ctx, W, H, NREF)
+            self.md_mvs = np.random.default_rng(5 + k).integers(-16, 17, size=(self.md.nsb, NREF, 2))
+            self.md.set_mvs(self.md_mvs, sp)
+            self.st = svtgpu.CdefState(ctx, W, H)
+            self.group = dist.new_group(backend=a.dist_backend) if n > 1 else None  # one communicator per slot
+            if n > 1:
+                self.st.set_fb_rows(*cdef_rows)
+                self.mse_t = torch.zeros((2, self.st.nfb, 64), dtype=torch.int64, device="cuda")
+                self.skip_t = torch.zeros(self.st.nfb, dtype=torch.uint8, device="cuda")
+                self.dir_t = torch.zeros((self.st.nfb, 64), dtype=torch.uint8, device="cuda")
+                self.var_t = torch.zeros((self.st.nfb, 64), dtype=torch.int32, device="cuda")
+                self.st.bind_tables(self.mse_t.data_ptr(), self.skip_t.data_ptr())
+                self.st.bind_dir_tables(self.dir_t.data_ptr(), self.var_t.data_ptr())
+            self.md_range = svtgpu.band(self.md.nsb, n, rank)  # MD batch: SB ranges, no collective
+            self.lr_rb, self.lr_re = svtgpu.lr_unit_rows(self.lr.units, n, rank)  # LR: unit-row bands, all-gather
+            self.ev = []  # per timed step: events on the streams the kernels run on
+            self.lf_levels = []
 
-    def step(timed):
-        es = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if timed else None
-        if timed:
-            es[0].record(stream)
-        # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
-        lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
-        dl.filter_to(R, D, lfp, 0, 3, sp)
-        if timed:
-            es[1].record(stream)
-            lf_levels.append(lfp.levels())
-        # CDEF stage on the deblocked frame
-        if n > 1:
-            st.clear_tables(sp)
-        st.search(D, S, ctrls, q, sp)
-        if timed:
-            es[2].record(stream)
-        if n > 1:
-            dist.all_reduce(mse_t)   # zero-padded band tables -> full frame tables (RCCL over xGMI)
-            dist.all_reduce(skip_t)
-            dist.all_reduce(dir_t)
-            dist.all_reduce(var_t)
-            st.set_fb_rows(0, nvfb)  # every rank applies the whole frame: the LR search bands read all of O
-        prm, _ = st.pick(ctrls, q, lam, sp)
-        st.apply(D, O, prm, sp)
-        if n > 1:
-            st.set_fb_rows(cdef_rows[0], cdef_rows[1])
-        if timed:
-            es[3].record(stream)
-        # MD distortion batch (source vs 7 references, every block shape): independent of the filter chain, on its
-        # own stream from here to the end of the step
-        md_stream.wait_stream(stream)
-        if timed:
-            es[6].record(md_stream)
-        md.run(S, md_refs, md_range[0], md_range[1], md_stream.cuda_stream)
-        if timed:
-            es[7].record(md_stream)
-        # LR search + apply on the CDEF output (boundary lines from the DLF output)
-        if n == 1:
-            lr_ft = lr.search(O, S, lr_ctrls, sp)
+        def step(self, timed):
+            torch.cuda.set_stream(self.stream)  # per thread
+            stream, md_stream, sp = self.stream, self.md_stream, self.stream.cuda_stream
+            R, S, D, O, L, st, lr, dl = self.R, self.S, self.D, self.O, self.L, self.st, self.lr, self.dl
+            es = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if timed else None
+            if timed:
+                es[0].record(stream)
+            # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
+            lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
+            dl.filter_to(R, D, lfp, 0, 3, sp)
+            if timed:
+                es[1].record(stream)
+                self.lf_levels.append(lfp.levels())
+            # CDEF stage on the deblocked frame
+            if n > 1:
+                st.clear_tables(sp)
+            st.search(D, S, ctrls, q, sp)
+            if timed:
+                es[2].record(stream)
+            if n > 1:
+                for t in (self.mse_t, self.skip_t, self.dir_t, self.var_t):  # zero-padded band tables -> frame
+                    dist.all_reduce(t, group=self.group)                    # tables (RCCL over xGMI)
+                st.set_fb_rows(0, nvfb)  # every rank applies the whole frame: the LR search bands read all of O
+            prm, _ = st.pick(ctrls, q, lam, sp)
+            st.apply(D, O, prm, sp)
+            if n > 1:
+                st.set_fb_rows(*cdef_rows)
+            if timed:
+                es[3].record(stream)
+            # MD distortion batch (source vs 7 references, every block shape): independent of the filter chain, on
+            # its own stream from here to the end of the step
+            md_stream.wait_stream(stream)
+            if timed:
+                es[6].record(md_stream)
+            self.md.run(S, md_refs, self.md_range[0], self.md_range[1], md_stream.cuda_stream)
+            if timed:
+                es[7].record(md_stream)
+            # LR search + apply on the CDEF output (boundary lines from the DLF output)
+            if n == 1:
+                lr_ft = lr.search(O, S, lr_ctrls, sp)
+            else:
+                recs = lr.search_units(O, S, lr_ctrls, self.lr_rb, self.lr_re, stream=sp)
+                recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, group=self.group,
+                                                device="cuda" if a.dist_backend == "nccl" else None)
+                lr_ft = []
+                for p in range(3):
+                    ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])
+                    lr.set_units(p, units_p, sp)
+                    lr_ft.append(ftp)
+            lr.apply(D, O, L, lr_ft, sp)
+            if timed:
+                es[4].record(stream)
+            stream.wait_stream(md_stream)  # the step ends when both streams are done
+            if timed:
+                es[5].record(stream)
+                self.ev.append(es)
+
+    F = a.frames_in_flight
+    slots = [Slot(k) for k in range(F)]
+    torch.cuda.synchronize()
+    lr = slots[0].lr
+
+    errors = []
+
+    def run(slot, steps, timed):
+        try:
+            for _ in range(steps):
+                slot.step(timed)
+        except BaseException as e:  # re-raised on the main thread
+            errors.append(e)
+
+    def run_all(steps, timed):
+        if F == 1:
+            run(slots[0], steps, timed)
         else:
-            recs = lr.search_units(O, S, lr_ctrls, lr_rb, lr_re, stream=sp)
-            recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, device="cuda" if a.dist_backend == "nccl" else None)
-            lr_ft = []
-            for p in range(3):
-                ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])
-                lr.set_units(p, units_p, sp)
-                lr_ft.append(ftp)
-        lr.apply(D, O, L, lr_ft, sp)
-        if timed:
-            es[4].record(stream)
-        stream.wait_stream(md_stream)  # the step ends when both streams are done
-        if timed:
-            es[5].record(stream)
-            ev.append(es)
+            th = [threading.Thread(target=run, args=(sl, steps, timed)) for sl in slots]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+        if errors:
+            raise errors[0]
 
-    for _ in range(a.warmup):
-        step(False)
+    run_all(a.warmup, False)
     # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
     # of every launch, accumulated on the device and read once after the timed region; HIP-event packets around
-    # each of the ~100 launches per search would cost ~20 us apiece)
+    # each of the ~100 launches per search would cost ~20 us apiece) -- slot 0's searches
     lr.profile(not a.no_kernel_timing)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(True)
+    run_all(a.steps, True)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -262,18 +301,20 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])] for es in ev],
-                       axis=0)
+    stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])]
+                        for es in slots[0].ev], axis=0)
+    frame_ms = float(np.mean([es[0].elapsed_time(es[5]) for es in slots[0].ev]))
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
-    value = W * H / (ms_per_step * 1e-3) / 1e6  # one frame per step for the whole job
+    value = F * W * H / (ms_per_step * 1e-3) / 1e6  # F frames per step for the whole job
     lr_cls = {c: {k: lr_tot[c][k] / max(lr_tot["searches"], 1) if lr_tot else 0.0 for k in ("launches", "ms", "bytes")}
               for c in svtgpu.LrState.PROFILE_CLASSES}
     # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
     # recon + source read once (2*S*B) + per-FB outputs (mse 2x64 u64, dir 64 u8, var 64 i32, skip)
     S_samples = 1.5 * W * H
     B = 2 if bd > 8 else 1
+    st = slots[0].st
     nfb_band = st.nfb if n == 1 else (int(rows[rank + 1]) - int(rows[rank])) * nhfb
     alg_bytes = 2 * S_samples * B / n + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
     achieved = alg_bytes / (search_ms * 1e-3) / 1e9
@@ -315,7 +356,8 @@ def main():
                                "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
                                "LR search+apply (RU 256/128, wn/sg level 1)"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
-                   "width": W, "height": H, "bit_depth": bd, "frames_per_step": 1,
+                   "width": W, "height": H, "bit_depth": bd, "frames_per_step": F,
+                   "frames_in_flight": F, "frame_latency_ms": round(frame_ms, 4),
                    "parallelism": "row_bands%d (CDEF FB rows, LR unit rows, MD SBs; DLF replicated)" % n if n > 1 else "single",
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
                                 "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_search_apply": round(lr_ms, 4),
@@ -323,12 +365,13 @@ def main():
                                 "note": "the MD batch runs on a second stream concurrently with the LR stage; the LR "
                                         "search runs its Wiener and self-guided chains on two streams"},
                    "lr_search_kernel_ms": {c: round(v["ms"], 4) for c, v in lr_cls.items()},
-                   "dlf_levels": list(lf_levels[-1]) if lf_levels else None},
+                   "dlf_levels": list(slots[0].lf_levels[-1]) if slots[0].lf_levels else None},
         "roofline": roof,
     }
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(src, rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample, lr_ctrls,
-                                           lr_us, md_ref_y, md_mvs)
+        s0 = slots[0]
+        out["cpu_baseline"] = cpu_baseline(s0.src, s0.rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample,
+                                           lr_ctrls, lr_us, md_ref_y, s0.md_mvs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if n > 1:

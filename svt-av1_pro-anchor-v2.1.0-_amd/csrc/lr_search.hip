@@ -166,7 +166,11 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
 // symmetric, and which also accumulate M) LD lanes each in the last wave(s); lanes stride over pixel pairs.
 // ---------------------------------------------------------------------------------------------
 constexpr int ST_W = 70, ST_SLOTS = 56;
-constexpr int SG_NC = 7; // candidates per self-guided descent pass (a depth-3 outcome tree)
+#ifndef SVTGPU_SG_NC
+#define SVTGPU_SG_NC 7
+#endif
+constexpr int SG_NC = SVTGPU_SG_NC; // candidates per self-guided descent pass (7: a depth-3 outcome tree)
+static_assert(SG_NC == 3 || SG_NC == 7 || SG_NC == 15, "a complete outcome tree of at most 32 nodes");
 template <int WIN>
 struct StatsCfg {
     static constexpr int HALF = WIN / 2, NPAIR = WIN * (WIN + 1) / 2, NOFF = WIN * (WIN - 1) / 2;
@@ -1109,11 +1113,15 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 // outcomes against the measured errors (report() decides exactly as the reference does) and stops at the first
 // candidate that was not evaluated, which becomes the next root.  While many descents are live the rounds are
 // VALU-bound and a deeper tree amortizes the per-pixel work over more candidates: the tree is always depth 3
-// (SG_SPEC_LIVE >= 0 would keep single-node trees while more than that many descents are live).
-constexpr int SG_SPEC_LIVE = -1;
+// The tree size follows the live count entering the round: 1 node while more than spec_live[0] descents are live,
+// 3 nodes while more than spec_live[1], else 7 (SgSpec; negative thresholds disable a level).
+struct SgSpec {
+    int32_t live1, live3;
+};
 // returns 1 when the descent stays live; *list_unit = its unit when this descent lists the unit's tiles
 __device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
-                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit) {
+                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit,
+                               const SgSpec spec) {
     Descent d = ds[i];
     if (d.done) return 0;
     unsigned long long *e = err + (size_t)i * SG_NC;
@@ -1132,7 +1140,10 @@ __device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int3
     }
     for (int c = 0; c < SG_NC; c++) e[c] = 0;
     if (!d.done) {
-        const int depth_nodes = (SG_SPEC_LIVE >= 0 && (first || cnt_cur[1] > SG_SPEC_LIVE)) ? 1 : SG_NC; // nodes
+        const int live_in     = first ? 1 << 30 : cnt_cur[1];
+        const int depth_nodes = (spec.live1 >= 0 && live_in > spec.live1)   ? 1
+                                : (spec.live3 >= 0 && live_in > spec.live3) ? 3
+                                                                            : SG_NC; // nodes
         Descent   tree[SG_NC / 2];
         uint32_t  mask = 1;
         int32_t  *cd   = cand + (size_t)i * SG_NC * 2;
@@ -1164,11 +1175,12 @@ __device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int3
 __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
                                                           unsigned long long *err, int32_t *cand, uint32_t *candm,
                                                           int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
-                                                          int32_t *cnt, int first, int stamp, unsigned long long *tk) {
+                                                          int32_t *cnt, int first, int stamp, const SgSpec spec,
+                                                          unsigned long long *tk) {
     PROF_BEGIN(tk);
     const int i    = blockIdx.x * blockDim.x + threadIdx.x;
     int       lu   = -1;
-    const int live = i < n ? sgr_advance_one(ds, i, err, cand, candm, ustamp, cnt_cur, first, stamp, &lu) : 0;
+    const int live = i < n ? sgr_advance_one(ds, i, err, cand, candm, ustamp, cnt_cur, first, stamp, &lu, spec) : 0;
     wave_count(&cnt[1], live);
     const int t0 = lu >= 0 ? tile0[lu] : 0, nt = lu >= 0 ? tile0[lu + 1] - t0 : 0, pos = wave_alloc(&cnt[0], nt);
     for (int j = 0; j < nt; j++) items[pos + j] = t0 + j;
@@ -1500,7 +1512,17 @@ void launch_stats(int win, Fn &&f) {
 }
 
 constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
+constexpr int SG_SPEC_LIVE1 = -1, SG_SPEC_LIVE3 = -1; // always 7-node self-guided trees
 constexpr int WN_TRIAL_GRID = 768; // persistent Wiener trial workgroups (3 per CU); SVTGPU_WN_GRID overrides (sweeps)
+SgSpec sg_spec() { // self-guided tree sizes by live count; SVTGPU_SG_SPEC="live1,live3" overrides (sweeps)
+    static const SgSpec v = [] {
+        SgSpec      r{SG_SPEC_LIVE1, SG_SPEC_LIVE3};
+        const char *e = std::getenv("SVTGPU_SG_SPEC");
+        if (e) std::sscanf(e, "%d,%d", &r.live1, &r.live3);
+        return r;
+    }();
+    return v;
+}
 int wn_trial_grid() {
     static const int g = [] {
         const char *e = std::getenv("SVTGPU_WN_GRID");
@@ -1740,7 +1762,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
                            npairs, d_t0, (unsigned long long *)dp(o_serr), (int32_t *)dp(o_cand),
                            (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp), (int32_t *)dp(o_sitems),
-                           (const int32_t *)cnt + 6, cnt + 2, 1, 1, (unsigned long long *)nullptr);
+                           (const int32_t *)cnt + 6, cnt + 2, 1, 1, sg_spec(), (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
     // Each chain runs in batches of ROUNDS_PER_BATCH rounds with the next batch already queued behind the one the
@@ -1784,7 +1806,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                     hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
                                        (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
                                        (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
-                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, C.g + 2, tk);
+                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, C.g + 2, sg_spec(), tk);
                 });
             }
         }
