@@ -285,6 +285,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     for (hipEvent_t e : s->ev_batch)
         if (e) (void)hipEventDestroy(e);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
+    if (s->h_flag) (void)hipHostFree(s->h_flag);
     lr_profiler_destroy(s->prof);
     delete s;
 }

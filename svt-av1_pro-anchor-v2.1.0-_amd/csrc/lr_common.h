@@ -24,7 +24,11 @@ struct SvtGpuLrState {
     hipEvent_t           pin_free; // the last copy out of h_pin has run: the host may rewrite it
     hipStream_t          wst;      // the search's Wiener chain (the caller's stream carries the self-guided one)
     hipEvent_t           ev_fork, ev_join;
-    hipEvent_t           ev_batch[4]; // [chain][slot]: a batch of descent rounds and its live-count read-back
+    hipEvent_t           ev_batch[4]; // unused (the batches publish through h_flag)
+    // [chain][slot] {sequence, live count} written by the device at the end of a batch of descent rounds (mapped
+    // pinned memory: the host polls it without runtime calls)
+    unsigned long long  *h_flag, *h_flag_dev;
+    unsigned long long   flag_seq;
 };
 void lr_profiler_destroy(void *prof);
 

@@ -160,28 +160,39 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
     PROF_END(tk);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Wiener statistics.  Output per tile: [pair (c1 <= c2)][r1 * 7 + r2] H blocks, then [c * 7 + r] M.
-// Off-diagonal column pairs get LO lanes each in the first waves, the WIN diagonal pairs (whose blocks are
-// symmetric, and which also accumulate M) LD lanes each in the last wave(s); lanes stride over pixel pairs.
-// ---------------------------------------------------------------------------------------------
-constexpr int ST_W = 70, ST_SLOTS = 56;
 #ifndef SVTGPU_SG_NC
 #define SVTGPU_SG_NC 7
 #endif
 constexpr int SG_NC = SVTGPU_SG_NC; // candidates per self-guided descent pass (7: a depth-3 outcome tree)
 static_assert(SG_NC == 3 || SG_NC == 7 || SG_NC == 15, "a complete outcome tree of at most 32 nodes");
+
+// ---------------------------------------------------------------------------------------------
+// Wiener statistics on the matrix cores.  Output per tile (unchanged layout): [pair (c1 <= c2)][r1 * 7 + r2] H
+// blocks, then [c * 7 + r] M -- raw sums of svt_av1_compute_stats (EbRestorationPick.c:671/708) before the
+// bit-depth division.
+//
+// Per pixel p the feature vector F_p holds the WIN x WIN window Y[r][c] = D[i + o + r][j + o + c] (D = dgd - avg
+// with a 3-pixel edge-clamped apron) and X = src - avg; the tile's Gram matrix G = sum_p F_p F_p^T contains every
+// H entry and M.  Exact integers on v_mfma_i32_16x16x64_i8: each value v in [-1023, 1023] splits into
+// v = 32 * hi + lo with hi = v >> 5 in [-32, 31] and lo = v & 31, so G = 1024 HH + 32 (HL + LH) + LL with three i32
+// accumulators per 16 x 16 feature block (|partials| <= 4096 px * 1024 < 2^31).  K = the 64 pixels of one tile row
+// per MFMA; the 4 waves take rows i = w (mod 4); only the upper feature blocks (mb <= nb) are computed.
+// Operands come straight from two byte planes (hi, lo) of D in LDS: lane l of feature block fb holds feature
+// 16 fb + (l & 15) for pixels 16 (l >> 4) .. +15 of the row (the probed gfx950 layout A[m = l & 15][k = 16 (l >> 4)
+// + j], B[k][n = l & 15], D[4 (l >> 4) + r][l & 15]); the window's column offset is an unaligned byte start, read
+// as 5 dwords and realigned with v_alignbyte.  Per wave the three accumulators fold into one i32 (|G_wave| <=
+// 1024 px * 1023^2 < 2^31), the four wave partials meet in LDS in i64 and scatter into the output layout.
+// ---------------------------------------------------------------------------------------------
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+constexpr int SM_RS = 72;                  // LDS row stride of the byte planes (70 used + realign slack)
+constexpr int SM_DROWS = 70, SM_XROWS = 64; // D rows (tile + 2 x 3 apron), X rows
+constexpr int SM_PLANE = (SM_DROWS + SM_XROWS) * SM_RS + 16; // one byte plane: D rows, then X rows, + read slack
+
 template <int WIN>
 struct StatsCfg {
-    static constexpr int HALF = WIN / 2, NPAIR = WIN * (WIN + 1) / 2, NOFF = WIN * (WIN - 1) / 2;
-    static constexpr int OFF_THR = WIN == 3 ? 128 : 192, LO = OFF_THR / NOFF, LD = (256 - OFF_THR) / WIN;
+    static constexpr int HALF = WIN / 2, NPAIR = WIN * (WIN + 1) / 2, NF = WIN * WIN + 1;
+    static constexpr int NFB = (NF + 15) / 16, NB = NFB * (NFB + 1) / 2, NVAL = (NPAIR + 1) * 49;
 };
-
-__device__ inline void off_pair(int win, int q, int *c1, int *c2) { // q-th (c1 < c2) pair
-    int a = 0;
-    while (q >= win - 1 - a) q -= win - 1 - a, a++;
-    *c1 = a, *c2 = a + 1 + q;
-}
 
 template <typename T, int WIN>
 __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, int tile_begin,
@@ -189,9 +200,10 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
                                                            unsigned long long *tk) {
     PROF_BEGIN(tk);
     using C = StatsCfg<WIN>;
-    constexpr int NVAL = (C::NPAIR + 1) * 49;
-    __shared__ int lds[256 * ST_SLOTS]; // staging (D pairs, S pairs), then the lane partials
-    uint32_t      *D2 = (uint32_t *)lds, *S2 = D2 + ST_W * ST_W;
+    constexpr int NFB = C::NFB, NB = C::NB, NVAL = C::NVAL;
+    // byte planes (hi, lo) during the products; afterwards the wave partials [4][NB][4][64] i32 and the output
+    constexpr int LDS_STAGE = 2 * SM_PLANE, LDS_RED = 4 * NB * 256 * 4 + NVAL * 8;
+    __shared__ __align__(16) uint8_t lds[LDS_STAGE > LDS_RED ? LDS_STAGE : LDS_RED];
     const int        tl = xcd_swizzle(blockIdx.x, gridDim.x);
     const Tile       t = A.tiles[tile_begin + tl];
     const PlaneArgs &P = A.pl[t.plane];
@@ -199,90 +211,134 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
     const long long  area = (long long)(u.h_end - u.h_start) * (u.v_end - u.v_start);
     const int        avg  = (int)(sum[t.unit] / (unsigned long long)area);
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    const int        sw = t.w + 6, hw2 = (t.w + 1) >> 1;
-    // D2[r][c] = (D[r][c], D[r][c + 1]) as int16 pairs, D = dgd - avg over the tile plus a 3-pixel apron
-    for (int i = threadIdx.x; i < (t.h + 6) * sw; i += 256) {
-        const int r = i / sw, c = i % sw, y = t.y0 + r - 3, x = t.x0 + c - 3;
-        const int lo = px(d, P.dstride, P.W, P.H, y, x) - avg, hi = px(d, P.dstride, P.W, P.H, y, x + 1) - avg;
-        D2[r * ST_W + c] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16);
-    }
-    for (int i = threadIdx.x; i < t.h * hw2; i += 256) {
-        const int r = i / hw2, j = 2 * (i % hw2);
-        const T  *sp = s + (size_t)(t.y0 + r) * P.sstride + t.x0 + j;
-        const int lo = (int)sp[0] - avg, hi = j + 1 < t.w ? (int)sp[1] - avg : 0;
-        S2[r * 32 + (j >> 1)] = (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16);
-    }
-    __syncthreads();
-    const int tid = threadIdx.x, o = 3 - C::HALF, items = t.h * hw2;
-    int       acc[ST_SLOTS];
+    const int        tid = threadIdx.x, o = 3 - C::HALF;
+    // ---- stage: D rows 0 .. h+5 (columns 0 .. w+5, edge-clamped), then X rows 0 .. h-1, as hi / lo bytes ----
+    {
+        uint32_t *hi = (uint32_t *)lds, *lo = (uint32_t *)(lds + SM_PLANE);
+        const int ng = (t.w + 6 + 3) >> 2, nd = (t.h + 6) * ng, nx = t.h * (t.w >> 2);
+        for (int it = tid; it < nd + nx; it += 256) {
+            int v[4], row;
+            if (it < nd) {
+                row          = it / ng;
+                const int g4 = it - row * ng, y = t.y0 + row - 3, x = t.x0 + 4 * g4 - 3;
 #pragma unroll
-    for (int k = 0; k < ST_SLOTS; k++) acc[k] = 0;
-    if (tid < C::OFF_THR) {
-        const int q = tid / C::LO;
-        if (q < C::NOFF) {
-            int c1, c2;
-            off_pair(WIN, q, &c1, &c2);
-            for (int it = tid % C::LO; it < items; it += C::LO) {
-                const int       i = it / hw2, j = 2 * (it - i * hw2);
-                const uint32_t  m = j + 1 < t.w ? 0xFFFFFFFFu : 0xFFFFu; // odd-width tail: drop the phantom pixel
-                const uint32_t *b = D2 + (i + o) * ST_W + j + o;
-                uint32_t        y1[WIN], y2[WIN];
+                for (int k = 0; k < 4; k++) v[k] = px(d, P.dstride, P.W, P.H, y, x + k) - avg;
+                row = row * (SM_RS / 4) + g4;
+            } else {
+                const int q = it - nd, r = q / (t.w >> 2), g4 = q - r * (t.w >> 2);
+                int       sv[4];
+                load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g4, sv);
 #pragma unroll
-                for (int r = 0; r < WIN; r++) y1[r] = b[r * ST_W + c1] & m, y2[r] = b[r * ST_W + c2];
-#pragma unroll
-                for (int r1 = 0; r1 < WIN; r1++)
-#pragma unroll
-                    for (int r2 = 0; r2 < WIN; r2++) acc[r1 * 7 + r2] = dot2(y1[r1], y2[r2], acc[r1 * 7 + r2]);
+                for (int k = 0; k < 4; k++) v[k] = sv[k] - avg;
+                row = (SM_DROWS + r) * (SM_RS / 4) + g4;
             }
-        }
-    } else {
-        const int c = (tid - C::OFF_THR) / C::LD;
-        if (c < WIN) {
-            for (int it = (tid - C::OFF_THR) % C::LD; it < items; it += C::LD) {
-                const int       i = it / hw2, j = 2 * (it - i * hw2);
-                const uint32_t  m = j + 1 < t.w ? 0xFFFFFFFFu : 0xFFFFu;
-                const uint32_t *b = D2 + (i + o) * ST_W + j + o;
-                const uint32_t  x = S2[i * 32 + (j >> 1)];
-                uint32_t        y[WIN];
+            uint32_t h4 = 0, l4 = 0;
 #pragma unroll
-                for (int r = 0; r < WIN; r++) y[r] = b[r * ST_W + c] & m;
-#pragma unroll
-                for (int r1 = 0; r1 < WIN; r1++) {
-#pragma unroll
-                    for (int r2 = r1; r2 < WIN; r2++) acc[r1 * 7 + r2] = dot2(y[r1], y[r2], acc[r1 * 7 + r2]);
-                    acc[49 + r1] = dot2(y[r1], x, acc[49 + r1]);
-                }
-            }
+            for (int k = 0; k < 4; k++) h4 |= (uint32_t)(v[k] >> 5 & 0xFF) << (8 * k), l4 |= (uint32_t)(v[k] & 31) << (8 * k);
+            hi[row] = h4, lo[row] = l4;
         }
     }
     __syncthreads();
+    // ---- products ----
+    const int w = tid >> 6, l = tid & 63, g = l >> 4;
+    int       fdw[NFB], fsh[NFB]; // dword address (row 0) and byte shift of this lane's feature per block
+    uint32_t  fmask[NFB];         // 0: padding feature
 #pragma unroll
-    for (int k = 0; k < ST_SLOTS; k++) lds[k * 256 + tid] = acc[k];
-    __syncthreads();
-    long long *out = part + (size_t)tl * NVAL;
-    for (int oi = tid; oi < NVAL; oi += 256) {
-        const int pair = oi / 49, k = oi % 49, r1 = k / 7, r2 = k % 7;
-        int       lane0 = 0, nl = 0, slot = 0;
-        if (r1 < WIN && r2 < WIN) {
-            if (pair < C::NPAIR) {
-                int c1 = 0, rem = pair; // pair -> (c1, c2), c1 <= c2
-                while (rem >= WIN - c1) rem -= WIN - c1, c1++;
-                const int c2 = c1 + rem;
-                if (c1 == c2) {
-                    lane0 = C::OFF_THR + c1 * C::LD, nl = C::LD, slot = min(r1, r2) * 7 + max(r1, r2);
-                } else {
-                    const int q = c1 * (2 * WIN - c1 - 1) / 2 + (c2 - c1 - 1);
-                    lane0 = q * C::LO, nl = C::LO, slot = k;
-                }
-            } else { // M: k = c * 7 + r
-                lane0 = C::OFF_THR + r1 * C::LD, nl = C::LD, slot = 49 + r2;
+    for (int fb = 0; fb < NFB; fb++) {
+        const int f = 16 * fb + (l & 15);
+        int       byte = 0;
+        fmask[fb]      = 0xFFFFFFFFu;
+        if (f < WIN * WIN) {
+            const int r = f / WIN, c = f - r * WIN;
+            byte        = (o + r) * SM_RS + 16 * g + c + o;
+        } else if (f == WIN * WIN) {
+            byte = SM_DROWS * SM_RS + 16 * g;
+        } else {
+            fmask[fb] = 0;
+        }
+        fdw[fb] = byte >> 2, fsh[fb] = byte & 3;
+    }
+    uint32_t cmask[4]; // pixel columns 16 g + 4 q .. +3 inside the tile
+#pragma unroll
+    for (int q = 0; q < 4; q++) cmask[q] = 16 * g + 4 * q < t.w ? 0xFFFFFFFFu : 0u;
+    v4i32 hh[NB], ll[NB], hl[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) hh[b] = ll[b] = hl[b] = v4i32{0, 0, 0, 0};
+    const uint32_t *H32 = (const uint32_t *)lds, *L32 = (const uint32_t *)(lds + SM_PLANE);
+    for (int i = w; i < t.h; i += 4) {
+        v4i32 fh[NFB], fl[NFB];
+#pragma unroll
+        for (int fb = 0; fb < NFB; fb++) {
+            const int rowdw = fdw[fb] + i * (SM_RS / 4), shb = fsh[fb] * 8;
+            uint32_t  a[5], b5[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) a[k] = H32[rowdw + k], b5[k] = L32[rowdw + k];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t m = cmask[q] & fmask[fb];
+                fh[fb][q] = (int)(__builtin_amdgcn_alignbyte(a[q + 1], a[q], shb >> 3) & m);
+                fl[fb][q] = (int)(__builtin_amdgcn_alignbyte(b5[q + 1], b5[q], shb >> 3) & m);
             }
         }
-        long long v = 0;
-        for (int l = 0; l < nl; l++) v += lds[slot * 256 + lane0 + l];
-        out[oi] = v;
+        int b = 0;
+#pragma unroll
+        for (int mb = 0; mb < NFB; mb++)
+#pragma unroll
+            for (int nb = mb; nb < NFB; nb++, b++) {
+                hh[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fh[mb], fh[nb], hh[b], 0, 0, 0);
+                ll[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fl[mb], fl[nb], ll[b], 0, 0, 0);
+                hl[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fh[mb], fl[nb], hl[b], 0, 0, 0);
+                hl[b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fl[mb], fh[nb], hl[b], 0, 0, 0);
+            }
     }
+    __syncthreads(); // the byte planes are no longer read
+    // ---- wave partials -> LDS [w][b][r][lane] ----
+    int *red = (int *)lds;
+#pragma unroll
+    for (int b = 0; b < NB; b++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) red[((w * NB + b) * 4 + r) * 64 + l] = 1024 * hh[b][r] + 32 * hl[b][r] + ll[b][r];
+    long long *out = (long long *)(lds + 4 * NB * 256 * 4);
+    for (int k = tid; k < NVAL; k += 256) out[k] = 0;
+    __syncthreads();
+    // ---- totals and scatter into the output layout (each unordered feature pair once) ----
+    constexpr int NW = WIN * WIN;
+    for (int e = tid; e < NB * 256; e += 256) {
+        const int b = e >> 8, r = (e >> 6) & 3, ln = e & 63;
+        int       mb = 0, bb = b;
+        while (bb >= NFB - mb) bb -= NFB - mb, mb++;
+        const int nb = mb + bb;
+        const int fm = 16 * mb + 4 * (ln >> 4) + r, fn = 16 * nb + (ln & 15);
+        if (mb == nb && fm > fn) continue;
+        const long long v = (long long)red[((0 * NB + b) * 4 + r) * 64 + ln] + red[((1 * NB + b) * 4 + r) * 64 + ln] +
+                            red[((2 * NB + b) * 4 + r) * 64 + ln] + red[((3 * NB + b) * 4 + r) * 64 + ln];
+        if (fm < NW && fn < NW) {
+            int r1 = fm / WIN, c1 = fm - r1 * WIN, r2 = fn / WIN, c2 = fn - r2 * WIN;
+            if (c1 > c2) {
+                const int tr = r1, tc = c1;
+                r1 = r2, c1 = c2, r2 = tr, c2 = tc;
+            }
+            const int pair = c1 * WIN - c1 * (c1 - 1) / 2 + (c2 - c1);
+            out[pair * 49 + r1 * 7 + r2] = v;
+            if (c1 == c2) out[pair * 49 + r2 * 7 + r1] = v;
+        } else if (fm < NW && fn == NW) {
+            const int r1 = fm / WIN, c1 = fm - r1 * WIN;
+            out[C::NPAIR * 49 + c1 * 7 + r1] = v;
+        }
+    }
+    __syncthreads();
+    long long *dst = part + (size_t)tl * NVAL;
+    for (int k = tid; k < NVAL; k += 256) dst[k] = out[k];
     PROF_END(tk);
+}
+
+// end of a batch of descent rounds: the chain's live count and the batch's sequence number to mapped host memory
+// (count first, then a system-scope fence, then the sequence word the host polls)
+__global__ void lr_publish_kernel(const int32_t *cnt, unsigned long long *flag, unsigned long long seq) {
+    if (threadIdx.x != 0) return;
+    flag[1] = (unsigned long long)(uint32_t)cnt[1];
+    __threadfence_system();
+    __hip_atomic_store(&flag[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // per unit: sum the tile partials (tiles of a unit are contiguous in the tile list)
@@ -290,7 +346,7 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
                                     long long *out, unsigned long long *tk) {
     PROF_BEGIN(tk);
     const int u = blockIdx.x, t0 = unit_tile0[u] - tile_begin, t1 = unit_tile0[u + 1] - tile_begin;
-    for (int k = threadIdx.x; k < nvals; k += blockDim.x) {
+    for (int k = blockIdx.y * blockDim.x + threadIdx.x; k < nvals; k += gridDim.y * blockDim.x) {
         long long s = 0;
         for (int t = t0; t < t1; t++) s += part[(size_t)t * nvals + k];
         out[(size_t)u * nvals + k] = s;
@@ -1699,7 +1755,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // projection rounds) are independent until the RD finish: the Wiener chain runs on a second stream, so its
     // latency-bound rounds fill the gaps of the self-guided work and the other way round.
     if (!s->wst) {
-        HIP_TRY(hipStreamCreateWithFlags(&s->wst, hipStreamNonBlocking));
+        // the Wiener chain (statistics, solve, ~48 trial rounds) is the search's critical path: its stream gets the
+        // highest priority so its workgroups are dispatched first while the self-guided filters fill the CUs
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&s->wst, hipStreamNonBlocking, greatest));
         HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
     }
@@ -1717,7 +1777,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             });
         });
         run(0, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n), dim3(256), 0, sw, (const long long *)part,
+            hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n, (q.nval + 255) / 256), dim3(256), 0, sw, (const long long *)part,
                                (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh, tk);
         });
         HIP_TRY(hipGetLastError());
@@ -1776,11 +1836,22 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     } ch[2];
     ch[0].live = n_wn > 0, ch[0].stream = sw;
     ch[1].live = npairs > 0, ch[1].stream = st;
-    int32_t *hcnt = (int32_t *)hp(h_cnt); // [chain][slot][2]
-    for (int k = 0; k < 4; k++)
-        if (!s->ev_batch[k]) HIP_TRY(hipEventCreateWithFlags(&s->ev_batch[k], hipEventDisableTiming));
+    if (!s->h_flag) {
+        HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void **)&s->h_flag_dev, s->h_flag, 0));
+        std::memset(s->h_flag, 0, 8 * 2 * 4);
+    }
+    unsigned long long want[4] = {0, 0, 0, 0}; // [chain][slot] sequence number of the batch in flight there
+    static const bool trace = std::getenv("SVTGPU_LR_TRACE") != nullptr; // host-side batch log (debugging)
+    const auto        t_tr0 = clk();
+    auto              tr    = [&](const char *what, int c, int g) {
+        if (trace)
+            std::fprintf(stderr, "lrtrace %9.1f us %s chain %d round %d\n",
+                         std::chrono::duration<double, std::micro>(clk() - t_tr0).count(), what, c, g);
+    };
     auto enqueue_batch = [&](int c) -> int {
         Chain &C = ch[c];
+        tr("enqueue", c, C.g);
         for (int b = 0; b < ROUNDS_PER_BATCH; b++, C.g++) {
             int32_t *cur = cnt + 4 * (C.g & 1), *nxt = cnt + 4 * ((C.g + 1) & 1);
             if (c == 0) {
@@ -1811,27 +1882,45 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             }
         }
         HIP_TRY(hipGetLastError());
-        const int k = (C.head + C.inflight) & 1; // the batch's live count, read after its last advance
-        HIP_TRY(hipMemcpyAsync(hcnt + (c * 2 + k) * 2, cnt + 4 * (C.g & 1) + 2 * c, 8, hipMemcpyDeviceToHost, C.stream));
-        HIP_TRY(hipEventRecord(s->ev_batch[c * 2 + k], C.stream));
+        const int k = (C.head + C.inflight) & 1; // the batch's live count, published after its last advance
+        want[c * 2 + k] = ++s->flag_seq;
+        hipLaunchKernelGGL(lr_publish_kernel, dim3(1), dim3(64), 0, C.stream, (const int32_t *)cnt + 4 * (C.g & 1) + 2 * c,
+                           s->h_flag_dev + (c * 2 + k) * 2, want[c * 2 + k]);
+        HIP_TRY(hipGetLastError());
         C.inflight++;
+        tr("enqueued", c, C.g);
         return SVTGPU_OK;
     };
     while (ch[0].live || ch[1].live) {
         for (int c = 0; c < 2; c++)
             while (ch[c].live && ch[c].inflight < 2)
                 if (int rc = enqueue_batch(c)) return rc;
-        bool consumed = false; // spin until the oldest batch of a live chain has landed
-        while (!consumed) {
+        bool       consumed = false; // spin until the oldest batch of a live chain has published its count
+        const auto t_spin   = clk();
+        for (unsigned it = 0; !consumed; it++) {
             for (int c = 0; c < 2 && !consumed; c++) {
                 Chain &C = ch[c];
                 if (!C.live || !C.inflight) continue;
-                const hipError_t q = hipEventQuery(s->ev_batch[c * 2 + C.head]);
-                if (q == hipErrorNotReady) continue;
-                HIP_TRY(q);
-                C.live = hcnt[(c * 2 + C.head) * 2 + 1] > 0;
+                const unsigned long long *f = s->h_flag + (c * 2 + C.head) * 2;
+                if (__atomic_load_n(f, __ATOMIC_ACQUIRE) != want[c * 2 + C.head]) continue;
+                C.live = __atomic_load_n(f + 1, __ATOMIC_RELAXED) > 0;
                 C.head ^= 1, C.inflight--, consumed = true;
+                tr(C.live ? "landed-live" : "landed-done", c, C.g);
                 if (C.g > MAX_ROUNDS) return SVTGPU_ERR_INVALID_ARG; // a descent always terminates; guard anyway
+            }
+            // a stalled word (a failed launch): after 200 ms of spinning let the runtime report the stream error
+            if (!consumed && (it & 4095) == 4095 && clk() - t_spin > std::chrono::milliseconds(200)) {
+                HIP_TRY(hipStreamSynchronize(sw));
+                HIP_TRY(hipStreamSynchronize(st));
+                bool any = false;
+                for (int c = 0; c < 2; c++)
+                    any |= ch[c].live && ch[c].inflight &&
+                           __atomic_load_n(s->h_flag + (c * 2 + ch[c].head) * 2, __ATOMIC_ACQUIRE) == want[c * 2 + ch[c].head];
+                if (!any) {
+                    svtgpu_set_last_hip_error(hipErrorUnknown, "LR descent batch word missing after synchronize",
+                                              __FILE__, __LINE__);
+                    return SVTGPU_ERR_HIP;
+                }
             }
         }
     }
