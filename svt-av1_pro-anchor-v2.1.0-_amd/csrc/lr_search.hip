@@ -530,8 +530,8 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
 
 // ---------------------------------------------------------------------------------------------
 // self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
-// registers; per ep the A/B maps (packed B << 9 | A) go to LDS, the filters to HBM, and the projection moments
-// mom[pair] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} (u = x<<4, s = (src<<4) - u, g = flt - u) to int64 atomics.
+// registers; per ep the A/B maps (packed B << 9 | A) go to LDS and the filters to HBM (the projection moments are
+// a separate pass over them, sgr_mom_kernel).
 // ---------------------------------------------------------------------------------------------
 constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
 
@@ -549,12 +549,8 @@ __device__ inline void sgr_ab_fast(int sum, int sq, int n, int s, int bd, const 
 }
 
 template <typename T>
-__global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long long *mom, unsigned long long *tk) {
+__global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    // the lane's moment partials stay 32-bit over groups of 4 pixels: f <= 32767 (the filter's weighted A/B
-    // sums are bounded by 32 * 256 * 1023 + 32 * 261111 < 2^24 before the >> 9), so |g| = |f - (x<<4)| <= 32767,
-    // g^2 * 4 < 2^32 (unsigned) and |g * s| * 4 < 2^31 with |s| = |(src - x) << 4| <= 16368
-    static_assert(SG_NP % 4 == 0, "moment partials are flushed every 4 pixels");
     __shared__ uint16_t v[SG_V * SG_V];
     // packed B << 9 | A (A <= 256, B < 2^19) of the r = 1 and r = 2 passes, double-buffered over eps: the maps of
     // ep e + 1 are built while ep e is filtered, one barrier per ep
@@ -562,7 +558,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
     __shared__ int      xby[256];
     const Tile       t = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
     const PlaneArgs &P = A.pl[t.plane];
-    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    const T         *d = (const T *)P.dgd;
     for (int i = threadIdx.x; i < (t.h + 6) * (t.w + 6); i += SG_NT) {
         const int r = i / (t.w + 6), c = i % (t.w + 6);
         v[r * SG_V + c] = (uint16_t)px(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 + c - 3);
@@ -588,16 +584,11 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
                 }
         }
     }
-    int pix[SG_NP], sv[SG_NP]; // this lane's pixels: threadIdx.x + k * SG_NT
+    int pix[SG_NP]; // this lane's pixels: threadIdx.x + k * SG_NT
 #pragma unroll
     for (int k = 0; k < SG_NP; k++) {
         const int i = threadIdx.x + k * SG_NT;
-        pix[k] = sv[k] = 0;
-        if (i < npx) {
-            const int y = i / t.w, x = i % t.w;
-            pix[k]      = v0[y * SG_V + x];
-            sv[k]       = ((int)s[(size_t)(t.y0 + y) * P.sstride + t.x0 + x] << 4) - (pix[k] << 4);
-        }
+        pix[k]      = i < npx ? v0[(i / t.w) * SG_V + i % t.w] : 0;
     }
     const size_t pn = (size_t)P.fstride * P.H;
     auto build_ab = [&](int e) { // A/B maps of ep index e into buffer e & 1
@@ -630,16 +621,12 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
         const int  ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
         const int *ab1e = ab1[e & 1], *ab2e = ab2[e & 1];
         int16_t  *f0g = P.flt + (size_t)e * 2 * pn, *f1g = f0g + pn;
-        uint32_t  m0 = 0, m1 = 0;   // sum g1^2, g2^2 over the current 4 pixels
-        int       m3 = 0, m4 = 0;   // sum g1*s, g2*s over the current 4 pixels
-        long long m2 = 0, M[4] = {0, 0, 0, 0}; // sum g1*g2; flushed 64-bit totals of m0, m1, m3, m4
 #pragma unroll
         for (int k = 0; k < SG_NP; k++) {
             const int i = threadIdx.x + k * SG_NT;
             if (i >= npx) break;
-            const int    y = i / t.w, x = i % t.w, c = (y + 1) * bw + x + 1, u = pix[k] << 4;
+            const int    y = i / t.w, x = i % t.w, c = (y + 1) * bw + x + 1;
             const size_t o = (size_t)(t.y0 + y) * P.fstride + t.x0 + x;
-            int          g1 = 0, g2 = 0;
             if (r0) {
                 const int *Q = ab2e + c;
                 int        aa, bb, sh;
@@ -657,10 +644,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
                     sh = 8;
                 }
                 const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << (sh - 1))) >> sh;
-#if SGR_EXP != 1
                 f0g[o]      = (int16_t)f;
-#endif
-                g1          = f - u;
             }
             if (r1) {
                 const int *Q  = ab1e + c;
@@ -669,38 +653,77 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, long
                 const int  a3 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
                 const int  aa = a4 * 4 + a3 * 3, bb = ((c4 - a4) >> 9) * 4 + ((c3 - a3) >> 9) * 3;
                 const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9;
-#if SGR_EXP != 1
                 f1g[o]      = (int16_t)f;
-#endif
-                g2          = f - u;
-            }
-            m0 += (uint32_t)__mul24(g1, g1);
-            m1 += (uint32_t)__mul24(g2, g2);
-            m2 += (long long)__mul24(g1, g2);
-            m3 += __mul24(g1, sv[k]);
-            m4 += __mul24(g2, sv[k]);
-            if (SG_NP > 4 && (k & 3) == 3) {
-                M[0] += m0, M[1] += m1, M[2] += m3, M[3] += m4;
-                m0 = m1 = 0, m3 = m4 = 0;
             }
         }
-        M[0] += m0, M[1] += m1, M[2] += m3, M[3] += m4;
-        const int       pair  = P.pair_base + (t.unit - P.unit_base) * P.ne + e;
+        __syncthreads(); // ep e + 2 rewrites this ep's buffer; ep e + 1's maps are complete
+    }
+    PROF_END(tk);
+}
+
+// projection moments mom[pair] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} (u = x<<4, s = (src<<4) - u, g = flt - u) of every
+// (unit, ep) from the stored filters: the tile's CDEF and source pixels are read once, 16 pixels per lane (4-pixel
+// chunks), and every ep's two filter planes stream past them -- a memory-bound pass that keeps the moment arithmetic
+// and its wave reductions out of the VALU-bound filter kernel (one reduction per ep per 1024 pixels instead of 256).
+// Lane partials stay 32-bit over a chunk: |f| <= 32767 (the filter's weighted A/B sums are bounded by
+// 32 * 256 * 1023 + 32 * 261111 < 2^24 before the >> 9), so |g| <= 32767, g^2 * 4 < 2^32 and |g * s| * 4 < 2^31 with
+// |s| <= 16368; g1 * g2 goes to 64 bits per pixel.
+template <typename T>
+__global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long long *mom, unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    constexpr int    NCH = 4;
+    const Tile       t   = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
+    const PlaneArgs &P   = A.pl[t.plane];
+    const int        cw  = t.w >> 2;
+    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
+    const size_t     pn = (size_t)P.fstride * P.H;
+    int              uu[NCH][4], ss[NCH][4]; // u = x << 4 and s = (src - x) << 4 per pixel
+    size_t           fo[NCH];
+    bool             on[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        const int ch = threadIdx.x + k * 256, y = t.y0 + (ch >> 4), x = t.x0 + (ch & 15) * 4;
+        on[k]        = (ch >> 4) < t.h && (ch & 15) < cw;
+        fo[k]        = (size_t)y * P.fstride + x;
+        int dv[4] = {0, 0, 0, 0}, sv[4] = {0, 0, 0, 0};
+        if (on[k]) {
+            load4(d + (size_t)y * P.dstride + x, dv);
+            load4(s + (size_t)y * P.sstride + x, sv);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) uu[k][j] = dv[j] << 4, ss[k][j] = (sv[j] - dv[j]) << 4;
+    }
+    const int pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
+    for (int e = 0; e < P.ne; e++) {
+        const int          ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const int16_t     *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+        unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            if (!on[k]) continue;
+            int a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
+            if (r0) load4s(f0 + fo[k], a0);
+            if (r1) load4s(f1 + fo[k], a1);
+            uint32_t m0 = 0, m1 = 0;
+            int      m3 = 0, m4 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int g1 = r0 ? a0[j] - uu[k][j] : 0, g2 = r1 ? a1[j] - uu[k][j] : 0;
+                m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
+                m3 += g1 * ss[k][j], m4 += g2 * ss[k][j];
+                M2 += (unsigned long long)(long long)(g1 * g2);
+            }
+            M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
+        }
         // wave totals on 32-bit DPP adds over limbs; the moments an ep's filters cannot produce stay zero
         unsigned long long tot[5] = {0, 0, 0, 0, 0};
-        if (SG_NP == 4) { // the lane partials are the (un-flushed) 32-bit sums
-            if (r0) tot[0] = wave_sum_u32_wide(m0), tot[3] = (unsigned long long)wave_sum_i32_wide(m3);
-            if (r1) tot[1] = wave_sum_u32_wide(m1), tot[4] = (unsigned long long)wave_sum_i32_wide(m4);
-        } else {
-            if (r0) tot[0] = wave_sum_u64_limbs(M[0]), tot[3] = wave_sum_u64_limbs(M[2]);
-            if (r1) tot[1] = wave_sum_u64_limbs(M[1]), tot[4] = wave_sum_u64_limbs(M[3]);
-        }
-        if (r0 && r1) tot[2] = wave_sum_u64_limbs((unsigned long long)m2);
+        if (r0) tot[0] = wave_sum_u64_limbs(M0), tot[3] = wave_sum_u64_limbs(M3);
+        if (r1) tot[1] = wave_sum_u64_limbs(M1), tot[4] = wave_sum_u64_limbs(M4);
+        if (r0 && r1) tot[2] = wave_sum_u64_limbs(M2);
         if ((threadIdx.x & 63) == WAVE_LAST)
 #pragma unroll
-            for (int k = 0; k < 5; k++)
-                if (tot[k]) atomicAdd((unsigned long long *)&mom[(size_t)pair * 5 + k], tot[k]);
-        __syncthreads(); // ep e + 2 rewrites this ep's buffer; ep e + 1's maps are complete
+            for (int q = 0; q < 5; q++)
+                if (tot[q]) atomicAdd((unsigned long long *)&mom[(size_t)(pb + e) * 5 + q], tot[q]);
     }
     PROF_END(tk);
 }
@@ -1783,7 +1806,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         HIP_TRY(hipGetLastError());
     }
     if (nt_sg) {
-        run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, (long long *)dp(o_mom), tk); });
+        run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
+        run(1, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(sgr_mom_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (long long *)dp(o_mom), tk);
+        });
         HIP_TRY(hipGetLastError());
     }
     mark(0);
