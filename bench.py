@@ -39,10 +39,23 @@ import time
 
 import numpy as np
 
-# the frames in flight need more than HIP's default 4 hardware queues per process (each frame runs on 3 streams);
-# set before the HIP runtime starts
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+FRAMES_IN_FLIGHT = 3  # default frames pipelined per GPU (measured: 1 -> 1498, 2 -> 1590, 3 -> 1750, 4 -> 1460 Mpx/s)
+
+
+def _frames_in_flight(argv):
+    for i, w in enumerate(argv):
+        if w == "--frames-in-flight" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if w.startswith("--frames-in-flight="):
+            return int(w.split("=", 1)[1])
+    return FRAMES_IN_FLIGHT
+
+
+# the frames in flight need more than HIP's default 4 hardware queues per process (each frame runs on 3 streams
+# and shares none); set before the HIP runtime starts
+_want_queues = max(8, 4 * _frames_in_flight(sys.argv[1:]))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < _want_queues:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(_want_queues, 32))
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
@@ -83,7 +96,7 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
                     help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
     ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
-    ap.add_argument("--frames-in-flight", type=int, default=2,
+    ap.add_argument("--frames-in-flight", type=int, default=FRAMES_IN_FLIGHT,
                     help="frames pipelined per GPU, each on its own streams and host thread (the encoder's "
                          "picture-level parallelism); a step processes one frame per slot")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -196,6 +209,7 @@ def main():
             self.lr_rb, self.lr_re = svtgpu.lr_unit_rows(self.lr.units, n, rank)  # LR: unit-row bands, all-gather
             self.ev = []  # per timed step: events on the streams the kernels run on
             self.lf_levels = []
+            self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
 
         def step(self, timed):
             torch.cuda.set_stream(self.stream)  # per thread
@@ -235,6 +249,7 @@ def main():
             if timed:
                 es[7].record(md_stream)
             # LR search + apply on the CDEF output (boundary lines from the DLF output)
+            self.at_lr.set()
             if n == 1:
                 lr_ft = lr.search(O, S, lr_ctrls, sp)
             else:
@@ -263,12 +278,19 @@ def main():
 
     def run(slot, steps, timed):
         try:
+            # frame k starts when frame k - 1 reaches its LR stage: the frames stay offset by part of a frame, so one's
+            # VALU-bound search overlaps the other's latency-bound stages (started together they run in lockstep and
+            # contend for the same units)
+            if slot.k > 0:
+                slots[slot.k - 1].at_lr.wait(60)  # bounded: a failed slot must not hang the next
             for _ in range(steps):
                 slot.step(timed)
         except BaseException as e:  # re-raised on the main thread
             errors.append(e)
 
     def run_all(steps, timed):
+        for sl in slots:
+            sl.at_lr.clear()
         if F == 1:
             run(slots[0], steps, timed)
         else:
