@@ -95,7 +95,12 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true", help="no HIP-event timing inside the LR search")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
                     help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
-    ap.add_argument("--cpu-sample", default="1920x1080", help="crop of the frame timed on the host CPU")
+    ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
+    ap.add_argument("--cpu-passes", type=int, default=6,
+                    help="reference CPU baseline: passes over the crops (sizes the sample to ~10-30 s of CPU work)")
+    ap.add_argument("--cpu-kind", choices=("reference", "port"), default="reference",
+                    help="CPU baseline: the reference's own C + AVX2 kernels (oracle/_ref/ref_bench, built from the "
+                         "reference sources by oracle/ref.mk) or the repo's C restatement (oracle/)")
     ap.add_argument("--frames-in-flight", type=int, default=FRAMES_IN_FLIGHT,
                     help="frames pipelined per GPU, each on its own streams and host thread (the encoder's "
                          "picture-level parallelism); a step processes one frame per slot")
@@ -104,36 +109,126 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, sample, lr_ctrls, lr_us, md_refs, md_mvs):
-    """The repo's scalar C restatement (oracle/) on one host core over a crop of the same frame: the same
-    stages as the GPU step (DLF pick + filter, CDEF search + pick + apply, LR search + apply, MD batch)."""
+def cpu_threads():
+    """Host threads for the CPU baseline: the cores this process may use, at most 16 (a GPU box's CPU share is 16 cores
+    per GPU while os.cpu_count() reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+
+
+def write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs):
+    """The input file of oracle/_ref/ref_bench (layout in oracle/ref_harness/ref_bench.c's main)."""
+    gx, gy = (int(x) for x in grid.split("x"))
+    H, W = rec[0].shape
+    hdr = np.array([W, H, bd, len(md_refs), q, lam, gx, gy, lr_ctrls.rdmult, *lr_ctrls.switchable_restore_cost,
+                    *lr_ctrls.wiener_restore_cost, *lr_ctrls.sgrproj_restore_cost], np.int32)
+    f.write(hdr.tobytes())
+    f.write(bytes(ctrls))
+    for planes in (src, rec):
+        for p in planes:
+            f.write(np.ascontiguousarray(p, np.uint16).tobytes())
+    f.write(np.ascontiguousarray(mi).tobytes())
+    for r in md_refs:
+        f.write(np.ascontiguousarray(r, np.uint16).tobytes())
+    f.write(np.ascontiguousarray(md_mvs, np.int32).tobytes())
+
+
+def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrls, md_refs, md_mvs, passes):
+    """The reference's own CPU path (oracle/_ref/ref_bench: its C with the AVX2/SSE2 kernels an AVX2 host binds) on the
+    host's cores, over the same crops as cpu_baseline. The frame, mode info, CDEF controls, LR rate inputs, MD
+    references and MVs are handed over in a file; the binary times itself (input loading excluded)."""
+    import subprocess
+    import tempfile
+    gx, gy = (int(x) for x in grid.split("x"))
+    H, W = rec[0].shape
+    nthr = min(cpu_threads(), gx * gy)
+    with tempfile.NamedTemporaryFile(prefix="ref_bench_", suffix=".bin", dir="/tmp", delete=True) as f:
+        write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs)
+        f.flush()
+        res = subprocess.run([REF_BENCH, f.name, str(nthr), str(passes)], capture_output=True, text=True, timeout=600)
+    if res.returncode != 0:
+        raise RuntimeError("ref_bench failed (%d): %s" % (res.returncode, res.stderr.strip()[-400:]))
+    kv = dict(t.split("=") for t in res.stdout.split()[1:])
+    px, dt = int(kv["px"]), float(kv["seconds"])
+    cw, ch = (W // gx) & ~63, (H // gy) & ~63
+    return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": nthr, "kind": "reference",
+            "sample": "the %d-bit frame cut into %dx%d crops of %dx%d, each through the same stages (DLF level search + "
+                      "filter, CDEF search + strength selection + apply at cdef_level %d, LR search + apply at wn/sg "
+                      "level 1, MD SAD/SSE/variance over 7 refs) by the reference's own C with its AVX2/SSE2 kernels "
+                      "(oracle/_ref/ref_bench), %d passes, %d host threads, %.1f s"
+                      % (bd, gx, gy, cw, ch, level, passes, nthr, dt)}
+
+
+def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, grid, lr_ctrls, lr_us, md_refs, md_mvs):
+    """The repo's C restatement (oracle/, gcc -O2) on the host's cores: the frame is cut into gx x gy crops and each
+    host thread runs the same stages as the GPU step (DLF pick + filter, CDEF search + pick + apply, LR search + apply,
+    MD batch) on one crop at a time (ctypes releases the GIL, so the threads run in parallel)."""
+    import threading as th
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: used here only as the reported CPU baseline
-    sw, sh = (int(x) for x in sample.split("x"))
-    mi_c = np.ascontiguousarray(mi[:sh // 4, :sw // 4])
-    crop = [rec[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in rec[1:]]
-    cs = [src[0][:sh, :sw]] + [p[:sh // 2, :sw // 2] for p in src[1:]]
-    crop = [np.ascontiguousarray(a) for a in crop]
-    cs = [np.ascontiguousarray(a) for a in cs]
+    gx, gy = (int(x) for x in grid.split("x"))
+    H, W = rec[0].shape
+    cw, ch = (W // gx) & ~63, (H // gy) & ~63  # crops on the 64-px grid (whole FBs, units, SBs)
     ctrls = oracle.controls(level)
-    t0 = time.perf_counter()
-    lfp = oracle.dlf_pick(crop, cs, bd, mi_c, lf_start, 0, 0, 0, 0, 0)
-    crop = oracle.dlf_frame(crop, bd, mi_c, lfp)
-    mse, skip, d, v = oracle.cdef_search_frame(crop, cs, bd, ctrls, q)
-    prm, fbs = oracle.cdef_pick(sw, sh, mse, skip, ctrls, q, lam)
-    cdef_out = oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
     octrls = oracle.lr_controls(1, 1, rdmult=lr_ctrls.rdmult, switchable=tuple(lr_ctrls.switchable_restore_cost),
                                 wiener=tuple(lr_ctrls.wiener_restore_cost), sgrproj=tuple(lr_ctrls.sgrproj_restore_cost))
-    ft, units, _ = oracle.lr_search_frame(cdef_out, cs, bd, lr_us, octrls)
-    oracle.lr_apply_frame(crop, cdef_out, bd, ft, lr_us, units)
-    nsb = ((sw + 63) // 64) * ((sh + 63) // 64)
-    oracle.md_dist_batch(cs[0], [np.ascontiguousarray(r[:sh, :sw]) for r in md_refs],
-                         bd, np.ascontiguousarray(md_mvs[:nsb], np.int32))
+    nsbx = (W + 63) // 64
+
+    def one(cx, cy):
+        y0, x0 = cy * ch, cx * cw
+        mi_c = np.ascontiguousarray(mi[y0 // 4:(y0 + ch) // 4, x0 // 4:(x0 + cw) // 4])
+        crop = [np.ascontiguousarray(rec[0][y0:y0 + ch, x0:x0 + cw])] + \
+               [np.ascontiguousarray(p[y0 // 2:(y0 + ch) // 2, x0 // 2:(x0 + cw) // 2]) for p in rec[1:]]
+        cs = [np.ascontiguousarray(src[0][y0:y0 + ch, x0:x0 + cw])] + \
+             [np.ascontiguousarray(p[y0 // 2:(y0 + ch) // 2, x0 // 2:(x0 + cw) // 2]) for p in src[1:]]
+        lfp = oracle.dlf_pick(crop, cs, bd, mi_c, lf_start, 0, 0, 0, 0, 0)
+        crop = oracle.dlf_frame(crop, bd, mi_c, lfp)
+        mse, skip, d, v = oracle.cdef_search_frame(crop, cs, bd, ctrls, q)
+        prm, fbs = oracle.cdef_pick(cw, ch, mse, skip, ctrls, q, lam)
+        cdef_out = oracle.cdef_apply_frame(crop, bd, None, d, v, prm, fbs)
+        ft, units, _ = oracle.lr_search_frame(cdef_out, cs, bd, lr_us, octrls)
+        oracle.lr_apply_frame(crop, cdef_out, bd, ft, lr_us, units)
+        sbs = [(y0 // 64 + r) * nsbx + x0 // 64 + c for r in range(ch // 64) for c in range(cw // 64)]
+        oracle.md_dist_batch(cs[0], [np.ascontiguousarray(r[y0:y0 + ch, x0:x0 + cw]) for r in md_refs], bd,
+                             np.ascontiguousarray(md_mvs[sbs], np.int32))
+
+    jobs = [(cx, cy) for cy in range(gy) for cx in range(gx)]
+    nthr = min(cpu_threads(), len(jobs))
+    lock, errors = th.Lock(), []
+
+    def worker():
+        while True:
+            with lock:
+                if not jobs:
+                    return
+                job = jobs.pop()
+            try:
+                one(*job)
+            except BaseException as e:
+                errors.append(e)
+                return
+
+    t0 = time.perf_counter()
+    threads = [th.Thread(target=worker) for _ in range(nthr)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
     dt = time.perf_counter() - t0
-    return {"value": round(sw * sh / dt / 1e6, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-            "sample": "%dx%d crop of the same %d-bit frame through the same stages (DLF pick+filter, CDEF "
-                      "search+pick+apply at cdef_level %d, LR search+apply at wn/sg level 1, MD batch 7 refs), scalar "
-                      "C restatement (oracle/), 1 thread, %.1f s" % (sw, sh, bd, level, dt)}
+    if errors:
+        raise errors[0]
+    px = gx * gy * cw * ch
+    return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": nthr, "kind": "port",
+            "sample": "the %d-bit frame cut into %dx%d crops of %dx%d, each through the same stages (DLF pick+filter, "
+                      "CDEF search+pick+apply at cdef_level %d, LR search+apply at wn/sg level 1, MD batch 7 refs) by the "
+                      "C restatement (oracle/, gcc -O2), %d host threads, %.1f s"
+                      % (bd, gx, gy, cw, ch, level, nthr, dt)}
 
 
 def main():
@@ -392,8 +487,12 @@ def main():
     }
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
         s0 = slots[0]
-        out["cpu_baseline"] = cpu_baseline(s0.src, s0.rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_sample,
-                                           lr_ctrls, lr_us, md_ref_y, s0.md_mvs)
+        if a.cpu_kind == "reference" and os.path.exists(REF_BENCH):
+            out["cpu_baseline"] = cpu_baseline_reference(s0.src, s0.rec, mi, ctrls, bd, a.cdef_level, q, lam,
+                                                         a.cpu_grid, lr_ctrls, md_ref_y, s0.md_mvs, a.cpu_passes)
+        else:
+            out["cpu_baseline"] = cpu_baseline(s0.src, s0.rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_grid,
+                                               lr_ctrls, lr_us, md_ref_y, s0.md_mvs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if n > 1:

@@ -27,16 +27,26 @@ MD_C     := Lib/Encoder/C_DEFAULT/EbComputeSAD_C.c Lib/Encoder/C_DEFAULT/varianc
             Lib/Common/Codec/EbPictureOperators.c
 # reference AVX2 sources (the CPU baseline the north star names)
 REF_AVX2 := Lib/Common/ASM_AVX2/cdef_block_avx2.c Lib/Encoder/ASM_AVX2/EbCdef_AVX2.c
+# ... and the rest of the AVX2 / SSE2 kernels an AVX2 host binds for the bench's stages (ref_bench)
+BENCH_SIMD := Lib/Common/ASM_AVX2/selfguided_avx2.c Lib/Common/ASM_AVX2/wiener_convolve_avx2.c \
+            Lib/Common/ASM_AVX2/highbd_convolve_avx2.c Lib/Encoder/ASM_AVX2/pickrst_avx2.c \
+            Lib/Encoder/ASM_AVX2/EbComputeSAD_Intrinsic_AVX2.c \
+            Lib/Encoder/ASM_AVX2/variance_avx2.c Lib/Encoder/ASM_AVX2/variance_impl_avx2.c \
+            Lib/Encoder/ASM_AVX2/highbd_variance_avx2.c Lib/Encoder/ASM_AVX2/sse_avx2.c \
+            Lib/Common/ASM_AVX2/EbPictureOperators_Intrinsic_AVX2.c Lib/Common/ASM_SSE2/EbDeblockingFilter_Intrinsic_SSE2.c \
+            Lib/Common/ASM_SSE2/EbPictureOperators_Intrinsic_SSE2.c
 
 C_OBJ    := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_C))
 DLF_OBJ  := $(patsubst %.c,$(OUT)/obj/%.o,$(DLF_C))
 MD_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(MD_C))
 LR_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(LR_C))
 AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
+SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
 
-all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr
+all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/ref_bench
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
+$(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
 # RunEmms (x86 `emms`, only reachable through aom_clear_system_state) lives in NASM sources this image cannot
 # assemble; the generic (non-x86) configuration of this file skips that call and computes the same values.
 $(OUT)/obj/Lib/Encoder/Codec/EbRestorationPick.o: CFLAGS += -UARCH_X86_64
@@ -56,8 +66,9 @@ $(OUT)/gen_golden_md: oracle/ref_harness/gen_golden_md.c $(MD_OBJ) $(C_OBJ)
 $(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(sort $(LR_OBJ) $(MD_OBJ) $(C_OBJ))
 	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
 
-$(OUT)/ref_cdef_bench: oracle/ref_harness/ref_cdef_bench.c $(C_OBJ) $(AVX2_OBJ)
-	$(CC) $(CFLAGS) -mavx2 $^ -o $@ -Wl,--gc-sections -lm -lpthread
+# the reference's CPU path on the bench workload (bench.py cpu_baseline, kind "reference")
+$(OUT)/ref_bench: oracle/ref_harness/ref_bench.c $(sort $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ)) $(AVX2_OBJ) $(SIMD_OBJ)
+	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
 
 clean:
 	rm -rf $(OUT)
