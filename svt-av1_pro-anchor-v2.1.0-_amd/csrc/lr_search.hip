@@ -584,12 +584,21 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                 }
         }
     }
-    int pix[SG_NP]; // this lane's pixels: threadIdx.x + k * SG_NT
+    // this lane's pixels (threadIdx.x + k * SG_NT): value, A/B map index, filter-plane offset and row parity -- the
+    // divisions by the tile width are done once here, not per ep (a division the compiler cannot hoist past the
+    // bounds checks costs ~15 VALU ops with quarter-rate multiplies)
+    int pix[SG_NP], pc[SG_NP], po[SG_NP];
+    uint32_t podd = 0, qodd = 0; // bit k: pixel k / map position k on an odd row
 #pragma unroll
     for (int k = 0; k < SG_NP; k++) {
-        const int i = threadIdx.x + k * SG_NT;
-        pix[k]      = i < npx ? v0[(i / t.w) * SG_V + i % t.w] : 0;
+        const int i = threadIdx.x + k * SG_NT, y = i / t.w, x = i - y * t.w;
+        pix[k] = i < npx ? v0[y * SG_V + x] : 0;
+        pc[k]  = (y + 1) * bw + x + 1;
+        po[k]  = (t.y0 + y) * P.fstride + t.x0 + x;
+        podd |= (uint32_t)(y & 1) << k;
     }
+#pragma unroll
+    for (int k = 0; k < SG_NQ; k++) qodd |= (uint32_t)(((threadIdx.x + k * SG_NT) / bw - 1) & 1) << k;
     const size_t pn = (size_t)P.fstride * P.H;
     auto build_ab = [&](int e) { // A/B maps of ep index e into buffer e & 1
         const int ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
@@ -608,7 +617,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                 sgr_ab_fast(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
                 m1[q] = (b << 9) | a;
             }
-            if (r0 && ((q / bw - 1) & 1)) {
+            if (r0 && (qodd >> k & 1)) {
                 sgr_ab_fast(s2[k], q2[k], 25, c_sgr_s[ep][0], P.bd, xby, &a, &b);
                 m2[q] = (b << 9) | a;
             }
@@ -625,12 +634,11 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
         for (int k = 0; k < SG_NP; k++) {
             const int i = threadIdx.x + k * SG_NT;
             if (i >= npx) break;
-            const int    y = i / t.w, x = i % t.w, c = (y + 1) * bw + x + 1;
-            const size_t o = (size_t)(t.y0 + y) * P.fstride + t.x0 + x;
+            const int c = pc[k], o = po[k];
             if (r0) {
                 const int *Q = ab2e + c;
                 int        aa, bb, sh;
-                if (!(y & 1)) {
+                if (!(podd >> k & 1)) {
                     const int c6 = Q[-bw] + Q[bw], c5 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
                     const int a6 = (Q[-bw] & 511) + (Q[bw] & 511);
                     const int a5 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
@@ -792,7 +800,7 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
                     const uint32_t g = pack2(a0[j] - u, a1[j] - u);
 #pragma unroll
                     for (int c = 0; c < SG_NC; c++) { // branch-free: candidates outside the tree have xq = 0
-                        const int ee = (dot2(g, xq[c], 0) + c0) >> 11;
+                        const int ee = dot2(g, xq[c], c0) >> 11; // c0 rides in the dot product's accumulator
                         acc[c] += (uint32_t)(ee * ee);
                     }
                 }
