@@ -741,6 +741,11 @@ __global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long l
 // evaluated on them.  Per pixel the filter differences (g1, g2) = (flt0 - u, flt1 - u) fit int16 (|g| < 2^15),
 // as do the xq pairs, so a candidate costs one v_dot2_i32_i16 plus the error.  Tiles are read in 4-pixel chunks
 // (tile widths and x offsets are multiples of 4), 16 chunks per row.
+typedef short v2i16s __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t pk_sub16(uint32_t a, uint32_t b) { // per-half a - b mod 2^16
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2i16s, a) - __builtin_bit_cast(v2i16s, b));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
                                                        int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
@@ -750,7 +755,7 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
     const int n = cnt[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
     constexpr int      NCH   = 4;
-    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated // chunks per lane (64 rows x 16 chunks / 256 lanes)
+    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated
     for (int it = blockIdx.x; it < n; it += gridDim.x) {
         const Tile       t = A.tiles[items[it]];
         const PlaneArgs &P = A.pl[t.plane];
@@ -758,46 +763,67 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
         npx_t += t.w * t.h; // profiling
         const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
         const size_t     pn = (size_t)P.fstride * P.H;
+        // chunk k of this lane: row (threadIdx.x >> 4) + 16 k, 4 pixels at column 4 (threadIdx.x & 15)
+        const int        fo0 = (t.y0 + (threadIdx.x >> 4)) * P.fstride + t.x0 + (threadIdx.x & 15) * 4;
+        const int        fos = 16 * P.fstride;
         uint32_t         px2[NCH][4]; // (x, x - src) per pixel
-        size_t           fo[NCH];
-        bool             on[NCH];
+        uint32_t         on = 0;      // bit k: chunk k inside the tile
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
             const int ch = threadIdx.x + k * 256, y = t.y0 + (ch >> 4), x = t.x0 + (ch & 15) * 4;
-            on[k]        = (ch >> 4) < t.h && (ch & 15) < cw;
-            fo[k]        = (size_t)y * P.fstride + x;
-            if (on[k]) {
+            if ((ch >> 4) < t.h && (ch & 15) < cw) {
+                on |= 1u << k;
                 int dv[4], sv[4];
                 load4(d + (size_t)y * P.dstride + x, dv);
                 load4(s + (size_t)y * P.sstride + x, sv);
 #pragma unroll
                 for (int j = 0; j < 4; j++) px2[k][j] = pack2(dv[j], dv[j] - sv[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) px2[k][j] = 0;
             }
         }
-        for (int e = 0; e < P.ne; e++) {
+        // the eps with a pending tree; their filter planes are fetched one ep ahead of the arithmetic
+        uint32_t act = 0;
+        for (int e = 0; e < P.ne; e++) act |= (candm[pb + e] != 0u) << e;
+        uint2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
+        auto  fetch = [&](int e, uint2 *x0, uint2 *x1) {
+            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+#pragma unroll
+            for (int k = 0; k < NCH; k++)
+                if (on >> k & 1) x0[k] = *(const uint2 *)(f0 + fo0 + k * fos), x1[k] = *(const uint2 *)(f1 + fo0 + k * fos);
+        };
+        int e = act ? __builtin_ctz(act) : -1;
+        if (e >= 0) fetch(e, w0, w1);
+        while (e >= 0) {
+            act &= act - 1;
+            const int en = act ? __builtin_ctz(act) : -1;
+            if (en >= 0) fetch(en, n0, n1);
             const int      pair = pb + e;
             const uint32_t mask = candm[pair];
-            if (!mask) continue;
             npx_e += t.w * t.h; // profiling
             uint32_t xq[SG_NC];
 #pragma unroll
             for (int c = 0; c < SG_NC; c++)
                 xq[c] = (mask >> c & 1) ? pack2(cand[(pair * SG_NC + c) * 2], cand[(pair * SG_NC + c) * 2 + 1]) : 0u;
-            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
-            uint32_t       acc[SG_NC];
+            uint32_t acc[SG_NC];
 #pragma unroll
             for (int c = 0; c < SG_NC; c++) acc[c] = 0;
 #pragma unroll
             for (int k = 0; k < NCH; k++) {
-                if (!on[k]) continue;
-                int a0[4], a1[4];
-                load4s(f0 + fo[k], a0);
-                load4s(f1 + fo[k], a1);
+                if (!(on >> k & 1)) continue;
+                // (flt0, flt1) int16 pairs of the 4 pixels, then g = (flt0 - u, flt1 - u) on packed 16-bit lanes
+                // (|g| < 2^15, so the wrapped halves are the exact differences)
+                const uint32_t fp[4] = {__builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x05040100u),
+                                        __builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x07060302u),
+                                        __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x05040100u),
+                                        __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x07060302u)};
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     // floor((v + 1024) / 2^11) + (x - src) == (v + 1024 + (x - src) * 2^11) >> 11
-                    const int      u = (int)(px2[k][j] & 0xFFFF) << 4, c0 = 1024 + (((int)px2[k][j] >> 16) << 11);
-                    const uint32_t g = pack2(a0[j] - u, a1[j] - u);
+                    const uint32_t uu = __umul24(px2[k][j] & 0xFFFF, 0x00100010u); // (x << 4, x << 4)
+                    const int      c0 = 1024 + (((int)px2[k][j] >> 16) << 11);
+                    const uint32_t g  = pk_sub16(fp[j], uu);
 #pragma unroll
                     for (int c = 0; c < SG_NC; c++) { // branch-free: candidates outside the tree have xq = 0
                         const int ee = dot2(g, xq[c], c0) >> 11; // c0 rides in the dot product's accumulator
@@ -811,6 +837,9 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
                 const unsigned long long w = wave_sum_u32_wide(acc[c]); // <= 16 pixels per lane: fits 32 bits
                 if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
             }
+#pragma unroll
+            for (int k = 0; k < NCH; k++) w0[k] = n0[k], w1[k] = n1[k];
+            e = en;
         }
     }
     if (pc && threadIdx.x == 0 && npx_t) {
