@@ -48,6 +48,8 @@ constexpr int PRJ_MIN0 = -96, PRJ_MAX0 = 31, PRJ_MIN1 = -32, PRJ_MAX1 = 95;
 const int     kTapMin[3] = {-5, -23, -17}, kTapMax[3] = {10, 8, 46};
 const int     kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
                               {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
+// r = 1 s values of the sets (c_sgr_s[.][1]): eps 2/11, 5/12 and 8/13 share theirs, so their r = 1 filters are equal
+const int     kHostSgrS1[16] = {3236, 2158, 1618, 1438, 1295, 1177, 1079, 996, 925, 863, 2589, 1618, 1177, 925, -1, -1};
 
 struct PlaneArgs {
     const void *dgd, *src;
@@ -55,6 +57,7 @@ struct PlaneArgs {
     int32_t     dstride, sstride, W, H, bd, fstride;
     int32_t     unit_base, pair_base, ne; // SGR pair of (unit, k) = pair_base + (unit - unit_base) * ne + k
     int32_t     eps[16];
+    int32_t     f1e[16];                  // the ep slot whose r = 1 plane holds slot k's (equal s: same filter)
     int32_t     win, nval;                // Wiener window and statistics values per unit
     int64_t     mh_off;                   // this plane's statistics in the M/H buffer (int64 elements)
 };
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
             m1[q] = (b << 9) | a, m2[q] = (b << 9) | a;
             continue;
 #endif
-            if (r1) {
+            if (r1 && P.f1e[e] == e) {
                 sgr_ab_fast(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
                 m1[q] = (b << 9) | a;
             }
@@ -654,7 +657,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                 const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << (sh - 1))) >> sh;
                 f0g[o]      = (int16_t)f;
             }
-            if (r1) {
+            if (r1 && P.f1e[e] == e) { // an ep sharing an earlier slot's r = 1 filter reads that plane
                 const int *Q  = ab1e + c;
                 const int  c4 = Q[0] + Q[-1] + Q[1] + Q[-bw] + Q[bw], c3 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
                 const int  a4 = (Q[0] & 511) + (Q[-1] & 511) + (Q[1] & 511) + (Q[-bw] & 511) + (Q[bw] & 511);
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long l
     const int pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
     for (int e = 0; e < P.ne; e++) {
         const int          ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-        const int16_t     *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+        const int16_t     *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
         for (int e = 0; e < P.ne; e++) act |= (candm[pb + e] != 0u) << e;
         uint2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
         auto  fetch = [&](int e, uint2 *x0, uint2 *x1) {
-            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
 #pragma unroll
             for (int k = 0; k < NCH; k++)
                 if (on >> k & 1) x0[k] = *(const uint2 *)(f0 + fo0 + k * fos), x1[k] = *(const uint2 *)(f1 + fo0 + k * fos);
@@ -860,7 +863,7 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
     const int        e = b[0], ep = b[1], xq0 = b[2], xq1 = b[3], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     const size_t     pn = (size_t)P.fstride * P.H;
-    const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = f0 + pn;
+    const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)(e >= 0 ? P.f1e[e] : e) * 2 * pn + pn;
     const int        maxv = (1 << P.bd) - 1;
     unsigned long long acc = 0;
     for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
@@ -1779,7 +1782,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         P.W = rec->pw[p], P.H = rec->ph[p], P.bd = rec->bit_depth, P.fstride = (P.W + 63) & ~63;
         P.flt       = s->d_flt + flt_off;
         P.unit_base = pp[p].unit_base, P.pair_base = pp[p].pair_base, P.ne = pp[p].ne;
-        for (int k = 0; k < pp[p].ne; k++) P.eps[k] = pp[p].eps[k];
+        for (int k = 0; k < pp[p].ne; k++) {
+            P.eps[k] = pp[p].eps[k], P.f1e[k] = k;
+            for (int j = 0; j < k; j++)
+                if (kHostSgrR[P.eps[k]][1] && kHostSgrS1[P.eps[j]] == kHostSgrS1[P.eps[k]]) {
+                    P.f1e[k] = j;
+                    break;
+                }
+        }
         P.win = pp[p].win, P.nval = pp[p].nval, P.mh_off = (int64_t)pp[p].mh_off;
         if (pp[p].sg) flt_off += (size_t)pp[p].ne * 2 * P.fstride * P.H;
     }
