@@ -554,11 +554,14 @@ __device__ inline void sgr_ab_fast(int sum, int sq, int n, int s, int bd, const 
 template <typename T>
 __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    __shared__ uint16_t v[SG_V * SG_V];
     // packed B << 9 | A (A <= 256, B < 2^19) of the r = 1 and r = 2 passes, double-buffered over eps: the maps of
     // ep e + 1 are built while ep e is filtered, one barrier per ep
     __shared__ int ab1[2][SG_B * SG_B], ab2[2][SG_B * SG_B];
     __shared__ int      xby[256];
+    // the tile with its 3-pixel border lives in ab1[1] until the box sums are taken (ab1[1] is first written by
+    // build_ab(1), after the barrier that follows build_ab(0)): 70 KB of LDS, two workgroups per CU
+    static_assert(SG_V * SG_V * 2 <= SG_B * SG_B * 4, "tile image fits the aliased map buffer");
+    uint16_t *const v = (uint16_t *)ab1[1];
     const Tile       t = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd;
