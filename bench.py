@@ -454,7 +454,8 @@ def main():
                 "note": "largest device-time kernel class of the step; launch durations from the device's "
                         "s_memrealtime clock (first workgroup start to last workgroup end, every launch of the timed "
                         "steps); achieved = algorithmic bytes (samples + filter planes touched) / device time; the "
-                        "class is VALU-bound, so its HBM fraction is low by construction"}
+                        "class is latency-bound (~17 KB and ~10 VALU ops per pixel per round, 64-73% of wave cycles "
+                        "waiting in the SQ counters; DESIGN.md 3.6), so its HBM fraction is low"}
     roof["traffic"], roof["traffic_source"] = measured_traffic(a.traffic_json, roof["kernel"], bd)
     out = {
         "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
