@@ -148,16 +148,27 @@ def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrl
     gx, gy = (int(x) for x in grid.split("x"))
     H, W = rec[0].shape
     nthr = min(cpu_threads(), gx * gy)
+    def run(f, threads, npass):
+        res = subprocess.run([REF_BENCH, f.name, str(threads), str(npass)], capture_output=True, text=True, timeout=600)
+        if res.returncode != 0:
+            raise RuntimeError("ref_bench failed (%d): %s" % (res.returncode, res.stderr.strip()[-400:]))
+        kv = dict(t.split("=") for t in res.stdout.split()[1:])
+        return int(kv["px"]), float(kv["seconds"])
+
     with tempfile.NamedTemporaryFile(prefix="ref_bench_", suffix=".bin", dir="/tmp", delete=True) as f:
         write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs)
         f.flush()
-        res = subprocess.run([REF_BENCH, f.name, str(nthr), str(passes)], capture_output=True, text=True, timeout=600)
-    if res.returncode != 0:
-        raise RuntimeError("ref_bench failed (%d): %s" % (res.returncode, res.stderr.strip()[-400:]))
-    kv = dict(t.split("=") for t in res.stdout.split()[1:])
-    px, dt = int(kv["px"]), float(kv["seconds"])
+        px, dt = run(f, nthr, passes)
+        px1, dt1 = run(f, 1, 1)  # one thread, one pass: the per-core rate
+    model = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as ci:
+            model = next(l.split(":", 1)[1].strip() for l in ci if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     cw, ch = (W // gx) & ~63, (H // gy) & ~63
     return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": nthr, "kind": "reference",
+            "single_thread_value": round(px1 / dt1 / 1e6, 4), "cpu": model,
             "sample": "the %d-bit frame cut into %dx%d crops of %dx%d, each through the same stages (DLF level search + "
                       "filter, CDEF search + strength selection + apply at cdef_level %d, LR search + apply at wn/sg "
                       "level 1, MD SAD/SSE/variance over 7 refs) by the reference's own C with its AVX2/SSE2 kernels "
