@@ -256,6 +256,16 @@ __global__ void fill_i8_kernel(int8_t *p, int n) {
     if (i < n) p[i] = 0;
 }
 
+// FB-chunk workgroups per step across the live chains (x 4 row tiles): more parts spread the accumulation, fewer
+// parts mean fewer u64 atomics into the 4096 totals (SVTGPU_PICK_PARTS for sweeps)
+static int pick_parts() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_PICK_PARTS");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 64;
+    }();
+    return v;
+}
+
 int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                           uint64_t lambda, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st) {
     const int nfb = s->nfb;
@@ -295,8 +305,9 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
             C.prev_shift   = step >= 1 && step < len && step >= nb; // shift before calls nb.. (refinements)
         }
         A.step = step;
-        // ~1024 workgroups per step whatever the number of live chains; chunk <= PICK_CHUNK FBs
-        const int want  = std::max(1, 256 / std::max(na, 1));
+        // ~256 workgroups per step whatever the number of live chains (64 parts x 4 row tiles: 256 parts spent
+        // more on the u64 atomics than they gained, 0.66 -> 0.59 ms per pick + apply); chunk <= PICK_CHUNK FBs
+        const int want  = std::max(1, pick_parts() / std::max(na, 1));
         A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_max + want - 1) / std::max(want, 1)));
         const int parts = std::max(1, (sb_max + A.chunk - 1) / A.chunk);
         const size_t lds = (size_t)A.chunk * 129 * 8;
