@@ -32,9 +32,6 @@
 
 #include "lr_common.h"
 
-#ifndef SGR_EXP
-#define SGR_EXP 0 // development experiments on sgr_flt_kernel (0 = the real kernel)
-#endif
 
 namespace {
 
@@ -614,11 +611,6 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
             const int q = threadIdx.x + k * SG_NT;
             if (q >= nq) break;
             int a, b;
-#if SGR_EXP == 3
-            a = s1[k] & 255, b = q1[k] & 0xFFFF;
-            m1[q] = (b << 9) | a, m2[q] = (b << 9) | a;
-            continue;
-#endif
             if (r1 && P.f1e[e] == e) {
                 sgr_ab_fast(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
                 m1[q] = (b << 9) | a;
