@@ -1959,10 +1959,17 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         tr("enqueued", c, C.g);
         return SVTGPU_OK;
     };
+    // every early exit below leaves no batch queued behind the caller: both chains' streams are drained, so the
+    // next search on this state may reuse d_work and the pinned staging at once (lr_search.hip:1977)
+    auto drain = [&](int rc) {
+        (void)hipStreamSynchronize(sw);
+        (void)hipStreamSynchronize(st);
+        return rc;
+    };
     while (ch[0].live || ch[1].live) {
         for (int c = 0; c < 2; c++)
             while (ch[c].live && ch[c].inflight < 2)
-                if (int rc = enqueue_batch(c)) return rc;
+                if (int rc = enqueue_batch(c)) return drain(rc);
         bool       consumed = false; // spin until the oldest batch of a live chain has published its count
         const auto t_spin   = clk();
         for (unsigned it = 0; !consumed; it++) {
@@ -1974,7 +1981,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 C.live = __atomic_load_n(f + 1, __ATOMIC_RELAXED) > 0;
                 C.head ^= 1, C.inflight--, consumed = true;
                 tr(C.live ? "landed-live" : "landed-done", c, C.g);
-                if (C.g > MAX_ROUNDS) return SVTGPU_ERR_INVALID_ARG; // a descent always terminates; guard anyway
+                if (C.g > MAX_ROUNDS) { // a descent always terminates; guard anyway (an internal failure)
+                    svtgpu_set_last_hip_error(hipErrorUnknown, "LR descent exceeded its round bound", __FILE__, __LINE__);
+                    return drain(SVTGPU_ERR_HIP);
+                }
             }
             // a stalled word (a failed launch): after 200 ms of spinning let the runtime report the stream error
             if (!consumed && (it & 4095) == 4095 && clk() - t_spin > std::chrono::milliseconds(200)) {
@@ -1987,7 +1997,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 if (!any) {
                     svtgpu_set_last_hip_error(hipErrorUnknown, "LR descent batch word missing after synchronize",
                                               __FILE__, __LINE__);
-                    return SVTGPU_ERR_HIP;
+                    return drain(SVTGPU_ERR_HIP);
                 }
             }
         }
