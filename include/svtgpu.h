@@ -128,12 +128,17 @@ typedef struct SvtGpuCdefControls {
     int8_t   default_second_pass_fs_uv[SVTGPU_CDEF_TOTAL_STRENGTHS]; /* -1 = chroma not tested */
     uint8_t  subsampling_factor;                                     /* 1, 2 or 4 */
     uint16_t zero_fs_cost_bias;                                      /* 0 = off, else x/64 */
+    /* use_reference_cdef_fs levels (11, 14, 15, 17): no strength search; the frame uses the strength pair the
+     * mode-decision configuration predicted from the references (pred_y_f / pred_uv_f, strength codes 0..63,
+     * set by the caller as EbModeDecisionConfigurationProcess.c:765-840 does) */
+    int8_t   use_reference_cdef_fs;
+    int8_t   pred_y_f;
+    int8_t   pred_uv_f;
 } SvtGpuCdefControls;
 
-/* Fill `c` exactly as set_cdef_controls(cdef_level) does (EncModeConfig.c:860-1330) for the
- * levels this library supports (1..17 minus use_reference_cdef_fs levels). Returns
- * SVTGPU_ERR_UNSUPPORTED for level 0 or reference-fs levels. fast_decode/resolution tweaks of the
- * zero_fs_cost_bias are applied by the caller. */
+/* Fill `c` exactly as set_cdef_controls(cdef_level) does (EncModeConfig.c:860-1330), levels 1..17
+ * (pred_y_f / pred_uv_f left 0). Returns SVTGPU_ERR_UNSUPPORTED for level 0 (CDEF off).
+ * fast_decode/resolution tweaks of the zero_fs_cost_bias are applied by the caller. */
 int svtgpu_cdef_controls_for_level(int cdef_level, SvtGpuCdefControls *c);
 
 /* Frame parameters chosen by the pick; layout mirrors CdefParams (EbAv1Structs.h:359-369). */
@@ -156,12 +161,22 @@ int32_t svtgpu_cdef_state_nfb(const SvtGpuCdefFrameState *s); /* nvfb*nhfb */
  * EbEncCdef.c:238).  Upload once per frame; NULL mask = every block listed. */
 int svtgpu_cdef_set_block_mask(SvtGpuCdefFrameState *s, const uint8_t *host_mask, void *stream);
 
-/* ≙ all segments of cdef_seg_search (EbCdefProcess.c:114-357) for SB64 frames.
- * recon = DLF output, source = input picture (same geometry/bit depth). */
+/* SB128 mode info: the BlockSize (EbDefinitions.h enum; 13 = 64X128, 14 = 128X64, 15 = 128X128) of the mode
+ * info at each 64x64 filter block's top-left, nfb bytes row-major — what cdef_seg_search and finish_cdef_search
+ * read (EbCdefProcess.c:188-199, EbEncCdef.c:805-812).  The search then folds each 128-wide area into its top-left
+ * filter block and the pick copies the area's strength into the other halves.  NULL = 64x64 superblocks.
+ * With frame bands (svtgpu_cdef_set_fb_rows) the band edges must fall on even filter-block rows. */
+int svtgpu_cdef_set_fb_bsize(SvtGpuCdefFrameState *s, const uint8_t *fb_bsize, void *stream);
+
+/* ≙ all segments of cdef_seg_search (EbCdefProcess.c:114-357).  recon = DLF output, source = input picture
+ * (same geometry/bit depth).  With use_reference_cdef_fs no strength is searched (EbCdefProcess.c:400): only
+ * the per-8x8 directions/variances the apply needs are computed (svt_av1_cdef_frame finds them itself then,
+ * EbEncCdef.c:403), and the mse table is zeroed. */
 int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                              const SvtGpuCdefControls *ctrls, int32_t base_q_idx, void *stream);
 
-/* ≙ finish_cdef_search (EbEncCdef.c:728-926) with svt_search_one_dual on the device.
+/* ≙ finish_cdef_search (EbEncCdef.c:728-926) with svt_search_one_dual on the device; with
+ * use_reference_cdef_fs its first branch (:744-789): one strength pair {pred_y_f, pred_uv_f}, index 0 everywhere.
  * lambda = full_lambda of the frame (computed by the encoder's lambda function table).
  * Writes params and the per-FB strength index (int8 per FB, host array of nfb entries) and keeps
  * the per-FB index on the device for svtgpu_cdef_apply_frame.  Synchronous (returns host data). */

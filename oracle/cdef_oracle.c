@@ -260,7 +260,8 @@ int oracle_cdef_controls_for_level(int level, SvtGpuCdefControls *c) {
         {3, 0, 7, 15},                                             /* L6 */
         {3, 0, 7, 15},                                             /* L7 */
         {3, 0, 7, 15},                                             /* L8 */
-        {2, 0, 15},                                                /* L9, L10, L12, L13, L16 */
+        {2, 0, 15},                                                /* L9, L10, L12, L13, L16 (+ L11, L14) */
+        {1, 0},                                                    /* L15, L17 */
     };
     memset(c, 0, sizeof(*c));
     int set, nsec, sec_uv_on, first_uv_on = 1;
@@ -286,7 +287,20 @@ int oracle_cdef_controls_for_level(int level, SvtGpuCdefControls *c) {
         sec_list[0] = 2;
         c->zero_fs_cost_bias = (level >= 12) ? 62 : 0;
         break;
-    default: return SVTGPU_ERR_UNSUPPORTED; /* 0 = off; 11, 14, 15, 17 use reference-frame strengths */
+    case 11: /* use_reference_cdef_fs levels: the controls of :1108-1267, no search at run time */
+    case 14:
+        set = 8, nsec = 1, sec_uv_on = 0, c->subsampling_factor = 4;
+        sec_list[0] = 2;
+        c->zero_fs_cost_bias     = level == 14 ? 62 : 0;
+        c->use_reference_cdef_fs = 1;
+        break;
+    case 15:
+    case 17:
+        set = 9, nsec = 0, sec_uv_on = 0, c->subsampling_factor = 4;
+        c->zero_fs_cost_bias     = 62;
+        c->use_reference_cdef_fs = 1;
+        break;
+    default: return SVTGPU_ERR_UNSUPPORTED; /* 0 = off */
     }
     const int8_t *fs = first_sets[set];
     c->first_pass_fs_num          = (uint8_t)fs[0];
@@ -320,12 +334,12 @@ static Geo geo_of(int32_t w, int32_t h) {
     return g;
 }
 
-/* svt_sb_compute_cdef_list (EbEncCdef.c:238-282) over a per-8x8 mask, SB64 only */
-static int fb_block_list(const Geo *g, const uint8_t *mask, int fbr, int fbc, SvtGpuCdefList *dl) {
-    const int maxr = MIN_(g->mi_rows - 16 * fbr, 16), maxc = MIN_(g->mi_cols - 16 * fbc, 16);
-    int       n = 0;
-    for (int r = 0; r < maxr; r += 2)
-        for (int c = 0; c < maxc; c += 2) {
+/* svt_sb_compute_cdef_list (EbEncCdef.c:238-282) over a per-8x8 mask: the listed 8x8 blocks of the area of
+ * nvb x nhb mi units at filter block (fbr, fbc) (16 x 16 for a 64x64 block, up to 32 for 128-wide SB128 blocks) */
+static int fb_block_list(const Geo *g, const uint8_t *mask, int fbr, int fbc, int nvb, int nhb, SvtGpuCdefList *dl) {
+    int n = 0;
+    for (int r = 0; r < nvb; r += 2)
+        for (int c = 0; c < nhb; c += 2) {
             const int br = 8 * fbr + r / 2, bc = 8 * fbc + c / 2;
             if (!mask || mask[br * g->b8_cols + bc]) {
                 dl[n].by = (uint8_t)(r >> 1);
@@ -349,7 +363,7 @@ static void stage_rect(uint16_t *dst, int dstride, const OracleFrame *f, int pli
 /* cdef_find_dir over the list (EbCdef.c:218-247) + the per-FB driver svt_cdef_filter_fb
  * (EbCdef.c:339-430) for 4:2:0 and the packed (dstride == 0) search output */
 static void filter_fb_packed(void *dst, int is16, const uint16_t *in, int pli, const SvtGpuCdefList *dl, int n,
-                             uint8_t dir[8][8], int32_t var[8][8], int *dirinit, int level, int sec, int damping,
+                             uint8_t dir[16][16], int32_t var[16][16], int *dirinit, int level, int sec, int damping,
                              int cs, int ss) {
     const int xdec = pli ? 1 : 0, ydec = xdec;
     int       pri  = level << cs;
@@ -392,38 +406,55 @@ static void filter_fb_packed(void *dst, int is16, const uint16_t *in, int pli, c
 }
 
 /* ------------------------------------------------------------------------------------------- */
-/* Search — Encoder/Codec/EbCdefProcess.c:114-357 (all segments, SB64)                          */
+/* Search — Encoder/Codec/EbCdefProcess.c:114-357 (all segments).  fb_bsize (NULL = SB64) is the BlockSize of */
+/* the mode info at each filter block's top-left: a 128x128 / 128x64 / 64x128 block is searched as one area   */
+/* (:188-205) whose list and distortion land in its top-left filter block; the other halves are left out of   */
+/* the pick (skip = 1 here).  dir / var are stored per 64x64 filter block, 8x8 blocks row-major.               */
 /* ------------------------------------------------------------------------------------------- */
-int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
-                             const SvtGpuCdefControls *ctrls, int32_t base_q_idx, uint64_t *mse, uint8_t *skip,
-                             uint8_t *dir_out, int32_t *var_out) {
+int oracle_cdef_search_frame_sb(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
+                                const uint8_t *fb_bsize, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                                uint64_t *mse, uint8_t *skip, uint8_t *dir_out, int32_t *var_out) {
     const Geo g      = geo_of(recon->width, recon->height);
     const int nfb    = g.nvfb * g.nhfb;
     const int cs     = recon->bit_depth > 8 ? recon->bit_depth - 8 : 0;
     const int is16   = recon->bit_depth > 8;
     const int damp   = 3 + (base_q_idx >> 6);
-    const int nfirst = ctrls->first_pass_fs_num, nsec = ctrls->default_second_pass_fs_num;
+    /* use_reference_cdef_fs: no strength search (EbCdefProcess.c:400); only the directions the apply needs */
+    const int ref_fs = ctrls->use_reference_cdef_fs;
+    const int nfirst = ref_fs ? 0 : ctrls->first_pass_fs_num, nsec = ref_fs ? 0 : ctrls->default_second_pass_fs_num;
     uint16_t *inbuf  = (uint16_t *)malloc(sizeof(uint16_t) * OR_CDEF_INBUF_SIZE);
     uint16_t *tmp    = (uint16_t *)malloc(sizeof(uint16_t) * 128 * 128);
-    SvtGpuCdefList dl[64];
+    SvtGpuCdefList dl[256];
     uint16_t      *in = inbuf + OR_CDEF_VBORDER * OR_CDEF_BSTRIDE + OR_CDEF_HBORDER;
     for (int fbr = 0; fbr < g.nvfb; fbr++)
         for (int fbc = 0; fbc < g.nhfb; fbc++) {
-            const int fb  = fbr * g.nhfb + fbc;
-            uint8_t   dir[8][8];
-            int32_t   var[8][8];
+            const int fb = fbr * g.nhfb + fbc;
+            const int bs = fb_bsize ? fb_bsize[fb] : 0; /* 13 64X128, 14 128X64, 15 128X128 */
+            uint64_t *m0 = mse + (size_t)fb * 64, *m1 = mse + ((size_t)nfb + fb) * 64;
+            if (((fbc & 1) && (bs == 15 || bs == 14)) || ((fbr & 1) && (bs == 15 || bs == 13))) {
+                skip[fb] = 1; /* a half of a 128-wide area: searched with its top-left block (:193-196) */
+                memset(m0, 0, 64 * sizeof(uint64_t));
+                memset(m1, 0, 64 * sizeof(uint64_t));
+                continue;
+            }
+            const int hb_step = (bs == 15 || bs == 14) ? 2 : 1, vb_step = (bs == 15 || bs == 13) ? 2 : 1;
+            const int nhb = MIN_(16 * hb_step, g.mi_cols - 16 * fbc), nvb = MIN_(16 * vb_step, g.mi_rows - 16 * fbr);
+            uint8_t   dir[16][16];
+            int32_t   var[16][16];
             memset(dir, 0, sizeof(dir));
             memset(var, 0, sizeof(var));
             int       dirinit = 0;
-            const int nhb = MIN_(16, g.mi_cols - 16 * fbc), nvb = MIN_(16, g.mi_rows - 16 * fbr);
-            const int n = fb_block_list(&g, block_mask, fbr, fbc, dl);
-            uint64_t *m0 = mse + (size_t)fb * 64, *m1 = mse + ((size_t)nfb + fb) * 64;
+            const int n = fb_block_list(&g, block_mask, fbr, fbc, nvb, nhb, dl);
             skip[fb] = n == 0;
             if (n == 0) {
                 memset(m0, 0, 64 * sizeof(uint64_t));
                 memset(m1, 0, 64 * sizeof(uint64_t));
-                memset(dir_out + (size_t)fb * 64, 0, 64);
-                memset(var_out + (size_t)fb * 64, 0, 64 * sizeof(int32_t));
+                for (int by = 0; by < nvb / 2; by++) /* every 8x8 block of the area: not listed */
+                    for (int bx = 0; bx < nhb / 2; bx++) {
+                        const int f = (fbr + by / 8) * g.nhfb + fbc + bx / 8, k = (by % 8) * 8 + bx % 8;
+                        dir_out[(size_t)f * 64 + k] = 0;
+                        var_out[(size_t)f * 64 + k] = 0;
+                    }
                 continue;
             }
             for (int pli = 0; pli < 3; pli++) {
@@ -432,13 +463,15 @@ int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, c
                     for (int i = 0; i < OR_CDEF_INBUF_SIZE; i++) inbuf[i] = OR_CDEF_VERY_LARGE;
                 const int yoff  = OR_CDEF_VBORDER * (fbr != 0);
                 const int xoff  = OR_CDEF_HBORDER * (fbc != 0);
-                const int ysize = (nvb << (2 - sub)) + OR_CDEF_VBORDER * (fbr + 1 < g.nvfb) + yoff;
-                const int xsize = (nhb << (2 - sub)) + OR_CDEF_HBORDER * (fbc + 1 < g.nhfb) + xoff;
+                const int ysize = (nvb << (2 - sub)) + OR_CDEF_VBORDER * (fbr + vb_step < g.nvfb) + yoff;
+                const int xsize = (nhb << (2 - sub)) + OR_CDEF_HBORDER * (fbc + hb_step < g.nhfb) + xoff;
                 stage_rect(in - yoff * OR_CDEF_BSTRIDE - xoff, OR_CDEF_BSTRIDE, recon, pli, (16 * fbr << (2 - sub)) - yoff,
                            (16 * fbc << (2 - sub)) - xoff, ysize, xsize);
                 int ss = ctrls->subsampling_factor;
                 ss     = pli ? 1 : MIN_(ss, 4); /* caps of EbCdefProcess.c:254-259 (4:2:0) */
                 const long soff = (long)(16 * fbr << (2 - sub)) * src->stride[pli] + (16 * fbc << (2 - sub));
+                if (ref_fs && pli == 0) /* a throw-away filter pass (any primary strength) finds the block directions */
+                    filter_fb_packed(tmp, is16, in, pli, dl, n, dir, var, &dirinit, 1, 0, damp, cs, ss);
                 for (int gi = 0; gi < nfirst + nsec; gi++) {
                     const int first = gi < nfirst;
                     const int code  = first ? ctrls->default_first_pass_fs[gi] : ctrls->default_second_pass_fs[gi - nfirst];
@@ -451,13 +484,13 @@ int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, c
                     const int pri = code / 4, sec = code % 4;
                     filter_fb_packed(tmp, is16, in, pli, dl, n, dir, var, &dirinit, pri, sec + (sec == 3), damp, cs, ss);
                     uint64_t d;
-                    const int bs = pli ? SVTGPU_BLOCK_4X4 : SVTGPU_BLOCK_8X8;
+                    const int bsz = pli ? SVTGPU_BLOCK_4X4 : SVTGPU_BLOCK_8X8;
                     if (is16)
                         d = oracle_compute_cdef_dist_16bit((const uint16_t *)src->plane[pli] + soff, src->stride[pli], tmp, dl,
-                                                           n, bs, cs, pli, (uint8_t)ss);
+                                                           n, bsz, cs, pli, (uint8_t)ss);
                     else
                         d = oracle_compute_cdef_dist_8bit((const uint8_t *)src->plane[pli] + soff, src->stride[pli],
-                                                          (const uint8_t *)tmp, dl, n, bs, cs, pli, (uint8_t)ss);
+                                                          (const uint8_t *)tmp, dl, n, bsz, cs, pli, (uint8_t)ss);
                     if (pli == 0)
                         m0[gi] = d * ss;
                     else if (pli == 1)
@@ -465,13 +498,29 @@ int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, c
                     else
                         m1[gi] += d * ss;
                 }
+                if (pli == 0 && nfirst + nsec == 0)
+                    memset(m0, 0, 64 * sizeof(uint64_t));
             }
-            memcpy(dir_out + (size_t)fb * 64, dir, 64);
-            memcpy(var_out + (size_t)fb * 64, var, 64 * sizeof(int32_t));
+            if (nfirst + nsec < 64) {
+                memset(m0 + nfirst + nsec, 0, (size_t)(64 - nfirst - nsec) * sizeof(uint64_t));
+                memset(m1 + nfirst + nsec, 0, (size_t)(64 - nfirst - nsec) * sizeof(uint64_t));
+            }
+            for (int by = 0; by < nvb / 2; by++) /* the area's 8x8 blocks into their own filter blocks */
+                for (int bx = 0; bx < nhb / 2; bx++) {
+                    const int f = (fbr + by / 8) * g.nhfb + fbc + bx / 8, k = (by % 8) * 8 + bx % 8;
+                    dir_out[(size_t)f * 64 + k] = dir[by][bx];
+                    var_out[(size_t)f * 64 + k] = var[by][bx];
+                }
         }
     free(inbuf);
     free(tmp);
     return SVTGPU_OK;
+}
+
+int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
+                             const SvtGpuCdefControls *ctrls, int32_t base_q_idx, uint64_t *mse, uint8_t *skip,
+                             uint8_t *dir_out, int32_t *var_out) {
+    return oracle_cdef_search_frame_sb(recon, src, block_mask, NULL, ctrls, base_q_idx, mse, skip, dir_out, var_out);
 }
 
 /* ------------------------------------------------------------------------------------------- */
@@ -483,6 +532,14 @@ int oracle_cdef_pick(int32_t width, int32_t height, const uint64_t *mse_in, cons
     const Geo g   = geo_of(width, height);
     const int nfb = g.nvfb * g.nhfb;
     const int end = ctrls->first_pass_fs_num + ctrls->default_second_pass_fs_num;
+    if (ctrls->use_reference_cdef_fs) { /* EbEncCdef.c:744-789 */
+        memset(params, 0, sizeof(*params));
+        memset(fb_strength, 0, (size_t)nfb);
+        params->cdef_damping        = (uint8_t)(3 + (base_q_idx >> 6));
+        params->cdef_y_strength[0]  = (uint8_t)ctrls->pred_y_f;
+        params->cdef_uv_strength[0] = (uint8_t)ctrls->pred_uv_f;
+        return SVTGPU_OK;
+    }
     uint64_t *mse = (uint64_t *)malloc(sizeof(uint64_t) * 2 * 64 * (size_t)nfb);
     memcpy(mse, mse_in, sizeof(uint64_t) * 2 * 64 * (size_t)nfb);
     uint64_t **rows[2];
@@ -586,14 +643,14 @@ int oracle_cdef_apply_frame(const OracleFrame *recon, OracleFrame *out, const ui
             uvs += uvs == 3;
             if (level == 0 && sec == 0 && uvl == 0 && uvs == 0)
                 continue;
-            const int n = fb_block_list(&g, block_mask, fbr, fbc, dl);
+            const int nhb = MIN_(16, g.mi_cols - 16 * fbc), nvb = MIN_(16, g.mi_rows - 16 * fbr);
+            const int n = fb_block_list(&g, block_mask, fbr, fbc, nvb, nhb, dl);
             if (n == 0)
                 continue;
             uint8_t dir[8][8];
             int32_t var[8][8];
             memcpy(dir, dir_in + (size_t)fb * 64, 64);
             memcpy(var, var_in + (size_t)fb * 64, 64 * sizeof(int32_t));
-            const int nhb = MIN_(16, g.mi_cols - 16 * fbc), nvb = MIN_(16, g.mi_rows - 16 * fbr);
             for (int pli = 0; pli < 3; pli++) {
                 const int sub = pli ? 1 : 0;
                 const int lv = pli ? uvl : level, sv = pli ? uvs : sec;

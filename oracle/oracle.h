@@ -46,6 +46,9 @@ uint64_t oracle_search_one_dual(int *lev0, int *lev1, int nb_strengths, uint64_t
 /* ---- frame level ---- */
 int oracle_cdef_controls_for_level(int cdef_level, SvtGpuCdefControls *c);
 /* mse: [2][nfb][64], skip: [nfb], dir: [nfb][64], var: [nfb][64]; block_mask as in svtgpu.h (NULL=all) */
+int oracle_cdef_search_frame_sb(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
+                                const uint8_t *fb_bsize, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                                uint64_t *mse, uint8_t *skip, uint8_t *dir_out, int32_t *var_out);
 int oracle_cdef_search_frame(const OracleFrame *recon, const OracleFrame *src, const uint8_t *block_mask,
                              const SvtGpuCdefControls *ctrls, int32_t base_q_idx, uint64_t *mse, uint8_t *skip,
                              uint8_t *dir, int32_t *var);

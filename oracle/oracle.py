@@ -37,6 +37,8 @@ _SIGS = {
                                       ctypes.POINTER(ctypes.POINTER(ctypes.POINTER(_U64))), ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int]),
     "oracle_cdef_controls_for_level": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(CdefControls)]),
+    "oracle_cdef_search_frame_sb": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P, _P,
+                                                   ctypes.POINTER(CdefControls), _I32, _P, _P, _P, _P]),
     "oracle_cdef_search_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
                                                 ctypes.POINTER(CdefControls), _I32, _P, _P, _P, _P]),
     "oracle_cdef_pick": (ctypes.c_int, [_I32, _I32, _P, _P, ctypes.POINTER(CdefControls), _I32, _U64,
@@ -120,7 +122,8 @@ def controls(level):
     return c
 
 
-def cdef_search_frame(rec, src, bd, ctrls, base_q_idx, mask=None):
+def cdef_search_frame(rec, src, bd, ctrls, base_q_idx, mask=None, fb_bsize=None):
+    """cdef_seg_search over the frame; fb_bsize (SB128): BlockSize at each filter block's top-left."""
     keep = []
     R, S = _frame(rec, bd, keep), _frame(src, bd, keep)
     h, w = rec[0].shape
@@ -130,8 +133,9 @@ def cdef_search_frame(rec, src, bd, ctrls, base_q_idx, mask=None):
     d = np.zeros((nfb, 64), np.uint8)
     v = np.zeros((nfb, 64), np.int32)
     m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
-    lib().oracle_cdef_search_frame(ctypes.byref(R), ctypes.byref(S), ptr(m), ctypes.byref(ctrls), base_q_idx,
-                                   ptr(mse), ptr(skip), ptr(d), ptr(v))
+    b = None if fb_bsize is None else np.ascontiguousarray(fb_bsize, np.uint8).reshape(-1)
+    lib().oracle_cdef_search_frame_sb(ctypes.byref(R), ctypes.byref(S), ptr(m), ptr(b), ctypes.byref(ctrls),
+                                      base_q_idx, ptr(mse), ptr(skip), ptr(d), ptr(v))
     return mse, skip, d, v
 
 
@@ -335,3 +339,35 @@ def lr_search_frame(rec, src, bd, unit_size, ctrls):
     rc = lib().oracle_lr_search_frame(ctypes.byref(R), ctypes.byref(S), ptr(us), ctypes.byref(ctrls), ptr(ft), up, rp)
     assert rc == 0
     return [int(x) for x in ft], units, recs
+
+
+# ------------------------------------------------------------------------------- CDEF with SB128 mode info
+def cdef_fb_kinds(fb_bsize, nvfb, nhfb):
+    """Per 64x64 FB (row-major): 0 plain, 1 128x128, 2 128x64, 3 64x128 top-left FB of the area, -1 the halves the
+    search skips (EbCdefProcess.c:188-199: BLOCK_64X128 = 13, BLOCK_128X64 = 14, BLOCK_128X128 = 15)."""
+    b = np.asarray(fb_bsize).reshape(nvfb, nhfb).astype(int)
+    r, c = np.mgrid[0:nvfb, 0:nhfb]
+    k = np.where(b == 15, 1, np.where(b == 14, 2, np.where(b == 13, 3, 0)))
+    half = ((c & 1) == 1) & ((b == 15) | (b == 14)) | ((r & 1) == 1) & ((b == 15) | (b == 13))
+    return np.where(half, -1, k).reshape(-1)
+
+
+def _area_parts(f, k, nvfb, nhfb):
+    r, c = divmod(f, nhfb)
+    parts = [f]
+    if k in (1, 2) and c + 1 < nhfb:
+        parts.append(f + 1)
+    if k in (1, 3) and r + 1 < nvfb:
+        parts.append(f + nhfb)
+    if k == 1 and c + 1 < nhfb and r + 1 < nvfb:
+        parts.append(f + nhfb + 1)
+    return parts
+
+
+def cdef_dup_sb128(fbs, kinds, nvfb, nhfb):
+    """finish_cdef_search copies an area's strength index into its halves (EbEncCdef.c:893-909)."""
+    fbs = np.array(fbs, np.int8, copy=True)
+    for f in np.nonzero(kinds > 0)[0]:
+        for p in _area_parts(int(f), int(kinds[f]), nvfb, nhfb)[1:]:
+            fbs[p] = fbs[f]
+    return fbs

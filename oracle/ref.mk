@@ -25,6 +25,10 @@ LR_C     := Lib/Common/Codec/convolve.c Lib/Common/Codec/EbRestoration.c Lib/Com
 MD_C     := Lib/Encoder/C_DEFAULT/EbComputeSAD_C.c Lib/Encoder/C_DEFAULT/variance.c Lib/Encoder/Codec/EbPsnr.c \
             Lib/Encoder/Codec/EbEncInterPrediction.c Lib/Common/C_DEFAULT/EbPictureOperators_C.c \
             Lib/Common/Codec/EbPictureOperators.c
+# frame-level drivers the pipeline generator reaches: get_recon_pic (EbRestProcess.c), the lambda table
+# (EbModeDecisionProcess.c), svt_aom_compute_rd_mult (EbRateControlProcess.c), the quantizer tables (EbInvTransforms.c)
+PIPE_C   := Lib/Encoder/Codec/EbRestProcess.c Lib/Encoder/Codec/EbModeDecisionProcess.c \
+            Lib/Encoder/Codec/EbRateControlProcess.c Lib/Common/Codec/EbInvTransforms.c
 # reference AVX2 sources (the CPU baseline the north star names)
 REF_AVX2 := Lib/Common/ASM_AVX2/cdef_block_avx2.c Lib/Encoder/ASM_AVX2/EbCdef_AVX2.c
 # ... and the rest of the AVX2 / SSE2 kernels an AVX2 host binds for the bench's stages (ref_bench)
@@ -42,8 +46,10 @@ MD_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(MD_C))
 LR_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(LR_C))
 AVX2_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(REF_AVX2))
 SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
+PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
-all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/ref_bench
+all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
+     $(OUT)/ref_bench
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -64,6 +70,12 @@ $(OUT)/gen_golden_md: oracle/ref_harness/gen_golden_md.c $(MD_OBJ) $(C_OBJ)
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm
 
 $(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(sort $(LR_OBJ) $(MD_OBJ) $(C_OBJ))
+	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
+
+# whole-frame DLF -> CDEF -> LR through the reference's own frame-level code; the two harness units compile the
+# reference's EbCdefProcess.c / EncModeConfig.c (static functions) as they lie
+$(OUT)/gen_golden_pipe: oracle/ref_harness/gen_golden_pipe.c oracle/ref_harness/ref_cdef_process.c \
+                        oracle/ref_harness/ref_mode_config.c $(sort $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ))
 	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
 
 # the reference's CPU path on the bench workload (bench.py cpu_baseline, kind "reference")

@@ -22,6 +22,7 @@ extern "C" int svtgpu_cdef_controls_for_level(int level, SvtGpuCdefControls *c) 
         uint16_t    bias;
     };
     Level L{};
+    bool  ref_fs = false; // use_reference_cdef_fs: strengths predicted from the references, no search
     switch (level) {
     case 1: L = {16, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, 3, {1, 2, 3}, true, 1, 0}; break;
     case 2: L = {12, {0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14}, 3, {1, 2, 3}, false, 1, 0}; break;
@@ -36,13 +37,18 @@ extern "C" int svtgpu_cdef_controls_for_level(int level, SvtGpuCdefControls *c) 
     case 12:
     case 13:
     case 16: L = {2, {0, 15}, 1, {2}, false, 4, 62}; break;
-    default: return SVTGPU_ERR_UNSUPPORTED; // 0: off; 11/14/15/17: use_reference_cdef_fs
+    case 11: L = {2, {0, 15}, 1, {2}, false, 4, 0}, ref_fs = true; break;
+    case 14: L = {2, {0, 15}, 1, {2}, false, 4, 62}, ref_fs = true; break;
+    case 15:
+    case 17: L = {1, {0}, 0, {0}, false, 4, 62}, ref_fs = true; break;
+    default: return SVTGPU_ERR_UNSUPPORTED; // 0: CDEF off
     }
     memset(c, 0, sizeof(*c));
     c->first_pass_fs_num          = (uint8_t)L.nfirst;
     c->default_second_pass_fs_num = (uint8_t)(L.nfirst * L.nsec);
     c->subsampling_factor         = L.ss;
     c->zero_fs_cost_bias          = L.bias;
+    c->use_reference_cdef_fs      = ref_fs;
     for (int i = 0, sf = 0; i < L.nfirst; i++) {
         const uint8_t p              = pf_gi[L.first[i]];
         c->default_first_pass_fs[i]    = p;
@@ -56,6 +62,9 @@ extern "C" int svtgpu_cdef_controls_for_level(int level, SvtGpuCdefControls *c) 
 }
 
 static int valid_controls(const SvtGpuCdefControls *c) {
+    if (c->use_reference_cdef_fs)
+        return c->pred_y_f >= 0 && c->pred_uv_f >= 0 && (c->subsampling_factor == 1 || c->subsampling_factor == 2 ||
+                                                         c->subsampling_factor == 4);
     const int n = c->first_pass_fs_num + c->default_second_pass_fs_num;
     if (n <= 0 || n > 64)
         return 0;
@@ -140,7 +149,8 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
 extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     if (!s)
         return;
-    void *bufs[] = {s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip,
+    delete[] s->h_fb_kind;
+    void *bufs[] = {s->d_fb_kind, s->d_mse_rem, s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip,
                     s->own_dir ? s->own_dir : s->d_dir, s->own_var ? (void *)s->own_var : (void *)s->d_var, s->d_fb_strength, s->d_pick_part,
                     s->d_pick_out, s->d_pick_lev, s->d_fb_list};
     for (void *b : bufs)
@@ -199,6 +209,38 @@ extern "C" int svtgpu_cdef_set_block_mask(SvtGpuCdefFrameState *s, const uint8_t
     return SVTGPU_OK;
 }
 
+extern "C" int svtgpu_cdef_set_fb_bsize(SvtGpuCdefFrameState *s, const uint8_t *fb_bsize, void *stream) {
+    if (!s)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (!fb_bsize) {
+        if (s->d_fb_kind) (void)hipFree(s->d_fb_kind);
+        if (s->d_mse_rem) (void)hipFree(s->d_mse_rem);
+        delete[] s->h_fb_kind;
+        s->d_fb_kind = nullptr, s->h_fb_kind = nullptr, s->d_mse_rem = nullptr;
+        return SVTGPU_OK;
+    }
+    if (!s->h_fb_kind) {
+        s->h_fb_kind = new int8_t[s->nfb];
+        HIP_TRY(hipMalloc(&s->d_fb_kind, s->nfb));
+        HIP_TRY(hipMalloc(&s->d_mse_rem, (size_t)3 * s->nfb * 64));
+    }
+    // BLOCK_64X128 = 13, BLOCK_128X64 = 14, BLOCK_128X128 = 15 (EbDefinitions.h); the parity tests of
+    // EbCdefProcess.c:193-196 mark the halves the search skips
+    const int nhfb = s->geo.nhfb;
+    for (int f = 0; f < s->nfb; f++) {
+        const int b = fb_bsize[f], fbr = f / nhfb, fbc = f - fbr * nhfb;
+        int8_t    k = 0;
+        if (((fbc & 1) && (b == 15 || b == 14)) || ((fbr & 1) && (b == 15 || b == 13)))
+            k = -1;
+        else if (b == 15 || b == 14 || b == 13)
+            k = (int8_t)(b == 15 ? 1 : b == 14 ? 2 : 3);
+        s->h_fb_kind[f] = k;
+    }
+    HIP_TRY(hipMemcpyAsync(s->d_fb_kind, s->h_fb_kind, s->nfb, hipMemcpyHostToDevice, pick_stream(s->ctx, stream)));
+    HIP_TRY(hipStreamSynchronize(pick_stream(s->ctx, stream))); // the host array may be reused at once
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                                         const SvtGpuCdefControls *ctrls, int32_t base_q_idx, void *stream) {
     if (!s || !recon || !source || !ctrls || !valid_controls(ctrls))
@@ -209,17 +251,44 @@ extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFra
     if (base_q_idx < 0 || base_q_idx > 255)
         return SVTGPU_ERR_INVALID_ARG;
     CdefStrengthTable tab;
+    hipStream_t       st = pick_stream(s->ctx, stream);
+    if (ctrls->use_reference_cdef_fs) { // directions / variances only: an empty strength table
+        memset(&tab, 0, sizeof(tab));
+        return svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6), st);
+    }
     build_table(ctrls, &tab);
-    return svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6),
-                                     pick_stream(s->ctx, stream));
+    if (int rc = svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6), st))
+        return rc;
+    if (!s->d_fb_kind)
+        return SVTGPU_OK;
+    unsigned long long uv_on = 0;
+    for (int gi = 0; gi < 64; gi++) // entries past the searched strengths are zero sums, like tested ones
+        uv_on |= (unsigned long long)(gi >= tab.nstr || tab.uv_on[gi] != 0) << gi;
+    return svtgpu_launch_cdef_sb128_fold(s, uv_on, recon->bit_depth - 8, ctrls->subsampling_factor, st);
 }
 
 extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                                 uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream) {
     if (!s || !ctrls || !params_out || !valid_controls(ctrls))
         return SVTGPU_ERR_INVALID_ARG;
-    return svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out,
-                                 pick_stream(s->ctx, stream));
+    hipStream_t st = pick_stream(s->ctx, stream);
+    if (ctrls->use_reference_cdef_fs) { // EbEncCdef.c:744-789: index 0 for every filter block, one pair
+        memset(params_out, 0, sizeof(*params_out));
+        params_out->cdef_damping        = (uint8_t)(3 + (base_q_idx >> 6));
+        params_out->cdef_bits           = 0;
+        params_out->cdef_y_strength[0]  = (uint8_t)ctrls->pred_y_f;
+        params_out->cdef_uv_strength[0] = (uint8_t)ctrls->pred_uv_f;
+        HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, s->nfb, st));
+        if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
+        return SVTGPU_OK;
+    }
+    if (int rc = svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, st))
+        return rc;
+    if (s->d_fb_kind) { // the halves of 128-wide areas take the area's index (EbEncCdef.c:893-909)
+        if (int rc = svtgpu_launch_cdef_sb128_dup(s, st)) return rc;
+        if (fb_strength_out) svtgpu_cdef_sb128_dup_host(s, fb_strength_out);
+    }
+    return SVTGPU_OK;
 }
 
 extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream) {

@@ -36,6 +36,7 @@ struct SearchArgs {
     uint8_t       *skip; // [nfb]
     uint8_t       *dir;  // [nfb][64]
     int32_t       *var;  // [nfb][64]
+    uint8_t       *rem;  // [3][nfb][64] low 2*cs bits of the luma / Cb / Cr sums before the shift, or null
     int32_t        nfb, fb0;
     int32_t        cs, ss, damping;
     CdefStrengthTable tab;
@@ -198,6 +199,8 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
         if (tid < 64) {
             A.mse[(size_t)fb * 64 + tid]           = 0;
             A.mse[((size_t)A.nfb + fb) * 64 + tid] = 0;
+            if (A.rem)
+                for (int k = 0; k < 3; k++) A.rem[((size_t)k * A.nfb + fb) * 64 + tid] = 0;
             A.dir[(size_t)fb * 64 + tid]           = 0;
             A.var[(size_t)fb * 64 + tid]           = 0;
         }
@@ -442,6 +445,14 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
         }
         A.mse[(size_t)fb * 64 + gi]           = m0;
         A.mse[((size_t)A.nfb + fb) * 64 + gi] = m1;
+        if (A.rem) { // what the shift drops: a 128-wide SB128 area shifts the sum of its parts (cdef_sb128.hip)
+            const int      src  = gi < nstr && A.tab.alias[gi] >= 0 ? A.tab.alias[gi] : gi;
+            const uint32_t mask = (1u << (2 * cs)) - 1;
+            const bool     on   = gi < nstr;
+            A.rem[(size_t)fb * 64 + gi]                   = on ? (uint8_t)(acc_l[src] & mask) : 0;
+            A.rem[((size_t)A.nfb + fb) * 64 + gi]         = on && A.tab.uv_on[gi] ? (uint8_t)(acc_c[0][src] & mask) : 0;
+            A.rem[((size_t)2 * A.nfb + fb) * 64 + gi]     = on && A.tab.uv_on[gi] ? (uint8_t)(acc_c[1][src] & mask) : 0;
+        }
         if (tid == 0) A.skip[fb] = 0;
     }
 }
@@ -464,6 +475,7 @@ int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon,
     A.skip    = s->d_skip;
     A.dir     = s->d_dir;
     A.var     = s->d_var;
+    A.rem     = s->d_fb_kind ? s->d_mse_rem : nullptr;
     A.nfb     = s->nfb;
     A.fb0     = s->fb_row_begin * s->geo.nhfb;
     A.cs      = recon->bit_depth - 8;

@@ -92,6 +92,9 @@ struct SvtGpuCdefFrameState {
     uint8_t       *own_skip;
     uint8_t       *own_dir;       // state-owned dir/var (d_dir/d_var may point at caller memory)
     int32_t       *own_var;
+    int8_t        *d_fb_kind;     // [nfb] SB128 areas (cdef_sb128.hip); null = SB64
+    int8_t        *h_fb_kind;     // host copy
+    uint8_t       *d_mse_rem;     // [3][nfb][64] remainders of the per-FB distortion shift (SB128 only)
 };
 
 // Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
@@ -118,6 +121,9 @@ struct CdefStrengthTable {
 int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src,
                               const CdefStrengthTable *tab, int32_t subsampling, int32_t damping,
                               hipStream_t st);
+int  svtgpu_launch_cdef_sb128_fold(SvtGpuCdefFrameState *s, unsigned long long uv_on, int cs, int ss, hipStream_t st);
+int  svtgpu_launch_cdef_sb128_dup(SvtGpuCdefFrameState *s, hipStream_t st);
+void svtgpu_cdef_sb128_dup_host(const SvtGpuCdefFrameState *s, int8_t *fbs);
 int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                              const SvtGpuCdefParams *p, hipStream_t st);
 

@@ -34,6 +34,9 @@ class CdefControls(ctypes.Structure):
         ("default_second_pass_fs_uv", ctypes.c_int8 * TOTAL_STRENGTHS),
         ("subsampling_factor", ctypes.c_uint8),
         ("zero_fs_cost_bias", ctypes.c_uint16),
+        ("use_reference_cdef_fs", ctypes.c_int8),
+        ("pred_y_f", ctypes.c_int8),
+        ("pred_uv_f", ctypes.c_int8),
     ]
 
     def strengths(self):
@@ -190,6 +193,7 @@ _SIGS = {
     "svtgpu_cdef_state_destroy": (None, [_P]),
     "svtgpu_cdef_state_nfb": (_I32, [_P]),
     "svtgpu_cdef_set_block_mask": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_cdef_set_fb_bsize": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_cdef_search_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(CdefControls), _I32, _P]),
     "svtgpu_cdef_pick": (ctypes.c_int, [_P, ctypes.POINTER(CdefControls), _I32, _U64, ctypes.POINTER(CdefParams),
                                         _P, _P]),
@@ -378,6 +382,15 @@ class CdefState:
         else:
             self._mask = np.ascontiguousarray(mask, dtype=np.uint8)
             check(lib().svtgpu_cdef_set_block_mask(self.h, ptr(self._mask), stream))
+
+    def set_fb_bsize(self, fb_bsize, stream=None):
+        """SB128 mode info: BlockSize at each 64x64 filter block's top-left (None = SB64)."""
+        if fb_bsize is None:
+            check(lib().svtgpu_cdef_set_fb_bsize(self.h, None, stream))
+        else:
+            self._fbb = np.ascontiguousarray(fb_bsize, dtype=np.uint8)
+            assert self._fbb.size == self.nfb
+            check(lib().svtgpu_cdef_set_fb_bsize(self.h, ptr(self._fbb), stream))
 
     def search(self, recon, source, ctrls, base_q_idx, stream=None):
         check(lib().svtgpu_cdef_search_frame(self.h, recon.h, source.h, ctypes.byref(ctrls), base_q_idx, stream))

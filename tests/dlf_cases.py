@@ -36,8 +36,10 @@ BH = [4, 8, 4, 8, 16, 8, 16, 32, 16, 32, 64, 32, 64, 128, 64, 128, 16, 4, 32, 8,
 _BS = {(w, h): b for b, (w, h) in enumerate(zip(BW, BH))}
 
 
-def random_mode_info(width, height, seed, p_skip=0.5, p_intra=0.3, segments=False, sb=64, min_block=4):
-    """Random partition of each SB into AV1 block shapes with random tx depth / skip / refs / modes."""
+def random_mode_info(width, height, seed, p_skip=0.5, p_intra=0.3, segments=False, sb=64, min_block=4,
+                     rect128=False):
+    """Random partition of each SB into AV1 block shapes with random tx depth / skip / refs / modes.
+    rect128 (sb=128): 128x64 and 64x128 blocks besides 128x128."""
     rng = np.random.default_rng(seed)
     mr, mc = ((height + 7) & ~7) >> 2, ((width + 7) & ~7) >> 2
     mi = np.zeros((mr, mc), LF_MI_DTYPE)
@@ -83,7 +85,12 @@ def random_mode_info(width, height, seed, p_skip=0.5, p_intra=0.3, segments=Fals
 
     for r in range(0, mr, sb // 4):
         for c in range(0, mc, sb // 4):
-            if sb == 128 and rng.random() < 0.3:
+            u = rng.random() if sb == 128 else 1.0
+            if rect128 and 0.2 <= u < 0.3:
+                place(r, c, 128, 64), place(r + 16, c, 128, 64)
+            elif rect128 and 0.3 <= u < 0.4:
+                place(r, c, 64, 128), place(r, c + 16, 64, 128)
+            elif u < (0.2 if rect128 else 0.3):
                 place(r, c, 128, 128)
             else:
                 for k in range(4 if sb == 128 else 1):

@@ -56,9 +56,10 @@ def test_controls_level1_match_encmodeconfig():
     assert c9.first_pass_fs_num == 2 and list(c9.default_first_pass_fs[:2]) == [0, 60]
     assert list(c9.default_second_pass_fs[:2]) == [2, 62] and list(c9.default_second_pass_fs_uv[:2]) == [-1, -1]
     assert c9.subsampling_factor == 4
-    for lvl in (0, 11, 14, 15, 17):
-        with pytest.raises(ValueError):
-            oracle.controls(lvl)
+    with pytest.raises(ValueError):
+        oracle.controls(0)  # CDEF off
+    for lvl in (11, 14, 15, 17):  # use_reference_cdef_fs levels (:1135-1300)
+        assert oracle.controls(lvl).use_reference_cdef_fs == 1
 
 
 # ---------------------------------------------------------------- deblocking (gen_golden_dlf.c)
