@@ -309,6 +309,33 @@ int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *o
 int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source, SvtGpuLfParams *params,
                     int32_t dlf_avg, int32_t dlf_avg_uv, int32_t temporal_layer_index,
                     int32_t early_exit_convergence, int32_t tx_mode_only_4x4, void *stream);
+/* LPF_PICK_FROM_Q: the loop-filter levels from the quantizer, no search (host only, no device work).
+ * ≙ svt_av1_pick_filter_level_by_q (EbDeblockingFilter.c:1036-1125), the path svt_av1_pick_filter_level takes
+ * for method >= LPF_PICK_FROM_Q (:1139-1146; the SB-based DLF levels 3..5).  Inputs are the fields it reads:
+ * the sequence bit depth, base_q_idx, the frame / slice type, the two temporal layer indices it uses
+ * (PictureControlSet's for the zero-strength threshold, the parent's for the reference-off rule), the input
+ * resolution class (ResolutionRange 0..6), DlfCtrls.zero_filter_strength_lvl, the per-64x64 ME distortions
+ * (rc_me_distortion, b64_count of them), and the loop-filter levels {y0, y1, u, v} of each SINGLE reference in
+ * ref_frame_type_arr (compound pairs are skipped by the reference; nref = 0 for none). */
+typedef struct SvtGpuDlfByQ {
+    int32_t         bit_depth;                 /* 8, 10 or 12 */
+    int32_t         base_q_idx;                /* 0..255 */
+    int32_t         frame_type;                /* KEY_FRAME = 0 */
+    int32_t         slice_type;                /* B_SLICE 0, P_SLICE 1, I_SLICE 2 */
+    int32_t         temporal_layer_index;      /* pcs->temporal_layer_index */
+    int32_t         ppcs_temporal_layer_index; /* pcs->ppcs->temporal_layer_index */
+    int32_t         input_resolution;          /* 0..6 */
+    int32_t         zero_filter_strength_lvl;  /* 0..3 */
+    int32_t         b64_count;
+    const uint32_t *me_sad;                    /* b64_count entries */
+    int32_t         nref;                      /* 0..7 */
+    int32_t         ref_levels[7][4];          /* {filter_level[0], filter_level[1], filter_level_u, filter_level_v} */
+} SvtGpuDlfByQ;
+int svtgpu_dlf_pick_by_q(const SvtGpuDlfByQ *in, int32_t filter_level[4]);
+/* ≙ qp_based_dlf_param (EbDeblockingFilter.c:992-1031): luma / chroma level guesses from base_q_idx */
+int svtgpu_dlf_qp_based_param(int32_t bit_depth, int32_t base_q_idx, int32_t frame_type, int32_t *filter_level_y,
+                              int32_t *filter_level_uv);
+
 /* Σ (a - b)^2 over one plane (svt_spatial_full_distortion_kernel / svt_full_distortion_kernel16_bits
  * over the frame, EbDeblockingFilter.c:716-838). Synchronous. */
 int svtgpu_plane_sse(const SvtGpuFrame *a, const SvtGpuFrame *b, int32_t plane, uint64_t *sse, void *stream);

@@ -110,6 +110,37 @@ class LfParams(ctypes.Structure):
         return p
 
 
+class DlfByQ(ctypes.Structure):
+    """SvtGpuDlfByQ: what svt_av1_pick_filter_level_by_q reads (EbDeblockingFilter.c:1036-1125)."""
+    _fields_ = [("bit_depth", ctypes.c_int32), ("base_q_idx", ctypes.c_int32), ("frame_type", ctypes.c_int32),
+                ("slice_type", ctypes.c_int32), ("temporal_layer_index", ctypes.c_int32),
+                ("ppcs_temporal_layer_index", ctypes.c_int32), ("input_resolution", ctypes.c_int32),
+                ("zero_filter_strength_lvl", ctypes.c_int32), ("b64_count", ctypes.c_int32),
+                ("me_sad", ctypes.POINTER(ctypes.c_uint32)), ("nref", ctypes.c_int32),
+                ("ref_levels", (ctypes.c_int32 * 4) * 7)]
+
+
+def dlf_pick_by_q(bit_depth, base_q_idx, frame_type, slice_type, temporal_layer_index, ppcs_temporal_layer_index,
+                  input_resolution, zero_filter_strength_lvl, me_sad, ref_levels):
+    """svtgpu_dlf_pick_by_q (host): LfParams levels (y0, y1, u, v) from the quantizer, no search."""
+    me = np.ascontiguousarray(me_sad, np.uint32)
+    a = DlfByQ(bit_depth, base_q_idx, frame_type, slice_type, temporal_layer_index, ppcs_temporal_layer_index,
+               input_resolution, zero_filter_strength_lvl, len(me), me.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+               len(ref_levels))
+    for i, lv in enumerate(ref_levels):
+        for k in range(4):
+            a.ref_levels[i][k] = int(lv[k])
+    out = (ctypes.c_int32 * 4)()
+    check(lib().svtgpu_dlf_pick_by_q(ctypes.byref(a), out))
+    return tuple(out)
+
+
+def dlf_qp_based_param(bit_depth, base_q_idx, frame_type):
+    y, uv = ctypes.c_int32(), ctypes.c_int32()
+    check(lib().svtgpu_dlf_qp_based_param(bit_depth, base_q_idx, frame_type, ctypes.byref(y), ctypes.byref(uv)))
+    return y.value, uv.value
+
+
 class RestUnit(ctypes.Structure):
     """SvtGpuRestUnit (RestorationUnitInfo, EbRestoration.h:169-188)."""
     _fields_ = [("type", ctypes.c_int32), ("vfilter", ctypes.c_int16 * 8), ("hfilter", ctypes.c_int16 * 8),
@@ -213,6 +244,8 @@ _SIGS = {
     "svtgpu_dlf_frame": (ctypes.c_int, [_P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_frame_to": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_dlf_pick_by_q": (ctypes.c_int, [_P, _P]),
+    "svtgpu_dlf_qp_based_param": (ctypes.c_int, [_I32, _I32, _I32, _P, _P]),
     "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
     **{"svtgpu_aom_sad%dx%d" % s: (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int]) for s in MD_SIZES},
     **{"svtgpu_aom_sad%dx%dx4d" % s: (None, [_P, ctypes.c_int, _P, ctypes.c_int, _P]) for s in MD_SIZES},

@@ -24,7 +24,7 @@ def ctx():
 def test_find_dir_shim_golden(ctx):
     L = svtgpu.lib()
     g = cc.load("cdef_find_dir.bin")
-    for n in range(0, len(g["dir"]), 3):
+    for n in range(len(g["dir"])):
         img = np.ascontiguousarray(g["img"][n])
         var = ctypes.c_int32()
         d = L.svtgpu_cdef_find_dir(ctypes.c_void_p(img.ctypes.data), 8, ctypes.byref(var), int(g["bd"][n]) - 8)
@@ -40,7 +40,7 @@ def test_find_dir_shim_golden(ctx):
 def test_filter_block_shim_golden(ctx):
     L = svtgpu.lib()
     g = cc.load("cdef_filter_block.bin")
-    bad = [n for n in range(0, len(g["out"]), 2)
+    bad = [n for n in range(len(g["out"]))
            if not np.array_equal(cc.run_filter_block(L.svtgpu_cdef_filter_block, g, n), g["out"][n])]
     assert not bad, bad[:10]
 

@@ -35,7 +35,7 @@ def test_lpf_shims_golden(ctx):
     g = cc.load("dlf_lpf.bin")
     meta, inp, out = g["meta"], g["in"], g["out"]
     bad = []
-    for n in range(0, len(meta), 2):
+    for n in range(len(meta)):
         kind, fn, bl, li, th = (int(x) for x in meta[n])
         vertical, length = fn >= 4, (4, 6, 8, 14)[fn & 3]
         lowbd = kind == 8
