@@ -51,6 +51,49 @@ typedef struct SvtGpuCdefList {
     uint8_t bx;
 } SvtGpuCdefList;
 
+/* Layout-identical to the reference's SgrParamsType (EbDefinitions.h:1768-1771): radii and s values of an ep. */
+typedef struct SvtGpuSgrParams {
+    int32_t r[2];
+    int32_t s[2];
+} SvtGpuSgrParams;
+
+/* Layout-identical to the reference's ConvolveParams (EbDefinitions.h:577-590); the Wiener shims read
+ * round_0 / round_1 only. */
+typedef struct SvtGpuConvolveParams {
+    int32_t  ref;
+    int32_t  do_average;
+    void    *dst;
+    int32_t  dst_stride;
+    int32_t  round_0;
+    int32_t  round_1;
+    int32_t  plane;
+    int32_t  is_compound;
+    int32_t  use_jnt_comp_avg;
+    int32_t  fwd_offset;
+    int32_t  bck_offset;
+    int32_t  use_dist_wtd_comp_avg;
+} SvtGpuConvolveParams;
+
+/* Type hooks for a C translation unit compiled against the reference's own headers (INTEGRATION.md §2;
+ * oracle/ref_harness/rtcd_bind.c): defining these to CdefList, BlockSize, SgrParamsType, ConvolveParams and
+ * EbBitDepth before including this header makes the shim prototypes name the reference's types, so every shim
+ * assigns to its RTCD function pointer without a cast.  The layouts are identical, so the ABI is the same. */
+#ifndef SVTGPU_CDEF_LIST_T
+#define SVTGPU_CDEF_LIST_T SvtGpuCdefList
+#endif
+#ifndef SVTGPU_BLOCK_SIZE_T
+#define SVTGPU_BLOCK_SIZE_T int32_t
+#endif
+#ifndef SVTGPU_SGR_PARAMS_T
+#define SVTGPU_SGR_PARAMS_T SvtGpuSgrParams
+#endif
+#ifndef SVTGPU_CONVOLVE_PARAMS_T
+#define SVTGPU_CONVOLVE_PARAMS_T SvtGpuConvolveParams
+#endif
+#ifndef SVTGPU_BIT_DEPTH_T
+#define SVTGPU_BIT_DEPTH_T int32_t
+#endif
+
 /* ---------------------------------------------------------------------------------------------
  * Library / device
  * ------------------------------------------------------------------------------------------- */
@@ -101,14 +144,25 @@ void svtgpu_cdef_filter_block(uint8_t *dst8, uint16_t *dst16, int32_t dstride, c
                               uint8_t subsampling_factor);
 /* replaces svt_compute_cdef_dist_16bit / _8bit (aom_dsp_rtcd.h:62-64); C: EbEncCdef.c:129/175 */
 uint64_t svtgpu_compute_cdef_dist_16bit(const uint16_t *dst, int32_t dstride, const uint16_t *src,
-                                        const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                        const SVTGPU_CDEF_LIST_T *dlist, int32_t cdef_count, SVTGPU_BLOCK_SIZE_T bsize,
                                         int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
 uint64_t svtgpu_compute_cdef_dist_8bit(const uint8_t *dst8, int32_t dstride, const uint8_t *src8,
-                                       const SvtGpuCdefList *dlist, int32_t cdef_count, int32_t bsize,
+                                       const SVTGPU_CDEF_LIST_T *dlist, int32_t cdef_count, SVTGPU_BLOCK_SIZE_T bsize,
                                        int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
 /* replaces svt_search_one_dual (aom_dsp_rtcd.h:239); C: EbEncCdef.c:627 */
 uint64_t svtgpu_search_one_dual(int *lev0, int *lev1, int nb_strengths, uint64_t **mse[2], int sb_count,
                                 int start_gi, int end_gi);
+/* replaces svt_cdef_filter_block_8xn_16 (common_dsp_rtcd.h:1100; AVX2 only in the reference,
+ * cdef_block_avx2.c:463): an 8-wide luma block, rows 0, s, 2s, ... (s = subsampling_factor) of `height`, into a
+ * uint16 dst; `in` points into a CDEF_BSTRIDE(=144)-stride buffer, pri_strength already adjusted */
+void svtgpu_cdef_filter_block_8xn_16(const uint16_t *const in, const int32_t pri_strength, const int32_t sec_strength,
+                                     const int32_t dir, int32_t pri_damping, int32_t sec_damping,
+                                     const int32_t coeff_shift, uint16_t *const dst, const int32_t dstride,
+                                     uint8_t height, uint8_t subsampling_factor);
+/* replaces svt_aom_copy_rect8_8bit_to_16bit (common_dsp_rtcd.h:1105; C EbCdef.c:303): the 8-bit -> 16-bit
+ * staging copy of the CDEF input buffer, v rows x h columns */
+void svtgpu_aom_copy_rect8_8bit_to_16bit(uint16_t *dst, int32_t dstride, const uint8_t *src, int32_t sstride, int32_t v,
+                                         int32_t h);
 
 /* ---------------------------------------------------------------------------------------------
  * CDEF — frame level (device-resident)
@@ -452,6 +506,45 @@ uint64_t svtgpu_spatial_full_distortion_kernel(uint8_t *input, uint32_t input_of
 uint64_t svtgpu_full_distortion_kernel16_bits(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
                                               uint8_t *recon, int32_t recon_offset, uint32_t recon_stride,
                                               uint32_t area_width, uint32_t area_height);
+/* ≙ svt_nxm_sad_kernel / svt_nxm_sad_kernel_sub_sampled (aom_dsp_rtcd.h:853-854): the MD fast-loop N x M SAD
+ * (C svt_fast_loop_nxm_sad_kernel, EbComputeSAD_C.c:20; the C "sub-sampled" entry is the full SAD too, :209) */
+uint32_t svtgpu_nxm_sad_kernel(const uint8_t *src, uint32_t src_stride, const uint8_t *ref, uint32_t ref_stride,
+                               uint32_t height, uint32_t width);
+uint32_t svtgpu_nxm_sad_kernel_sub_sampled(const uint8_t *src, uint32_t src_stride, const uint8_t *ref,
+                                           uint32_t ref_stride, uint32_t height, uint32_t width);
+/* ≙ svt_aom_mse16x16 (aom_dsp_rtcd.h:241, C EbPsnr.c:76) and svt_aom_highbd_8_mse16x16 (:262, C variance.c:453;
+ * 16-bit samples CONVERT_TO_BYTEPTR-encoded, *sse only) */
+uint32_t svtgpu_aom_mse16x16(const uint8_t *src_ptr, int32_t source_stride, const uint8_t *ref_ptr,
+                             int32_t recon_stride, uint32_t *sse);
+void     svtgpu_aom_highbd_8_mse16x16(const uint8_t *src_ptr, int32_t source_stride, const uint8_t *ref_ptr,
+                                      int32_t recon_stride, uint32_t *sse);
+/* ≙ variance_highbd (aom_dsp_rtcd.h:867, C svt_aom_variance_highbd_c variance.c:278): any w x h, 16-bit */
+uint32_t svtgpu_aom_variance_highbd(const uint16_t *a, int a_stride, const uint16_t *b, int b_stride, int w, int h,
+                                    uint32_t *sse);
+/* ≙ svt_aom_sub_pixel_variance{W}x{H} (aom_dsp_rtcd.h:587-753, C SUBPIX_VAR variance.c:308): 2-tap bilinear
+ * (1/8 pel offsets xoffset, yoffset in 0..7) of a (H + 1) x (W + 1) source window, then the W x H variance */
+uint32_t svtgpu_aom_sub_pixel_variance4x4(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance4x8(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance8x4(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance8x8(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance8x16(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance16x8(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance16x16(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance16x32(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance32x16(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance32x32(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance32x64(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance64x32(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance64x64(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance64x128(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance128x64(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance128x128(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance4x16(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance16x4(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance8x32(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance32x8(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance16x64(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
+uint32_t svtgpu_aom_sub_pixel_variance64x16(const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset, const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);
 
 /* Batched MD distortion (the frame-level GPU boundary; no single reference equivalent: it evaluates what
  * the MD candidate loops evaluate block by block through svt_aom_mefn_ptr, av1me.c:29-174).
@@ -480,21 +573,18 @@ void    svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offs
 /* =========================================================================================
  * Loop restoration
  * ========================================================================================= */
-/* RTCD-compatible per-block shims (common_dsp_rtcd.h:174-185).  SvtGpuConvolveParams mirrors the fields
- * of ConvolveParams the Wiener convolve reads (round_0, round_1); 16-bit planes are passed
- * CONVERT_TO_BYTEPTR-encoded (EbDefinitions.h:950-951), as in the reference. */
-typedef struct SvtGpuConvolveParams {
-    int32_t round_0, round_1;
-} SvtGpuConvolveParams;
+/* RTCD-compatible per-block shims (common_dsp_rtcd.h:174-185).  The Wiener convolve reads round_0 / round_1 of
+ * the ConvolveParams (full layout at the top of this header); 16-bit planes are passed CONVERT_TO_BYTEPTR-encoded
+ * (EbDefinitions.h:950-951), as in the reference. */
 /* ≙ svt_av1_wiener_convolve_add_src (C convolve.c:109-151): 8-tap separable, src row/col -3..+4 */
 void svtgpu_av1_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst, ptrdiff_t dst_stride,
                                         const int16_t *filter_x, const int16_t *filter_y, int32_t w, int32_t h,
-                                        const SvtGpuConvolveParams *conv_params);
+                                        const SVTGPU_CONVOLVE_PARAMS_T *conv_params);
 /* ≙ svt_av1_highbd_wiener_convolve_add_src (C convolve.c:194-232) */
 void svtgpu_av1_highbd_wiener_convolve_add_src(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst,
                                                ptrdiff_t dst_stride, const int16_t *filter_x,
                                                const int16_t *filter_y, int32_t w, int32_t h,
-                                               const SvtGpuConvolveParams *conv_params, int32_t bd);
+                                               const SVTGPU_CONVOLVE_PARAMS_T *conv_params, int32_t bd);
 /* ≙ svt_av1_selfguided_restoration (C EbRestoration.c:923-955): flt0/flt1 of one processing unit, input read
  * with a 3-sample border */
 void svtgpu_av1_selfguided_restoration(const uint8_t *dgd8, int32_t width, int32_t height, int32_t dgd_stride,
@@ -504,6 +594,27 @@ void svtgpu_av1_selfguided_restoration(const uint8_t *dgd8, int32_t width, int32
 void svtgpu_apply_selfguided_restoration(const uint8_t *dat8, int32_t width, int32_t height, int32_t stride,
                                          int32_t eps, const int32_t *xqd, uint8_t *dst8, int32_t dst_stride,
                                          int32_t *tmpbuf, int32_t bit_depth, int32_t highbd);
+/* ≙ svt_av1_compute_stats / _highbd (aom_dsp_rtcd.h:66-68, C EbRestorationPick.c:671 / :708): the Wiener
+ * statistics M[win^2] and H[win^2][win^2] of a unit; dgd read with a win/2 border */
+void svtgpu_av1_compute_stats(int32_t wiener_win, const uint8_t *dgd8, const uint8_t *src8, int32_t h_start,
+                              int32_t h_end, int32_t v_start, int32_t v_end, int32_t dgd_stride, int32_t src_stride,
+                              int64_t *M, int64_t *H);
+void svtgpu_av1_compute_stats_highbd(int32_t wiener_win, const uint8_t *dgd8, const uint8_t *src8, int32_t h_start,
+                                     int32_t h_end, int32_t v_start, int32_t v_end, int32_t dgd_stride,
+                                     int32_t src_stride, int64_t *M, int64_t *H, SVTGPU_BIT_DEPTH_T bit_depth);
+/* ≙ svt_av1_lowbd_pixel_proj_error / svt_av1_highbd_pixel_proj_error (aom_dsp_rtcd.h:79-81, C :167 / :232) */
+int64_t svtgpu_av1_lowbd_pixel_proj_error(const uint8_t *src8, int32_t width, int32_t height, int32_t src_stride,
+                                          const uint8_t *dat8, int32_t dat_stride, int32_t *flt0, int32_t flt0_stride,
+                                          int32_t *flt1, int32_t flt1_stride, int32_t xq[2],
+                                          const SVTGPU_SGR_PARAMS_T *params);
+int64_t svtgpu_av1_highbd_pixel_proj_error(const uint8_t *src8, int32_t width, int32_t height, int32_t src_stride,
+                                           const uint8_t *dat8, int32_t dat_stride, int32_t *flt0, int32_t flt0_stride,
+                                           int32_t *flt1, int32_t flt1_stride, int32_t xq[2],
+                                           const SVTGPU_SGR_PARAMS_T *params);
+/* ≙ svt_get_proj_subspace (aom_dsp_rtcd.h:212, C EbRestorationPick.c:560): least-squares xq of a unit */
+void svtgpu_get_proj_subspace(const uint8_t *src8, int width, int height, int src_stride, const uint8_t *dat8,
+                              int dat_stride, int use_highbitdepth, int32_t *flt0, int flt0_stride, int32_t *flt1,
+                              int flt1_stride, int *xq, const SVTGPU_SGR_PARAMS_T *params);
 
 /* Per restoration unit parameters (RestorationUnitInfo, EbRestoration.h:169-188). */
 #define SVTGPU_RESTORE_NONE 0

@@ -49,7 +49,7 @@ SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
 PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
-     $(OUT)/ref_bench
+     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -76,6 +76,21 @@ $(OUT)/gen_golden_lr: oracle/ref_harness/gen_golden_lr.c $(sort $(LR_OBJ) $(MD_O
 # reference's EbCdefProcess.c / EncModeConfig.c (static functions) as they lie
 $(OUT)/gen_golden_pipe: oracle/ref_harness/gen_golden_pipe.c oracle/ref_harness/ref_cdef_process.c \
                         oracle/ref_harness/ref_mode_config.c $(sort $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ))
+	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
+
+# the same frame code with the reference's RTCD pointers bound to libsvtgpu's shims (no casts: the compile fails on
+# any prototype mismatch); run on the GPU box by tests/test_rtcd_bind.py
+SVTGPU_SO := svt-av1_pro-anchor-v2.1.0-_amd/lib/libsvtgpu.so
+$(OUT)/rtcd_pipe: oracle/ref_harness/gen_golden_pipe.c oracle/ref_harness/ref_cdef_process.c \
+                  oracle/ref_harness/ref_mode_config.c $(sort $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ)) $(SVTGPU_SO)
+	@mkdir -p $(OUT)/obj/bind
+	$(CC) $(filter-out -w,$(CFLAGS)) -DSVTGPU_BIND -Iinclude -Werror=incompatible-pointer-types \
+	    -c oracle/ref_harness/gen_golden_pipe.c -o $(OUT)/obj/bind/gen_golden_pipe.o
+	$(CC) $(CFLAGS) $(OUT)/obj/bind/gen_golden_pipe.o $(filter-out %gen_golden_pipe.c,$(filter %.c,$^)) $(filter %.o,$^) \
+	    -o $@ -Wl,--gc-sections -L$(dir $(SVTGPU_SO)) -lsvtgpu -Wl,-rpath,'$$ORIGIN/../../$(dir $(SVTGPU_SO))' -lm -lpthread
+
+# the round-2 RTCD shims (C, and the AVX2-only svt_cdef_filter_block_8xn_16)
+$(OUT)/gen_golden_shims: oracle/ref_harness/gen_golden_shims.c $(sort $(LR_OBJ) $(MD_OBJ) $(C_OBJ)) $(AVX2_OBJ)
 	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread
 
 # the reference's CPU path on the bench workload (bench.py cpu_baseline, kind "reference")

@@ -95,6 +95,57 @@ static void bind_c_kernels(void) {
     svt_aom_highbd_8_mse16x16              = svt_aom_highbd_8_mse16x16_c;
 }
 
+#ifdef SVTGPU_BIND
+/* rtcd_pipe: the same frame code with every RTCD pointer the path calls bound to libsvtgpu's device shims.  The
+ * shim prototypes name the reference's own types (the type hooks of include/svtgpu.h), so every assignment below
+ * compiles under -Werror=incompatible-pointer-types without a cast. */
+#define SVTGPU_CDEF_LIST_T CdefList
+#define SVTGPU_BLOCK_SIZE_T BlockSize
+#define SVTGPU_SGR_PARAMS_T SgrParamsType
+#define SVTGPU_CONVOLVE_PARAMS_T ConvolveParams
+#define SVTGPU_BIT_DEPTH_T EbBitDepth
+#include "svtgpu.h"
+static void bind_device_kernels(void) {
+    svt_aom_lpf_horizontal_4               = svtgpu_lpf_horizontal_4;
+    svt_aom_lpf_horizontal_6               = svtgpu_lpf_horizontal_6;
+    svt_aom_lpf_horizontal_8               = svtgpu_lpf_horizontal_8;
+    svt_aom_lpf_horizontal_14              = svtgpu_lpf_horizontal_14;
+    svt_aom_lpf_vertical_4                 = svtgpu_lpf_vertical_4;
+    svt_aom_lpf_vertical_6                 = svtgpu_lpf_vertical_6;
+    svt_aom_lpf_vertical_8                 = svtgpu_lpf_vertical_8;
+    svt_aom_lpf_vertical_14                = svtgpu_lpf_vertical_14;
+    svt_aom_highbd_lpf_horizontal_4        = svtgpu_highbd_lpf_horizontal_4;
+    svt_aom_highbd_lpf_horizontal_6        = svtgpu_highbd_lpf_horizontal_6;
+    svt_aom_highbd_lpf_horizontal_8        = svtgpu_highbd_lpf_horizontal_8;
+    svt_aom_highbd_lpf_horizontal_14       = svtgpu_highbd_lpf_horizontal_14;
+    svt_aom_highbd_lpf_vertical_4          = svtgpu_highbd_lpf_vertical_4;
+    svt_aom_highbd_lpf_vertical_6          = svtgpu_highbd_lpf_vertical_6;
+    svt_aom_highbd_lpf_vertical_8          = svtgpu_highbd_lpf_vertical_8;
+    svt_aom_highbd_lpf_vertical_14         = svtgpu_highbd_lpf_vertical_14;
+    svt_spatial_full_distortion_kernel     = svtgpu_spatial_full_distortion_kernel;
+    svt_full_distortion_kernel16_bits      = svtgpu_full_distortion_kernel16_bits;
+    svt_cdef_filter_block                  = svtgpu_cdef_filter_block;
+    svt_cdef_filter_block_8xn_16           = svtgpu_cdef_filter_block_8xn_16;
+    svt_aom_cdef_find_dir                  = svtgpu_cdef_find_dir;
+    svt_aom_cdef_find_dir_dual             = svtgpu_cdef_find_dir_dual;
+    svt_compute_cdef_dist_16bit            = svtgpu_compute_cdef_dist_16bit;
+    svt_compute_cdef_dist_8bit             = svtgpu_compute_cdef_dist_8bit;
+    svt_search_one_dual                    = svtgpu_search_one_dual;
+    svt_aom_copy_rect8_8bit_to_16bit       = svtgpu_aom_copy_rect8_8bit_to_16bit;
+    svt_av1_wiener_convolve_add_src        = svtgpu_av1_wiener_convolve_add_src;
+    svt_av1_highbd_wiener_convolve_add_src = svtgpu_av1_highbd_wiener_convolve_add_src;
+    svt_av1_selfguided_restoration         = svtgpu_av1_selfguided_restoration;
+    svt_apply_selfguided_restoration       = svtgpu_apply_selfguided_restoration;
+    svt_av1_compute_stats                  = svtgpu_av1_compute_stats;
+    svt_av1_compute_stats_highbd           = svtgpu_av1_compute_stats_highbd;
+    svt_get_proj_subspace                  = svtgpu_get_proj_subspace;
+    svt_av1_lowbd_pixel_proj_error         = svtgpu_av1_lowbd_pixel_proj_error;
+    svt_av1_highbd_pixel_proj_error        = svtgpu_av1_highbd_pixel_proj_error;
+    svt_aom_mse16x16                       = svtgpu_aom_mse16x16;
+    svt_aom_highbd_8_mse16x16              = svtgpu_aom_highbd_8_mse16x16;
+}
+#endif
+
 /* input header (int32), written by tests/pipeline_cases.py:write_input */
 enum {
     I_MAGIC, I_W, I_H, I_BD, I_Q, I_CDEF_LVL, I_DLF_LVL, I_WN_LVL, I_SG_LVL, I_LF0, I_LF1, I_LFU, I_LFV, I_SHARP,
@@ -610,6 +661,13 @@ static int run_ctrls(const char *out_path) {
 
 int main(int argc, char **argv) {
     bind_c_kernels();
+#ifdef SVTGPU_BIND
+    if (!svtgpu_device_available()) {
+        fprintf(stderr, "rtcd_pipe: no gfx950 device\n");
+        return 3;
+    }
+    bind_device_kernels();
+#endif
     if (argc == 4 && !strcmp(argv[1], "pipe")) return run_pipe(argv[2], argv[3]);
     if (argc == 3 && !strcmp(argv[1], "byq")) return run_byq(argv[2]);
     if (argc == 3 && !strcmp(argv[1], "ctrls")) return run_ctrls(argv[2]);

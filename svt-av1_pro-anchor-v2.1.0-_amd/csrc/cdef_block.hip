@@ -232,6 +232,55 @@ extern "C" uint64_t svtgpu_compute_cdef_dist_8bit(const uint8_t *dst8, int32_t d
     return cdef_dist_host<uint8_t>(dst8, dstride, src8, dlist, cdef_count, bsize, coeff_shift, pli, subsampling_factor);
 }
 
+// svt_cdef_filter_block_8xn_16 (AVX2 only in the reference, cdef_block_avx2.c:463-548): rows 0, s, 2s, ... of an
+// 8-wide block in steps of two rows (i and i + s per 2s), the same per-sample filter as svt_cdef_filter_block_c
+extern "C" void svtgpu_cdef_filter_block_8xn_16(const uint16_t *const in, const int32_t pri_strength,
+                                                const int32_t sec_strength, const int32_t dir, int32_t pri_damping,
+                                                int32_t sec_damping, const int32_t coeff_shift, uint16_t *const dst,
+                                                const int32_t dstride, uint8_t height, uint8_t subsampling_factor) {
+    const int ss = subsampling_factor ? subsampling_factor : 1;
+    const int bh = (height + 2 * ss - 1) / (2 * ss) * (2 * ss); // the AVX2 loop writes row pairs
+    if (bh * 8 > 1024) return;
+    const int ws = 8 + 2 * CDEF_BORDER, wh = bh + 2 * CDEF_BORDER;
+    std::vector<uint16_t> win((size_t)ws * wh);
+    for (int r = 0; r < wh; r++)
+        memcpy(&win[(size_t)r * ws], in + (long)(r - CDEF_BORDER) * 144 - CDEF_BORDER, (size_t)ws * 2);
+    hipStream_t st   = svtgpu_default_stream();
+    char       *d    = (char *)g_scratch.get(win.size() * 2 + 2 * 1024 + 256);
+    uint16_t   *dout = (uint16_t *)(d + ((win.size() * 2 + 15) & ~(size_t)15));
+    HIP_OR_DIE(hipMemcpyAsync(d, win.data(), win.size() * 2, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(cdef_filter_block_kernel, dim3(1), dim3(bh * 8), 0, st, (const uint16_t *)d, ws, bh, 8,
+                       pri_strength, sec_strength, dir, pri_damping, sec_damping, coeff_shift, ss, dout);
+    HIP_OR_DIE(hipGetLastError());
+    std::vector<uint16_t> out((size_t)bh * 8);
+    HIP_OR_DIE(hipMemcpyAsync(out.data(), dout, out.size() * 2, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int i = 0; i < bh; i += ss) memcpy(dst + (long)i * dstride, &out[(size_t)i * 8], 16);
+}
+
+// svt_aom_copy_rect8_8bit_to_16bit_c (EbCdef.c:303-311): widen a v x h block of 8-bit samples
+__global__ void copy_rect8_kernel(uint16_t *dst, const uint8_t *src, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+extern "C" void svtgpu_aom_copy_rect8_8bit_to_16bit(uint16_t *dst, int32_t dstride, const uint8_t *src, int32_t sstride,
+                                                    int32_t v, int32_t h) {
+    if (v <= 0 || h <= 0) return;
+    std::vector<uint8_t> hs((size_t)v * h);
+    for (int r = 0; r < v; r++) memcpy(&hs[(size_t)r * h], src + (long)r * sstride, (size_t)h);
+    hipStream_t st = svtgpu_default_stream();
+    char       *d  = (char *)g_scratch.get(hs.size() * 3 + 64);
+    uint16_t   *d16 = (uint16_t *)(d + ((hs.size() + 15) & ~(size_t)15));
+    HIP_OR_DIE(hipMemcpyAsync(d, hs.data(), hs.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(copy_rect8_kernel, dim3((unsigned)((hs.size() + 255) / 256)), dim3(256), 0, st, d16,
+                       (const uint8_t *)d, (int)hs.size());
+    HIP_OR_DIE(hipGetLastError());
+    std::vector<uint16_t> out(hs.size());
+    HIP_OR_DIE(hipMemcpyAsync(out.data(), d16, out.size() * 2, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    for (int r = 0; r < v; r++) memcpy(dst + (long)r * dstride, &out[(size_t)r * h], (size_t)h * 2);
+}
+
 // ---------------------------------------------------------------------------------------------
 // svt_search_one_dual_c (EbEncCdef.c:627-695): one lane per (j, k) pair + argmin workgroup
 // ---------------------------------------------------------------------------------------------

@@ -311,6 +311,127 @@ extern "C" uint64_t svtgpu_full_distortion_kernel16_bits(uint8_t *input, uint32_
     return s.sse;
 }
 
+// svt_nxm_sad_kernel / svt_nxm_sad_kernel_sub_sampled (aom_dsp_rtcd.h:853-854): the C versions of both are the
+// full N x M SAD (svt_fast_loop_nxm_sad_kernel, EbComputeSAD_C.c:20-37; svt_nxm_sad_kernel_helper_c, :209-212)
+extern "C" uint32_t svtgpu_nxm_sad_kernel(const uint8_t *src, uint32_t src_stride, const uint8_t *ref,
+                                          uint32_t ref_stride, uint32_t height, uint32_t width) {
+    Stats s;
+    block_stats<uint8_t>(src, (int)src_stride, &ref, (int)ref_stride, 1, (int)width, (int)height, &s);
+    return (uint32_t)s.sad;
+}
+extern "C" uint32_t svtgpu_nxm_sad_kernel_sub_sampled(const uint8_t *src, uint32_t src_stride, const uint8_t *ref,
+                                                      uint32_t ref_stride, uint32_t height, uint32_t width) {
+    return svtgpu_nxm_sad_kernel(src, src_stride, ref, ref_stride, height, width);
+}
+// svt_aom_mse16x16_c (EbPsnr.c:76-81): sse - sum^2 / 256, *sse = sse
+extern "C" uint32_t svtgpu_aom_mse16x16(const uint8_t *src_ptr, int32_t source_stride, const uint8_t *ref_ptr,
+                                        int32_t recon_stride, uint32_t *sse) {
+    Stats s;
+    block_stats<uint8_t>(src_ptr, source_stride, &ref_ptr, recon_stride, 1, 16, 16, &s);
+    return var8(s, 256, sse);
+}
+// svt_aom_highbd_8_mse16x16_c (variance.c:453-467): *sse = (uint32) sum of squared differences, 16-bit samples
+extern "C" void svtgpu_aom_highbd_8_mse16x16(const uint8_t *src_ptr, int32_t source_stride, const uint8_t *ref_ptr,
+                                             int32_t recon_stride, uint32_t *sse) {
+    Stats           s;
+    const uint16_t *r = short_ptr(ref_ptr);
+    block_stats<uint16_t>(short_ptr(src_ptr), source_stride, &r, recon_stride, 1, 16, 16, &s);
+    *sse = (uint32_t)s.sse;
+}
+// svt_aom_variance_highbd_c (variance.c:278-296): uint32 sse, int sum, sse - sum^2 / (w*h)
+extern "C" uint32_t svtgpu_aom_variance_highbd(const uint16_t *a, int a_stride, const uint16_t *b, int b_stride, int w,
+                                               int h, uint32_t *sse) {
+    Stats s;
+    block_stats<uint16_t>(a, a_stride, &b, b_stride, 1, w, h, &s);
+    *sse = (uint32_t)s.sse;
+    return (uint32_t)((int64_t)*sse - (s.sum * s.sum) / (w * h));
+}
+
+// ---------------------------------------------------------------------------------------------
+// svt_aom_sub_pixel_variance{W}x{H}_c (variance.c:308-318): 2-tap bilinear first pass over H+1 rows (u16),
+// second pass (u8), then the W x H variance against b.  bilinear_filters_2t[k] = {128 - 16k, 16k}, FILTER_BITS 7.
+// One workgroup: the filtered block lives in LDS; the statistics reduce in the workgroup.
+// ---------------------------------------------------------------------------------------------
+namespace {
+__global__ __launch_bounds__(256) void subpel_var_kernel(const uint8_t *a, int as, const uint8_t *b, int w, int h,
+                                                         int xoff, int yoff, unsigned long long *out) {
+    __shared__ uint16_t f1[129 * 128];
+    __shared__ long long red[2][4];
+    const int fx0 = 128 - 16 * xoff, fx1 = 16 * xoff, fy0 = 128 - 16 * yoff, fy1 = 16 * yoff;
+    for (int i = threadIdx.x; i < (h + 1) * w; i += 256) {
+        const int r = i / w, c = i - r * w;
+        f1[i] = (uint16_t)(((int)a[r * as + c] * fx0 + (int)a[r * as + c + 1] * fx1 + 64) >> 7);
+    }
+    __syncthreads();
+    unsigned long long sse = 0;
+    long long          sum = 0;
+    for (int i = threadIdx.x; i < h * w; i += 256) {
+        const int v = ((int)f1[i] * fy0 + (int)f1[i + w] * fy1 + 64) >> 7;
+        const int d = (int)(uint8_t)v - (int)b[i];
+        sse += (unsigned long long)(d * d);
+        sum += d;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sse += __shfl_down(sse, o, 64);
+        sum += __shfl_down(sum, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = (long long)sse, red[1][threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x < 2) out[threadIdx.x] = (unsigned long long)(red[threadIdx.x][0] + red[threadIdx.x][1] +
+                                                                 red[threadIdx.x][2] + red[threadIdx.x][3]);
+}
+
+uint32_t subpel_var(const uint8_t *a, int a_stride, int xoff, int yoff, const uint8_t *b, int b_stride, int w, int h,
+                    uint32_t *sse) {
+    // the first pass reads (h + 1) rows and w + 1 columns of a (the second tap multiplies by 0 at offset 0)
+    std::vector<uint8_t> ha((size_t)(h + 1) * (w + 1)), hb((size_t)h * w);
+    for (int r = 0; r <= h; r++) memcpy(&ha[(size_t)r * (w + 1)], a + (long)r * a_stride, (size_t)w + 1);
+    for (int r = 0; r < h; r++) memcpy(&hb[(size_t)r * w], b + (long)r * b_stride, (size_t)w);
+    hipStream_t st = svtgpu_default_stream();
+    static thread_local uint8_t *d = nullptr;
+    if (!d) HIP_OR_DIE(hipMalloc(&d, 129 * 129 + 128 * 128 + 64));
+    unsigned long long *dr = (unsigned long long *)(d + 129 * 129 + 128 * 128 + 16);
+    HIP_OR_DIE(hipMemcpyAsync(d, ha.data(), ha.size(), hipMemcpyHostToDevice, st));
+    HIP_OR_DIE(hipMemcpyAsync(d + 129 * 129, hb.data(), hb.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(subpel_var_kernel, dim3(1), dim3(256), 0, st, d, w + 1, d + 129 * 129, w, h, xoff & 7, yoff & 7, dr);
+    HIP_OR_DIE(hipGetLastError());
+    unsigned long long r[2];
+    HIP_OR_DIE(hipMemcpyAsync(r, dr, sizeof r, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    *sse = (uint32_t)r[0];
+    return *sse - (uint32_t)(((int64_t)r[1] * (int64_t)r[1]) / (w * h));
+}
+} // namespace
+
+#define SUBPEL_VAR_SHIM(W, H)                                                                                      \
+    extern "C" uint32_t svtgpu_aom_sub_pixel_variance##W##x##H(const uint8_t *src_ptr, int source_stride,          \
+                                                               int xoffset, int yoffset, const uint8_t *ref_ptr,   \
+                                                               int ref_stride, uint32_t *sse) {                    \
+        return subpel_var(src_ptr, source_stride, xoffset, yoffset, ref_ptr, ref_stride, W, H, sse);             \
+    }
+SUBPEL_VAR_SHIM(4, 4)
+SUBPEL_VAR_SHIM(4, 8)
+SUBPEL_VAR_SHIM(8, 4)
+SUBPEL_VAR_SHIM(8, 8)
+SUBPEL_VAR_SHIM(8, 16)
+SUBPEL_VAR_SHIM(16, 8)
+SUBPEL_VAR_SHIM(16, 16)
+SUBPEL_VAR_SHIM(16, 32)
+SUBPEL_VAR_SHIM(32, 16)
+SUBPEL_VAR_SHIM(32, 32)
+SUBPEL_VAR_SHIM(32, 64)
+SUBPEL_VAR_SHIM(64, 32)
+SUBPEL_VAR_SHIM(64, 64)
+SUBPEL_VAR_SHIM(64, 128)
+SUBPEL_VAR_SHIM(128, 64)
+SUBPEL_VAR_SHIM(128, 128)
+SUBPEL_VAR_SHIM(4, 16)
+SUBPEL_VAR_SHIM(16, 4)
+SUBPEL_VAR_SHIM(8, 32)
+SUBPEL_VAR_SHIM(32, 8)
+SUBPEL_VAR_SHIM(16, 64)
+SUBPEL_VAR_SHIM(64, 16)
+
 // ---------------------------------------------------------------------------------------------
 // batch object
 // ---------------------------------------------------------------------------------------------

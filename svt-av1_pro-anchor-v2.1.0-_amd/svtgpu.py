@@ -181,7 +181,17 @@ LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYP
 
 
 class ConvolveParams(ctypes.Structure):
-    _fields_ = [("round_0", ctypes.c_int32), ("round_1", ctypes.c_int32)]
+    """SvtGpuConvolveParams: the reference's ConvolveParams layout (EbDefinitions.h:577-590)."""
+    _fields_ = [("ref", ctypes.c_int32), ("do_average", ctypes.c_int32), ("dst", ctypes.c_void_p),
+                ("dst_stride", ctypes.c_int32), ("round_0", ctypes.c_int32), ("round_1", ctypes.c_int32),
+                ("plane", ctypes.c_int32), ("is_compound", ctypes.c_int32), ("use_jnt_comp_avg", ctypes.c_int32),
+                ("fwd_offset", ctypes.c_int32), ("bck_offset", ctypes.c_int32),
+                ("use_dist_wtd_comp_avg", ctypes.c_int32)]
+
+
+class SgrParams(ctypes.Structure):
+    """SvtGpuSgrParams: the reference's SgrParamsType (EbDefinitions.h:1768-1771)."""
+    _fields_ = [("r", ctypes.c_int32 * 2), ("s", ctypes.c_int32 * 2)]
 
 
 MD_SIZES = [(4, 4), (4, 8), (8, 4), (8, 8), (8, 16), (16, 8), (16, 16), (16, 32), (32, 16), (32, 32), (32, 64),
@@ -262,6 +272,27 @@ _SIGS = {
                                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "svtgpu_full_distortion_kernel16_bits": (_U64, [_P, ctypes.c_uint32, ctypes.c_uint32, _P, ctypes.c_int32,
                                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_nxm_sad_kernel": (ctypes.c_uint32, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32]),
+    "svtgpu_nxm_sad_kernel_sub_sampled": (ctypes.c_uint32, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32,
+                                                            ctypes.c_uint32]),
+    "svtgpu_aom_mse16x16": (ctypes.c_uint32, [_P, _I32, _P, _I32, ctypes.POINTER(ctypes.c_uint32)]),
+    "svtgpu_aom_highbd_8_mse16x16": (None, [_P, _I32, _P, _I32, ctypes.POINTER(ctypes.c_uint32)]),
+    "svtgpu_aom_variance_highbd": (ctypes.c_uint32, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_uint32)]),
+    **{"svtgpu_aom_sub_pixel_variance%dx%d" % s: (ctypes.c_uint32, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
+                                                                    ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)])
+       for s in MD_SIZES},
+    "svtgpu_cdef_filter_block_8xn_16": (None, [_P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _I32, ctypes.c_uint8,
+                                               ctypes.c_uint8]),
+    "svtgpu_aom_copy_rect8_8bit_to_16bit": (None, [_P, _I32, _P, _I32, _I32, _I32]),
+    "svtgpu_av1_compute_stats": (None, [_I32, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P]),
+    "svtgpu_av1_compute_stats_highbd": (None, [_I32, _P, _P, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _I32]),
+    "svtgpu_av1_lowbd_pixel_proj_error": (ctypes.c_int64, [_P, _I32, _I32, _I32, _P, _I32, _P, _I32, _P, _I32, _P, _P]),
+    "svtgpu_av1_highbd_pixel_proj_error": (ctypes.c_int64, [_P, _I32, _I32, _I32, _P, _I32, _P, _I32, _P, _I32, _P,
+                                                            _P]),
+    "svtgpu_get_proj_subspace": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int,
+                                        _P, ctypes.c_int, _P, ctypes.c_int, _P, _P]),
     "svtgpu_md_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "svtgpu_md_batch_destroy": (None, [_P]),
     "svtgpu_md_batch_nsb": (_I32, [_P]),

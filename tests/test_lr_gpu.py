@@ -32,7 +32,7 @@ def test_wiener_shims_golden(ctx):
         fx, fy = (np.ascontiguousarray(g["taps"][n][k * 8:(k + 1) * 8]).copy() for k in range(2))
         inp = g["in%d" % n].copy()
         r0, r1 = oracle.wiener_round(bd)
-        cp = svtgpu.ConvolveParams(r0, r1)
+        cp = svtgpu.ConvolveParams(round_0=r0, round_1=r1)
         if bd == 8:
             i8 = inp.astype(np.uint8)
             o8 = np.zeros((h, w), np.uint8)

@@ -1,0 +1,43 @@
+"""The drop-in boundary, end to end: the reference's own frame code with its RTCD function pointers bound to the
+libsvtgpu shims.
+
+oracle/_ref/rtcd_pipe is oracle/ref_harness/gen_golden_pipe.c compiled against the reference headers with
+-DSVTGPU_BIND and -Werror=incompatible-pointer-types: every shim (loop filter x16, CDEF filter / 8xn / find_dir /
+dist / search_one_dual / copy_rect8, Wiener and self-guided filters, compute_stats, pixel_proj_error,
+get_proj_subspace, mse16x16, the full-distortion kernels) is assigned to the reference's pointer without a cast,
+and svt_av1_pick_filter_level, svt_av1_loop_filter_frame, cdef_seg_search / finish_cdef_search /
+svt_av1_cdef_frame, restoration_seg_search / rest_finish_search / svt_av1_loop_restoration_filter_frame then run
+through the device.  Every output must equal the pure-C run of the same code (tests/golden/pipe_<case>.npz)."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import golden_io
+import pipeline_cases as pc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RTCD_PIPE = os.path.join(ROOT, "oracle", "_ref", "rtcd_pipe")
+CASES = ["mini10b", "mini8c"]  # few CDEF strengths: the per-block shims are synchronous round trips
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(RTCD_PIPE), reason="oracle/_ref/rtcd_pipe not built (needs /root/reference)")
+@pytest.mark.parametrize("case", CASES)
+def test_reference_frame_code_through_device_shims(case):
+    src, rec, mi = pc.inputs(case)
+    g = pc.load(case)
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        pc.write_input(fin, case, src, rec, mi)
+        res = subprocess.run([RTCD_PIPE, "pipe", fin, fout], capture_output=True, text=True, timeout=280)
+        assert res.returncode == 0, res.stderr[-2000:]
+        out = golden_io.load(fout)
+    assert set(k for k in g if k != "input_sha") <= set(out), sorted(set(g) - set(out))
+    for k in g:
+        if k == "input_sha":
+            continue
+        np.testing.assert_array_equal(out[k], g[k], err_msg="%s: %s differs between the C and the device-shim runs"
+                                      % (case, k))
