@@ -39,5 +39,9 @@ def test_reference_frame_code_through_device_shims(case):
     for k in g:
         if k == "input_sha":
             continue
-        np.testing.assert_array_equal(out[k], g[k], err_msg="%s: %s differs between the C and the device-shim runs"
-                                      % (case, k))
+        a, b = np.array(out[k]), np.array(g[k])
+        if k.startswith("lr_units"):  # {type, vfilter[8], hfilter[8], ep, xqd[2]}: the fields of the unused filter
+            for arr in (a, b):     # are whatever RestorationUnitInfo held before (uninitialised in the reference)
+                arr[arr[:, 0] != 1, 1:17] = 0
+                arr[arr[:, 0] != 2, 17:20] = 0
+        np.testing.assert_array_equal(a, b, err_msg="%s: %s differs between the C and the device-shim runs" % (case, k))
