@@ -106,7 +106,30 @@ def parse():
                          "picture-level parallelism); a step processes one frame per slot")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for the real runs; gloo rehearses N > 1 ranks sharing one GPU")
+    ap.add_argument("--split", default="frames", choices=("frames", "bands"),
+                    help="N > 1: 'frames' = every rank filters its own frames (pictures are independent objects of "
+                         "the in-loop filter path; no data-path collective, weak scaling); 'bands' = one frame per "
+                         "step cut into row bands across the ranks (SURVEY §8e; RCCL exchanges, strong scaling)")
+    ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
     return ap.parse_args()
+
+
+def spawn_ranks(a):
+    """`--gpus N` outside a torch.distributed launcher: start the N ranks as children (one process per GPU) before
+    this process touches the device, and return their exit code.  Inside a launcher WORLD_SIZE must equal N."""
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world:
+        if world != a.gpus:
+            raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d: refusing to report one as the other"
+                             % (a.gpus, world))
+        return None
+    if a.gpus <= 1:
+        return None
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(a.master_port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
 
 
 def cpu_threads():
@@ -244,6 +267,9 @@ def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, grid, lr_ctrls, lr_u
 
 def main():
     a = parse()
+    rc = spawn_ranks(a)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -257,14 +283,17 @@ def main():
         else:
             dist.init_process_group("gloo")
     n = world
+    banded = n > 1 and a.split == "bands"  # else every rank runs whole frames of its own
     W, H, bd = a.width, a.height, a.bit_depth
     q, lam = a.base_q_idx, 60000
 
     ctx = svtgpu.Context(local)
     ctrls = svtgpu.cdef_controls(a.cdef_level)
     nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
-    rows = np.linspace(0, nvfb, n + 1).round().astype(int)
-    cdef_rows = (int(rows[rank]), int(rows[rank + 1]))
+    nb = n if banded else 1
+    rb = rank if banded else 0
+    rows = np.linspace(0, nvfb, nb + 1).round().astype(int)
+    cdef_rows = (int(rows[rb]), int(rows[rb + 1]))
     mi = synth.mode_info(W, H, 3)
     lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
     # loop restoration: RU 256 / 128, wn_filter_lvl 1 + sg_filter_lvl 1 (maximum search work); the rate
@@ -291,7 +320,8 @@ def main():
             self.stream = torch.cuda.Stream()
             self.md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
             sp = self.stream.cuda_stream
-            self.src, self.rec = synth.frame_pair(W, H, bd, seed=0x5EED0003 + 0x100 * k)
+            # frames split: each rank filters different pictures
+            self.src, self.rec = synth.frame_pair(W, H, bd, seed=0x5EED0003 + 0x100 * k + (0 if banded else 0x10000 * rank))
             self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
             self.R.upload(self.rec, sp)
             self.S.upload(self.src, sp)
@@ -302,8 +332,8 @@ def main():
             self.md_mvs = np.random.default_rng(5 + k).integers(-16, 17, size=(self.md.nsb, NREF, 2))
             self.md.set_mvs(self.md_mvs, sp)
             self.st = svtgpu.CdefState(ctx, W, H)
-            self.group = dist.new_group(backend=a.dist_backend) if n > 1 else None  # one communicator per slot
-            if n > 1:
+            self.group = dist.new_group(backend=a.dist_backend) if banded else None  # one communicator per slot
+            if banded:
                 self.st.set_fb_rows(*cdef_rows)
                 self.mse_t = torch.zeros((2, self.st.nfb, 64), dtype=torch.int64, device="cuda")
                 self.skip_t = torch.zeros(self.st.nfb, dtype=torch.uint8, device="cuda")
@@ -311,8 +341,8 @@ def main():
                 self.var_t = torch.zeros((self.st.nfb, 64), dtype=torch.int32, device="cuda")
                 self.st.bind_tables(self.mse_t.data_ptr(), self.skip_t.data_ptr())
                 self.st.bind_dir_tables(self.dir_t.data_ptr(), self.var_t.data_ptr())
-            self.md_range = svtgpu.band(self.md.nsb, n, rank)  # MD batch: SB ranges, no collective
-            self.lr_rb, self.lr_re = svtgpu.lr_unit_rows(self.lr.units, n, rank)  # LR: unit-row bands, all-gather
+            self.md_range = svtgpu.band(self.md.nsb, nb, rb)  # MD batch: SB ranges, no collective
+            self.lr_rb, self.lr_re = svtgpu.lr_unit_rows(self.lr.units, nb, rb)  # LR: unit-row bands, all-gather
             self.ev = []  # per timed step: events on the streams the kernels run on
             self.lf_levels = []
             self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
@@ -331,18 +361,18 @@ def main():
                 es[1].record(stream)
                 self.lf_levels.append(lfp.levels())
             # CDEF stage on the deblocked frame
-            if n > 1:
+            if banded:
                 st.clear_tables(sp)
             st.search(D, S, ctrls, q, sp)
             if timed:
                 es[2].record(stream)
-            if n > 1:
+            if banded:
                 for t in (self.mse_t, self.skip_t, self.dir_t, self.var_t):  # zero-padded band tables -> frame
                     dist.all_reduce(t, group=self.group)                    # tables (RCCL over xGMI)
                 st.set_fb_rows(0, nvfb)  # every rank applies the whole frame: the LR search bands read all of O
             prm, _ = st.pick(ctrls, q, lam, sp)
             st.apply(D, O, prm, sp)
-            if n > 1:
+            if banded:
                 st.set_fb_rows(*cdef_rows)
             if timed:
                 es[3].record(stream)
@@ -356,7 +386,7 @@ def main():
                 es[7].record(md_stream)
             # LR search + apply on the CDEF output (boundary lines from the DLF output)
             self.at_lr.set()
-            if n == 1:
+            if not banded:
                 lr_ft = lr.search(O, S, lr_ctrls, sp)
             else:
                 recs = lr.search_units(O, S, lr_ctrls, self.lr_rb, self.lr_re, stream=sp)
@@ -435,7 +465,8 @@ def main():
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
-    value = F * W * H / (ms_per_step * 1e-3) / 1e6  # F frames per step for the whole job
+    frames_per_step = F * (1 if banded else n)  # frames split: every rank filters F frames per step
+    value = frames_per_step * W * H / (ms_per_step * 1e-3) / 1e6  # the whole job's luma pixels per second
     lr_cls = {c: {k: lr_tot[c][k] / max(lr_tot["searches"], 1) if lr_tot else 0.0 for k in ("launches", "ms", "bytes")}
               for c in svtgpu.LrState.PROFILE_CLASSES}
     # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
@@ -443,8 +474,8 @@ def main():
     S_samples = 1.5 * W * H
     B = 2 if bd > 8 else 1
     st = slots[0].st
-    nfb_band = st.nfb if n == 1 else (int(rows[rank + 1]) - int(rows[rank])) * nhfb
-    alg_bytes = 2 * S_samples * B / n + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
+    nfb_band = (cdef_rows[1] - cdef_rows[0]) * nhfb
+    alg_bytes = 2 * S_samples * B * nfb_band / st.nfb + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
     achieved = alg_bytes / (search_ms * 1e-3) / 1e9
     evals = nfb_band * 6144 * ctrls.strengths().__len__()  # (sample, strength) filter evaluations
     roof = {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
@@ -477,7 +508,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if banded else "weak",
         "vs_baseline": None,
         "dtype": "u16" if bd > 8 else "u8",
         "data": "synthetic",
@@ -485,9 +516,12 @@ def main():
                                "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
                                "LR search+apply (RU 256/128, wn/sg level 1)"
                                % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
-                   "width": W, "height": H, "bit_depth": bd, "frames_per_step": F,
-                   "frames_in_flight": F, "frame_latency_ms": round(frame_ms, 4),
-                   "parallelism": "row_bands%d (CDEF FB rows, LR unit rows, MD SBs; DLF replicated)" % n if n > 1 else "single",
+                   "width": W, "height": H, "bit_depth": bd, "frames_per_step": frames_per_step,
+                   "frames_in_flight": F, "frame_latency_ms": round(frame_ms, 4), "ranks_requested": a.gpus,
+                   "ranks": n,
+                   "parallelism": ("row_bands%d (CDEF FB rows, LR unit rows, MD SBs; DLF replicated)" % n if banded
+                                   else "frames%d (each rank filters its own pictures; no data-path collective)" % n
+                                   if n > 1 else "single"),
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
                                 "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_search_apply": round(lr_ms, 4),
                                 "md_sad_sse_var": round(md_ms, 4),

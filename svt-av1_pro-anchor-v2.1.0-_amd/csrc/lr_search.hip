@@ -1211,6 +1211,192 @@ __global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n,
     PROF_END(tk);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The Wiener descents as one persistent work-queue kernel.  A work item is one tile of a unit whose descent has a
+// pending candidate; workers (persistent workgroups) claim items in order from an append-only log, evaluate the
+// tile's SSE for the unit's candidate and count the unit's arrivals; the workgroup that completes a unit's round
+// runs the descent step (Descent::report / next, exactly as wiener_advance_one) and appends the unit's tiles for
+// its next candidate.  No workgroup ever waits for a specific other one -- an idle worker polls the log until an
+// item appears or no descent is live -- so the kernel needs no co-residency and drains when the last descent ends.
+// Rounds of different units interleave freely: no launch boundary, no host poll, no per-round advance kernel.
+// ---------------------------------------------------------------------------------------------
+struct WnQueue {
+    int32_t head;   // next log index to claim
+    int32_t alloc;  // log entries reserved by producers
+    int32_t live;   // descents not done
+    int32_t error;  // log overflow: the search is abandoned (SVTGPU_ERR_HIP)
+};
+
+__device__ inline int q_load(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+
+// append the tiles of unit u to the log (every lane of the workgroup calls this; lane 0 reserves)
+__device__ inline void q_append(WnQueue *q, int32_t *log, int cap, const int32_t *tile0, int u, int *s_pos) {
+    const int t0 = tile0[u], nt = tile0[u + 1] - t0;
+    if (threadIdx.x == 0) {
+        const int pos = atomicAdd(&q->alloc, nt);
+        if (pos + nt > cap) {
+            atomicExch(&q->error, 1);
+            atomicExch(&q->live, 0); // stop every worker; the host reports the failure
+        }
+        *s_pos = pos;
+    }
+    __syncthreads();
+    const int pos = *s_pos;
+    if (pos + nt <= cap)
+        for (int k = threadIdx.x; k < nt; k += blockDim.x)
+            __hip_atomic_store(log + pos + k, t0 + k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+}
+
+// first descent step of every unit (the solve's seed is the first candidate) and the initial log
+__global__ __launch_bounds__(256) void wiener_queue_start_kernel(Descent *ds, int n, unsigned long long *err,
+                                                                 int16_t *taps, int32_t *wact, int32_t *ctag,
+                                                                 int32_t *arr, const int32_t *tile0, WnQueue *q,
+                                                                 int32_t *log, int cap) {
+    __shared__ int s_pos;
+    const int u = blockIdx.x; // one workgroup per unit: the append uses the whole group
+    __shared__ int s_live;
+    if (threadIdx.x == 0) {
+        arr[u]  = 0;
+        s_live  = wiener_advance_one(ds, u, err, taps, wact, ctag, 1);
+        if (s_live) atomicAdd(&q->live, 1);
+        __threadfence();
+    }
+    __syncthreads();
+    if (s_live) q_append(q, log, cap, tile0, u, &s_pos);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, Descent *ds, int16_t *taps,
+                                                           int32_t *wact, int32_t *ctag, int32_t *arr,
+                                                           unsigned long long *err, const int32_t *tile0,
+                                                           uint32_t *tcache, WnQueue *q, int32_t *log, int cap,
+                                                           unsigned long long *pc, unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    constexpr int VS = 72;
+    __shared__ __align__(16) uint16_t v[71 * VS];
+    __shared__ __align__(16) uint32_t tq[36 * 64];
+    __shared__ __align__(16) uint16_t sv[64 * 64];
+    __shared__ int s_item, s_last, s_pos;
+    unsigned long long npx = 0;
+    for (;;) {
+        // ---- claim the next log entry and wait until it is published (or nothing is live any more) ----
+        if (threadIdx.x == 0) {
+            const int idx = atomicAdd(&q->head, 1);
+            int       it  = 0;
+            for (;;) {
+                if (idx < cap) it = q_load(log + idx);
+                if (it || idx >= cap) break;
+                if (q_load(&q->live) == 0) break; // every descent ended: no entry will be published any more
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_item = it - 1;
+        }
+        __syncthreads();
+        const int ti = s_item;
+        if (ti < 0) break;
+        const Tile       t = A.tiles[ti];
+        const PlaneArgs &P = A.pl[t.plane];
+        const int        u = t.unit, mode = __hip_atomic_load(wact + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const T         *d = (const T *)P.dgd, *src = (const T *)P.src;
+        // ---- stage: source tile, and the bordered CDEF tile or the cached horizontal pass ----
+        for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+            const int r = i >> 4, g = i & 15;
+            if (r < t.h && 4 * g < t.w) {
+                int qv[4];
+                load4(src + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g, qv);
+                *(uint2 *)(sv + r * 64 + 4 * g) = make_uint2(pack2(qv[0], qv[1]), pack2(qv[2], qv[3]));
+            }
+        }
+        if (mode == 2) {
+            const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
+            for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = tc[i];
+        } else {
+            const int rows = t.h + 7, ng = (t.w + 8) >> 2;
+            for (int i = threadIdx.x; i < 71 * 18; i += 256) {
+                const int r = i / 18, g = i - r * 18;
+                if (r < rows && g < ng)
+                    *(uint2 *)(v + r * VS + 4 * g) = load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * g);
+            }
+        }
+        __syncthreads();
+        // ---- the candidate's SSE over the tile (the passes of wiener_trial_kernel) ----
+        const int16_t *tp = taps + u * 16;
+        int            h[8], w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            h[k] = __hip_atomic_load(tp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+            w[k] = __hip_atomic_load(tp + 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
+        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
+        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
+        const int      rows = t.h + 7, nyp = (t.h + 1) >> 1;
+        const WienerRound rr = wiener_round(P.bd);
+        if (mode != 2) {
+            const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
+            uint16_t *tq16 = (uint16_t *)tq;
+            const int xh   = 2 * (threadIdx.x & 31);
+            if (xh < t.w)
+                for (int r = threadIdx.x >> 5; r < rows; r += 8) {
+                    const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
+                    const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
+                    const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
+                    const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
+                    const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
+                    tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
+                    tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
+                }
+            __syncthreads();
+            if (mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
+                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
+                for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
+            }
+        }
+        uint32_t  e    = 0;
+        const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
+        const int x    = threadIdx.x & 63;
+        if (x < t.w)
+            for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
+                const int       y  = 2 * yp;
+                const uint32_t *c  = tq + yp * 64 + x;
+                const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
+                const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
+                const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
+                const uint16_t *sp = sv + y * 64 + x;
+                const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
+                e += (uint32_t)(d0 * d0);
+                if (y + 1 < t.h) {
+                    const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[64];
+                    e += (uint32_t)(d1 * d1);
+                }
+            }
+        const unsigned long long et = wave_sum_u32_wide(e);
+        if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[u], et);
+        npx += (unsigned long long)(t.w * t.h);
+        __syncthreads(); // every wave's SSE (and the tile cache) is in memory before the arrival
+        // ---- arrival; the workgroup completing the unit's round runs its descent step ----
+        if (threadIdx.x == 0) {
+            __threadfence();
+            const int nt = tile0[u + 1] - tile0[u];
+            const int a  = atomicAdd(&arr[u], 1);
+            s_last       = a == nt - 1;
+            if (s_last) {
+                __threadfence(); // acquire the other tiles' SSE / cache writes
+                arr[u] = 0;
+                const int live = wiener_advance_one(ds, u, err, taps, wact, ctag, 0);
+                __threadfence();
+                if (!live) atomicSub(&q->live, 1);
+                s_last = live;
+            }
+        }
+        __syncthreads();
+        if (s_last) q_append(q, log, cap, tile0, u, &s_pos);
+    }
+    if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
+    PROF_END(tk);
+}
+
 // svt_decode_xq (EbRestoration.c:634-646): xq of the ep's absent filter is 0
 __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
     const int x0 = d.val(0, 0), x1 = d.val(0, 1), r0 = c_sgr_r[d.ep][0], r1 = c_sgr_r[d.ep][1];
@@ -1637,6 +1823,22 @@ SgSpec sg_spec() { // self-guided tree sizes by live count; SVTGPU_SG_SPEC="live
     }();
     return v;
 }
+// persistent Wiener queue workers (SVTGPU_WN_QUEUE=0 selects the per-round trial/advance launches instead;
+// SVTGPU_WN_QGRID sets the worker count)
+bool wn_use_queue() {
+    static const bool v = [] {
+        const char *e = std::getenv("SVTGPU_WN_QUEUE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+int wn_queue_grid() {
+    static const int g = [] {
+        const char *e = std::getenv("SVTGPU_WN_QGRID");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 1024;
+    }();
+    return g;
+}
 int wn_trial_grid() {
     static const int g = [] {
         const char *e = std::getenv("SVTGPU_WN_GRID");
@@ -1741,6 +1943,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
                  o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
                  o_witems = dc(4 * (size_t)nt_wn), o_cnt = dc(32);
+    // the Wiener work queue: per-unit arrivals, the queue counters and the append-only log of tile items
+    const int    wq_cap = 192 * nt_wn + 4096;
+    const size_t o_warr = dc(4 * (size_t)n_wn), o_wq = dc(sizeof(WnQueue)), o_wlog = dc(4 * (size_t)wq_cap);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -1875,7 +2080,24 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    if (n_wn) {
+    const bool wn_queue = wn_use_queue();
+    if (n_wn && wn_queue) { // the whole Wiener descent in one persistent kernel (no host poll, no round launches)
+        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
+        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
+        HIP_TRY(hipMemsetAsync(dp(o_wq), 0, sizeof(WnQueue), sw));
+        HIP_TRY(hipMemsetAsync(dp(o_wlog), 0, 4 * (size_t)wq_cap, sw));
+        hipLaunchKernelGGL(wiener_queue_start_kernel, dim3(n_wn), dim3(256), 0, sw, (Descent *)dp(o_wds), n_wn,
+                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
+                           (int32_t *)dp(o_ctag), (int32_t *)dp(o_warr), (const int32_t *)d_t0, (WnQueue *)dp(o_wq),
+                           (int32_t *)dp(o_wlog), wq_cap);
+        run(2, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(wiener_queue_kernel<T>, dim3(std::min(nt_wn, wn_queue_grid())), dim3(256), 0, sw, A,
+                               (Descent *)dp(o_wds), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag),
+                               (int32_t *)dp(o_warr), (unsigned long long *)dp(o_werr), (const int32_t *)d_t0,
+                               (uint32_t *)dp(o_tcache), (WnQueue *)dp(o_wq), (int32_t *)dp(o_wlog), wq_cap, pc, tk);
+        });
+        HIP_TRY(hipGetLastError());
+    } else if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
         HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
         hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, sw, (Descent *)dp(o_wds), n_wn,
@@ -1902,7 +2124,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         int         g = 0, head = 0, inflight = 0; // round index; ring of two batches in flight
         hipStream_t stream;
     } ch[2];
-    ch[0].live = n_wn > 0, ch[0].stream = sw;
+    ch[0].live = n_wn > 0 && !wn_queue, ch[0].stream = sw;
     ch[1].live = npairs > 0, ch[1].stream = st;
     if (!s->h_flag) {
         HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
@@ -2021,7 +2243,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
+    if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), dp(o_wq), sizeof(WnQueue), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (n_wn && wn_queue && ((const WnQueue *)hp(h_cnt))->error) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener work queue overflow", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
     mark(3);
     // ---- phase 5 (host): per-unit results and, for the whole frame, the RD finish ----
     const uint64_t                 *sse0 = (const uint64_t *)hp(h_sse), *sse2 = (const uint64_t *)hp(h_sse2);
