@@ -1284,10 +1284,15 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
         if (threadIdx.x == 0) {
             const int idx = atomicAdd(&q->head, 1);
             int       it  = 0;
-            for (;;) {
+            for (unsigned spin = 0;; spin++) {
                 if (idx < cap) it = q_load(log + idx);
                 if (it || idx >= cap) break;
                 if (q_load(&q->live) == 0) break; // every descent ended: no entry will be published any more
+                if (spin > (1u << 25)) {          // a bound every worker reaches (~seconds): never spin forever
+                    atomicExch(&q->error, 2);
+                    atomicExch(&q->live, 0);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
             s_item = it - 1;
