@@ -29,6 +29,9 @@ struct SvtGpuLrState {
     // pinned memory: the host polls it without runtime calls)
     unsigned long long  *h_flag, *h_flag_dev;
     unsigned long long   flag_seq;
+    // uncached device memory shared by the persistent Wiener queue's workgroups (coherent without cache flushes)
+    void                *d_qarena;
+    size_t               qarena_bytes;
 };
 void lr_profiler_destroy(void *prof);
 

@@ -1227,7 +1227,16 @@ struct WnQueue {
     int32_t error;  // log overflow: the search is abandoned (SVTGPU_ERR_HIP)
 };
 
-__device__ inline int q_load(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
+// Every word the workers share lives in uncached device memory (hipDeviceMallocUncached): reads and writes go
+// to memory, so no cache flush or invalidate is ever needed (an agent-scope fence writes back and invalidates the
+// whole L2 of the XCD -- per tile, that stalls every kernel on the device).  Ordering is by completion: a
+// producer waits for its stores to be acknowledged before it publishes, a consumer issues its reads after the
+// publishing word has arrived.
+__device__ inline void wait_mem() {
+    __builtin_amdgcn_s_waitcnt(0); // vmcnt (loads and stores on gfx9), expcnt, lgkmcnt
+    asm volatile("" ::: "memory");
+}
+__device__ inline int q_load(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // append the tiles of unit u to the log (every lane of the workgroup calls this; lane 0 reserves)
 __device__ inline void q_append(WnQueue *q, int32_t *log, int cap, const int32_t *tile0, int u, int *s_pos) {
@@ -1244,23 +1253,25 @@ __device__ inline void q_append(WnQueue *q, int32_t *log, int cap, const int32_t
     const int pos = *s_pos;
     if (pos + nt <= cap)
         for (int k = threadIdx.x; k < nt; k += blockDim.x)
-            __hip_atomic_store(log + pos + k, t0 + k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(log + pos + k, t0 + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
 }
 
 // first descent step of every unit (the solve's seed is the first candidate) and the initial log
-__global__ __launch_bounds__(256) void wiener_queue_start_kernel(Descent *ds, int n, unsigned long long *err,
-                                                                 int16_t *taps, int32_t *wact, int32_t *ctag,
-                                                                 int32_t *arr, const int32_t *tile0, WnQueue *q,
-                                                                 int32_t *log, int cap) {
+__global__ __launch_bounds__(256) void wiener_queue_start_kernel(const Descent *ds_in, Descent *ds, int n,
+                                                                 unsigned long long *err, int16_t *taps,
+                                                                 int32_t *wact, int32_t *ctag, int32_t *arr,
+                                                                 const int32_t *tile0, WnQueue *q, int32_t *log,
+                                                                 int cap) {
     __shared__ int s_pos;
     const int u = blockIdx.x; // one workgroup per unit: the append uses the whole group
     __shared__ int s_live;
     if (threadIdx.x == 0) {
-        arr[u]  = 0;
-        s_live  = wiener_advance_one(ds, u, err, taps, wact, ctag, 1);
+        arr[u] = 0, err[u] = 0, ctag[u] = -1;
+        ds[u]  = ds_in[u];
+        s_live = wiener_advance_one(ds, u, err, taps, wact, ctag, 1);
         if (s_live) atomicAdd(&q->live, 1);
-        __threadfence();
+        wait_mem();
     }
     __syncthreads();
     if (s_live) q_append(q, log, cap, tile0, u, &s_pos);
@@ -1296,6 +1307,7 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
                 __builtin_amdgcn_s_sleep(2);
             }
             s_item = it - 1;
+            wait_mem();
         }
         __syncthreads();
         const int ti = s_item;
@@ -1379,18 +1391,17 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
         const unsigned long long et = wave_sum_u32_wide(e);
         if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[u], et);
         npx += (unsigned long long)(t.w * t.h);
-        __syncthreads(); // every wave's SSE (and the tile cache) is in memory before the arrival
+        wait_mem();      // this wave's SSE add and tile-cache stores are acknowledged
+        __syncthreads(); // ... by every wave, before the arrival
         // ---- arrival; the workgroup completing the unit's round runs its descent step ----
         if (threadIdx.x == 0) {
-            __threadfence();
             const int nt = tile0[u + 1] - tile0[u];
-            const int a  = atomicAdd(&arr[u], 1);
+            const int a  = atomicAdd(&arr[u], 1); // after every wave's stores completed (wait_mem, barrier)
             s_last       = a == nt - 1;
             if (s_last) {
-                __threadfence(); // acquire the other tiles' SSE / cache writes
                 arr[u] = 0;
                 const int live = wiener_advance_one(ds, u, err, taps, wact, ctag, 0);
-                __threadfence();
+                wait_mem(); // the new candidate is in memory before its tiles are published
                 if (!live) atomicSub(&q->live, 1);
                 s_last = live;
             }
@@ -1840,7 +1851,7 @@ bool wn_use_queue() {
 int wn_queue_grid() {
     static const int g = [] {
         const char *e = std::getenv("SVTGPU_WN_QGRID");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 1024;
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 512; // 2 per CU: the self-guided filters keep room (1024 starves them)
     }();
     return g;
 }
@@ -1948,9 +1959,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
                  o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
                  o_witems = dc(4 * (size_t)nt_wn), o_cnt = dc(32);
-    // the Wiener work queue: per-unit arrivals, the queue counters and the append-only log of tile items
-    const int    wq_cap = 192 * nt_wn + 4096;
-    const size_t o_warr = dc(4 * (size_t)n_wn), o_wq = dc(sizeof(WnQueue)), o_wlog = dc(4 * (size_t)wq_cap);
+    // the Wiener work queue's shared words, in the uncached arena: counters, the append-only log of tile items,
+    // per-unit arrivals / SSE / taps / modes / descents, and the horizontal-pass cache
+    const int wq_cap = 192 * nt_wn + 4096;
+    Carver    qc;
+    const size_t q_wq = qc(sizeof(WnQueue)), q_log = qc(4 * (size_t)wq_cap), q_arr = qc(4 * (size_t)n_wn),
+                 q_err = qc(8 * (size_t)n_wn), q_taps = qc(32 * (size_t)n_wn), q_wact = qc(4 * (size_t)n_wn),
+                 q_ctag = qc(4 * (size_t)n_wn), q_ds = qc(sizeof(Descent) * (size_t)n_wn),
+                 q_tc = qc((size_t)36 * 64 * 4 * nt_wn);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -2086,22 +2102,29 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     mark(1);
     // ---- phase 3: descent rounds on the device ----
     const bool wn_queue = wn_use_queue();
+    uint8_t   *qa       = nullptr;
     if (n_wn && wn_queue) { // the whole Wiener descent in one persistent kernel (no host poll, no round launches)
-        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
-        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
-        HIP_TRY(hipMemsetAsync(dp(o_wq), 0, sizeof(WnQueue), sw));
-        HIP_TRY(hipMemsetAsync(dp(o_wlog), 0, 4 * (size_t)wq_cap, sw));
-        hipLaunchKernelGGL(wiener_queue_start_kernel, dim3(n_wn), dim3(256), 0, sw, (Descent *)dp(o_wds), n_wn,
-                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
-                           (int32_t *)dp(o_ctag), (int32_t *)dp(o_warr), (const int32_t *)d_t0, (WnQueue *)dp(o_wq),
-                           (int32_t *)dp(o_wlog), wq_cap);
+        if (qc.off > s->qarena_bytes) {
+            if (s->d_qarena) (void)hipFree(s->d_qarena);
+            s->d_qarena = nullptr, s->qarena_bytes = 0;
+            HIP_TRY(hipExtMallocWithFlags(&s->d_qarena, qc.off, hipDeviceMallocUncached));
+            s->qarena_bytes = qc.off;
+        }
+        qa = (uint8_t *)s->d_qarena;
+        HIP_TRY(hipMemsetAsync(qa + q_wq, 0, q_arr - q_wq, sw)); // counters and the log
+        hipLaunchKernelGGL(wiener_queue_start_kernel, dim3(n_wn), dim3(256), 0, sw, (const Descent *)dp(o_wds),
+                           (Descent *)(qa + q_ds), n_wn, (unsigned long long *)(qa + q_err), (int16_t *)(qa + q_taps),
+                           (int32_t *)(qa + q_wact), (int32_t *)(qa + q_ctag), (int32_t *)(qa + q_arr),
+                           (const int32_t *)d_t0, (WnQueue *)(qa + q_wq), (int32_t *)(qa + q_log), wq_cap);
         run(2, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_queue_kernel<T>, dim3(std::min(nt_wn, wn_queue_grid())), dim3(256), 0, sw, A,
-                               (Descent *)dp(o_wds), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag),
-                               (int32_t *)dp(o_warr), (unsigned long long *)dp(o_werr), (const int32_t *)d_t0,
-                               (uint32_t *)dp(o_tcache), (WnQueue *)dp(o_wq), (int32_t *)dp(o_wlog), wq_cap, pc, tk);
+                               (Descent *)(qa + q_ds), (int16_t *)(qa + q_taps), (int32_t *)(qa + q_wact),
+                               (int32_t *)(qa + q_ctag), (int32_t *)(qa + q_arr), (unsigned long long *)(qa + q_err),
+                               (const int32_t *)d_t0, (uint32_t *)(qa + q_tc), (WnQueue *)(qa + q_wq),
+                               (int32_t *)(qa + q_log), wq_cap, pc, tk);
         });
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(dp(o_wds), qa + q_ds, sizeof(Descent) * (size_t)n_wn, hipMemcpyDeviceToDevice, sw));
     } else if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
         HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
@@ -2248,7 +2271,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
-    if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), dp(o_wq), sizeof(WnQueue), hipMemcpyDeviceToHost, st));
+    if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), qa + q_wq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (n_wn && wn_queue && ((const WnQueue *)hp(h_cnt))->error) {
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener work queue overflow", __FILE__, __LINE__);
