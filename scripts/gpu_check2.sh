@@ -1,0 +1,16 @@
+#!/bin/bash
+# Diagnostic + all GPU tests without -x, smoke, bench, kernel-trace profile.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 120 python -u scripts/diag_stats.py > gpurun_out/diag_stats.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+case $rc in 0|1) ;; *) echo "exit $rc"; exit $rc;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1 &&
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
+rc2=$?
+echo "pytest $rc rest $rc2"
+exit $rc2

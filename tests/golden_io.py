@@ -24,7 +24,9 @@ def load(path):
         off += 4 * nd
         dtype = np.dtype(_DT[dt.decode()])
         n = int(np.prod(dims)) if dims else 1
-        arr = np.frombuffer(data, dtype=dtype, count=n, offset=off).reshape(dims)
+        # a copy: records start at arbitrary byte offsets, and the highbd shims take CONVERT_TO_BYTEPTR pointers
+        # (address >> 1), which need 2-byte aligned uint16 data
+        arr = np.frombuffer(data, dtype=dtype, count=n, offset=off).reshape(dims).copy()
         off += n * dtype.itemsize
         out[name] = arr
     return out
