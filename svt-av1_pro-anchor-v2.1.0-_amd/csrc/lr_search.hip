@@ -12,10 +12,14 @@
 //                         pairs (diagonal groups also form M); per-tile partials are reduced per unit
 //   sgr_flt_kernel        box sums of a tile once, then for every searched ep the A/B maps, both self-guided
 //                         filters (kept in HBM as int16) and the 2x2 projection moments in exact int64
-//   wiener_trial_kernel / proj_err_kernel
-//                         the SSE of one candidate per live descent (grid-stride over a device work list)
-//   *_advance_kernel      the coordinate descents of finer_tile_search_wiener_seg / finer_search_pixel_proj_error
-//                         run on the device: report the last error, propose the next candidate, rebuild the list
+//   wiener_unit_kernel    (default) the whole Wiener descent of finer_tile_search_wiener_seg per unit inside one
+//                         workgroup: candidate SSE over the unit's tiles, descent step in LDS, no global sync
+//   sgr_queue_kernel      (default) the self-guided descents of finer_search_pixel_proj_error as a persistent
+//                         work queue: a worker evaluates a unit tile's pending candidate trees, the worker completing
+//                         the unit's pass steps its descents and re-publishes its tiles
+//   wiener_queue_kernel, wiener_trial_kernel / proj_err_kernel + *_advance_kernel
+//                         the alternatives kept for A/B (SVTGPU_WN_UNIT=0, SVTGPU_WN_QUEUE=0, SVTGPU_SG_QUEUE=0): a
+//                         Wiener work queue, and per-round launches with a host-polled batch loop
 //   sgr_best_kernel, sgr_sse_kernel
 //                         best ep per unit (strict <) and the SSE of its clipped output
 // The host does what is sequential in the reference and cheap: the int64 fixed-point Wiener decomposition, the
@@ -744,18 +748,22 @@ __device__ inline uint32_t pk_sub16(uint32_t a, uint32_t b) { // per-half a - b 
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2i16s, a) - __builtin_bit_cast(v2i16s, b));
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
-                                                       int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
-                                                       unsigned long long *err, unsigned long long *pc,
-                                                       unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    const int n = cnt[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
-    constexpr int      NCH   = 4;
-    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated
-    for (int it = blockIdx.x; it < n; it += gridDim.x) {
-        const Tile       t = A.tiles[items[it]];
+// a word another workgroup of the same launch may have written (the work-queue kernels keep such words in uncached
+// memory and read them with vector loads); a plain load otherwise
+template <bool SHARED, typename W>
+__device__ inline W ld_shared(const W *p) {
+    if constexpr (SHARED) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
+// the candidate trees of every ep of tile ti's unit with a pending tree, evaluated over the tile; the errors are
+// added to err[pair * SG_NC + node]
+template <typename T, bool SHARED>
+__device__ inline void proj_tile(const SearchArgs &A, int ti, const int32_t *cand, const uint32_t *candm,
+                                 unsigned long long *err, unsigned long long &npx_t, unsigned long long &npx_e) {
+    constexpr int NCH = 4;
+    {
+        const Tile       t = A.tiles[ti];
         const PlaneArgs &P = A.pl[t.plane];
         const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne, cw = t.w >> 2;
         npx_t += t.w * t.h; // profiling
@@ -783,7 +791,7 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
         }
         // the eps with a pending tree; their filter planes are fetched one ep ahead of the arithmetic
         uint32_t act = 0;
-        for (int e = 0; e < P.ne; e++) act |= (candm[pb + e] != 0u) << e;
+        for (int e = 0; e < P.ne; e++) act |= (ld_shared<SHARED>(candm + pb + e) != 0u) << e;
         uint2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
         auto  fetch = [&](int e, uint2 *x0, uint2 *x1) {
             const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
@@ -798,12 +806,14 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
             const int en = act ? __builtin_ctz(act) : -1;
             if (en >= 0) fetch(en, n0, n1);
             const int      pair = pb + e;
-            const uint32_t mask = candm[pair];
+            const uint32_t mask = ld_shared<SHARED>(candm + pair);
             npx_e += t.w * t.h; // profiling
             uint32_t xq[SG_NC];
 #pragma unroll
             for (int c = 0; c < SG_NC; c++)
-                xq[c] = (mask >> c & 1) ? pack2(cand[(pair * SG_NC + c) * 2], cand[(pair * SG_NC + c) * 2 + 1]) : 0u;
+                xq[c] = (mask >> c & 1) ? pack2(ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2),
+                                                ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2 + 1))
+                                        : 0u;
             uint32_t acc[SG_NC];
 #pragma unroll
             for (int c = 0; c < SG_NC; c++) acc[c] = 0;
@@ -840,6 +850,18 @@ __global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const
             e = en;
         }
     }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
+                                                       int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
+                                                       unsigned long long *err, unsigned long long *pc,
+                                                       unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    const int n = cnt[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
+    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated
+    for (int it = blockIdx.x; it < n; it += gridDim.x) proj_tile<T, false>(A, items[it], cand, candm, err, npx_t, npx_e);
     if (pc && threadIdx.x == 0 && npx_t) {
         atomicAdd(pc + PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_e);
         atomicAdd(pc + 2 * PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_t);
@@ -1175,21 +1197,42 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // ---------------------------------------------------------------------------------------------
 __device__ inline int32_t htag(const Descent &d) { return (int32_t)(d.vals & 0xFFFFFF); } // hfilter taps 0..2
 
+// Words written by other workgroups of a work-queue kernel are read with agent-scope atomic loads, which miss in the
+// CU's vector L1: a plain load may return a line that this CU cached in an earlier pass (SHARED = false: plain loads,
+// the per-round launches, where every such word was written by an earlier launch)
+template <bool SHARED>
+__device__ inline uint64_t ld64(const void *p) {
+    if constexpr (SHARED) return __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *(const uint64_t *)p;
+}
+template <bool SHARED>
+__device__ inline Descent load_descent(const Descent *p) {
+    static_assert(sizeof(Descent) % 8 == 0, "Descent in 64-bit words");
+    if constexpr (!SHARED) {
+        return *p;
+    } else {
+        Descent d;
+        for (int k = 0; k < (int)(sizeof(Descent) / 8); k++) ((uint64_t *)&d)[k] = ld64<true>((const uint64_t *)p + k);
+        return d;
+    }
+}
+
 // returns 1 when the unit has a pending candidate (its tiles go on the next trial's list)
+template <bool SHARED = false>
 __device__ int wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
                                   int32_t *ctag, int first) {
-    Descent d = ds[u];
+    Descent d = load_descent<SHARED>(ds + u);
     if (d.done) return 0;
     // a mode-3 trial stored the horizontal pass of the candidate's hfilter (a vertical move leaves it unchanged)
-    if (!first && wact[u] == 3) ctag[u] = htag(d);
-    if (!first) d.report((int64_t)err[u]);
+    if (!first && ld_shared<SHARED>(wact + u) == 3) ctag[u] = htag(d);
+    if (!first) d.report((int64_t)ld64<SHARED>(err + u));
     err[u]  = 0;
     wact[u] = 0;
     if (d.next()) {
         int v[3];
         d.taps(0, v), set_wiener_taps(taps + 16 * u, v); // f = 0: hfilter, f = 1: vfilter
         d.taps(1, v), set_wiener_taps(taps + 16 * u + 8, v);
-        wact[u] = (d.init || d.mf != 1) ? 1 : (ctag[u] == htag(d) ? 2 : 3);
+        wact[u] = (d.init || d.mf != 1) ? 1 : (ld_shared<SHARED>(ctag + u) == htag(d) ? 2 : 3);
         ds[u]   = d;
         return 1;
     }
@@ -1269,7 +1312,7 @@ __global__ __launch_bounds__(256) void wiener_queue_start_kernel(const Descent *
     if (threadIdx.x == 0) {
         arr[u] = 0, err[u] = 0, ctag[u] = -1;
         ds[u]  = ds_in[u];
-        s_live = wiener_advance_one(ds, u, err, taps, wact, ctag, 1);
+        s_live = wiener_advance_one<true>(ds, u, err, taps, wact, ctag, 1);
         if (s_live) atomicAdd(&q->live, 1);
         wait_mem();
     }
@@ -1325,9 +1368,9 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
                 *(uint2 *)(sv + r * 64 + 4 * g) = make_uint2(pack2(qv[0], qv[1]), pack2(qv[2], qv[3]));
             }
         }
-        if (mode == 2) {
-            const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
-            for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = tc[i];
+        if (mode == 2) { // another workgroup may have stored this pass: loads that miss in this CU's L1
+            const uint64_t *tc = (const uint64_t *)(tcache + (size_t)ti * 36 * 64);
+            for (int i = threadIdx.x; i < 36 * 64 / 2; i += 256) ((uint64_t *)tq)[i] = ld64<true>(tc + i);
         } else {
             const int rows = t.h + 7, ng = (t.w + 8) >> 2;
             for (int i = threadIdx.x; i < 71 * 18; i += 256) {
@@ -1400,7 +1443,7 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
             s_last       = a == nt - 1;
             if (s_last) {
                 arr[u] = 0;
-                const int live = wiener_advance_one(ds, u, err, taps, wact, ctag, 0);
+                const int live = wiener_advance_one<true>(ds, u, err, taps, wact, ctag, 0);
                 wait_mem(); // the new candidate is in memory before its tiles are published
                 if (!live) atomicSub(&q->live, 1);
                 s_last = live;
@@ -1410,6 +1453,148 @@ __global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, D
         if (s_last) q_append(q, log, cap, tile0, u, &s_pos);
     }
     if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
+    PROF_END(tk);
+}
+
+// ---------------------------------------------------------------------------------------------
+// The Wiener descent of one unit per workgroup (finer_tile_search_wiener_seg, EbRestorationPick.c:1042-1146, run to
+// its end without leaving the CU): NG groups of 256 lanes take the unit's <= 64x64 tiles NG at a time, each group
+// filters its tile with the candidate (the passes of wiener_queue_kernel) into a per-lane SSE; the workgroup reduces
+// the unit's SSE and lane 0 takes the descent step (Descent::report / next) for the next candidate.  The descent
+// state and taps live in LDS; nothing is shared with another workgroup, so a round costs three workgroup barriers
+// per NG tiles instead of global arrivals, polling and uncached memory.  The horizontal pass of the current hfilter
+// is cached per tile in ordinary global memory (written and read by this workgroup only, ordered by its barriers),
+// so vertical-filter moves run only the vertical pass.
+// ---------------------------------------------------------------------------------------------
+template <typename T, int NG>
+__global__ __launch_bounds__(256 * NG) void wiener_unit_kernel(const SearchArgs A, Descent *ds, const int32_t *tile0,
+                                                               uint32_t *tcache, unsigned long long *pc,
+                                                               unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    constexpr int VS = 72;
+    __shared__ __align__(16) uint16_t vbuf[NG][71 * VS];
+    __shared__ __align__(16) uint32_t tqbuf[NG][36 * 64];
+    __shared__ uint64_t               s_draw[sizeof(Descent) / 8]; // Descent has initializers: raw LDS
+    __shared__ unsigned long long     s_part[4 * NG];
+    __shared__ int16_t                s_taps[16];
+    __shared__ int                    s_mode, s_ctag;
+    Descent  &D  = *(Descent *)s_draw;
+    const int u  = blockIdx.x, g = threadIdx.x >> 8, lt = threadIdx.x & 255;
+    const int t0 = tile0[u], nt = tile0[u + 1] - t0;
+    auto      propose = [&]() { // lane 0: the next candidate's taps and evaluation mode, or s_mode = 0 when done
+        if (D.next()) {
+            int v[3];
+            D.taps(0, v), set_wiener_taps(s_taps, v); // f = 0: hfilter, f = 1: vfilter
+            D.taps(1, v), set_wiener_taps(s_taps + 8, v);
+            s_mode = (D.init || D.mf != 1) ? 1 : (s_ctag == htag(D) ? 2 : 3);
+        } else {
+            s_mode = 0;
+        }
+    };
+    if (threadIdx.x == 0) {
+        D      = ds[u];
+        s_ctag = -1;
+        s_mode = 0;
+        if (!D.done) propose();
+    }
+    __syncthreads();
+    uint16_t *const    v = vbuf[g];
+    uint32_t *const    tq = tqbuf[g];
+    unsigned long long npx = 0;
+    while (const int mode = s_mode) {
+        int h[8], w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) h[k] = s_taps[k], w[k] = s_taps[8 + k];
+        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
+        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
+        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
+        unsigned long long eu = 0;
+        for (int base = 0; base < nt; base += NG) { // every lane runs the same iterations (workgroup barriers)
+            const int  ti = t0 + base + g;
+            const bool on = base + g < nt;
+            const Tile t  = on ? A.tiles[ti] : A.tiles[t0];
+            const PlaneArgs &P = A.pl[t.plane];
+            const T         *d = (const T *)P.dgd, *src = (const T *)P.src;
+            const WienerRound rr = wiener_round(P.bd);
+            // ---- stage: the bordered CDEF tile or the cached horizontal pass into LDS, this lane's source rows ----
+            const int x = lt & 63, nyp = (t.h + 1) >> 1;
+            if (on) {
+                if (mode == 2) {
+                    const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
+                    for (int i = lt; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = tc[i];
+                } else {
+                    const int rows = t.h + 7, ng = (t.w + 8) >> 2;
+                    for (int i = lt; i < 71 * 18; i += 256) {
+                        const int r = i / 18, gg = i - r * 18;
+                        if (r < rows && gg < ng)
+                            *(uint2 *)(v + r * VS + 4 * gg) =
+                                load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * gg);
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- horizontal pass (modes 1 and 3) ----
+            if (on && mode != 2) {
+                const int rows = t.h + 7;
+                const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
+                uint16_t *tq16 = (uint16_t *)tq;
+                const int xh   = 2 * (lt & 31);
+                if (xh < t.w)
+                    for (int r = lt >> 5; r < rows; r += 8) {
+                        const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
+                        const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
+                        const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
+                        const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
+                        const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
+                        tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
+                        tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
+                    }
+            }
+            __syncthreads();
+            if (on && mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
+                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
+                for (int i = lt; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
+            }
+            // ---- vertical pass and the SSE against the source ----
+            uint32_t  e    = 0;
+            const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
+            if (on && x < t.w) {
+                const T *sq = src + (size_t)t.y0 * P.sstride + t.x0 + x;
+#pragma unroll 2
+                for (int yp = lt >> 6; yp < nyp; yp += 4) {
+                    const int       y  = 2 * yp;
+                    const int       a0 = sq[(size_t)y * P.sstride], a1 = y + 1 < t.h ? (int)sq[(size_t)(y + 1) * P.sstride] : 0;
+                    const uint32_t *c  = tq + yp * 64 + x;
+                    const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
+                    const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
+                    const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
+                    const int d0 = min(max(s0 >> rr.r1, 0), maxv) - a0;
+                    e += (uint32_t)(d0 * d0);
+                    if (y + 1 < t.h) {
+                        const int d1 = min(max(s1 >> rr.r1, 0), maxv) - a1;
+                        e += (uint32_t)(d1 * d1);
+                    }
+                }
+            }
+            eu += e;
+            if (on && lt == 0) npx += (unsigned long long)(t.w * t.h);
+            __syncthreads(); // the next tiles restage v / tq
+        }
+        const unsigned long long et = wave_sum(eu);
+        if ((threadIdx.x & 63) == WAVE_LAST) s_part[threadIdx.x >> 6] = et;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long err = 0;
+            for (int k = 0; k < 4 * NG; k++) err += s_part[k];
+            if (s_mode == 3) s_ctag = htag(D); // the evaluated candidate's hfilter pass is now cached
+            D.report((int64_t)err);
+            propose();
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ds[u] = D;
+    if (pc && lt == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
     PROF_END(tk);
 }
 
@@ -1434,19 +1619,21 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 struct SgSpec {
     int32_t live1, live3;
 };
-// returns 1 when the descent stays live; *list_unit = its unit when this descent lists the unit's tiles
-__device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
-                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit,
-                               const SgSpec spec) {
-    Descent d = ds[i];
+// one step of descent i: replay the evaluated tree against its errors, then build the next tree of depth_nodes nodes;
+// returns 1 when the descent stays live
+// (tree: SG_NC / 2 nodes of scratch -- LDS in the queue kernels, where registers are scarce)
+template <bool SHARED = false>
+__device__ int sgr_descent_step(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
+                                int first, int depth_nodes, Descent *tree) {
+    Descent d = load_descent<SHARED>(ds + i);
     if (d.done) return 0;
     unsigned long long *e = err + (size_t)i * SG_NC;
     if (first) {
         d.next(); // the seed itself is the first candidate
     } else {
-        const uint32_t evaluated = candm[i];
+        const uint32_t evaluated = ld_shared<SHARED>(candm + i);
         for (int node = 0;;) {
-            const int64_t v     = (int64_t)e[node];
+            const int64_t v     = (int64_t)ld64<SHARED>(e + node);
             const bool    worse = !d.init && v > d.err;
             d.report(v);
             if (!d.next()) break;
@@ -1456,11 +1643,6 @@ __device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int3
     }
     for (int c = 0; c < SG_NC; c++) e[c] = 0;
     if (!d.done) {
-        const int live_in     = first ? 1 << 30 : cnt_cur[1];
-        const int depth_nodes = (spec.live1 >= 0 && live_in > spec.live1)   ? 1
-                                : (spec.live3 >= 0 && live_in > spec.live3) ? 3
-                                                                            : SG_NC; // nodes
-        Descent   tree[SG_NC / 2];
         uint32_t  mask = 1;
         int32_t  *cd   = cand + (size_t)i * SG_NC * 2;
         decode_xq(d, cd);
@@ -1479,13 +1661,27 @@ __device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int3
             }
         }
         candm[i] = mask;
-        if (atomicExch(&ustamp[d.unit], stamp) != stamp) *list_unit = d.unit; // listed once per round
-        ds[i] = d;
+        ds[i]    = d;
         return 1;
     }
     candm[i] = 0;
     ds[i]    = d;
     return 0;
+}
+
+// returns 1 when the descent stays live; *list_unit = its unit when this descent lists the unit's tiles
+__device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
+                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit,
+                               const SgSpec spec) {
+    const int live_in     = first ? 1 << 30 : cnt_cur[1];
+    const int depth_nodes = (spec.live1 >= 0 && live_in > spec.live1)   ? 1
+                            : (spec.live3 >= 0 && live_in > spec.live3) ? 3
+                                                                        : SG_NC; // nodes
+    Descent tree[SG_NC / 2];
+    if (!sgr_descent_step(ds, i, err, cand, candm, first, depth_nodes, tree)) return 0;
+    const int u = ds[i].unit;
+    if (atomicExch(&ustamp[u], stamp) != stamp) *list_unit = u; // listed once per round
+    return 1;
 }
 
 __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
@@ -1504,17 +1700,115 @@ __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, co
 }
 
 // ---------------------------------------------------------------------------------------------
+// The self-guided descents as one persistent work-queue kernel (the scheme of wiener_queue_kernel).  A work item is
+// one tile of a unit with a pending tree on any of its eps; the worker evaluates every pending tree of the unit over
+// the tile (proj_tile) and counts the unit's arrivals; the workgroup that completes the unit's pass steps all of the
+// unit's descents (one lane per ep, sgr_descent_step with the full SG_NC-node tree) and appends the unit's tiles again
+// while any of them is live.  q->live counts units with a live descent.
+// ---------------------------------------------------------------------------------------------
+__device__ inline int unit_plane(const SearchArgs &A, int nplanes, int u) {
+    int p = 0;
+    while (p + 1 < nplanes && u >= A.pl[p + 1].unit_base) p++;
+    return p;
+}
+
+__device__ inline int q_claim(WnQueue *q, const int32_t *log, int cap, int *s_item) { // every lane calls this
+    if (threadIdx.x == 0) {
+        const int idx = atomicAdd(&q->head, 1);
+        int       it  = 0;
+        for (unsigned spin = 0;; spin++) {
+            if (idx < cap) it = q_load(log + idx);
+            if (it || idx >= cap) break;
+            if (q_load(&q->live) == 0) break; // every descent ended: no entry will be published any more
+            if (spin > (1u << 25)) {          // a bound every worker reaches (~seconds): never spin forever
+                atomicExch(&q->error, 2);
+                atomicExch(&q->live, 0);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        *s_item = it - 1;
+        wait_mem();
+    }
+    __syncthreads();
+    return *s_item;
+}
+
+// the unit's first step (every descent's seed is its first candidate), one workgroup per global unit
+__global__ __launch_bounds__(64) void sgr_queue_start_kernel(const SearchArgs A, int nplanes, const Descent *ds_in,
+                                                             Descent *ds, unsigned long long *err, int32_t *cand,
+                                                             uint32_t *candm, int32_t *arr, const int32_t *tile0,
+                                                             WnQueue *q, int32_t *log, int cap) {
+    __shared__ int     s_pos;
+    __shared__ uint64_t s_treeraw[16 * (SG_NC / 2) * sizeof(Descent) / 8]; // Descent has initializers: raw LDS
+    Descent (*s_tree)[SG_NC / 2] = (Descent(*)[SG_NC / 2])s_treeraw;
+    const int          u = blockIdx.x;
+    const int      p = unit_plane(A, nplanes, u);
+    const PlaneArgs &P = A.pl[p];
+    if (P.ne == 0) return;
+    const int pb = P.pair_base + (u - P.unit_base) * P.ne;
+    int       live = 0;
+    if (threadIdx.x == 0) arr[u] = 0;
+    if (threadIdx.x < P.ne) {
+        ds[pb + threadIdx.x] = ds_in[pb + threadIdx.x];
+        for (int c = 0; c < SG_NC; c++) err[(size_t)(pb + threadIdx.x) * SG_NC + c] = 0;
+        live = sgr_descent_step<true>(ds, pb + threadIdx.x, err, cand, candm, 1, SG_NC, s_tree[threadIdx.x]);
+    }
+    wait_mem();
+    live = __syncthreads_or(live);
+    if (!live) return;
+    if (threadIdx.x == 0) atomicAdd(&q->live, 1);
+    q_append(q, log, cap, tile0, u, &s_pos);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void sgr_queue_kernel(const SearchArgs A, Descent *ds, int32_t *cand,
+                                                        uint32_t *candm, unsigned long long *err, int32_t *arr,
+                                                        const int32_t *tile0, WnQueue *q, int32_t *log, int cap,
+                                                        unsigned long long *pc, unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    __shared__ int     s_item, s_last, s_pos;
+    __shared__ uint64_t s_treeraw[16 * (SG_NC / 2) * sizeof(Descent) / 8]; // Descent has initializers: raw LDS
+    Descent (*s_tree)[SG_NC / 2] = (Descent(*)[SG_NC / 2])s_treeraw;
+    unsigned long long npx_t = 0, npx_e = 0;
+    for (;;) {
+        const int ti = q_claim(q, log, cap, &s_item);
+        if (ti < 0) break;
+        const Tile t = A.tiles[ti];
+        proj_tile<T, true>(A, ti, cand, candm, err, npx_t, npx_e);
+        wait_mem();      // this wave's error adds are acknowledged
+        __syncthreads(); // ... by every wave, before the arrival
+        if (threadIdx.x == 0) {
+            const int a = atomicAdd(&arr[t.unit], 1);
+            s_last      = a == tile0[t.unit + 1] - tile0[t.unit] - 1;
+            if (s_last) arr[t.unit] = 0;
+        }
+        __syncthreads();
+        if (!s_last) continue;
+        const PlaneArgs &P  = A.pl[t.plane];
+        const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
+        int              live = 0;
+        if (threadIdx.x < P.ne)
+            live = sgr_descent_step<true>(ds, pb + threadIdx.x, err, cand, candm, 0, SG_NC, s_tree[threadIdx.x]);
+        wait_mem(); // the new trees are in memory before the unit's tiles are published
+        live = __syncthreads_or(live);
+        if (live) q_append(q, log, cap, tile0, t.unit, &s_pos);
+        else if (threadIdx.x == 0) atomicSub(&q->live, 1);
+    }
+    if (pc && threadIdx.x == 0 && npx_t) {
+        atomicAdd(pc + PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_e);
+        atomicAdd(pc + 2 * PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_t);
+    }
+    PROF_END(tk);
+}
+
+// ---------------------------------------------------------------------------------------------
 // descent seeds on the device
 // ---------------------------------------------------------------------------------------------
 struct SeedCfg {
     int32_t wn_use_refinement, wn_max_one_step, sg_refine[2];
 };
 
-__device__ inline int unit_plane(const SearchArgs &A, int nplanes, int u) {
-    int p = 0;
-    while (p + 1 < nplanes && u >= A.pl[p + 1].unit_base) p++;
-    return p;
-}
 
 // wiener_decompose_sep_sym + finalize + compute_score (EbRestorationPick.c:906-1040, 1337-1419), one workgroup
 // per unit; the unit's descent starts from the finalized taps unless the score says the filter does not help
@@ -1848,6 +2142,37 @@ bool wn_use_queue() {
     }();
     return v;
 }
+// one workgroup per unit runs the whole Wiener descent (default); SVTGPU_WN_UNIT=0 selects the work queue
+bool wn_use_unit() {
+    static const bool v = [] {
+        const char *e = std::getenv("SVTGPU_WN_UNIT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+int wn_unit_ng() { // tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG: 2 or 4)
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_WN_NG");
+        return e && std::atoi(e) == 2 ? 2 : 4;
+    }();
+    return v;
+}
+// persistent self-guided queue workers (SVTGPU_SG_QUEUE=0 selects the per-round projection/advance launches;
+// SVTGPU_SG_QGRID sets the worker count)
+bool sg_use_queue() {
+    static const bool v = [] {
+        const char *e = std::getenv("SVTGPU_SG_QUEUE");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+int sg_queue_grid() {
+    static const int g = [] {
+        const char *e = std::getenv("SVTGPU_SG_QGRID");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 512;
+    }();
+    return g;
+}
 int wn_queue_grid() {
     static const int g = [] {
         const char *e = std::getenv("SVTGPU_WN_QGRID");
@@ -1967,6 +2292,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                  q_err = qc(8 * (size_t)n_wn), q_taps = qc(32 * (size_t)n_wn), q_wact = qc(4 * (size_t)n_wn),
                  q_ctag = qc(4 * (size_t)n_wn), q_ds = qc(sizeof(Descent) * (size_t)n_wn),
                  q_tc = qc((size_t)36 * 64 * 4 * nt_wn);
+    // the self-guided queue's: counters, log, per-unit arrivals, per-(unit, ep) tree errors, candidates, masks, descents
+    const int    sq_cap = 256 * nt_sg + 4096;
+    const size_t q_sq = qc(sizeof(WnQueue)), q_slog = qc(4 * (size_t)sq_cap), q_sarr = qc(4 * (size_t)n_all),
+                 q_serr = qc(8 * SG_NC * (size_t)npairs), q_scand = qc(8 * SG_NC * (size_t)npairs),
+                 q_scandm = qc(4 * (size_t)npairs), q_sds = qc(sizeof(Descent) * (size_t)npairs);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -2101,9 +2431,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    const bool wn_queue = wn_use_queue();
+    const bool wn_unit = wn_use_unit(), wn_queue = !wn_unit && wn_use_queue(), sg_queue = sg_use_queue();
     uint8_t   *qa       = nullptr;
-    if (n_wn && wn_queue) { // the whole Wiener descent in one persistent kernel (no host poll, no round launches)
+    if ((n_wn && wn_queue) || (npairs && sg_queue)) {
         if (qc.off > s->qarena_bytes) {
             if (s->d_qarena) (void)hipFree(s->d_qarena);
             s->d_qarena = nullptr, s->qarena_bytes = 0;
@@ -2111,6 +2441,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             s->qarena_bytes = qc.off;
         }
         qa = (uint8_t *)s->d_qarena;
+    }
+    if (n_wn && wn_queue) { // the whole Wiener descent in one persistent kernel (no host poll, no round launches)
         HIP_TRY(hipMemsetAsync(qa + q_wq, 0, q_arr - q_wq, sw)); // counters and the log
         hipLaunchKernelGGL(wiener_queue_start_kernel, dim3(n_wn), dim3(256), 0, sw, (const Descent *)dp(o_wds),
                            (Descent *)(qa + q_ds), n_wn, (unsigned long long *)(qa + q_err), (int16_t *)(qa + q_taps),
@@ -2125,6 +2457,16 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(dp(o_wds), qa + q_ds, sizeof(Descent) * (size_t)n_wn, hipMemcpyDeviceToDevice, sw));
+    } else if (n_wn && wn_unit) { // the whole Wiener descent of every unit inside one workgroup
+        run(2, [&](unsigned long long *tk) {
+            if (wn_unit_ng() == 2)
+                hipLaunchKernelGGL((wiener_unit_kernel<T, 2>), dim3(n_wn), dim3(512), 0, sw, A, (Descent *)dp(o_wds),
+                                   (const int32_t *)d_t0, (uint32_t *)dp(o_tcache), pc, tk);
+            else
+                hipLaunchKernelGGL((wiener_unit_kernel<T, 4>), dim3(n_wn), dim3(1024), 0, sw, A, (Descent *)dp(o_wds),
+                                   (const int32_t *)d_t0, (uint32_t *)dp(o_tcache), pc, tk);
+        });
+        HIP_TRY(hipGetLastError());
     } else if (n_wn) {
         HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
         HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
@@ -2134,7 +2476,21 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                            (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
-    if (npairs) {
+    if (npairs && sg_queue) { // the whole self-guided descent in one persistent kernel
+        HIP_TRY(hipMemsetAsync(qa + q_sq, 0, q_sarr - q_sq, st)); // counters and the log
+        hipLaunchKernelGGL(sgr_queue_start_kernel, dim3(n_all), dim3(64), 0, st, A, nplanes, (const Descent *)dp(o_sds),
+                           (Descent *)(qa + q_sds), (unsigned long long *)(qa + q_serr), (int32_t *)(qa + q_scand),
+                           (uint32_t *)(qa + q_scandm), (int32_t *)(qa + q_sarr), (const int32_t *)d_t0,
+                           (WnQueue *)(qa + q_sq), (int32_t *)(qa + q_slog), sq_cap);
+        run(3, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(sgr_queue_kernel<T>, dim3(std::min(nt_sg, sg_queue_grid())), dim3(256), 0, st, A,
+                               (Descent *)(qa + q_sds), (int32_t *)(qa + q_scand), (uint32_t *)(qa + q_scandm),
+                               (unsigned long long *)(qa + q_serr), (int32_t *)(qa + q_sarr), (const int32_t *)d_t0,
+                               (WnQueue *)(qa + q_sq), (int32_t *)(qa + q_slog), sq_cap, pc, tk);
+        });
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(dp(o_sds), qa + q_sds, sizeof(Descent) * (size_t)npairs, hipMemcpyDeviceToDevice, st));
+    } else if (npairs) {
         HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * SG_NC * (size_t)npairs, st));
         HIP_TRY(hipMemsetAsync(dp(o_ustamp), 0, 4 * (size_t)n_all, st));
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
@@ -2152,8 +2508,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         int         g = 0, head = 0, inflight = 0; // round index; ring of two batches in flight
         hipStream_t stream;
     } ch[2];
-    ch[0].live = n_wn > 0 && !wn_queue, ch[0].stream = sw;
-    ch[1].live = npairs > 0, ch[1].stream = st;
+    ch[0].live = n_wn > 0 && !wn_queue && !wn_unit, ch[0].stream = sw;
+    ch[1].live = npairs > 0 && !sg_queue, ch[1].stream = st;
     if (!s->h_flag) {
         HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&s->h_flag_dev, s->h_flag, 0));
@@ -2272,9 +2628,15 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
     if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), qa + q_wq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
+    if (npairs && sg_queue)
+        HIP_TRY(hipMemcpyAsync(hp(h_cnt + 16), qa + q_sq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (n_wn && wn_queue && ((const WnQueue *)hp(h_cnt))->error) {
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener work queue overflow", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    if (npairs && sg_queue && ((const WnQueue *)hp(h_cnt + 16))->error) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR self-guided work queue overflow", __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;
     }
     mark(3);
