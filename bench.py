@@ -93,7 +93,7 @@ def parse():
     ap.add_argument("--base-q-idx", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no HIP-event timing inside the LR search")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc", "traffic.json"),
                     help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
     ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
     ap.add_argument("--cpu-passes", type=int, default=6,
@@ -111,7 +111,51 @@ def parse():
                          "the in-loop filter path; no data-path collective, weak scaling); 'bands' = one frame per "
                          "step cut into row bands across the ranks (SURVEY §8e; RCCL exchanges, strong scaling)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
+    ap.add_argument("--stages", default="all", choices=("all", "cdef"),
+                    help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
+                         "configs 1/2)")
+    ap.add_argument("--no-matrix", action="store_true",
+                    help="skip the extra configurations (north_star matrix + config 1) run as child processes")
     return ap.parse_args()
+
+
+# the north_star reporting matrix beside the headline 4K 10-bit line: (label, argv) of child bench runs, started
+# before this process touches the GPU; their JSON lines are summarised under config.matrix
+MATRIX = [
+    ("config1_1080p8_cdef", ["--width", "1920", "--height", "1080", "--bit-depth", "8", "--stages", "cdef",
+                             "--cpu-grid", "4x4", "--cpu-passes", "120", "--steps", "20", "--warmup", "3",
+                             "--frames-in-flight", "1"]),
+    ("pipeline_1080p8", ["--width", "1920", "--height", "1080", "--bit-depth", "8", "--no-cpu-baseline",
+                         "--steps", "12", "--warmup", "2"]),
+    ("pipeline_1080p10", ["--width", "1920", "--height", "1080", "--bit-depth", "10", "--no-cpu-baseline",
+                          "--steps", "12", "--warmup", "2"]),
+    ("pipeline_4k8", ["--width", "3840", "--height", "2160", "--bit-depth", "8", "--no-cpu-baseline",
+                      "--steps", "10", "--warmup", "2"]),
+]
+
+
+def run_matrix():
+    """Each extra configuration as a child bench process (sequential, before this process initialises the GPU)."""
+    import subprocess
+    res = {}
+    for label, argv in MATRIX:
+        try:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--no-matrix"] + argv, capture_output=True,
+                               text=True, timeout=300)
+            line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode != 0 or not line:
+                res[label] = {"error": "exit %d: %s" % (r.returncode, r.stderr.strip()[-300:])}
+                continue
+            d = json.loads(line[-1])
+            c = d["config"]
+            res[label] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+                          "frames_in_flight": c["frames_in_flight"], "workload": c["workload"],
+                          "pipeline_frac_hbm": c.get("pipeline_roofline", {}).get("frac")}
+            if "cpu_baseline" in d:
+                res[label]["cpu_baseline"] = d["cpu_baseline"]
+        except (OSError, ValueError, subprocess.TimeoutExpired) as e:
+            res[label] = {"error": repr(e)[:300]}
+    return res
 
 
 def spawn_ranks(a):
@@ -162,7 +206,8 @@ def write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md
     f.write(np.ascontiguousarray(md_mvs, np.int32).tobytes())
 
 
-def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrls, md_refs, md_mvs, passes):
+def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrls, md_refs, md_mvs, passes,
+                           stages="all"):
     """The reference's own CPU path (oracle/_ref/ref_bench: its C with the AVX2/SSE2 kernels an AVX2 host binds) on the
     host's cores, over the same crops as cpu_baseline. The frame, mode info, CDEF controls, LR rate inputs, MD
     references and MVs are handed over in a file; the binary times itself (input loading excluded)."""
@@ -172,7 +217,9 @@ def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrl
     H, W = rec[0].shape
     nthr = min(cpu_threads(), gx * gy)
     def run(f, threads, npass):
-        res = subprocess.run([REF_BENCH, f.name, str(threads), str(npass)], capture_output=True, text=True, timeout=600)
+        env = dict(os.environ, REF_BENCH_STAGES="2" if stages == "cdef" else "15")
+        res = subprocess.run([REF_BENCH, f.name, str(threads), str(npass)], capture_output=True, text=True, timeout=600,
+                             env=env)
         if res.returncode != 0:
             raise RuntimeError("ref_bench failed (%d): %s" % (res.returncode, res.stderr.strip()[-400:]))
         kv = dict(t.split("=") for t in res.stdout.split()[1:])
@@ -192,11 +239,14 @@ def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrl
     cw, ch = (W // gx) & ~63, (H // gy) & ~63
     return {"value": round(px / dt / 1e6, 4), "unit": "Mpixels/s", "cores": nthr, "kind": "reference",
             "single_thread_value": round(px1 / dt1 / 1e6, 4), "cpu": model,
-            "sample": "the %d-bit frame cut into %dx%d crops of %dx%d, each through the same stages (DLF level search + "
-                      "filter, CDEF search + strength selection + apply at cdef_level %d, LR search + apply at wn/sg "
-                      "level 1, MD SAD/SSE/variance over 7 refs) by the reference's own C with its AVX2/SSE2 kernels "
-                      "(oracle/_ref/ref_bench), %d passes, %d host threads, %.1f s"
-                      % (bd, gx, gy, cw, ch, level, passes, nthr, dt)}
+            "sample": ("the %d-bit frame cut into %dx%d crops of %dx%d, each through " % (bd, gx, gy, cw, ch)) +
+                      ("CDEF search + strength selection + apply at cdef_level %d on the recon (the reference's "
+                       "%s path)" % (level, "8-bit (is_16bit_pipeline = 0)" if bd == 8 else "16-bit")
+                       if stages == "cdef" else
+                       "the same stages (DLF level search + filter, CDEF search + strength selection + apply at "
+                       "cdef_level %d, LR search + apply at wn/sg level 1, MD SAD/SSE/variance over 7 refs)" % level) +
+                      (" by the reference's own C with its AVX2/SSE2 kernels (oracle/_ref/ref_bench), %d passes, %d "
+                       "host threads, %.1f s" % (passes, nthr, dt))}
 
 
 def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, grid, lr_ctrls, lr_us, md_refs, md_mvs):
@@ -270,6 +320,9 @@ def main():
     rc = spawn_ranks(a)
     if rc is not None:
         sys.exit(rc)
+    matrix = None
+    if not a.no_matrix and int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.stages == "all":
+        matrix = run_matrix()  # before this process touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -354,6 +407,21 @@ def main():
             es = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if timed else None
             if timed:
                 es[0].record(stream)
+            if a.stages == "cdef":  # CDEF search + pick + apply on the recon (configs 1/2); events keep the layout
+                if timed:
+                    es[1].record(stream)
+                st.search(R, S, ctrls, q, sp)
+                if timed:
+                    es[2].record(stream)
+                prm, _ = st.pick(ctrls, q, lam, sp)
+                st.apply(R, O, prm, sp)
+                self.at_lr.set()
+                if timed:
+                    for i in (3, 4, 5):
+                        es[i].record(stream)
+                    es[6].record(stream), es[7].record(stream)
+                    self.ev.append(es)
+                return
             # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
             lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
             dl.filter_to(R, D, lfp, 0, 3, sp)
@@ -439,6 +507,7 @@ def main():
             raise errors[0]
 
     run_all(a.warmup, False)
+    svtgpu.transfer_bytes(reset=True)
     # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
     # of every launch, accumulated on the device and read once after the timed region; HIP-event packets around
     # each of the ~100 launches per search would cost ~20 us apiece) -- slot 0's searches
@@ -455,6 +524,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     lr_tot = lr.profile(False) if not a.no_kernel_timing else None
+    h2d, d2h = svtgpu.transfer_bytes(reset=True)
     if n > 1:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -484,21 +554,47 @@ def main():
             "note": "VALU-bound kernel (64 strengths per sample read); HBM fraction is low by "
                     "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))}
     lr_names = {"stats": "wiener_stats_kernel (+unit sums)", "sgr_filters": "sgr_flt_kernel",
-                "wiener_trials": "wiener_trial_kernel", "projection": "proj_err_kernel", "other": "lr descent kernels"}
-    dom = max(lr_cls, key=lambda c: lr_cls[c]["ms"])
-    if lr_cls[dom]["ms"] > search_ms:
+                "wiener_trials": "wiener_unit_kernel", "projection": "sgr_queue_kernel", "other": "lr descent kernels",
+                "sgr_moments": "sgr_mom_kernel"}
+    # the largest device-time kernel of the step among the streaming kernels (the persistent descent kernels'
+    # durations include their descents' dependent rounds, not streaming time)
+    dom = max(("stats", "sgr_filters", "sgr_moments"), key=lambda c: lr_cls[c]["ms"])
+    if a.stages == "all" and lr_cls[dom]["ms"] > search_ms:
         c = lr_cls[dom]
         ach = c["bytes"] / (c["ms"] * 1e-3) / 1e9
         roof = {"kernel": lr_names[dom], "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
                 "avg_launch_ms": round(c["ms"] / max(c["launches"], 1), 5), "launches_per_step": c["launches"],
                 "ms_per_step": round(c["ms"], 4),
-                "note": "largest device-time kernel class of the step; launch durations from the device's "
-                        "s_memrealtime clock (first workgroup start to last workgroup end, every launch of the timed "
-                        "steps); achieved = algorithmic bytes (samples + filter planes touched) / device time; the "
-                        "class is latency-bound (~17 KB and ~10 VALU ops per pixel per round, 64-73% of wave cycles "
-                        "waiting in the SQ counters; DESIGN.md 3.6), so its HBM fraction is low"}
+                "note": "largest device-time kernel of the step; launch durations from the device's s_memrealtime "
+                        "clock (first workgroup start to last workgroup end, every launch of slot 0's timed searches; "
+                        "with several frames in flight the other frames' kernels share the CUs); achieved = "
+                        "algorithmic bytes (CDEF samples read once, the 16 eps' int16 filter planes written once) / "
+                        "device time; the kernel is VALU-bound (A/B maps and both filters of 16 eps per pixel), so "
+                        "its HBM fraction is low by construction (DESIGN.md 3.5)"}
     roof["traffic"], roof["traffic_source"] = measured_traffic(a.traffic_json, roof["kernel"], bd)
+    # SURVEY §8(d) algorithmic bytes per frame by stage, over slot 0's stage times (HIP events; with several frames in
+    # flight the stages share the device with the other frames), and the pipeline total over the wall time per frame
+    SB = S_samples * B
+    nsb = ((W + 63) // 64) * ((H + 63) // 64)
+    stage_bytes = {"dlf_pick_filter": 2 * SB, "cdef_search": alg_bytes, "cdef_pick_apply": 2 * SB,
+                   "lr_search_apply": 4 * SB, "md_sad_sse_var": nsb * (1 + NREF) * 64 * 64 * B}
+    stage_t = {"dlf_pick_filter": dlf_ms, "cdef_search": search_ms, "cdef_pick_apply": cdef_rest_ms,
+               "lr_search_apply": lr_ms, "md_sad_sse_var": md_ms}
+    stage_roof = {k: {"alg_MB": round(stage_bytes[k] / 1e6, 2), "ms": round(stage_t[k], 4),
+                      "frac": round(stage_bytes[k] / max(stage_t[k], 1e-9) * 1e-6 / HBM_PEAK_GBS, 5)}
+                  for k in stage_bytes if a.stages == "all" or k in ("cdef_search", "cdef_pick_apply")}
+    pipe_bytes = (10 * SB if a.stages == "all" else 4 * SB)
+    frame_wall_ms = ms_per_step / frames_per_step
+    pipe_roof = {"alg_MB_per_frame": round(pipe_bytes / 1e6, 2), "ms_per_frame": round(frame_wall_ms, 4),
+                 "achieved_GBs": round(pipe_bytes / (frame_wall_ms * 1e-3) / 1e9, 2),
+                 "frac": round(pipe_bytes / (frame_wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                 "definition": "SURVEY §8(d): %s per frame, each input read once and each output written once; "
+                               "over the whole job's wall time per frame" % ("10*S*B" if a.stages == "all" else "4*S*B")}
+    nfr_timed = a.steps * frames_per_step / max(n, 1)
+    xfer = {"h2d_bytes_per_frame": round(h2d / nfr_timed), "d2h_bytes_per_frame": round(d2h / nfr_timed),
+            "note": "host<->device bytes of the frame-level entry points during the timed steps (per-frame results: "
+                    "DLF trial SSEs, CDEF pick, LR search records and chosen units; inputs stay resident in HBM)"}
     out = {
         "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
         "value": round(value, 3),
@@ -528,14 +624,23 @@ def main():
                                 "note": "the MD batch runs on a second stream concurrently with the LR stage; the LR "
                                         "search runs its Wiener and self-guided chains on two streams"},
                    "lr_search_kernel_ms": {c: round(v["ms"], 4) for c, v in lr_cls.items()},
-                   "dlf_levels": list(slots[0].lf_levels[-1]) if slots[0].lf_levels else None},
+                   "dlf_levels": list(slots[0].lf_levels[-1]) if slots[0].lf_levels else None,
+                   "stage_roofline": stage_roof, "pipeline_roofline": pipe_roof, "transfers": xfer},
         "roofline": roof,
     }
+    if a.stages == "cdef":
+        out["config"]["workload"] = ("cdef_search+pick+apply on the recon (SURVEY §8d configs 1/2); %dx%d %d-bit 4:2:0, "
+                                     "cdef_level %d (%d strengths)" % (W, H, bd, a.cdef_level, len(ctrls.strengths())))
+        out["metric"] = "CDEF search+apply Mpixels/s"
+        out["config"].pop("lr_search_kernel_ms")
+    if matrix is not None:
+        out["config"]["matrix"] = matrix
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
         s0 = slots[0]
         if a.cpu_kind == "reference" and os.path.exists(REF_BENCH):
             out["cpu_baseline"] = cpu_baseline_reference(s0.src, s0.rec, mi, ctrls, bd, a.cdef_level, q, lam,
-                                                         a.cpu_grid, lr_ctrls, md_ref_y, s0.md_mvs, a.cpu_passes)
+                                                         a.cpu_grid, lr_ctrls, md_ref_y, s0.md_mvs, a.cpu_passes,
+                                                         a.stages)
         else:
             out["cpu_baseline"] = cpu_baseline(s0.src, s0.rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_grid,
                                                lr_ctrls, lr_us, md_ref_y, s0.md_mvs)

@@ -680,14 +680,15 @@ int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const Svt
 int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
                            const SvtGpuLrUnitSearch *records, int32_t *frame_type_out, SvtGpuRestUnit *units_out);
 /* Device-time profile of the searches timed since the previous read, by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
- * + moments, 2 Wiener trials, 3 projection errors, 4 Wiener decomposition, descent advance rounds, SGR SSE.  Each
+ * (sgr_flt_kernel), 2 Wiener descents (unit kernel / queue / trial rounds), 3 self-guided descents (queue / projection
+ * rounds), 4 Wiener decomposition, descent advance rounds, SGR SSE, 5 self-guided projection moments.  Each
  * launch is timed from its first workgroup's start to its last workgroup's end on the device's 100 MHz
  * s_memrealtime clock (per-launch HIP event packets would cost more than these launches); bytes = algorithmic
  * HBM bytes of the class (compulsory reads/writes of the samples and filter planes the launches touch). */
 typedef struct SvtGpuLrProfile {
-    int32_t launches[5]; /* totals over `searches` searches */
-    float   ms[5];
-    double  bytes[5];
+    int32_t launches[6]; /* totals over `searches` searches */
+    float   ms[6];
+    double  bytes[6];
     int32_t searches;
 } SvtGpuLrProfile;
 /* enable != 0 turns timing of the following searches on (0 off): a bit mask of the classes to time (bit c =
@@ -695,6 +696,9 @@ typedef struct SvtGpuLrProfile {
  * (untimed classes read 0), which are then reset; reading synchronizes the device.  The timings accumulate on the
  * device: a timed search adds one small launch and no copies or host synchronization. */
 int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *totals);
+/* Host <-> device bytes moved by the frame-level entry points since the last reset (copies and the results read from
+ * mapped memory; per-block shims excluded) -- measurement only, no reference counterpart.  reset != 0 zeroes them. */
+int svtgpu_transfer_bytes(uint64_t *h2d, uint64_t *d2h, int32_t reset);
 /* controls of wn_filter_lvl / sg_filter_lvl (EncModeConfig.c:1329-1445); rate fields are left zero */
 int svtgpu_lr_controls_for_level(int32_t wn_level, int32_t sg_level, SvtGpuLrSearchControls *c);
 

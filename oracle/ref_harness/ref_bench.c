@@ -22,6 +22,9 @@
  *
  * usage: ref_bench <input.bin> <threads> [passes]   (input written by bench.py: header, CDEF controls, planes, mi, refs,
  *        MVs; every pass runs every crop once)
+ *        REF_BENCH_STAGES = bit mask of the stages run (1 DLF, 2 CDEF search + pick + apply, 4 LR, 8 MD; default 15);
+ *        8-bit input runs the CDEF stage alone on the reference's 8-bit path
+ *        (is_16bit_pipeline = 0: svt_aom_copy_sb8_16 from 8-bit recon, svt_compute_cdef_dist_8bit, 8-bit apply).
  * prints: ref_bench px=<luma pixels> seconds=<wall> threads=<T>
  */
 #include <pthread.h>
@@ -72,6 +75,11 @@ void     svt_cdef_filter_block_8xn_16_avx2(const uint16_t *const in, const int32
 uint64_t svt_aom_compute_cdef_dist_16bit_avx2(const uint16_t *dst, int32_t dstride, const uint16_t *src,
                                               const CdefList *dlist, int32_t cdef_count, BlockSize bsize,
                                               int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+uint64_t svt_aom_compute_cdef_dist_8bit_avx2(const uint8_t *dst8, int32_t dstride, const uint8_t *src8,
+                                             const CdefList *dlist, int32_t cdef_count, BlockSize bsize,
+                                             int32_t coeff_shift, int32_t pli, uint8_t subsampling_factor);
+void     svt_aom_copy_rect8_8bit_to_16bit_avx2(uint16_t *dst, int32_t dstride, const uint8_t *src, int32_t sstride,
+                                               int32_t v, int32_t h);
 uint64_t svt_search_one_dual_avx2(int *lev0, int *lev1, int nb_strengths, uint64_t **mse[2], int sb_count,
                                   int start_gi, int end_gi);
 uint64_t svt_full_distortion_kernel16_bits_avx2(uint8_t *input, uint32_t input_offset, uint32_t input_stride,
@@ -108,9 +116,9 @@ static void bind_kernels(void) {
     svt_aom_cdef_find_dir                  = svt_aom_cdef_find_dir_avx2;
     svt_aom_cdef_find_dir_dual             = svt_aom_cdef_find_dir_dual_avx2;
     svt_compute_cdef_dist_16bit            = svt_aom_compute_cdef_dist_16bit_avx2;
-    svt_compute_cdef_dist_8bit             = svt_aom_compute_cdef_dist_8bit_c;
+    svt_compute_cdef_dist_8bit             = svt_aom_compute_cdef_dist_8bit_avx2;
     svt_search_one_dual                    = svt_search_one_dual_avx2;
-    svt_aom_copy_rect8_8bit_to_16bit       = svt_aom_copy_rect8_8bit_to_16bit_c;
+    svt_aom_copy_rect8_8bit_to_16bit       = svt_aom_copy_rect8_8bit_to_16bit_avx2;
     svt_av1_wiener_convolve_add_src        = svt_av1_wiener_convolve_add_src_avx2;
     svt_av1_highbd_wiener_convolve_add_src = svt_av1_highbd_wiener_convolve_add_src_avx2;
     svt_av1_selfguided_restoration         = svt_av1_selfguided_restoration_avx2;
@@ -257,6 +265,13 @@ static double now(void) {
 static double          g_stage[5]; /* summed over threads: DLF, CDEF search, CDEF pick + apply, LR, MD */
 static pthread_mutex_t g_stage_lock = PTHREAD_MUTEX_INITIALIZER;
 static int             g_verbose;
+static int             g_stages = 15;
+
+static uint8_t *to8(const uint16_t *p, size_t n) { /* an 8-bit plane of the crop (the 8-bit pipeline's buffers) */
+    uint8_t *o = xmalloc(n);
+    for (size_t i = 0; i < n; i++) o[i] = (uint8_t)p[i];
+    return o;
+}
 
 static void run_crop(const Crop *c, int32_t *tmpbuf) {
     double ts[6];
@@ -315,11 +330,21 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     svt_av1_loop_filter_init(pcs);
     const int last[4] = {32, 32, 16, 16}; /* bench.py's previous-frame levels */
     struct LoopFilter *lf = &fh->loop_filter_params;
-    lf->filter_level[0] = lf->filter_level[1] = dlf_search(pcs, &trial, rec, src, last, 0, 2, W, H);
-    lf->filter_level_u = dlf_search(pcs, &trial, rec, src, last, 1, 0, W, H);
-    lf->filter_level_v = dlf_search(pcs, &trial, rec, src, last, 2, 0, W, H);
-    svt_av1_loop_filter_frame(&pic, pcs, 0, 3); /* rec[] is now the DLF output */
+    if (g_stages & 1) {
+        lf->filter_level[0] = lf->filter_level[1] = dlf_search(pcs, &trial, rec, src, last, 0, 2, W, H);
+        lf->filter_level_u = dlf_search(pcs, &trial, rec, src, last, 1, 0, W, H);
+        lf->filter_level_v = dlf_search(pcs, &trial, rec, src, last, 2, 0, W, H);
+        svt_av1_loop_filter_frame(&pic, pcs, 0, 3); /* rec[] is now the DLF output */
+    }
     ts[1] = now();
+    /* the 8-bit pipeline's planes (8-bit input: CDEF only) */
+    const int is16 = bd > 8;
+    uint8_t  *src8[3] = {NULL, NULL, NULL}, *rec8[3] = {NULL, NULL, NULL}, *cdf8[3] = {NULL, NULL, NULL};
+    if (!is16)
+        for (int p = 0; p < 3; p++) {
+            const size_t n = (size_t)(W >> (p > 0)) * (H >> (p > 0));
+            src8[p] = to8(src[p], n), rec8[p] = to8(rec[p], n), cdf8[p] = to8(rec[p], n);
+        }
     /* ---- CDEF search: cdef_seg_search over the crop (one segment) ---- */
     const int nvfb = (mi_rows + 15) / 16, nhfb = (mi_cols + 15) / 16, nfb = nvfb * nhfb;
     const int nstr = cctl.first_pass_fs_num + cctl.default_second_pass_fs_num;
@@ -331,7 +356,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     DECLARE_ALIGNED(32, uint16_t, tmp_dst[1 << (MAX_SB_SIZE_LOG2 * 2)]);
     const int pri_damping = 3 + (q >> 6);
     static const int bsz[3] = {BLOCK_8X8, BLOCK_4X4, BLOCK_4X4};
-    for (int fbr = 0; fbr < nvfb; fbr++)
+    for (int fbr = 0; fbr < nvfb && (g_stages & 2); fbr++)
         for (int fbc = 0; fbc < nhfb; fbc++) {
             const int fb = fbr * nhfb + fbc, lr = 16 * fbr, lc = 16 * fbc;
             const int nhb = AOMMIN(16, mi_cols - lc), nvb = AOMMIN(16, mi_rows - lr);
@@ -347,8 +372,9 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
                 const int yoff = CDEF_VBORDER * (fbr != 0), xoff = CDEF_HBORDER * (fbc != 0);
                 const int ysize = (nvb << mi_l2) + CDEF_VBORDER * (fbr + 1 < nvfb) + yoff;
                 const int xsize = (nhb << mi_l2) + CDEF_HBORDER * (fbc + 1 < nhfb) + xoff;
-                svt_aom_copy_sb8_16(&in[-yoff * CDEF_BSTRIDE - xoff], CDEF_BSTRIDE, (uint8_t *)rec[pli],
-                                    (lr << mi_l2) - yoff, (lc << mi_l2) - xoff, pw, ysize, xsize, 1);
+                svt_aom_copy_sb8_16(&in[-yoff * CDEF_BSTRIDE - xoff], CDEF_BSTRIDE,
+                                    is16 ? (uint8_t *)rec[pli] : rec8[pli], (lr << mi_l2) - yoff, (lc << mi_l2) - xoff,
+                                    pw, ysize, xsize, is16);
                 const uint8_t ssf = AOMMIN(cctl.subsampling_factor, pli ? 1 : 4);
                 for (int gi = 0; gi < nstr; gi++) {
                     const int first = gi < cctl.first_pass_fs_num;
@@ -359,11 +385,15 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
                     }
                     const int fs = first ? cctl.default_first_pass_fs[k] : cctl.default_second_pass_fs[k];
                     const int ps = fs / CDEF_SEC_STRENGTHS, ss = fs % CDEF_SEC_STRENGTHS;
-                    svt_cdef_filter_fb(NULL, tmp_dst, 0, in, sub, sub, dir, &dirinit, var, pli, dlist, cnt, ps,
-                                       ss + (ss == 3), pri_damping, pri_damping, cs, ssf);
-                    const uint64_t d = svt_compute_cdef_dist_16bit(src[pli] + (lr << mi_l2) * pw + (lc << mi_l2), pw,
-                                                                   tmp_dst, dlist, cnt, (BlockSize)bsz[pli], cs, pli,
-                                                                   ssf);
+                    svt_cdef_filter_fb(is16 ? NULL : (uint8_t *)tmp_dst, is16 ? tmp_dst : NULL, 0, in, sub, sub, dir,
+                                       &dirinit, var, pli, dlist, cnt, ps, ss + (ss == 3), pri_damping, pri_damping,
+                                       cs, ssf);
+                    const size_t   o = (size_t)(lr << mi_l2) * pw + (lc << mi_l2);
+                    const uint64_t d =
+                        is16 ? svt_compute_cdef_dist_16bit(src[pli] + o, pw, tmp_dst, dlist, cnt, (BlockSize)bsz[pli], cs,
+                                                           pli, ssf)
+                             : svt_compute_cdef_dist_8bit(src8[pli] + o, pw, (uint8_t *)tmp_dst, dlist, cnt,
+                                                          (BlockSize)bsz[pli], cs, pli, ssf);
                     if (pli < 2)
                         mse[pli * nfb + fb][gi] = d * ssf;
                     else
@@ -375,7 +405,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     /* ---- CDEF pick: finish_cdef_search's greedy + RD (EbEncCdef.c:697-890) ---- */
     uint64_t **m0 = xmalloc(sizeof(uint64_t *) * nfb), **m1 = xmalloc(sizeof(uint64_t *) * nfb);
     int       *fbl = xmalloc(sizeof(int) * nfb), sb_count = 0;
-    for (int fb = 0; fb < nfb; fb++)
+    for (int fb = 0; fb < nfb && (g_stages & 2); fb++)
         if (!skipfb[fb]) {
             if (cctl.zero_fs_cost_bias)
                 for (int p = 0; p < 2; p++) mse[p * nfb + fb][0] = (cctl.zero_fs_cost_bias * mse[p * nfb + fb][0]) >> 6;
@@ -384,7 +414,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     uint64_t **mm[2] = {m0, m1};
     int        best_lev[4][2][16], nbits = 0;
     uint64_t   best_cost = (uint64_t)1 << 63;
-    for (int i = 0; i <= 3; i++) {
+    for (int i = 0; i <= 3 && (g_stages & 2); i++) {
         const int nb = 1 << i;
         int      *l0 = best_lev[i][0], *l1 = best_lev[i][1];
         memset(l0, 0, sizeof best_lev[i][0]), memset(l1, 0, sizeof best_lev[i][1]);
@@ -432,14 +462,17 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
             const int yoff = CDEF_VBORDER * (fbr != 0), xoff = CDEF_HBORDER * (fbc != 0);
             const int ysize = (nvb << mi_l2) + CDEF_VBORDER * (fbr + 1 < nvfb) + yoff;
             const int xsize = (nhb << mi_l2) + CDEF_HBORDER * (fbc + 1 < nhfb) + xoff;
-            svt_aom_copy_sb8_16(&in[-yoff * CDEF_BSTRIDE - xoff], CDEF_BSTRIDE, (uint8_t *)rec[pli],
-                                (lr << mi_l2) - yoff, (lc << mi_l2) - xoff, pw, ysize, xsize, 1);
-            svt_cdef_filter_fb(NULL, cdf[pli] + (lr << mi_l2) * pw + (lc << mi_l2), pw, in, sub, sub, dir, &dirinit,
+            svt_aom_copy_sb8_16(&in[-yoff * CDEF_BSTRIDE - xoff], CDEF_BSTRIDE,
+                                is16 ? (uint8_t *)rec[pli] : rec8[pli], (lr << mi_l2) - yoff, (lc << mi_l2) - xoff, pw,
+                                ysize, xsize, is16);
+            const size_t o = (size_t)(lr << mi_l2) * pw + (lc << mi_l2);
+            svt_cdef_filter_fb(is16 ? NULL : cdf8[pli] + o, is16 ? cdf[pli] + o : NULL, pw, in, sub, sub, dir, &dirinit,
                                var, pli, dlist, cnt, lvl[pli], sec[pli], pri_damping, pri_damping, cs, 1);
         }
     }
     ts[3] = now();
     /* ---- LR: whole-crop search (one segment) + RD finish + apply ---- */
+    if (g_stages & 4) {
     cm->frm_size.frame_width = cm->frm_size.superres_upscaled_width = W;
     cm->frm_size.frame_height = cm->frm_size.superres_upscaled_height = H;
     cm->subsampling_x = cm->subsampling_y = 1, cm->use_highbitdepth = bd > 8, cm->bit_depth = bd;
@@ -470,6 +503,8 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     restoration_seg_search(tmpbuf, &yc, &ys, &yt, pcs, 0);
     rest_finish_search(pcs);
     svt_av1_loop_restoration_filter_frame(tmpbuf, &yc, cm, 0);
+    free(yd.buffer_alloc), free(yc.buffer_alloc), free(ys.buffer_alloc), free(yt.buffer_alloc);
+    }
     ts[4] = now();
     if (g_verbose) {
         int nt[3][4] = {{0}};
@@ -487,7 +522,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     static const int sh[19] = {4, 8, 4, 8, 16, 8, 16, 32, 16, 32, 64, 32, 64, 16, 4, 32, 8, 64, 16};
     const int        nref = hdr[H_NREF], Wf = hdr[H_W], Hf = hdr[H_H], nsbx = (Wf + 63) / 64;
     volatile uint64_t sink = 0;
-    for (int sy = 0; sy < H; sy += 64)
+    for (int sy = 0; sy < H && (g_stages & 8); sy += 64)
         for (int sx = 0; sx < W; sx += 64) {
             const int sb = ((c->y0 + sy) / 64) * nsbx + (c->x0 + sx) / 64;
             uint16_t *s  = g_src[0] + (size_t)(c->y0 + sy) * Wf + c->x0 + sx;
@@ -516,7 +551,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     /* buffers of the crop (the picture structures' own allocations are left to process exit) */
     for (int p = 0; p < 3; p++) free(src[p]), free(rec[p]), free(trl[p]), free(cdf[p]);
     free(mse), free(skipfb), free(m0), free(m1), free(fbl), free(blocks), free(cells);
-    free(yd.buffer_alloc), free(yc.buffer_alloc), free(ys.buffer_alloc), free(yt.buffer_alloc);
+    for (int p = 0; p < 3; p++) free(src8[p]), free(rec8[p]), free(cdf8[p]);
 }
 
 /* ------------------------------------------------------------------------------------------- threads */
@@ -551,8 +586,9 @@ int main(int argc, char **argv) {
     read_all(f, hdr, sizeof hdr);
     read_all(f, &cctl, sizeof cctl);
     const int W = hdr[H_W], H = hdr[H_H], nref = hdr[H_NREF];
-    if (hdr[H_BD] != 10 || (W & 63) || (H & 7) || nref < 0 || nref > 16) {
-        fprintf(stderr, "ref_bench: unsupported input (10-bit, width multiple of 64)\n");
+    if (getenv("REF_BENCH_STAGES")) g_stages = atoi(getenv("REF_BENCH_STAGES")) & 15;
+    if ((hdr[H_BD] != 10 && !(hdr[H_BD] == 8 && g_stages == 2)) || (W & 63) || (H & 7) || nref < 0 || nref > 16) {
+        fprintf(stderr, "ref_bench: unsupported input (10-bit, or 8-bit with the CDEF stage alone; width multiple of 64)\n");
         return 1;
     }
     for (int k = 0; k < 2; k++) {

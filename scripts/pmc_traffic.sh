@@ -6,10 +6,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/traffic
 export TMPDIR=/tmp
-K="wiener_trial|proj_err|sgr_flt|wiener_stats|cdef_search|dlf_tile|md_"
+K="sgr_flt|sgr_mom|wiener_unit|sgr_queue|wiener_stats|cdef_search|cdef_apply|dlf_tile|lr_apply|md_dist|unit_sums"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/ubench/fetch_cal.hip -o gpurun_out/traffic/fetch_cal &&
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/traffic/cal_fetch -o run --output-format csv -- gpurun_out/traffic/fetch_cal > gpurun_out/traffic/cal.log 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/traffic/cal_write -o run --output-format csv -- gpurun_out/traffic/fetch_cal >> gpurun_out/traffic/cal.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d gpurun_out/traffic/bench_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/traffic/bench_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d gpurun_out/traffic/bench_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/traffic/bench_write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d gpurun_out/traffic/bench_fetch -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-matrix > gpurun_out/traffic/bench_fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d gpurun_out/traffic/bench_write -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-matrix > gpurun_out/traffic/bench_write.log 2>&1
 echo "exit $?"

@@ -204,6 +204,7 @@ extern "C" int svtgpu_cdef_set_block_mask(SvtGpuCdefFrameState *s, const uint8_t
         return SVTGPU_OK;
     }
     s->mask_all = 0;
+    svtgpu_count_xfer(0, (size_t)s->geo.b8_rows * s->geo.b8_cols);
     HIP_TRY(hipMemcpyAsync(s->d_mask, host_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols, hipMemcpyHostToDevice,
                            pick_stream(s->ctx, stream)));
     return SVTGPU_OK;
@@ -236,6 +237,7 @@ extern "C" int svtgpu_cdef_set_fb_bsize(SvtGpuCdefFrameState *s, const uint8_t *
             k = (int8_t)(b == 15 ? 1 : b == 14 ? 2 : 3);
         s->h_fb_kind[f] = k;
     }
+    svtgpu_count_xfer(0, s->nfb);
     HIP_TRY(hipMemcpyAsync(s->d_fb_kind, s->h_fb_kind, s->nfb, hipMemcpyHostToDevice, pick_stream(s->ctx, stream)));
     HIP_TRY(hipStreamSynchronize(pick_stream(s->ctx, stream))); // the host array may be reused at once
     return SVTGPU_OK;
@@ -294,6 +296,7 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
 extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream) {
     if (!s || !fb_strength)
         return SVTGPU_ERR_INVALID_ARG;
+    svtgpu_count_xfer(0, s->nfb);
     HIP_TRY(hipMemcpyAsync(s->d_fb_strength, fb_strength, s->nfb, hipMemcpyHostToDevice, pick_stream(s->ctx, stream)));
     return SVTGPU_OK;
 }
@@ -319,6 +322,7 @@ extern "C" int svtgpu_cdef_read_state(SvtGpuCdefFrameState *s, uint64_t *mse, ui
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t  st  = pick_stream(s->ctx, stream);
     const size_t nfb = s->nfb;
+    svtgpu_count_xfer(1, (mse ? nfb * 2 * 64 * 8 : 0) + (skip ? nfb : 0) + (dir ? nfb * 64 : 0) + (var ? nfb * 64 * 4 : 0));
     if (mse) HIP_TRY(hipMemcpyAsync(mse, s->d_mse, nfb * 2 * 64 * 8, hipMemcpyDeviceToHost, st));
     if (skip) HIP_TRY(hipMemcpyAsync(skip, s->d_skip, nfb, hipMemcpyDeviceToHost, st));
     if (dir) HIP_TRY(hipMemcpyAsync(dir, s->d_dir, nfb * 64, hipMemcpyDeviceToHost, st));

@@ -335,6 +335,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         params->cdef_uv_strength[j] = (uint8_t)h_out->gi[16 + j];
     }
     if (fb_strength_out) memcpy(fb_strength_out, h_fbs, nfb);
+    svtgpu_count_xfer(1, sizeof(PickOut) + (fb_strength_out ? nfb : 0)); // mapped memory
     // gi -> strength code (filter_map, EbEncCdef.c:911-919); damping (:921)
     const int nf = ctrls->first_pass_fs_num;
     for (int i = 0; i < nb; i++) {

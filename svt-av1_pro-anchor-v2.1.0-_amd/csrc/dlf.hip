@@ -613,7 +613,11 @@ int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
         a.seq    = ++s->seq;
         if (int rc = launch_tile(a, recon->bytes_per_sample, true, st)) return rc;
         if (int rc = svtgpu_wait_seq(s->h_sse + MAX_JOBS * MAX_TRIALS, a.seq, st)) return rc;
-        for (int j = 0; j < a.njob; j++) srch[who[j]]->feed(lv[who[j]], m[j], s->h_sse + j * MAX_TRIALS);
+        svtgpu_count_xfer(1, 8); // the sequence word
+        for (int j = 0; j < a.njob; j++) {
+            svtgpu_count_xfer(1, 8 * (size_t)m[j]); // the job's trial SSEs (mapped memory)
+            srch[who[j]]->feed(lv[who[j]], m[j], s->h_sse + j * MAX_TRIALS);
+        }
     }
 }
 
@@ -685,6 +689,7 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
     }
     hipStream_t st = pick_stream(s->ctx, stream);
     HIP_TRY(hipMemcpyAsync(s->d_mi, mi, n * sizeof(SvtGpuLfMi), hipMemcpyHostToDevice, st));
+    svtgpu_count_xfer(0, n * sizeof(SvtGpuLfMi));
     for (int c = 0; c < 2; c++)
         for (int d = 0; d < 2; d++) {
             hipLaunchKernelGGL(dlf_edge_records_kernel, dim3((s->uw[c] + 127) / 128, s->uh[c]), dim3(128), 0, st,

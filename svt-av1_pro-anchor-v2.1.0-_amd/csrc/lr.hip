@@ -308,6 +308,7 @@ extern "C" int svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpu
     }
     hipStream_t st = pick_stream(s->ctx, stream);
     HIP_TRY(hipMemcpyAsync(s->d_units[plane], units, sizeof(SvtGpuRestUnit) * n, hipMemcpyHostToDevice, st));
+    svtgpu_count_xfer(0, sizeof(SvtGpuRestUnit) * n);
     HIP_TRY(hipStreamSynchronize(st));
     return SVTGPU_OK;
 }

@@ -1969,21 +1969,22 @@ __global__ __launch_bounds__(PROF_NL) void prof_fold_kernel(unsigned long long *
     if (t0 != ~0ull && t1 >= t0) atomicAdd(&acc[cls.c[i]], t1 - t0);
 }
 
+constexpr int NCLS = 6; // classes of SvtGpuLrProfile
 struct LrProfiler {
     unsigned long long *d_clk = nullptr; // [PROF_NL][PROF_SP] workgroup starts (min), then the same of ends (max)
     unsigned long long *d_px  = nullptr; // [3][PROF_SP] evaluated pixels: trials, projection (pixel, ep), projection tiles
     unsigned long long *d_acc = nullptr; // [5] ticks per class, over the searches since the last read
     int                 nl = 0, searches = 0;
     ProfClasses         cls{};
-    int32_t             launches[5] = {0, 0, 0, 0, 0};
-    double              static_bytes[5] = {0, 0, 0, 0, 0}, bps = 2;
+    int32_t             launches[NCLS] = {0, 0, 0, 0, 0, 0};
+    double              static_bytes[NCLS] = {0, 0, 0, 0, 0, 0}, bps = 2;
     bool                ok   = false;
-    int32_t             mask = 31; // classes timed (bit c)
+    int32_t             mask = 63; // classes timed (bit c)
     LrProfiler() {
         ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess &&
-             hipMalloc(&d_acc, 8 * 5) == hipSuccess && hipMemset(d_clk, 0xFF, 8 * PROF_NL * PROF_SP) == hipSuccess &&
+             hipMalloc(&d_acc, 8 * NCLS) == hipSuccess && hipMemset(d_clk, 0xFF, 8 * PROF_NL * PROF_SP) == hipSuccess &&
              hipMemset(d_clk + PROF_NL * PROF_SP, 0, 8 * PROF_NL * PROF_SP) == hipSuccess &&
-             hipMemset(d_px, 0, 24 * PROF_SP) == hipSuccess && hipMemset(d_acc, 0, 8 * 5) == hipSuccess &&
+             hipMemset(d_px, 0, 24 * PROF_SP) == hipSuccess && hipMemset(d_acc, 0, 8 * NCLS) == hipSuccess &&
              hipDeviceSynchronize() == hipSuccess;
     }
     ~LrProfiler() {
@@ -2007,7 +2008,7 @@ struct LrProfiler {
         return SVTGPU_OK;
     }
     int read(SvtGpuLrProfile *out) { // totals since the last read, then reset
-        unsigned long long acc[5], pxs[3 * PROF_SP], px[3] = {0, 0, 0};
+        unsigned long long acc[NCLS], pxs[3 * PROF_SP], px[3] = {0, 0, 0};
         HIP_TRY(hipDeviceSynchronize());
         HIP_TRY(hipMemcpy(acc, d_acc, sizeof acc, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(pxs, d_px, sizeof pxs, hipMemcpyDeviceToHost));
@@ -2016,7 +2017,7 @@ struct LrProfiler {
         HIP_TRY(hipDeviceSynchronize());
         for (int k = 0; k < 3 * PROF_SP; k++) px[k / PROF_SP] += pxs[k];
         std::memset(out, 0, sizeof *out);
-        for (int c = 0; c < 5; c++) {
+        for (int c = 0; c < NCLS; c++) {
             out->launches[c] = launches[c];
             out->ms[c]       = (float)(acc[c] * 1e-5); // 100 MHz ticks
             out->bytes[c]    = static_bytes[c];
@@ -2025,7 +2026,7 @@ struct LrProfiler {
         out->bytes[3] += (double)px[1] * 4 + (double)px[2] * 2 * bps; // flt per (pixel, ep), x/source per tile
         out->searches = searches;
         searches      = 0;
-        for (int c = 0; c < 5; c++) launches[c] = 0, static_bytes[c] = 0;
+        for (int c = 0; c < NCLS; c++) launches[c] = 0, static_bytes[c] = 0;
         return SVTGPU_OK;
     }
 };
@@ -2360,6 +2361,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
             std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
             HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
+            svtgpu_count_xfer(0, plan_span);
             s->plan_bytes.assign(pl, pl + plan_span);
             s->plan_work = s->d_work;
         }
@@ -2405,7 +2407,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (nt_sg) {
         run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
-        run(1, [&](unsigned long long *tk) {
+        run(5, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_mom_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (long long *)dp(o_mom), tk);
         });
         HIP_TRY(hipGetLastError());
@@ -2585,6 +2587,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 const unsigned long long *f = s->h_flag + (c * 2 + C.head) * 2;
                 if (__atomic_load_n(f, __ATOMIC_ACQUIRE) != want[c * 2 + C.head]) continue;
                 C.live = __atomic_load_n(f + 1, __ATOMIC_RELAXED) > 0;
+                svtgpu_count_xfer(1, 16); // the batch's mapped words
                 C.head ^= 1, C.inflight--, consumed = true;
                 tr(C.live ? "landed-live" : "landed-done", c, C.g);
                 if (C.g > MAX_ROUNDS) { // a descent always terminates; guard anyway (an internal failure)
@@ -2627,6 +2630,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
+    svtgpu_count_xfer(1, res_span + ((n_wn && wn_queue) ? sizeof(WnQueue) : 0) + ((npairs && sg_queue) ? sizeof(WnQueue) : 0));
     if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), qa + q_wq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
     if (npairs && sg_queue)
         HIP_TRY(hipMemcpyAsync(hp(h_cnt + 16), qa + q_sq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
@@ -2677,19 +2681,23 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (frame_type) // d_units holds the planes back to back in the same order: one upload
         HIP_TRY(hipMemcpyAsync(s->d_units[0], out, sizeof(SvtGpuRestUnit) * n_all, hipMemcpyHostToDevice, st));
+    if (frame_type) svtgpu_count_xfer(0, sizeof(SvtGpuRestUnit) * n_all);
     if (prof) { // algorithmic bytes per class (sample bytes bps, filter planes int16); the pixel-count parts at read
         const double bps = (double)sizeof(T);
-        double       all = 0, wn = 0, sgb = 0, sgp = 0;
+        double       all = 0, wn = 0, sgb = 0, sgp = 0, sgw = 0; // sgw: filter planes written (equal r = 1 shared)
         for (int p = 0; p < nplanes; p++) {
             double area = 0;
             for (int i = pp[p].tile_base; i < pp[p].tile_base + pp[p].nt; i++) area += (double)tiles[i].w * tiles[i].h;
             all += area;
             if (pp[p].wn) wn += area;
             if (pp[p].sg) sgb += area, sgp += area * pp[p].ne;
+            for (int k = 0; k < pp[p].ne; k++)
+                sgw += area * ((kHostSgrR[A.pl[p].eps[k]][0] > 0) + (kHostSgrR[A.pl[p].eps[k]][1] > 0 && A.pl[p].f1e[k] == k));
         }
         prof->bps = bps;
         prof->static_bytes[0] += (all + wn) * 2 * bps; // unit sums, statistics: x and source
-        prof->static_bytes[1] += sgb * 2 * bps + sgp * 4; // x and source in, flt0/flt1 out
+        prof->static_bytes[1] += sgb * bps + sgw * 2;     // filters: x in, the int16 planes out (each once)
+        prof->static_bytes[5] += sgb * 2 * bps + sgp * 4; // moments: x, source and every ep's two planes in
         prof->static_bytes[4] += sgb * (4 + 2 * bps);     // the chosen ep's SSE
     }
     // no wait for the units upload: the next search waits for this event before it rewrites the pinned staging
@@ -2747,7 +2755,7 @@ extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfi
         s->prof = pr;
     }
     if (enable) {
-        pr->mask = enable < 0 ? 31 : enable & 31;
+        pr->mask = enable < 0 ? 63 : enable & 63;
     } else if (pr) {
         delete pr;
         s->prof = nullptr;

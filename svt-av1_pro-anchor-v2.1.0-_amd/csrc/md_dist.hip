@@ -490,6 +490,7 @@ extern "C" int svtgpu_md_set_mvs(SvtGpuMdBatch *b, const int16_t *mv, void *stre
     hipStream_t st = pick_stream(b->ctx, stream);
     HIP_TRY(hipMemcpyAsync(b->d_mv, mv, (size_t)b->nsbx * b->nsby * b->nref * 2 * sizeof(int16_t),
                            hipMemcpyHostToDevice, st));
+    svtgpu_count_xfer(0, (size_t)b->nsbx * b->nsby * b->nref * 2 * sizeof(int16_t));
     HIP_TRY(hipStreamSynchronize(st));
     return SVTGPU_OK;
 }
@@ -535,6 +536,7 @@ extern "C" int svtgpu_md_read(SvtGpuMdBatch *b, uint32_t *out, int32_t sb_begin,
     if (!b || !out || sb_begin < 0 || sb_end > nsb || sb_begin > sb_end) return SVTGPU_ERR_INVALID_ARG;
     hipStream_t  st  = pick_stream(b->ctx, stream);
     const size_t row = (size_t)b->nref * 3 * kBlocks;
+    svtgpu_count_xfer(1, (size_t)(sb_end - sb_begin) * row * sizeof(uint32_t));
     HIP_TRY(hipMemcpyAsync(out, b->d_out + sb_begin * row, (sb_end - sb_begin) * row * sizeof(uint32_t),
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

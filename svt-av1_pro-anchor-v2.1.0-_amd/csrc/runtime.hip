@@ -1,4 +1,5 @@
 // runtime.hip — device/context/frame management of the C ABI (include/svtgpu.h).
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -94,6 +95,15 @@ SvtGpuContext        *svtgpu_default_context() {
     return g_default_ctx;
 }
 hipStream_t svtgpu_default_stream() { return svtgpu_default_context()->stream; }
+
+static std::atomic<unsigned long long> g_xfer[2];
+void svtgpu_count_xfer(int d2h, size_t bytes) { g_xfer[d2h ? 1 : 0] += bytes; }
+extern "C" int svtgpu_transfer_bytes(uint64_t *h2d, uint64_t *d2h, int32_t reset) {
+    if (h2d) *h2d = g_xfer[0].load();
+    if (d2h) *d2h = g_xfer[1].load();
+    if (reset) g_xfer[0] = 0, g_xfer[1] = 0;
+    return SVTGPU_OK;
+}
 
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st) {
     const auto t0 = std::chrono::steady_clock::now();

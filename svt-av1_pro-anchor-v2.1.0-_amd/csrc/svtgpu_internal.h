@@ -133,6 +133,8 @@ hipStream_t svtgpu_default_stream();
 // the stream's own synchronize wakes the host up tens of microseconds later, once per host round trip.  Falls
 // back to synchronizing `st` (and fails if the word is still missing after it).
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st);
+// host <-> device bytes of the frame-level entry points (copies and mapped-memory results), for the bench's report
+void svtgpu_count_xfer(int d2h, size_t bytes);
 SvtGpuContext *svtgpu_default_context();
 static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;

@@ -174,7 +174,7 @@ class LrSearchControls(ctypes.Structure):
                 ("sgrproj_restore_cost", ctypes.c_int32 * 2)]
 
 
-LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 5), ("ms", np.float32, 5), ("bytes", np.float64, 5),
+LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 6), ("ms", np.float32, 6), ("bytes", np.float64, 6),
                              ("searches", np.int32)], align=True)
 LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYPE), ("sgrproj", REST_UNIT_DTYPE)],
                                 align=True)
@@ -317,6 +317,7 @@ _SIGS = {
     "svtgpu_lr_search_units": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P, _P, _P, _P]),
     "svtgpu_lr_finish_plane": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _I32, _I32, _P, _P, _P]),
     "svtgpu_lr_profile": (ctypes.c_int, [_P, _I32, _P]),
+    "svtgpu_transfer_bytes": (ctypes.c_int, [_P, _P, _I32]),
 }
 
 _lib = None
@@ -643,7 +644,7 @@ class LrState:
                                            stream))
         return records
 
-    PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other")
+    PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other", "sgr_moments")
 
     def profile(self, enable=True):
         """svtgpu_lr_profile: device-clock timing of the searches (enable: True = every class, a class name or a
@@ -753,3 +754,11 @@ def declared_symbols(header=HEADER_PATH):
     txt = open(header).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(svtgpu_[a-z0-9_]+)\s*\(", txt)))
+
+
+def transfer_bytes(reset=False):
+    """svtgpu_transfer_bytes: (host-to-device, device-to-host) bytes moved by the frame-level entry points since the
+    last reset (copies and results read from mapped memory)."""
+    h2d, d2h = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib().svtgpu_transfer_bytes(ctypes.byref(h2d), ctypes.byref(d2h), 1 if reset else 0))
+    return int(h2d.value), int(d2h.value)
