@@ -571,6 +571,56 @@ void    svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offs
 
 
 /* =========================================================================================
+ * Open-loop motion-estimation SAD
+ * ========================================================================================= */
+#ifndef SVTGPU_BOOL_T
+#define SVTGPU_BOOL_T
+typedef uint8_t Bool; /* EbSvtAv1.h:82 */
+#endif
+/* RTCD-compatible shims (synchronous, host pointers), each replacing the pointer it names:
+ * svt_ext_all_sad_calculation_8x8_16x16 (aom_dsp_rtcd.h:850; C EbMotionEstimation.c:336) -- 8 positions x .. x+7 of a
+ *   64x64 block: 8x8 / 16x16 SADs (Z-order), best SAD/MV updates (strict <), p_eight_sad16x16[16][8] */
+void svtgpu_ext_all_sad_calculation_8x8_16x16(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                              uint32_t mv, uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
+                                              uint32_t *p_best_mv8x8, uint32_t *p_best_mv16x16,
+                                              uint32_t p_eight_sad16x16[16][8], uint32_t p_eight_sad8x8[64][8],
+                                              Bool sub_sad);
+/* svt_ext_eight_sad_calculation_32x32_64x64 (aom_dsp_rtcd.h:851; C EbMotionEstimation.c:370) */
+void svtgpu_ext_eight_sad_calculation_32x32_64x64(uint32_t p_sad16x16[16][8], uint32_t *p_best_sad_32x32,
+                                                  uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                                  uint32_t *p_best_mv64x64, uint32_t mv, uint32_t p_sad32x32[4][8]);
+/* svt_ext_sad_calculation_8x8_16x16 (aom_dsp_rtcd.h:839; C EbMotionEstimation.c:99) -- one 16x16 at one position */
+void svtgpu_ext_sad_calculation_8x8_16x16(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                          uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16, uint32_t *p_best_mv8x8,
+                                          uint32_t *p_best_mv16x16, uint32_t mv, uint32_t *p_sad16x16,
+                                          uint32_t *p_sad8x8, Bool sub_sad);
+/* svt_ext_sad_calculation_32x32_64x64 (aom_dsp_rtcd.h:845; C EbMotionEstimation.c:172) */
+void svtgpu_ext_sad_calculation_32x32_64x64(uint32_t *p_sad16x16, uint32_t *p_best_sad_32x32,
+                                            uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                            uint32_t *p_best_mv64x64, uint32_t mv, uint32_t *p_sad32x32);
+/* svt_sad_loop_kernel (aom_dsp_rtcd.h:776; C EbComputeSAD_C.c:58) -- full search of a block over an area */
+void svtgpu_sad_loop_kernel(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                            uint32_t block_height, uint32_t block_width, uint64_t *best_sad, int16_t *x_search_center,
+                            int16_t *y_search_center, uint32_t src_stride_raw, uint8_t skip_search_line,
+                            int16_t search_area_width, int16_t search_area_height);
+/* Frame level: the integer full-pel search of every 64x64 block against every reference (≙ the per-block
+ * open_loop_me_fullpel_search_sblock, EbMotionEstimation.c:782-818, after the best SADs are reset to MAX_SAD_VALUE,
+ * :1363-1364).  origin[sb][r] = {x, y} is the search-area origin relative to the block (the MV of search position
+ * (0, 0)); the search covers sa_w x sa_h positions (sa_w <= 192); sub_sad = the SUB_SAD_SEARCH method (8x8 SADs over
+ * rows 0, 2, 4, 6, doubled).  8-bit luma; reference samples outside the frame read the nearest edge sample (the
+ * padded reference pictures).  Output per (sb, r): 85 best SADs and MVs -- [0, 64) 8x8, [64, 80) 16x16, [80, 84) 32x32,
+ * [84] 64x64, in the reference's Z-order numbering (me_ctx->p_best_sad_8x8 ...); MV = (y << 16) | (uint16_t)x. */
+#define SVTGPU_ME_BLOCKS 85
+typedef struct SvtGpuMeBatch SvtGpuMeBatch;
+int  svtgpu_me_batch_create(SvtGpuContext *ctx, int32_t width, int32_t height, int32_t nref, SvtGpuMeBatch **out);
+void svtgpu_me_batch_destroy(SvtGpuMeBatch *b);
+int  svtgpu_me_set_origins(SvtGpuMeBatch *b, const int16_t *origin, void *stream); /* host [nsb][nref][2] */
+int  svtgpu_me_search(SvtGpuMeBatch *b, const SvtGpuFrame *source, const SvtGpuFrame *const *refs, int32_t sa_w,
+                      int32_t sa_h, int32_t sub_sad, int32_t sb_begin, int32_t sb_end, void *stream);
+int  svtgpu_me_read(SvtGpuMeBatch *b, uint32_t *best_sad, uint32_t *best_mv, int32_t sb_begin, int32_t sb_end,
+                    void *stream); /* host [sb_end - sb_begin][nref][85] each (nullable) */
+
+/* =========================================================================================
  * Loop restoration
  * ========================================================================================= */
 /* RTCD-compatible per-block shims (common_dsp_rtcd.h:174-185).  The Wiener convolve reads round_0 / round_1 of

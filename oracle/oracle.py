@@ -77,6 +77,10 @@ _SIGS = {
     "oracle_dlf_pick": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
                                        ctypes.POINTER(LfParams), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int]),
+    "oracle_me_search": (ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]),
+    "oracle_sad_loop": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P,
+                               ctypes.c_uint32, ctypes.c_uint8, ctypes.c_int16, ctypes.c_int16]),
 }
 _lib = None
 
@@ -371,3 +375,29 @@ def cdef_dup_sb128(fbs, kinds, nvfb, nhfb):
         for p in _area_parts(int(f), int(kinds[f]), nvfb, nhfb)[1:]:
             fbs[p] = fbs[f]
     return fbs
+
+
+def me_search(src, refs, origin, saw, sah, sub=0, sb_range=None):
+    """Open-loop full-pel ME of every 64x64 block (8-bit luma) against every reference (me_oracle.c); returns
+    (best_sad, best_mv) uint32 [nsb][nref][85] for the blocks in sb_range (default: all)."""
+    h, w = src.shape
+    nsb = ((w + 63) // 64) * ((h + 63) // 64)
+    b, e = sb_range if sb_range else (0, nsb)
+    src = np.ascontiguousarray(src, np.uint8)
+    rs = [np.ascontiguousarray(r, np.uint8) for r in refs]
+    arr = (ctypes.c_void_p * len(rs))(*[r.ctypes.data for r in rs])
+    org = np.ascontiguousarray(origin, np.int16)
+    assert org.shape == (nsb, len(rs), 2)
+    sad = np.zeros((e - b, len(rs), 85), np.uint32)
+    mv = np.zeros((e - b, len(rs), 85), np.uint32)
+    assert lib().oracle_me_search(ptr(src), ctypes.cast(arr, ctypes.c_void_p), len(rs), w, h, ptr(org), saw, sah,
+                                  int(sub), b, e, ptr(sad), ptr(mv)) == 0
+    return sad, mv
+
+
+def sad_loop(src, ss, ref, rs, bh, bw, src_stride_raw, skip, saw, sah):
+    """svt_sad_loop_kernel_c restated: (best_sad, x, y) over flat uint8 buffers."""
+    best, xc, yc = ctypes.c_uint64(0), ctypes.c_int16(-1), ctypes.c_int16(-1)
+    lib().oracle_sad_loop(ptr(np.ascontiguousarray(src, np.uint8)), ss, ptr(np.ascontiguousarray(ref, np.uint8)), rs,
+                          bh, bw, ctypes.byref(best), ctypes.byref(xc), ctypes.byref(yc), src_stride_raw, skip, saw, sah)
+    return best.value, xc.value, yc.value

@@ -49,7 +49,7 @@ SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
 PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
-     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench
+     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -100,3 +100,9 @@ $(OUT)/ref_bench: oracle/ref_harness/ref_bench.c $(sort $(LR_OBJ) $(MD_OBJ) $(DL
 clean:
 	rm -rf $(OUT)
 .PHONY: all clean
+
+# open-loop ME SAD: the reference's EbMotionEstimation.c kernels + svt_sad_loop_kernel_c
+ME_C     := Lib/Encoder/Codec/EbMotionEstimation.c
+ME_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(ME_C))
+$(OUT)/gen_golden_me: oracle/ref_harness/gen_golden_me.c $(sort $(ME_OBJ) $(MD_OBJ) $(C_OBJ))
+	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm -lpthread

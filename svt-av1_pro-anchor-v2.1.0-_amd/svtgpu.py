@@ -294,6 +294,19 @@ _SIGS = {
     "svtgpu_get_proj_subspace": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int,
                                         _P, ctypes.c_int, _P, ctypes.c_int, _P, _P]),
     "svtgpu_md_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_me_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_me_batch_destroy": (None, [_P]),
+    "svtgpu_me_set_origins": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_me_search": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_me_read": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P]),
+    "svtgpu_ext_all_sad_calculation_8x8_16x16": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P,
+                                                        _P, _P, _P, _P, _P, ctypes.c_uint8]),
+    "svtgpu_ext_eight_sad_calculation_32x32_64x64": (None, [_P, _P, _P, _P, _P, ctypes.c_uint32, _P]),
+    "svtgpu_ext_sad_calculation_8x8_16x16": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, _P, _P, _P, _P,
+                                                    ctypes.c_uint32, _P, _P, ctypes.c_uint8]),
+    "svtgpu_ext_sad_calculation_32x32_64x64": (None, [_P, _P, _P, _P, _P, ctypes.c_uint32, _P]),
+    "svtgpu_sad_loop_kernel": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P,
+                                      _P, _P, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_int16, ctypes.c_int16]),
     "svtgpu_md_batch_destroy": (None, [_P]),
     "svtgpu_md_batch_nsb": (_I32, [_P]),
     "svtgpu_md_set_mvs": (ctypes.c_int, [_P, _P, _P]),
@@ -545,6 +558,47 @@ class DlfState:
     def close(self):
         if self.h:
             lib().svtgpu_dlf_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MeBatch:
+    """Open-loop full-pel ME (svtgpu_me_search): every 64x64 block x reference over a search area; per (block,
+    reference) the 85 best SADs / MVs in the reference's Z-order numbering (64 8x8, 16 16x16, 4 32x32, 1 64x64)."""
+
+    def __init__(self, ctx, width, height, nref):
+        self.ctx, self.width, self.height, self.nref = ctx, width, height, nref
+        h = _P()
+        check(lib().svtgpu_me_batch_create(ctx.h, width, height, nref, ctypes.byref(h)))
+        self.h = h
+        self.nsb = ((width + 63) // 64) * ((height + 63) // 64)
+
+    def set_origins(self, origin, stream=None):
+        a = np.ascontiguousarray(origin, dtype=np.int16)
+        assert a.shape == (self.nsb, self.nref, 2), a.shape
+        check(lib().svtgpu_me_set_origins(self.h, ptr(a), stream))
+
+    def search(self, source, refs, saw, sah, sub=0, sb_begin=0, sb_end=None, stream=None):
+        assert len(refs) == self.nref
+        arr = (_P * self.nref)(*[r.h for r in refs])
+        end = self.nsb if sb_end is None else sb_end
+        check(lib().svtgpu_me_search(self.h, source.h, arr, saw, sah, int(sub), sb_begin, end, stream))
+
+    def read(self, sb_begin=0, sb_end=None, stream=None):
+        end = self.nsb if sb_end is None else sb_end
+        sad = np.empty((end - sb_begin, self.nref, 85), np.uint32)
+        mv = np.empty((end - sb_begin, self.nref, 85), np.uint32)
+        check(lib().svtgpu_me_read(self.h, ptr(sad), ptr(mv), sb_begin, end, stream))
+        return sad, mv
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_me_batch_destroy(self.h)
             self.h = None
 
     def __del__(self):

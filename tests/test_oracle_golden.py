@@ -213,3 +213,23 @@ def test_compute_stats_golden():
         M, H = np.zeros(win * win, np.int64), np.zeros(win ** 4, np.int64)
         L.oracle_compute_stats(win, oracle.ptr(d), oracle.ptr(s), st, w, h, bd, oracle.ptr(M), oracle.ptr(H))
         assert np.array_equal(M, g["M%d" % n]) and np.array_equal(H, g["H%d" % n]), (n, bd, win)
+
+
+# ---- open-loop ME SAD (me_oracle.c vs the reference's EbMotionEstimation.c / EbComputeSAD_C.c) ----
+def test_oracle_me_search_vs_reference():
+    import me_cases as mc
+    for src, refs, origin, saw, sah, sub, sad, mv in mc.frames(mc.golden()):
+        osad, omv = oracle.me_search(src, refs, origin, saw, sah, sub)
+        np.testing.assert_array_equal(osad, sad)
+        np.testing.assert_array_equal(omv, mv)
+
+
+def test_oracle_sad_loop_vs_reference():
+    import me_cases as mc
+    for s, r, m in mc.loop_cases(mc.golden()):
+        bw, bh, saw, sah, ss, rs, srr, skip, best, c = m
+        got = oracle.sad_loop(s, ss, r, rs, bh, bw, srr, skip, saw, sah)
+        want_c = ((c & 0xFFFF) ^ 0x8000) - 0x8000, ((c >> 16) ^ 0x8000) - 0x8000
+        assert got[0] == best, m
+        if best < 0xffffff:
+            assert got[1:] == want_c, m
