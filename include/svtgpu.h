@@ -621,6 +621,36 @@ int  svtgpu_me_read(SvtGpuMeBatch *b, uint32_t *best_sad, uint32_t *best_mv, int
                     void *stream); /* host [sb_end - sb_begin][nref][85] each (nullable) */
 
 /* =========================================================================================
+ * Frame-buffer work around the path
+ * ========================================================================================= */
+/* RTCD-compatible shims (synchronous, host pointers):
+ * svt_convert_8bit_to_16bit / svt_convert_16bit_to_8bit (common_dsp_rtcd.h:154-156; C EbPackUnPack_C.c:270-283) */
+void svtgpu_convert_8bit_to_16bit(uint8_t *src, uint32_t src_stride, uint16_t *dst, uint32_t dst_stride, uint32_t width,
+                                  uint32_t height);
+void svtgpu_convert_16bit_to_8bit(uint16_t *src, uint32_t src_stride, uint8_t *dst, uint32_t dst_stride, uint32_t width,
+                                  uint32_t height);
+/* svt_aom_generate_padding / svt_aom_generate_padding16_bit (EbMcp.h:46-51; C EbMcp.c:95-240): src_pic is the padded
+ * buffer's first sample, the visible area starts at (padding_width, padding_height) */
+void svtgpu_aom_generate_padding(uint8_t *src_pic, uint32_t src_stride, uint32_t original_src_width,
+                                 uint32_t original_src_height, uint32_t padding_width, uint32_t padding_height);
+void svtgpu_aom_generate_padding16_bit(uint16_t *src_pic, uint32_t src_stride, uint32_t original_src_width,
+                                       uint32_t original_src_height, uint32_t padding_width, uint32_t padding_height);
+/* svt_extend_frame (EbRestoration.c:197): data = first visible sample (CONVERT_TO_BYTEPTR-encoded when highbd) */
+void svtgpu_extend_frame(uint8_t *data, int32_t width, int32_t height, int32_t stride, int32_t border_horz,
+                         int32_t border_vert, int32_t highbd);
+/* Device-pointer versions (asynchronous on `stream`, nullable = the library's default stream); bits = 8 or 16,
+ * strides in samples: */
+int svtgpu_convert_plane(const void *src, int32_t src_bits, int32_t src_stride, void *dst, int32_t dst_bits,
+                         int32_t dst_stride, int32_t width, int32_t height, void *stream);
+int svtgpu_pad_plane(void *buf, int32_t bits, int32_t stride, int32_t width, int32_t height, int32_t pad_width,
+                     int32_t pad_height, void *stream);
+int svtgpu_extend_plane(void *data, int32_t bits, int32_t stride, int32_t width, int32_t height, int32_t border_horz,
+                        int32_t border_vert, void *stream);
+/* svt_convert_pic_8bit_to_16bit (EbRestProcess.c:235-272) and the 16 -> 8 copy-back of non-reference pictures
+ * (EbRestProcess.c:670-697) on device frames: all three planes, direction from the frames' bit depths */
+int svtgpu_frame_convert(const SvtGpuFrame *src, SvtGpuFrame *dst, void *stream);
+
+/* =========================================================================================
  * Loop restoration
  * ========================================================================================= */
 /* RTCD-compatible per-block shims (common_dsp_rtcd.h:174-185).  The Wiener convolve reads round_0 / round_1 of

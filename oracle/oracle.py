@@ -81,6 +81,10 @@ _SIGS = {
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]),
     "oracle_sad_loop": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P,
                                ctypes.c_uint32, ctypes.c_uint8, ctypes.c_int16, ctypes.c_int16]),
+    "oracle_convert": (None, [_P, ctypes.c_int, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int]),
+    "oracle_pad": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_extend": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
 }
 _lib = None
 
@@ -401,3 +405,20 @@ def sad_loop(src, ss, ref, rs, bh, bw, src_stride_raw, skip, saw, sah):
     lib().oracle_sad_loop(ptr(np.ascontiguousarray(src, np.uint8)), ss, ptr(np.ascontiguousarray(ref, np.uint8)), rs,
                           bh, bw, ctypes.byref(best), ctypes.byref(xc), ctypes.byref(yc), src_stride_raw, skip, saw, sah)
     return best.value, xc.value, yc.value
+
+
+def convert(src, ss, dst, ds, w, h):
+    """svt_convert_8bit_to_16bit / 16bit_to_8bit restated, in place on the flat dst buffer (frame_oracle.c)."""
+    sb, db = src.dtype.itemsize * 8, dst.dtype.itemsize * 8
+    lib().oracle_convert(ptr(src), sb, ss, ptr(dst), db, ds, w, h)
+
+
+def pad(buf, stride, w, h, pw, ph):
+    """svt_aom_generate_padding(16_bit) restated, in place on the flat padded buffer."""
+    lib().oracle_pad(ptr(buf), buf.dtype.itemsize * 8, stride, w, h, pw, ph)
+
+
+def extend(buf, offset, stride, w, h, bh, bv):
+    """svt_extend_frame restated, in place; offset = index of the first visible sample in the flat buffer."""
+    lib().oracle_extend(ctypes.c_void_p(buf.ctypes.data + offset * buf.dtype.itemsize), buf.dtype.itemsize * 8,
+                        stride, w, h, bh, bv)

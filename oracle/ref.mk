@@ -49,7 +49,7 @@ SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
 PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
-     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me
+     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me $(OUT)/gen_golden_frame
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -105,4 +105,10 @@ clean:
 ME_C     := Lib/Encoder/Codec/EbMotionEstimation.c
 ME_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(ME_C))
 $(OUT)/gen_golden_me: oracle/ref_harness/gen_golden_me.c $(sort $(ME_OBJ) $(MD_OBJ) $(C_OBJ))
+	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm -lpthread
+
+# frame-buffer work around the path: conversions, reference padding, frame extension
+FRAME_C  := Lib/Common/C_DEFAULT/EbPackUnPack_C.c Lib/Common/Codec/EbMcp.c
+FRAME_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(FRAME_C))
+$(OUT)/gen_golden_frame: oracle/ref_harness/gen_golden_frame.c $(sort $(FRAME_OBJ) $(LR_OBJ) $(MD_OBJ) $(C_OBJ))
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm -lpthread

@@ -295,6 +295,17 @@ _SIGS = {
                                         _P, ctypes.c_int, _P, ctypes.c_int, _P, _P]),
     "svtgpu_md_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "svtgpu_me_batch_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_convert_8bit_to_16bit": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_convert_16bit_to_8bit": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_aom_generate_padding": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_uint32]),
+    "svtgpu_aom_generate_padding16_bit": (None, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, ctypes.c_uint32]),
+    "svtgpu_extend_frame": (None, [_P, _I32, _I32, _I32, _I32, _I32, _I32]),
+    "svtgpu_convert_plane": (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_pad_plane": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_extend_plane": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_frame_convert": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_me_batch_destroy": (None, [_P]),
     "svtgpu_me_set_origins": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_me_search": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P]),

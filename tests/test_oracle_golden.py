@@ -233,3 +233,21 @@ def test_oracle_sad_loop_vs_reference():
         assert got[0] == best, m
         if best < 0xffffff:
             assert got[1:] == want_c, m
+
+
+# ---- frame-buffer work (frame_oracle.c vs the reference's EbPackUnPack_C.c / EbMcp.c / EbRestoration.c) ----
+def test_oracle_frame_ops_vs_reference():
+    import frame_cases as fc
+    g = fc.golden()
+    for src, d0, d1, w, h, ss, ds in fc.conv_cases(g):
+        d = d0.copy()
+        oracle.convert(src, ss, d, ds, w, h)
+        np.testing.assert_array_equal(d, d1)
+    for b0, b1, w, h, st, pw, ph in fc.pad_cases(g):
+        b = b0.copy()
+        oracle.pad(b, st, w, h, pw, ph)
+        np.testing.assert_array_equal(b, b1)
+    for b0, b1, w, h, st, bh, bv, off in fc.ext_cases(g):
+        b = b0.copy()
+        oracle.extend(b, off, st, w, h, bh, bv)
+        np.testing.assert_array_equal(b, b1)
