@@ -315,6 +315,69 @@ def cpu_baseline(src, rec, mi, lf_start, bd, level, q, lam, grid, lr_ctrls, lr_u
                       % (bd, gx, gy, cw, ch, level, nthr, dt)}
 
 
+def measure_next_rows(ctx, torch, W, H, reps=20):
+    """The §8(f) rows beside the pipeline, timed with HIP events on the stream they run on (rank 0, N = 1): the
+    frame-buffer kernels against the HBM roofline (their bytes are the algorithmic bytes: every touched sample read or
+    written once), and the open-loop ME full-pel search (VALU-bound: v_sad_u8 over every position)."""
+    import ctypes
+    L = svtgpu.lib()
+    st = torch.cuda.Stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    out = {}
+
+    def timed(fn):
+        fn()  # warm
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    def hbm(name, ms, nbytes, what):
+        out[name] = {"ms": round(ms, 5), "alg_MB": round(nbytes / 1e6, 3),
+                     "achieved_GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                     "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "what": what}
+
+    src8, _ = synth.frame_pair(W, H, 8, seed=0x5EED0031)
+    f8, f16, g8 = svtgpu.Frame(ctx, W, H, 8), svtgpu.Frame(ctx, W, H, 10), svtgpu.Frame(ctx, W, H, 8)
+    f8.upload(src8)
+    torch.cuda.synchronize()
+    S = 1.5 * W * H
+    hbm("convert_8to16", timed(lambda: L.svtgpu_frame_convert(f8.h, f16.h, sp)), 3 * S,
+        "svt_convert_pic_8bit_to_16bit, 3 planes (1 B read + 2 B written per sample)")
+    hbm("convert_16to8", timed(lambda: L.svtgpu_frame_convert(f16.h, g8.h, sp)), 3 * S,
+        "16 -> 8 copy-back of a non-reference picture, 3 planes (2 B read + 1 B written per sample)")
+    pw = ph = 80
+    stride = W + 2 * pw
+    buf = torch.zeros((H + 2 * ph) * stride, dtype=torch.int16, device="cuda")
+    border = (H + 2 * ph) * stride - W * H
+    hbm("pad_ref_luma_16bit", timed(lambda: L.svtgpu_pad_plane(ctypes.c_void_p(buf.data_ptr()), 16, stride, W, H, pw, ph,
+                                                                sp)),
+        2 * (border + 2 * H + 2 * stride), "svt_aom_generate_padding16_bit of a 4K luma plane, 80-sample border "
+                                           "(border samples written, edge samples read)")
+    # open-loop ME: every 64x64 block x 2 references, 32 x 32 full-pel positions
+    nref, saw, sah = 2, 32, 32
+    refs = []
+    for k in range(nref):
+        rf = svtgpu.Frame(ctx, W, H, 8)
+        rf.upload(synth.frame_pair(W, H, 8, seed=0x5EED0032 + k)[0])
+        refs.append(rf)
+    me = svtgpu.MeBatch(ctx, W, H, nref)
+    me.set_origins(np.random.default_rng(3).integers(-24, -8, size=(me.nsb, nref, 2)).astype(np.int16))
+    torch.cuda.synchronize()
+    ms = timed(lambda: me.search(f8, refs, saw, sah, 0, stream=st.cuda_stream))
+    tasks = me.nsb * nref
+    out["me_fullpel_search"] = {"ms": round(ms, 4), "blocks_x_refs": tasks, "positions": saw * sah,
+                                "block_positions_per_s": round(tasks * saw * sah / (ms * 1e-3), 1),
+                                "sad_Gops": round(tasks * saw * sah * 4096 / (ms * 1e-3) / 1e9, 1),
+                                "what": "svtgpu_me_search: %dx%d 8-bit, %d refs, %dx%d positions, 85 bests per block "
+                                        "(VALU-bound: v_sad_u8)" % (W, H, nref, saw, sah)}
+    return out
+
+
 def main():
     a = parse()
     rc = spawn_ranks(a)
@@ -635,6 +698,8 @@ def main():
         out["config"].pop("lr_search_kernel_ms")
     if matrix is not None:
         out["config"]["matrix"] = matrix
+    if rank == 0 and n == 1 and a.stages == "all" and not a.no_matrix:
+        out["config"]["next_rows"] = measure_next_rows(ctx, torch, W, H)
     if rank == 0 and n == 1 and not a.no_cpu_baseline:
         s0 = slots[0]
         if a.cpu_kind == "reference" and os.path.exists(REF_BENCH):
