@@ -389,6 +389,8 @@ struct SvtGpuDlfState {
     unsigned long long *h_sse_dev; // its device address
     unsigned long long  seq;       // last trial launch's sequence number
     int32_t        have_mi;
+    hipStream_t    hi_stream = nullptr; // highest-priority stream of the level search's trial launches (lazy)
+    hipEvent_t     hi_ev     = nullptr;
 };
 
 namespace {
@@ -669,6 +671,8 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
 extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     if (!s) return;
     (void)hipFree(s->d_mi);
+    if (s->hi_ev) (void)hipEventDestroy(s->hi_ev);
+    if (s->hi_stream) (void)hipStreamDestroy(s->hi_stream);
     for (int c = 0; c < 2; c++)
         for (int d = 0; d < 2; d++) (void)hipFree(s->d_rec[c][d]);
     (void)hipFree(s->d_scratch);
@@ -779,7 +783,11 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
-    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st))) return rc;
+    // the bisection's dependent trial launches (each followed by a host wait) on a highest-priority stream ordered
+    // after the caller's (svtgpu_priority_stream); every trial result has been waited for when the search returns
+    hipStream_t ts = st;
+    if ((rc = svtgpu_priority_stream(&s->hi_stream, &s->hi_ev, st, &ts))) return rc;
+    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, ts))) return rc;
     p.filter_level[0] = p.filter_level[1] = ys.best;
     p.filter_level_u = search_uv ? us.best : last[2];
     p.filter_level_v = search_uv ? vs.best : last[3];
