@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "lr_common.h"
@@ -772,7 +773,10 @@ __device__ inline void proj_tile(const SearchArgs &A, int ti, const int32_t *can
         // chunk k of this lane: row (threadIdx.x >> 4) + 16 k, 4 pixels at column 4 (threadIdx.x & 15)
         const int        fo0 = (t.y0 + (threadIdx.x >> 4)) * P.fstride + t.x0 + (threadIdx.x & 15) * 4;
         const int        fos = 16 * P.fstride;
-        uint32_t         px2[NCH][4]; // (x, x - src) per pixel
+        // per pixel, independent of the ep: u = (x << 4, x << 4) packed, and c0 = 1024 + (x - src) * 2^11 -- the
+        // rounding and source terms that ride in the dot product's accumulator
+        uint32_t         uu[NCH][4];
+        int32_t          c0[NCH][4];
         uint32_t         on = 0;      // bit k: chunk k inside the tile
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
@@ -783,10 +787,10 @@ __device__ inline void proj_tile(const SearchArgs &A, int ti, const int32_t *can
                 load4(d + (size_t)y * P.dstride + x, dv);
                 load4(s + (size_t)y * P.sstride + x, sv);
 #pragma unroll
-                for (int j = 0; j < 4; j++) px2[k][j] = pack2(dv[j], dv[j] - sv[j]);
+                for (int j = 0; j < 4; j++) uu[k][j] = __umul24((uint32_t)dv[j], 0x00100010u), c0[k][j] = 1024 + ((dv[j] - sv[j]) << 11);
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) px2[k][j] = 0;
+                for (int j = 0; j < 4; j++) uu[k][j] = 0, c0[k][j] = 0;
             }
         }
         // the eps with a pending tree; their filter planes are fetched one ep ahead of the arithmetic
@@ -806,44 +810,63 @@ __device__ inline void proj_tile(const SearchArgs &A, int ti, const int32_t *can
             const int en = act ? __builtin_ctz(act) : -1;
             if (en >= 0) fetch(en, n0, n1);
             const int      pair = pb + e;
-            const uint32_t mask = ld_shared<SHARED>(candm + pair);
+            // the tree's nodes compacted to the front (the mask is the same for every lane): a partial tree (descents
+            // near their end) evaluates only its nodes
+            const uint32_t mask = __builtin_amdgcn_readfirstlane(ld_shared<SHARED>(candm + pair));
             npx_e += t.w * t.h; // profiling
-            uint32_t xq[SG_NC];
+            const int nv = __builtin_popcount(mask);
+            uint32_t  xq[SG_NC];
+            {
+                uint32_t m = mask;
 #pragma unroll
-            for (int c = 0; c < SG_NC; c++)
-                xq[c] = (mask >> c & 1) ? pack2(ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2),
-                                                ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2 + 1))
-                                        : 0u;
-            uint32_t acc[SG_NC];
-#pragma unroll
-            for (int c = 0; c < SG_NC; c++) acc[c] = 0;
-#pragma unroll
-            for (int k = 0; k < NCH; k++) {
-                if (!(on >> k & 1)) continue;
-                // (flt0, flt1) int16 pairs of the 4 pixels, then g = (flt0 - u, flt1 - u) on packed 16-bit lanes
-                // (|g| < 2^15, so the wrapped halves are the exact differences)
-                const uint32_t fp[4] = {__builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x05040100u),
-                                        __builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x07060302u),
-                                        __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x05040100u),
-                                        __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x07060302u)};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    // floor((v + 1024) / 2^11) + (x - src) == (v + 1024 + (x - src) * 2^11) >> 11
-                    const uint32_t uu = __umul24(px2[k][j] & 0xFFFF, 0x00100010u); // (x << 4, x << 4)
-                    const int      c0 = 1024 + (((int)px2[k][j] >> 16) << 11);
-                    const uint32_t g  = pk_sub16(fp[j], uu);
-#pragma unroll
-                    for (int c = 0; c < SG_NC; c++) { // branch-free: candidates outside the tree have xq = 0
-                        const int ee = dot2(g, xq[c], c0) >> 11; // c0 rides in the dot product's accumulator
-                        acc[c] += (uint32_t)(ee * ee);
+                for (int i = 0; i < SG_NC; i++) {
+                    xq[i] = 0u;
+                    if (m) {
+                        const int c = __builtin_ctz(m);
+                        m &= m - 1;
+                        xq[i] = pack2(ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2),
+                                      ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2 + 1));
                     }
                 }
             }
+            uint32_t acc[SG_NC];
 #pragma unroll
-            for (int c = 0; c < SG_NC; c++) {
-                if (!(mask >> c & 1)) continue;
-                const unsigned long long w = wave_sum_u32_wide(acc[c]); // <= 16 pixels per lane: fits 32 bits
-                if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
+            for (int c = 0; c < SG_NC; c++) acc[c] = 0;
+            auto eval = [&](auto full) {
+#pragma unroll
+                for (int k = 0; k < NCH; k++) {
+                    if (!(on >> k & 1)) continue;
+                    // (flt0, flt1) int16 pairs of the 4 pixels, then g = (flt0 - u, flt1 - u) on packed 16-bit lanes
+                    // (|g| < 2^15, so the wrapped halves are the exact differences)
+                    const uint32_t fp[4] = {__builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x05040100u),
+                                            __builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x07060302u),
+                                            __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x05040100u),
+                                            __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x07060302u)};
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        // floor((v + 1024) / 2^11) + (x - src) == (v + 1024 + (x - src) * 2^11) >> 11
+                        const uint32_t g = pk_sub16(fp[j], uu[k][j]);
+#pragma unroll
+                        for (int c = 0; c < SG_NC; c++) {
+                            if (!decltype(full)::value && c >= nv) break; // uniform: a scalar branch
+                            const int ee = dot2(g, xq[c], c0[k][j]) >> 11; // c0 rides in the accumulator
+                            acc[c] += (uint32_t)(ee * ee);
+                        }
+                    }
+                }
+            };
+            if (nv == SG_NC) eval(std::true_type());
+            else eval(std::false_type());
+            {
+                uint32_t m = mask;
+#pragma unroll
+                for (int i = 0; i < SG_NC; i++) {
+                    if (!m) break;
+                    const int c = __builtin_ctz(m);
+                    m &= m - 1;
+                    const unsigned long long w = wave_sum_u32_wide(acc[i]); // <= 16 pixels per lane: fits 32 bits
+                    if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
+                }
             }
 #pragma unroll
             for (int k = 0; k < NCH; k++) w0[k] = n0[k], w1[k] = n1[k];
@@ -1725,7 +1748,7 @@ __device__ inline int q_claim(WnQueue *q, const int32_t *log, int cap, int *s_it
                 atomicExch(&q->live, 0);
                 break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(8); // ~0.2 us: idle workers spend few instructions polling
         }
         *s_item = it - 1;
         wait_mem();

@@ -228,11 +228,13 @@ def test_cdef_band_search_allreduce(ctx, nb):
 
 
 @pytest.mark.parametrize("top", [1 << 31, 1 << 40])
-def test_cdef_pick_bound_tables_vs_oracle(ctx, top):
+@pytest.mark.parametrize("w,h", [(1024, 512), (3840, 2160)])
+def test_cdef_pick_bound_tables_vs_oracle(ctx, top, w, h):
     """The frame pick over arbitrary mse tables: entries just below 2^31 (the 32-bit accumulation path, sums of
-    two entries up to 2^32 - 2) and up to 2^40 (the 64-bit path), random skipped FBs; bit-exact vs the oracle."""
+    two entries up to 2^32 - 2) and up to 2^40 (the 64-bit path), random skipped FBs; bit-exact vs the oracle.
+    At 3840x2160 (2040 FBs) the default launch shape stages the largest FB chunks (PICK_CHUNK) per workgroup."""
     import torch
-    w, h, q, lam = 1024, 512, 128, 60000
+    q, lam = 128, 60000
     ctrls = svtgpu.cdef_controls(1)
     st = svtgpu.CdefState(ctx, w, h)
     rng = np.random.default_rng(top % 1000003)
