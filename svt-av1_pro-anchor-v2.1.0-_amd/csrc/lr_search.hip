@@ -14,12 +14,13 @@
 //                         filters (kept in HBM as int16) and the 2x2 projection moments in exact int64
 //   wiener_unit_kernel    (default) the whole Wiener descent of finer_tile_search_wiener_seg per unit inside one
 //                         workgroup: candidate SSE over the unit's tiles, descent step in LDS, no global sync
-//   sgr_queue_kernel      (default) the self-guided descents of finer_search_pixel_proj_error as a persistent
+//   sgr_queue_kernel      (opt-in, SVTGPU_SG_QUEUE=1) the self-guided descents of finer_search_pixel_proj_error as a persistent
 //                         work queue: a worker evaluates a unit tile's pending candidate trees, the worker completing
 //                         the unit's pass steps its descents and re-publishes its tiles
-//   wiener_queue_kernel, wiener_trial_kernel / proj_err_kernel + *_advance_kernel
-//                         the alternatives kept for A/B (SVTGPU_WN_UNIT=0, SVTGPU_WN_QUEUE=0, SVTGPU_SG_QUEUE=0): a
-//                         Wiener work queue, and per-round launches with a host-polled batch loop
+//   proj_err_kernel + sgr_advance_kernel
+//                         (default) the self-guided descents as per-round launches with a host-polled batch loop
+//   wiener_queue_kernel, wiener_trial_kernel + wiener_advance_kernel
+//                         the Wiener alternatives kept for A/B (SVTGPU_WN_UNIT=0, SVTGPU_WN_QUEUE=0)
 //   sgr_best_kernel, sgr_sse_kernel
 //                         best ep per unit (strict <) and the SSE of its clipped output
 // The host does what is sequential in the reference and cheap: the int64 fixed-point Wiener decomposition, the
@@ -2181,12 +2182,13 @@ int wn_unit_ng() { // tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG:
     }();
     return v;
 }
-// persistent self-guided queue workers (SVTGPU_SG_QUEUE=0 selects the per-round projection/advance launches;
-// SVTGPU_SG_QGRID sets the worker count)
+// persistent self-guided queue workers: opt-in (SVTGPU_SG_QUEUE=1; SVTGPU_SG_QGRID sets the worker count).  With the
+// hoisted per-pixel terms and partial-tree evaluation the per-round projection launches measured faster at three
+// frames in flight (1963-1980 vs 1864-1889 Mpx/s, same box)
 bool sg_use_queue() {
     static const bool v = [] {
         const char *e = std::getenv("SVTGPU_SG_QUEUE");
-        return !(e && std::atoi(e) == 0);
+        return e && std::atoi(e) != 0;
     }();
     return v;
 }
