@@ -603,6 +603,16 @@ void svtgpu_sad_loop_kernel(uint8_t *src, uint32_t src_stride, uint8_t *ref, uin
                             uint32_t block_height, uint32_t block_width, uint64_t *best_sad, int16_t *x_search_center,
                             int16_t *y_search_center, uint32_t src_stride_raw, uint8_t skip_search_line,
                             int16_t search_area_width, int16_t search_area_height);
+/* svt_pme_sad_loop_kernel (aom_dsp_rtcd.h:866; C EbProductCodingLoop.c:1801) -- the MD full-pel refinement: cost =
+ * SAD + svt_aom_fp_mv_err_cost (mcomp.c:771) over the reference's visiting order; mv_cost_params is the reference's
+ * MV_COST_PARAMS (mcomp.h:37), read with its layout */
+struct svt_mv_cost_param;
+void svtgpu_pme_sad_loop_kernel(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                                uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                                uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                                int16_t search_position_start_x, int16_t search_position_start_y,
+                                int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                                int16_t mvx, int16_t mvy);
 /* Frame level: the integer full-pel search of every 64x64 block against every reference (≙ the per-block
  * open_loop_me_fullpel_search_sblock, EbMotionEstimation.c:782-818, after the best SADs are reset to MAX_SAD_VALUE,
  * :1363-1364).  origin[sb][r] = {x, y} is the search-area origin relative to the block (the MV of search position

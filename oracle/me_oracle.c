@@ -10,6 +10,8 @@
  *                      (svt_ext_sad_calculation_8x8_16x16_c :99-170 + svt_ext_sad_calculation_32x32_64x64_c :172-210).
  *                      The reference window is cut from the frame with edge replication (the padded reference).
  *   oracle_sad_loop    svt_sad_loop_kernel_c (EbComputeSAD_C.c:58-99).
+ *   oracle_pme_sad_loop svt_pme_sad_loop_kernel_c (EbProductCodingLoop.c:1801-1852): the MD full-pel search, SAD plus
+ *                      the MV rate of svt_aom_fp_mv_err_cost for each of the six MV_COST_TYPEs.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -116,6 +118,54 @@ void oracle_sad_loop(const uint8_t *src, uint32_t ss, const uint8_t *ref, uint32
         for (int x = 0; x < saw; x++) {
             const uint32_t s = sad_rect(src, (int)ss, ref + (size_t)y * src_stride_raw + x, (int)rs, (int)bw, (int)bh);
             if (s < *best_sad) *best_sad = s, *xc = (int16_t)x, *yc = (int16_t)y;
+        }
+    }
+}
+
+/* svt_pme_sad_loop_kernel_c (EbProductCodingLoop.c:1801-1852) with svt_aom_fp_mv_err_cost (mcomp.c:43-68, 771):
+ * p = the reference's MV_COST_PARAMS (mcomp.h:37-48) read through its layout */
+typedef struct {
+    const int16_t *ref_mv; /* MV {row, col} */
+    int16_t        full_ref_mv[2];
+    uint8_t        mv_cost_type;
+    const int     *mvjcost;
+    const int     *mvcost[2];
+    int            error_per_bit, early_exit_th, sad_per_bit;
+} OracleMvCost;
+
+static int mv_err_cost(int row, int col, const OracleMvCost *p) {
+    const int dr = row - p->ref_mv[0], dc = col - p->ref_mv[1], ar = abs(dr), ac = abs(dc);
+    switch (p->mv_cost_type) {
+    case 0: {
+        const int j = dr == 0 ? (dc == 0 ? 0 : 1) : (dc == 0 ? 2 : 3);
+        const int r = dr < -(1 << 14) ? -(1 << 14) : dr > (1 << 14) ? (1 << 14) : dr;
+        const int c = dc < -(1 << 14) ? -(1 << 14) : dc > (1 << 14) ? (1 << 14) : dc;
+        const int64_t bits = (int64_t)p->mvjcost[j] + p->mvcost[0][r] + p->mvcost[1][c];
+        return (int)((bits * p->error_per_bit + (1 << 13)) >> 14);
+    }
+    case 1: return (2 * (ar + ac)) >> 3;
+    case 2: return 0;
+    case 3: return (ar + ac) >> 3;
+    case 4: return (int)(((int64_t)((ar + ac) << 8) * p->error_per_bit + (1 << 13)) >> 14);
+    default: return 0;
+    }
+}
+
+void oracle_pme_sad_loop(const void *params, const uint8_t *src, uint32_t ss, const uint8_t *ref, uint32_t rs,
+                         uint32_t bh, uint32_t bw, uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                         int16_t sx, int16_t sy, int16_t saw, int16_t sah, int16_t step, int16_t mvx, int16_t mvy) {
+    const OracleMvCost *p = (const OracleMvCost *)params;
+    int col_num = 0, step_x = 1;
+    for (int y = 0; y < sah; y += step) {
+        for (int x = 0; x < saw; x += step_x) {
+            if (saw - x < 8 && col_num == 0) continue;
+            if (col_num == 7) col_num = 0, step_x = step;
+            else col_num++, step_x = 1;
+            const uint32_t cost0 = sad_rect(src, (int)ss, ref + (size_t)y * rs + x, (int)rs, (int)bw, (int)bh);
+            const int16_t  col   = (int16_t)(mvx + (int)(uint32_t)(sx + x) * 8);
+            const int16_t  row   = (int16_t)(mvy + (int)(uint32_t)(sy + y) * 8);
+            const uint32_t cost  = cost0 + (uint32_t)mv_err_cost(row, col, p);
+            if (cost < *best_cost) *best_cost = cost, *best_mvx = col, *best_mvy = row;
         }
     }
 }

@@ -85,6 +85,9 @@ _SIGS = {
                               ctypes.c_int]),
     "oracle_pad": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "oracle_extend": (None, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "oracle_pme_sad_loop": (None, [_P, _P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                   _P, _P, _P, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16,
+                                   ctypes.c_int16, ctypes.c_int16, ctypes.c_int16]),
 }
 _lib = None
 

@@ -102,7 +102,8 @@ clean:
 .PHONY: all clean
 
 # open-loop ME SAD: the reference's EbMotionEstimation.c kernels + svt_sad_loop_kernel_c
-ME_C     := Lib/Encoder/Codec/EbMotionEstimation.c
+ME_C     := Lib/Encoder/Codec/EbMotionEstimation.c Lib/Encoder/Codec/EbProductCodingLoop.c Lib/Encoder/Codec/mcomp.c \
+            Lib/Encoder/Codec/EbRateDistortionCost.c
 ME_OBJ   := $(patsubst %.c,$(OUT)/obj/%.o,$(ME_C))
 $(OUT)/gen_golden_me: oracle/ref_harness/gen_golden_me.c $(sort $(ME_OBJ) $(MD_OBJ) $(C_OBJ))
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm -lpthread

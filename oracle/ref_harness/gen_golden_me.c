@@ -17,7 +17,15 @@
 #include <string.h>
 
 #include "EbDefinitions.h"
+#include "mcomp.h"
 #include "golden_io.h"
+
+void svt_pme_sad_loop_kernel_c(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                               uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                               uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                               int16_t search_position_start_x, int16_t search_position_start_y,
+                               int16_t search_area_width, int16_t search_area_height, int16_t search_step, int16_t mvx,
+                               int16_t mvy);
 
 void svt_ext_all_sad_calculation_8x8_16x16_c(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
                                              uint32_t mv, uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
@@ -190,6 +198,53 @@ static void gen_calls(GoldenFile *g, Rng *r) {
     free(blk), free(win), free(srcs), free(wins);
 }
 
+/* svt_pme_sad_loop_kernel_c (EbProductCodingLoop.c:1801) with every MV cost type (mcomp.c:43-68) and random
+ * entropy tables; the running best starts at a random value */
+static void gen_pme(GoldenFile *g, Rng *r) {
+    enum { N = 40, TAB = 2 * (1 << 14) + 1 };
+    static int jc[4], tab[2][TAB];
+    for (int k = 0; k < 4; k++) jc[k] = (int)rng_below(r, 2000);
+    for (int c = 0; c < 2; c++)
+        for (int k = 0; k < TAB; k++) tab[c][k] = 100 + (int)rng_below(r, 3000) + abs(k - (1 << 14)) / 4;
+    golden_put1(g, "pme_jc", 'i', 4, jc);
+    golden_put2(g, "pme_tab", 'i', 2, TAB, tab);
+    int32_t meta[N][20];
+    for (int n = 0; n < N; n++) {
+        static const int bs[][2] = {{8, 8}, {16, 16}, {32, 16}, {16, 64}, {64, 64}, {128, 128}, {4, 16}, {24, 8}};
+        const int bw = bs[n % 8][0], bh = bs[n % 8][1];
+        const int saw = 1 + (int)rng_below(r, 48), sah = 1 + (int)rng_below(r, 20), step = 1 + (int)rng_below(r, 3);
+        const int ss = 160, rs = 240, rows = sah + bh + 2;
+        uint8_t  *s = malloc((size_t)ss * bh), *rf = malloc((size_t)rs * rows);
+        const int base = (int)rng_below(r, 256);
+        for (int k = 0; k < ss * bh; k++) s[k] = (uint8_t)clampi(base + (int)rng_below(r, 61) - 30, 0, 255);
+        for (int k = 0; k < rs * rows; k++) rf[k] = (uint8_t)clampi(base + (int)rng_below(r, 61) - 30, 0, 255);
+        MV             ref_mv = {(int16_t)((int)rng_below(r, 400) - 200), (int16_t)((int)rng_below(r, 400) - 200)};
+        MV_COST_PARAMS p;
+        memset(&p, 0, sizeof p);
+        p.ref_mv       = &ref_mv;
+        p.mv_cost_type = (MV_COST_TYPE)(n % 6);
+        p.mvjcost      = jc;
+        p.mvcost[0]    = tab[0] + (1 << 14), p.mvcost[1] = tab[1] + (1 << 14);
+        p.error_per_bit = 1 + (int)rng_below(r, 400);
+        const int16_t sx = (int16_t)((int)rng_below(r, 40) - 20), sy = (int16_t)((int)rng_below(r, 40) - 20);
+        const int16_t mvx = (int16_t)((int)rng_below(r, 600) - 300), mvy = (int16_t)((int)rng_below(r, 600) - 300);
+        uint32_t      best = rng_below(r, 3) ? 0xFFFFFFFFu : (uint32_t)rng_below(r, (uint32_t)(bw * bh * 30));
+        int16_t       bx = 111, by = -111;
+        meta[n][10] = (int32_t)best;
+        svt_pme_sad_loop_kernel_c(&p, s, ss, rf, rs, bh, bw, &best, &bx, &by, sx, sy, (int16_t)saw, (int16_t)sah,
+                                  (int16_t)step, mvx, mvy);
+        int32_t *m = meta[n];
+        m[0] = bw, m[1] = bh, m[2] = saw, m[3] = sah, m[4] = step, m[5] = ss, m[6] = rs, m[7] = rows;
+        m[8] = ref_mv.row, m[9] = ref_mv.col, m[11] = (int32_t)p.mv_cost_type, m[12] = p.error_per_bit;
+        m[13] = sx, m[14] = sy, m[15] = mvx, m[16] = mvy, m[17] = (int32_t)best, m[18] = bx, m[19] = by;
+        char nm[32];
+        snprintf(nm, sizeof nm, "pme_src%d", n), golden_put1(g, nm, 'B', (uint32_t)(ss * bh), s);
+        snprintf(nm, sizeof nm, "pme_ref%d", n), golden_put1(g, nm, 'B', (uint32_t)(rs * rows), rf);
+        free(s), free(rf);
+    }
+    golden_put2(g, "pme_meta", 'i', N, 20, meta);
+}
+
 int main(int argc, char **argv) {
     const char *dir = argc > 1 ? argv[1] : "tests/golden";
     char        path[512];
@@ -198,6 +253,7 @@ int main(int argc, char **argv) {
     Rng        r = {0x4D45534144000001ull};
     gen_frames(&g, &r);
     gen_calls(&g, &r);
+    gen_pme(&g, &r);
     golden_close(&g);
     printf("wrote %s\n", path);
     return 0;

@@ -16,6 +16,8 @@
 // x), and the four waves' results are merged lexicographically -- the first minimum of the reference's scan.
 // Samples outside the reference frame read the nearest edge sample: the encoder's reference pictures are padded by
 // edge replication (svt_aom_generate_padding, EbMcp.c:95-150), so any search inside the padding reads the same values.
+#include <algorithm>
+#include <climits>
 #include <cstring>
 #include <vector>
 
@@ -455,5 +457,131 @@ extern "C" void svtgpu_sad_loop_kernel(uint8_t *src, uint32_t src_stride, uint8_
         *best_sad        = sad;
         *x_search_center = (int16_t)(p % (uint32_t)search_area_width);
         *y_search_center = (int16_t)(p / (uint32_t)search_area_width);
+    }
+}
+
+// ---- svt_pme_sad_loop_kernel (aom_dsp_rtcd.h:866; C EbProductCodingLoop.c:1801-1852): the MD full-pel refinement,
+// cost = SAD + svt_aom_fp_mv_err_cost (mcomp.c:43-68, 771) at every visited position ----
+namespace {
+// layout of the reference's svt_mv_cost_param (mcomp.h:37-48): the shim reads the caller's struct through this view
+struct MvCostView {
+    const int16_t *ref_mv; // MV {row, col}
+    int16_t        full_ref_mv[2];
+    uint8_t        mv_cost_type;
+    const int     *mvjcost;
+    const int     *mvcost[2];
+    int            error_per_bit, early_exit_th, sad_per_bit;
+};
+struct PmeArgs {
+    const uint8_t *src, *ref;
+    int            ss, rs, bh, bw, npos;
+    const int32_t *pos;                  // [npos] (x, y) search indices packed x | y << 16, in the reference's order
+    int            start_x, start_y, mvx, mvy, ref_row, ref_col, type, epb;
+    const int     *jc;                   // mvjcost[4]
+    const int     *rc, *cc;              // mvcost[0][row_lo ..], mvcost[1][col_lo ..] (clipped index ranges)
+    int            row_lo, col_lo;
+};
+
+__device__ inline int pme_mv_cost(const PmeArgs &a, int row, int col) { // svt_mv_err_cost (mcomp.c:43-68)
+    const int dr = row - a.ref_row, dc = col - a.ref_col, ar = abs(dr), ac = abs(dc);
+    switch (a.type) {
+    case 0: { // MV_COST_ENTROPY: joint + components, clipped to [MV_LOW, MV_UPP]
+        if (!a.rc) return 0;
+        const int j = dr == 0 ? (dc == 0 ? 0 : 1) : (dc == 0 ? 2 : 3);
+        const int r = min(max(dr, -(1 << 14)), 1 << 14), c = min(max(dc, -(1 << 14)), 1 << 14);
+        const long long bits = (long long)a.jc[j] + a.rc[r - a.row_lo] + a.cc[c - a.col_lo];
+        return (int)((bits * a.epb + (1ll << 13)) >> 14); // RDDIV_BITS + AV1_PROB_COST_SHIFT - RD_EPB_SHIFT + 4
+    }
+    case 1: return (2 * (ar + ac)) >> 3; // SSE_LAMBDA_LOWRES
+    case 2: return 0;                    // SSE_LAMBDA_MIDRES = 0
+    case 3: return (ar + ac) >> 3;       // SSE_LAMBDA_HDRES
+    case 4: return (int)(((long long)((ar + ac) << 8) * a.epb + (1ll << 13)) >> 14); // MV_COST_OPT
+    default: return 0;
+    }
+}
+
+__global__ __launch_bounds__(256) void pme_kernel(const PmeArgs a, unsigned long long *out) {
+    unsigned long long best = ~0ull; // (cost << 32) | order
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < a.npos; p += gridDim.x * blockDim.x) {
+        const int xi = a.pos[p] & 0xFFFF, yi = a.pos[p] >> 16;
+        const uint8_t *r = a.ref + (size_t)yi * a.rs + xi;
+        uint32_t       s = 0;
+        for (int y = 0; y < a.bh; y++)
+            for (int x = 0; x < a.bw; x++) s += (uint32_t)abs((int)a.src[y * a.ss + x] - (int)r[y * a.rs + x]);
+        const int16_t col = (int16_t)(a.mvx + (int)(uint32_t)(a.start_x + xi) * 8);
+        const int16_t row = (int16_t)(a.mvy + (int)(uint32_t)(a.start_y + yi) * 8);
+        const uint32_t cost = s + (uint32_t)pme_mv_cost(a, row, col);
+        const unsigned long long key = ((unsigned long long)cost << 32) | (uint32_t)p;
+        best = key < best ? key : best;
+    }
+    for (int o = 32; o; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o, 64);
+        best = v < best ? v : best;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMin(out, best);
+}
+} // namespace
+
+extern "C" void svtgpu_pme_sad_loop_kernel(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src,
+                                           uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                           uint32_t block_height, uint32_t block_width, uint32_t *best_cost,
+                                           int16_t *best_mvx, int16_t *best_mvy, int16_t search_position_start_x,
+                                           int16_t search_position_start_y, int16_t search_area_width,
+                                           int16_t search_area_height, int16_t search_step, int16_t mvx, int16_t mvy) {
+    const MvCostView *mc = (const MvCostView *)mv_cost_params;
+    // the visited positions in the reference's order (EbProductCodingLoop.c:1812-1826): groups of 8 columns, then a
+    // jump of search_step; a group is not started when fewer than 8 columns remain.  col_num and the column step
+    // carry over from one search row to the next, as there
+    std::vector<int32_t> pos;
+    int maxx = 0, maxy = 0, col_num = 0, step_x = 1;
+    for (int y = 0; y < search_area_height; y += search_step) {
+        for (int x = 0; x < search_area_width; x += step_x) {
+            if (search_area_width - x < 8 && col_num == 0) continue;
+            if (col_num == 7) col_num = 0, step_x = search_step;
+            else col_num++, step_x = 1;
+            pos.push_back(x | (y << 16));
+            maxx = std::max(maxx, x), maxy = std::max(maxy, y);
+        }
+    }
+    if (pos.empty()) return;
+    hipStream_t st = svtgpu_default_stream();
+    PmeArgs     a;
+    std::memset(&a, 0, sizeof a);
+    a.ss = (int)src_stride, a.rs = (int)ref_stride, a.bh = (int)block_height, a.bw = (int)block_width;
+    a.npos = (int)pos.size(), a.start_x = search_position_start_x, a.start_y = search_position_start_y;
+    a.mvx = mvx, a.mvy = mvy, a.ref_row = mc->ref_mv[0], a.ref_col = mc->ref_mv[1], a.type = mc->mv_cost_type;
+    a.epb = mc->error_per_bit;
+    Span s, r, p, o, jc, rc, cc;
+    upload_span(st, s, src, (size_t)(block_height - 1) * src_stride + block_width);
+    upload_span(st, r, ref, (size_t)(maxy + block_height - 1) * ref_stride + maxx + block_width);
+    a.src = s.d, a.ref = r.d;
+    a.pos = upload_words(st, p, pos.data(), pos.size());
+    if (a.type == 0 && mc->mvcost[0] && mc->mvcost[1] && mc->mvjcost) {
+        // the clipped component indices the positions can reach
+        auto clip = [](int v) { return std::min(std::max(v, -(1 << 14)), 1 << 14); };
+        int rlo = INT32_MAX, rhi = INT32_MIN, clo = INT32_MAX, chi = INT32_MIN;
+        for (int32_t q : pos) {
+            const int16_t col = (int16_t)(mvx + (int)(uint32_t)(search_position_start_x + (q & 0xFFFF)) * 8);
+            const int16_t row = (int16_t)(mvy + (int)(uint32_t)(search_position_start_y + (q >> 16)) * 8);
+            const int     rr = clip(row - a.ref_row), cc2 = clip(col - a.ref_col);
+            rlo = std::min(rlo, rr), rhi = std::max(rhi, rr), clo = std::min(clo, cc2), chi = std::max(chi, cc2);
+        }
+        a.row_lo = rlo, a.col_lo = clo;
+        a.jc = upload_words(st, jc, mc->mvjcost, 4);
+        a.rc = upload_words(st, rc, mc->mvcost[0] + rlo, (size_t)(rhi - rlo + 1));
+        a.cc = upload_words(st, cc, mc->mvcost[1] + clo, (size_t)(chi - clo + 1));
+    }
+    const unsigned long long init = ~0ull;
+    unsigned long long      *d    = upload_words(st, o, &init, 1);
+    hipLaunchKernelGGL(pme_kernel, dim3(std::min(256, (a.npos + 255) / 256)), dim3(256), 0, st, a, d);
+    HIP_OR_DIE(hipGetLastError());
+    unsigned long long best = 0;
+    HIP_OR_DIE(hipMemcpyAsync(&best, d, 8, hipMemcpyDeviceToHost, st));
+    HIP_OR_DIE(hipStreamSynchronize(st));
+    const uint32_t cost = (uint32_t)(best >> 32), q = (uint32_t)pos[(uint32_t)best];
+    if (cost < *best_cost) { // strict "<" against the caller's running best, first position in order on ties
+        *best_cost = cost;
+        *best_mvx  = (int16_t)(mvx + (int)(uint32_t)(search_position_start_x + (int)(q & 0xFFFF)) * 8);
+        *best_mvy  = (int16_t)(mvy + (int)(uint32_t)(search_position_start_y + (int)(q >> 16)) * 8);
     }
 }

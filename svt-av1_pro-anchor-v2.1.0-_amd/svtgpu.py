@@ -318,6 +318,9 @@ _SIGS = {
     "svtgpu_ext_sad_calculation_32x32_64x64": (None, [_P, _P, _P, _P, _P, ctypes.c_uint32, _P]),
     "svtgpu_sad_loop_kernel": (None, [_P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P,
                                       _P, _P, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_int16, ctypes.c_int16]),
+    "svtgpu_pme_sad_loop_kernel": (None, [_P, _P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, _P, _P, _P, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16,
+                                          ctypes.c_int16, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16]),
     "svtgpu_md_batch_destroy": (None, [_P]),
     "svtgpu_md_batch_nsb": (_I32, [_P]),
     "svtgpu_md_set_mvs": (ctypes.c_int, [_P, _P, _P]),

@@ -72,6 +72,7 @@ def test_device_kernels_4k_vs_oracle():
     oracle.convert(src8.ravel(), W, want.ravel(), W + 64, W, H)
     np.testing.assert_array_equal(out16, want)
     back = torch.zeros((H, W), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the fill runs on torch's stream, the conversion on the library's
     assert L.svtgpu_convert_plane(ctypes.c_void_p(d16.data_ptr()), 16, W + 64, ctypes.c_void_p(back.data_ptr()), 8, W,
                                   W, H, None) == 0
     torch.cuda.synchronize()

@@ -133,3 +133,15 @@ def test_me_search_4k_vs_oracle(ctx, saw, sah, sub):
     my = np.where(my >= 32768, my - 65536, my)
     ox, oy = origin[..., 0:1].astype(np.int32), origin[..., 1:2].astype(np.int32)
     assert ((mx >= ox) & (mx < ox + saw) & (my >= oy) & (my < oy + sah)).all()
+
+
+def test_pme_sad_loop_shim_golden(g):
+    """svt_pme_sad_loop_kernel (MD full-pel search, SAD + MV rate of every MV_COST_TYPE) against the reference's own
+    results on 40 golden calls: block sizes 4..128, steps 1..3, search areas not a multiple of 8."""
+    L = svtgpu.lib()
+    for p, keep, s, r, m in mc.pme_cases(g):
+        bw, bh, saw, sah, step, ss, rs = m[:7]
+        best, bx, by = ctypes.c_uint32(m[10] & 0xFFFFFFFF), ctypes.c_int16(111), ctypes.c_int16(-111)
+        L.svtgpu_pme_sad_loop_kernel(ctypes.byref(p), P(s), ss, P(r), rs, bh, bw, ctypes.byref(best),
+                                     ctypes.byref(bx), ctypes.byref(by), m[13], m[14], saw, sah, step, m[15], m[16])
+        assert (best.value, bx.value, by.value) == (m[17] & 0xFFFFFFFF, m[18], m[19]), m

@@ -251,3 +251,15 @@ def test_oracle_frame_ops_vs_reference():
         b = b0.copy()
         oracle.extend(b, off, st, w, h, bh, bv)
         np.testing.assert_array_equal(b, b1)
+
+
+def test_oracle_pme_sad_loop_vs_reference():
+    import ctypes
+    import me_cases as mc
+    for p, keep, s, r, m in mc.pme_cases(mc.golden()):
+        bw, bh, saw, sah, step, ss, rs = m[:7]
+        best, bx, by = ctypes.c_uint32(m[10] & 0xFFFFFFFF), ctypes.c_int16(111), ctypes.c_int16(-111)
+        oracle.lib().oracle_pme_sad_loop(ctypes.byref(p), oracle.ptr(s), ss, oracle.ptr(r), rs, bh, bw,
+                                         ctypes.byref(best), ctypes.byref(bx), ctypes.byref(by), m[13], m[14], saw, sah,
+                                         step, m[15], m[16])
+        assert (best.value, bx.value, by.value) == (m[17] & 0xFFFFFFFF, m[18], m[19]), m
