@@ -539,7 +539,7 @@ __global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, c
 // registers; per ep the A/B maps (packed B << 9 | A) go to LDS and the filters to HBM (the projection moments are
 // a separate pass over them, sgr_mom_kernel).
 // ---------------------------------------------------------------------------------------------
-constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT, SG_NP = 64 * 64 / SG_NT;
+constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT;
 
 // A, B of a self-guided pass from its box sums with 24-bit multiplies where the operands provably fit:
 // b <= 25*1023 >> (bd-8) < 2^24; a*n <= 1.64e6*25 < 2^32 with a < 2^24; (256-A)*sum <= 255*25575 < 2^24 and
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
     if (threadIdx.x < 256) xby[threadIdx.x] = c_x_by_xplus1[threadIdx.x];
     __syncthreads();
     const uint16_t *v0 = v + 3 * SG_V + 3;
-    const int       bw = t.w + 2, nq = (t.h + 2) * bw, npx = t.w * t.h;
+    const int       bw = t.w + 2, nq = (t.h + 2) * bw;
     int             s1[SG_NQ], q1[SG_NQ], s2[SG_NQ], q2[SG_NQ];
 #pragma unroll
     for (int k = 0; k < SG_NQ; k++) {
@@ -593,19 +593,17 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                 }
         }
     }
-    // this lane's pixels (threadIdx.x + k * SG_NT): value, A/B map index, filter-plane offset and row parity -- the
-    // divisions by the tile width are done once here, not per ep (a division the compiler cannot hoist past the
-    // bounds checks costs ~15 VALU ops with quarter-rate multiplies)
-    int pix[SG_NP], pc[SG_NP], po[SG_NP];
-    uint32_t podd = 0, qodd = 0; // bit k: pixel k / map position k on an odd row
+    // this lane's pixels: a column of 4 rows (fy0 .. fy0 + 3, fy0 even) at column fx, so the 3-wide map rows a filter
+    // reads are loaded and summed once for the column (6 rows for the r = 1 filter, 3 for r = 2) instead of once
+    // per pixel.  The division by the tile width is done once here, not per ep
+    const int fr = (int)threadIdx.x / t.w, fx = (int)threadIdx.x - fr * t.w, fy0 = 4 * fr;
+    const bool fon = fy0 < t.h;
+    int        pix[4];
 #pragma unroll
-    for (int k = 0; k < SG_NP; k++) {
-        const int i = threadIdx.x + k * SG_NT, y = i / t.w, x = i - y * t.w;
-        pix[k] = i < npx ? v0[y * SG_V + x] : 0;
-        pc[k]  = (y + 1) * bw + x + 1;
-        po[k]  = (t.y0 + y) * P.fstride + t.x0 + x;
-        podd |= (uint32_t)(y & 1) << k;
-    }
+    for (int k = 0; k < 4; k++) pix[k] = fon && fy0 + k < t.h ? v0[(fy0 + k) * SG_V + fx] : 0;
+    const int   fq  = fx + 1;                                             // map column of the lane's pixels
+    const size_t fo = (size_t)(t.y0 + fy0) * P.fstride + t.x0 + fx;       // filter-plane offset of row fy0
+    uint32_t    qodd = 0; // bit k: map position k on an odd row
 #pragma unroll
     for (int k = 0; k < SG_NQ; k++) qodd |= (uint32_t)(((threadIdx.x + k * SG_NT) / bw - 1) & 1) << k;
     const size_t pn = (size_t)P.fstride * P.H;
@@ -634,38 +632,55 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
         const int  ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
         const int *ab1e = ab1[e & 1], *ab2e = ab2[e & 1];
         int16_t  *f0g = P.flt + (size_t)e * 2 * pn, *f1g = f0g + pn;
+        if (fon) {
+            // 3-wide sums of map row ry (pixel-row coordinates -1 .. t.h; rows past the tile are clamped, their
+            // pixels are not stored): packed (B << 9 | A) and A-only sums of the row triple and of its centre
+            struct Row { int s, sa, c, ca; };
+            auto row = [&](const int *M, int ry) {
+                const int *Q = M + (min(ry, t.h) + 1) * bw + fq;
+                const int  l = Q[-1], c = Q[0], r = Q[1];
+                Row        w;
+                w.c = c, w.ca = c & 511, w.s = l + c + r, w.sa = (l & 511) + w.ca + (r & 511);
+                return w;
+            };
+            const int nk = min(4, t.h - fy0);
+            if (r0) { // r = 2 maps exist on odd rows: fy0 - 1, fy0 + 1, fy0 + 3
+                Row up = row(ab2e, fy0 - 1);
 #pragma unroll
-        for (int k = 0; k < SG_NP; k++) {
-            const int i = threadIdx.x + k * SG_NT;
-            if (i >= npx) break;
-            const int c = pc[k], o = po[k];
-            if (r0) {
-                const int *Q = ab2e + c;
-                int        aa, bb, sh;
-                if (!(podd >> k & 1)) {
-                    const int c6 = Q[-bw] + Q[bw], c5 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
-                    const int a6 = (Q[-bw] & 511) + (Q[bw] & 511);
-                    const int a5 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
-                    aa = a6 * 6 + a5 * 5;
-                    bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5; // sums of packed words: exact (no carry into B)
-                    sh = 9;
-                } else {
-                    const int a6 = Q[0] & 511, a5 = (Q[-1] & 511) + (Q[1] & 511);
-                    aa = a6 * 6 + a5 * 5;
-                    bb = (Q[0] >> 9) * 6 + ((Q[-1] >> 9) + (Q[1] >> 9)) * 5;
-                    sh = 8;
+                for (int h = 0; h < 2; h++) {
+                    const int k = 2 * h;
+                    if (k >= nk) break;
+                    const Row dn = row(ab2e, fy0 + k + 1);
+                    { // even row fy0 + k: rows above and below, weights 6 (centres) and 5 (corners)
+                        const int c6 = up.c + dn.c, a6 = up.ca + dn.ca;
+                        const int c5 = up.s - up.c + dn.s - dn.c, a5 = up.sa - up.ca + dn.sa - dn.ca;
+                        const int aa = a6 * 6 + a5 * 5, bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5;
+                        f0g[fo + (size_t)k * P.fstride] =
+                            (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9);
+                    }
+                    if (k + 1 < nk) { // odd row fy0 + k + 1: its own row, weights 6 (centre) and 5 (sides)
+                        const int a6 = dn.ca, a5 = dn.sa - dn.ca;
+                        const int aa = a6 * 6 + a5 * 5, bb = ((dn.c - a6) >> 9) * 6 + ((dn.s - dn.c - a5) >> 9) * 5;
+                        f0g[fo + (size_t)(k + 1) * P.fstride] =
+                            (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k + 1]) + bb + (1 << 7)) >> 8);
+                    }
+                    up = dn;
                 }
-                const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << (sh - 1))) >> sh;
-                f0g[o]      = (int16_t)f;
             }
             if (r1 && P.f1e[e] == e) { // an ep sharing an earlier slot's r = 1 filter reads that plane
-                const int *Q  = ab1e + c;
-                const int  c4 = Q[0] + Q[-1] + Q[1] + Q[-bw] + Q[bw], c3 = Q[-bw - 1] + Q[bw - 1] + Q[-bw + 1] + Q[bw + 1];
-                const int  a4 = (Q[0] & 511) + (Q[-1] & 511) + (Q[1] & 511) + (Q[-bw] & 511) + (Q[bw] & 511);
-                const int  a3 = (Q[-bw - 1] & 511) + (Q[bw - 1] & 511) + (Q[-bw + 1] & 511) + (Q[bw + 1] & 511);
-                const int  aa = a4 * 4 + a3 * 3, bb = ((c4 - a4) >> 9) * 4 + ((c3 - a3) >> 9) * 3;
-                const int f = ((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9;
-                f1g[o]      = (int16_t)f;
+                Row pv = row(ab1e, fy0 - 1), cu = row(ab1e, fy0);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (k >= nk) break;
+                    const Row nx = row(ab1e, fy0 + k + 1);
+                    // weights 4: the row triple and the centres above/below; 3: the four corners
+                    const int c4 = cu.s + pv.c + nx.c, a4 = cu.sa + pv.ca + nx.ca;
+                    const int c3 = pv.s - pv.c + nx.s - nx.c, a3 = pv.sa - pv.ca + nx.sa - nx.ca;
+                    const int aa = a4 * 4 + a3 * 3, bb = ((c4 - a4) >> 9) * 4 + ((c3 - a3) >> 9) * 3;
+                    f1g[fo + (size_t)k * P.fstride] =
+                        (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9);
+                    pv = cu, cu = nx;
+                }
             }
         }
         __syncthreads(); // ep e + 2 rewrites this ep's buffer; ep e + 1's maps are complete
