@@ -82,13 +82,14 @@ int64_t oracle_sse16(const uint16_t *a, int as, const uint16_t *b, int bs, int w
 static const int kShapeW[19] = {4, 4, 8, 8, 8, 16, 16, 16, 32, 32, 32, 64, 64, 4, 16, 8, 32, 16, 64};
 static const int kShapeH[19] = {4, 8, 4, 8, 16, 8, 16, 32, 16, 32, 64, 32, 64, 16, 4, 32, 8, 64, 16};
 
-int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs, int nref, const int16_t *mv,
-                         uint32_t *out) {
+/* SBs [sb_begin, sb_end) only; out indexed from sb_begin (SB subsets of frames too large for the whole oracle) */
+int oracle_md_dist_batch_range(const OracleFrame *src, const OracleFrame *const *refs, int nref, const int16_t *mv,
+                               int sb_begin, int sb_end, uint32_t *out) {
     const int W = src->width, H = src->height, hb = src->bit_depth > 8;
-    const int nsbx = (W + 63) / 64, nsby = (H + 63) / 64;
+    const int nsbx = (W + 63) / 64;
     uint16_t  s16[64 * 64], r16[64 * 64];
     uint8_t   s8[64 * 64], r8[64 * 64];
-    for (int sb = 0; sb < nsbx * nsby; sb++) {
+    for (int sb = sb_begin; sb < sb_end; sb++) {
         const int ox = (sb % nsbx) * 64, oy = (sb / nsbx) * 64;
         for (int y = 0; y < 64; y++)
             for (int x = 0; x < 64; x++) {
@@ -109,7 +110,7 @@ int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs,
                     r16[y * 64 + x] = hb ? ((const uint16_t *)R->plane[0])[i] : ((const uint8_t *)R->plane[0])[i];
                     r8[y * 64 + x]  = (uint8_t)r16[y * 64 + x];
                 }
-            uint32_t *o = out + ((long)sb * nref + r) * 3 * SVTGPU_MD_BLOCKS;
+            uint32_t *o = out + ((long)(sb - sb_begin) * nref + r) * 3 * SVTGPU_MD_BLOCKS;
             int       k = 0;
             for (int s = 0; s < 19; s++) {
                 const int w = kShapeW[s], h = kShapeH[s];
@@ -131,4 +132,10 @@ int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs,
         }
     }
     return SVTGPU_OK;
+}
+
+int oracle_md_dist_batch(const OracleFrame *src, const OracleFrame *const *refs, int nref, const int16_t *mv,
+                         uint32_t *out) {
+    return oracle_md_dist_batch_range(src, refs, nref, mv, 0, ((src->width + 63) / 64) * ((src->height + 63) / 64),
+                                      out);
 }

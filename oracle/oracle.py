@@ -57,6 +57,9 @@ _SIGS = {
     "oracle_sse16": (ctypes.c_int64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "oracle_md_dist_batch": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(ctypes.POINTER(OracleFrame)),
                                             ctypes.c_int, _P, _P]),
+    "oracle_md_dist_batch_range": (ctypes.c_int, [ctypes.POINTER(OracleFrame),
+                                                  ctypes.POINTER(ctypes.POINTER(OracleFrame)), ctypes.c_int, _P,
+                                                  ctypes.c_int, ctypes.c_int, _P]),
     "oracle_wiener_round": (None, [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "oracle_wiener_convolve": (None, [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int]),
@@ -247,8 +250,9 @@ def block_dist(src, ref, w, h, bd):
     return sad, sse.value, var
 
 
-def md_dist_batch(src_y, ref_ys, bd, mv):
-    """Batched MD distortion over all SBs / refs / shapes; returns uint32 [nsb][nref][3][849]."""
+def md_dist_batch(src_y, ref_ys, bd, mv, sb_range=None):
+    """Batched MD distortion over all SBs (or SBs [b, e) of sb_range) / refs / shapes; returns uint32
+    [nsb][nref][3][849]."""
     keep = []
     h, w = src_y.shape
     dummy = [np.zeros((h // 2, w // 2), src_y.dtype)] * 2
@@ -258,8 +262,9 @@ def md_dist_batch(src_y, ref_ys, bd, mv):
     nsb = ((w + 63) // 64) * ((h + 63) // 64)
     mv = np.ascontiguousarray(mv, np.int16)
     assert mv.shape == (nsb, len(ref_ys), 2)
-    out = np.zeros((nsb, len(ref_ys), 3, MD_BLOCKS), np.uint32)
-    lib().oracle_md_dist_batch(ctypes.byref(S), arr, len(Rs), ptr(mv), ptr(out))
+    b, e = sb_range if sb_range else (0, nsb)
+    out = np.zeros((e - b, len(ref_ys), 3, MD_BLOCKS), np.uint32)
+    lib().oracle_md_dist_batch_range(ctypes.byref(S), arr, len(Rs), ptr(mv), b, e, ptr(out))
     return out
 
 

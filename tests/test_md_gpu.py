@@ -82,3 +82,45 @@ def test_md_layout(ctx):
     w, h, o = svtgpu.md_layout()
     assert list(zip(w, h)) == oracle.MD_SHAPES
     assert o[-1] + 4096 // (w[-1] * h[-1]) == svtgpu.MD_BLOCKS
+
+
+def test_md_batch_8k_10bit(ctx):
+    """Config 5's frame on one GPU: 7680x4320 10-bit, 7 references, MVs reaching past the frame edges.  SB subsets
+    (first, middle and last SB rows' ends) against the oracle; on the whole frame, the shape hierarchy: for every SB
+    and reference the SADs of each shape's blocks sum to the 64x64 block's (the SSEs to within their rounding), and
+    variance <= SSE."""
+    import time
+    w, h, bd, nref = 7680, 4320, 10, 7
+    t0 = time.time()
+    src, _ = synth.frame_pair(w, h, bd, seed=0x5EED0580)
+    rng = np.random.default_rng(0x5EED0581)  # references: shifted source plus noise (fast at 8K)
+    refs = [np.clip(np.roll(src[0].astype(np.int32), (3 * k - 9, 5 - 2 * k), axis=(0, 1)) +
+                    rng.integers(-24, 25, size=(h, w)), 0, 1023).astype(np.uint16) for k in range(nref)]
+    mv = mc.mvs(w, h, nref, 8, rng_max=40)
+    S = svtgpu.Frame(ctx, w, h, bd)
+    S.upload(src)
+    R = []
+    for r in refs:
+        f = svtgpu.Frame(ctx, w, h, bd)
+        f.upload([r, src[1], src[2]])
+        R.append(f)
+    b = svtgpu.MdBatch(ctx, w, h, nref)
+    assert b.nsb == 120 * 68
+    b.set_mvs(mv)
+    b.run(S, R)
+    got = b.read()
+    print("8K MD batch: setup + run + read %.1f s" % (time.time() - t0))
+    for lo, hi in ((0, 4), (b.nsb // 2 - 2, b.nsb // 2 + 2), (b.nsb - 4, b.nsb)):
+        want = oracle.md_dist_batch(src[0], refs, bd, mv, sb_range=(lo, hi))
+        assert np.array_equal(got[lo:hi], want), (lo, hi)
+    wl, hl, off = svtgpu.md_layout()
+    whole = int(off[[s for s in range(len(wl)) if wl[s] == 64 and hl[s] == 64][0]])  # the 64x64 block
+    g64 = got.astype(np.uint64)
+    for s in range(len(wl)):
+        n = 4096 // (wl[s] * hl[s])
+        tot = g64[:, :, 0, off[s]:off[s] + n].sum(axis=-1)  # SAD: additive over a shape's tiling of the SB
+        assert np.array_equal(tot, g64[:, :, 0, whole]), (wl[s], hl[s])
+        # 10-bit SSE: each block's is rounded (>> 4, highbd_10_variance), so the sum is within n / 2 of the whole's
+        d = g64[:, :, 1, off[s]:off[s] + n].sum(axis=-1).astype(np.int64) - g64[:, :, 1, whole].astype(np.int64)
+        assert (np.abs(d) <= n // 2 + 1).all(), (wl[s], hl[s], int(np.abs(d).max()))
+    assert (got[:, :, 2, :] <= got[:, :, 1, :]).all()

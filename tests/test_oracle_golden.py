@@ -263,3 +263,16 @@ def test_oracle_pme_sad_loop_vs_reference():
                                          ctypes.byref(best), ctypes.byref(bx), ctypes.byref(by), m[13], m[14], saw, sah,
                                          step, m[15], m[16])
         assert (best.value, bx.value, by.value) == (m[17] & 0xFFFFFFFF, m[18], m[19]), m
+
+
+def test_oracle_md_batch_sb_range():
+    """The SB-range oracle (used on 8K subsets) equals the matching rows of the whole-frame oracle."""
+    import md_cases as mc
+    import synth
+    w, h, bd, nref = 200, 136, 10, 2
+    src, _ = synth.frame_pair(w, h, bd, seed=0x5EED0590)
+    refs = mc.ref_frames(w, h, bd, nref, 0x5EED0591)
+    mv = mc.mvs(w, h, nref, 3, rng_max=30)
+    whole = oracle.md_dist_batch(src[0], refs, bd, mv)
+    for b, e in ((0, 3), (5, 12), (9, 12)):
+        assert np.array_equal(oracle.md_dist_batch(src[0], refs, bd, mv, sb_range=(b, e)), whole[b:e])
