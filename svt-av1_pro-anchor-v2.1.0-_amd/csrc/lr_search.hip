@@ -2422,7 +2422,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         // highest priority so its workgroups are dispatched first while the self-guided filters fill the CUs
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&s->wst, hipStreamNonBlocking, greatest));
+        static const int wprio = [] { // SVTGPU_WN_PRIO=0: the Wiener chain at normal priority (A/B)
+            const char *e = std::getenv("SVTGPU_WN_PRIO");
+            return e ? std::atoi(e) : 1;
+        }();
+        HIP_TRY(hipStreamCreateWithPriority(&s->wst, hipStreamNonBlocking, wprio ? greatest : least));
         HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
     }
