@@ -84,8 +84,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--bit-depth", type=int, default=10)
@@ -123,14 +123,14 @@ def parse():
 # before this process touches the GPU; their JSON lines are summarised under config.matrix
 MATRIX = [
     ("config1_1080p8_cdef", ["--width", "1920", "--height", "1080", "--bit-depth", "8", "--stages", "cdef",
-                             "--cpu-grid", "4x4", "--cpu-passes", "120", "--steps", "20", "--warmup", "3",
+                             "--cpu-grid", "4x4", "--cpu-passes", "120", "--steps", "100", "--warmup", "5",
                              "--frames-in-flight", "1"]),
     ("pipeline_1080p8", ["--width", "1920", "--height", "1080", "--bit-depth", "8", "--no-cpu-baseline",
-                         "--steps", "12", "--warmup", "2"]),
+                         "--steps", "60", "--warmup", "5"]),
     ("pipeline_1080p10", ["--width", "1920", "--height", "1080", "--bit-depth", "10", "--no-cpu-baseline",
-                          "--steps", "12", "--warmup", "2"]),
+                          "--steps", "60", "--warmup", "5"]),
     ("pipeline_4k8", ["--width", "3840", "--height", "2160", "--bit-depth", "8", "--no-cpu-baseline",
-                      "--steps", "10", "--warmup", "2"]),
+                      "--steps", "40", "--warmup", "5"]),
 ]
 
 
