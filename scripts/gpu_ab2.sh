@@ -11,7 +11,7 @@ tail -3 gpurun_out/pytest_gpu.log
 i=0
 for cfg in "$@"; do
   for f in 1 3; do
-    env $cfg timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-matrix --frames-in-flight $f > gpurun_out/ab_${i}_f$f.log 2>&1 || exit $?
+    env $cfg timeout -k 10 300 python bench.py --steps ${STEPS:-60} --warmup 5 --no-cpu-baseline --no-matrix --frames-in-flight $f > gpurun_out/ab_${i}_f$f.log 2>&1 || exit $?
     echo "[$cfg] F=$f $(tail -1 gpurun_out/ab_${i}_f$f.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["config"]["stage_ms"]["lr_search_apply"], d["config"].get("lr_search_kernel_ms"))')"
   done
   i=$((i+1))

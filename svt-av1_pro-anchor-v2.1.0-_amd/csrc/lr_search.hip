@@ -2190,10 +2190,13 @@ bool wn_use_unit() {
     }();
     return v;
 }
-int wn_unit_ng() { // tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG: 2 or 4)
+// tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG: 2 or 4).  2 by default: at three frames in flight the
+// 512-lane workgroups leave room on the CUs for the other frames' kernels (2030-2047 vs 2012-2019 Mpx/s, same box,
+// profiles/r02/s16); a lone frame's descent is 1 % faster with 4
+int wn_unit_ng() {
     static const int v = [] {
         const char *e = std::getenv("SVTGPU_WN_NG");
-        return e && std::atoi(e) == 2 ? 2 : 4;
+        return e && std::atoi(e) == 4 ? 4 : 2;
     }();
     return v;
 }
