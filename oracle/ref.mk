@@ -84,10 +84,16 @@ SVTGPU_SO := svt-av1_pro-anchor-v2.1.0-_amd/lib/libsvtgpu.so
 $(OUT)/rtcd_pipe: oracle/ref_harness/gen_golden_pipe.c oracle/ref_harness/ref_cdef_process.c \
                   oracle/ref_harness/ref_mode_config.c $(sort $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ)) $(SVTGPU_SO)
 	@mkdir -p $(OUT)/obj/bind
-	$(CC) $(filter-out -w,$(CFLAGS)) -DSVTGPU_BIND -Iinclude -Werror=incompatible-pointer-types \
+	$(CC) $(filter-out -w,$(CFLAGS)) -DSVTGPU_BIND -Iinclude -Werror=incompatible-pointer-types -Werror=discarded-qualifiers \
 	    -c oracle/ref_harness/gen_golden_pipe.c -o $(OUT)/obj/bind/gen_golden_pipe.o
 	$(CC) $(CFLAGS) $(OUT)/obj/bind/gen_golden_pipe.o $(filter-out %gen_golden_pipe.c,$(filter %.c,$^)) $(filter %.o,$^) \
 	    -o $@ -Wl,--gc-sections -L$(dir $(SVTGPU_SO)) -lsvtgpu -Wl,-rpath,'$$ORIGIN/../../$(dir $(SVTGPU_SO))' -lm -lpthread
+
+# compile-only check of every shim prototype against the reference's pointer types (tests/test_rtcd_bind.py, CPU)
+bindcheck:
+	$(CC) $(filter-out -w,$(CFLAGS)) -DSVTGPU_BIND -Iinclude -Werror=incompatible-pointer-types \
+	    -Werror=discarded-qualifiers -fsyntax-only oracle/ref_harness/gen_golden_pipe.c
+.PHONY: bindcheck
 
 # the round-2 RTCD shims (C, and the AVX2-only svt_cdef_filter_block_8xn_16)
 $(OUT)/gen_golden_shims: oracle/ref_harness/gen_golden_shims.c $(sort $(LR_OBJ) $(MD_OBJ) $(C_OBJ)) $(AVX2_OBJ)

@@ -4,7 +4,10 @@ libsvtgpu shims.
 oracle/_ref/rtcd_pipe is oracle/ref_harness/gen_golden_pipe.c compiled against the reference headers with
 -DSVTGPU_BIND and -Werror=incompatible-pointer-types: every shim (loop filter x16, CDEF filter / 8xn / find_dir /
 dist / search_one_dual / copy_rect8, Wiener and self-guided filters, compute_stats, pixel_proj_error,
-get_proj_subspace, mse16x16, the full-distortion kernels) is assigned to the reference's pointer without a cast,
+get_proj_subspace, mse16x16, the full-distortion kernels; and, compile-only, the ME / MD distortion / frame-buffer
+shims: sad / x4d / variance / highbd variance / sub-pixel variance of all sizes, sse, nxm SAD, the open-loop ME and
+MD full-pel search kernels, the 8 <-> 16-bit conversions, padding, frame extension) is assigned to the reference's
+pointer without a cast,
 and svt_av1_pick_filter_level, svt_av1_loop_filter_frame, cdef_seg_search / finish_cdef_search /
 svt_av1_cdef_frame, restoration_seg_search / rest_finish_search / svt_av1_loop_restoration_filter_frame then run
 through the device.  Every output must equal the pure-C run of the same code (tests/golden/pipe_<case>.npz)."""
@@ -45,3 +48,12 @@ def test_reference_frame_code_through_device_shims(case):
                 arr[arr[:, 0] != 1, 1:17] = 0
                 arr[arr[:, 0] != 2, 17:20] = 0
         np.testing.assert_array_equal(a, b, err_msg="%s: %s differs between the C and the device-shim runs" % (case, k))
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/Source"), reason="reference headers not present")
+def test_shim_prototypes_match_reference_pointers():
+    """CPU, compile-only: include/svtgpu.h against the reference's RTCD headers under -Werror=incompatible-pointer-types
+    and -Werror=discarded-qualifiers (oracle/ref.mk bindcheck)."""
+    r = subprocess.run(["make", "-s", "-f", "oracle/ref.mk", "bindcheck"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
