@@ -544,14 +544,18 @@ constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT -
 // A, B of a self-guided pass from its box sums with 24-bit multiplies where the operands provably fit:
 // b <= 25*1023 >> (bd-8) < 2^24; a*n <= 1.64e6*25 < 2^32 with a < 2^24; (256-A)*sum <= 255*25575 < 2^24 and
 // times one_by_x (<= 455) < 2^32.  Only p*s wraps like the reference's u32 product and keeps the full multiply.
-__device__ inline void sgr_ab_fast(int sum, int sq, int n, int s, int bd, const int *x_by_xplus1, int *A, int *B) {
-    const uint32_t a = (uint32_t)((sq + ((1 << (2 * (bd - 8))) >> 1)) >> (2 * (bd - 8)));
-    const uint32_t b = (uint32_t)((sum + ((1 << (bd - 8)) >> 1)) >> (bd - 8));
+// Split in two so that a lane's table lookups (A = x_by_xplus1[z]) of all its positions are issued together:
+// sgr_z gives the clamped table index, sgr_ab_pack the packed map word (B << 9 | A).  sh = bd - 8.
+__device__ inline uint32_t sgr_z(int sum, int sq, int n, int s, int sh) {
+    const uint32_t a = (uint32_t)((sq + ((1 << (2 * sh)) >> 1)) >> (2 * sh));
+    const uint32_t b = (uint32_t)((sum + ((1 << sh) >> 1)) >> sh);
     const uint32_t an = __umul24(a, (uint32_t)n), bb = __umul24(b, b);
     const uint32_t p  = an < bb ? 0u : an - bb;
-    const uint32_t z  = (p * (uint32_t)s + (1u << 19)) >> 20;
-    *A                = x_by_xplus1[min(z, 255u)];
-    *B = (int)((__umul24(__umul24((uint32_t)(256 - *A), (uint32_t)sum), (uint32_t)c_one_by_x[n - 1]) + (1u << 11)) >> 12);
+    return min((p * (uint32_t)s + (1u << 19)) >> 20, 255u);
+}
+__device__ inline int sgr_ab_pack(int A, int sum, int n) {
+    const int B = (int)((__umul24(__umul24((uint32_t)(256 - A), (uint32_t)sum), (uint32_t)c_one_by_x[n - 1]) + (1u << 11)) >> 12);
+    return (B << 9) | A;
 }
 
 template <typename T>
@@ -607,21 +611,36 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
 #pragma unroll
     for (int k = 0; k < SG_NQ; k++) qodd |= (uint32_t)(((threadIdx.x + k * SG_NT) / bw - 1) & 1) << k;
     const size_t pn = (size_t)P.fstride * P.H;
+    const int sh = P.bd - 8;
     auto build_ab = [&](int e) { // A/B maps of ep index e into buffer e & 1
         const int ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
         int      *m1 = ab1[e & 1], *m2 = ab2[e & 1];
+        if (r1 && P.f1e[e] == e) { // r = 1 (3x3) at every map position
+            const int sp = c_sgr_s[ep][1];
+            uint32_t  z[SG_NQ];
+            int       a[SG_NQ];
 #pragma unroll
-        for (int k = 0; k < SG_NQ; k++) {
-            const int q = threadIdx.x + k * SG_NT;
-            if (q >= nq) break;
-            int a, b;
-            if (r1 && P.f1e[e] == e) {
-                sgr_ab_fast(s1[k], q1[k], 9, c_sgr_s[ep][1], P.bd, xby, &a, &b);
-                m1[q] = (b << 9) | a;
+            for (int k = 0; k < SG_NQ; k++) z[k] = sgr_z(s1[k], q1[k], 9, sp, sh);
+#pragma unroll
+            for (int k = 0; k < SG_NQ; k++) a[k] = xby[z[k]]; // the lookups in flight together
+#pragma unroll
+            for (int k = 0; k < SG_NQ; k++) {
+                const int q = threadIdx.x + k * SG_NT;
+                if (q < nq) m1[q] = sgr_ab_pack(a[k], s1[k], 9);
             }
-            if (r0 && (qodd >> k & 1)) {
-                sgr_ab_fast(s2[k], q2[k], 25, c_sgr_s[ep][0], P.bd, xby, &a, &b);
-                m2[q] = (b << 9) | a;
+        }
+        if (r0) { // r = 2 (5x5) on the odd rows
+            const int sp = c_sgr_s[ep][0];
+            uint32_t  z[SG_NQ];
+            int       a[SG_NQ];
+#pragma unroll
+            for (int k = 0; k < SG_NQ; k++) z[k] = (qodd >> k & 1) ? sgr_z(s2[k], q2[k], 25, sp, sh) : 0u;
+#pragma unroll
+            for (int k = 0; k < SG_NQ; k++) a[k] = xby[z[k]];
+#pragma unroll
+            for (int k = 0; k < SG_NQ; k++) {
+                const int q = threadIdx.x + k * SG_NT;
+                if (q < nq && (qodd >> k & 1)) m2[q] = sgr_ab_pack(a[k], s2[k], 25);
             }
         }
     };
