@@ -740,16 +740,31 @@ __global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long l
         for (int j = 0; j < 4; j++) uu[k][j] = dv[j] << 4, ss[k][j] = (sv[j] - dv[j]) << 4;
     }
     const int pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
+    // the next ep's two filter planes are loaded while this ep's moments are formed and reduced
+    int2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
+    auto fetch = [&](int e, int2 *x0, int2 *x1) {
+        const int      ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            x0[k] = x1[k] = make_int2(0, 0);
+            if (!on[k]) continue;
+            if (r0) x0[k] = *(const int2 *)(f0 + fo[k]);
+            if (r1) x1[k] = *(const int2 *)(f1 + fo[k]);
+        }
+    };
+    if (P.ne > 0) fetch(0, w0, w1);
     for (int e = 0; e < P.ne; e++) {
         const int          ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-        const int16_t     *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
+        if (e + 1 < P.ne) fetch(e + 1, n0, n1);
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
             if (!on[k]) continue;
-            int a0[4] = {0, 0, 0, 0}, a1[4] = {0, 0, 0, 0};
-            if (r0) load4s(f0 + fo[k], a0);
-            if (r1) load4s(f1 + fo[k], a1);
+            const int a0[4] = {(int)(int16_t)(w0[k].x & 0xFFFF), w0[k].x >> 16, (int)(int16_t)(w0[k].y & 0xFFFF),
+                               w0[k].y >> 16};
+            const int a1[4] = {(int)(int16_t)(w1[k].x & 0xFFFF), w1[k].x >> 16, (int)(int16_t)(w1[k].y & 0xFFFF),
+                               w1[k].y >> 16};
             uint32_t m0 = 0, m1 = 0;
             int      m3 = 0, m4 = 0;
 #pragma unroll
@@ -770,6 +785,8 @@ __global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long l
 #pragma unroll
             for (int q = 0; q < 5; q++)
                 if (tot[q]) atomicAdd((unsigned long long *)&mom[(size_t)(pb + e) * 5 + q], tot[q]);
+#pragma unroll
+        for (int k = 0; k < NCH; k++) w0[k] = n0[k], w1[k] = n1[k];
     }
     PROF_END(tk);
 }
