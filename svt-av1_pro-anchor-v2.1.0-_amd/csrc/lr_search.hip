@@ -152,12 +152,27 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     uint32_t ps = 0, pe = 0; // <= 16 samples per lane: fits 32 bits
-    for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
-        const int y = t.y0 + i / t.w, x = t.x0 + i % t.w;
-        const int dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
-        ps += (unsigned)dv;
-        pe += (uint32_t)((dv - sv) * (dv - sv));
+    // 4-sample chunks (tile x offsets and widths are multiples of 4): chunk k of this lane is row
+    // (threadIdx.x >> 4) + 16 k, columns 4 (threadIdx.x & 15) .. + 3; all four chunks' loads are issued first
+    int dv[4][4], sv[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = (threadIdx.x >> 4) + 16 * k, c = 4 * (threadIdx.x & 15);
+#pragma unroll
+        for (int j = 0; j < 4; j++) dv[k][j] = sv[k][j] = 0;
+        if (r < t.h && c < t.w) {
+            load4(d + (size_t)(t.y0 + r) * P.dstride + t.x0 + c, dv[k]);
+            load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + c, sv[k]);
+        }
     }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int e = dv[k][j] - sv[k][j];
+            ps += (uint32_t)dv[k][j];
+            pe += (uint32_t)(e * e);
+        }
     const unsigned long long tsum = wave_sum_u32_wide(ps), tsse = wave_sum_u32_wide(pe);
     if ((threadIdx.x & 63) == WAVE_LAST) {
         atomicAdd(&sum[t.unit], tsum);
