@@ -973,17 +973,31 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
     const int16_t   *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)(e >= 0 ? P.f1e[e] : e) * 2 * pn + pn;
     const int        maxv = (1 << P.bd) - 1;
     unsigned long long acc = 0;
-    for (int i = threadIdx.x; i < t.w * t.h; i += 256) {
-        const int    y = t.y0 + i / t.w, x = t.x0 + i % t.w;
+    // 4-sample chunks as in unit_sums_kernel: chunk k of this lane is row (threadIdx.x >> 4) + 16 k, columns
+    // 4 (threadIdx.x & 15) .. + 3
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = (threadIdx.x >> 4) + 16 * k, c = 4 * (threadIdx.x & 15);
+        if (r >= t.h || c >= t.w) continue;
+        const int    y = t.y0 + r, x = t.x0 + c;
         const size_t o = (size_t)y * P.fstride + x;
-        const int    dv = d[(size_t)y * P.dstride + x], sv = s[(size_t)y * P.sstride + x];
-        const int    u = dv << 4;
-        int          v = u << 7;
-        if (r0 > 0) v += xq0 * (f0[o] - u);
-        if (r1 > 0) v += xq1 * (f1[o] - u);
-        const int16_t w  = (int16_t)((v + (1 << 10)) >> 11);
-        const int     ov = min(max((int)w, 0), maxv);
-        acc += (unsigned long long)((ov - sv) * (ov - sv));
+        int          dv[4], sv[4], g0[4] = {0, 0, 0, 0}, g1[4] = {0, 0, 0, 0};
+        load4(d + (size_t)y * P.dstride + x, dv);
+        load4(s + (size_t)y * P.sstride + x, sv);
+        if (r0 > 0) load4s(f0 + o, g0);
+        if (r1 > 0) load4s(f1 + o, g1);
+        uint32_t e2 = 0; // 4 squared errors of at most 1023^2
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int u = dv[j] << 4;
+            int       v = u << 7;
+            if (r0 > 0) v += xq0 * (g0[j] - u);
+            if (r1 > 0) v += xq1 * (g1[j] - u);
+            const int16_t w  = (int16_t)((v + (1 << 10)) >> 11);
+            const int     ov = min(max((int)w, 0), maxv);
+            e2 += (uint32_t)((ov - sv[j]) * (ov - sv[j]));
+        }
+        acc += e2;
     }
     const unsigned long long at = wave_sum(acc);
     if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], at);
