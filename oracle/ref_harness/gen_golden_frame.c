@@ -35,7 +35,7 @@ int main(int argc, char **argv) {
     Rng        r = {0x4652414D45000001ull};
     svt_memcpy = svt_memcpy_c;
     enum { N = 12 };
-    int32_t meta[3][N][8];
+    int32_t meta[3][N][8] = {{{0}}}; /* fields a case does not use stay 0: the fixture is reproducible */
     for (int n = 0; n < N; n++) {
         /* conversion: w x h inside strides with slack; the destination's slack keeps its old contents */
         const int w = 1 + (int)rng_below(&r, 200), h = 1 + (int)rng_below(&r, 40);

@@ -53,7 +53,7 @@ static void gen_proj(const char *dir) {
                 dat[y * w + x] = in[(y + 3) * st + x + 3];
                 src[y * w + x] = (uint16_t)clampi(dat[y * w + x] + (int)rng_below(&r, 2 * (8 << (bd - 8)) + 1) - (8 << (bd - 8)), 0, maxv);
             }
-        int32_t *f0 = malloc(sizeof(int32_t) * (size_t)w * h), *f1 = malloc(sizeof(int32_t) * (size_t)w * h);
+        int32_t *f0 = calloc((size_t)w * h, sizeof(int32_t)), *f1 = calloc((size_t)w * h, sizeof(int32_t)); /* r = 0 eps leave one unwritten */
         uint8_t *in8 = malloc((size_t)(h + 6) * st), *src8 = malloc((size_t)w * h), *dat8 = malloc((size_t)w * h);
         for (int k = 0; k < (h + 6) * st; k++) in8[k] = (uint8_t)in[k];
         for (int k = 0; k < w * h; k++) src8[k] = (uint8_t)src[k], dat8[k] = (uint8_t)dat[k];

@@ -223,10 +223,17 @@ extern "C" int svtgpu_cdef_set_fb_bsize(SvtGpuCdefFrameState *s, const uint8_t *
         s->d_fb_kind = nullptr, s->h_fb_kind = nullptr, s->d_mse_rem = nullptr;
         return SVTGPU_OK;
     }
-    if (!s->h_fb_kind) {
-        s->h_fb_kind = new int8_t[s->nfb];
-        HIP_TRY(hipMalloc(&s->d_fb_kind, s->nfb));
-        HIP_TRY(hipMalloc(&s->d_mse_rem, (size_t)3 * s->nfb * 64));
+    if (!s->h_fb_kind) { // all three buffers or none: the search folds SB128 areas only when d_fb_kind is set
+        int8_t  *dk = nullptr;
+        uint8_t *dr = nullptr;
+        hipError_t e = hipMalloc(&dk, s->nfb);
+        if (e == hipSuccess) e = hipMalloc(&dr, (size_t)3 * s->nfb * 64);
+        if (e != hipSuccess) {
+            if (dk) (void)hipFree(dk);
+            svtgpu_set_last_hip_error(e, "cdef sb128 tables", __FILE__, __LINE__);
+            return e == hipErrorOutOfMemory ? SVTGPU_ERR_OOM : SVTGPU_ERR_HIP;
+        }
+        s->d_fb_kind = dk, s->d_mse_rem = dr, s->h_fb_kind = new int8_t[s->nfb];
     }
     // BLOCK_64X128 = 13, BLOCK_128X64 = 14, BLOCK_128X128 = 15 (EbDefinitions.h); the parity tests of
     // EbCdefProcess.c:193-196 mark the halves the search skips

@@ -1702,6 +1702,249 @@ __global__ __launch_bounds__(256 * NG) void wiener_unit_kernel(const SearchArgs 
     PROF_END(tk);
 }
 
+// ---------------------------------------------------------------------------------------------
+// The Wiener descent of one unit per workgroup with the whole unit resident on the CU (default).
+// finer_tile_search_wiener_seg (EbRestorationPick.c:1042-1146) evaluates ~40 candidates one after the other, each
+// over every pixel of the unit; the critical path of the search is that chain for the largest unit.  Here nothing
+// of a candidate touches global memory:
+//   * 1024 lanes; lane = (column pair cp, row segment sg) of the unit: output columns x = 2cp, 2cp+1, rows
+//     [sg*R, sg*R+R).  A wave holds 64 consecutive column pairs of one segment, so per-segment control is uniform;
+//   * the lane's source pixels stay in registers (one packed (x, x+1) pair per row);
+//   * the edge-clamped CDEF window of the unit (rows -3..h+2, columns -4..w+5, 16-bit) is staged into LDS once
+//     when it fits; larger units (the frame's bottom unit row, 256 x 376 at 4K) read it from global memory, where
+//     only this workgroup touches it (L2-resident);
+//   * per candidate every lane walks its rows with a rolling window of four vertical pairs of the horizontal pass
+//     per column (the rows y-3 .. y+4 the vertical pass needs), computing one new pair of horizontal rows per pair
+//     of output rows: 4 v_dot2 per horizontal and per vertical output, the add-source term folded into the centre
+//     taps, the SSE as one v_dot2 of the packed (out - src) pair with itself;
+//   * two workgroup barriers per candidate: the SSE reduction and lane 0's descent step (Descent::report / next,
+//     exactly as the other Wiener paths), whose taps every lane reads back into scalar registers.
+// The candidate count per unit is bounded (WR_MAX_ROUNDS; a descent always ends far earlier): on overflow the
+// descent stops and *status is set, which search_frame reports as SVTGPU_ERR_HIP.
+// ---------------------------------------------------------------------------------------------
+constexpr int WR_NT = 1024, WR_RMAX = 32, WR_MAX_ROUNDS = 4096;
+constexpr int WR_LDS_CAP = 152 * 1024; // largest CDEF window kept in LDS (bytes); larger units read global memory
+
+// geometry of a unit in the lane layout: column-pair slots per segment (a multiple of 64), segments, rows per segment
+struct WrGeo {
+    int cpw, nseg, R;
+};
+__host__ __device__ inline WrGeo wr_geo(int w, int h) {
+    WrGeo g;
+    g.cpw  = (((w + 1) >> 1) + 63) & ~63;
+    g.nseg = WR_NT / g.cpw;
+    g.R    = (h + g.nseg - 1) / g.nseg;
+    return g;
+}
+__host__ __device__ inline int wr_window_bytes(int w, int h) { return (h + 6) * ((w + 10) >> 1) * 4; }
+// LDS mode: the window in LDS and the source rows in registers; else both are read from global memory per candidate
+__host__ __device__ inline bool wr_lds_mode(int w, int h, int lds_cap) {
+    return wr_window_bytes(w, h) <= lds_cap && wr_geo(w, h).R <= WR_RMAX;
+}
+
+// the 5 packed sample pairs of window row r (unit rows -3.., columns x-4 .. x+5) for output columns x, x+1
+template <typename T, bool LDSW>
+__device__ inline void wr_fetch(const uint32_t *win, int ws, const PlaneArgs &P, int ux, int uy, int hw, int xc, int r,
+                                uint32_t *p) {
+    r = min(r, hw - 1); // rows past the window only feed outputs that are never used
+    if constexpr (LDSW) {
+        const uint32_t *q = win + r * ws + (xc >> 1);
+#pragma unroll
+        for (int k = 0; k < 5; k++) p[k] = q[k];
+    } else {
+        const T  *d  = (const T *)P.dgd;
+        const int fy = min(max(uy - 3 + r, 0), P.H - 1), fx = ux + xc - 4;
+        const T  *row = d + (size_t)fy * P.dstride;
+        if (fx >= 0 && fx + 10 <= P.W) {
+            if constexpr (sizeof(T) == 2) {
+                const uint32_t *q = (const uint32_t *)(row + fx);
+#pragma unroll
+                for (int k = 0; k < 5; k++) p[k] = q[k];
+            } else {
+                const uint16_t *q = (const uint16_t *)(row + fx);
+#pragma unroll
+                for (int k = 0; k < 5; k++) p[k] = (uint32_t)(q[k] & 0xFF) | ((uint32_t)(q[k] >> 8) << 16);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const int c0 = min(max(fx + 2 * k, 0), P.W - 1), c1 = min(max(fx + 2 * k + 1, 0), P.W - 1);
+                p[k] = (uint32_t)row[c0] | ((uint32_t)row[c1] << 16);
+            }
+        }
+    }
+}
+
+template <typename T, bool LDSW>
+__device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, const uint32_t *win, int ws, int ux,
+                       int uy, int w, int h, int *s_mode, int16_t *s_taps, unsigned long long *s_part, int32_t *status,
+                       unsigned long long &npx) {
+    const WrGeo g  = wr_geo(w, h);
+    const int   cp = threadIdx.x % g.cpw, sg = threadIdx.x / g.cpw, x = 2 * cp;
+    const int   seg0 = sg * g.R, nrows = sg < g.nseg ? max(0, min(g.R, h - seg0)) : 0;
+    const int   xc = min(x, (w - 1) & ~1), hw = h + 6; // an addressable column for lanes right of the unit
+    const uint32_t dmask = x >= w ? 0u : x + 1 >= w ? 0xFFFFu : 0xFFFFFFFFu;
+    // the lane's source pixels, one (x, x+1) pair per row: registers (LDS mode, <= WR_RMAX rows), else global memory
+    const T   *sbase = (const T *)P.src + (size_t)(uy + seg0) * P.sstride + ux + xc;
+    const bool s1    = xc + 1 < w; // an odd unit width: the lane's second column is outside the unit
+    auto       load_src = [&](int k) -> uint32_t {
+        const T *q = sbase + (size_t)k * P.sstride;
+        return (uint32_t)q[0] | ((uint32_t)(s1 ? q[1] : 0) << 16);
+    };
+    uint32_t sv[LDSW ? WR_RMAX : 1];
+    if constexpr (LDSW) {
+#pragma unroll
+        for (int k = 0; k < WR_RMAX; k++)
+            if (k < nrows) sv[k] = load_src(k);
+    }
+    const WienerRound rr  = wiener_round(P.bd);
+    const int         lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, maxv = (1 << P.bd) - 1;
+    const int         hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1)), vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
+    const int         jend = ((nrows + 1) >> 1) + 3;
+    int               rounds = 0;
+    while (*s_mode) {
+        // the candidate's taps (uniform: scalar registers), the add-source 128 folded into the centre taps
+        int hf[8], vf[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) hf[k] = s_taps[k], vf[k] = s_taps[8 + k];
+        hf[3] += 128, vf[3] += 128;
+        auto sp = [](int lo, int hi) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)pack2(lo, hi)); };
+        const uint32_t He0 = sp(0, hf[0]), He1 = sp(hf[1], hf[2]), He2 = sp(hf[3], hf[4]), He3 = sp(hf[5], hf[6]);
+        const uint32_t Ho0 = sp(hf[0], hf[1]), Ho1 = sp(hf[2], hf[3]), Ho2 = sp(hf[4], hf[5]), Ho3 = sp(hf[6], 0);
+        const uint32_t Ve0 = sp(vf[0], vf[1]), Ve1 = sp(vf[2], vf[3]), Ve2 = sp(vf[4], vf[5]), Ve3 = sp(vf[6], 0);
+        const uint32_t Vo0 = sp(0, vf[0]), Vo1 = sp(vf[1], vf[2]), Vo2 = sp(vf[3], vf[4]), Vo3 = sp(vf[5], vf[6]);
+        auto hclip = [&](int s) { return min(max(s >> rr.r0, 0), lim); };
+        auto vclip = [&](int s) { return min(max(s >> rr.r1, 0), maxv); };
+        uint32_t hq0[4] = {0, 0, 0, 0}, hq1[4] = {0, 0, 0, 0}; // vertical pairs of the horizontal pass, x and x+1
+        uint32_t pa[5], pb[5], na[5], nb[5];
+        int      e = 0; // <= 2 * 77 squared errors of <= 1023^2
+        // step j: the horizontal pass of window rows seg0+2j, +1 (unit rows seg0+2j-3, -2) at columns x, x+1 (pa, pb);
+        // from j = 3 on, output rows seg0+2i, +1 (i = j-3) from horizontal rows 2i-3 .. 2i+4 against source pairs sa, sb
+        auto step = [&](int j, uint32_t sa, uint32_t sb) {
+            const int a0 = hclip(dot2(pa[3], He3, dot2(pa[2], He2, dot2(pa[1], He1, dot2(pa[0], He0, hb)))));
+            const int b0 = hclip(dot2(pa[4], Ho3, dot2(pa[3], Ho2, dot2(pa[2], Ho1, dot2(pa[1], Ho0, hb)))));
+            const int a1 = hclip(dot2(pb[3], He3, dot2(pb[2], He2, dot2(pb[1], He1, dot2(pb[0], He0, hb)))));
+            const int b1 = hclip(dot2(pb[4], Ho3, dot2(pb[3], Ho2, dot2(pb[2], Ho1, dot2(pb[1], Ho0, hb)))));
+            hq0[0] = hq0[1], hq0[1] = hq0[2], hq0[2] = hq0[3], hq0[3] = pack2(a0, a1);
+            hq1[0] = hq1[1], hq1[1] = hq1[2], hq1[2] = hq1[3], hq1[3] = pack2(b0, b1);
+            if (j >= 3) {
+                const int i  = j - 3;
+                const int o0 = vclip(dot2(hq0[3], Ve3, dot2(hq0[2], Ve2, dot2(hq0[1], Ve1, dot2(hq0[0], Ve0, vb)))));
+                const int o1 = vclip(dot2(hq1[3], Ve3, dot2(hq1[2], Ve2, dot2(hq1[1], Ve1, dot2(hq1[0], Ve0, vb)))));
+                const uint32_t d0 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(o0, o1)) -
+                                                                          __builtin_bit_cast(v2i16, sa)) & dmask;
+                e = dot2(d0, d0, e);
+                if (2 * i + 1 < nrows) {
+                    const int q0 = vclip(dot2(hq0[3], Vo3, dot2(hq0[2], Vo2, dot2(hq0[1], Vo1, dot2(hq0[0], Vo0, vb)))));
+                    const int q1 = vclip(dot2(hq1[3], Vo3, dot2(hq1[2], Vo2, dot2(hq1[1], Vo1, dot2(hq1[0], Vo0, vb)))));
+                    const uint32_t d1 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(q0, q1)) -
+                                                                              __builtin_bit_cast(v2i16, sb)) & dmask;
+                    e = dot2(d1, d1, e);
+                }
+            }
+        };
+        if (nrows) {
+            wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0, na);
+            wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 1, nb);
+        }
+        if constexpr (LDSW) { // unrolled: the source pairs are addressed by constants
+#pragma unroll
+            for (int j = 0; j < WR_RMAX / 2 + 3; j++) {
+                if (j < jend) { // uniform per wave (one segment per wave)
+#pragma unroll
+                    for (int k = 0; k < 5; k++) pa[k] = na[k], pb[k] = nb[k];
+                    if (j + 1 < jend) { // the next pair of window rows is in flight during this step
+                        wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 2, na);
+                        wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 3, nb);
+                    }
+                    step(j, j >= 3 ? sv[2 * j - 6] : 0u, j >= 3 ? sv[2 * j - 5] : 0u);
+                }
+            }
+        } else { // window and source rows from global memory, one step ahead
+            uint32_t sa = 0, sb = 0;
+#pragma unroll 1
+            for (int j = 0; j < jend; j++) {
+#pragma unroll
+                for (int k = 0; k < 5; k++) pa[k] = na[k], pb[k] = nb[k];
+                const uint32_t ca = sa, cb = sb;
+                if (j + 1 < jend) {
+                    wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 2, na);
+                    wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 3, nb);
+                }
+                const int in = j - 2; // the output pair of the next step
+                if (in >= 0 && 2 * in < nrows) sa = load_src(2 * in), sb = 2 * in + 1 < nrows ? load_src(2 * in + 1) : 0u;
+                step(j, ca, cb);
+            }
+        }
+        // the unit's SSE, then lane 0's descent step
+        const unsigned long long et = wave_sum_u32_wide((uint32_t)e);
+        if ((threadIdx.x & 63) == WAVE_LAST) s_part[threadIdx.x >> 6] = et;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long err = 0;
+            for (int k = 0; k < WR_NT / 64; k++) err += s_part[k];
+            npx += (unsigned long long)w * h;
+            D.report((int64_t)err);
+            *s_mode = 0;
+            if (++rounds > WR_MAX_ROUNDS) {
+                atomicOr(status, 1); // a descent always ends: an internal failure, reported by the host
+            } else if (D.next()) {
+                int v[3];
+                D.taps(0, v), set_wiener_taps(s_taps, v); // f = 0: hfilter, f = 1: vfilter
+                D.taps(1, v), set_wiener_taps(s_taps + 8, v);
+                *s_mode = 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, Descent *ds, const int32_t *order,
+                                                           int lds_cap, int32_t *status, unsigned long long *pc,
+                                                           unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    extern __shared__ uint32_t wr_win[]; // the unit's CDEF window (LDS mode)
+    __shared__ uint64_t           s_draw[sizeof(Descent) / 8];
+    __shared__ unsigned long long s_part[WR_NT / 64];
+    __shared__ int16_t            s_taps[16];
+    __shared__ int                s_mode;
+    Descent        &D = *(Descent *)s_draw;
+    const int       u = order[blockIdx.x];
+    const URect     ur = A.units[u];
+    const PlaneArgs &P = A.pl[A.tiles[A.tile0[u]].plane];
+    const int       ux = ur.h_start, uy = ur.v_start, w = ur.h_end - ur.h_start, h = ur.v_end - ur.v_start;
+    const int       ws = (w + 10) >> 1;
+    const bool      lds = wr_lds_mode(w, h, lds_cap);
+    if (threadIdx.x == 0) {
+        D      = ds[u];
+        s_mode = 0;
+        if (!D.done && D.next()) {
+            int v[3];
+            D.taps(0, v), set_wiener_taps(s_taps, v);
+            D.taps(1, v), set_wiener_taps(s_taps + 8, v);
+            s_mode = 1;
+        }
+    }
+    if (lds) { // stage the edge-clamped window: rows uy-3 .., columns ux-4 .. (pairs)
+        const T *d = (const T *)P.dgd;
+        for (int i = threadIdx.x; i < (h + 6) * ws; i += WR_NT) {
+            const int r = i / ws, c = 2 * (i - r * ws);
+            const int fy = min(max(uy - 3 + r, 0), P.H - 1), f0 = min(max(ux - 4 + c, 0), P.W - 1),
+                      f1 = min(max(ux - 3 + c, 0), P.W - 1);
+            const T *row = d + (size_t)fy * P.dstride;
+            wr_win[i]    = (uint32_t)row[f0] | ((uint32_t)row[f1] << 16);
+        }
+    }
+    __syncthreads();
+    unsigned long long npx = 0;
+    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, &s_mode, s_taps, s_part, status, npx);
+    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, &s_mode, s_taps, s_part, status, npx);
+    if (threadIdx.x == 0) ds[u] = D;
+    if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
+    PROF_END(tk);
+}
+
 // svt_decode_xq (EbRestoration.c:634-646): xq of the ep's absent filter is 0
 __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
     const int x0 = d.val(0, 0), x1 = d.val(0, 1), r0 = c_sgr_r[d.ep][0], r1 = c_sgr_r[d.ep][1];
@@ -2255,6 +2498,23 @@ bool wn_use_unit() {
     }();
     return v;
 }
+// largest Wiener window staged in LDS (SVTGPU_WR_LDS_CAP overrides: measurements of the global-memory path)
+int wr_lds_cap() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_WR_LDS_CAP");
+        return e ? std::atoi(e) : WR_LDS_CAP;
+    }();
+    return v;
+}
+// the unit-resident Wiener kernel (default; SVTGPU_WN_RES=0 selects the tiled unit kernel, which also takes units
+// too large for the resident layout)
+bool wn_use_res() {
+    static const bool v = [] {
+        const char *e = std::getenv("SVTGPU_WN_RES");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
 // tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG: 2 or 4).  2 by default: at three frames in flight the
 // 512-lane workgroups leave room on the CUs for the other frames' kernels (2030-2047 vs 2012-2019 Mpx/s, same box,
 // profiles/r02/s16); a lone frame's descent is 1 % faster with 4
@@ -2375,16 +2635,33 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         if ((t.x0 & 3) || (t.w & 3)) return SVTGPU_ERR_UNSUPPORTED;
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
     if (n_all == 0) return SVTGPU_OK; // an empty band
+    // the resident Wiener kernel takes every unit whose rows fit its registers (all units of the 4K / 1080p frames);
+    // its workgroups start with the largest units (the longest chains); windows up to WR_LDS_CAP live in LDS
+    std::vector<int32_t> wr_order(n_wn);
+    bool                 wr_ok  = wn_use_res();
+    int                  wr_lds = 0;
+    for (int u = 0; u < n_wn; u++) {
+        const URect &r = units[u];
+        const int    w = r.h_end - r.h_start, h = r.v_end - r.v_start;
+        wr_order[u]    = u;
+        if (w > 384) wr_ok = false; // wider than the lane layout (unit sizes above 256)
+        if (wr_lds_mode(w, h, wr_lds_cap())) wr_lds = std::max(wr_lds, wr_window_bytes(w, h));
+    }
+    std::stable_sort(wr_order.begin(), wr_order.end(), [&](int a, int b) {
+        auto area = [&](int u) { return (units[u].h_end - units[u].h_start) * (units[u].v_end - units[u].v_start); };
+        return area(a) > area(b);
+    });
     // ---- device scratch and pinned staging ----
     // three contiguous spans keep the host traffic to one copy each: the plan (uploaded when it changes), the
     // accumulators zeroed per search, the results read back (o_sse is the last zeroed and the first read)
     Carver       dc;
-    const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1));
+    const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
+                 o_worder = dc(4 * (size_t)n_wn);
     const size_t plan_span = dc.off;
     const size_t o_sum = dc(8 * n_all), o_mom = dc(40 * (size_t)npairs), o_sse = dc(8 * n_all);
     const size_t zero_span = dc.off - o_sum;
     const size_t o_sse2 = dc(8 * (size_t)n_sg), o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
-                 o_sds = dc(sizeof(Descent) * npairs);
+                 o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8);
     const size_t res_span = dc.off - o_sse;
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
     const size_t o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
@@ -2466,6 +2743,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         std::memcpy(pl + o_tiles, tiles.data(), sizeof(Tile) * nt_all);
         std::memcpy(pl + o_units, units.data(), sizeof(URect) * n_all);
         std::memcpy(pl + o_t0, tile0.data(), 4 * (n_all + 1));
+        std::memcpy(pl + o_worder, wr_order.data(), 4 * (size_t)n_wn);
         if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
             std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
             HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
@@ -2571,6 +2849,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(dp(o_wds), qa + q_ds, sizeof(Descent) * (size_t)n_wn, hipMemcpyDeviceToDevice, sw));
+    } else if (n_wn && wn_unit && wr_ok) { // the whole Wiener descent of every unit, resident on one CU each
+        HIP_TRY(hipMemsetAsync(dp(o_wstat), 0, 8, sw));
+        run(2, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wn), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
+                               (const int32_t *)dp(o_worder), wr_lds, (int32_t *)dp(o_wstat), pc, tk);
+        });
+        HIP_TRY(hipGetLastError());
     } else if (n_wn && wn_unit) { // the whole Wiener descent of every unit inside one workgroup
         run(2, [&](unsigned long long *tk) {
             if (wn_unit_ng() == 2)
@@ -2749,6 +3034,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipStreamSynchronize(st));
     if (n_wn && wn_queue && ((const WnQueue *)hp(h_cnt))->error) {
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener work queue overflow", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    if (n_wn && wn_unit && wr_ok && *(const int32_t *)hp(h_res + (o_wstat - o_sse))) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener descent exceeded its round bound", __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;
     }
     if (npairs && sg_queue && ((const WnQueue *)hp(h_cnt + 16))->error) {
