@@ -1741,6 +1741,16 @@ __host__ __device__ inline int wr_window_bytes(int w, int h) { return (h + 6) * 
 __host__ __device__ inline bool wr_lds_mode(int w, int h, int lds_cap) {
     return wr_window_bytes(w, h) <= lds_cap && wr_geo(w, h).R <= WR_RMAX;
 }
+// A workgroup's share of a unit: rows [y0, y1) of unit `unit`.  A unit too large for one CU's LDS and registers (the
+// frame's bottom unit row: 256 x 376 at 4K) is cut into `nparts` row parts on as many workgroups; each evaluates every
+// candidate over its rows, the parts' SSEs meet through words in uncached memory (xch[2 * (first + part) + parity]:
+// {round << 48 | partial SSE}, double-buffered by round parity), and every part takes the same descent step.  The
+// parts of a unit are adjacent in the launch order and there are far fewer parted workgroups than CUs, so a waiting
+// part's partner is always dispatched; the wait is bounded all the same (status bit 2).
+struct WrItem {
+    int32_t unit, y0, y1, part, nparts, first; // first: the item index of part 0 (exchange slots)
+};
+constexpr int WR_MAX_PARTS = 4;
 
 // the 5 packed sample pairs of window row r (unit rows -3.., columns x-4 .. x+5) for output columns x, x+1
 template <typename T, bool LDSW>
@@ -1777,8 +1787,8 @@ __device__ inline void wr_fetch(const uint32_t *win, int ws, const PlaneArgs &P,
 
 template <typename T, bool LDSW>
 __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, const uint32_t *win, int ws, int ux,
-                       int uy, int w, int h, int *s_mode, int16_t *s_taps, unsigned long long *s_part, int32_t *status,
-                       unsigned long long &npx) {
+                       int uy, int w, int h, const WrItem &it, unsigned long long *xch, int *s_mode, int16_t *s_taps,
+                       unsigned long long *s_part, int32_t *status, unsigned long long &npx) {
     const WrGeo g  = wr_geo(w, h);
     const int   cp = threadIdx.x % g.cpw, sg = threadIdx.x / g.cpw, x = 2 * cp;
     const int   seg0 = sg * g.R, nrows = sg < g.nseg ? max(0, min(g.R, h - seg0)) : 0;
@@ -1884,11 +1894,34 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
             unsigned long long err = 0;
             for (int k = 0; k < WR_NT / 64; k++) err += s_part[k];
             npx += (unsigned long long)w * h;
-            D.report((int64_t)err);
+            ++rounds;
+            bool ok = rounds <= WR_MAX_ROUNDS; // a descent always ends: an internal failure, reported by the host
+            if (!ok) atomicOr(status, 1);
+            if (ok && it.nparts > 1) { // publish this part's SSE, add the other parts' SSEs of the same round
+                const unsigned long long tag = (unsigned long long)(rounds & 0xFFFF) << 48, low = (1ull << 48) - 1;
+                __hip_atomic_store(xch + 2 * (it.first + it.part) + (rounds & 1), tag | err, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                for (int q = 0; q < it.nparts && ok; q++) {
+                    if (q == it.part) continue;
+                    for (unsigned spin = 0;; spin++) {
+                        const unsigned long long v = __hip_atomic_load(xch + 2 * (it.first + q) + (rounds & 1),
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((v & ~low) == tag) {
+                            err += v & low;
+                            break;
+                        }
+                        if (spin > (1u << 24)) { // ~seconds: never wait forever
+                            atomicOr(status, 2);
+                            ok = false;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+            }
+            if (ok) D.report((int64_t)err);
             *s_mode = 0;
-            if (++rounds > WR_MAX_ROUNDS) {
-                atomicOr(status, 1); // a descent always ends: an internal failure, reported by the host
-            } else if (D.next()) {
+            if (ok && D.next()) {
                 int v[3];
                 D.taps(0, v), set_wiener_taps(s_taps, v); // f = 0: hfilter, f = 1: vfilter
                 D.taps(1, v), set_wiener_taps(s_taps + 8, v);
@@ -1900,22 +1933,23 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
 }
 
 template <typename T>
-__global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, Descent *ds, const int32_t *order,
-                                                           int lds_cap, int32_t *status, unsigned long long *pc,
-                                                           unsigned long long *tk) {
+__global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, Descent *ds, const WrItem *items,
+                                                           int lds_cap, unsigned long long *xch, int32_t *status,
+                                                           unsigned long long *pc, unsigned long long *tk) {
     PROF_BEGIN(tk);
-    extern __shared__ uint32_t wr_win[]; // the unit's CDEF window (LDS mode)
+    extern __shared__ uint32_t wr_win[]; // the part's CDEF window (LDS mode)
     __shared__ uint64_t           s_draw[sizeof(Descent) / 8];
     __shared__ unsigned long long s_part[WR_NT / 64];
     __shared__ int16_t            s_taps[16];
     __shared__ int                s_mode;
-    Descent        &D = *(Descent *)s_draw;
-    const int       u = order[blockIdx.x];
-    const URect     ur = A.units[u];
-    const PlaneArgs &P = A.pl[A.tiles[A.tile0[u]].plane];
-    const int       ux = ur.h_start, uy = ur.v_start, w = ur.h_end - ur.h_start, h = ur.v_end - ur.v_start;
-    const int       ws = (w + 10) >> 1;
-    const bool      lds = wr_lds_mode(w, h, lds_cap);
+    Descent         &D  = *(Descent *)s_draw;
+    const WrItem     it = items[blockIdx.x];
+    const int        u  = it.unit;
+    const URect      ur = A.units[u];
+    const PlaneArgs &P  = A.pl[A.tiles[A.tile0[u]].plane];
+    const int        ux = ur.h_start, uy = ur.v_start + it.y0, w = ur.h_end - ur.h_start, h = it.y1 - it.y0;
+    const int        ws = (w + 10) >> 1;
+    const bool       lds = wr_lds_mode(w, h, lds_cap);
     if (threadIdx.x == 0) {
         D      = ds[u];
         s_mode = 0;
@@ -1938,9 +1972,9 @@ __global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, D
     }
     __syncthreads();
     unsigned long long npx = 0;
-    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, &s_mode, s_taps, s_part, status, npx);
-    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, &s_mode, s_taps, s_part, status, npx);
-    if (threadIdx.x == 0) ds[u] = D;
+    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx);
+    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx);
+    if (threadIdx.x == 0 && it.part == 0) ds[u] = D;
     if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
     PROF_END(tk);
 }
@@ -2637,26 +2671,44 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     if (n_all == 0) return SVTGPU_OK; // an empty band
     // the resident Wiener kernel takes every unit whose rows fit its registers (all units of the 4K / 1080p frames);
     // its workgroups start with the largest units (the longest chains); windows up to WR_LDS_CAP live in LDS
-    std::vector<int32_t> wr_order(n_wn);
-    bool                 wr_ok  = wn_use_res();
-    int                  wr_lds = 0;
-    for (int u = 0; u < n_wn; u++) {
-        const URect &r = units[u];
-        const int    w = r.h_end - r.h_start, h = r.v_end - r.v_start;
-        wr_order[u]    = u;
-        if (w > 384) wr_ok = false; // wider than the lane layout (unit sizes above 256)
-        if (wr_lds_mode(w, h, wr_lds_cap())) wr_lds = std::max(wr_lds, wr_window_bytes(w, h));
+    // The resident Wiener kernel takes every unit up to 384 columns wide (unit sizes <= 256): a unit is cut into the
+    // fewest row parts that fit one CU's LDS and registers each (global-memory mode when no cut up to WR_MAX_PARTS
+    // does); workgroups start with the largest parts (the longest chains), the parts of a unit adjacent.
+    std::vector<WrItem> wr_items;
+    bool                wr_ok = wn_use_res(), wr_parted = false;
+    int                 wr_lds = 0;
+    {
+        std::vector<int> ord(n_wn);
+        std::vector<int> np(n_wn, 1);
+        for (int u = 0; u < n_wn; u++) {
+            const URect &r = units[u];
+            const int    w = r.h_end - r.h_start, h = r.v_end - r.v_start;
+            ord[u]         = u;
+            if (w > 384) wr_ok = false; // wider than the lane layout (unit sizes above 256)
+            int k = 1;
+            while (k < WR_MAX_PARTS && !wr_lds_mode(w, (h + k - 1) / k, wr_lds_cap())) k++;
+            np[u] = wr_lds_mode(w, (h + k - 1) / k, wr_lds_cap()) ? k : 1;
+            if (np[u] > 1) wr_parted = true;
+            const int hp = (h + np[u] - 1) / np[u];
+            if (wr_lds_mode(w, hp, wr_lds_cap())) wr_lds = std::max(wr_lds, wr_window_bytes(w, hp));
+        }
+        auto part_area = [&](int u) {
+            return (units[u].h_end - units[u].h_start) * ((units[u].v_end - units[u].v_start + np[u] - 1) / np[u]);
+        };
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return part_area(a) > part_area(b); });
+        for (int u : ord) {
+            const int h = units[u].v_end - units[u].v_start, first = (int)wr_items.size();
+            for (int k = 0; k < np[u]; k++)
+                wr_items.push_back({u, h * k / np[u], h * (k + 1) / np[u], k, np[u], first});
+        }
     }
-    std::stable_sort(wr_order.begin(), wr_order.end(), [&](int a, int b) {
-        auto area = [&](int u) { return (units[u].h_end - units[u].h_start) * (units[u].v_end - units[u].v_start); };
-        return area(a) > area(b);
-    });
+    const int n_wr = (int)wr_items.size();
     // ---- device scratch and pinned staging ----
     // three contiguous spans keep the host traffic to one copy each: the plan (uploaded when it changes), the
     // accumulators zeroed per search, the results read back (o_sse is the last zeroed and the first read)
     Carver       dc;
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
-                 o_worder = dc(4 * (size_t)n_wn);
+                 o_witem = dc(sizeof(WrItem) * (size_t)n_wr);
     const size_t plan_span = dc.off;
     const size_t o_sum = dc(8 * n_all), o_mom = dc(40 * (size_t)npairs), o_sse = dc(8 * n_all);
     const size_t zero_span = dc.off - o_sum;
@@ -2683,6 +2735,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t q_sq = qc(sizeof(WnQueue)), q_slog = qc(4 * (size_t)sq_cap), q_sarr = qc(4 * (size_t)n_all),
                  q_serr = qc(8 * SG_NC * (size_t)npairs), q_scand = qc(8 * SG_NC * (size_t)npairs),
                  q_scandm = qc(4 * (size_t)npairs), q_sds = qc(sizeof(Descent) * (size_t)npairs);
+    const size_t q_wrx = qc(16 * (size_t)n_wr); // the parted resident Wiener units' SSE exchange words
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -2743,7 +2796,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         std::memcpy(pl + o_tiles, tiles.data(), sizeof(Tile) * nt_all);
         std::memcpy(pl + o_units, units.data(), sizeof(URect) * n_all);
         std::memcpy(pl + o_t0, tile0.data(), 4 * (n_all + 1));
-        std::memcpy(pl + o_worder, wr_order.data(), 4 * (size_t)n_wn);
+        std::memcpy(pl + o_witem, wr_items.data(), sizeof(WrItem) * (size_t)n_wr);
         if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
             std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
             HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
@@ -2825,7 +2878,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // ---- phase 3: descent rounds on the device ----
     const bool wn_unit = wn_use_unit(), wn_queue = !wn_unit && wn_use_queue(), sg_queue = sg_use_queue();
     uint8_t   *qa       = nullptr;
-    if ((n_wn && wn_queue) || (npairs && sg_queue)) {
+    if ((n_wn && wn_queue) || (npairs && sg_queue) || (n_wn && wn_unit && wr_ok && wr_parted)) {
         if (qc.off > s->qarena_bytes) {
             if (s->d_qarena) (void)hipFree(s->d_qarena);
             s->d_qarena = nullptr, s->qarena_bytes = 0;
@@ -2851,9 +2904,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         HIP_TRY(hipMemcpyAsync(dp(o_wds), qa + q_ds, sizeof(Descent) * (size_t)n_wn, hipMemcpyDeviceToDevice, sw));
     } else if (n_wn && wn_unit && wr_ok) { // the whole Wiener descent of every unit, resident on one CU each
         HIP_TRY(hipMemsetAsync(dp(o_wstat), 0, 8, sw));
+        if (wr_parted) HIP_TRY(hipMemsetAsync(qa + q_wrx, 0, 16 * (size_t)n_wr, sw));
         run(2, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wn), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
-                               (const int32_t *)dp(o_worder), wr_lds, (int32_t *)dp(o_wstat), pc, tk);
+            hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
+                               (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa + q_wrx),
+                               (int32_t *)dp(o_wstat), pc, tk);
         });
         HIP_TRY(hipGetLastError());
     } else if (n_wn && wn_unit) { // the whole Wiener descent of every unit inside one workgroup
