@@ -129,6 +129,53 @@ int svtgpu_frame_download(const SvtGpuFrame *f, int plane, void *host, int32_t h
 int svtgpu_frame_copy(SvtGpuFrame *dst, const SvtGpuFrame *src, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * A picture tiled over several GPUs (BASELINE.json config 4).  No reference counterpart: the
+ * reference splits a picture into segments for its worker threads (cdef_seg_search / restoration_seg_search per
+ * segment, EbEncHandle.c:503-514) and gathers their results under a mutex (EbCdefProcess.c:406, EbRestProcess.c:614).
+ * Here each rank (one process per GPU) takes a tile, and the frame-level calls exchange what the reference's
+ * gather hands to its sequential finish: the DLF trial SSEs, the CDEF search tables and the LR search records.
+ * ------------------------------------------------------------------------------------------- */
+#define SVTGPU_COMM_ID_BYTES 128
+typedef struct SvtGpuComm SvtGpuComm;
+/* RCCL over xGMI: rank 0 creates the id, the caller broadcasts its bytes (any transport), every rank creates its
+ * communicator on its device.  One communicator per frame in flight. */
+int svtgpu_comm_unique_id(uint8_t id[SVTGPU_COMM_ID_BYTES]);
+int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t rank, const uint8_t id[SVTGPU_COMM_ID_BYTES],
+                       SvtGpuComm **out);
+/* A caller-supplied host transport (e.g. MPI or gloo): allreduce_u64 sums n uint64 element-wise over the ranks in
+ * place (every rank receives the sums) and returns 0.  Device buffers are staged through pinned host memory.  For
+ * rehearsals on CPUs and for several ranks on one GPU (RCCL needs one rank per device). */
+typedef struct SvtGpuHostTransport {
+    void *user;
+    int (*allreduce_u64)(void *user, uint64_t *buf, size_t n);
+} SvtGpuHostTransport;
+int     svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGpuHostTransport *t, SvtGpuComm **out);
+void    svtgpu_comm_destroy(SvtGpuComm *c);
+int32_t svtgpu_comm_nranks(const SvtGpuComm *c);
+int32_t svtgpu_comm_rank(const SvtGpuComm *c);
+/* element-wise sum of n uint64 over the ranks, in place; on_device: buf is device memory (enqueued on `stream` with
+ * RCCL), else host memory (synchronous) */
+int svtgpu_comm_allreduce_u64(SvtGpuComm *c, void *buf, size_t n, int32_t on_device, void *stream);
+
+/* The tiles of a gx x gy split of a width x height picture and what rank `rank` (row-major) computes.  Tile edges
+ * fall on the luma restoration-unit grid (unit_size[0], a multiple of 64: also filter-block and superblock edges), so
+ * each rank's loop-restoration units lie in its own part of the frame:
+ *   tile       {x0, y0, x1, y1} luma: the rank's share of the DLF trial SSEs (a partition of the frame);
+ *   fb_rect    {col0, row0, col1, row1}: the 64x64 CDEF filter blocks it searches (a partition);
+ *   lr_units   per plane {col0, row0, col1, row1} unit indices it searches (a partition of each plane's units);
+ *   lr_out     per plane {x0, y0, x1, y1} plane samples: the union of those units, the part of the final picture the
+ *              rank produces (a partition);
+ *   cdef_out   {x0, y0, x1, y1} luma: the CDEF output its LR search and apply read (lr_out plus an 8-sample apron);
+ *   dlf_out    {x0, y0, x1, y1} luma: the DLF output its CDEF search / apply and LR boundary lines read (its tile and
+ *              lr_out plus a 16-sample apron).
+ * Host only.  SVTGPU_ERR_INVALID_ARG when some rank would get no unit. */
+typedef struct SvtGpuTilePlan {
+    int32_t tile[4], fb_rect[4], lr_units[3][4], lr_out[3][4], cdef_out[4], dlf_out[4];
+} SvtGpuTilePlan;
+int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy, int32_t rank,
+                     SvtGpuTilePlan *out);
+
+/* ---------------------------------------------------------------------------------------------
  * CDEF — per-block RTCD shims (host pointers, synchronous)
  * ------------------------------------------------------------------------------------------- */
 /* replaces svt_aom_cdef_find_dir (common_dsp_rtcd.h:1017); C: EbCdef.c:150 */
@@ -250,6 +297,13 @@ int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, S
  * [fb_row_begin, fb_row_end).  Samples outside the band are still read as filter context (apron), so
  * the picture passed in must hold valid samples for the band +-3 rows.  Default: all rows. */
 int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32_t fb_row_end);
+/* A picture tiled over GPUs (svtgpu_tile_plan): the search covers the filter blocks of fb_rect = {col0, row0, col1,
+ * row1} only and leaves zeros elsewhere in the tables; svtgpu_cdef_pick first sums the mse / skip / dir / var tables
+ * over `comm` (one contributor per entry: the gather of every rank's blocks; the pick is then the same on every rank);
+ * the apply writes only the luma rectangle out_rect = {x0, y0, x1, y1} (chroma halved, rounded outward), reading
+ * the DLF output 2 samples around it.  NULL rects: the whole frame; NULL comm: no exchange. */
+int svtgpu_cdef_set_tile(SvtGpuCdefFrameState *s, const int32_t fb_rect[4], const int32_t out_rect[4],
+                         SvtGpuComm *comm);
 /* Use caller-owned device memory for the search tables: mse [2][nfb][64] uint64 and skip [nfb] uint8
  * (e.g. buffers all-reduced with RCCL between the search and the pick).  NULL, NULL restores the
  * state's own buffers.  svtgpu_cdef_clear_tables zeroes both (a band search then leaves zeros —
@@ -363,6 +417,12 @@ int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *o
 int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source, SvtGpuLfParams *params,
                     int32_t dlf_avg, int32_t dlf_avg_uv, int32_t temporal_layer_index,
                     int32_t early_exit_convergence, int32_t tx_mode_only_4x4, void *stream);
+/* A picture tiled over GPUs (svtgpu_tile_plan): the level search measures each trial's SSE over the luma
+ * rectangle sse_rect = {x0, y0, x1, y1} (the rank's tile; chroma halved) and sums it over `comm` before every
+ * bisection step, so every rank takes the same steps; svtgpu_dlf_frame(_to) writes only out_rect (chroma halved,
+ * rounded outward), reading the input 12 samples around it.  Rect edges are multiples of 8 (or the frame edge).
+ * NULL rects: the whole frame; NULL comm: no exchange. */
+int svtgpu_dlf_set_tile(SvtGpuDlfState *s, const int32_t sse_rect[4], const int32_t out_rect[4], SvtGpuComm *comm);
 /* LPF_PICK_FROM_Q: the loop-filter levels from the quantizer, no search (host only, no device work).
  * ≙ svt_av1_pick_filter_level_by_q (EbDeblockingFilter.c:1036-1125), the path svt_av1_pick_filter_level takes
  * for method >= LPF_PICK_FROM_Q (:1139-1146; the SB-based DLF levels 3..5).  Inputs are the fields it reads:
@@ -769,6 +829,12 @@ int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const Svt
  * work, usable without a GPU); returns SVTGPU_OK with *frame_type_out = NONE for a plane that is not searched. */
 int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
                            const SvtGpuLrUnitSearch *records, int32_t *frame_type_out, SvtGpuRestUnit *units_out);
+/* A picture tiled over GPUs (svtgpu_tile_plan): svtgpu_lr_search_frame searches only the units of units[p] = {col0,
+ * row0, col1, row1} of each plane, sums the zero-padded per-unit records over `comm` (the gather), and runs the RD
+ * finish of every plane on every rank (the same frame types and units everywhere); svtgpu_lr_apply_frame writes only
+ * out[p] = {x0, y0, x1, y1} (plane samples), reading the CDEF output 3 samples and the DLF output 3 rows around it.
+ * NULL arrays: the whole frame; NULL comm: no exchange. */
+int svtgpu_lr_set_tile(SvtGpuLrState *s, const int32_t units[3][4], const int32_t out[3][4], SvtGpuComm *comm);
 /* Device-time profile of the searches timed since the previous read, by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
  * (sgr_flt_kernel), 2 Wiener descents (unit kernel / queue / trial rounds), 3 self-guided descents (queue / projection
  * rounds), 4 Wiener decomposition, descent advance rounds, SGR SSE, 5 self-guided projection moments.  Each

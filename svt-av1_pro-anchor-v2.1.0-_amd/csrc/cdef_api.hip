@@ -123,7 +123,7 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
     s->pick_parts = 64;
     const size_t nfb = s->nfb;
     bool ok = hipMalloc(&s->d_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols) == hipSuccess &&
-              hipMalloc(&s->d_mse, nfb * 2 * 64 * 8) == hipSuccess && hipMalloc(&s->d_skip, nfb) == hipSuccess &&
+              hipMalloc(&s->d_mse, nfb * 2 * 64 * 8) == hipSuccess && hipMalloc(&s->d_skip, (nfb + 7) & ~(size_t)7) == hipSuccess &&
               hipMalloc(&s->d_dir, nfb * 64) == hipSuccess && hipMalloc(&s->d_var, nfb * 64 * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
               hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096) * 8) == hipSuccess &&
@@ -136,13 +136,14 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
         return SVTGPU_ERR_OOM;
     }
     HIP_TRY(hipMemset(s->d_fb_strength, 0, nfb));
+    HIP_TRY(hipMemset(s->d_skip, 0, (nfb + 7) & ~(size_t)7)); // the padding stays 0 (the tables' word sums)
     HIP_TRY(hipMemset(s->d_skip, 1, nfb));
     s->own_mse      = s->d_mse;
     s->own_skip     = s->d_skip;
     s->own_dir      = s->d_dir;
     s->own_var      = s->d_var;
-    s->fb_row_begin = 0;
-    s->fb_row_end   = s->geo.nvfb;
+    s->fb_rect[0] = s->fb_rect[1] = 0, s->fb_rect[2] = s->geo.nhfb, s->fb_rect[3] = s->geo.nvfb;
+    s->out_rect[0] = s->out_rect[1] = 0, s->out_rect[2] = width, s->out_rect[3] = height;
     *out = s;
     return SVTGPU_OK;
 }
@@ -165,8 +166,25 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
 extern "C" int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32_t fb_row_end) {
     if (!s || fb_row_begin < 0 || fb_row_end > s->geo.nvfb || fb_row_begin >= fb_row_end)
         return SVTGPU_ERR_INVALID_ARG;
-    s->fb_row_begin = fb_row_begin;
-    s->fb_row_end   = fb_row_end;
+    s->fb_rect[0] = 0, s->fb_rect[1] = fb_row_begin, s->fb_rect[2] = s->geo.nhfb, s->fb_rect[3] = fb_row_end;
+    s->out_rect[0] = 0, s->out_rect[1] = fb_row_begin * 64, s->out_rect[2] = s->width;
+    s->out_rect[3] = std::min(s->height, fb_row_end * 64);
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_cdef_set_tile(SvtGpuCdefFrameState *s, const int32_t fb_rect[4], const int32_t out_rect[4],
+                                    SvtGpuComm *comm) {
+    if (!s) return SVTGPU_ERR_INVALID_ARG;
+    const int32_t all_fb[4] = {0, 0, s->geo.nhfb, s->geo.nvfb}, all_px[4] = {0, 0, s->width, s->height};
+    const int32_t *f = fb_rect ? fb_rect : all_fb, *o = out_rect ? out_rect : all_px;
+    if (f[0] < 0 || f[1] < 0 || f[2] > s->geo.nhfb || f[3] > s->geo.nvfb || f[0] >= f[2] || f[1] >= f[3] ||
+        o[0] < 0 || o[1] < 0 || o[2] > s->width || o[3] > s->height || o[0] >= o[2] || o[1] >= o[3] ||
+        ((o[0] | o[1] | o[2] | o[3]) & 1))
+        return SVTGPU_ERR_INVALID_ARG;
+    if (s->d_fb_kind && ((f[0] | f[1]) & 1)) return SVTGPU_ERR_INVALID_ARG; // SB128 areas are never cut
+    std::memcpy(s->fb_rect, f, sizeof s->fb_rect);
+    std::memcpy(s->out_rect, o, sizeof s->out_rect);
+    s->comm = comm;
     return SVTGPU_OK;
 }
 
@@ -191,7 +209,7 @@ extern "C" int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream) {
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
     HIP_TRY(hipMemsetAsync(s->d_mse, 0, (size_t)s->nfb * 2 * 64 * 8, st));
-    HIP_TRY(hipMemsetAsync(s->d_skip, 0, (size_t)s->nfb, st));
+    HIP_TRY(hipMemsetAsync(s->d_skip, 0, ((size_t)s->nfb + 7) & ~(size_t)7, st));
     HIP_TRY(hipMemsetAsync(s->d_dir, 0, (size_t)s->nfb * 64, st));
     HIP_TRY(hipMemsetAsync(s->d_var, 0, (size_t)s->nfb * 64 * 4, st));
     return SVTGPU_OK;
@@ -264,6 +282,9 @@ extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFra
         return SVTGPU_ERR_INVALID_ARG;
     CdefStrengthTable tab;
     hipStream_t       st = pick_stream(s->ctx, stream);
+    // tiled over GPUs: zeros outside this rank's filter blocks, so the pick's word sums over the ranks gather the tables
+    if (s->comm && svtgpu_comm_nranks(s->comm) > 1)
+        if (int rc = svtgpu_cdef_clear_tables(s, st)) return rc;
     if (ctrls->use_reference_cdef_fs) { // directions / variances only: an empty strength table
         memset(&tab, 0, sizeof(tab));
         return svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6), st);
@@ -284,6 +305,15 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
     if (!s || !ctrls || !params_out || !valid_controls(ctrls))
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
+    if (s->comm && svtgpu_comm_nranks(s->comm) > 1) { // the ranks' search tables (zero elsewhere) summed = gathered
+        const size_t nfb = s->nfb;
+        if (int rc = svtgpu_comm_sum(s->comm, s->d_dir, nfb * 64 / 8, true, st)) return rc;
+        if (int rc = svtgpu_comm_sum(s->comm, s->d_var, nfb * 64 * 4 / 8, true, st)) return rc;
+        if (!ctrls->use_reference_cdef_fs) {
+            if (int rc = svtgpu_comm_sum(s->comm, s->d_mse, nfb * 2 * 64, true, st)) return rc;
+            if (int rc = svtgpu_comm_sum(s->comm, s->d_skip, (nfb + 7) / 8, true, st)) return rc;
+        }
+    }
     if (ctrls->use_reference_cdef_fs) { // EbEncCdef.c:744-789: index 0 for every filter block, one pair
         memset(params_out, 0, sizeof(*params_out));
         params_out->cdef_damping        = (uint8_t)(3 + (base_q_idx >> 6));

@@ -16,7 +16,8 @@ struct ApplyArgs {
     const void *rec[3];
     void       *out[3];
     int32_t     rstride[3], ostride[3];
-    int32_t     width, height, b8_cols, nhfb, cs, fb0;
+    int32_t     width, height, b8_cols, nhfb, cs, fb0, fbw; // filter blocks fb0 + (i / fbw) * nhfb + i % fbw
+    int32_t     rect[4];                                    // luma {x0, y0, x1, y1} written (chroma halved)
     const uint8_t *mask;
     const uint8_t *dir;
     const int32_t *var;
@@ -38,10 +39,10 @@ __device__ void stage_tile_a(uint16_t *tile, int ts, int n, const T *plane, int 
 }
 
 template <typename T>
-__device__ void copy_fb_plane(const T *src, int sst, T *dst, int dst_st, int r0, int c0, int n, int pw, int ph) {
+__device__ void copy_fb_plane(const T *src, int sst, T *dst, int dst_st, int r0, int c0, int n, const int *lim) {
     for (int i = threadIdx.x; i < n * n; i += NT) {
         const int r = i / n, c = i - r * n;
-        if (r0 + r < ph && c0 + c < pw)
+        if (r0 + r >= lim[1] && r0 + r < lim[3] && c0 + c >= lim[0] && c0 + c < lim[2])
             dst[(long)(r0 + r) * dst_st + c0 + c] = src[(long)(r0 + r) * sst + c0 + c];
     }
 }
@@ -52,7 +53,8 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     __shared__ uint16_t ctile[2][CT * CT];
     __shared__ uint8_t  slisted[64];
     __shared__ int32_t  nlisted;
-    const int fb = A.fb0 + xcd_swizzle(blockIdx.x, gridDim.x), fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
+    const int fi = xcd_swizzle(blockIdx.x, gridDim.x), fb = A.fb0 + (fi / A.fbw) * A.nhfb + fi % A.fbw;
+    const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
     const int cs = A.cs;
     const int si = A.fb_strength[fb];
     int level = A.prm.cdef_y_strength[si] >> 2, sec = A.prm.cdef_y_strength[si] & 3;
@@ -75,8 +77,11 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         const T  *src = (const T *)A.rec[pli];
         T        *dst = (T *)A.out[pli];
         const int lv = pli ? uvl : level, sv = pli ? uvs : sec;
+        const int sh = pli > 0; // the samples written: the plane clipped to the rect (chroma halved, rounded outward)
+        const int lim[4] = {A.rect[0] >> sh, A.rect[1] >> sh, min(pw[pli], (A.rect[2] + sh) >> sh),
+                            min(ph[pli], (A.rect[3] + sh) >> sh)};
         if (!fb_on || !(lv || sv)) { // unfiltered plane: pass-through (:404 `level || sec_strength`)
-            copy_fb_plane<T>(src, A.rstride[pli], dst, A.ostride[pli], r0, c0, n, pw[pli], ph[pli]);
+            copy_fb_plane<T>(src, A.rstride[pli], dst, A.ostride[pli], r0, c0, n, lim);
             continue;
         }
         uint16_t *tile = pli ? ctile[pli - 1] : ltile;
@@ -88,7 +93,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         const int lb = pli ? 2 : 3;
         for (int i = tid; i < n * n; i += NT) {
             const int r = i / n, c = i - r * n;
-            if (r0 + r >= ph[pli] || c0 + c >= pw[pli]) continue;
+            if (r0 + r < lim[1] || r0 + r >= lim[3] || c0 + c < lim[0] || c0 + c >= lim[2]) continue;
             const int b = (r >> lb) * 8 + (c >> lb);
             const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + CDEF_BORDER;
             int v = p[0];
@@ -115,17 +120,23 @@ int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
     A.height      = recon->height;
     A.b8_cols     = s->geo.b8_cols;
     A.nhfb        = s->geo.nhfb;
-    A.fb0         = s->fb_row_begin * s->geo.nhfb;
+    // the filter blocks that hold a sample of the output rect
+    const int c0 = s->out_rect[0] / 64, r0 = s->out_rect[1] / 64, c1 = (s->out_rect[2] + 63) / 64,
+              r1 = (s->out_rect[3] + 63) / 64;
+    A.fb0         = r0 * s->geo.nhfb + c0;
+    A.fbw         = c1 - c0;
+    for (int i = 0; i < 4; i++) A.rect[i] = s->out_rect[i];
     A.cs          = recon->bit_depth - 8;
     A.mask        = s->mask_all ? nullptr : s->d_mask;
     A.dir         = s->d_dir;
     A.var         = s->d_var;
     A.fb_strength = s->d_fb_strength;
     A.prm         = *p;
+    const dim3 grid((r1 - r0) * A.fbw);
     if (recon->bit_depth > 8)
-        hipLaunchKernelGGL(cdef_apply_kernel<uint16_t>, dim3((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb), dim3(NT), 0, st, A);
+        hipLaunchKernelGGL(cdef_apply_kernel<uint16_t>, grid, dim3(NT), 0, st, A);
     else
-        hipLaunchKernelGGL(cdef_apply_kernel<uint8_t>, dim3((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb), dim3(NT), 0, st, A);
+        hipLaunchKernelGGL(cdef_apply_kernel<uint8_t>, grid, dim3(NT), 0, st, A);
     HIP_TRY(hipGetLastError());
     return SVTGPU_OK;
 }

@@ -17,8 +17,8 @@
 // kind: 0 plain 64x64, 1 128x128, 2 128x64, 3 64x128 (top-left FB of the area), -1 a skipped half
 __global__ void __launch_bounds__(64) cdef_sb128_fold_kernel(uint64_t *mse, uint8_t *skip, const uint8_t *rem,
                                                              const int8_t *kind, int nfb, int nhfb, int nvfb,
-                                                             unsigned long long uv_on, int cs, int ss, int fb0) {
-    const int f = fb0 + blockIdx.x, k = kind[f], gi = threadIdx.x;
+                                                             unsigned long long uv_on, int cs, int ss, int fb0, int fbw) {
+    const int f = fb0 + (blockIdx.x / fbw) * nhfb + blockIdx.x % fbw, k = kind[f], gi = threadIdx.x;
     if (k <= 0) return;
     const int fbr = f / nhfb, fbc = f - fbr * nhfb;
     int       part[4], np = 0;
@@ -64,10 +64,11 @@ __global__ void cdef_sb128_dup_kernel(int8_t *fbs, const int8_t *kind, int nfb, 
 }
 
 int svtgpu_launch_cdef_sb128_fold(SvtGpuCdefFrameState *s, unsigned long long uv_on, int cs, int ss, hipStream_t st) {
-    const int fb0 = s->fb_row_begin * s->geo.nhfb, fb1 = s->fb_row_end * s->geo.nhfb;
-    if (fb1 > fb0)
-        hipLaunchKernelGGL(cdef_sb128_fold_kernel, dim3(fb1 - fb0), dim3(64), 0, st, s->d_mse, s->d_skip, s->d_mse_rem,
-                           s->d_fb_kind, s->nfb, s->geo.nhfb, s->geo.nvfb, uv_on, cs, ss, fb0);
+    const int fbw = s->fb_rect[2] - s->fb_rect[0], n = fbw * (s->fb_rect[3] - s->fb_rect[1]);
+    if (n > 0)
+        hipLaunchKernelGGL(cdef_sb128_fold_kernel, dim3(n), dim3(64), 0, st, s->d_mse, s->d_skip, s->d_mse_rem,
+                           s->d_fb_kind, s->nfb, s->geo.nhfb, s->geo.nvfb, uv_on, cs, ss,
+                           s->fb_rect[1] * s->geo.nhfb + s->fb_rect[0], fbw);
     HIP_TRY(hipGetLastError());
     return SVTGPU_OK;
 }

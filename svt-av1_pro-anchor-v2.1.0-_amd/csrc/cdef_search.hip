@@ -37,7 +37,7 @@ struct SearchArgs {
     uint8_t       *dir;  // [nfb][64]
     int32_t       *var;  // [nfb][64]
     uint8_t       *rem;  // [3][nfb][64] low 2*cs bits of the luma / Cb / Cr sums before the shift, or null
-    int32_t        nfb, fb0;
+    int32_t        nfb, fb0, fbw; // searched filter blocks: fb0 + (i / fbw) * nhfb + i % fbw
     int32_t        cs, ss, damping;
     CdefStrengthTable tab;
 };
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     __shared__ int32_t  nlisted;
     __shared__ CdefGroupTable grp[4]; // luma A, luma B, chroma A, chroma B
 
-    const int fb = A.fb0 + xcd_swizzle(blockIdx.x, gridDim.x);
+    const int fi = xcd_swizzle(blockIdx.x, gridDim.x), fb = A.fb0 + (fi / A.fbw) * A.nhfb + fi % A.fbw;
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int cs = A.cs;
@@ -477,12 +477,13 @@ int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon,
     A.var     = s->d_var;
     A.rem     = s->d_fb_kind ? s->d_mse_rem : nullptr;
     A.nfb     = s->nfb;
-    A.fb0     = s->fb_row_begin * s->geo.nhfb;
+    A.fb0     = s->fb_rect[1] * s->geo.nhfb + s->fb_rect[0];
+    A.fbw     = s->fb_rect[2] - s->fb_rect[0];
     A.cs      = recon->bit_depth - 8;
     A.ss      = subsampling;
     A.damping = damping;
     A.tab     = *tab;
-    const dim3 grid((s->fb_row_end - s->fb_row_begin) * s->geo.nhfb);
+    const dim3 grid((s->fb_rect[3] - s->fb_rect[1]) * A.fbw);
     if (recon->bit_depth > 8)
         hipLaunchKernelGGL(cdef_search_kernel<uint16_t>, grid, dim3(NT), 0, st, A);
     else

@@ -1,0 +1,208 @@
+// comm.hip — the frame-level exchanges of a picture tiled over several GPUs (BASELINE.json config 4).
+//
+// One communicator per frame in flight and rank; every exchange of the path is an element-wise sum of uint64 words
+// over the ranks:
+//   * DLF level search: the trial SSEs of the rank's tile (search_filter_level, EbDeblockingFilter.c:886-991, sums
+//     picture_sse_calculations over the whole frame; the tiles partition it);
+//   * CDEF pick: the zero-padded mse / skip / dir / var tables of the rank's filter blocks (cdef_seg_search's
+//     per-segment outputs gathered for finish_cdef_search, EbCdefProcess.c:114 / EbEncCdef.c:728): one contributor
+//     per entry, so the word sums are the gather;
+//   * LR finish: the zero-padded per-unit search records (restoration_seg_search's outputs gathered for
+//     rest_finish_search, EbRestorationPick.c:1471 / :1555).
+// Two transports behind one object:
+//   * RCCL over xGMI (ncclAllReduce on the caller's stream, buffers in device memory) — the GPU path;
+//   * a host transport supplied by the caller (a function that sums uint64 words over the ranks, e.g. an MPI or gloo
+//     binding): device buffers are staged through pinned host memory.  Used by the CPU-side rehearsals and by tests
+//     that run several ranks on one GPU (RCCL refuses two ranks on one device).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "svtgpu_internal.h"
+
+struct SvtGpuComm {
+    int32_t             nranks = 1, rank = 0;
+    ncclComm_t          nccl   = nullptr;
+    SvtGpuHostTransport host{};
+    bool                is_host = false;
+    uint64_t           *pin = nullptr; // host staging (host transport: device buffers; RCCL: host buffers go via dev)
+    size_t              pin_words = 0;
+    uint64_t           *dev = nullptr; // device staging of host buffers (RCCL)
+    size_t              dev_words = 0;
+    int                 device = 0;
+};
+
+namespace {
+int nccl_fail(ncclResult_t r, const char *what) {
+    char msg[256];
+    std::snprintf(msg, sizeof msg, "%s: %s", what, ncclGetErrorString(r));
+    svtgpu_set_last_hip_error(hipErrorUnknown, msg, __FILE__, __LINE__);
+    return SVTGPU_ERR_HIP;
+}
+int grow_pin(SvtGpuComm *c, size_t n) {
+    if (n <= c->pin_words) return SVTGPU_OK;
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr, c->pin_words = 0;
+    HIP_TRY(hipHostMalloc((void **)&c->pin, n * 8, hipHostMallocDefault));
+    c->pin_words = n;
+    return SVTGPU_OK;
+}
+int grow_dev(SvtGpuComm *c, size_t n) {
+    if (n <= c->dev_words) return SVTGPU_OK;
+    if (c->dev) (void)hipFree(c->dev);
+    c->dev = nullptr, c->dev_words = 0;
+    HIP_TRY(hipMalloc((void **)&c->dev, n * 8));
+    c->dev_words = n;
+    return SVTGPU_OK;
+}
+} // namespace
+
+extern "C" int svtgpu_comm_unique_id(uint8_t id[SVTGPU_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == SVTGPU_COMM_ID_BYTES, "ncclUniqueId is 128 bytes");
+    if (!id) return SVTGPU_ERR_INVALID_ARG;
+    ncclUniqueId u;
+    if (ncclResult_t r = ncclGetUniqueId(&u)) return nccl_fail(r, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof u);
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t rank,
+                                  const uint8_t id[SVTGPU_COMM_ID_BYTES], SvtGpuComm **out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return SVTGPU_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclComm_t comm = nullptr;
+    if (ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank)) return nccl_fail(r, "ncclCommInitRank");
+    auto *c   = new SvtGpuComm();
+    c->nranks = nranks, c->rank = rank, c->nccl = comm, c->device = ctx->device;
+    *out      = c;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGpuHostTransport *t, SvtGpuComm **out) {
+    if (!t || !t->allreduce_u64 || !out || nranks < 1 || rank < 0 || rank >= nranks) return SVTGPU_ERR_INVALID_ARG;
+    auto *c    = new SvtGpuComm();
+    c->nranks  = nranks, c->rank = rank, c->host = *t, c->is_host = true;
+    *out       = c;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_comm_destroy(SvtGpuComm *c) {
+    if (!c) return;
+    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->pin) (void)hipHostFree(c->pin);
+    if (c->dev) (void)hipFree(c->dev);
+    delete c;
+}
+
+extern "C" int32_t svtgpu_comm_nranks(const SvtGpuComm *c) { return c ? c->nranks : 0; }
+extern "C" int32_t svtgpu_comm_rank(const SvtGpuComm *c) { return c ? c->rank : -1; }
+
+// The element-wise sum of n uint64 over the ranks, in place.  Device buffers: enqueued on `st` (RCCL) or staged through
+// host memory with a synchronization (host transport).  Host buffers: synchronous either way.
+int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st) {
+    if (!c || c->nranks == 1 || n == 0) return SVTGPU_OK;
+    if (!buf) return SVTGPU_ERR_INVALID_ARG;
+    if (c->is_host) {
+        uint64_t *h = (uint64_t *)buf;
+        if (on_device) {
+            if (int rc = grow_pin(c, n)) return rc;
+            HIP_TRY(hipMemcpyAsync(c->pin, buf, n * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            h = c->pin;
+        }
+        if (c->host.allreduce_u64(c->host.user, h, n) != 0) {
+            svtgpu_set_last_hip_error(hipErrorUnknown, "host transport all-reduce failed", __FILE__, __LINE__);
+            return SVTGPU_ERR_HIP;
+        }
+        if (on_device) HIP_TRY(hipMemcpyAsync(buf, c->pin, n * 8, hipMemcpyHostToDevice, st));
+        return SVTGPU_OK;
+    }
+    void *d = buf;
+    if (!on_device) {
+        if (int rc = grow_dev(c, n)) return rc;
+        HIP_TRY(hipMemcpyAsync(c->dev, buf, n * 8, hipMemcpyHostToDevice, st));
+        d = c->dev;
+    }
+    if (ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, st)) return nccl_fail(r, "ncclAllReduce");
+    if (!on_device) {
+        HIP_TRY(hipMemcpyAsync(buf, c->dev, n * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_comm_allreduce_u64(SvtGpuComm *c, void *buf, size_t n, int32_t on_device, void *stream) {
+    if (!c) return SVTGPU_ERR_INVALID_ARG;
+    // a host transport on host memory touches no device (usable without a GPU)
+    hipStream_t st = stream ? (hipStream_t)stream : (c->is_host && !on_device) ? nullptr : svtgpu_default_stream();
+    return svtgpu_comm_sum(c, buf, n, on_device != 0, st);
+}
+
+// ---------------------------------------------------------------------------------------------
+// tile plan (host only)
+// ---------------------------------------------------------------------------------------------
+namespace {
+int units_of(int size, int extent) { return std::max((extent + (size >> 1)) / size, 1); } // count_units_in_tile
+int split_at(int n, int k, int i) { return (int)((long long)n * i / k); }
+void grow(int32_t *r, int a, int w, int h) {
+    r[0] = std::max(0, r[0] - a), r[1] = std::max(0, r[1] - a);
+    r[2] = std::min(w, r[2] + a), r[3] = std::min(h, r[3] + a);
+}
+} // namespace
+
+extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy,
+                                int32_t rank, SvtGpuTilePlan *out) {
+    if (!unit_size || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7) || gx < 1 || gy < 1 ||
+        rank < 0 || rank >= gx * gy)
+        return SVTGPU_ERR_INVALID_ARG;
+    for (int p = 0; p < 3; p++)
+        if (unit_size[p] < (p ? 32 : 64) || unit_size[p] > 256 || (unit_size[p] & (unit_size[p] - 1)))
+            return SVTGPU_ERR_INVALID_ARG;
+    SvtGpuTilePlan o;
+    std::memset(&o, 0, sizeof o);
+    const int tx = rank % gx, ty = rank / gx, U = unit_size[0];
+    const int nux = units_of(U, width), nuy = units_of(U, height);
+    if (nux < gx || nuy < gy) return SVTGPU_ERR_INVALID_ARG; // a rank without a unit
+    const int c0 = split_at(nux, gx, tx), c1 = split_at(nux, gx, tx + 1);
+    const int r0 = split_at(nuy, gy, ty), r1 = split_at(nuy, gy, ty + 1);
+    // the tile: unit-grid edges (multiples of 64: filter-block edges too); the frame edge closes the last tile
+    o.tile[0] = c0 * U, o.tile[1] = r0 * U;
+    o.tile[2] = c1 == nux ? width : c1 * U, o.tile[3] = r1 == nuy ? height : r1 * U;
+    o.fb_rect[0] = o.tile[0] / 64, o.fb_rect[1] = o.tile[1] / 64;
+    o.fb_rect[2] = (o.tile[2] + 63) / 64, o.fb_rect[3] = (o.tile[3] + 63) / 64;
+    for (int p = 0; p < 3; p++) {
+        const int pw = p ? width / 2 : width, ph = p ? height / 2 : height, up = unit_size[p], off = p ? 4 : 8;
+        const int hx = units_of(up, pw), hy = units_of(up, ph);
+        // the luma unit columns / rows when the plane's unit grid matches luma's (chroma units of half the luma size),
+        // else an even split of the plane's own grid
+        const bool same = hx == nux && hy == nuy;
+        const int  a0 = same ? c0 : split_at(hx, gx, tx), a1 = same ? c1 : split_at(hx, gx, tx + 1);
+        const int  b0 = same ? r0 : split_at(hy, gy, ty), b1 = same ? r1 : split_at(hy, gy, ty + 1);
+        if (a0 >= a1 || b0 >= b1) return SVTGPU_ERR_INVALID_ARG;
+        o.lr_units[p][0] = a0, o.lr_units[p][1] = b0, o.lr_units[p][2] = a1, o.lr_units[p][3] = b1;
+        // the units' samples: columns [a0 U, a1 U) (the last unit to the plane edge), rows start RESTORATION_UNIT_OFFSET
+        // above the unit grid (foreach_rest_unit_in_tile, EbRestoration.c:1257-1294)
+        o.lr_out[p][0] = a0 * up, o.lr_out[p][2] = a1 == hx ? pw : a1 * up;
+        o.lr_out[p][1] = b0 == 0 ? 0 : b0 * up - off, o.lr_out[p][3] = b1 == hy ? ph : b1 * up - off;
+    }
+    // CDEF output read by the LR search / apply of these units: 3 samples around them (8: whole 8x8 blocks); chroma
+    // units map onto the same luma area when the grids match, else take their bounding box
+    int32_t c[4];
+    std::memcpy(c, o.lr_out[0], sizeof c);
+    for (int p = 1; p < 3; p++) {
+        c[0] = std::min(c[0], 2 * o.lr_out[p][0]), c[1] = std::min(c[1], 2 * o.lr_out[p][1]);
+        c[2] = std::max(c[2], std::min(width, 2 * o.lr_out[p][2])), c[3] = std::max(c[3], std::min(height, 2 * o.lr_out[p][3]));
+    }
+    grow(c, 8, width, height);
+    std::memcpy(o.cdef_out, c, sizeof c);
+    // DLF output read by the CDEF search of the tile's filter blocks and by the CDEF apply / LR boundary lines above
+    int32_t d[4] = {std::min(c[0], o.tile[0]), std::min(c[1], o.tile[1]), std::max(c[2], o.tile[2]),
+                    std::max(c[3], o.tile[3])};
+    grow(d, 8, width, height);
+    std::memcpy(o.dlf_out, d, sizeof d);
+    *out = o;
+    return SVTGPU_OK;
+}

@@ -195,6 +195,7 @@ struct DlfPlaneJob {
     int32_t         src_stride, dst_stride, ref_stride;
     int32_t         units_w;  // records per row (= pw / 4)
     int32_t         pw, ph, tiles_x, tiles;
+    int32_t         ox, oy, ow, oh; // the region filtered / measured (a tile of a picture split over GPUs)
     int32_t         ntrial;
     uint8_t         lvl[MAX_TRIALS][2][128]; // [trial][dir][class] filter level
 };
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     const DlfPlaneJob &J = a.job[jb];
     const int tr = TRIAL ? tb % J.ntrial : 0;
     if (TRIAL) tb /= J.ntrial;
-    const int x0 = (tb % J.tiles_x) * TILE, y0 = (tb / J.tiles_x) * TILE;
+    const int x0 = J.ox + (tb % J.tiles_x) * TILE, y0 = J.oy + (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
 
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         }
         *(uint2 *)&t[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
     }
-    const int tw = min(TILE, J.pw - x0), th = min(TILE, J.ph - y0);
+    const int tw = min(TILE, J.ox + J.ow - x0), th = min(TILE, J.oy + J.oh - y0);
     {
         __syncthreads();
         // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
@@ -391,6 +392,10 @@ struct SvtGpuDlfState {
     int32_t        have_mi;
     hipStream_t    hi_stream = nullptr; // highest-priority stream of the level search's trial launches (lazy)
     hipEvent_t     hi_ev     = nullptr;
+    // frame tiling over GPUs (svtgpu_dlf_set_tile): trial SSEs over sse_rect, summed over `comm`; the apply writes
+    // out_rect (luma {x0, y0, x1, y1}; the whole frame by default)
+    int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
+    SvtGpuComm    *comm = nullptr;
 };
 
 namespace {
@@ -443,7 +448,7 @@ bool plane_active(const SvtGpuLfParams &p, int plane) {
     return plane == 1 ? p.filter_level_u != 0 : p.filter_level_v != 0;
 }
 
-DlfPlaneJob plane_job(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane) {
+DlfPlaneJob plane_job(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane, bool trial) {
     DlfPlaneJob j;
     std::memset(&j, 0, sizeof j);
     const int ch = plane > 0;
@@ -452,8 +457,14 @@ DlfPlaneJob plane_job(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane) {
     j.units_w = s->uw[ch];
     j.pw      = f->pw[plane];
     j.ph      = f->ph[plane];
-    j.tiles_x = (j.pw + TILE - 1) / TILE;
-    j.tiles   = j.tiles_x * ((j.ph + TILE - 1) / TILE);
+    // trials measure the SSE rectangle, the apply writes the output rectangle (luma coordinates; chroma halved,
+    // rounded outward); both the whole plane unless a tile is set
+    const int32_t *r = trial ? s->sse_rect : s->out_rect;
+    const int      sh = plane > 0;
+    j.ox      = r[0] >> sh, j.oy = r[1] >> sh;
+    j.ow      = std::min(j.pw, (r[2] + sh) >> sh) - j.ox, j.oh = std::min(j.ph, (r[3] + sh) >> sh) - j.oy;
+    j.tiles_x = (j.ow + TILE - 1) / TILE;
+    j.tiles   = j.ow > 0 && j.oh > 0 ? j.tiles_x * ((j.oh + TILE - 1) / TILE) : 0;
     return j;
 }
 
@@ -590,7 +601,7 @@ int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
                 first = false;
             }
             DlfPlaneJob &J = a.job[a.njob];
-            J              = plane_job(s, recon, plane);
+            J              = plane_job(s, recon, plane, true);
             J.src          = recon->plane[plane];
             J.src_stride   = recon->stride[plane];
             J.ref          = src->plane[plane];
@@ -616,10 +627,13 @@ int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
         if (int rc = launch_tile(a, recon->bytes_per_sample, true, st)) return rc;
         if (int rc = svtgpu_wait_seq(s->h_sse + MAX_JOBS * MAX_TRIALS, a.seq, st)) return rc;
         svtgpu_count_xfer(1, 8); // the sequence word
-        for (int j = 0; j < a.njob; j++) {
-            svtgpu_count_xfer(1, 8 * (size_t)m[j]); // the job's trial SSEs (mapped memory)
-            srch[who[j]]->feed(lv[who[j]], m[j], s->h_sse + j * MAX_TRIALS);
-        }
+        unsigned long long sse[MAX_JOBS * MAX_TRIALS];
+        std::memcpy(sse, s->h_sse, sizeof sse);
+        for (int j = 0; j < a.njob; j++) svtgpu_count_xfer(1, 8 * (size_t)m[j]); // the job's trial SSEs (mapped memory)
+        // a picture tiled over GPUs: every rank measured its tile; the frame's SSE is the sum over the ranks, and
+        // every rank then takes the same bisection step
+        if (int rc = svtgpu_comm_sum(s->comm, sse, MAX_JOBS * MAX_TRIALS, false, st)) return rc;
+        for (int j = 0; j < a.njob; j++) srch[who[j]]->feed(lv[who[j]], m[j], sse + j * MAX_TRIALS);
     }
 }
 
@@ -644,6 +658,7 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
     s->mi_rows = height >> 2;
     s->uw[0]   = width / 4, s->uh[0] = height / 4;
     s->uw[1]   = width / 8, s->uh[1] = height / 8;
+    s->sse_rect[2] = s->out_rect[2] = width, s->sse_rect[3] = s->out_rect[3] = height;
     hipError_t e = hipMalloc(&s->d_mi, sizeof(SvtGpuLfMi) * s->mi_rows * s->mi_cols);
     for (int c = 0; c < 2 && e == hipSuccess; c++)
         for (int d = 0; d < 2 && e == hipSuccess; d++)
@@ -705,6 +720,21 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
     return SVTGPU_OK;
 }
 
+extern "C" int svtgpu_dlf_set_tile(SvtGpuDlfState *s, const int32_t sse_rect[4], const int32_t out_rect[4],
+                                   SvtGpuComm *comm) {
+    if (!s) return SVTGPU_ERR_INVALID_ARG;
+    const int32_t whole[4] = {0, 0, s->width, s->height};
+    const int32_t *r[2]    = {sse_rect ? sse_rect : whole, out_rect ? out_rect : whole};
+    for (const int32_t *q : r) // 8-aligned (chroma 4-aligned: the tile staging reads aligned 4-sample groups)
+        if (q[0] < 0 || q[1] < 0 || q[2] > s->width || q[3] > s->height || q[0] >= q[2] || q[1] >= q[3] ||
+            ((q[0] | q[1]) & 7) || ((q[2] & 7) && q[2] != s->width) || ((q[3] & 7) && q[3] != s->height))
+            return SVTGPU_ERR_INVALID_ARG;
+    std::memcpy(s->sse_rect, r[0], sizeof s->sse_rect);
+    std::memcpy(s->out_rect, r[1], sizeof s->out_rect);
+    s->comm = comm;
+    return SVTGPU_OK;
+}
+
 namespace {
 // filter planes [ps, pe) of `in` into `out`; in == out is allowed (the plane is staged in scratch)
 int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
@@ -716,15 +746,19 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
         if (pl == 0 && !plane_active(*params, 0)) luma_off = true; // no plane is filtered (:575-577)
         const size_t bps = in->bytes_per_sample;
         const bool   on  = !luma_off && plane_active(*params, pl);
-        if (!on) {
-            if (in != out)
-                HIP_TRY(hipMemcpy2DAsync(out->plane[pl], out->stride[pl] * bps, in->plane[pl], in->stride[pl] * bps,
-                                         in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
+        if (!on) { // the output rectangle of the plane passes through
+            const DlfPlaneJob R = plane_job(s, in, pl, false);
+            if (in != out && R.ow > 0 && R.oh > 0) {
+                const size_t io = ((size_t)R.oy * in->stride[pl] + R.ox) * bps, oo = ((size_t)R.oy * out->stride[pl] + R.ox) * bps;
+                HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[pl] + oo, out->stride[pl] * bps,
+                                         (const uint8_t *)in->plane[pl] + io, in->stride[pl] * bps, R.ow * bps, R.oh,
+                                         hipMemcpyDeviceToDevice, st));
+            }
             continue;
         }
         DlfTileArgs  a = base_args(in, L);
         DlfPlaneJob &J = a.job[0];
-        J              = plane_job(s, in, pl);
+        J              = plane_job(s, in, pl, false);
         a.njob         = 1;
         if (in == out) {
             HIP_TRY(hipMemcpy2DAsync(s->d_scratch, in->pw[pl] * bps, in->plane[pl], in->stride[pl] * bps,

@@ -104,6 +104,7 @@ struct LrPlaneArgs {
     void                 *out;
     int32_t               dlf_stride, cdef_stride, out_stride;
     int32_t               W, H, ss, unit_size, hunits, vunits, nchunks, bd;
+    int32_t               k0, c0, nc; // the (stripe, column chunk) tiles written: k0 + i / nc, c0 + i % nc
     const SvtGpuRestUnit *units;
 };
 
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrPlaneArgs a) {
     __shared__ uint16_t t[VR * TW];        // Wiener intermediate
     __shared__ int      AB[2][(TH + 2) * (TW + 2)];
     const int S = 64 >> a.ss, off = 8 >> a.ss, cwmax = 64 >> a.ss;
-    const int k = blockIdx.x / a.nchunks, c = blockIdx.x % a.nchunks;
+    const int k = a.k0 + blockIdx.x / a.nc, c = a.c0 + blockIdx.x % a.nc;
     const int y0 = max(0, k * S - off), y1 = min((k + 1) * S - off, a.H);
     const int x0 = c * cwmax, w = min(cwmax, a.W - x0), h = y1 - y0;
     if (h <= 0 || w <= 0) return;
@@ -258,6 +259,8 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
         s->unit_size[p] = unit_size[p];
         s->hunits[p]    = count_units(unit_size[p], pw);
         s->vunits[p]    = count_units(unit_size[p], ph);
+        s->tile_units[p][0] = s->tile_units[p][1] = 0, s->tile_units[p][2] = s->hunits[p], s->tile_units[p][3] = s->vunits[p];
+        s->tile_out[p][0] = s->tile_out[p][1] = 0, s->tile_out[p][2] = pw, s->tile_out[p][3] = ph;
         nu += (size_t)s->hunits[p] * s->vunits[p];
     }
     e = hipMalloc(&s->d_units[0], sizeof(SvtGpuRestUnit) * nu);
@@ -324,9 +327,12 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
     hipStream_t  st  = pick_stream(s->ctx, stream);
     const size_t bps = cdef_out->bytes_per_sample;
     for (int p = 0; p < 3; p++) {
+        const int32_t *r = s->tile_out[p]; // the samples written (the whole plane unless tiled over GPUs)
         if (frame_type[p] == SVTGPU_RESTORE_NONE) {
-            HIP_TRY(hipMemcpy2DAsync(out->plane[p], out->stride[p] * bps, cdef_out->plane[p], cdef_out->stride[p] * bps,
-                                     cdef_out->pw[p] * bps, cdef_out->ph[p], hipMemcpyDeviceToDevice, st));
+            const size_t io = ((size_t)r[1] * cdef_out->stride[p] + r[0]) * bps, oo = ((size_t)r[1] * out->stride[p] + r[0]) * bps;
+            HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[p] + oo, out->stride[p] * bps,
+                                     (const uint8_t *)cdef_out->plane[p] + io, cdef_out->stride[p] * bps,
+                                     (r[2] - r[0]) * bps, r[3] - r[1], hipMemcpyDeviceToDevice, st));
             continue;
         }
         LrPlaneArgs a;
@@ -344,10 +350,12 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
         a.vunits      = s->vunits[p];
         a.bd          = cdef_out->bit_depth;
         a.units       = s->d_units[p];
-        const int S = 64 >> a.ss, off = 8 >> a.ss;
-        a.nchunks     = (a.W + (64 >> a.ss) - 1) / (64 >> a.ss);
-        const int nstripes = (a.H + off + S - 1) / S;
-        const dim3 grid(nstripes * a.nchunks);
+        const int S = 64 >> a.ss, off = 8 >> a.ss, cw = 64 >> a.ss;
+        a.nchunks     = (a.W + cw - 1) / cw;
+        // the rect is a union of whole (stripe, chunk) tiles (svtgpu_lr_set_tile checks)
+        a.k0 = (r[1] + off) / S, a.c0 = r[0] / cw, a.nc = (r[2] + cw - 1) / cw - a.c0;
+        const int nk = (r[3] + off + S - 1) / S - a.k0;
+        const dim3 grid(nk * a.nc);
         if (bps == 2)
             hipLaunchKernelGGL(lr_apply_kernel<uint16_t>, grid, dim3(NTHR), 0, st, a);
         else

@@ -32,6 +32,10 @@ struct SvtGpuLrState {
     // uncached device memory shared by the persistent Wiener queue's workgroups (coherent without cache flushes)
     void                *d_qarena;
     size_t               qarena_bytes;
+    // a picture tiled over GPUs (svtgpu_lr_set_tile): the units searched {col0, row0, col1, row1} and the samples
+    // written {x0, y0, x1, y1} per plane, the exchange of the search records (null: one rank)
+    int32_t              tile_units[3][4], tile_out[3][4];
+    SvtGpuComm          *comm;
 };
 void lr_profiler_destroy(void *prof);
 

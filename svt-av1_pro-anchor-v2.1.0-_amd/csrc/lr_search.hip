@@ -2601,8 +2601,8 @@ int plane_win(const SvtGpuLrSearchControls *c, int p) {
 // is the whole frame and the RD finish runs and sets the state's units.
 template <typename T>
 int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *src, const SvtGpuLrSearchControls *c,
-                 int nplanes, const int32_t *rb, const int32_t *re, int32_t *frame_type,
-                 SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
+                 int nplanes, const int32_t *rb, const int32_t *re, const int32_t *cb, const int32_t *ce,
+                 int32_t *frame_type, SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
     // SVTGPU_LR_TIMING=1 prints the host-side phase times (wall clock, including the waits) to stderr
     static const bool timing = std::getenv("SVTGPU_LR_TIMING") != nullptr;
     auto              clk    = [] { return std::chrono::steady_clock::now(); };
@@ -2629,9 +2629,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             const int uh = (H - y0 < ext) ? H - y0 : usz;
             int       vs = std::max(0, y0 - off), ve = y0 + uh;
             if (ve < H) ve -= off;
-            for (int x0 = 0; x0 < W; uidx++) {
+            for (int x0 = 0, ucol = 0; x0 < W; uidx++, ucol++) {
                 const int uw = (W - x0 < ext) ? W - x0 : usz;
-                if (urow >= rb[p] && urow < re[p]) {
+                if (urow >= rb[p] && urow < re[p] && ucol >= cb[p] && ucol < ce[p]) {
                     tile0.push_back((int)tiles.size());
                     for (int y = vs; y < ve; y += 64)
                         for (int x = x0; x < x0 + uw; x += 64)
@@ -3243,11 +3243,65 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
     if (int rc = check_search_args(s, recon, source, ctrls)) return rc;
     hipStream_t st      = pick_stream(s->ctx, stream);
     const int   nplanes = searched_planes(ctrls);
-    int32_t     rb[3] = {0, 0, 0}, re[3] = {s->vunits[0], s->vunits[1], s->vunits[2]};
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
-    return recon->bytes_per_sample == 2
-        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, frame_type_out, search_out, st)
-        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, frame_type_out, search_out, st);
+    if (!s->comm || svtgpu_comm_nranks(s->comm) == 1) {
+        int32_t rb[3] = {0, 0, 0}, re[3] = {s->vunits[0], s->vunits[1], s->vunits[2]};
+        int32_t cb[3] = {0, 0, 0}, ce[3] = {s->hunits[0], s->hunits[1], s->hunits[2]};
+        return recon->bytes_per_sample == 2
+            ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, frame_type_out, search_out, st)
+            : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, frame_type_out, search_out, st);
+    }
+    // a picture tiled over GPUs: this rank's units, the zero-padded records summed over the ranks (one contributor per
+    // unit: the gather restoration_seg_search's segments leave for rest_finish_search), then the finish of every
+    // plane on every rank (EbRestorationPick.c:1555-1634, sequential over the units), identical everywhere
+    size_t nrec = 0, base[3];
+    for (int p = 0; p < 3; p++) base[p] = nrec, nrec += (size_t)s->hunits[p] * s->vunits[p];
+    std::vector<SvtGpuLrUnitSearch> rec(nrec);
+    std::memset(rec.data(), 0, sizeof(SvtGpuLrUnitSearch) * nrec);
+    SvtGpuLrUnitSearch *outs[3] = {rec.data() + base[0], rec.data() + base[1], rec.data() + base[2]};
+    int32_t             rb[3], re[3], cb[3], ce[3];
+    for (int p = 0; p < 3; p++)
+        cb[p] = s->tile_units[p][0], rb[p] = s->tile_units[p][1], ce[p] = s->tile_units[p][2], re[p] = s->tile_units[p][3];
+    int rc = recon->bytes_per_sample == 2
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, outs, st)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, outs, st);
+    if (rc) return rc;
+    static_assert(sizeof(SvtGpuLrUnitSearch) % 8 == 0, "records travel as uint64 words");
+    if ((rc = svtgpu_comm_sum(s->comm, rec.data(), nrec * sizeof(SvtGpuLrUnitSearch) / 8, false, st))) return rc;
+    std::vector<SvtGpuRestUnit> units(nrec);
+    std::memset(units.data(), 0, sizeof(SvtGpuRestUnit) * nrec);
+    for (int p = 0; p < nplanes; p++) {
+        const int n = s->hunits[p] * s->vunits[p];
+        finish_plane(ctrls, p, plane_win(ctrls, p), outs[p], n, &frame_type_out[p], units.data() + base[p]);
+        if (search_out && search_out[p]) std::memcpy(search_out[p], outs[p], sizeof(SvtGpuLrUnitSearch) * n);
+    }
+    HIP_TRY(hipMemcpyAsync(s->d_units[0], units.data(), sizeof(SvtGpuRestUnit) * nrec, hipMemcpyHostToDevice, st));
+    svtgpu_count_xfer(0, sizeof(SvtGpuRestUnit) * nrec);
+    HIP_TRY(hipStreamSynchronize(st)); // the host staging of the units goes out of scope
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_lr_set_tile(SvtGpuLrState *s, const int32_t units[3][4], const int32_t out[3][4],
+                                  SvtGpuComm *comm) {
+    if (!s) return SVTGPU_ERR_INVALID_ARG;
+    for (int p = 0; p < 3; p++) {
+        const int pw = p ? s->width / 2 : s->width, ph = p ? s->height / 2 : s->height;
+        const int32_t all_u[4] = {0, 0, s->hunits[p], s->vunits[p]}, all_o[4] = {0, 0, pw, ph};
+        const int32_t *u = units ? units[p] : all_u, *o = out ? out[p] : all_o;
+        if (u[0] < 0 || u[1] < 0 || u[2] > s->hunits[p] || u[3] > s->vunits[p] || u[0] > u[2] || u[1] > u[3])
+            return SVTGPU_ERR_INVALID_ARG;
+        // the output rect is a union of whole (stripe, 64 >> ss column) tiles of the apply
+        const int S = 64 >> (p > 0), off = 8 >> (p > 0), cw = 64 >> (p > 0);
+        auto row_ok = [&](int y) { return y == 0 || y == ph || (y + off) % S == 0; };
+        auto col_ok = [&](int x) { return x == pw || x % cw == 0; };
+        if (o[0] < 0 || o[1] < 0 || o[2] > pw || o[3] > ph || o[0] > o[2] || o[1] > o[3] || !col_ok(o[0]) ||
+            !col_ok(o[2]) || !row_ok(o[1]) || !row_ok(o[3]))
+            return SVTGPU_ERR_INVALID_ARG;
+        std::memcpy(s->tile_units[p], u, sizeof s->tile_units[p]);
+        std::memcpy(s->tile_out[p], o, sizeof s->tile_out[p]);
+    }
+    s->comm = comm;
+    return SVTGPU_OK;
 }
 
 extern "C" int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
@@ -3261,9 +3315,10 @@ extern "C" int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon
         if (row_begin[p] < 0 || row_end[p] > s->vunits[p] || row_begin[p] > row_end[p] || !search_out[p])
             return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
+    const int32_t cb[3] = {0, 0, 0}, ce[3] = {s->hunits[0], s->hunits[1], s->hunits[2]};
     return recon->bytes_per_sample == 2
-        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, nullptr, search_out, st)
-        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, nullptr, search_out, st);
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, cb, ce, nullptr, search_out, st)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, row_begin, row_end, cb, ce, nullptr, search_out, st);
 }
 
 extern "C" int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,

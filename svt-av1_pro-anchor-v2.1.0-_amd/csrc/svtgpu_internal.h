@@ -87,7 +87,9 @@ struct SvtGpuCdefFrameState {
     uint8_t       *h_pick_dev;    // its device address
     int32_t        pick_parts;
     int32_t        mask_all;      // mask == every block
-    int32_t        fb_row_begin, fb_row_end; // band of FB rows searched/applied (tiling)
+    int32_t        fb_rect[4];    // {col0, row0, col1, row1}: the filter blocks searched (tiling over GPUs)
+    int32_t        out_rect[4];   // {x0, y0, x1, y1} luma: the samples the apply writes (tiling over GPUs)
+    SvtGpuComm    *comm;          // the pick's exchange of the search tables (tiling over GPUs; null: none)
     uint64_t      *own_mse;       // state-owned tables (d_mse/d_skip may point at caller memory)
     uint8_t       *own_skip;
     uint8_t       *own_dir;       // state-owned dir/var (d_dir/d_var may point at caller memory)
@@ -135,6 +137,8 @@ hipStream_t svtgpu_default_stream();
 // the stream's own synchronize wakes the host up tens of microseconds later, once per host round trip.  Falls
 // back to synchronizing `st` (and fails if the word is still missing after it).
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st);
+// element-wise sum of n uint64 over the ranks of `c` (comm.hip); nullptr or a one-rank comm: nothing to do
+int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st);
 // host <-> device bytes of the frame-level entry points (copies and mapped-memory results), for the bench's report
 void svtgpu_count_xfer(int d2h, size_t bytes);
 // Chains of short dependent launches with host waits in between (the CDEF pick, the DLF level search) run on a

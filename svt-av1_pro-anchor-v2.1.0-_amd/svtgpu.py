@@ -345,6 +345,17 @@ _SIGS = {
     "svtgpu_lr_finish_plane": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _I32, _I32, _P, _P, _P]),
     "svtgpu_lr_profile": (ctypes.c_int, [_P, _I32, _P]),
     "svtgpu_transfer_bytes": (ctypes.c_int, [_P, _P, _I32]),
+    "svtgpu_comm_unique_id": (ctypes.c_int, [_P]),
+    "svtgpu_comm_create": (ctypes.c_int, [_P, _I32, _I32, _P, ctypes.POINTER(_P)]),
+    "svtgpu_comm_create_host": (ctypes.c_int, [_I32, _I32, _P, ctypes.POINTER(_P)]),
+    "svtgpu_comm_destroy": (None, [_P]),
+    "svtgpu_comm_nranks": (_I32, [_P]),
+    "svtgpu_comm_rank": (_I32, [_P]),
+    "svtgpu_comm_allreduce_u64": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _I32, _P]),
+    "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
+    "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
+    "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
+    "svtgpu_lr_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
 }
 
 _lib = None
@@ -458,6 +469,103 @@ def cdef_controls(level):
     return c
 
 
+class TilePlan(ctypes.Structure):
+    """SvtGpuTilePlan: what one rank of a picture tiled over GPUs computes (svtgpu_tile_plan)."""
+    _fields_ = [("tile", _I32 * 4), ("fb_rect", _I32 * 4), ("lr_units", (_I32 * 4) * 3), ("lr_out", (_I32 * 4) * 3),
+                ("cdef_out", _I32 * 4), ("dlf_out", _I32 * 4)]
+
+    def rects(self):
+        return {k: (np.array(getattr(self, k)).tolist()) for k, _ in self._fields_}
+
+
+def tile_grid(n):
+    """gx x gy of n ranks: the widest split with gx <= gy (1x1, 1x2, 2x2, 2x4 for 1, 2, 4, 8 GPUs)."""
+    gx = max(d for d in range(1, int(n ** 0.5) + 1) if n % d == 0)
+    return gx, n // gx
+
+
+def tile_plan(width, height, unit_size, gx, gy, rank):
+    us = np.ascontiguousarray(unit_size, np.int32)
+    t = TilePlan()
+    check(lib().svtgpu_tile_plan(width, height, ptr(us), gx, gy, rank, ctypes.byref(t)))
+    return t
+
+
+_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t)
+
+
+class _HostTransport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allreduce_u64", _ALLREDUCE_FN)]
+
+
+class Comm:
+    """SvtGpuComm: the ranks of a picture tiled over GPUs.  Comm.rccl: RCCL over xGMI (one rank per device; rank 0
+    makes the id with unique_id(), the caller broadcasts it); Comm.host: a host transport, `fn(words)` summing a uint64
+    numpy array over the ranks in place (e.g. a gloo all_reduce) — several ranks on one GPU, CPU rehearsals."""
+
+    def __init__(self, h, keep=None):
+        self.h, self._keep = h, keep
+
+    @staticmethod
+    def unique_id():
+        b = (ctypes.c_uint8 * 128)()
+        check(lib().svtgpu_comm_unique_id(b))
+        return bytes(b)
+
+    @classmethod
+    def rccl(cls, ctx, nranks, rank, uid):
+        b = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        h = _P()
+        check(lib().svtgpu_comm_create(ctx.h, nranks, rank, b, ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def host(cls, nranks, rank, fn):
+        def cb(user, buf, n):
+            try:
+                a = np.ctypeslib.as_array(buf, shape=(n,))
+                fn(a)
+                return 0
+            except Exception:  # reported through the library's return code
+                import traceback
+                traceback.print_exc()
+                return -1
+        f = _ALLREDUCE_FN(cb)
+        t = _HostTransport(None, f)
+        h = _P()
+        check(lib().svtgpu_comm_create_host(nranks, rank, ctypes.byref(t), ctypes.byref(h)))
+        return cls(h, keep=(f, t))
+
+    @property
+    def nranks(self):
+        return lib().svtgpu_comm_nranks(self.h)
+
+    def allreduce(self, words, stream=None):
+        """Sum a host uint64 array over the ranks in place."""
+        a = np.ascontiguousarray(words, np.uint64)
+        check(lib().svtgpu_comm_allreduce_u64(self.h, ptr(a), a.size, 0, stream))
+        return a
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _rect(r):
+    return None if r is None else (_I32 * 4)(*[int(x) for x in r])
+
+
+def _rects3(r):
+    return None if r is None else ((_I32 * 4) * 3)(*[(_I32 * 4)(*[int(x) for x in q]) for q in r])
+
+
 class CdefState:
     """Device search state of one frame (mse_seg / skip_cdef_seg / cdef_dir_data)."""
 
@@ -511,6 +619,10 @@ class CdefState:
     def set_fb_rows(self, begin, end):
         check(lib().svtgpu_cdef_set_fb_rows(self.h, begin, end))
 
+    def set_tile(self, fb_rect=None, out_rect=None, comm=None):
+        """svtgpu_cdef_set_tile: search fb_rect, pick over the tables summed over `comm`, apply into out_rect."""
+        check(lib().svtgpu_cdef_set_tile(self.h, _rect(fb_rect), _rect(out_rect), comm.h if comm else None))
+
     def bind_tables(self, mse_dev_ptr, skip_dev_ptr):
         check(lib().svtgpu_cdef_bind_tables(self.h, mse_dev_ptr, skip_dev_ptr))
 
@@ -559,6 +671,10 @@ class DlfState:
 
     def filter_to(self, src, out, params, plane_start=0, plane_end=3, stream=None):
         check(lib().svtgpu_dlf_frame_to(self.h, src.h, out.h, ctypes.byref(params), plane_start, plane_end, stream))
+
+    def set_tile(self, sse_rect=None, out_rect=None, comm=None):
+        """svtgpu_dlf_set_tile: trial SSEs over sse_rect summed over `comm`; the filter writes out_rect."""
+        check(lib().svtgpu_dlf_set_tile(self.h, _rect(sse_rect), _rect(out_rect), comm.h if comm else None))
 
     def pick(self, recon, source, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=2,
              only_4x4=0, stream=None):
@@ -732,6 +848,10 @@ class LrState:
                    "bytes": float(raw["bytes"][0][i])} for i, c in enumerate(self.PROFILE_CLASSES)}
         out["searches"] = int(raw["searches"][0])
         return out
+
+    def set_tile(self, units=None, out=None, comm=None):
+        """svtgpu_lr_set_tile: search units[p], records summed over `comm`, finish everywhere, apply into out[p]."""
+        check(lib().svtgpu_lr_set_tile(self.h, _rects3(units), _rects3(out), comm.h if comm else None))
 
     def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
         ft = np.ascontiguousarray(frame_type, np.int32)

@@ -255,3 +255,96 @@ def check(case, out, what):
                sse=[g["lr_sse%d" % p] for p in range(3)], rec_params=[g["lr_rec%d" % p] for p in range(3)])
     lr_cases.compare_search(out["ft"], out["units"], out["recs"], ref)
     _planes_equal(g, "lr", out["lr"], digest, what + " " + case)
+
+
+# --------------------------------------------------------------------------- one rank of a picture tiled over GPUs
+def run_gpu_tiled(case, rank, world, comm, ctx=None):
+    """This rank's part of `case` with the picture tiled over `world` ranks (svtgpu_tile_plan, 1 x 2 / 2 x 2 / 2 x 4
+    grids): the frame-level calls exchange the DLF trial SSEs, the CDEF search tables and the LR search records over
+    `comm` (svtgpu.Comm).  Returns the rank's crops (the DLF output over its tile, the CDEF and LR outputs over its
+    LR units) plus the frame-level decisions every rank takes; assemble_tiled() puts the ranks' parts together."""
+    import svtgpu
+    c = pc.CASES[case]
+    g = pc.load(case)
+    src, rec, mi = pc.inputs(case)
+    bd, w, h = c["bd"], c["w"], c["h"]
+    us = [c["us"][0], c["us"][1], c["us"][1]]
+    gx, gy = svtgpu.tile_grid(world)
+    plan = svtgpu.tile_plan(w, h, us, gx, gy, rank).rects()
+    ctx = ctx or svtgpu.Context()
+    S, R, D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(5))
+    S.upload(src)
+    R.upload(rec)
+    dl = svtgpu.DlfState(ctx, w, h)
+    dl.set_mode_info(mi)
+    dl.set_tile(plan["tile"], plan["dlf_out"], comm)
+    dc = dlf_ctrls(c["dlf_level"])
+    lfp = dl.pick(R, S, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"], c["only4x4"])
+    dl.filter_to(R, D, lfp)
+    st = svtgpu.CdefState(ctx, w, h)
+    st.set_block_mask(pc.cdef_mask(mi))
+    if c["sb"] == 128:
+        st.set_fb_bsize(np.ascontiguousarray(mi)["bsize"][::16, ::16].reshape(-1))
+    st.set_tile(plan["fb_rect"], plan["cdef_out"], comm)
+    ctrls = svtgpu.cdef_controls(c["cdef_level"])
+    ctrls.pred_y_f, ctrls.pred_uv_f = c["pred"]
+    st.search(D, S, ctrls, c["q"])
+    prm, fbs = st.pick(ctrls, c["q"], int(g["cdef_lambda"][0]))
+    tables = st.read()  # after the pick: every rank's blocks, summed over the ranks
+    nb = 1 << prm.cdef_bits
+    applied = int(prm.cdef_y_strength[0] != 0 or prm.cdef_uv_strength[0] != 0 or nb != 1)
+    if applied:
+        st.apply(D, C, prm)
+    else:
+        svtgpu.check(svtgpu.lib().svtgpu_frame_copy(C.h, D.h, None))
+    lr = svtgpu.LrState(ctx, w, h, us)
+    lr.set_tile(plan["lr_units"], plan["lr_out"], comm)
+    lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
+    ft, recs = lr.search(C, S, lrc, records=True)
+    units = [svtgpu.lr_finish_plane(lrc, p, recs[p])[1] for p in range(3)]
+    if any(ft):
+        lr.apply(D, C, O, ft)
+    else:
+        svtgpu.check(svtgpu.lib().svtgpu_frame_copy(O.h, C.h, None))
+    ctx.synchronize()
+
+    def crop(planes, rects):
+        return [np.ascontiguousarray(planes[p][r[1]:r[3], r[0]:r[2]]) for p, r in enumerate(rects)]
+    t = plan["tile"]
+    tile3 = [t, [t[0] // 2, t[1] // 2, t[2] // 2, t[3] // 2], [t[0] // 2, t[1] // 2, t[2] // 2, t[3] // 2]]
+    out = dict(rank=rank, plan=plan, tile3=tile3, lf=lfp.levels(), dlf=crop(D.download(), tile3), tables=tables,
+               prm=prm.as_tuple(), nb=nb, fbs=fbs, applied=applied, cdef=crop(C.download(), plan["lr_out"]), ft=ft,
+               units=units, recs=recs, lr=crop(O.download(), plan["lr_out"]))
+    for x in (S, R, D, C, O, dl, st, lr):
+        x.close()
+    return out
+
+
+def assemble_tiled(case, parts):
+    """The ranks' parts of run_gpu_tiled as one run_gpu-style result (frame-level decisions must agree)."""
+    import svtgpu
+    c = pc.CASES[case]
+    src, rec, mi = pc.inputs(case)
+    w, h = c["w"], c["h"]
+    p0 = parts[0]
+    for q in parts[1:]:
+        assert tuple(q["lf"]) == tuple(p0["lf"]) and q["prm"] == p0["prm"] and list(q["ft"]) == list(p0["ft"])
+        assert np.array_equal(q["fbs"], p0["fbs"])
+        for a, b in zip(q["tables"], p0["tables"]):
+            assert np.array_equal(a, b)
+        for p in range(3):
+            assert q["recs"][p].tobytes() == p0["recs"][p].tobytes()
+    shapes = [(h, w), (h // 2, w // 2), (h // 2, w // 2)]
+    full = {k: [np.zeros(s, np.uint16) - 1 for s in shapes] for k in ("dlf", "cdef", "lr")}
+    for q in parts:
+        for key, rects in (("dlf", q["tile3"]), ("cdef", q["plan"]["lr_out"]), ("lr", q["plan"]["lr_out"])):
+            for p, r in enumerate(rects):
+                full[key][p][r[1]:r[3], r[0]:r[2]] = q[key][p]
+    prm = svtgpu.CdefParams()
+    prm.cdef_damping, prm.cdef_bits = p0["prm"][0], p0["prm"][1]
+    for k, (y, uv) in enumerate(zip(p0["prm"][2], p0["prm"][3])):
+        prm.cdef_y_strength[k], prm.cdef_uv_strength[k] = y, uv
+    lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
+    return dict(src=src, rec=rec, mi=mi, lf=p0["lf"], dlf=full["dlf"], tables=p0["tables"], prm=prm, nb=p0["nb"],
+                fbs=p0["fbs"], applied=p0["applied"], cdef=full["cdef"], ft=p0["ft"], units=p0["units"],
+                recs=p0["recs"], lrc=lrc, lr=full["lr"])
