@@ -1,34 +1,36 @@
 #!/usr/bin/env python
 """bench.py — MI355X in-loop-filter hot path throughput (BASELINE.json metric).
 
-A "step" = one 4K 10-bit 4:2:0 frame through the device-resident in-loop filter pipeline:
-  DLF stage (EbDlfProcess.c, dlf level 1): full-image level search (svt_av1_pick_filter_level) and
-      the frame filter (svt_av1_loop_filter_frame) into the DLF output frame;
-  CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64
-      strengths, cdef_level 1) -> frame-level strength pick (finish_cdef_search) -> apply
-      (svt_av1_cdef_frame).
-  LR stage (EbRestProcess.c): loop-restoration search (restoration_seg_search + rest_finish_search,
-      wn/sg filter level 1: 7-tap Wiener with refinement, 16 SGR eps with refinement) on the CDEF output and
-      the apply (svt_av1_loop_restoration_filter_frame; RU 256 luma / 128 chroma; stripe boundary lines
-      from the DLF output);
-  MD distortion stage: SAD / SSE / variance of every AV1 block shape of every SB against 7 reference
-      frames at one full-pel motion vector per (SB, reference) (SURVEY.md §8d config 5 workload at 4K).
-Inputs are synthetic (recon = source + blocking/ringing, 16x16 non-skip inter blocks
-with hashed 4/8/16 transforms) and resident in HBM before timing.
+A "step" = one 4K 10-bit 4:2:0 frame per frame slot through the device-resident in-loop filter pipeline:
+  mode info: the frame's mode-info grid uploaded and its deblocking edge records rebuilt (an encoder hands over a new
+      grid every frame);
+  DLF stage (EbDlfProcess.c, dlf level 1): full-image level search (svt_av1_pick_filter_level) and the frame filter
+      (svt_av1_loop_filter_frame);
+  CDEF stage (EbCdefProcess.c / EbEncCdef.c): strength search over all 64x64 filter blocks (64 strengths, cdef_level
+      1) -> frame-level strength pick (finish_cdef_search) -> apply (svt_av1_cdef_frame);
+  LR stage (EbRestProcess.c): loop-restoration search (restoration_seg_search + rest_finish_search, wn/sg filter level
+      1: 7-tap Wiener with refinement, 16 SGR eps with refinement) on the CDEF output and the apply
+      (svt_av1_loop_restoration_filter_frame; RU 256 luma / 128 chroma; stripe boundary lines from the DLF output);
+  MD distortion stage: SAD / SSE / variance of every AV1 block shape of every SB against 7 reference frames at one
+      full-pel motion vector per (SB, reference) (SURVEY.md §8d config 5 workload at 4K).
+Inputs: the 4K 10-bit (and 1080p 8-bit) frames, mode info and frame-level controls (base_q_idx, starting
+loop-filter levels, the CDEF lambda, the LR rate inputs) are those of the reference-pinned pipeline cases
+(tests/pipeline_cases.py c3_4k10 / c1_1080p8; tests/golden/pipe_*.npz hold the reference's own outputs on them and
+tests/test_pipeline_golden.py checks the GPU against them bit-exact): the timed frames are the checked frames.
+Other sizes use the same integer generator, unpinned.  Inputs are resident in HBM before timing.
 
-N = 1: the whole frame on one GPU.  N > 1 (torchrun, one rank per GPU): the DLF stage is replicated
-(every rank deblocks the whole frame: its level search needs whole-frame SSEs); the CDEF frame is
-tiled into bands of filter-block rows; each rank searches its band, the [2][nFB][64] mse table and
-skip flags and the per-8x8 dir/var tables are all-reduce-summed over RCCL (zeros outside each band),
-every rank runs the (replicated, deterministic) pick and applies the whole frame (0.12 ms; the LR search
-bands below read all of it); the LR search is split by unit rows (each rank
-searches its units, the per-unit records are all-gathered over RCCL and every rank runs the host RD
-finish, then the replicated apply); the MD batch is split by superblock ranges (no exchange) — strong
-scaling of one frame per step.
+N = 1: the whole frame on one GPU.  N > 1 (one rank per GPU; `--gpus N` spawns its ranks, or torchrun):
+  tiles (default): every frame is tiled over the ranks (svtgpu_tile_plan: 1x2, 2x2, 2x4 grids on the restoration-unit
+      grid); each rank runs the DLF trials, the CDEF search, the LR search and all three applies on its tile, and the
+      frame-level calls exchange over RCCL (libsvtgpu's own communicator, one per frame slot): the DLF trial SSEs
+      before every bisection step, the CDEF search tables before the pick, the LR search records before the RD
+      finish; the MD batch takes an SB range per rank.  Strong scaling: a step is the same F frames at every N.
+  frames (opt-in, secondary): every rank filters whole pictures of its own, no exchange (weak scaling).
 
-Prints ONE JSON line on rank 0 (contract in the task description): value = luma Mpixels/s of the
-whole job, plus `roofline` for the dominant kernel (timed with HIP events on the stream it runs
-on) and `cpu_baseline` (the repo's C restatement on this host, rank 0, N = 1, bounded sample).
+Prints ONE JSON line on rank 0 (contract in the task description): value = luma Mpixels/s of the whole job, plus
+`roofline` for the largest device-time kernel of the step (timed live on the stream it runs on; traffic and VALU
+issue from the committed PMC profile) and `cpu_baseline` (the reference's own CPU path on this host, rank 0, N = 1,
+bounded sample).
 """
 import argparse
 import json
@@ -63,22 +65,36 @@ sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
 import svtgpu  # noqa: E402
 import synth  # noqa: E402
 
-def measured_traffic(path, kernel, bd):
-    """HBM-side bytes per launch of `kernel` from the committed PMC summary (scripts/pmc_traffic.py): FETCH_SIZE and
-    WRITE_SIZE need their own rocprofv3 --pmc passes, so they are collected by a separate profiled run of this bench
-    and read back here.  None when no summary covers the kernel."""
+def pmc_summary(path, kernel, bd):
+    """Per-launch PMC figures of `kernel` from the committed summary (scripts/pmc_traffic.py / pmc_sq.py over
+    rocprofv3 --pmc passes of this bench, which cannot run inside it): traffic bytes (2 x FETCH_SIZE + WRITE_SIZE)
+    and SQ_INSTS_VALU.  ({}, None) when no summary covers the kernel."""
     try:
         summary = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
-    name = kernel.split()[0] + ("<unsigned short>" if bd > 8 else "<unsigned char>")
+        return {}, None
+    name = kernel + ("<unsigned short>" if bd > 8 else "<unsigned char>")
     k = summary.get("kernels", {}).get(name)
     if not k:
-        return None, None
-    return k["traffic_bytes"], "%s (%s; %d launches)" % (os.path.relpath(path, ROOT), summary["method"], k["launches"])
+        return {}, None
+    return k, "%s (%s; %d launches)" % (os.path.relpath(path, ROOT), summary["method"], k["launches"])
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 instruction every 2 cycles per SIMD (SIMD32), 2.4 GHz
+VALU_PEAK_INSTS = 256 * 4 * 0.5 * 2.4e9
+
+# BASELINE configurations whose frames and frame-level controls are the reference-pinned pipeline cases
+# (tests/pipeline_cases.py; the reference's outputs on them in tests/golden/pipe_<case>.npz, checked bit-exact by
+# tests/test_pipeline_golden.py; tests/test_bench_inputs.py checks these constants against the cases and fixtures)
+PINNED = {
+    (3840, 2160, 10): dict(case="c3_4k10", seed=0x5EED0003, q=160, lf=(16, 16, 8, 8), lam=206765, rdmult=7000,
+                           sw=(300, 700, 900), wc=(250, 800), sc=(250, 900), us=(256, 128)),
+    (1920, 1080, 8): dict(case="c1_1080p8", seed=0x5EED0002, q=160, lf=(16, 16, 8, 8), lam=207229, rdmult=7000,
+                          sw=(300, 700, 900), wc=(250, 800), sc=(250, 900), us=(256, 128)),
+}
+UNPINNED = dict(case=None, q=160, lf=(16, 16, 8, 8), lam=206765, rdmult=7000, sw=(300, 700, 900), wc=(250, 800),
+                sc=(250, 900), us=(256, 128))
 
 
 def parse():
@@ -90,11 +106,11 @@ def parse():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--bit-depth", type=int, default=10)
     ap.add_argument("--cdef-level", type=int, default=1)
-    ap.add_argument("--base-q-idx", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true", help="no HIP-event timing inside the LR search")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc", "traffic.json"),
-                    help="per-launch HBM traffic from scripts/pmc_traffic.sh (PMC passes cannot run inside the bench)")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="no device-clock timing inside the LR search")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03", "pmc", "kernels.json"),
+                    help="per-launch traffic / VALU counters from scripts/pmc_traffic.sh (PMC passes cannot run inside "
+                         "the bench)")
     ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
     ap.add_argument("--cpu-passes", type=int, default=6,
                     help="reference CPU baseline: passes over the crops (sizes the sample to ~10-30 s of CPU work)")
@@ -105,11 +121,14 @@ def parse():
                     help="frames pipelined per GPU, each on its own streams and host thread (the encoder's "
                          "picture-level parallelism); a step processes one frame per slot")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="nccl (= RCCL over xGMI) for the real runs; gloo rehearses N > 1 ranks sharing one GPU")
-    ap.add_argument("--split", default="frames", choices=("frames", "bands"),
-                    help="N > 1: 'frames' = every rank filters its own frames (pictures are independent objects of "
-                         "the in-loop filter path; no data-path collective, weak scaling); 'bands' = one frame per "
-                         "step cut into row bands across the ranks (SURVEY §8e; RCCL exchanges, strong scaling)")
+                    help="the tiles' exchanges: nccl = libsvtgpu's RCCL communicator over xGMI (one rank per GPU); "
+                         "gloo = the library's host transport over gloo (rehearses N > 1 ranks sharing one GPU)")
+    ap.add_argument("--split", default="tiles", choices=("tiles", "frames"),
+                    help="N > 1: 'tiles' = every frame tiled over the ranks with RCCL exchanges (SURVEY §8e, BASELINE "
+                         "config 4; strong scaling); 'frames' = every rank filters pictures of its own (weak scaling)")
+    ap.add_argument("--inputs", default="pinned", choices=("pinned", "synth"),
+                    help="pinned: the reference-pinned pipeline case of this size when there is one (else synth); "
+                         "synth: the float generator (synth.frame_pair)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
     ap.add_argument("--stages", default="all", choices=("all", "cdef"),
                     help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
@@ -189,12 +208,12 @@ def cpu_threads():
 REF_BENCH = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
 
 
-def write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs):
+def write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs, lf_start):
     """The input file of oracle/_ref/ref_bench (layout in oracle/ref_harness/ref_bench.c's main)."""
     gx, gy = (int(x) for x in grid.split("x"))
     H, W = rec[0].shape
     hdr = np.array([W, H, bd, len(md_refs), q, lam, gx, gy, lr_ctrls.rdmult, *lr_ctrls.switchable_restore_cost,
-                    *lr_ctrls.wiener_restore_cost, *lr_ctrls.sgrproj_restore_cost], np.int32)
+                    *lr_ctrls.wiener_restore_cost, *lr_ctrls.sgrproj_restore_cost, *lf_start], np.int32)
     f.write(hdr.tobytes())
     f.write(bytes(ctrls))
     for planes in (src, rec):
@@ -207,7 +226,7 @@ def write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md
 
 
 def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrls, md_refs, md_mvs, passes,
-                           stages="all"):
+                           lf_start, stages="all"):
     """The reference's own CPU path (oracle/_ref/ref_bench: its C with the AVX2/SSE2 kernels an AVX2 host binds) on the
     host's cores, over the same crops as cpu_baseline. The frame, mode info, CDEF controls, LR rate inputs, MD
     references and MVs are handed over in a file; the binary times itself (input loading excluded)."""
@@ -226,7 +245,7 @@ def cpu_baseline_reference(src, rec, mi, ctrls, bd, level, q, lam, grid, lr_ctrl
         return int(kv["px"]), float(kv["seconds"])
 
     with tempfile.NamedTemporaryFile(prefix="ref_bench_", suffix=".bin", dir="/tmp", delete=True) as f:
-        write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs)
+        write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, grid, lr_ctrls, md_refs, md_mvs, lf_start)
         f.flush()
         px, dt = run(f, nthr, passes)
         px1, dt1 = run(f, 1, 1)  # one thread, one pass: the per-core rate
@@ -378,6 +397,34 @@ def measure_next_rows(ctx, torch, W, H, reps=20):
     return out
 
 
+def roofline_of(kernels, bd, pmc_json):
+    """The `roofline` object for the largest device-time kernel of the step.  kernels: name -> {ms (device time per
+    frame), launches (per frame), alg_bytes (SURVEY §8(d) bytes per frame: the samples the kernel's job reads once and
+    the outputs it must write), what}.  traffic / SQ_INSTS_VALU per launch come from the committed PMC summary."""
+    name = max(kernels, key=lambda k: kernels[k]["ms"])
+    k = kernels[name]
+    per_launch_ms = k["ms"] / max(k["launches"], 1)
+    alg = k["alg_bytes"] / max(k["launches"], 1)
+    ach = alg / (per_launch_ms * 1e-3) / 1e9
+    pmc, src = pmc_summary(pmc_json, name, bd)
+    traffic = pmc.get("traffic_bytes")
+    valu = pmc.get("SQ_INSTS_VALU")
+    out = {"kernel": name, "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic, "alg_bytes_per_launch": round(alg),
+           "avg_launch_ms": round(per_launch_ms, 5), "launches_per_frame": k["launches"],
+           "ms_per_frame": round(k["ms"], 4),
+           "valu": round(valu / (per_launch_ms * 1e-3 * VALU_PEAK_INSTS), 4) if valu else None,
+           "valu_insts_per_launch": valu, "pmc_source": src,
+           "all_kernels_ms_per_frame": {n: round(v["ms"], 4) for n, v in sorted(kernels.items(), key=lambda x: -x[1]["ms"])},
+           "note": "the largest device-time kernel of the step (device time per frame, timed live: HIP events for "
+                   "the CDEF search and MD batch, the device's s_memrealtime clock for the LR search kernels -- first "
+                   "workgroup start to last workgroup end of every launch); achieved = SURVEY §8(d) algorithmic "
+                   "bytes (%s) / its launch duration; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch and valu = "
+                   "SQ_INSTS_VALU / (launch duration x %.3g wave-instructions/s VALU issue peak), both from %s" %
+                   (k["what"], VALU_PEAK_INSTS, os.path.relpath(pmc_json, ROOT))}
+    return out
+
+
 def main():
     a = parse()
     rc = spawn_ranks(a)
@@ -393,30 +440,24 @@ def main():
     import torch.distributed as dist
     local = local % max(1, torch.cuda.device_count())  # ranks > GPUs only in a gloo rehearsal on one GPU
     torch.cuda.set_device(local)
-    if world > 1:
-        if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
     n = world
-    banded = n > 1 and a.split == "bands"  # else every rank runs whole frames of its own
+    if n > 1:  # control only (barriers, the max-over-ranks time, the RCCL ids): the data path is libsvtgpu's RCCL
+        dist.init_process_group("gloo")
+    tiled = n > 1 and a.split == "tiles"
     W, H, bd = a.width, a.height, a.bit_depth
-    q, lam = a.base_q_idx, 60000
+    pin = PINNED.get((W, H, bd)) if a.inputs == "pinned" else None
+    cfg = pin or UNPINNED
+    q, lam = cfg["q"], cfg["lam"]
+    lr_us = [cfg["us"][0], cfg["us"][1], cfg["us"][1]]
 
     ctx = svtgpu.Context(local)
     ctrls = svtgpu.cdef_controls(a.cdef_level)
-    nvfb, nhfb = (H // 4 + 15) // 16, (W // 4 + 15) // 16
-    nb = n if banded else 1
-    rb = rank if banded else 0
-    rows = np.linspace(0, nvfb, nb + 1).round().astype(int)
-    cdef_rows = (int(rows[rb]), int(rows[rb + 1]))
     mi = synth.mode_info(W, H, 3)
-    lf_start = svtgpu.LfParams.make(32, 32, 16, 16)  # the previous frame's levels (search start)
-    # loop restoration: RU 256 / 128, wn_filter_lvl 1 + sg_filter_lvl 1 (maximum search work); the rate
-    # inputs (rdmult, restore-type costs) come from the encoder's entropy state: fixed representative values
-    lr_us = [256, 128, 128]
-    lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=7000, switchable=(300, 700, 900), wiener=(250, 800),
-                                  sgrproj=(250, 900))
+    mi_bytes = mi.nbytes
+    lf_start = svtgpu.LfParams.make(*cfg["lf"])  # the previous frame's levels (search start)
+    lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=cfg["rdmult"], switchable=cfg["sw"], wiener=cfg["wc"], sgrproj=cfg["sc"])
+    gx, gy = svtgpu.tile_grid(n) if tiled else (1, 1)
+    plan = svtgpu.tile_plan(W, H, lr_us, gx, gy, rank).rects() if tiled else None
     NREF = 7
     md_refs, md_ref_y = [], []  # reference frames of the MD batch, shared by the frames in flight
     for r in range(NREF):
@@ -427,38 +468,50 @@ def main():
         md_ref_y.append(rs[0])
     torch.cuda.synchronize()
 
+    def frame_inputs(k):
+        if pin:  # the pinned case's frames (every slot the same pictures; nothing is cached between frames)
+            return synth.frame_pair_int(W, H, bd, pin["seed"])
+        return synth.frame_pair_int(W, H, bd, 0x5EED0010 + 0x100 * k + 0x10000 * (0 if tiled else rank)) \
+            if a.inputs == "pinned" else synth.frame_pair(W, H, bd, seed=0x5EED0003 + 0x100 * k + 0x10000 * rank)
+
+    def make_comm(k):
+        """One communicator per frame slot (created in slot order on every rank: RCCL's init is collective)."""
+        if not tiled:
+            return None
+        if a.dist_backend == "nccl":
+            uid = [svtgpu.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            return svtgpu.Comm.rccl(ctx, n, rank, uid[0])
+        grp = dist.new_group(backend="gloo")
+
+        def allreduce(words):
+            dist.all_reduce(torch.from_numpy(words.view(np.int64)), group=grp)
+        return svtgpu.Comm.host(n, rank, allreduce)
+
     class Slot:
-        """One frame in flight: its own input frames, stage states, streams and (N > 1) process group."""
+        """One frame in flight: its own input frames, stage states, streams and (tiles) communicator."""
 
         def __init__(self, k):
             self.k = k
-            # a non-default torch stream: the library launches on it, torch events time it, RCCL orders on it
-            self.stream = torch.cuda.Stream()
+            self.stream = torch.cuda.Stream()     # the library launches on it, torch events time it
             self.md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
             sp = self.stream.cuda_stream
-            # frames split: each rank filters different pictures
-            self.src, self.rec = synth.frame_pair(W, H, bd, seed=0x5EED0003 + 0x100 * k + (0 if banded else 0x10000 * rank))
+            self.src, self.rec = frame_inputs(k)
             self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
             self.R.upload(self.rec, sp)
             self.S.upload(self.src, sp)
             self.dl = svtgpu.DlfState(ctx, W, H)
-            self.dl.set_mode_info(mi, sp)
             self.lr = svtgpu.LrState(ctx, W, H, lr_us)
             self.md = svtgpu.MdBatch(ctx, W, H, NREF)
             self.md_mvs = np.random.default_rng(5 + k).integers(-16, 17, size=(self.md.nsb, NREF, 2))
             self.md.set_mvs(self.md_mvs, sp)
             self.st = svtgpu.CdefState(ctx, W, H)
-            self.group = dist.new_group(backend=a.dist_backend) if banded else None  # one communicator per slot
-            if banded:
-                self.st.set_fb_rows(*cdef_rows)
-                self.mse_t = torch.zeros((2, self.st.nfb, 64), dtype=torch.int64, device="cuda")
-                self.skip_t = torch.zeros(self.st.nfb, dtype=torch.uint8, device="cuda")
-                self.dir_t = torch.zeros((self.st.nfb, 64), dtype=torch.uint8, device="cuda")
-                self.var_t = torch.zeros((self.st.nfb, 64), dtype=torch.int32, device="cuda")
-                self.st.bind_tables(self.mse_t.data_ptr(), self.skip_t.data_ptr())
-                self.st.bind_dir_tables(self.dir_t.data_ptr(), self.var_t.data_ptr())
-            self.md_range = svtgpu.band(self.md.nsb, nb, rb)  # MD batch: SB ranges, no collective
-            self.lr_rb, self.lr_re = svtgpu.lr_unit_rows(self.lr.units, nb, rb)  # LR: unit-row bands, all-gather
+            self.comm = make_comm(k)
+            if tiled:
+                self.dl.set_tile(plan["tile"], plan["dlf_out"], self.comm)
+                self.st.set_tile(plan["fb_rect"], plan["cdef_out"], self.comm)
+                self.lr.set_tile(plan["lr_units"], plan["lr_out"], self.comm)
+            self.md_range = svtgpu.band(self.md.nsb, n, rank) if tiled else (0, self.md.nsb)
             self.ev = []  # per timed step: events on the streams the kernels run on
             self.lf_levels = []
             self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
@@ -485,26 +538,19 @@ def main():
                     es[6].record(stream), es[7].record(stream)
                     self.ev.append(es)
                 return
-            # DLF stage: level search (host-driven bisection, one fused trial kernel per step) + frame filter
+            # the frame's mode info: upload + edge records; DLF level search + frame filter
+            dl.set_mode_info(mi, sp)
             lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
             dl.filter_to(R, D, lfp, 0, 3, sp)
             if timed:
                 es[1].record(stream)
                 self.lf_levels.append(lfp.levels())
-            # CDEF stage on the deblocked frame
-            if banded:
-                st.clear_tables(sp)
+            # CDEF stage on the deblocked frame (tiles: this rank's filter blocks; the pick sums the tables)
             st.search(D, S, ctrls, q, sp)
             if timed:
                 es[2].record(stream)
-            if banded:
-                for t in (self.mse_t, self.skip_t, self.dir_t, self.var_t):  # zero-padded band tables -> frame
-                    dist.all_reduce(t, group=self.group)                    # tables (RCCL over xGMI)
-                st.set_fb_rows(0, nvfb)  # every rank applies the whole frame: the LR search bands read all of O
             prm, _ = st.pick(ctrls, q, lam, sp)
             st.apply(D, O, prm, sp)
-            if banded:
-                st.set_fb_rows(*cdef_rows)
             if timed:
                 es[3].record(stream)
             # MD distortion batch (source vs 7 references, every block shape): independent of the filter chain, on
@@ -515,19 +561,10 @@ def main():
             self.md.run(S, md_refs, self.md_range[0], self.md_range[1], md_stream.cuda_stream)
             if timed:
                 es[7].record(md_stream)
-            # LR search + apply on the CDEF output (boundary lines from the DLF output)
+            # LR search + apply on the CDEF output (tiles: this rank's units; the records are summed before the
+            # finish) with the boundary lines from the DLF output
             self.at_lr.set()
-            if not banded:
-                lr_ft = lr.search(O, S, lr_ctrls, sp)
-            else:
-                recs = lr.search_units(O, S, lr_ctrls, self.lr_rb, self.lr_re, stream=sp)
-                recs = svtgpu.gather_lr_records(recs, lr.units, n, rank, group=self.group,
-                                                device="cuda" if a.dist_backend == "nccl" else None)
-                lr_ft = []
-                for p in range(3):
-                    ftp, units_p = svtgpu.lr_finish_plane(lr_ctrls, p, recs[p])
-                    lr.set_units(p, units_p, sp)
-                    lr_ft.append(ftp)
+            lr_ft = lr.search(O, S, lr_ctrls, sp)
             lr.apply(D, O, L, lr_ft, sp)
             if timed:
                 es[4].record(stream)
@@ -540,6 +577,16 @@ def main():
     slots = [Slot(k) for k in range(F)]
     torch.cuda.synchronize()
     lr = slots[0].lr
+    # host -> device bytes of a frame's inputs (recon + source; resident before timing) and their PCIe-inclusive
+    # upload rate from pageable host memory, measured once here
+    s0 = slots[0]
+    t_up = time.perf_counter()
+    for _ in range(3):
+        s0.R.upload(s0.rec, s0.stream.cuda_stream)
+        s0.S.upload(s0.src, s0.stream.cuda_stream)
+    torch.cuda.synchronize()
+    up_s = (time.perf_counter() - t_up) / 3
+    in_bytes = sum(p.nbytes for p in s0.rec) + sum(p.nbytes for p in s0.src)
 
     errors = []
 
@@ -572,8 +619,7 @@ def main():
     run_all(a.warmup, False)
     svtgpu.transfer_bytes(reset=True)
     # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
-    # of every launch, accumulated on the device and read once after the timed region; HIP-event packets around
-    # each of the ~100 launches per search would cost ~20 us apiece) -- slot 0's searches
+    # of every launch, accumulated on the device and read once after the timed region) -- slot 0's searches
     lr.profile(not a.no_kernel_timing)
     torch.cuda.synchronize()
     if n > 1:
@@ -589,7 +635,7 @@ def main():
     lr_tot = lr.profile(False) if not a.no_kernel_timing else None
     h2d, d2h = svtgpu.transfer_bytes(reset=True)
     if n > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])]
@@ -598,66 +644,73 @@ def main():
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
-    frames_per_step = F * (1 if banded else n)  # frames split: every rank filters F frames per step
+    frames_per_step = F * (1 if tiled else n)  # frames split: every rank filters F frames per step
     value = frames_per_step * W * H / (ms_per_step * 1e-3) / 1e6  # the whole job's luma pixels per second
     lr_cls = {c: {k: lr_tot[c][k] / max(lr_tot["searches"], 1) if lr_tot else 0.0 for k in ("launches", "ms", "bytes")}
               for c in svtgpu.LrState.PROFILE_CLASSES}
-    # roofline of the dominant kernel (cdef_search): algorithmic bytes per launch:
-    # recon + source read once (2*S*B) + per-FB outputs (mse 2x64 u64, dir 64 u8, var 64 i32, skip)
+    # SURVEY §8(d) algorithmic bytes; per rank: its share of the frame (tiles)
     S_samples = 1.5 * W * H
     B = 2 if bd > 8 else 1
-    st = slots[0].st
-    nfb_band = (cdef_rows[1] - cdef_rows[0]) * nhfb
-    alg_bytes = 2 * S_samples * B * nfb_band / st.nfb + nfb_band * (2 * 64 * 8 + 64 + 64 * 4 + 1)
-    achieved = alg_bytes / (search_ms * 1e-3) / 1e9
-    evals = nfb_band * 6144 * ctrls.strengths().__len__()  # (sample, strength) filter evaluations
-    roof = {"kernel": "cdef_search_kernel", "bound": "hbm", "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None, "avg_launch_ms": round(search_ms, 4),
-            "note": "VALU-bound kernel (64 strengths per sample read); HBM fraction is low by "
-                    "construction. filter evaluations/s = %.3g" % (evals / (search_ms * 1e-3))}
-    lr_names = {"stats": "wiener_stats_kernel (+unit sums)", "sgr_filters": "sgr_flt_kernel",
-                "wiener_trials": "wiener_unit_kernel", "projection": "sgr_queue_kernel", "other": "lr descent kernels",
-                "sgr_moments": "sgr_mom_kernel"}
-    # the largest device-time kernel of the step among the streaming kernels (the persistent descent kernels'
-    # durations include their descents' dependent rounds, not streaming time)
-    dom = max(("stats", "sgr_filters", "sgr_moments"), key=lambda c: lr_cls[c]["ms"])
-    if a.stages == "all" and lr_cls[dom]["ms"] > search_ms:
-        c = lr_cls[dom]
-        ach = c["bytes"] / (c["ms"] * 1e-3) / 1e9
-        roof = {"kernel": lr_names[dom], "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None,
-                "avg_launch_ms": round(c["ms"] / max(c["launches"], 1), 5), "launches_per_step": c["launches"],
-                "ms_per_step": round(c["ms"], 4),
-                "note": "largest device-time kernel of the step; launch durations from the device's s_memrealtime "
-                        "clock (first workgroup start to last workgroup end, every launch of slot 0's timed searches; "
-                        "with several frames in flight the other frames' kernels share the CUs); achieved = "
-                        "algorithmic bytes (CDEF samples read once, the 16 eps' int16 filter planes written once) / "
-                        "device time; the kernel is VALU-bound (A/B maps and both filters of 16 eps per pixel), so "
-                        "its HBM fraction is low by construction (DESIGN.md 3.5)"}
-    roof["traffic"], roof["traffic_source"] = measured_traffic(a.traffic_json, roof["kernel"], bd)
+    share = 1.0
+    if tiled:
+        t_ = plan["tile"]
+        share = (t_[2] - t_[0]) * (t_[3] - t_[1]) / float(W * H)
+    SB = S_samples * B * share
+    st0 = slots[0].st
+    nfb_mine = st0.nfb * share
+    nsb = ((W + 63) // 64) * ((H + 63) // 64)
+    nsb_mine = slots[0].md_range[1] - slots[0].md_range[0]
+    cdef_alg = 2 * SB + nfb_mine * (2 * 64 * 8 + 64 + 64 * 4 + 1)
+    kernels = {"cdef_search_kernel": dict(ms=search_ms, launches=1, alg_bytes=cdef_alg,
+                                          what="recon + source read once, 2*S*B, + the per-FB mse/dir/var/skip outputs")}
+    if a.stages == "all":
+        kernels["md_dist_kernel"] = dict(ms=md_ms, launches=1, alg_bytes=nsb_mine * (1 + NREF) * 64 * 64 * B,
+                                         what="(1 + refs) x 64 x 64 x B per superblock")
+        if lr_tot:
+            lr_kern = {"wiener_trials": ("wiener_res_kernel", 2 * SB, "the CDEF output and source of the searched "
+                                                                      "planes read once, 2*S*B"),
+                       "sgr_filters": ("sgr_flt_kernel", SB, "the CDEF output read once, S*B"),
+                       "projection": ("proj_err_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B"),
+                       "sgr_moments": ("sgr_mom_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
+            for cls, (kn, alg, what) in lr_kern.items():
+                c = lr_cls[cls]
+                if c["launches"] > 0:
+                    kernels[kn] = dict(ms=c["ms"], launches=c["launches"], alg_bytes=alg, what=what)
+    roof = roofline_of(kernels, bd, a.pmc_json)
     # SURVEY §8(d) algorithmic bytes per frame by stage, over slot 0's stage times (HIP events; with several frames in
     # flight the stages share the device with the other frames), and the pipeline total over the wall time per frame
-    SB = S_samples * B
-    nsb = ((W + 63) // 64) * ((H + 63) // 64)
-    stage_bytes = {"dlf_pick_filter": 2 * SB, "cdef_search": alg_bytes, "cdef_pick_apply": 2 * SB,
-                   "lr_search_apply": 4 * SB, "md_sad_sse_var": nsb * (1 + NREF) * 64 * 64 * B}
+    stage_bytes = {"dlf_pick_filter": 2 * SB, "cdef_search": cdef_alg, "cdef_pick_apply": 2 * SB,
+                   "lr_search_apply": 4 * SB, "md_sad_sse_var": nsb_mine * (1 + NREF) * 64 * 64 * B}
     stage_t = {"dlf_pick_filter": dlf_ms, "cdef_search": search_ms, "cdef_pick_apply": cdef_rest_ms,
                "lr_search_apply": lr_ms, "md_sad_sse_var": md_ms}
     stage_roof = {k: {"alg_MB": round(stage_bytes[k] / 1e6, 2), "ms": round(stage_t[k], 4),
                       "frac": round(stage_bytes[k] / max(stage_t[k], 1e-9) * 1e-6 / HBM_PEAK_GBS, 5)}
                   for k in stage_bytes if a.stages == "all" or k in ("cdef_search", "cdef_pick_apply")}
-    pipe_bytes = (10 * SB if a.stages == "all" else 4 * SB)
+    pipe_bytes = (10 if a.stages == "all" else 4) * S_samples * B
     frame_wall_ms = ms_per_step / frames_per_step
     pipe_roof = {"alg_MB_per_frame": round(pipe_bytes / 1e6, 2), "ms_per_frame": round(frame_wall_ms, 4),
                  "achieved_GBs": round(pipe_bytes / (frame_wall_ms * 1e-3) / 1e9, 2),
-                 "frac": round(pipe_bytes / (frame_wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-                 "definition": "SURVEY §8(d): %s per frame, each input read once and each output written once; "
-                               "over the whole job's wall time per frame" % ("10*S*B" if a.stages == "all" else "4*S*B")}
-    nfr_timed = a.steps * frames_per_step / max(n, 1)
+                 "frac": round(pipe_bytes / (frame_wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS / max(n if tiled else 1, 1), 5),
+                 "definition": "SURVEY §8(d): %s per frame, each input read once and each output written once; over the "
+                               "whole job's wall time per frame%s" % ("10*S*B" if a.stages == "all" else "4*S*B",
+                                                                      ", against N x 8 TB/s" if tiled else "")}
+    nfr_timed = a.steps * F
     xfer = {"h2d_bytes_per_frame": round(h2d / nfr_timed), "d2h_bytes_per_frame": round(d2h / nfr_timed),
-            "note": "host<->device bytes of the frame-level entry points during the timed steps (per-frame results: "
-                    "DLF trial SSEs, CDEF pick, LR search records and chosen units; inputs stay resident in HBM)"}
+            "mode_info_h2d_bytes_per_frame": mi_bytes if a.stages == "all" else 0,
+            "input_bytes_per_frame": in_bytes,
+            "input_upload_ms": round(up_s * 1e3, 3),
+            "input_upload_GBs": round(in_bytes / up_s / 1e9, 2),
+            "pcie_inclusive_Mpx_s": round(W * H / (frame_wall_ms * 1e-3 + up_s) / 1e6, 2) if n == 1 else None,
+            "note": "h2d/d2h: host<->device bytes of the frame-level entry points during the timed steps on this rank "
+                    "(the per-frame mode-info grid, DLF trial SSEs, CDEF pick, LR records and units); the frame inputs "
+                    "(recon + source, input_bytes_per_frame) are resident before timing -- an encoder uploads them "
+                    "per frame at input_upload_GBs (pageable host memory, measured here), giving "
+                    "pcie_inclusive_Mpx_s if the upload were serialized with the step (never `value`)"}
+    if tiled:
+        xfer["rccl_exchange_bytes_per_frame"] = {
+            "cdef_tables": st0.nfb * (2 * 64 * 8 + 64 + 64 * 4) + ((st0.nfb + 7) // 8) * 8,
+            "lr_records": sum(hu * vu for hu, vu in lr.units) * svtgpu.LR_UNIT_SEARCH_DTYPE.itemsize,
+            "dlf_trial_sses": "6 x 8 B per bisection step"}
     out = {
         "metric": "CDEF+restoration+SAD Mpixels/s on 4K10b",
         "value": round(value, 3),
@@ -667,25 +720,33 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if banded else "weak",
+        "scaling": "weak" if (n > 1 and not tiled) else "strong",
         "vs_baseline": None,
         "dtype": "u16" if bd > 8 else "u8",
         "data": "synthetic",
-        "config": {"workload": "dlf_pick+filter -> cdef_search+pick+apply -> lr_search+apply, + md batch; %dx%d %d-bit 4:2:0, dlf level 1 "
-                               "(full-image search), cdef_level %d (%d strengths); MD SAD/SSE/var 7 refs x 849 blocks/SB; "
-                               "LR search+apply (RU 256/128, wn/sg level 1)"
-                               % (W, H, bd, a.cdef_level, len(ctrls.strengths())),
+        "config": {"workload": "mode info -> dlf_pick+filter -> cdef_search+pick+apply -> lr_search+apply, + md batch; "
+                               "%dx%d %d-bit 4:2:0, dlf level 1 (full-image search), cdef_level %d (%d strengths); MD "
+                               "SAD/SSE/var 7 refs x 849 blocks/SB; LR search+apply (RU %d/%d, wn/sg level 1)"
+                               % (W, H, bd, a.cdef_level, len(ctrls.strengths()), lr_us[0], lr_us[1]),
+                   "inputs": ("the reference-pinned pipeline case %s (integer generator seed %#x, base_q_idx %d, start "
+                              "levels %s, CDEF lambda %d; tests/golden/pipe_%s.npz)" %
+                              (pin["case"], pin["seed"], q, cfg["lf"], lam, pin["case"])) if pin else
+                             "synthetic, unpinned (%s generator)" % ("integer" if a.inputs == "pinned" else "float"),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": frames_per_step,
                    "frames_in_flight": F, "frame_latency_ms": round(frame_ms, 4), "ranks_requested": a.gpus,
                    "ranks": n,
-                   "parallelism": ("row_bands%d (CDEF FB rows, LR unit rows, MD SBs; DLF replicated)" % n if banded
+                   "parallelism": ("tiles%dx%d (each frame tiled over the ranks: DLF trials/filter, CDEF search/apply, "
+                                   "LR search/apply per tile; RCCL sums of the DLF trial SSEs, CDEF tables, LR records "
+                                   "through libsvtgpu's communicator; MD by SB ranges)" % (gx, gy) if tiled
                                    else "frames%d (each rank filters its own pictures; no data-path collective)" % n
                                    if n > 1 else "single"),
+                   "tile": plan["tile"] if tiled else None,
                    "stage_ms": {"dlf_pick_filter": round(dlf_ms, 4), "cdef_search": round(search_ms, 4),
                                 "cdef_pick_apply": round(cdef_rest_ms, 4), "lr_search_apply": round(lr_ms, 4),
                                 "md_sad_sse_var": round(md_ms, 4),
-                                "note": "the MD batch runs on a second stream concurrently with the LR stage; the LR "
-                                        "search runs its Wiener and self-guided chains on two streams"},
+                                "note": "slot 0, rank 0, HIP events; dlf_pick_filter includes the mode-info upload and "
+                                        "edge records; the MD batch runs on a second stream concurrently with the LR "
+                                        "stage; the LR search runs its Wiener and self-guided chains on two streams"},
                    "lr_search_kernel_ms": {c: round(v["ms"], 4) for c, v in lr_cls.items()},
                    "dlf_levels": list(slots[0].lf_levels[-1]) if slots[0].lf_levels else None,
                    "stage_roofline": stage_roof, "pipeline_roofline": pipe_roof, "transfers": xfer},
@@ -705,12 +766,15 @@ def main():
         if a.cpu_kind == "reference" and os.path.exists(REF_BENCH):
             out["cpu_baseline"] = cpu_baseline_reference(s0.src, s0.rec, mi, ctrls, bd, a.cdef_level, q, lam,
                                                          a.cpu_grid, lr_ctrls, md_ref_y, s0.md_mvs, a.cpu_passes,
-                                                         a.stages)
+                                                         cfg["lf"], a.stages)
         else:
             out["cpu_baseline"] = cpu_baseline(s0.src, s0.rec, mi, lf_start, bd, a.cdef_level, q, lam, a.cpu_grid,
                                                lr_ctrls, lr_us, md_ref_y, s0.md_mvs)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    for sl in slots:
+        if sl.comm is not None:
+            sl.comm.close()
     if n > 1:
         dist.destroy_process_group()
 

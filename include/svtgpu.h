@@ -398,7 +398,8 @@ typedef struct SvtGpuLfParams {
 typedef struct SvtGpuDlfState SvtGpuDlfState;
 int  svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuDlfState **out);
 void svtgpu_dlf_state_destroy(SvtGpuDlfState *s);
-/* upload the mi grid ((h+7)/8*2 rows x (w+7)/8*2 cols records) */
+/* upload the mi grid ((h+7)/8*2 rows x (w+7)/8*2 cols records): asynchronous on `stream` through pinned staging,
+ * the caller may reuse its buffer on return (one grid per frame) */
 int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream);
 /* ≙ svt_av1_loop_filter_frame(frame, pcs, plane_start, plane_end) (EbDeblockingFilter.c:624-653):
  * all vertical edges of each plane, then all horizontal edges (equivalent to the reference's

@@ -134,7 +134,7 @@ static void bind_kernels(void) {
 
 /* ------------------------------------------------------------------------------------------- input */
 enum { H_W, H_H, H_BD, H_NREF, H_Q, H_LAMBDA, H_GX, H_GY, H_RDMULT, H_SW0, H_SW1, H_SW2, H_WN0, H_WN1, H_SG0, H_SG1,
-       H_N };
+       H_LF0, H_LF1, H_LFU, H_LFV, H_N };
 static int32_t            hdr[H_N];
 static SvtGpuCdefControls cctl;
 static uint16_t          *g_src[3], *g_rec[3], **g_ref;
@@ -328,7 +328,7 @@ static void run_crop(const Crop *c, int32_t *tmpbuf) {
     pic.buffer_y = (uint8_t *)rec[0], pic.buffer_cb = (uint8_t *)rec[1], pic.buffer_cr = (uint8_t *)rec[2];
     trial.buffer_y = (uint8_t *)trl[0], trial.buffer_cb = (uint8_t *)trl[1], trial.buffer_cr = (uint8_t *)trl[2];
     svt_av1_loop_filter_init(pcs);
-    const int last[4] = {32, 32, 16, 16}; /* bench.py's previous-frame levels */
+    const int last[4] = {hdr[H_LF0], hdr[H_LF1], hdr[H_LFU], hdr[H_LFV]}; /* the previous frame's levels */
     struct LoopFilter *lf = &fh->loop_filter_params;
     if (g_stages & 1) {
         lf->filter_level[0] = lf->filter_level[1] = dlf_search(pcs, &trial, rec, src, last, 0, 2, W, H);

@@ -396,6 +396,8 @@ struct SvtGpuDlfState {
     // out_rect (luma {x0, y0, x1, y1}; the whole frame by default)
     int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
     SvtGpuComm    *comm = nullptr;
+    SvtGpuLfMi    *h_mi = nullptr;      // pinned staging of the mode info (one upload per frame, asynchronous)
+    hipEvent_t     mi_free = nullptr;   // the previous upload has read h_mi
 };
 
 namespace {
@@ -686,6 +688,8 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
 extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     if (!s) return;
     (void)hipFree(s->d_mi);
+    if (s->h_mi) (void)hipHostFree(s->h_mi);
+    if (s->mi_free) (void)hipEventDestroy(s->mi_free);
     if (s->hi_ev) (void)hipEventDestroy(s->hi_ev);
     if (s->hi_stream) (void)hipStreamDestroy(s->hi_stream);
     for (int c = 0; c < 2; c++)
@@ -707,7 +711,17 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
             return SVTGPU_ERR_INVALID_ARG;
     }
     hipStream_t st = pick_stream(s->ctx, stream);
-    HIP_TRY(hipMemcpyAsync(s->d_mi, mi, n * sizeof(SvtGpuLfMi), hipMemcpyHostToDevice, st));
+    // the caller's grid goes through pinned staging, so the upload is asynchronous and the caller may reuse its
+    // buffer at once (an encoder hands over a new grid every frame)
+    if (!s->h_mi) {
+        HIP_TRY(hipHostMalloc((void **)&s->h_mi, n * sizeof(SvtGpuLfMi), hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&s->mi_free, hipEventDisableTiming));
+    } else {
+        HIP_TRY(hipEventSynchronize(s->mi_free)); // the previous frame's upload has read the staging
+    }
+    std::memcpy(s->h_mi, mi, n * sizeof(SvtGpuLfMi));
+    HIP_TRY(hipMemcpyAsync(s->d_mi, s->h_mi, n * sizeof(SvtGpuLfMi), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipEventRecord(s->mi_free, st));
     svtgpu_count_xfer(0, n * sizeof(SvtGpuLfMi));
     for (int c = 0; c < 2; c++)
         for (int d = 0; d < 2; d++) {
@@ -715,7 +729,6 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
                                s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->d_rec[c][d]);
             HIP_TRY(hipGetLastError());
         }
-    HIP_TRY(hipStreamSynchronize(st)); // the caller's mi buffer may be reused after return
     s->have_mi = 1;
     return SVTGPU_OK;
 }

@@ -49,6 +49,54 @@ def frame_pair(width, height, bit_depth, seed):
     return src, rec
 
 
+# ---------------------------------------------------------------------------------------------
+# integer-only generator (bit-identical on every host): the inputs of the reference-pinned pipeline cases
+# (tests/pipeline_cases.py; tests/golden/pipe_*.npz hold the reference's outputs on them) and of bench.py
+# ---------------------------------------------------------------------------------------------
+def _plane_int(rng, h, w, bd):
+    """Gradient + oriented triangle-wave texture per 64x64 block + uniform noise, integers only."""
+    maxv = (1 << bd) - 1
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.int64)
+    base = maxv // 4 + (xx * (maxv // 3)) // max(w, 1) + (yy * (maxv // 5)) // max(h, 1)
+    nbh, nbw = (h + 63) // 64, (w + 63) // 64
+    dirs = np.array([(1, 0), (0, 1), (1, 1), (1, -1), (2, 1), (1, 2), (2, -1), (1, -2)], np.int64)
+    d = dirs[rng.integers(0, 8, size=(nbh, nbw))]
+    period = rng.integers(3, 13, size=(nbh, nbw)).astype(np.int64)
+    amp = rng.integers(maxv // 60 + 1, maxv // 8 + 2, size=(nbh, nbw)).astype(np.int64)
+
+    def up(a):
+        return np.repeat(np.repeat(a, 64, 0), 64, 1)[:h, :w]
+
+    dx, dy, P, A = up(d[..., 0]), up(d[..., 1]), up(period), up(amp)
+    t = np.mod(xx * dx + yy * dy, 2 * P)
+    tex = A * (np.abs(t - P) * 2 - P) // P
+    k = 3 << (bd - 8)
+    noise = rng.integers(-k, k + 1, size=(h, w))
+    return np.clip(base + tex + noise, 0, maxv)
+
+
+def _coded_int(rng, src, bd):
+    h, w = src.shape
+    maxv = (1 << bd) - 1
+    q = 6 << (bd - 8)
+    dc = rng.integers(-q // 2, q // 2 + 1, size=((h + 7) // 8, (w + 7) // 8))
+    ring = rng.integers(-q, q + 1, size=(h, w))
+    return np.clip(src + np.repeat(np.repeat(dc, 8, 0), 8, 1)[:h, :w] + ring, 0, maxv)
+
+
+def frame_pair_int(width, height, bit_depth, seed):
+    """(source_planes, recon_planes) from the integer generator (PCG64 integer draws, integer arithmetic)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dt = np.uint16 if bit_depth > 8 else np.uint8
+    src, rec = [], []
+    for p in range(3):
+        ph, pw = (height, width) if p == 0 else (height // 2, width // 2)
+        s = _plane_int(rng, ph, pw, bit_depth)
+        src.append(s.astype(dt))
+        rec.append(_coded_int(rng, s, bit_depth).astype(dt))
+    return src, rec
+
+
 def block_mask(width, height, seed, p_skip=0.0):
     """Per-8x8 'filter this block' mask (1 = listed); p_skip = probability a block is skipped."""
     rng = np.random.Generator(np.random.PCG64(seed ^ 0xB10C))

@@ -71,47 +71,10 @@ CASES = {
 SMALL = [k for k, c in CASES.items() if not c["digest"]]
 
 
-def _plane(rng, h, w, bd):
-    """Gradient + oriented triangle-wave texture per 64x64 block + uniform noise, integers only."""
-    maxv = (1 << bd) - 1
-    yy, xx = np.mgrid[0:h, 0:w].astype(np.int64)
-    base = maxv // 4 + (xx * (maxv // 3)) // max(w, 1) + (yy * (maxv // 5)) // max(h, 1)
-    nbh, nbw = (h + 63) // 64, (w + 63) // 64
-    dirs = np.array([(1, 0), (0, 1), (1, 1), (1, -1), (2, 1), (1, 2), (2, -1), (1, -2)], np.int64)
-    d = dirs[rng.integers(0, 8, size=(nbh, nbw))]
-    period = rng.integers(3, 13, size=(nbh, nbw)).astype(np.int64)
-    amp = rng.integers(maxv // 60 + 1, maxv // 8 + 2, size=(nbh, nbw)).astype(np.int64)
-
-    def up(a):
-        return np.repeat(np.repeat(a, 64, 0), 64, 1)[:h, :w]
-
-    dx, dy, P, A = up(d[..., 0]), up(d[..., 1]), up(period), up(amp)
-    t = np.mod(xx * dx + yy * dy, 2 * P)
-    tex = A * (np.abs(t - P) * 2 - P) // P
-    k = 3 << (bd - 8)
-    noise = rng.integers(-k, k + 1, size=(h, w))
-    return np.clip(base + tex + noise, 0, maxv)
-
-
-def _coded(rng, src, bd):
-    h, w = src.shape
-    maxv = (1 << bd) - 1
-    q = 6 << (bd - 8)
-    dc = rng.integers(-q // 2, q // 2 + 1, size=((h + 7) // 8, (w + 7) // 8))
-    ring = rng.integers(-q, q + 1, size=(h, w))
-    return np.clip(src + np.repeat(np.repeat(dc, 8, 0), 8, 1)[:h, :w] + ring, 0, maxv)
-
-
 def frame_pair(w, h, bd, seed):
-    rng = np.random.Generator(np.random.PCG64(seed))
-    dt = np.uint16 if bd > 8 else np.uint8
-    src, rec = [], []
-    for p in range(3):
-        ph, pw = (h, w) if p == 0 else (h // 2, w // 2)
-        s = _plane(rng, ph, pw, bd)
-        src.append(s.astype(dt))
-        rec.append(_coded(rng, s, bd).astype(dt))
-    return src, rec
+    """The integer-only generator (synth.frame_pair_int, shared with bench.py)."""
+    import synth
+    return synth.frame_pair_int(w, h, bd, seed)
 
 
 def mode_info(c):
