@@ -33,7 +33,7 @@ def test_ref_bench_agrees_with_oracle_on_a_crop():
     nsb = (W // 64) * (H // 64)
     mvs = np.random.default_rng(5).integers(-16, 17, size=(nsb, 2, 2))
     with tempfile.NamedTemporaryFile(suffix=".bin") as f:
-        bench.write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, "2x1", lr_ctrls, refs, mvs)
+        bench.write_ref_bench_input(f, src, rec, mi, ctrls, bd, q, lam, "2x1", lr_ctrls, refs, mvs, (16, 16, 8, 8))
         f.flush()
         res = subprocess.run([REF_BENCH, f.name, "2"], capture_output=True, text=True, timeout=300,
                              env=dict(os.environ, REF_BENCH_VERBOSE="1"))
@@ -47,7 +47,7 @@ def test_ref_bench_agrees_with_oracle_on_a_crop():
     mi_c = np.ascontiguousarray(mi[:ch // 4, :cw // 4])
     crop = [np.ascontiguousarray(rec[0][:ch, :cw])] + [np.ascontiguousarray(p[:ch // 2, :cw // 2]) for p in rec[1:]]
     cs = [np.ascontiguousarray(src[0][:ch, :cw])] + [np.ascontiguousarray(p[:ch // 2, :cw // 2]) for p in src[1:]]
-    lfp = oracle.dlf_pick(crop, cs, bd, mi_c, svtgpu.LfParams.make(32, 32, 16, 16), 0, 0, 0, 0, 0)
+    lfp = oracle.dlf_pick(crop, cs, bd, mi_c, svtgpu.LfParams.make(16, 16, 8, 8), 0, 0, 0, 0, 0)
     assert ref_lv == [lfp.filter_level[0], lfp.filter_level[1], lfp.filter_level_u, lfp.filter_level_v]
     crop = oracle.dlf_frame(crop, bd, mi_c, lfp)
     oc = oracle.controls(1)
