@@ -158,8 +158,6 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_pick) (void)hipHostFree(s->h_pick);
-    if (s->hi_ev) (void)hipEventDestroy(s->hi_ev);
-    if (s->hi_stream) (void)hipStreamDestroy(s->hi_stream);
     delete s;
 }
 
@@ -324,12 +322,7 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
         if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
         return SVTGPU_OK;
     }
-    // The pick is a chain of ~40 short dependent launches: with other pictures' long kernels on the device each of
-    // them waits for free CU slots, so it runs on a highest-priority stream (the dispatcher hands it the next free
-    // slots); it ends with a host wait, so the caller's later work is ordered after it
-    hipStream_t ps = st;
-    if (int rc = svtgpu_priority_stream(&s->hi_stream, &s->hi_ev, st, &ps)) return rc;
-    if (int rc = svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, ps))
+    if (int rc = svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, st))
         return rc;
     if (s->d_fb_kind) { // the halves of 128-wide areas take the area's index (EbEncCdef.c:893-909)
         if (int rc = svtgpu_launch_cdef_sb128_dup(s, st)) return rc;

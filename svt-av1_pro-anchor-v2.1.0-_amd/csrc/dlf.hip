@@ -390,8 +390,6 @@ struct SvtGpuDlfState {
     unsigned long long *h_sse_dev; // its device address
     unsigned long long  seq;       // last trial launch's sequence number
     int32_t        have_mi;
-    hipStream_t    hi_stream = nullptr; // highest-priority stream of the level search's trial launches (lazy)
-    hipEvent_t     hi_ev     = nullptr;
     // frame tiling over GPUs (svtgpu_dlf_set_tile): trial SSEs over sse_rect, summed over `comm`; the apply writes
     // out_rect (luma {x0, y0, x1, y1}; the whole frame by default)
     int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
@@ -690,8 +688,6 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     (void)hipFree(s->d_mi);
     if (s->h_mi) (void)hipHostFree(s->h_mi);
     if (s->mi_free) (void)hipEventDestroy(s->mi_free);
-    if (s->hi_ev) (void)hipEventDestroy(s->hi_ev);
-    if (s->hi_stream) (void)hipStreamDestroy(s->hi_stream);
     for (int c = 0; c < 2; c++)
         for (int d = 0; d < 2; d++) (void)hipFree(s->d_rec[c][d]);
     (void)hipFree(s->d_scratch);
@@ -830,11 +826,7 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
-    // the bisection's dependent trial launches (each followed by a host wait) on a highest-priority stream ordered
-    // after the caller's (svtgpu_priority_stream); every trial result has been waited for when the search returns
-    hipStream_t ts = st;
-    if ((rc = svtgpu_priority_stream(&s->hi_stream, &s->hi_ev, st, &ts))) return rc;
-    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, ts))) return rc;
+    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st))) return rc;
     p.filter_level[0] = p.filter_level[1] = ys.best;
     p.filter_level_u = search_uv ? us.best : last[2];
     p.filter_level_v = search_uv ? vs.best : last[3];

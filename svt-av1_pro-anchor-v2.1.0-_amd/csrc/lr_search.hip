@@ -10,22 +10,20 @@
 //   wiener_stats_kernel   the 7x7 (5x5, 3x3) Wiener statistics M, H of svt_av1_compute_stats: a lane group per
 //                         window-column pair accumulates its 7x7 block with v_dot2_i32_i16 over horizontal pixel
 //                         pairs (diagonal groups also form M); per-tile partials are reduced per unit
-//   sgr_flt_kernel        box sums of a tile once, then for every searched ep the A/B maps, both self-guided
-//                         filters (kept in HBM as int16) and the 2x2 projection moments in exact int64
-//   wiener_unit_kernel    (default) the whole Wiener descent of finer_tile_search_wiener_seg per unit inside one
-//                         workgroup: candidate SSE over the unit's tiles, descent step in LDS, no global sync
-//   sgr_queue_kernel      (opt-in, SVTGPU_SG_QUEUE=1) the self-guided descents of finer_search_pixel_proj_error as a persistent
-//                         work queue: a worker evaluates a unit tile's pending candidate trees, the worker completing
-//                         the unit's pass steps its descents and re-publishes its tiles
+//   sgr_flt_kernel        box sums of a tile once, then for every searched ep the A/B maps and both self-guided
+//                         filters (kept in HBM as int16); sgr_mom_kernel forms the 2x2 projection moments from them
+//   wiener_solve_kernel   the int64 fixed-point Wiener decomposition and score per unit (the descent's seed)
+//   wiener_res_kernel     the whole Wiener descent of finer_tile_search_wiener_seg per unit with the unit resident on
+//                         the CU: CDEF window in LDS, source in registers, a rolling horizontal pass per lane; units
+//                         too large for one CU are cut into row parts whose SSEs meet each candidate
+//   sgr_seed_kernel       the 2x2 projection solve (double, as the reference) per (unit, ep)
 //   proj_err_kernel + sgr_advance_kernel
-//                         (default) the self-guided descents as per-round launches with a host-polled batch loop
-//   wiener_queue_kernel, wiener_trial_kernel + wiener_advance_kernel
-//                         the Wiener alternatives kept for A/B (SVTGPU_WN_UNIT=0, SVTGPU_WN_QUEUE=0)
+//                         the self-guided descents of finer_search_pixel_proj_error as per-round launches (a speculative
+//                         7-node outcome tree per descent and round) with a host-polled batch loop
 //   sgr_best_kernel, sgr_sse_kernel
 //                         best ep per unit (strict <) and the SSE of its clipped output
-// The host does what is sequential in the reference and cheap: the int64 fixed-point Wiener decomposition, the
-// 2x2 projection solve in double, and the RD pass over the units.  A frame costs four host synchronisations plus
-// one per batch of descent rounds.
+// The host does what is sequential in the reference and cheap: the RD pass over the units (rest_finish_search).  A
+// frame costs a host wait per batch of self-guided rounds plus the final read-back.
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -387,167 +385,6 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 // pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
 // ---------------------------------------------------------------------------------------------
 __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16); }
-
-template <typename T>
-__device__ inline uint2 load_group(const T *d, int stride, int W, int H, int yy, int xx) {
-    int q[4];
-    if (yy >= 0 && yy < H && xx >= 0 && xx + 4 <= W) {
-        load4(d + (size_t)yy * stride + xx, q);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; j++) q[j] = px(d, stride, W, H, yy, xx + j);
-    }
-    return make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
-}
-
-// one tile's inputs in flight: record index, mode, and this lane's share of the pixels
-struct TrialFetch {
-    int   ti, mode;
-    uint2 dg[5];  // CDEF pixel groups (modes 1, 3): 71 rows x 18 groups over 256 lanes
-    uint4 tcv[3]; // cached horizontal pass (mode 2): 36 x 64 u32 over 256 lanes
-    uint2 sg[4];  // source groups: 64 rows x 16 groups
-};
-
-template <typename T>
-__device__ inline void trial_fetch(const SearchArgs &A, const int32_t *wact, const uint32_t *tcache, int ti,
-                                   TrialFetch &f) {
-    const Tile       t = A.tiles[ti];
-    const PlaneArgs &P = A.pl[t.plane];
-    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    f.ti   = ti;
-    f.mode = wact[t.unit];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int i = threadIdx.x + k * 256, r = i >> 4, g = i & 15;
-        if (r < t.h && 4 * g < t.w) {
-            int q[4];
-            load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g, q);
-            f.sg[k] = make_uint2(pack2(q[0], q[1]), pack2(q[2], q[3]));
-        }
-    }
-    if (f.mode == 2) {
-        const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int i = threadIdx.x + k * 256;
-            if (i < 36 * 64 / 4) f.tcv[k] = tc[i];
-        }
-    } else {
-        const int rows = t.h + 7, ng = (t.w + 8) >> 2;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
-            if (i < 71 * 18 && r < rows && g < ng) f.dg[k] = load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * g);
-        }
-    }
-}
-
-// wact[unit]: 0 no pending candidate; 1 full evaluation; a vertical-filter move (the candidate's hfilter is the
-// unit's current one): 2 the horizontal pass of that hfilter is cached per tile (tcache) -- only the vertical pass
-// runs; 3 not cached yet -- full evaluation that also stores its horizontal pass.
-template <typename T>
-__global__ __launch_bounds__(256) void wiener_trial_kernel(const SearchArgs A, const int16_t *taps,
-                                                                const int32_t *wact, const int32_t *items,
-                                                                const int32_t *cnt_cur, int32_t *cnt_next,
-                                                                unsigned long long *err, unsigned long long *pc,
-                                                                unsigned long long *tk, uint32_t *tcache) {
-    PROF_BEGIN(tk);
-    constexpr int VS = 72;
-    __shared__ __align__(16) uint16_t v[71 * VS];
-    __shared__ __align__(16) uint32_t tq[36 * 64]; // tq[r/2][x] = (tmp[r][x], tmp[r+1][x]), r even
-    __shared__ __align__(16) uint16_t sv[64 * 64]; // the source tile
-    // the next advance lists its tiles and counts its live descents there
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
-    const int n  = cnt_cur[0];
-    const int lb = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int i0 = (int)((long long)n * lb / gridDim.x), i1 = (int)((long long)n * (lb + 1) / gridDim.x);
-    unsigned long long npx = 0;
-    TrialFetch f;
-    if (i0 < i1) trial_fetch<T>(A, wact, tcache, items[i0], f);
-    for (int it = i0; it < i1; it++) {
-        const int        ti = f.ti, mode = f.mode;
-        const Tile       t  = A.tiles[ti];
-        const PlaneArgs &P  = A.pl[t.plane];
-        // stage the fetched tile
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int i = threadIdx.x + k * 256, r = i >> 4, g = i & 15;
-            if (r < t.h && 4 * g < t.w) *(uint2 *)(sv + r * 64 + 4 * g) = f.sg[k];
-        }
-        if (mode == 2) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const int i = threadIdx.x + k * 256;
-                if (i < 36 * 64 / 4) ((uint4 *)tq)[i] = f.tcv[k];
-            }
-        } else {
-            const int rows = t.h + 7, ng = (t.w + 8) >> 2;
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                const int i = threadIdx.x + k * 256, r = i / 18, g = i - r * 18;
-                if (i < 71 * 18 && r < rows && g < ng) *(uint2 *)(v + r * VS + 4 * g) = f.dg[k];
-            }
-        }
-        __syncthreads();
-        if (it + 1 < i1) trial_fetch<T>(A, wact, tcache, items[it + 1], f); // in flight during the passes
-        const int16_t *tp = taps + t.unit * 16;
-        int            h[8], w[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) h[k] = tp[k], w[k] = tp[8 + k];
-        // pair weights: even output x (pairs at x, x+2, ...) and odd output x+1; the same for rows
-        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
-        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
-        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
-        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
-        const int      rows = t.h + 7, nyp = (t.h + 1) >> 1;
-        const WienerRound rr = wiener_round(P.bd);
-        if (mode != 2) {
-            const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
-            uint16_t *tq16 = (uint16_t *)tq;
-            const int xh   = 2 * (threadIdx.x & 31);
-            if (xh < t.w)
-                for (int r = threadIdx.x >> 5; r < rows; r += 8) {
-                    const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
-                    const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
-                    const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
-                    const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
-                    const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
-                    tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
-                    tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
-                }
-            __syncthreads();
-            if (mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
-                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
-                for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
-            }
-        }
-        uint32_t  e    = 0; // <= 32 outputs per lane: fits 32 bits
-        const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
-        const int x    = threadIdx.x & 63;
-        if (x < t.w)
-            for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
-                const int       y  = 2 * yp;
-                const uint32_t *c  = tq + yp * 64 + x;
-                const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
-                const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
-                const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
-                const uint16_t *sp = sv + y * 64 + x;
-                const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
-                e += (uint32_t)(d0 * d0);
-                if (y + 1 < t.h) {
-                    const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[64];
-                    e += (uint32_t)(d1 * d1);
-                }
-            }
-        const unsigned long long et = wave_sum_u32_wide(e);
-        if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[t.unit], et);
-        npx += (unsigned long long)(t.w * t.h);
-        __syncthreads(); // the next tile overwrites the LDS images
-    }
-    if (pc && threadIdx.x == 0 && npx) // profiling: evaluated pixels (spread over PROF_SP counters)
-        atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
-    PROF_END(tk);
-}
 
 // ---------------------------------------------------------------------------------------------
 // self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
@@ -1299,7 +1136,6 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 // candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
 // the other one, the advance kernel fills it).
 // ---------------------------------------------------------------------------------------------
-__device__ inline int32_t htag(const Descent &d) { return (int32_t)(d.vals & 0xFFFFFF); } // hfilter taps 0..2
 
 // Words written by other workgroups of a work-queue kernel are read with agent-scope atomic loads, which miss in the
 // CU's vector L1: a plain load may return a line that this CU cached in an earlier pass (SHARED = false: plain loads,
@@ -1319,387 +1155,6 @@ __device__ inline Descent load_descent(const Descent *p) {
         for (int k = 0; k < (int)(sizeof(Descent) / 8); k++) ((uint64_t *)&d)[k] = ld64<true>((const uint64_t *)p + k);
         return d;
     }
-}
-
-// returns 1 when the unit has a pending candidate (its tiles go on the next trial's list)
-template <bool SHARED = false>
-__device__ int wiener_advance_one(Descent *ds, int u, unsigned long long *err, int16_t *taps, int32_t *wact,
-                                  int32_t *ctag, int first) {
-    Descent d = load_descent<SHARED>(ds + u);
-    if (d.done) return 0;
-    // a mode-3 trial stored the horizontal pass of the candidate's hfilter (a vertical move leaves it unchanged)
-    if (!first && ld_shared<SHARED>(wact + u) == 3) ctag[u] = htag(d);
-    if (!first) d.report((int64_t)ld64<SHARED>(err + u));
-    err[u]  = 0;
-    wact[u] = 0;
-    if (d.next()) {
-        int v[3];
-        d.taps(0, v), set_wiener_taps(taps + 16 * u, v); // f = 0: hfilter, f = 1: vfilter
-        d.taps(1, v), set_wiener_taps(taps + 16 * u + 8, v);
-        wact[u] = (d.init || d.mf != 1) ? 1 : (ld_shared<SHARED>(ctag + u) == htag(d) ? 2 : 3);
-        ds[u]   = d;
-        return 1;
-    }
-    ds[u] = d;
-    return 0;
-}
-
-__global__ __launch_bounds__(256) void wiener_advance_kernel(Descent *ds, int n, unsigned long long *err,
-                                                             int16_t *taps, int32_t *wact, int32_t *ctag,
-                                                             const int32_t *tile0, int32_t *items, int32_t *cnt,
-                                                             int first, unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    const int u    = blockIdx.x * blockDim.x + threadIdx.x;
-    const int live = u < n ? wiener_advance_one(ds, u, err, taps, wact, ctag, first) : 0;
-    wave_count(&cnt[1], live);
-    // list the unit's tiles for the next trial (Wiener units are the first units: global index u)
-    const int t0 = live ? tile0[u] : 0, nt = live ? tile0[u + 1] - t0 : 0, pos = wave_alloc(&cnt[0], nt);
-    for (int k = 0; k < nt; k++) items[pos + k] = t0 + k;
-    PROF_END(tk);
-}
-
-// ---------------------------------------------------------------------------------------------
-// The Wiener descents as one persistent work-queue kernel.  A work item is one tile of a unit whose descent has a
-// pending candidate; workers (persistent workgroups) claim items in order from an append-only log, evaluate the
-// tile's SSE for the unit's candidate and count the unit's arrivals; the workgroup that completes a unit's round
-// runs the descent step (Descent::report / next, exactly as wiener_advance_one) and appends the unit's tiles for
-// its next candidate.  No workgroup ever waits for a specific other one -- an idle worker polls the log until an
-// item appears or no descent is live -- so the kernel needs no co-residency and drains when the last descent ends.
-// Rounds of different units interleave freely: no launch boundary, no host poll, no per-round advance kernel.
-// ---------------------------------------------------------------------------------------------
-struct WnQueue {
-    int32_t head;   // next log index to claim
-    int32_t alloc;  // log entries reserved by producers
-    int32_t live;   // descents not done
-    int32_t error;  // log overflow: the search is abandoned (SVTGPU_ERR_HIP)
-};
-
-// Every word the workers share lives in uncached device memory (hipDeviceMallocUncached): reads and writes go
-// to memory, so no cache flush or invalidate is ever needed (an agent-scope fence writes back and invalidates the
-// whole L2 of the XCD -- per tile, that stalls every kernel on the device).  Ordering is by completion: a
-// producer waits for its stores to be acknowledged before it publishes, a consumer issues its reads after the
-// publishing word has arrived.
-__device__ inline void wait_mem() {
-    __builtin_amdgcn_s_waitcnt(0); // vmcnt (loads and stores on gfx9), expcnt, lgkmcnt
-    asm volatile("" ::: "memory");
-}
-__device__ inline int q_load(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// append the tiles of unit u to the log (every lane of the workgroup calls this; lane 0 reserves)
-__device__ inline void q_append(WnQueue *q, int32_t *log, int cap, const int32_t *tile0, int u, int *s_pos) {
-    const int t0 = tile0[u], nt = tile0[u + 1] - t0;
-    if (threadIdx.x == 0) {
-        const int pos = atomicAdd(&q->alloc, nt);
-        if (pos + nt > cap) {
-            atomicExch(&q->error, 1);
-            atomicExch(&q->live, 0); // stop every worker; the host reports the failure
-        }
-        *s_pos = pos;
-    }
-    __syncthreads();
-    const int pos = *s_pos;
-    if (pos + nt <= cap)
-        for (int k = threadIdx.x; k < nt; k += blockDim.x)
-            __hip_atomic_store(log + pos + k, t0 + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-}
-
-// first descent step of every unit (the solve's seed is the first candidate) and the initial log
-__global__ __launch_bounds__(256) void wiener_queue_start_kernel(const Descent *ds_in, Descent *ds, int n,
-                                                                 unsigned long long *err, int16_t *taps,
-                                                                 int32_t *wact, int32_t *ctag, int32_t *arr,
-                                                                 const int32_t *tile0, WnQueue *q, int32_t *log,
-                                                                 int cap) {
-    __shared__ int s_pos;
-    const int u = blockIdx.x; // one workgroup per unit: the append uses the whole group
-    __shared__ int s_live;
-    if (threadIdx.x == 0) {
-        arr[u] = 0, err[u] = 0, ctag[u] = -1;
-        ds[u]  = ds_in[u];
-        s_live = wiener_advance_one<true>(ds, u, err, taps, wact, ctag, 1);
-        if (s_live) atomicAdd(&q->live, 1);
-        wait_mem();
-    }
-    __syncthreads();
-    if (s_live) q_append(q, log, cap, tile0, u, &s_pos);
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void wiener_queue_kernel(const SearchArgs A, Descent *ds, int16_t *taps,
-                                                           int32_t *wact, int32_t *ctag, int32_t *arr,
-                                                           unsigned long long *err, const int32_t *tile0,
-                                                           uint32_t *tcache, WnQueue *q, int32_t *log, int cap,
-                                                           unsigned long long *pc, unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    constexpr int VS = 72;
-    __shared__ __align__(16) uint16_t v[71 * VS];
-    __shared__ __align__(16) uint32_t tq[36 * 64];
-    __shared__ __align__(16) uint16_t sv[64 * 64];
-    __shared__ int s_item, s_last, s_pos;
-    unsigned long long npx = 0;
-    for (;;) {
-        // ---- claim the next log entry and wait until it is published (or nothing is live any more) ----
-        if (threadIdx.x == 0) {
-            const int idx = atomicAdd(&q->head, 1);
-            int       it  = 0;
-            for (unsigned spin = 0;; spin++) {
-                if (idx < cap) it = q_load(log + idx);
-                if (it || idx >= cap) break;
-                if (q_load(&q->live) == 0) break; // every descent ended: no entry will be published any more
-                if (spin > (1u << 25)) {          // a bound every worker reaches (~seconds): never spin forever
-                    atomicExch(&q->error, 2);
-                    atomicExch(&q->live, 0);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            s_item = it - 1;
-            wait_mem();
-        }
-        __syncthreads();
-        const int ti = s_item;
-        if (ti < 0) break;
-        const Tile       t = A.tiles[ti];
-        const PlaneArgs &P = A.pl[t.plane];
-        const int        u = t.unit, mode = __hip_atomic_load(wact + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const T         *d = (const T *)P.dgd, *src = (const T *)P.src;
-        // ---- stage: source tile, and the bordered CDEF tile or the cached horizontal pass ----
-        for (int i = threadIdx.x; i < 64 * 16; i += 256) {
-            const int r = i >> 4, g = i & 15;
-            if (r < t.h && 4 * g < t.w) {
-                int qv[4];
-                load4(src + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g, qv);
-                *(uint2 *)(sv + r * 64 + 4 * g) = make_uint2(pack2(qv[0], qv[1]), pack2(qv[2], qv[3]));
-            }
-        }
-        if (mode == 2) { // another workgroup may have stored this pass: loads that miss in this CU's L1
-            const uint64_t *tc = (const uint64_t *)(tcache + (size_t)ti * 36 * 64);
-            for (int i = threadIdx.x; i < 36 * 64 / 2; i += 256) ((uint64_t *)tq)[i] = ld64<true>(tc + i);
-        } else {
-            const int rows = t.h + 7, ng = (t.w + 8) >> 2;
-            for (int i = threadIdx.x; i < 71 * 18; i += 256) {
-                const int r = i / 18, g = i - r * 18;
-                if (r < rows && g < ng)
-                    *(uint2 *)(v + r * VS + 4 * g) = load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * g);
-            }
-        }
-        __syncthreads();
-        // ---- the candidate's SSE over the tile (the passes of wiener_trial_kernel) ----
-        const int16_t *tp = taps + u * 16;
-        int            h[8], w[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            h[k] = __hip_atomic_load(tp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-            w[k] = __hip_atomic_load(tp + 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
-        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
-        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
-        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
-        const int      rows = t.h + 7, nyp = (t.h + 1) >> 1;
-        const WienerRound rr = wiener_round(P.bd);
-        if (mode != 2) {
-            const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
-            uint16_t *tq16 = (uint16_t *)tq;
-            const int xh   = 2 * (threadIdx.x & 31);
-            if (xh < t.w)
-                for (int r = threadIdx.x >> 5; r < rows; r += 8) {
-                    const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
-                    const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
-                    const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
-                    const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
-                    const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
-                    tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
-                    tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
-                }
-            __syncthreads();
-            if (mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
-                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
-                for (int i = threadIdx.x; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
-            }
-        }
-        uint32_t  e    = 0;
-        const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
-        const int x    = threadIdx.x & 63;
-        if (x < t.w)
-            for (int yp = threadIdx.x >> 6; yp < nyp; yp += 4) {
-                const int       y  = 2 * yp;
-                const uint32_t *c  = tq + yp * 64 + x;
-                const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
-                const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
-                const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
-                const uint16_t *sp = sv + y * 64 + x;
-                const int d0 = min(max(s0 >> rr.r1, 0), maxv) - (int)sp[0];
-                e += (uint32_t)(d0 * d0);
-                if (y + 1 < t.h) {
-                    const int d1 = min(max(s1 >> rr.r1, 0), maxv) - (int)sp[64];
-                    e += (uint32_t)(d1 * d1);
-                }
-            }
-        const unsigned long long et = wave_sum_u32_wide(e);
-        if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[u], et);
-        npx += (unsigned long long)(t.w * t.h);
-        wait_mem();      // this wave's SSE add and tile-cache stores are acknowledged
-        __syncthreads(); // ... by every wave, before the arrival
-        // ---- arrival; the workgroup completing the unit's round runs its descent step ----
-        if (threadIdx.x == 0) {
-            const int nt = tile0[u + 1] - tile0[u];
-            const int a  = atomicAdd(&arr[u], 1); // after every wave's stores completed (wait_mem, barrier)
-            s_last       = a == nt - 1;
-            if (s_last) {
-                arr[u] = 0;
-                const int live = wiener_advance_one<true>(ds, u, err, taps, wact, ctag, 0);
-                wait_mem(); // the new candidate is in memory before its tiles are published
-                if (!live) atomicSub(&q->live, 1);
-                s_last = live;
-            }
-        }
-        __syncthreads();
-        if (s_last) q_append(q, log, cap, tile0, u, &s_pos);
-    }
-    if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
-    PROF_END(tk);
-}
-
-// ---------------------------------------------------------------------------------------------
-// The Wiener descent of one unit per workgroup (finer_tile_search_wiener_seg, EbRestorationPick.c:1042-1146, run to
-// its end without leaving the CU): NG groups of 256 lanes take the unit's <= 64x64 tiles NG at a time, each group
-// filters its tile with the candidate (the passes of wiener_queue_kernel) into a per-lane SSE; the workgroup reduces
-// the unit's SSE and lane 0 takes the descent step (Descent::report / next) for the next candidate.  The descent
-// state and taps live in LDS; nothing is shared with another workgroup, so a round costs three workgroup barriers
-// per NG tiles instead of global arrivals, polling and uncached memory.  The horizontal pass of the current hfilter
-// is cached per tile in ordinary global memory (written and read by this workgroup only, ordered by its barriers),
-// so vertical-filter moves run only the vertical pass.
-// ---------------------------------------------------------------------------------------------
-template <typename T, int NG>
-__global__ __launch_bounds__(256 * NG) void wiener_unit_kernel(const SearchArgs A, Descent *ds, const int32_t *tile0,
-                                                               uint32_t *tcache, unsigned long long *pc,
-                                                               unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    constexpr int VS = 72;
-    __shared__ __align__(16) uint16_t vbuf[NG][71 * VS];
-    __shared__ __align__(16) uint32_t tqbuf[NG][36 * 64];
-    __shared__ uint64_t               s_draw[sizeof(Descent) / 8]; // Descent has initializers: raw LDS
-    __shared__ unsigned long long     s_part[4 * NG];
-    __shared__ int16_t                s_taps[16];
-    __shared__ int                    s_mode, s_ctag;
-    Descent  &D  = *(Descent *)s_draw;
-    const int u  = blockIdx.x, g = threadIdx.x >> 8, lt = threadIdx.x & 255;
-    const int t0 = tile0[u], nt = tile0[u + 1] - t0;
-    auto      propose = [&]() { // lane 0: the next candidate's taps and evaluation mode, or s_mode = 0 when done
-        if (D.next()) {
-            int v[3];
-            D.taps(0, v), set_wiener_taps(s_taps, v); // f = 0: hfilter, f = 1: vfilter
-            D.taps(1, v), set_wiener_taps(s_taps + 8, v);
-            s_mode = (D.init || D.mf != 1) ? 1 : (s_ctag == htag(D) ? 2 : 3);
-        } else {
-            s_mode = 0;
-        }
-    };
-    if (threadIdx.x == 0) {
-        D      = ds[u];
-        s_ctag = -1;
-        s_mode = 0;
-        if (!D.done) propose();
-    }
-    __syncthreads();
-    uint16_t *const    v = vbuf[g];
-    uint32_t *const    tq = tqbuf[g];
-    unsigned long long npx = 0;
-    while (const int mode = s_mode) {
-        int h[8], w[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) h[k] = s_taps[k], w[k] = s_taps[8 + k];
-        const uint32_t He[4] = {pack2(0, h[0]), pack2(h[1], h[2]), pack2(h[3], h[4]), pack2(h[5], h[6])};
-        const uint32_t Ho[4] = {pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
-        const uint32_t Ve[4] = {pack2(w[0], w[1]), pack2(w[2], w[3]), pack2(w[4], w[5]), pack2(w[6], w[7])};
-        const uint32_t Vo[4] = {pack2(0, w[0]), pack2(w[1], w[2]), pack2(w[3], w[4]), pack2(w[5], w[6])};
-        unsigned long long eu = 0;
-        for (int base = 0; base < nt; base += NG) { // every lane runs the same iterations (workgroup barriers)
-            const int  ti = t0 + base + g;
-            const bool on = base + g < nt;
-            const Tile t  = on ? A.tiles[ti] : A.tiles[t0];
-            const PlaneArgs &P = A.pl[t.plane];
-            const T         *d = (const T *)P.dgd, *src = (const T *)P.src;
-            const WienerRound rr = wiener_round(P.bd);
-            // ---- stage: the bordered CDEF tile or the cached horizontal pass into LDS, this lane's source rows ----
-            const int x = lt & 63, nyp = (t.h + 1) >> 1;
-            if (on) {
-                if (mode == 2) {
-                    const uint4 *tc = (const uint4 *)(tcache + (size_t)ti * 36 * 64);
-                    for (int i = lt; i < 36 * 64 / 4; i += 256) ((uint4 *)tq)[i] = tc[i];
-                } else {
-                    const int rows = t.h + 7, ng = (t.w + 8) >> 2;
-                    for (int i = lt; i < 71 * 18; i += 256) {
-                        const int r = i / 18, gg = i - r * 18;
-                        if (r < rows && gg < ng)
-                            *(uint2 *)(v + r * VS + 4 * gg) =
-                                load_group(d, P.dstride, P.W, P.H, t.y0 + r - 3, t.x0 - 4 + 4 * gg);
-                    }
-                }
-            }
-            __syncthreads();
-            // ---- horizontal pass (modes 1 and 3) ----
-            if (on && mode != 2) {
-                const int rows = t.h + 7;
-                const int lim = (1 << (P.bd + 1 + 7 - rr.r0)) - 1, hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1));
-                uint16_t *tq16 = (uint16_t *)tq;
-                const int xh   = 2 * (lt & 31);
-                if (xh < t.w)
-                    for (int r = lt >> 5; r < rows; r += 8) {
-                        const uint32_t *pr = (const uint32_t *)(v + r * VS + xh);
-                        const uint32_t  p0 = pr[0], p1 = pr[1], p2 = pr[2], p3 = pr[3], p4 = pr[4];
-                        const int s0 = dot2(p0, He[0], dot2(p1, He[1], dot2(p2, He[2], dot2(p3, He[3], hb + (int)((p2 & 0xFFFF) << 7)))));
-                        const int s1 = dot2(p1, Ho[0], dot2(p2, Ho[1], dot2(p3, Ho[2], dot2(p4, Ho[3], hb + (int)((p2 >> 16) << 7)))));
-                        const int o  = ((r >> 1) * 64 + xh) * 2 + (r & 1);
-                        tq16[o]      = (uint16_t)min(max(s0 >> rr.r0, 0), lim);
-                        tq16[o + 2]  = (uint16_t)min(max(s1 >> rr.r0, 0), lim);
-                    }
-            }
-            __syncthreads();
-            if (on && mode == 3) { // cache this hfilter's horizontal pass for the vertical moves that follow
-                uint32_t *tc = tcache + (size_t)ti * 36 * 64;
-                for (int i = lt; i < 36 * 64 / 4; i += 256) ((uint4 *)tc)[i] = ((const uint4 *)tq)[i];
-            }
-            // ---- vertical pass and the SSE against the source ----
-            uint32_t  e    = 0;
-            const int maxv = (1 << P.bd) - 1, vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
-            if (on && x < t.w) {
-                const T *sq = src + (size_t)t.y0 * P.sstride + t.x0 + x;
-#pragma unroll 2
-                for (int yp = lt >> 6; yp < nyp; yp += 4) {
-                    const int       y  = 2 * yp;
-                    const int       a0 = sq[(size_t)y * P.sstride], a1 = y + 1 < t.h ? (int)sq[(size_t)(y + 1) * P.sstride] : 0;
-                    const uint32_t *c  = tq + yp * 64 + x;
-                    const uint32_t  q0 = c[0], q1 = c[64], q2 = c[128], q3 = c[192];
-                    const int s0 = dot2(q0, Ve[0], dot2(q1, Ve[1], dot2(q2, Ve[2], dot2(q3, Ve[3], vb + (int)((q1 >> 16) << 7)))));
-                    const int s1 = dot2(q0, Vo[0], dot2(q1, Vo[1], dot2(q2, Vo[2], dot2(q3, Vo[3], vb + (int)((q2 & 0xFFFF) << 7)))));
-                    const int d0 = min(max(s0 >> rr.r1, 0), maxv) - a0;
-                    e += (uint32_t)(d0 * d0);
-                    if (y + 1 < t.h) {
-                        const int d1 = min(max(s1 >> rr.r1, 0), maxv) - a1;
-                        e += (uint32_t)(d1 * d1);
-                    }
-                }
-            }
-            eu += e;
-            if (on && lt == 0) npx += (unsigned long long)(t.w * t.h);
-            __syncthreads(); // the next tiles restage v / tq
-        }
-        const unsigned long long et = wave_sum(eu);
-        if ((threadIdx.x & 63) == WAVE_LAST) s_part[threadIdx.x >> 6] = et;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long err = 0;
-            for (int k = 0; k < 4 * NG; k++) err += s_part[k];
-            if (s_mode == 3) s_ctag = htag(D); // the evaluated candidate's hfilter pass is now cached
-            D.report((int64_t)err);
-            propose();
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) ds[u] = D;
-    if (pc && lt == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
-    PROF_END(tk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2080,107 +1535,11 @@ __global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, co
     PROF_END(tk);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The self-guided descents as one persistent work-queue kernel (the scheme of wiener_queue_kernel).  A work item is
-// one tile of a unit with a pending tree on any of its eps; the worker evaluates every pending tree of the unit over
-// the tile (proj_tile) and counts the unit's arrivals; the workgroup that completes the unit's pass steps all of the
-// unit's descents (one lane per ep, sgr_descent_step with the full SG_NC-node tree) and appends the unit's tiles again
-// while any of them is live.  q->live counts units with a live descent.
-// ---------------------------------------------------------------------------------------------
+// the plane of global unit u
 __device__ inline int unit_plane(const SearchArgs &A, int nplanes, int u) {
     int p = 0;
     while (p + 1 < nplanes && u >= A.pl[p + 1].unit_base) p++;
     return p;
-}
-
-__device__ inline int q_claim(WnQueue *q, const int32_t *log, int cap, int *s_item) { // every lane calls this
-    if (threadIdx.x == 0) {
-        const int idx = atomicAdd(&q->head, 1);
-        int       it  = 0;
-        for (unsigned spin = 0;; spin++) {
-            if (idx < cap) it = q_load(log + idx);
-            if (it || idx >= cap) break;
-            if (q_load(&q->live) == 0) break; // every descent ended: no entry will be published any more
-            if (spin > (1u << 25)) {          // a bound every worker reaches (~seconds): never spin forever
-                atomicExch(&q->error, 2);
-                atomicExch(&q->live, 0);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8); // ~0.2 us: idle workers spend few instructions polling
-        }
-        *s_item = it - 1;
-        wait_mem();
-    }
-    __syncthreads();
-    return *s_item;
-}
-
-// the unit's first step (every descent's seed is its first candidate), one workgroup per global unit
-__global__ __launch_bounds__(64) void sgr_queue_start_kernel(const SearchArgs A, int nplanes, const Descent *ds_in,
-                                                             Descent *ds, unsigned long long *err, int32_t *cand,
-                                                             uint32_t *candm, int32_t *arr, const int32_t *tile0,
-                                                             WnQueue *q, int32_t *log, int cap) {
-    __shared__ int     s_pos;
-    __shared__ uint64_t s_treeraw[16 * (SG_NC / 2) * sizeof(Descent) / 8]; // Descent has initializers: raw LDS
-    Descent (*s_tree)[SG_NC / 2] = (Descent(*)[SG_NC / 2])s_treeraw;
-    const int          u = blockIdx.x;
-    const int      p = unit_plane(A, nplanes, u);
-    const PlaneArgs &P = A.pl[p];
-    if (P.ne == 0) return;
-    const int pb = P.pair_base + (u - P.unit_base) * P.ne;
-    int       live = 0;
-    if (threadIdx.x == 0) arr[u] = 0;
-    if (threadIdx.x < P.ne) {
-        ds[pb + threadIdx.x] = ds_in[pb + threadIdx.x];
-        for (int c = 0; c < SG_NC; c++) err[(size_t)(pb + threadIdx.x) * SG_NC + c] = 0;
-        live = sgr_descent_step<true>(ds, pb + threadIdx.x, err, cand, candm, 1, SG_NC, s_tree[threadIdx.x]);
-    }
-    wait_mem();
-    live = __syncthreads_or(live);
-    if (!live) return;
-    if (threadIdx.x == 0) atomicAdd(&q->live, 1);
-    q_append(q, log, cap, tile0, u, &s_pos);
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void sgr_queue_kernel(const SearchArgs A, Descent *ds, int32_t *cand,
-                                                        uint32_t *candm, unsigned long long *err, int32_t *arr,
-                                                        const int32_t *tile0, WnQueue *q, int32_t *log, int cap,
-                                                        unsigned long long *pc, unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    __shared__ int     s_item, s_last, s_pos;
-    __shared__ uint64_t s_treeraw[16 * (SG_NC / 2) * sizeof(Descent) / 8]; // Descent has initializers: raw LDS
-    Descent (*s_tree)[SG_NC / 2] = (Descent(*)[SG_NC / 2])s_treeraw;
-    unsigned long long npx_t = 0, npx_e = 0;
-    for (;;) {
-        const int ti = q_claim(q, log, cap, &s_item);
-        if (ti < 0) break;
-        const Tile t = A.tiles[ti];
-        proj_tile<T, true>(A, ti, cand, candm, err, npx_t, npx_e);
-        wait_mem();      // this wave's error adds are acknowledged
-        __syncthreads(); // ... by every wave, before the arrival
-        if (threadIdx.x == 0) {
-            const int a = atomicAdd(&arr[t.unit], 1);
-            s_last      = a == tile0[t.unit + 1] - tile0[t.unit] - 1;
-            if (s_last) arr[t.unit] = 0;
-        }
-        __syncthreads();
-        if (!s_last) continue;
-        const PlaneArgs &P  = A.pl[t.plane];
-        const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
-        int              live = 0;
-        if (threadIdx.x < P.ne)
-            live = sgr_descent_step<true>(ds, pb + threadIdx.x, err, cand, candm, 0, SG_NC, s_tree[threadIdx.x]);
-        wait_mem(); // the new trees are in memory before the unit's tiles are published
-        live = __syncthreads_or(live);
-        if (live) q_append(q, log, cap, tile0, t.unit, &s_pos);
-        else if (threadIdx.x == 0) atomicSub(&q->live, 1);
-    }
-    if (pc && threadIdx.x == 0 && npx_t) {
-        atomicAdd(pc + PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_e);
-        atomicAdd(pc + 2 * PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_t);
-    }
-    PROF_END(tk);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2505,30 +1864,12 @@ void launch_stats(int win, Fn &&f) {
 
 constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
 constexpr int SG_SPEC_LIVE1 = -1, SG_SPEC_LIVE3 = -1; // always 7-node self-guided trees
-constexpr int WN_TRIAL_GRID = 768; // persistent Wiener trial workgroups (3 per CU); SVTGPU_WN_GRID overrides (sweeps)
 SgSpec sg_spec() { // self-guided tree sizes by live count; SVTGPU_SG_SPEC="live1,live3" overrides (sweeps)
     static const SgSpec v = [] {
         SgSpec      r{SG_SPEC_LIVE1, SG_SPEC_LIVE3};
         const char *e = std::getenv("SVTGPU_SG_SPEC");
         if (e) std::sscanf(e, "%d,%d", &r.live1, &r.live3);
         return r;
-    }();
-    return v;
-}
-// persistent Wiener queue workers (SVTGPU_WN_QUEUE=0 selects the per-round trial/advance launches instead;
-// SVTGPU_WN_QGRID sets the worker count)
-bool wn_use_queue() {
-    static const bool v = [] {
-        const char *e = std::getenv("SVTGPU_WN_QUEUE");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-// one workgroup per unit runs the whole Wiener descent (default); SVTGPU_WN_UNIT=0 selects the work queue
-bool wn_use_unit() {
-    static const bool v = [] {
-        const char *e = std::getenv("SVTGPU_WN_UNIT");
-        return !(e && std::atoi(e) == 0);
     }();
     return v;
 }
@@ -2539,56 +1880,6 @@ int wr_lds_cap() {
         return e ? std::atoi(e) : WR_LDS_CAP;
     }();
     return v;
-}
-// the unit-resident Wiener kernel (default; SVTGPU_WN_RES=0 selects the tiled unit kernel, which also takes units
-// too large for the resident layout)
-bool wn_use_res() {
-    static const bool v = [] {
-        const char *e = std::getenv("SVTGPU_WN_RES");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-// tile groups of 256 lanes per unit workgroup (SVTGPU_WN_NG: 2 or 4).  2 by default: at three frames in flight the
-// 512-lane workgroups leave room on the CUs for the other frames' kernels (2030-2047 vs 2012-2019 Mpx/s, same box,
-// profiles/r02/s16); a lone frame's descent is 1 % faster with 4
-int wn_unit_ng() {
-    static const int v = [] {
-        const char *e = std::getenv("SVTGPU_WN_NG");
-        return e && std::atoi(e) == 4 ? 4 : 2;
-    }();
-    return v;
-}
-// persistent self-guided queue workers: opt-in (SVTGPU_SG_QUEUE=1; SVTGPU_SG_QGRID sets the worker count).  With the
-// hoisted per-pixel terms and partial-tree evaluation the per-round projection launches measured faster at three
-// frames in flight (1963-1980 vs 1864-1889 Mpx/s, same box)
-bool sg_use_queue() {
-    static const bool v = [] {
-        const char *e = std::getenv("SVTGPU_SG_QUEUE");
-        return e && std::atoi(e) != 0;
-    }();
-    return v;
-}
-int sg_queue_grid() {
-    static const int g = [] {
-        const char *e = std::getenv("SVTGPU_SG_QGRID");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 512;
-    }();
-    return g;
-}
-int wn_queue_grid() {
-    static const int g = [] {
-        const char *e = std::getenv("SVTGPU_WN_QGRID");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 512; // 2 per CU: the self-guided filters keep room (1024 starves them)
-    }();
-    return g;
-}
-int wn_trial_grid() {
-    static const int g = [] {
-        const char *e = std::getenv("SVTGPU_WN_GRID");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : WN_TRIAL_GRID;
-    }();
-    return g;
 }
 
 // plane p's Wiener window for the controls
@@ -2675,7 +1966,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // fewest row parts that fit one CU's LDS and registers each (global-memory mode when no cut up to WR_MAX_PARTS
     // does); workgroups start with the largest parts (the longest chains), the parts of a unit adjacent.
     std::vector<WrItem> wr_items;
-    bool                wr_ok = wn_use_res(), wr_parted = false;
+    bool                wr_parted = false;
     int                 wr_lds = 0;
     {
         std::vector<int> ord(n_wn);
@@ -2684,7 +1975,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             const URect &r = units[u];
             const int    w = r.h_end - r.h_start, h = r.v_end - r.v_start;
             ord[u]         = u;
-            if (w > 384) wr_ok = false; // wider than the lane layout (unit sizes above 256)
             int k = 1;
             while (k < WR_MAX_PARTS && !wr_lds_mode(w, (h + k - 1) / k, wr_lds_cap())) k++;
             np[u] = wr_lds_mode(w, (h + k - 1) / k, wr_lds_cap()) ? k : 1;
@@ -2716,26 +2006,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                  o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8);
     const size_t res_span = dc.off - o_sse;
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_taps = dc(32 * (size_t)n_wn), o_werr = dc(8 * (size_t)n_wn),
-                 o_wact = dc(4 * (size_t)n_wn), o_ctag = dc(4 * (size_t)n_wn),
-                 o_tcache = dc((size_t)36 * 64 * 4 * nt_wn);
     const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
-                 o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all), o_best = dc(16 * (size_t)n_sg),
-                 o_witems = dc(4 * (size_t)nt_wn), o_cnt = dc(32);
-    // the Wiener work queue's shared words, in the uncached arena: counters, the append-only log of tile items,
-    // per-unit arrivals / SSE / taps / modes / descents, and the horizontal-pass cache
-    const int wq_cap = 192 * nt_wn + 4096;
-    Carver    qc;
-    const size_t q_wq = qc(sizeof(WnQueue)), q_log = qc(4 * (size_t)wq_cap), q_arr = qc(4 * (size_t)n_wn),
-                 q_err = qc(8 * (size_t)n_wn), q_taps = qc(32 * (size_t)n_wn), q_wact = qc(4 * (size_t)n_wn),
-                 q_ctag = qc(4 * (size_t)n_wn), q_ds = qc(sizeof(Descent) * (size_t)n_wn),
-                 q_tc = qc((size_t)36 * 64 * 4 * nt_wn);
-    // the self-guided queue's: counters, log, per-unit arrivals, per-(unit, ep) tree errors, candidates, masks, descents
-    const int    sq_cap = 256 * nt_sg + 4096;
-    const size_t q_sq = qc(sizeof(WnQueue)), q_slog = qc(4 * (size_t)sq_cap), q_sarr = qc(4 * (size_t)n_all),
-                 q_serr = qc(8 * SG_NC * (size_t)npairs), q_scand = qc(8 * SG_NC * (size_t)npairs),
-                 q_scandm = qc(4 * (size_t)npairs), q_sds = qc(sizeof(Descent) * (size_t)npairs);
-    const size_t q_wrx = qc(16 * (size_t)n_wr); // the parted resident Wiener units' SSE exchange words
+                 o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all),
+                 o_best = dc(16 * (size_t)n_sg), o_cnt = dc(32);
+    // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
+    Carver       qc;
+    const size_t q_wrx = qc(16 * (size_t)n_wr);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -2876,9 +2152,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    const bool wn_unit = wn_use_unit(), wn_queue = !wn_unit && wn_use_queue(), sg_queue = sg_use_queue();
-    uint8_t   *qa       = nullptr;
-    if ((n_wn && wn_queue) || (npairs && sg_queue) || (n_wn && wn_unit && wr_ok && wr_parted)) {
+    uint8_t *qa = nullptr;
+    if (n_wn && wr_parted) {
         if (qc.off > s->qarena_bytes) {
             if (s->d_qarena) (void)hipFree(s->d_qarena);
             s->d_qarena = nullptr, s->qarena_bytes = 0;
@@ -2887,64 +2162,17 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         qa = (uint8_t *)s->d_qarena;
     }
-    if (n_wn && wn_queue) { // the whole Wiener descent in one persistent kernel (no host poll, no round launches)
-        HIP_TRY(hipMemsetAsync(qa + q_wq, 0, q_arr - q_wq, sw)); // counters and the log
-        hipLaunchKernelGGL(wiener_queue_start_kernel, dim3(n_wn), dim3(256), 0, sw, (const Descent *)dp(o_wds),
-                           (Descent *)(qa + q_ds), n_wn, (unsigned long long *)(qa + q_err), (int16_t *)(qa + q_taps),
-                           (int32_t *)(qa + q_wact), (int32_t *)(qa + q_ctag), (int32_t *)(qa + q_arr),
-                           (const int32_t *)d_t0, (WnQueue *)(qa + q_wq), (int32_t *)(qa + q_log), wq_cap);
-        run(2, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(wiener_queue_kernel<T>, dim3(std::min(nt_wn, wn_queue_grid())), dim3(256), 0, sw, A,
-                               (Descent *)(qa + q_ds), (int16_t *)(qa + q_taps), (int32_t *)(qa + q_wact),
-                               (int32_t *)(qa + q_ctag), (int32_t *)(qa + q_arr), (unsigned long long *)(qa + q_err),
-                               (const int32_t *)d_t0, (uint32_t *)(qa + q_tc), (WnQueue *)(qa + q_wq),
-                               (int32_t *)(qa + q_log), wq_cap, pc, tk);
-        });
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(dp(o_wds), qa + q_ds, sizeof(Descent) * (size_t)n_wn, hipMemcpyDeviceToDevice, sw));
-    } else if (n_wn && wn_unit && wr_ok) { // the whole Wiener descent of every unit, resident on one CU each
+    if (n_wn) { // the whole Wiener descent of every unit, resident on one CU each (or a few, for the largest)
         HIP_TRY(hipMemsetAsync(dp(o_wstat), 0, 8, sw));
         if (wr_parted) HIP_TRY(hipMemsetAsync(qa + q_wrx, 0, 16 * (size_t)n_wr, sw));
         run(2, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
-                               (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa + q_wrx),
+                               (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa ? qa + q_wrx : nullptr),
                                (int32_t *)dp(o_wstat), pc, tk);
         });
         HIP_TRY(hipGetLastError());
-    } else if (n_wn && wn_unit) { // the whole Wiener descent of every unit inside one workgroup
-        run(2, [&](unsigned long long *tk) {
-            if (wn_unit_ng() == 2)
-                hipLaunchKernelGGL((wiener_unit_kernel<T, 2>), dim3(n_wn), dim3(512), 0, sw, A, (Descent *)dp(o_wds),
-                                   (const int32_t *)d_t0, (uint32_t *)dp(o_tcache), pc, tk);
-            else
-                hipLaunchKernelGGL((wiener_unit_kernel<T, 4>), dim3(n_wn), dim3(1024), 0, sw, A, (Descent *)dp(o_wds),
-                                   (const int32_t *)d_t0, (uint32_t *)dp(o_tcache), pc, tk);
-        });
-        HIP_TRY(hipGetLastError());
-    } else if (n_wn) {
-        HIP_TRY(hipMemsetAsync(dp(o_werr), 0, 8 * (size_t)n_wn, sw));
-        HIP_TRY(hipMemsetAsync(dp(o_ctag), 0xFF, 4 * (size_t)n_wn, sw)); // no cached horizontal pass
-        hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, sw, (Descent *)dp(o_wds), n_wn,
-                           (unsigned long long *)dp(o_werr), (int16_t *)dp(o_taps), (int32_t *)dp(o_wact),
-                           (int32_t *)dp(o_ctag), (const int32_t *)d_t0, (int32_t *)dp(o_witems), cnt, 1,
-                           (unsigned long long *)nullptr);
-        HIP_TRY(hipGetLastError());
     }
-    if (npairs && sg_queue) { // the whole self-guided descent in one persistent kernel
-        HIP_TRY(hipMemsetAsync(qa + q_sq, 0, q_sarr - q_sq, st)); // counters and the log
-        hipLaunchKernelGGL(sgr_queue_start_kernel, dim3(n_all), dim3(64), 0, st, A, nplanes, (const Descent *)dp(o_sds),
-                           (Descent *)(qa + q_sds), (unsigned long long *)(qa + q_serr), (int32_t *)(qa + q_scand),
-                           (uint32_t *)(qa + q_scandm), (int32_t *)(qa + q_sarr), (const int32_t *)d_t0,
-                           (WnQueue *)(qa + q_sq), (int32_t *)(qa + q_slog), sq_cap);
-        run(3, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(sgr_queue_kernel<T>, dim3(std::min(nt_sg, sg_queue_grid())), dim3(256), 0, st, A,
-                               (Descent *)(qa + q_sds), (int32_t *)(qa + q_scand), (uint32_t *)(qa + q_scandm),
-                               (unsigned long long *)(qa + q_serr), (int32_t *)(qa + q_sarr), (const int32_t *)d_t0,
-                               (WnQueue *)(qa + q_sq), (int32_t *)(qa + q_slog), sq_cap, pc, tk);
-        });
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(dp(o_sds), qa + q_sds, sizeof(Descent) * (size_t)npairs, hipMemcpyDeviceToDevice, st));
-    } else if (npairs) {
+    if (npairs) {
         HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * SG_NC * (size_t)npairs, st));
         HIP_TRY(hipMemsetAsync(dp(o_ustamp), 0, 4 * (size_t)n_all, st));
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
@@ -2953,17 +2181,18 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                            (const int32_t *)cnt + 6, cnt + 2, 1, 1, sg_spec(), (unsigned long long *)nullptr);
         HIP_TRY(hipGetLastError());
     }
-    // Each chain runs in batches of ROUNDS_PER_BATCH rounds with the next batch already queued behind the one the
-    // host is checking (a chain whose descents have all finished turns the queued rounds into no-op launches), so
-    // neither stream waits for the host between batches.
+    // The self-guided chain runs in batches of ROUNDS_PER_BATCH rounds with the next batch already queued behind the one
+    // the host is checking (a chain whose descents have all finished turns the queued rounds into no-op launches), so
+    // its stream never waits for the host between batches.  (Chain 0, the Wiener descents of earlier rounds, runs
+    // inside wiener_res_kernel now; the two-chain bookkeeping is kept for the flag layout.)
     const int gs = std::max(1, nt_sg);
     struct Chain {
         bool        live;
         int         g = 0, head = 0, inflight = 0; // round index; ring of two batches in flight
         hipStream_t stream;
     } ch[2];
-    ch[0].live = n_wn > 0 && !wn_queue && !wn_unit, ch[0].stream = sw;
-    ch[1].live = npairs > 0 && !sg_queue, ch[1].stream = st;
+    ch[0].live = false, ch[0].stream = sw;
+    ch[1].live = npairs > 0, ch[1].stream = st;
     if (!s->h_flag) {
         HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&s->h_flag_dev, s->h_flag, 0));
@@ -2982,20 +2211,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         tr("enqueue", c, C.g);
         for (int b = 0; b < ROUNDS_PER_BATCH; b++, C.g++) {
             int32_t *cur = cnt + 4 * (C.g & 1), *nxt = cnt + 4 * ((C.g + 1) & 1);
-            if (c == 0) {
-                run(2, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_trial_kernel<T>, dim3(std::min(nt_wn, wn_trial_grid())), dim3(256), 0, sw,
-                                       A, (const int16_t *)dp(o_taps), (const int32_t *)dp(o_wact),
-                                       (const int32_t *)dp(o_witems), (const int32_t *)cur, nxt,
-                                       (unsigned long long *)dp(o_werr), pc, tk, (uint32_t *)dp(o_tcache));
-                });
-                run(4, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(wiener_advance_kernel, dim3((n_wn + 255) / 256), dim3(256), 0, sw,
-                                       (Descent *)dp(o_wds), n_wn, (unsigned long long *)dp(o_werr),
-                                       (int16_t *)dp(o_taps), (int32_t *)dp(o_wact), (int32_t *)dp(o_ctag),
-                                       (const int32_t *)d_t0, (int32_t *)dp(o_witems), nxt, 0, tk);
-                });
-            } else {
+            {
                 run(3, [&](unsigned long long *tk) {
                     hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
                                        (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
@@ -3082,21 +2298,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
-    svtgpu_count_xfer(1, res_span + ((n_wn && wn_queue) ? sizeof(WnQueue) : 0) + ((npairs && sg_queue) ? sizeof(WnQueue) : 0));
-    if (n_wn && wn_queue) HIP_TRY(hipMemcpyAsync(hp(h_cnt), qa + q_wq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
-    if (npairs && sg_queue)
-        HIP_TRY(hipMemcpyAsync(hp(h_cnt + 16), qa + q_sq, sizeof(WnQueue), hipMemcpyDeviceToHost, st));
+    svtgpu_count_xfer(1, res_span);
     HIP_TRY(hipStreamSynchronize(st));
-    if (n_wn && wn_queue && ((const WnQueue *)hp(h_cnt))->error) {
-        svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener work queue overflow", __FILE__, __LINE__);
-        return SVTGPU_ERR_HIP;
-    }
-    if (n_wn && wn_unit && wr_ok && *(const int32_t *)hp(h_res + (o_wstat - o_sse))) {
-        svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener descent exceeded its round bound", __FILE__, __LINE__);
-        return SVTGPU_ERR_HIP;
-    }
-    if (npairs && sg_queue && ((const WnQueue *)hp(h_cnt + 16))->error) {
-        svtgpu_set_last_hip_error(hipErrorUnknown, "LR self-guided work queue overflow", __FILE__, __LINE__);
+    if (n_wn && *(const int32_t *)hp(h_res + (o_wstat - o_sse))) { // status bits of wiener_res_kernel
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener descent: round bound or part exchange timed out",
+                                  __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;
     }
     mark(3);

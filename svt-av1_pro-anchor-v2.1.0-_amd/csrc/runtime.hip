@@ -106,25 +106,6 @@ extern "C" int svtgpu_transfer_bytes(uint64_t *h2d, uint64_t *d2h, int32_t reset
     return SVTGPU_OK;
 }
 
-int svtgpu_priority_stream(hipStream_t *hs, hipEvent_t *ev, hipStream_t after, hipStream_t *out) {
-    static const bool on = [] { // opt-in: measured slower at three frames in flight (1689-1709 vs 1849-1869 Mpx/s)
-        const char *e = std::getenv("SVTGPU_HIPRIO");
-        return e && std::atoi(e) != 0;
-    }();
-    *out = after;
-    if (!on) return SVTGPU_OK;
-    if (!*hs) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(hs, hipStreamNonBlocking, greatest));
-        HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    }
-    HIP_TRY(hipEventRecord(*ev, after));
-    HIP_TRY(hipStreamWaitEvent(*hs, *ev, 0));
-    *out = *hs;
-    return SVTGPU_OK;
-}
-
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st) {
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 0;; it++) {

@@ -97,8 +97,6 @@ struct SvtGpuCdefFrameState {
     int8_t        *d_fb_kind;     // [nfb] SB128 areas (cdef_sb128.hip); null = SB64
     int8_t        *h_fb_kind;     // host copy
     uint8_t       *d_mse_rem;     // [3][nfb][64] remainders of the per-FB distortion shift (SB128 only)
-    hipStream_t    hi_stream;     // highest-priority stream of the pick's dependent launches (lazy)
-    hipEvent_t     hi_ev;
 };
 
 // Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
@@ -141,11 +139,6 @@ int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long 
 int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st);
 // host <-> device bytes of the frame-level entry points (copies and mapped-memory results), for the bench's report
 void svtgpu_count_xfer(int d2h, size_t bytes);
-// Chains of short dependent launches with host waits in between (the CDEF pick, the DLF level search) run on a
-// highest-priority stream ordered after the caller's stream `after`: *out = that stream (created in *hs / *ev on
-// first use) when SVTGPU_HIPRIO=1, else `after` itself (the default: the priority streams measured slower).  The chain's callers wait for its last result on the
-// host, so the caller's later work is ordered after it.
-int svtgpu_priority_stream(hipStream_t *hs, hipEvent_t *ev, hipStream_t after, hipStream_t *out);
 SvtGpuContext *svtgpu_default_context();
 static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;

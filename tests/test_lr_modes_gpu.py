@@ -1,0 +1,33 @@
+"""The global-memory mode of the resident Wiener kernel (wiener_res_kernel): units whose CDEF window does not fit the
+CU's LDS (no row-part cut up to WR_MAX_PARTS fits) read it and the source from global memory per candidate.  No
+frame of the default configurations takes that path, so it runs here on the pipeline goldens with the LDS cap set
+to 0 (SVTGPU_WR_LDS_CAP, read once per process: a child process) -- bit-exact against the reference like the
+default path (every selectable path under a test)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+sys.path[:0] = [%r, %r, %r, %r]
+import torch
+if torch.cuda.is_available():
+    torch.cuda.init()
+import pipeline_run as prun
+for case in ("mini10", "sb128_10", "c3_4k10"):
+    prun.check(case, prun.run_gpu(case), "wr global mode")
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+def test_wiener_global_memory_mode_bit_exact():
+    code = CHILD % (ROOT, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"), os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, SVTGPU_WR_LDS_CAP="0"))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
