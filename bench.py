@@ -130,7 +130,7 @@ def parse():
                     help="pinned: the reference-pinned pipeline case of this size when there is one (else synth); "
                          "synth: the float generator (synth.frame_pair)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
-    ap.add_argument("--stages", default="all", choices=("all", "cdef"),
+    ap.add_argument("--stages", default="all", choices=("all", "cdef", "md"),
                     help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
                          "configs 1/2)")
     ap.add_argument("--no-matrix", action="store_true",
@@ -150,6 +150,8 @@ MATRIX = [
                           "--steps", "60", "--warmup", "5"]),
     ("pipeline_4k8", ["--width", "3840", "--height", "2160", "--bit-depth", "8", "--no-cpu-baseline",
                       "--steps", "40", "--warmup", "5"]),
+    ("config5_8k10_md", ["--width", "7680", "--height", "4320", "--bit-depth", "10", "--stages", "md",
+                         "--no-cpu-baseline", "--steps", "50", "--warmup", "5"]),
 ]
 
 
@@ -170,6 +172,8 @@ def run_matrix():
             res[label] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
                           "frames_in_flight": c["frames_in_flight"], "workload": c["workload"],
                           "pipeline_frac_hbm": c.get("pipeline_roofline", {}).get("frac")}
+            if "md_roofline" in c:
+                res[label]["md_roofline"] = c["md_roofline"]
             if "cpu_baseline" in d:
                 res[label]["cpu_baseline"] = d["cpu_baseline"]
         except (OSError, ValueError, subprocess.TimeoutExpired) as e:
@@ -425,6 +429,76 @@ def roofline_of(kernels, bd, pmc_json):
     return out
 
 
+def bench_md(a, torch, dist, n, rank, local):
+    """BASELINE configs[4]: the mode-decision distortion batch of one frame -- SAD, SSE and variance of every AV1 block
+    shape <= 64x64 of every SB against NREF references (md_dist_kernel) -- split over the ranks by SB ranges (strong
+    scaling, no exchange), with each GPU's HBM rate against the roofline ((1 + refs) x 64 x 64 x B per
+    SB read once; the per-shape outputs written once)."""
+    W, H, bd = a.width, a.height, a.bit_depth
+    B = 2 if bd > 8 else 1
+    NREF = 7
+    ctx = svtgpu.Context(local)
+    src, _ = synth.frame_pair_int(W, H, bd, 0x5EED0008)
+    S = svtgpu.Frame(ctx, W, H, bd)
+    S.upload(src)
+    refs = []
+    for r in range(NREF):
+        rs, _ = synth.frame_pair_int(W, H, bd, 0x5EED0009 + 17 * r)
+        f = svtgpu.Frame(ctx, W, H, bd)
+        f.upload(rs)
+        refs.append(f)
+    md = svtgpu.MdBatch(ctx, W, H, NREF)
+    md.set_mvs(np.random.default_rng(8).integers(-16, 17, size=(md.nsb, NREF, 2)))
+    sb0, sb1 = svtgpu.band(md.nsb, n, rank)
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    for _ in range(a.warmup):
+        md.run(S, refs, sb0, sb1, sp)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(a.steps):
+        md.run(S, refs, sb0, sb1, sp)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gpu_ms = e0.elapsed_time(e1) / a.steps  # this rank's device time per step
+    if n > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt * 1e3 / a.steps
+    nsb_mine = sb1 - sb0
+    alg_in = nsb_mine * (1 + NREF) * 64 * 64 * B
+    alg_out = nsb_mine * NREF * 3 * svtgpu.MD_BLOCKS * 4
+    gbs = (alg_in + alg_out) / (gpu_ms * 1e-3) / 1e9
+    out = {"metric": "MD SAD/SSE/variance Mpixels/s on 8K10b; per-GPU HBM GB/s vs roofline", "value": round(W * H / (ms_per_step * 1e-3) / 1e6, 3),
+           "unit": "Mpixels/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u16" if bd > 8 else "u8",
+           "data": "synthetic",
+           "config": {"workload": "md_dist_kernel: every SB x %d refs x all %d block shapes <= 64x64 (SAD, SSE, variance); "
+                                  "%dx%d %d-bit, %d SBs split over %d rank(s) by SB ranges" % (NREF, svtgpu.MD_BLOCKS, W, H, bd,
+                                                                                            md.nsb, n),
+                      "width": W, "height": H, "bit_depth": bd, "frames_in_flight": 1, "nsb": md.nsb,
+                      "sb_range": [sb0, sb1], "parallelism": "sb%d (SB ranges, no exchange)" % n if n > 1 else "single",
+                      "md_roofline": {"alg_in_MB_per_gpu": round(alg_in / 1e6, 2), "out_MB_per_gpu": round(alg_out / 1e6, 2),
+                                      "gpu_ms_per_frame": round(gpu_ms, 4), "achieved_GBs_per_gpu": round(gbs, 1),
+                                      "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                      "note": "rank 0's HIP-event time per step; bytes = the SB samples of the source and "
+                                              "every reference read once (SURVEY §8(d)) + the u32 [SB][ref][3][%d] "
+                                              "outputs written once" % svtgpu.MD_BLOCKS}}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    md.close()
+
+
 def main():
     a = parse()
     rc = spawn_ranks(a)
@@ -443,6 +517,11 @@ def main():
     n = world
     if n > 1:  # control only (barriers, the max-over-ranks time, the RCCL ids): the data path is libsvtgpu's RCCL
         dist.init_process_group("gloo")
+    if a.stages == "md":
+        bench_md(a, torch, dist, n, rank, local)
+        if n > 1:
+            dist.destroy_process_group()
+        return
     tiled = n > 1 and a.split == "tiles"
     W, H, bd = a.width, a.height, a.bit_depth
     pin = PINNED.get((W, H, bd)) if a.inputs == "pinned" else None

@@ -5,7 +5,8 @@
  * encoder's DLF -> CDEF -> REST processes run it (EbDlfProcess.c:96-136, EbCdefProcess.c:398-520 / :663-670,
  * EbRestProcess.c:552-630), on a recon/source pair and a mode-info grid handed in by tests/golden/
  * make_pipeline_golden.py:
- *   svt_av1_loop_filter_init + svt_av1_pick_filter_level(FULL_IMAGE) + svt_av1_loop_filter_frame
+ *   svt_av1_loop_filter_init + svt_av1_pick_filter_level(FULL_IMAGE) + svt_av1_loop_filter_frame, or at the SB-based
+ *   DLF levels (3-5) the encode loop's pick_filter_level(FROM_Q) + svt_aom_loop_filter_sb per SB in raster order
  *   svt_aom_link_eb_to_aom_buffer_desc + svt_av1_loop_restoration_save_boundary_lines(after_cdef = 0)
  *   cdef_seg_search (per segment) + finish_cdef_search + svt_av1_cdef_frame
  *   svt_av1_loop_restoration_save_boundary_lines(after_cdef = 1)
@@ -35,6 +36,10 @@
 #include "golden_io.h"
 
 void        svt_av1_loop_filter_init(PictureControlSet *pcs);
+void        svt_aom_loop_filter_sb(EbPictureBufferDesc *frame_buffer, PictureControlSet *pcs, int32_t mi_row,
+                                   int32_t mi_col, int32_t plane_start, int32_t plane_end, uint8_t last_col);
+void        svt_av1_loop_filter_frame_init(FrameHeader *frm_hdr, LoopFilterInfoN *lf_info, int32_t plane_start,
+                                           int32_t plane_end);
 void        svt_av1_loop_filter_frame(EbPictureBufferDesc *frame_buffer, PictureControlSet *pcs, int32_t plane_start,
                                       int32_t plane_end);
 EbErrorType qp_based_dlf_param(PictureControlSet *pcs, int32_t *filter_level_y, int32_t *filter_level_uv);
@@ -283,7 +288,8 @@ void bind_check_me_md_frame(void) {
 enum {
     I_MAGIC, I_W, I_H, I_BD, I_Q, I_CDEF_LVL, I_DLF_LVL, I_WN_LVL, I_SG_LVL, I_LF0, I_LF1, I_LFU, I_LFV, I_SHARP,
     I_MRD, I_TL, I_FRAME_TYPE, I_UPDATE_TYPE, I_HIER, I_RDMULT, I_SW0, I_SW1, I_SW2, I_WC0, I_WC1, I_SC0, I_SC1,
-    I_US_Y, I_US_UV, I_CDEF_SC, I_CDEF_SR, I_REST_SC, I_REST_SR, I_ONLY4X4, I_SB, I_PRED_Y, I_PRED_UV, I_COUNT = 64
+    I_US_Y, I_US_UV, I_CDEF_SC, I_CDEF_SR, I_REST_SC, I_REST_SR, I_ONLY4X4, I_SB, I_PRED_Y, I_PRED_UV, I_MESAD,
+    I_IN_RES, I_SLICE_TYPE, I_COUNT = 64
 };
 #define PIPE_MAGIC 0x45504950
 
@@ -490,8 +496,30 @@ static int run_pipe(const char *in_path, const char *out_path) {
     GoldenFile g = golden_open(out_path);
     golden_put1(&g, "header", 'i', I_COUNT, hdr);
 
-    /* ---- DLF (EbDlfProcess.c:96-106) ---- */
-    if (ppcs->dlf_ctrls.enabled) {
+    /* ---- DLF (EbDlfProcess.c:96-106), or the SB-based DLF of the encode loop (EbCodingLoop.c:2260-2281) ---- */
+    if (ppcs->dlf_ctrls.enabled && ppcs->dlf_ctrls.sb_based_dlf) {
+        /* LPF_PICK_FROM_Q: no listed references (their levels never force 0), every SB's ME distortion = I_MESAD */
+        pcs->slice_type        = (SliceType)hdr[I_SLICE_TYPE];
+        ppcs->input_resolution = (EbInputResolution)hdr[I_IN_RES];
+        ppcs->tot_ref_frame_types = 0;
+        const int nsb64        = ((W + 63) / 64) * ((H + 63) / 64);
+        pcs->b64_total_count   = (uint16_t)nsb64;
+        ppcs->rc_me_distortion = calloc((size_t)nsb64, sizeof(uint32_t));
+        for (int b = 0; b < nsb64; b++) ppcs->rc_me_distortion[b] = (uint32_t)hdr[I_MESAD];
+        /* the encode loop's order: SBs in raster order, each filtered right after its own coding */
+        for (int sy = 0; sy < H; sy += SB)
+            for (int sx = 0; sx < W; sx += SB) {
+                if (sx == 0 && sy == 0) {
+                    svt_av1_loop_filter_init(pcs);
+                    svt_av1_pick_filter_level(ppcs->enhanced_pic, pcs, LPF_PICK_FROM_Q);
+                    svt_av1_loop_filter_frame_init(fh, &ppcs->lf_info, 0, 3);
+                }
+                if (lf->filter_level[0] || lf->filter_level[1]) {
+                    const int sbw = SB < W - sx ? SB : W - sx;
+                    svt_aom_loop_filter_sb(recon, pcs, sy >> 2, sx >> 2, 0, 3, (uint8_t)(sx + sbw == W));
+                }
+            }
+    } else if (ppcs->dlf_ctrls.enabled) {
         svt_av1_loop_filter_init(pcs);
         svt_av1_pick_filter_level(ppcs->enhanced_pic, pcs, LPF_PICK_FROM_FULL_IMAGE);
         svt_av1_loop_filter_frame(recon, pcs, 0, 3);

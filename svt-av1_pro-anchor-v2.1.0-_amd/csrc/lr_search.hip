@@ -1455,6 +1455,42 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 struct SgSpec {
     int32_t live1, live3;
 };
+// the speculative tree of depth_nodes nodes below d's pending candidate: node n's xq pair at cd[2n], the mask of the
+// nodes built (tree: SG_NC / 2 nodes of scratch)
+__device__ uint32_t sgr_tree(const Descent &d, int depth_nodes, int32_t *cd, Descent *tree) {
+    uint32_t mask = 1;
+    decode_xq(d, cd);
+    tree[0] = d;
+    for (int nd = 0; nd < SG_NC / 2; nd++) {
+        if (!(mask >> nd & 1) || 2 * nd + 1 >= depth_nodes) continue;
+        for (int w = 1; w >= 0; w--) {
+            if (w && tree[nd].init) continue; // the seed's outcome does not steer the descent
+            Descent c = tree[nd];
+            c.report_outcome(w != 0, 0);
+            if (!c.next()) continue;
+            const int ch = 2 * nd + (w ? 1 : 2);
+            decode_xq(c, cd + 2 * ch);
+            mask |= 1u << ch;
+            if (ch < SG_NC / 2) tree[ch] = c;
+        }
+    }
+    return mask;
+}
+
+// the descent's steps through an evaluated tree (errors by node): exactly the reference's decisions, stopping at the
+// first candidate that was not evaluated (the next root) or at the end of the descent
+template <typename ErrAt>
+__device__ void sgr_replay(Descent &d, uint32_t evaluated, ErrAt &&err_at) {
+    for (int node = 0;;) {
+        const int64_t v     = err_at(node);
+        const bool    worse = !d.init && v > d.err;
+        d.report(v);
+        if (!d.next()) break;
+        node = 2 * node + (worse ? 1 : 2);
+        if (node >= SG_NC || !(evaluated >> node & 1)) break;
+    }
+}
+
 // one step of descent i: replay the evaluated tree against its errors, then build the next tree of depth_nodes nodes;
 // returns 1 when the descent stays live
 // (tree: SG_NC / 2 nodes of scratch -- LDS in the queue kernels, where registers are scarce)
@@ -1467,36 +1503,11 @@ __device__ int sgr_descent_step(Descent *ds, int i, unsigned long long *err, int
     if (first) {
         d.next(); // the seed itself is the first candidate
     } else {
-        const uint32_t evaluated = ld_shared<SHARED>(candm + i);
-        for (int node = 0;;) {
-            const int64_t v     = (int64_t)ld64<SHARED>(e + node);
-            const bool    worse = !d.init && v > d.err;
-            d.report(v);
-            if (!d.next()) break;
-            node = 2 * node + (worse ? 1 : 2);
-            if (node >= SG_NC || !(evaluated >> node & 1)) break;
-        }
+        sgr_replay(d, ld_shared<SHARED>(candm + i), [&](int node) { return (int64_t)ld64<SHARED>(e + node); });
     }
     for (int c = 0; c < SG_NC; c++) e[c] = 0;
     if (!d.done) {
-        uint32_t  mask = 1;
-        int32_t  *cd   = cand + (size_t)i * SG_NC * 2;
-        decode_xq(d, cd);
-        tree[0] = d;
-        for (int nd = 0; nd < SG_NC / 2; nd++) {
-            if (!(mask >> nd & 1) || 2 * nd + 1 >= depth_nodes) continue;
-            for (int w = 1; w >= 0; w--) {
-                if (w && tree[nd].init) continue; // the seed's outcome does not steer the descent
-                Descent c = tree[nd];
-                c.report_outcome(w != 0, 0);
-                if (!c.next()) continue;
-                const int ch = 2 * nd + (w ? 1 : 2);
-                decode_xq(c, cd + 2 * ch);
-                mask |= 1u << ch;
-                if (ch < SG_NC / 2) tree[ch] = c;
-            }
-        }
-        candm[i] = mask;
+        candm[i] = sgr_tree(d, depth_nodes, cand + (size_t)i * SG_NC * 2, tree);
         ds[i]    = d;
         return 1;
     }
@@ -1614,17 +1625,23 @@ __global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, i
 
 // svt_get_proj_subspace_c (:417-500) from the exact integer moments, encode_xq (:502-518), and the descent of
 // finer_search_pixel_proj_error (:320-413) seeded there; one lane per (unit, ep)
+__device__ Descent sgr_seed(const SearchArgs &A, int p, int i, const int64_t *m, const SeedCfg &cfg);
+
 __global__ void sgr_seed_kernel(const SearchArgs A, int nplanes, int npairs, const int64_t *mom, const SeedCfg cfg,
                                 Descent *ds) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npairs) return;
     int p = 0;
     while (p + 1 < nplanes && i >= A.pl[p + 1].pair_base) p++;
+    ds[i] = sgr_seed(A, p, i, mom + (size_t)i * 5, cfg);
+}
+
+// pair i (plane p) from its moments m[5] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s}: the seeded descent
+__device__ Descent sgr_seed(const SearchArgs &A, int p, int i, const int64_t *m, const SeedCfg &cfg) {
     const PlaneArgs &P  = A.pl[p];
     const int        ul = (i - P.pair_base) / P.ne, k = (i - P.pair_base) % P.ne, ep = P.eps[k];
     const URect      ur = A.units[P.unit_base + ul];
     const double     size = (double)((ur.h_end - ur.h_start) * (ur.v_end - ur.v_start));
-    const int64_t   *m    = mom + (size_t)i * 5;
     double H00 = (double)m[0], H11 = (double)m[1], H01 = (double)m[2], C0 = (double)m[3], C1 = (double)m[4];
     H00 /= size, H01 /= size, H11 /= size;
     const double H10 = H01;
@@ -1660,7 +1677,7 @@ __global__ void sgr_seed_kernel(const SearchArgs A, int nplanes, int npairs, con
     d.skipm = (r0 == 0 ? 1u : 0u) | (r1 == 0 ? 2u : 0u);
     d.set_val(0, 0, xd0), d.set_val(0, 1, xd1);
     d.begin();
-    ds[i] = d;
+    return d;
 }
 
 // best ep per unit (strict <, first) -> best[unit] = {ep index, ep, xq0, xq1}
@@ -1680,6 +1697,306 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
     best[4 * u + 1] = ep;
     best[4 * u + 2] = c_sgr_r[ep][0] == 0 ? 0 : x0;
     best[4 * u + 3] = c_sgr_r[ep][0] == 0 ? 128 - x1 : c_sgr_r[ep][1] == 0 ? 0 : 128 - x0 - x1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The self-guided search of one (unit, ep) per workgroup with the unit resident on the CU (default).
+// search_selfguided_restoration (EbRestorationPick.c:550-652) per ep: the projection subspace from the filtered unit
+// (svt_get_proj_subspace, :417-500), encode_xq, then finer_search_pixel_proj_error's descent (:320-411), every
+// candidate a pass over all the unit's pixels.  The filter planes of the ep (sgr_flt_kernel) are read exactly once.
+// A workgroup is 15 pixel waves and one control wave:
+//   * pixel lane l (0..959) owns 4-pixel chunks l, l + 960, ... of the unit (row-major over 4-pixel columns), at most
+//     SR_KMAX of them: g = (flt0 - u, flt1 - u) packed int16 per pixel in registers (72 VGPRs), the (x - src) pairs
+//     in LDS (135 KB); chunks past the unit hold zeros, which add nothing to any sum.  The pixel waves form the five
+//     projection moments (exact 64-bit sums, as sgr_mom_kernel) while loading, and per pass the errors of the
+//     pending candidates -- per pixel and candidate one v_dot2 with the rounding and (x - src) * 2^11 terms in its
+//     accumulator, a shift, a multiply-add;
+//   * the control wave holds the descent in registers and steps it between the passes, lane-parallel: lane c sums
+//     candidate c's wave partials (and exchanges it with the other row parts), every lane replays the evaluated tree
+//     (sgr_replay: the reference's decisions), and lane n builds node n of the next speculative tree by applying the
+//     outcomes on its path to the root (the per-round path's sgr_tree, one node per lane); lane 0 seeds the descent
+//     from the moments (sgr_seed: the reference's double arithmetic).  Two workgroup barriers per pass, nothing in
+//     global memory, and the pixel waves' registers are never live in the control code;
+//   * units larger than SR_MAX_PX (the frame's bottom luma unit row, 256 x 376 at 4K) are cut into row parts on
+//     workgroups adjacent in their XCD's dispatch order; their moments and candidate errors meet through uncached
+//     memory each pass (tagged 64-bit words, double-buffered by pass parity, bounded waits), every part taking the
+//     same steps.
+// The pass count is bounded (SR_MAX_PASSES; a descent ends far earlier): on overflow or a timed-out exchange the
+// descent stops and *status is set, which search_frame reports as SVTGPU_ERR_HIP.
+// ---------------------------------------------------------------------------------------------
+constexpr int SR_NT = 1024, SR_PW = 15, SR_PL = SR_PW * 64, SR_KMAX = 18, SR_MAX_PX = SR_PL * SR_KMAX * 4;
+constexpr int SR_MAX_PASSES = 4096, SR_MAX_PARTS = 8;
+constexpr int SR_LDS = SR_KMAX * SR_PL * 8; // the (x - src) pairs of the part
+struct SrItem {
+    int32_t pair, y0, y1, part, nparts, first; // rows [y0, y1) of the pair's unit; part q at grid position first + 8 q
+};
+constexpr unsigned long long SR_LOW = (1ull << 48) - 1;
+
+// one lane's value of exchange round r, summed over the row parts (this part's value published first).  Every value
+// fits 48 bits two's complement: a part holds <= 2^17 pixels, g in [-16368, 32767], |s| < 2^14, and a projection
+// error |e| <= (352 * 32767 + 2^21) / 2^11 < 6657 (|xq0| <= 96, |xq1| <= 256), e^2 < 2^26.  false: timed out
+__device__ bool sr_exchange_lane(unsigned long long *xch, const SrItem &it, int r, int q, long long &v,
+                                 int32_t *status) {
+    const unsigned long long tag = (unsigned long long)((r + 1) & 0xFFFF) << 48;
+    __hip_atomic_store(xch + ((size_t)(it.first + 8 * it.part) * 2 + (r & 1)) * 8 + q, tag | ((unsigned long long)v & SR_LOW),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long add = 0;
+    for (int p = 0; p < it.nparts; p++) {
+        if (p == it.part) continue;
+        const unsigned long long *o = xch + ((size_t)(it.first + 8 * p) * 2 + (r & 1)) * 8 + q;
+        for (unsigned spin = 0;; spin++) {
+            const unsigned long long w = __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((w & ~SR_LOW) == tag) {
+                add += (long long)(w << 16) >> 16;
+                break;
+            }
+            if (spin > (1u << 24)) { // ~seconds: never wait forever
+                atomicOr(status, 2);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    v += add;
+    return true;
+}
+
+// control wave: node n (= this lane) of the speculative tree below d's pending candidate -- the root's state with the
+// outcomes on the path to n applied (children of m: 2m + 1 after a worse outcome, 2m + 2 otherwise); nodes exist up
+// to SG_NC, a node's children only below SG_NC / 2, and the seed's outcome does not steer the descent.  The tree's
+// candidates go to s_xq compacted in node order, the node mask to *s_mask, the count to *s_nv (0: the descent ended)
+__device__ __forceinline__ void sr_tree_lanes(const Descent &d, bool live, int nodes, uint32_t *s_xq, uint32_t *s_mask,
+                                              int *s_nv) {
+    const int n  = threadIdx.x & 63;
+    bool      ok = live && n < nodes; // nodes: 1, 3 or SG_NC (a complete tree)
+    uint32_t  xv = 0;
+    if (ok) {
+        int path = 0, depth = 0; // outcome bits from the node up to the root
+        for (int m = n; m > 0; m = (m - 1) >> 1) path |= (m & 1) << depth++;
+        Descent c = d;
+        for (int i = depth - 1; i >= 0 && ok; i--) {
+            const bool worse = path >> i & 1;
+            if (worse && c.init) ok = false;
+            else {
+                c.report_outcome(worse, 0);
+                ok = c.next();
+            }
+        }
+        int32_t x[2];
+        decode_xq(c, x);
+        xv = pack2(x[0], x[1]);
+    }
+    const unsigned long long mask = __ballot(ok);
+    if (ok) s_xq[__popcll(mask & ((1ull << n) - 1))] = xv;
+    if (n == 0) *s_mask = (uint32_t)mask, *s_nv = (int)__popcll(mask);
+}
+
+// one pass over the resident pixels: the errors of the first nv (<= NV) candidates, wave totals into s_red[wave].
+// Candidates past nv are evaluated with xq = 0 and dropped (NV = nv up to 4; 7 for trees of 5-7 nodes).
+template <int NV>
+__device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const uint2 *dx, int pl, int K, int nv,
+                                        const uint32_t *s_xq, unsigned long long (*s_red)[SG_NC]) {
+    uint32_t xq[NV], acc[NV];
+#pragma unroll
+    for (int c = 0; c < NV; c++) xq[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(c < nv ? s_xq[c] : 0u)), acc[c] = 0;
+#pragma unroll
+    for (int kk = 0; kk < SR_KMAX; kk++) {
+        if (kk < K) { // uniform
+            const uint2 dw = dx[kk * SR_PL + pl];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t w  = q < 2 ? dw.x : dw.y;
+                const int      d1 = (q & 1) ? (int)w >> 16 : (int)(w << 16) >> 16;
+                const int      c0 = 1024 + d1 * 2048; // floor((v + 1024) / 2^11) + (x - src) == (v + c0) >> 11
+#pragma unroll
+                for (int c = 0; c < NV; c++) {
+                    const int ee = dot2(g[kk][q], xq[c], c0) >> 11;
+                    acc[c] += (uint32_t)(ee * ee);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NV; c++)
+        if (c < nv) {
+            const unsigned long long t = wave_sum_u32_wide(acc[c]); // <= 72 e^2 < 2^32 per lane
+            if ((pl & 63) == WAVE_LAST) s_red[pl >> 6][c] = t;
+        }
+}
+
+template <typename T>
+__global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
+                                                        const SeedCfg cfg, int nodes, Descent *ds,
+                                                        unsigned long long *xch, int32_t *status,
+                                                        unsigned long long *stat, unsigned long long *tk) {
+    PROF_BEGIN(tk);
+    extern __shared__ uint2 sr_dx[];                   // [chunk k][pixel lane]: (x - src) of pixels 0, 1 | 2, 3 (int16)
+    __shared__ unsigned long long s_red[SR_PW][SG_NC]; // wave partials: the moments, then each pass's errors
+    __shared__ uint32_t           s_xq[SG_NC];         // the pending tree's candidates (xq pairs), compacted
+    __shared__ uint32_t           s_mask;              // its nodes
+    __shared__ int                s_nv;                // its candidate count (0: the descent has ended)
+    const SrItem it = items[blockIdx.x];
+    if (it.pair < 0) return; // an empty slot of the XCD-ordered grid (uniform)
+    int p = 0;
+    while (p + 1 < nplanes && it.pair >= A.pl[p + 1].pair_base) p++;
+    const PlaneArgs &P  = A.pl[p];
+    const int        ul = (it.pair - P.pair_base) / P.ne, k = it.pair - P.pair_base - ul * P.ne, ep = P.eps[k];
+    const URect      ur = A.units[P.unit_base + ul];
+    const int        cw = (ur.h_end - ur.h_start) >> 2, nch = cw * (it.y1 - it.y0), K = (nch + SR_PL - 1) / SR_PL;
+    if (K > SR_KMAX || nch <= 0) { // the host plans parts of <= SR_MAX_PX pixels; never index past the registers
+        if (threadIdx.x == 0) atomicOr(status, 4);
+        return;
+    }
+    if (threadIdx.x < SR_PL) {
+        // ================= pixel waves =================
+        const int      pl = threadIdx.x, r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
+        const T       *d = (const T *)P.dgd, *s = (const T *)P.src;
+        const size_t   pn = (size_t)P.fstride * P.H;
+        // an ep without one of the filters reads a plane that holds no data: its g half is zeroed
+        const int16_t *f0 = P.flt + (size_t)k * 2 * pn, *f1 = P.flt + (size_t)P.f1e[k] * 2 * pn + pn;
+        const uint32_t gmask = (r0 ? 0x0000FFFFu : 0u) | (r1 ? 0xFFFF0000u : 0u);
+        // ---- load the part: g in registers, (x - src) in LDS, the moments on the way ----
+        uint32_t           g[SR_KMAX][4];
+        unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
+#pragma unroll
+        for (int kb = 0; kb < SR_KMAX; kb += 3) {
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) g[kb + j][q] = 0u;
+            if (kb >= K) continue; // uniform
+            int2 dv2[3], sv2[3], a0[3], a1[3];
+            bool on[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) { // all loads of 3 chunks in flight together (addresses clamped into the part)
+                const int c = pl + (kb + j) * SR_PL, cc = min(c, nch - 1), row = cc / cw, col = cc - row * cw;
+                const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
+                on[j] = c < nch;
+                const size_t fo = (size_t)y * P.fstride + x;
+                if constexpr (sizeof(T) == 2) {
+                    dv2[j] = *(const int2 *)(d + (size_t)y * P.dstride + x);
+                    sv2[j] = *(const int2 *)(s + (size_t)y * P.sstride + x);
+                } else {
+                    dv2[j].x = *(const int *)(d + (size_t)y * P.dstride + x), dv2[j].y = 0;
+                    sv2[j].x = *(const int *)(s + (size_t)y * P.sstride + x), sv2[j].y = 0;
+                }
+                a0[j] = *(const int2 *)(f0 + fo);
+                a1[j] = *(const int2 *)(f1 + fo);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int kk = kb + j;
+                int       dv[4], sv[4];
+                if constexpr (sizeof(T) == 2) {
+                    dv[0] = dv2[j].x & 0xFFFF, dv[1] = (uint32_t)dv2[j].x >> 16, dv[2] = dv2[j].y & 0xFFFF, dv[3] = (uint32_t)dv2[j].y >> 16;
+                    sv[0] = sv2[j].x & 0xFFFF, sv[1] = (uint32_t)sv2[j].x >> 16, sv[2] = sv2[j].y & 0xFFFF, sv[3] = (uint32_t)sv2[j].y >> 16;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) dv[q] = ((uint32_t)dv2[j].x >> (8 * q)) & 0xFF, sv[q] = ((uint32_t)sv2[j].x >> (8 * q)) & 0xFF;
+                }
+                const uint32_t fw[4] = {__builtin_amdgcn_perm((uint32_t)a1[j].x, (uint32_t)a0[j].x, 0x05040100u),
+                                        __builtin_amdgcn_perm((uint32_t)a1[j].x, (uint32_t)a0[j].x, 0x07060302u),
+                                        __builtin_amdgcn_perm((uint32_t)a1[j].y, (uint32_t)a0[j].y, 0x05040100u),
+                                        __builtin_amdgcn_perm((uint32_t)a1[j].y, (uint32_t)a0[j].y, 0x07060302u)};
+                uint32_t m0 = 0, m1 = 0; // <= 4 g^2 < 2^32
+                int      m3 = 0, m4 = 0; // |4 g s| < 2^31
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    // g = (flt0 - u, flt1 - u) on packed 16-bit lanes (|g| < 2^15: the wrapped halves are exact)
+                    const uint32_t gq = on[j] ? pk_sub16(fw[q], __umul24((uint32_t)dv[q], 0x00100010u)) & gmask : 0u;
+                    const int      g1 = (int)(int16_t)(gq & 0xFFFF), g2 = (int)gq >> 16, ss = (sv[q] - dv[q]) << 4;
+                    m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
+                    m3 += g1 * ss, m4 += g2 * ss;
+                    M2 += (unsigned long long)(long long)(g1 * g2);
+                    g[kk][q] = gq;
+                }
+                M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
+                sr_dx[kk * SR_PL + pl] = on[j] ? make_uint2(pack2(dv[0] - sv[0], dv[1] - sv[1]), pack2(dv[2] - sv[2], dv[3] - sv[3]))
+                                               : make_uint2(0u, 0u);
+            }
+        }
+        {
+            const unsigned long long t[5] = {wave_sum_u64_limbs(M0), wave_sum_u64_limbs(M1), wave_sum_u64_limbs(M2),
+                                             wave_sum_u64_limbs(M3), wave_sum_u64_limbs(M4)};
+            if ((pl & 63) == WAVE_LAST)
+#pragma unroll
+                for (int q = 0; q < 5; q++) s_red[pl >> 6][q] = t[q];
+        }
+        __syncthreads(); // B1: the moments are in s_red
+        __syncthreads(); // B2: the first tree is in s_xq
+        for (;;) {
+            const int nv = __builtin_amdgcn_readfirstlane(s_nv);
+            if (nv == 0) break;
+            switch (nv) {
+            case 1: sr_pass<1>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            case 2: sr_pass<2>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            case 3: sr_pass<3>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            case 4: sr_pass<4>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            default: sr_pass<SG_NC>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            }
+            __syncthreads(); // B3: the pass's errors are in s_red
+            __syncthreads(); // B4: the next tree (or the end) is in s_xq / s_nv
+        }
+    } else {
+        // ================= control wave =================
+        // stat (SVTGPU_SR_STATS diagnostics, else null): items, passes, candidate-pixels, load / descent / control
+        // ticks (100 MHz), pixels
+        const int                lane = threadIdx.x & 63;
+        const unsigned long long t0   = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+        unsigned long long       tctl = 0, ncp = 0;
+        __syncthreads(); // B1
+        const unsigned long long t1 = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+        long long v  = 0; // lane q < 5: moment q over the workgroup (and the other row parts)
+        bool      ok = true;
+        if (lane < 5) {
+            unsigned long long t = 0;
+            for (int w = 0; w < SR_PW; w++) t += s_red[w][lane];
+            v = (long long)t;
+            if (it.nparts > 1) ok = sr_exchange_lane(xch, it, 0, lane, v, status);
+        }
+        ok = __ballot(!ok) == 0;
+        long long mv[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) mv[q] = __shfl(v, q, 64);
+        Descent D = sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg); // the same in every lane
+        D.next(); // the seed itself is the first candidate
+        sr_tree_lanes(D, ok, nodes, s_xq, &s_mask, &s_nv);
+        __syncthreads(); // B2
+        for (int pass = 1;; pass++) {
+            const int nv = __builtin_amdgcn_readfirstlane(s_nv);
+            if (nv == 0) break;
+            const uint32_t mask = __builtin_amdgcn_readfirstlane(s_mask);
+            __syncthreads(); // B3
+            const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+            ncp += (unsigned long long)nv * nch * 4;
+            long long e = 0; // lane c < nv: compacted candidate c's error
+            ok = true;
+            if (lane < nv) {
+                unsigned long long t = 0;
+                for (int w = 0; w < SR_PW; w++) t += s_red[w][lane];
+                e = (long long)t;
+                if (it.nparts > 1) ok = sr_exchange_lane(xch, it, pass, lane, e, status);
+            }
+            ok = __ballot(!ok) == 0;
+            if (pass > SR_MAX_PASSES) {
+                if (lane == 0) atomicOr(status, 1);
+                ok = false;
+            }
+            if (ok) // the same steps in every lane
+                sgr_replay(D, mask, [&](int node) { return (int64_t)__shfl(e, __popc(mask & ((1u << node) - 1)), 64); });
+            sr_tree_lanes(D, ok && !D.done, nodes, s_xq, &s_mask, &s_nv);
+            if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
+            __syncthreads(); // B4
+            if (stat && lane == 0 && s_nv == 0) atomicAdd(stat + 1, (unsigned long long)pass);
+        }
+        if (lane == 0 && it.part == 0) ds[it.pair] = D;
+        if (stat && lane == 0) {
+            atomicAdd(stat + 0, 1ull), atomicAdd(stat + 2, ncp), atomicAdd(stat + 3, t1 - t0);
+            atomicAdd(stat + 4, __builtin_amdgcn_s_memrealtime() - t1), atomicAdd(stat + 5, tctl);
+            atomicAdd(stat + 6, (unsigned long long)nch * 4);
+        }
+    }
+    PROF_END(tk);
 }
 
 struct Carver {
@@ -1882,6 +2199,35 @@ int wr_lds_cap() {
     return v;
 }
 
+// the resident self-guided search (default); SVTGPU_SG_RES=0 selects the per-round path (A/B measurements)
+bool use_sg_res() {
+    static const bool v = [] {
+        const char *e = std::getenv("SVTGPU_SG_RES");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
+
+// largest row part of the resident self-guided search (pixels); SVTGPU_SR_PART_PX lowers it (tests of the parted path)
+int sr_part_px() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_SR_PART_PX");
+        return e ? std::max(64, std::min(std::atoi(e), SR_MAX_PX)) : SR_MAX_PX;
+    }();
+    return v;
+}
+
+// candidates per pass of the resident self-guided search: a complete speculative tree of 1, 3 or 7 nodes
+// (SVTGPU_SR_TREE for A/B measurements)
+int sr_tree_nodes() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_SR_TREE");
+        const int   n = e ? std::atoi(e) : SG_NC;
+        return n == 1 || n == 3 ? n : SG_NC;
+    }();
+    return v;
+}
+
 // plane p's Wiener window for the controls
 int plane_win(const SvtGpuLrSearchControls *c, int p) {
     const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
@@ -1993,17 +2339,63 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
     }
     const int n_wr = (int)wr_items.size();
+    // The resident self-guided search (sgr_res_kernel): one item per (unit row part, ep).  Workgroups are dealt
+    // round-robin over the 8 XCDs (block b on XCD b mod 8), so the grid is laid out as 8 lanes (positions r, r + 8, ...):
+    // a unit's items -- its eps, and the row parts of each -- go to one lane, consecutively.  The eps of a unit then
+    // read its CDEF and source samples through one L2, and the parts of an item sit next to each other in their XCD's
+    // in-order dispatch, so a waiting part's partners are always dispatched after it (never behind other waiting
+    // parts).  Units are dealt largest first to the lane with the least work; empty slots (pair -1) pad the lanes.
+    const bool           sg_res = use_sg_res();
+    std::vector<SrItem>  sr_items;
+    bool                 sr_parted = false;
+    if (sg_res && npairs) {
+        std::vector<std::vector<SrItem>> lanes(8);
+        std::vector<long long>           load(8, 0);
+        std::vector<int>                 ord;
+        for (int p = 0; p < nplanes; p++)
+            if (pp[p].sg)
+                for (int u = 0; u < pp[p].n; u++) ord.push_back(pp[p].unit_base + u);
+        auto area = [&](int u) { return (long long)(units[u].h_end - units[u].h_start) * (units[u].v_end - units[u].v_start); };
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return area(a) > area(b); });
+        for (int u : ord) {
+            int p = 0;
+            while (p + 1 < nplanes && u >= pp[p + 1].unit_base) p++;
+            const PlanePlan &q = pp[p];
+            const int        cw = (units[u].h_end - units[u].h_start) >> 2, h = units[u].v_end - units[u].v_start;
+            const int        maxrows = std::max(1, sr_part_px() / 4 / std::max(cw, 1)), np = (h + maxrows - 1) / maxrows;
+            if (np > SR_MAX_PARTS) return SVTGPU_ERR_UNSUPPORTED; // a unit wider than 1024 x 4 samples per row part
+            sr_parted |= np > 1;
+            const int lane = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            for (int k = 0; k < q.ne; k++) {
+                const int first = (int)lanes[lane].size(); // lane-local; made global below
+                for (int part = 0; part < np; part++)
+                    lanes[lane].push_back({q.pair_base + (u - q.unit_base) * q.ne + k, h * part / np, h * (part + 1) / np,
+                                           part, np, first});
+            }
+            load[lane] += area(u) * q.ne;
+        }
+        size_t len = 0;
+        for (auto &l : lanes) len = std::max(len, l.size());
+        sr_items.assign(8 * len, SrItem{-1, 0, 0, 0, 1, 0});
+        for (int r = 0; r < 8; r++)
+            for (size_t m = 0; m < lanes[r].size(); m++) {
+                SrItem it = lanes[r][m];
+                it.first  = 8 * it.first + r; // parts of an item: positions first, first + 8, ...
+                sr_items[8 * m + r] = it;
+            }
+    }
+    const int n_sr = (int)sr_items.size();
     // ---- device scratch and pinned staging ----
     // three contiguous spans keep the host traffic to one copy each: the plan (uploaded when it changes), the
     // accumulators zeroed per search, the results read back (o_sse is the last zeroed and the first read)
     Carver       dc;
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
-                 o_witem = dc(sizeof(WrItem) * (size_t)n_wr);
+                 o_witem = dc(sizeof(WrItem) * (size_t)n_wr), o_sritem = dc(sizeof(SrItem) * (size_t)n_sr);
     const size_t plan_span = dc.off;
     const size_t o_sum = dc(8 * n_all), o_mom = dc(40 * (size_t)npairs), o_sse = dc(8 * n_all);
     const size_t zero_span = dc.off - o_sum;
     const size_t o_sse2 = dc(8 * (size_t)n_sg), o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
-                 o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8);
+                 o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8), o_sstat = dc(8);
     const size_t res_span = dc.off - o_sse;
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
     const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
@@ -2011,7 +2403,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                  o_best = dc(16 * (size_t)n_sg), o_cnt = dc(32);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
-    const size_t q_wrx = qc(16 * (size_t)n_wr);
+    const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
@@ -2073,6 +2465,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         std::memcpy(pl + o_units, units.data(), sizeof(URect) * n_all);
         std::memcpy(pl + o_t0, tile0.data(), 4 * (n_all + 1));
         std::memcpy(pl + o_witem, wr_items.data(), sizeof(WrItem) * (size_t)n_wr);
+        std::memcpy(pl + o_sritem, sr_items.data(), sizeof(SrItem) * (size_t)n_sr);
         if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
             std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
             HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
@@ -2126,9 +2519,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (nt_sg) {
         run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
-        run(5, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(sgr_mom_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (long long *)dp(o_mom), tk);
-        });
+        if (!sg_res)
+            run(5, [&](unsigned long long *tk) {
+                hipLaunchKernelGGL(sgr_mom_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (long long *)dp(o_mom), tk);
+            });
         HIP_TRY(hipGetLastError());
     }
     mark(0);
@@ -2143,7 +2537,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
     }
-    if (npairs) {
+    if (npairs && !sg_res) {
         run(4, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_seed_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, A, sg_planes, npairs,
                                (const int64_t *)dp(o_mom), cfg, (Descent *)dp(o_sds));
@@ -2153,7 +2547,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     mark(1);
     // ---- phase 3: descent rounds on the device ----
     uint8_t *qa = nullptr;
-    if (n_wn && wr_parted) {
+    if ((n_wn && wr_parted) || (n_sr && sr_parted)) {
         if (qc.off > s->qarena_bytes) {
             if (s->d_qarena) (void)hipFree(s->d_qarena);
             s->d_qarena = nullptr, s->qarena_bytes = 0;
@@ -2172,7 +2566,21 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
     }
-    if (npairs) {
+    static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
+    static unsigned long long *sr_stat = nullptr;
+    if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 64));
+    if (n_sr) { // the whole self-guided search of every (unit, ep), resident on one CU each (or a few)
+        HIP_TRY(hipMemsetAsync(dp(o_sstat), 0, 8, st));
+        if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 64, st));
+        if (sr_parted) HIP_TRY(hipMemsetAsync(qa + q_srx, 0, 128 * (size_t)n_sr, st));
+        run(3, [&](unsigned long long *tk) {
+            hipLaunchKernelGGL(sgr_res_kernel<T>, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
+                               (const SrItem *)dp(o_sritem), cfg, sr_tree_nodes(), (Descent *)dp(o_sds),
+                               (unsigned long long *)(sr_parted ? qa + q_srx : nullptr), (int32_t *)dp(o_sstat),
+                               sr_stat, tk);
+        });
+        HIP_TRY(hipGetLastError());
+    } else if (npairs) {
         HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * SG_NC * (size_t)npairs, st));
         HIP_TRY(hipMemsetAsync(dp(o_ustamp), 0, 4 * (size_t)n_all, st));
         hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
@@ -2192,7 +2600,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         hipStream_t stream;
     } ch[2];
     ch[0].live = false, ch[0].stream = sw;
-    ch[1].live = npairs > 0, ch[1].stream = st;
+    ch[1].live = npairs > 0 && !sg_res, ch[1].stream = st;
     if (!s->h_flag) {
         HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipHostGetDevicePointer((void **)&s->h_flag_dev, s->h_flag, 0));
@@ -2305,6 +2713,20 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                                   __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;
     }
+    if (n_sr && sr_stat) {
+        unsigned long long v[8];
+        HIP_TRY(hipMemcpy(v, sr_stat, 64, hipMemcpyDeviceToHost));
+        const double n = (double)std::max(1ull, v[0]);
+        std::fprintf(stderr, "sgr_res: %llu items, %.2f passes/item, %.2f candidates/pass, %.0f px/item, ticks/item "
+                     "load %.2f us, descent %.2f us (control %.2f us)\n", v[0], v[1] / n,
+                     v[1] ? (double)v[2] / (double)v[6] * n / v[1] : 0.0, v[6] / n, v[3] / n * 0.01, v[4] / n * 0.01,
+                     v[5] / n * 0.01);
+    }
+    if (n_sr && *(const int32_t *)hp(h_res + (o_sstat - o_sse))) { // status bits of sgr_res_kernel
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR self-guided descent: pass bound, part plan or exchange failed",
+                                  __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
     mark(3);
     // ---- phase 5 (host): per-unit results and, for the whole frame, the RD finish ----
     const uint64_t                 *sse0 = (const uint64_t *)hp(h_sse), *sse2 = (const uint64_t *)hp(h_sse2);
@@ -2359,7 +2781,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         prof->bps = bps;
         prof->static_bytes[0] += (all + wn) * 2 * bps; // unit sums, statistics: x and source
         prof->static_bytes[1] += sgb * bps + sgw * 2;     // filters: x in, the int16 planes out (each once)
-        prof->static_bytes[5] += sgb * 2 * bps + sgp * 4; // moments: x, source and every ep's two planes in
+        if (sg_res) prof->static_bytes[3] += sgb * 2 * bps + sgp * 4; // resident search: x, source, the planes, once
+        else prof->static_bytes[5] += sgb * 2 * bps + sgp * 4;        // moments: x, source and every ep's two planes in
         prof->static_bytes[4] += sgb * (4 + 2 * bps);     // the chosen ep's SSE
     }
     // no wait for the units upload: the next search waits for this event before it rewrites the pinned staging

@@ -22,7 +22,8 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 MAGIC = 0x45504950
 HEADER = ["magic", "w", "h", "bd", "q", "cdef_level", "dlf_level", "wn_level", "sg_level", "lf0", "lf1", "lfu", "lfv",
           "sharp", "mrd", "tl", "frame_type", "update_type", "hier", "rdmult", "sw0", "sw1", "sw2", "wc0", "wc1", "sc0",
-          "sc1", "us_y", "us_uv", "cdef_sc", "cdef_sr", "rest_sc", "rest_sr", "only4x4", "sb", "pred_y", "pred_uv"]
+          "sc1", "us_y", "us_uv", "cdef_sc", "cdef_sr", "rest_sc", "rest_sr", "only4x4", "sb", "pred_y", "pred_uv",
+          "mesad", "in_res", "slice"]
 HEADER_WORDS = 64
 KEY_FRAME, INTER_FRAME = 0, 1
 KF_UPDATE, LF_UPDATE, GF_UPDATE, ARF_UPDATE, INTNL_ARF_UPDATE = 0, 1, 2, 3, 6
@@ -32,7 +33,8 @@ _BASE = dict(q=160, cdef_level=1, dlf_level=1, wn_level=1, sg_level=1, lf=(16, 1
              ref_deltas=(1, 0, 0, 0, -1, 0, -1, -1), mode_deltas=(0, 0), tl=0, frame_type=INTER_FRAME,
              update_type=ARF_UPDATE, hier=3, rdmult=7000, sw=(300, 700, 900), wc=(250, 800), sc=(250, 900),
              us=(64, 32), cdef_seg=(1, 1), rest_seg=(1, 1), only4x4=0, sb=64, pred=(0, 0),
-             mi=("random", 1, 0.3), seed=1, digest=False)
+             mi=("random", 1, 0.3), seed=1, digest=False, mesad=0, in_res=0, slice=0)
+B_SLICE, P_SLICE, I_SLICE = 0, 1, 2
 
 
 def _case(**kw):
@@ -63,6 +65,18 @@ CASES = {
     # reference filter strengths (use_reference_cdef_fs): no search, strengths from the MDC prediction
     "reffs_10": _case(w=256, h=192, bd=10, q=150, cdef_level=17, pred=(9, 6), mi=("random", 19, 0.4), seed=109),
     "reffs_8": _case(w=200, h=136, bd=8, q=60, cdef_level=11, pred=(0, 0), mi=("random", 20, 0.4), seed=110),
+    # the SB-based DLF levels 3/4/5 (presets M6 and up, EncModeConfig.c:1516-1609): LPF_PICK_FROM_Q levels and the
+    # encode loop's per-SB filter (EbCodingLoop.c:2260-2281) -- ME distortions above / between / below the
+    # zero-strength thresholds (disable_dlf_th, EbDeblockingFilter.c:26) of the level and resolution class
+    "sbdlf10": _case(w=320, h=200, bd=10, q=150, dlf_level=3, mesad=5000, in_res=1, mi=("random", 21, 0.3), seed=111),
+    "sbdlf8_128": _case(w=384, h=256, bd=8, q=200, dlf_level=4, sb=128, mesad=20000, in_res=0, tl=1,
+                        mi=("random128", 22, 0.2), seed=112),
+    "sbdlf10_zero": _case(w=136, h=96, bd=10, q=60, dlf_level=4, mesad=100, in_res=0, mi=("random", 25, 0.3),
+                          seed=115),
+    "sbdlf10_uv0": _case(w=256, h=192, bd=10, q=120, dlf_level=5, mesad=7000, in_res=0, mi=("random", 23, 0.4),
+                         seed=113),
+    "sbdlf8_key": _case(w=200, h=136, bd=8, q=90, dlf_level=3, frame_type=KEY_FRAME, update_type=KF_UPDATE,
+                        slice=I_SLICE, mesad=0, mi=("random", 24, 0.3), seed=114),
     # BASELINE.json configs[1] (1080p 8-bit) and configs[2] (4K 10-bit, the bench workload): digests only
     "c1_1080p8": _case(w=1920, h=1080, bd=8, us=(256, 128), mi=("bench", 0x5EED0002), seed=0x5EED0002,
                        digest=True),
@@ -110,7 +124,8 @@ def header(c):
              update_type=c["update_type"], hier=c["hier"], rdmult=c["rdmult"], sw0=c["sw"][0], sw1=c["sw"][1],
              sw2=c["sw"][2], wc0=c["wc"][0], wc1=c["wc"][1], sc0=c["sc"][0], sc1=c["sc"][1], us_y=c["us"][0],
              us_uv=c["us"][1], cdef_sc=c["cdef_seg"][0], cdef_sr=c["cdef_seg"][1], rest_sc=c["rest_seg"][0],
-             rest_sr=c["rest_seg"][1], only4x4=c["only4x4"], sb=c["sb"], pred_y=c["pred"][0], pred_uv=c["pred"][1])
+             rest_sr=c["rest_seg"][1], only4x4=c["only4x4"], sb=c["sb"], pred_y=c["pred"][0], pred_uv=c["pred"][1],
+             mesad=c["mesad"], in_res=c["in_res"], slice=c["slice"])
     hdr = np.zeros(HEADER_WORDS, np.int32)
     for i, k in enumerate(HEADER):
         hdr[i] = v[k]

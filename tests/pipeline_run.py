@@ -30,6 +30,34 @@ def dlf_ctrls(level):
                 zero_lvl=int(e[5]))
 
 
+def nsb64(c):
+    return ((c["w"] + 63) // 64) * ((c["h"] + 63) // 64)
+
+
+def sb_dlf_params(c, levels):
+    """The loop-filter parameters of the SB-based DLF levels (3-5): svt_av1_pick_filter_level(LPF_PICK_FROM_Q) sets the
+    four levels and zeroes the sharpness (EbDeblockingFilter.c:1147-1150); the per-SB filter of the encode loop
+    (svt_aom_loop_filter_sb in raster order, EbCodingLoop.c:2260-2281) equals the frame filter with those levels:
+    an edge's filter never reads or writes samples past its neighbouring blocks, so no edge sees another's output
+    within a direction whatever the SB order, and every vertical edge of an SB is filtered before the horizontal
+    edges that read its samples in both orders."""
+    from svtgpu import LfParams
+    if c["mrd"]:
+        return LfParams.make(*levels, 0, ref_deltas=c["ref_deltas"], mode_deltas=c["mode_deltas"])
+    return LfParams.make(*levels, 0)
+
+
+def gpu_dlf_pick(dl, R, S, c):
+    """The frame's loop-filter levels on libsvtgpu: the device level search (DLF levels 1, 2) or LPF_PICK_FROM_Q (the
+    SB-based levels 3-5: every SB's ME distortion the case's `mesad`, no listed references)."""
+    import svtgpu
+    dc = dlf_ctrls(c["dlf_level"])
+    if dc["sb_based"]:
+        return sb_dlf_params(c, svtgpu.dlf_pick_by_q(c["bd"], c["q"], c["frame_type"], c["slice"], c["tl"], c["tl"],
+                                                     c["in_res"], dc["zero_lvl"], [c["mesad"]] * nsb64(c), []))
+    return dl.pick(R, S, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"], c["only4x4"])
+
+
 def cdef_ctrl_row(level):
     e = ctrl_tables()["cdef"][level]
     return dict(enabled=int(e[0]), n1=int(e[1]), n2=int(e[2]), ref_fs=int(e[3]), bias=int(e[6]))
@@ -127,8 +155,11 @@ def run_oracle(case):
     src, rec, mi = pc.inputs(case)
     bd, w, h = c["bd"], c["w"], c["h"]
     dc = dlf_ctrls(c["dlf_level"])
-    lfp = oracle.dlf_pick(rec, src, bd, mi, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"],
-                          c["only4x4"])
+    if dc["sb_based"]:  # LPF_PICK_FROM_Q levels (pinned on their own: test_dlf_byq) + the frame filter
+        lfp = sb_dlf_params(c, [int(x) for x in g["lf_levels"]])
+    else:
+        lfp = oracle.dlf_pick(rec, src, bd, mi, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"],
+                              c["only4x4"])
     dlf = oracle.dlf_frame(rec, bd, mi, lfp)
     mask = pc.cdef_mask(mi)
     ctrls = oracle.controls(c["cdef_level"])
@@ -164,8 +195,7 @@ def run_gpu(case, ctx=None):
     R.upload(rec)
     dl = svtgpu.DlfState(ctx, w, h)
     dl.set_mode_info(mi)
-    dc = dlf_ctrls(c["dlf_level"])
-    lfp = dl.pick(R, S, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"], c["only4x4"])
+    lfp = gpu_dlf_pick(dl, R, S, c)
     dl.filter_to(R, D, lfp)
     st = svtgpu.CdefState(ctx, w, h)
     st.set_block_mask(pc.cdef_mask(mi))
@@ -278,8 +308,7 @@ def run_gpu_tiled(case, rank, world, comm, ctx=None):
     dl = svtgpu.DlfState(ctx, w, h)
     dl.set_mode_info(mi)
     dl.set_tile(plan["tile"], plan["dlf_out"], comm)
-    dc = dlf_ctrls(c["dlf_level"])
-    lfp = dl.pick(R, S, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"], c["only4x4"])
+    lfp = gpu_dlf_pick(dl, R, S, c)
     dl.filter_to(R, D, lfp)
     st = svtgpu.CdefState(ctx, w, h)
     st.set_block_mask(pc.cdef_mask(mi))
