@@ -49,7 +49,8 @@ SIMD_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(BENCH_SIMD))
 PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
-     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me $(OUT)/gen_golden_frame
+     $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me $(OUT)/gen_golden_frame \
+     $(OUT)/rtcd_install
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -88,6 +89,14 @@ $(OUT)/rtcd_pipe: oracle/ref_harness/gen_golden_pipe.c oracle/ref_harness/ref_cd
 	    -c oracle/ref_harness/gen_golden_pipe.c -o $(OUT)/obj/bind/gen_golden_pipe.o
 	$(CC) $(CFLAGS) $(OUT)/obj/bind/gen_golden_pipe.o $(filter-out %gen_golden_pipe.c,$(filter %.c,$^)) $(filter %.o,$^) \
 	    -o $@ -Wl,--gc-sections -L$(dir $(SVTGPU_SO)) -lsvtgpu -Wl,-rpath,'$$ORIGIN/../../$(dir $(SVTGPU_SO))' -lm -lpthread
+
+# the install point of the RTCD shims against the reference's own init_fn_ptr (av1me.c): pointer comparisons only,
+# no device call (tests/test_rtcd_bind.py, CPU)
+$(OUT)/rtcd_install: oracle/ref_harness/rtcd_install.c $(OUT)/obj/Lib/Encoder/Codec/av1me.o $(sort $(MD_OBJ) $(C_OBJ)) \
+                     $(SVTGPU_SO)
+	$(CC) $(filter-out -w,$(CFLAGS)) -Iinclude -Werror=incompatible-pointer-types -Werror=discarded-qualifiers \
+	    $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -L$(dir $(SVTGPU_SO)) -lsvtgpu \
+	    -Wl,-rpath,'$$ORIGIN/../../$(dir $(SVTGPU_SO))' -ldl -lm -lpthread
 
 # compile-only check of every shim prototype against the reference's pointer types (tests/test_rtcd_bind.py, CPU)
 bindcheck:

@@ -101,182 +101,18 @@ static void bind_c_kernels(void) {
 }
 
 #ifdef SVTGPU_BIND
-/* rtcd_pipe: the same frame code with every RTCD pointer the path calls bound to libsvtgpu's device shims.  The
- * shim prototypes name the reference's own types (the type hooks of include/svtgpu.h), so every assignment below
- * compiles under -Werror=incompatible-pointer-types without a cast. */
-#define SVTGPU_CDEF_LIST_T CdefList
-#define SVTGPU_BLOCK_SIZE_T BlockSize
-#define SVTGPU_SGR_PARAMS_T SgrParamsType
-#define SVTGPU_CONVOLVE_PARAMS_T ConvolveParams
-#define SVTGPU_BIT_DEPTH_T EbBitDepth
-#include "svtgpu.h"
-static void bind_device_kernels(void) {
-    svt_aom_lpf_horizontal_4               = svtgpu_lpf_horizontal_4;
-    svt_aom_lpf_horizontal_6               = svtgpu_lpf_horizontal_6;
-    svt_aom_lpf_horizontal_8               = svtgpu_lpf_horizontal_8;
-    svt_aom_lpf_horizontal_14              = svtgpu_lpf_horizontal_14;
-    svt_aom_lpf_vertical_4                 = svtgpu_lpf_vertical_4;
-    svt_aom_lpf_vertical_6                 = svtgpu_lpf_vertical_6;
-    svt_aom_lpf_vertical_8                 = svtgpu_lpf_vertical_8;
-    svt_aom_lpf_vertical_14                = svtgpu_lpf_vertical_14;
-    svt_aom_highbd_lpf_horizontal_4        = svtgpu_highbd_lpf_horizontal_4;
-    svt_aom_highbd_lpf_horizontal_6        = svtgpu_highbd_lpf_horizontal_6;
-    svt_aom_highbd_lpf_horizontal_8        = svtgpu_highbd_lpf_horizontal_8;
-    svt_aom_highbd_lpf_horizontal_14       = svtgpu_highbd_lpf_horizontal_14;
-    svt_aom_highbd_lpf_vertical_4          = svtgpu_highbd_lpf_vertical_4;
-    svt_aom_highbd_lpf_vertical_6          = svtgpu_highbd_lpf_vertical_6;
-    svt_aom_highbd_lpf_vertical_8          = svtgpu_highbd_lpf_vertical_8;
-    svt_aom_highbd_lpf_vertical_14         = svtgpu_highbd_lpf_vertical_14;
-    svt_spatial_full_distortion_kernel     = svtgpu_spatial_full_distortion_kernel;
-    svt_full_distortion_kernel16_bits      = svtgpu_full_distortion_kernel16_bits;
-    svt_cdef_filter_block                  = svtgpu_cdef_filter_block;
-    svt_cdef_filter_block_8xn_16           = svtgpu_cdef_filter_block_8xn_16;
-    svt_aom_cdef_find_dir                  = svtgpu_cdef_find_dir;
-    svt_aom_cdef_find_dir_dual             = svtgpu_cdef_find_dir_dual;
-    svt_compute_cdef_dist_16bit            = svtgpu_compute_cdef_dist_16bit;
-    svt_compute_cdef_dist_8bit             = svtgpu_compute_cdef_dist_8bit;
-    svt_search_one_dual                    = svtgpu_search_one_dual;
-    svt_aom_copy_rect8_8bit_to_16bit       = svtgpu_aom_copy_rect8_8bit_to_16bit;
-    svt_av1_wiener_convolve_add_src        = svtgpu_av1_wiener_convolve_add_src;
-    svt_av1_highbd_wiener_convolve_add_src = svtgpu_av1_highbd_wiener_convolve_add_src;
-    svt_av1_selfguided_restoration         = svtgpu_av1_selfguided_restoration;
-    svt_apply_selfguided_restoration       = svtgpu_apply_selfguided_restoration;
-    svt_av1_compute_stats                  = svtgpu_av1_compute_stats;
-    svt_av1_compute_stats_highbd           = svtgpu_av1_compute_stats_highbd;
-    svt_get_proj_subspace                  = svtgpu_get_proj_subspace;
-    svt_av1_lowbd_pixel_proj_error         = svtgpu_av1_lowbd_pixel_proj_error;
-    svt_av1_highbd_pixel_proj_error        = svtgpu_av1_highbd_pixel_proj_error;
-    svt_aom_mse16x16                       = svtgpu_aom_mse16x16;
-    svt_aom_highbd_8_mse16x16              = svtgpu_aom_highbd_8_mse16x16;
-}
-/* compile-time check of the other shims (ME, MD distortion, frame buffers): each assigned to the reference's RTCD
- * pointer, or to a pointer of the direct-call function's type, without a cast.  Not called. */
+/* rtcd_pipe: the same frame code with every RTCD pointer bound to libsvtgpu's device shims by the encoder's own install
+ * header (include/svtgpu_rtcd.h): each assignment compiles under -Werror=incompatible-pointer-types
+ * without a cast */
 #include "EbMcp.h"
-void bind_check_me_md_frame(void);
-void bind_check_me_md_frame(void) {
-    svt_aom_highbd_10_variance128x128         = svtgpu_aom_highbd_10_variance128x128;
-    svt_aom_highbd_10_variance128x64          = svtgpu_aom_highbd_10_variance128x64;
-    svt_aom_highbd_10_variance16x16           = svtgpu_aom_highbd_10_variance16x16;
-    svt_aom_highbd_10_variance16x32           = svtgpu_aom_highbd_10_variance16x32;
-    svt_aom_highbd_10_variance16x4            = svtgpu_aom_highbd_10_variance16x4;
-    svt_aom_highbd_10_variance16x64           = svtgpu_aom_highbd_10_variance16x64;
-    svt_aom_highbd_10_variance16x8            = svtgpu_aom_highbd_10_variance16x8;
-    svt_aom_highbd_10_variance32x16           = svtgpu_aom_highbd_10_variance32x16;
-    svt_aom_highbd_10_variance32x32           = svtgpu_aom_highbd_10_variance32x32;
-    svt_aom_highbd_10_variance32x64           = svtgpu_aom_highbd_10_variance32x64;
-    svt_aom_highbd_10_variance32x8            = svtgpu_aom_highbd_10_variance32x8;
-    svt_aom_highbd_10_variance4x16            = svtgpu_aom_highbd_10_variance4x16;
-    svt_aom_highbd_10_variance4x4             = svtgpu_aom_highbd_10_variance4x4;
-    svt_aom_highbd_10_variance4x8             = svtgpu_aom_highbd_10_variance4x8;
-    svt_aom_highbd_10_variance64x128          = svtgpu_aom_highbd_10_variance64x128;
-    svt_aom_highbd_10_variance64x16           = svtgpu_aom_highbd_10_variance64x16;
-    svt_aom_highbd_10_variance64x32           = svtgpu_aom_highbd_10_variance64x32;
-    svt_aom_highbd_10_variance64x64           = svtgpu_aom_highbd_10_variance64x64;
-    svt_aom_highbd_10_variance8x16            = svtgpu_aom_highbd_10_variance8x16;
-    svt_aom_highbd_10_variance8x32            = svtgpu_aom_highbd_10_variance8x32;
-    svt_aom_highbd_10_variance8x4             = svtgpu_aom_highbd_10_variance8x4;
-    svt_aom_highbd_10_variance8x8             = svtgpu_aom_highbd_10_variance8x8;
-    svt_aom_highbd_sse                        = svtgpu_aom_highbd_sse;
-    svt_aom_sad128x128                        = svtgpu_aom_sad128x128;
-    svt_aom_sad128x128x4d                     = svtgpu_aom_sad128x128x4d;
-    svt_aom_sad128x64                         = svtgpu_aom_sad128x64;
-    svt_aom_sad128x64x4d                      = svtgpu_aom_sad128x64x4d;
-    svt_aom_sad16x16                          = svtgpu_aom_sad16x16;
-    svt_aom_sad16x16x4d                       = svtgpu_aom_sad16x16x4d;
-    svt_aom_sad16x32                          = svtgpu_aom_sad16x32;
-    svt_aom_sad16x32x4d                       = svtgpu_aom_sad16x32x4d;
-    svt_aom_sad16x4                           = svtgpu_aom_sad16x4;
-    svt_aom_sad16x4x4d                        = svtgpu_aom_sad16x4x4d;
-    svt_aom_sad16x64                          = svtgpu_aom_sad16x64;
-    svt_aom_sad16x64x4d                       = svtgpu_aom_sad16x64x4d;
-    svt_aom_sad16x8                           = svtgpu_aom_sad16x8;
-    svt_aom_sad16x8x4d                        = svtgpu_aom_sad16x8x4d;
-    svt_aom_sad32x16                          = svtgpu_aom_sad32x16;
-    svt_aom_sad32x16x4d                       = svtgpu_aom_sad32x16x4d;
-    svt_aom_sad32x32                          = svtgpu_aom_sad32x32;
-    svt_aom_sad32x32x4d                       = svtgpu_aom_sad32x32x4d;
-    svt_aom_sad32x64                          = svtgpu_aom_sad32x64;
-    svt_aom_sad32x64x4d                       = svtgpu_aom_sad32x64x4d;
-    svt_aom_sad32x8                           = svtgpu_aom_sad32x8;
-    svt_aom_sad32x8x4d                        = svtgpu_aom_sad32x8x4d;
-    svt_aom_sad4x16                           = svtgpu_aom_sad4x16;
-    svt_aom_sad4x16x4d                        = svtgpu_aom_sad4x16x4d;
-    svt_aom_sad4x4                            = svtgpu_aom_sad4x4;
-    svt_aom_sad4x4x4d                         = svtgpu_aom_sad4x4x4d;
-    svt_aom_sad4x8                            = svtgpu_aom_sad4x8;
-    svt_aom_sad4x8x4d                         = svtgpu_aom_sad4x8x4d;
-    svt_aom_sad64x128                         = svtgpu_aom_sad64x128;
-    svt_aom_sad64x128x4d                      = svtgpu_aom_sad64x128x4d;
-    svt_aom_sad64x16                          = svtgpu_aom_sad64x16;
-    svt_aom_sad64x16x4d                       = svtgpu_aom_sad64x16x4d;
-    svt_aom_sad64x32                          = svtgpu_aom_sad64x32;
-    svt_aom_sad64x32x4d                       = svtgpu_aom_sad64x32x4d;
-    svt_aom_sad64x64                          = svtgpu_aom_sad64x64;
-    svt_aom_sad64x64x4d                       = svtgpu_aom_sad64x64x4d;
-    svt_aom_sad8x16                           = svtgpu_aom_sad8x16;
-    svt_aom_sad8x16x4d                        = svtgpu_aom_sad8x16x4d;
-    svt_aom_sad8x32                           = svtgpu_aom_sad8x32;
-    svt_aom_sad8x32x4d                        = svtgpu_aom_sad8x32x4d;
-    svt_aom_sad8x4                            = svtgpu_aom_sad8x4;
-    svt_aom_sad8x4x4d                         = svtgpu_aom_sad8x4x4d;
-    svt_aom_sad8x8                            = svtgpu_aom_sad8x8;
-    svt_aom_sad8x8x4d                         = svtgpu_aom_sad8x8x4d;
-    svt_aom_sse                               = svtgpu_aom_sse;
-    svt_aom_sub_pixel_variance128x128         = svtgpu_aom_sub_pixel_variance128x128;
-    svt_aom_sub_pixel_variance128x64          = svtgpu_aom_sub_pixel_variance128x64;
-    svt_aom_sub_pixel_variance16x16           = svtgpu_aom_sub_pixel_variance16x16;
-    svt_aom_sub_pixel_variance16x32           = svtgpu_aom_sub_pixel_variance16x32;
-    svt_aom_sub_pixel_variance16x4            = svtgpu_aom_sub_pixel_variance16x4;
-    svt_aom_sub_pixel_variance16x64           = svtgpu_aom_sub_pixel_variance16x64;
-    svt_aom_sub_pixel_variance16x8            = svtgpu_aom_sub_pixel_variance16x8;
-    svt_aom_sub_pixel_variance32x16           = svtgpu_aom_sub_pixel_variance32x16;
-    svt_aom_sub_pixel_variance32x32           = svtgpu_aom_sub_pixel_variance32x32;
-    svt_aom_sub_pixel_variance32x64           = svtgpu_aom_sub_pixel_variance32x64;
-    svt_aom_sub_pixel_variance32x8            = svtgpu_aom_sub_pixel_variance32x8;
-    svt_aom_sub_pixel_variance4x16            = svtgpu_aom_sub_pixel_variance4x16;
-    svt_aom_sub_pixel_variance4x4             = svtgpu_aom_sub_pixel_variance4x4;
-    svt_aom_sub_pixel_variance4x8             = svtgpu_aom_sub_pixel_variance4x8;
-    svt_aom_sub_pixel_variance64x128          = svtgpu_aom_sub_pixel_variance64x128;
-    svt_aom_sub_pixel_variance64x16           = svtgpu_aom_sub_pixel_variance64x16;
-    svt_aom_sub_pixel_variance64x32           = svtgpu_aom_sub_pixel_variance64x32;
-    svt_aom_sub_pixel_variance64x64           = svtgpu_aom_sub_pixel_variance64x64;
-    svt_aom_sub_pixel_variance8x16            = svtgpu_aom_sub_pixel_variance8x16;
-    svt_aom_sub_pixel_variance8x32            = svtgpu_aom_sub_pixel_variance8x32;
-    svt_aom_sub_pixel_variance8x4             = svtgpu_aom_sub_pixel_variance8x4;
-    svt_aom_sub_pixel_variance8x8             = svtgpu_aom_sub_pixel_variance8x8;
-    svt_aom_variance128x128                   = svtgpu_aom_variance128x128;
-    svt_aom_variance128x64                    = svtgpu_aom_variance128x64;
-    svt_aom_variance16x16                     = svtgpu_aom_variance16x16;
-    svt_aom_variance16x32                     = svtgpu_aom_variance16x32;
-    svt_aom_variance16x4                      = svtgpu_aom_variance16x4;
-    svt_aom_variance16x64                     = svtgpu_aom_variance16x64;
-    svt_aom_variance16x8                      = svtgpu_aom_variance16x8;
-    svt_aom_variance32x16                     = svtgpu_aom_variance32x16;
-    svt_aom_variance32x32                     = svtgpu_aom_variance32x32;
-    svt_aom_variance32x64                     = svtgpu_aom_variance32x64;
-    svt_aom_variance32x8                      = svtgpu_aom_variance32x8;
-    svt_aom_variance4x16                      = svtgpu_aom_variance4x16;
-    svt_aom_variance4x4                       = svtgpu_aom_variance4x4;
-    svt_aom_variance4x8                       = svtgpu_aom_variance4x8;
-    svt_aom_variance64x128                    = svtgpu_aom_variance64x128;
-    svt_aom_variance64x16                     = svtgpu_aom_variance64x16;
-    svt_aom_variance64x32                     = svtgpu_aom_variance64x32;
-    svt_aom_variance64x64                     = svtgpu_aom_variance64x64;
-    svt_aom_variance8x16                      = svtgpu_aom_variance8x16;
-    svt_aom_variance8x32                      = svtgpu_aom_variance8x32;
-    svt_aom_variance8x4                       = svtgpu_aom_variance8x4;
-    svt_aom_variance8x8                       = svtgpu_aom_variance8x8;
-    svt_convert_16bit_to_8bit                 = svtgpu_convert_16bit_to_8bit;
-    svt_convert_8bit_to_16bit                 = svtgpu_convert_8bit_to_16bit;
-    svt_ext_all_sad_calculation_8x8_16x16     = svtgpu_ext_all_sad_calculation_8x8_16x16;
-    svt_ext_eight_sad_calculation_32x32_64x64 = svtgpu_ext_eight_sad_calculation_32x32_64x64;
-    svt_ext_sad_calculation_32x32_64x64       = svtgpu_ext_sad_calculation_32x32_64x64;
-    svt_ext_sad_calculation_8x8_16x16         = svtgpu_ext_sad_calculation_8x8_16x16;
-    svt_nxm_sad_kernel                        = svtgpu_nxm_sad_kernel;
-    svt_nxm_sad_kernel_sub_sampled            = svtgpu_nxm_sad_kernel_sub_sampled;
-    svt_pme_sad_loop_kernel                   = svtgpu_pme_sad_loop_kernel;
-    sad_16b_kernel                            = svtgpu_sad_16b_kernel;
-    svt_sad_loop_kernel                       = svtgpu_sad_loop_kernel;
+#include "svtgpu_rtcd.h"
+static void bind_device_kernels(void) {
+    svtgpu_install_filter_rtcd();
+    svtgpu_install_me_md_rtcd(); /* compiled and installed; the frame code here calls none of them */
+}
+/* the frame-buffer functions the reference calls directly (not through RTCD): a pointer of each one's type */
+void bind_check_frame(void);
+void bind_check_frame(void) {
     __typeof__(&svt_aom_generate_padding)       pad8  = svtgpu_aom_generate_padding;
     __typeof__(&svt_aom_generate_padding16_bit) pad16 = svtgpu_aom_generate_padding16_bit;
     __typeof__(&svt_extend_frame)               ext   = svtgpu_extend_frame;

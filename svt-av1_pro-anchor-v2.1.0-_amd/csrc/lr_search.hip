@@ -1724,7 +1724,14 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
 // The pass count is bounded (SR_MAX_PASSES; a descent ends far earlier): on overflow or a timed-out exchange the
 // descent stops and *status is set, which search_frame reports as SVTGPU_ERR_HIP.
 // ---------------------------------------------------------------------------------------------
-constexpr int SR_NT = 1024, SR_PW = 15, SR_PL = SR_PW * 64, SR_KMAX = 18, SR_MAX_PX = SR_PL * SR_KMAX * 4;
+#ifndef SVTGPU_SR_NT
+#define SVTGPU_SR_NT 1024 // workgroup size (512: two workgroups per CU, dev builds)
+#endif
+#ifndef SVTGPU_SR_KMAX
+#define SVTGPU_SR_KMAX 18 // resident 4-pixel chunks per pixel lane
+#endif
+constexpr int SR_NT = SVTGPU_SR_NT, SR_PW = SR_NT / 64 - 1, SR_PL = SR_PW * 64, SR_KMAX = SVTGPU_SR_KMAX;
+constexpr int SR_MAX_PX = SR_PL * SR_KMAX * 4;
 constexpr int SR_MAX_PASSES = 4096, SR_MAX_PARTS = 8;
 constexpr int SR_LDS = SR_KMAX * SR_PL * 8; // the (x - src) pairs of the part
 struct SrItem {
@@ -1791,6 +1798,36 @@ __device__ __forceinline__ void sr_tree_lanes(const Descent &d, bool live, int n
     if (n == 0) *s_mask = (uint32_t)mask, *s_nv = (int)__popcll(mask);
 }
 
+// wave-uniform copies (scalar registers) of a 64-bit lane value and of a struct
+__device__ __forceinline__ long long readlane64(long long v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l),
+                   hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)v >> 32), l);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+template <typename S>
+__device__ __forceinline__ S uniform(const S &v) {
+    static_assert(sizeof(S) % 4 == 0, "whole dwords");
+    S r;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(S) / 4); k++)
+        ((int *)&r)[k] = __builtin_amdgcn_readfirstlane(((const int *)&v)[k]);
+    return r;
+}
+// the next tree: a single node (the pending candidate itself) from the uniform descent, else one node per lane
+__device__ __forceinline__ void sr_tree_publish(const Descent &d, bool live, int nodes, uint32_t *s_xq,
+                                                uint32_t *s_mask, int *s_nv) {
+    if (nodes == 1) {
+        if ((threadIdx.x & 63) == 0) {
+            int32_t x[2];
+            decode_xq(d, x);
+            s_xq[0] = pack2(x[0], x[1]);
+            *s_mask = 1, *s_nv = live ? 1 : 0;
+        }
+    } else {
+        sr_tree_lanes(d, live, nodes, s_xq, s_mask, s_nv);
+    }
+}
+
 // one pass over the resident pixels: the errors of the first nv (<= NV) candidates, wave totals into s_red[wave].
 // Candidates past nv are evaluated with xq = 0 and dropped (NV = nv up to 4; 7 for trees of 5-7 nodes).
 template <int NV>
@@ -1825,7 +1862,7 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
 }
 
 template <typename T>
-__global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
+__global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
                                                         const SeedCfg cfg, int nodes, Descent *ds,
                                                         unsigned long long *xch, int32_t *status,
                                                         unsigned long long *stat, unsigned long long *tk) {
@@ -1863,13 +1900,15 @@ __global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int 
 #pragma unroll
             for (int j = 0; j < 3; j++)
 #pragma unroll
-                for (int q = 0; q < 4; q++) g[kb + j][q] = 0u;
+                for (int q = 0; q < 4; q++)
+                    if (kb + j < SR_KMAX) g[kb + j][q] = 0u;
             if (kb >= K) continue; // uniform
             int2 dv2[3], sv2[3], a0[3], a1[3];
             bool on[3];
 #pragma unroll
             for (int j = 0; j < 3; j++) { // all loads of 3 chunks in flight together (addresses clamped into the part)
-                const int c = pl + (kb + j) * SR_PL, cc = min(c, nch - 1), row = cc / cw, col = cc - row * cw;
+                const int c = kb + j < SR_KMAX ? pl + (kb + j) * SR_PL : nch, cc = min(c, nch - 1), row = cc / cw,
+                          col = cc - row * cw;
                 const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
                 on[j] = c < nch;
                 const size_t fo = (size_t)y * P.fstride + x;
@@ -1886,6 +1925,7 @@ __global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int 
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const int kk = kb + j;
+                if (kk >= SR_KMAX) break;
                 int       dv[4], sv[4];
                 if constexpr (sizeof(T) == 2) {
                     dv[0] = dv2[j].x & 0xFFFF, dv[1] = (uint32_t)dv2[j].x >> 16, dv[2] = dv2[j].y & 0xFFFF, dv[3] = (uint32_t)dv2[j].y >> 16;
@@ -1957,10 +1997,11 @@ __global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int 
         ok = __ballot(!ok) == 0;
         long long mv[5];
 #pragma unroll
-        for (int q = 0; q < 5; q++) mv[q] = __shfl(v, q, 64);
-        Descent D = sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg); // the same in every lane
+        for (int q = 0; q < 5; q++) mv[q] = readlane64(v, q);
+        // the descent is wave-uniform from here on: kept in scalar registers, stepped by the scalar unit
+        Descent D = uniform(sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg));
         D.next(); // the seed itself is the first candidate
-        sr_tree_lanes(D, ok, nodes, s_xq, &s_mask, &s_nv);
+        sr_tree_publish(D, ok, nodes, s_xq, &s_mask, &s_nv);
         __syncthreads(); // B2
         for (int pass = 1;; pass++) {
             const int nv = __builtin_amdgcn_readfirstlane(s_nv);
@@ -1982,9 +2023,19 @@ __global__ __launch_bounds__(SR_NT) void sgr_res_kernel(const SearchArgs A, int 
                 if (lane == 0) atomicOr(status, 1);
                 ok = false;
             }
-            if (ok) // the same steps in every lane
-                sgr_replay(D, mask, [&](int node) { return (int64_t)__shfl(e, __popc(mask & ((1u << node) - 1)), 64); });
-            sr_tree_lanes(D, ok && !D.done, nodes, s_xq, &s_mask, &s_nv);
+            if (ok) { // the same steps in every lane (the errors made uniform: scalar code)
+                long long ev[SG_NC];
+#pragma unroll
+                for (int c = 0; c < SG_NC; c++) ev[c] = c < nv ? readlane64(e, c) : 0;
+                sgr_replay(D, mask, [&](int node) {
+                    const int i = __popc(mask & ((1u << node) - 1));
+                    long long r = ev[0];
+#pragma unroll
+                    for (int c = 1; c < SG_NC; c++) r = i == c ? ev[c] : r;
+                    return (int64_t)r;
+                });
+            }
+            sr_tree_publish(D, ok && !D.done, nodes, s_xq, &s_mask, &s_nv);
             if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
             __syncthreads(); // B4
             if (stat && lane == 0 && s_nv == 0) atomicAdd(stat + 1, (unsigned long long)pass);

@@ -57,3 +57,17 @@ def test_shim_prototypes_match_reference_pointers():
     r = subprocess.run(["make", "-s", "-f", "oracle/ref.mk", "bindcheck"], cwd=ROOT, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+
+
+RTCD_INSTALL = os.path.join(ROOT, "oracle", "_ref", "rtcd_install")
+
+
+@pytest.mark.skipif(not os.path.exists(RTCD_INSTALL), reason="oracle/_ref/rtcd_install not built (needs /root/reference)")
+def test_install_point_before_init_fn_ptr():
+    """The install point of include/svtgpu_rtcd.h: the reference's init_fn_ptr (av1me.c:31, called
+    at EbEncHandle.c:1546) copies the 110 sad / x4d / variance / highbd variance / sub-pixel variance pointers of the 22
+    block sizes into svt_aom_mefn_ptr[], which ME and MD call.  Installed between the RTCD setup (:1531) and that
+    call, every entry is a libsvtgpu shim; installed after it, none is.  Pointer comparisons only (CPU)."""
+    res = subprocess.run([RTCD_INSTALL], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert res.stdout.split() == ["documented", "110/110", "late", "0/110"], res.stdout
