@@ -749,8 +749,7 @@ def main():
             lr_kern = {"wiener_trials": ("wiener_res_kernel", 2 * SB, "the CDEF output and source of the searched "
                                                                       "planes read once, 2*S*B"),
                        "sgr_filters": ("sgr_flt_kernel", SB, "the CDEF output read once, S*B"),
-                       "projection": ("proj_err_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B"),
-                       "sgr_moments": ("sgr_mom_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
+                       "projection": ("sgr_res_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
             for cls, (kn, alg, what) in lr_kern.items():
                 c = lr_cls[cls]
                 if c["launches"] > 0:

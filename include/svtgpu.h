@@ -836,9 +836,9 @@ int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, i
  * out[p] = {x0, y0, x1, y1} (plane samples), reading the CDEF output 3 samples and the DLF output 3 rows around it.
  * NULL arrays: the whole frame; NULL comm: no exchange. */
 int svtgpu_lr_set_tile(SvtGpuLrState *s, const int32_t units[3][4], const int32_t out[3][4], SvtGpuComm *comm);
-/* Device-time profile of the searches timed since the previous read, by kernel class: 0 unit sums + Wiener statistics, 1 self-guided filters
- * (sgr_flt_kernel), 2 Wiener descents (unit kernel / queue / trial rounds), 3 self-guided descents (queue / projection
- * rounds), 4 Wiener decomposition, descent advance rounds, SGR SSE, 5 self-guided projection moments.  Each
+/* Device-time profile of the searches timed since the previous read, by kernel class: 0 unit sums + Wiener
+ * statistics, 1 self-guided filters (sgr_flt_kernel), 2 Wiener descents (wiener_res_kernel), 3 self-guided searches
+ * (sgr_res_kernel: moments, seeds and descents), 4 Wiener decomposition and the chosen ep's SSE, 5 unused.  Each
  * launch is timed from its first workgroup's start to its last workgroup's end on the device's 100 MHz
  * s_memrealtime clock (per-launch HIP event packets would cost more than these launches); bytes = algorithmic
  * HBM bytes of the class (compulsory reads/writes of the samples and filter planes the launches touch). */

@@ -286,10 +286,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     if (s->wst) (void)hipStreamSynchronize(s->wst), (void)hipStreamDestroy(s->wst);
     if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
     if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-    for (hipEvent_t e : s->ev_batch)
-        if (e) (void)hipEventDestroy(e);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
-    if (s->h_flag) (void)hipHostFree(s->h_flag);
     lr_profiler_destroy(s->prof);
     delete s;
 }

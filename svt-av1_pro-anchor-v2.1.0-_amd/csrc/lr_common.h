@@ -24,12 +24,7 @@ struct SvtGpuLrState {
     hipEvent_t           pin_free; // the last copy out of h_pin has run: the host may rewrite it
     hipStream_t          wst;      // the search's Wiener chain (the caller's stream carries the self-guided one)
     hipEvent_t           ev_fork, ev_join;
-    hipEvent_t           ev_batch[4]; // unused (the batches publish through h_flag)
-    // [chain][slot] {sequence, live count} written by the device at the end of a batch of descent rounds (mapped
-    // pinned memory: the host polls it without runtime calls)
-    unsigned long long  *h_flag, *h_flag_dev;
-    unsigned long long   flag_seq;
-    // uncached device memory shared by the persistent Wiener queue's workgroups (coherent without cache flushes)
+    // uncached device memory: the exchange words of the resident descents' row parts (coherent without cache flushes)
     void                *d_qarena;
     size_t               qarena_bytes;
     // a picture tiled over GPUs (svtgpu_lr_set_tile): the units searched {col0, row0, col1, row1} and the samples

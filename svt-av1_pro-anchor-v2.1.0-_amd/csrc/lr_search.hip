@@ -11,19 +11,19 @@
 //                         window-column pair accumulates its 7x7 block with v_dot2_i32_i16 over horizontal pixel
 //                         pairs (diagonal groups also form M); per-tile partials are reduced per unit
 //   sgr_flt_kernel        box sums of a tile once, then for every searched ep the A/B maps and both self-guided
-//                         filters (kept in HBM as int16); sgr_mom_kernel forms the 2x2 projection moments from them
+//                         filters (kept in HBM as int16)
 //   wiener_solve_kernel   the int64 fixed-point Wiener decomposition and score per unit (the descent's seed)
 //   wiener_res_kernel     the whole Wiener descent of finer_tile_search_wiener_seg per unit with the unit resident on
 //                         the CU: CDEF window in LDS, source in registers, a rolling horizontal pass per lane; units
 //                         too large for one CU are cut into row parts whose SSEs meet each candidate
-//   sgr_seed_kernel       the 2x2 projection solve (double, as the reference) per (unit, ep)
-//   proj_err_kernel + sgr_advance_kernel
-//                         the self-guided descents of finer_search_pixel_proj_error as per-round launches (a speculative
-//                         7-node outcome tree per descent and round) with a host-polled batch loop
+//   sgr_res_kernel        the whole self-guided search of one (unit, ep) with the unit resident on the CU: the
+//                         ep's filter planes read once into registers, the projection moments, the seed (the 2x2
+//                         double solve, as the reference) and finer_search_pixel_proj_error's descent, stepped by a
+//                         control wave between passes over the resident pixels
 //   sgr_best_kernel, sgr_sse_kernel
 //                         best ep per unit (strict <) and the SSE of its clipped output
 // The host does what is sequential in the reference and cheap: the RD pass over the units (rest_finish_search).  A
-// frame costs a host wait per batch of self-guided rounds plus the final read-back.
+// frame costs one host wait (the final read-back).
 #include <algorithm>
 #include <chrono>
 #include <climits>
@@ -79,31 +79,6 @@ __device__ inline int px(const T *p, int stride, int W, int H, int y, int x) {
 // wave total in lane 63 (svtgpu_internal.h)
 __device__ inline unsigned long long wave_sum(unsigned long long v) { return wave_sum_lane63(v); }
 constexpr int WAVE_LAST = 63;
-
-// Work lists and live counts filled by thousands of lanes: one atomic per wave instead of one per lane (a single
-// counter hit by every lane serializes).  Every lane of the wave must call these.
-__device__ inline int wave_prefix(int v, int &total) { // exclusive prefix over the wave, and the wave total
-    const int lane = threadIdx.x & 63;
-    int       x    = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    total = __shfl(x, 63, 64);
-    return x - v;
-}
-__device__ inline int wave_alloc(int32_t *counter, int v) { // this lane's first slot of v in the counted list
-    int       tot;
-    const int ex   = wave_prefix(v, tot);
-    int       base = 0;
-    if ((threadIdx.x & 63) == 0 && tot) base = atomicAdd(counter, tot);
-    return __shfl(base, 0, 64) + ex;
-}
-__device__ inline void wave_count(int32_t *counter, bool live) {
-    const unsigned long long b = __ballot(live);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(counter, (int)__popcll(b));
-}
 
 // Kernel timing for svtgpu_lr_profile: with a slot `tk`, the earliest workgroup start (atomicMin) and the latest
 // workgroup end (atomicMax, at tk + PROF_NL * PROF_SP) of a launch on the 100 MHz s_memrealtime clock, spread over
@@ -351,15 +326,6 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
     PROF_END(tk);
 }
 
-// end of a batch of descent rounds: the chain's live count and the batch's sequence number to mapped host memory
-// (count first, then a system-scope fence, then the sequence word the host polls)
-__global__ void lr_publish_kernel(const int32_t *cnt, unsigned long long *flag, unsigned long long seq) {
-    if (threadIdx.x != 0) return;
-    flag[1] = (unsigned long long)(uint32_t)cnt[1];
-    __threadfence_system();
-    __hip_atomic_store(&flag[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // per unit: sum the tile partials (tiles of a unit are contiguous in the tile list)
 __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_tile0, int tile_begin, int nvals,
                                     long long *out, unsigned long long *tk) {
@@ -389,7 +355,7 @@ __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF
 // ---------------------------------------------------------------------------------------------
 // self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
 // registers; per ep the A/B maps (packed B << 9 | A) go to LDS and the filters to HBM (the projection moments are
-// a separate pass over them, sgr_mom_kernel).
+// the resident search, sgr_res_kernel).
 // ---------------------------------------------------------------------------------------------
 constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT;
 
@@ -559,241 +525,9 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
     PROF_END(tk);
 }
 
-// projection moments mom[pair] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s} (u = x<<4, s = (src<<4) - u, g = flt - u) of every
-// (unit, ep) from the stored filters: the tile's CDEF and source pixels are read once, 16 pixels per lane (4-pixel
-// chunks), and every ep's two filter planes stream past them -- a memory-bound pass that keeps the moment arithmetic
-// and its wave reductions out of the VALU-bound filter kernel (one reduction per ep per 1024 pixels instead of 256).
-// Lane partials stay 32-bit over a chunk: |f| <= 32767 (the filter's weighted A/B sums are bounded by
-// 32 * 256 * 1023 + 32 * 261111 < 2^24 before the >> 9), so |g| <= 32767, g^2 * 4 < 2^32 and |g * s| * 4 < 2^31 with
-// |s| <= 16368; g1 * g2 goes to 64 bits per pixel.
-template <typename T>
-__global__ __launch_bounds__(256) void sgr_mom_kernel(const SearchArgs A, long long *mom, unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    constexpr int    NCH = 4;
-    const Tile       t   = A.tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
-    const PlaneArgs &P   = A.pl[t.plane];
-    const int        cw  = t.w >> 2;
-    const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-    const size_t     pn = (size_t)P.fstride * P.H;
-    int              uu[NCH][4], ss[NCH][4]; // u = x << 4 and s = (src - x) << 4 per pixel
-    size_t           fo[NCH];
-    bool             on[NCH];
-#pragma unroll
-    for (int k = 0; k < NCH; k++) {
-        const int ch = threadIdx.x + k * 256, y = t.y0 + (ch >> 4), x = t.x0 + (ch & 15) * 4;
-        on[k]        = (ch >> 4) < t.h && (ch & 15) < cw;
-        fo[k]        = (size_t)y * P.fstride + x;
-        int dv[4] = {0, 0, 0, 0}, sv[4] = {0, 0, 0, 0};
-        if (on[k]) {
-            load4(d + (size_t)y * P.dstride + x, dv);
-            load4(s + (size_t)y * P.sstride + x, sv);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) uu[k][j] = dv[j] << 4, ss[k][j] = (sv[j] - dv[j]) << 4;
-    }
-    const int pb = P.pair_base + (t.unit - P.unit_base) * P.ne;
-    // the next ep's two filter planes are loaded while this ep's moments are formed and reduced
-    int2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
-    auto fetch = [&](int e, int2 *x0, int2 *x1) {
-        const int      ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-        const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
-#pragma unroll
-        for (int k = 0; k < NCH; k++) {
-            x0[k] = x1[k] = make_int2(0, 0);
-            if (!on[k]) continue;
-            if (r0) x0[k] = *(const int2 *)(f0 + fo[k]);
-            if (r1) x1[k] = *(const int2 *)(f1 + fo[k]);
-        }
-    };
-    if (P.ne > 0) fetch(0, w0, w1);
-    for (int e = 0; e < P.ne; e++) {
-        const int          ep = P.eps[e], r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
-        if (e + 1 < P.ne) fetch(e + 1, n0, n1);
-        unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
-#pragma unroll
-        for (int k = 0; k < NCH; k++) {
-            if (!on[k]) continue;
-            const int a0[4] = {(int)(int16_t)(w0[k].x & 0xFFFF), w0[k].x >> 16, (int)(int16_t)(w0[k].y & 0xFFFF),
-                               w0[k].y >> 16};
-            const int a1[4] = {(int)(int16_t)(w1[k].x & 0xFFFF), w1[k].x >> 16, (int)(int16_t)(w1[k].y & 0xFFFF),
-                               w1[k].y >> 16};
-            uint32_t m0 = 0, m1 = 0;
-            int      m3 = 0, m4 = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int g1 = r0 ? a0[j] - uu[k][j] : 0, g2 = r1 ? a1[j] - uu[k][j] : 0;
-                m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
-                m3 += g1 * ss[k][j], m4 += g2 * ss[k][j];
-                M2 += (unsigned long long)(long long)(g1 * g2);
-            }
-            M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
-        }
-        // wave totals on 32-bit DPP adds over limbs; the moments an ep's filters cannot produce stay zero
-        unsigned long long tot[5] = {0, 0, 0, 0, 0};
-        if (r0) tot[0] = wave_sum_u64_limbs(M0), tot[3] = wave_sum_u64_limbs(M3);
-        if (r1) tot[1] = wave_sum_u64_limbs(M1), tot[4] = wave_sum_u64_limbs(M4);
-        if (r0 && r1) tot[2] = wave_sum_u64_limbs(M2);
-        if ((threadIdx.x & 63) == WAVE_LAST)
-#pragma unroll
-            for (int q = 0; q < 5; q++)
-                if (tot[q]) atomicAdd((unsigned long long *)&mom[(size_t)(pb + e) * 5 + q], tot[q]);
-#pragma unroll
-        for (int k = 0; k < NCH; k++) w0[k] = n0[k], w1[k] = n1[k];
-    }
-    PROF_END(tk);
-}
-
-// projection errors of the candidate trees of every listed tile: the tile's CDEF and source pixels are read once
-// (packed per pixel as (x, x - src) int16 pairs), then every ep of the unit with a pending tree (candm != 0) is
-// evaluated on them.  Per pixel the filter differences (g1, g2) = (flt0 - u, flt1 - u) fit int16 (|g| < 2^15),
-// as do the xq pairs, so a candidate costs one v_dot2_i32_i16 plus the error.  Tiles are read in 4-pixel chunks
-// (tile widths and x offsets are multiples of 4), 16 chunks per row.
 typedef short v2i16s __attribute__((ext_vector_type(2)));
 __device__ inline uint32_t pk_sub16(uint32_t a, uint32_t b) { // per-half a - b mod 2^16
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(v2i16s, a) - __builtin_bit_cast(v2i16s, b));
-}
-
-// a word another workgroup of the same launch may have written (the work-queue kernels keep such words in uncached
-// memory and read them with vector loads); a plain load otherwise
-template <bool SHARED, typename W>
-__device__ inline W ld_shared(const W *p) {
-    if constexpr (SHARED) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-
-// the candidate trees of every ep of tile ti's unit with a pending tree, evaluated over the tile; the errors are
-// added to err[pair * SG_NC + node]
-template <typename T, bool SHARED>
-__device__ inline void proj_tile(const SearchArgs &A, int ti, const int32_t *cand, const uint32_t *candm,
-                                 unsigned long long *err, unsigned long long &npx_t, unsigned long long &npx_e) {
-    constexpr int NCH = 4;
-    {
-        const Tile       t = A.tiles[ti];
-        const PlaneArgs &P = A.pl[t.plane];
-        const int        pb = P.pair_base + (t.unit - P.unit_base) * P.ne, cw = t.w >> 2;
-        npx_t += t.w * t.h; // profiling
-        const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
-        const size_t     pn = (size_t)P.fstride * P.H;
-        // chunk k of this lane: row (threadIdx.x >> 4) + 16 k, 4 pixels at column 4 (threadIdx.x & 15)
-        const int        fo0 = (t.y0 + (threadIdx.x >> 4)) * P.fstride + t.x0 + (threadIdx.x & 15) * 4;
-        const int        fos = 16 * P.fstride;
-        // per pixel, independent of the ep: u = (x << 4, x << 4) packed, and c0 = 1024 + (x - src) * 2^11 -- the
-        // rounding and source terms that ride in the dot product's accumulator
-        uint32_t         uu[NCH][4];
-        int32_t          c0[NCH][4];
-        uint32_t         on = 0;      // bit k: chunk k inside the tile
-#pragma unroll
-        for (int k = 0; k < NCH; k++) {
-            const int ch = threadIdx.x + k * 256, y = t.y0 + (ch >> 4), x = t.x0 + (ch & 15) * 4;
-            if ((ch >> 4) < t.h && (ch & 15) < cw) {
-                on |= 1u << k;
-                int dv[4], sv[4];
-                load4(d + (size_t)y * P.dstride + x, dv);
-                load4(s + (size_t)y * P.sstride + x, sv);
-#pragma unroll
-                for (int j = 0; j < 4; j++) uu[k][j] = __umul24((uint32_t)dv[j], 0x00100010u), c0[k][j] = 1024 + ((dv[j] - sv[j]) << 11);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; j++) uu[k][j] = 0, c0[k][j] = 0;
-            }
-        }
-        // the eps with a pending tree; their filter planes are fetched one ep ahead of the arithmetic
-        uint32_t act = 0;
-        for (int e = 0; e < P.ne; e++) act |= (ld_shared<SHARED>(candm + pb + e) != 0u) << e;
-        uint2 w0[NCH], w1[NCH], n0[NCH], n1[NCH];
-        auto  fetch = [&](int e, uint2 *x0, uint2 *x1) {
-            const int16_t *f0 = P.flt + (size_t)e * 2 * pn, *f1 = P.flt + (size_t)P.f1e[e] * 2 * pn + pn;
-#pragma unroll
-            for (int k = 0; k < NCH; k++)
-                if (on >> k & 1) x0[k] = *(const uint2 *)(f0 + fo0 + k * fos), x1[k] = *(const uint2 *)(f1 + fo0 + k * fos);
-        };
-        int e = act ? __builtin_ctz(act) : -1;
-        if (e >= 0) fetch(e, w0, w1);
-        while (e >= 0) {
-            act &= act - 1;
-            const int en = act ? __builtin_ctz(act) : -1;
-            if (en >= 0) fetch(en, n0, n1);
-            const int      pair = pb + e;
-            // the tree's nodes compacted to the front (the mask is the same for every lane): a partial tree (descents
-            // near their end) evaluates only its nodes
-            const uint32_t mask = __builtin_amdgcn_readfirstlane(ld_shared<SHARED>(candm + pair));
-            npx_e += t.w * t.h; // profiling
-            const int nv = __builtin_popcount(mask);
-            uint32_t  xq[SG_NC];
-            {
-                uint32_t m = mask;
-#pragma unroll
-                for (int i = 0; i < SG_NC; i++) {
-                    xq[i] = 0u;
-                    if (m) {
-                        const int c = __builtin_ctz(m);
-                        m &= m - 1;
-                        xq[i] = pack2(ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2),
-                                      ld_shared<SHARED>(cand + (pair * SG_NC + c) * 2 + 1));
-                    }
-                }
-            }
-            uint32_t acc[SG_NC];
-#pragma unroll
-            for (int c = 0; c < SG_NC; c++) acc[c] = 0;
-            auto eval = [&](auto full) {
-#pragma unroll
-                for (int k = 0; k < NCH; k++) {
-                    if (!(on >> k & 1)) continue;
-                    // (flt0, flt1) int16 pairs of the 4 pixels, then g = (flt0 - u, flt1 - u) on packed 16-bit lanes
-                    // (|g| < 2^15, so the wrapped halves are the exact differences)
-                    const uint32_t fp[4] = {__builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x05040100u),
-                                            __builtin_amdgcn_perm(w1[k].x, w0[k].x, 0x07060302u),
-                                            __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x05040100u),
-                                            __builtin_amdgcn_perm(w1[k].y, w0[k].y, 0x07060302u)};
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        // floor((v + 1024) / 2^11) + (x - src) == (v + 1024 + (x - src) * 2^11) >> 11
-                        const uint32_t g = pk_sub16(fp[j], uu[k][j]);
-#pragma unroll
-                        for (int c = 0; c < SG_NC; c++) {
-                            if (!decltype(full)::value && c >= nv) break; // uniform: a scalar branch
-                            const int ee = dot2(g, xq[c], c0[k][j]) >> 11; // c0 rides in the accumulator
-                            acc[c] += (uint32_t)(ee * ee);
-                        }
-                    }
-                }
-            };
-            if (nv == SG_NC) eval(std::true_type());
-            else eval(std::false_type());
-            {
-                uint32_t m = mask;
-#pragma unroll
-                for (int i = 0; i < SG_NC; i++) {
-                    if (!m) break;
-                    const int c = __builtin_ctz(m);
-                    m &= m - 1;
-                    const unsigned long long w = wave_sum_u32_wide(acc[i]); // <= 16 pixels per lane: fits 32 bits
-                    if ((threadIdx.x & 63) == WAVE_LAST) atomicAdd(&err[(size_t)pair * SG_NC + c], w);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < NCH; k++) w0[k] = n0[k], w1[k] = n1[k];
-            e = en;
-        }
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void proj_err_kernel(const SearchArgs A, const int32_t *items, const int32_t *cnt,
-                                                       int32_t *cnt_next, const int32_t *cand, const uint32_t *candm,
-                                                       unsigned long long *err, unsigned long long *pc,
-                                                       unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    const int n = cnt[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) cnt_next[0] = cnt_next[1] = 0;
-    unsigned long long npx_t = 0, npx_e = 0; // profiling: pixels of the tiles read, of the (pixel, ep) evaluated
-    for (int it = blockIdx.x; it < n; it += gridDim.x) proj_tile<T, false>(A, items[it], cand, candm, err, npx_t, npx_e);
-    if (pc && threadIdx.x == 0 && npx_t) {
-        atomicAdd(pc + PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_e);
-        atomicAdd(pc + 2 * PROF_SP + (blockIdx.x & (PROF_SP - 1)), npx_t);
-    }
-    PROF_END(tk);
 }
 
 // SSE of the chosen self-guided output (apply_selfguided_restoration: projection, int16 wrap, clip)
@@ -1131,33 +865,6 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 }
 
 // ---------------------------------------------------------------------------------------------
-// device-side descent rounds, one lane per descent.  A descent that is not done holds one pending candidate
-// whose error the trial kernel accumulated in err[].  cnt[0] = listed items, cnt[1] = descents with a pending
-// candidate; the counters alternate between two parities (round g reads parity g & 1, the trial kernel clears
-// the other one, the advance kernel fills it).
-// ---------------------------------------------------------------------------------------------
-
-// Words written by other workgroups of a work-queue kernel are read with agent-scope atomic loads, which miss in the
-// CU's vector L1: a plain load may return a line that this CU cached in an earlier pass (SHARED = false: plain loads,
-// the per-round launches, where every such word was written by an earlier launch)
-template <bool SHARED>
-__device__ inline uint64_t ld64(const void *p) {
-    if constexpr (SHARED) return __hip_atomic_load((const uint64_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *(const uint64_t *)p;
-}
-template <bool SHARED>
-__device__ inline Descent load_descent(const Descent *p) {
-    static_assert(sizeof(Descent) % 8 == 0, "Descent in 64-bit words");
-    if constexpr (!SHARED) {
-        return *p;
-    } else {
-        Descent d;
-        for (int k = 0; k < (int)(sizeof(Descent) / 8); k++) ((uint64_t *)&d)[k] = ld64<true>((const uint64_t *)p + k);
-        return d;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // The Wiener descent of one unit per workgroup with the whole unit resident on the CU (default).
 // finer_tile_search_wiener_seg (EbRestorationPick.c:1042-1146) evaluates ~40 candidates one after the other, each
 // over every pixel of the unit; the critical path of the search is that chain for the largest unit.  Here nothing
@@ -1444,17 +1151,7 @@ __device__ inline void decode_xq(const Descent &d, int32_t *xq) {
 // Self-guided descents evaluate a speculative tree per pass: node 0 is the pending candidate, node n's children
 // 2n+1 / 2n+2 are the candidates proposed after a worse / not-worse outcome of node n.  The walk replays the
 // outcomes against the measured errors (report() decides exactly as the reference does) and stops at the first
-// candidate outside the evaluated tree, which becomes the next root.
-// Self-guided descents evaluate a speculative tree per pass: node 0 is the pending candidate, node n's children
-// 2n+1 / 2n+2 are the candidates proposed after a worse / not-worse outcome of node n.  The walk replays the
-// outcomes against the measured errors (report() decides exactly as the reference does) and stops at the first
-// candidate that was not evaluated, which becomes the next root.  While many descents are live the rounds are
-// VALU-bound and a deeper tree amortizes the per-pixel work over more candidates: the tree is always depth 3
-// The tree size follows the live count entering the round: 1 node while more than spec_live[0] descents are live,
-// 3 nodes while more than spec_live[1], else 7 (SgSpec; negative thresholds disable a level).
-struct SgSpec {
-    int32_t live1, live3;
-};
+// candidate that was not evaluated, which becomes the next root.
 // the speculative tree of depth_nodes nodes below d's pending candidate: node n's xq pair at cd[2n], the mask of the
 // nodes built (tree: SG_NC / 2 nodes of scratch)
 __device__ uint32_t sgr_tree(const Descent &d, int depth_nodes, int32_t *cd, Descent *tree) {
@@ -1489,61 +1186,6 @@ __device__ void sgr_replay(Descent &d, uint32_t evaluated, ErrAt &&err_at) {
         node = 2 * node + (worse ? 1 : 2);
         if (node >= SG_NC || !(evaluated >> node & 1)) break;
     }
-}
-
-// one step of descent i: replay the evaluated tree against its errors, then build the next tree of depth_nodes nodes;
-// returns 1 when the descent stays live
-// (tree: SG_NC / 2 nodes of scratch -- LDS in the queue kernels, where registers are scarce)
-template <bool SHARED = false>
-__device__ int sgr_descent_step(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
-                                int first, int depth_nodes, Descent *tree) {
-    Descent d = load_descent<SHARED>(ds + i);
-    if (d.done) return 0;
-    unsigned long long *e = err + (size_t)i * SG_NC;
-    if (first) {
-        d.next(); // the seed itself is the first candidate
-    } else {
-        sgr_replay(d, ld_shared<SHARED>(candm + i), [&](int node) { return (int64_t)ld64<SHARED>(e + node); });
-    }
-    for (int c = 0; c < SG_NC; c++) e[c] = 0;
-    if (!d.done) {
-        candm[i] = sgr_tree(d, depth_nodes, cand + (size_t)i * SG_NC * 2, tree);
-        ds[i]    = d;
-        return 1;
-    }
-    candm[i] = 0;
-    ds[i]    = d;
-    return 0;
-}
-
-// returns 1 when the descent stays live; *list_unit = its unit when this descent lists the unit's tiles
-__device__ int sgr_advance_one(Descent *ds, int i, unsigned long long *err, int32_t *cand, uint32_t *candm,
-                               int32_t *ustamp, const int32_t *cnt_cur, int first, int stamp, int *list_unit,
-                               const SgSpec spec) {
-    const int live_in     = first ? 1 << 30 : cnt_cur[1];
-    const int depth_nodes = (spec.live1 >= 0 && live_in > spec.live1)   ? 1
-                            : (spec.live3 >= 0 && live_in > spec.live3) ? 3
-                                                                        : SG_NC; // nodes
-    Descent tree[SG_NC / 2];
-    if (!sgr_descent_step(ds, i, err, cand, candm, first, depth_nodes, tree)) return 0;
-    const int u = ds[i].unit;
-    if (atomicExch(&ustamp[u], stamp) != stamp) *list_unit = u; // listed once per round
-    return 1;
-}
-
-__global__ __launch_bounds__(256) void sgr_advance_kernel(Descent *ds, int n, const int32_t *tile0,
-                                                          unsigned long long *err, int32_t *cand, uint32_t *candm,
-                                                          int32_t *ustamp, int32_t *items, const int32_t *cnt_cur,
-                                                          int32_t *cnt, int first, int stamp, const SgSpec spec,
-                                                          unsigned long long *tk) {
-    PROF_BEGIN(tk);
-    const int i    = blockIdx.x * blockDim.x + threadIdx.x;
-    int       lu   = -1;
-    const int live = i < n ? sgr_advance_one(ds, i, err, cand, candm, ustamp, cnt_cur, first, stamp, &lu, spec) : 0;
-    wave_count(&cnt[1], live);
-    const int t0 = lu >= 0 ? tile0[lu] : 0, nt = lu >= 0 ? tile0[lu + 1] - t0 : 0, pos = wave_alloc(&cnt[0], nt);
-    for (int j = 0; j < nt; j++) items[pos + j] = t0 + j;
-    PROF_END(tk);
 }
 
 // the plane of global unit u
@@ -1625,17 +1267,6 @@ __global__ __launch_bounds__(256) void wiener_solve_kernel(const SearchArgs A, i
 
 // svt_get_proj_subspace_c (:417-500) from the exact integer moments, encode_xq (:502-518), and the descent of
 // finer_search_pixel_proj_error (:320-413) seeded there; one lane per (unit, ep)
-__device__ Descent sgr_seed(const SearchArgs &A, int p, int i, const int64_t *m, const SeedCfg &cfg);
-
-__global__ void sgr_seed_kernel(const SearchArgs A, int nplanes, int npairs, const int64_t *mom, const SeedCfg cfg,
-                                Descent *ds) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npairs) return;
-    int p = 0;
-    while (p + 1 < nplanes && i >= A.pl[p + 1].pair_base) p++;
-    ds[i] = sgr_seed(A, p, i, mom + (size_t)i * 5, cfg);
-}
-
 // pair i (plane p) from its moments m[5] = {Σg1², Σg2², Σg1g2, Σg1·s, Σg2·s}: the seeded descent
 __device__ Descent sgr_seed(const SearchArgs &A, int p, int i, const int64_t *m, const SeedCfg &cfg) {
     const PlaneArgs &P  = A.pl[p];
@@ -1708,7 +1339,7 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
 //   * pixel lane l (0..959) owns 4-pixel chunks l, l + 960, ... of the unit (row-major over 4-pixel columns), at most
 //     SR_KMAX of them: g = (flt0 - u, flt1 - u) packed int16 per pixel in registers (72 VGPRs), the (x - src) pairs
 //     in LDS (135 KB); chunks past the unit hold zeros, which add nothing to any sum.  The pixel waves form the five
-//     projection moments (exact 64-bit sums, as sgr_mom_kernel) while loading, and per pass the errors of the
+//     projection moments (exact 64-bit sums) while loading, and per pass the errors of the
 //     pending candidates -- per pixel and candidate one v_dot2 with the rounding and (x - src) * 2^11 terms in its
 //     accumulator, a shift, a multiply-add;
 //   * the control wave holds the descent in registers and steps it between the passes, lane-parallel: lane c sums
@@ -1724,11 +1355,14 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
 // The pass count is bounded (SR_MAX_PASSES; a descent ends far earlier): on overflow or a timed-out exchange the
 // descent stops and *status is set, which search_frame reports as SVTGPU_ERR_HIP.
 // ---------------------------------------------------------------------------------------------
+// Two 512-lane workgroups per CU (7 pixel waves + 1 control wave each, 68 KB of LDS): one workgroup's loads, control
+// steps and barriers overlap the other's passes (1024-lane workgroups, one per CU: 2204 vs 2366 Mpx/s at three frames
+// in flight, 1656 vs 1740 at one, same box, profiles/r03/srvar)
 #ifndef SVTGPU_SR_NT
-#define SVTGPU_SR_NT 1024 // workgroup size (512: two workgroups per CU, dev builds)
+#define SVTGPU_SR_NT 512
 #endif
 #ifndef SVTGPU_SR_KMAX
-#define SVTGPU_SR_KMAX 18 // resident 4-pixel chunks per pixel lane
+#define SVTGPU_SR_KMAX 19 // resident 4-pixel chunks per pixel lane: parts of <= 34048 pixels (256 x 133 luma)
 #endif
 constexpr int SR_NT = SVTGPU_SR_NT, SR_PW = SR_NT / 64 - 1, SR_PL = SR_PW * 64, SR_KMAX = SVTGPU_SR_KMAX;
 constexpr int SR_MAX_PX = SR_PL * SR_KMAX * 4;
@@ -2230,31 +1864,11 @@ void launch_stats(int win, Fn &&f) {
     else f(std::integral_constant<int, 3>());
 }
 
-constexpr int ROUNDS_PER_BATCH = 8, MAX_ROUNDS = 4096;
-constexpr int SG_SPEC_LIVE1 = -1, SG_SPEC_LIVE3 = -1; // always 7-node self-guided trees
-SgSpec sg_spec() { // self-guided tree sizes by live count; SVTGPU_SG_SPEC="live1,live3" overrides (sweeps)
-    static const SgSpec v = [] {
-        SgSpec      r{SG_SPEC_LIVE1, SG_SPEC_LIVE3};
-        const char *e = std::getenv("SVTGPU_SG_SPEC");
-        if (e) std::sscanf(e, "%d,%d", &r.live1, &r.live3);
-        return r;
-    }();
-    return v;
-}
 // largest Wiener window staged in LDS (SVTGPU_WR_LDS_CAP overrides: measurements of the global-memory path)
 int wr_lds_cap() {
     static const int v = [] {
         const char *e = std::getenv("SVTGPU_WR_LDS_CAP");
         return e ? std::atoi(e) : WR_LDS_CAP;
-    }();
-    return v;
-}
-
-// the resident self-guided search (default); SVTGPU_SG_RES=0 selects the per-round path (A/B measurements)
-bool use_sg_res() {
-    static const bool v = [] {
-        const char *e = std::getenv("SVTGPU_SG_RES");
-        return !e || std::atoi(e) != 0;
     }();
     return v;
 }
@@ -2269,12 +1883,15 @@ int sr_part_px() {
 }
 
 // candidates per pass of the resident self-guided search: a complete speculative tree of 1, 3 or 7 nodes
-// (SVTGPU_SR_TREE for A/B measurements)
+// (SVTGPU_SR_TREE for A/B measurements).  One: the descent's own candidate sequence, 7.1 passes per (unit, ep) at 4K
+// against 3.9 (3 nodes) and 2.7 (7 nodes) -- the resident passes are cheap, and a larger tree's evaluated-but-unused
+// candidates cost the other frames' work at three frames in flight (2366 / 2321 Mpx/s for 1 / 3 nodes,
+// profiles/r03/srvar)
 int sr_tree_nodes() {
     static const int v = [] {
         const char *e = std::getenv("SVTGPU_SR_TREE");
-        const int   n = e ? std::atoi(e) : SG_NC;
-        return n == 1 || n == 3 ? n : SG_NC;
+        const int   n = e ? std::atoi(e) : 1;
+        return n == 3 || n == 7 ? n : 1;
     }();
     return v;
 }
@@ -2396,10 +2013,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // read its CDEF and source samples through one L2, and the parts of an item sit next to each other in their XCD's
     // in-order dispatch, so a waiting part's partners are always dispatched after it (never behind other waiting
     // parts).  Units are dealt largest first to the lane with the least work; empty slots (pair -1) pad the lanes.
-    const bool           sg_res = use_sg_res();
     std::vector<SrItem>  sr_items;
     bool                 sr_parted = false;
-    if (sg_res && npairs) {
+    if (npairs) {
         std::vector<std::vector<SrItem>> lanes(8);
         std::vector<long long>           load(8, 0);
         std::vector<int>                 ord;
@@ -2443,15 +2059,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
                  o_witem = dc(sizeof(WrItem) * (size_t)n_wr), o_sritem = dc(sizeof(SrItem) * (size_t)n_sr);
     const size_t plan_span = dc.off;
-    const size_t o_sum = dc(8 * n_all), o_mom = dc(40 * (size_t)npairs), o_sse = dc(8 * n_all);
+    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all);
     const size_t zero_span = dc.off - o_sum;
     const size_t o_sse2 = dc(8 * (size_t)n_sg), o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
                  o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8), o_sstat = dc(8);
     const size_t res_span = dc.off - o_sse;
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_cand = dc(8 * SG_NC * (size_t)npairs), o_candm = dc(4 * (size_t)npairs),
-                 o_serr = dc(8 * SG_NC * (size_t)npairs), o_sitems = dc(4 * (size_t)nt_sg), o_ustamp = dc(4 * (size_t)n_all),
-                 o_best = dc(16 * (size_t)n_sg), o_cnt = dc(32);
+    const size_t o_best = dc(16 * (size_t)n_sg);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
     const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
@@ -2526,8 +2140,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
     }
     HIP_TRY(hipMemsetAsync(dp(o_sum), 0, zero_span, st));
-    auto *cnt = (int32_t *)dp(o_cnt); // [parity][wn items, wn live, sg items, sg live]
-    HIP_TRY(hipMemsetAsync(cnt, 0, 32, st));
     run(0, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
@@ -2570,10 +2182,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (nt_sg) {
         run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
-        if (!sg_res)
-            run(5, [&](unsigned long long *tk) {
-                hipLaunchKernelGGL(sgr_mom_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (long long *)dp(o_mom), tk);
-            });
         HIP_TRY(hipGetLastError());
     }
     mark(0);
@@ -2585,13 +2193,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         run(4, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, sw, A, nplanes, (const int64_t *)dp(o_mh),
                                cfg, (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu), tk);
-        });
-        HIP_TRY(hipGetLastError());
-    }
-    if (npairs && !sg_res) {
-        run(4, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(sgr_seed_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, A, sg_planes, npairs,
-                               (const int64_t *)dp(o_mom), cfg, (Descent *)dp(o_sds));
         });
         HIP_TRY(hipGetLastError());
     }
@@ -2631,112 +2232,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                                sr_stat, tk);
         });
         HIP_TRY(hipGetLastError());
-    } else if (npairs) {
-        HIP_TRY(hipMemsetAsync(dp(o_serr), 0, 8 * SG_NC * (size_t)npairs, st));
-        HIP_TRY(hipMemsetAsync(dp(o_ustamp), 0, 4 * (size_t)n_all, st));
-        hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st, (Descent *)dp(o_sds),
-                           npairs, d_t0, (unsigned long long *)dp(o_serr), (int32_t *)dp(o_cand),
-                           (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp), (int32_t *)dp(o_sitems),
-                           (const int32_t *)cnt + 6, cnt + 2, 1, 1, sg_spec(), (unsigned long long *)nullptr);
-        HIP_TRY(hipGetLastError());
-    }
-    // The self-guided chain runs in batches of ROUNDS_PER_BATCH rounds with the next batch already queued behind the one
-    // the host is checking (a chain whose descents have all finished turns the queued rounds into no-op launches), so
-    // its stream never waits for the host between batches.  (Chain 0, the Wiener descents of earlier rounds, runs
-    // inside wiener_res_kernel now; the two-chain bookkeeping is kept for the flag layout.)
-    const int gs = std::max(1, nt_sg);
-    struct Chain {
-        bool        live;
-        int         g = 0, head = 0, inflight = 0; // round index; ring of two batches in flight
-        hipStream_t stream;
-    } ch[2];
-    ch[0].live = false, ch[0].stream = sw;
-    ch[1].live = npairs > 0 && !sg_res, ch[1].stream = st;
-    if (!s->h_flag) {
-        HIP_TRY(hipHostMalloc((void **)&s->h_flag, 8 * 2 * 4, hipHostMallocMapped | hipHostMallocCoherent));
-        HIP_TRY(hipHostGetDevicePointer((void **)&s->h_flag_dev, s->h_flag, 0));
-        std::memset(s->h_flag, 0, 8 * 2 * 4);
-    }
-    unsigned long long want[4] = {0, 0, 0, 0}; // [chain][slot] sequence number of the batch in flight there
-    static const bool trace = std::getenv("SVTGPU_LR_TRACE") != nullptr; // host-side batch log (debugging)
-    const auto        t_tr0 = clk();
-    auto              tr    = [&](const char *what, int c, int g) {
-        if (trace)
-            std::fprintf(stderr, "lrtrace %9.1f us %s chain %d round %d\n",
-                         std::chrono::duration<double, std::micro>(clk() - t_tr0).count(), what, c, g);
-    };
-    auto enqueue_batch = [&](int c) -> int {
-        Chain &C = ch[c];
-        tr("enqueue", c, C.g);
-        for (int b = 0; b < ROUNDS_PER_BATCH; b++, C.g++) {
-            int32_t *cur = cnt + 4 * (C.g & 1), *nxt = cnt + 4 * ((C.g + 1) & 1);
-            {
-                run(3, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(proj_err_kernel<T>, dim3(gs), dim3(256), 0, st, A, (const int32_t *)dp(o_sitems),
-                                       (const int32_t *)cur + 2, nxt + 2, (const int32_t *)dp(o_cand),
-                                       (const uint32_t *)dp(o_candm), (unsigned long long *)dp(o_serr), pc, tk);
-                });
-                run(4, [&](unsigned long long *tk) {
-                    hipLaunchKernelGGL(sgr_advance_kernel, dim3((npairs + 255) / 256), dim3(256), 0, st,
-                                       (Descent *)dp(o_sds), npairs, d_t0, (unsigned long long *)dp(o_serr),
-                                       (int32_t *)dp(o_cand), (uint32_t *)dp(o_candm), (int32_t *)dp(o_ustamp),
-                                       (int32_t *)dp(o_sitems), (const int32_t *)cur + 2, nxt + 2, 0, C.g + 2, sg_spec(), tk);
-                });
-            }
-        }
-        HIP_TRY(hipGetLastError());
-        const int k = (C.head + C.inflight) & 1; // the batch's live count, published after its last advance
-        want[c * 2 + k] = ++s->flag_seq;
-        hipLaunchKernelGGL(lr_publish_kernel, dim3(1), dim3(64), 0, C.stream, (const int32_t *)cnt + 4 * (C.g & 1) + 2 * c,
-                           s->h_flag_dev + (c * 2 + k) * 2, want[c * 2 + k]);
-        HIP_TRY(hipGetLastError());
-        C.inflight++;
-        tr("enqueued", c, C.g);
-        return SVTGPU_OK;
-    };
-    // every early exit below leaves no batch queued behind the caller: both chains' streams are drained, so the
-    // next search on this state may reuse d_work and the pinned staging at once (lr_search.hip:1977)
-    auto drain = [&](int rc) {
-        (void)hipStreamSynchronize(sw);
-        (void)hipStreamSynchronize(st);
-        return rc;
-    };
-    while (ch[0].live || ch[1].live) {
-        for (int c = 0; c < 2; c++)
-            while (ch[c].live && ch[c].inflight < 2)
-                if (int rc = enqueue_batch(c)) return drain(rc);
-        bool       consumed = false; // spin until the oldest batch of a live chain has published its count
-        const auto t_spin   = clk();
-        for (unsigned it = 0; !consumed; it++) {
-            for (int c = 0; c < 2 && !consumed; c++) {
-                Chain &C = ch[c];
-                if (!C.live || !C.inflight) continue;
-                const unsigned long long *f = s->h_flag + (c * 2 + C.head) * 2;
-                if (__atomic_load_n(f, __ATOMIC_ACQUIRE) != want[c * 2 + C.head]) continue;
-                C.live = __atomic_load_n(f + 1, __ATOMIC_RELAXED) > 0;
-                svtgpu_count_xfer(1, 16); // the batch's mapped words
-                C.head ^= 1, C.inflight--, consumed = true;
-                tr(C.live ? "landed-live" : "landed-done", c, C.g);
-                if (C.g > MAX_ROUNDS) { // a descent always terminates; guard anyway (an internal failure)
-                    svtgpu_set_last_hip_error(hipErrorUnknown, "LR descent exceeded its round bound", __FILE__, __LINE__);
-                    return drain(SVTGPU_ERR_HIP);
-                }
-            }
-            // a stalled word (a failed launch): after 200 ms of spinning let the runtime report the stream error
-            if (!consumed && (it & 4095) == 4095 && clk() - t_spin > std::chrono::milliseconds(200)) {
-                HIP_TRY(hipStreamSynchronize(sw));
-                HIP_TRY(hipStreamSynchronize(st));
-                bool any = false;
-                for (int c = 0; c < 2; c++)
-                    any |= ch[c].live && ch[c].inflight &&
-                           __atomic_load_n(s->h_flag + (c * 2 + ch[c].head) * 2, __ATOMIC_ACQUIRE) == want[c * 2 + ch[c].head];
-                if (!any) {
-                    svtgpu_set_last_hip_error(hipErrorUnknown, "LR descent batch word missing after synchronize",
-                                              __FILE__, __LINE__);
-                    return drain(SVTGPU_ERR_HIP);
-                }
-            }
-        }
     }
     mark(2);
     // ---- phase 4: best ep and its clipped SSE; read back the descents ----
@@ -2832,8 +2327,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         prof->bps = bps;
         prof->static_bytes[0] += (all + wn) * 2 * bps; // unit sums, statistics: x and source
         prof->static_bytes[1] += sgb * bps + sgw * 2;     // filters: x in, the int16 planes out (each once)
-        if (sg_res) prof->static_bytes[3] += sgb * 2 * bps + sgp * 4; // resident search: x, source, the planes, once
-        else prof->static_bytes[5] += sgb * 2 * bps + sgp * 4;        // moments: x, source and every ep's two planes in
+        prof->static_bytes[3] += sgb * 2 * bps + sgp * 4; // resident search: x, source and every ep's planes, once
         prof->static_bytes[4] += sgb * (4 + 2 * bps);     // the chosen ep's SSE
     }
     // no wait for the units upload: the next search waits for this event before it rewrites the pinned staging
@@ -2841,8 +2335,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipEventRecord(s->pin_free, st));
     mark(4);
     if (timing)
-        std::fprintf(stderr, "lr_search ms: stats+flt %.3f  host-solve %.3f  rounds(%d wn, %d sg) %.3f  best %.3f  finish %.3f\n",
-                     t_ph[0], t_ph[1], ch[0].g, ch[1].g, t_ph[2], t_ph[3], t_ph[4]);
+        std::fprintf(stderr, "lr_search ms: stats+flt %.3f  seeds %.3f  descents %.3f  best %.3f  finish %.3f\n",
+                     t_ph[0], t_ph[1], t_ph[2], t_ph[3], t_ph[4]);
     return SVTGPU_OK;
 }
 } // namespace

@@ -58,3 +58,29 @@ def test_sgr_resident_row_parts_bit_exact():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, SVTGPU_SR_PART_PX="4096"))
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+
+
+CHILD_TREE = r"""
+import sys
+sys.path[:0] = [%r, %r, %r, %r]
+import torch
+if torch.cuda.is_available():
+    torch.cuda.init()
+import pipeline_run as prun
+for case in ("mini10", "mini8d", "sb128_10", "sbdlf10"):
+    prun.check(case, prun.run_gpu(case), "sr tree")
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nodes", ["3", "7"])
+def test_sgr_resident_speculative_trees_bit_exact(nodes):
+    """The resident self-guided search evaluates one candidate per pass by default; SVTGPU_SR_TREE=3 / 7 evaluate a
+    complete speculative outcome tree per pass (each node built by one control lane from the root's state along its
+    path) -- fewer passes, the same decisions: bit-exact against the reference."""
+    code = CHILD_TREE % (ROOT, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"), os.path.join(ROOT, "oracle"),
+                         os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, SVTGPU_SR_TREE=nodes))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
