@@ -200,6 +200,45 @@ static void *read_all(const char *path, size_t *n) {
     return b;
 }
 
+/* the Wiener statistics of every searched unit, recorded from the reference's own svt_av1_compute_stats(_highbd)_c
+ * calls inside restoration_seg_search: {plane, win, h_start, h_end, v_start, v_end} and M / H per call */
+static struct {
+    EbPictureBufferDesc *pic;
+    int                  n, cap_m, cap_h, nm, nh;
+    int32_t             *meta;
+    int64_t             *M, *H;
+} g_rec;
+static void rec_stats(int32_t win, const uint8_t *dgd, int32_t hs, int32_t he, int32_t vs, int32_t ve, const int64_t *M,
+                      const int64_t *H) {
+    const int win2 = win * win, hbd = g_rec.pic->bit_depth > EB_EIGHT_BIT;
+    int       plane = -1;
+    for (int p = 0; p < 3; p++) {
+        int            st;
+        const uint8_t *b  = plane_ptr(g_rec.pic, p, &st);
+        const size_t   sz = (size_t)st * (p ? g_rec.pic->height / 2 : g_rec.pic->height) << hbd;
+        const uint8_t *a  = hbd ? (const uint8_t *)((uintptr_t)dgd << 1) : dgd;
+        if (a >= b && a < b + sz) plane = p;
+    }
+    g_rec.meta = realloc(g_rec.meta, sizeof(int32_t) * 6 * (g_rec.n + 1));
+    int32_t *m = g_rec.meta + 6 * g_rec.n++;
+    m[0] = plane, m[1] = win, m[2] = hs, m[3] = he, m[4] = vs, m[5] = ve;
+    g_rec.M = realloc(g_rec.M, sizeof(int64_t) * (g_rec.nm + win2));
+    g_rec.H = realloc(g_rec.H, sizeof(int64_t) * (g_rec.nh + win2 * win2));
+    memcpy(g_rec.M + g_rec.nm, M, sizeof(int64_t) * win2), g_rec.nm += win2;
+    memcpy(g_rec.H + g_rec.nh, H, sizeof(int64_t) * win2 * win2), g_rec.nh += win2 * win2;
+}
+static void rec_compute_stats(int32_t win, const uint8_t *dgd, const uint8_t *src, int32_t hs, int32_t he, int32_t vs,
+                              int32_t ve, int32_t ds, int32_t ss, int64_t *M, int64_t *H) {
+    svt_av1_compute_stats_c(win, dgd, src, hs, he, vs, ve, ds, ss, M, H);
+    rec_stats(win, dgd, hs, he, vs, ve, M, H);
+}
+static void rec_compute_stats_highbd(int32_t win, const uint8_t *dgd, const uint8_t *src, int32_t hs, int32_t he,
+                                     int32_t vs, int32_t ve, int32_t ds, int32_t ss, int64_t *M, int64_t *H,
+                                     EbBitDepth bd) {
+    svt_av1_compute_stats_highbd_c(win, dgd, src, hs, he, vs, ve, ds, ss, M, H, bd);
+    rec_stats(win, dgd, hs, he, vs, ve, M, H);
+}
+
 /* ------------------------------------------------------------------------------------------- */
 static int run_pipe(const char *in_path, const char *out_path) {
     size_t         nbytes;
@@ -452,9 +491,23 @@ static int run_pipe(const char *in_path, const char *out_path) {
     svt_aom_link_eb_to_aom_buffer_desc(trial, &trial_frame_rst, 0, 0, hbd);
     svt_aom_link_eb_to_aom_buffer_desc(recon, &org_fts, 0, 0, hbd);
     int32_t *tmpbuf = malloc(RESTORATION_TMPBUF_SIZE);
+#ifndef SVTGPU_BIND
+    g_rec.pic                    = recon; /* record the statistics the search computes (the C kernels, unchanged) */
+    svt_av1_compute_stats        = rec_compute_stats;
+    svt_av1_compute_stats_highbd = rec_compute_stats_highbd;
+#endif
     for (int s = 0; s < pcs->rest_segments_total_count; s++)
         restoration_seg_search(tmpbuf, &org_fts, &cpi_source, &trial_frame_rst, pcs, (uint32_t)s);
     rest_finish_search(pcs);
+#ifndef SVTGPU_BIND
+    svt_av1_compute_stats        = svt_av1_compute_stats_c;
+    svt_av1_compute_stats_highbd = svt_av1_compute_stats_highbd_c;
+    if (g_rec.n) {
+        golden_put2(&g, "wn_stats_meta", 'i', (uint32_t)g_rec.n, 6, g_rec.meta);
+        golden_put1(&g, "wn_stats_M", 'q', (uint32_t)g_rec.nm, g_rec.M);
+        golden_put1(&g, "wn_stats_H", 'q', (uint32_t)g_rec.nh, g_rec.H);
+    }
+#endif
     int32_t ft[3];
     for (int p = 0; p < 3; p++) ft[p] = pcs->rst_info[p].frame_restoration_type;
     if (ft[0] != RESTORE_NONE || ft[1] != RESTORE_NONE || ft[2] != RESTORE_NONE)
@@ -470,12 +523,18 @@ static int run_pipe(const char *in_path, const char *out_path) {
             const RestorationUnitInfo *ui = &rsi->unit_info[k];
             int32_t                   *e  = u + 20 * k;
             e[0]                          = ft[p] == RESTORE_NONE ? 0 : ui->restoration_type;
-            for (int q = 0; q < 8; q++) e[1 + q] = ui->wiener_info.vfilter[q], e[9 + q] = ui->wiener_info.hfilter[q];
-            e[17] = ui->sgrproj_info.ep, e[18] = ui->sgrproj_info.xqd[0], e[19] = ui->sgrproj_info.xqd[1];
+            /* the parameters of the unit's own type only: the reference leaves the others' fields unwritten (their
+             * bytes differ from run to run), so they are stored as zeros and the fixtures are reproducible */
+            if (e[0] == RESTORE_WIENER)
+                for (int q = 0; q < 8; q++) e[1 + q] = ui->wiener_info.vfilter[q], e[9 + q] = ui->wiener_info.hfilter[q];
+            if (e[0] == RESTORE_SGRPROJ)
+                e[17] = ui->sgrproj_info.ep, e[18] = ui->sgrproj_info.xqd[0], e[19] = ui->sgrproj_info.xqd[1];
             const RestUnitSearchInfo *rs = &pcs->rusi_picture[p][k];
             for (int q = 0; q < 3; q++) ss[3 * k + q] = rs->sse[q] == INT64_MAX ? -1 : rs->sse[q];
-            for (int q = 0; q < 8; q++) sp[19 * k + q] = rs->wiener.vfilter[q], sp[19 * k + 8 + q] = rs->wiener.hfilter[q];
-            sp[19 * k + 16] = rs->sgrproj.ep, sp[19 * k + 17] = rs->sgrproj.xqd[0], sp[19 * k + 18] = rs->sgrproj.xqd[1];
+            if (rs->sse[1] != INT64_MAX)
+                for (int q = 0; q < 8; q++) sp[19 * k + q] = rs->wiener.vfilter[q], sp[19 * k + 8 + q] = rs->wiener.hfilter[q];
+            if (rs->sse[2] != INT64_MAX)
+                sp[19 * k + 16] = rs->sgrproj.ep, sp[19 * k + 17] = rs->sgrproj.xqd[0], sp[19 * k + 18] = rs->sgrproj.xqd[1];
         }
         char nm[32];
         snprintf(nm, sizeof nm, "lr_units%d", p);

@@ -7,10 +7,10 @@
 # Each step under its own time limit; the script stops at the first failure.  Output under gpurun_out/r03prof.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r03prof
+O=gpurun_out/${PROF_OUT:-r03prof}
 mkdir -p $O
 export TMPDIR=/tmp
-K="wiener_res|proj_err|sgr_advance|sgr_flt|sgr_mom|sgr_sse|unit_sums|wiener_stats|wiener_solve|cdef_search|cdef_apply|sod_step|dlf_tile|dlf_edge|lr_apply|md_dist"
+K="wiener_res|sgr_res|sgr_flt|sgr_sse|unit_sums|wiener_stats|wiener_solve|cdef_search|cdef_apply|sod_step|dlf_tile|dlf_edge|lr_apply|md_dist"
 B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-matrix --frames-in-flight 1 --no-kernel-timing"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/ubench/fetch_cal.hip -o $O/fetch_cal &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/cal_fetch -o run --output-format csv -- $O/fetch_cal > $O/cal.log 2>&1 &&

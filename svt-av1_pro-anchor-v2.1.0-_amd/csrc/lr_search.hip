@@ -209,7 +209,9 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
     // ---- stage: D rows 0 .. h+5 (columns 0 .. w+5, edge-clamped), then X rows 0 .. h-1, as hi / lo bytes ----
     {
         uint32_t *hi = (uint32_t *)lds, *lo = (uint32_t *)(lds + SM_PLANE);
-        const int ng = (t.w + 6 + 3) >> 2, nd = (t.h + 6) * ng, nx = t.h * (t.w >> 2);
+        // (the frame search's tiles are 4-aligned; the per-unit shim's last tile may end inside a group of 4 -- its
+        // source reads stay inside the staged window and the products mask those pixels, below)
+        const int ng = (t.w + 6 + 3) >> 2, nd = (t.h + 6) * ng, gw = (t.w + 3) >> 2, nx = t.h * gw;
         for (int it = tid; it < nd + nx; it += 256) {
             int v[4], row;
             if (it < nd) {
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
                 for (int k = 0; k < 4; k++) v[k] = px(d, P.dstride, P.W, P.H, y, x + k) - avg;
                 row = row * (SM_RS / 4) + g4;
             } else {
-                const int q = it - nd, r = q / (t.w >> 2), g4 = q - r * (t.w >> 2);
+                const int q = it - nd, r = q / gw, g4 = q - r * gw;
                 int       sv[4];
                 load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + 4 * g4, sv);
 #pragma unroll
@@ -254,7 +256,10 @@ __global__ __launch_bounds__(256) void wiener_stats_kernel(const SearchArgs A, i
     }
     uint32_t cmask[4]; // pixel columns 16 g + 4 q .. +3 inside the tile
 #pragma unroll
-    for (int q = 0; q < 4; q++) cmask[q] = 16 * g + 4 * q < t.w ? 0xFFFFFFFFu : 0u;
+    for (int q = 0; q < 4; q++) { // byte j = pixel column 16 g + 4 q + j
+        const int c = 16 * g + 4 * q;
+        cmask[q]    = c + 4 <= t.w ? 0xFFFFFFFFu : c >= t.w ? 0u : 0xFFFFFFFFu >> (8 * (4 - (t.w - c)));
+    }
     v4i32 hh[NB], ll[NB], hl[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) hh[b] = ll[b] = hl[b] = v4i32{0, 0, 0, 0};
@@ -1896,6 +1901,82 @@ int sr_tree_nodes() {
     return v;
 }
 
+// The statistics of one unit on the matrix cores (svt_av1_compute_stats(_highbd) for 8- and 10-bit samples: the
+// RTCD shim of lr_shims.hip): the unit, its source and a 3-sample border are staged as a small frame (the border
+// replicated past the reference's `half` samples, which no feature of a smaller window reads), cut into <= 64 x 64
+// tiles, run through wiener_stats_kernel and summed per entry; M and H are assembled exactly as wiener_solve_kernel
+// does, each int64 total divided once (EbRestorationPick.c:671-760).
+template <typename T>
+int stats_unit_mfma(int win, const T *dgd, const T *src, int h_start, int h_end, int v_start, int v_end,
+                    int dgd_stride, int src_stride, int64_t *M, int64_t *H, int div) {
+    static_assert(sizeof(T) <= 2, "8- or 16-bit samples");
+    const int half = win >> 1, w = h_end - h_start, h = v_end - v_start;
+    if (w <= 0 || h <= 0 || (win != 7 && win != 5 && win != 3)) return SVTGPU_ERR_INVALID_ARG;
+    const int FW = ((w + 3) & ~3) + 3 + 8, FH = h + 6; // staged frame: unit at (3, 3); 4-aligned source rows + slack
+    std::vector<T> fd((size_t)FW * FH), fs((size_t)FW * FH, (T)0);
+    unsigned long long sum = 0;
+    for (int y = -3; y < h + 3; y++) {
+        const int yy = std::min(std::max(y, -half), h - 1 + half); // the rows the reference may read
+        const T  *row = dgd + (long)(v_start + yy) * dgd_stride + h_start;
+        for (int x = -3; x < FW - 3; x++) fd[(size_t)(y + 3) * FW + x + 3] = row[std::min(std::max(x, -half), w - 1 + half)];
+    }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            fs[(size_t)(y + 3) * FW + x + 3] = src[(long)(v_start + y) * src_stride + h_start + x];
+            sum += dgd[(long)(v_start + y) * dgd_stride + h_start + x];
+        }
+    std::vector<Tile> tiles;
+    for (int y = 0; y < h; y += 64)
+        for (int x = 0; x < w; x += 64) tiles.push_back({0, 0, 3 + x, 3 + y, std::min(64, w - x), std::min(64, h - y)});
+    const URect u{3, 3 + w, 3, 3 + h};
+    const int   nt = (int)tiles.size(), npair = win * (win + 1) / 2, nval = (npair + 1) * 49;
+    Carver      c;
+    const size_t o_d = c(sizeof(T) * fd.size()), o_s = c(sizeof(T) * fs.size()), o_t = c(sizeof(Tile) * nt),
+                 o_u = c(sizeof(URect)), o_t0 = c(8), o_sum = c(8), o_part = c(8 * (size_t)nt * nval);
+    static thread_local void  *buf = nullptr;
+    static thread_local size_t cap = 0;
+    if (c.off > cap) {
+        if (buf) (void)hipFree(buf);
+        buf = nullptr, cap = 0;
+        HIP_TRY(hipMalloc(&buf, c.off));
+        cap = c.off;
+    }
+    uint8_t    *d  = (uint8_t *)buf;
+    hipStream_t st = svtgpu_default_stream();
+    const int32_t t0[2] = {0, nt};
+    HIP_TRY(hipMemcpyAsync(d + o_d, fd.data(), sizeof(T) * fd.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d + o_s, fs.data(), sizeof(T) * fs.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d + o_t, tiles.data(), sizeof(Tile) * nt, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d + o_u, &u, sizeof u, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d + o_t0, t0, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d + o_sum, &sum, 8, hipMemcpyHostToDevice, st));
+    SearchArgs A;
+    std::memset(&A, 0, sizeof A);
+    PlaneArgs &P = A.pl[0];
+    P.dgd = d + o_d, P.src = d + o_s, P.dstride = P.sstride = FW, P.W = FW, P.H = FH;
+    P.bd = sizeof(T) == 1 ? 8 : 10, P.win = win, P.nval = nval;
+    A.tiles = (const Tile *)(d + o_t), A.units = (const URect *)(d + o_u), A.tile0 = (const int32_t *)(d + o_t0);
+    launch_stats(win, [&](auto wc) {
+        hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(nt), dim3(256), 0, st, A, 0,
+                           (const unsigned long long *)(d + o_sum), (long long *)(d + o_part), nullptr);
+    });
+    HIP_TRY(hipGetLastError());
+    std::vector<long long> part((size_t)nt * nval);
+    HIP_TRY(hipMemcpyAsync(part.data(), d + o_part, 8 * part.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<long long> blk(nval, 0);
+    for (int t = 0; t < nt; t++)
+        for (int k = 0; k < nval; k++) blk[k] += part[(size_t)t * nval + k];
+    const int win2 = win * win;
+    for (int k = 0; k < win2; k++) M[k] = blk[npair * 49 + (k / win) * 7 + k % win] / div;
+    for (int t = 0; t < win2 * win2; t++) { // H[k][l]: k = ck * win + rk (the reference's y[] order)
+        const int k = t / win2, l = t % win2, ck = k / win, rk = k % win, cl = l / win, rl = l % win;
+        const int c1 = std::min(ck, cl), c2 = std::max(ck, cl), r1 = ck <= cl ? rk : rl, r2 = ck <= cl ? rl : rk;
+        H[t] = blk[(c1 * win - c1 * (c1 - 1) / 2 + (c2 - c1)) * 49 + r1 * 7 + r2] / div;
+    }
+    return SVTGPU_OK;
+}
+
 // plane p's Wiener window for the controls
 int plane_win(const SvtGpuLrSearchControls *c, int p) {
     const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
@@ -2340,6 +2421,15 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     return SVTGPU_OK;
 }
 } // namespace
+
+int svtgpu_stats_unit_mfma8(int win, const uint8_t *dgd, const uint8_t *src, int h_start, int h_end, int v_start,
+                            int v_end, int dgd_stride, int src_stride, int64_t *M, int64_t *H) {
+    return stats_unit_mfma<uint8_t>(win, dgd, src, h_start, h_end, v_start, v_end, dgd_stride, src_stride, M, H, 1);
+}
+int svtgpu_stats_unit_mfma16(int win, const uint16_t *dgd, const uint16_t *src, int h_start, int h_end, int v_start,
+                             int v_end, int dgd_stride, int src_stride, int64_t *M, int64_t *H, int div) {
+    return stats_unit_mfma<uint16_t>(win, dgd, src, h_start, h_end, v_start, v_end, dgd_stride, src_stride, M, H, div);
+}
 
 extern "C" int svtgpu_lr_controls_for_level(int32_t wn, int32_t sg, SvtGpuLrSearchControls *c) {
     if (!c) return SVTGPU_ERR_INVALID_ARG;

@@ -3,7 +3,8 @@
 // The frame-level search (lr_search.hip) keeps its statistics, filter planes and projections on the device; these
 // entry points exist so the reference's own search loop (EbRestorationPick.c) and its unit tests can run on the
 // device through the function pointers they already call:
-//   svtgpu_av1_compute_stats(_highbd)      ≙ svt_av1_compute_stats(_highbd)   (aom_dsp_rtcd.h:66-68, C :671 / :708)
+//   svtgpu_av1_compute_stats(_highbd)      ≙ svt_av1_compute_stats(_highbd)   (aom_dsp_rtcd.h:66-68, C :671 / :708):
+//                                            the frame search's MFMA kernel (8/10-bit), a VALU kernel (12-bit)
 //   svtgpu_av1_lowbd/highbd_pixel_proj_error ≙ svt_av1_*_pixel_proj_error     (aom_dsp_rtcd.h:79-81, C :167 / :232)
 //   svtgpu_get_proj_subspace               ≙ svt_get_proj_subspace            (aom_dsp_rtcd.h:212, C :560)
 // Every sum is integer on the device; get_proj_subspace's double sums are sums of integers below 2^53 in the
@@ -187,10 +188,13 @@ int64_t pixel_proj_error(const T *src, int32_t width, int32_t height, int32_t sr
 }
 } // namespace
 
+// 8- and 10-bit: the frame search's MFMA statistics kernel (svtgpu_stats_unit_mfma*, lr_search.hip), so the reference's
+// own compute_stats vectors check it directly; 12-bit samples overflow its i32 wave fold and take the VALU kernel above
 extern "C" void svtgpu_av1_compute_stats(int32_t wiener_win, const uint8_t *dgd8, const uint8_t *src8, int32_t h_start,
                                          int32_t h_end, int32_t v_start, int32_t v_end, int32_t dgd_stride,
                                          int32_t src_stride, int64_t *M, int64_t *H) {
-    compute_stats<uint8_t>(wiener_win, dgd8, src8, h_start, h_end, v_start, v_end, dgd_stride, src_stride, M, H, 1);
+    if (svtgpu_stats_unit_mfma8(wiener_win, dgd8, src8, h_start, h_end, v_start, v_end, dgd_stride, src_stride, M, H))
+        svtgpu_fatal("svtgpu_av1_compute_stats");
 }
 
 extern "C" void svtgpu_av1_compute_stats_highbd(int32_t wiener_win, const uint8_t *dgd8, const uint8_t *src8,
@@ -198,6 +202,12 @@ extern "C" void svtgpu_av1_compute_stats_highbd(int32_t wiener_win, const uint8_
                                                 int32_t dgd_stride, int32_t src_stride, int64_t *M, int64_t *H,
                                                 int32_t bit_depth) {
     const int div = bit_depth == 12 ? 16 : bit_depth == 10 ? 4 : 1; // EbRestorationPick.c:716-720
+    if (bit_depth <= 10) {
+        if (svtgpu_stats_unit_mfma16(wiener_win, short_ptr(dgd8), short_ptr(src8), h_start, h_end, v_start, v_end,
+                                     dgd_stride, src_stride, M, H, div))
+            svtgpu_fatal("svtgpu_av1_compute_stats_highbd");
+        return;
+    }
     compute_stats<uint16_t>(wiener_win, short_ptr(dgd8), short_ptr(src8), h_start, h_end, v_start, v_end, dgd_stride,
                             src_stride, M, H, div);
 }

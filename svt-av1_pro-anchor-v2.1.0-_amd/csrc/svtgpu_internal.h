@@ -130,6 +130,11 @@ int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
                              const SvtGpuCdefParams *p, hipStream_t st);
 
 hipStream_t svtgpu_default_stream();
+// svt_av1_compute_stats(_highbd) of one unit on the matrix cores (lr_search.hip; 8- and 10-bit samples)
+int svtgpu_stats_unit_mfma8(int win, const uint8_t *dgd, const uint8_t *src, int h_start, int h_end, int v_start,
+                            int v_end, int dgd_stride, int src_stride, int64_t *M, int64_t *H);
+int svtgpu_stats_unit_mfma16(int win, const uint16_t *dgd, const uint16_t *src, int h_start, int h_end, int v_start,
+                             int v_end, int dgd_stride, int src_stride, int64_t *M, int64_t *H, int div);
 // Host wait for a small device result: the kernel's last workgroup writes the payload into mapped pinned memory,
 // then (after a system-scope fence) the sequence word `seq`.  Spinning on that word returns as soon as it lands;
 // the stream's own synchronize wakes the host up tens of microseconds later, once per host round trip.  Falls

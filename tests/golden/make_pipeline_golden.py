@@ -22,7 +22,7 @@ import pipeline_cases as pc  # noqa: E402
 
 GEN = os.path.join(ROOT, "oracle", "_ref", "gen_golden_pipe")
 OUT = os.path.join(ROOT, "tests", "golden")
-DIGEST_KEYS = ("dlf", "cdef", "lr", "cdef_mse", "cdef_dir", "cdef_var")
+DIGEST_KEYS = ("dlf", "cdef", "lr", "cdef_mse", "cdef_dir", "cdef_var", "wn_stats_M", "wn_stats_H")
 
 
 def run_case(name):

@@ -190,3 +190,40 @@ def test_lr_search_units_bands(ctx, nb):
         fin_ft, fin_units = svtgpu.lr_finish_plane(ctrls, p, merged[p])
         assert fin_ft == ft[p] == want_ft[p]
         assert fin_units.tobytes() == want_units[p].tobytes(), p
+
+
+@pytest.mark.parametrize("case", ["mini10", "mini8", "sb128_10", "mini8c", "c3_4k10"])
+def test_wiener_stats_mfma_vs_reference(ctx, case):
+    """The MFMA Wiener statistics (wiener_stats_kernel: the i8 hi/lo Gram on v_mfma_i32_16x16x64_i8) compared entry by
+    entry with the reference's own svt_av1_compute_stats(_highbd)_c, which gen_golden_pipe records for every unit its
+    restoration_seg_search visits (M and H of each call; SHA-256 of the whole 4K set).  The compute_stats RTCD shim
+    runs the search's kernel on one unit, here over the device's own CDEF output of the case -- a Gram error that
+    flips no tap downstream fails here."""
+    import pipeline_cases as pc
+    import pipeline_run as prun
+    c, g = pc.CASES[case], pc.load(case)
+    out = prun.run_gpu(case, ctx)
+    L, hbd = svtgpu.lib(), c["bd"] > 8
+    pad = [np.pad(np.ascontiguousarray(a, np.uint16 if hbd else np.uint8), 4, mode="edge") for a in out["cdef"]]
+    srcs = [np.ascontiguousarray(a, np.uint16 if hbd else np.uint8) for a in out["src"]]
+    Ms, Hs = [], []
+    for row in g["wn_stats_meta"]:
+        p, win, hs, he, vs, ve = (int(x) for x in row)
+        d, s = pad[p], srcs[p]
+        M, H = np.zeros(win * win, np.int64), np.zeros(win ** 4, np.int64)
+        dp = _at(d, 4, 4, enc=hbd)
+        sp = _at(s, 0, 0, enc=hbd)
+        args = (win, dp, sp, hs, he, vs, ve, d.shape[1], s.shape[1], M.ctypes.data_as(ctypes.c_void_p),
+                H.ctypes.data_as(ctypes.c_void_p))
+        if hbd:
+            L.svtgpu_av1_compute_stats_highbd(*args, c["bd"])
+        else:
+            L.svtgpu_av1_compute_stats(*args)
+        Ms.append(M)
+        Hs.append(H)
+    M, H = np.concatenate(Ms), np.concatenate(Hs)
+    if c["digest"]:
+        assert pc.digest(M) == str(g["sha_wn_stats_M"]) and pc.digest(H) == str(g["sha_wn_stats_H"]), case
+    else:
+        np.testing.assert_array_equal(M, g["wn_stats_M"], err_msg=case)
+        np.testing.assert_array_equal(H, g["wn_stats_H"], err_msg=case)
