@@ -38,10 +38,10 @@ def test_reference_frame_code_through_device_shims(case):
         res = subprocess.run([RTCD_PIPE, "pipe", fin, fout], capture_output=True, text=True, timeout=280)
         assert res.returncode == 0, res.stderr[-2000:]
         out = golden_io.load(fout)
-    assert set(k for k in g if k != "input_sha") <= set(out), sorted(set(g) - set(out))
-    for k in g:
-        if k == "input_sha":
-            continue
+    # the statistics record (wn_stats_*) comes from the pure-C run's recording kernels only
+    keys = set(k for k in g if k != "input_sha" and not k.startswith("wn_stats_"))
+    assert keys <= set(out), sorted(keys - set(out))
+    for k in sorted(keys):
         a, b = np.array(out[k]), np.array(g[k])
         if k.startswith("lr_units"):  # {type, vfilter[8], hfilter[8], ep, xqd[2]}: the fields of the unused filter
             for arr in (a, b):     # are whatever RestorationUnitInfo held before (uninitialised in the reference)
