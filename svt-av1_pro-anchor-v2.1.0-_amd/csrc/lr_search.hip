@@ -363,6 +363,7 @@ __device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF
 // the resident search, sgr_res_kernel).
 // ---------------------------------------------------------------------------------------------
 constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT;
+constexpr int SG_NQ2 = ((SG_B + 1) / 2 * SG_B + SG_NT - 1) / SG_NT; // r = 2 map positions per lane (odd rows only)
 
 // A, B of a self-guided pass from its box sums with 24-bit multiplies where the operands provably fit:
 // b <= 25*1023 >> (bd-8) < 2^24; a*n <= 1.64e6*25 < 2^32 with a < 2^24; (256-A)*sum <= 255*25575 < 2^24 and
@@ -402,21 +403,37 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
     if (threadIdx.x < 256) xby[threadIdx.x] = c_x_by_xplus1[threadIdx.x];
     __syncthreads();
     const uint16_t *v0 = v + 3 * SG_V + 3;
-    const int       bw = t.w + 2, nq = (t.h + 2) * bw;
-    int             s1[SG_NQ], q1[SG_NQ], s2[SG_NQ], q2[SG_NQ];
+    const int       bw = t.w + 2, nq = (t.h + 2) * bw, nq2 = (t.h + 3) / 2 * bw;
+    // the r = 1 map at every position q (map row q / bw = pixel row - 1 .. t.h); the r = 2 map only on the odd pixel
+    // rows (-1, 1, ..): dense position i -> map row 2 (i / bw), so no lane idles on the even rows
+    int s1[SG_NQ], q1[SG_NQ], s2[SG_NQ2], q2[SG_NQ2], m2q[SG_NQ2];
 #pragma unroll
     for (int k = 0; k < SG_NQ; k++) {
         const int q = threadIdx.x + k * SG_NT;
-        s1[k] = q1[k] = s2[k] = q2[k] = 0;
+        s1[k] = q1[k] = 0;
         if (q < nq) {
             const int y = q / bw - 1, x = q % bw - 1;
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                for (int dx = -1; dx <= 1; dx++) {
+                    const int p = v0[(y + dy) * SG_V + x + dx];
+                    s1[k] += p, q1[k] += p * p;
+                }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SG_NQ2; k++) {
+        const int i = threadIdx.x + k * SG_NT, row = i / bw, x = i - row * bw - 1, y = 2 * row - 1;
+        s2[k] = q2[k] = 0;
+        m2q[k] = i < nq2 ? (y + 1) * bw + x + 1 : -1; // the map index the filters read
+        if (i < nq2) {
 #pragma unroll
             for (int dy = -2; dy <= 2; dy++)
 #pragma unroll
                 for (int dx = -2; dx <= 2; dx++) {
                     const int p = v0[(y + dy) * SG_V + x + dx];
                     s2[k] += p, q2[k] += p * p;
-                    if (dy >= -1 && dy <= 1 && dx >= -1 && dx <= 1) s1[k] += p, q1[k] += p * p;
                 }
         }
     }
@@ -430,9 +447,6 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
     for (int k = 0; k < 4; k++) pix[k] = fon && fy0 + k < t.h ? v0[(fy0 + k) * SG_V + fx] : 0;
     const int   fq  = fx + 1;                                             // map column of the lane's pixels
     const size_t fo = (size_t)(t.y0 + fy0) * P.fstride + t.x0 + fx;       // filter-plane offset of row fy0
-    uint32_t    qodd = 0; // bit k: map position k on an odd row
-#pragma unroll
-    for (int k = 0; k < SG_NQ; k++) qodd |= (uint32_t)(((threadIdx.x + k * SG_NT) / bw - 1) & 1) << k;
     const size_t pn = (size_t)P.fstride * P.H;
     const int sh = P.bd - 8;
     auto build_ab = [&](int e) { // A/B maps of ep index e into buffer e & 1
@@ -454,17 +468,15 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
         }
         if (r0) { // r = 2 (5x5) on the odd rows
             const int sp = c_sgr_s[ep][0];
-            uint32_t  z[SG_NQ];
-            int       a[SG_NQ];
+            uint32_t  z[SG_NQ2];
+            int       a[SG_NQ2];
 #pragma unroll
-            for (int k = 0; k < SG_NQ; k++) z[k] = (qodd >> k & 1) ? sgr_z(s2[k], q2[k], 25, sp, sh) : 0u;
+            for (int k = 0; k < SG_NQ2; k++) z[k] = sgr_z(s2[k], q2[k], 25, sp, sh);
 #pragma unroll
-            for (int k = 0; k < SG_NQ; k++) a[k] = xby[z[k]];
+            for (int k = 0; k < SG_NQ2; k++) a[k] = xby[z[k]];
 #pragma unroll
-            for (int k = 0; k < SG_NQ; k++) {
-                const int q = threadIdx.x + k * SG_NT;
-                if (q < nq && (qodd >> k & 1)) m2[q] = sgr_ab_pack(a[k], s2[k], 25);
-            }
+            for (int k = 0; k < SG_NQ2; k++)
+                if (m2q[k] >= 0) m2[m2q[k]] = sgr_ab_pack(a[k], s2[k], 25);
         }
     };
     build_ab(0);
