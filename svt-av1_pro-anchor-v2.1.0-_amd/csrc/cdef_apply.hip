@@ -5,7 +5,8 @@
 // outside the frame (:549-568), so the result equals filtering each FB out-of-place from the DLF
 // output — which is what this kernel does: one workgroup per 64x64 FB reads its (+-2 px) tile into
 // LDS once and writes every output sample of the FB exactly once (filtered, or copied when the FB /
-// block / plane is not filtered).  HBM-bound: 1 read + 1 write per sample (+ the 2-px apron).
+// block / plane is not filtered).  1 read + 1 write per sample (+ the 2-px apron); ~130 integer ops per filtered
+// sample, done two samples per lane on packed int16.
 #include "cdef_common.h"
 
 #define NT 256
@@ -38,15 +39,55 @@ __device__ void stage_tile_a(uint16_t *tile, int ts, int n, const T *plane, int 
     }
 }
 
-template <typename T>
-__device__ void copy_fb_plane(const T *src, int sst, T *dst, int dst_st, int r0, int c0, int n, const int *lim) {
-    for (int i = threadIdx.x; i < n * n; i += NT) {
-        const int r = i / n, c = i - r * n;
-        if (r0 + r >= lim[1] && r0 + r < lim[3] && c0 + c >= lim[0] && c0 + c < lim[2])
-            dst[(long)(r0 + r) * dst_st + c0 + c] = src[(long)(r0 + r) * sst + c0 + c];
+// Two horizontally adjacent output samples (tile row r, columns c, c + 1; one block) of svt_cdef_filter_block_c
+// (EbCdef.c:253-300) on packed int16 lanes, as the search kernel evaluates them: the primary taps with threshold
+// `pri` (strength-adjusted) and weights {4, 2} / {3, 3}, the secondary taps with `sec`, the clamp to the taps' range
+// (0x7F7F outside the frame excluded from the maximum).  The int16 sums wrap exactly as the reference's int16_t sum.
+__device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int ts, int r, int c, int pri, int sec, int dir,
+                                                  int damp, int cs) {
+    const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + CDEF_BORDER);
+    const int       xa = (int16_t)p0[0], xb = (int16_t)p0[1];
+    const s16x2     x  = {(short)xa, (short)xb};
+    const s16x2     pthr = {(short)pri, (short)pri}, sthr = {(short)sec, (short)sec};
+    const unsigned short psh = (unsigned short)max(0, damp - msb32_dev((uint32_t)pri)),
+                         ssh = (unsigned short)max(0, damp - msb32_dev((uint32_t)sec));
+    const u16x2     psv = {psh, psh}, ssv = {ssh, ssh};
+    const int       podd = (pri >> cs) & 1;
+    s16x2           lo = x, hi = x, sum = {0, 0};
+    const int       ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int   op = cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k);
+        const int   o0 = cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k);
+        const int   o1 = cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k);
+        const int   o[6] = {op, -op, o0, -o0, o1, -o1};
+        const short pw = (short)(k ? (podd ? 3 : 2) : (podd ? 3 : 4)), sw = (short)(k ? 1 : 2);
+        s16x2       ps = {0, 0}, ss = {0, 0};
+#pragma unroll
+        for (int t = 0; t < 6; t++) {
+            const s16x2 v  = {(short)p0[o[t]], (short)p0[o[t] + 1]};
+            const s16x2 d  = v - x;
+            const s16x2 ad = __builtin_elementwise_abs(d);
+            const s16x2 sg = {(short)(d.x < 0 ? -1 : 1), (short)(d.y < 0 ? -1 : 1)};
+            lo             = __builtin_elementwise_min(lo, v);
+            const s16x2 vh = {(short)(v.x != CDEF_VERY_LARGE_V ? v.x : x.x), (short)(v.y != CDEF_VERY_LARGE_V ? v.y : x.y)};
+            hi             = __builtin_elementwise_max(hi, vh);
+            if (t < 2) { // constrain(d, thr, damping) = sign(d) * min(|d|, max(0, thr - (|d| >> shift)))
+                ps = ps + __builtin_elementwise_min(ad, __builtin_elementwise_max(pthr - (s16x2)((u16x2)ad >> psv),
+                                                                                  (s16x2){0, 0})) * sg;
+            } else {
+                ss = ss + __builtin_elementwise_min(ad, __builtin_elementwise_max(sthr - (s16x2)((u16x2)ad >> ssv),
+                                                                                  (s16x2){0, 0})) * sg;
+            }
+        }
+        sum = sum + ps * (s16x2){pw, pw} + ss * (s16x2){sw, sw};
     }
+    const s16x2 rnd = (sum + (s16x2){8, 8} + (sum >> (s16x2){15, 15})) >> (s16x2){4, 4};
+    return __builtin_elementwise_max(__builtin_elementwise_min(x + rnd, hi), lo);
 }
 
+// One workgroup per FB: the filtered planes' tiles staged together (one barrier), then every lane writes 8-sample
+// row segments (luma 512, chroma 2 x 128 per FB) as four packed pairs with one vector store each segment.
 template <typename T>
 __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     __shared__ uint16_t ltile[LT * LT];
@@ -72,37 +113,64 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     __syncthreads();
     const bool fb_on = !(level == 0 && sec == 0 && uvl == 0 && uvs == 0) && nlisted > 0; // :397-402
     const int  pw[3] = {A.width, A.width >> 1, A.width >> 1}, ph[3] = {A.height, A.height >> 1, A.height >> 1};
-    for (int pli = 0; pli < 3; pli++) {
-        const int n = pli ? 32 : 64, r0 = n * fbr, c0 = n * fbc;
-        const T  *src = (const T *)A.rec[pli];
-        T        *dst = (T *)A.out[pli];
-        const int lv = pli ? uvl : level, sv = pli ? uvs : sec;
-        const int sh = pli > 0; // the samples written: the plane clipped to the rect (chroma halved, rounded outward)
+    bool       on[3];
+#pragma unroll
+    for (int pli = 0; pli < 3; pli++) { // filtered planes: stage their tiles (:404 `level || sec_strength`)
+        on[pli] = fb_on && (pli ? (uvl || uvs) : (level || sec));
+        if (!on[pli]) continue;
+        const int n = pli ? 32 : 64;
+        stage_tile_a<T>(pli ? ctile[pli - 1] : ltile, pli ? CT : LT, n, (const T *)A.rec[pli], A.rstride[pli], pw[pli],
+                        ph[pli], n * fbr, n * fbc);
+    }
+    __syncthreads();
+    for (int sgi = tid; sgi < 512 + 2 * 128; sgi += NT) {
+        const int pli = sgi < 512 ? 0 : 1 + ((sgi - 512) >> 7), loc = pli ? (sgi - 512) & 127 : sgi;
+        const int n = pli ? 32 : 64, spr = n >> 3, r = loc / spr, c0 = 8 * (loc - r * spr);
+        const int R0 = n * fbr, C0 = n * fbc, sh = pli > 0;
         const int lim[4] = {A.rect[0] >> sh, A.rect[1] >> sh, min(pw[pli], (A.rect[2] + sh) >> sh),
                             min(ph[pli], (A.rect[3] + sh) >> sh)};
-        if (!fb_on || !(lv || sv)) { // unfiltered plane: pass-through (:404 `level || sec_strength`)
-            copy_fb_plane<T>(src, A.rstride[pli], dst, A.ostride[pli], r0, c0, n, lim);
-            continue;
-        }
-        uint16_t *tile = pli ? ctile[pli - 1] : ltile;
-        const int ts   = pli ? CT : LT;
-        stage_tile_a<T>(tile, ts, n, src, A.rstride[pli], pw[pli], ph[pli], r0, c0);
-        __syncthreads();
-        const int pri = lv << cs, secs = sv << cs;
-        const int damp = A.prm.cdef_damping + cs - (pli != 0);
-        const int lb = pli ? 2 : 3;
-        for (int i = tid; i < n * n; i += NT) {
-            const int r = i / n, c = i - r * n;
-            if (r0 + r < lim[1] || r0 + r >= lim[3] || c0 + c < lim[0] || c0 + c >= lim[2]) continue;
-            const int b = (r >> lb) * 8 + (c >> lb);
-            const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + CDEF_BORDER;
-            int v = p[0];
-            if (slisted[b]) {
-                const int t = pli ? pri : cdef_adjust_strength(pri, A.var[(size_t)fb * 64 + b]);
-                const int d = pri ? A.dir[(size_t)fb * 64 + b] : 0;
-                v           = cdef_filter_px(p, ts, t, secs, d, damp, damp, cs);
+        const int y = R0 + r, x0 = C0 + c0;
+        if (y < lim[1] || y >= lim[3] || x0 + 8 <= lim[0] || x0 >= lim[2]) continue;
+        T         out[8];
+        const T  *src = (const T *)A.rec[pli] + (long)y * A.rstride[pli] + x0;
+        if (!on[pli]) { // pass-through
+#pragma unroll
+            for (int j = 0; j < 8; j++) out[j] = x0 + j < pw[pli] ? src[j] : (T)0;
+        } else {
+            const uint16_t *tile = pli ? ctile[pli - 1] : ltile;
+            const int       ts = pli ? CT : LT, lb = pli ? 2 : 3;
+            const int       pri = (pli ? uvl : level) << cs, secs = (pli ? uvs : sec) << cs;
+            const int       damp = A.prm.cdef_damping + cs - (pli != 0);
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const int c = c0 + 2 * h, b = (r >> lb) * 8 + (c >> lb);
+                const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + CDEF_BORDER;
+                s16x2 v = {(short)p[0], (short)p[1]};
+                if (slisted[b]) {
+                    const int t = pli ? pri : cdef_adjust_strength(pri, A.var[(size_t)fb * 64 + b]);
+                    const int d = pri ? A.dir[(size_t)fb * 64 + b] : 0;
+                    v           = cdef_filter_pair(tile, ts, r, c, t, secs, d, damp, cs);
+                }
+                out[2 * h] = (T)v.x, out[2 * h + 1] = (T)v.y;
             }
-            dst[(long)(r0 + r) * A.ostride[pli] + c0 + c] = (T)v;
+        }
+        T *dst = (T *)A.out[pli] + (long)y * A.ostride[pli] + x0;
+        if (x0 >= lim[0] && x0 + 8 <= lim[2]) { // whole segment inside: one vector store
+            if constexpr (sizeof(T) == 2) {
+                uint4 w;
+                w.x = (uint32_t)out[0] | ((uint32_t)out[1] << 16), w.y = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
+                w.z = (uint32_t)out[4] | ((uint32_t)out[5] << 16), w.w = (uint32_t)out[6] | ((uint32_t)out[7] << 16);
+                *(uint4 *)dst = w;
+            } else {
+                uint2 w;
+                w.x = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
+                w.y = (uint32_t)out[4] | ((uint32_t)out[5] << 8) | ((uint32_t)out[6] << 16) | ((uint32_t)out[7] << 24);
+                *(uint2 *)dst = w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (x0 + j >= lim[0] && x0 + j < lim[2]) dst[j] = out[j];
         }
     }
 }
