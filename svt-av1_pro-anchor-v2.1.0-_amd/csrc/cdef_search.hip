@@ -48,23 +48,74 @@ struct PriPair { // two horizontally adjacent samples, packed int16 (lo half = l
     s16x2 sg[4]; // sign(p - x) as +-1
 };
 
+// 8 samples from an 8-aligned position of a plane as four packed int16 pairs (one 16-B / 8-B load)
 template <typename T>
-__device__ __forceinline__ uint16_t ld_px(const void *base, long idx) {
-    return (uint16_t)((const T *)base)[idx];
+__device__ __forceinline__ void ld_seg8(const void *base, long idx, s16x2 out[4]) {
+    const T *p = (const T *)base + idx;
+    if constexpr (sizeof(T) == 2) {
+        const uint4 w = *(const uint4 *)p;
+        out[0] = __builtin_bit_cast(s16x2, w.x), out[1] = __builtin_bit_cast(s16x2, w.y);
+        out[2] = __builtin_bit_cast(s16x2, w.z), out[3] = __builtin_bit_cast(s16x2, w.w);
+    } else {
+        const uint2 b = *(const uint2 *)p;
+        out[0] = __builtin_bit_cast(s16x2, (b.x & 0xFF) | ((b.x & 0xFF00) << 8));
+        out[1] = __builtin_bit_cast(s16x2, ((b.x >> 16) & 0xFF) | ((b.x >> 8) & 0xFF0000));
+        out[2] = __builtin_bit_cast(s16x2, (b.y & 0xFF) | ((b.y & 0xFF00) << 8));
+        out[3] = __builtin_bit_cast(s16x2, ((b.y >> 16) & 0xFF) | ((b.y >> 8) & 0xFF0000));
+    }
 }
 
-// Stage a plane tile (rows r0-2 .. r0+n+1, cols c0-2 .. c0+n+1) into LDS, 0x7F7F outside the plane.
-template <typename T>
-__device__ void stage_tile(uint16_t *tile, int ts, int n, const void *plane, int stride, int pw, int ph, int r0,
-                           int c0) {
-    const int span = n + 2 * CDEF_BORDER;
-    for (int i = threadIdx.x; i < span * span; i += NT) {
-        const int r = i / span, c = i - r * span;
-        const int fr = r0 + r - CDEF_BORDER, fc = c0 + c - CDEF_BORDER;
-        uint16_t  v  = CDEF_VERY_LARGE_V;
-        if (fr >= 0 && fc >= 0 && fr < ph && fc < pw)
-            v = ld_px<T>(plane, (long)fr * stride + fc);
-        tile[r * ts + c] = v;
+// Stage a plane tile (rows r0-2 .. r0+n+1, cols c0-2 .. c0+n+1) into LDS, 0x7F7F outside the plane: every interior
+// 8-sample row segment one vector load (all of a lane's loads in flight before the first LDS store) and four 4-B LDS
+// stores (the tile rows keep the bank-spreading stride TS; the interior starts at column 2), the apron one sample each.
+// The rows are padded to 256 B, so a segment that starts inside the plane reads only its own row.
+template <typename T, int N, int TS>
+__device__ __forceinline__ void stage_tile(uint16_t *tile, const void *plane_, int stride, int pw, int ph, int r0,
+                                           int c0) {
+    const T      *plane = (const T *)plane_;
+    constexpr int ROWS = N + 2 * CDEF_BORDER, SEGS = N / 8, NI = ROWS * SEGS, IT = (NI + NT - 1) / NT;
+    constexpr int NB = ROWS * 4, IB = (NB + NT - 1) / NT;
+    uint4         v[IT];
+#pragma unroll
+    for (int u = 0; u < IT; u++) {
+        const int i = threadIdx.x + u * NT, r = i / SEGS, sg = i % SEGS;
+        const int fr = r0 + r - CDEF_BORDER, fc = c0 + 8 * sg;
+        v[u] = (uint4){0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu, 0x7F7F7F7Fu};
+        if (i >= NI || fr < 0 || fr >= ph || fc >= pw) continue;
+        const T *src = plane + (long)fr * stride + fc;
+        if constexpr (sizeof(T) == 2) {
+            v[u] = *(const uint4 *)src;
+        } else {
+            const uint2 b = *(const uint2 *)src;
+            v[u] = (uint4){(b.x & 0xFF) | ((b.x & 0xFF00) << 8), ((b.x >> 16) & 0xFF) | ((b.x >> 8) & 0xFF0000),
+                           (b.y & 0xFF) | ((b.y & 0xFF00) << 8), ((b.y >> 16) & 0xFF) | ((b.y >> 8) & 0xFF0000)};
+        }
+        if (fc + 8 > pw) { // the plane's last segment of a row (chroma widths of 4 mod 8)
+            uint32_t *q = &v[u].x;
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (fc + j >= pw) q[j >> 1] = (j & 1) ? (q[j >> 1] & 0xFFFFu) | 0x7F7F0000u : (q[j >> 1] & 0xFFFF0000u) | 0x7F7Fu;
+        }
+    }
+    uint16_t b[IB];
+#pragma unroll
+    for (int u = 0; u < IB; u++) {
+        const int i = threadIdx.x + u * NT, r = i >> 2, k = i & 3, dc = k < 2 ? k - 2 : N + k - 2;
+        const int fr = r0 + r - CDEF_BORDER, fc = c0 + dc;
+        b[u] = CDEF_VERY_LARGE_V;
+        if (i < NB && fr >= 0 && fr < ph && fc >= 0 && fc < pw) b[u] = (uint16_t)plane[(long)fr * stride + fc];
+    }
+#pragma unroll
+    for (int u = 0; u < IT; u++) {
+        const int i = threadIdx.x + u * NT, r = i / SEGS, sg = i % SEGS;
+        if (i >= NI) continue;
+        uint32_t *d = (uint32_t *)(tile + r * TS + CDEF_BORDER + 8 * sg); // 4-B aligned: TS and the offset are even
+        d[0] = v[u].x, d[1] = v[u].y, d[2] = v[u].z, d[3] = v[u].w;
+    }
+#pragma unroll
+    for (int u = 0; u < IB; u++) {
+        const int i = threadIdx.x + u * NT, r = i >> 2, k = i & 3, dc = k < 2 ? k - 2 : N + k - 2;
+        if (i < NB) tile[r * TS + CDEF_BORDER + dc] = b[u];
     }
 }
 
@@ -156,8 +207,8 @@ __device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
 
 template <typename T>
 __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
-    __shared__ uint16_t ltile[LT * LT];
-    __shared__ uint16_t ctile[2][CT * CT];
+    __shared__ __attribute__((aligned(16))) uint16_t ltile[LT * LT];
+    __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CT * CT];
     __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
     __shared__ uint32_t sstat[64][2];     // per block source sum, sum^2 (luma)
     __shared__ uint64_t acc_l[64];        // per gi luma distortion
@@ -208,9 +259,9 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     }
 
     // ---- stage tiles ----
-    stage_tile<T>(ltile, LT, 64, A.rec[0], A.rstride[0], A.width, A.height, 64 * fbr, 64 * fbc);
-    stage_tile<T>(ctile[0], CT, 32, A.rec[1], A.rstride[1], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
-    stage_tile<T>(ctile[1], CT, 32, A.rec[2], A.rstride[2], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
+    stage_tile<T, 64, LT>(ltile, A.rec[0], A.rstride[0], A.width, A.height, 64 * fbr, 64 * fbc);
+    stage_tile<T, 32, CT>(ctile[0], A.rec[1], A.rstride[1], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
+    stage_tile<T, 32, CT>(ctile[1], A.rec[2], A.rstride[2], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
     __syncthreads();
 
     // ---- direction per 8x8 luma block (svt_aom_cdef_find_dir_c, EbCdef.c:150-210) ----
@@ -292,12 +343,7 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
         const unsigned short vm = valid ? 0xFFFF : 0;
         // source row (registers), zeroed outside the measured set
         s16x2 sp[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-        if (valid) {
-            const long o = (long)(64 * fbr + r) * A.sstride[0] + 64 * fbc + c0;
-#pragma unroll
-            for (int h = 0; h < 4; h++)
-                sp[h] = (s16x2){(short)ld_px<T>(A.src[0], o + 2 * h), (short)ld_px<T>(A.src[0], o + 2 * h + 1)};
-        }
+        if (valid) ld_seg8<T>(A.src[0], (long)(64 * fbr + r) * A.sstride[0] + 64 * fbc + c0, sp);
         {
             uint32_t s1 = 0, s2 = 0;
 #pragma unroll
@@ -386,15 +432,15 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
         s16x2 sp[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
         unsigned short vm[4];
         int  dirb[4];
+        const int cb0 = by * 8 + (c0 >> 2); // the segment's two 4x4 chroma blocks: cb0, cb0 + 1
+        if (slisted[cb0] || slisted[cb0 + 1]) // inside the plane: listed blocks are in the frame, widths are even
+            ld_seg8<T>(A.src[1 + pl], (long)(32 * fbr + r) * A.sstride[1 + pl] + 32 * fbc + c0, sp);
 #pragma unroll
         for (int h = 0; h < 4; h++) {
-            const int cb = by * 8 + ((c0 + 2 * h) >> 2);
+            const int cb = cb0 + (h >> 1);
             vm[h]   = slisted[cb] ? 0xFFFF : 0;
             dirb[h] = sdir[cb];
-            if (slisted[cb]) {
-                const long o = (long)(32 * fbr + r) * A.sstride[1 + pl] + 32 * fbc + c0 + 2 * h;
-                sp[h] = (s16x2){(short)ld_px<T>(A.src[1 + pl], o), (short)ld_px<T>(A.src[1 + pl], o + 1)};
-            }
+            if (!slisted[cb]) sp[h] = (s16x2){0, 0};
         }
         for (int g = 0; g < 2; g++) {
             const CdefGroupTable &G = grp[2 + g];

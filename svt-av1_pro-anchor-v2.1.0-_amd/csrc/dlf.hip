@@ -71,21 +71,34 @@ __device__ __forceinline__ int tx_log2(const SvtGpuLfMi &m, int vert, int chroma
     return vert ? c_tx_lw[d][m.bsize] : c_tx_lh[d][m.bsize];
 }
 
+// A record read from a grid that was not checked on the host (svtgpu_dlf_set_mode_info_device): fields outside the
+// ranges the tables are indexed by raise *bad and are clamped, so no table read leaves its bounds.
+__device__ __forceinline__ SvtGpuLfMi checked_mi(SvtGpuLfMi m, unsigned long long *bad) {
+    if (bad && (m.bsize >= kNumBsize || m.tx_depth > 2 || m.ref_frame0 < 0 || m.ref_frame0 > 7 || m.mode > 24 ||
+                m.segment_id > 7)) {
+        *bad = 1;
+        m.bsize = min((int)m.bsize, kNumBsize - 1), m.tx_depth = min((int)m.tx_depth, 2);
+        m.ref_frame0 = (int8_t)min(max((int)m.ref_frame0, 0), 7), m.mode = min((int)m.mode, 24);
+        m.segment_id = min((int)m.segment_id, 7);
+    }
+    return m;
+}
+
 __global__ void dlf_edge_records_kernel(const SvtGpuLfMi *__restrict__ mi, int mi_cols, int units_w, int units_h,
-                                        int chroma, int vert, uint32_t *__restrict__ rec) {
+                                        int chroma, int vert, uint32_t *__restrict__ rec, unsigned long long *bad) {
     const int ux = blockIdx.x * blockDim.x + threadIdx.x;
     const int uy = blockIdx.y;
     if (ux >= units_w || uy >= units_h) return;
     const int ss     = chroma;
     const int x      = ux * 4, y = uy * 4;
     const int mi_row = ss | ((y << ss) >> 2), mi_col = ss | ((x << ss) >> 2);
-    const SvtGpuLfMi m = mi[mi_row * mi_cols + mi_col];
+    const SvtGpuLfMi m = checked_mi(mi[mi_row * mi_cols + mi_col], bad);
     const int coord    = vert ? x : y;
     uint32_t  r        = 0;
     const int lt       = tx_log2(m, vert, chroma);
     if (coord && !(coord & ((1 << lt) - 1))) { // a transform edge with a block on the other side
-        const SvtGpuLfMi p = vert ? mi[mi_row * mi_cols + mi_col - (1 << ss)]
-                                  : mi[(mi_row - (1 << ss)) * mi_cols + mi_col];
+        const SvtGpuLfMi p = checked_mi(vert ? mi[mi_row * mi_cols + mi_col - (1 << ss)]
+                                             : mi[(mi_row - (1 << ss)) * mi_cols + mi_col], bad);
         const int cur_skip = m.skip && m.ref_frame0 > 0;
         const int pv_skip  = p.skip && p.ref_frame0 > 0;
         const int lpb      = chroma ? (vert ? c_uvbs_lw[m.bsize] : c_uvbs_lh[m.bsize])
@@ -232,33 +245,54 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
 
-    // edge records reaching the tile (no records outside the plane: length 0)
+    // edge records reaching the tile (no records outside the plane: length 0) and the tile + apron (samples outside
+    // the plane are never read by an active edge), 4 samples per item (gx is a multiple of 4: aligned 8-B / 4-B
+    // loads); every load of a lane is issued before the first LDS store
     constexpr int RV_R = LW / 4, RV_C = TILE / 4 + 3, RH_R = TILE / 4 + 3, RH_C = TILE / 4;
-    for (int i = tid; i < RV_R * RV_C; i += NTHR) {
-        const int ur = gy / 4 + i / RV_C, uc = (x0 - 4) / 4 + i % RV_C;
-        rv[i] = (ur >= 0 && uc >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_v[(size_t)ur * J.units_w + uc] : 0u;
-    }
-    for (int i = tid; i < RH_R * RH_C; i += NTHR) {
-        const int ur = (y0 - 4) / 4 + i / RH_C, uc = x0 / 4 + i % RH_C;
-        rh[i] = (ur >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_h[(size_t)ur * J.units_w + uc] : 0u;
-    }
-
-    // stage the tile + apron (samples outside the plane are never read by an active edge), 4 per item;
-    // gx is a multiple of 4, so interior groups are aligned
-    for (int i = tid; i < LW * LW / 4; i += NTHR) {
-        const int r = gy + i / (LW / 4), c = gx + 4 * (i % (LW / 4));
-        uint16_t  q[4];
-        if (r >= 0 && r < J.ph && c >= 0 && c + 4 <= J.pw) {
-            const T *sp = src + (size_t)r * J.src_stride + c;
+    constexpr int NV = RV_R * RV_C, NH = RH_R * RH_C, IR = (NV + NTHR - 1) / NTHR, IH = (NH + NTHR - 1) / NTHR;
+    constexpr int NS = LW * LW / 4, IS = (NS + NTHR - 1) / NTHR;
+    uint32_t      vrec[IR], hrec[IH];
+    uint2         q[IS];
 #pragma unroll
-            for (int j = 0; j < 4; j++) q[j] = (uint16_t)sp[j];
+    for (int u = 0; u < IR; u++) {
+        const int i = tid + u * NTHR, ur = gy / 4 + i / RV_C, uc = (x0 - 4) / 4 + i % RV_C;
+        vrec[u] = (i < NV && ur >= 0 && uc >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_v[(size_t)ur * J.units_w + uc] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < IH; u++) {
+        const int i = tid + u * NTHR, ur = (y0 - 4) / 4 + i / RH_C, uc = x0 / 4 + i % RH_C;
+        hrec[u] = (i < NH && ur >= 0 && ur * 4 < J.ph && uc * 4 < J.pw) ? J.rec_h[(size_t)ur * J.units_w + uc] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < IS; u++) {
+        const int i = tid + u * NTHR, r = gy + i / (LW / 4), c = gx + 4 * (i % (LW / 4));
+        q[u] = make_uint2(0u, 0u);
+        if (i >= NS || r < 0 || r >= J.ph) continue;
+        const T *sp = src + (size_t)r * J.src_stride + c;
+        if (c >= 0 && c + 4 <= J.pw) {
+            if constexpr (sizeof(T) == 2) {
+                q[u] = *(const uint2 *)sp;
+            } else {
+                const uint32_t b = *(const uint32_t *)sp;
+                q[u] = make_uint2((b & 0xFF) | ((b & 0xFF00) << 8), ((b >> 16) & 0xFF) | ((b >> 8) & 0xFF0000));
+            }
         } else {
+            uint32_t w[2] = {0u, 0u};
 #pragma unroll
             for (int j = 0; j < 4; j++)
-                q[j] = (r >= 0 && c + j >= 0 && r < J.ph && c + j < J.pw) ? (uint16_t)src[(size_t)r * J.src_stride + c + j] : 0;
+                if (c + j >= 0 && c + j < J.pw) w[j >> 1] |= (uint32_t)(uint16_t)sp[j] << (16 * (j & 1));
+            q[u] = make_uint2(w[0], w[1]);
         }
-        *(uint2 *)&t[4 * i] = make_uint2(q[0] | (uint32_t)q[1] << 16, q[2] | (uint32_t)q[3] << 16);
     }
+#pragma unroll
+    for (int u = 0; u < IR; u++)
+        if (tid + u * NTHR < NV) rv[tid + u * NTHR] = vrec[u];
+#pragma unroll
+    for (int u = 0; u < IH; u++)
+        if (tid + u * NTHR < NH) rh[tid + u * NTHR] = hrec[u];
+#pragma unroll
+    for (int u = 0; u < IS; u++)
+        if (tid + u * NTHR < NS) *(uint2 *)&t[4 * (tid + u * NTHR)] = q[u];
     const int tw = min(TILE, J.ox + J.ow - x0), th = min(TILE, J.oy + J.oh - y0);
     {
         __syncthreads();
@@ -307,11 +341,20 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             uint32_t  s = 0; // <= 16 samples per lane
             const T  *ref = (const T *)J.ref;
             const int c = tid % TILE;
-            if (c < tw)
-                for (int r = tid / TILE; r < th; r += NTHR / TILE) {
-                    const int d = (int)t[(APRON + r) * LW + APRON + c] - (int)ref[(size_t)(y0 + r) * J.ref_stride + x0 + c];
+            if (c < tw) {
+                int rv16[TILE / (NTHR / TILE)]; // the lane's source samples, all loads in flight together
+#pragma unroll
+                for (int k = 0; k < TILE / (NTHR / TILE); k++) {
+                    const int r = tid / TILE + k * (NTHR / TILE);
+                    rv16[k] = r < th ? (int)ref[(size_t)(y0 + r) * J.ref_stride + x0 + c] : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < TILE / (NTHR / TILE); k++) {
+                    const int r = tid / TILE + k * (NTHR / TILE);
+                    const int d = r < th ? (int)t[(APRON + r) * LW + APRON + c] - rv16[k] : 0;
                     s += (uint32_t)(d * d);
                 }
+            }
             const unsigned long long sw = wave_sum_u32_wide(s);
             if ((tid & 63) == 63) red[tid >> 6] = sw;
             __syncthreads();
@@ -321,10 +364,17 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
                 atomicAdd(&a.sse[jb * MAX_TRIALS + tr], tot);
             }
         } else {
+            // 4 samples per item: x0 is a multiple of 64 and tw of 4, so every item is whole and aligned
             T *dst = (T *)J.dst;
-            for (int i = tid; i < TILE * TILE; i += NTHR) {
-                const int r = i / TILE, c = i % TILE;
-                if (r < th && c < tw) dst[(size_t)(y0 + r) * J.dst_stride + x0 + c] = (T)t[(APRON + r) * LW + APRON + c];
+            for (int i = tid; i < TILE * TILE / 4; i += NTHR) {
+                const int r = i / (TILE / 4), c = 4 * (i % (TILE / 4));
+                if (r >= th || c >= tw) continue;
+                const uint2 w = *(const uint2 *)&t[(APRON + r) * LW + APRON + c];
+                T *d = dst + (size_t)(y0 + r) * J.dst_stride + x0 + c;
+                if constexpr (sizeof(T) == 2)
+                    *(uint2 *)d = w;
+                else
+                    *(uint32_t *)d = (w.x & 0xFF) | ((w.x >> 8) & 0xFF00) | ((w.y & 0xFF) << 16) | ((w.y & 0xFF0000) << 8);
             }
         }
     }
@@ -390,6 +440,7 @@ struct SvtGpuDlfState {
     unsigned long long *h_sse_dev; // its device address
     unsigned long long  seq;       // last trial launch's sequence number
     int32_t        have_mi;
+    int32_t        mi_on_device = 0; // the last grid came through svtgpu_dlf_set_mode_info_device (checked there)
     // frame tiling over GPUs (svtgpu_dlf_set_tile): trial SSEs over sse_rect, summed over `comm`; the apply writes
     // out_rect (luma {x0, y0, x1, y1}; the whole frame by default)
     int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
@@ -669,9 +720,9 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
     if (e == hipSuccess) e = hipMemset(s->d_sse, 0, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS);
     if (e == hipSuccess) e = hipMemset(s->d_arrive, 0, sizeof(unsigned int));
     if (e == hipSuccess)
-        e = hipHostMalloc(&s->h_sse, sizeof(unsigned long long) * (MAX_JOBS * MAX_TRIALS + 1),
+        e = hipHostMalloc(&s->h_sse, sizeof(unsigned long long) * (MAX_JOBS * MAX_TRIALS + 2),
                           hipHostMallocMapped | hipHostMallocCoherent);
-    if (e == hipSuccess) s->h_sse[MAX_JOBS * MAX_TRIALS] = 0;
+    if (e == hipSuccess) s->h_sse[MAX_JOBS * MAX_TRIALS] = s->h_sse[MAX_JOBS * MAX_TRIALS + 1] = 0;
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&s->h_sse_dev, s->h_sse, 0);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
@@ -697,6 +748,28 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     delete s;
 }
 
+namespace {
+// the edge records of both plane types and directions from s->d_mi; `bad` (device-side checks) or null
+int edge_records(SvtGpuDlfState *s, hipStream_t st, unsigned long long *bad) {
+    for (int c = 0; c < 2; c++)
+        for (int d = 0; d < 2; d++) {
+            hipLaunchKernelGGL(dlf_edge_records_kernel, dim3((s->uw[c] + 127) / 128, s->uh[c]), dim3(128), 0, st,
+                               s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->d_rec[c][d], bad);
+            HIP_TRY(hipGetLastError());
+        }
+    s->have_mi = 1;
+    return SVTGPU_OK;
+}
+
+// a device-side check raised the flag: the grid handed over had records out of range (cleared when reported)
+bool take_bad_mi(SvtGpuDlfState *s) {
+    volatile unsigned long long *f = s->h_sse + MAX_JOBS * MAX_TRIALS + 1;
+    if (!*f) return false;
+    *f = 0;
+    return true;
+}
+} // namespace
+
 extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream) {
     if (!s || !mi) return SVTGPU_ERR_INVALID_ARG;
     const size_t n = (size_t)s->mi_rows * s->mi_cols;
@@ -719,14 +792,19 @@ extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi,
     HIP_TRY(hipMemcpyAsync(s->d_mi, s->h_mi, n * sizeof(SvtGpuLfMi), hipMemcpyHostToDevice, st));
     HIP_TRY(hipEventRecord(s->mi_free, st));
     svtgpu_count_xfer(0, n * sizeof(SvtGpuLfMi));
-    for (int c = 0; c < 2; c++)
-        for (int d = 0; d < 2; d++) {
-            hipLaunchKernelGGL(dlf_edge_records_kernel, dim3((s->uw[c] + 127) / 128, s->uh[c]), dim3(128), 0, st,
-                               s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->d_rec[c][d]);
-            HIP_TRY(hipGetLastError());
-        }
-    s->have_mi = 1;
-    return SVTGPU_OK;
+    s->mi_on_device = 0;
+    return edge_records(s, st, nullptr);
+}
+
+extern "C" int svtgpu_dlf_set_mode_info_device(SvtGpuDlfState *s, const SvtGpuLfMi *d_mi, void *stream) {
+    if (!s || !d_mi) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    // a grid already in HBM (an encoder whose mode decision runs on the device): one copy in stream order, checked
+    // by the records kernel itself -- no host pass over the records, no PCIe
+    HIP_TRY(hipMemcpyAsync(s->d_mi, d_mi, (size_t)s->mi_rows * s->mi_cols * sizeof(SvtGpuLfMi),
+                           hipMemcpyDeviceToDevice, st));
+    s->mi_on_device = 1;
+    return edge_records(s, st, s->h_sse_dev + MAX_JOBS * MAX_TRIALS + 1);
 }
 
 extern "C" int svtgpu_dlf_set_tile(SvtGpuDlfState *s, const int32_t sse_rect[4], const int32_t out_rect[4],
@@ -827,6 +905,11 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
     if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st))) return rc;
+    if (s->mi_on_device) { // the grid was checked by the records kernel: its verdict, once the stream has passed it
+        s->mi_on_device = 0;
+        HIP_TRY(hipStreamSynchronize(st));
+        if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
+    }
     p.filter_level[0] = p.filter_level[1] = ys.best;
     p.filter_level_u = search_uv ? us.best : last[2];
     p.filter_level_v = search_uv ? vs.best : last[3];

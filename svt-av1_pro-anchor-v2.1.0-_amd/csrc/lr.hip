@@ -26,13 +26,14 @@ constexpr int SGR_MAXPX = 64 * 64 / NTHR;
 template <typename T>
 __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h, int eps, const int32_t *xqd,
                          int bd, T *out, size_t os) {
-    const int bw = w + 2;
-    int       f0[SGR_MAXPX];
-    const int r0 = c_sgr_r[eps][0], r1 = c_sgr_r[eps][1];
+    const int     bw = w + 2;
+    const FastDiv dbw(bw), dw(w);
+    int           f0[SGR_MAXPX];
+    const int     r0 = c_sgr_r[eps][0], r1 = c_sgr_r[eps][1];
     if (r0 > 0) { // r = 2 on odd rows -1, 1, 3, ...
         const int nrow = (h + 3) / 2;
         for (int i = threadIdx.x; i < nrow * bw; i += NTHR) {
-            const int y = 2 * (i / bw) - 1, x = i % bw - 1;
+            const int q = dbw(i), y = 2 * q - 1, x = i - q * bw - 1;
             sgr_ab(v, vs, y, x, 2, c_sgr_s[eps][0], bd, &A[(y + 1) * bw + x + 1], &B[(y + 1) * bw + x + 1]);
         }
         __syncthreads();
@@ -40,7 +41,7 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
         for (int k = 0; k < SGR_MAXPX; k++) {
             const int i = threadIdx.x + k * NTHR;
             if (i >= w * h) break;
-            const int y = i / w, x = i % w;
+            const int y = dw(i), x = i - y * w;
             const int *a = A + (y + 1) * bw + x + 1, *b = B + (y + 1) * bw + x + 1;
             int        aa, bb, nb;
             if (!(y & 1)) {
@@ -59,7 +60,7 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
     }
     if (r1 > 0) {
         for (int i = threadIdx.x; i < (h + 2) * bw; i += NTHR) {
-            const int y = i / bw - 1, x = i % bw - 1;
+            const int q = dbw(i), y = q - 1, x = i - q * bw - 1;
             sgr_ab(v, vs, y, x, 1, c_sgr_s[eps][1], bd, &A[i], &B[i]);
         }
         __syncthreads();
@@ -77,7 +78,7 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
     for (int k = 0; k < SGR_MAXPX; k++) {
         const int i = threadIdx.x + k * NTHR;
         if (i >= w * h) break;
-        const int y = i / w, x = i % w;
+        const int y = dw(i), x = i - y * w;
         const int u = (int)v[y * vs + x] << 4;
         int       val = u << 7;
         if (r0 > 0) val += xq0 * (f0[k] - u);
@@ -97,8 +98,9 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
 // frame apply: one workgroup per (stripe, column chunk) of a plane
 // ---------------------------------------------------------------------------------------------
 constexpr int TW = 64, TH = 64;
-constexpr int VS = TW + 8;            // virtual tile columns -3 .. TW+4
-constexpr int VR = TH + 7;            // virtual tile rows -3 .. TH+3
+constexpr int VC0 = 8;                // virtual tile column 0 at LDS column 8 (16-B aligned rows and interior)
+constexpr int VS  = VC0 + TW + 8;     // virtual tile columns -3 .. TW+4
+constexpr int VR  = TH + 7;           // virtual tile rows -3 .. TH+3
 struct LrPlaneArgs {
     const void           *dlf, *cdef;
     void                 *out;
@@ -110,9 +112,11 @@ struct LrPlaneArgs {
 
 template <typename T>
 __global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrPlaneArgs a) {
-    __shared__ uint16_t v[VR * VS];
-    __shared__ uint16_t t[VR * TW];        // Wiener intermediate
+    __shared__ __attribute__((aligned(16))) uint16_t v[VR * VS];
+    // a unit is Wiener or self-guided: the Wiener intermediate (VR x TW u16) shares the A/B arrays' LDS
     __shared__ int      AB[2][(TH + 2) * (TW + 2)];
+    static_assert(VR * TW * 2 <= sizeof(int) * (TH + 2) * (TW + 2), "Wiener intermediate in AB[0]");
+    uint16_t *t = (uint16_t *)AB[0];
     const int S = 64 >> a.ss, off = 8 >> a.ss, cwmax = 64 >> a.ss;
     const int k = a.k0 + blockIdx.x / a.nc, c = a.c0 + blockIdx.x % a.nc;
     const int y0 = max(0, k * S - off), y1 = min((k + 1) * S - off, a.H);
@@ -122,31 +126,74 @@ __global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrPlaneArgs a) {
     const SvtGpuRestUnit u = a.units[ur * a.hunits + uc];
     const T *cdef = (const T *)a.cdef, *dlf = (const T *)a.dlf;
     T       *out  = (T *)a.out;
-    if (u.type == SVTGPU_RESTORE_NONE) {
-        for (int i = threadIdx.x; i < w * h; i += NTHR) {
-            const int y = i / w, x = i % w;
-            out[(size_t)(y0 + y) * a.out_stride + x0 + x] = cdef[(size_t)(y0 + y) * a.cdef_stride + x0 + x];
+    const int segs = (w + 7) >> 3, lseg = cwmax == 64 ? 3 : 2; // 8-sample row segments (w is a multiple of 4)
+    if (u.type == SVTGPU_RESTORE_NONE) { // copy: one vector load / store per segment
+        for (int i = threadIdx.x; i < h << lseg; i += NTHR) {
+            const int y = i >> lseg, sg = i & ((1 << lseg) - 1), x = x0 + 8 * sg;
+            if (sg >= segs) continue;
+            const T *src = cdef + (size_t)(y0 + y) * a.cdef_stride + x;
+            T       *dst = out + (size_t)(y0 + y) * a.out_stride + x;
+            if (x + 8 <= x0 + w) {
+                if constexpr (sizeof(T) == 2) *(uint4 *)dst = *(const uint4 *)src;
+                else *(uint2 *)dst = *(const uint2 *)src;
+            } else {
+                for (int j = 0; j < x0 + w - x; j++) dst[j] = src[j];
+            }
         }
         return;
     }
-    // virtual stripe input (svt_aom_setup_processing_stripe_boundary with saved lines, EbRestoration.c:271-352)
+    // virtual stripe input (svt_aom_setup_processing_stripe_boundary with saved lines, EbRestoration.c:271-352):
+    // the source row of each virtual row, then the row's interior as 8-sample vector loads (all issued before the
+    // LDS stores) and its 3 + 5 apron columns (edge-replicated) one sample each
     const int copy_above = y0 != 0;
     const int copy_below = !(y0 + S - (y0 == 0 ? off : 0) >= a.H);
-    const int vw         = w + 8;
-    for (int i = threadIdx.x; i < (h + 7) * vw; i += NTHR) {
-        const int r = i / vw - 3, cc = i % vw - 3;
-        const int x = min(max(x0 + cc, 0), a.W - 1);
-        int       val;
-        if (r < 0 && copy_above)
-            val = dlf[(size_t)(y0 + (r == -1 ? -1 : -2)) * a.dlf_stride + x];
-        else if (r >= h && r < h + 3 && copy_below)
-            val = dlf[(size_t)min(y1 + (r == h ? 0 : 1), a.H - 1) * a.dlf_stride + x];
-        else
-            val = cdef[(size_t)min(max(y0 + r, 0), a.H - 1) * a.cdef_stride + x];
-        v[(r + 3) * VS + cc + 3] = (uint16_t)val;
+    auto row_of = [&](int r) -> const T * {
+        if (r < 0 && copy_above) return dlf + (size_t)(y0 + (r == -1 ? -1 : -2)) * a.dlf_stride;
+        if (r >= h && r < h + 3 && copy_below) return dlf + (size_t)min(y1 + (r == h ? 0 : 1), a.H - 1) * a.dlf_stride;
+        return cdef + (size_t)min(max(y0 + r, 0), a.H - 1) * a.cdef_stride;
+    };
+    constexpr int IT = (VR * 8 + NTHR - 1) / NTHR;
+    uint4         seg[IT];
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+        const int i = threadIdx.x + q * NTHR, r = (i >> lseg) - 3, sg = i & ((1 << lseg) - 1), x = x0 + 8 * sg;
+        if (r >= h + 4 || sg >= segs) continue;
+        const T *src = row_of(r) + x;
+        if (x + 8 <= a.W) {
+            if constexpr (sizeof(T) == 2) {
+                seg[q] = *(const uint4 *)src;
+            } else {
+                const uint2 b = *(const uint2 *)src;
+                seg[q].x = (b.x & 0xFF) | ((b.x & 0xFF00) << 8), seg[q].y = ((b.x >> 16) & 0xFF) | ((b.x >> 8) & 0xFF0000);
+                seg[q].z = (b.y & 0xFF) | ((b.y & 0xFF00) << 8), seg[q].w = ((b.y >> 16) & 0xFF) | ((b.y >> 8) & 0xFF0000);
+            }
+        } else { // the plane's last segment (chroma widths of 4 mod 8): edge-replicated past W
+            uint32_t *o = &seg[q].x;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                o[j] = (uint32_t)(uint16_t)src[min(2 * j, a.W - 1 - x)] |
+                       ((uint32_t)(uint16_t)src[min(2 * j + 1, a.W - 1 - x)] << 16);
+        }
+    }
+    constexpr int IB = (VR * 8 + NTHR - 1) / NTHR; // apron: columns -3..-1 and w..w+4 of each row
+    uint16_t      ab[IB];
+#pragma unroll
+    for (int q = 0; q < IB; q++) {
+        const int i = threadIdx.x + q * NTHR, r = (i >> 3) - 3, j = i & 7, cc = j < 3 ? j - 3 : w + j - 3;
+        ab[q] = r < h + 4 ? (uint16_t)row_of(r)[min(max(x0 + cc, 0), a.W - 1)] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < IT; q++) {
+        const int i = threadIdx.x + q * NTHR, r = (i >> lseg) - 3, sg = i & ((1 << lseg) - 1);
+        if (r < h + 4 && sg < segs) *(uint4 *)(v + (r + 3) * VS + VC0 + 8 * sg) = seg[q];
+    }
+#pragma unroll
+    for (int q = 0; q < IB; q++) {
+        const int i = threadIdx.x + q * NTHR, r = (i >> 3) - 3, j = i & 7, cc = j < 3 ? j - 3 : w + j - 3;
+        if (r < h + 4) v[(r + 3) * VS + VC0 + cc] = ab[q];
     }
     __syncthreads();
-    const uint16_t *v0 = v + 3 * VS + 3;
+    const uint16_t *v0 = v + 3 * VS + VC0;
     T              *o0 = out + (size_t)y0 * a.out_stride + x0;
     if (u.type == SVTGPU_RESTORE_WIENER)
         wiener_tile(v0, VS, t, TW, w, h, u.hfilter, u.vfilter, a.bd, o0, (size_t)a.out_stride);

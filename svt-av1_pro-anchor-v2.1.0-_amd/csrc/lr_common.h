@@ -76,16 +76,25 @@ __host__ __device__ inline WienerRound wiener_round(int bd) {
 // tile filters over an LDS image `v` (u16, row stride vs) whose (0,0) is the tile's first output
 // ---------------------------------------------------------------------------------------------
 // Wiener: horizontal 8-tap pass into t (rows -3..h+3 -> t rows 0..h+6), vertical pass into out.
+// i / d for 0 <= i < 2^25, 1 <= d <= 128 by one 64-bit multiply: m = ceil(2^32 / d) (exact in that range: the
+// error i * (m - 2^32 / d) / 2^32 stays below the distance 1/d to the next integer)
+struct FastDiv {
+    uint64_t m;
+    __device__ explicit FastDiv(uint32_t d) : m(0xFFFFFFFFull / d + 1) {}
+    __device__ int operator()(int i) const { return (int)(((uint64_t)(uint32_t)i * m) >> 32); }
+};
+
 template <typename T>
 __device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int w, int h, const int16_t *fx,
                             const int16_t *fy, int bd, T *out, size_t os) {
     const WienerRound rr  = wiener_round(bd);
     const int         lim = (1 << (bd + 1 + 7 - rr.r0)) - 1;
+    const FastDiv     dw(w);
     int16_t           hx[8], vy[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) hx[k] = fx[k], vy[k] = fy[k];
     for (int i = threadIdx.x; i < (h + 7) * w; i += NTHR) {
-        const int       y = i / w - 3, x = i % w;
+        const int       q = dw(i), y = q - 3, x = i - q * w;
         const uint16_t *s = v + y * vs + x - 3;
         int             sum = ((int)s[3] << 7) + (1 << (bd + 6));
 #pragma unroll
@@ -95,7 +104,7 @@ __device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int 
     __syncthreads();
     const int maxv = (1 << bd) - 1;
     for (int i = threadIdx.x; i < h * w; i += NTHR) {
-        const int       y = i / w, x = i % w;
+        const int       y = dw(i), x = i - y * w;
         const uint16_t *c = t + y * ts + x; // rows y-3 .. y+4 of the intermediate
         int             sum = ((int)c[3 * ts] << 7) - (1 << (bd + rr.r1 - 1));
 #pragma unroll

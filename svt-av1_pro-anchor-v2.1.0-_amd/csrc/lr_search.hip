@@ -100,6 +100,13 @@ typedef short v2i16 __attribute__((ext_vector_type(2)));
 __device__ inline int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
 }
+// the same with a wave-uniform accumulator input held in an SGPR: the VOP3P form, where the compiler would copy a
+// constant into the destination of an accumulating v_dot2c for every call
+__device__ inline int dot2_s(uint32_t a, uint32_t b, int c_uniform) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c_uniform));
+    return r;
+}
 
 template <typename T>
 __device__ inline void load4(const T *p, int *v) {
@@ -1486,7 +1493,9 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
                                         const uint32_t *s_xq, unsigned long long (*s_red)[SG_NC]) {
     uint32_t xq[NV], acc[NV];
 #pragma unroll
-    for (int c = 0; c < NV; c++) xq[c] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(c < nv ? s_xq[c] : 0u)), acc[c] = 0;
+    // the candidates stay in VGPRs: v_dot2_i32_i16 (VOP3) then takes the rounding constant from an SGPR, with no
+    // per-pixel copy into an accumulating v_dot2c
+    for (int c = 0; c < NV; c++) xq[c] = c < nv ? s_xq[c] : 0u, acc[c] = 0;
 #pragma unroll
     for (int kk = 0; kk < SR_KMAX; kk++) {
         if (kk < K) { // uniform
@@ -1494,11 +1503,11 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const uint32_t w  = q < 2 ? dw.x : dw.y;
-                const int      d1 = (q & 1) ? (int)w >> 16 : (int)(w << 16) >> 16;
-                const int      c0 = 1024 + d1 * 2048; // floor((v + 1024) / 2^11) + (x - src) == (v + c0) >> 11
+                // floor((v + 1024) / 2^11) + (x - src): the int16 half is added as an SDWA operand (no extraction)
+                const int      d1 = (q & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)w;
 #pragma unroll
                 for (int c = 0; c < NV; c++) {
-                    const int ee = dot2(g[kk][q], xq[c], c0) >> 11;
+                    const int ee = (dot2_s(g[kk][q], xq[c], 1024) >> 11) + d1;
                     acc[c] += (uint32_t)(ee * ee);
                 }
             }
@@ -2152,10 +2161,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
                  o_witem = dc(sizeof(WrItem) * (size_t)n_wr), o_sritem = dc(sizeof(SrItem) * (size_t)n_sr);
     const size_t plan_span = dc.off;
-    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all);
+    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_sse2 = dc(8 * (size_t)n_sg), o_wstat = dc(8),
+                 o_sstat = dc(8);
     const size_t zero_span = dc.off - o_sum;
-    const size_t o_sse2 = dc(8 * (size_t)n_sg), o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
-                 o_sds = dc(sizeof(Descent) * npairs), o_wstat = dc(8), o_sstat = dc(8);
+    const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
+                 o_sds = dc(sizeof(Descent) * npairs);
     const size_t res_span = dc.off - o_sse;
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
     const size_t o_best = dc(16 * (size_t)n_sg);
@@ -2232,7 +2242,24 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             s->plan_work = s->d_work;
         }
     }
+    // Every accumulator, status word and exchange arena is zeroed here, before the first kernel: a memset queued
+    // behind the filters would wait for a CU slot while the resident Wiener descent holds them (~140 us at 4K).
     HIP_TRY(hipMemsetAsync(dp(o_sum), 0, zero_span, st));
+    uint8_t *qa = nullptr;
+    if ((n_wn && wr_parted) || (n_sr && sr_parted)) {
+        if (qc.off > s->qarena_bytes) {
+            if (s->d_qarena) (void)hipFree(s->d_qarena);
+            s->d_qarena = nullptr, s->qarena_bytes = 0;
+            HIP_TRY(hipExtMallocWithFlags(&s->d_qarena, qc.off, hipDeviceMallocUncached));
+            s->qarena_bytes = qc.off;
+        }
+        qa = (uint8_t *)s->d_qarena;
+        HIP_TRY(hipMemsetAsync(qa, 0, qc.off, st));
+    }
+    static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
+    static unsigned long long *sr_stat = nullptr;
+    if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 64));
+    if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 64, st));
     run(0, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
@@ -2291,19 +2318,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     mark(1);
     // ---- phase 3: descent rounds on the device ----
-    uint8_t *qa = nullptr;
-    if ((n_wn && wr_parted) || (n_sr && sr_parted)) {
-        if (qc.off > s->qarena_bytes) {
-            if (s->d_qarena) (void)hipFree(s->d_qarena);
-            s->d_qarena = nullptr, s->qarena_bytes = 0;
-            HIP_TRY(hipExtMallocWithFlags(&s->d_qarena, qc.off, hipDeviceMallocUncached));
-            s->qarena_bytes = qc.off;
-        }
-        qa = (uint8_t *)s->d_qarena;
-    }
     if (n_wn) { // the whole Wiener descent of every unit, resident on one CU each (or a few, for the largest)
-        HIP_TRY(hipMemsetAsync(dp(o_wstat), 0, 8, sw));
-        if (wr_parted) HIP_TRY(hipMemsetAsync(qa + q_wrx, 0, 16 * (size_t)n_wr, sw));
         run(2, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
                                (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa ? qa + q_wrx : nullptr),
@@ -2311,13 +2326,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
     }
-    static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
-    static unsigned long long *sr_stat = nullptr;
-    if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 64));
     if (n_sr) { // the whole self-guided search of every (unit, ep), resident on one CU each (or a few)
-        HIP_TRY(hipMemsetAsync(dp(o_sstat), 0, 8, st));
-        if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 64, st));
-        if (sr_parted) HIP_TRY(hipMemsetAsync(qa + q_srx, 0, 128 * (size_t)n_sr, st));
         run(3, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_res_kernel<T>, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
                                (const SrItem *)dp(o_sritem), cfg, sr_tree_nodes(), (Descent *)dp(o_sds),
@@ -2331,7 +2340,6 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     if (n_sg) {
         hipLaunchKernelGGL(sgr_best_kernel, dim3((n_sg + 255) / 256), dim3(256), 0, st, (const Descent *)dp(o_sds), A,
                            sg_planes, n_sg, (int32_t *)dp(o_best));
-        HIP_TRY(hipMemsetAsync(dp(o_sse2), 0, 8 * (size_t)n_sg, st));
         run(4, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
                                (unsigned long long *)dp(o_sse2), tk);

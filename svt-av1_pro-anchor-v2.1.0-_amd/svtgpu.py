@@ -251,6 +251,7 @@ _SIGS = {
     "svtgpu_dlf_state_create": (ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(_P)]),
     "svtgpu_dlf_state_destroy": (None, [_P]),
     "svtgpu_dlf_set_mode_info": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_dlf_set_mode_info_device": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_dlf_frame": (ctypes.c_int, [_P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_frame_to": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
@@ -663,8 +664,15 @@ class DlfState:
         if a.dtype != LF_MI_DTYPE:
             a = np.ascontiguousarray(a.astype(np.uint8).reshape(self.mi_rows, self.mi_cols, 8))
         assert a.nbytes == self.mi_rows * self.mi_cols * 8, (a.shape, self.mi_rows, self.mi_cols)
-        check(lib().svtgpu_dlf_set_mode_info(self.h, ptr(a), stream))
-        self.ctx.synchronize(stream)
+        check(lib().svtgpu_dlf_set_mode_info(self.h, ptr(a), stream))  # staged: `mi` is free on return
+
+    def set_mode_info_device(self, d_mi, stream=None):
+        """The grid from device memory: a CUDA tensor of mi_rows * mi_cols * 8 bytes (or its address)."""
+        if hasattr(d_mi, "data_ptr"):
+            assert d_mi.is_cuda and d_mi.is_contiguous() and d_mi.numel() * d_mi.element_size() == \
+                self.mi_rows * self.mi_cols * 8, (d_mi.shape, self.mi_rows, self.mi_cols)
+            d_mi = d_mi.data_ptr()
+        check(lib().svtgpu_dlf_set_mode_info_device(self.h, _P(d_mi), stream))
 
     def filter(self, frame, params, plane_start=0, plane_end=3, stream=None):
         check(lib().svtgpu_dlf_frame(self.h, frame.h, ctypes.byref(params), plane_start, plane_end, stream))

@@ -160,3 +160,37 @@ def test_plane_sse(ctx):
         for p in range(3):
             want = int(((src[p].astype(np.int64) - rec[p].astype(np.int64)) ** 2).sum())
             assert svtgpu.plane_sse(A, B, p) == want
+
+
+# ------------------------------------------------------------------ mode info handed over in device memory
+@pytest.mark.parametrize("w,h,bd,seed,pk,mk", FRAME_CASES[:3])
+def test_dlf_mode_info_device_matches_host(ctx, w, h, bd, seed, pk, mk):
+    """svtgpu_dlf_set_mode_info_device (the grid already in HBM, checked by the records kernel) filters and searches
+    exactly like the host hand-over; a grid with a record out of range is reported by the next pick."""
+    import torch
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0100 + seed)
+    mi = dc.random_mode_info(w, h, seed, **mk)
+    prm = _params(dict(pk, segments=mk.get("segments", False)), seed)
+    want = oracle.dlf_frame(rec, bd, mi, prm)
+    R, S, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(3))
+    R.upload(rec)
+    S.upload(src)
+    d_mi = torch.from_numpy(np.ascontiguousarray(mi).view(np.uint8).reshape(-1).copy()).cuda()
+    host, dev = svtgpu.DlfState(ctx, w, h), svtgpu.DlfState(ctx, w, h)
+    host.set_mode_info(mi)
+    dev.set_mode_info_device(d_mi)
+    dev.filter_to(R, O, prm)
+    got = O.download()
+    for p in range(3):
+        assert np.array_equal(got[p], want[p]), p
+    start = svtgpu.LfParams.make(16, 16, 8, 8)
+    a = host.pick(R, S, start)
+    b = dev.pick(R, S, start)
+    assert a.levels() == b.levels()
+    bad = np.ascontiguousarray(mi).copy()
+    bad.view(np.uint8).reshape(-1, 8)[len(bad.reshape(-1)) // 2, 0] = 200  # bsize out of range
+    dev.set_mode_info_device(torch.from_numpy(bad.view(np.uint8).reshape(-1).copy()).cuda())
+    with pytest.raises(svtgpu.SvtGpuError, match="error"):
+        dev.pick(R, S, start)
+    dev.set_mode_info_device(d_mi)  # the flag was cleared when reported
+    assert dev.pick(R, S, start).levels() == a.levels()
