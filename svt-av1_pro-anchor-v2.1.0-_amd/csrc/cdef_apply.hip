@@ -29,6 +29,7 @@ struct ApplyArgs {
     const int32_t *var;
     const int8_t  *fb_strength;
     SvtGpuCdefParams prm;
+    unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
 };
 
 // 8 samples of a row from (fr, fc) as 16-bit values, 0x7F7F (CDEF_VERY_LARGE_V) outside the plane: one 16-B (8-B)
@@ -86,55 +87,61 @@ __device__ __forceinline__ void stage_tile_v(uint16_t *tile, const T *plane, int
         if (threadIdx.x + u * NT < NB) tile[bo[u]] = b[u];
 }
 
-// Two horizontally adjacent output samples (tile row r, columns c, c + 1; one block) of svt_cdef_filter_block_c
-// (EbCdef.c:253-300) on packed int16 lanes, as the search kernel evaluates them: the primary taps with threshold
-// `pri` (strength-adjusted) and weights {4, 2} / {3, 3}, the secondary taps with `sec`, the clamp to the taps' range
-// (0x7F7F outside the frame excluded from the maximum).  The int16 sums wrap exactly as the reference's int16_t sum.
-__device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int ts, int r, int c, int pri, int sec, int dir,
-                                                  int damp, int cs) {
-    const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + TC0);
-    const int       xa = (int16_t)p0[0], xb = (int16_t)p0[1];
-    const s16x2     x  = {(short)xa, (short)xb};
-    const s16x2     pthr = {(short)pri, (short)pri}, sthr = {(short)sec, (short)sec};
-    const unsigned short psh = (unsigned short)max(0, damp - msb32_dev((uint32_t)pri)),
-                         ssh = (unsigned short)max(0, damp - msb32_dev((uint32_t)sec));
-    const u16x2     psv = {psh, psh}, ssv = {ssh, ssh};
-    const int       podd = (pri >> cs) & 1;
-    s16x2           lo = x, hi = x, sum = {0, 0};
-    const int       ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
+// Two horizontally adjacent output samples (the pair at p, p + 1 of a tile; one block) of svt_cdef_filter_block_c
+// (EbCdef.c:253-300) on packed int16 lanes: the primary taps (offsets op_k, +-) with threshold `pthr` (strength-
+// adjusted, shift psh) and weights pw0 / pw1 ({4, 2} or {3, 3}), the secondary taps (o0_k, o1_k, +-) with sthr /
+// ssh and weights {2, 1}, then the clamp to the taps' range.  `ofs` holds the block's tap offsets (int16 halves:
+// k = 0 low, k = 1 high) for op, o0, o1.  constrain(d, thr, damping) = sign(d) * min(|d|, m) with
+// m = max(0, thr - (|d| >> shift)) >= 0 is the clamp of d to [-m, m].  EDGE: taps outside the frame (0x7F7F, bit 14
+// set; samples stay below 2^12) are left out of the maximum -- not needed for an FB whose apron is inside the
+// frame.  The int16 sums wrap exactly as the reference's int16_t sum.
+template <bool EDGE>
+__device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *p0, uint4 ofs, s16x2 pthr, u16x2 psh, s16x2 pw0,
+                                                  s16x2 pw1, s16x2 sthr, u16x2 ssh) {
+    const s16x2 x  = {(short)p0[0], (short)p0[1]};
+    s16x2       lo = x, hi = x, sum = {0, 0};
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-        const int   op = cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k);
-        const int   o0 = cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k);
-        const int   o1 = cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k);
-        const int   o[6] = {op, -op, o0, -o0, o1, -o1};
-        const short pw = (short)(k ? (podd ? 3 : 2) : (podd ? 3 : 4)), sw = (short)(k ? 1 : 2);
-        s16x2       ps = {0, 0}, ss = {0, 0};
+        const int op = (int)(int16_t)(k ? ofs.x >> 16 : ofs.x), o0 = (int)(int16_t)(k ? ofs.y >> 16 : ofs.y),
+                  o1 = (int)(int16_t)(k ? ofs.z >> 16 : ofs.z);
+        const int o[6] = {op, -op, o0, -o0, o1, -o1};
+        s16x2     ps = {0, 0}, ss = {0, 0};
 #pragma unroll
         for (int t = 0; t < 6; t++) {
             const s16x2 v  = {(short)p0[o[t]], (short)p0[o[t] + 1]};
             const s16x2 d  = v - x;
-            const s16x2 sg = d >> (s16x2){15, 15}; // -1 where d < 0, else 0
-            const s16x2 ad = (d ^ sg) - sg;
-            lo             = __builtin_elementwise_min(lo, v);
-            // taps outside the frame (0x7F7F: bit 14 set, samples stay below 2^12) drop out of the maximum as 0
-            const s16x2 out = (s16x2)((u16x2)v >> (u16x2){14, 14});
-            hi              = __builtin_elementwise_max(hi, v & (out - (s16x2){1, 1}));
-            // constrain(d, thr, damping) = sign(d) * min(|d|, max(0, thr - (|d| >> shift))): the sign by xor / sub
-            if (t < 2) {
-                const s16x2 m = __builtin_elementwise_min(ad, __builtin_elementwise_max(pthr - (s16x2)((u16x2)ad >> psv),
-                                                                                        (s16x2){0, 0}));
-                ps = ps + ((m ^ sg) - sg);
+            const s16x2 ad = __builtin_elementwise_max(d, (s16x2){0, 0} - d);
+            lo = __builtin_elementwise_min(lo, v);
+            if (EDGE) {
+                const s16x2 out = (s16x2)((u16x2)v >> (u16x2){14, 14});
+                hi = __builtin_elementwise_max(hi, v & (out - (s16x2){1, 1}));
             } else {
-                const s16x2 m = __builtin_elementwise_min(ad, __builtin_elementwise_max(sthr - (s16x2)((u16x2)ad >> ssv),
-                                                                                        (s16x2){0, 0}));
-                ss = ss + ((m ^ sg) - sg);
+                hi = __builtin_elementwise_max(hi, v);
             }
+            const s16x2 m = __builtin_elementwise_max((t < 2 ? pthr : sthr) - (s16x2)((u16x2)ad >> (t < 2 ? psh : ssh)),
+                                                      (s16x2){0, 0});
+            const s16x2 c = __builtin_elementwise_max(__builtin_elementwise_min(d, m), (s16x2){0, 0} - m);
+            if (t < 2) ps = ps + c;
+            else ss = ss + c;
         }
-        sum = sum + ps * (s16x2){pw, pw} + ss * (s16x2){sw, sw};
+        sum = sum + ps * (k ? pw1 : pw0) + ss * (k ? (s16x2){1, 1} : (s16x2){2, 2});
     }
     const s16x2 rnd = (sum + (s16x2){8, 8} + (sum >> (s16x2){15, 15})) >> (s16x2){4, 4};
     return __builtin_elementwise_max(__builtin_elementwise_min(x + rnd, hi), lo);
+}
+
+// the tap offsets of direction `dir` in a tile of row stride ts, packed as cdef_filter_pair reads them
+__device__ __forceinline__ uint4 cdef_tap_offsets(int dir, int ts) {
+    const int ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
+    uint32_t  w[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int o[3] = {cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k), cdef_dir_dy(ds0, k) * ts + cdef_dir_dx(ds0, k),
+                          cdef_dir_dy(ds1, k) * ts + cdef_dir_dx(ds1, k)};
+#pragma unroll
+        for (int q = 0; q < 3; q++) w[q] |= (uint32_t)(uint16_t)o[q] << (16 * k);
+    }
+    return (uint4){w[0], w[1], w[2], 0u};
 }
 
 // One workgroup per FB: the filtered planes' tiles staged together (one barrier), then every lane writes 8-sample
@@ -143,9 +150,11 @@ template <typename T>
 __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     __shared__ __attribute__((aligned(16))) uint16_t ltile[LR * LT];
     __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CR * CT];
-    __shared__ uint8_t  slisted[64], sdir[64];
-    __shared__ int16_t  sadj[64]; // luma primary strength of each 8x8 block, adjusted by its variance
+    __shared__ uint8_t  slisted[64];
+    __shared__ uint32_t sadj[64];    // luma: the block's variance-adjusted primary strength | its shift << 16
+    __shared__ uint4    sofs[2][64]; // the block's tap offsets in the luma / chroma tile
     __shared__ int32_t  nlisted;
+    wgclk_mark(A.wgclk, 0);
     const int fi = xcd_swizzle(blockIdx.x, gridDim.x), fb = A.fb0 + (fi / A.fbw) * A.nhfb + fi % A.fbw;
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
     const int cs = A.cs;
@@ -159,9 +168,12 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     if (tid < 64) {
         const int br = 8 * fbr + (tid >> 3), bc = 8 * fbc + (tid & 7);
         const int l = (8 * br < A.height) && (8 * bc < A.width) && (A.mask ? A.mask[br * A.b8_cols + bc] : 1);
-        slisted[tid] = (uint8_t)l;
-        sdir[tid]    = l ? A.dir[(size_t)fb * 64 + tid] : 0;
-        sadj[tid]    = (int16_t)(l ? cdef_adjust_strength(level << cs, A.var[(size_t)fb * 64 + tid]) : 0);
+        slisted[tid]  = (uint8_t)l;
+        const int dir = l ? A.dir[(size_t)fb * 64 + tid] : 0; // pri_strength ? dir : 0 (EbCdef.c:404)
+        const int t   = l ? cdef_adjust_strength(level << cs, A.var[(size_t)fb * 64 + tid]) : 0;
+        sadj[tid]     = (uint32_t)t | ((uint32_t)max(0, A.prm.cdef_damping + cs - msb32_dev((uint32_t)t)) << 16);
+        sofs[0][tid]  = cdef_tap_offsets(level ? dir : 0, LT);
+        sofs[1][tid]  = cdef_tap_offsets(uvl ? dir : 0, CT);
         if (l) atomicAdd(&nlisted, 1);
     }
     __syncthreads();
@@ -203,30 +215,53 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     }
     // filtered planes: one horizontal pair of samples per lane, consecutive lanes along a row -- a wave's LDS reads
     // of one tap cover 32 consecutive words per tile row (2 lanes per bank, the b32 minimum), and its stores are
-    // whole rows (luma 2048 pairs, chroma 2 x 512)
-    for (int i = tid; i < 2048 + 2 * 512; i += NT) {
-        const int pli = i < 2048 ? 0 : 1 + ((i - 2048) >> 9);
+    // whole rows (luma 2048 pairs, chroma 2 x 512).  An FB whose 2-px apron lies inside the frame has no 0x7F7F taps.
+    const bool interior = fbr > 0 && fbc > 0 && 64 * fbr + 68 <= A.height && 64 * fbc + 68 <= A.width; // chroma: +34
+#pragma unroll
+    for (int pli = 0; pli < 3; pli++) {
         if (!on[pli]) continue;
-        const int j = pli ? (i - 2048) & 511 : i, lp = pli ? 4 : 5; // log2 pairs per row
-        const int r = j >> lp, c = 2 * (j & ((1 << lp) - 1)), n = pli ? 32 : 64, sh = pli > 0;
-        const int y = n * fbr + r, x = n * fbc + c;
-        if (y < (A.rect[1] >> sh) || y >= min(ph[pli], (A.rect[3] + sh) >> sh) || x < (A.rect[0] >> sh) ||
-            x >= min(pw[pli], (A.rect[2] + sh) >> sh))
-            continue; // the rect's x bounds and the plane width are even: a pair is inside or outside whole
+        const int n = pli ? 32 : 64, lp = pli ? 4 : 5, lb = pli ? 2 : 3, ts = pli ? CT : LT, sh = pli > 0;
+        const int xlo = A.rect[0] >> sh, ylo = A.rect[1] >> sh, xhi = min(pw[pli], (A.rect[2] + sh) >> sh),
+                  yhi = min(ph[pli], (A.rect[3] + sh) >> sh);
         const uint16_t *tile = pli ? ctile[pli - 1] : ltile;
-        const int       ts = pli ? CT : LT, lb = pli ? 2 : 3, b = (r >> lb) * 8 + (c >> lb);
-        const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + TC0;
-        s16x2           v = {(short)p[0], (short)p[1]};
-        if (slisted[b]) {
-            const int pri = (pli ? uvl : level) << cs, secs = (pli ? uvs : sec) << cs;
-            const int damp = A.prm.cdef_damping + cs - (pli != 0);
-            v = cdef_filter_pair(tile, ts, r, c, pli ? pri : sadj[b], secs, pri ? sdir[b] : 0, damp, cs);
+        // plane-uniform strengths: the chroma primary (no variance adjustment, EbCdef.c:401) and the secondary
+        const int   damp = A.prm.cdef_damping + cs - (pli != 0);
+        const int   cpri = uvl << cs, secs = (pli ? uvs : sec) << cs, podd_c = (cpri >> cs) & 1;
+        const s16x2 sthr = {(short)secs, (short)secs};
+        const unsigned short ss = (unsigned short)max(0, damp - msb32_dev((uint32_t)secs)),
+                             cs_sh = (unsigned short)max(0, damp - msb32_dev((uint32_t)cpri));
+        const u16x2 ssh = {ss, ss};
+        T *out = (T *)A.out[pli];
+        for (int j = tid; j < (n * n) >> 1; j += NT) {
+            const int r = j >> lp, c = 2 * (j & ((1 << lp) - 1));
+            const int y = n * fbr + r, x = n * fbc + c;
+            if (y < ylo || y >= yhi || x < xlo || x >= xhi) continue; // x bounds are even: a pair is in or out whole
+            const int       b = (r >> lb) * 8 + (c >> lb);
+            const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + TC0;
+            s16x2           v = {(short)p[0], (short)p[1]};
+            if (slisted[b]) {
+                int t = cpri, psh = cs_sh, podd = podd_c;
+                if (!pli) {
+                    const uint32_t a = sadj[b];
+                    t = (int)(a & 0xFFFF), psh = (int)(a >> 16), podd = (t >> cs) & 1;
+                }
+                const s16x2 pthr = {(short)t, (short)t};
+                const u16x2 pshv = {(unsigned short)psh, (unsigned short)psh};
+                const s16x2 pw0 = podd ? (s16x2){3, 3} : (s16x2){4, 4}, pw1 = podd ? (s16x2){3, 3} : (s16x2){2, 2};
+                const uint4 ofs = sofs[pli != 0][b];
+                v = interior ? cdef_filter_pair<false>(p, ofs, pthr, pshv, pw0, pw1, sthr, ssh)
+                             : cdef_filter_pair<true>(p, ofs, pthr, pshv, pw0, pw1, sthr, ssh);
+            }
+            T *dst = out + (long)y * A.ostride[pli] + x;
+            if constexpr (sizeof(T) == 2)
+                *(uint32_t *)dst = (uint32_t)(uint16_t)v.x | ((uint32_t)(uint16_t)v.y << 16);
+            else
+                *(uint16_t *)dst = (uint16_t)((uint8_t)v.x | ((uint8_t)v.y << 8));
         }
-        T *dst = (T *)A.out[pli] + (long)y * A.ostride[pli] + x;
-        if constexpr (sizeof(T) == 2)
-            *(uint32_t *)dst = (uint32_t)(uint16_t)v.x | ((uint32_t)(uint16_t)v.y << 16);
-        else
-            *(uint16_t *)dst = (uint16_t)((uint8_t)v.x | ((uint8_t)v.y << 8));
+    }
+    if (A.wgclk) {
+        __syncthreads();
+        wgclk_mark(A.wgclk, 1);
     }
 }
 
@@ -256,10 +291,12 @@ int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
     A.fb_strength = s->d_fb_strength;
     A.prm         = *p;
     const dim3 grid((r1 - r0) * A.fbw);
+    A.wgclk = svtgpu_wgclk_begin((int)grid.x);
     if (recon->bit_depth > 8)
         hipLaunchKernelGGL(cdef_apply_kernel<uint16_t>, grid, dim3(NT), 0, st, A);
     else
         hipLaunchKernelGGL(cdef_apply_kernel<uint8_t>, grid, dim3(NT), 0, st, A);
     HIP_TRY(hipGetLastError());
+    svtgpu_wgclk_end("cdef_apply", (int)grid.x, st);
     return SVTGPU_OK;
 }

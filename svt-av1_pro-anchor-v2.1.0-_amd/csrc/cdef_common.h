@@ -9,21 +9,19 @@
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// (dy, dx) of svt_aom_eb_cdef_directions[dir][k] (EbCdef.c:99-122), dir in 0..7
+// (dy, dx) of svt_aom_eb_cdef_directions[dir][k] (EbCdef.c:99-122), dir in 0..7.  The tables are nibbles of
+// 32-bit constants (value + 2 at bits 4*dir): a per-lane direction costs one bit-field extract, where a local
+// array indexed by a lane-varying dir would live in scratch memory (one memory load per lookup).
+//   dir:        0   1   2   3   4   5   6   7
+//   k=0 dy:    -1   0   0   0   1   1   1   1
+//   k=1 dy:    -2  -1   0   1   2   2   2   2
+//   k=0 dx:     1   1   1   1   1   0   0   0
+//   k=1 dx:     2   2   2   2   2   1   0  -1
 __device__ __forceinline__ int cdef_dir_dy(int dir, int k) {
-    // dir:        0   1   2   3   4   5   6   7
-    // k=0 dy:    -1   0   0   0   1   1   1   1
-    // k=1 dy:    -2  -1   0   1   2   2   2   2
-    const int t0[8] = {-1, 0, 0, 0, 1, 1, 1, 1};
-    const int t1[8] = {-2, -1, 0, 1, 2, 2, 2, 2};
-    return k ? t1[dir] : t0[dir];
+    return (int)__builtin_amdgcn_ubfe(k ? 0x44443210u : 0x33332221u, 4 * (dir & 7), 4) - 2;
 }
 __device__ __forceinline__ int cdef_dir_dx(int dir, int k) {
-    // k=0 dx:     1   1   1   1   1   0   0   0
-    // k=1 dx:     2   2   2   2   2   1   0  -1
-    const int t0[8] = {1, 1, 1, 1, 1, 0, 0, 0};
-    const int t1[8] = {2, 2, 2, 2, 2, 1, 0, -1};
-    return k ? t1[dir] : t0[dir];
+    return (int)__builtin_amdgcn_ubfe(k ? 0x12344444u : 0x22233333u, 4 * (dir & 7), 4) - 2;
 }
 
 __device__ __forceinline__ int msb32_dev(uint32_t v) { return 31 - __clz((int)(v | 1u)); }

@@ -31,12 +31,13 @@ struct StepArgs {
     const uint64_t *wmse;   // [sb_count][2][64] compacted, bias applied
     const int32_t  *count;  // sb_count, the number of non-skipped FBs (device)
     const int32_t  *wide;   // nonzero when some wmse entry is >= 2^31 (the 32-bit path would not be exact)
-    int32_t         chunk, start_gi, end_gi, step;
+    int32_t         chunk, start_gi, end_gi, step, na; // na: chains in this launch
     uint64_t       *tot;    // [3][4][4096] rotating tot_mse accumulators
     int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
     int32_t        *fin;    // [4][32] final list per chain
     uint64_t       *best;   // [4] value returned by each chain's last call
     StepChain       ch[MAX_CHAINS];
+    unsigned long long *wgclk; // diagnostics or null
 };
 
 // ---- compaction: non-skipped FBs in raster order, zero-strength bias (EbEncCdef.c:820-851) ----
@@ -116,11 +117,16 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     __shared__ uint64_t bv[NT];
     __shared__ int32_t  bi[NT];
     __shared__ int32_t  sl[32];
-    const StepChain C = A.ch[blockIdx.z];
+    // 1-D grid of 4 row tiles x parts x chains, ordered part-major on the logical index and placed so that
+    // consecutive logical indices share an XCD: the 4 * na workgroups staging one FB chunk read it through one L2
+    wgclk_mark(A.wgclk, 0);
+    const int li = xcd_swizzle(blockIdx.x, gridDim.x), tx = li & 3, tz = (li >> 2) % A.na, ty = (li >> 2) / A.na;
+    const int nparts = gridDim.x / (4 * A.na);
+    const StepChain C = A.ch[tz];
     const int t = threadIdx.x, c = C.chain;
-    const int lead = blockIdx.x == 0 && blockIdx.y == 0;
+    const int lead = tx == 0 && ty == 0;
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
-    const int f0 = blockIdx.y * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
+    const int f0 = ty * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
     // 0. start staging this workgroup's FB chunk (independent of the previous call's result)
     if (nfb > 0) { // every load of the lane in flight before the first LDS store (<= PICK_CHUNK * 64 / NT each)
@@ -159,7 +165,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     // 2. zero this workgroup's slice of the accumulator used by the next step
     {
         uint64_t *nxt = A.tot + ((size_t)((A.step + 1) % 3) * MAX_CHAINS + c) * 4096;
-        const int nwg = gridDim.x * gridDim.y, wg = blockIdx.y * gridDim.x + blockIdx.x;
+        const int nwg = 4 * nparts, wg = ty * 4 + tx;
         for (int e = wg * NT + t; e < 4096; e += nwg * NT) nxt[e] = 0;
     }
     if (nfb <= 0) return;
@@ -175,7 +181,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     __syncthreads();
     // 4. accumulate.  When every entry is < 2^31 (the usual case: the check is in pick_gather_kernel), m0 + m1
     // and the min stay in 32 bits and only the running sum is 64-bit: 4 ALU ops per term instead of 7
-    const int k = t & 63, j0 = 16 * blockIdx.x + 4 * (t >> 6);
+    const int k = t & 63, j0 = 16 * tx + 4 * (t >> 6);
     uint64_t  acc[4] = {0, 0, 0, 0};
     if (!*A.wide) {
         const uint32_t *m32 = (const uint32_t *)dyn; // low words: entry e of the chunk at m32[2 * e]
@@ -204,6 +210,10 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         for (int u = 0; u < 4; u++)
             if (j0 + u >= A.start_gi && j0 + u < A.end_gi)
                 atomicAdd((unsigned long long *)&cur[(j0 + u) * 64 + k], (unsigned long long)acc[u]);
+    if (A.wgclk) {
+        __syncthreads();
+        wgclk_mark(A.wgclk, 1);
+    }
 }
 
 // ---- RD choice over the number of signalled strengths (EbEncCdef.c:853-872) ----
@@ -317,7 +327,10 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_max + want - 1) / std::max(want, 1)));
         const int parts = std::max(1, (sb_max + A.chunk - 1) / A.chunk);
         const size_t lds = (size_t)A.chunk * 129 * 8;
-        hipLaunchKernelGGL(sod_step_kernel, dim3(4, parts, na), dim3(NT), lds, st, A);
+        A.na    = na;
+        A.wgclk = svtgpu_wgclk_begin(4 * parts * na);
+        hipLaunchKernelGGL(sod_step_kernel, dim3(4 * parts * na), dim3(NT), lds, st, A);
+        svtgpu_wgclk_end("sod_step", 4 * parts * na, st);
     }
     HIP_TRY(hipGetLastError());
     int32_t *d_gis = A.fin + MAX_CHAINS * 32, *d_nb = d_gis + 32;

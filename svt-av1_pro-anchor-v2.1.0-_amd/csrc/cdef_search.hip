@@ -206,7 +206,7 @@ __device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
+__global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) {
     __shared__ __attribute__((aligned(16))) uint16_t ltile[LT * LT];
     __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CT * CT];
     __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
@@ -265,16 +265,12 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     __syncthreads();
 
     // ---- direction per 8x8 luma block (svt_aom_cdef_find_dir_c, EbCdef.c:150-210) ----
-    // wave w computes directions 2w and 2w+1 for block = lane (direction wave-uniform)
+    // wave w computes directions 2w and 2w+1 for block = lane (direction wave-uniform); the block's rows are read
+    // from LDS inside each direction's accumulation (4 dword reads per row) instead of being held in 64 registers
     {
         const int b = lane, by = b >> 3, bx = b & 7;
-        int       xv[64];
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int j = 0; j < 8; j++)
-                xv[i * 8 + j] = ((int)ltile[(8 * by + i + CDEF_BORDER) * LT + 8 * bx + j + CDEF_BORDER] >> cs) - 128;
         const int w840[9] = {0, 840, 420, 280, 210, 168, 140, 120, 105};
+        const uint16_t *blk = ltile + (8 * by + CDEF_BORDER) * LT + 8 * bx + CDEF_BORDER; // 4-B aligned
 #pragma unroll
         for (int dd = 0; dd < 2; dd++) {
             const int d = 2 * wave + dd;
@@ -283,8 +279,12 @@ __global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
             for (int k = 0; k < 15; k++) line[k] = 0;
             int cost = 0;
             switch (d) { // partial-sum line of sample (i, j) per direction (EbCdef.c:171-179)
-#define ACC(EXPR)                                                                  \
-    _Pragma("unroll") for (int i = 0; i < 8; i++) _Pragma("unroll") for (int j = 0; j < 8; j++) line[EXPR] += xv[i * 8 + j];
+#define ACC(EXPR)                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < 8; i++) {                                                            \
+        const uint32_t *rw = (const uint32_t *)(blk + i * LT);                                                 \
+        const uint32_t  w[4] = {rw[0], rw[1], rw[2], rw[3]};                                                   \
+        _Pragma("unroll") for (int j = 0; j < 8; j++) line[EXPR] += (int)((w[j >> 1] >> (16 * (j & 1)) & 0xFFFFu) >> cs) - 128; \
+    }
             case 0: ACC(i + j) break;
             case 1: ACC(i + j / 2) break;
             case 2: ACC(i) break;

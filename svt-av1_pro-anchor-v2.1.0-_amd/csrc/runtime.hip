@@ -1,5 +1,7 @@
 // runtime.hip — device/context/frame management of the C ABI (include/svtgpu.h).
 #include <atomic>
+#include <cstdio>
+#include <vector>
 #include <cstdlib>
 #include <chrono>
 #include <cstring>
@@ -198,4 +200,40 @@ extern "C" int svtgpu_frame_copy(SvtGpuFrame *dst, const SvtGpuFrame *src, void 
         HIP_TRY(hipMemcpy2DAsync(dst->plane[p], dst->stride[p] * b, src->plane[p], src->stride[p] * b, src->pw[p] * b,
                                  src->ph[p], hipMemcpyDeviceToDevice, pick_stream(dst->ctx, stream)));
     return SVTGPU_OK;
+}
+
+// ---- diagnostics: per-workgroup clocks (svtgpu_internal.h wgclk_mark) ----
+namespace {
+unsigned long long *g_wgclk     = nullptr;
+size_t              g_wgclk_cap = 0;
+} // namespace
+unsigned long long *svtgpu_wgclk_begin(int nblocks) {
+    static const char *path = std::getenv("SVTGPU_WGCLK");
+    if (!path || nblocks <= 0) return nullptr;
+    const size_t bytes = 32 * (size_t)nblocks;
+    if (bytes > g_wgclk_cap) {
+        if (g_wgclk) (void)hipFree(g_wgclk);
+        g_wgclk = nullptr, g_wgclk_cap = 0;
+        if (hipMalloc(&g_wgclk, bytes) != hipSuccess) return nullptr;
+        g_wgclk_cap = bytes;
+    }
+    (void)hipMemset(g_wgclk, 0, bytes);
+    return g_wgclk;
+}
+void svtgpu_wgclk_end(const char *kernel, int nblocks, hipStream_t st) {
+    static const char *path = std::getenv("SVTGPU_WGCLK");
+    if (!path || !g_wgclk || nblocks <= 0) return;
+    std::vector<unsigned long long> h(4 * (size_t)nblocks);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), g_wgclk, 32 * (size_t)nblocks, hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    if (FILE *f = std::fopen(path, "ab")) {
+        char name[64] = {0};
+        std::strncpy(name, kernel, sizeof name - 1);
+        const long long n = nblocks;
+        std::fwrite(name, 1, sizeof name, f);
+        std::fwrite(&n, 8, 1, f);
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+    }
 }

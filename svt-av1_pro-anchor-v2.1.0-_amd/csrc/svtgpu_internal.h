@@ -149,6 +149,24 @@ static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;
 }
 
+// Diagnostics (SVTGPU_WGCLK=<file>, never on by default): per-workgroup start / end on the 100 MHz s_memrealtime
+// clock plus the hardware id words (HW_ID: wave / SIMD / CU / SE, XCC_ID), 4 words per workgroup, appended to the
+// file by the launching host code (svtgpu_wgclk_*).  Written by lane 0 with vector stores.
+__device__ __forceinline__ void wgclk_mark(unsigned long long *buf, int end) {
+    if (!buf || threadIdx.x) return;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    unsigned long long      *q = buf + 4 * (size_t)blockIdx.x;
+    if (!end) {
+        q[0] = t;
+        q[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4); // HW_REG_HW_ID
+        q[3] = (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
+    } else {
+        q[1] = t;
+    }
+}
+unsigned long long *svtgpu_wgclk_begin(int nblocks);               // null unless SVTGPU_WGCLK is set
+void                svtgpu_wgclk_end(const char *kernel, int nblocks, hipStream_t st); // sync + append
+
 // XCD-aware block order (speed only, never correctness): workgroups are dealt round-robin over the 8 XCDs, so
 // blocks b, b + 8, ... share one XCD's L2.  Give each such group a contiguous range of logical indices so tiles that
 // share halo lines (the neighbours of a row-major tile list) are read through the same L2.  Bijective for any n.
