@@ -95,10 +95,17 @@ __device__ __forceinline__ void stage_tile_v(uint16_t *tile, const T *plane, int
 // m = max(0, thr - (|d| >> shift)) >= 0 is the clamp of d to [-m, m].  EDGE: taps outside the frame (0x7F7F, bit 14
 // set; samples stay below 2^12) are left out of the maximum -- not needed for an FB whose apron is inside the
 // frame.  The int16 sums wrap exactly as the reference's int16_t sum.
+// The pair of samples at 16-bit index a of an LDS tile from two aligned dwords (one ds_read2_b32) and a funnel
+// shift: a dword read at an odd sample index is a misaligned LDS access, which the LDS serves far below its rate.
+__device__ __forceinline__ s16x2 lds_pair(const uint16_t *tile, int a) {
+    const uint32_t *w = (const uint32_t *)tile + (a >> 1);
+    return __builtin_bit_cast(s16x2, __builtin_amdgcn_alignbit(w[1], w[0], (a & 1) * 16));
+}
+
 template <bool EDGE>
-__device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *p0, uint4 ofs, s16x2 pthr, u16x2 psh, s16x2 pw0,
-                                                  s16x2 pw1, s16x2 sthr, u16x2 ssh) {
-    const s16x2 x  = {(short)p0[0], (short)p0[1]};
+__device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *tile, int a0, uint4 ofs, s16x2 pthr, u16x2 psh,
+                                                  s16x2 pw0, s16x2 pw1, s16x2 sthr, u16x2 ssh) {
+    const s16x2 x  = __builtin_bit_cast(s16x2, *(const uint32_t *)(tile + a0)); // a0 is even
     s16x2       lo = x, hi = x, sum = {0, 0};
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -108,7 +115,7 @@ __device__ __forceinline__ s16x2 cdef_filter_pair(const uint16_t *p0, uint4 ofs,
         s16x2     ps = {0, 0}, ss = {0, 0};
 #pragma unroll
         for (int t = 0; t < 6; t++) {
-            const s16x2 v  = {(short)p0[o[t]], (short)p0[o[t] + 1]};
+            const s16x2 v  = lds_pair(tile, a0 + o[t]);
             const s16x2 d  = v - x;
             const s16x2 ad = __builtin_elementwise_max(d, (s16x2){0, 0} - d);
             lo = __builtin_elementwise_min(lo, v);
@@ -177,6 +184,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         if (l) atomicAdd(&nlisted, 1);
     }
     __syncthreads();
+    wgclk_mark(A.wgclk, 1);
     const bool fb_on = !(level == 0 && sec == 0 && uvl == 0 && uvs == 0) && nlisted > 0; // :397-402
     const int  pw[3] = {A.width, A.width >> 1, A.width >> 1}, ph[3] = {A.height, A.height >> 1, A.height >> 1};
     bool       on[3];
@@ -191,6 +199,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
                                 32 * fbc);
     }
     __syncthreads();
+    wgclk_mark(A.wgclk, 2);
     // planes not filtered: 8-sample row segments copied with one vector load / store each
     for (int sgi = tid; sgi < 512 + 2 * 128; sgi += NT) {
         const int pli = sgi < 512 ? 0 : 1 + ((sgi - 512) >> 7), loc = pli ? (sgi - 512) & 127 : sgi;
@@ -213,6 +222,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
                 if (x0 + j >= lim[0] && x0 + j < lim[2]) dst[j] = src[j];
         }
     }
+    wgclk_mark(A.wgclk, 3);
     // filtered planes: one horizontal pair of samples per lane, consecutive lanes along a row -- a wave's LDS reads
     // of one tap cover 32 consecutive words per tile row (2 lanes per bank, the b32 minimum), and its stores are
     // whole rows (luma 2048 pairs, chroma 2 x 512).  An FB whose 2-px apron lies inside the frame has no 0x7F7F taps.
@@ -237,8 +247,8 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
             const int y = n * fbr + r, x = n * fbc + c;
             if (y < ylo || y >= yhi || x < xlo || x >= xhi) continue; // x bounds are even: a pair is in or out whole
             const int       b = (r >> lb) * 8 + (c >> lb);
-            const uint16_t *p = tile + (r + CDEF_BORDER) * ts + c + TC0;
-            s16x2           v = {(short)p[0], (short)p[1]};
+            const int       a0 = (r + CDEF_BORDER) * ts + c + TC0; // even: ts, c and TC0 are
+            s16x2           v  = __builtin_bit_cast(s16x2, *(const uint32_t *)(tile + a0));
             if (slisted[b]) {
                 int t = cpri, psh = cs_sh, podd = podd_c;
                 if (!pli) {
@@ -249,8 +259,8 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
                 const u16x2 pshv = {(unsigned short)psh, (unsigned short)psh};
                 const s16x2 pw0 = podd ? (s16x2){3, 3} : (s16x2){4, 4}, pw1 = podd ? (s16x2){3, 3} : (s16x2){2, 2};
                 const uint4 ofs = sofs[pli != 0][b];
-                v = interior ? cdef_filter_pair<false>(p, ofs, pthr, pshv, pw0, pw1, sthr, ssh)
-                             : cdef_filter_pair<true>(p, ofs, pthr, pshv, pw0, pw1, sthr, ssh);
+                v = interior ? cdef_filter_pair<false>(tile, a0, ofs, pthr, pshv, pw0, pw1, sthr, ssh)
+                             : cdef_filter_pair<true>(tile, a0, ofs, pthr, pshv, pw0, pw1, sthr, ssh);
             }
             T *dst = out + (long)y * A.ostride[pli] + x;
             if constexpr (sizeof(T) == 2)
@@ -261,7 +271,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     }
     if (A.wgclk) {
         __syncthreads();
-        wgclk_mark(A.wgclk, 1);
+        wgclk_mark(A.wgclk, 5);
     }
 }
 

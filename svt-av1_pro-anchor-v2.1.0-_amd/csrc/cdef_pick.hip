@@ -79,7 +79,7 @@ __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *
 
 // First minimum of tot over [start, end)^2 (svt_search_one_dual's final loop, EbEncCdef.c:670-679),
 // computed by every workgroup that needs it.  Returns (best, e = j*64 + k) through LDS.
-__device__ void tot_argmin(const uint64_t *tot, int start, int end, uint64_t *bv, int32_t *bi) {
+__device__ __forceinline__ void tot_argmin(const uint64_t *tot, int start, int end, uint64_t *bv, int32_t *bi) {
     const int t    = threadIdx.x;
     uint64_t  best = (uint64_t)1 << 63; // best_tot_mse initial value (EbEncCdef.c:632)
     int       idx  = 1 << 30;
@@ -128,18 +128,19 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
     const int f0 = ty * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
-    // 0. start staging this workgroup's FB chunk (independent of the previous call's result)
-    if (nfb > 0) { // every load of the lane in flight before the first LDS store (<= PICK_CHUNK * 64 / NT each)
-        const uint4  *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
-        uint4        *dst = (uint4 *)dyn;
-        constexpr int IT  = PICK_CHUNK * 64 / NT;
-        uint4         v[IT];
-#pragma unroll
-        for (int u = 0; u < IT; u++) v[u] = src[min(t + u * NT, nfb * 64 - 1)]; // clamped: unconditional loads
-#pragma unroll
-        for (int u = 0; u < IT; u++)
-            if (t + u * NT < nfb * 64) dst[t + u * NT] = v[u];
-    }
+    const int wide = *A.wide;
+    // 0. issue the loads of this workgroup's FB chunk (independent of the previous call's result); they stay in
+    // flight through the previous call's argmin and land in LDS after it (<= PICK_CHUNK * 64 / NT each)
+    static_assert(PICK_CHUNK * 64 / NT == 12, "twelve staging registers per lane");
+    // unconditional loads, the index clamped into the chunk (a chunk past the live FBs reads its first entry:
+    // f0 < the FB count the buffer holds, so the address is inside it); named registers, not an array, so they
+    // stay in VGPRs across the argmin
+    const uint4 *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
+    const int    lim = max(nfb, 1) * 64 - 1;
+#define LD(u) const uint4 v##u = src[min(t + (u) * NT, lim)];
+    LD(0) LD(1) LD(2) LD(3) LD(4) LD(5) LD(6) LD(7) LD(8) LD(9) LD(10) LD(11)
+#undef LD
+    wgclk_mark(A.wgclk, 1);
     // 1. selection entering this call
     if (t < 32) sl[t] = A.step ? A.lev[((size_t)(A.step - 1) * MAX_CHAINS + c) * 32 + t] : 0;
     if (C.prev_nb_sel >= 0) {
@@ -156,11 +157,19 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
             if (lead && C.nb_sel < 0) A.best[c] = any ? bv[0] : ((uint64_t)1 << 63);
         }
     }
+    if (nfb > 0) {
+        uint4 *dst = (uint4 *)dyn;
+#define ST(u) \
+    if (t + (u) * NT < nfb * 64) dst[t + (u) * NT] = v##u;
+        ST(0) ST(1) ST(2) ST(3) ST(4) ST(5) ST(6) ST(7) ST(8) ST(9) ST(10) ST(11)
+#undef ST
+    }
     __syncthreads();
     if (C.nb_sel < 0) { // the chain's last call has finished: publish its list
         if (t < 32) A.fin[c * 32 + t] = sl[t];
         return;
     }
+    wgclk_mark(A.wgclk, 2);
     if (lead && t < 32) A.lev[((size_t)A.step * MAX_CHAINS + c) * 32 + t] = sl[t];
     // 2. zero this workgroup's slice of the accumulator used by the next step
     {
@@ -179,13 +188,14 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         sbest[t] = b;
     }
     __syncthreads();
+    wgclk_mark(A.wgclk, 3);
     // 4. accumulate.  When every entry is < 2^31 (the usual case: the check is in pick_gather_kernel), m0 + m1
     // and the min stay in 32 bits and only the running sum is 64-bit: 4 ALU ops per term instead of 7
     const int k = t & 63, j0 = 16 * tx + 4 * (t >> 6);
     uint64_t  acc[4] = {0, 0, 0, 0};
-    if (!*A.wide) {
+    if (!wide) {
         const uint32_t *m32 = (const uint32_t *)dyn; // low words: entry e of the chunk at m32[2 * e]
-        for (int f = 0; f < nfb; f++) {
+        auto term = [&](int f) {
             const uint64_t b64 = sbest[f];
             const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[2 * (f * 128 + 64 + k)];
 #pragma unroll
@@ -193,7 +203,13 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
                 const uint32_t v = m32[2 * (f * 128 + j0 + u)] + m1k;
                 acc[u] += min(v, b);
             }
+        };
+        int f = 0;
+        for (; f + 4 <= nfb; f += 4) { // 4 FBs per iteration: their LDS reads issue together
+#pragma unroll
+            for (int q = 0; q < 4; q++) term(f + q);
         }
+        for (; f < nfb; f++) term(f);
     } else {
         for (int f = 0; f < nfb; f++) {
             const uint64_t b = sbest[f], m1k = m[f][64 + k];
@@ -204,6 +220,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
             }
         }
     }
+    wgclk_mark(A.wgclk, 4);
     uint64_t *cur = A.tot + ((size_t)(A.step % 3) * MAX_CHAINS + c) * 4096;
     if (k >= A.start_gi && k < A.end_gi)
 #pragma unroll
@@ -212,7 +229,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
                 atomicAdd((unsigned long long *)&cur[(j0 + u) * 64 + k], (unsigned long long)acc[u]);
     if (A.wgclk) {
         __syncthreads();
-        wgclk_mark(A.wgclk, 1);
+        wgclk_mark(A.wgclk, 5);
     }
 }
 

@@ -40,6 +40,7 @@ struct SearchArgs {
     int32_t        nfb, fb0, fbw; // searched filter blocks: fb0 + (i / fbw) * nhfb + i % fbw
     int32_t        cs, ss, damping;
     CdefStrengthTable tab;
+    unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
 };
 
 struct PriPair { // two horizontally adjacent samples, packed int16 (lo half = left sample)
@@ -131,10 +132,18 @@ __device__ __forceinline__ s16x2 constrain2(s16x2 ad, s16x2 sg, s16x2 thr, u16x2
 
 // Neighbourhood of the pair at tile (r, c), (r, c+1) for direction `dir`: keeps the primary taps
 // and the clamp range, and returns the secondary sums S[1..3] for the secondary codes in `sec_used`.
+// The pair of samples at 16-bit index a of an LDS tile from two aligned dwords (one ds_read2_b32) and a funnel
+// shift: a dword read at an odd sample index is a misaligned LDS access, which the LDS serves far below its rate.
+__device__ __forceinline__ uint32_t lds_pair_u32(const uint16_t *tile, int a) {
+    const uint32_t *w = (const uint32_t *)tile + (a >> 1);
+    return __builtin_amdgcn_alignbit(w[1], w[0], (a & 1) * 16);
+}
+
 __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t *tile, int ts, int r, int c,
                                           int dir, int sec_used, int sdamp, int cs) {
-    const uint16_t *p0 = tile + (r + CDEF_BORDER) * ts + (c + CDEF_BORDER);
-    const int       xa = (int16_t)p0[0], xb = (int16_t)p0[1];
+    const int       a0 = (r + CDEF_BORDER) * ts + (c + CDEF_BORDER); // even: ts and c are
+    const uint32_t  xw = *(const uint32_t *)(tile + a0);
+    const int       xa = (int16_t)(xw & 0xFFFF), xb = (int16_t)(xw >> 16);
     int             loa = xa, hia = xa, lob = xb, hib = xb;
     const int       ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
     s16x2           sad[8], ssg[8];
@@ -146,7 +155,8 @@ __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t
         const int o[6] = {op, -op, o0, -o0, o1, -o1};
 #pragma unroll
         for (int t = 0; t < 6; t++) {
-            const int va = (int16_t)p0[o[t]], vb = (int16_t)p0[o[t] + 1];
+            const uint32_t vw = lds_pair_u32(tile, a0 + o[t]);
+            const int      va = (int16_t)(vw & 0xFFFF), vb = (int16_t)(vw >> 16);
             if (va != CDEF_VERY_LARGE_V) hia = max(hia, va);
             if (vb != CDEF_VERY_LARGE_V) hib = max(hib, vb);
             loa = min(loa, va);
@@ -206,7 +216,7 @@ __device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) {
+__global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
     __shared__ __attribute__((aligned(16))) uint16_t ltile[LT * LT];
     __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CT * CT];
     __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
@@ -220,6 +230,7 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
     __shared__ int32_t  nlisted;
     __shared__ CdefGroupTable grp[4]; // luma A, luma B, chroma A, chroma B
 
+    wgclk_mark(A.wgclk, 0);
     const int fi = xcd_swizzle(blockIdx.x, gridDim.x), fb = A.fb0 + (fi / A.fbw) * A.nhfb + fi % A.fbw;
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -258,12 +269,14 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
         return;
     }
 
+    wgclk_mark(A.wgclk, 1);
     // ---- stage tiles ----
     stage_tile<T, 64, LT>(ltile, A.rec[0], A.rstride[0], A.width, A.height, 64 * fbr, 64 * fbc);
     stage_tile<T, 32, CT>(ctile[0], A.rec[1], A.rstride[1], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
     stage_tile<T, 32, CT>(ctile[1], A.rec[2], A.rstride[2], A.width >> 1, A.height >> 1, 32 * fbr, 32 * fbc);
     __syncthreads();
 
+    wgclk_mark(A.wgclk, 2);
     // ---- direction per 8x8 luma block (svt_aom_cdef_find_dir_c, EbCdef.c:150-210) ----
     // wave w computes directions 2w and 2w+1 for block = lane (direction wave-uniform); the block's rows are read
     // from LDS inside each direction's accumulation (4 dword reads per row) instead of being held in 64 registers
@@ -334,6 +347,7 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
     const int ss    = A.ss;
     const int nstr  = A.tab.nstr;
 
+    wgclk_mark(A.wgclk, 3);
     // ================= luma: 2 passes of 32 blocks; lane = one 8-sample row =================
     for (int pass = 0; pass < 2; pass++) {
         const int bip = tid >> 3, row = tid & 7; // block in pass, row in block
@@ -424,6 +438,7 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
         __syncthreads();
     }
 
+    wgclk_mark(A.wgclk, 4);
     // ================= chroma: both planes in one pass; lane = one 8-sample row =================
     {
         const int pl = tid >> 7, q = tid & 127, r = q >> 2, c0 = (q & 3) * 8;
@@ -501,6 +516,7 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
         }
         if (tid == 0) A.skip[fb] = 0;
     }
+    wgclk_mark(A.wgclk, 5);
 }
 
 int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src,
@@ -530,10 +546,12 @@ int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon,
     A.damping = damping;
     A.tab     = *tab;
     const dim3 grid((s->fb_rect[3] - s->fb_rect[1]) * A.fbw);
+    A.wgclk = svtgpu_wgclk_begin((int)grid.x);
     if (recon->bit_depth > 8)
         hipLaunchKernelGGL(cdef_search_kernel<uint16_t>, grid, dim3(NT), 0, st, A);
     else
         hipLaunchKernelGGL(cdef_search_kernel<uint8_t>, grid, dim3(NT), 0, st, A);
     HIP_TRY(hipGetLastError());
+    svtgpu_wgclk_end("cdef_search", (int)grid.x, st);
     return SVTGPU_OK;
 }

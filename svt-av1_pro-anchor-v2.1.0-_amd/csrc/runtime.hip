@@ -210,7 +210,7 @@ size_t              g_wgclk_cap = 0;
 unsigned long long *svtgpu_wgclk_begin(int nblocks) {
     static const char *path = std::getenv("SVTGPU_WGCLK");
     if (!path || nblocks <= 0) return nullptr;
-    const size_t bytes = 32 * (size_t)nblocks;
+    const size_t bytes = 64 * (size_t)nblocks;
     if (bytes > g_wgclk_cap) {
         if (g_wgclk) (void)hipFree(g_wgclk);
         g_wgclk = nullptr, g_wgclk_cap = 0;
@@ -223,9 +223,9 @@ unsigned long long *svtgpu_wgclk_begin(int nblocks) {
 void svtgpu_wgclk_end(const char *kernel, int nblocks, hipStream_t st) {
     static const char *path = std::getenv("SVTGPU_WGCLK");
     if (!path || !g_wgclk || nblocks <= 0) return;
-    std::vector<unsigned long long> h(4 * (size_t)nblocks);
+    std::vector<unsigned long long> h(8 * (size_t)nblocks);
     if (hipStreamSynchronize(st) != hipSuccess ||
-        hipMemcpy(h.data(), g_wgclk, 32 * (size_t)nblocks, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(h.data(), g_wgclk, 64 * (size_t)nblocks, hipMemcpyDeviceToHost) != hipSuccess)
         return;
     if (FILE *f = std::fopen(path, "ab")) {
         char name[64] = {0};

@@ -149,19 +149,17 @@ static inline hipStream_t pick_stream(SvtGpuContext *ctx, void *stream) {
     return stream ? (hipStream_t)stream : ctx->stream;
 }
 
-// Diagnostics (SVTGPU_WGCLK=<file>, never on by default): per-workgroup start / end on the 100 MHz s_memrealtime
-// clock plus the hardware id words (HW_ID: wave / SIMD / CU / SE, XCC_ID), 4 words per workgroup, appended to the
-// file by the launching host code (svtgpu_wgclk_*).  Written by lane 0 with vector stores.
-__device__ __forceinline__ void wgclk_mark(unsigned long long *buf, int end) {
+// Diagnostics (SVTGPU_WGCLK=<file>, never on by default): per workgroup 8 words -- up to 6 time marks on the 100 MHz
+// s_memrealtime clock (slot 0 = start; the kernel's phases after it; unused slots stay 0) and the hardware id words
+// (HW_ID: wave / SIMD / CU / SE; XCC_ID) -- appended to the file by the launching host code (svtgpu_wgclk_*).
+// Written by lane 0 with vector stores.
+__device__ __forceinline__ void wgclk_mark(unsigned long long *buf, int slot) {
     if (!buf || threadIdx.x) return;
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    unsigned long long      *q = buf + 4 * (size_t)blockIdx.x;
-    if (!end) {
-        q[0] = t;
-        q[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4); // HW_REG_HW_ID
-        q[3] = (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
-    } else {
-        q[1] = t;
+    unsigned long long *q = buf + 8 * (size_t)blockIdx.x;
+    q[slot]               = __builtin_amdgcn_s_memrealtime();
+    if (!slot) {
+        q[6] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4); // HW_REG_HW_ID
+        q[7] = (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20); // HW_REG_XCC_ID
     }
 }
 unsigned long long *svtgpu_wgclk_begin(int nblocks);               // null unless SVTGPU_WGCLK is set
