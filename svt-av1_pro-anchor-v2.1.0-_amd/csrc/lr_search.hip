@@ -1077,6 +1077,9 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
         if ((threadIdx.x & 63) == WAVE_LAST) s_part[threadIdx.x >> 6] = et;
         __syncthreads();
         if (threadIdx.x == 0) {
+            // the descent step is the unit's serial critical path: its wave issues ahead of the other workgroups'
+            // pixel waves on this SIMD while it runs
+            __builtin_amdgcn_s_setprio(3);
             unsigned long long err = 0;
             for (int k = 0; k < WR_NT / 64; k++) err += s_part[k];
             npx += (unsigned long long)w * h;
@@ -1113,6 +1116,7 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
                 D.taps(1, v), set_wiener_taps(s_taps + 8, v);
                 *s_mode = 1;
             }
+            __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();
     }
@@ -1640,7 +1644,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
     } else {
         // ================= control wave =================
         // stat (SVTGPU_SR_STATS diagnostics, else null): items, passes, candidate-pixels, load / descent / control
-        // ticks (100 MHz), pixels
+        // ticks (100 MHz), pixels.  The control steps are the item's serial critical path: this wave issues ahead of
+        // the other workgroup's pixel waves on its SIMD (it waits at the barriers otherwise)
+        __builtin_amdgcn_s_setprio(3);
         const int                lane = threadIdx.x & 63;
         const unsigned long long t0   = stat ? __builtin_amdgcn_s_memrealtime() : 0;
         unsigned long long       tctl = 0, ncp = 0;
