@@ -29,6 +29,7 @@ def main(path, only=None, show=6):
     for name, rows in per.items():
         print("%s: %d launches (us; p10/p50/p90)" % (name, len(rows)))
         for a in rows[:show] + (rows[-2:] if len(rows) > show else []):
+            a = a[a[:, 0] > 0]  # workgroups that recorded a start
             t0 = a[:, 0].min()
             last = np.where(a[:, 1:6] > 0, a[:, 1:6], 0).max(axis=1)  # the workgroup's last mark
             done = last > 0

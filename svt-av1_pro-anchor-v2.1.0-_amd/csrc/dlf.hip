@@ -223,6 +223,7 @@ struct DlfTileArgs {
     unsigned int       *arrive;
     unsigned long long *out; // [MAX_JOBS][MAX_TRIALS] sums, then the sequence word (svtgpu_wait_seq)
     unsigned long long  seq;
+    unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
 };
 
 template <typename T, bool TRIAL>
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
     const int tid = threadIdx.x;
+    wgclk_mark(a.wgclk, 0);
     // one (plane job, tile, trial) per workgroup: the trials of a tile are neighbours after the XCD swizzle, so
     // the second staging of a tile hits the L2; one working image in LDS (18 KB) keeps 8 waves per SIMD
     const int b = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -296,6 +298,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     const int tw = min(TILE, J.ox + J.ow - x0), th = min(TILE, J.oy + J.oh - y0);
     {
         __syncthreads();
+        wgclk_mark(a.wgclk, 1);
         // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
         for (int i = tid; i < ((DLF_EXP & 1) ? 0 : RV_R * RV_C * 4); i += NTHR) {
             const int line = i & 3, e = (i >> 2) % RV_C, sr = (i >> 2) / RV_C;
@@ -316,6 +319,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
                 if (k >= 7 - h && k < 7 + h) row[k - 7] = (uint16_t)F[k];
         }
         __syncthreads();
+        wgclk_mark(a.wgclk, 2);
         // horizontal edges y0-4 .. y0+64 over the tile's 64 columns
         for (int i = tid; i < ((DLF_EXP & 2) ? 0 : RH_R * RH_C * 4); i += NTHR) {
             const int col = i % TILE, e = i / TILE;
@@ -336,6 +340,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
                 if (k >= 7 - h && k < 7 + h) c[(k - 7) * LW] = (uint16_t)F[k];
         }
         __syncthreads();
+        wgclk_mark(a.wgclk, 3);
         // emit the tile
         if (TRIAL) {
             uint32_t  s = 0; // <= 16 samples per lane
@@ -378,6 +383,7 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             }
         }
     }
+    wgclk_mark(a.wgclk, 5);
     // trial: the last workgroup to finish reads the sums (8-B agent atomics on both sides; this lane's SSE adds have
     // completed before its arrival is counted) and re-arms the accumulators for the next launch
     if (TRIAL && tid == 0) {
@@ -529,9 +535,11 @@ DlfTileArgs base_args(const SvtGpuFrame *f, const LevelTables &L) {
     return a;
 }
 
-int launch_tile(const DlfTileArgs &a, int bps, bool trial, hipStream_t st) {
+int launch_tile(const DlfTileArgs &a0, int bps, bool trial, hipStream_t st) {
     int tiles = 0; // workgroups: one per tile (apply) or per (tile, trial)
-    for (int j = 0; j < a.njob; j++) tiles += a.job[j].tiles * (trial ? a.job[j].ntrial : 1);
+    for (int j = 0; j < a0.njob; j++) tiles += a0.job[j].tiles * (trial ? a0.job[j].ntrial : 1);
+    DlfTileArgs a = a0;
+    a.wgclk       = svtgpu_wgclk_begin(tiles);
     if (bps == 2) {
         if (trial) hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, true>), dim3(tiles), dim3(NTHR), 0, st, a);
         else       hipLaunchKernelGGL((dlf_tile_kernel<uint16_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);
@@ -540,6 +548,7 @@ int launch_tile(const DlfTileArgs &a, int bps, bool trial, hipStream_t st) {
         else       hipLaunchKernelGGL((dlf_tile_kernel<uint8_t, false>), dim3(tiles), dim3(NTHR), 0, st, a);
     }
     HIP_TRY(hipGetLastError());
+    svtgpu_wgclk_end(trial ? "dlf_trial" : "dlf_apply", tiles, st);
     return SVTGPU_OK;
 }
 

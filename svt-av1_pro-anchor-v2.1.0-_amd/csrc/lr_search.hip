@@ -410,6 +410,13 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
     if (threadIdx.x < 256) xby[threadIdx.x] = c_x_by_xplus1[threadIdx.x];
     __syncthreads();
     const uint16_t *v0 = v + 3 * SG_V + 3;
+    // The box sums read a row's 3 / 5 samples as aligned dword pairs and a funnel shift (sr_lds_pair) plus one 16-bit
+    // read: adjacent 16-bit reads merged by the compiler into one dword / quad read would be misaligned for half the
+    // lanes, which the LDS serves far below its rate.  Index a of v (4-B aligned: the int array ab1[1]).
+    auto lds_pair = [&](int a) {
+        const uint32_t *w = (const uint32_t *)v + (a >> 1);
+        return __builtin_amdgcn_alignbit(w[1], w[0], (a & 1) * 16);
+    };
     const int       bw = t.w + 2, nq = (t.h + 2) * bw, nq2 = (t.h + 3) / 2 * bw;
     // the r = 1 map at every position q (map row q / bw = pixel row - 1 .. t.h); the r = 2 map only on the odd pixel
     // rows (-1, 1, ..): dense position i -> map row 2 (i / bw), so no lane idles on the even rows
@@ -421,12 +428,13 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
         if (q < nq) {
             const int y = q / bw - 1, x = q % bw - 1;
 #pragma unroll
-            for (int dy = -1; dy <= 1; dy++)
+            for (int dy = -1; dy <= 1; dy++) {
+                const int      a  = (y + dy + 3) * SG_V + x + 3; // sample (y + dy, x) of the tile image
+                const uint32_t pr = lds_pair(a - 1);
+                const int      p[3] = {(int)(pr & 0xFFFF), (int)(pr >> 16), (int)v[a + 1]};
 #pragma unroll
-                for (int dx = -1; dx <= 1; dx++) {
-                    const int p = v0[(y + dy) * SG_V + x + dx];
-                    s1[k] += p, q1[k] += p * p;
-                }
+                for (int j = 0; j < 3; j++) s1[k] += p[j], q1[k] += p[j] * p[j];
+            }
         }
     }
 #pragma unroll
@@ -436,12 +444,13 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
         m2q[k] = i < nq2 ? (y + 1) * bw + x + 1 : -1; // the map index the filters read
         if (i < nq2) {
 #pragma unroll
-            for (int dy = -2; dy <= 2; dy++)
+            for (int dy = -2; dy <= 2; dy++) {
+                const int      a  = (y + dy + 3) * SG_V + x + 3;
+                const uint32_t pa = lds_pair(a - 2), pb = lds_pair(a);
+                const int      p[5] = {(int)(pa & 0xFFFF), (int)(pa >> 16), (int)(pb & 0xFFFF), (int)(pb >> 16), (int)v[a + 2]};
 #pragma unroll
-                for (int dx = -2; dx <= 2; dx++) {
-                    const int p = v0[(y + dy) * SG_V + x + dx];
-                    s2[k] += p, q2[k] += p * p;
-                }
+                for (int j = 0; j < 5; j++) s2[k] += p[j], q2[k] += p[j] * p[j];
+            }
         }
     }
     // this lane's pixels: a column of 4 rows (fy0 .. fy0 + 3, fy0 even) at column fx, so the 3-wide map rows a filter
