@@ -84,21 +84,38 @@ struct FastDiv {
     __device__ int operator()(int i) const { return (int)(((uint64_t)(uint32_t)i * m) >> 32); }
 };
 
+typedef short v2i16lr __attribute__((ext_vector_type(2)));
+
 template <typename T>
 __device__ void wiener_tile(const uint16_t *v, int vs, uint16_t *t, int ts, int w, int h, const int16_t *fx,
                             const int16_t *fy, int bd, T *out, size_t os) {
     const WienerRound rr  = wiener_round(bd);
     const int         lim = (1 << (bd + 1 + 7 - rr.r0)) - 1;
     const FastDiv     dw(w);
-    int16_t           hx[8], vy[8];
+    int16_t           vy[8];
+    // horizontal taps as int16 pairs for v_dot2, the add-source term folded into the centre tap (|tap3 + 128| fits)
+    uint32_t          hp[4];
 #pragma unroll
-    for (int k = 0; k < 8; k++) hx[k] = fx[k], vy[k] = fy[k];
+    for (int k = 0; k < 4; k++)
+        hp[k] = (uint32_t)(uint16_t)(fx[2 * k] + (2 * k == 3 ? 128 : 0)) |
+                ((uint32_t)(uint16_t)(fx[2 * k + 1] + (2 * k + 1 == 3 ? 128 : 0)) << 16);
+#pragma unroll
+    for (int k = 0; k < 8; k++) vy[k] = fy[k];
+    // the 8 samples x-3 .. x+4 of a row from 5 aligned dwords and funnel shifts (`v` is 4-byte aligned): adjacent
+    // 16-bit reads merged by the compiler would be misaligned for half the lanes, far below the LDS rate
+    const uint32_t *vw = (const uint32_t *)v;
     for (int i = threadIdx.x; i < (h + 7) * w; i += NTHR) {
         const int       q = dw(i), y = q - 3, x = i - q * w;
-        const uint16_t *s = v + y * vs + x - 3;
-        int             sum = ((int)s[3] << 7) + (1 << (bd + 6));
+        const int       a = y * vs + x - 3, sh = (a & 1) * 16;
+        const uint32_t *wp = vw + (a >> 1);
+        uint32_t        wd[5];
 #pragma unroll
-        for (int k = 0; k < 8; k++) sum += (int)s[k] * hx[k];
+        for (int k = 0; k < 5; k++) wd[k] = wp[k];
+        int sum = 1 << (bd + 6);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            sum = __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16lr, __builtin_amdgcn_alignbit(wd[k + 1], wd[k], sh)),
+                                         __builtin_bit_cast(v2i16lr, hp[k]), sum, false);
         t[(y + 3) * ts + x] = (uint16_t)min(max((sum + (1 << (rr.r0 - 1))) >> rr.r0, 0), lim);
     }
     __syncthreads();
