@@ -45,8 +45,8 @@ struct SearchArgs {
 
 struct PriPair { // two horizontally adjacent samples, packed int16 (lo half = left sample)
     s16x2 x, lo, hi;
-    s16x2 ad[4]; // |p - x| of the primary taps: (k0,+), (k0,-), (k1,+), (k1,-)
-    s16x2 sg[4]; // sign(p - x) as +-1
+    s16x2 d[4]; // p - x of the primary taps: (k0,+), (k0,-), (k1,+), (k1,-) (the magnitude is formed per use: fewer
+                // live registers, so the kernel holds three waves per SIMD)
 };
 
 // 8 samples from an 8-aligned position of a plane as four packed int16 pairs (one 16-B / 8-B load)
@@ -123,11 +123,12 @@ __device__ __forceinline__ void stage_tile(uint16_t *tile, const void *plane_, i
 __device__ __forceinline__ s16x2 splat16(int v) { return (s16x2){(short)v, (short)v}; }
 __device__ __forceinline__ u16x2 splatu16(int v) { return (u16x2){(unsigned short)v, (unsigned short)v}; }
 
-// sign(d) * min(|d|, max(0, thr - (|d| >> shift))) == constrain(d, thr, damping) (EbCdef.c:85-91)
-__device__ __forceinline__ s16x2 constrain2(s16x2 ad, s16x2 sg, s16x2 thr, u16x2 sh) {
-    const s16x2 a = (s16x2)(((u16x2)ad) >> sh);
-    const s16x2 c = __builtin_elementwise_max(thr - a, (s16x2){0, 0});
-    return __builtin_elementwise_min(ad, c) * sg;
+// constrain(d, thr, damping) = sign(d) * min(|d|, m), m = max(0, thr - (|d| >> shift)) (EbCdef.c:85-91): m >= 0, so it
+// is the clamp of d to [-m, m]
+__device__ __forceinline__ s16x2 constrain2(s16x2 d, s16x2 thr, u16x2 sh) {
+    const s16x2 ad = __builtin_elementwise_max(d, (s16x2){0, 0} - d);
+    const s16x2 m  = __builtin_elementwise_max(thr - (s16x2)(((u16x2)ad) >> sh), (s16x2){0, 0});
+    return __builtin_elementwise_max(__builtin_elementwise_min(d, m), (s16x2){0, 0} - m);
 }
 
 // Neighbourhood of the pair at tile (r, c), (r, c+1) for direction `dir`: keeps the primary taps
@@ -146,7 +147,7 @@ __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t
     const int       xa = (int16_t)(xw & 0xFFFF), xb = (int16_t)(xw >> 16);
     int             loa = xa, hia = xa, lob = xb, hib = xb;
     const int       ds0 = (dir + 2) & 7, ds1 = (dir + 6) & 7;
-    s16x2           sad[8], ssg[8];
+    s16x2           sd[8];
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const int op = cdef_dir_dy(dir, k) * ts + cdef_dir_dx(dir, k);
@@ -161,16 +162,11 @@ __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t
             if (vb != CDEF_VERY_LARGE_V) hib = max(hib, vb);
             loa = min(loa, va);
             lob = min(lob, vb);
-            const int   da = va - xa, db = vb - xb;
-            const s16x2 ad = {(short)abs(da), (short)abs(db)};
-            const s16x2 sg = {(short)(da < 0 ? -1 : 1), (short)(db < 0 ? -1 : 1)};
-            if (t < 2) {
-                P.ad[2 * k + t] = ad;
-                P.sg[2 * k + t] = sg;
-            } else {
-                sad[4 * k + t - 2] = ad;
-                ssg[4 * k + t - 2] = sg;
-            }
+            const s16x2 dd = {(short)(va - xa), (short)(vb - xb)};
+            if (t < 2)
+                P.d[2 * k + t] = dd;
+            else
+                sd[4 * k + t - 2] = dd;
         }
     }
     P.x  = (s16x2){(short)xa, (short)xb};
@@ -187,8 +183,8 @@ __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t
         s16x2       a0 = {0, 0}, a1 = {0, 0};
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            a0 = a0 + constrain2(sad[t], ssg[t], thr, sh);         // k = 0, tap weight 2
-            a1 = a1 + constrain2(sad[4 + t], ssg[4 + t], thr, sh); // k = 1, tap weight 1
+            a0 = a0 + constrain2(sd[t], thr, sh);     // k = 0, tap weight 2
+            a1 = a1 + constrain2(sd[4 + t], thr, sh); // k = 1, tap weight 1
         }
         S[sc] = (a0 << (s16x2){1, 1}) + a1;
     }
@@ -196,8 +192,8 @@ __device__ __forceinline__ void load_pair(PriPair &P, s16x2 S[4], const uint16_t
 
 // primary sum for threshold `thr` (already strength-adjusted), weights {4,2} or {3,3}
 __device__ __forceinline__ s16x2 pri_sum(const PriPair &P, s16x2 thr, u16x2 sh, s16x2 w0, s16x2 w1) {
-    const s16x2 k0 = constrain2(P.ad[0], P.sg[0], thr, sh) + constrain2(P.ad[1], P.sg[1], thr, sh);
-    const s16x2 k1 = constrain2(P.ad[2], P.sg[2], thr, sh) + constrain2(P.ad[3], P.sg[3], thr, sh);
+    const s16x2 k0 = constrain2(P.d[0], thr, sh) + constrain2(P.d[1], thr, sh);
+    const s16x2 k1 = constrain2(P.d[2], thr, sh) + constrain2(P.d[3], thr, sh);
     return k0 * w0 + k1 * w1;
 }
 
@@ -216,7 +212,7 @@ __device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(NT) cdef_search_kernel(const SearchArgs A) {
+__global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) {
     __shared__ __attribute__((aligned(16))) uint16_t ltile[LT * LT];
     __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CT * CT];
     __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
