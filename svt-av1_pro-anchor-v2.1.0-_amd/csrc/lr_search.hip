@@ -1469,6 +1469,34 @@ __device__ __forceinline__ void sr_tree_lanes(const Descent &d, bool live, int n
     if (n == 0) *s_mask = (uint32_t)mask, *s_nv = (int)__popcll(mask);
 }
 
+// control wave, one-candidate passes: the two candidates that can follow d's pending one -- lane 1 after a worse
+// outcome, lane 2 after a not-worse one (the seed's outcome does not steer: no worse child) -- built while the pixel
+// waves evaluate the pending candidate, so that after its error only the choice between them is left before the next
+// pass.  (ok*, x*) wave-uniform; !ok: the descent ends on that outcome.
+__device__ __forceinline__ void sr_children(const Descent &d, uint32_t &xw, bool &okw, uint32_t &xb, bool &okb) {
+    const int n  = threadIdx.x & 63;
+    bool      ok = n == 1 || n == 2;
+    uint32_t  xv = 0;
+    if (ok) {
+        const bool worse = n == 1;
+        Descent    c     = d;
+        if (worse && c.init) {
+            ok = false;
+        } else {
+            c.report_outcome(worse, 0);
+            ok = c.next();
+        }
+        if (ok) {
+            int32_t x[2];
+            decode_xq(c, x);
+            xv = pack2(x[0], x[1]);
+        }
+    }
+    const unsigned long long m = __ballot(ok);
+    okw = (m >> 1) & 1, okb = (m >> 2) & 1;
+    xw  = (uint32_t)__builtin_amdgcn_readlane((int)xv, 1), xb = (uint32_t)__builtin_amdgcn_readlane((int)xv, 2);
+}
+
 // wave-uniform copies (scalar registers) of a 64-bit lane value and of a struct
 __device__ __forceinline__ long long readlane64(long long v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l),
@@ -1682,6 +1710,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
             const int nv = __builtin_amdgcn_readfirstlane(s_nv);
             if (nv == 0) break;
             const uint32_t mask = __builtin_amdgcn_readfirstlane(s_mask);
+            uint32_t       xw = 0, xb = 0;
+            bool           okw = false, okb = false;
+            if (nodes == 1) sr_children(D, xw, okw, xb, okb); // during the pass
             __syncthreads(); // B3
             const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
             ncp += (unsigned long long)nv * nch * 4;
@@ -1697,6 +1728,23 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
             if (pass > SR_MAX_PASSES) {
                 if (lane == 0) atomicOr(status, 1);
                 ok = false;
+            }
+            if (nodes == 1) { // the outcome picks a prepared child; the descent itself steps after the barrier
+                const long long e0    = readlane64(e, 0);
+                const bool      worse = !D.init && e0 > D.err;
+                if (lane == 0) {
+                    s_xq[0] = worse ? xw : xb;
+                    s_mask  = 1;
+                    s_nv    = ok && (worse ? okw : okb) ? 1 : 0;
+                }
+                if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
+                __syncthreads(); // B4
+                if (stat && lane == 0 && s_nv == 0) atomicAdd(stat + 1, (unsigned long long)pass);
+                if (ok) { // the same state change as the choice above, with the error value kept
+                    D.report(e0);
+                    D.next();
+                }
+                continue;
             }
             if (ok) { // the same steps in every lane (the errors made uniform: scalar code)
                 long long ev[SG_NC];
