@@ -232,6 +232,11 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
     __shared__ unsigned long long red[NTHR / 64];
+    // this workgroup's level table (per direction and level class) and the per-level thresholds (mblim | lim << 8 |
+    // hev << 16), looked up per edge with lane-varying indices: from LDS, not from the kernel arguments (a
+    // lane-varying index into the argument block is a memory load per lookup)
+    __shared__ uint8_t  s_lvl[2][128];
+    __shared__ uint32_t s_thr[64];
     const int tid = threadIdx.x;
     wgclk_mark(a.wgclk, 0);
     // one (plane job, tile, trial) per workgroup: the trials of a tile are neighbours after the XCD swizzle, so
@@ -246,6 +251,8 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     const int x0 = J.ox + (tb % J.tiles_x) * TILE, y0 = J.oy + (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
+    s_lvl[tid >> 7][tid & 127] = J.lvl[tr][tid >> 7][tid & 127]; // NTHR == 256 entries
+    if (tid < 64) s_thr[tid] = (uint32_t)a.mblim[tid] | ((uint32_t)a.lim[tid] << 8) | ((uint32_t)a.hev[tid] << 16);
 
     // edge records reaching the tile (no records outside the plane: length 0) and the tile + apron (samples outside
     // the plane are never read by an active edge), 4 samples per item (gx is a multiple of 4: aligned 8-B / 4-B
@@ -305,15 +312,15 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             const uint32_t r = rv[sr * RV_C + e];
             const int len = r & 15;
             if (!len) continue;
-            const int cur = J.lvl[tr][0][(r >> 8) & 127], prv = J.lvl[tr][0][(r >> 16) & 127];
+            const int cur = s_lvl[0][(r >> 8) & 127], prv = s_lvl[0][(r >> 16) & 127];
             if (!cur && !prv) continue;
-            const int lvl = cur ? cur : prv;
+            const uint32_t th = s_thr[cur ? cur : prv];
             uint16_t *row = &t[(sr * 4 + line) * LW + (APRON - 4 + e * 4)];
             const int h = half_taps(len);
             int F[14];
 #pragma unroll
             for (int k = 0; k < 14; k++) F[k] = (k >= 7 - h && k < 7 + h) ? row[k - 7] : 0;
-            filter_line(F, len, a.mblim[lvl], a.lim[lvl], a.hev[lvl], a.bd);
+            filter_line(F, len, th & 0xFF, (th >> 8) & 0xFF, th >> 16, a.bd);
 #pragma unroll
             for (int k = 0; k < 14; k++)
                 if (k >= 7 - h && k < 7 + h) row[k - 7] = (uint16_t)F[k];
@@ -326,15 +333,15 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
             const uint32_t r = rh[e * RH_C + col / 4];
             const int len = r & 15;
             if (!len) continue;
-            const int cur = J.lvl[tr][1][(r >> 8) & 127], prv = J.lvl[tr][1][(r >> 16) & 127];
+            const int cur = s_lvl[1][(r >> 8) & 127], prv = s_lvl[1][(r >> 16) & 127];
             if (!cur && !prv) continue;
-            const int lvl = cur ? cur : prv;
+            const uint32_t th = s_thr[cur ? cur : prv];
             uint16_t *c = &t[(APRON - 4 + e * 4) * LW + APRON + col];
             const int h = half_taps(len);
             int F[14];
 #pragma unroll
             for (int k = 0; k < 14; k++) F[k] = (k >= 7 - h && k < 7 + h) ? c[(k - 7) * LW] : 0;
-            filter_line(F, len, a.mblim[lvl], a.lim[lvl], a.hev[lvl], a.bd);
+            filter_line(F, len, th & 0xFF, (th >> 8) & 0xFF, th >> 16, a.bd);
 #pragma unroll
             for (int k = 0; k < 14; k++)
                 if (k >= 7 - h && k < 7 + h) c[(k - 7) * LW] = (uint16_t)F[k];

@@ -1402,6 +1402,7 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
 #define SVTGPU_SR_KMAX 19 // resident 4-pixel chunks per pixel lane: parts of <= 34048 pixels (256 x 133 luma)
 #endif
 constexpr int SR_NT = SVTGPU_SR_NT, SR_PW = SR_NT / 64 - 1, SR_PL = SR_PW * 64, SR_KMAX = SVTGPU_SR_KMAX;
+constexpr int SR_LB = 4; // chunks whose loads are in flight together in the load phase
 constexpr int SR_MAX_PX = SR_PL * SR_KMAX * 4;
 constexpr int SR_MAX_PASSES = 4096, SR_MAX_PARTS = 8;
 constexpr int SR_LDS = SR_KMAX * SR_PL * 8; // the (x - src) pairs of the part
@@ -1597,17 +1598,17 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         uint32_t           g[SR_KMAX][4];
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
 #pragma unroll
-        for (int kb = 0; kb < SR_KMAX; kb += 3) {
+        for (int kb = 0; kb < SR_KMAX; kb += SR_LB) {
 #pragma unroll
-            for (int j = 0; j < 3; j++)
+            for (int j = 0; j < SR_LB; j++)
 #pragma unroll
                 for (int q = 0; q < 4; q++)
                     if (kb + j < SR_KMAX) g[kb + j][q] = 0u;
             if (kb >= K) continue; // uniform
-            int2 dv2[3], sv2[3], a0[3], a1[3];
-            bool on[3];
+            int2 dv2[SR_LB], sv2[SR_LB], a0[SR_LB], a1[SR_LB];
+            bool on[SR_LB];
 #pragma unroll
-            for (int j = 0; j < 3; j++) { // all loads of 3 chunks in flight together (addresses clamped into the part)
+            for (int j = 0; j < SR_LB; j++) { // all loads of SR_LB chunks in flight together (addresses clamped into the part)
                 const int c = kb + j < SR_KMAX ? pl + (kb + j) * SR_PL : nch, cc = min(c, nch - 1), row = cc / cw,
                           col = cc - row * cw;
                 const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
@@ -1624,7 +1625,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 a1[j] = *(const int2 *)(f1 + fo);
             }
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
+            for (int j = 0; j < SR_LB; j++) {
                 const int kk = kb + j;
                 if (kk >= SR_KMAX) break;
                 int       dv[4], sv[4];

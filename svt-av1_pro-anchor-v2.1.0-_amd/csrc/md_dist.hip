@@ -72,6 +72,18 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
         s_src[i] = src[(size_t)y * a.src_stride + x];
     }
     const int cy = tid >> 4, cx = tid & 15;
+    // the shape (pixel count) of each output block this lane writes, looked up once (the shape table is indexed per
+    // lane: every lookup is a memory load, so not once per reference)
+    constexpr int KO = (kBlocks + 255) / 256;
+    int           npx[KO];
+#pragma unroll
+    for (int j = 0; j < KO; j++) {
+        const int k = tid + 256 * j;
+        int       sh = 0;
+        if (k < kBlocks)
+            while (k >= c_off[sh + 1]) sh++;
+        npx[j] = c_w[sh] * c_h[sh];
+    }
     for (int r = 0; r < a.nref; r++) {
         const int mx = a.mv[((size_t)sb * a.nref + r) * 2], my = a.mv[((size_t)sb * a.nref + r) * 2 + 1];
         const T  *ref = (const T *)a.ref[r];
@@ -118,10 +130,11 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
         }
         __syncthreads();
         uint32_t *out = a.out + ((size_t)sb * a.nref + r) * 3 * kBlocks;
-        for (int k = tid; k < kBlocks; k += 256) {
-            int s = 0;
-            while (k >= c_off[s + 1]) s++;
-            const int n = c_w[s] * c_h[s];
+#pragma unroll
+        for (int j = 0; j < KO; j++) {
+            const int k = tid + 256 * j;
+            if (k >= kBlocks) break;
+            const int n = npx[j];
             uint32_t  e, v;
             if (a.highbd) { // highbd_10_variance: sse rounded >> 4, sum rounded >> 2, clamped at 0
                 e                = (s_sse[k] + 8u) >> 4;
