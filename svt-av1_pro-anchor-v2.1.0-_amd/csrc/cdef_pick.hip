@@ -32,6 +32,7 @@ struct StepArgs {
     const int32_t  *count;  // sb_count, the number of non-skipped FBs (device)
     const int32_t  *wide;   // nonzero when some wmse entry is >= 2^31 (the 32-bit path would not be exact)
     int32_t         chunk, start_gi, end_gi, step, na; // na: chains in this launch
+    int32_t         fb_alloc;                           // FB rows the wmse table holds
     uint64_t       *tot;    // [3][4][4096] rotating tot_mse accumulators
     int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
     int32_t        *fin;    // [4][32] final list per chain
@@ -78,14 +79,16 @@ __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *
 }
 
 // First minimum of tot over [start, end)^2 (svt_search_one_dual's final loop, EbEncCdef.c:670-679),
-// computed by every workgroup that needs it.  Returns (best, e = j*64 + k) through LDS.
-__device__ __forceinline__ void tot_argmin(const uint64_t *tot, int start, int end, uint64_t *bv, int32_t *bi) {
+// computed by every workgroup that needs it from the lane's 16 entries tv[u] = tot[u * NT + t] (loaded by the caller
+// at the top of the step).  Returns (best, e = j*64 + k) through LDS.
+__device__ __forceinline__ void tot_argmin(const uint64_t (&tv)[4096 / NT], int start, int end, uint64_t *bv, int32_t *bi) {
     const int t    = threadIdx.x;
     uint64_t  best = (uint64_t)1 << 63; // best_tot_mse initial value (EbEncCdef.c:632)
     int       idx  = 1 << 30;
+#pragma unroll
     for (int u = 0; u < 4096 / NT; u++) { // ascending e per lane keeps the first minimum
         const int      e = u * NT + t, j = e >> 6, k = e & 63;
-        const uint64_t v = tot[e];
+        const uint64_t v = tv[u];
         if (j >= start && j < end && k >= start && k < end && v < best) {
             best = v;
             idx  = e;
@@ -126,25 +129,31 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int t = threadIdx.x, c = C.chain;
     const int lead = tx == 0 && ty == 0;
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
-    const int f0 = ty * A.chunk, nfb = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
+    const int f0 = ty * A.chunk;
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
-    const int wide = *A.wide;
-    // 0. issue the loads of this workgroup's FB chunk (independent of the previous call's result); they stay in
-    // flight through the previous call's argmin and land in LDS after it (<= PICK_CHUNK * 64 / NT each)
+    // 0. every global load of the step issued before anything waits on one: the previous call's totals, this
+    // workgroup's FB chunk (clamped into the allocated table, not the live count, so no load waits for the count)
+    // and the live count and width flag.  The chunk stays in named registers (not an array: VGPRs, not scratch)
+    // through the argmin and lands in LDS after it (<= PICK_CHUNK * 64 / NT each)
+    uint64_t tv[4096 / NT];
+    {
+        const uint64_t *tot = A.tot + ((size_t)((A.step + 2) % 3) * MAX_CHAINS + c) * 4096;
+#pragma unroll
+        for (int u = 0; u < 4096 / NT; u++) tv[u] = C.prev_nb_sel >= 0 ? tot[u * NT + t] : 0;
+    }
     static_assert(PICK_CHUNK * 64 / NT == 12, "twelve staging registers per lane");
-    // unconditional loads, the index clamped into the chunk (a chunk past the live FBs reads its first entry:
-    // f0 < the FB count the buffer holds, so the address is inside it); named registers, not an array, so they
-    // stay in VGPRs across the argmin
     const uint4 *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
-    const int    lim = max(nfb, 1) * 64 - 1;
+    const int    lim = min(A.chunk, A.fb_alloc - f0) * 64 - 1; // f0 < fb_alloc: the grid covers the table
 #define LD(u) const uint4 v##u = src[min(t + (u) * NT, lim)];
     LD(0) LD(1) LD(2) LD(3) LD(4) LD(5) LD(6) LD(7) LD(8) LD(9) LD(10) LD(11)
 #undef LD
+    const int nfb  = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
+    const int wide = *A.wide;
     wgclk_mark(A.wgclk, 1);
     // 1. selection entering this call
     if (t < 32) sl[t] = A.step ? A.lev[((size_t)(A.step - 1) * MAX_CHAINS + c) * 32 + t] : 0;
     if (C.prev_nb_sel >= 0) {
-        tot_argmin(A.tot + ((size_t)((A.step + 2) % 3) * MAX_CHAINS + c) * 4096, A.start_gi, A.end_gi, bv, bi);
+        tot_argmin(tv, A.start_gi, A.end_gi, bv, bi);
         if (t == 0) {
             const bool any = bi[0] < (1 << 30); // no candidate: (1 << 63, 0, 0) like the reference
             sl[C.prev_nb_sel]      = any ? bi[0] >> 6 : 0;
@@ -313,6 +322,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
 
     StepArgs A;
     A.wmse     = wmse;
+    A.fb_alloc = nfb;
     A.count    = d_count;
     A.start_gi = 0;
     A.end_gi   = end;
