@@ -226,8 +226,56 @@ struct DlfTileArgs {
     unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
 };
 
+// The edges of one direction that filter anything (a length and a nonzero level on either side), listed in LDS
+// grouped by filter length (4, 6, 8, 14): a wave then runs lines of one length, where interleaved lengths made every
+// lane pay for every filter variant of its wave.  Order within a group is free (edges of one direction never overlap).
+// Returns the count; list[] holds record indices.  Ends with a barrier.
+__device__ __forceinline__ int list_edges(const uint32_t *rec, int n, const uint8_t *lvl, uint16_t *list, int *s_cnt) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    auto bucket = [&](int ri) {
+        const uint32_t r   = rec[ri];
+        const int      len = r & 15;
+        if (!len || (!lvl[(r >> 8) & 127] && !lvl[(r >> 16) & 127])) return -1;
+        return len == 4 ? 0 : len == 6 ? 1 : len == 8 ? 2 : 3;
+    };
+    if (tid < 8) s_cnt[tid] = 0; // [0, 4): counts, then cursors; [4, 8): group starts
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += NTHR) {
+        const int b = i0 + tid < n ? bucket(i0 + tid) : -1;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const unsigned long long m = __ballot(b == g);
+            if (m && lane == __ffsll((long long)m) - 1) atomicAdd(&s_cnt[g], (int)__popcll(m));
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int o = 0;
+        for (int g = 0; g < 4; g++) {
+            const int c = s_cnt[g];
+            s_cnt[4 + g] = o, s_cnt[g] = o, o += c;
+        }
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += NTHR) {
+        const int b = i0 + tid < n ? bucket(i0 + tid) : -1;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const unsigned long long m = __ballot(b == g);
+            if (!m) continue;
+            const int leader = __ffsll((long long)m) - 1;
+            int       base   = 0;
+            if (lane == leader) base = atomicAdd(&s_cnt[g], (int)__popcll(m));
+            base = __shfl(base, leader);
+            if (b == g) list[base + __popcll(m & ((1ull << lane) - 1))] = (uint16_t)(i0 + tid);
+        }
+    }
+    __syncthreads();
+    return s_cnt[3]; // the last group's cursor ends at the total
+}
+
 template <typename T, bool TRIAL>
-__global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
+__global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a) {
     __shared__ __align__(16) uint16_t t[LW * LW];
     __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
     __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
@@ -237,6 +285,8 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     // lane-varying index into the argument block is a memory load per lookup)
     __shared__ uint8_t  s_lvl[2][128];
     __shared__ uint32_t s_thr[64];
+    __shared__ uint16_t s_list[(LW / 4) * (TILE / 4 + 3)]; // list_edges (>= the horizontal count, 19 x 16)
+    __shared__ int      s_cnt[8];
     const int tid = threadIdx.x;
     wgclk_mark(a.wgclk, 0);
     // one (plane job, tile, trial) per workgroup: the trials of a tile are neighbours after the XCD swizzle, so
@@ -306,14 +356,13 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
     {
         __syncthreads();
         wgclk_mark(a.wgclk, 1);
-        // vertical edges x0-4 .. x0+64 over all 88 rows: (segment row, edge, line) per item
-        for (int i = tid; i < ((DLF_EXP & 1) ? 0 : RV_R * RV_C * 4); i += NTHR) {
-            const int line = i & 3, e = (i >> 2) % RV_C, sr = (i >> 2) / RV_C;
-            const uint32_t r = rv[sr * RV_C + e];
+        // vertical edges x0-4 .. x0+64 over all 88 rows: (listed edge, line) per item
+        const int nve = list_edges(rv, NV, s_lvl[0], s_list, s_cnt);
+        for (int i = tid; i < ((DLF_EXP & 1) ? 0 : nve * 4); i += NTHR) {
+            const int ri = s_list[i >> 2], line = i & 3, e = ri % RV_C, sr = ri / RV_C;
+            const uint32_t r = rv[ri];
             const int len = r & 15;
-            if (!len) continue;
             const int cur = s_lvl[0][(r >> 8) & 127], prv = s_lvl[0][(r >> 16) & 127];
-            if (!cur && !prv) continue;
             const uint32_t th = s_thr[cur ? cur : prv];
             uint16_t *row = &t[(sr * 4 + line) * LW + (APRON - 4 + e * 4)];
             const int h = half_taps(len);
@@ -327,14 +376,13 @@ __global__ __launch_bounds__(NTHR) void dlf_tile_kernel(const DlfTileArgs a) {
         }
         __syncthreads();
         wgclk_mark(a.wgclk, 2);
-        // horizontal edges y0-4 .. y0+64 over the tile's 64 columns
-        for (int i = tid; i < ((DLF_EXP & 2) ? 0 : RH_R * RH_C * 4); i += NTHR) {
-            const int col = i % TILE, e = i / TILE;
-            const uint32_t r = rh[e * RH_C + col / 4];
+        // horizontal edges y0-4 .. y0+64 over the tile's 64 columns: (listed 4-column edge segment, column) per item
+        const int nhe = list_edges(rh, NH, s_lvl[1], s_list, s_cnt);
+        for (int i = tid; i < ((DLF_EXP & 2) ? 0 : nhe * 4); i += NTHR) {
+            const int ri = s_list[i >> 2], e = ri / RH_C, col = 4 * (ri % RH_C) + (i & 3);
+            const uint32_t r = rh[ri];
             const int len = r & 15;
-            if (!len) continue;
             const int cur = s_lvl[1][(r >> 8) & 127], prv = s_lvl[1][(r >> 16) & 127];
-            if (!cur && !prv) continue;
             const uint32_t th = s_thr[cur ? cur : prv];
             uint16_t *c = &t[(APRON - 4 + e * 4) * LW + APRON + col];
             const int h = half_taps(len);
