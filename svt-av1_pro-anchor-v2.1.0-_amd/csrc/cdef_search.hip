@@ -22,8 +22,8 @@
 #include "cdef_common.h"
 
 #define NT 256
-#define LT 68 // luma tile: rows/cols -2..65
-#define CT 36 // chroma tile: rows/cols -2..33
+#define LT 70 // luma tile row stride (68 columns -2..65 used): an odd dword stride spreads a wave's rows over the LDS banks
+#define CT 38 // chroma tile row stride (36 columns used), odd in dwords likewise
 
 struct SearchArgs {
     const void    *rec[3];
@@ -213,8 +213,8 @@ __device__ __forceinline__ uint32_t oct_sum(uint32_t v) {
 
 template <typename T>
 __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) {
-    __shared__ __attribute__((aligned(16))) uint16_t ltile[LT * LT];
-    __shared__ __attribute__((aligned(16))) uint16_t ctile[2][CT * CT];
+    __shared__ __attribute__((aligned(16))) uint16_t ltile[(64 + 2 * CDEF_BORDER) * LT];
+    __shared__ __attribute__((aligned(16))) uint16_t ctile[2][(32 + 2 * CDEF_BORDER) * CT];
     __shared__ uint32_t stats[64][32][3]; // per pass: [gi][block-in-pass][sum_d, sum_d2, sse]
     __shared__ uint32_t sstat[64][2];     // per block source sum, sum^2 (luma)
     __shared__ uint64_t acc_l[64];        // per gi luma distortion
