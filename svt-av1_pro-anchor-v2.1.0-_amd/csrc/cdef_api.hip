@@ -128,7 +128,8 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
               hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
               hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096) * 8) == hipSuccess &&
               hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, (size_t)(41 * 4 * 32 + 4 * 32 + 64) * 4) == hipSuccess &&
-              hipMalloc(&s->d_fb_list, (nfb + 1) * 4) == hipSuccess &&
+              hipMalloc(&s->d_fb_list, (2 * nfb + 1) * 4) == hipSuccess &&
+              hipMalloc(&s->d_pick_xch, SVTGPU_PICK_XCH_BYTES) == hipSuccess &&
               hipHostMalloc((void **)&s->h_pick, 512 + nfb, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
               hipHostGetDevicePointer((void **)&s->h_pick_dev, s->h_pick, 0) == hipSuccess;
     if (!ok) {
@@ -136,6 +137,7 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
         return SVTGPU_ERR_OOM;
     }
     HIP_TRY(hipMemset(s->d_fb_strength, 0, nfb));
+    HIP_TRY(hipMemset(s->d_pick_xch, 0, SVTGPU_PICK_XCH_BYTES)); // no word carries a valid tag
     HIP_TRY(hipMemset(s->d_skip, 0, (nfb + 7) & ~(size_t)7)); // the padding stays 0 (the tables' word sums)
     HIP_TRY(hipMemset(s->d_skip, 1, nfb));
     s->own_mse      = s->d_mse;
@@ -154,7 +156,7 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     delete[] s->h_fb_kind;
     void *bufs[] = {s->d_fb_kind, s->d_mse_rem, s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip,
                     s->own_dir ? s->own_dir : s->d_dir, s->own_var ? (void *)s->own_var : (void *)s->d_var, s->d_fb_strength, s->d_pick_part,
-                    s->d_pick_out, s->d_pick_lev, s->d_fb_list};
+                    s->d_pick_out, s->d_pick_lev, s->d_fb_list, s->d_pick_xch};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_pick) (void)hipHostFree(s->h_pick);

@@ -11,6 +11,8 @@
 // nb (:853-872) and the per-FB assignment run on the device too and write the result straight into mapped
 // pinned memory: one host synchronisation per pick.  The filter_map remap (:911-919) stays on the host.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "svtgpu_internal.h"
@@ -42,10 +44,13 @@ struct StepArgs {
 };
 
 // ---- compaction: non-skipped FBs in raster order, zero-strength bias (EbEncCdef.c:820-851) ----
-__global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_list, int32_t *count) {
+__global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_list, int32_t *count, int32_t *wide,
+                                    int32_t *fb_inv, uint64_t *tot0) {
     __shared__ int32_t base;
     __shared__ int32_t wsum[NT / 64];
-    if (threadIdx.x == 0) base = 0;
+    if (threadIdx.x == 0) base = 0, *wide = 0; // the gather raises the width flag
+    if (tot0) // the first step's accumulators (launch path)
+        for (int e = threadIdx.x; e < MAX_CHAINS * 4096; e += NT) tot0[e] = 0;
     __syncthreads();
     for (int c0 = 0; c0 < nfb; c0 += NT) {
         const int  fb   = c0 + threadIdx.x;
@@ -58,6 +63,7 @@ __global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_li
         int off = base;
         for (int i = 0; i < w; i++) off += wsum[i];
         if (keep) fb_list[off + pre] = fb;
+        if (fb < nfb) fb_inv[fb] = keep ? off + pre : -1; // FB -> its row in the compacted tables
         __syncthreads();
         if (threadIdx.x == 0) base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
         __syncthreads();
@@ -242,60 +248,294 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     }
 }
 
+// ---- the same greedy chains in one persistent launch ----
+// PS_GRID workgroups stay resident for all NSTEPS + 1 steps: workgroup (chunk ci, row group g) keeps FB chunk ci
+// (<= PS_CH FBs) in LDS from the first step to the last and accumulates rows 16 g .. 16 g + 15 of every live chain's
+// tot over it.  A step is two exchanges through tagged 64-bit words (an 8-bit tag of the pick and step above a
+// 56-bit value, stored and polled with agent-scope atomics: a word is valid by itself, no fence or counter):
+//   1. the partial sums of every chunk -> the workgroup that owns row j of chain c sums its 64 entries over the 64
+//      chunks and publishes the row's first minimum (value, index);
+//   2. every workgroup reads the rows' minima of every live chain and takes the first minimum of the call
+//      (svt_search_one_dual's final loop, EbEncCdef.c:670-679), which every workgroup folds into the same selection.
+// The words of one exchange are rewritten at every step before anyone can read the next step's (a workgroup
+// reaches step s + 1 only after every row owner has read step s), so one buffer serves all steps; the pick's
+// 2-bit epoch in the tag keeps the previous pick's words apart.  Co-residency: PS_GRID workgroups of <= 34 KB
+// LDS and 256 threads (several fit per CU, and a pick launched beside another finds room); a poll gives up after
+// a bounded wait and sets a status bit, so a grid that cannot drain still ends.  Partial sums fit 56 bits:
+// an entry is < 2^41 (a 64x64 block's SSE at 12 bits is < 2^37), a chunk sums <= PS_CH of them, a total <= 2^15.
+#define PS_GRID  256
+#define PS_NCH   64  // FB chunks (x 4 row groups = PS_GRID)
+#define PS_CH    32  // FBs per chunk at most: frames up to 2048 non-skipped 64x64 blocks (3840x2160: 2040)
+constexpr unsigned long long PS_LOW = (1ull << 56) - 1;
+
+struct PersistArgs {
+    const uint64_t     *wmse;   // [fb_alloc][2][64] compacted, bias applied
+    const int32_t      *count;  // live FB count (device)
+    const int32_t      *wide;   // some entry >= 2^31: 64-bit terms
+    int32_t             chunk, fb_alloc, end_gi;
+    uint32_t            epoch;  // low 2 bits tag this pick's words
+    unsigned long long *part;   // [PS_NCH][4][4096] tagged partial sums
+    unsigned long long *amin;   // [4][64][2] tagged row minima: value, index
+    int32_t            *fin;    // [4][32] final list per chain
+    uint64_t           *best;   // [4]
+    int32_t            *status; // bit 0: a poll gave up
+    unsigned long long *stat;   // diagnostics (SVTGPU_PICK_STATS) or null: ticks of compute, exchange 1, exchange 2
+};
+
+// chain c's call at step s (the host schedule of the launch path): nb_sel = selection size of this call (-1: the
+// chain finished with the previous call; -2: the chain ended before), prev = the previous call's size (-1: none)
+struct ChainStep {
+    int nb, nb_sel, prev, shift;
+};
+__device__ __forceinline__ ChainStep chain_step(int c, int step) {
+    const int nb = 1 << c, len = 5 * nb;
+    ChainStep r;
+    r.nb     = nb;
+    r.nb_sel = step > len ? -2 : step < len ? (step < nb ? step : nb - 1) : -1;
+    r.prev   = step == 0 || step > len ? -1 : (step - 1 < nb ? step - 1 : nb - 1);
+    r.shift  = step >= 1 && step < len && step >= nb;
+    return r;
+}
+
+// poll the N tagged words p[i * stride] (those with use set) until every tag matches; false after the bounded wait
+template <int N>
+__device__ __forceinline__ bool ps_poll(const unsigned long long *p, size_t stride, bool use, unsigned long long (&v)[N],
+                                        unsigned long long tag) {
+    if (!use) return true;
+    uint32_t pend = (1u << N) - 1; // words still to see: a re-poll loads only those
+    for (unsigned spin = 0;; spin++) {
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (pend >> i & 1) {
+                v[i] = __hip_atomic_load(p + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v[i] & ~PS_LOW) == tag) pend &= ~(1u << i);
+            }
+        if (!pend) return true;
+        if (spin > (1u << 20)) return false; // ~0.1 s
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// the sum of the N tagged words p[i * stride] (their 56-bit values), each added once its tag is seen
+template <int N>
+__device__ __forceinline__ bool ps_poll_sum(const unsigned long long *p, size_t stride, unsigned long long tag,
+                                            unsigned long long &sum) {
+    uint32_t pend = (1u << N) - 1;
+    sum           = 0;
+    for (unsigned spin = 0;; spin++) {
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (pend >> i & 1) {
+                const unsigned long long v = __hip_atomic_load(p + i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v & ~PS_LOW) == tag) pend &= ~(1u << i), sum += v & PS_LOW;
+            }
+        if (!pend) return true;
+        if (spin > (1u << 20)) return false; // ~0.1 s
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+__device__ __forceinline__ void ps_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(NT, 4) sod_persist_kernel(const PersistArgs A) {
+    __shared__ __attribute__((aligned(16))) uint64_t m64[PS_CH * 128]; // the chunk: u64 rows, or u32 rows (narrow)
+    __shared__ uint64_t sb[MAX_CHAINS][PS_CH];                          // per-FB best over each chain's selection
+    __shared__ int32_t  sl[MAX_CHAINS][32];                             // selections ([0,16) luma, [16,32) chroma)
+    __shared__ uint64_t red[NT];
+    __shared__ int      s_fail;
+    const uint32_t *m32 = (const uint32_t *)m64;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int li = xcd_swizzle(blockIdx.x, gridDim.x), ci = li >> 2, g = li & 3; // a chunk's 4 groups share an XCD
+    const int f0 = ci * A.chunk, end = A.end_gi;
+    const int nfb  = max(0, min(*A.count - f0, A.chunk));
+    const int wide = *A.wide;
+    const unsigned long long ep = (unsigned long long)(A.epoch & 3) << 62;
+    unsigned long long       tk[3] = {0, 0, 0}, t0 = 0;
+    if (t == 0) s_fail = 0;
+    // the chunk into LDS, once (narrow: the low words, entry e of FB f at m32[f * 128 + e])
+    for (int e = t; e < nfb * 128; e += NT) {
+        const uint64_t v = A.wmse[(size_t)f0 * 128 + e];
+        if (wide) m64[e] = v;
+        else ((uint32_t *)m64)[e] = (uint32_t)v;
+    }
+    if (t < MAX_CHAINS * 32) sl[t >> 5][t & 31] = 0;
+    __syncthreads();
+    for (int step = 0; step <= NSTEPS; step++) {
+        const unsigned long long tag = ep | (unsigned long long)(step + 1) << 56, ptag = ep | (unsigned long long)step << 56;
+        if (A.stat && t == 0) t0 = __builtin_amdgcn_s_memrealtime();
+        // 1. the previous call's first minimum per chain (wave c: lane j holds row j's minimum), folded into the
+        // selection; a finishing chain publishes its list and value
+        {
+            const int       c = w;
+            const ChainStep C = chain_step(c, step);
+            if (C.prev >= 0) {
+                unsigned long long v[2] = {PS_LOW, PS_LOW};
+                if (!ps_poll<2>(A.amin + (c * 64 + lane) * 2, 1, lane < end, v, ptag)) s_fail = 1;
+                unsigned long long bv = v[0] & PS_LOW;
+                int                bi = (v[1] & PS_LOW) == PS_LOW ? (1 << 30) : (int)(v[1] & PS_LOW);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long ov = __shfl_xor(bv, o);
+                    const int                oi = __shfl_xor(bi, o);
+                    if (ov < bv || (ov == bv && oi < bi)) bv = ov, bi = oi;
+                }
+                if (lane == 0) {
+                    const bool any = bi < (1 << 30);
+                    sl[c][C.prev]      = any ? bi >> 6 : 0;
+                    sl[c][16 + C.prev] = any ? bi & 63 : 0;
+                    if (C.shift)
+                        for (int q = 0; q < C.nb - 1; q++) sl[c][q] = sl[c][q + 1], sl[c][16 + q] = sl[c][16 + q + 1];
+                    if (li == 0 && C.nb_sel == -1) A.best[c] = any ? bv : ((uint64_t)1 << 63);
+                }
+            }
+        }
+        __syncthreads();
+        if (li == 0 && t < MAX_CHAINS * 32 && chain_step(t >> 5, step).nb_sel == -1) A.fin[t] = sl[t >> 5][t & 31];
+        if (step == NSTEPS) break; // the last step only finishes the longest chain
+        if (A.stat && t == 0) tk[2] += __builtin_amdgcn_s_memrealtime() - t0, t0 = __builtin_amdgcn_s_memrealtime();
+        // 2. per-FB best over each live chain's selection (EbEncCdef.c:645-651): wave c, lane f
+        {
+            const int       c = w;
+            const ChainStep C = chain_step(c, step);
+            if (C.nb_sel >= 0 && lane < nfb) {
+                uint64_t b = (uint64_t)1 << 63;
+                for (int q = 0; q < C.nb_sel; q++) {
+                    const int      j = sl[c][q], k = sl[c][16 + q];
+                    const uint64_t v = wide ? m64[lane * 128 + j] + m64[lane * 128 + 64 + k]
+                                            : (uint64_t)m32[lane * 128 + j] + m32[lane * 128 + 64 + k];
+                    b = v < b ? v : b;
+                }
+                sb[c][lane] = b;
+            }
+        }
+        __syncthreads();
+        // 3. partial sums of rows 16 g + 4 w + {0..3}, column k = lane, of every live chain over the chunk
+        const int j0 = 16 * g + 4 * w, k = lane;
+#pragma unroll 1
+        for (int c = 0; c < MAX_CHAINS; c++) {
+            if (chain_step(c, step).nb_sel < 0) continue;
+            uint64_t acc[4] = {0, 0, 0, 0};
+            if (!wide) {
+#pragma unroll 4
+                for (int f = 0; f < nfb; f++) {
+                    const uint64_t b64 = sb[c][f];
+                    const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[f * 128 + 64 + k];
+                    const uint4    m0 = *(const uint4 *)&m32[f * 128 + j0];
+                    acc[0] += min(m0.x + m1k, b), acc[1] += min(m0.y + m1k, b);
+                    acc[2] += min(m0.z + m1k, b), acc[3] += min(m0.w + m1k, b);
+                }
+            } else {
+#pragma unroll 1
+                for (int f = 0; f < nfb; f++) {
+                    const uint64_t b = sb[c][f], m1k = m64[f * 128 + 64 + k];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t v = m64[f * 128 + j0 + u] + m1k;
+                        acc[u] += v < b ? v : b;
+                    }
+                }
+            }
+            if (k < end)
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (j0 + u < end) ps_store(A.part + ((size_t)(ci * 4 + c) * 4096 + (j0 + u) * 64 + k), tag | acc[u]);
+        }
+        if (A.stat && t == 0) tk[0] += __builtin_amdgcn_s_memrealtime() - t0, t0 = __builtin_amdgcn_s_memrealtime();
+        // 4. row owners: row j of the a-th live chain belongs to workgroup a * 64 + j (a < live chains, j < end)
+        {
+            int na = 0, c = -1;
+            for (int q = 0; q < MAX_CHAINS; q++)
+                if (chain_step(q, step).nb_sel >= 0) {
+                    if (na == (li >> 6)) c = q;
+                    na++;
+                }
+            const int j = li & 63;
+            if (c >= 0 && j < end) {
+                unsigned long long s = 0;
+                if (k < end && !ps_poll_sum<PS_NCH / 4>(A.part + (size_t)(w * 4 + c) * 4096 + j * 64 + k, (size_t)16 * 4096, tag, s))
+                    s_fail = 1;
+                red[t] = s;
+                __syncthreads();
+                if (w == 0) {
+                    unsigned long long bv = PS_LOW;
+                    int                bi = 1 << 30;
+                    if (k < end) bv = red[k] + red[64 + k] + red[128 + k] + red[192 + k], bi = j * 64 + k;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const unsigned long long ov = __shfl_xor(bv, o);
+                        const int                oi = __shfl_xor(bi, o);
+                        if (ov < bv || (ov == bv && oi < bi)) bv = ov, bi = oi;
+                    }
+                    if (lane == 0) {
+                        ps_store(A.amin + (c * 64 + j) * 2, tag | (bv & PS_LOW));
+                        ps_store(A.amin + (c * 64 + j) * 2 + 1, tag | (unsigned long long)bi);
+                    }
+                }
+            }
+        }
+        if (A.stat && t == 0) tk[1] += __builtin_amdgcn_s_memrealtime() - t0;
+    }
+    __syncthreads();
+    if (t == 0 && s_fail) atomicOr(A.status, 1);
+    if (A.stat && t == 0 && li == 0) A.stat[0] += tk[0], A.stat[1] += tk[1], A.stat[2] += tk[2], A.stat[3] += 1;
+}
+
 // ---- RD choice over the number of signalled strengths (EbEncCdef.c:853-872) ----
 struct PickOut {
-    int32_t  sb_count, nbits;
+    int32_t  sb_count, nbits, status, pad;
     int32_t  gi[32]; // [0, 16) luma, [16, 32) chroma strength indices of the chosen list (zero past nb)
     uint64_t best[MAX_CHAINS];
 };
-__global__ void pick_finish_kernel(const uint64_t *best, const int32_t *fin, const int32_t *count, uint64_t lambda,
-                                   int32_t *gis, int32_t *nb_out, PickOut *out) {
-    if (threadIdx.x != 0) return;
-    const int sb_count  = *count;
-    uint64_t  best_cost = (uint64_t)1 << 63;
-    int       nbits = 0, chosen = -1; // no list chosen: the strengths stay zero
-    for (int i = 0; i <= 3; i++) {
-        const int      nb   = 1 << i;
-        const int      bits = sb_count * i + nb * 6 * 2;
-        const int64_t  rate = (int64_t)bits << 9;                                                  // av1_cost_literal
-        const uint64_t cost = (uint64_t)(((rate * (int64_t)lambda + 256) >> 9) + ((int64_t)(best[i] * 16) << 7)); // RDCOST
-        if (cost < best_cost) best_cost = cost, nbits = i, chosen = i;
-    }
-    const int nb = 1 << nbits;
-    for (int j = 0; j < 16; j++) {
-        gis[j]      = chosen >= 0 && j < nb ? fin[chosen * 32 + j] : 0;
-        gis[16 + j] = chosen >= 0 && j < nb ? fin[chosen * 32 + 16 + j] : 0;
-        out->gi[j] = gis[j], out->gi[16 + j] = gis[16 + j];
-    }
-    *nb_out       = nb;
-    out->sb_count = sb_count;
-    out->nbits    = nbits;
-    for (int c = 0; c < MAX_CHAINS; c++) out->best[c] = best[c];
-}
-
-// ---- per-FB strength index (EbEncCdef.c:866-890); also into the host's copy ----
-__global__ void pick_assign_kernel(const uint64_t *wmse, const int32_t *fb_list, const int32_t *count, const int32_t *d_nb,
-                                   const int32_t *ygi, int8_t *fb_strength, int8_t *host_fbs) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *count) return;
-    const int nb = *d_nb;
-    const uint64_t *m0 = wmse + (size_t)i * 128, *m1 = m0 + 64;
-    uint64_t        best = (uint64_t)1 << 63;
-    int             bg   = 0;
-    for (int g = 0; g < nb; g++) {
-        const uint64_t c = m0[ygi[g]] + m1[ygi[16 + g]];
-        if (c < best) {
-            best = c;
-            bg   = g;
+__global__ void pick_final_kernel(const uint64_t *best, const int32_t *fin, const int32_t *count, uint64_t lambda,
+                                  PickOut *out, int32_t *status, const uint64_t *wmse, const int32_t *fb_inv, int nfb,
+                                  int8_t *fb_strength, int8_t *host_fbs) {
+    __shared__ int32_t gi[32];
+    __shared__ int32_t s_nb;
+    const int t = threadIdx.x;
+    if (t == 0) { // every workgroup makes the same choice; workgroup 0 publishes it
+        const int sb_count  = *count;
+        uint64_t  best_cost = (uint64_t)1 << 63;
+        int       nbits = 0, chosen = -1; // no list chosen: the strengths stay zero
+        for (int i = 0; i <= 3; i++) {
+            const int      nb   = 1 << i;
+            const int      bits = sb_count * i + nb * 6 * 2;
+            const int64_t  rate = (int64_t)bits << 9;                                                  // av1_cost_literal
+            const uint64_t cost = (uint64_t)(((rate * (int64_t)lambda + 256) >> 9) + ((int64_t)(best[i] * 16) << 7)); // RDCOST
+            if (cost < best_cost) best_cost = cost, nbits = i, chosen = i;
+        }
+        const int nb = 1 << nbits;
+        for (int j = 0; j < 16; j++) {
+            gi[j]      = chosen >= 0 && j < nb ? fin[chosen * 32 + j] : 0;
+            gi[16 + j] = chosen >= 0 && j < nb ? fin[chosen * 32 + 16 + j] : 0;
+        }
+        s_nb = nb;
+        if (blockIdx.x == 0) {
+            for (int j = 0; j < 32; j++) out->gi[j] = gi[j];
+            out->sb_count = sb_count;
+            out->nbits    = nbits;
+            for (int c = 0; c < MAX_CHAINS; c++) out->best[c] = best[c];
+            out->status = *status; // the persistent kernel's (0 on the launch path), re-armed for the next pick
+            *status     = 0;
         }
     }
-    fb_strength[fb_list[i]] = (int8_t)bg;
-    if (host_fbs) host_fbs[fb_list[i]] = (int8_t)bg;
-}
-
-__global__ void fill_i8_kernel(int8_t *p, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = 0;
+    __syncthreads();
+    // per-FB strength index (EbEncCdef.c:866-890), skipped FBs 0; also into the host's copy
+    const int fb = blockIdx.x * blockDim.x + t;
+    if (fb >= nfb) return;
+    const int i  = fb_inv[fb];
+    int       bg = 0;
+    if (i >= 0) {
+        const uint64_t *m0 = wmse + (size_t)i * 128, *m1 = m0 + 64;
+        uint64_t        bc = (uint64_t)1 << 63;
+        for (int g = 0; g < s_nb; g++) {
+            const uint64_t c = m0[gi[g]] + m1[gi[16 + g]];
+            if (c < bc) bc = c, bg = g;
+        }
+    }
+    fb_strength[fb] = (int8_t)bg;
+    if (host_fbs) host_fbs[fb] = (int8_t)bg;
 }
 
 // FB-chunk workgroups per step across the live chains (x 4 row tiles): more parts spread the accumulation, fewer
@@ -317,25 +557,53 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     uint64_t *wmse = s->d_pick_part; // layout: [nfb*128] wmse, then partials
     const size_t wmse_elems = (size_t)nfb * 128;
     int32_t  *d_count = s->d_fb_list + nfb;
-    hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count);
+    StepArgs  A;
+    A.lev  = s->d_pick_lev;                                  // [NSTEPS+1][4][32]
+    A.fin  = s->d_pick_lev + (NSTEPS + 1) * MAX_CHAINS * 32; // [4][32]
+    A.wide = A.fin + MAX_CHAINS * 32 + 33;                   // after the chosen list (32) and nb
+    // the persistent launch (SVTGPU_PICK_PERSIST=1; default: the launch per step) while its chunks hold every FB
+    const char *pe      = std::getenv("SVTGPU_PICK_PERSIST");
+    const bool  persist = pe && pe[0] == '1' && nfb <= PS_NCH * PS_CH;
+    int32_t    *d_inv   = s->d_fb_list + nfb + 1;
+    A.tot               = wmse + wmse_elems; // [3][4][4096]
+    hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count,
+                       (int32_t *)A.wide, d_inv, persist ? nullptr : A.tot);
     const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device
 
-    StepArgs A;
     A.wmse     = wmse;
     A.fb_alloc = nfb;
     A.count    = d_count;
     A.start_gi = 0;
     A.end_gi   = end;
-    A.tot      = wmse + wmse_elems;                            // [3][4][4096]
-    A.lev      = s->d_pick_lev;                                // [NSTEPS+1][4][32]
-    A.fin      = s->d_pick_lev + (NSTEPS + 1) * MAX_CHAINS * 32; // [4][32]
     A.best     = s->d_pick_out;
-    A.wide     = A.fin + MAX_CHAINS * 32 + 33; // after the chosen list (32) and nb
-    HIP_TRY(hipMemsetAsync(A.lev, 0, sizeof(int32_t) * ((NSTEPS + 2) * MAX_CHAINS * 32 + 64), st));
-    HIP_TRY(hipMemsetAsync(A.tot, 0, sizeof(uint64_t) * MAX_CHAINS * 4096, st)); // tot[0]
     hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
                        (int)ctrls->zero_fs_cost_bias, wmse, (int32_t *)A.wide);
-    for (int step = 0; step <= NSTEPS; step++) {
+    unsigned long long *xch = (unsigned long long *)s->d_pick_xch, *stat = nullptr;
+    int32_t            *d_status = (int32_t *)(xch + PS_NCH * 4 * 4096 + 4 * 64 * 2);
+    if (persist) {
+        static const bool stats = std::getenv("SVTGPU_PICK_STATS") != nullptr;
+        if (s->pick_xch_end != end) { // words of a different strength count could carry a current tag
+            HIP_TRY(hipMemsetAsync(xch, 0, SVTGPU_PICK_XCH_BYTES, st));
+            s->pick_xch_end = end;
+        }
+        if (stats) stat = xch + PS_NCH * 4 * 4096 + 4 * 64 * 2 + 8;
+        PersistArgs P;
+        P.wmse     = wmse;
+        P.count    = d_count;
+        P.wide     = A.wide;
+        P.chunk    = std::max(1, (nfb + PS_NCH - 1) / PS_NCH);
+        P.fb_alloc = nfb;
+        P.end_gi   = end;
+        P.epoch    = s->pick_epoch++;
+        P.part     = xch;
+        P.amin     = xch + PS_NCH * 4 * 4096;
+        P.fin      = A.fin;
+        P.best     = A.best;
+        P.status   = d_status;
+        P.stat     = stat;
+        hipLaunchKernelGGL(sod_persist_kernel, dim3(PS_GRID), dim3(NT), 0, st, P);
+    }
+    for (int step = 0; step <= NSTEPS && !persist; step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {
             const int nb = 1 << c, len = 5 * nb; // nb calls + 4*nb refinements
@@ -360,19 +628,26 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         svtgpu_wgclk_end("sod_step", 4 * parts * na, st);
     }
     HIP_TRY(hipGetLastError());
-    int32_t *d_gis = A.fin + MAX_CHAINS * 32, *d_nb = d_gis + 32;
     PickOut *h_out = (PickOut *)s->h_pick;
     int8_t  *h_fbs = (int8_t *)(s->h_pick + 512);
     static_assert(sizeof(PickOut) <= 512, "pick output slot");
-    hipLaunchKernelGGL(pick_finish_kernel, dim3(1), dim3(64), 0, st, (const uint64_t *)s->d_pick_out, (const int32_t *)A.fin,
-                       (const int32_t *)d_count, (uint64_t)lambda, d_gis, d_nb, (PickOut *)s->h_pick_dev);
-    HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, nfb, st));
     int8_t *host_fbs = fb_strength_out ? (int8_t *)(s->h_pick_dev + 512) : nullptr;
-    if (host_fbs) hipLaunchKernelGGL(fill_i8_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, host_fbs, nfb);
-    hipLaunchKernelGGL(pick_assign_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, wmse, s->d_fb_list, d_count, d_nb,
-                       d_gis, s->d_fb_strength, host_fbs);
+    hipLaunchKernelGGL(pick_final_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, (const uint64_t *)s->d_pick_out,
+                       (const int32_t *)A.fin, (const int32_t *)d_count, (uint64_t)lambda, (PickOut *)s->h_pick_dev,
+                       d_status, (const uint64_t *)wmse, (const int32_t *)d_inv, nfb, s->d_fb_strength, host_fbs);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st)); // the only wait of the pick
+    if (h_out->status) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "CDEF pick: the persistent step exchange timed out", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    if (stat) {
+        unsigned long long v[4];
+        HIP_TRY(hipMemcpy(v, stat, sizeof v, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(stat, 0, sizeof v));
+        std::fprintf(stderr, "sod_persist (workgroup 0): compute+store %.1f us, reduce %.1f us, minima %.1f us\n",
+                     v[0] * 0.01, v[1] * 0.01, v[2] * 0.01);
+    }
     memset(params, 0, sizeof(*params));
     const int nbits = h_out->nbits, nb = 1 << nbits;
     params->cdef_bits = (uint8_t)nbits;

@@ -67,6 +67,10 @@ static inline FrameGeo frame_geo(int32_t w, int32_t h) {
     return g;
 }
 
+// persistent pick exchange (cdef_pick.hip): [64 chunks][4 chains][4096] partial sums, [4][64][2] row minima,
+// then status and diagnostics words
+#define SVTGPU_PICK_XCH_BYTES ((size_t)(64 * 4 * 4096 + 4 * 64 * 2 + 16) * 8)
+
 struct SvtGpuCdefFrameState {
     SvtGpuContext *ctx;
     int32_t        width, height;
@@ -82,7 +86,10 @@ struct SvtGpuCdefFrameState {
     uint64_t      *d_pick_part;   // partial tot_mse tables
     uint64_t      *d_pick_out;    // [chains][4] (best, j, k)
     int32_t       *d_pick_lev;    // [chains][2][16]
-    int32_t       *d_fb_list;     // compacted non-skip FB indices
+    int32_t       *d_fb_list;     // compacted non-skip FB indices [nfb], their count, FB -> index or -1 [nfb]
+    uint64_t      *d_pick_xch;    // persistent pick: tagged partial sums, row minima, status, diagnostics (cdef_pick.hip)
+    uint32_t       pick_epoch;    // picks run by the persistent kernel (tags its exchange words)
+    int32_t        pick_xch_end;  // the strength count of the words in d_pick_xch (0: none written)
     uint8_t       *h_pick;        // pinned, mapped: the pick's result (PickOut) then the per-FB strengths [nfb]
     uint8_t       *h_pick_dev;    // its device address
     int32_t        pick_parts;

@@ -227,13 +227,16 @@ def test_cdef_band_search_allreduce(ctx, nb):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("persist", ["1", "0"])
 @pytest.mark.parametrize("top", [1 << 31, 1 << 40])
 @pytest.mark.parametrize("w,h", [(1024, 512), (3840, 2160)])
-def test_cdef_pick_bound_tables_vs_oracle(ctx, top, w, h):
+def test_cdef_pick_bound_tables_vs_oracle(ctx, top, w, h, persist, monkeypatch):
     """The frame pick over arbitrary mse tables: entries just below 2^31 (the 32-bit accumulation path, sums of
     two entries up to 2^32 - 2) and up to 2^40 (the 64-bit path), random skipped FBs; bit-exact vs the oracle.
-    At 3840x2160 (2040 FBs) the default launch shape stages the largest FB chunks (PICK_CHUNK) per workgroup."""
+    Both pick paths: the persistent kernel (default; 3840x2160 fills its 64 chunks of 32 FBs) and the launch per
+    step (SVTGPU_PICK_PERSIST=0; at 3840x2160 the default launch shape stages the largest FB chunks)."""
     import torch
+    monkeypatch.setenv("SVTGPU_PICK_PERSIST", persist)
     q, lam = 128, 60000
     ctrls = svtgpu.cdef_controls(1)
     st = svtgpu.CdefState(ctx, w, h)
@@ -249,3 +252,10 @@ def test_cdef_pick_bound_tables_vs_oracle(ctx, top, w, h):
     oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
     assert prm.as_tuple() == oprm.as_tuple()
     assert np.array_equal(fbs, ofbs)
+    # again on the same state (the persistent kernel's exchange words of the previous pick stay behind), then at a
+    # level with fewer strengths (the words are cleared), then back
+    for lv in (1, 5, 1):
+        c2 = svtgpu.cdef_controls(lv)
+        prm2, fbs2 = st.pick(c2, q, lam)
+        oprm2, ofbs2 = oracle.cdef_pick(w, h, mse, skip, c2, q, lam)
+        assert prm2.as_tuple() == oprm2.as_tuple() and np.array_equal(fbs2, ofbs2), lv
