@@ -185,7 +185,10 @@ static_assert(SG_NC == 3 || SG_NC == 7 || SG_NC == 15, "a complete outcome tree 
 // 1024 px * 1023^2 < 2^31), the four wave partials meet in LDS in i64 and scatter into the output layout.
 // ---------------------------------------------------------------------------------------------
 typedef int v4i32 __attribute__((ext_vector_type(4)));
-constexpr int SM_RS = 72;                  // LDS row stride of the byte planes (70 used + realign slack)
+// LDS row stride of the byte planes (70 used + realign slack): 19 dwords, so the rows a feature block's lanes read
+// (<= 4 rows at dword offsets 4 g + {0, 1}) fall in distinct banks of each 32-lane group -- with 18 the rows two
+// apart met in one bank (1.75-2 LDS cycles per read instead of 1.0-1.25)
+constexpr int SM_RS = 76;
 constexpr int SM_DROWS = 70, SM_XROWS = 64; // D rows (tile + 2 x 3 apron), X rows
 constexpr int SM_PLANE = (SM_DROWS + SM_XROWS) * SM_RS + 16; // one byte plane: D rows, then X rows, + read slack
 
