@@ -33,17 +33,47 @@ __constant__ int c_w[kShapes] = MD_W, c_h[kShapes] = MD_H, c_off[kShapes + 1] = 
 struct Step {
     int s, c, horiz;
 };
-__constant__ int  c_pass_end[8] = {2, 5, 7, 10, 12, 15, 17, 18};
-__constant__ Step c_steps[18]   = {
-    {2, 0, 1}, {1, 0, 0},               // 8x4, 4x8 from 4x4
-    {3, 2, 0}, {14, 2, 1}, {13, 1, 0},  // 8x8, 16x4, 4x16
-    {5, 3, 1}, {4, 3, 0},               // 16x8, 8x16
-    {6, 5, 0}, {16, 5, 1}, {15, 4, 0},  // 16x16, 32x8, 8x32
-    {8, 6, 1}, {7, 6, 0},               // 32x16, 16x32
-    {9, 8, 0}, {18, 8, 1}, {17, 7, 0},  // 32x32, 64x16, 16x64
-    {11, 9, 1}, {10, 9, 0},             // 64x32, 32x64
-    {12, 11, 0},                        // 64x64
+constexpr int lg2i(int v) { return v <= 1 ? 0 : 1 + lg2i(v / 2); }
+// a reduction step with its shifts (every count is a power of two): shape s (output offset off_s) from child shape c
+// (offset off_c); blocks of s per SB row 1 << lg_ncol, blocks of s 1 << lg_n, blocks of c per SB row 1 << lg_ccol
+struct StepX {
+    int16_t off_s, off_c;
+    int8_t  lg_ncol, lg_n, lg_ccol, horiz;
 };
+#define MD_STEP(S, C, HZ)                                                                                          \
+    StepX {                                                                                                        \
+        (int16_t)h_off[S], (int16_t)h_off[C], (int8_t)lg2i(64 / h_w[S]), (int8_t)lg2i(4096 / (h_w[S] * h_h[S])),     \
+            (int8_t)lg2i(64 / h_w[C]), (int8_t)(HZ)                                                                \
+    }
+__constant__ int  c_pass_end[8] = {2, 5, 7, 10, 12, 15, 17, 18};
+__constant__ StepX c_steps[18]  = {
+    MD_STEP(2, 0, 1), MD_STEP(1, 0, 0),                    // 8x4, 4x8 from 4x4
+    MD_STEP(3, 2, 0), MD_STEP(14, 2, 1), MD_STEP(13, 1, 0), // 8x8, 16x4, 4x16
+    MD_STEP(5, 3, 1), MD_STEP(4, 3, 0),                    // 16x8, 8x16
+    MD_STEP(6, 5, 0), MD_STEP(16, 5, 1), MD_STEP(15, 4, 0), // 16x16, 32x8, 8x32
+    MD_STEP(8, 6, 1), MD_STEP(7, 6, 0),                    // 32x16, 16x32
+    MD_STEP(9, 8, 0), MD_STEP(18, 8, 1), MD_STEP(17, 7, 0), // 32x32, 64x16, 16x64
+    MD_STEP(11, 9, 1), MD_STEP(10, 9, 0),                  // 64x32, 32x64
+    MD_STEP(12, 11, 0),                                    // 64x64
+};
+#undef MD_STEP
+
+// four samples of a row from x (in the picture, 4 * sizeof(T) bytes): aligned dword loads and a funnel shift (the
+// dwords read stay inside [x, x + 3] rounded out to dwords)
+template <typename T>
+__device__ __forceinline__ void row4(const T *row, int x, int (&v)[4]) {
+    const uint32_t *p = (const uint32_t *)((uintptr_t)(row + x) & ~(uintptr_t)3);
+    const int       b = (int)((uintptr_t)(row + x) & 3); // byte misalignment
+    if constexpr (sizeof(T) == 2) {
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[b ? 2 : 1];
+        const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, b * 8), hi = __builtin_amdgcn_alignbit(w2, w1, b * 8);
+        v[0] = lo & 0xFFFF, v[1] = lo >> 16, v[2] = hi & 0xFFFF, v[3] = hi >> 16;
+    } else {
+        const uint32_t w0 = p[0], w1 = p[b ? 1 : 0];
+        const uint32_t q = __builtin_amdgcn_alignbyte(w1, w0, b);
+        v[0] = q & 0xFF, v[1] = (q >> 8) & 0xFF, v[2] = (q >> 16) & 0xFF, v[3] = q >> 24;
+    }
+}
 
 struct MdArgs {
     const void    *src;
@@ -98,11 +128,18 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
             int y = ry + cy * 4 + i;
             if (!rin) y = min(max(y, 0), H - 1);
             const T *row = ref + (size_t)y * rs;
+            int      rv[4];
+            if (rin) { // the row segment lies inside the picture: aligned dword loads
+                row4<T>(row, rx + cx * 4, rv);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) rv[j] = (int)row[min(max(rx + cx * 4 + j, 0), W - 1)];
+            }
+            const uint2 sw = *(const uint2 *)&s_src[(cy * 4 + i) * 64 + cx * 4]; // four source samples
+            const int   sv[4] = {(int)(sw.x & 0xFFFF), (int)(sw.x >> 16), (int)(sw.y & 0xFFFF), (int)(sw.y >> 16)};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                int x = rx + cx * 4 + j;
-                if (!rin) x = min(max(x, 0), W - 1);
-                const int d = (int)s_src[(cy * 4 + i) * 64 + cx * 4 + j] - (int)row[x];
+                const int d = sv[j] - rv[j];
                 sad += (uint32_t)abs(d);
                 sse += (uint32_t)(d * d);
                 sum += d;
@@ -114,14 +151,13 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
         for (int p = 0; p < 8; p++) {
             __syncthreads();
             for (; st < c_pass_end[p]; st++) {
-                const Step q    = c_steps[st];
-                const int  ncol = 64 / c_w[q.s], n = 4096 / (c_w[q.s] * c_h[q.s]);
-                const int  ccol = 64 / c_w[q.c];
+                const StepX q = c_steps[st];
+                const int   n = 1 << q.lg_n, mcol = (1 << q.lg_ncol) - 1, ccol = 1 << q.lg_ccol;
                 for (int b = tid; b < n; b += 256) {
-                    const int bi = b / ncol, bj = b % ncol;
-                    const int c0 = q.horiz ? bi * ccol + 2 * bj : 2 * bi * ccol + bj;
+                    const int bi = b >> q.lg_ncol, bj = b & mcol;
+                    const int c0 = q.horiz ? (bi << q.lg_ccol) + 2 * bj : ((2 * bi) << q.lg_ccol) + bj;
                     const int c1 = q.horiz ? c0 + 1 : c0 + ccol;
-                    const int dst = c_off[q.s] + b, x0 = c_off[q.c] + c0, x1 = c_off[q.c] + c1;
+                    const int dst = q.off_s + b, x0 = q.off_c + c0, x1 = q.off_c + c1;
                     s_sad[dst] = s_sad[x0] + s_sad[x1];
                     s_sse[dst] = s_sse[x0] + s_sse[x1];
                     s_sum[dst] = s_sum[x0] + s_sum[x1];
