@@ -41,7 +41,7 @@ import time
 
 import numpy as np
 
-FRAMES_IN_FLIGHT = 3  # default frames pipelined per GPU (measured: 1 -> 1498, 2 -> 1590, 3 -> 1750, 4 -> 1460 Mpx/s)
+FRAMES_IN_FLIGHT = 4  # default frames pipelined per GPU (round 3 final kernels: 2 -> 2672, 3 -> 2846, 4 -> 2914, 5 -> 2772 Mpx/s)
 
 
 def _frames_in_flight(argv):
