@@ -20,7 +20,7 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT --kernel-include-regex "$K" -d $O/sqA -o run --output-format csv -- $B > $O/sqA.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_MISC SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "$K" -d $O/sqB -o run --output-format csv -- $B > $O/sqB.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f1 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix --frames-in-flight 1 > $O/trace_f1.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f3 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix > $O/trace_f3.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f4 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix > $O/trace_f4.log 2>&1
 rc=$?
 echo "exit $rc"
 exit $rc
