@@ -45,12 +45,10 @@ struct StepArgs {
 
 // ---- compaction: non-skipped FBs in raster order, zero-strength bias (EbEncCdef.c:820-851) ----
 __global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_list, int32_t *count, int32_t *wide,
-                                    int32_t *fb_inv, uint64_t *tot0) {
+                                    int32_t *fb_inv) {
     __shared__ int32_t base;
     __shared__ int32_t wsum[NT / 64];
     if (threadIdx.x == 0) base = 0, *wide = 0; // the gather raises the width flag
-    if (tot0) // the first step's accumulators (launch path)
-        for (int e = threadIdx.x; e < MAX_CHAINS * 4096; e += NT) tot0[e] = 0;
     __syncthreads();
     for (int c0 = 0; c0 < nfb; c0 += NT) {
         const int  fb   = c0 + threadIdx.x;
@@ -72,8 +70,10 @@ __global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_li
 }
 
 __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *fb_list, const int32_t *count,
-                                   int bias, uint64_t *wmse, int32_t *wide) {
+                                   int bias, uint64_t *wmse, int32_t *wide, uint64_t *tot0) {
     const int i = blockIdx.x;
+    if (tot0) // the first step's accumulators (launch path), spread over the grid
+        for (int e = i * 128 + threadIdx.x; e < MAX_CHAINS * 4096; e += gridDim.x * 128) tot0[e] = 0;
     if (i >= *count) return;
     const int fb = fb_list[i];
     const int p = threadIdx.x >> 6, g = threadIdx.x & 63; // 128 threads
@@ -567,7 +567,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     int32_t    *d_inv   = s->d_fb_list + nfb + 1;
     A.tot               = wmse + wmse_elems; // [3][4][4096]
     hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count,
-                       (int32_t *)A.wide, d_inv, persist ? nullptr : A.tot);
+                       (int32_t *)A.wide, d_inv);
     const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device
 
     A.wmse     = wmse;
@@ -577,7 +577,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     A.end_gi   = end;
     A.best     = s->d_pick_out;
     hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
-                       (int)ctrls->zero_fs_cost_bias, wmse, (int32_t *)A.wide);
+                       (int)ctrls->zero_fs_cost_bias, wmse, (int32_t *)A.wide, persist ? nullptr : A.tot);
     unsigned long long *xch = (unsigned long long *)s->d_pick_xch, *stat = nullptr;
     int32_t            *d_status = (int32_t *)(xch + PS_NCH * 4 * 4096 + 4 * 64 * 2);
     if (persist) {
