@@ -259,3 +259,29 @@ def test_cdef_pick_bound_tables_vs_oracle(ctx, top, w, h, persist, monkeypatch):
         prm2, fbs2 = st.pick(c2, q, lam)
         oprm2, ofbs2 = oracle.cdef_pick(w, h, mse, skip, c2, q, lam)
         assert prm2.as_tuple() == oprm2.as_tuple() and np.array_equal(fbs2, ofbs2), lv
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("frac", [1.0, 0.999])
+def test_cdef_pick_all_or_almost_all_skipped(ctx, frac, persist, monkeypatch):
+    """Edge cases of the pick's compaction: every FB skipped (no rows: the chains return the reference's (1 << 63)
+    sentinel and the RD choice keeps one zero strength) and a single live FB; both pick paths; bit-exact vs the
+    oracle, skipped FBs get index 0."""
+    import torch
+    monkeypatch.setenv("SVTGPU_PICK_PERSIST", persist)
+    w, h, q, lam = 1920, 1080, 128, 60000
+    ctrls = svtgpu.cdef_controls(1)
+    st = svtgpu.CdefState(ctx, w, h)
+    rng = np.random.default_rng(1234)
+    mse = rng.integers(0, 1 << 30, size=(2, st.nfb, 64), dtype=np.int64).astype(np.uint64)
+    skip = np.ones(st.nfb, np.uint8)
+    if frac < 1.0:
+        skip[st.nfb // 2] = 0
+    mse_t = torch.from_numpy(mse.view(np.int64)).cuda()
+    skip_t = torch.from_numpy(skip).cuda()
+    st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+    torch.cuda.synchronize()
+    prm, fbs = st.pick(ctrls, q, lam)
+    oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
+    assert prm.as_tuple() == oprm.as_tuple()
+    assert np.array_equal(fbs, ofbs)
