@@ -1351,8 +1351,9 @@ __device__ Descent sgr_seed(const SearchArgs &A, int p, int i, const int64_t *m,
     return d;
 }
 
-// best ep per unit (strict <, first) -> best[unit] = {ep index, ep, xq0, xq1}
-__global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplanes, int n, int32_t *best) {
+// best ep per unit (strict <, first) -> best[unit] = {ep index, ep, xq0, xq1}, raw[unit] = the descent's two values
+// (what the host's records hold: only these come back, not every (unit, ep) descent)
+__global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplanes, int n, int32_t *best, int32_t *raw) {
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= n) return;
     int p = 0;
@@ -1368,6 +1369,7 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
     best[4 * u + 1] = ep;
     best[4 * u + 2] = c_sgr_r[ep][0] == 0 ? 0 : x0;
     best[4 * u + 3] = c_sgr_r[ep][0] == 0 ? 128 - x1 : c_sgr_r[ep][1] == 0 ? 0 : 128 - x0 - x1;
+    raw[2 * u] = x0, raw[2 * u + 1] = x1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2232,17 +2234,17 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                  o_sstat = dc(8);
     const size_t zero_span = dc.off - o_sum;
     const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
-                 o_sds = dc(sizeof(Descent) * npairs);
-    const size_t res_span = dc.off - o_sse;
+                 o_best = dc(16 * (size_t)n_sg), o_braw = dc(8 * (size_t)n_sg);
+    const size_t res_span = dc.off - o_sse; // the (unit, ep) descents stay on the device: the best ep's come back
+    const size_t o_sds = dc(sizeof(Descent) * npairs);
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_best = dc(16 * (size_t)n_sg);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
     const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
     const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
-                 h_wds = h_res + (o_wds - o_sse), h_sds = h_res + (o_sds - o_sse);
+                 h_wds = h_res + (o_wds - o_sse), h_best = h_res + (o_best - o_sse), h_braw = h_res + (o_braw - o_sse);
     if (dc.off > s->work_bytes) {
         (void)hipFree(s->d_work);
         s->d_work = nullptr, s->work_bytes = 0;
@@ -2406,7 +2408,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // ---- phase 4: best ep and its clipped SSE; read back the descents ----
     if (n_sg) {
         hipLaunchKernelGGL(sgr_best_kernel, dim3((n_sg + 255) / 256), dim3(256), 0, st, (const Descent *)dp(o_sds), A,
-                           sg_planes, n_sg, (int32_t *)dp(o_best));
+                           sg_planes, n_sg, (int32_t *)dp(o_best), (int32_t *)dp(o_braw));
         run(4, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
                                (unsigned long long *)dp(o_sse2), tk);
@@ -2417,7 +2419,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
     if (prof)
         if (int rc = prof->finish(st)) return rc; // fold the launch timings on the device, no read-back
-    Descent        *hw = (Descent *)hp(h_wds), *hs = (Descent *)hp(h_sds);
+    Descent        *hw = (Descent *)hp(h_wds);
+    const int32_t  *hbest = (const int32_t *)hp(h_best), *hraw = (const int32_t *)hp(h_braw);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
     svtgpu_count_xfer(1, res_span);
@@ -2462,13 +2465,9 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 hw[gu].taps(1, v), set_wiener_taps(R.wiener.vfilter, v);
             }
             if (q.sg) {
-                const Descent *d  = hs + q.pair_base + u * q.ne;
-                int64_t        be = -1;
-                int            bk = 0;
-                for (int k = 0; k < q.ne; k++)
-                    if (be == -1 || d[k].err < be) be = d[k].err, bk = k;
+                const int bk = hbest[4 * gu]; // sgr_best_kernel: the first ep of least error
                 R.sgrproj.type = SVTGPU_RESTORE_SGRPROJ, R.sgrproj.ep = q.eps[bk];
-                R.sgrproj.xqd[0] = d[bk].val(0, 0), R.sgrproj.xqd[1] = d[bk].val(0, 1);
+                R.sgrproj.xqd[0] = hraw[2 * gu], R.sgrproj.xqd[1] = hraw[2 * gu + 1];
                 R.sse[2] = (int64_t)sse2[gu];
             }
             if (search_out && search_out[p]) search_out[p][uloc[gu]] = R;
