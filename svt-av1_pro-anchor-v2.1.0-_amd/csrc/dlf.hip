@@ -520,6 +520,27 @@ struct LevelTables {
 
 static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 
+// the level per (segment, reference, mode) class of one plane and direction whose base level is lv
+// (svt_av1_loop_filter_frame_init, EbDeblockingFilter.c)
+static void fill_level_table(const SvtGpuLfParams &p, int pl, int dir, int lv, uint8_t *out) {
+    static const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
+    for (int seg = 0; seg < 8; seg++) {
+        int ls = lv;
+        if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
+            ls = clampi(ls + p.seg_feature_data[seg][feat[pl][dir]], 0, 63);
+        for (int ref = 0; ref < 8; ref++)
+            for (int mode = 0; mode < 2; mode++) {
+                int v = ls;
+                if (p.mode_ref_delta_enabled) {
+                    const int scale = 1 << (ls >> 5);
+                    v = ls + p.ref_deltas[ref] * scale + (ref > 0 ? p.mode_deltas[mode] * scale : 0);
+                    v = clampi(v, 0, 63);
+                }
+                out[seg * 16 + ref * 2 + mode] = (uint8_t)v;
+            }
+    }
+}
+
 void build_level_tables(const SvtGpuLfParams &p, LevelTables &L) {
     std::memset(&L, 0, sizeof L);
     const int sh = p.sharpness_level;
@@ -534,24 +555,8 @@ void build_level_tables(const SvtGpuLfParams &p, LevelTables &L) {
     const int base[3][2] = {{p.filter_level[0], p.filter_level[1]},
                             {p.filter_level_u, p.filter_level_u},
                             {p.filter_level_v, p.filter_level_v}};
-    const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
     for (int pl = 0; pl < 3; pl++)
-        for (int seg = 0; seg < 8; seg++)
-            for (int dir = 0; dir < 2; dir++) {
-                int lv = base[pl][dir];
-                if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
-                    lv = clampi(lv + p.seg_feature_data[seg][feat[pl][dir]], 0, 63);
-                for (int ref = 0; ref < 8; ref++)
-                    for (int mode = 0; mode < 2; mode++) {
-                        int v = lv;
-                        if (p.mode_ref_delta_enabled) {
-                            const int scale = 1 << (lv >> 5);
-                            v = lv + p.ref_deltas[ref] * scale + (ref > 0 ? p.mode_deltas[mode] * scale : 0);
-                            v = clampi(v, 0, 63);
-                        }
-                        L.lvl[pl][dir][seg * 16 + ref * 2 + mode] = (uint8_t)v;
-                    }
-            }
+        for (int dir = 0; dir < 2; dir++) fill_level_table(p, pl, dir, base[pl][dir], L.lvl[pl][dir]);
 }
 
 // is the plane filtered at all with these levels (svt_aom_loop_filter_sb :575-582)
@@ -722,13 +727,17 @@ int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
             J.ref          = src->plane[plane];
             J.ref_stride   = src->stride[plane];
             J.ntrial       = mi;
-            for (int k = 0; k < mi; k++) {
+            for (int k = 0; k < mi; k++) { // the trial's tables of this plane only (try_filter_frame's levels)
                 SvtGpuLfParams q = p;
                 set_trial_level(q, plane, srch[i]->dir, lv[i][k]);
-                build_level_tables(q, L);
+                const int  base[3][2] = {{q.filter_level[0], q.filter_level[1]},
+                                         {q.filter_level_u, q.filter_level_u},
+                                         {q.filter_level_v, q.filter_level_v}};
                 const bool on = plane_active(q, plane);
-                for (int dir = 0; dir < 2; dir++)
-                    if (on) std::memcpy(J.lvl[k][dir], L.lvl[plane][dir], 128);
+                for (int dir = 0; dir < 2; dir++) {
+                    if (on) fill_level_table(q, plane, dir, base[plane][dir], J.lvl[k][dir]);
+                    else std::memset(J.lvl[k][dir], 0, 128);
+                }
             }
             m[a.njob]   = mi;
             who[a.njob] = i;
