@@ -20,6 +20,8 @@
 //    horizontal edges over the tile's columns; the tile is either written out (apply) or compared with
 //    the source for the SSE of a level trial — recon is never modified by a trial, so the search
 //    needs no backup/restore copies, and a trial reads each sample once.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -213,6 +215,15 @@ struct DlfPlaneJob {
     uint8_t         lvl[MAX_TRIALS][2][128]; // [trial][dir][class] filter level
 };
 
+// a device-resident level search (svtgpu_dlf_pick with SVTGPU_DLF_DEVICE=1): the levels and level tables of the next
+// trial launch, written by dlf_search_step_kernel from the previous launch's SSEs (no host decision between trials)
+struct DlfDevPlan {
+    int32_t ntrial[MAX_JOBS];                   // levels of each job in the next trial launch (0: the job has none)
+    int32_t lv[MAX_JOBS][MAX_TRIALS];
+    uint8_t lvl[MAX_JOBS][MAX_TRIALS][2][128];  // [job][trial][dir][class]
+    int32_t done;                               // every search has finished
+};
+
 struct DlfTileArgs {
     DlfPlaneJob job[MAX_JOBS];
     int32_t     njob, bd;
@@ -224,6 +235,7 @@ struct DlfTileArgs {
     unsigned long long *out; // [MAX_JOBS][MAX_TRIALS] sums, then the sequence word (svtgpu_wait_seq)
     unsigned long long  seq;
     unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
+    const DlfDevPlan   *plan;  // trial mode: levels from the device plan (the grid covers MAX_TRIALS per job) or null
 };
 
 // The edges of one direction that filter anything (a length and a nonzero level on either side), listed in LDS
@@ -298,10 +310,12 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a) 
     const DlfPlaneJob &J = a.job[jb];
     const int tr = TRIAL ? tb % J.ntrial : 0;
     if (TRIAL) tb /= J.ntrial;
+    if (TRIAL && a.plan && tr >= a.plan->ntrial[jb]) return; // a level the device plan does not try this launch
     const int x0 = J.ox + (tb % J.tiles_x) * TILE, y0 = J.oy + (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
-    s_lvl[tid >> 7][tid & 127] = J.lvl[tr][tid >> 7][tid & 127]; // NTHR == 256 entries
+    s_lvl[tid >> 7][tid & 127] = (TRIAL && a.plan) ? a.plan->lvl[jb][tr][tid >> 7][tid & 127]
+                                                   : J.lvl[tr][tid >> 7][tid & 127]; // NTHR == 256 entries
     if (tid < 64) s_thr[tid] = (uint32_t)a.mblim[tid] | ((uint32_t)a.lim[tid] << 8) | ((uint32_t)a.hev[tid] << 16);
 
     // edge records reaching the tile (no records outside the plane: length 0) and the tile + apron (samples outside
@@ -441,7 +455,7 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a) 
     wgclk_mark(a.wgclk, 5);
     // trial: the last workgroup to finish reads the sums (8-B agent atomics on both sides; this lane's SSE adds have
     // completed before its arrival is counted) and re-arms the accumulators for the next launch
-    if (TRIAL && tid == 0) {
+    if (TRIAL && tid == 0 && !a.plan) { // (device plan: dlf_search_step_kernel reads the sums in stream order)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (atomicAdd(a.arrive, 1u) == gridDim.x - 1) {
             for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) a.out[q] = atomicExch(&a.sse[q], 0ull);
@@ -506,6 +520,8 @@ struct SvtGpuDlfState {
     // out_rect (luma {x0, y0, x1, y1}; the whole frame by default)
     int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
     SvtGpuComm    *comm = nullptr;
+    void          *d_search = nullptr;  // DlfDevSearch: the device-resident level search (SVTGPU_DLF_DEVICE)
+    void          *h_search = nullptr;  // its pinned host copy
     SvtGpuLfMi    *h_mi = nullptr;      // pinned staging of the mode info (one upload per frame, asynchronous)
     hipEvent_t     mi_free = nullptr;   // the previous upload has read h_mi
 };
@@ -518,12 +534,12 @@ struct LevelTables {
     uint8_t mblim[64], lim[64], hev[64];
 };
 
-static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+__host__ __device__ static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 
 // the level per (segment, reference, mode) class of one plane and direction whose base level is lv
 // (svt_av1_loop_filter_frame_init, EbDeblockingFilter.c)
-static void fill_level_table(const SvtGpuLfParams &p, int pl, int dir, int lv, uint8_t *out) {
-    static const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
+__host__ __device__ static void fill_level_table(const SvtGpuLfParams &p, int pl, int dir, int lv, uint8_t *out) {
+    const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
     for (int seg = 0; seg < 8; seg++) {
         int ls = lv;
         if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
@@ -560,7 +576,7 @@ void build_level_tables(const SvtGpuLfParams &p, LevelTables &L) {
 }
 
 // is the plane filtered at all with these levels (svt_aom_loop_filter_sb :575-582)
-bool plane_active(const SvtGpuLfParams &p, int plane) {
+__host__ __device__ bool plane_active(const SvtGpuLfParams &p, int plane) {
     if (plane == 0) return p.filter_level[0] || p.filter_level[1];
     return plane == 1 ? p.filter_level_u != 0 : p.filter_level_v != 0;
 }
@@ -616,7 +632,7 @@ bool frame_matches(const SvtGpuDlfState *s, const SvtGpuFrame *f) {
     return f && f->width == s->width && f->height == s->height && (f->bit_depth == 8 || f->bit_depth == 10);
 }
 
-void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_filter_frame (:841-883)
+__host__ __device__ void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_filter_frame (:841-883)
     if (plane == 0) {
         if (dir != 1) p.filter_level[0] = lvl;
         if (dir != 0) p.filter_level[1] = lvl;
@@ -630,15 +646,16 @@ void set_trial_level(SvtGpuLfParams &p, int plane, int dir, int lvl) { // try_fi
 // next step needs (advancing over steps whose levels are already known), feed() records their SSE.  Independent
 // searches (U and V) then share launches.
 struct LevelSearch {
-    int     plane, dir, early_exit, only4x4;
-    int     mid, step, direction = 0, conv = 0, best;
+    int     plane = 0, dir = 0, early_exit = 0, only4x4 = 0;
+    int     mid = 0, step = 0, direction = 0, conv = 0, best = 0;
     int64_t best_err = 0, bias = 0, err[64];
     int     phase = 0; // 0: the start level; 1: bisection steps; 2: done
     int     lo = 0, hi = 0;
     bool    try_lo = false, try_hi = false;
     int     req[MAX_TRIALS], nreq = 0;
 
-    LevelSearch(const int last[4], int dlf_avg, int early_exit_, int only4x4_, int plane_, int dir_)
+    __host__ __device__ LevelSearch() {}
+    __host__ __device__ LevelSearch(const int last[4], int dlf_avg, int early_exit_, int only4x4_, int plane_, int dir_)
         : plane(plane_), dir(dir_), early_exit(early_exit_), only4x4(only4x4_) {
         const int start = plane == 0 ? (dlf_avg ? last[0] : last[dir]) : last[plane + 1];
         mid  = clampi(start, 0, 63);
@@ -648,12 +665,12 @@ struct LevelSearch {
         req[0] = mid, nreq = 1;
     }
     // the next bisection step's candidates (try lo / hi around mid), or done
-    void next_request() {
+    __host__ __device__ void next_request() {
         if (step <= 0) {
             phase = 2, nreq = 0;
             return;
         }
-        hi   = std::min(mid + step, 63), lo = std::max(mid - step, 0);
+        hi   = mid + step < 63 ? mid + step : 63, lo = mid - step > 0 ? mid - step : 0;
         bias = (best_err >> (15 - (mid / 8))) * step;
         if (!only4x4) bias >>= 1;
         try_lo = direction <= 0 && lo != mid, try_hi = direction >= 0 && hi != mid;
@@ -661,7 +678,7 @@ struct LevelSearch {
         if (try_lo) req[nreq++] = lo;
         if (try_hi) req[nreq++] = hi;
     }
-    void resolve() {
+    __host__ __device__ void resolve() {
         if (phase == 0) {
             best_err = err[mid], best = mid, phase = 1;
         } else {
@@ -684,7 +701,7 @@ struct LevelSearch {
         }
         next_request();
     }
-    int pending(int *lv) {
+    __host__ __device__ int pending(int *lv) {
         while (phase != 2) {
             int m = 0;
             for (int k = 0; k < nreq; k++) {
@@ -697,10 +714,116 @@ struct LevelSearch {
         }
         return 0;
     }
-    void feed(const int *lv, int m, const unsigned long long *sse) {
+    __host__ __device__ void feed(const int *lv, int m, const unsigned long long *sse) {
         for (int k = 0; k < m; k++) err[lv[k]] = (int64_t)sse[k];
     }
 };
+
+// The device-resident form of the searches (SVTGPU_DLF_DEVICE=1): the plane searches, the frame's parameters and the
+// next trial launch's plan live in HBM; after each trial launch one single-lane kernel feeds the SSEs to the searches
+// and writes the next plan, so the bisection advances with no host decision between trials.  The host enqueues a
+// chunk of (trial, step) pairs and reads the state back once per chunk; launches after the searches have finished
+// find an empty plan (every workgroup returns at once).
+struct DlfDevSearch {
+    LevelSearch    srch[MAX_JOBS];
+    int32_t        ns;
+    SvtGpuLfParams p;
+    DlfDevPlan     plan;
+};
+
+// the next launch's levels per search and each (search, level)'s tables: that plane's only, as run_searches builds
+__host__ __device__ void plan_next(DlfDevSearch &S) {
+    S.plan.done = 1;
+    for (int i = 0; i < MAX_JOBS; i++) {
+        const int m = i < S.ns ? S.srch[i].pending(S.plan.lv[i]) : 0;
+        S.plan.ntrial[i] = m;
+        if (m) S.plan.done = 0;
+        const int plane = i < S.ns ? S.srch[i].plane : 0, dir = i < S.ns ? S.srch[i].dir : 0;
+        for (int k = 0; k < m; k++) {
+            SvtGpuLfParams q = S.p;
+            set_trial_level(q, plane, dir, S.plan.lv[i][k]);
+            const int  base[3][2] = {{q.filter_level[0], q.filter_level[1]},
+                                     {q.filter_level_u, q.filter_level_u},
+                                     {q.filter_level_v, q.filter_level_v}};
+            const bool on = plane_active(q, plane);
+            for (int d = 0; d < 2; d++) {
+                if (on) fill_level_table(q, plane, d, base[plane][d], S.plan.lvl[i][k][d]);
+                else
+                    for (int c = 0; c < 128; c++) S.plan.lvl[i][k][d][c] = 0;
+            }
+        }
+    }
+}
+
+// one bisection decision per search from the last trial launch's sums (which it re-zeroes), then the next plan
+__global__ void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
+    if (threadIdx.x != 0) return;
+    DlfDevSearch &D = *S;
+    if (D.plan.done) return;
+    for (int i = 0; i < D.ns; i++)
+        if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], sse + i * MAX_TRIALS);
+    for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) sse[q] = 0;
+    plan_next(D);
+}
+
+int dlf_device_chunk() { // (trial, step) pairs per host read-back; 0: the host-driven search
+    static const int k = [] {
+        const char *e = std::getenv("SVTGPU_DLF_DEVICE");
+        return e ? std::max(0, std::min(64, std::atoi(e) == 1 ? 6 : std::atoi(e))) : 0;
+    }();
+    return k;
+}
+
+int run_searches_device(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, const SvtGpuLfParams &p,
+                        LevelSearch *const *srch, int ns, hipStream_t st, int chunk) {
+    if (!s->d_search) {
+        HIP_TRY(hipMalloc(&s->d_search, sizeof(DlfDevSearch)));
+        HIP_TRY(hipHostMalloc(&s->h_search, sizeof(DlfDevSearch), hipHostMallocDefault));
+    }
+    DlfDevSearch &H = *(DlfDevSearch *)s->h_search; // pinned: the caller's previous pick has read it back
+    DlfDevSearch *D = (DlfDevSearch *)s->d_search;
+    for (int i = 0; i < ns; i++) H.srch[i] = *srch[i];
+    H.ns = ns;
+    H.p  = p;
+    plan_next(H);
+    if (!H.plan.done) {
+        HIP_TRY(hipMemcpyAsync(D, &H, sizeof H, hipMemcpyHostToDevice, st));
+        svtgpu_count_xfer(0, sizeof H);
+        LevelTables L;
+        build_level_tables(p, L);
+        DlfTileArgs a = base_args(recon, L);
+        for (int i = 0; i < ns; i++) { // the grid covers MAX_TRIALS levels of every search; the plan says which run
+            const int    plane = srch[i]->plane;
+            DlfPlaneJob &J     = a.job[i];
+            J                  = plane_job(s, recon, plane, true);
+            J.src              = recon->plane[plane];
+            J.src_stride       = recon->stride[plane];
+            J.ref              = src->plane[plane];
+            J.ref_stride       = src->stride[plane];
+            J.ntrial           = MAX_TRIALS;
+        }
+        a.njob = ns;
+        a.sse  = s->d_sse;
+        a.plan = &D->plan;
+        for (int launches = 0;;) {
+            for (int k = 0; k < chunk; k++, launches++) {
+                if (int rc = launch_tile(a, recon->bytes_per_sample, true, st)) return rc;
+                // a picture tiled over GPUs: the frame's SSEs are the sums over the ranks (every rank then takes the
+                // same decision)
+                if (int rc = svtgpu_comm_sum(s->comm, s->d_sse, MAX_JOBS * MAX_TRIALS, true, st)) return rc;
+                hipLaunchKernelGGL(dlf_search_step_kernel, dim3(1), dim3(64), 0, st, D, s->d_sse);
+                HIP_TRY(hipGetLastError());
+            }
+            HIP_TRY(hipMemcpyAsync(&H, D, sizeof H, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            svtgpu_count_xfer(1, sizeof H);
+            if (H.plan.done) break;
+            if (launches >= 1024) return SVTGPU_ERR_HIP; // a level search ends after far fewer trials
+        }
+    }
+    for (int i = 0; i < ns; i++) *srch[i] = H.srch[i];
+    return SVTGPU_OK;
+}
 
 // run searches side by side: each launch evaluates the pending levels of every unfinished search (one plane job
 // each), the SSE of every (job, level) comes back through mapped pinned memory; recon is never modified
@@ -818,6 +941,8 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     (void)hipFree(s->d_sse);
     (void)hipFree(s->d_arrive);
     if (s->h_sse) (void)hipHostFree(s->h_sse);
+    (void)hipFree(s->d_search);
+    if (s->h_search) (void)hipHostFree(s->h_search);
     delete s;
 }
 
@@ -977,7 +1102,10 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
-    if ((rc = run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st))) return rc;
+    const int   chunk  = dlf_device_chunk();
+    if ((rc = chunk ? run_searches_device(s, recon, source, p, all, search_uv ? 3 : 1, st, chunk)
+                    : run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st)))
+        return rc;
     if (s->mi_on_device) { // the grid was checked by the records kernel: its verdict, once the stream has passed it
         s->mi_on_device = 0;
         HIP_TRY(hipStreamSynchronize(st));

@@ -1,0 +1,49 @@
+"""The device-resident DLF level search (SVTGPU_DLF_DEVICE, §8(f) row 2): the FULL_IMAGE bisection of
+search_filter_level (EbDeblockingFilter.c:886-991) decided on the device between trial launches (dlf_search_step_kernel),
+the host reading the state back once per chunk of (trial, step) pairs.  Run on the pipeline goldens whose DLF search
+is the frame bisection (dlf_level 1/2: mini8, mini10, mini10b, mini8c, sb128_10, c3_4k10; every plane's start level,
+luma-only 4x4 transforms, levels near 0 and 63) in a child process (the switch is read once per process), with the
+default chunk and with chunks of 2 and 4 (several read-backs per search): the levels and every output plane
+bit-exact against the reference, like the host-driven search.  The tiled form (two ranks on one GPU, the trial SSEs
+summed over the ranks between the trial and the decision) runs the tiled test's workers with the switch set."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+sys.path[:0] = [%r, %r, %r, %r]
+import torch
+if torch.cuda.is_available():
+    torch.cuda.init()
+import pipeline_run as prun
+for case in %r:
+    prun.check(case, prun.run_gpu(case), "dlf device search")
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk,cases", [
+    ("1", ("mini8", "mini10", "mini10b", "mini8c", "mini10e", "sb128_10", "c3_4k10")),
+    ("2", ("mini10", "mini8c")),
+    ("4", ("c1_1080p8",)),
+])
+def test_dlf_device_search_bit_exact(chunk, cases):
+    code = CHILD % (ROOT, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"), os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "tests"), tuple(cases))
+    # "1" selects the default chunk (6 trial launches per read-back); other values are the chunk itself
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, SVTGPU_DLF_DEVICE=chunk))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_dlf_device_search_tiled_two_ranks(monkeypatch):
+    import test_tiled_gpu
+    monkeypatch.setenv("SVTGPU_DLF_DEVICE", "3")  # inherited by the spawned ranks
+    test_tiled_gpu.test_two_ranks_one_gpu_bit_exact()
