@@ -755,15 +755,28 @@ __host__ __device__ void plan_next(DlfDevSearch &S) {
     }
 }
 
-// one bisection decision per search from the last trial launch's sums (which it re-zeroes), then the next plan
-__global__ void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
-    if (threadIdx.x != 0) return;
-    DlfDevSearch &D = *S;
-    if (D.plan.done) return;
-    for (int i = 0; i < D.ns; i++)
-        if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], sse + i * MAX_TRIALS);
-    for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) sse[q] = 0;
-    plan_next(D);
+// one bisection decision per search from the last trial launch's sums (which it re-zeroes), then the next plan.  The
+// state is copied into LDS by the wave and walked there by one lane (the search is a chain of dependent reads: from
+// global memory each would wait a full memory latency), then written back
+static_assert(sizeof(DlfDevSearch) % 4 == 0, "word copies of the search state");
+__global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
+    constexpr int NW = (int)(sizeof(DlfDevSearch) / 4);
+    __shared__ __align__(16) uint32_t w[NW];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NW; i += 64) w[i] = ((const uint32_t *)S)[i];
+    __syncthreads();
+    DlfDevSearch &D = *(DlfDevSearch *)w;
+    if (D.plan.done) return; // uniform: every lane read the same word
+    if (tid == 0) {
+        unsigned long long v[MAX_JOBS * MAX_TRIALS];
+        for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) v[q] = sse[q];
+        for (int i = 0; i < D.ns; i++)
+            if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], v + i * MAX_TRIALS);
+        plan_next(D);
+    }
+    __syncthreads();
+    if (tid < MAX_JOBS * MAX_TRIALS) sse[tid] = 0;
+    for (int i = tid; i < NW; i += 64) ((uint32_t *)S)[i] = w[i];
 }
 
 int dlf_device_chunk() { // (trial, step) pairs per host read-back; 0: the host-driven search
