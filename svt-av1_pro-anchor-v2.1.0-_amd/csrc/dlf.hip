@@ -538,23 +538,24 @@ __host__ __device__ static inline int clampi(int v, int lo, int hi) { return v <
 
 // the level per (segment, reference, mode) class of one plane and direction whose base level is lv
 // (svt_av1_loop_filter_frame_init, EbDeblockingFilter.c)
-__host__ __device__ static void fill_level_table(const SvtGpuLfParams &p, int pl, int dir, int lv, uint8_t *out) {
+// one (segment, reference, mode) class of it: cls = seg * 16 + ref * 2 + mode
+__host__ __device__ static inline uint8_t level_entry(const SvtGpuLfParams &p, int pl, int dir, int lv, int cls) {
     const int feat[3][2] = {{1, 2}, {3, 3}, {4, 4}}; // SEG_LVL_ALT_LF_{Y_V, Y_H, U, V}
-    for (int seg = 0; seg < 8; seg++) {
-        int ls = lv;
-        if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
-            ls = clampi(ls + p.seg_feature_data[seg][feat[pl][dir]], 0, 63);
-        for (int ref = 0; ref < 8; ref++)
-            for (int mode = 0; mode < 2; mode++) {
-                int v = ls;
-                if (p.mode_ref_delta_enabled) {
-                    const int scale = 1 << (ls >> 5);
-                    v = ls + p.ref_deltas[ref] * scale + (ref > 0 ? p.mode_deltas[mode] * scale : 0);
-                    v = clampi(v, 0, 63);
-                }
-                out[seg * 16 + ref * 2 + mode] = (uint8_t)v;
-            }
+    const int seg = cls >> 4, ref = (cls >> 1) & 7, mode = cls & 1;
+    int       ls  = lv;
+    if (p.segmentation_enabled && p.seg_feature_enabled[seg][feat[pl][dir]])
+        ls = clampi(ls + p.seg_feature_data[seg][feat[pl][dir]], 0, 63);
+    int v = ls;
+    if (p.mode_ref_delta_enabled) {
+        const int scale = 1 << (ls >> 5);
+        v = ls + p.ref_deltas[ref] * scale + (ref > 0 ? p.mode_deltas[mode] * scale : 0);
+        v = clampi(v, 0, 63);
     }
+    return (uint8_t)v;
+}
+
+__host__ __device__ static void fill_level_table(const SvtGpuLfParams &p, int pl, int dir, int lv, uint8_t *out) {
+    for (int cls = 0; cls < 128; cls++) out[cls] = level_entry(p, pl, dir, lv, cls);
 }
 
 void build_level_tables(const SvtGpuLfParams &p, LevelTables &L) {
@@ -731,28 +732,37 @@ struct DlfDevSearch {
     DlfDevPlan     plan;
 };
 
-// the next launch's levels per search and each (search, level)'s tables: that plane's only, as run_searches builds
-__host__ __device__ void plan_next(DlfDevSearch &S) {
+// the next launch's levels per search (the bisection steps), then each (search, level)'s tables: that plane's only, as
+// run_searches builds them (try_filter_frame sets one plane's level; the other levels and the class deltas stay)
+__host__ __device__ void plan_levels(DlfDevSearch &S) {
     S.plan.done = 1;
     for (int i = 0; i < MAX_JOBS; i++) {
         const int m = i < S.ns ? S.srch[i].pending(S.plan.lv[i]) : 0;
         S.plan.ntrial[i] = m;
         if (m) S.plan.done = 0;
-        const int plane = i < S.ns ? S.srch[i].plane : 0, dir = i < S.ns ? S.srch[i].dir : 0;
-        for (int k = 0; k < m; k++) {
-            SvtGpuLfParams q = S.p;
-            set_trial_level(q, plane, dir, S.plan.lv[i][k]);
-            const int  base[3][2] = {{q.filter_level[0], q.filter_level[1]},
-                                     {q.filter_level_u, q.filter_level_u},
-                                     {q.filter_level_v, q.filter_level_v}};
-            const bool on = plane_active(q, plane);
-            for (int d = 0; d < 2; d++) {
-                if (on) fill_level_table(q, plane, d, base[plane][d], S.plan.lvl[i][k][d]);
-                else
-                    for (int c = 0; c < 128; c++) S.plan.lvl[i][k][d][c] = 0;
-            }
-        }
     }
+}
+// table entry e of [MAX_JOBS][MAX_TRIALS][2][128] (entries of levels the plan does not try are left as they are)
+__host__ __device__ inline void plan_table_entry(DlfDevSearch &S, int e) {
+    const int cls = e & 127, d = (e >> 7) & 1, k = (e >> 8) % MAX_TRIALS, i = (e >> 8) / MAX_TRIALS;
+    if (i >= S.ns || k >= S.plan.ntrial[i]) return;
+    const int plane = S.srch[i].plane, lvl = S.plan.lv[i][k];
+    int       l0 = S.p.filter_level[0], l1 = S.p.filter_level[1], lu = S.p.filter_level_u, lvv = S.p.filter_level_v;
+    if (plane == 0) { // set_trial_level
+        if (S.srch[i].dir != 1) l0 = lvl;
+        if (S.srch[i].dir != 0) l1 = lvl;
+    } else if (plane == 1)
+        lu = lvl;
+    else
+        lvv = lvl;
+    const bool on   = plane == 0 ? (l0 || l1) : plane == 1 ? lu != 0 : lvv != 0; // plane_active
+    const int  base = plane == 0 ? (d == 0 ? l0 : l1) : plane == 1 ? lu : lvv;
+    S.plan.lvl[i][k][d][cls] = on ? level_entry(S.p, plane, d, base, cls) : 0;
+}
+constexpr int PLAN_ENTRIES = MAX_JOBS * MAX_TRIALS * 2 * 128;
+void plan_next(DlfDevSearch &S) { // host
+    plan_levels(S);
+    for (int e = 0; e < PLAN_ENTRIES; e++) plan_table_entry(S, e);
 }
 
 // one bisection decision per search from the last trial launch's sums (which it re-zeroes), then the next plan.  The
@@ -772,8 +782,10 @@ __global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, un
         for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) v[q] = sse[q];
         for (int i = 0; i < D.ns; i++)
             if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], v + i * MAX_TRIALS);
-        plan_next(D);
+        plan_levels(D);
     }
+    __syncthreads();
+    for (int e = tid; e < PLAN_ENTRIES; e += 64) plan_table_entry(D, e); // the tables: one entry per lane and pass
     __syncthreads();
     if (tid < MAX_JOBS * MAX_TRIALS) sse[tid] = 0;
     for (int i = tid; i < NW; i += 64) ((uint32_t *)S)[i] = w[i];
