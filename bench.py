@@ -108,7 +108,7 @@ def parse():
     ap.add_argument("--cdef-level", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no device-clock timing inside the LR search")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03", "pmc", "kernels.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04", "pmc", "kernels.json"),
                     help="per-launch traffic / VALU counters from scripts/pmc_traffic.sh (PMC passes cannot run inside "
                          "the bench)")
     ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
@@ -730,8 +730,10 @@ def main():
     ms_per_step = dt * 1e3 / a.steps
     frames_per_step = F * (1 if tiled else n)  # frames split: every rank filters F frames per step
     value = frames_per_step * W * H / (ms_per_step * 1e-3) / 1e6  # the whole job's luma pixels per second
-    lr_cls = {c: {k: lr_tot[c][k] / max(lr_tot["searches"], 1) if lr_tot else 0.0 for k in ("launches", "ms", "bytes")}
-              for c in svtgpu.LrState.PROFILE_CLASSES}
+    def lr_classes(tot):
+        return {c: {k: tot[c][k] / max(tot["searches"], 1) if tot else 0.0 for k in ("launches", "ms", "bytes")}
+                for c in svtgpu.LrState.PROFILE_CLASSES}
+    lr_cls = lr_classes(lr_tot)
     # SURVEY §8(d) algorithmic bytes; per rank: its share of the frame (tiles)
     S_samples = 1.5 * W * H
     B = 2 if bd > 8 else 1
@@ -745,21 +747,53 @@ def main():
     nsb = ((W + 63) // 64) * ((H + 63) // 64)
     nsb_mine = slots[0].md_range[1] - slots[0].md_range[0]
     cdef_alg = 2 * SB + nfb_mine * (2 * 64 * 8 + 64 + 64 * 4 + 1)
-    kernels = {"cdef_search_kernel": dict(ms=search_ms, launches=1, alg_bytes=cdef_alg,
-                                          what="recon + source read once, 2*S*B, + the per-FB mse/dir/var/skip outputs")}
-    if a.stages == "all":
-        kernels["md_dist_kernel"] = dict(ms=md_ms, launches=1, alg_bytes=nsb_mine * (1 + NREF) * 64 * 64 * B,
-                                         what="(1 + refs) x 64 x 64 x B per superblock")
-        if lr_tot:
-            lr_kern = {"wiener_trials": ("wiener_res_kernel", 2 * SB, "the CDEF output and source of the searched "
-                                                                      "planes read once, 2*S*B"),
-                       "sgr_filters": ("sgr_flt_kernel", SB, "the CDEF output read once, S*B"),
-                       "projection": ("sgr_res_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
-            for cls, (kn, alg, what) in lr_kern.items():
-                c = lr_cls[cls]
-                if c["launches"] > 0:
-                    kernels[kn] = dict(ms=c["ms"], launches=c["launches"], alg_bytes=alg, what=what)
-    roof = roofline_of(kernels, bd, a.pmc_json)
+
+    def kernel_table(search_ms_, md_ms_, lr_cls_, have_lr):
+        kernels = {"cdef_search_kernel": dict(ms=search_ms_, launches=1, alg_bytes=cdef_alg,
+                                              what="recon + source read once, 2*S*B, + the per-FB mse/dir/var/skip "
+                                                   "outputs")}
+        if a.stages == "all":
+            kernels["md_dist_kernel"] = dict(ms=md_ms_, launches=1, alg_bytes=nsb_mine * (1 + NREF) * 64 * 64 * B,
+                                             what="(1 + refs) x 64 x 64 x B per superblock")
+            if have_lr:
+                lr_kern = {"wiener_trials": ("wiener_res_kernel", 2 * SB, "the CDEF output and source of the searched "
+                                                                          "planes read once, 2*S*B"),
+                           "sgr_filters": ("sgr_flt_kernel", SB, "the CDEF output read once, S*B"),
+                           "projection": ("sgr_res_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
+                for cls, (kn, alg, what) in lr_kern.items():
+                    c = lr_cls_[cls]
+                    if c["launches"] > 0:
+                        kernels[kn] = dict(ms=c["ms"], launches=c["launches"], alg_bytes=alg, what=what)
+        return kernels
+    kernels_f = kernel_table(search_ms, md_ms, lr_cls, bool(lr_tot))
+    # The roofline's durations come from the condition its PMC counters were collected in: one frame in flight
+    # (scripts/pmc_r04.sh runs the bench at F = 1).  With F > 1 slot 0 runs alone for a short timed phase after the
+    # main one; the contended figures of the F-frame run are reported beside it.
+    iso = None
+    if F > 1:
+        s0 = slots[0]
+        s0.ev = []
+        lr.profile(not a.no_kernel_timing)
+        iso_steps = max(10, min(a.steps, 40))
+        torch.cuda.synchronize()
+        for _ in range(iso_steps):
+            s0.step(True)
+        torch.cuda.synchronize()
+        iso_tot = lr.profile(False) if not a.no_kernel_timing else None
+        iso_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])]
+                          for es in s0.ev], axis=0)
+        iso = dict(steps=iso_steps, frame_ms=float(np.mean([es[0].elapsed_time(es[5]) for es in s0.ev])),
+                   kernels=kernel_table(float(iso_ms[1]), float(iso_ms[4]), lr_classes(iso_tot), bool(iso_tot)))
+    roof = roofline_of(iso["kernels"] if iso else kernels_f, bd, a.pmc_json)
+    roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run; the PMC counters' "
+                         "condition)" % iso["steps"]) if iso else "one frame in flight (the main run)"
+    if iso:
+        cont = roofline_of(kernels_f, bd, a.pmc_json)
+        roof["contended"] = {"frames_in_flight": F, "kernel": cont["kernel"], "avg_launch_ms": cont["avg_launch_ms"],
+                             "ms_per_frame": cont["ms_per_frame"], "achieved": cont["achieved"], "frac": cont["frac"],
+                             "all_kernels_ms_per_frame": cont["all_kernels_ms_per_frame"],
+                             "note": "the same accounting over the main run's %d frames in flight: kernels share the "
+                                     "CUs with the other frames' kernels, so launch durations include queueing" % F}
     # SURVEY §8(d) algorithmic bytes per frame by stage, over slot 0's stage times (HIP events; with several frames in
     # flight the stages share the device with the other frames), and the pipeline total over the wall time per frame
     stage_bytes = {"dlf_pick_filter": 2 * SB, "cdef_search": cdef_alg, "cdef_pick_apply": 2 * SB,

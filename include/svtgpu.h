@@ -174,6 +174,10 @@ typedef struct SvtGpuTilePlan {
 } SvtGpuTilePlan;
 int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy, int32_t rank,
                      SvtGpuTilePlan *out);
+/* The same for a picture of sb_size (64 or 128) superblocks: with 128 the tile edges are also multiples of 128, so no
+ * 128x128 CDEF area is cut (svtgpu_tile_plan = sb_size 64). */
+int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t unit_size[3], int32_t sb_size, int32_t gx,
+                        int32_t gy, int32_t rank, SvtGpuTilePlan *out);
 
 /* ---------------------------------------------------------------------------------------------
  * CDEF — per-block RTCD shims (host pointers, synchronous)
@@ -299,15 +303,16 @@ int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, S
 int svtgpu_cdef_set_fb_rows(SvtGpuCdefFrameState *s, int32_t fb_row_begin, int32_t fb_row_end);
 /* A picture tiled over GPUs (svtgpu_tile_plan): the search covers the filter blocks of fb_rect = {col0, row0, col1,
  * row1} only and leaves zeros elsewhere in the tables; svtgpu_cdef_pick first sums the mse / skip / dir / var tables
- * over `comm` (one contributor per entry: the gather of every rank's blocks; the pick is then the same on every rank);
- * the apply writes only the luma rectangle out_rect = {x0, y0, x1, y1} (chroma halved, rounded outward), reading
+ * over `comm` (one contributor per entry: the gather of every rank's blocks; the pick is then the same on every rank;
+ * the sums run once per search: a second pick on the same search reads the gathered tables); the apply writes only the luma rectangle out_rect = {x0, y0, x1, y1} (chroma halved, rounded outward), reading
  * the DLF output 2 samples around it.  NULL rects: the whole frame; NULL comm: no exchange. */
 int svtgpu_cdef_set_tile(SvtGpuCdefFrameState *s, const int32_t fb_rect[4], const int32_t out_rect[4],
                          SvtGpuComm *comm);
 /* Use caller-owned device memory for the search tables: mse [2][nfb][64] uint64 and skip [nfb] uint8
  * (e.g. buffers all-reduced with RCCL between the search and the pick).  NULL, NULL restores the
  * state's own buffers.  svtgpu_cdef_clear_tables zeroes both (a band search then leaves zeros —
- * the identity of an all-reduce-sum — outside its rows). */
+ * the identity of an all-reduce-sum — outside its rows).  The library touches exactly nfb bytes of a
+ * bound skip table (the tiled pick sums it through a padded copy of its own). */
 int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, void *skip_dev);
 /* The same for the per-8x8 direction/variance tables the apply reuses: dir [nfb][64] uint8, var [nfb][64]
  * int32 (zero outside a band after svtgpu_cdef_clear_tables, so an all-reduce-sum completes them and every
@@ -404,7 +409,8 @@ int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stre
 /* the same from a grid already in device memory (`d_mi`, same layout; e.g. written by a device mode decision):
  * copied in stream order (the caller may overwrite `d_mi` once `stream` has passed this call), no host pass and no
  * PCIe.  The records kernel checks the fields; a grid with records out of range is clamped and reported as
- * SVTGPU_ERR_INVALID_ARG by the next svtgpu_dlf_pick. */
+ * SVTGPU_ERR_INVALID_ARG by the next svtgpu_dlf_pick, or by the next svtgpu_dlf_frame(_to) when no pick ran (the
+ * FROM_Q levels); each upload is judged on its own. */
 int svtgpu_dlf_set_mode_info_device(SvtGpuDlfState *s, const SvtGpuLfMi *d_mi, void *stream);
 /* ≙ svt_av1_loop_filter_frame(frame, pcs, plane_start, plane_end) (EbDeblockingFilter.c:624-653):
  * all vertical edges of each plane, then all horizontal edges (equivalent to the reference's

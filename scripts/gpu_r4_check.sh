@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-4 check: the new tiled / RCCL tests first (world 2, 4, 8 on one GPU; one-rank RCCL), then the whole -m gpu
+# suite, smoke() and the default bench, into gpurun_out/$1.  Every GPU step under its own time limit; stop at the
+# first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/${1:-r4check}
+mkdir -p $O
+export TMPDIR=/tmp
+T="python -u -m pytest -x -v --timeout 250 --timeout-method thread"
+[ -n "$SKIP_TILED" ] || timeout -k 10 900 $T tests/test_tiled_gpu.py -m gpu > $O/tiled.log 2>&1 || { echo "tiled failed"; tail -40 $O/tiled.log; exit 1; }
+[ -n "$SKIP_TILED" ] || grep -E "passed|failed" $O/tiled.log | tail -1
+if [ -z "$QUICK" ]; then
+timeout -k 10 1000 $T tests -m gpu --deselect tests/test_tiled_gpu.py > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+grep -E "passed|failed" $O/pytest.log | tail -1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py --no-matrix > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["ms_per_step"], r["kernel"], r["avg_launch_ms"], r["frac"], r.get("contended", {}).get("kernel"), d["cpu_baseline"]["value"] if d.get("cpu_baseline") else None)'
+fi
+echo done

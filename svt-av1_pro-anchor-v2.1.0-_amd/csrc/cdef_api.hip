@@ -140,6 +140,9 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
     HIP_TRY(hipMemset(s->d_pick_xch, 0, SVTGPU_PICK_XCH_BYTES)); // no word carries a valid tag
     HIP_TRY(hipMemset(s->d_skip, 0, (nfb + 7) & ~(size_t)7)); // the padding stays 0 (the tables' word sums)
     HIP_TRY(hipMemset(s->d_skip, 1, nfb));
+    // the memsets above run on the null stream: done before any call on the caller's (non-blocking) streams, whose
+    // first search may clear these tables
+    HIP_TRY(hipStreamSynchronize(nullptr));
     s->own_mse      = s->d_mse;
     s->own_skip     = s->d_skip;
     s->own_dir      = s->d_dir;
@@ -208,10 +211,12 @@ extern "C" int svtgpu_cdef_clear_tables(SvtGpuCdefFrameState *s, void *stream) {
     if (!s)
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
+    // exactly nfb skip bytes: a bound skip table is [nfb] (svtgpu.h); the state's own copy keeps its zero padding
     HIP_TRY(hipMemsetAsync(s->d_mse, 0, (size_t)s->nfb * 2 * 64 * 8, st));
-    HIP_TRY(hipMemsetAsync(s->d_skip, 0, ((size_t)s->nfb + 7) & ~(size_t)7, st));
+    HIP_TRY(hipMemsetAsync(s->d_skip, 0, (size_t)s->nfb, st));
     HIP_TRY(hipMemsetAsync(s->d_dir, 0, (size_t)s->nfb * 64, st));
     HIP_TRY(hipMemsetAsync(s->d_var, 0, (size_t)s->nfb * 64 * 4, st));
+    s->gathered = 0;
     return SVTGPU_OK;
 }
 
@@ -283,8 +288,9 @@ extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFra
     CdefStrengthTable tab;
     hipStream_t       st = pick_stream(s->ctx, stream);
     // tiled over GPUs: zeros outside this rank's filter blocks, so the pick's word sums over the ranks gather the tables
-    if (s->comm && svtgpu_comm_nranks(s->comm) > 1)
+    if (svtgpu_comm_tiled(s->comm))
         if (int rc = svtgpu_cdef_clear_tables(s, st)) return rc;
+    s->gathered = 0; // this rank's blocks only until the next pick sums them
     if (ctrls->use_reference_cdef_fs) { // directions / variances only: an empty strength table
         memset(&tab, 0, sizeof(tab));
         return svtgpu_launch_cdef_search(s, recon, source, &tab, ctrls->subsampling_factor, 3 + (base_q_idx >> 6), st);
@@ -305,14 +311,21 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
     if (!s || !ctrls || !params_out || !valid_controls(ctrls))
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
-    if (s->comm && svtgpu_comm_nranks(s->comm) > 1) { // the ranks' search tables (zero elsewhere) summed = gathered
+    // the ranks' search tables (zero elsewhere) summed = gathered; once per search, so a second pick on the same
+    // search (another level, another lambda) reads the gathered tables instead of summing them again
+    if (svtgpu_comm_tiled(s->comm) && !s->gathered) {
         const size_t nfb = s->nfb;
         if (int rc = svtgpu_comm_sum(s->comm, s->d_dir, nfb * 64 / 8, true, st)) return rc;
         if (int rc = svtgpu_comm_sum(s->comm, s->d_var, nfb * 64 * 4 / 8, true, st)) return rc;
         if (!ctrls->use_reference_cdef_fs) {
             if (int rc = svtgpu_comm_sum(s->comm, s->d_mse, nfb * 2 * 64, true, st)) return rc;
-            if (int rc = svtgpu_comm_sum(s->comm, s->d_skip, (nfb + 7) / 8, true, st)) return rc;
+            // word sums over the state's padded copy: a bound table is exactly [nfb] bytes
+            const size_t words = (nfb + 7) / 8;
+            if (s->d_skip != s->own_skip) HIP_TRY(hipMemcpyAsync(s->own_skip, s->d_skip, nfb, hipMemcpyDeviceToDevice, st));
+            if (int rc = svtgpu_comm_sum(s->comm, s->own_skip, words, true, st)) return rc;
+            if (s->d_skip != s->own_skip) HIP_TRY(hipMemcpyAsync(s->d_skip, s->own_skip, nfb, hipMemcpyDeviceToDevice, st));
         }
+        s->gathered = 1;
     }
     if (ctrls->use_reference_cdef_fs) { // EbEncCdef.c:744-789: index 0 for every filter block, one pair
         memset(params_out, 0, sizeof(*params_out));

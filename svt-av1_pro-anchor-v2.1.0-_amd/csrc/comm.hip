@@ -98,12 +98,15 @@ extern "C" void svtgpu_comm_destroy(SvtGpuComm *c) {
 }
 
 extern "C" int32_t svtgpu_comm_nranks(const SvtGpuComm *c) { return c ? c->nranks : 0; }
+bool svtgpu_comm_tiled(const SvtGpuComm *c) { return c && (c->nranks > 1 || !c->is_host); }
 extern "C" int32_t svtgpu_comm_rank(const SvtGpuComm *c) { return c ? c->rank : -1; }
 
 // The element-wise sum of n uint64 over the ranks, in place.  Device buffers: enqueued on `st` (RCCL) or staged through
 // host memory with a synchronization (host transport).  Host buffers: synchronous either way.
+// A one-rank host transport is the identity and returns at once; a one-rank RCCL communicator still runs the
+// collective (the same code path, transfers and stream ordering as the N-GPU run).
 int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st) {
-    if (!c || c->nranks == 1 || n == 0) return SVTGPU_OK;
+    if (!c || n == 0 || (c->nranks == 1 && c->is_host)) return SVTGPU_OK;
     if (!buf) return SVTGPU_ERR_INVALID_ARG;
     if (c->is_host) {
         uint64_t *h = (uint64_t *)buf;
@@ -117,7 +120,10 @@ int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStrea
             svtgpu_set_last_hip_error(hipErrorUnknown, "host transport all-reduce failed", __FILE__, __LINE__);
             return SVTGPU_ERR_HIP;
         }
-        if (on_device) HIP_TRY(hipMemcpyAsync(buf, c->pin, n * 8, hipMemcpyHostToDevice, st));
+        if (on_device) { // the pinned staging is reused by the next sum, maybe from another stream: wait for the copy
+            HIP_TRY(hipMemcpyAsync(buf, c->pin, n * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
         return SVTGPU_OK;
     }
     void *d = buf;
@@ -153,10 +159,10 @@ void grow(int32_t *r, int a, int w, int h) {
 }
 } // namespace
 
-extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy,
-                                int32_t rank, SvtGpuTilePlan *out) {
+extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t unit_size[3], int32_t sb_size,
+                                   int32_t gx, int32_t gy, int32_t rank, SvtGpuTilePlan *out) {
     if (!unit_size || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7) || gx < 1 || gy < 1 ||
-        rank < 0 || rank >= gx * gy)
+        rank < 0 || rank >= gx * gy || (sb_size != 64 && sb_size != 128))
         return SVTGPU_ERR_INVALID_ARG;
     for (int p = 0; p < 3; p++)
         if (unit_size[p] < (p ? 32 : 64) || unit_size[p] > 256 || (unit_size[p] & (unit_size[p] - 1)))
@@ -165,9 +171,12 @@ extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t uni
     std::memset(&o, 0, sizeof o);
     const int tx = rank % gx, ty = rank / gx, U = unit_size[0];
     const int nux = units_of(U, width), nuy = units_of(U, height);
-    if (nux < gx || nuy < gy) return SVTGPU_ERR_INVALID_ARG; // a rank without a unit
-    const int c0 = split_at(nux, gx, tx), c1 = split_at(nux, gx, tx + 1);
-    const int r0 = split_at(nuy, gy, ty), r1 = split_at(nuy, gy, ty + 1);
+    // tile edges on the unit grid and on the superblock grid: with 64-sample units in a SB128 picture the units go in
+    // pairs, so no 128x128 CDEF area (searched as one, EbCdefProcess.c:193-196) is cut
+    const int k = std::max(1, sb_size / U), gux = (nux + k - 1) / k, guy = (nuy + k - 1) / k;
+    if (gux < gx || guy < gy) return SVTGPU_ERR_INVALID_ARG; // a rank without a unit
+    const int c0 = std::min(nux, k * split_at(gux, gx, tx)), c1 = std::min(nux, k * split_at(gux, gx, tx + 1));
+    const int r0 = std::min(nuy, k * split_at(guy, gy, ty)), r1 = std::min(nuy, k * split_at(guy, gy, ty + 1));
     // the tile: unit-grid edges (multiples of 64: filter-block edges too); the frame edge closes the last tile
     o.tile[0] = c0 * U, o.tile[1] = r0 * U;
     o.tile[2] = c1 == nux ? width : c1 * U, o.tile[3] = r1 == nuy ? height : r1 * U;
@@ -205,4 +214,9 @@ extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t uni
     std::memcpy(o.dlf_out, d, sizeof d);
     *out = o;
     return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy,
+                                int32_t rank, SvtGpuTilePlan *out) {
+    return svtgpu_tile_plan_sb(width, height, unit_size, 64, gx, gy, rank, out);
 }

@@ -799,8 +799,8 @@ int dlf_device_chunk() { // (trial, step) pairs per host read-back; 0: the host-
     return k;
 }
 
-int run_searches_device(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, const SvtGpuLfParams &p,
-                        LevelSearch *const *srch, int ns, hipStream_t st, int chunk) {
+int run_searches_device_body(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src,
+                             const SvtGpuLfParams &p, LevelSearch *const *srch, int ns, hipStream_t st, int chunk) {
     if (!s->d_search) {
         HIP_TRY(hipMalloc(&s->d_search, sizeof(DlfDevSearch)));
         HIP_TRY(hipHostMalloc(&s->h_search, sizeof(DlfDevSearch), hipHostMallocDefault));
@@ -843,11 +843,23 @@ int run_searches_device(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGp
             HIP_TRY(hipStreamSynchronize(st));
             svtgpu_count_xfer(1, sizeof H);
             if (H.plan.done) break;
-            if (launches >= 1024) return SVTGPU_ERR_HIP; // a level search ends after far fewer trials
+            if (launches >= 1024) { // a level search ends after far fewer trials
+                svtgpu_set_last_hip_error(hipErrorUnknown, "dlf device level search: no convergence after 1024 trials",
+                                          __FILE__, __LINE__);
+                return SVTGPU_ERR_HIP;
+            }
         }
     }
     for (int i = 0; i < ns; i++) *srch[i] = H.srch[i];
     return SVTGPU_OK;
+}
+
+// the device search; on any error exit the trial accumulators are zeroed again (the next pick assumes them zero)
+int run_searches_device(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src, const SvtGpuLfParams &p,
+                        LevelSearch *const *srch, int ns, hipStream_t st, int chunk) {
+    const int rc = run_searches_device_body(s, recon, src, p, srch, ns, st, chunk);
+    if (rc) (void)hipMemsetAsync(s->d_sse, 0, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS, st);
+    return rc;
 }
 
 // run searches side by side: each launch evaluates the pending levels of every unfinished search (one plane job
@@ -1026,6 +1038,8 @@ extern "C" int svtgpu_dlf_set_mode_info_device(SvtGpuDlfState *s, const SvtGpuLf
     // by the records kernel itself -- no host pass over the records, no PCIe
     HIP_TRY(hipMemcpyAsync(s->d_mi, d_mi, (size_t)s->mi_rows * s->mi_cols * sizeof(SvtGpuLfMi),
                            hipMemcpyDeviceToDevice, st));
+    // this grid's verdict only: the flag word (mapped memory) is cleared in stream order before its records kernel
+    HIP_TRY(hipMemsetAsync(s->h_sse_dev + MAX_JOBS * MAX_TRIALS + 1, 0, sizeof(unsigned long long), st));
     s->mi_on_device = 1;
     return edge_records(s, st, s->h_sse_dev + MAX_JOBS * MAX_TRIALS + 1);
 }
@@ -1049,6 +1063,11 @@ namespace {
 // filter planes [ps, pe) of `in` into `out`; in == out is allowed (the plane is staged in scratch)
 int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
                    int32_t ps, int32_t pe, hipStream_t st) {
+    if (s->mi_on_device) { // a device grid no pick has reported on (the FROM_Q levels): its verdict first
+        s->mi_on_device = 0;
+        HIP_TRY(hipStreamSynchronize(st));
+        if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
+    }
     LevelTables L;
     build_level_tables(*params, L);
     bool luma_off = false;

@@ -312,6 +312,7 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
     }
     e = hipMalloc(&s->d_units[0], sizeof(SvtGpuRestUnit) * nu);
     if (e == hipSuccess) e = hipMemset(s->d_units[0], 0, sizeof(SvtGpuRestUnit) * nu);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) s->d_units[0] = nullptr;
     for (int p = 1; p < 3 && s->d_units[0]; p++) s->d_units[p] = s->d_units[p - 1] + s->hunits[p - 1] * s->vunits[p - 1];
     if (e != hipSuccess) {

@@ -2594,7 +2594,7 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
     hipStream_t st      = pick_stream(s->ctx, stream);
     const int   nplanes = searched_planes(ctrls);
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
-    if (!s->comm || svtgpu_comm_nranks(s->comm) == 1) {
+    if (!svtgpu_comm_tiled(s->comm)) {
         int32_t rb[3] = {0, 0, 0}, re[3] = {s->vunits[0], s->vunits[1], s->vunits[2]};
         int32_t cb[3] = {0, 0, 0}, ce[3] = {s->hunits[0], s->hunits[1], s->hunits[2]};
         return recon->bytes_per_sample == 2

@@ -514,6 +514,7 @@ extern "C" int svtgpu_md_batch_create(SvtGpuContext *ctx, int32_t width, int32_t
     hipError_t   e   = hipMalloc(&b->d_mv, nsb * nref * 2 * sizeof(int16_t));
     if (e == hipSuccess) e = hipMalloc(&b->d_out, nsb * nref * 3 * kBlocks * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(b->d_mv, 0, nsb * nref * 2 * sizeof(int16_t));
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) {
         svtgpu_md_batch_destroy(b);
         svtgpu_set_last_hip_error(e, "md batch alloc", __FILE__, __LINE__);

@@ -288,6 +288,7 @@ extern "C" int svtgpu_me_batch_create(SvtGpuContext *ctx, int32_t width, int32_t
     if (e == hipSuccess) e = hipMalloc(&b->d_sad, n * kOut * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMalloc(&b->d_mv, n * kOut * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(b->d_origin, 0, n * 2 * sizeof(int16_t));
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) {
         svtgpu_me_batch_destroy(b);
         svtgpu_set_last_hip_error(e, "me batch alloc", __FILE__, __LINE__);

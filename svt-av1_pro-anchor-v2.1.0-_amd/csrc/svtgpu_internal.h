@@ -97,8 +97,9 @@ struct SvtGpuCdefFrameState {
     int32_t        fb_rect[4];    // {col0, row0, col1, row1}: the filter blocks searched (tiling over GPUs)
     int32_t        out_rect[4];   // {x0, y0, x1, y1} luma: the samples the apply writes (tiling over GPUs)
     SvtGpuComm    *comm;          // the pick's exchange of the search tables (tiling over GPUs; null: none)
+    int32_t        gathered;      // the tables already hold every rank's blocks (summed since the last search)
     uint64_t      *own_mse;       // state-owned tables (d_mse/d_skip may point at caller memory)
-    uint8_t       *own_skip;
+    uint8_t       *own_skip;      // [nfb rounded up to 8]: the padding stays 0 (the skip table's word sums)
     uint8_t       *own_dir;       // state-owned dir/var (d_dir/d_var may point at caller memory)
     int32_t       *own_var;
     int8_t        *d_fb_kind;     // [nfb] SB128 areas (cdef_sb128.hip); null = SB64
@@ -149,6 +150,8 @@ int svtgpu_stats_unit_mfma16(int win, const uint16_t *dgd, const uint16_t *src, 
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st);
 // element-wise sum of n uint64 over the ranks of `c` (comm.hip); nullptr or a one-rank comm: nothing to do
 int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st);
+// the tiled (gather) path runs: a comm of several ranks, or a one-rank RCCL comm (the N-GPU code path on one device)
+bool svtgpu_comm_tiled(const SvtGpuComm *c);
 // host <-> device bytes of the frame-level entry points (copies and mapped-memory results), for the bench's report
 void svtgpu_count_xfer(int d2h, size_t bytes);
 SvtGpuContext *svtgpu_default_context();

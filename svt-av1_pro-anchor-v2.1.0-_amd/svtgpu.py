@@ -354,6 +354,7 @@ _SIGS = {
     "svtgpu_comm_rank": (_I32, [_P]),
     "svtgpu_comm_allreduce_u64": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _I32, _P]),
     "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
+    "svtgpu_tile_plan_sb": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_lr_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
@@ -485,10 +486,10 @@ def tile_grid(n):
     return gx, n // gx
 
 
-def tile_plan(width, height, unit_size, gx, gy, rank):
+def tile_plan(width, height, unit_size, gx, gy, rank, sb=64):
     us = np.ascontiguousarray(unit_size, np.int32)
     t = TilePlan()
-    check(lib().svtgpu_tile_plan(width, height, ptr(us), gx, gy, rank, ctypes.byref(t)))
+    check(lib().svtgpu_tile_plan_sb(width, height, ptr(us), sb, gx, gy, rank, ctypes.byref(t)))
     return t
 
 
@@ -546,6 +547,10 @@ class Comm:
         a = np.ascontiguousarray(words, np.uint64)
         check(lib().svtgpu_comm_allreduce_u64(self.h, ptr(a), a.size, 0, stream))
         return a
+
+    def allreduce_device(self, dev_ptr, n, stream=None):
+        """Sum n uint64 words of device memory over the ranks in place (enqueued on `stream`)."""
+        check(lib().svtgpu_comm_allreduce_u64(self.h, ctypes.c_void_p(dev_ptr), n, 1, stream))
 
     def close(self):
         if self.h:

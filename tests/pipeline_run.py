@@ -300,7 +300,7 @@ def run_gpu_tiled(case, rank, world, comm, ctx=None):
     bd, w, h = c["bd"], c["w"], c["h"]
     us = [c["us"][0], c["us"][1], c["us"][1]]
     gx, gy = svtgpu.tile_grid(world)
-    plan = svtgpu.tile_plan(w, h, us, gx, gy, rank).rects()
+    plan = svtgpu.tile_plan(w, h, us, gx, gy, rank, sb=c["sb"]).rects()
     ctx = ctx or svtgpu.Context()
     S, R, D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(5))
     S.upload(src)

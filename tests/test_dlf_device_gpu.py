@@ -43,7 +43,9 @@ def test_dlf_device_search_bit_exact(chunk, cases):
 
 
 @pytest.mark.gpu
-def test_dlf_device_search_tiled_two_ranks(monkeypatch):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_dlf_device_search_tiled(monkeypatch, world):
     import test_tiled_gpu
     monkeypatch.setenv("SVTGPU_DLF_DEVICE", "3")  # inherited by the spawned ranks
-    test_tiled_gpu.test_two_ranks_one_gpu_bit_exact()
+    test_tiled_gpu.test_ranks_one_gpu_bit_exact(world)

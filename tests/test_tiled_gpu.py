@@ -1,13 +1,19 @@
 """A picture tiled over ranks (BASELINE.json config 4) on the device path, bit-exact.
 
-Two processes (torch.distributed gloo, world size 2) share the one GPU of the test box; each runs the whole
-pipeline of a case on its tile through the library's frame-level calls with a host-transport communicator
-(svtgpu.Comm.host over gloo: RCCL needs one rank per device), so every exchange goes through the C ABI:
-the DLF trial SSEs before each bisection step, the CDEF search tables before the pick, the LR search records
-before the finish.  The ranks' crops (DLF output over each tile, CDEF and LR outputs over each rank's LR
-units) are assembled on rank 0 and compared with the reference's outputs of the case, digests included for
-the 4K 10-bit bench configuration (tests/golden/pipe_c3_4k10.npz) — the same check as the one-rank run.
-A one-rank RCCL communicator is exercised on its own (the 8-GPU path of bench.py)."""
+World sizes 2, 4 and 8 (svtgpu.tile_grid: 1 x 2, 2 x 2 and the 2 x 4 grid of the 8-GPU run): that many processes
+(torch.distributed gloo) share the one GPU of the test box; each runs the whole pipeline of a case on its tile through
+the library's frame-level calls with a host-transport communicator (svtgpu.Comm.host over gloo: RCCL needs one rank
+per device), so every exchange goes through the C ABI: the DLF trial SSEs before each bisection step, the CDEF search
+tables before the pick, the LR search records before the finish.  The ranks' crops (DLF output over each tile, CDEF
+and LR outputs over each rank's LR units) are assembled on rank 0 and compared with the reference's outputs of the
+case, digests included for the 4K 10-bit bench configuration (tests/golden/pipe_c3_4k10.npz) — the same check as the
+one-rank run.  The cases are chosen so that tile columns cross the frame at 64-sample edges that are not multiples of
+128 (mini10b, mini10e, mini8c), at 128 in a SB128 picture (sb128_10) and at 1792 / 1024 in the 4K / 1080p bench
+pictures; the rows at 64-sample steps (mini8c at 2 x 4).
+
+The RCCL transport runs too: a one-rank RCCL communicator takes the tiled path (svtgpu_comm_tiled) with every
+exchange an ncclAllReduce — host buffers (DLF trial SSEs, LR records) and device buffers (CDEF tables) — on the whole
+pipeline of the 4K bench case; the 8-GPU bench runs exactly these calls."""
 import os
 import socket
 
@@ -15,9 +21,14 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
+import pipeline_cases as pc
 import pipeline_run as prun
 
-CASES = ["mini10", "sb128_10", "c3_4k10"]
+WORLD_CASES = {
+    2: ["mini10", "sb128_10", "c3_4k10"],
+    4: ["mini10b", "mini10e", "sb128_10", "sbdlf8_key", "c3_4k10"],
+    8: ["mini8c", "c1_1080p8", "c3_4k10"],
+}
 
 
 def _free_port():
@@ -26,7 +37,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, cases, q):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -42,7 +53,7 @@ def _worker(rank, world, port, q):
 
         comm = svtgpu.Comm.host(world, rank, allreduce)
         ctx = svtgpu.Context(0)
-        for case in CASES:
+        for case in cases:
             part = prun.run_gpu_tiled(case, rank, world, comm, ctx)
             parts = [None] * world
             dist.all_gather_object(parts, part)
@@ -52,6 +63,7 @@ def _worker(rank, world, port, q):
                     q.put((case, "ok"))
                 except AssertionError as e:
                     q.put((case, "FAIL: %s" % str(e)[:2000]))
+            print("rank %d/%d: %s done" % (rank, world, case), flush=True)
         comm.close()
     except BaseException as e:  # reported to the parent
         q.put(("rank %d" % rank, "ERROR: %r" % e))
@@ -61,16 +73,19 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_two_ranks_one_gpu_bit_exact():
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ranks_one_gpu_bit_exact(world):
+    cases = WORLD_CASES[world]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = []
     try:
-        while len(res) < len(CASES):
+        while len(res) < len(cases):
             item = q.get(timeout=300)
             res.append(item)
             assert not item[1].startswith("ERROR"), item
@@ -84,13 +99,96 @@ def test_two_ranks_one_gpu_bit_exact():
     assert all(p.exitcode == 0 for p in procs)
 
 
-@pytest.mark.gpu
-def test_rccl_one_rank_comm():
-    """svtgpu_comm_create (RCCL) with one rank: the sums are the identity, and the tiled calls accept it."""
+def test_world_cases_cross_tile_columns():
+    """CPU check of the case choice: every listed world really cuts the case into its grid, and the grids include
+    column edges off the 128-sample grid."""
+    import svtgpu
+    off128 = False
+    for world, cases in WORLD_CASES.items():
+        gx, gy = svtgpu.tile_grid(world)
+        for case in cases:
+            c = pc.CASES[case]
+            us = [c["us"][0], c["us"][1], c["us"][1]]
+            plans = [svtgpu.tile_plan(c["w"], c["h"], us, gx, gy, r, sb=c["sb"]).rects() for r in range(world)]
+            xs = sorted({p["tile"][0] for p in plans})
+            assert len(xs) == gx and len({p["tile"][1] for p in plans}) == gy, (world, case)
+            off128 |= any(x % 128 for x in xs)
+            if c["sb"] == 128:
+                assert all(x % 128 == 0 for x in xs), (world, case, xs)
+    assert off128
+
+
+@pytest.fixture(scope="module")
+def rccl1():
     import svtgpu
     ctx = svtgpu.Context(0)
     comm = svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id())
+    yield ctx, comm
+    comm.close()
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_allreduce(rccl1):
+    """svtgpu_comm_create (RCCL) with one rank: ncclAllReduce runs on host buffers (staged through the comm's device
+    buffer) and on device buffers (on the caller's stream); one rank's sum is the identity."""
+    import torch
+    ctx, comm = rccl1
     assert comm.nranks == 1
     a = np.arange(17, dtype=np.uint64) * np.uint64(0x100000001)
     assert np.array_equal(comm.allreduce(a.copy()), a)
-    comm.close()
+    big = np.random.default_rng(3).integers(0, 1 << 62, size=300001, dtype=np.uint64)
+    assert np.array_equal(comm.allreduce(big.copy()), big)
+    t = torch.from_numpy(big.view(np.int64)).cuda()
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(t.cpu().numpy().view(np.uint64), big)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["sb128_10", "c3_4k10"])
+def test_rccl_one_rank_pipeline(rccl1, case):
+    """The whole tiled pipeline over a one-rank RCCL communicator (every exchange an ncclAllReduce) equals the
+    reference's outputs of the case."""
+    ctx, comm = rccl1
+    part = prun.run_gpu_tiled(case, 0, 1, comm, ctx)
+    prun.check(case, prun.assemble_tiled(case, [part]), "rccl x1")
+
+
+@pytest.mark.gpu
+def test_cdef_bound_tables_exact_size_tiled_pick_twice(rccl1):
+    """1080p (510 filter blocks, not a multiple of 8): a bound skip table of exactly nfb bytes is never written past
+    its end by the tiled search / pick (guard bytes after it), and a second pick on the same search (tiled: the tables
+    are summed once) gives the same result as the first and as an untiled state."""
+    import torch
+    import svtgpu
+    import synth
+    ctx, comm = rccl1
+    w, h, bd, q, lam = 1920, 1080, 8, 160, 60000
+    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0099)
+    R, S = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+    R.upload(rec)
+    S.upload(src)
+    ctrls = svtgpu.cdef_controls(1)
+    ref = svtgpu.CdefState(ctx, w, h)
+    ref.search(R, S, ctrls, q)
+    prm0, fbs0 = ref.pick(ctrls, q, lam)
+    st = svtgpu.CdefState(ctx, w, h)
+    nfb = st.nfb
+    assert nfb % 8
+    mse = torch.zeros((2, nfb, 64), dtype=torch.int64, device="cuda")
+    guard = torch.full((nfb + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    st.bind_tables(mse.data_ptr(), guard.data_ptr())
+    st.set_tile(None, None, comm)
+    st.search(R, S, ctrls, q)
+    prm1, fbs1 = st.pick(ctrls, q, lam)
+    prm2, fbs2 = st.pick(ctrls, q, lam)
+    torch.cuda.synchronize()
+    g = guard.cpu().numpy()
+    assert (g[nfb:] == 0xA5).all(), "skip table written past nfb bytes"
+    assert prm1.as_tuple() == prm0.as_tuple() == prm2.as_tuple()
+    assert np.array_equal(fbs1, fbs0) and np.array_equal(fbs2, fbs0)
+    for x in (R, S, ref, st):
+        x.close()
