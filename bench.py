@@ -133,6 +133,8 @@ def parse():
     ap.add_argument("--stages", default="all", choices=("all", "cdef", "md"),
                     help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
                          "configs 1/2)")
+    ap.add_argument("--no-tile-projection", dest="tile_projection", action="store_false",
+                    help="N = 1: skip the emulated ranks of 2/4/8-GPU tiled pictures (config.tile_projection)")
     ap.add_argument("--no-matrix", action="store_true",
                     help="skip the extra configurations (north_star matrix + config 1) run as child processes")
     return ap.parse_args()
@@ -539,6 +541,7 @@ def main():
     lf_start = svtgpu.LfParams.make(*cfg["lf"])  # the previous frame's levels (search start)
     lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=cfg["rdmult"], switchable=cfg["sw"], wiener=cfg["wc"], sgrproj=cfg["sc"])
     gx, gy = svtgpu.tile_grid(n) if tiled else (1, 1)
+    md_nsb = ((W + 63) // 64) * ((H + 63) // 64)
     plan = svtgpu.tile_plan(W, H, lr_us, gx, gy, rank).rects() if tiled else None
     NREF = 7
     md_refs, md_ref_y = [], []  # reference frames of the MD batch, shared by the frames in flight
@@ -573,36 +576,46 @@ def main():
     class Slot:
         """One frame in flight: its own input frames, stage states, streams and (tiles) communicator."""
 
-        def __init__(self, k):
+        def __init__(self, k, tplan=None, comm=None, md_range=None):
+            """tplan: this rank's SvtGpuTilePlan rects (a tiled picture; comm its communicator), None: the whole frame.
+            md_range: the MD batch's superblock range (default: all)."""
             self.k = k
             self.stream = torch.cuda.Stream()     # the library launches on it, torch events time it
             self.md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
             sp = self.stream.cuda_stream
             self.src, self.rec = frame_inputs(k)
             self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
-            self.R.upload(self.rec, sp)
-            self.S.upload(self.src, sp)
+            # a rank of a tiled picture receives only the part of the inputs its calls read (the plan's in_rect)
+            inr = tplan["in_rect"] if tplan else None
+            self.R.upload(self.rec, sp, rect=inr)
+            self.S.upload(self.src, sp, rect=inr)
+            self.in_rect = inr
             self.dl = svtgpu.DlfState(ctx, W, H)
             self.lr = svtgpu.LrState(ctx, W, H, lr_us)
             self.md = svtgpu.MdBatch(ctx, W, H, NREF)
             self.md_mvs = np.random.default_rng(5 + k).integers(-16, 17, size=(self.md.nsb, NREF, 2))
             self.md.set_mvs(self.md_mvs, sp)
             self.st = svtgpu.CdefState(ctx, W, H)
-            self.comm = make_comm(k)
-            if tiled:
-                self.dl.set_tile(plan["tile"], plan["dlf_out"], self.comm)
-                self.st.set_tile(plan["fb_rect"], plan["cdef_out"], self.comm)
-                self.lr.set_tile(plan["lr_units"], plan["lr_out"], self.comm)
-            self.md_range = svtgpu.band(self.md.nsb, n, rank) if tiled else (0, self.md.nsb)
+            self.comm = comm
+            if tplan:
+                self.dl.set_tile(tplan["tile"], tplan["dlf_out"], comm)
+                self.st.set_tile(tplan["fb_rect"], tplan["cdef_out"], comm)
+                self.lr.set_tile(tplan["lr_units"], tplan["lr_out"], comm)
+            self.md_range = md_range or (0, self.md.nsb)
             self.ev = []  # per timed step: events on the streams the kernels run on
             self.lf_levels = []
             self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
+
+        def close(self):
+            for x in (self.R, self.S, self.D, self.O, self.L, self.dl, self.lr, self.md, self.st, self.comm):
+                if x is not None and hasattr(x, "close"):
+                    x.close()
 
         def step(self, timed):
             torch.cuda.set_stream(self.stream)  # per thread
             stream, md_stream, sp = self.stream, self.md_stream, self.stream.cuda_stream
             R, S, D, O, L, st, lr, dl = self.R, self.S, self.D, self.O, self.L, self.st, self.lr, self.dl
-            es = [torch.cuda.Event(enable_timing=True) for _ in range(8)] if timed else None
+            es = [torch.cuda.Event(enable_timing=True) for _ in range(9)] if timed else None
             if timed:
                 es[0].record(stream)
             if a.stages == "cdef":  # CDEF search + pick + apply on the recon (configs 1/2); events keep the layout
@@ -615,7 +628,7 @@ def main():
                 st.apply(R, O, prm, sp)
                 self.at_lr.set()
                 if timed:
-                    for i in (3, 4, 5):
+                    for i in (8, 3, 4, 5):
                         es[i].record(stream)
                     es[6].record(stream), es[7].record(stream)
                     self.ev.append(es)
@@ -632,6 +645,8 @@ def main():
             if timed:
                 es[2].record(stream)
             prm, _ = st.pick(ctrls, q, lam, sp)
+            if timed:
+                es[8].record(stream)
             st.apply(D, O, prm, sp)
             if timed:
                 es[3].record(stream)
@@ -656,7 +671,7 @@ def main():
                 self.ev.append(es)
 
     F = a.frames_in_flight
-    slots = [Slot(k) for k in range(F)]
+    slots = [Slot(k, plan, make_comm(k), svtgpu.band(md_nsb, n, rank)) if tiled else Slot(k) for k in range(F)]
     torch.cuda.synchronize()
     lr = slots[0].lr
     # host -> device bytes of a frame's inputs (recon + source + mode-info grid; resident before timing) and their
@@ -674,7 +689,7 @@ def main():
 
     errors = []
 
-    def run(slot, steps, timed):
+    def run(slot, steps, timed, slots=slots):
         try:
             # frame k starts when frame k - 1 reaches its LR stage: the frames stay offset by part of a frame, so one's
             # VALU-bound search overlaps the other's latency-bound stages (started together they run in lockstep and
@@ -686,13 +701,13 @@ def main():
         except BaseException as e:  # re-raised on the main thread
             errors.append(e)
 
-    def run_all(steps, timed):
+    def run_all(steps, timed, slots=slots):
         for sl in slots:
             sl.at_lr.clear()
-        if F == 1:
-            run(slots[0], steps, timed)
+        if len(slots) == 1:
+            run(slots[0], steps, timed, slots)
         else:
-            th = [threading.Thread(target=run, args=(sl, steps, timed)) for sl in slots]
+            th = [threading.Thread(target=run, args=(sl, steps, timed, slots)) for sl in slots]
             for t in th:
                 t.start()
             for t in th:
@@ -784,6 +799,50 @@ def main():
                           for es in s0.ev], axis=0)
         iso = dict(steps=iso_steps, frame_ms=float(np.mean([es[0].elapsed_time(es[5]) for es in s0.ev])),
                    kernels=kernel_table(float(iso_ms[1]), float(iso_ms[4]), lr_classes(iso_tot), bool(iso_tot)))
+    # Strong-scaling projection of BASELINE config 4 on this one GPU: the rank with the largest tile of an N-rank
+    # picture runs alone with the same F frames in flight, its exchanges a one-rank RCCL communicator (every
+    # ncclAllReduce issued, none crossing xGMI).  Its time per step is the N-GPU job's step time up to the collectives'
+    # xGMI latency; the stage times split each stage into this rank's share and the replicated work (the CDEF pick,
+    # the host decisions).
+    projection = None
+    if n == 1 and a.stages == "all" and a.tile_projection:
+        projection = {}
+        for nn in (2, 4, 8):
+            ggx, ggy = svtgpu.tile_grid(nn)
+            plans = [svtgpu.tile_plan(W, H, lr_us, ggx, ggy, r).rects() for r in range(nn)]
+            area = [(p_["tile"][2] - p_["tile"][0]) * (p_["tile"][3] - p_["tile"][1]) for p_ in plans]
+            r_big = int(np.argmax(area))
+            emu = [Slot(k, plans[r_big], svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id()),
+                        svtgpu.band(md_nsb, nn, r_big)) for k in range(F)]
+            torch.cuda.synchronize()
+            run_all(3, False, emu)
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            nsteps = max(10, min(a.steps, 30))
+            run_all(nsteps, True, emu)
+            torch.cuda.synchronize()
+            ms_e = (time.perf_counter() - te) * 1e3 / nsteps
+            ev0 = emu[0].ev
+            sm = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7]),
+                          es[2].elapsed_time(es[8])] for es in ev0], axis=0)
+            projection["n%d" % nn] = {
+                "grid": "%dx%d" % (ggx, ggy), "rank": r_big, "tile": plans[r_big]["tile"],
+                "tile_share": round(area[r_big] / float(W * H), 4), "ms_per_step": round(ms_e, 4),
+                "projected_Mpx_s": round(F * W * H / (ms_e * 1e-3) / 1e6, 1),
+                "frame_latency_ms": round(float(np.mean([es[0].elapsed_time(es[5]) for es in ev0])), 4),
+                "stage_ms": {"dlf_pick_filter": round(float(sm[0]), 4), "cdef_search": round(float(sm[1]), 4),
+                             "cdef_pick_apply": round(float(sm[2]), 4), "lr_search_apply": round(float(sm[3]), 4),
+                             "md_sad_sse_var": round(float(sm[4]), 4)},
+                "cdef_pick_ms": round(float(sm[5]), 4)}
+            for sl in emu:
+                sl.close()
+        full_pick = float(np.mean([es[2].elapsed_time(es[8]) for es in slots[0].ev]))
+        projection["note"] = ("one rank of an N-GPU tiled picture emulated on this GPU (the rank with the largest tile, "
+                              "F = %d frames in flight, one-rank RCCL communicators): ms_per_step ~ the N-GPU job's step "
+                              "time without the xGMI latency of its collectives (DLF trial SSEs per bisection step, CDEF "
+                              "tables 2.1 MB, LR records); projected_Mpx_s = F x W x H / ms_per_step.  Replicated per "
+                              "rank whatever N: the CDEF pick (%.3f ms at N = 1, cdef_pick_ms per N), the DLF bisection's "
+                              "host decisions and the LR RD finish" % (F, full_pick))
     roof = roofline_of(iso["kernels"] if iso else kernels_f, bd, a.pmc_json)
     roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run; the PMC counters' "
                          "condition)" % iso["steps"]) if iso else "one frame in flight (the main run)"
@@ -865,6 +924,7 @@ def main():
                                         "stage; the LR search runs its Wiener and self-guided chains on two streams"},
                    "lr_search_kernel_ms": {c: round(v["ms"], 4) for c, v in lr_cls.items()},
                    "dlf_levels": list(slots[0].lf_levels[-1]) if slots[0].lf_levels else None,
+                   "tile_projection": projection,
                    "stage_roofline": stage_roof, "pipeline_roofline": pipe_roof, "transfers": xfer},
         "roofline": roof,
     }

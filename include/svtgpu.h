@@ -126,6 +126,10 @@ void    *svtgpu_frame_plane_ptr(SvtGpuFrame *f, int plane); /* device pointer */
  * host buffer is pageable (then HIP makes it synchronous). */
 int svtgpu_frame_upload(SvtGpuFrame *f, int plane, const void *host, int32_t host_stride, void *stream);
 int svtgpu_frame_download(const SvtGpuFrame *f, int plane, void *host, int32_t host_stride, void *stream);
+/* Only the samples of rect = {x0, y0, x1, y1} (plane coordinates) of one plane; `host` is the plane's origin as for
+ * svtgpu_frame_upload.  A rank of a tiled picture uploads its SvtGpuTilePlan::in_rect (chroma halved, outward). */
+int svtgpu_frame_upload_rect(SvtGpuFrame *f, int plane, const void *host, int32_t host_stride, const int32_t rect[4],
+                             void *stream);
 int svtgpu_frame_copy(SvtGpuFrame *dst, const SvtGpuFrame *src, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
@@ -167,10 +171,12 @@ int svtgpu_comm_allreduce_u64(SvtGpuComm *c, void *buf, size_t n, int32_t on_dev
  *              rank produces (a partition);
  *   cdef_out   {x0, y0, x1, y1} luma: the CDEF output its LR search and apply read (lr_out plus an 8-sample apron);
  *   dlf_out    {x0, y0, x1, y1} luma: the DLF output its CDEF search / apply and LR boundary lines read (its tile and
- *              lr_out plus a 16-sample apron).
+ *              lr_out plus a 16-sample apron);
+ *   in_rect    {x0, y0, x1, y1} luma: the recon and source samples the rank's calls read (dlf_out plus the deblocking
+ *              filter's 16-sample reach): what a rank uploads of each input picture.
  * Host only.  SVTGPU_ERR_INVALID_ARG when some rank would get no unit. */
 typedef struct SvtGpuTilePlan {
-    int32_t tile[4], fb_rect[4], lr_units[3][4], lr_out[3][4], cdef_out[4], dlf_out[4];
+    int32_t tile[4], fb_rect[4], lr_units[3][4], lr_out[3][4], cdef_out[4], dlf_out[4], in_rect[4];
 } SvtGpuTilePlan;
 int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy, int32_t rank,
                      SvtGpuTilePlan *out);

@@ -212,6 +212,8 @@ extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t 
                     std::max(c[3], o.tile[3])};
     grow(d, 8, width, height);
     std::memcpy(o.dlf_out, d, sizeof d);
+    grow(d, 16, width, height); // the deblocking filter reads up to 8 samples across an edge of the written area
+    std::memcpy(o.in_rect, d, sizeof d);
     *out = o;
     return SVTGPU_OK;
 }

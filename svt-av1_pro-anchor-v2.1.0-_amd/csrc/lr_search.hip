@@ -1535,27 +1535,42 @@ __device__ __forceinline__ void sr_tree_publish(const Descent &d, bool live, int
 
 // one pass over the resident pixels: the errors of the first nv (<= NV) candidates, wave totals into s_red[wave].
 // Candidates past nv are evaluated with xq = 0 and dropped (NV = nv up to 4; 7 for trees of 5-7 nodes).
+// The (x - src) pairs are read from LDS four chunks at a time: one LDS latency per group of four chunks instead of
+// one per chunk (the load phase leaves zeros in the chunks from K up to the next multiple of four, so a group never
+// needs a per-chunk guard).  Issuing the next group's reads before the current group spills the load phase's registers.
 template <int NV>
 __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const uint2 *dx, int pl, int K, int nv,
                                         const uint32_t *s_xq, unsigned long long (*s_red)[SG_NC]) {
+    static_assert(SR_LB == 4, "the load phase zero-fills whole groups of four chunks");
+    constexpr int GS = NV == 1 ? 4 : 1, NG = (SR_KMAX + GS - 1) / GS;
     uint32_t xq[NV], acc[NV];
 #pragma unroll
     // the candidates stay in VGPRs: v_dot2_i32_i16 (VOP3) then takes the rounding constant from an SGPR, with no
     // per-pixel copy into an accumulating v_dot2c
     for (int c = 0; c < NV; c++) xq[c] = c < nv ? s_xq[c] : 0u, acc[c] = 0;
 #pragma unroll
-    for (int kk = 0; kk < SR_KMAX; kk++) {
-        if (kk < K) { // uniform
-            const uint2 dw = dx[kk * SR_PL + pl];
+    for (int gi = 0; gi < NG; gi++) {
+        const int kb = GS * gi;
+        if (kb < K) { // uniform: the group's reads issued together
+            uint2 cur[GS];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t w  = q < 2 ? dw.x : dw.y;
-                // floor((v + 1024) / 2^11) + (x - src): the int16 half is added as an SDWA operand (no extraction)
-                const int      d1 = (q & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)w;
+            for (int j = 0; j < GS; j++)
+                if (kb + j < SR_KMAX) cur[j] = dx[(kb + j) * SR_PL + pl];
 #pragma unroll
-                for (int c = 0; c < NV; c++) {
-                    const int ee = (dot2_s(g[kk][q], xq[c], 1024) >> 11) + d1;
-                    acc[c] += (uint32_t)(ee * ee);
+            for (int j = 0; j < GS; j++) {
+                const int kk = kb + j;
+                if (kk >= SR_KMAX) break;
+                const uint2 dw = cur[j];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t w  = q < 2 ? dw.x : dw.y;
+                    // floor((v + 1024) / 2^11) + (x - src): the int16 half is added as an SDWA operand (no extraction)
+                    const int      d1 = (q & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)w;
+#pragma unroll
+                    for (int c = 0; c < NV; c++) {
+                        const int ee = (dot2_s(g[kk][q], xq[c], 1024) >> 11) + d1;
+                        acc[c] += (uint32_t)(ee * ee);
+                    }
                 }
             }
         }
@@ -1563,12 +1578,14 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
 #pragma unroll
     for (int c = 0; c < NV; c++)
         if (c < nv) {
-            const unsigned long long t = wave_sum_u32_wide(acc[c]); // <= 72 e^2 < 2^32 per lane
+            const unsigned long long t = wave_sum_u32_wide(acc[c]); // <= 76 e^2 < 2^32 per lane
             if ((pl & 63) == WAVE_LAST) s_red[pl >> 6][c] = t;
         }
 }
 
-template <typename T>
+// TREE: the speculative-tree variants (nodes 3 / 7, several candidates per pass); the default one-candidate kernel
+// compiles only sr_pass<1>, which leaves the registers for its grouped LDS reads
+template <typename T, bool TREE>
 __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
                                                         const SeedCfg cfg, int nodes, Descent *ds,
                                                         unsigned long long *xch, int32_t *status,
@@ -1671,19 +1688,35 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         }
         __syncthreads(); // B1: the moments are in s_red
         __syncthreads(); // B2: the first tree is in s_xq
+        // diagnostics (stat): pixel wave 0's pass time (B2/B4 release to its arrival at B3) and its wait from B3 to the
+        // B4 release
+        unsigned long long tpass = 0, twait = 0, tmark = stat ? __builtin_amdgcn_s_memrealtime() : 0;
         for (;;) {
             const int nv = __builtin_amdgcn_readfirstlane(s_nv);
             if (nv == 0) break;
-            switch (nv) {
-            case 1: sr_pass<1>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
-            case 2: sr_pass<2>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
-            case 3: sr_pass<3>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
-            case 4: sr_pass<4>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
-            default: sr_pass<SG_NC>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+            if constexpr (!TREE) {
+                sr_pass<1>(g, sr_dx, pl, K, 1, s_xq, s_red);
+            } else {
+                switch (nv) {
+                case 1: sr_pass<1>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+                case 2: sr_pass<2>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+                case 3: sr_pass<3>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+                case 4: sr_pass<4>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+                default: sr_pass<SG_NC>(g, sr_dx, pl, K, nv, s_xq, s_red); break;
+                }
+            }
+            if (stat) {
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                tpass += t - tmark, tmark = t;
             }
             __syncthreads(); // B3: the pass's errors are in s_red
             __syncthreads(); // B4: the next tree (or the end) is in s_xq / s_nv
+            if (stat) {
+                const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                twait += t - tmark, tmark = t;
+            }
         }
+        if (stat && pl == 0) atomicAdd(stat + 7, tpass), atomicAdd(stat + 8, twait);
     } else {
         // ================= control wave =================
         // stat (SVTGPU_SR_STATS diagnostics, else null): items, passes, candidate-pixels, load / descent / control
@@ -1692,7 +1725,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         __builtin_amdgcn_s_setprio(3);
         const int                lane = threadIdx.x & 63;
         const unsigned long long t0   = stat ? __builtin_amdgcn_s_memrealtime() : 0;
-        unsigned long long       tctl = 0, ncp = 0;
+        unsigned long long       tctl = 0, ncp = 0, tpre = 0;
         __syncthreads(); // B1
         const unsigned long long t1 = stat ? __builtin_amdgcn_s_memrealtime() : 0;
         long long v  = 0; // lane q < 5: moment q over the workgroup (and the other row parts)
@@ -1718,7 +1751,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
             const uint32_t mask = __builtin_amdgcn_readfirstlane(s_mask);
             uint32_t       xw = 0, xb = 0;
             bool           okw = false, okb = false;
+            const unsigned long long tc0 = stat ? __builtin_amdgcn_s_memrealtime() : 0;
             if (nodes == 1) sr_children(D, xw, okw, xb, okb); // during the pass
+            if (stat) tpre += __builtin_amdgcn_s_memrealtime() - tc0;
             __syncthreads(); // B3
             const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
             ncp += (unsigned long long)nv * nch * 4;
@@ -1773,7 +1808,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         if (stat && lane == 0) {
             atomicAdd(stat + 0, 1ull), atomicAdd(stat + 2, ncp), atomicAdd(stat + 3, t1 - t0);
             atomicAdd(stat + 4, __builtin_amdgcn_s_memrealtime() - t1), atomicAdd(stat + 5, tctl);
-            atomicAdd(stat + 6, (unsigned long long)nch * 4);
+            atomicAdd(stat + 6, (unsigned long long)nch * 4), atomicAdd(stat + 9, tpre);
         }
     }
     PROF_END(tk);
@@ -2327,8 +2362,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *sr_stat = nullptr;
-    if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 64));
-    if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 64, st));
+    if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 128));
+    if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 128, st));
     run(0, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
@@ -2397,8 +2432,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (n_sr) { // the whole self-guided search of every (unit, ep), resident on one CU each (or a few)
         run(3, [&](unsigned long long *tk) {
-            hipLaunchKernelGGL(sgr_res_kernel<T>, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
-                               (const SrItem *)dp(o_sritem), cfg, sr_tree_nodes(), (Descent *)dp(o_sds),
+            const int nodes = sr_tree_nodes();
+            auto kern = nodes == 1 ? sgr_res_kernel<T, false> : sgr_res_kernel<T, true>;
+            hipLaunchKernelGGL(kern, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
+                               (const SrItem *)dp(o_sritem), cfg, nodes, (Descent *)dp(o_sds),
                                (unsigned long long *)(sr_parted ? qa + q_srx : nullptr), (int32_t *)dp(o_sstat),
                                sr_stat, tk);
         });
@@ -2431,13 +2468,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         return SVTGPU_ERR_HIP;
     }
     if (n_sr && sr_stat) {
-        unsigned long long v[8];
-        HIP_TRY(hipMemcpy(v, sr_stat, 64, hipMemcpyDeviceToHost));
+        unsigned long long v[16];
+        HIP_TRY(hipMemcpy(v, sr_stat, 128, hipMemcpyDeviceToHost));
         const double n = (double)std::max(1ull, v[0]);
         std::fprintf(stderr, "sgr_res: %llu items, %.2f passes/item, %.2f candidates/pass, %.0f px/item, ticks/item "
-                     "load %.2f us, descent %.2f us (control %.2f us)\n", v[0], v[1] / n,
+                     "load %.2f us, descent %.2f us (control %.2f us; pixel wave 0: passes %.2f us, waits B3-B4 %.2f "
+                     "us; control wave before B3 %.2f us)\n", v[0], v[1] / n,
                      v[1] ? (double)v[2] / (double)v[6] * n / v[1] : 0.0, v[6] / n, v[3] / n * 0.01, v[4] / n * 0.01,
-                     v[5] / n * 0.01);
+                     v[5] / n * 0.01, v[7] / n * 0.01, v[8] / n * 0.01, v[9] / n * 0.01);
     }
     if (n_sr && *(const int32_t *)hp(h_res + (o_sstat - o_sse))) { // status bits of sgr_res_kernel
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR self-guided descent: pass bound, part plan or exchange failed",

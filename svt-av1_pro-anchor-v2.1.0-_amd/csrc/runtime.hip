@@ -181,6 +181,22 @@ extern "C" int svtgpu_frame_upload(SvtGpuFrame *f, int plane, const void *host, 
     return SVTGPU_OK;
 }
 
+extern "C" int svtgpu_frame_upload_rect(SvtGpuFrame *f, int plane, const void *host, int32_t host_stride,
+                                        const int32_t rect[4], void *stream) {
+    if (!f || !host || !rect || plane < 0 || plane > 2 || host_stride < f->pw[plane] || rect[0] < 0 || rect[1] < 0 ||
+        rect[2] > f->pw[plane] || rect[3] > f->ph[plane] || rect[0] > rect[2] || rect[1] > rect[3])
+        return SVTGPU_ERR_INVALID_ARG;
+    if (rect[0] == rect[2] || rect[1] == rect[3]) return SVTGPU_OK;
+    const size_t b = f->bytes_per_sample;
+    svtgpu_count_xfer(0, (size_t)(rect[2] - rect[0]) * (rect[3] - rect[1]) * b);
+    HIP_TRY(hipMemcpy2DAsync((uint8_t *)f->plane[plane] + ((size_t)rect[1] * f->stride[plane] + rect[0]) * b,
+                             f->stride[plane] * b,
+                             (const uint8_t *)host + ((size_t)rect[1] * host_stride + rect[0]) * b, host_stride * b,
+                             (size_t)(rect[2] - rect[0]) * b, rect[3] - rect[1], hipMemcpyHostToDevice,
+                             pick_stream(f->ctx, stream)));
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_frame_download(const SvtGpuFrame *f, int plane, void *host, int32_t host_stride, void *stream) {
     if (!f || !host || plane < 0 || plane > 2 || host_stride < f->pw[plane])
         return SVTGPU_ERR_INVALID_ARG;

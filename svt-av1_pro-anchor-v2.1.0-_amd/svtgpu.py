@@ -219,6 +219,7 @@ _SIGS = {
     "svtgpu_frame_plane_ptr": (_P, [_P, ctypes.c_int]),
     "svtgpu_frame_upload": (ctypes.c_int, [_P, ctypes.c_int, _P, _I32, _P]),
     "svtgpu_frame_download": (ctypes.c_int, [_P, ctypes.c_int, _P, _I32, _P]),
+    "svtgpu_frame_upload_rect": (ctypes.c_int, [_P, ctypes.c_int, _P, _I32, _P, _P]),
     "svtgpu_frame_copy": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_cdef_find_dir": (ctypes.c_uint8, [_P, _I32, ctypes.POINTER(_I32), _I32]),
     "svtgpu_cdef_find_dir_dual": (None, [_P, _P, ctypes.c_int, ctypes.POINTER(_I32), ctypes.POINTER(_I32), _I32,
@@ -436,13 +437,19 @@ class Frame:
     def plane_shape(self, p):
         return (self.height, self.width) if p == 0 else (self.height // 2, self.width // 2)
 
-    def upload(self, planes, stream=None):
+    def upload(self, planes, stream=None, rect=None):
+        """All samples, or (rect = luma {x0, y0, x1, y1}) only those of the rectangle: chroma halved, rounded outward
+        (svtgpu_frame_upload_rect; a rank of a tiled picture uploads its plan's in_rect)."""
         keep = []
         for p, a in enumerate(planes):
             a = np.ascontiguousarray(a, dtype=self.dtype)
             assert a.shape == self.plane_shape(p), (a.shape, self.plane_shape(p))
             keep.append(a)
-            check(lib().svtgpu_frame_upload(self.h, p, ptr(a), a.shape[1], stream))
+            if rect is None:
+                check(lib().svtgpu_frame_upload(self.h, p, ptr(a), a.shape[1], stream))
+            else:
+                r = chroma_rect(rect, a.shape) if p else [int(v) for v in rect]
+                check(lib().svtgpu_frame_upload_rect(self.h, p, ptr(a), a.shape[1], _rect(r), stream))
         self.ctx.synchronize(stream)  # host buffers must outlive the copies
 
     def download(self, stream=None):
@@ -474,10 +481,15 @@ def cdef_controls(level):
 class TilePlan(ctypes.Structure):
     """SvtGpuTilePlan: what one rank of a picture tiled over GPUs computes (svtgpu_tile_plan)."""
     _fields_ = [("tile", _I32 * 4), ("fb_rect", _I32 * 4), ("lr_units", (_I32 * 4) * 3), ("lr_out", (_I32 * 4) * 3),
-                ("cdef_out", _I32 * 4), ("dlf_out", _I32 * 4)]
+                ("cdef_out", _I32 * 4), ("dlf_out", _I32 * 4), ("in_rect", _I32 * 4)]
 
     def rects(self):
         return {k: (np.array(getattr(self, k)).tolist()) for k, _ in self._fields_}
+
+
+def chroma_rect(r, shape):
+    """A luma rectangle {x0, y0, x1, y1} on a 4:2:0 chroma plane of `shape` (rows, cols): halved, rounded outward."""
+    return [int(r[0]) // 2, int(r[1]) // 2, min(shape[1], (int(r[2]) + 1) // 2), min(shape[0], (int(r[3]) + 1) // 2)]
 
 
 def tile_grid(n):

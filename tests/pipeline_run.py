@@ -303,8 +303,13 @@ def run_gpu_tiled(case, rank, world, comm, ctx=None):
     plan = svtgpu.tile_plan(w, h, us, gx, gy, rank, sb=c["sb"]).rects()
     ctx = ctx or svtgpu.Context()
     S, R, D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(5))
-    S.upload(src)
-    R.upload(rec)
+    # the rank's inputs: only the plan's in_rect of the recon and the source, the rest of both pictures poisoned (a
+    # read outside in_rect changes the outputs, which are checked against the reference's)
+    rng = np.random.default_rng(7 + rank)
+    for F in (S, R):
+        F.upload([rng.integers(0, 1 << bd, size=F.plane_shape(p), dtype=np.uint16) for p in range(3)])
+    S.upload(src, rect=plan["in_rect"])
+    R.upload(rec, rect=plan["in_rect"])
     dl = svtgpu.DlfState(ctx, w, h)
     dl.set_mode_info(mi)
     dl.set_tile(plan["tile"], plan["dlf_out"], comm)
