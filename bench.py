@@ -133,6 +133,11 @@ def parse():
     ap.add_argument("--stages", default="all", choices=("all", "cdef", "md"),
                     help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
                          "configs 1/2)")
+    ap.add_argument("--host-timing", action="store_true",
+                    help="report the host thread's wall / CPU ms per frame-level call (config.host_ms, slot 0)")
+    ap.add_argument("--emulate-rank", type=int, default=0, metavar="N",
+                    help="N = 1 only: run the largest rank of an N-GPU tiled picture alone (one-rank RCCL "
+                         "communicators); value is then the projected N-GPU job throughput F x W x H / step time")
     ap.add_argument("--no-tile-projection", dest="tile_projection", action="store_false",
                     help="N = 1: skip the emulated ranks of 2/4/8-GPU tiled pictures (config.tile_projection)")
     ap.add_argument("--no-matrix", action="store_true",
@@ -403,6 +408,22 @@ def measure_next_rows(ctx, torch, W, H, reps=20):
     return out
 
 
+class HostClock:
+    """--host-timing: the host thread's wall and CPU time in each frame-level call of a step (CPU time includes the
+    library's spin-waits on mapped memory; wall time includes every wait)."""
+
+    def __init__(self, on):
+        self.on, self.t = on, {}
+        if on:
+            self.w, self.c = time.perf_counter(), time.thread_time()
+
+    def __call__(self, name):
+        if self.on:
+            w, c = time.perf_counter(), time.thread_time()
+            self.t[name] = ((w - self.w) * 1e3, (c - self.c) * 1e3)
+            self.w, self.c = w, c
+
+
 def roofline_of(kernels, bd, pmc_json):
     """The `roofline` object for the largest device-time kernel of the step.  kernels: name -> {ms (device time per
     frame), launches (per frame), alg_bytes (SURVEY §8(d) bytes per frame: the samples the kernel's job reads once and
@@ -543,6 +564,12 @@ def main():
     gx, gy = svtgpu.tile_grid(n) if tiled else (1, 1)
     md_nsb = ((W + 63) // 64) * ((H + 63) // 64)
     plan = svtgpu.tile_plan(W, H, lr_us, gx, gy, rank).rects() if tiled else None
+    emu_rank = None
+    if a.emulate_rank > 1 and n == 1 and a.stages == "all":  # one rank of an N-GPU tiled picture, alone on this GPU
+        egx, egy = svtgpu.tile_grid(a.emulate_rank)
+        eplans = [svtgpu.tile_plan(W, H, lr_us, egx, egy, r).rects() for r in range(a.emulate_rank)]
+        emu_rank = int(np.argmax([(p_["tile"][2] - p_["tile"][0]) * (p_["tile"][3] - p_["tile"][1]) for p_ in eplans]))
+        plan = eplans[emu_rank]
     NREF = 7
     md_refs, md_ref_y = [], []  # reference frames of the MD batch, shared by the frames in flight
     for r in range(NREF):
@@ -603,6 +630,7 @@ def main():
                 self.lr.set_tile(tplan["lr_units"], tplan["lr_out"], comm)
             self.md_range = md_range or (0, self.md.nsb)
             self.ev = []  # per timed step: events on the streams the kernels run on
+            self.ht = []  # --host-timing: per timed step, {call: (wall ms, thread CPU ms)}
             self.lf_levels = []
             self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
 
@@ -634,20 +662,27 @@ def main():
                     self.ev.append(es)
                 return
             # the frame's mode info: upload + edge records; DLF level search + frame filter
+            hc = HostClock(timed and a.host_timing)
             dl.set_mode_info_device(mi_dev, sp)
+            hc("mode_info")
             lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
+            hc("dlf_pick")
             dl.filter_to(R, D, lfp, 0, 3, sp)
+            hc("dlf_filter")
             if timed:
                 es[1].record(stream)
                 self.lf_levels.append(lfp.levels())
             # CDEF stage on the deblocked frame (tiles: this rank's filter blocks; the pick sums the tables)
             st.search(D, S, ctrls, q, sp)
+            hc("cdef_search")
             if timed:
                 es[2].record(stream)
             prm, _ = st.pick(ctrls, q, lam, sp)
+            hc("cdef_pick")
             if timed:
                 es[8].record(stream)
             st.apply(D, O, prm, sp)
+            hc("cdef_apply")
             if timed:
                 es[3].record(stream)
             # MD distortion batch (source vs 7 references, every block shape): independent of the filter chain, on
@@ -656,13 +691,18 @@ def main():
             if timed:
                 es[6].record(md_stream)
             self.md.run(S, md_refs, self.md_range[0], self.md_range[1], md_stream.cuda_stream)
+            hc("md")
             if timed:
                 es[7].record(md_stream)
             # LR search + apply on the CDEF output (tiles: this rank's units; the records are summed before the
             # finish) with the boundary lines from the DLF output
             self.at_lr.set()
             lr_ft = lr.search(O, S, lr_ctrls, sp)
+            hc("lr_search")
             lr.apply(D, O, L, lr_ft, sp)
+            hc("lr_apply")
+            if hc.on:
+                self.ht.append(hc.t)
             if timed:
                 es[4].record(stream)
             stream.wait_stream(md_stream)  # the step ends when both streams are done
@@ -671,7 +711,11 @@ def main():
                 self.ev.append(es)
 
     F = a.frames_in_flight
-    slots = [Slot(k, plan, make_comm(k), svtgpu.band(md_nsb, n, rank)) if tiled else Slot(k) for k in range(F)]
+    if emu_rank is not None:
+        slots = [Slot(k, plan, svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id()),
+                      svtgpu.band(md_nsb, a.emulate_rank, emu_rank)) for k in range(F)]
+    else:
+        slots = [Slot(k, plan, make_comm(k), svtgpu.band(md_nsb, n, rank)) if tiled else Slot(k) for k in range(F)]
     torch.cuda.synchronize()
     lr = slots[0].lr
     # host -> device bytes of a frame's inputs (recon + source + mode-info grid; resident before timing) and their
@@ -740,6 +784,7 @@ def main():
     stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])]
                         for es in slots[0].ev], axis=0)
     frame_ms = float(np.mean([es[0].elapsed_time(es[5]) for es in slots[0].ev]))
+    ht_main = list(slots[0].ht)  # --host-timing: the main run's (the iso phase below appends its own)
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
@@ -805,7 +850,7 @@ def main():
     # xGMI latency; the stage times split each stage into this rank's share and the replicated work (the CDEF pick,
     # the host decisions).
     projection = None
-    if n == 1 and a.stages == "all" and a.tile_projection:
+    if n == 1 and a.stages == "all" and a.tile_projection and emu_rank is None:
         projection = {}
         for nn in (2, 4, 8):
             ggx, ggy = svtgpu.tile_grid(nn)
@@ -935,6 +980,21 @@ def main():
         out["config"].pop("lr_search_kernel_ms")
     if matrix is not None:
         out["config"]["matrix"] = matrix
+    if a.host_timing and ht_main:
+        def host_table(ht):
+            return {k: [round(float(np.mean([t[k][0] for t in ht])), 4), round(float(np.mean([t[k][1] for t in ht])), 4)]
+                    for k in ht[0]}
+        out["config"]["host_ms"] = host_table(ht_main)
+        out["config"]["host_ms"]["note"] = ("slot 0 per timed step: [wall ms, thread CPU ms] in each call, %d frames in "
+                                            "flight" % F)
+        if iso and len(slots[0].ht) > len(ht_main):
+            out["config"]["host_ms_f1"] = host_table(slots[0].ht[len(ht_main):])
+    if emu_rank is not None:
+        out["config"]["emulated"] = {"ranks": a.emulate_rank, "rank": emu_rank, "tile": plan["tile"],
+                                     "note": "this GPU ran one rank of an N-GPU tiled picture alone (one-rank RCCL "
+                                             "communicators: every exchange issued, none over xGMI); value = F x W x H "
+                                             "/ this rank's step time, the N-GPU job's rate up to the collectives' "
+                                             "latency"}
     if rank == 0 and n == 1 and a.stages == "all" and not a.no_matrix:
         out["config"]["next_rows"] = measure_next_rows(ctx, torch, W, H)
     if rank == 0 and n == 1 and not a.no_cpu_baseline:

@@ -330,6 +330,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     (void)hipFree(s->d_flt);
     (void)hipFree(s->d_work);
     if (s->d_qarena) (void)hipFree(s->d_qarena);
+    if (s->d_sxarena) (void)hipFree(s->d_sxarena);
     if (s->pin_free) (void)hipEventSynchronize(s->pin_free), (void)hipEventDestroy(s->pin_free);
     if (s->wst) (void)hipStreamSynchronize(s->wst), (void)hipStreamDestroy(s->wst);
     if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);

@@ -27,6 +27,11 @@ struct SvtGpuLrState {
     // uncached device memory: the exchange words of the resident descents' row parts (coherent without cache flushes)
     void                *d_qarena;
     size_t               qarena_bytes;
+    // cached device memory for the self-guided row parts' exchange when it stays in one XCD's L2 (SVTGPU_SR_XCH=l2),
+    // and the search count that tags its words (a line left in an L2 by an earlier search never matches a tag)
+    void                *d_sxarena;
+    size_t               sxarena_bytes;
+    uint32_t             sx_epoch;
     // a picture tiled over GPUs (svtgpu_lr_set_tile): the units searched {col0, row0, col1, row1} and the samples
     // written {x0, y0, x1, y1} per plane, the exchange of the search records (null: one rank)
     int32_t              tile_units[3][4], tile_out[3][4];

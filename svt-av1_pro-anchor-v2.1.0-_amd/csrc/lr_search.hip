@@ -1419,11 +1419,19 @@ constexpr unsigned long long SR_LOW = (1ull << 48) - 1;
 // one lane's value of exchange round r, summed over the row parts (this part's value published first).  Every value
 // fits 48 bits two's complement: a part holds <= 2^17 pixels, g in [-16368, 32767], |s| < 2^14, and a projection
 // error |e| <= (352 * 32767 + 2^21) / 2^11 < 6657 (|xq0| <= 96, |xq1| <= 256), e^2 < 2^26.  false: timed out
+// xmode bit 8: the words live in cached memory and stay in the XCD's L2 (every part of an item runs on one XCD: grid
+// positions first + 8 q); the store is a plain one (the CU's L1 writes through to the L2), the polls bypass the L1
+// (agent-scope loads).  Bits 0-7: the search's epoch, in the tag with the exchange round, so that a line an earlier
+// search left in an L2 never passes for this one's.  xmode 0: uncached memory, agent-scope stores.
 __device__ bool sr_exchange_lane(unsigned long long *xch, const SrItem &it, int r, int q, long long &v,
-                                 int32_t *status) {
-    const unsigned long long tag = (unsigned long long)((r + 1) & 0xFFFF) << 48;
-    __hip_atomic_store(xch + ((size_t)(it.first + 8 * it.part) * 2 + (r & 1)) * 8 + q, tag | ((unsigned long long)v & SR_LOW),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                 int32_t *status, unsigned xmode) {
+    const unsigned long long tag = (unsigned long long)(((xmode & 0xFF) << 8) | ((r + 1) & 0xFF)) << 48;
+    unsigned long long *mine = xch + ((size_t)(it.first + 8 * it.part) * 2 + (r & 1)) * 8 + q;
+    const unsigned long long word = tag | ((unsigned long long)v & SR_LOW);
+    if (xmode & 0x100)
+        __hip_atomic_store(mine, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        __hip_atomic_store(mine, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     long long add = 0;
     for (int p = 0; p < it.nparts; p++) {
         if (p == it.part) continue;
@@ -1475,32 +1483,33 @@ __device__ __forceinline__ void sr_tree_lanes(const Descent &d, bool live, int n
     if (n == 0) *s_mask = (uint32_t)mask, *s_nv = (int)__popcll(mask);
 }
 
-// control wave, one-candidate passes: the two candidates that can follow d's pending one -- lane 1 after a worse
-// outcome, lane 2 after a not-worse one (the seed's outcome does not steer: no worse child) -- built while the pixel
-// waves evaluate the pending candidate, so that after its error only the choice between them is left before the next
-// pass.  (ok*, x*) wave-uniform; !ok: the descent ends on that outcome.
+// control wave, one-candidate passes: the two candidates that can follow d's pending one -- after a worse outcome and
+// after a not-worse one (the seed's outcome does not steer: no worse child) -- built while the pixel waves evaluate the
+// pending candidate, so that after its error only the choice between them is left before the next pass.  d is
+// wave-uniform, so both children are built one after the other in scalar registers (the scalar unit, no divergent
+// lanes: two lanes each stepping one child ran both paths on the vector unit, as long as the pixel pass itself).
+// (ok*, x*) wave-uniform; !ok: the descent ends on that outcome.
 __device__ __forceinline__ void sr_children(const Descent &d, uint32_t &xw, bool &okw, uint32_t &xb, bool &okb) {
-    const int n  = threadIdx.x & 63;
-    bool      ok = n == 1 || n == 2;
-    uint32_t  xv = 0;
-    if (ok) {
-        const bool worse = n == 1;
-        Descent    c     = d;
-        if (worse && c.init) {
-            ok = false;
-        } else {
-            c.report_outcome(worse, 0);
-            ok = c.next();
-        }
-        if (ok) {
+    okw = false, xw = 0;
+    if (!d.init) {
+        Descent c = d;
+        c.report_outcome(true, 0);
+        okw = c.next();
+        if (okw) {
             int32_t x[2];
             decode_xq(c, x);
-            xv = pack2(x[0], x[1]);
+            xw = pack2(x[0], x[1]);
         }
     }
-    const unsigned long long m = __ballot(ok);
-    okw = (m >> 1) & 1, okb = (m >> 2) & 1;
-    xw  = (uint32_t)__builtin_amdgcn_readlane((int)xv, 1), xb = (uint32_t)__builtin_amdgcn_readlane((int)xv, 2);
+    Descent c = d;
+    c.report_outcome(false, 0);
+    okb = c.next();
+    xb  = 0;
+    if (okb) {
+        int32_t x[2];
+        decode_xq(c, x);
+        xb = pack2(x[0], x[1]);
+    }
 }
 
 // wave-uniform copies (scalar registers) of a 64-bit lane value and of a struct
@@ -1588,7 +1597,7 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
 template <typename T, bool TREE>
 __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
                                                         const SeedCfg cfg, int nodes, Descent *ds,
-                                                        unsigned long long *xch, int32_t *status,
+                                                        unsigned long long *xch, unsigned xmode, int32_t *status,
                                                         unsigned long long *stat, unsigned long long *tk) {
     PROF_BEGIN(tk);
     extern __shared__ uint2 sr_dx[];                   // [chunk k][pixel lane]: (x - src) of pixels 0, 1 | 2, 3 (int16)
@@ -1734,7 +1743,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
             unsigned long long t = 0;
             for (int w = 0; w < SR_PW; w++) t += s_red[w][lane];
             v = (long long)t;
-            if (it.nparts > 1) ok = sr_exchange_lane(xch, it, 0, lane, v, status);
+            if (it.nparts > 1) ok = sr_exchange_lane(xch, it, 0, lane, v, status, xmode);
         }
         ok = __ballot(!ok) == 0;
         long long mv[5];
@@ -1763,7 +1772,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 unsigned long long t = 0;
                 for (int w = 0; w < SR_PW; w++) t += s_red[w][lane];
                 e = (long long)t;
-                if (it.nparts > 1) ok = sr_exchange_lane(xch, it, pass, lane, e, status);
+                if (it.nparts > 1) ok = sr_exchange_lane(xch, it, pass, lane, e, status, xmode);
             }
             ok = __ballot(!ok) == 0;
             if (pass > SR_MAX_PASSES) {
@@ -2360,6 +2369,24 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         qa = (uint8_t *)s->d_qarena;
         HIP_TRY(hipMemsetAsync(qa, 0, qc.off, st));
     }
+    // the self-guided row parts' exchange words: uncached memory (default) or, with SVTGPU_SR_XCH=l2, cached memory that
+    // stays in the XCD's L2 (no memset: the search epoch tags the words)
+    static const bool sr_l2 = [] {
+        const char *e = std::getenv("SVTGPU_SR_XCH");
+        return e && !std::strcmp(e, "l2");
+    }();
+    unsigned sr_xmode = 0;
+    if (n_sr && sr_parted && sr_l2) {
+        const size_t need = 128 * (size_t)n_sr;
+        if (need > s->sxarena_bytes) {
+            if (s->d_sxarena) (void)hipFree(s->d_sxarena);
+            s->d_sxarena = nullptr, s->sxarena_bytes = 0;
+            HIP_TRY(hipMalloc(&s->d_sxarena, need));
+            HIP_TRY(hipMemsetAsync(s->d_sxarena, 0, need, st));
+            s->sxarena_bytes = need;
+        }
+        sr_xmode = 0x100u | (++s->sx_epoch & 0xFFu);
+    }
     static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *sr_stat = nullptr;
     if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 128));
@@ -2436,8 +2463,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             auto kern = nodes == 1 ? sgr_res_kernel<T, false> : sgr_res_kernel<T, true>;
             hipLaunchKernelGGL(kern, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
                                (const SrItem *)dp(o_sritem), cfg, nodes, (Descent *)dp(o_sds),
-                               (unsigned long long *)(sr_parted ? qa + q_srx : nullptr), (int32_t *)dp(o_sstat),
-                               sr_stat, tk);
+                               (unsigned long long *)(sr_parted ? (sr_l2 ? (uint8_t *)s->d_sxarena : qa + q_srx) : nullptr),
+                               sr_xmode, (int32_t *)dp(o_sstat), sr_stat, tk);
         });
         HIP_TRY(hipGetLastError());
     }

@@ -1,0 +1,65 @@
+"""Register budget of the gfx950 kernels (CPU test, no GPU): the code objects in the library's build objects are
+unbundled (clang-offload-bundler) and their AMDGPU metadata read (llvm-readelf --notes).  A kernel that spills VGPRs to
+scratch memory runs several times slower (a 6-register overshoot of the resident self-guided search spilled 186
+registers and took its load phase from 13 to 27 us per item), so every hot kernel must stay spill-free; the list
+names the few that carry a known, measured-harmless spill."""
+import glob
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD = os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd", "build")
+LLVM = "/opt/rocm/lib/llvm/bin"
+# kernel name fragment -> spilled VGPRs allowed: the known spills of round 3's measured kernels (a few registers each,
+# outside their inner loops); anything above these, or in any other kernel, fails
+ALLOWED = {"wiener_res_kernel": 1, "cdef_search_kernelIt": 3, "cdef_search_kernelIh": 6, "dlf_tile_kernelIhLb1": 1}
+
+
+def _kernels(obj, tmp):
+    fat = os.path.join(tmp, "fat.bin")
+    co = os.path.join(tmp, "k.co")
+    sections = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "-S", obj], check=True, capture_output=True,
+                              text=True).stdout
+    if ".hip_fatbin" not in sections:  # host code only
+        return {}
+    subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, obj, os.devnull],
+                   check=True, capture_output=True)
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--input=" + fat, "--output=" + co, "--unbundle"],
+                   check=True, capture_output=True)
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                           text=True).stdout
+    out, name = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.match(r"\s+\.(vgpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size):\s+(\d+)", line)
+        if m and name:
+            out.setdefault(name, {})[m.group(1)] = int(m.group(2))
+    return out
+
+
+@pytest.mark.skipif(not os.path.isdir(BUILD) or not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")),
+                    reason="needs the built objects and the ROCm LLVM tools")
+def test_no_vgpr_spills():
+    objs = sorted(glob.glob(os.path.join(BUILD, "*.o")))
+    assert objs, "no build objects"
+    bad, seen = [], 0
+    tmp = tempfile.mkdtemp()
+    try:
+        for obj in objs:
+            for name, m in _kernels(obj, tmp).items():
+                seen += 1
+                allow = max([v for k, v in ALLOWED.items() if k in name], default=0)
+                if m.get("vgpr_spill_count", 0) > allow:
+                    bad.append((os.path.basename(obj), name, m))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    assert seen > 50, seen
+    assert not bad, bad
