@@ -163,6 +163,7 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_pick) (void)hipHostFree(s->h_pick);
+    svtgpu_prio_destroy(&s->prio);
     delete s;
 }
 
@@ -337,13 +338,20 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
         if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
         return SVTGPU_OK;
     }
-    if (int rc = svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, st))
+    hipStream_t hs;
+    if (int rc = svtgpu_prio_enter(&s->prio, st, &hs)) return rc;
+    if (int rc = svtgpu_cdef_pick_impl(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, hs)) {
+        (void)svtgpu_prio_leave(&s->prio, hs, st);
         return rc;
+    }
     if (s->d_fb_kind) { // the halves of 128-wide areas take the area's index (EbEncCdef.c:893-909)
-        if (int rc = svtgpu_launch_cdef_sb128_dup(s, st)) return rc;
+        if (int rc = svtgpu_launch_cdef_sb128_dup(s, hs)) {
+            (void)svtgpu_prio_leave(&s->prio, hs, st);
+            return rc;
+        }
         if (fb_strength_out) svtgpu_cdef_sb128_dup_host(s, fb_strength_out);
     }
-    return SVTGPU_OK;
+    return svtgpu_prio_leave(&s->prio, hs, st);
 }
 
 extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream) {

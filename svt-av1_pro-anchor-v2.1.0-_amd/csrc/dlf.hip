@@ -523,6 +523,7 @@ struct SvtGpuDlfState {
     void          *d_search = nullptr;  // DlfDevSearch: the device-resident level search (SVTGPU_DLF_DEVICE)
     void          *h_search = nullptr;  // its pinned host copy
     SvtGpuLfMi    *h_mi = nullptr;      // pinned staging of the mode info (one upload per frame, asynchronous)
+    SvtGpuPrioLane prio;                // the level search's trial launches
     hipEvent_t     mi_free = nullptr;   // the previous upload has read h_mi
 };
 
@@ -979,6 +980,7 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     (void)hipFree(s->d_arrive);
     if (s->h_sse) (void)hipHostFree(s->h_sse);
     (void)hipFree(s->d_search);
+    svtgpu_prio_destroy(&s->prio);
     if (s->h_search) (void)hipHostFree(s->h_search);
     delete s;
 }
@@ -1147,9 +1149,12 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
     const int   chunk  = dlf_device_chunk();
-    if ((rc = chunk ? run_searches_device(s, recon, source, p, all, search_uv ? 3 : 1, st, chunk)
-                    : run_searches(s, recon, source, p, all, search_uv ? 3 : 1, st)))
-        return rc;
+    hipStream_t hs;
+    if ((rc = svtgpu_prio_enter(&s->prio, st, &hs))) return rc;
+    rc = chunk ? run_searches_device(s, recon, source, p, all, search_uv ? 3 : 1, hs, chunk)
+               : run_searches(s, recon, source, p, all, search_uv ? 3 : 1, hs);
+    if (int rj = svtgpu_prio_leave(&s->prio, hs, st)) rc = rc ? rc : rj;
+    if (rc) return rc;
     if (s->mi_on_device) { // the grid was checked by the records kernel: its verdict, once the stream has passed it
         s->mi_on_device = 0;
         HIP_TRY(hipStreamSynchronize(st));

@@ -1419,7 +1419,7 @@ constexpr unsigned long long SR_LOW = (1ull << 48) - 1;
 // one lane's value of exchange round r, summed over the row parts (this part's value published first).  Every value
 // fits 48 bits two's complement: a part holds <= 2^17 pixels, g in [-16368, 32767], |s| < 2^14, and a projection
 // error |e| <= (352 * 32767 + 2^21) / 2^11 < 6657 (|xq0| <= 96, |xq1| <= 256), e^2 < 2^26.  false: timed out
-// xmode bit 8: the words live in cached memory and stay in the XCD's L2 (every part of an item runs on one XCD: grid
+// xmode bit 9: one-part items keep the two-barrier pass loop (A/B).  Bit 8: the words live in cached memory and stay in the XCD's L2 (every part of an item runs on one XCD: grid
 // positions first + 8 q); the store is a plain one (the CU's L1 writes through to the L2), the polls bypass the L1
 // (agent-scope loads).  Bits 0-7: the search's epoch, in the tag with the exchange round, so that a line an earlier
 // search left in an L2 never passes for this one's.  xmode 0: uncached memory, agent-scope stores.
@@ -1601,7 +1601,11 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                                                         unsigned long long *stat, unsigned long long *tk) {
     PROF_BEGIN(tk);
     extern __shared__ uint2 sr_dx[];                   // [chunk k][pixel lane]: (x - src) of pixels 0, 1 | 2, 3 (int16)
-    __shared__ unsigned long long s_red[SR_PW][SG_NC]; // wave partials: the moments, then each pass's errors
+    // wave partials: the moments, then each pass's errors; two buffers by pass parity (the one-barrier path of
+    // one-part items reads a pass's partials while the next pass writes the other buffer)
+    __shared__ unsigned long long s_red2[2][SR_PW][SG_NC];
+    unsigned long long (*const s_red)[SG_NC] = s_red2[0];
+    __shared__ uint32_t           s_ch[2][8];          // one-barrier path: the children of each pass's candidate
     __shared__ uint32_t           s_xq[SG_NC];         // the pending tree's candidates (xq pairs), compacted
     __shared__ uint32_t           s_mask;              // its nodes
     __shared__ int                s_nv;                // its candidate count (0: the descent has ended)
@@ -1626,25 +1630,56 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         const int16_t *f0 = P.flt + (size_t)k * 2 * pn, *f1 = P.flt + (size_t)P.f1e[k] * 2 * pn + pn;
         const uint32_t gmask = (r0 ? 0x0000FFFFu : 0u) | (r1 ? 0xFFFF0000u : 0u);
         // ---- load the part: g in registers, (x - src) in LDS, the moments on the way ----
-        uint32_t           g[SR_KMAX][4];
+        // Chunk kk of this lane is chunk c = pl + kk * SR_PL of the part (row-major over 4-sample columns); its
+        // (row, column) advance by a fixed step from one kk to the next (no division per chunk).  Chunks past the part
+        // read the part's last chunk (addresses stay inside) and contribute zeros.
+        const int      dr = SR_PL / cw, dc = SR_PL - dr * cw, lastc = nch - 1, lrow = lastc / cw, lcol = lastc - lrow * cw;
+        int            crow = pl / cw, ccol = pl - crow * cw; // chunk 0 of this lane
+        auto           chunk_at = [&](int kk, int &row, int &col) {   // (row, col) of chunk kk, clamped into the part
+            row = crow, col = ccol;
+            if (pl + kk * SR_PL >= nch) row = lrow, col = lcol;
+        };
+        auto           advance = [&]() {
+            crow += dr, ccol += dc;
+            if (ccol >= cw) ccol -= cw, crow++;
+        };
+        // 1. the ep's two filter planes of every chunk, straight into g (raw int16 pairs: flt0 of pixels 0, 1 | 2, 3
+        //    then flt1 of them): every HBM read of the part in flight at once, one memory round trip per item
+        uint32_t g[SR_KMAX][4];
+#pragma unroll
+        for (int kk = 0; kk < SR_KMAX; kk++) {
+            g[kk][0] = g[kk][1] = g[kk][2] = g[kk][3] = 0u;
+            if (kk < K) { // uniform
+                int row, col;
+                chunk_at(kk, row, col);
+                const size_t fo = (size_t)(ur.v_start + it.y0 + row) * P.fstride + ur.h_start + 4 * col;
+                const uint2  a0 = *(const uint2 *)(f0 + fo), a1 = *(const uint2 *)(f1 + fo);
+                g[kk][0] = a0.x, g[kk][1] = a0.y, g[kk][2] = a1.x, g[kk][3] = a1.y;
+                advance();
+            }
+        }
+        // 2. the CDEF output and the source in groups of SR_LB chunks (the eps of a unit read them through one L2):
+        //    g formed in place, (x - src) to LDS, the moments
+        crow = pl / cw, ccol = pl - crow * cw;
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
+        constexpr int LB2 = 2; // chunks per group here: g holds every chunk already
 #pragma unroll
-        for (int kb = 0; kb < SR_KMAX; kb += SR_LB) {
+        for (int kb = 0; kb < SR_KMAX; kb += LB2) {
+            if (kb >= K) { // uniform: zeros up to the next multiple of SR_LB (sr_pass reads whole groups)
+                if (kb < ((K + SR_LB - 1) & ~(SR_LB - 1)))
 #pragma unroll
-            for (int j = 0; j < SR_LB; j++)
+                    for (int j = 0; j < LB2; j++)
+                        if (kb + j < SR_KMAX) sr_dx[(kb + j) * SR_PL + pl] = make_uint2(0u, 0u);
+                continue;
+            }
+            int2 dv2[LB2], sv2[LB2];
+            bool on[LB2];
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (kb + j < SR_KMAX) g[kb + j][q] = 0u;
-            if (kb >= K) continue; // uniform
-            int2 dv2[SR_LB], sv2[SR_LB], a0[SR_LB], a1[SR_LB];
-            bool on[SR_LB];
-#pragma unroll
-            for (int j = 0; j < SR_LB; j++) { // all loads of SR_LB chunks in flight together (addresses clamped into the part)
-                const int c = kb + j < SR_KMAX ? pl + (kb + j) * SR_PL : nch, cc = min(c, nch - 1), row = cc / cw,
-                          col = cc - row * cw;
+            for (int j = 0; j < LB2; j++) { // the group's loads in flight together
+                int row, col;
+                chunk_at(kb + j, row, col);
+                on[j] = kb + j < SR_KMAX && pl + (kb + j) * SR_PL < nch;
                 const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
-                on[j] = c < nch;
-                const size_t fo = (size_t)y * P.fstride + x;
                 if constexpr (sizeof(T) == 2) {
                     dv2[j] = *(const int2 *)(d + (size_t)y * P.dstride + x);
                     sv2[j] = *(const int2 *)(s + (size_t)y * P.sstride + x);
@@ -1652,11 +1687,10 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     dv2[j].x = *(const int *)(d + (size_t)y * P.dstride + x), dv2[j].y = 0;
                     sv2[j].x = *(const int *)(s + (size_t)y * P.sstride + x), sv2[j].y = 0;
                 }
-                a0[j] = *(const int2 *)(f0 + fo);
-                a1[j] = *(const int2 *)(f1 + fo);
+                advance();
             }
 #pragma unroll
-            for (int j = 0; j < SR_LB; j++) {
+            for (int j = 0; j < LB2; j++) {
                 const int kk = kb + j;
                 if (kk >= SR_KMAX) break;
                 int       dv[4], sv[4];
@@ -1667,10 +1701,10 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
 #pragma unroll
                     for (int q = 0; q < 4; q++) dv[q] = ((uint32_t)dv2[j].x >> (8 * q)) & 0xFF, sv[q] = ((uint32_t)sv2[j].x >> (8 * q)) & 0xFF;
                 }
-                const uint32_t fw[4] = {__builtin_amdgcn_perm((uint32_t)a1[j].x, (uint32_t)a0[j].x, 0x05040100u),
-                                        __builtin_amdgcn_perm((uint32_t)a1[j].x, (uint32_t)a0[j].x, 0x07060302u),
-                                        __builtin_amdgcn_perm((uint32_t)a1[j].y, (uint32_t)a0[j].y, 0x05040100u),
-                                        __builtin_amdgcn_perm((uint32_t)a1[j].y, (uint32_t)a0[j].y, 0x07060302u)};
+                const uint32_t fw[4] = {__builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x05040100u),
+                                        __builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x07060302u),
+                                        __builtin_amdgcn_perm(g[kk][3], g[kk][1], 0x05040100u),
+                                        __builtin_amdgcn_perm(g[kk][3], g[kk][1], 0x07060302u)};
                 uint32_t m0 = 0, m1 = 0; // <= 4 g^2 < 2^32
                 int      m3 = 0, m4 = 0; // |4 g s| < 2^31
 #pragma unroll
@@ -1700,6 +1734,36 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         // diagnostics (stat): pixel wave 0's pass time (B2/B4 release to its arrival at B3) and its wait from B3 to the
         // B4 release
         unsigned long long tpass = 0, twait = 0, tmark = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
+            // One barrier per pass: every pixel wave takes the outcome itself from the pass's wave partials and the
+            // two children the control wave prepared during the pass (the control wave decides identically and
+            // steps the descent while the next pass runs)
+            uint32_t xq   = __builtin_amdgcn_readfirstlane(s_xq[0]);
+            bool     live = __builtin_amdgcn_readfirstlane(s_nv) != 0;
+            for (int pass = 1; live; pass++) {
+                const uint32_t xl[1] = {xq};
+                sr_pass<1>(g, sr_dx, pl, K, 1, xl, s_red2[pass & 1]);
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    tpass += t - tmark, tmark = t;
+                }
+                __syncthreads(); // B3: the pass's errors and the candidate's children are in LDS
+                unsigned long long e0 = 0;
+#pragma unroll
+                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
+                const uint32_t *ch    = s_ch[pass & 1];
+                const long long err   = (long long)(((unsigned long long)ch[5] << 32) | ch[4]);
+                const bool      worse = !ch[6] && (long long)e0 > err;
+                live = (worse ? ch[2] : ch[3]) && pass <= SR_MAX_PASSES;
+                xq   = worse ? ch[0] : ch[1];
+                xq   = __builtin_amdgcn_readfirstlane(xq);
+                live = __builtin_amdgcn_readfirstlane((int)live) != 0;
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    twait += t - tmark, tmark = t;
+                }
+            }
+        } else
         for (;;) {
             const int nv = __builtin_amdgcn_readfirstlane(s_nv);
             if (nv == 0) break;
@@ -1753,6 +1817,42 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         Descent D = uniform(sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg));
         D.next(); // the seed itself is the first candidate
         sr_tree_publish(D, ok, nodes, s_xq, &s_mask, &s_nv);
+        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
+            // the one-barrier path (see the pixel waves): the children of each pending candidate go to s_ch by pass
+            // parity before the pass's barrier; after it the outcome is taken exactly as the pixel waves take it
+            auto publish_children = [&](int pass) {
+                uint32_t xw = 0, xb = 0;
+                bool     okw = false, okb = false;
+                sr_children(D, xw, okw, xb, okb);
+                if (lane == 0) {
+                    uint32_t *ch = s_ch[pass & 1];
+                    ch[0] = xw, ch[1] = xb, ch[2] = okw, ch[3] = okb;
+                    ch[4] = (uint32_t)(unsigned long long)D.err, ch[5] = (uint32_t)((unsigned long long)D.err >> 32);
+                    ch[6] = D.init;
+                }
+            };
+            bool live = ok;
+            if (live) publish_children(1);
+            __syncthreads(); // B2
+            int pass = 1;
+            for (; live; pass++) {
+                __syncthreads(); // B3
+                const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+                ncp += (unsigned long long)nch * 4;
+                unsigned long long e0 = 0;
+#pragma unroll
+                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
+                D.report((int64_t)e0);
+                live = D.next();
+                if (pass > SR_MAX_PASSES) {
+                    if (lane == 0) atomicOr(status, 1);
+                    live = false;
+                }
+                if (live) publish_children(pass + 1); // during the next pass
+                if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
+            }
+            if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
+        } else {
         __syncthreads(); // B2
         for (int pass = 1;; pass++) {
             const int nv = __builtin_amdgcn_readfirstlane(s_nv);
@@ -1812,6 +1912,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
             if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
             __syncthreads(); // B4
             if (stat && lane == 0 && s_nv == 0) atomicAdd(stat + 1, (unsigned long long)pass);
+        }
         }
         if (lane == 0 && it.part == 0) ds[it.pair] = D;
         if (stat && lane == 0) {
@@ -2387,6 +2488,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         sr_xmode = 0x100u | (++s->sx_epoch & 0xFFu);
     }
+    static const bool sr_two_barriers = [] { // SVTGPU_SR_1B=0: one-part items take the two-barrier path too (A/B)
+        const char *e = std::getenv("SVTGPU_SR_1B");
+        return e && !std::strcmp(e, "0");
+    }();
+    if (sr_two_barriers) sr_xmode |= 0x200u;
     static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *sr_stat = nullptr;
     if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 128));

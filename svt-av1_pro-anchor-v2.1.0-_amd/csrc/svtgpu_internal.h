@@ -67,6 +67,20 @@ static inline FrameGeo frame_geo(int32_t w, int32_t h) {
     return g;
 }
 
+// A high-priority lane for a call's latency-bound launch chains (the CDEF pick's 41 dependent steps, the DLF level
+// search's trial launches): the work forks from the caller's stream onto a stream of the greatest priority and joins
+// back, so stream order for the caller is unchanged, and the dispatcher hands those small launches the next free CU
+// slots instead of queueing them behind other frames' resident kernels.  Opt-in (SVTGPU_HIPRIO=1): measured slower
+// (runtime.hip).
+struct SvtGpuPrioLane {
+    hipStream_t hs   = nullptr;
+    hipEvent_t  fork = nullptr, join = nullptr;
+};
+// the stream to launch on (the lane's, or `st` itself when the lane is off); svtgpu_prio_leave joins it back into st
+int  svtgpu_prio_enter(SvtGpuPrioLane *l, hipStream_t st, hipStream_t *out);
+int  svtgpu_prio_leave(SvtGpuPrioLane *l, hipStream_t hs, hipStream_t st);
+void svtgpu_prio_destroy(SvtGpuPrioLane *l);
+
 // persistent pick exchange (cdef_pick.hip): [64 chunks][4 chains][4096] partial sums, [4][64][2] row minima,
 // then status and diagnostics words
 #define SVTGPU_PICK_XCH_BYTES ((size_t)(64 * 4 * 4096 + 4 * 64 * 2 + 16) * 8)
@@ -105,6 +119,7 @@ struct SvtGpuCdefFrameState {
     int8_t        *d_fb_kind;     // [nfb] SB128 areas (cdef_sb128.hip); null = SB64
     int8_t        *h_fb_kind;     // host copy
     uint8_t       *d_mse_rem;     // [3][nfb][64] remainders of the per-FB distortion shift (SB128 only)
+    SvtGpuPrioLane prio;          // the pick's launch chain
 };
 
 // Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
