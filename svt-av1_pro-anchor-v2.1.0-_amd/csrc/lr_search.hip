@@ -100,6 +100,12 @@ typedef short v2i16 __attribute__((ext_vector_type(2)));
 __device__ inline int dot2(uint32_t a, uint32_t b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2i16, a), __builtin_bit_cast(v2i16, b), c, false);
 }
+// clamp of a lane value to [0, hi] (hi wave-uniform) in one instruction (the compiler emits a max and a min)
+__device__ inline int clamp0_s(int v, int hi_uniform) {
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "s"(hi_uniform));
+    return r;
+}
 // the same with a wave-uniform accumulator input held in an SGPR: the VOP3P form, where the compiler would copy a
 // constant into the destination of an accumulating v_dot2c for every call
 __device__ inline int dot2_s(uint32_t a, uint32_t b, int c_uniform) {
@@ -986,10 +992,18 @@ __device__ inline void wr_fetch(const uint32_t *win, int ws, const PlaneArgs &P,
 template <typename T, bool LDSW>
 __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, const uint32_t *win, int ws, int ux,
                        int uy, int w, int h, const WrItem &it, unsigned long long *xch, int *s_mode, int16_t *s_taps,
-                       unsigned long long *s_part, int32_t *status, unsigned long long &npx) {
+                       unsigned long long *s_part, int32_t *status, unsigned long long &npx, unsigned long long *stat) {
+    // diagnostics (SVTGPU_WR_STATS): thread 0's pass time (candidate start to the first barrier), its control step
+    // and the whole descent, in 100 MHz ticks, kept in LDS ({run start, pass, control, mark}: no registers)
+    __shared__ unsigned long long s_wt[6];
+    __shared__ uint32_t           s_wp[WR_NT / 64]; // each wave's pass time of the current candidate
+    if (stat && threadIdx.x == 0)
+        s_wt[0] = s_wt[3] = __builtin_amdgcn_s_memrealtime(), s_wt[1] = s_wt[2] = s_wt[4] = s_wt[5] = 0;
     const WrGeo g  = wr_geo(w, h);
-    const int   cp = threadIdx.x % g.cpw, sg = threadIdx.x / g.cpw, x = 2 * cp;
-    const int   seg0 = sg * g.R, nrows = sg < g.nseg ? max(0, min(g.R, h - seg0)) : 0;
+    // a wave holds 64 column pairs of one row segment (cpw is a multiple of 64): the segment's values are wave-uniform,
+    // which readfirstlane tells the compiler -- the row loop then branches on scalars instead of masking lanes
+    const int   cp = threadIdx.x % g.cpw, sg = __builtin_amdgcn_readfirstlane((int)threadIdx.x / g.cpw), x = 2 * cp;
+    const int   seg0 = sg * g.R, nrows = __builtin_amdgcn_readfirstlane(sg < g.nseg ? max(0, min(g.R, h - seg0)) : 0);
     const int   xc = min(x, (w - 1) & ~1), hw = h + 6; // an addressable column for lanes right of the unit
     const uint32_t dmask = x >= w ? 0u : x + 1 >= w ? 0xFFFFu : 0xFFFFFFFFu;
     // the lane's source pixels, one (x, x+1) pair per row: registers (LDS mode, <= WR_RMAX rows), else global memory
@@ -1021,30 +1035,30 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
         const uint32_t Ho0 = sp(hf[0], hf[1]), Ho1 = sp(hf[2], hf[3]), Ho2 = sp(hf[4], hf[5]), Ho3 = sp(hf[6], 0);
         const uint32_t Ve0 = sp(vf[0], vf[1]), Ve1 = sp(vf[2], vf[3]), Ve2 = sp(vf[4], vf[5]), Ve3 = sp(vf[6], 0);
         const uint32_t Vo0 = sp(0, vf[0]), Vo1 = sp(vf[1], vf[2]), Vo2 = sp(vf[3], vf[4]), Vo3 = sp(vf[5], vf[6]);
-        auto hclip = [&](int s) { return min(max(s >> rr.r0, 0), lim); };
-        auto vclip = [&](int s) { return min(max(s >> rr.r1, 0), maxv); };
+        auto hclip = [&](int s) { return clamp0_s(s >> rr.r0, lim); };
+        auto vclip = [&](int s) { return clamp0_s(s >> rr.r1, maxv); };
         uint32_t hq0[4] = {0, 0, 0, 0}, hq1[4] = {0, 0, 0, 0}; // vertical pairs of the horizontal pass, x and x+1
         uint32_t pa[5], pb[5], na[5], nb[5];
         int      e = 0; // <= 2 * 77 squared errors of <= 1023^2
         // step j: the horizontal pass of window rows seg0+2j, +1 (unit rows seg0+2j-3, -2) at columns x, x+1 (pa, pb);
         // from j = 3 on, output rows seg0+2i, +1 (i = j-3) from horizontal rows 2i-3 .. 2i+4 against source pairs sa, sb
         auto step = [&](int j, uint32_t sa, uint32_t sb) {
-            const int a0 = hclip(dot2(pa[3], He3, dot2(pa[2], He2, dot2(pa[1], He1, dot2(pa[0], He0, hb)))));
-            const int b0 = hclip(dot2(pa[4], Ho3, dot2(pa[3], Ho2, dot2(pa[2], Ho1, dot2(pa[1], Ho0, hb)))));
-            const int a1 = hclip(dot2(pb[3], He3, dot2(pb[2], He2, dot2(pb[1], He1, dot2(pb[0], He0, hb)))));
-            const int b1 = hclip(dot2(pb[4], Ho3, dot2(pb[3], Ho2, dot2(pb[2], Ho1, dot2(pb[1], Ho0, hb)))));
+            const int a0 = hclip(dot2(pa[3], He3, dot2(pa[2], He2, dot2(pa[1], He1, dot2_s(pa[0], He0, hb)))));
+            const int b0 = hclip(dot2(pa[4], Ho3, dot2(pa[3], Ho2, dot2(pa[2], Ho1, dot2_s(pa[1], Ho0, hb)))));
+            const int a1 = hclip(dot2(pb[3], He3, dot2(pb[2], He2, dot2(pb[1], He1, dot2_s(pb[0], He0, hb)))));
+            const int b1 = hclip(dot2(pb[4], Ho3, dot2(pb[3], Ho2, dot2(pb[2], Ho1, dot2_s(pb[1], Ho0, hb)))));
             hq0[0] = hq0[1], hq0[1] = hq0[2], hq0[2] = hq0[3], hq0[3] = pack2(a0, a1);
             hq1[0] = hq1[1], hq1[1] = hq1[2], hq1[2] = hq1[3], hq1[3] = pack2(b0, b1);
             if (j >= 3) {
                 const int i  = j - 3;
-                const int o0 = vclip(dot2(hq0[3], Ve3, dot2(hq0[2], Ve2, dot2(hq0[1], Ve1, dot2(hq0[0], Ve0, vb)))));
-                const int o1 = vclip(dot2(hq1[3], Ve3, dot2(hq1[2], Ve2, dot2(hq1[1], Ve1, dot2(hq1[0], Ve0, vb)))));
+                const int o0 = vclip(dot2(hq0[3], Ve3, dot2(hq0[2], Ve2, dot2(hq0[1], Ve1, dot2_s(hq0[0], Ve0, vb)))));
+                const int o1 = vclip(dot2(hq1[3], Ve3, dot2(hq1[2], Ve2, dot2(hq1[1], Ve1, dot2_s(hq1[0], Ve0, vb)))));
                 const uint32_t d0 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(o0, o1)) -
                                                                           __builtin_bit_cast(v2i16, sa)) & dmask;
                 e = dot2(d0, d0, e);
                 if (2 * i + 1 < nrows) {
-                    const int q0 = vclip(dot2(hq0[3], Vo3, dot2(hq0[2], Vo2, dot2(hq0[1], Vo1, dot2(hq0[0], Vo0, vb)))));
-                    const int q1 = vclip(dot2(hq1[3], Vo3, dot2(hq1[2], Vo2, dot2(hq1[1], Vo1, dot2(hq1[0], Vo0, vb)))));
+                    const int q0 = vclip(dot2(hq0[3], Vo3, dot2(hq0[2], Vo2, dot2(hq0[1], Vo1, dot2_s(hq0[0], Vo0, vb)))));
+                    const int q1 = vclip(dot2(hq1[3], Vo3, dot2(hq1[2], Vo2, dot2(hq1[1], Vo1, dot2_s(hq1[0], Vo0, vb)))));
                     const uint32_t d1 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(q0, q1)) -
                                                                               __builtin_bit_cast(v2i16, sb)) & dmask;
                     e = dot2(d1, d1, e);
@@ -1087,7 +1101,15 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
         // the unit's SSE, then lane 0's descent step
         const unsigned long long et = wave_sum_u32_wide((uint32_t)e);
         if ((threadIdx.x & 63) == WAVE_LAST) s_part[threadIdx.x >> 6] = et;
+        if (stat && (threadIdx.x & 63) == 0) s_wp[threadIdx.x >> 6] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - s_wt[3]);
+        if (stat && threadIdx.x == 0) s_wt[1] += __builtin_amdgcn_s_memrealtime() - s_wt[3];
         __syncthreads();
+        if (stat && threadIdx.x == 0) {
+            uint32_t mx = 0, mn = ~0u;
+            for (int q = 0; q < WR_NT / 64; q++) mx = max(mx, s_wp[q]), mn = min(mn, s_wp[q]);
+            s_wt[4] += mx, s_wt[5] += mn;
+            s_wt[3] = __builtin_amdgcn_s_memrealtime();
+        }
         if (threadIdx.x == 0) {
             // the descent step is the unit's serial critical path: its wave issues ahead of the other workgroups'
             // pixel waves on this SIMD while it runs
@@ -1130,14 +1152,24 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
             }
             __builtin_amdgcn_s_setprio(0);
         }
+        if (stat && threadIdx.x == 0) s_wt[2] += __builtin_amdgcn_s_memrealtime() - s_wt[3];
         __syncthreads();
+        if (stat && threadIdx.x == 0) s_wt[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (stat && threadIdx.x == 0) {
+        atomicAdd(stat + 0, 1ull), atomicAdd(stat + 1, (unsigned long long)rounds);
+        atomicAdd(stat + 2, __builtin_amdgcn_s_memrealtime() - s_wt[0]), atomicAdd(stat + 3, s_wt[2]);
+        atomicAdd(stat + 4, s_wt[1]), atomicAdd(stat + 5, (unsigned long long)w * h);
+        atomicAdd(stat + 6, (unsigned long long)(it.nparts > 1)), atomicAdd(stat + 7, s_wt[4]);
+        atomicAdd(stat + 8, s_wt[5]);
     }
 }
 
 template <typename T>
 __global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, Descent *ds, const WrItem *items,
                                                            int lds_cap, unsigned long long *xch, int32_t *status,
-                                                           unsigned long long *pc, unsigned long long *tk) {
+                                                           unsigned long long *pc, unsigned long long *stat,
+                                                           unsigned long long *tk) {
     PROF_BEGIN(tk);
     extern __shared__ uint32_t wr_win[]; // the part's CDEF window (LDS mode)
     __shared__ uint64_t           s_draw[sizeof(Descent) / 8];
@@ -1174,8 +1206,8 @@ __global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, D
     }
     __syncthreads();
     unsigned long long npx = 0;
-    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx);
-    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx);
+    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat);
+    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat);
     if (threadIdx.x == 0 && it.part == 0) ds[u] = D;
     if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
     PROF_END(tk);
@@ -2493,6 +2525,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         return e && !std::strcmp(e, "0");
     }();
     if (sr_two_barriers) sr_xmode |= 0x200u;
+    static const bool   wr_stats = std::getenv("SVTGPU_WR_STATS") != nullptr; // per-search diagnostics to stderr
+    static unsigned long long *wr_stat = nullptr;
+    if (wr_stats && !wr_stat) HIP_TRY(hipMalloc(&wr_stat, 128));
+    if (wr_stat) HIP_TRY(hipMemsetAsync(wr_stat, 0, 128, st));
     static const bool   sr_stats = std::getenv("SVTGPU_SR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *sr_stat = nullptr;
     if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 128));
@@ -2559,7 +2595,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         run(2, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
                                (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa ? qa + q_wrx : nullptr),
-                               (int32_t *)dp(o_wstat), pc, tk);
+                               (int32_t *)dp(o_wstat), pc, wr_stat, tk);
         });
         HIP_TRY(hipGetLastError());
     }
@@ -2599,6 +2635,15 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener descent: round bound or part exchange timed out",
                                   __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;
+    }
+    if (n_wr && wr_stat) {
+        unsigned long long v[16];
+        HIP_TRY(hipMemcpy(v, wr_stat, 128, hipMemcpyDeviceToHost));
+        const double n = (double)std::max(1ull, v[0]), r = (double)std::max(1ull, v[1]);
+        std::fprintf(stderr, "wiener_res: %llu items (%llu parted), %.1f candidates/item, %.0f px/item, per candidate: "
+                     "%.2f us (thread 0: pass %.2f us, control %.2f us; wave passes: slowest %.2f us, fastest %.2f "
+                     "us)\n", v[0], v[6], v[1] / n, v[5] / n, v[2] / r * 0.01, v[4] / r * 0.01, v[3] / r * 0.01,
+                     v[7] / r * 0.01, v[8] / r * 0.01);
     }
     if (n_sr && sr_stat) {
         unsigned long long v[16];
