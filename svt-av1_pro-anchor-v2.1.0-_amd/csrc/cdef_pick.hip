@@ -39,6 +39,7 @@ struct StepArgs {
     int32_t        *lev;    // [NSTEPS+1][4][32] selection list entering each call
     int32_t        *fin;    // [4][32] final list per chain
     uint64_t       *best;   // [4] value returned by each chain's last call
+    uint64_t       *val;    // [NSTEPS+1][4] value of the call before each step (the period shortcut's copy source)
     StepChain       ch[MAX_CHAINS];
     unsigned long long *wgclk; // diagnostics or null
 };
@@ -137,7 +138,24 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
     const int f0 = ty * A.chunk;
     uint64_t *sbest = dyn + (size_t)A.chunk * 128;
-    // 0. every global load of the step issued before anything waits on one: the previous call's totals, this
+    // the period shortcut.  A chain's refinement calls (EbEncCdef.c:714-726) are a deterministic function of the
+    // ordered selection entering them (entries [0, nb - 1) of lev[s]); once the selection entering call s equals the
+    // one entering call s - nb, calls s, s + 1, ... repeat calls s - nb, ... result for result (the greedy loop has
+    // settled into re-adding what it drops), so they are copied instead of recomputed: every workgroup reads the same
+    // two lists and makes the same decision.  lp = lev[s - 1 - nb] (the previous call's period twin), lr = lev[s - nb]
+    // (whose slot nb - 1 holds the twin's result).  These loads go first: a repeat is known as soon as they land, and
+    // then only the chain's lead workgroup stays (to write the step's list and value; no other has work)
+    const int s = A.step, nb = C.nb;
+    int       lcur = 0, lp = 0, lr = 0;
+    const bool chk_prev = C.prev_nb_sel >= 0 && s - 1 - nb >= nb, chk_cur = C.nb_sel >= 0 && s - nb >= nb;
+    if ((t & 63) < 32) {
+        if (chk_prev) {
+            lcur = A.lev[((size_t)(s - 1) * MAX_CHAINS + c) * 32 + (t & 31)];
+            lp   = A.lev[((size_t)(s - 1 - nb) * MAX_CHAINS + c) * 32 + (t & 31)];
+        }
+        if (chk_prev || chk_cur) lr = A.lev[((size_t)(s - nb) * MAX_CHAINS + c) * 32 + (t & 31)];
+    }
+    // 0. then every other global load of the step, issued before anything waits on one: the previous call's totals, this
     // workgroup's FB chunk (clamped into the allocated table, not the live count, so no load waits for the count)
     // and the live count and width flag.  The chunk stays in named registers (not an array: VGPRs, not scratch)
     // through the argmin and lands in LDS after it (<= PICK_CHUNK * 64 / NT each)
@@ -153,23 +171,36 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
 #define LD(u) const uint4 v##u = src[min(t + (u) * NT, lim)];
     LD(0) LD(1) LD(2) LD(3) LD(4) LD(5) LD(6) LD(7) LD(8) LD(9) LD(10) LD(11)
 #undef LD
-    const int nfb  = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
-    const int wide = *A.wide;
+    const int  nfb  = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
+    const int  wide = *A.wide;
+    const bool in_state = (t & 15) < nb - 1 && (t & 63) < 32; // lanes holding entries [0, nb - 1) of both halves
+    const bool prev_rep = chk_prev && !__ballot(in_state && lcur != lp);
+    if (prev_rep && !lead) return; // a repeated previous call makes this one a repeat too
     wgclk_mark(A.wgclk, 1);
     // 1. selection entering this call
     if (t < 32) sl[t] = A.step ? A.lev[((size_t)(A.step - 1) * MAX_CHAINS + c) * 32 + t] : 0;
     if (C.prev_nb_sel >= 0) {
-        tot_argmin(tv, A.start_gi, A.end_gi, bv, bi);
-        if (t == 0) {
+        uint64_t pv;
+        int      pj, pk;
+        if (prev_rep) { // the previous call repeated its twin: the twin's result and value
+            pj = __shfl(lr, nb - 1), pk = __shfl(lr, 16 + nb - 1);
+            pv = A.val[(size_t)(s - nb) * MAX_CHAINS + c];
+        } else {
+            tot_argmin(tv, A.start_gi, A.end_gi, bv, bi);
             const bool any = bi[0] < (1 << 30); // no candidate: (1 << 63, 0, 0) like the reference
-            sl[C.prev_nb_sel]      = any ? bi[0] >> 6 : 0;
-            sl[16 + C.prev_nb_sel] = any ? bi[0] & 63 : 0;
+            pj = any ? bi[0] >> 6 : 0, pk = any ? bi[0] & 63 : 0;
+            pv = any ? bv[0] : ((uint64_t)1 << 63);
+        }
+        if (t == 0) {
+            sl[C.prev_nb_sel]      = pj;
+            sl[16 + C.prev_nb_sel] = pk;
             if (C.prev_shift)
                 for (int q = 0; q < C.nb - 1; q++) {
                     sl[q]      = sl[q + 1];
                     sl[16 + q] = sl[16 + q + 1];
                 }
-            if (lead && C.nb_sel < 0) A.best[c] = any ? bv[0] : ((uint64_t)1 << 63);
+            if (lead) A.val[(size_t)s * MAX_CHAINS + c] = pv;
+            if (lead && C.nb_sel < 0) A.best[c] = pv;
         }
     }
     if (nfb > 0) {
@@ -186,6 +217,8 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     }
     wgclk_mark(A.wgclk, 2);
     if (lead && t < 32) A.lev[((size_t)A.step * MAX_CHAINS + c) * 32 + t] = sl[t];
+    // this call repeats its twin: nothing to accumulate (nor to zero: the chain's later calls repeat too)
+    if (chk_cur && !__ballot(in_state && sl[t & 31] != lr)) return;
     // 2. zero this workgroup's slice of the accumulator used by the next step
     {
         uint64_t *nxt = A.tot + ((size_t)((A.step + 1) % 3) * MAX_CHAINS + c) * 4096;
@@ -565,7 +598,8 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     const char *pe      = std::getenv("SVTGPU_PICK_PERSIST");
     const bool  persist = pe && pe[0] == '1' && nfb <= PS_NCH * PS_CH;
     int32_t    *d_inv   = s->d_fb_list + nfb + 1;
-    A.tot               = wmse + wmse_elems; // [3][4][4096]
+    A.tot               = wmse + wmse_elems;                          // [3][4][4096]
+    A.val               = A.tot + (size_t)3 * MAX_CHAINS * 4096;      // [NSTEPS+1][4]
     hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count,
                        (int32_t *)A.wide, d_inv);
     const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device

@@ -948,7 +948,8 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
     for (int c = 0; c < 2 && e == hipSuccess; c++)
         for (int d = 0; d < 2 && e == hipSuccess; d++)
             e = hipMalloc(&s->d_rec[c][d], sizeof(uint32_t) * s->uw[c] * s->uh[c]);
-    if (e == hipSuccess) e = hipMalloc(&s->d_scratch, (size_t)width * height * 2);
+    if (e == hipSuccess) // the three planes' copies for an in-place apply
+        e = hipMalloc(&s->d_scratch, ((size_t)width * height + 2 * (size_t)((width + 1) >> 1) * ((height + 1) >> 1)) * 2);
     if (e == hipSuccess) e = hipMalloc(&s->d_sse, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS);
     if (e == hipSuccess) e = hipMalloc(&s->d_arrive, sizeof(unsigned int));
     if (e == hipSuccess) e = hipMemset(s->d_sse, 0, sizeof(unsigned long long) * MAX_JOBS * MAX_TRIALS);
@@ -1062,7 +1063,8 @@ extern "C" int svtgpu_dlf_set_tile(SvtGpuDlfState *s, const int32_t sse_rect[4],
 }
 
 namespace {
-// filter planes [ps, pe) of `in` into `out`; in == out is allowed (the plane is staged in scratch)
+// filter planes [ps, pe) of `in` into `out`, the filtered planes in one launch (one job per plane); in == out is
+// allowed (the planes are staged in scratch)
 int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
                    int32_t ps, int32_t pe, hipStream_t st) {
     if (s->mi_on_device) { // a device grid no pick has reported on (the FROM_Q levels): its verdict first
@@ -1072,7 +1074,9 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
     }
     LevelTables L;
     build_level_tables(*params, L);
-    bool luma_off = false;
+    bool        luma_off = false;
+    DlfTileArgs a        = base_args(in, L);
+    size_t      sc_off   = 0; // bytes of scratch used by earlier planes
     for (int pl = ps; pl < pe; pl++) {
         if (pl == 0 && !plane_active(*params, 0)) luma_off = true; // no plane is filtered (:575-577)
         const size_t bps = in->bytes_per_sample;
@@ -1087,14 +1091,16 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
             }
             continue;
         }
-        DlfTileArgs  a = base_args(in, L);
-        DlfPlaneJob &J = a.job[0];
+        DlfPlaneJob &J = a.job[a.njob];
         J              = plane_job(s, in, pl, false);
-        a.njob         = 1;
+        if (!J.tiles) continue;
+        a.njob++;
         if (in == out) {
-            HIP_TRY(hipMemcpy2DAsync(s->d_scratch, in->pw[pl] * bps, in->plane[pl], in->stride[pl] * bps,
+            void *sc = (uint8_t *)s->d_scratch + sc_off;
+            sc_off += (size_t)in->pw[pl] * in->ph[pl] * bps;
+            HIP_TRY(hipMemcpy2DAsync(sc, in->pw[pl] * bps, in->plane[pl], in->stride[pl] * bps,
                                      in->pw[pl] * bps, in->ph[pl], hipMemcpyDeviceToDevice, st));
-            J.src        = s->d_scratch;
+            J.src        = sc;
             J.src_stride = in->pw[pl];
         } else {
             J.src        = in->plane[pl];
@@ -1104,9 +1110,8 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
         J.dst_stride = out->stride[pl];
         J.ntrial     = 1;
         for (int dir = 0; dir < 2; dir++) std::memcpy(J.lvl[0][dir], L.lvl[pl][dir], 128);
-        int rc = launch_tile(a, (int)bps, false, st);
-        if (rc) return rc;
     }
+    if (a.njob) return launch_tile(a, (int)in->bytes_per_sample, false, st);
     return SVTGPU_OK;
 }
 } // namespace

@@ -110,15 +110,26 @@ struct LrPlaneArgs {
     const SvtGpuRestUnit *units;
 };
 
+// the filtered planes of one frame in one launch: the planes' tile grids back to back (fewer launch boundaries and
+// one tail instead of three for a kernel of ~20 us per plane)
+struct LrApplyArgs {
+    LrPlaneArgs pl[3];
+    int32_t     nplanes, end[3]; // end[i]: first block past plane i of the launch
+};
+
 template <typename T>
-__global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrPlaneArgs a) {
+__global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrApplyArgs args) {
+    int pi = 0;
+    while (pi + 1 < args.nplanes && (int)blockIdx.x >= args.end[pi]) pi++;
+    const LrPlaneArgs &a   = args.pl[pi];
+    const int          blk = (int)blockIdx.x - (pi ? args.end[pi - 1] : 0);
     __shared__ __attribute__((aligned(16))) uint16_t v[VR * VS];
     // a unit is Wiener or self-guided: the Wiener intermediate (VR x TW u16) shares the A/B arrays' LDS
     __shared__ int      AB[2][(TH + 2) * (TW + 2)];
     static_assert(VR * TW * 2 <= sizeof(int) * (TH + 2) * (TW + 2), "Wiener intermediate in AB[0]");
     uint16_t *t = (uint16_t *)AB[0];
     const int S = 64 >> a.ss, off = 8 >> a.ss, cwmax = 64 >> a.ss;
-    const int k = a.k0 + blockIdx.x / a.nc, c = a.c0 + blockIdx.x % a.nc;
+    const int k = a.k0 + blk / a.nc, c = a.c0 + blk % a.nc;
     const int y0 = max(0, k * S - off), y1 = min((k + 1) * S - off, a.H);
     const int x0 = c * cwmax, w = min(cwmax, a.W - x0), h = y1 - y0;
     if (h <= 0 || w <= 0) return;
@@ -372,6 +383,9 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
     if (cdef_out->bit_depth != 8 && cdef_out->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
     hipStream_t  st  = pick_stream(s->ctx, stream);
     const size_t bps = cdef_out->bytes_per_sample;
+    LrApplyArgs  L;
+    L.nplanes = 0;
+    int nblk  = 0;
     for (int p = 0; p < 3; p++) {
         const int32_t *r = s->tile_out[p]; // the samples written (the whole plane unless tiled over GPUs)
         if (frame_type[p] == SVTGPU_RESTORE_NONE) {
@@ -381,7 +395,7 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
                                      (r[2] - r[0]) * bps, r[3] - r[1], hipMemcpyDeviceToDevice, st));
             continue;
         }
-        LrPlaneArgs a;
+        LrPlaneArgs &a = L.pl[L.nplanes];
         a.dlf         = deblocked->plane[p];
         a.cdef        = cdef_out->plane[p];
         a.out         = out->plane[p];
@@ -401,13 +415,15 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
         // the rect is a union of whole (stripe, chunk) tiles (svtgpu_lr_set_tile checks)
         a.k0 = (r[1] + off) / S, a.c0 = r[0] / cw, a.nc = (r[2] + cw - 1) / cw - a.c0;
         const int nk = (r[3] + off + S - 1) / S - a.k0;
-        const dim3 grid(nk * a.nc);
-        if (bps == 2)
-            hipLaunchKernelGGL(lr_apply_kernel<uint16_t>, grid, dim3(NTHR), 0, st, a);
-        else
-            hipLaunchKernelGGL(lr_apply_kernel<uint8_t>, grid, dim3(NTHR), 0, st, a);
-        HIP_TRY(hipGetLastError());
+        nblk += nk * a.nc;
+        L.end[L.nplanes++] = nblk;
     }
+    if (!nblk) return SVTGPU_OK;
+    if (bps == 2)
+        hipLaunchKernelGGL(lr_apply_kernel<uint16_t>, dim3(nblk), dim3(NTHR), 0, st, L);
+    else
+        hipLaunchKernelGGL(lr_apply_kernel<uint8_t>, dim3(nblk), dim3(NTHR), 0, st, L);
+    HIP_TRY(hipGetLastError());
     return SVTGPU_OK;
 }
 

@@ -285,3 +285,65 @@ def test_cdef_pick_all_or_almost_all_skipped(ctx, frac, persist, monkeypatch):
     oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
     assert prm.as_tuple() == oprm.as_tuple()
     assert np.array_equal(fbs, ofbs)
+
+
+def _settle_calls(mse, skip, end=64):
+    """First call of each greedy chain (nb = 1, 2, 4, 8; EbEncCdef.c:697-727) whose ordered selection repeats the
+    one nb calls earlier -- from there on the device copies the chain's calls instead of recomputing them (the
+    period shortcut in sod_step_kernel); None if the chain never settles.  numpy, for the coverage bookkeeping of
+    the test below only."""
+    keep = skip == 0
+    m0 = mse[0][keep][:, :end].astype(np.int64)
+    m1 = mse[1][keep][:, :end].astype(np.int64)
+    V = m0[:, :, None] + m1[:, None, :]
+    out = []
+    for c in range(4):
+        nb, sl, lev, res, first = 1 << c, [0] * 32, [], None, None
+        for s in range(5 * nb + 1):
+            if s > 0:
+                prev = min(s - 1, nb - 1)
+                sl[prev], sl[16 + prev] = res
+                if nb <= s < 5 * nb:
+                    sl[:nb - 1], sl[16:16 + nb - 1] = sl[1:nb], sl[17:16 + nb]
+            lev.append(list(sl))
+            if s == 5 * nb:
+                break
+            nsel = min(s, nb - 1)
+            if first is None and s - nb >= nb and all(lev[s][q] == lev[s - nb][q] and lev[s][16 + q] == lev[s - nb][16 + q]
+                                                      for q in range(nb - 1)):
+                first = s
+            b = (np.full(m0.shape[0], 1 << 62, np.int64) if nsel == 0 else
+                 np.min(np.stack([m0[:, sl[q]] + m1[:, sl[16 + q]] for q in range(nsel)]), axis=0))
+            e = int(np.argmin(np.minimum(V, b[:, None, None]).sum(0)))
+            res = (e // end, e % end)
+        out.append(first)
+    return out
+
+
+def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch):
+    """The launch-per-step pick's period shortcut: convex per-FB strength curves (random optimum and scale per FB)
+    whose greedy chains settle at different calls -- and, for some seeds, never -- bit-exact vs the oracle, the
+    pick repeated on the same state (the step values of the previous pick stay behind)."""
+    import torch
+    monkeypatch.setenv("SVTGPU_PICK_PERSIST", "0")
+    w, h, q, lam = 1920, 1080, 128, 60000
+    ctrls = svtgpu.cdef_controls(1)
+    st = svtgpu.CdefState(ctx, w, h)
+    seen = set()
+    for seed in range(6):
+        rng = np.random.default_rng(seed)
+        j = np.arange(64)
+        opt = rng.integers(0, 64, size=(2, st.nfb, 1))
+        scale = rng.integers(1 << 10, 1 << 20, size=(2, st.nfb, 1))
+        mse = (scale * (64 + (j - opt) ** 2) + rng.integers(0, 1 << 12, size=(2, st.nfb, 64))).astype(np.uint64)
+        skip = (rng.random(st.nfb) < 0.1).astype(np.uint8)
+        seen.update(x is None for x in _settle_calls(mse, skip)[1:])
+        mse_t = torch.from_numpy(mse.view(np.int64)).cuda()
+        skip_t = torch.from_numpy(skip).cuda()
+        st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+        torch.cuda.synchronize()
+        oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
+        for _ in range(2):
+            prm, fbs = st.pick(ctrls, q, lam)
+            assert prm.as_tuple() == oprm.as_tuple() and np.array_equal(fbs, ofbs), seed
+    assert seen == {True, False}  # settled and unsettled chains both covered
