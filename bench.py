@@ -73,8 +73,12 @@ def pmc_summary(path, kernel, bd):
         summary = json.load(open(path))
     except (OSError, ValueError):
         return {}, None
-    name = kernel + ("<unsigned short>" if bd > 8 else "<unsigned char>")
-    k = summary.get("kernels", {}).get(name)
+    ty = "unsigned short" if bd > 8 else "unsigned char"
+    ks = summary.get("kernels", {})
+    k = ks.get("%s<%s>" % (kernel, ty))
+    if not k:  # a kernel with more template arguments (sgr_res_kernel<T, TREE>): the instance that ran most
+        cand = [v for n, v in ks.items() if n.startswith("%s<%s," % (kernel, ty))]
+        k = max(cand, key=lambda v: v.get("launches", 0)) if cand else None
     if not k:
         return {}, None
     return k, "%s (%s; %d launches)" % (os.path.relpath(path, ROOT), summary["method"], k["launches"])

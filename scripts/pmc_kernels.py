@@ -39,7 +39,8 @@ def main(d, out):
                         (16, "HIP_vector_type<unsigned int, 4u> "))}
     cal["write_16B_lane"] = cw.get("write_16", {}).get("WRITE_SIZE", 0) / gib_kb
     res = {"method": "2 x FETCH_SIZE + WRITE_SIZE per launch (bytes) and SQ counters per launch, separate rocprofv3 "
-                     "--pmc passes over bench.py --steps 2 --warmup 1 --frames-in-flight 1; FETCH_SIZE x 2 per the "
+                     "--pmc passes over bench.py --steps 2 --warmup 1 --frames-in-flight 1 --no-tile-projection (full 4K frames "
+                     "only); FETCH_SIZE x 2 per the "
                      "gfx950 correction",
            "calibration_counter_per_byte": cal, "kernels": {}}
     for k in sorted(set(f) & set(w)):

@@ -11,7 +11,7 @@ O=gpurun_out/${PROF_OUT:-r04prof}
 mkdir -p $O
 export TMPDIR=/tmp
 K="wiener_res|sgr_res|sgr_flt|sgr_sse|unit_sums|wiener_stats|wiener_solve|cdef_search|cdef_apply|sod_step|dlf_tile|dlf_edge|lr_apply|md_dist"
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-matrix --frames-in-flight 1 --no-kernel-timing"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-matrix --no-tile-projection --frames-in-flight 1 --no-kernel-timing"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/ubench/fetch_cal.hip -o $O/fetch_cal &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/cal_fetch -o run --output-format csv -- $O/fetch_cal > $O/cal.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/cal_write -o run --output-format csv -- $O/fetch_cal >> $O/cal.log 2>&1 &&
@@ -19,8 +19,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" -d $O
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" -d $O/bench_write -o run --output-format csv -- $B > $O/bench_write.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT --kernel-include-regex "$K" -d $O/sqA -o run --output-format csv -- $B > $O/sqA.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_MISC SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "$K" -d $O/sqB -o run --output-format csv -- $B > $O/sqB.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f1 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix --frames-in-flight 1 > $O/trace_f1.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f4 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix > $O/trace_f4.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f1 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix --no-tile-projection --frames-in-flight 1 > $O/trace_f1.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_f4 -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-matrix --no-tile-projection > $O/trace_f4.log 2>&1
 rc=$?
 echo "exit $rc"
 exit $rc
