@@ -15,3 +15,7 @@ for f in 1 4; do
   echo "F=$f $(grep '^{' $O/b_f$f.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); c=d["config"]; print(d["value"], c["frame_latency_ms"], c["stage_ms"])')"
 done
 echo done
+if [ -n "$EMU" ]; then
+  timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-matrix --no-tile-projection --emulate-rank 8 > $O/b_e8.log 2>&1 || { echo "emulated bench failed"; tail -20 $O/b_e8.log; exit 1; }
+  echo "E8 $(grep '^{' $O/b_e8.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); c=d["config"]; print(d["value"], c["frame_latency_ms"], c["stage_ms"])')"
+fi

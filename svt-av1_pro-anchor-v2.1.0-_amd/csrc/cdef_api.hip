@@ -120,6 +120,7 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
     s->geo       = frame_geo(width, height);
     s->nfb       = s->geo.nvfb * s->geo.nhfb;
     s->mask_all  = 1;
+    s->pick_settle = 24; // the first pick checks after step 24 (then after the previous pick's settling step)
     s->pick_parts = 64;
     const size_t nfb = s->nfb;
     bool ok = hipMalloc(&s->d_mask, (size_t)s->geo.b8_rows * s->geo.b8_cols) == hipSuccess &&

@@ -515,6 +515,52 @@ __global__ void __launch_bounds__(NT, 4) sod_persist_kernel(const PersistArgs A)
     if (A.stat && t == 0 && li == 0) A.stat[0] += tk[0], A.stat[1] += tk[1], A.stat[2] += tk[2], A.stat[3] += 1;
 }
 
+// ---- the settle check: the launch path's steps after T skipped when every chain has settled by then ----
+// After step T's launch every chain c (nb = 1 << c, calls 0 .. L - 1, L = 5 nb) has either finished (L <= T) or
+// entered call T with the selection lev[T].  If lev[T]'s state (entries [0, nb - 1) of both halves) equals lev[T - nb]'s
+// with T - nb >= nb, the chain repeats with period nb from call T - nb on (sod_step_kernel's period shortcut), so its
+// last call L - 1 equals call a = T - nb + (L - 1 - T + nb) mod nb: the final list is lev[a] with slot nb - 1 taken from
+// lev[b] (b = the period twin of L: lev[t][nb - 1] is the result of call t - 1) and the value val[a + 1] -- exactly what
+// steps T + 1 .. L would produce.  One lane per chain; out[0] = 1 when every unfinished chain settled (their fin / best
+// written), out[1] = the latest step at which a chain that needs one settled (or finished): the host's next T.
+struct SettleOut {
+    int32_t settled, step;
+};
+__global__ void pick_settle_kernel(const int32_t *lev, const uint64_t *val, int32_t *fin, uint64_t *best, int T,
+                                   SettleOut *out) {
+    __shared__ int s_ok[MAX_CHAINS], s_at[MAX_CHAINS];
+    const int c = threadIdx.x;
+    if (c < MAX_CHAINS) {
+        const int nb = 1 << c, L = 5 * nb;
+        auto lv   = [&](int s, int i) { return lev[((size_t)s * MAX_CHAINS + c) * 32 + i]; };
+        auto same = [&](int s1, int s2) {
+            for (int q = 0; q < nb - 1; q++)
+                if (lv(s1, q) != lv(s2, q) || lv(s1, 16 + q) != lv(s2, 16 + q)) return false;
+            return true;
+        };
+        int at = L; // the first step from which the chain repeats (L: it finishes first)
+        for (int st = 2 * nb; st <= min(T, L - 1); st++)
+            if (same(st, st - nb)) {
+                at = st;
+                break;
+            }
+        bool ok = L <= T || at <= T;
+        if (L > T && ok) {
+            const int base = T - nb, a = base + (L - 1 - base) % nb, b = base + (L - base) % nb;
+            for (int i = 0; i < 32; i++) fin[c * 32 + i] = lv(a, i);
+            fin[c * 32 + nb - 1]      = lv(b, nb - 1);
+            fin[c * 32 + 16 + nb - 1] = lv(b, 16 + nb - 1);
+            best[c]                   = val[(size_t)(a + 1) * MAX_CHAINS + c];
+        }
+        s_ok[c] = ok, s_at[c] = at;
+    }
+    __syncthreads();
+    if (c == 0) {
+        out->settled = s_ok[0] && s_ok[1] && s_ok[2] && s_ok[3];
+        out->step    = max(max(s_at[0], s_at[1]), max(s_at[2], s_at[3]));
+    }
+}
+
 // ---- RD choice over the number of signalled strengths (EbEncCdef.c:853-872) ----
 struct PickOut {
     int32_t  sb_count, nbits, status, pad;
@@ -637,6 +683,17 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         P.stat     = stat;
         hipLaunchKernelGGL(sod_persist_kernel, dim3(PS_GRID), dim3(NT), 0, st, P);
     }
+    // the settle checkpoint (SVTGPU_PICK_SETTLE=0: off): after step T one small kernel checks whether every chain has
+    // settled into its period and, if so, writes the final lists, and the host skips the remaining launches (one
+    // wait instead of up to 40 - T dependent launches, each of which waits for free CU slots when other frames' kernels
+    // hold the device).  T follows the last pick's settling step; an unsettled check moves it 4 steps later
+    static const bool settle_on = [] {
+        const char *e = std::getenv("SVTGPU_PICK_SETTLE");
+        return !(e && e[0] == '0');
+    }();
+    SettleOut *h_settle = (SettleOut *)(s->h_pick + 448), *d_settle = (SettleOut *)(s->h_pick_dev + 448);
+    static_assert(sizeof(PickOut) <= 448, "pick output slot below the settle record");
+    const int T = settle_on ? std::min(std::max(s->pick_settle, 16), NSTEPS) : NSTEPS;
     for (int step = 0; step <= NSTEPS && !persist; step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {
@@ -660,6 +717,18 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         A.wgclk = svtgpu_wgclk_begin(4 * parts * na);
         hipLaunchKernelGGL(sod_step_kernel, dim3(4 * parts * na), dim3(NT), lds, st, A);
         svtgpu_wgclk_end("sod_step", 4 * parts * na, st);
+        if (step == T && T < NSTEPS) {
+            hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
+                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipStreamSynchronize(st));
+            svtgpu_count_xfer(1, sizeof(SettleOut));
+            if (h_settle->settled) {
+                s->pick_settle = h_settle->step;
+                break;
+            }
+            s->pick_settle = std::min(T + 4, NSTEPS - 4); // keep checking: a later frame may settle
+        }
     }
     HIP_TRY(hipGetLastError());
     PickOut *h_out = (PickOut *)s->h_pick;

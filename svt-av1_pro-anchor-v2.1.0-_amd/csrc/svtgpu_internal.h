@@ -103,6 +103,7 @@ struct SvtGpuCdefFrameState {
     int32_t       *d_fb_list;     // compacted non-skip FB indices [nfb], their count, FB -> index or -1 [nfb]
     uint64_t      *d_pick_xch;    // persistent pick: tagged partial sums, row minima, status, diagnostics (cdef_pick.hip)
     uint32_t       pick_epoch;    // picks run by the persistent kernel (tags its exchange words)
+    int32_t        pick_settle;   // the launch path's settle checkpoint: the step after which the pick checks
     int32_t        pick_xch_end;  // the strength count of the words in d_pick_xch (0: none written)
     uint8_t       *h_pick;        // pinned, mapped: the pick's result (PickOut) then the per-FB strengths [nfb]
     uint8_t       *h_pick_dev;    // its device address
