@@ -20,7 +20,7 @@
 #define NT 256
 #define MAX_CHAINS 4
 #define NSTEPS 40            // longest chain: nb = 8 → 8 + 32 calls (EbEncCdef.c:714-726)
-#define PICK_CHUNK 48        // max FBs per workgroup (staged in LDS: <= 48.4 KB; a multiple of 4)
+#define PICK_CHUNK 48        // max FBs per workgroup (a multiple of 4; their low words staged in LDS: <= 24.4 KB)
 
 struct StepChain {
     int32_t chain;       // 0..3 (nb = 1 << chain)
@@ -122,10 +122,12 @@ __device__ __forceinline__ void tot_argmin(const uint64_t (&tv)[4096 / NT], int 
 // grid (4 tiles of 16 rows j, FB chunks, chains).  The chunk's mse rows are staged in LDS; lane
 // k = t & 63, wave q owns rows 16*tile + 4*q + {0..3}; partials meet through u64 atomics.
 __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t dyn[]; // [chunk][128] mse rows + [chunk] best
-    uint64_t (*m)[128] = (uint64_t(*)[128])dyn;
-    __shared__ uint64_t bv[NT];
-    __shared__ int32_t  bi[NT];
+    // [chunk][128] low words of the mse rows + [chunk] best (half the 64-bit rows): when other frames' kernels hold
+    // most of a CU's LDS, a step's workgroups find room beside them
+    extern __shared__ __attribute__((aligned(16))) uint64_t dyn[];
+    const uint32_t *m32 = (const uint32_t *)dyn; // entry e of FB f of the chunk at m32[f * 128 + e]
+    __shared__ uint64_t bv[NT / 64];
+    __shared__ int32_t  bi[NT / 64];
     __shared__ int32_t  sl[32];
     // 1-D grid of 4 row tiles x parts x chains, ordered part-major on the logical index and placed so that
     // consecutive logical indices share an XCD: the 4 * na workgroups staging one FB chunk read it through one L2
@@ -137,7 +139,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int lead = tx == 0 && ty == 0;
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
     const int f0 = ty * A.chunk;
-    uint64_t *sbest = dyn + (size_t)A.chunk * 128;
+    uint64_t *sbest = dyn + (size_t)A.chunk * 64;
     // the period shortcut.  A chain's refinement calls (EbEncCdef.c:714-726) are a deterministic function of the
     // ordered selection entering them (entries [0, nb - 1) of lev[s]); once the selection entering call s equals the
     // one entering call s - nb, calls s, s + 1, ... repeat calls s - nb, ... result for result (the greedy loop has
@@ -204,9 +206,9 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         }
     }
     if (nfb > 0) {
-        uint4 *dst = (uint4 *)dyn;
+        uint2 *dst = (uint2 *)dyn; // the low words (the 64-bit path reads the table itself)
 #define ST(u) \
-    if (t + (u) * NT < nfb * 64) dst[t + (u) * NT] = v##u;
+    if (t + (u) * NT < nfb * 64) dst[t + (u) * NT] = make_uint2(v##u.x, v##u.z);
         ST(0) ST(1) ST(2) ST(3) ST(4) ST(5) ST(6) ST(7) ST(8) ST(9) ST(10) ST(11)
 #undef ST
     }
@@ -227,10 +229,12 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     }
     if (nfb <= 0) return;
     // 3. per-FB best over the selection (EbEncCdef.c:645-651)
+    const uint64_t *gm = A.wmse + (size_t)f0 * 128; // the chunk's full entries (64-bit path)
     if (t < nfb) {
         uint64_t b = (uint64_t)1 << 63;
         for (int g = 0; g < C.nb_sel; g++) {
-            const uint64_t v = m[t][sl[g]] + m[t][64 + sl[16 + g]];
+            const uint64_t v = wide ? gm[t * 128 + sl[g]] + gm[t * 128 + 64 + sl[16 + g]]
+                                    : (uint64_t)m32[t * 128 + sl[g]] + m32[t * 128 + 64 + sl[16 + g]];
             b = v < b ? v : b;
         }
         sbest[t] = b;
@@ -242,15 +246,12 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int k = t & 63, j0 = 16 * tx + 4 * (t >> 6);
     uint64_t  acc[4] = {0, 0, 0, 0};
     if (!wide) {
-        const uint32_t *m32 = (const uint32_t *)dyn; // low words: entry e of the chunk at m32[2 * e]
         auto term = [&](int f) {
             const uint64_t b64 = sbest[f];
-            const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[2 * (f * 128 + 64 + k)];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t v = m32[2 * (f * 128 + j0 + u)] + m1k;
-                acc[u] += min(v, b);
-            }
+            const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[f * 128 + 64 + k];
+            const uint4    m0 = *(const uint4 *)&m32[f * 128 + j0]; // j0 is a multiple of 4
+            acc[0] += min(m0.x + m1k, b), acc[1] += min(m0.y + m1k, b);
+            acc[2] += min(m0.z + m1k, b), acc[3] += min(m0.w + m1k, b);
         };
         int f = 0;
         for (; f + 4 <= nfb; f += 4) { // 4 FBs per iteration: their LDS reads issue together
@@ -259,11 +260,11 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         }
         for (; f < nfb; f++) term(f);
     } else {
-        for (int f = 0; f < nfb; f++) {
-            const uint64_t b = sbest[f], m1k = m[f][64 + k];
+        for (int f = 0; f < nfb; f++) { // entries >= 2^31 somewhere in the frame: the full entries from the table
+            const uint64_t b = sbest[f], m1k = gm[f * 128 + 64 + k];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const uint64_t v = m[f][j0 + u] + m1k;
+                const uint64_t v = gm[f * 128 + j0 + u] + m1k;
                 acc[u] += v < b ? v : b;
             }
         }
@@ -627,6 +628,16 @@ static int pick_parts() {
     return v;
 }
 
+// FBs per workgroup at most (SVTGPU_PICK_CHUNK, a multiple of 4 up to PICK_CHUNK, for sweeps)
+static int pick_chunk() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_PICK_CHUNK");
+        const int   c = e ? std::atoi(e) : 0;
+        return c >= 4 && c <= PICK_CHUNK ? c & ~3 : PICK_CHUNK;
+    }();
+    return v;
+}
+
 int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                           uint64_t lambda, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st) {
     const int nfb = s->nfb;
@@ -710,9 +721,9 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         // ~256 workgroups per step whatever the number of live chains (64 parts x 4 row tiles: 256 parts spent
         // more on the u64 atomics than they gained, 0.66 -> 0.59 ms per pick + apply); chunk <= PICK_CHUNK FBs
         const int want  = std::max(1, pick_parts() / std::max(na, 1));
-        A.chunk         = std::min(PICK_CHUNK, std::max(4, (sb_max + want - 1) / std::max(want, 1)));
+        A.chunk         = std::min(pick_chunk(), std::max(4, (sb_max + want - 1) / std::max(want, 1)));
         const int parts = std::max(1, (sb_max + A.chunk - 1) / A.chunk);
-        const size_t lds = (size_t)A.chunk * 129 * 8;
+        const size_t lds = (size_t)A.chunk * (128 * 4 + 8);
         A.na    = na;
         A.wgclk = svtgpu_wgclk_begin(4 * parts * na);
         hipLaunchKernelGGL(sod_step_kernel, dim3(4 * parts * na), dim3(NT), lds, st, A);
