@@ -42,20 +42,38 @@ import time
 import numpy as np
 
 FRAMES_IN_FLIGHT = 4  # default frames pipelined per GPU (round 3 final kernels: 2 -> 2672, 3 -> 2846, 4 -> 2914, 5 -> 2772 Mpx/s)
+# default when a rank filters a tile of the picture (N > 1, or an emulated rank): its stages are shorter but their
+# latency chains are not, so more frames overlap (round 4, emulated 8-GPU rank, 16 hardware queues: F = 4 5.9-6.0,
+# F = 5 7.1, F = 6 7.6-7.7 Gpx/s; profiles/r04/queues)
+TILED_FRAMES_IN_FLIGHT = 6
+# hardware queues per process: HIP's default 4 would serialize the frames' streams, but past 16 the queues are
+# time-sliced and every frame's latency chain stretches (emulated 8-GPU rank: F = 6 with 16 queues 7.6 Gpx/s, with 18
+# 4.8; F = 8 with 32 queues 1.7); whole frames run the same with 8, 12 or 16 (3.03-3.06 Gpx/s at F = 4)
+MAX_HW_QUEUES = 16
+
+
+def _arg(argv, name):
+    for i, w in enumerate(argv):
+        if w == name and i + 1 < len(argv):
+            return argv[i + 1]
+        if w.startswith(name + "="):
+            return w.split("=", 1)[1]
+    return None
+
+
+def _tiled(argv):
+    """A rank of a tiled picture: N > 1 (the default split) or an emulated rank."""
+    n = int(_arg(argv, "--gpus") or os.environ.get("WORLD_SIZE", 1))
+    return (n > 1 and (_arg(argv, "--split") or "tiles") == "tiles") or int(_arg(argv, "--emulate-rank") or 0) > 1
 
 
 def _frames_in_flight(argv):
-    for i, w in enumerate(argv):
-        if w == "--frames-in-flight" and i + 1 < len(argv):
-            return int(argv[i + 1])
-        if w.startswith("--frames-in-flight="):
-            return int(w.split("=", 1)[1])
-    return FRAMES_IN_FLIGHT
+    f = _arg(argv, "--frames-in-flight")
+    return int(f) if f else (TILED_FRAMES_IN_FLIGHT if _tiled(argv) else FRAMES_IN_FLIGHT)
 
 
-# the frames in flight need more than HIP's default 4 hardware queues per process (each frame runs on 3 streams
-# and shares none); set before the HIP runtime starts
-_want_queues = max(8, 4 * _frames_in_flight(sys.argv[1:]))
+# set before the HIP runtime starts: 4 queues per frame in flight (3 streams each), at most MAX_HW_QUEUES
+_want_queues = int(os.environ.get("SVTGPU_BENCH_QUEUES", 0)) or min(MAX_HW_QUEUES, max(8, 4 * _frames_in_flight(sys.argv[1:])))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < _want_queues:
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(_want_queues, 32))
 
@@ -121,9 +139,11 @@ def parse():
     ap.add_argument("--cpu-kind", choices=("reference", "port"), default="reference",
                     help="CPU baseline: the reference's own C + AVX2 kernels (oracle/_ref/ref_bench, built from the "
                          "reference sources by oracle/ref.mk) or the repo's C restatement (oracle/)")
-    ap.add_argument("--frames-in-flight", type=int, default=FRAMES_IN_FLIGHT,
+    ap.add_argument("--frames-in-flight", type=int, default=None,
                     help="frames pipelined per GPU, each on its own streams and host thread (the encoder's "
-                         "picture-level parallelism); a step processes one frame per slot")
+                         "picture-level parallelism); a step processes one frame per slot.  Default %d, %d for a rank "
+                         "of a tiled picture (and the tile projection's emulated ranks)" % (FRAMES_IN_FLIGHT,
+                                                                                            TILED_FRAMES_IN_FLIGHT))
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="the tiles' exchanges: nccl = libsvtgpu's RCCL communicator over xGMI (one rank per GPU); "
                          "gloo = the library's host transport over gloo (rehearses N > 1 ranks sharing one GPU)")
@@ -146,7 +166,11 @@ def parse():
                     help="N = 1: skip the emulated ranks of 2/4/8-GPU tiled pictures (config.tile_projection)")
     ap.add_argument("--no-matrix", action="store_true",
                     help="skip the extra configurations (north_star matrix + config 1) run as child processes")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.explicit_frames = a.frames_in_flight is not None
+    if a.frames_in_flight is None:
+        a.frames_in_flight = _frames_in_flight(sys.argv[1:])
+    return a
 
 
 # the north_star reporting matrix beside the headline 4K 10-bit line: (label, argv) of child bench runs, started
@@ -861,8 +885,9 @@ def main():
             plans = [svtgpu.tile_plan(W, H, lr_us, ggx, ggy, r).rects() for r in range(nn)]
             area = [(p_["tile"][2] - p_["tile"][0]) * (p_["tile"][3] - p_["tile"][1]) for p_ in plans]
             r_big = int(np.argmax(area))
+            Fe = F if a.explicit_frames else TILED_FRAMES_IN_FLIGHT  # a tiled rank's default
             emu = [Slot(k, plans[r_big], svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id()),
-                        svtgpu.band(md_nsb, nn, r_big)) for k in range(F)]
+                        svtgpu.band(md_nsb, nn, r_big)) for k in range(Fe)]
             torch.cuda.synchronize()
             run_all(3, False, emu)
             torch.cuda.synchronize()
@@ -877,7 +902,7 @@ def main():
             projection["n%d" % nn] = {
                 "grid": "%dx%d" % (ggx, ggy), "rank": r_big, "tile": plans[r_big]["tile"],
                 "tile_share": round(area[r_big] / float(W * H), 4), "ms_per_step": round(ms_e, 4),
-                "projected_Mpx_s": round(F * W * H / (ms_e * 1e-3) / 1e6, 1),
+                "frames_in_flight": Fe, "projected_Mpx_s": round(Fe * W * H / (ms_e * 1e-3) / 1e6, 1),
                 "frame_latency_ms": round(float(np.mean([es[0].elapsed_time(es[5]) for es in ev0])), 4),
                 "stage_ms": {"dlf_pick_filter": round(float(sm[0]), 4), "cdef_search": round(float(sm[1]), 4),
                              "cdef_pick_apply": round(float(sm[2]), 4), "lr_search_apply": round(float(sm[3]), 4),
@@ -887,11 +912,11 @@ def main():
                 sl.close()
         full_pick = float(np.mean([es[2].elapsed_time(es[8]) for es in slots[0].ev]))
         projection["note"] = ("one rank of an N-GPU tiled picture emulated on this GPU (the rank with the largest tile, "
-                              "F = %d frames in flight, one-rank RCCL communicators): ms_per_step ~ the N-GPU job's step "
+                              "frames_in_flight frames in flight, one-rank RCCL communicators): ms_per_step ~ the N-GPU job's step "
                               "time without the xGMI latency of its collectives (DLF trial SSEs per bisection step, CDEF "
                               "tables 2.1 MB, LR records); projected_Mpx_s = F x W x H / ms_per_step.  Replicated per "
                               "rank whatever N: the CDEF pick (%.3f ms at N = 1, cdef_pick_ms per N), the DLF bisection's "
-                              "host decisions and the LR RD finish" % (F, full_pick))
+                              "host decisions and the LR RD finish" % full_pick)
     roof = roofline_of(iso["kernels"] if iso else kernels_f, bd, a.pmc_json)
     roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run; the PMC counters' "
                          "condition)" % iso["steps"]) if iso else "one frame in flight (the main run)"
