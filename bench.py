@@ -216,6 +216,47 @@ def run_matrix():
     return res
 
 
+def run_projection(a):
+    """Strong-scaling projection of BASELINE config 4 on this one GPU: for N = 2, 4, 8 a child bench process runs the
+    rank with the largest tile of an N-rank picture alone (--emulate-rank N: its own process and hardware queues like a
+    real rank, the tiled rank's default frames in flight, one-rank RCCL communicators -- every ncclAllReduce issued,
+    none crossing xGMI).  Its value is F x W x H / its step time: the N-GPU job's throughput up to the collectives'
+    xGMI latency.  Sequential, before this process initialises the GPU."""
+    import subprocess
+    res = {}
+    for nn in (2, 4, 8):
+        argv = ["--no-matrix", "--no-tile-projection", "--no-cpu-baseline", "--emulate-rank", str(nn),
+                "--width", str(a.width), "--height", str(a.height), "--bit-depth", str(a.bit_depth),
+                "--cdef-level", str(a.cdef_level), "--steps", str(max(10, min(a.steps, 40))), "--warmup", "5"]
+        if a.explicit_frames:
+            argv += ["--frames-in-flight", str(a.frames_in_flight)]
+        try:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, capture_output=True, text=True,
+                               timeout=300)
+            line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            if r.returncode != 0 or not line:
+                res["n%d" % nn] = {"error": "exit %d: %s" % (r.returncode, r.stderr.strip()[-300:])}
+                continue
+            d = json.loads(line[-1])
+            c = d["config"]
+            e = c.get("emulated", {})
+            res["n%d" % nn] = {"grid": e.get("grid"), "rank": e.get("rank"), "tile": e.get("tile"),
+                               "tile_share": e.get("tile_share"), "frames_in_flight": c["frames_in_flight"],
+                               "ms_per_step": d["ms_per_step"], "projected_Mpx_s": d["value"],
+                               "frame_latency_ms": c["frame_latency_ms"],
+                               "stage_ms": {k: v for k, v in c["stage_ms"].items() if k != "note"},
+                               "cdef_pick_ms": e.get("cdef_pick_ms")}
+        except (OSError, ValueError, subprocess.TimeoutExpired) as ex:
+            res["n%d" % nn] = {"error": repr(ex)[:300]}
+    res["note"] = ("one rank of an N-GPU tiled picture emulated on this GPU as its own process (bench --emulate-rank N: "
+                   "the rank with the largest tile, frames_in_flight frames in flight, one-rank RCCL communicators): "
+                   "ms_per_step ~ the N-GPU job's step time without the xGMI latency of its collectives (DLF trial SSEs "
+                   "per bisection step, CDEF tables 2.1 MB, LR records); projected_Mpx_s = F x W x H / ms_per_step.  "
+                   "Replicated per rank whatever N: the CDEF pick (cdef_pick_ms), the DLF bisection's host decisions "
+                   "and the LR RD finish")
+    return res
+
+
 def spawn_ranks(a):
     """`--gpus N` outside a torch.distributed launcher: start the N ranks as children (one process per GPU) before
     this process touches the device, and return their exit code.  Inside a launcher WORLD_SIZE must equal N."""
@@ -558,6 +599,10 @@ def main():
     matrix = None
     if not a.no_matrix and int(os.environ.get("WORLD_SIZE", "1")) == 1 and a.stages == "all":
         matrix = run_matrix()  # before this process touches the GPU
+    projection = None
+    if (a.tile_projection and a.emulate_rank <= 1 and a.stages == "all" and a.gpus == 1
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1):
+        projection = run_projection(a)  # likewise
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -872,51 +917,6 @@ def main():
                           for es in s0.ev], axis=0)
         iso = dict(steps=iso_steps, frame_ms=float(np.mean([es[0].elapsed_time(es[5]) for es in s0.ev])),
                    kernels=kernel_table(float(iso_ms[1]), float(iso_ms[4]), lr_classes(iso_tot), bool(iso_tot)))
-    # Strong-scaling projection of BASELINE config 4 on this one GPU: the rank with the largest tile of an N-rank
-    # picture runs alone with the same F frames in flight, its exchanges a one-rank RCCL communicator (every
-    # ncclAllReduce issued, none crossing xGMI).  Its time per step is the N-GPU job's step time up to the collectives'
-    # xGMI latency; the stage times split each stage into this rank's share and the replicated work (the CDEF pick,
-    # the host decisions).
-    projection = None
-    if n == 1 and a.stages == "all" and a.tile_projection and emu_rank is None:
-        projection = {}
-        for nn in (2, 4, 8):
-            ggx, ggy = svtgpu.tile_grid(nn)
-            plans = [svtgpu.tile_plan(W, H, lr_us, ggx, ggy, r).rects() for r in range(nn)]
-            area = [(p_["tile"][2] - p_["tile"][0]) * (p_["tile"][3] - p_["tile"][1]) for p_ in plans]
-            r_big = int(np.argmax(area))
-            Fe = F if a.explicit_frames else TILED_FRAMES_IN_FLIGHT  # a tiled rank's default
-            emu = [Slot(k, plans[r_big], svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id()),
-                        svtgpu.band(md_nsb, nn, r_big)) for k in range(Fe)]
-            torch.cuda.synchronize()
-            run_all(3, False, emu)
-            torch.cuda.synchronize()
-            te = time.perf_counter()
-            nsteps = max(10, min(a.steps, 30))
-            run_all(nsteps, True, emu)
-            torch.cuda.synchronize()
-            ms_e = (time.perf_counter() - te) * 1e3 / nsteps
-            ev0 = emu[0].ev
-            sm = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7]),
-                          es[2].elapsed_time(es[8])] for es in ev0], axis=0)
-            projection["n%d" % nn] = {
-                "grid": "%dx%d" % (ggx, ggy), "rank": r_big, "tile": plans[r_big]["tile"],
-                "tile_share": round(area[r_big] / float(W * H), 4), "ms_per_step": round(ms_e, 4),
-                "frames_in_flight": Fe, "projected_Mpx_s": round(Fe * W * H / (ms_e * 1e-3) / 1e6, 1),
-                "frame_latency_ms": round(float(np.mean([es[0].elapsed_time(es[5]) for es in ev0])), 4),
-                "stage_ms": {"dlf_pick_filter": round(float(sm[0]), 4), "cdef_search": round(float(sm[1]), 4),
-                             "cdef_pick_apply": round(float(sm[2]), 4), "lr_search_apply": round(float(sm[3]), 4),
-                             "md_sad_sse_var": round(float(sm[4]), 4)},
-                "cdef_pick_ms": round(float(sm[5]), 4)}
-            for sl in emu:
-                sl.close()
-        full_pick = float(np.mean([es[2].elapsed_time(es[8]) for es in slots[0].ev]))
-        projection["note"] = ("one rank of an N-GPU tiled picture emulated on this GPU (the rank with the largest tile, "
-                              "frames_in_flight frames in flight, one-rank RCCL communicators): ms_per_step ~ the N-GPU job's step "
-                              "time without the xGMI latency of its collectives (DLF trial SSEs per bisection step, CDEF "
-                              "tables 2.1 MB, LR records); projected_Mpx_s = F x W x H / ms_per_step.  Replicated per "
-                              "rank whatever N: the CDEF pick (%.3f ms at N = 1, cdef_pick_ms per N), the DLF bisection's "
-                              "host decisions and the LR RD finish" % full_pick)
     roof = roofline_of(iso["kernels"] if iso else kernels_f, bd, a.pmc_json)
     roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run; the PMC counters' "
                          "condition)" % iso["steps"]) if iso else "one frame in flight (the main run)"
@@ -1019,7 +1019,12 @@ def main():
         if iso and len(slots[0].ht) > len(ht_main):
             out["config"]["host_ms_f1"] = host_table(slots[0].ht[len(ht_main):])
     if emu_rank is not None:
-        out["config"]["emulated"] = {"ranks": a.emulate_rank, "rank": emu_rank, "tile": plan["tile"],
+        tl = plan["tile"]
+        out["config"]["emulated"] = {"ranks": a.emulate_rank, "rank": emu_rank, "tile": tl,
+                                     "grid": "%dx%d" % svtgpu.tile_grid(a.emulate_rank),
+                                     "tile_share": round((tl[2] - tl[0]) * (tl[3] - tl[1]) / float(W * H), 4),
+                                     "cdef_pick_ms": round(float(np.mean([es[2].elapsed_time(es[8])
+                                                                          for es in slots[0].ev])), 4),
                                      "note": "this GPU ran one rank of an N-GPU tiled picture alone (one-rank RCCL "
                                              "communicators: every exchange issued, none over xGMI); value = F x W x H "
                                              "/ this rank's step time, the N-GPU job's rate up to the collectives' "
