@@ -792,12 +792,16 @@ __global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, un
     for (int i = tid; i < NW; i += 64) ((uint32_t *)S)[i] = w[i];
 }
 
-int dlf_device_chunk() { // (trial, step) pairs per host read-back; 0: the host-driven search
+// (trial, step) pairs per host read-back; 0: the host-driven search.  Default: the device search for a tile of a
+// picture spread over ranks (its trial launches are small, so the host round trips and the all-reduce waits between
+// them dominate: emulated 8-GPU rank 7.7-7.9 -> 8.1 Gpx/s), the host-driven one for a whole picture (its launches
+// sized per step beat the device plan's full-shape grid: 3053 vs 2949 Mpx/s).  SVTGPU_DLF_DEVICE=0|1|n overrides.
+int dlf_device_chunk(const SvtGpuDlfState *s) {
     static const int k = [] {
         const char *e = std::getenv("SVTGPU_DLF_DEVICE");
-        return e ? std::max(0, std::min(64, std::atoi(e) == 1 ? 6 : std::atoi(e))) : 0;
+        return e ? std::max(0, std::min(64, std::atoi(e) == 1 ? 6 : std::atoi(e))) : -1;
     }();
-    return k;
+    return k >= 0 ? k : (svtgpu_comm_tiled(s->comm) ? 6 : 0);
 }
 
 int run_searches_device_body(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *src,
@@ -1153,7 +1157,7 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     LevelSearch us(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 1, 0);
     LevelSearch vs(last, dlf_avg, early_exit_convergence, tx_mode_only_4x4, 2, 0);
     LevelSearch *all[3] = {&ys, &us, &vs};
-    const int   chunk  = dlf_device_chunk();
+    const int   chunk  = dlf_device_chunk(s);
     hipStream_t hs;
     if ((rc = svtgpu_prio_enter(&s->prio, st, &hs))) return rc;
     rc = chunk ? run_searches_device(s, recon, source, p, all, search_uv ? 3 : 1, hs, chunk)

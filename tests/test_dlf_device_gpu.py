@@ -49,3 +49,13 @@ def test_dlf_device_search_tiled(monkeypatch, world):
     import test_tiled_gpu
     monkeypatch.setenv("SVTGPU_DLF_DEVICE", "3")  # inherited by the spawned ranks
     test_tiled_gpu.test_ranks_one_gpu_bit_exact(world)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_dlf_host_search_tiled(monkeypatch):
+    """Tiled ranks default to the device search; the host-driven bisection with its per-step all-reduce stays
+    available (SVTGPU_DLF_DEVICE=0) and bit-exact."""
+    import test_tiled_gpu
+    monkeypatch.setenv("SVTGPU_DLF_DEVICE", "0")
+    test_tiled_gpu.test_ranks_one_gpu_bit_exact(2)
