@@ -15,7 +15,9 @@ timeout -k 10 1000 $T tests -m gpu --deselect tests/test_tiled_gpu.py > $O/pytes
 grep -E "passed|failed" $O/pytest.log | tail -1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-timeout -k 10 600 python bench.py --no-matrix > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
+fi
+if [ -z "$NO_BENCH" ]; then
+timeout -k 10 900 python bench.py $BENCH_ARGS > $O/bench.log 2>&1 || { echo "bench failed"; tail -20 $O/bench.log; exit 1; }
 grep '^{' $O/bench.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["ms_per_step"], r["kernel"], r["avg_launch_ms"], r["frac"], r.get("contended", {}).get("kernel"), d["cpu_baseline"]["value"] if d.get("cpu_baseline") else None)'
 fi
 echo done
