@@ -346,7 +346,10 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
     wgclk_mark(A.wgclk, 3);
     // ================= luma: 2 passes of 32 blocks; lane = one 8-sample row =================
     for (int pass = 0; pass < 2; pass++) {
-        const int bip = tid >> 3, row = tid & 7; // block in pass, row in block
+        // block in pass, row in block.  A wave holds one row of 8 blocks; its lower half the even block columns, its
+        // upper half the odd ones: the half-wave's rows then sit at 35 r + 8 j dwords (r < 8, j < 4), 32 distinct
+        // banks for every tap read (with the 4 adjacent blocks of a half, (r, j) and (r + 4, j + 3) shared a bank)
+        const int bip = ((tid >> 6) << 3) | (((tid >> 3) & 3) << 1) | ((tid >> 5) & 1), row = tid & 7;
         const int b = 32 * pass + bip, by = b >> 3, bx = b & 7;
         const int r = 8 * by + row, c0 = 8 * bx;
         const bool valid = slisted[b] && (row % ss == 0);
@@ -437,7 +440,10 @@ __global__ void __launch_bounds__(NT, 3) cdef_search_kernel(const SearchArgs A) 
     wgclk_mark(A.wgclk, 4);
     // ================= chroma: both planes in one pass; lane = one 8-sample row =================
     {
-        const int pl = tid >> 7, q = tid & 127, r = q >> 2, c0 = (q & 3) * 8;
+        // plane, row, segment.  A half-wave holds rows {4h .. 4h + 3, 4h + 16 .. 4h + 19} (h < 4) and the 4 segments of
+        // each: at the 19-dword row stride those are 32 distinct banks (8 consecutive rows shared 4 of them pairwise)
+        const int pl = tid >> 7, q = tid & 127, hq = q >> 5, rr = (q >> 2) & 7;
+        const int r = 4 * hq + (rr & 3) + 16 * (rr >> 2), c0 = (q & 3) * 8;
         const int by = r >> 2;
         const uint16_t *tile = ctile[pl];
         s16x2 sp[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
