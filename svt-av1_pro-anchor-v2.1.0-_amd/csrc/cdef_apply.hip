@@ -243,7 +243,10 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         const u16x2 ssh = {ss, ss};
         T *out = (T *)A.out[pli];
         for (int j = tid; j < (n * n) >> 1; j += NT) {
-            const int r = j >> lp, c = 2 * (j & ((1 << lp) - 1));
+            // luma: a half-wave is one tile row (32 pairs); chroma: a half-wave holds two rows of 16 pairs, taken two
+            // apart (r, r + 2: 48 dwords, disjoint banks; adjacent rows, 24 dwords apart, shared 8 banks pairwise)
+            const int r = pli ? ((j >> 6) << 2) | (((j >> 4) & 1) << 1) | ((j >> 5) & 1) : j >> lp;
+            const int c = 2 * (j & ((1 << lp) - 1));
             const int y = n * fbr + r, x = n * fbc + c;
             if (y < ylo || y >= yhi || x < xlo || x >= xhi) continue; // x bounds are even: a pair is in or out whole
             const int       b = (r >> lb) * 8 + (c >> lb);
