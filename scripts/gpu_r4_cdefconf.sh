@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${1:-r4cdefconf}
 mkdir -p $O
 export TMPDIR=/tmp
-B="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-matrix --no-tile-projection --frames-in-flight 1 --no-kernel-timing"
+B="python3 bench.py --steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline --no-matrix --no-tile-projection --frames-in-flight 1 --no-kernel-timing"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 250 --timeout-method thread tests/test_cdef_gpu.py tests/test_pipeline_golden.py -m gpu > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVE_CYCLES --kernel-include-regex "${K:-cdef_search|cdef_apply}" -d $O/pmc -o run --output-format csv -- $B > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }

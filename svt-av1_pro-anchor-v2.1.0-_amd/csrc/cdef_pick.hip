@@ -20,7 +20,10 @@
 #define NT 256
 #define MAX_CHAINS 4
 #define NSTEPS 40            // longest chain: nb = 8 → 8 + 32 calls (EbEncCdef.c:714-726)
-#define PICK_CHUNK 48        // max FBs per workgroup (a multiple of 4; their low words staged in LDS: <= 24.4 KB)
+#define PICK_CHUNK 48        // max FBs per workgroup (a multiple of 4; their low words staged in LDS: <= 25.7 KB)
+// LDS row of a staged FB (dwords): 128 entries + 4, so the per-FB best (a lane per FB reading its row) spreads over 8
+// banks instead of one, and rows stay 16-B aligned for the accumulation's quad reads
+#define MROW 132
 
 struct StepChain {
     int32_t chain;       // 0..3 (nb = 1 << chain)
@@ -125,7 +128,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     // [chunk][128] low words of the mse rows + [chunk] best (half the 64-bit rows): when other frames' kernels hold
     // most of a CU's LDS, a step's workgroups find room beside them
     extern __shared__ __attribute__((aligned(16))) uint64_t dyn[];
-    const uint32_t *m32 = (const uint32_t *)dyn; // entry e of FB f of the chunk at m32[f * 128 + e]
+    const uint32_t *m32 = (const uint32_t *)dyn; // entry e of FB f of the chunk at m32[f * MROW + e]
     __shared__ uint64_t bv[NT / 64];
     __shared__ int32_t  bi[NT / 64];
     __shared__ int32_t  sl[32];
@@ -139,7 +142,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     const int lead = tx == 0 && ty == 0;
     if (C.nb_sel < 0 && !lead) return; // finalize-only entry: one workgroup
     const int f0 = ty * A.chunk;
-    uint64_t *sbest = dyn + (size_t)A.chunk * 64;
+    uint64_t *sbest = dyn + (size_t)A.chunk * (MROW / 2);
     // the period shortcut.  A chain's refinement calls (EbEncCdef.c:714-726) are a deterministic function of the
     // ordered selection entering them (entries [0, nb - 1) of lev[s]); once the selection entering call s equals the
     // one entering call s - nb, calls s, s + 1, ... repeat calls s - nb, ... result for result (the greedy loop has
@@ -206,9 +209,9 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         }
     }
     if (nfb > 0) {
-        uint2 *dst = (uint2 *)dyn; // the low words (the 64-bit path reads the table itself)
+        uint2 *dst = (uint2 *)dyn; // the low words (the 64-bit path reads the table itself), rows MROW dwords apart
 #define ST(u) \
-    if (t + (u) * NT < nfb * 64) dst[t + (u) * NT] = make_uint2(v##u.x, v##u.z);
+    if (t + (u) * NT < nfb * 64) dst[((t + (u) * NT) >> 6) * (MROW / 2) + ((t + (u) * NT) & 63)] = make_uint2(v##u.x, v##u.z);
         ST(0) ST(1) ST(2) ST(3) ST(4) ST(5) ST(6) ST(7) ST(8) ST(9) ST(10) ST(11)
 #undef ST
     }
@@ -234,7 +237,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         uint64_t b = (uint64_t)1 << 63;
         for (int g = 0; g < C.nb_sel; g++) {
             const uint64_t v = wide ? gm[t * 128 + sl[g]] + gm[t * 128 + 64 + sl[16 + g]]
-                                    : (uint64_t)m32[t * 128 + sl[g]] + m32[t * 128 + 64 + sl[16 + g]];
+                                    : (uint64_t)m32[t * MROW + sl[g]] + m32[t * MROW + 64 + sl[16 + g]];
             b = v < b ? v : b;
         }
         sbest[t] = b;
@@ -248,8 +251,8 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     if (!wide) {
         auto term = [&](int f) {
             const uint64_t b64 = sbest[f];
-            const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[f * 128 + 64 + k];
-            const uint4    m0 = *(const uint4 *)&m32[f * 128 + j0]; // j0 is a multiple of 4
+            const uint32_t b = b64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)b64, m1k = m32[f * MROW + 64 + k];
+            const uint4    m0 = *(const uint4 *)&m32[f * MROW + j0]; // j0 and MROW are multiples of 4
             acc[0] += min(m0.x + m1k, b), acc[1] += min(m0.y + m1k, b);
             acc[2] += min(m0.z + m1k, b), acc[3] += min(m0.w + m1k, b);
         };
@@ -723,7 +726,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         const int want  = std::max(1, pick_parts() / std::max(na, 1));
         A.chunk         = std::min(pick_chunk(), std::max(4, (sb_max + want - 1) / std::max(want, 1)));
         const int parts = std::max(1, (sb_max + A.chunk - 1) / A.chunk);
-        const size_t lds = (size_t)A.chunk * (128 * 4 + 8);
+        const size_t lds = (size_t)A.chunk * (MROW * 4 + 8);
         A.na    = na;
         A.wgclk = svtgpu_wgclk_begin(4 * parts * na);
         hipLaunchKernelGGL(sod_step_kernel, dim3(4 * parts * na), dim3(NT), lds, st, A);
