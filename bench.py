@@ -33,6 +33,7 @@ issue from the committed PMC profile) and `cpu_baseline` (the reference's own CP
 bounded sample).
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -147,6 +148,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="the tiles' exchanges: nccl = libsvtgpu's RCCL communicator over xGMI (one rank per GPU); "
                          "gloo = the library's host transport over gloo (rehearses N > 1 ranks sharing one GPU)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=60000,
+                    help="deadline of every tile exchange (DLF trial SSEs, CDEF tables, LR records): a rank whose peer "
+                         "never arrives fails with the exchange named instead of hanging the node")
     ap.add_argument("--split", default="tiles", choices=("tiles", "frames"),
                     help="N > 1: 'tiles' = every frame tiled over the ranks with RCCL exchanges (SURVEY §8e, BASELINE "
                          "config 4; strong scaling); 'frames' = every rank filters pictures of its own (weak scaling)")
@@ -612,7 +616,7 @@ def main():
     torch.cuda.set_device(local)
     n = world
     if n > 1:  # control only (barriers, the max-over-ranks time, the RCCL ids): the data path is libsvtgpu's RCCL
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(milliseconds=4 * a.comm_timeout_ms))
     if a.stages == "md":
         bench_md(a, torch, dist, n, rank, local)
         if n > 1:
@@ -666,12 +670,18 @@ def main():
         if a.dist_backend == "nccl":
             uid = [svtgpu.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            return svtgpu.Comm.rccl(ctx, n, rank, uid[0])
-        grp = dist.new_group(backend="gloo")
+            c = svtgpu.Comm.rccl(ctx, n, rank, uid[0])
+        else:
+            grp = dist.new_group(backend="gloo")
 
-        def allreduce(words):
-            dist.all_reduce(torch.from_numpy(words.view(np.int64)), group=grp)
-        return svtgpu.Comm.host(n, rank, allreduce)
+            def allreduce(words, timeout_ms):  # bounded by the communicator's deadline
+                w = dist.all_reduce(torch.from_numpy(words.view(np.int64)), group=grp, async_op=True)
+                w.wait(timeout=datetime.timedelta(milliseconds=timeout_ms))
+            c = svtgpu.Comm.host(n, rank, allreduce)
+        # every exchange bounded: a rank whose peer never arrives exits non-zero with the exchange named
+        c.set_timeout(a.comm_timeout_ms)
+        c.set_slot(k)
+        return c
 
     class Slot:
         """One frame in flight: its own input frames, stage states, streams and (tiles) communicator."""

@@ -160,6 +160,21 @@ int32_t svtgpu_comm_rank(const SvtGpuComm *c);
 /* element-wise sum of n uint64 over the ranks, in place; on_device: buf is device memory (enqueued on `stream` with
  * RCCL), else host memory (synchronous) */
 int svtgpu_comm_allreduce_u64(SvtGpuComm *c, void *buf, size_t n, int32_t on_device, void *stream);
+/* Every exchange is bounded by the communicator's deadline (default 60000 ms, SVTGPU_COMM_TIMEOUT_MS overrides it).
+ * A frame-level call whose exchange does not complete in time (a peer rank skipped it, or failed before reaching it)
+ * returns SVTGPU_ERR_HIP, svtgpu_error_string names the exchange ("DLF trial SSEs", "CDEF search tables", "LR search
+ * records"), the frame slot and the exchange's sequence number; an RCCL communicator is aborted (ncclCommAbort ends
+ * this rank's pending collectives) and the communicator fails every later call (svtgpu_comm_failed).  A host
+ * transport bounds its own wait by svtgpu_comm_timeout_ms and returns non-zero when it expires. */
+int     svtgpu_comm_set_timeout(SvtGpuComm *c, int32_t timeout_ms);
+int32_t svtgpu_comm_timeout_ms(const SvtGpuComm *c);
+int     svtgpu_comm_set_slot(SvtGpuComm *c, int32_t frame_slot); /* the frame slot named in a timeout's message */
+int32_t svtgpu_comm_failed(const SvtGpuComm *c);
+/* host wait for `stream`, bounded by the deadline while one of the communicator's device-side exchanges (enqueued
+ * without a host wait: svtgpu_comm_allreduce_u64 on device memory) is outstanding */
+int     svtgpu_comm_sync(SvtGpuComm *c, void *stream);
+/* test support: holds `stream` busy for `ms` milliseconds (<= 10000) with one spinning wave */
+int     svtgpu_debug_stall(SvtGpuContext *ctx, void *stream, int32_t ms);
 
 /* The tiles of a gx x gy split of a width x height picture and what rank `rank` (row-major) computes.  Tile edges
  * fall on the luma restoration-unit grid (unit_size[0], a multiple of 64: also filter-block and superblock edges), so

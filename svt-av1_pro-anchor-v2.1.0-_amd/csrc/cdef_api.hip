@@ -189,7 +189,8 @@ extern "C" int svtgpu_cdef_set_tile(SvtGpuCdefFrameState *s, const int32_t fb_re
     if (s->d_fb_kind && ((f[0] | f[1]) & 1)) return SVTGPU_ERR_INVALID_ARG; // SB128 areas are never cut
     std::memcpy(s->fb_rect, f, sizeof s->fb_rect);
     std::memcpy(s->out_rect, o, sizeof s->out_rect);
-    s->comm = comm;
+    s->comm     = comm;
+    s->gathered = 0; // another comm or tile: the tables hold this rank's blocks only until the next pick sums them
     return SVTGPU_OK;
 }
 
@@ -198,6 +199,7 @@ extern "C" int svtgpu_cdef_bind_tables(SvtGpuCdefFrameState *s, void *mse_dev, v
         return SVTGPU_ERR_INVALID_ARG;
     s->d_mse  = mse_dev ? (uint64_t *)mse_dev : s->own_mse;
     s->d_skip = skip_dev ? (uint8_t *)skip_dev : s->own_skip;
+    s->gathered = 0; // freshly bound tables are this rank's until the next pick sums them
     return SVTGPU_OK;
 }
 
@@ -206,6 +208,7 @@ extern "C" int svtgpu_cdef_bind_dir_tables(SvtGpuCdefFrameState *s, void *dir_de
         return SVTGPU_ERR_INVALID_ARG;
     s->d_dir = dir_dev ? (uint8_t *)dir_dev : s->own_dir;
     s->d_var = var_dev ? (int32_t *)var_dev : s->own_var;
+    s->gathered = 0;
     return SVTGPU_OK;
 }
 
@@ -317,14 +320,14 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
     // search (another level, another lambda) reads the gathered tables instead of summing them again
     if (svtgpu_comm_tiled(s->comm) && !s->gathered) {
         const size_t nfb = s->nfb;
-        if (int rc = svtgpu_comm_sum(s->comm, s->d_dir, nfb * 64 / 8, true, st)) return rc;
-        if (int rc = svtgpu_comm_sum(s->comm, s->d_var, nfb * 64 * 4 / 8, true, st)) return rc;
+        if (int rc = svtgpu_comm_sum(s->comm, s->d_dir, nfb * 64 / 8, true, st, SVTGPU_XCH_CDEF)) return rc;
+        if (int rc = svtgpu_comm_sum(s->comm, s->d_var, nfb * 64 * 4 / 8, true, st, SVTGPU_XCH_CDEF)) return rc;
         if (!ctrls->use_reference_cdef_fs) {
-            if (int rc = svtgpu_comm_sum(s->comm, s->d_mse, nfb * 2 * 64, true, st)) return rc;
+            if (int rc = svtgpu_comm_sum(s->comm, s->d_mse, nfb * 2 * 64, true, st, SVTGPU_XCH_CDEF)) return rc;
             // word sums over the state's padded copy: a bound table is exactly [nfb] bytes
             const size_t words = (nfb + 7) / 8;
             if (s->d_skip != s->own_skip) HIP_TRY(hipMemcpyAsync(s->own_skip, s->d_skip, nfb, hipMemcpyDeviceToDevice, st));
-            if (int rc = svtgpu_comm_sum(s->comm, s->own_skip, words, true, st)) return rc;
+            if (int rc = svtgpu_comm_sum(s->comm, s->own_skip, words, true, st, SVTGPU_XCH_CDEF)) return rc;
             if (s->d_skip != s->own_skip) HIP_TRY(hipMemcpyAsync(s->d_skip, s->own_skip, nfb, hipMemcpyDeviceToDevice, st));
         }
         s->gathered = 1;

@@ -707,7 +707,11 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     }();
     SettleOut *h_settle = (SettleOut *)(s->h_pick + 448), *d_settle = (SettleOut *)(s->h_pick_dev + 448);
     static_assert(sizeof(PickOut) <= 448, "pick output slot below the settle record");
-    const int T = settle_on ? std::min(std::max(s->pick_settle, 16), NSTEPS) : NSTEPS;
+    // after two consecutive checks that found a chain unsettled the next 8 picks skip the check (its host wait saves
+    // nothing on a sequence that does not settle), then it is tried again from step 24
+    const bool check = settle_on && s->pick_skip == 0;
+    if (s->pick_skip > 0 && --s->pick_skip == 0) s->pick_settle = 24;
+    const int T = check ? std::min(std::max(s->pick_settle, 16), NSTEPS) : NSTEPS;
     for (int step = 0; step <= NSTEPS && !persist; step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {
@@ -735,13 +739,15 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
             hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
                                (const uint64_t *)A.val, A.fin, A.best, T, d_settle);
             HIP_TRY(hipGetLastError());
-            HIP_TRY(hipStreamSynchronize(st));
+            if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded behind the tables' exchange
             svtgpu_count_xfer(1, sizeof(SettleOut));
             if (h_settle->settled) {
                 s->pick_settle = h_settle->step;
+                s->pick_miss   = 0;
                 break;
             }
             s->pick_settle = std::min(T + 4, NSTEPS - 4); // keep checking: a later frame may settle
+            if (++s->pick_miss >= 2) s->pick_skip = 8, s->pick_miss = 0;
         }
     }
     HIP_TRY(hipGetLastError());
@@ -753,7 +759,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
                        (const int32_t *)A.fin, (const int32_t *)d_count, (uint64_t)lambda, (PickOut *)s->h_pick_dev,
                        d_status, (const uint64_t *)wmse, (const int32_t *)d_inv, nfb, s->d_fb_strength, host_fbs);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st)); // the only wait of the pick
+    if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // the only wait of the pick (bounded when tiled)
     if (h_out->status) {
         svtgpu_set_last_hip_error(hipErrorUnknown, "CDEF pick: the persistent step exchange timed out", __FILE__, __LINE__);
         return SVTGPU_ERR_HIP;

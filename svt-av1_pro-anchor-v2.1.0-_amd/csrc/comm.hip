@@ -14,12 +14,42 @@
 //   * a host transport supplied by the caller (a function that sums uint64 words over the ranks, e.g. an MPI or gloo
 //     binding): device buffers are staged through pinned host memory.  Used by the CPU-side rehearsals and by tests
 //     that run several ranks on one GPU (RCCL refuses two ranks on one device).
+//
+// Every exchange is bounded (round 5): a rank whose peer never arrives (a skipped exchange, a peer that failed before
+// its all-reduce) must not hang the node.  The device-side collectives are enqueued without a host wait (the CDEF
+// tables before the pick, the DLF trial SSEs between a trial and its step kernel), so each one records an event in a
+// small ring, and every host wait of a frame-level call that may sit behind a collective goes through
+// svtgpu_comm_wait: it polls against the communicator's deadline and, when it expires while a collective is still
+// outstanding, names that exchange (what, frame slot, sequence number), aborts the RCCL communicator (ncclCommAbort
+// ends the pending collectives on this rank) and returns SVTGPU_ERR_HIP; the communicator then fails every later call.
+// A host transport gets the deadline from svtgpu_comm_timeout_ms and reports an expired wait by returning non-zero.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "svtgpu_internal.h"
+
+namespace {
+constexpr int XCH_RING = 32;
+struct XchRecord {
+    hipEvent_t  ev   = nullptr;
+    const char *what = nullptr;
+    uint64_t    seq  = 0;
+    size_t      words = 0;
+    bool        live = false;
+};
+int default_timeout_ms() {
+    static const int v = [] {
+        const char *e = std::getenv("SVTGPU_COMM_TIMEOUT_MS");
+        const int   t = e ? std::atoi(e) : 0;
+        return t > 0 ? t : 60000;
+    }();
+    return v;
+}
+} // namespace
 
 struct SvtGpuComm {
     int32_t             nranks = 1, rank = 0;
@@ -31,6 +61,13 @@ struct SvtGpuComm {
     uint64_t           *dev = nullptr; // device staging of host buffers (RCCL)
     size_t              dev_words = 0;
     int                 device = 0;
+    int32_t             timeout_ms = 0;  // deadline of every exchange
+    int32_t             slot       = -1; // the frame slot it serves (error messages only)
+    uint64_t            seq        = 0;  // exchanges issued
+    bool                failed     = false;
+    char                fail_msg[320] = {0};
+    XchRecord           ring[XCH_RING]; // the device-side collectives not yet seen complete
+    hipEvent_t          wait_ev = nullptr;
 };
 
 namespace {
@@ -47,6 +84,41 @@ int grow_pin(SvtGpuComm *c, size_t n) {
     HIP_TRY(hipHostMalloc((void **)&c->pin, n * 8, hipHostMallocDefault));
     c->pin_words = n;
     return SVTGPU_OK;
+}
+// a communicator that timed out (or whose RCCL call failed) fails every later call with the first message
+int comm_failed(SvtGpuComm *c) {
+    svtgpu_set_last_hip_error(hipErrorUnknown, c->fail_msg, __FILE__, __LINE__);
+    return SVTGPU_ERR_HIP;
+}
+void slot_str(const SvtGpuComm *c, char *b, size_t n) {
+    if (c->slot >= 0) std::snprintf(b, n, "frame slot %d", c->slot);
+    else std::snprintf(b, n, "frame slot unset");
+}
+// the deadline expired with `r` outstanding: name it, abort RCCL, fail from now on
+int comm_timeout(SvtGpuComm *c, const XchRecord &r) {
+    char sl[32];
+    slot_str(c, sl, sizeof sl);
+    std::snprintf(c->fail_msg, sizeof c->fail_msg,
+                  "exchange timed out: the all-reduce of the %s (%s, rank %d of %d, exchange #%llu, %zu words) did not "
+                  "complete within %d ms -- a peer rank skipped or never reached it; RCCL communicator aborted",
+                  r.what, sl, c->rank, c->nranks, (unsigned long long)r.seq, r.words, c->timeout_ms);
+    c->failed = true;
+    if (c->nccl) (void)ncclCommAbort(c->nccl); // ends this rank's pending collectives
+    c->nccl = nullptr;
+    return comm_failed(c);
+}
+// drop the ring's completed collectives; the oldest outstanding one, or null
+const XchRecord *prune(SvtGpuComm *c) {
+    const XchRecord *oldest = nullptr;
+    for (auto &r : c->ring) {
+        if (!r.live) continue;
+        if (hipEventQuery(r.ev) == hipSuccess) {
+            r.live = false;
+            continue;
+        }
+        if (!oldest || r.seq < oldest->seq) oldest = &r;
+    }
+    return oldest;
 }
 int grow_dev(SvtGpuComm *c, size_t n) {
     if (n <= c->dev_words) return SVTGPU_OK;
@@ -77,6 +149,14 @@ extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t ra
     if (ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank)) return nccl_fail(r, "ncclCommInitRank");
     auto *c   = new SvtGpuComm();
     c->nranks = nranks, c->rank = rank, c->nccl = comm, c->device = ctx->device;
+    c->timeout_ms = default_timeout_ms();
+    for (auto &r : c->ring)
+        if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+            svtgpu_comm_destroy(c);
+            svtgpu_set_last_hip_error(hipErrorOutOfMemory, "comm events", __FILE__, __LINE__);
+            return SVTGPU_ERR_HIP;
+        }
+    HIP_TRY(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
     *out      = c;
     return SVTGPU_OK;
 }
@@ -85,6 +165,7 @@ extern "C" int svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGp
     if (!t || !t->allreduce_u64 || !out || nranks < 1 || rank < 0 || rank >= nranks) return SVTGPU_ERR_INVALID_ARG;
     auto *c    = new SvtGpuComm();
     c->nranks  = nranks, c->rank = rank, c->host = *t, c->is_host = true;
+    c->timeout_ms = default_timeout_ms();
     *out       = c;
     return SVTGPU_OK;
 }
@@ -92,6 +173,9 @@ extern "C" int svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGp
 extern "C" void svtgpu_comm_destroy(SvtGpuComm *c) {
     if (!c) return;
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    for (auto &r : c->ring)
+        if (r.ev) (void)hipEventDestroy(r.ev);
+    if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->dev) (void)hipFree(c->dev);
     delete c;
@@ -101,13 +185,60 @@ extern "C" int32_t svtgpu_comm_nranks(const SvtGpuComm *c) { return c ? c->nrank
 bool svtgpu_comm_tiled(const SvtGpuComm *c) { return c && (c->nranks > 1 || !c->is_host); }
 extern "C" int32_t svtgpu_comm_rank(const SvtGpuComm *c) { return c ? c->rank : -1; }
 
+extern "C" int svtgpu_comm_set_timeout(SvtGpuComm *c, int32_t timeout_ms) {
+    if (!c || timeout_ms <= 0) return SVTGPU_ERR_INVALID_ARG;
+    c->timeout_ms = timeout_ms;
+    return SVTGPU_OK;
+}
+extern "C" int32_t svtgpu_comm_timeout_ms(const SvtGpuComm *c) { return c ? c->timeout_ms : 0; }
+extern "C" int svtgpu_comm_set_slot(SvtGpuComm *c, int32_t slot) {
+    if (!c) return SVTGPU_ERR_INVALID_ARG;
+    c->slot = slot;
+    return SVTGPU_OK;
+}
+extern "C" int32_t svtgpu_comm_failed(const SvtGpuComm *c) { return c && c->failed ? 1 : 0; }
+
+// Host wait for `st` bounded by the communicator's deadline while one of its device-side collectives is outstanding
+// (any stream: the caller's waits reach the collective through stream order or events).  No communicator, a host
+// transport (its sums are synchronous) or nothing outstanding: the runtime's own wait.
+int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
+    if (!c || c->is_host || !prune(c)) {
+        HIP_TRY(hipStreamSynchronize(st));
+        return SVTGPU_OK;
+    }
+    HIP_TRY(hipEventRecord(c->wait_ev, st));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; it++) {
+        const hipError_t q = hipEventQuery(c->wait_ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) HIP_TRY(q);
+        if ((it & 63) != 63) continue;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->timeout_ms)) {
+            if (const XchRecord *r = prune(c)) return comm_timeout(c, *r);
+            HIP_TRY(hipEventSynchronize(c->wait_ev)); // every exchange done: an ordinary (long) wait
+            break;
+        }
+        std::this_thread::yield();
+    }
+    (void)prune(c);
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_comm_sync(SvtGpuComm *c, void *stream) {
+    if (!c) return SVTGPU_ERR_INVALID_ARG;
+    if (c->failed) return comm_failed(c);
+    return svtgpu_comm_wait(c, stream ? (hipStream_t)stream : svtgpu_default_stream());
+}
+
 // The element-wise sum of n uint64 over the ranks, in place.  Device buffers: enqueued on `st` (RCCL) or staged through
 // host memory with a synchronization (host transport).  Host buffers: synchronous either way.
 // A one-rank host transport is the identity and returns at once; a one-rank RCCL communicator still runs the
 // collective (the same code path, transfers and stream ordering as the N-GPU run).
-int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st) {
+int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st, const char *what) {
     if (!c || n == 0 || (c->nranks == 1 && c->is_host)) return SVTGPU_OK;
     if (!buf) return SVTGPU_ERR_INVALID_ARG;
+    if (c->failed) return comm_failed(c);
+    const uint64_t seq = ++c->seq;
     if (c->is_host) {
         uint64_t *h = (uint64_t *)buf;
         if (on_device) {
@@ -117,8 +248,14 @@ int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStrea
             h = c->pin;
         }
         if (c->host.allreduce_u64(c->host.user, h, n) != 0) {
-            svtgpu_set_last_hip_error(hipErrorUnknown, "host transport all-reduce failed", __FILE__, __LINE__);
-            return SVTGPU_ERR_HIP;
+            char sl[32];
+            slot_str(c, sl, sizeof sl);
+            std::snprintf(c->fail_msg, sizeof c->fail_msg,
+                          "exchange failed: the host-transport all-reduce of the %s (%s, rank %d of %d, exchange #%llu, "
+                          "%zu words) returned an error or timed out (deadline %d ms)",
+                          what, sl, c->rank, c->nranks, (unsigned long long)seq, n, c->timeout_ms);
+            c->failed = true;
+            return comm_failed(c);
         }
         if (on_device) { // the pinned staging is reused by the next sum, maybe from another stream: wait for the copy
             HIP_TRY(hipMemcpyAsync(buf, c->pin, n * 8, hipMemcpyHostToDevice, st));
@@ -132,10 +269,21 @@ int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStrea
         HIP_TRY(hipMemcpyAsync(c->dev, buf, n * 8, hipMemcpyHostToDevice, st));
         d = c->dev;
     }
-    if (ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, st)) return nccl_fail(r, "ncclAllReduce");
+    if (ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, st)) {
+        std::snprintf(c->fail_msg, sizeof c->fail_msg, "ncclAllReduce of the %s (exchange #%llu): %s", what,
+                      (unsigned long long)seq, ncclGetErrorString(r));
+        c->failed = true;
+        return comm_failed(c);
+    }
+    // the ring slot of this exchange: an outstanding collective 32 exchanges back is waited for (bounded) first
+    XchRecord *slot = &c->ring[seq % XCH_RING];
+    if (slot->live && hipEventQuery(slot->ev) != hipSuccess)
+        if (int rc = svtgpu_comm_wait(c, st)) return rc;
+    HIP_TRY(hipEventRecord(slot->ev, st));
+    slot->what = what, slot->seq = seq, slot->words = n, slot->live = true;
     if (!on_device) {
         HIP_TRY(hipMemcpyAsync(buf, c->dev, n * 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        return svtgpu_comm_wait(c, st);
     }
     return SVTGPU_OK;
 }
@@ -144,7 +292,7 @@ extern "C" int svtgpu_comm_allreduce_u64(SvtGpuComm *c, void *buf, size_t n, int
     if (!c) return SVTGPU_ERR_INVALID_ARG;
     // a host transport on host memory touches no device (usable without a GPU)
     hipStream_t st = stream ? (hipStream_t)stream : (c->is_host && !on_device) ? nullptr : svtgpu_default_stream();
-    return svtgpu_comm_sum(c, buf, n, on_device != 0, st);
+    return svtgpu_comm_sum(c, buf, n, on_device != 0, st, "caller's words (svtgpu_comm_allreduce_u64)");
 }
 
 // ---------------------------------------------------------------------------------------------

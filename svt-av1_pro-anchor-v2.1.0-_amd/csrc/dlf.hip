@@ -840,12 +840,12 @@ int run_searches_device_body(SvtGpuDlfState *s, const SvtGpuFrame *recon, const 
                 if (int rc = launch_tile(a, recon->bytes_per_sample, true, st)) return rc;
                 // a picture tiled over GPUs: the frame's SSEs are the sums over the ranks (every rank then takes the
                 // same decision)
-                if (int rc = svtgpu_comm_sum(s->comm, s->d_sse, MAX_JOBS * MAX_TRIALS, true, st)) return rc;
+                if (int rc = svtgpu_comm_sum(s->comm, s->d_sse, MAX_JOBS * MAX_TRIALS, true, st, SVTGPU_XCH_DLF)) return rc;
                 hipLaunchKernelGGL(dlf_search_step_kernel, dim3(1), dim3(64), 0, st, D, s->d_sse);
                 HIP_TRY(hipGetLastError());
             }
             HIP_TRY(hipMemcpyAsync(&H, D, sizeof H, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded behind the SSE exchanges
             svtgpu_count_xfer(1, sizeof H);
             if (H.plan.done) break;
             if (launches >= 1024) { // a level search ends after far fewer trials
@@ -921,7 +921,7 @@ int run_searches(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame 
         for (int j = 0; j < a.njob; j++) svtgpu_count_xfer(1, 8 * (size_t)m[j]); // the job's trial SSEs (mapped memory)
         // a picture tiled over GPUs: every rank measured its tile; the frame's SSE is the sum over the ranks, and
         // every rank then takes the same bisection step
-        if (int rc = svtgpu_comm_sum(s->comm, sse, MAX_JOBS * MAX_TRIALS, false, st)) return rc;
+        if (int rc = svtgpu_comm_sum(s->comm, sse, MAX_JOBS * MAX_TRIALS, false, st, SVTGPU_XCH_DLF)) return rc;
         for (int j = 0; j < a.njob; j++) srch[who[j]]->feed(lv[who[j]], m[j], sse + j * MAX_TRIALS);
     }
 }

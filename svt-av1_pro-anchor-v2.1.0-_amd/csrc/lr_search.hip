@@ -2518,7 +2518,15 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             HIP_TRY(hipMemsetAsync(s->d_sxarena, 0, need, st));
             s->sxarena_bytes = need;
         }
-        sr_xmode = 0x100u | (++s->sx_epoch & 0xFFu);
+        // the tag holds 8 epoch bits: when they wrap, clear the arena so no word left 256 searches ago passes for this
+        // one's.  Test-only mode: the words are visible to an item's parts only through one XCD's L2, which
+        // holds while workgroups are dealt round-robin over the 8 XCDs (SPX partition mode, positions first + 8 q);
+        // another placement makes the partner polls time out (status word -> SVTGPU_ERR_HIP), never a wrong sum
+        if ((++s->sx_epoch & 0xFFu) == 0) {
+            HIP_TRY(hipMemsetAsync(s->d_sxarena, 0, s->sxarena_bytes, st));
+            ++s->sx_epoch;
+        }
+        sr_xmode = 0x100u | (s->sx_epoch & 0xFFu);
     }
     static const bool sr_two_barriers = [] { // SVTGPU_SR_1B=0: one-part items take the two-barrier path too (A/B)
         const char *e = std::getenv("SVTGPU_SR_1B");
@@ -2833,7 +2841,7 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
         : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, outs, st);
     if (rc) return rc;
     static_assert(sizeof(SvtGpuLrUnitSearch) % 8 == 0, "records travel as uint64 words");
-    if ((rc = svtgpu_comm_sum(s->comm, rec.data(), nrec * sizeof(SvtGpuLrUnitSearch) / 8, false, st))) return rc;
+    if ((rc = svtgpu_comm_sum(s->comm, rec.data(), nrec * sizeof(SvtGpuLrUnitSearch) / 8, false, st, SVTGPU_XCH_LR))) return rc;
     std::vector<SvtGpuRestUnit> units(nrec);
     std::memset(units.data(), 0, sizeof(SvtGpuRestUnit) * nrec);
     for (int p = 0; p < nplanes; p++) {

@@ -72,6 +72,19 @@ extern "C" void svtgpu_context_destroy(SvtGpuContext *ctx) {
 
 extern "C" void *svtgpu_context_stream(SvtGpuContext *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+// Test support (the exchange deadline's abort path): one wave that spins on the 100 MHz s_memrealtime clock for `ms`
+// milliseconds (at most 10 s; every lane leaves at the same bound), holding `stream` busy.
+__global__ void stall_kernel(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+extern "C" int svtgpu_debug_stall(SvtGpuContext *ctx, void *stream, int32_t ms) {
+    if (!ctx || ms < 0 || ms > 10000) return SVTGPU_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, pick_stream(ctx, stream), 100000ull * (unsigned)ms);
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_synchronize(SvtGpuContext *ctx, void *stream) {
     if (!ctx)
         return SVTGPU_ERR_INVALID_ARG;

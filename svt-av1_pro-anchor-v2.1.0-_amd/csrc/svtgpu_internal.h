@@ -104,6 +104,8 @@ struct SvtGpuCdefFrameState {
     uint64_t      *d_pick_xch;    // persistent pick: tagged partial sums, row minima, status, diagnostics (cdef_pick.hip)
     uint32_t       pick_epoch;    // picks run by the persistent kernel (tags its exchange words)
     int32_t        pick_settle;   // the launch path's settle checkpoint: the step after which the pick checks
+    int32_t        pick_miss;     // consecutive checks that found a chain unsettled
+    int32_t        pick_skip;     // picks left that run without the check (after 2 misses: 8)
     int32_t        pick_xch_end;  // the strength count of the words in d_pick_xch (0: none written)
     uint8_t       *h_pick;        // pinned, mapped: the pick's result (PickOut) then the per-FB strengths [nfb]
     uint8_t       *h_pick_dev;    // its device address
@@ -164,8 +166,15 @@ int svtgpu_stats_unit_mfma16(int win, const uint16_t *dgd, const uint16_t *src, 
 // the stream's own synchronize wakes the host up tens of microseconds later, once per host round trip.  Falls
 // back to synchronizing `st` (and fails if the word is still missing after it).
 int svtgpu_wait_seq(const volatile unsigned long long *flag, unsigned long long seq, hipStream_t st);
-// element-wise sum of n uint64 over the ranks of `c` (comm.hip); nullptr or a one-rank comm: nothing to do
-int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st);
+// element-wise sum of n uint64 over the ranks of `c` (comm.hip); nullptr or a one-rank comm: nothing to do.  `what`
+// names the exchange in a timeout's message (SVTGPU_XCH_*)
+int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStream_t st, const char *what);
+#define SVTGPU_XCH_DLF "DLF trial SSEs"
+#define SVTGPU_XCH_CDEF "CDEF search tables"
+#define SVTGPU_XCH_LR "LR search records"
+// host wait for `st`, bounded by c's deadline while one of its device-side collectives is outstanding (comm.hip);
+// c == nullptr: hipStreamSynchronize
+int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st);
 // the tiled (gather) path runs: a comm of several ranks, or a one-rank RCCL comm (the N-GPU code path on one device)
 bool svtgpu_comm_tiled(const SvtGpuComm *c);
 // host <-> device bytes of the frame-level entry points (copies and mapped-memory results), for the bench's report

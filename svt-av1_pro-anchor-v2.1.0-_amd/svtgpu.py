@@ -354,6 +354,12 @@ _SIGS = {
     "svtgpu_comm_nranks": (_I32, [_P]),
     "svtgpu_comm_rank": (_I32, [_P]),
     "svtgpu_comm_allreduce_u64": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _I32, _P]),
+    "svtgpu_comm_set_timeout": (ctypes.c_int, [_P, _I32]),
+    "svtgpu_comm_timeout_ms": (_I32, [_P]),
+    "svtgpu_comm_set_slot": (ctypes.c_int, [_P, _I32]),
+    "svtgpu_comm_failed": (_I32, [_P]),
+    "svtgpu_comm_sync": (ctypes.c_int, [_P, _P]),
+    "svtgpu_debug_stall": (ctypes.c_int, [_P, _P, _I32]),
     "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
     "svtgpu_tile_plan_sb": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
@@ -411,6 +417,10 @@ class Context:
 
     def synchronize(self, stream=None):
         check(lib().svtgpu_synchronize(self.h, stream))
+
+    def debug_stall(self, ms, stream=None):
+        """Test support: hold `stream` busy for `ms` milliseconds (one spinning wave)."""
+        check(lib().svtgpu_debug_stall(self.h, stream, int(ms)))
 
     def close(self):
         if self.h:
@@ -515,7 +525,10 @@ class _HostTransport(ctypes.Structure):
 class Comm:
     """SvtGpuComm: the ranks of a picture tiled over GPUs.  Comm.rccl: RCCL over xGMI (one rank per device; rank 0
     makes the id with unique_id(), the caller broadcasts it); Comm.host: a host transport, `fn(words)` summing a uint64
-    numpy array over the ranks in place (e.g. a gloo all_reduce) — several ranks on one GPU, CPU rehearsals."""
+    numpy array over the ranks in place (e.g. a gloo all_reduce) — several ranks on one GPU, CPU rehearsals.  Every
+    exchange is bounded by `timeout_ms` (a host transport bounds its own wait by it: `fn(words, timeout_ms)` when fn
+    takes two arguments, raising on expiry); an expired exchange raises SvtGpuError naming it, and the communicator
+    fails from then on (`failed`)."""
 
     def __init__(self, h, keep=None):
         self.h, self._keep = h, keep
@@ -535,10 +548,17 @@ class Comm:
 
     @classmethod
     def host(cls, nranks, rank, fn):
+        import inspect
+        two = len(inspect.signature(fn).parameters) >= 2
+        box = []  # the Comm, for its deadline
+
         def cb(user, buf, n):
             try:
                 a = np.ctypeslib.as_array(buf, shape=(n,))
-                fn(a)
+                if two:
+                    fn(a, box[0]().timeout_ms)
+                else:
+                    fn(a)
                 return 0
             except Exception:  # reported through the library's return code
                 import traceback
@@ -548,11 +568,32 @@ class Comm:
         t = _HostTransport(None, f)
         h = _P()
         check(lib().svtgpu_comm_create_host(nranks, rank, ctypes.byref(t), ctypes.byref(h)))
-        return cls(h, keep=(f, t))
+        c = cls(h, keep=(f, t))
+        import weakref
+        box.append(weakref.ref(c))  # no reference cycle through the callback
+        return c
 
     @property
     def nranks(self):
         return lib().svtgpu_comm_nranks(self.h)
+
+    @property
+    def timeout_ms(self):
+        return lib().svtgpu_comm_timeout_ms(self.h)
+
+    def set_timeout(self, ms):
+        check(lib().svtgpu_comm_set_timeout(self.h, int(ms)))
+
+    def set_slot(self, slot):
+        check(lib().svtgpu_comm_set_slot(self.h, int(slot)))
+
+    @property
+    def failed(self):
+        return bool(lib().svtgpu_comm_failed(self.h))
+
+    def sync(self, stream=None):
+        """Wait for `stream`, bounded by the deadline while a device-side exchange is outstanding."""
+        check(lib().svtgpu_comm_sync(self.h, stream))
 
     def allreduce(self, words, stream=None):
         """Sum a host uint64 array over the ranks in place."""

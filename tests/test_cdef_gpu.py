@@ -320,10 +320,13 @@ def _settle_calls(mse, skip, end=64):
     return out
 
 
-def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch):
+@pytest.mark.parametrize("scale_hi", [1 << 20, 1 << 14])
+def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch, scale_hi):
     """The launch-per-step pick's period shortcut: convex per-FB strength curves (random optimum and scale per FB)
     whose greedy chains settle at different calls -- and, for some seeds, never -- bit-exact vs the oracle, the
-    pick repeated on the same state (the step values of the previous pick stay behind)."""
+    pick repeated on the same state (the step values of the previous pick stay behind).  scale_hi 2^20: entries above
+    2^31 (the 64-bit path); 2^14: every entry below 2^31 (pick_gather's `wide` stays 0), so the steps stage the low words in LDS (the padded
+    132-dword rows, the 32-bit per-FB best) -- both with settled and unsettled chains."""
     import torch
     monkeypatch.setenv("SVTGPU_PICK_PERSIST", "0")
     w, h, q, lam = 1920, 1080, 128, 60000
@@ -334,8 +337,9 @@ def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch):
         rng = np.random.default_rng(seed)
         j = np.arange(64)
         opt = rng.integers(0, 64, size=(2, st.nfb, 1))
-        scale = rng.integers(1 << 10, 1 << 20, size=(2, st.nfb, 1))
+        scale = rng.integers(1 << 10, scale_hi, size=(2, st.nfb, 1))
         mse = (scale * (64 + (j - opt) ** 2) + rng.integers(0, 1 << 12, size=(2, st.nfb, 64))).astype(np.uint64)
+        assert (mse.max() < (1 << 31)) == (scale_hi < (1 << 17))
         skip = (rng.random(st.nfb) < 0.1).astype(np.uint8)
         seen.update(x is None for x in _settle_calls(mse, skip)[1:])
         mse_t = torch.from_numpy(mse.view(np.int64)).cuda()

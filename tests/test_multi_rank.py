@@ -164,3 +164,63 @@ def test_tiled_exchanges(world):
         assert cdef_ok and pick_ok, "rank %d: CDEF table exchange" % rank
         assert dlf_ok, "rank %d: DLF SSE sum" % rank
         assert md_ok, "rank %d: MD SB bands" % rank
+
+
+def _skip_worker(rank, world, port, out):
+    """Rank 1 skips an exchange (and stays alive past the deadline); rank 0's exchange must end with the named error
+    within the deadline instead of hanging."""
+    import datetime
+    import time
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(backend="gloo")  # the data exchanges' own group; the default group stays for control
+    try:
+        def allreduce(words, timeout_ms):  # the host transport bounds its wait by the communicator's deadline
+            w = dist.all_reduce(torch.from_numpy(words.view(np.int64)), group=grp, async_op=True)
+            w.wait(timeout=datetime.timedelta(milliseconds=timeout_ms))
+
+        comm = svtgpu.Comm.host(world, rank, allreduce)
+        comm.set_timeout(1500)
+        comm.set_slot(3)
+        assert comm.timeout_ms == 1500
+        a = np.arange(8, dtype=np.uint64)
+        ok = np.array_equal(comm.allreduce(a.copy()), a * world)  # one matched exchange first
+        if rank == 0:
+            t0 = time.monotonic()
+            try:
+                comm.allreduce(a.copy())
+                msg = "no error"
+            except svtgpu.SvtGpuError as e:
+                msg = str(e)
+            dt = time.monotonic() - t0
+            try:  # the communicator fails every later call
+                comm.allreduce(a.copy())
+                later = "no error"
+            except svtgpu.SvtGpuError as e:
+                later = str(e)
+            out.put((ok, msg, dt, comm.failed, later))
+        else:
+            time.sleep(4.0)  # skipped the exchange; alive past rank 0's deadline
+        dist.barrier()
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_transport_skipped_exchange_times_out():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skip_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    ok, msg, dt, failed, later = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+    assert "exchange failed" in msg and "caller's words" in msg and "frame slot 3" in msg and "exchange #2" in msg, msg
+    assert dt < 1.5 + 2.0, dt  # the deadline, not a hang
+    assert failed and "exchange #2" in later
+    assert all(p.exitcode == 0 for p in procs)

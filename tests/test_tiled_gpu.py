@@ -192,3 +192,158 @@ def test_cdef_bound_tables_exact_size_tiled_pick_twice(rccl1):
     assert np.array_equal(fbs1, fbs0) and np.array_equal(fbs2, fbs0)
     for x in (R, S, ref, st):
         x.close()
+
+
+@pytest.mark.gpu
+def test_rccl_exchange_deadline_aborts():
+    """The RCCL branch of the exchange deadline (one rank): a collective held behind a stalled stream is still
+    outstanding when the deadline expires, so the bounded wait names it, aborts the communicator (ncclCommAbort) and
+    fails every later call; the stream itself drains (the stall ends on its own clock).  A deadline that expires with
+    no collective outstanding is an ordinary wait (no false timeout)."""
+    import time
+    import torch
+    import svtgpu
+    ctx = svtgpu.Context(0)
+    comm = svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id())
+    comm.set_timeout(400)
+    comm.set_slot(2)
+    s = torch.cuda.Stream()
+    t = torch.arange(64, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    # no collective outstanding: a stall longer than the deadline is waited for, not reported
+    comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
+    ctx.debug_stall(900, s.cuda_stream)
+    time.sleep(0.05)
+    comm.sync(s.cuda_stream)
+    assert not comm.failed
+    # the collective queued behind the stall: outstanding at the deadline
+    ctx.debug_stall(2500, s.cuda_stream)
+    comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
+    t0 = time.monotonic()
+    with pytest.raises(svtgpu.SvtGpuError) as ei:
+        comm.sync(s.cuda_stream)
+    dt = time.monotonic() - t0
+    msg = str(ei.value)
+    assert "exchange timed out" in msg and "caller's words" in msg and "frame slot 2" in msg and "aborted" in msg, msg
+    assert dt < 2.0, dt
+    assert comm.failed
+    with pytest.raises(svtgpu.SvtGpuError):
+        comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
+    ctx.synchronize(s.cuda_stream)  # the stall drains on its own
+    assert torch.equal(t.cpu(), torch.arange(64, dtype=torch.int64))
+    comm.close()
+    ctx.close()
+
+
+def _skip_pick_worker(rank, world, port, q):
+    import datetime
+    import time
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(backend="gloo")
+    try:
+        import svtgpu
+        import synth
+
+        def allreduce(words, timeout_ms):
+            w = dist.all_reduce(torch.from_numpy(words.view(np.int64)), group=grp, async_op=True)
+            w.wait(timeout=datetime.timedelta(milliseconds=timeout_ms))
+
+        comm = svtgpu.Comm.host(world, rank, allreduce)
+        comm.set_timeout(2000)
+        comm.set_slot(1)
+        ctx = svtgpu.Context(0)
+        w, h, bd, qi, lam = 640, 384, 10, 128, 60000
+        src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0777)
+        R, S = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+        R.upload(rec)
+        S.upload(src)
+        plan = svtgpu.tile_plan(w, h, [64, 32, 32], *svtgpu.tile_grid(world), rank).rects()
+        st = svtgpu.CdefState(ctx, w, h)
+        st.set_tile(plan["fb_rect"], plan["cdef_out"], comm)
+        ctrls = svtgpu.cdef_controls(1)
+        st.search(R, S, ctrls, qi)
+        if rank == 0:
+            t0 = time.monotonic()
+            try:
+                st.pick(ctrls, qi, lam)
+                msg = "no error"
+            except svtgpu.SvtGpuError as e:
+                msg = str(e)
+            q.put((msg, time.monotonic() - t0, comm.failed))
+        else:
+            time.sleep(5.0)  # skips the pick's exchange, alive past rank 0's deadline
+        dist.barrier()
+        for x in (st, R, S, comm):
+            x.close()
+    except BaseException as e:
+        q.put(("ERROR: %r" % e, 0.0, False))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(180)
+def test_skipped_cdef_exchange_times_out_named():
+    """Two ranks of a tiled picture on the one GPU (host transport over gloo): rank 1 searches its filter blocks but
+    never reaches the pick; rank 0's pick returns the named error ("CDEF search tables", frame slot, exchange number)
+    within the communicator's deadline instead of hanging."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_skip_pick_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        msg, dt, failed = q.get(timeout=150)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert "exchange failed" in msg and "CDEF search tables" in msg and "frame slot 1" in msg, msg
+    assert dt < 2.0 + 3.0, dt
+    assert failed
+
+
+@pytest.mark.gpu
+def test_cdef_rebind_tables_between_picks_sums_again():
+    """binding other tables (or another tile / comm) between two picks with no search in between must make
+    the next pick sum the tables over the ranks again.  A two-rank host communicator in one process whose other rank
+    contributes zeros (the transport is the identity and counts its calls): after a rebind the pick exchanges again
+    and picks from the new tables, equal to an untiled pick over them."""
+    import torch
+    import svtgpu
+    ctx = svtgpu.Context(0)
+    calls = []
+    comm = svtgpu.Comm.host(2, 0, lambda words: calls.append(words.size))
+    w, h, q, lam = 1024, 512, 128, 60000
+    ctrls = svtgpu.cdef_controls(1)
+    st, ref = svtgpu.CdefState(ctx, w, h), svtgpu.CdefState(ctx, w, h)
+    st.set_tile(None, None, comm)
+    rng = np.random.default_rng(77)
+    picks = []
+    for k in range(2):
+        mse = rng.integers(1 << 20, 1 << 30, size=(2, st.nfb, 64), dtype=np.int64).astype(np.uint64)
+        skip = (rng.random(st.nfb) < 0.1).astype(np.uint8)
+        mse_t = torch.from_numpy(mse.view(np.int64)).cuda()
+        skip_t = torch.from_numpy(skip).cuda()
+        torch.cuda.synchronize()
+        n0 = len(calls)
+        st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+        prm, fbs = st.pick(ctrls, q, lam)
+        assert len(calls) > n0, "pick %d after a rebind did not exchange the tables" % k
+        ref.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+        rprm, rfbs = ref.pick(ctrls, q, lam)
+        assert prm.as_tuple() == rprm.as_tuple() and np.array_equal(fbs, rfbs), k
+        picks.append(prm.as_tuple())
+        n1 = len(calls)
+        st.pick(ctrls, q, lam)  # same tables, no rebind: gathered already, no second exchange
+        assert len(calls) == n1
+        del mse_t, skip_t
+    for x in (st, ref, comm, ctx):
+        x.close()
