@@ -173,6 +173,9 @@ int32_t svtgpu_comm_failed(const SvtGpuComm *c);
 /* host wait for `stream`, bounded by the deadline while one of the communicator's device-side exchanges (enqueued
  * without a host wait: svtgpu_comm_allreduce_u64 on device memory) is outstanding */
 int     svtgpu_comm_sync(SvtGpuComm *c, void *stream);
+/* the number of per-block RTCD shim calls this process made (each runs on the process-wide default context): evidence
+ * that an encoder with the shims installed really ran its kernels on the device */
+uint64_t svtgpu_shim_calls(void);
 /* test support: holds `stream` busy for `ms` milliseconds (<= 10000) with one spinning wave */
 int     svtgpu_debug_stall(SvtGpuContext *ctx, void *stream, int32_t ms);
 

@@ -1,0 +1,49 @@
+# oracle/enc.mk — builds the REFERENCE ENCODER itself (every C source of Source/Lib/Common, Source/Lib/Encoder and
+# third_party/fastfeat, straight from /root/reference with gcc) into oracle/_ref/enc/libsvtenc.so, and the drop-in
+# harness that links it with libsvtgpu (oracle/ref_harness/enc_drop_in.c; tests/test_encoder_drop_in.py).
+# Test infrastructure only: the encoder's public API drives its own DLF / CDEF / LR process
+# bodies with libsvtgpu installed.  The reference's cmake build is NOT used.
+#
+# C-only configuration (the reference's COMPILE_C_ONLY: no ARCH_X86_64, so its NASM sources -- which this image cannot
+# assemble -- are not needed and the RTCD setup binds the C kernels).  One generated file: EbVersion.h, which the
+# reference's cmake instantiates from its own template Source/Lib/Common/Codec/EbVersion.h.in (configure_file,
+# Source/Lib/Common/Codec/CMakeLists.txt:15-17) with the project version of CMakeLists.txt:14 (2.1.0); the recipe
+# does the same substitution with sed, into the build directory.
+#
+#   make -f oracle/enc.mk -j8            # from the repo root
+REF      ?= /root/reference
+OUT      ?= oracle/_ref/enc
+S        := $(REF)/Source
+CC       ?= gcc
+SVTGPU   := svt-av1_pro-anchor-v2.1.0-_amd/lib
+INC      := -I$(S)/API -I$(S)/Lib/Common/Codec -I$(S)/Lib/Common/C_DEFAULT -I$(S)/Lib/Encoder/Codec \
+            -I$(S)/Lib/Encoder/C_DEFAULT -I$(S)/Lib/Encoder/Globals -I$(REF)/third_party/fastfeat -I$(REF) -I$(OUT)/gen
+CFLAGS   := -O2 -fPIC -w -std=gnu99 $(INC)
+ENC_SRC  := $(wildcard $(S)/Lib/Common/Codec/*.c $(S)/Lib/Common/C_DEFAULT/*.c $(S)/Lib/Encoder/Codec/*.c \
+                       $(S)/Lib/Encoder/C_DEFAULT/*.c $(S)/Lib/Encoder/Globals/*.c $(REF)/third_party/fastfeat/*.c)
+ENC_OBJ  := $(patsubst $(REF)/%.c,$(OUT)/obj/%.o,$(ENC_SRC))
+
+all: $(OUT)/libsvtenc.so $(OUT)/enc_drop_in
+
+$(OUT)/gen/EbVersion.h: $(S)/Lib/Common/Codec/EbVersion.h.in
+	@mkdir -p $(dir $@)
+	sed 's/@PACKAGE_VERSION_STRING@/v2.1.0/' $< > $@
+
+$(OUT)/obj/%.o: $(REF)/%.c $(OUT)/gen/EbVersion.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/libsvtenc.so: $(ENC_OBJ)
+	$(CC) -shared -o $@ $^ -lm -lpthread
+
+# the harness: the reference's public API + include/svtgpu_rtcd.h (no casts: the install compiles against the
+# reference's own RTCD declarations), the frame-level hooks (enc_frame_hooks.c) defined in the executable
+$(OUT)/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_frame_hooks.c $(OUT)/libsvtenc.so \
+                    $(SVTGPU)/libsvtgpu.so
+	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
+	    -L$(OUT) -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../$(SVTGPU)' \
+	    -ldl -lm -lpthread
+
+clean:
+	rm -rf $(OUT)
+.PHONY: all clean

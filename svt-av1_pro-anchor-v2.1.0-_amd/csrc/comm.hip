@@ -95,13 +95,14 @@ void slot_str(const SvtGpuComm *c, char *b, size_t n) {
     else std::snprintf(b, n, "frame slot unset");
 }
 // the deadline expired with `r` outstanding: name it, abort RCCL, fail from now on
-int comm_timeout(SvtGpuComm *c, const XchRecord &r) {
+int comm_timeout(SvtGpuComm *c, const XchRecord &r, long long waited_ms) {
     char sl[32];
     slot_str(c, sl, sizeof sl);
     std::snprintf(c->fail_msg, sizeof c->fail_msg,
                   "exchange timed out: the all-reduce of the %s (%s, rank %d of %d, exchange #%llu, %zu words) did not "
-                  "complete within %d ms -- a peer rank skipped or never reached it; RCCL communicator aborted",
-                  r.what, sl, c->rank, c->nranks, (unsigned long long)r.seq, r.words, c->timeout_ms);
+                  "complete within %d ms (detected after %lld ms) -- a peer rank skipped or never reached it; RCCL "
+                  "communicator aborted",
+                  r.what, sl, c->rank, c->nranks, (unsigned long long)r.seq, r.words, c->timeout_ms, waited_ms);
     c->failed = true;
     if (c->nccl) (void)ncclCommAbort(c->nccl); // ends this rank's pending collectives
     c->nccl = nullptr;
@@ -213,8 +214,10 @@ int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
         if (q == hipSuccess) break;
         if (q != hipErrorNotReady) HIP_TRY(q);
         if ((it & 63) != 63) continue;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->timeout_ms)) {
-            if (const XchRecord *r = prune(c)) return comm_timeout(c, *r);
+        const auto waited = std::chrono::steady_clock::now() - t0;
+        if (waited > std::chrono::milliseconds(c->timeout_ms)) {
+            if (const XchRecord *r = prune(c))
+                return comm_timeout(c, *r, std::chrono::duration_cast<std::chrono::milliseconds>(waited).count());
             HIP_TRY(hipEventSynchronize(c->wait_ev)); // every exchange done: an ordinary (long) wait
             break;
         }

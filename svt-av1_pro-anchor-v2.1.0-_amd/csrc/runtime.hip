@@ -110,7 +110,13 @@ SvtGpuContext        *svtgpu_default_context() {
         svtgpu_fatal("svtgpu per-block shim called without a usable gfx950 device");
     return g_default_ctx;
 }
-hipStream_t svtgpu_default_stream() { return svtgpu_default_context()->stream; }
+// every per-block shim launches on the default context's stream: its uses count the shim calls (svtgpu_shim_calls)
+static std::atomic<unsigned long long> g_shim_calls{0};
+hipStream_t svtgpu_default_stream() {
+    g_shim_calls.fetch_add(1, std::memory_order_relaxed);
+    return svtgpu_default_context()->stream;
+}
+extern "C" uint64_t svtgpu_shim_calls(void) { return g_shim_calls.load(); }
 
 static std::atomic<unsigned long long> g_xfer[2];
 void svtgpu_count_xfer(int d2h, size_t bytes) { g_xfer[d2h ? 1 : 0] += bytes; }

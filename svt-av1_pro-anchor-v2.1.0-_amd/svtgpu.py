@@ -360,6 +360,7 @@ _SIGS = {
     "svtgpu_comm_failed": (_I32, [_P]),
     "svtgpu_comm_sync": (ctypes.c_int, [_P, _P]),
     "svtgpu_debug_stall": (ctypes.c_int, [_P, _P, _I32]),
+    "svtgpu_shim_calls": (ctypes.c_uint64, []),
     "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
     "svtgpu_tile_plan_sb": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),

@@ -225,7 +225,12 @@ def test_rccl_exchange_deadline_aborts():
     dt = time.monotonic() - t0
     msg = str(ei.value)
     assert "exchange timed out" in msg and "caller's words" in msg and "frame slot 2" in msg and "aborted" in msg, msg
-    assert dt < 2.0, dt
+    # detected at the deadline; the abort itself may then wait for the stalled (non-RCCL) kernel on the stream -- a
+    # hung collective's own kernel ends on ncclCommAbort's abort flag
+    import re
+    detected = int(re.search(r"detected after (\d+) ms", msg).group(1))
+    assert 400 <= detected < 1000, msg
+    assert dt < 2.5 + 1.0, dt
     assert comm.failed
     with pytest.raises(svtgpu.SvtGpuError):
         comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
