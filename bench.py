@@ -158,6 +158,8 @@ def parse():
                     help="pinned: the reference-pinned pipeline case of this size when there is one (else synth); "
                          "synth: the float generator (synth.frame_pair)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
+    ap.add_argument("--lr-levels", default="1,1", metavar="WN,SG",
+                    help="diagnostic only (sensitivity runs; the headline is 1,1): the Wiener / self-guided search levels")
     ap.add_argument("--stages", default="all", choices=("all", "cdef", "md"),
                     help="'all' = the whole step; 'cdef' = CDEF search + pick + apply on the recon alone (SURVEY §8d "
                          "configs 1/2)")
@@ -637,7 +639,9 @@ def main():
     # whose mode decision runs on the device hands it over there); each step copies it into the DLF state
     mi_dev = torch.from_numpy(np.ascontiguousarray(mi).view(np.uint8).reshape(-1).copy()).cuda(local)
     lf_start = svtgpu.LfParams.make(*cfg["lf"])  # the previous frame's levels (search start)
-    lr_ctrls = svtgpu.lr_controls(1, 1, rdmult=cfg["rdmult"], switchable=cfg["sw"], wiener=cfg["wc"], sgrproj=cfg["sc"])
+    wn_lv, sg_lv = (int(x) for x in a.lr_levels.split(","))
+    lr_ctrls = svtgpu.lr_controls(wn_lv, sg_lv, rdmult=cfg["rdmult"], switchable=cfg["sw"], wiener=cfg["wc"],
+                                  sgrproj=cfg["sc"])
     gx, gy = svtgpu.tile_grid(n) if tiled else (1, 1)
     md_nsb = ((W + 63) // 64) * ((H + 63) // 64)
     plan = svtgpu.tile_plan(W, H, lr_us, gx, gy, rank).rects() if tiled else None

@@ -42,7 +42,7 @@ $(OUT)/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_fram
                     $(SVTGPU)/libsvtgpu.so
 	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
 	    -L$(OUT) -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../$(SVTGPU)' \
-	    -ldl -lm -lpthread
+	    -rdynamic -ldl -lm -lpthread
 
 clean:
 	rm -rf $(OUT)

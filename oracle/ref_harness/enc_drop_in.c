@@ -9,7 +9,7 @@
  *   rtcd   the same, with include/svtgpu_rtcd.h's svtgpu_install_filter_rtcd() called right after svt_av1_enc_init:
  *          the encoder's DLF / CDEF / LR / full-distortion RTCD pointers (read at call time by svt_aom_dlf_kernel,
  *          svt_aom_cdef_kernel, svt_aom_rest_kernel and mode decision) now run libsvtgpu's device kernels;
- *   frame  rtcd, plus the frame-level entry points: enc_frame_hooks.c defines the encoder's frame-level filter calls
+ *   frame  the frame-level entry points alone (the RTCD pointers stay the encoder's C): enc_frame_hooks.c defines the encoder's frame-level filter calls
  *          (svt_av1_pick_filter_level, svt_av1_loop_filter_frame, finish_cdef_search, svt_av1_cdef_frame,
  *          rest_finish_search, svt_av1_loop_restoration_filter_frame; EbDlfProcess.c:55-153, EbCdefProcess.c:364-738,
  *          EbRestProcess.c:520-640) in this executable; ELF symbol interposition makes the library's calls land on them,
@@ -17,7 +17,7 @@
  * tests/test_encoder_drop_in.py compares the three bitstreams byte for byte.
  *
  *   enc_drop_in <cpu|rtcd|frame> <out.obu> [width height frames preset qp]
- * Prints one line: "<mode> bytes <n> frames <n> shim_calls <n> frame_calls <n>".
+ * Prints one line: "<mode> bytes <n> packets <n> shim_calls <n> frame_calls <n> frame_fallbacks <n>".
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -33,8 +33,10 @@
 #include "EbMcp.h"
 #include "svtgpu_rtcd.h"
 
-uint64_t enc_frame_hook_calls(void); /* enc_frame_hooks.c (frame mode) or the stub below (cpu / rtcd builds) */
+uint64_t enc_frame_hook_calls(void); /* enc_frame_hooks.c: hooked frame-level calls served by libsvtgpu */
+uint64_t enc_frame_hook_fallbacks(void); /* ... and those left to the encoder's own function */
 void     enc_frame_hooks_enable(int on);
+void     enc_frame_hook_kinds(uint64_t out[7]);
 
 /* a deterministic synthetic 10-bit picture: gradients, a moving disc, texture and noise (LCG) */
 static void fill_frame(uint16_t *y, uint16_t *u, uint16_t *v, int w, int h, int k) {
@@ -76,15 +78,15 @@ int main(int argc, char **argv) {
         return 2;
     }
     const char *mode   = argv[1];
-    const int   rtcd   = !strcmp(mode, "rtcd") || !strcmp(mode, "frame");
+    const int   rtcd   = !strcmp(mode, "rtcd");
     const int   frame  = !strcmp(mode, "frame");
     const int   w      = argc > 3 ? atoi(argv[3]) : 320;
     const int   h      = argc > 4 ? atoi(argv[4]) : 192;
     const int   nfr    = argc > 5 ? atoi(argv[5]) : 5;
     const int   preset = argc > 6 ? atoi(argv[6]) : 2;
     const int   qp     = argc > 7 ? atoi(argv[7]) : 40;
-    if (!rtcd && strcmp(mode, "cpu")) return 2;
-    if (rtcd && !svtgpu_device_available()) {
+    if (!rtcd && !frame && strcmp(mode, "cpu")) return 2;
+    if ((rtcd || frame) && !svtgpu_device_available()) {
         fprintf(stderr, "enc_drop_in: no gfx950 device\n");
         return 3;
     }
@@ -175,8 +177,16 @@ int main(int argc, char **argv) {
     fclose(out);
     check(svt_av1_enc_deinit(enc), "svt_av1_enc_deinit");
     check(svt_av1_enc_deinit_handle(enc), "svt_av1_enc_deinit_handle");
-    printf("%s bytes %zu packets %d shim_calls %llu frame_calls %llu\n", mode, total, got,
-           (unsigned long long)(rtcd ? svtgpu_shim_calls() : 0), (unsigned long long)enc_frame_hook_calls());
+    printf("%s bytes %zu packets %d shim_calls %llu frame_calls %llu frame_fallbacks %llu\n", mode, total, got,
+           (unsigned long long)(rtcd || frame ? svtgpu_shim_calls() : 0), (unsigned long long)enc_frame_hook_calls(),
+           (unsigned long long)enc_frame_hook_fallbacks());
+    if (frame) {
+        uint64_t k[7];
+        enc_frame_hook_kinds(k);
+        printf("frame kinds dlf_pick %llu dlf_frame %llu cdef_pick %llu cdef_apply %llu lr_search %llu lr_apply %llu "
+               "lr_on %llu\n", (unsigned long long)k[0], (unsigned long long)k[1], (unsigned long long)k[2],
+               (unsigned long long)k[3], (unsigned long long)k[4], (unsigned long long)k[5], (unsigned long long)k[6]);
+    }
     free(y), free(u), free(v);
     return 0;
 }

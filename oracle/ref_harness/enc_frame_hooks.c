@@ -1,19 +1,539 @@
 /*
- * enc_frame_hooks.c — the frame-level entry points of libsvtgpu inside the reference encoder (test infrastructure).
- * Placeholder of the interposed frame-level calls: the hooks are off and every call stays the encoder's own.
+ * enc_frame_hooks.c — libsvtgpu's frame-level entry points inside the reference encoder (test infrastructure; the
+ * `frame` mode of enc_drop_in, tests/test_encoder_drop_in.py).
+ *
+ * The encoder's process bodies call their frame-level filter functions across translation units of libsvtenc.so,
+ * through the PLT.  This file defines the same symbols in the executable, so ELF symbol interposition binds the
+ * library's calls here (no reference source is edited or copied):
+ *   svt_aom_dlf_kernel   (EbDlfProcess.c:96-106):  svt_av1_pick_filter_level(FULL_IMAGE) -> svtgpu_dlf_pick,
+ *                                                  svt_av1_loop_filter_frame              -> svtgpu_dlf_frame;
+ *   svt_aom_cdef_kernel  (EbCdefProcess.c:509-515): finish_cdef_search -> svtgpu_cdef_search_frame + svtgpu_cdef_pick
+ *                                                  (the whole-frame device search; the process body's own per-segment
+ *                                                  cdef_seg_search is static and still runs, its tables unused),
+ *                                                  svt_av1_cdef_frame -> svtgpu_cdef_apply_frame;
+ *   svt_aom_rest_kernel  (EbRestProcess.c:580-626): restoration_seg_search -> nothing (the device searches the frame),
+ *                                                  rest_finish_search -> svtgpu_lr_search_frame + svtgpu_lr_finish_plane,
+ *                                                  svt_av1_loop_restoration_filter_frame -> svtgpu_lr_apply_frame.
+ * Each hook moves the encoder's picture buffers to the device (svtgpu_frame_upload) and its results back into the
+ * encoder's own structures exactly where the reference function writes them (frame header fields, mode-info grid,
+ * restoration units, the recon samples).  Configurations the library does not cover (DLF methods other than
+ * FULL_IMAGE, delta LF, superres / resize, the previous-frame Wiener coefficients, the reference-based SGR ep range,
+ * frame sizes off the 8-sample grid) call the encoder's own function (dlsym RTLD_NEXT) and count a fallback.
  */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
-static int      g_on;
-static uint64_t g_calls;
+#include "EbDefinitions.h"
+#include "EbPictureControlSet.h"
+#include "EbSequenceControlSet.h"
+#include "EbDeblockingFilter.h"
+#include "EbRestoration.h"
+#include "EbModeDecisionProcess.h"
+#include "EbInterPrediction.h"
+#include "aom_dsp_rtcd.h"
+#include "common_dsp_rtcd.h"
+#include "EbMcp.h"
+#include "svtgpu_rtcd.h"
 
-void enc_frame_hooks_enable(int on) {
-    if (on) {
-        fprintf(stderr, "enc_drop_in: frame-level hooks not built\n");
-        exit(5);
-    }
-    g_on = on;
-}
+void    svt_aom_get_recon_pic(PictureControlSet *pcs, EbPictureBufferDesc **recon_ptr, Bool is_highbd);
+int32_t svt_sb_all_skip(PictureControlSet *pcs, const Av1Common *const cm, int32_t mi_row, int32_t mi_col);
+
+static int             g_on;
+static uint64_t        g_calls, g_fallbacks;
+/* device calls by kind: DLF pick, DLF filter, CDEF pick, CDEF apply, LR search, LR apply; and frames whose LR search
+ * chose a filter for some plane (so the apply really filtered) */
+enum { K_DLF_PICK, K_DLF_FRAME, K_CDEF_PICK, K_CDEF_APPLY, K_LR_SEARCH, K_LR_APPLY, K_LR_ON, K_N };
+static uint64_t g_kind[K_N];
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static SvtGpuContext  *g_ctx;
+
+void enc_frame_hooks_enable(int on) { g_on = on; }
 uint64_t enc_frame_hook_calls(void) { return g_calls; }
+uint64_t enc_frame_hook_fallbacks(void) { return g_fallbacks; }
+void enc_frame_hook_kinds(uint64_t out[7]) { memcpy(out, g_kind, sizeof g_kind); }
+
+static void die(const char *what, int rc) {
+    fprintf(stderr, "enc_frame_hooks: %s failed (%d): %s\n", what, rc, svtgpu_error_string(rc));
+    exit(6);
+}
+#define GPU(call)                              \
+    do {                                       \
+        int rc_ = (call);                      \
+        if (rc_ != SVTGPU_OK) die(#call, rc_); \
+    } while (0)
+
+static void count_kind(int fallback, int kind) {
+    pthread_mutex_lock(&g_mu);
+    if (fallback) g_fallbacks++;
+    else g_calls++, g_kind[kind]++;
+    pthread_mutex_unlock(&g_mu);
+}
+#define count(fb) count_kind(fb, KIND)
+
+/* ---- per-picture device state (the encoder runs several pictures through the stages at once) ---- */
+typedef struct Ctx {
+    PictureControlSet    *pcs;
+    int                   w, h, bd;
+    SvtGpuFrame          *R, *S, *D, *O, *L; /* recon in, source, deblocked (pre-CDEF), CDEF output, LR output */
+    SvtGpuDlfState       *dlf;
+    SvtGpuCdefFrameState *cdef;
+    SvtGpuLrState        *lr;
+    int32_t               lr_units[3];
+    int                   d_valid, cdef_searched, lr_searched;
+    int32_t               lr_ft[3];
+} Ctx;
+static Ctx g_ctxs[64];
+
+static Ctx *ctx_of(PictureControlSet *pcs) {
+    pthread_mutex_lock(&g_mu);
+    if (!g_ctx) GPU(svtgpu_context_create(0, &g_ctx));
+    Ctx *c = NULL;
+    for (int i = 0; i < 64 && !c; i++)
+        if (g_ctxs[i].pcs == pcs) c = &g_ctxs[i];
+    for (int i = 0; i < 64 && !c; i++)
+        if (!g_ctxs[i].pcs) c = &g_ctxs[i], c->pcs = pcs;
+    pthread_mutex_unlock(&g_mu);
+    if (!c) die("ctx_of: more than 64 pictures in flight", -1);
+    SequenceControlSet *scs = pcs->scs;
+    Av1Common          *cm  = pcs->ppcs->av1_cm;
+    const int w = cm->frm_size.frame_width, h = cm->frm_size.frame_height, bd = (int)scs->static_config.encoder_bit_depth;
+    if (c->R && (c->w != w || c->h != h || c->bd != bd)) die("picture geometry changed", -1);
+    if (!c->R) {
+        c->w = w, c->h = h, c->bd = bd;
+        SvtGpuFrame **f[5] = {&c->R, &c->S, &c->D, &c->O, &c->L};
+        for (int i = 0; i < 5; i++) GPU(svtgpu_frame_create(g_ctx, w, h, bd, f[i]));
+        GPU(svtgpu_dlf_state_create(g_ctx, w, h, &c->dlf));
+        GPU(svtgpu_cdef_state_create(g_ctx, w, h, &c->cdef));
+    }
+    return c;
+}
+
+/* the visible-area origin and stride (samples) of each plane of an encoder picture buffer */
+static void pic_planes(const EbPictureBufferDesc *p, int is16, void *pl[3], int32_t st[3]) {
+    const int b = is16 ? 2 : 1;
+    pl[0] = p->buffer_y + (size_t)(p->org_x + p->org_y * p->stride_y) * b;
+    pl[1] = p->buffer_cb + (size_t)((p->org_x >> 1) + (p->org_y >> 1) * p->stride_cb) * b;
+    pl[2] = p->buffer_cr + (size_t)((p->org_x >> 1) + (p->org_y >> 1) * p->stride_cr) * b;
+    st[0] = p->stride_y, st[1] = p->stride_cb, st[2] = p->stride_cr;
+}
+static void upload_pic(SvtGpuFrame *f, const EbPictureBufferDesc *p, int is16, int p0, int p1) {
+    void   *pl[3];
+    int32_t st[3];
+    pic_planes(p, is16, pl, st);
+    for (int q = p0; q < p1; q++) GPU(svtgpu_frame_upload(f, q, pl[q], st[q], NULL));
+}
+static void download_pic(SvtGpuFrame *f, EbPictureBufferDesc *p, int is16, int p0, int p1) {
+    void   *pl[3];
+    int32_t st[3];
+    pic_planes(p, is16, pl, st);
+    for (int q = p0; q < p1; q++) GPU(svtgpu_frame_download(f, q, pl[q], st[q], NULL));
+    GPU(svtgpu_synchronize(g_ctx, NULL));
+}
+/* Yv12BufferConfig planes (16-bit buffers are CONVERT_TO_BYTEPTR addresses) */
+static void yv12_planes(const Yv12BufferConfig *y, int hbd, void *pl[3], int32_t st[3]) {
+    uint8_t *b[3] = {y->y_buffer, y->u_buffer, y->v_buffer};
+    for (int q = 0; q < 3; q++) pl[q] = hbd ? (void *)CONVERT_TO_SHORTPTR(b[q]) : (void *)b[q];
+    st[0] = y->y_stride, st[1] = st[2] = y->uv_stride;
+}
+
+/* the library covers 4:2:0 pictures on the 8-sample grid, 8/10-bit, without superres / resize */
+static int frame_supported(PictureControlSet *pcs) {
+    SequenceControlSet *scs = pcs->scs;
+    Av1Common          *cm  = pcs->ppcs->av1_cm;
+    const int w = cm->frm_size.frame_width, h = cm->frm_size.frame_height, bd = (int)scs->static_config.encoder_bit_depth;
+    return g_on && (w & 7) == 0 && (h & 7) == 0 && (bd == 8 || bd == 10) &&
+           scs->static_config.encoder_color_format == EB_YUV420 && scs->static_config.superres_mode == SUPERRES_NONE &&
+           scs->static_config.resize_mode == RESIZE_NONE && cm->frm_size.superres_upscaled_width == w &&
+           (scs->seq_header.sb_size == BLOCK_64X64 || scs->seq_header.sb_size == BLOCK_128X128);
+}
+
+/* The deblocked picture, before CDEF: the DLF process saves the restoration stripe boundaries from it
+ * (EbDlfProcess.c:112-114, after_cdef = 0); the device LR apply reads those rows from this copy (D) instead */
+typedef void (*SaveLinesFn)(const Yv12BufferConfig *, Av1Common *, int32_t);
+void svt_av1_loop_restoration_save_boundary_lines(const Yv12BufferConfig *frame, Av1Common *cm, int32_t after_cdef) {
+    static SaveLinesFn orig;
+    if (!orig) orig = (SaveLinesFn)dlsym(RTLD_NEXT, "svt_av1_loop_restoration_save_boundary_lines");
+    if (g_on && !after_cdef && frame_supported(cm->child_pcs)) {
+        Ctx    *c = ctx_of(cm->child_pcs);
+        void   *pl[3];
+        int32_t st[3];
+        yv12_planes(frame, cm->use_highbitdepth, pl, st);
+        for (int q = 0; q < 3; q++) GPU(svtgpu_frame_upload(c->D, q, pl[q], st[q], NULL));
+        GPU(svtgpu_synchronize(g_ctx, NULL));
+        c->d_valid = 1;
+    }
+    orig(frame, cm, after_cdef); /* the encoder's own boundary buffers stay filled (any fallback apply reads them) */
+}
+
+/* ============================== deblocking ============================== */
+static void lf_params(PictureControlSet *pcs, SvtGpuLfParams *p) {
+    FrameHeader             *fh = &pcs->ppcs->frm_hdr;
+    const struct LoopFilter *lf = &fh->loop_filter_params;
+    memset(p, 0, sizeof *p);
+    p->filter_level[0] = lf->filter_level[0], p->filter_level[1] = lf->filter_level[1];
+    p->filter_level_u = lf->filter_level_u, p->filter_level_v = lf->filter_level_v;
+    p->sharpness_level        = lf->sharpness_level;
+    p->mode_ref_delta_enabled = lf->mode_ref_delta_enabled;
+    for (int k = 0; k < 8; k++) p->ref_deltas[k] = lf->ref_deltas[k];
+    for (int k = 0; k < 2; k++) p->mode_deltas[k] = lf->mode_deltas[k];
+    p->segmentation_enabled = fh->segmentation_params.segmentation_enabled;
+    for (int s = 0; s < 8; s++)
+        for (int f = 0; f < 8; f++) {
+            p->seg_feature_data[s][f]    = fh->segmentation_params.feature_data[s][f];
+            p->seg_feature_enabled[s][f] = fh->segmentation_params.feature_enabled[s][f];
+        }
+}
+static void set_mode_info(Ctx *c, PictureControlSet *pcs) {
+    Av1Common *cm = pcs->ppcs->av1_cm;
+    const int  mr = ((c->h + 7) & ~7) >> 2, mc = ((c->w + 7) & ~7) >> 2;
+    SvtGpuLfMi *mi = calloc((size_t)mr * mc, sizeof *mi);
+    for (int r = 0; r < mr; r++)
+        for (int q = 0; q < mc; q++) {
+            const BlockModeInfoEnc *b = &pcs->mi_grid_base[(size_t)r * cm->mi_stride + q]->mbmi.block_mi;
+            SvtGpuLfMi          *m = &mi[(size_t)r * mc + q];
+            m->bsize = (uint8_t)b->bsize, m->tx_depth = b->tx_depth, m->skip = b->skip;
+            m->ref_frame0 = (int8_t)b->ref_frame[0], m->mode = (uint8_t)b->mode, m->segment_id = b->segment_id;
+        }
+    GPU(svtgpu_dlf_set_mode_info(c->dlf, mi, NULL));
+    GPU(svtgpu_synchronize(g_ctx, NULL));
+    free(mi);
+}
+static int dlf_supported(PictureControlSet *pcs) {
+    return frame_supported(pcs) && !pcs->ppcs->frm_hdr.delta_lf_params.delta_lf_present;
+}
+
+typedef EbErrorType (*PickFn)(EbPictureBufferDesc *, PictureControlSet *, LpfPickMethod);
+#undef KIND
+#define KIND K_DLF_PICK
+EbErrorType svt_av1_pick_filter_level(EbPictureBufferDesc *srcBuffer, PictureControlSet *pcs, LpfPickMethod method) {
+    static PickFn orig;
+    if (!orig) orig = (PickFn)dlsym(RTLD_NEXT, "svt_av1_pick_filter_level");
+    if (!g_on) return orig(srcBuffer, pcs, method);
+    if (method != LPF_PICK_FROM_FULL_IMAGE || !dlf_supported(pcs)) {
+        count(1);
+        return orig(srcBuffer, pcs, method);
+    }
+    count(0);
+    SequenceControlSet      *scs  = pcs->scs;
+    PictureParentControlSet *ppcs = pcs->ppcs;
+    struct LoopFilter       *lf   = &ppcs->frm_hdr.loop_filter_params;
+    lf->sharpness_level           = 0; /* EbDeblockingFilter.c:1136 */
+    /* dlf_avg: the search starts from the references' average levels (:1172-1203) */
+    if (ppcs->dlf_ctrls.dlf_avg && ppcs->tot_ref_frame_types > 0) {
+        int32_t t0 = 0, t1 = 0, tu = 0, tv = 0, n = 0;
+        for (uint32_t it = 0; it < ppcs->tot_ref_frame_types; ++it) {
+            MvReferenceFrame rf[2];
+            av1_set_ref_frame(rf, ppcs->ref_frame_type_arr[it]);
+            if (rf[1] != NONE_FRAME) continue;
+            const EbReferenceObject *ro =
+                pcs->ref_pic_ptr_array[get_list_idx(rf[0])][get_ref_frame_idx(rf[0])]->object_ptr;
+            t0 += ro->filter_level[0], t1 += ro->filter_level[1], tu += ro->filter_level_u, tv += ro->filter_level_v;
+            n++;
+        }
+        lf->filter_level[0] = t0 / n, lf->filter_level[1] = t1 / n, lf->filter_level_u = tu / n;
+        lf->filter_level_v = tv / n;
+    }
+    Ctx *c = ctx_of(pcs);
+    const int is16 = scs->is_16bit_pipeline;
+    EbPictureBufferDesc *recon;
+    svt_aom_get_recon_pic(pcs, &recon, is16);
+    upload_pic(c->R, recon, is16, 0, 3);
+    upload_pic(c->S, is16 ? pcs->input_frame16bit : ppcs->enhanced_pic, is16, 0, 3);
+    set_mode_info(c, pcs);
+    SvtGpuLfParams p;
+    lf_params(pcs, &p);
+    GPU(svtgpu_dlf_pick(c->dlf, c->R, c->S, &p, ppcs->dlf_ctrls.dlf_avg, ppcs->dlf_ctrls.dlf_avg_uv,
+                        pcs->temporal_layer_index, ppcs->dlf_ctrls.early_exit_convergence,
+                        ppcs->frm_hdr.tx_mode == ONLY_4X4, NULL));
+    lf->filter_level[0] = p.filter_level[0], lf->filter_level[1] = p.filter_level[1];
+    lf->filter_level_u = p.filter_level_u, lf->filter_level_v = p.filter_level_v;
+    return EB_ErrorNone;
+}
+
+typedef void (*LfFrameFn)(EbPictureBufferDesc *, PictureControlSet *, int32_t, int32_t);
+#undef KIND
+#define KIND K_DLF_FRAME
+void svt_av1_loop_filter_frame(EbPictureBufferDesc *frame_buffer, PictureControlSet *pcs, int32_t plane_start,
+                               int32_t plane_end) {
+    static LfFrameFn orig;
+    if (!orig) orig = (LfFrameFn)dlsym(RTLD_NEXT, "svt_av1_loop_filter_frame");
+    if (!g_on) return orig(frame_buffer, pcs, plane_start, plane_end);
+    if (!dlf_supported(pcs)) {
+        count(1);
+        return orig(frame_buffer, pcs, plane_start, plane_end);
+    }
+    count(0);
+    Ctx      *c    = ctx_of(pcs);
+    const int is16 = pcs->scs->is_16bit_pipeline;
+    upload_pic(c->R, frame_buffer, is16, plane_start, plane_end);
+    set_mode_info(c, pcs);
+    SvtGpuLfParams p;
+    lf_params(pcs, &p);
+    GPU(svtgpu_dlf_frame(c->dlf, c->R, &p, plane_start, plane_end, NULL));
+    download_pic(c->R, frame_buffer, is16, plane_start, plane_end);
+}
+
+/* ================================= CDEF ================================= */
+static void cdef_controls(const CdefControls *cc, SvtGpuCdefControls *g) {
+    memset(g, 0, sizeof *g);
+    g->first_pass_fs_num          = cc->first_pass_fs_num;
+    g->default_second_pass_fs_num = cc->default_second_pass_fs_num;
+    memcpy(g->default_first_pass_fs, cc->default_first_pass_fs, sizeof g->default_first_pass_fs);
+    memcpy(g->default_second_pass_fs, cc->default_second_pass_fs, sizeof g->default_second_pass_fs);
+    memcpy(g->default_first_pass_fs_uv, cc->default_first_pass_fs_uv, sizeof g->default_first_pass_fs_uv);
+    memcpy(g->default_second_pass_fs_uv, cc->default_second_pass_fs_uv, sizeof g->default_second_pass_fs_uv);
+    g->subsampling_factor    = cc->subsampling_factor;
+    g->zero_fs_cost_bias     = cc->zero_fs_cost_bias;
+    g->use_reference_cdef_fs = cc->use_reference_cdef_fs;
+    g->pred_y_f              = cc->pred_y_f;
+    g->pred_uv_f             = cc->pred_uv_f;
+}
+
+typedef void (*FinishFn)(PictureControlSet *);
+#undef KIND
+#define KIND K_CDEF_PICK
+void finish_cdef_search(PictureControlSet *pcs) {
+    static FinishFn orig;
+    if (!orig) orig = (FinishFn)dlsym(RTLD_NEXT, "finish_cdef_search");
+    if (!g_on) return orig(pcs);
+    if (!frame_supported(pcs)) {
+        count(1);
+        return orig(pcs);
+    }
+    count(0);
+    SequenceControlSet      *scs  = pcs->scs;
+    PictureParentControlSet *ppcs = pcs->ppcs;
+    FrameHeader             *fh   = &ppcs->frm_hdr;
+    Av1Common               *cm   = ppcs->av1_cm;
+    Ctx                     *c    = ctx_of(pcs);
+    const int                is16 = scs->is_16bit_pipeline;
+    /* the DLF output (pcs->cdef_input_recon, EbDlfProcess.c:117-127) and the source */
+    EbPictureBufferDesc *recon;
+    svt_aom_get_recon_pic(pcs, &recon, is16);
+    upload_pic(c->D, recon, is16, 0, 3);
+    upload_pic(c->S, is16 ? pcs->input_frame16bit : ppcs->enhanced_pic, is16, 0, 3);
+    /* the 8x8 blocks svt_sb_compute_cdef_list lists (any of the four mi non-skip) and the SB128 areas */
+    const int mr = cm->mi_rows, mc = cm->mi_cols, b8r = mr >> 1, b8c = mc >> 1;
+    uint8_t  *mask = malloc((size_t)b8r * b8c);
+    for (int r = 0; r < b8r; r++)
+        for (int q = 0; q < b8c; q++) {
+            int all = 1;
+            for (int dr = 0; dr < 2; dr++)
+                for (int dq = 0; dq < 2; dq++)
+                    all &= pcs->mi_grid_base[(size_t)(2 * r + dr) * cm->mi_stride + 2 * q + dq]->mbmi.block_mi.skip != 0;
+            mask[(size_t)r * b8c + q] = (uint8_t)!all;
+        }
+    GPU(svtgpu_cdef_set_block_mask(c->cdef, mask, NULL));
+    const int nvfb = (mr + 15) / 16, nhfb = (mc + 15) / 16, nfb = nvfb * nhfb;
+    uint8_t  *fbb  = malloc((size_t)nfb);
+    for (int f = 0; f < nfb; f++)
+        fbb[f] = (uint8_t)pcs->mi_grid_base[(size_t)16 * (f / nhfb) * cm->mi_stride + 16 * (f % nhfb)]->mbmi.block_mi.bsize;
+    GPU(svtgpu_cdef_set_fb_bsize(c->cdef, scs->seq_header.sb_size == BLOCK_128X128 ? fbb : NULL, NULL));
+    SvtGpuCdefControls gc;
+    cdef_controls(&ppcs->cdef_ctrls, &gc);
+    const int q = fh->quantization_params.base_q_idx;
+    GPU(svtgpu_cdef_search_frame(c->cdef, c->D, c->S, &gc, q, NULL));
+    uint32_t fast_lambda = 0, full_lambda = 0; /* EbEncCdef.c:807-814 */
+    (*svt_aom_av1_lambda_assignment_function_table[ppcs->pred_structure])(
+        pcs, &fast_lambda, &full_lambda, (uint8_t)ppcs->enhanced_pic->bit_depth, (uint8_t)q, FALSE);
+    SvtGpuCdefParams prm;
+    int8_t          *fbs = malloc((size_t)nfb);
+    GPU(svtgpu_cdef_pick(c->cdef, &gc, q, full_lambda, &prm, fbs, NULL));
+    uint8_t *skip = malloc((size_t)nfb);
+    GPU(svtgpu_cdef_read_state(c->cdef, NULL, skip, NULL, NULL, NULL));
+    /* the frame header and the per-FB indices where finish_cdef_search writes them (EbEncCdef.c:874-926) */
+    fh->cdef_params.cdef_bits    = prm.cdef_bits;
+    fh->cdef_params.cdef_damping = prm.cdef_damping;
+    ppcs->nb_cdef_strengths      = 1 << prm.cdef_bits;
+    for (int j = 0; j < ppcs->nb_cdef_strengths; j++)
+        fh->cdef_params.cdef_y_strength[j] = prm.cdef_y_strength[j],
+        fh->cdef_params.cdef_uv_strength[j] = prm.cdef_uv_strength[j];
+    for (int f = 0; f < nfb; f++) {
+        const int fbr = f / nhfb, fbc = f % nhfb;
+        const int idx = 16 * fbr * pcs->mi_stride + 16 * fbc;
+        const BlockSize bs = pcs->mi_grid_base[idx]->mbmi.block_mi.bsize;
+        if (((fbc & 1) && (bs == BLOCK_128X128 || bs == BLOCK_128X64)) ||
+            ((fbr & 1) && (bs == BLOCK_128X128 || bs == BLOCK_64X128)))
+            continue; /* the second half of a 128-wide area */
+        if (gc.use_reference_cdef_fs ? svt_sb_all_skip(pcs, cm, fbr * 16, fbc * 16) : skip[f]) continue;
+        const int8_t g = fbs[f];
+        pcs->mi_grid_base[idx]->mbmi.cdef_strength = g;
+        if (bs == BLOCK_128X128 || bs == BLOCK_128X64) pcs->mi_grid_base[idx + 16]->mbmi.cdef_strength = g;
+        if (bs == BLOCK_128X128 || bs == BLOCK_64X128) pcs->mi_grid_base[idx + 16 * pcs->mi_stride]->mbmi.cdef_strength = g;
+        if (bs == BLOCK_128X128) pcs->mi_grid_base[idx + 16 * pcs->mi_stride + 16]->mbmi.cdef_strength = g;
+    }
+    c->cdef_searched = 1;
+    free(mask), free(fbb), free(fbs), free(skip);
+}
+
+typedef void (*CdefFrameFn)(SequenceControlSet *, PictureControlSet *);
+#undef KIND
+#define KIND K_CDEF_APPLY
+void svt_av1_cdef_frame(SequenceControlSet *scs, PictureControlSet *pcs) {
+    static CdefFrameFn orig;
+    if (!orig) orig = (CdefFrameFn)dlsym(RTLD_NEXT, "svt_av1_cdef_frame");
+    Ctx *c = g_on && frame_supported(pcs) ? ctx_of(pcs) : NULL;
+    if (!c || !c->cdef_searched) {
+        if (g_on) count(1);
+        return orig(scs, pcs);
+    }
+    count(0);
+    const FrameHeader *fh = &pcs->ppcs->frm_hdr;
+    SvtGpuCdefParams   prm;
+    memset(&prm, 0, sizeof prm);
+    prm.cdef_damping = (uint8_t)fh->cdef_params.cdef_damping;
+    prm.cdef_bits    = (uint8_t)fh->cdef_params.cdef_bits;
+    for (int j = 0; j < (1 << prm.cdef_bits); j++)
+        prm.cdef_y_strength[j] = (uint8_t)fh->cdef_params.cdef_y_strength[j],
+        prm.cdef_uv_strength[j] = (uint8_t)fh->cdef_params.cdef_uv_strength[j];
+    GPU(svtgpu_cdef_apply_frame(c->cdef, c->D, c->O, &prm, NULL));
+    EbPictureBufferDesc *recon;
+    svt_aom_get_recon_pic(pcs, &recon, scs->is_16bit_pipeline);
+    download_pic(c->O, recon, scs->is_16bit_pipeline, 0, 3);
+    c->cdef_searched = 0;
+}
+
+/* ========================== loop restoration ========================== */
+static int lr_supported(PictureControlSet *pcs) {
+    Av1Common *cm = pcs->ppcs->av1_cm;
+    if (!frame_supported(pcs)) return 0;
+    if (cm->wn_filter_ctrls.enabled && cm->wn_filter_ctrls.use_prev_frame_coeffs) return 0;
+    if (cm->sg_filter_ctrls.enabled && cm->sg_filter_ctrls.step_range < 16) return 0; /* reference-based ep range */
+    if (cm->use_boundaries_in_rest_search) return 0; /* the device search runs without stripe boundaries */
+    return ((cm->frm_size.frame_width >> 1) & 3) == 0;                               /* 4-sample chunks per plane */
+}
+static void lr_controls(PictureControlSet *pcs, SvtGpuLrSearchControls *lc) {
+    Av1Common        *cm = pcs->ppcs->av1_cm;
+    const Macroblock *x  = pcs->ppcs->av1x;
+    memset(lc, 0, sizeof *lc);
+    lc->wn_enabled                 = cm->wn_filter_ctrls.enabled;
+    lc->wn_use_chroma              = cm->wn_filter_ctrls.use_chroma;
+    lc->wn_filter_tap_lvl          = cm->wn_filter_ctrls.filter_tap_lvl;
+    lc->wn_use_refinement          = cm->wn_filter_ctrls.use_refinement;
+    lc->wn_max_one_refinement_step = cm->wn_filter_ctrls.max_one_refinement_step;
+    lc->sg_enabled                 = cm->sg_filter_ctrls.enabled;
+    lc->sg_use_chroma              = cm->sg_filter_ctrls.use_chroma;
+    for (int k = 0; k < 2; k++) {
+        lc->sg_start_ep[k] = cm->sg_filter_ctrls.start_ep[k], lc->sg_end_ep[k] = cm->sg_filter_ctrls.end_ep[k];
+        lc->sg_ep_inc[k] = cm->sg_filter_ctrls.ep_inc[k], lc->sg_refine[k] = cm->sg_filter_ctrls.refine[k];
+    }
+    lc->rdmult = x->rdmult;
+    for (int k = 0; k < 3; k++) lc->switchable_restore_cost[k] = x->switchable_restore_cost[k];
+    for (int k = 0; k < 2; k++) lc->wiener_restore_cost[k] = x->wiener_restore_cost[k];
+    for (int k = 0; k < 2; k++) lc->sgrproj_restore_cost[k] = x->sgrproj_restore_cost[k];
+}
+
+typedef void (*SegSearchFn)(int32_t *, Yv12BufferConfig *, const Yv12BufferConfig *, Yv12BufferConfig *,
+                            PictureControlSet *, uint32_t);
+void restoration_seg_search(int32_t *rst_tmpbuf, Yv12BufferConfig *org_fts, const Yv12BufferConfig *src,
+                            Yv12BufferConfig *trial_frame_rst, PictureControlSet *pcs, uint32_t segment_index) {
+    static SegSearchFn orig;
+    if (!orig) orig = (SegSearchFn)dlsym(RTLD_NEXT, "restoration_seg_search");
+    if (g_on && lr_supported(pcs)) return; /* the device searches the whole frame in rest_finish_search */
+    orig(rst_tmpbuf, org_fts, src, trial_frame_rst, pcs, segment_index);
+}
+
+#undef KIND
+#define KIND K_LR_SEARCH
+void rest_finish_search(PictureControlSet *pcs) {
+    static FinishFn orig;
+    if (!orig) orig = (FinishFn)dlsym(RTLD_NEXT, "rest_finish_search");
+    if (!g_on || !lr_supported(pcs)) {
+        if (g_on) count(1);
+        return orig(pcs);
+    }
+    count(0);
+    SequenceControlSet *scs  = pcs->scs;
+    Av1Common          *cm   = pcs->ppcs->av1_cm;
+    Ctx                *c    = ctx_of(pcs);
+    const int           is16 = scs->is_16bit_pipeline;
+    int32_t             us[3];
+    for (int p = 0; p < 3; p++) us[p] = pcs->rst_info[p].restoration_unit_size;
+    if (!c->lr || memcmp(us, c->lr_units, sizeof us)) {
+        if (c->lr) svtgpu_lr_state_destroy(c->lr);
+        GPU(svtgpu_lr_state_create(g_ctx, c->w, c->h, us, &c->lr));
+        memcpy(c->lr_units, us, sizeof us);
+    }
+    /* the CDEF output the search reads (EbRestProcess.c:562) and the source (:563) */
+    EbPictureBufferDesc *recon;
+    svt_aom_get_recon_pic(pcs, &recon, is16);
+    upload_pic(c->O, recon, is16, 0, 3);
+    upload_pic(c->S, is16 ? pcs->input_frame16bit : pcs->ppcs->enhanced_unscaled_pic, is16, 0, 3);
+    SvtGpuLrSearchControls lc;
+    lr_controls(pcs, &lc);
+    SvtGpuLrUnitSearch *rec[3];
+    int32_t             n[3];
+    for (int p = 0; p < 3; p++) {
+        int32_t hu, vu;
+        GPU(svtgpu_lr_units(c->lr, p, &hu, &vu));
+        n[p]   = hu * vu;
+        rec[p] = calloc((size_t)n[p], sizeof **rec);
+    }
+    int32_t ft[3];
+    GPU(svtgpu_lr_search_frame(c->lr, c->O, c->S, &lc, ft, rec, NULL));
+    const int nplanes = ((lc.wn_enabled && lc.wn_use_chroma) || (lc.sg_enabled && lc.sg_use_chroma)) ? 3 : 1;
+    for (int p = 0; p < 3; p++) {
+        RestorationInfo *ri = &pcs->rst_info[p];
+        if (p >= nplanes) { /* luma-only search: chroma off (EbRestorationPick.c:1626-1629) */
+            ri->frame_restoration_type = RESTORE_NONE;
+            continue;
+        }
+        SvtGpuRestUnit *units = calloc((size_t)n[p], sizeof *units);
+        int32_t         t;
+        GPU(svtgpu_lr_finish_plane(&lc, p, n[p], rec[p], &t, units));
+        if (t != ft[p]) die("lr finish: frame type differs from the search's", t);
+        ri->frame_restoration_type = (RestorationType)t;
+        if (t != RESTORE_NONE)
+            for (int u = 0; u < n[p]; u++) { /* copy_unit_info (EbRestorationPick.c:1202-1209) */
+                RestorationUnitInfo *ui = &ri->unit_info[u];
+                ui->restoration_type    = (RestorationType)units[u].type;
+                if (units[u].type == RESTORE_WIENER)
+                    for (int k = 0; k < 8; k++)
+                        ui->wiener_info.vfilter[k] = units[u].vfilter[k], ui->wiener_info.hfilter[k] = units[u].hfilter[k];
+                else if (units[u].type == RESTORE_SGRPROJ)
+                    ui->sgrproj_info.ep = units[u].ep, ui->sgrproj_info.xqd[0] = units[u].xqd[0],
+                    ui->sgrproj_info.xqd[1] = units[u].xqd[1];
+            }
+        /* search_sgrproj_seg counts each unit's best ep (EbRestorationPick.c:1256; the frame's ep for later frames) */
+        if (lc.sg_enabled && (p == 0 || lc.sg_use_chroma))
+            for (int u = 0; u < n[p]; u++) cm->sg_frame_ep_cnt[rec[p][u].sgrproj.ep]++;
+        free(units);
+    }
+    for (int p = 0; p < 3; p++) c->lr_ft[p] = pcs->rst_info[p].frame_restoration_type, free(rec[p]);
+    if (c->lr_ft[0] || c->lr_ft[1] || c->lr_ft[2]) count_kind(0, K_LR_ON), g_calls--;
+    c->lr_searched = 1;
+}
+
+typedef void (*LrFrameFn)(int32_t *, Yv12BufferConfig *, Av1Common *, int32_t);
+#undef KIND
+#define KIND K_LR_APPLY
+void svt_av1_loop_restoration_filter_frame(int32_t *rst_tmpbuf, Yv12BufferConfig *frame, Av1Common *cm,
+                                           int32_t optimized_lr) {
+    static LrFrameFn orig;
+    if (!orig) orig = (LrFrameFn)dlsym(RTLD_NEXT, "svt_av1_loop_restoration_filter_frame");
+    PictureControlSet *pcs = cm->child_pcs;
+    Ctx               *c   = g_on && frame_supported(pcs) ? ctx_of(pcs) : NULL;
+    if (!c || !c->lr_searched) {
+        if (g_on) count(1);
+        return orig(rst_tmpbuf, frame, cm, optimized_lr);
+    }
+    if (!c->d_valid) { /* no deblocked copy of this picture: the encoder's own apply (its boundary buffers) */
+        count(1);
+        c->lr_searched = 0;
+        return orig(rst_tmpbuf, frame, cm, optimized_lr);
+    }
+    count(0);
+    void   *pl[3];
+    int32_t st[3];
+    yv12_planes(frame, cm->use_highbitdepth, pl, st);
+    for (int q = 0; q < 3; q++) GPU(svtgpu_frame_upload(c->O, q, pl[q], st[q], NULL));
+    GPU(svtgpu_lr_apply_frame(c->lr, c->D, c->O, c->L, c->lr_ft, NULL));
+    for (int q = 0; q < 3; q++) GPU(svtgpu_frame_download(c->L, q, pl[q], st[q], NULL));
+    GPU(svtgpu_synchronize(g_ctx, NULL));
+    c->lr_searched = 0, c->d_valid = 0;
+}

@@ -5,7 +5,10 @@ oracle/ref_harness/enc_drop_in.c drives it through its public API (svt_av1_enc_i
 _send_picture / _get_packet) over a synthetic 10-bit 4:2:0 clip with deblocking, CDEF and loop restoration (Wiener +
 self-guided, preset 2) on.  The bitstream with include/svtgpu_rtcd.h's svtgpu_install_filter_rtcd() called after
 svt_av1_enc_init (the encoder's own process bodies then run libsvtgpu's device kernels through its RTCD pointers)
-must equal the bitstream of the encoder as built, byte for byte.  Test infrastructure: the reference build lives in
+must equal the bitstream of the encoder as built, byte for byte; so must the bitstream with the frame-level hooks
+(oracle/ref_harness/enc_frame_hooks.c: the encoder's own DLF / CDEF / LR process bodies call svtgpu_dlf_pick /
+svtgpu_dlf_frame, svtgpu_cdef_search_frame / _pick / _apply_frame and svtgpu_lr_search_frame / _finish_plane /
+_apply_frame in place of their frame-level C functions, bound by ELF symbol interposition).  Test infrastructure: the reference build lives in
 oracle/_ref (git-ignored; built here by __graft_entry__.build(), shipped to the GPU box with the tree)."""
 import os
 import subprocess
@@ -21,8 +24,13 @@ needs_exe = pytest.mark.skipif(not os.path.exists(EXE), reason="oracle/_ref/enc 
 def _encode(mode, path, *args, timeout=600):
     r = subprocess.run([EXE, mode, path] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, (mode, r.returncode, r.stderr[-2000:])
-    line = [l for l in r.stdout.splitlines() if l.startswith(mode + " bytes")][-1].split()
-    return {line[i]: int(line[i + 1]) for i in range(1, len(line) - 1, 2)}
+    out = {}
+    for l in r.stdout.splitlines():  # "<mode> bytes <n> packets <n> ..." and (frame mode) "frame kinds <k> <n> ..."
+        f = l.split()
+        if f[:2] == [mode, "bytes"] or f[:2] == ["frame", "kinds"]:
+            start = 1 if f[1] == "bytes" else 2
+            out.update({f[i]: int(f[i + 1]) for i in range(start, len(f) - 1, 2)})
+    return out
 
 
 @needs_exe
@@ -45,4 +53,23 @@ def test_encoder_bitstream_identical_with_filter_rtcd(tmp_path, geom):
     ic = _encode("cpu", cpu, *geom)
     ig = _encode("rtcd", gpu, *geom)
     assert ig["shim_calls"] > 1000, ig
+    assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(gpu, "rb").read(), (ic, ig)
+
+
+@needs_exe
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("geom", [(320, 192, 5, 2, 40), (256, 144, 3, 2, 20), (384, 256, 4, 1, 32)])
+def test_encoder_bitstream_identical_with_frame_hooks(tmp_path, geom):
+    """The encoder's DLF / CDEF / LR process bodies calling libsvtgpu's frame-level API (level searches, strength
+    pick, restoration search + RD finish, the three frame filters on the device) write the same bitstream as the
+    encoder as built; every hooked call was served by the device path (no fallback)."""
+    cpu, gpu = str(tmp_path / "cpu.obu"), str(tmp_path / "frame.obu")
+    ic = _encode("cpu", cpu, *geom)
+    ig = _encode("frame", gpu, *geom)
+    assert ig["frame_calls"] >= 3 * geom[2] and ig["frame_fallbacks"] == 0, ig
+    # every stage ran on the device for every frame, and restoration really filtered some frames
+    for k in ("dlf_pick", "dlf_frame", "cdef_pick", "lr_search"):
+        assert ig[k] >= geom[2], (k, ig)
+    assert ig["cdef_apply"] >= 1 and ig["lr_apply"] >= 1 and ig["lr_on"] >= 1, ig
     assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(gpu, "rb").read(), (ic, ig)
