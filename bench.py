@@ -514,13 +514,16 @@ def roofline_of(kernels, bd, pmc_json):
     out = {"kernel": name, "bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 6), "traffic": traffic, "alg_bytes_per_launch": round(alg),
            "avg_launch_ms": round(per_launch_ms, 5), "launches_per_frame": k["launches"],
+           "avg_launch_ms_device_clock": (round(k["ms_clock"] / max(k["launches"], 1), 5) if "ms_clock" in k else None),
            "ms_per_frame": round(k["ms"], 4),
            "valu": round(valu / (per_launch_ms * 1e-3 * VALU_PEAK_INSTS), 4) if valu else None,
            "valu_insts_per_launch": valu, "pmc_source": src,
            "all_kernels_ms_per_frame": {n: round(v["ms"], 4) for n, v in sorted(kernels.items(), key=lambda x: -x[1]["ms"])},
-           "note": "the largest device-time kernel of the step (device time per frame, timed live: HIP events for "
-                   "the CDEF search and MD batch, the device's s_memrealtime clock for the LR search kernels -- first "
-                   "workgroup start to last workgroup end of every launch); achieved = SURVEY §8(d) algorithmic "
+           "note": "the largest device-time kernel of the step (device time per frame, timed live with HIP events "
+                   "on the stream each kernel runs on: the CDEF search and MD batch by the bench, the LR search "
+                   "kernels inside the library around each launch (svtgpu_lr_profile ms_events, the span rocprofv3's "
+                   "kernel trace reports); avg_launch_ms_device_clock = the device's s_memrealtime clock, first "
+                   "workgroup start to last workgroup end); achieved = SURVEY §8(d) algorithmic "
                    "bytes (%s) / its launch duration; traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch and valu = "
                    "SQ_INSTS_VALU / (launch duration x %.3g wave-instructions/s VALU issue peak), both from %s" %
                    (k["what"], VALU_PEAK_INSTS, os.path.relpath(pmc_json, ROOT))}
@@ -878,7 +881,8 @@ def main():
     frames_per_step = F * (1 if tiled else n)  # frames split: every rank filters F frames per step
     value = frames_per_step * W * H / (ms_per_step * 1e-3) / 1e6  # the whole job's luma pixels per second
     def lr_classes(tot):
-        return {c: {k: tot[c][k] / max(tot["searches"], 1) if tot else 0.0 for k in ("launches", "ms", "bytes")}
+        return {c: {k: tot[c][k] / max(tot["searches"], 1) if tot else 0.0
+                    for k in ("launches", "ms", "ms_events", "bytes")}
                 for c in svtgpu.LrState.PROFILE_CLASSES}
     lr_cls = lr_classes(lr_tot)
     # SURVEY §8(d) algorithmic bytes; per rank: its share of the frame (tiles)
@@ -909,8 +913,9 @@ def main():
                            "projection": ("sgr_res_kernel", 2 * SB, "the CDEF output and source read once, 2*S*B")}
                 for cls, (kn, alg, what) in lr_kern.items():
                     c = lr_cls_[cls]
-                    if c["launches"] > 0:
-                        kernels[kn] = dict(ms=c["ms"], launches=c["launches"], alg_bytes=alg, what=what)
+                    if c["launches"] > 0:  # HIP events around each launch (rocprofv3's span); the device clock beside
+                        kernels[kn] = dict(ms=c["ms_events"] or c["ms"], ms_clock=c["ms"], launches=c["launches"],
+                                           alg_bytes=alg, what=what)
         return kernels
     kernels_f = kernel_table(search_ms, md_ms, lr_cls, bool(lr_tot))
     # The roofline's durations come from the condition its PMC counters were collected in: one frame in flight
@@ -920,7 +925,7 @@ def main():
     if F > 1:
         s0 = slots[0]
         s0.ev = []
-        lr.profile(not a.no_kernel_timing)
+        lr.profile(not a.no_kernel_timing, events=True)  # the roofline's launch spans: HIP events (rocprofv3's span)
         iso_steps = max(10, min(a.steps, 40))
         torch.cuda.synchronize()
         for _ in range(iso_steps):

@@ -879,12 +879,14 @@ int svtgpu_lr_set_tile(SvtGpuLrState *s, const int32_t units[3][4], const int32_
  * HBM bytes of the class (compulsory reads/writes of the samples and filter planes the launches touch). */
 typedef struct SvtGpuLrProfile {
     int32_t launches[6]; /* totals over `searches` searches */
-    float   ms[6];
+    float   ms[6];        /* the device clock: first workgroup start to last workgroup end of each launch */
     double  bytes[6];
     int32_t searches;
+    float   ms_events[6]; /* HIP events around each launch on its stream (the span rocprofv3's kernel trace reports) */
 } SvtGpuLrProfile;
 /* enable != 0 turns timing of the following searches on (0 off): a bit mask of the classes to time (bit c =
- * class c; -1 = all).  `totals` (nullable) first receives the sums over the searches timed since the previous read
+ * class c; -1 = all); bit 6 also brackets each timed launch with HIP events (ms_events: the span rocprofv3 reports;
+ * events between launches can change how the two LR chains interleave, so they are a separate, opt-in bit).  `totals` (nullable) first receives the sums over the searches timed since the previous read
  * (untimed classes read 0), which are then reset; reading synchronizes the device.  The timings accumulate on the
  * device: a timed search adds one small launch and no copies or host synchronization. */
 int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *totals);

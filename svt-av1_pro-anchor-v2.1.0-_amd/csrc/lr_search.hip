@@ -1637,7 +1637,12 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
     // one-part items reads a pass's partials while the next pass writes the other buffer)
     __shared__ unsigned long long s_red2[2][SR_PW][SG_NC];
     unsigned long long (*const s_red)[SG_NC] = s_red2[0];
-    __shared__ uint32_t           s_ch[2][8];          // one-barrier path: the children of each pass's candidate
+    __shared__ uint32_t           s_ch[2][8];          // one-barrier path (SVTGPU_SR_CHILDREN=1): each pass's children
+    // one-barrier path: the seeded descent every wave steps itself (raw storage: Descent has member initializers)
+    __shared__ __attribute__((aligned(8))) unsigned char s_desc_raw[sizeof(Descent)];
+    Descent &s_desc = *reinterpret_cast<Descent *>(s_desc_raw);
+    __shared__ unsigned long long s_etot[2]; // self-stepping row parts: each pass's error summed over the parts
+    __shared__ int                s_xok[2];  // ... and whether the exchange succeeded
     __shared__ uint32_t           s_xq[SG_NC];         // the pending tree's candidates (xq pairs), compacted
     __shared__ uint32_t           s_mask;              // its nodes
     __shared__ int                s_nv;                // its candidate count (0: the descent has ended)
@@ -1653,7 +1658,10 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         if (threadIdx.x == 0) atomicOr(status, 4);
         return;
     }
-    if (threadIdx.x < SR_PL) {
+    // the wave's role from a scalar (readfirstlane) condition: the compiler then treats each role's code as uniform
+    // control flow -- with `threadIdx.x < SR_PL` it could not prove the branch wave-uniform and compiled the control
+    // wave's descent steps as exec-masked vector code with scratch traffic
+    if (__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) < SR_PW) {
         // ================= pixel waves =================
         const int      pl = threadIdx.x, r0 = c_sgr_r[ep][0], r1 = c_sgr_r[ep][1];
         const T       *d = (const T *)P.dgd, *s = (const T *)P.src;
@@ -1766,7 +1774,81 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         // diagnostics (stat): pixel wave 0's pass time (B2/B4 release to its arrival at B3) and its wait from B3 to the
         // B4 release
         unsigned long long tpass = 0, twait = 0, tmark = stat ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
+        if (!TREE && it.nparts == 1 && !(xmode & 0x600)) {
+            // One barrier per pass, and no wave waits on another's descent step: every wave (pixel and control) holds
+            // the seeded descent in its own scalar registers and steps it itself from the pass's wave partials --
+            // report + next once per pass, the same decisions everywhere (the errors are the same LDS words).  Before
+            // this the control wave stepped the descent and built both children of every candidate (three steps per
+            // pass, serial) while the pixel waves waited at the barrier: 13 us of descent per item, 8 of them control
+            Descent  Dw   = uniform(s_desc);
+            bool     live = __builtin_amdgcn_readfirstlane(s_nv) != 0;
+            uint32_t xq   = 0;
+            {
+                int32_t x[2];
+                decode_xq(Dw, x);
+                xq = __builtin_amdgcn_readfirstlane(pack2(x[0], x[1]));
+            }
+            for (int pass = 1; live; pass++) {
+                const uint32_t xl[1] = {xq};
+                sr_pass<1>(g, sr_dx, pl, K, 1, xl, s_red2[pass & 1]);
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    tpass += t - tmark, tmark = t;
+                }
+                __syncthreads(); // B3: the pass's wave partials are in LDS
+                unsigned long long e0 = 0;
+#pragma unroll
+                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
+                Dw.report(readlane64((long long)e0, 0));
+                live = Dw.next() && pass <= SR_MAX_PASSES;
+                if (live) {
+                    int32_t x[2];
+                    decode_xq(Dw, x);
+                    xq = __builtin_amdgcn_readfirstlane(pack2(x[0], x[1]));
+                }
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    twait += t - tmark, tmark = t;
+                }
+            }
+        } else if (!TREE && !(xmode & 0x600)) {
+            // Row parts, self-stepping: the control wave sums this part's wave partials, exchanges the sum with the
+            // other parts and leaves the frame-unit total in LDS (B4); then every wave steps its own copy of the
+            // descent -- no children built, no wave waits on another's step
+            Descent  Dw   = uniform(s_desc);
+            bool     live = __builtin_amdgcn_readfirstlane(s_nv) != 0;
+            uint32_t xq   = 0;
+            {
+                int32_t x[2];
+                decode_xq(Dw, x);
+                xq = __builtin_amdgcn_readfirstlane(pack2(x[0], x[1]));
+            }
+            for (int pass = 1; live; pass++) {
+                const uint32_t xl[1] = {xq};
+                sr_pass<1>(g, sr_dx, pl, K, 1, xl, s_red);
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    tpass += t - tmark, tmark = t;
+                }
+                __syncthreads(); // B3: the pass's wave partials are in s_red
+                __syncthreads(); // B4: the parts' total is in s_etot
+                const bool okx = __builtin_amdgcn_readfirstlane(s_xok[pass & 1]) != 0;
+                if (okx) {
+                    Dw.report(readlane64((long long)s_etot[pass & 1], 0));
+                    live = Dw.next() && pass <= SR_MAX_PASSES;
+                } else
+                    live = false;
+                if (live) {
+                    int32_t x[2];
+                    decode_xq(Dw, x);
+                    xq = __builtin_amdgcn_readfirstlane(pack2(x[0], x[1]));
+                }
+                if (stat) {
+                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                    twait += t - tmark, tmark = t;
+                }
+            }
+        } else if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
             // One barrier per pass: every pixel wave takes the outcome itself from the pass's wave partials and the
             // two children the control wave prepared during the pass (the control wave decides identically and
             // steps the descent while the next pass runs)
@@ -1849,7 +1931,55 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         Descent D = uniform(sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg));
         D.next(); // the seed itself is the first candidate
         sr_tree_publish(D, ok, nodes, s_xq, &s_mask, &s_nv);
-        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
+        if (!TREE && it.nparts == 1 && !(xmode & 0x600)) {
+            // the self-stepping path (see the pixel waves): the seeded descent to LDS for every wave, then the same
+            // report + next per pass as everyone else
+            if (lane == 0) s_desc = D;
+            __syncthreads(); // B2
+            bool live = ok;
+            int  pass = 1;
+            for (; live; pass++) {
+                __syncthreads(); // B3
+                const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+                ncp += (unsigned long long)nch * 4;
+                unsigned long long e0 = 0;
+#pragma unroll
+                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
+                D.report(readlane64((long long)e0, 0));
+                live = D.next() && pass <= SR_MAX_PASSES;
+                if (pass > SR_MAX_PASSES && lane == 0) atomicOr(status, 1);
+                if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
+            }
+            if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
+        } else if (!TREE && nodes == 1 && !(xmode & 0x600)) {
+            // self-stepping row parts (see the pixel waves): the exchange between B3 and B4, the step after B4
+            if (lane == 0) s_desc = D;
+            __syncthreads(); // B2
+            bool live = ok;
+            int  pass = 1;
+            for (; live; pass++) {
+                __syncthreads(); // B3
+                const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
+                ncp += (unsigned long long)nch * 4;
+                if (lane == 0) {
+                    unsigned long long t = 0;
+                    for (int w = 0; w < SR_PW; w++) t += s_red[w][0];
+                    long long e   = (long long)t;
+                    const bool ex = sr_exchange_lane(xch, it, pass, 0, e, status, xmode);
+                    s_etot[pass & 1] = (unsigned long long)e, s_xok[pass & 1] = ex;
+                }
+                __syncthreads(); // B4
+                const bool okx = __builtin_amdgcn_readfirstlane(s_xok[pass & 1]) != 0;
+                if (okx) {
+                    D.report(readlane64((long long)s_etot[pass & 1], 0));
+                    live = D.next() && pass <= SR_MAX_PASSES;
+                    if (pass > SR_MAX_PASSES && lane == 0) atomicOr(status, 1);
+                } else
+                    live = false;
+                if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
+            }
+            if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
+        } else if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
             // the one-barrier path (see the pixel waves): the children of each pending candidate go to s_ch by pass
             // parity before the pass's barrier; after it the outcome is taken exactly as the pixel waves take it
             auto publish_children = [&](int pass) {
@@ -1874,7 +2004,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 unsigned long long e0 = 0;
 #pragma unroll
                 for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
-                D.report((int64_t)e0);
+                // the error made wave-uniform (an LDS load is a vector value to the compiler): the descent's state and
+                // every branch of its step then stay scalar instead of exec-masked vector code
+                D.report(readlane64((long long)e0, 0));
                 live = D.next();
                 if (pass > SR_MAX_PASSES) {
                     if (lane == 0) atomicOr(status, 1);
@@ -1948,9 +2080,13 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         }
         if (lane == 0 && it.part == 0) ds[it.pair] = D;
         if (stat && lane == 0) {
+            const unsigned long long te = __builtin_amdgcn_s_memrealtime();
             atomicAdd(stat + 0, 1ull), atomicAdd(stat + 2, ncp), atomicAdd(stat + 3, t1 - t0);
-            atomicAdd(stat + 4, __builtin_amdgcn_s_memrealtime() - t1), atomicAdd(stat + 5, tctl);
+            atomicAdd(stat + 4, te - t1), atomicAdd(stat + 5, tctl);
             atomicAdd(stat + 6, (unsigned long long)nch * 4), atomicAdd(stat + 9, tpre);
+            if (it.nparts > 1) // the row-part items apart: count, load, descent, control ticks
+                atomicAdd(stat + 10, 1ull), atomicAdd(stat + 11, t1 - t0), atomicAdd(stat + 12, te - t1),
+                    atomicAdd(stat + 13, tctl);
         }
     }
     PROF_END(tk);
@@ -1994,6 +2130,7 @@ struct LrProfiler {
     double              static_bytes[NCLS] = {0, 0, 0, 0, 0, 0}, bps = 2;
     bool                ok   = false;
     int32_t             mask = 63; // classes timed (bit c)
+    bool                events = false; // bit 6 of the enable mask: HIP events around the timed launches too
     LrProfiler() {
         ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess &&
              hipMalloc(&d_acc, 8 * NCLS) == hipSuccess && hipMemset(d_clk, 0xFF, 8 * PROF_NL * PROF_SP) == hipSuccess &&
@@ -2002,9 +2139,32 @@ struct LrProfiler {
              hipDeviceSynchronize() == hipSuccess;
     }
     ~LrProfiler() {
+        for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
         (void)hipFree(d_clk);
         (void)hipFree(d_px);
         (void)hipFree(d_acc);
+    }
+    // HIP events around every timed launch on its own stream: the launch duration as the command processor sees it
+    // (rocprofv3's kernel trace measures the same span; the device clock above starts at the first workgroup and ends
+    // at the last), summed per class at read time
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, int>> ev_used; // (class, index of the start event; the end event follows it)
+    size_t                  ev_next = 0;
+    int ev_begin(int c, hipStream_t st) {
+        if (!events || !(mask >> c & 1)) return -1;
+        while (ev_pool.size() < ev_next + 2) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return -1;
+            ev_pool.push_back(e);
+        }
+        const int i = (int)ev_next;
+        ev_next += 2;
+        if (hipEventRecord(ev_pool[i], st) != hipSuccess) return -1;
+        ev_used.push_back({c, i});
+        return i;
+    }
+    void ev_end(int i, hipStream_t st) {
+        if (i >= 0) (void)hipEventRecord(ev_pool[i + 1], st);
     }
     void start() { nl = 0; }
     // the timing slot of one launch of class c (nullptr: not timed)
@@ -2031,6 +2191,11 @@ struct LrProfiler {
         HIP_TRY(hipDeviceSynchronize());
         for (int k = 0; k < 3 * PROF_SP; k++) px[k / PROF_SP] += pxs[k];
         std::memset(out, 0, sizeof *out);
+        for (auto &u : ev_used) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, ev_pool[u.second], ev_pool[u.second + 1]) == hipSuccess) out->ms_events[u.first] += ms;
+        }
+        ev_used.clear(), ev_next = 0;
         for (int c = 0; c < NCLS; c++) {
             out->launches[c] = launches[c];
             out->ms[c]       = (float)(acc[c] * 1e-5); // 100 MHz ticks
@@ -2470,7 +2635,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // ---- phase 1: sums, Wiener statistics, self-guided filters and moments ----
     LrProfiler         *prof = (LrProfiler *)s->prof;
     unsigned long long *pc   = prof ? prof->d_px : nullptr;
-    auto                run  = [&](int c, auto &&launch) { launch(prof ? prof->slot(c) : nullptr); };
+    auto run = [&](int c, hipStream_t ls, auto &&launch) {
+        const int ev = prof ? prof->ev_begin(c, ls) : -1;
+        launch(prof ? prof->slot(c) : nullptr);
+        if (prof) prof->ev_end(ev, ls);
+    };
     if (prof) prof->start();
     {
         uint8_t *pl = (uint8_t *)hp(h_plan);
@@ -2533,6 +2702,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         return e && !std::strcmp(e, "0");
     }();
     if (sr_two_barriers) sr_xmode |= 0x200u;
+    static const bool sr_children_path = [] { // SVTGPU_SR_CHILDREN=1: the round-4 one-barrier path (control-built children)
+        const char *e = std::getenv("SVTGPU_SR_CHILDREN");
+        return e && e[0] == '1';
+    }();
+    if (sr_children_path) sr_xmode |= 0x400u;
     static const bool   wr_stats = std::getenv("SVTGPU_WR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *wr_stat = nullptr;
     if (wr_stats && !wr_stat) HIP_TRY(hipMalloc(&wr_stat, 128));
@@ -2541,7 +2715,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     static unsigned long long *sr_stat = nullptr;
     if (sr_stats && !sr_stat) HIP_TRY(hipMalloc(&sr_stat, 128));
     if (sr_stat) HIP_TRY(hipMemsetAsync(sr_stat, 0, 128, st));
-    run(0, [&](unsigned long long *tk) {
+    run(0, st, [&](unsigned long long *tk) {
         hipLaunchKernelGGL(unit_sums_kernel<T>, dim3(nt_all), dim3(256), 0, st, A, (unsigned long long *)dp(o_sum),
                            (unsigned long long *)dp(o_sse), tk);
     });
@@ -2569,20 +2743,20 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         const PlanePlan &q = pp[p];
         if (!q.wn) continue;
         long long *part = (long long *)dp(o_part) + q.part_off, *mh = (long long *)dp(o_mh) + q.mh_off;
-        run(0, [&](unsigned long long *tk) {
+        run(0, sw, [&](unsigned long long *tk) {
             launch_stats(q.win, [&](auto wc) {
                 hipLaunchKernelGGL((wiener_stats_kernel<T, decltype(wc)::value>), dim3(q.nt), dim3(256), 0, sw, A,
                                    q.tile_base, (const unsigned long long *)dp(o_sum), part, tk);
             });
         });
-        run(0, [&](unsigned long long *tk) {
+        run(0, sw, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(reduce_parts_kernel, dim3(q.n, (q.nval + 255) / 256), dim3(256), 0, sw, (const long long *)part,
                                (const int32_t *)d_t0 + q.unit_base, q.tile_base, q.nval, mh, tk);
         });
         HIP_TRY(hipGetLastError());
     }
     if (nt_sg) {
-        run(1, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
+        run(1, st, [&](unsigned long long *tk) { hipLaunchKernelGGL(sgr_flt_kernel<T>, dim3(nt_sg), dim3(SG_NT), 0, st, A, tk); });
         HIP_TRY(hipGetLastError());
     }
     mark(0);
@@ -2591,7 +2765,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     cfg.wn_use_refinement = c->wn_use_refinement, cfg.wn_max_one_step = c->wn_max_one_refinement_step;
     cfg.sg_refine[0] = c->sg_refine[0], cfg.sg_refine[1] = c->sg_refine[1];
     if (n_wn) {
-        run(4, [&](unsigned long long *tk) {
+        run(4, sw, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_solve_kernel, dim3(n_wn), dim3(256), 0, sw, A, nplanes, (const int64_t *)dp(o_mh),
                                cfg, (Descent *)dp(o_wds), (SvtGpuRestUnit *)dp(o_wu), tk);
         });
@@ -2600,7 +2774,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     mark(1);
     // ---- phase 3: descent rounds on the device ----
     if (n_wn) { // the whole Wiener descent of every unit, resident on one CU each (or a few, for the largest)
-        run(2, [&](unsigned long long *tk) {
+        run(2, sw, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
                                (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa ? qa + q_wrx : nullptr),
                                (int32_t *)dp(o_wstat), pc, wr_stat, tk);
@@ -2608,7 +2782,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         HIP_TRY(hipGetLastError());
     }
     if (n_sr) { // the whole self-guided search of every (unit, ep), resident on one CU each (or a few)
-        run(3, [&](unsigned long long *tk) {
+        run(3, st, [&](unsigned long long *tk) {
             const int nodes = sr_tree_nodes();
             auto kern = nodes == 1 ? sgr_res_kernel<T, false> : sgr_res_kernel<T, true>;
             hipLaunchKernelGGL(kern, dim3(n_sr), dim3(SR_NT), SR_LDS, st, A, sg_planes,
@@ -2623,7 +2797,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     if (n_sg) {
         hipLaunchKernelGGL(sgr_best_kernel, dim3((n_sg + 255) / 256), dim3(256), 0, st, (const Descent *)dp(o_sds), A,
                            sg_planes, n_sg, (int32_t *)dp(o_best), (int32_t *)dp(o_braw));
-        run(4, [&](unsigned long long *tk) {
+        run(4, st, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(sgr_sse_kernel<T>, dim3(nt_sg), dim3(256), 0, st, A, (const int32_t *)dp(o_best),
                                (unsigned long long *)dp(o_sse2), tk);
         });
@@ -2662,6 +2836,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                      "us; control wave before B3 %.2f us)\n", v[0], v[1] / n,
                      v[1] ? (double)v[2] / (double)v[6] * n / v[1] : 0.0, v[6] / n, v[3] / n * 0.01, v[4] / n * 0.01,
                      v[5] / n * 0.01, v[7] / n * 0.01, v[8] / n * 0.01, v[9] / n * 0.01);
+        const double m = (double)std::max(1ull, v[10]), o = (double)std::max(1ull, v[0] - v[10]);
+        std::fprintf(stderr, "sgr_res: row-part items %llu: load %.2f us, descent %.2f us (control %.2f us); one-part "
+                     "items %llu: load %.2f us, descent %.2f us (control %.2f us)\n", v[10], v[11] / m * 0.01,
+                     v[12] / m * 0.01, v[13] / m * 0.01, v[0] - v[10], (v[3] - v[11]) / o * 0.01,
+                     (v[4] - v[12]) / o * 0.01, (v[5] - v[13]) / o * 0.01);
     }
     if (n_sr && *(const int32_t *)hp(h_res + (o_sstat - o_sse))) { // status bits of sgr_res_kernel
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR self-guided descent: pass bound, part plan or exchange failed",
@@ -2785,7 +2964,8 @@ extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfi
         s->prof = pr;
     }
     if (enable) {
-        pr->mask = enable < 0 ? 63 : enable & 63;
+        pr->mask   = enable < 0 ? 63 : enable & 63;
+        pr->events = enable > 0 && (enable & 64);
     } else if (pr) {
         delete pr;
         s->prof = nullptr;

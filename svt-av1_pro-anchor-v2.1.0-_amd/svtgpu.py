@@ -175,7 +175,7 @@ class LrSearchControls(ctypes.Structure):
 
 
 LR_PROFILE_DTYPE = np.dtype([("launches", np.int32, 6), ("ms", np.float32, 6), ("bytes", np.float64, 6),
-                             ("searches", np.int32)], align=True)
+                             ("searches", np.int32), ("ms_events", np.float32, 6)], align=True)
 LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYPE), ("sgrproj", REST_UNIT_DTYPE)],
                                 align=True)
 
@@ -897,9 +897,10 @@ class LrState:
 
     PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other", "sgr_moments")
 
-    def profile(self, enable=True):
+    def profile(self, enable=True, events=False):
         """svtgpu_lr_profile: device-clock timing of the searches (enable: True = every class, a class name or a
-        list of names = those classes, False = off).  Returns the per-class {launches, ms, bytes} totals of the
+        list of names = those classes, False = off).  Returns the per-class {launches, ms (device clock), ms_events
+        (HIP events around each launch), bytes} totals of the
         searches timed since the previous call (kernel classes of svtgpu.h; untimed classes read 0) plus
         "searches", their count; reading synchronizes the device."""
         if enable is True:
@@ -909,10 +910,13 @@ class LrState:
         else:
             names = [enable] if isinstance(enable, str) else list(enable)
             mask = sum(1 << self.PROFILE_CLASSES.index(c) for c in names)
+        if mask and events:
+            mask = (63 if mask < 0 else mask) | 64
         raw = np.zeros(1, LR_PROFILE_DTYPE)
         check(lib().svtgpu_lr_profile(self.h, mask, ptr(raw)))
         out = {c: {"launches": int(raw["launches"][0][i]), "ms": float(raw["ms"][0][i]),
-                   "bytes": float(raw["bytes"][0][i])} for i, c in enumerate(self.PROFILE_CLASSES)}
+                   "ms_events": float(raw["ms_events"][0][i]), "bytes": float(raw["bytes"][0][i])}
+               for i, c in enumerate(self.PROFILE_CLASSES)}
         out["searches"] = int(raw["searches"][0])
         return out
 
