@@ -921,8 +921,10 @@ __host__ __device__ inline void set_wiener_taps(int16_t *t, const int *v) { // s
 //     per column (the rows y-3 .. y+4 the vertical pass needs), computing one new pair of horizontal rows per pair
 //     of output rows: 4 v_dot2 per horizontal and per vertical output, the add-source term folded into the centre
 //     taps, the SSE as one v_dot2 of the packed (out - src) pair with itself;
-//   * two workgroup barriers per candidate: the SSE reduction and lane 0's descent step (Descent::report / next,
-//     exactly as the other Wiener paths), whose taps every lane reads back into scalar registers.
+//   * one workgroup barrier per candidate (one-part units): the SSE reduction; every wave then steps its own copy of
+//     the descent (Descent::report / next, exactly as the other Wiener paths) in scalar registers and takes the next
+//     candidate's taps from it.  Row-part units (and SVTGPU_WR_CLASSIC=1) keep two barriers: lane 0 exchanges the
+//     parts' SSEs, steps the descent and writes the taps to LDS.
 // The candidate count per unit is bounded (WR_MAX_ROUNDS; a descent always ends far earlier): on overflow the
 // descent stops and *status is set, which search_frame reports as SVTGPU_ERR_HIP.
 // ---------------------------------------------------------------------------------------------
@@ -989,10 +991,27 @@ __device__ inline void wr_fetch(const uint32_t *win, int ws, const PlaneArgs &P,
     }
 }
 
+// wave-uniform copies (scalar registers) of a 64-bit lane value and of a struct
+__device__ __forceinline__ long long readlane64(long long v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l),
+                   hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)v >> 32), l);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+template <typename S>
+__device__ __forceinline__ S uniform(const S &v) {
+    static_assert(sizeof(S) % 4 == 0, "whole dwords");
+    S r;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(S) / 4); k++)
+        ((int *)&r)[k] = __builtin_amdgcn_readfirstlane(((const int *)&v)[k]);
+    return r;
+}
+
 template <typename T, bool LDSW>
 __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, const uint32_t *win, int ws, int ux,
                        int uy, int w, int h, const WrItem &it, unsigned long long *xch, int *s_mode, int16_t *s_taps,
-                       unsigned long long *s_part, int32_t *status, unsigned long long &npx, unsigned long long *stat) {
+                       unsigned long long *s_part, int32_t *status, unsigned long long &npx, unsigned long long *stat,
+                       bool classic) {
     // diagnostics (SVTGPU_WR_STATS): thread 0's pass time (candidate start to the first barrier), its control step
     // and the whole descent, in 100 MHz ticks, kept in LDS ({run start, pass, control, mark}: no registers)
     __shared__ unsigned long long s_wt[6];
@@ -1024,11 +1043,12 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
     const int         hb = (1 << (P.bd + 6)) + (1 << (rr.r0 - 1)), vb = (1 << (rr.r1 - 1)) - (1 << (P.bd + rr.r1 - 1));
     const int         jend = ((nrows + 1) >> 1) + 3;
     int               rounds = 0;
-    while (*s_mode) {
-        // the candidate's taps (uniform: scalar registers), the add-source 128 folded into the centre taps
+    // one candidate over the lane's rows: its error sum.  Taps uniform (scalar registers), the add-source 128 folded
+    // into the centre taps
+    auto eval = [&](const int *tap_h, const int *tap_v) -> int {
         int hf[8], vf[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) hf[k] = s_taps[k], vf[k] = s_taps[8 + k];
+        for (int k = 0; k < 8; k++) hf[k] = tap_h[k], vf[k] = tap_v[k];
         hf[3] += 128, vf[3] += 128;
         auto sp = [](int lo, int hi) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)pack2(lo, hi)); };
         const uint32_t He0 = sp(0, hf[0]), He1 = sp(hf[1], hf[2]), He2 = sp(hf[3], hf[4]), He3 = sp(hf[5], hf[6]);
@@ -1097,6 +1117,49 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
                 if (in >= 0 && 2 * in < nrows) sa = load_src(2 * in), sb = 2 * in + 1 < nrows ? load_src(2 * in + 1) : 0u;
                 step(j, ca, cb);
             }
+        }
+        return e;
+    };
+    // Self-stepping (one-part units, default): every wave holds the descent in its own scalar registers and steps it
+    // from the candidate's SSE -- one barrier per candidate, no wave waits on thread 0's step through LDS (which cost
+    // ~1.1 of the ~9 us per candidate).  SVTGPU_WR_CLASSIC=1 keeps thread 0's step (the row-part units always do:
+    // their SSE exchange runs on one thread)
+    if (it.nparts == 1 && !classic) {
+        __shared__ unsigned long long s_part2[2][WR_NT / 64];
+        Descent Dw   = uniform(D);
+        bool    live = __builtin_amdgcn_readfirstlane(*s_mode) != 0;
+        while (live) {
+            int tv[3], th[8], tvv[8];
+            Dw.taps(0, tv);
+            th[0] = th[6] = tv[0], th[1] = th[5] = tv[1], th[2] = th[4] = tv[2], th[3] = -2 * (tv[0] + tv[1] + tv[2]), th[7] = 0;
+            Dw.taps(1, tv);
+            tvv[0] = tvv[6] = tv[0], tvv[1] = tvv[5] = tv[1], tvv[2] = tvv[4] = tv[2], tvv[3] = -2 * (tv[0] + tv[1] + tv[2]);
+            tvv[7] = 0;
+            const int e = eval(th, tvv);
+            const unsigned long long et = wave_sum_u32_wide((uint32_t)e);
+            if ((threadIdx.x & 63) == WAVE_LAST) s_part2[rounds & 1][threadIdx.x >> 6] = et;
+            if (stat && threadIdx.x == 0) s_wt[1] += __builtin_amdgcn_s_memrealtime() - s_wt[3];
+            __syncthreads();
+            unsigned long long err = 0;
+#pragma unroll
+            for (int k = 0; k < WR_NT / 64; k++) err += s_part2[rounds & 1][k];
+            npx += (unsigned long long)w * h;
+            ++rounds;
+            const bool ok = rounds <= WR_MAX_ROUNDS; // a descent always ends: an internal failure, reported by the host
+            if (!ok && threadIdx.x == 0) atomicOr(status, 1);
+            if (ok) Dw.report(readlane64((long long)err, 0));
+            live = ok && Dw.next();
+            if (stat && threadIdx.x == 0) s_wt[3] = __builtin_amdgcn_s_memrealtime();
+        }
+        if (threadIdx.x == 0) D = Dw;
+    } else
+    while (*s_mode) {
+        int e;
+        {
+            int th[8], tvv[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) th[k] = s_taps[k], tvv[k] = s_taps[8 + k];
+            e = eval(th, tvv);
         }
         // the unit's SSE, then lane 0's descent step
         const unsigned long long et = wave_sum_u32_wide((uint32_t)e);
@@ -1169,7 +1232,7 @@ template <typename T>
 __global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, Descent *ds, const WrItem *items,
                                                            int lds_cap, unsigned long long *xch, int32_t *status,
                                                            unsigned long long *pc, unsigned long long *stat,
-                                                           unsigned long long *tk) {
+                                                           unsigned long long *tk, int classic) {
     PROF_BEGIN(tk);
     extern __shared__ uint32_t wr_win[]; // the part's CDEF window (LDS mode)
     __shared__ uint64_t           s_draw[sizeof(Descent) / 8];
@@ -1206,8 +1269,8 @@ __global__ __launch_bounds__(WR_NT) void wiener_res_kernel(const SearchArgs A, D
     }
     __syncthreads();
     unsigned long long npx = 0;
-    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat);
-    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat);
+    if (lds) wr_run<T, true>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat, classic != 0);
+    else wr_run<T, false>(A, P, D, wr_win, ws, ux, uy, w, h, it, xch, &s_mode, s_taps, s_part, status, npx, stat, classic != 0);
     if (threadIdx.x == 0 && it.part == 0) ds[u] = D;
     if (pc && threadIdx.x == 0 && npx) atomicAdd(pc + (blockIdx.x & (PROF_SP - 1)), npx);
     PROF_END(tk);
@@ -1544,21 +1607,6 @@ __device__ __forceinline__ void sr_children(const Descent &d, uint32_t &xw, bool
     }
 }
 
-// wave-uniform copies (scalar registers) of a 64-bit lane value and of a struct
-__device__ __forceinline__ long long readlane64(long long v, int l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l),
-                   hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((unsigned long long)v >> 32), l);
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
-template <typename S>
-__device__ __forceinline__ S uniform(const S &v) {
-    static_assert(sizeof(S) % 4 == 0, "whole dwords");
-    S r;
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(S) / 4); k++)
-        ((int *)&r)[k] = __builtin_amdgcn_readfirstlane(((const int *)&v)[k]);
-    return r;
-}
 // the next tree: a single node (the pending candidate itself) from the uniform descent, else one node per lane
 __device__ __forceinline__ void sr_tree_publish(const Descent &d, bool live, int nodes, uint32_t *s_xq,
                                                 uint32_t *s_mask, int *s_nv) {
@@ -1628,16 +1676,18 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
 // compiles only sr_pass<1>, which leaves the registers for its grouped LDS reads
 template <typename T, bool TREE>
 __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, int nplanes, const SrItem *items,
-                                                        const SeedCfg cfg, int nodes, Descent *ds,
+                                                        const SeedCfg cfg, int nodes_arg, Descent *ds,
                                                         unsigned long long *xch, unsigned xmode, int32_t *status,
                                                         unsigned long long *stat, unsigned long long *tk) {
     PROF_BEGIN(tk);
+    // one node per pass in the default kernel: a compile-time constant there, so the per-lane tree builder (a
+    // divergent Descent copy per lane) is not compiled in and the descent keeps to registers
+    const int nodes = TREE ? nodes_arg : 1;
     extern __shared__ uint2 sr_dx[];                   // [chunk k][pixel lane]: (x - src) of pixels 0, 1 | 2, 3 (int16)
     // wave partials: the moments, then each pass's errors; two buffers by pass parity (the one-barrier path of
     // one-part items reads a pass's partials while the next pass writes the other buffer)
     __shared__ unsigned long long s_red2[2][SR_PW][SG_NC];
     unsigned long long (*const s_red)[SG_NC] = s_red2[0];
-    __shared__ uint32_t           s_ch[2][8];          // one-barrier path (SVTGPU_SR_CHILDREN=1): each pass's children
     // one-barrier path: the seeded descent every wave steps itself (raw storage: Descent has member initializers)
     __shared__ __attribute__((aligned(8))) unsigned char s_desc_raw[sizeof(Descent)];
     Descent &s_desc = *reinterpret_cast<Descent *>(s_desc_raw);
@@ -1774,7 +1824,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         // diagnostics (stat): pixel wave 0's pass time (B2/B4 release to its arrival at B3) and its wait from B3 to the
         // B4 release
         unsigned long long tpass = 0, twait = 0, tmark = stat ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (!TREE && it.nparts == 1 && !(xmode & 0x600)) {
+        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
             // One barrier per pass, and no wave waits on another's descent step: every wave (pixel and control) holds
             // the seeded descent in its own scalar registers and steps it itself from the pass's wave partials --
             // report + next once per pass, the same decisions everywhere (the errors are the same LDS words).  Before
@@ -1811,7 +1861,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     twait += t - tmark, tmark = t;
                 }
             }
-        } else if (!TREE && !(xmode & 0x600)) {
+        } else if (!TREE && !(xmode & 0x200)) {
             // Row parts, self-stepping: the control wave sums this part's wave partials, exchanges the sum with the
             // other parts and leaves the frame-unit total in LDS (B4); then every wave steps its own copy of the
             // descent -- no children built, no wave waits on another's step
@@ -1843,35 +1893,6 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     decode_xq(Dw, x);
                     xq = __builtin_amdgcn_readfirstlane(pack2(x[0], x[1]));
                 }
-                if (stat) {
-                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-                    twait += t - tmark, tmark = t;
-                }
-            }
-        } else if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
-            // One barrier per pass: every pixel wave takes the outcome itself from the pass's wave partials and the
-            // two children the control wave prepared during the pass (the control wave decides identically and
-            // steps the descent while the next pass runs)
-            uint32_t xq   = __builtin_amdgcn_readfirstlane(s_xq[0]);
-            bool     live = __builtin_amdgcn_readfirstlane(s_nv) != 0;
-            for (int pass = 1; live; pass++) {
-                const uint32_t xl[1] = {xq};
-                sr_pass<1>(g, sr_dx, pl, K, 1, xl, s_red2[pass & 1]);
-                if (stat) {
-                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-                    tpass += t - tmark, tmark = t;
-                }
-                __syncthreads(); // B3: the pass's errors and the candidate's children are in LDS
-                unsigned long long e0 = 0;
-#pragma unroll
-                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
-                const uint32_t *ch    = s_ch[pass & 1];
-                const long long err   = (long long)(((unsigned long long)ch[5] << 32) | ch[4]);
-                const bool      worse = !ch[6] && (long long)e0 > err;
-                live = (worse ? ch[2] : ch[3]) && pass <= SR_MAX_PASSES;
-                xq   = worse ? ch[0] : ch[1];
-                xq   = __builtin_amdgcn_readfirstlane(xq);
-                live = __builtin_amdgcn_readfirstlane((int)live) != 0;
                 if (stat) {
                     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
                     twait += t - tmark, tmark = t;
@@ -1931,7 +1952,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         Descent D = uniform(sgr_seed(A, p, it.pair, (const int64_t *)mv, cfg));
         D.next(); // the seed itself is the first candidate
         sr_tree_publish(D, ok, nodes, s_xq, &s_mask, &s_nv);
-        if (!TREE && it.nparts == 1 && !(xmode & 0x600)) {
+        if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
             // the self-stepping path (see the pixel waves): the seeded descent to LDS for every wave, then the same
             // report + next per pass as everyone else
             if (lane == 0) s_desc = D;
@@ -1951,7 +1972,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
             }
             if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
-        } else if (!TREE && nodes == 1 && !(xmode & 0x600)) {
+        } else if (!TREE && nodes == 1 && !(xmode & 0x200)) {
             // self-stepping row parts (see the pixel waves): the exchange between B3 and B4, the step after B4
             if (lane == 0) s_desc = D;
             __syncthreads(); // B2
@@ -1976,43 +1997,6 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     if (pass > SR_MAX_PASSES && lane == 0) atomicOr(status, 1);
                 } else
                     live = false;
-                if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
-            }
-            if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
-        } else if (!TREE && it.nparts == 1 && !(xmode & 0x200)) {
-            // the one-barrier path (see the pixel waves): the children of each pending candidate go to s_ch by pass
-            // parity before the pass's barrier; after it the outcome is taken exactly as the pixel waves take it
-            auto publish_children = [&](int pass) {
-                uint32_t xw = 0, xb = 0;
-                bool     okw = false, okb = false;
-                sr_children(D, xw, okw, xb, okb);
-                if (lane == 0) {
-                    uint32_t *ch = s_ch[pass & 1];
-                    ch[0] = xw, ch[1] = xb, ch[2] = okw, ch[3] = okb;
-                    ch[4] = (uint32_t)(unsigned long long)D.err, ch[5] = (uint32_t)((unsigned long long)D.err >> 32);
-                    ch[6] = D.init;
-                }
-            };
-            bool live = ok;
-            if (live) publish_children(1);
-            __syncthreads(); // B2
-            int pass = 1;
-            for (; live; pass++) {
-                __syncthreads(); // B3
-                const unsigned long long tb = stat ? __builtin_amdgcn_s_memrealtime() : 0;
-                ncp += (unsigned long long)nch * 4;
-                unsigned long long e0 = 0;
-#pragma unroll
-                for (int w = 0; w < SR_PW; w++) e0 += s_red2[pass & 1][w][0];
-                // the error made wave-uniform (an LDS load is a vector value to the compiler): the descent's state and
-                // every branch of its step then stay scalar instead of exec-masked vector code
-                D.report(readlane64((long long)e0, 0));
-                live = D.next();
-                if (pass > SR_MAX_PASSES) {
-                    if (lane == 0) atomicOr(status, 1);
-                    live = false;
-                }
-                if (live) publish_children(pass + 1); // during the next pass
                 if (stat) tctl += __builtin_amdgcn_s_memrealtime() - tb;
             }
             if (stat && lane == 0) atomicAdd(stat + 1, (unsigned long long)(pass - 1));
@@ -2697,16 +2681,15 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         sr_xmode = 0x100u | (s->sx_epoch & 0xFFu);
     }
-    static const bool sr_two_barriers = [] { // SVTGPU_SR_1B=0: one-part items take the two-barrier path too (A/B)
-        const char *e = std::getenv("SVTGPU_SR_1B");
+    static const bool sr_two_barriers = [] { // SVTGPU_SR_1B=0 (A/B): every item on the two-barrier path, the control
+        const char *e = std::getenv("SVTGPU_SR_1B"); // wave stepping the descent alone (round 3's form)
         return e && !std::strcmp(e, "0");
     }();
     if (sr_two_barriers) sr_xmode |= 0x200u;
-    static const bool sr_children_path = [] { // SVTGPU_SR_CHILDREN=1: the round-4 one-barrier path (control-built children)
-        const char *e = std::getenv("SVTGPU_SR_CHILDREN");
-        return e && e[0] == '1';
+    static const bool wr_classic = [] { // SVTGPU_WR_CLASSIC=1 (A/B): the round-4 Wiener step (thread 0, two barriers)
+        const char *e = std::getenv("SVTGPU_WR_CLASSIC");
+        return e && std::atoi(e) != 0;
     }();
-    if (sr_children_path) sr_xmode |= 0x400u;
     static const bool   wr_stats = std::getenv("SVTGPU_WR_STATS") != nullptr; // per-search diagnostics to stderr
     static unsigned long long *wr_stat = nullptr;
     if (wr_stats && !wr_stat) HIP_TRY(hipMalloc(&wr_stat, 128));
@@ -2777,7 +2760,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         run(2, sw, [&](unsigned long long *tk) {
             hipLaunchKernelGGL(wiener_res_kernel<T>, dim3(n_wr), dim3(WR_NT), wr_lds, sw, A, (Descent *)dp(o_wds),
                                (const WrItem *)dp(o_witem), wr_lds, (unsigned long long *)(qa ? qa + q_wrx : nullptr),
-                               (int32_t *)dp(o_wstat), pc, wr_stat, tk);
+                               (int32_t *)dp(o_wstat), pc, wr_stat, tk, (int)wr_classic);
         });
         HIP_TRY(hipGetLastError());
     }

@@ -63,3 +63,19 @@ def test_no_vgpr_spills():
         shutil.rmtree(tmp, ignore_errors=True)
     assert seen > 50, seen
     assert not bad, bad
+
+
+@pytest.mark.skipif(not os.path.isdir(BUILD) or not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")),
+                    reason="needs the built objects and the ROCm LLVM tools")
+def test_resident_descents_keep_state_in_registers():
+    """The default resident descents hold no stack object: a `Descent` the compiler leaves in memory turns every
+    report / next of the per-pass step into a chain of scratch loads and stores (round 5: the control wave's descent
+    sat in a 128-byte private segment while two stepping paths shared it -- 287 scratch instructions)."""
+    tmp = tempfile.mkdtemp()
+    try:
+        ks = _kernels(os.path.join(BUILD, "lr_search.o"), tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    hot = {n: m for n, m in ks.items() if "wiener_res_kernel" in n or ("sgr_res_kernel" in n and "Lb0" in n)}
+    assert len(hot) == 4, sorted(ks)
+    assert all(m.get("private_segment_fixed_size", 0) == 0 for m in hot.values()), hot
