@@ -815,7 +815,11 @@ typedef struct SvtGpuRestUnit {
 } SvtGpuRestUnit;
 
 typedef struct SvtGpuLrState SvtGpuLrState;
-/* unit_size[plane]: restoration_unit_size (64/128/256 luma; chroma usually luma >> 1) */
+/* unit_size[plane]: restoration_unit_size (64/128/256 luma; chroma usually luma >> 1).  width / height: the
+ * picture's crop size (frm_size.frame_width / _height, EbPictureControlSet.c:1207; any size >= 8), which the
+ * restoration units, the search and the filter cover (chroma (width + 1) >> 1, the reference's crop_widths); the
+ * frames handed to the search and the apply are the 8-aligned coded size (the deblocking / CDEF extent, mi_cols x 4).
+ * Samples right of / below the crop keep the CDEF output in the apply. */
 int  svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, const int32_t unit_size[3],
                             SvtGpuLrState **out);
 void svtgpu_lr_state_destroy(SvtGpuLrState *s);

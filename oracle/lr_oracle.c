@@ -210,7 +210,7 @@ int oracle_lr_units(int size, int extent) { return MAX_((extent + (size >> 1)) /
  * dlf rows around internal stripe edges. */
 static void lr_plane(const OracleFrame *dlf, const OracleFrame *cdef, OracleFrame *out, int p, int unit_size,
                      const SvtGpuRestUnit *units) {
-    const int ss = p > 0, W = p ? cdef->width >> 1 : cdef->width, H = p ? cdef->height >> 1 : cdef->height;
+    const int ss = p > 0, W = p ? (cdef->width + 1) >> 1 : cdef->width, H = p ? (cdef->height + 1) >> 1 : cdef->height;
     const int bd = cdef->bit_depth;
     const int full = 64 >> ss, off = 8 >> ss, procw = 64 >> ss;
     const int hunits = oracle_lr_units(unit_size, W);
@@ -281,7 +281,7 @@ static void lr_plane(const OracleFrame *dlf, const OracleFrame *cdef, OracleFram
 int oracle_lr_apply_frame(const OracleFrame *dlf, const OracleFrame *cdef, OracleFrame *out, const int *frame_type,
                           const int *unit_size, const SvtGpuRestUnit *const *units) {
     for (int p = 0; p < 3; p++) {
-        const int W = p ? cdef->width >> 1 : cdef->width, H = p ? cdef->height >> 1 : cdef->height;
+        const int W = p ? (cdef->width + 1) >> 1 : cdef->width, H = p ? (cdef->height + 1) >> 1 : cdef->height;
         if (frame_type[p] == SVTGPU_RESTORE_NONE) {
             for (int y = 0; y < H; y++)
                 for (int x = 0; x < W; x++) set_px(out, p, y, x, plane_px(cdef, p, y, x));

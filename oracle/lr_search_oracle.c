@@ -551,7 +551,7 @@ int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, 
     const int plane_end = ((c->wn_enabled && c->wn_use_chroma) || (c->sg_enabled && c->sg_use_chroma)) ? 2 : 0;
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
     for (int p = 0; p <= plane_end; p++) {
-        const int W = p ? recon->width >> 1 : recon->width, H = p ? recon->height >> 1 : recon->height;
+        const int W = p ? (recon->width + 1) >> 1 : recon->width, H = p ? (recon->height + 1) >> 1 : recon->height;
         const Pl  dgd = {recon->plane[p], recon->stride[p], W, H, hb}, src = {source->plane[p], source->stride[p], W, H, hb};
         const int usz = unit_size[p], hu = oracle_lr_units(usz, W), vu = oracle_lr_units(usz, H), n = hu * vu;
         const int ext = usz * 3 / 2, off = 8 >> (p > 0);

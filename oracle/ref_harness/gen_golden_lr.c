@@ -229,6 +229,9 @@ static void gen_frames(const char *dir) {
     static const LrCase cases[] = {
         {200, 136, 8, 64, {3, 1, 2}},   {256, 200, 10, 64, {3, 3, 3}}, {136, 72, 10, 128, {1, 0, 2}},
         {320, 256, 8, 128, {2, 1, 0}},  {392, 232, 10, 256, {3, 3, 1}}, {64, 48, 8, 64, {3, 2, 2}},
+        /* crop sizes that are not multiples of 8 (frm_size.frame_width = input width - pad): odd chroma widths and
+         * heights, a last unit column and stripe ending inside a 4-sample group */
+        {202, 138, 10, 64, {3, 3, 3}},  {134, 74, 8, 64, {1, 2, 3}},   {250, 90, 10, 128, {2, 3, 1}},
     };
     const int ncase = (int)(sizeof(cases) / sizeof(cases[0]));
     char      path[512];
@@ -337,6 +340,8 @@ static void gen_search(const char *dir) {
     static const SearchCase cases[] = {
         {136, 72, 8, 64, 1, 1}, {200, 136, 10, 64, 1, 1}, {256, 144, 10, 128, 2, 2},
         {160, 96, 8, 64, 3, 3}, {128, 128, 10, 64, 4, 4}, {96, 64, 8, 128, 1, 0},
+        /* crop sizes that are not multiples of 8 (see gen_frames) */
+        {202, 138, 10, 64, 1, 1}, {134, 74, 8, 64, 2, 2}, {250, 90, 10, 128, 1, 1}, {198, 102, 8, 64, 3, 3},
     };
     const int ncase = (int)(sizeof(cases) / sizeof(cases[0]));
     char      path[512];
@@ -362,8 +367,8 @@ static void gen_search(const char *dir) {
         cm->subsampling_x = cm->subsampling_y = 1;
         cm->use_highbitdepth                   = hb;
         cm->bit_depth                          = c->bd;
-        cm->mi_rows                            = c->h >> 2;
-        cm->mi_cols                            = c->w >> 2;
+        cm->mi_rows                            = ((c->h + 7) & ~7) >> 2; /* the 8-aligned coded size */
+        cm->mi_cols                            = ((c->w + 7) & ~7) >> 2;
         set_ctrls(cm, c->wn, c->sg);
         x->rdmult = 1000 + (int)rng_below(&r, 20000);
         for (int k = 0; k < 3; k++) x->switchable_restore_cost[k] = 100 + (int)rng_below(&r, 2000);
@@ -410,8 +415,11 @@ static void gen_search(const char *dir) {
                 const RestorationUnitInfo *ui = &rsi->unit_info[k];
                 int32_t                   *e  = u + 20 * k;
                 e[0]                          = ft[p] == RESTORE_NONE ? 0 : ui->restoration_type;
-                for (int q = 0; q < 8; q++) e[1 + q] = ui->wiener_info.vfilter[q], e[9 + q] = ui->wiener_info.hfilter[q];
-                e[17] = ui->sgrproj_info.ep, e[18] = ui->sgrproj_info.xqd[0], e[19] = ui->sgrproj_info.xqd[1];
+                /* only the parameters of the unit's own type: the reference leaves the others unwritten */
+                if (e[0] == RESTORE_WIENER)
+                    for (int q = 0; q < 8; q++) e[1 + q] = ui->wiener_info.vfilter[q], e[9 + q] = ui->wiener_info.hfilter[q];
+                if (e[0] == RESTORE_SGRPROJ)
+                    e[17] = ui->sgrproj_info.ep, e[18] = ui->sgrproj_info.xqd[0], e[19] = ui->sgrproj_info.xqd[1];
                 const RestUnitSearchInfo *rs = &pcs->rusi_picture[p][k];
                 for (int q = 0; q < 3; q++) ss[3 * k + q] = rs->sse[q] == INT64_MAX ? -1 : rs->sse[q];
                 for (int q = 0; q < 8; q++) sp[19 * k + q] = rs->wiener.vfilter[q], sp[19 * k + 8 + q] = rs->wiener.hfilter[q];

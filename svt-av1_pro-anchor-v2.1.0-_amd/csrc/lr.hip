@@ -299,8 +299,7 @@ int count_units(int size, int extent) { return std::max((extent + (size >> 1)) /
 
 extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, const int32_t unit_size[3],
                                       SvtGpuLrState **out) {
-    if (!ctx || !out || !unit_size || width <= 0 || height <= 0 || (width & 7) || (height & 7))
-        return SVTGPU_ERR_INVALID_ARG;
+    if (!ctx || !out || !unit_size || width < 8 || height < 8) return SVTGPU_ERR_INVALID_ARG;
     for (int p = 0; p < 3; p++) {
         const int u = unit_size[p], minu = p ? 32 : 64;
         if (u < minu || u > 256 || (u & (u - 1))) return SVTGPU_ERR_INVALID_ARG;
@@ -313,7 +312,7 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
     hipError_t e     = hipSuccess;
     size_t     nu    = 0;
     for (int p = 0; p < 3; p++) {
-        const int pw = p ? width / 2 : width, ph = p ? height / 2 : height;
+        const int pw = lr_plane_w(s, p), ph = lr_plane_h(s, p);
         s->unit_size[p] = unit_size[p];
         s->hunits[p]    = count_units(unit_size[p], pw);
         s->vunits[p]    = count_units(unit_size[p], ph);
@@ -376,9 +375,10 @@ extern "C" int svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpu
 extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *deblocked, const SvtGpuFrame *cdef_out,
                                      SvtGpuFrame *out, const int32_t frame_type[3], void *stream) {
     auto ok = [&](const SvtGpuFrame *f) {
-        return f && f->width == s->width && f->height == s->height && f->bit_depth == cdef_out->bit_depth;
+        return lr_frame_fits(s, f) && f->bit_depth == cdef_out->bit_depth;
     };
-    if (!s || !cdef_out || !ok(deblocked) || !ok(out) || !frame_type || out == cdef_out || out == deblocked)
+    if (!s || !cdef_out || !ok(cdef_out) || !ok(deblocked) || !ok(out) || !frame_type || out == cdef_out ||
+        out == deblocked)
         return SVTGPU_ERR_INVALID_ARG;
     if (cdef_out->bit_depth != 8 && cdef_out->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
     hipStream_t  st  = pick_stream(s->ctx, stream);
@@ -388,6 +388,22 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
     int nblk  = 0;
     for (int p = 0; p < 3; p++) {
         const int32_t *r = s->tile_out[p]; // the samples written (the whole plane unless tiled over GPUs)
+        // a crop size below the coded size: the samples right of / below the restored area keep the CDEF output
+        // (the reference filters crop_widths x crop_heights only, EbRestoration.c:1216-1217)
+        const int pw = lr_plane_w(s, p), ph = lr_plane_h(s, p);
+        if (r[2] == pw && pw < cdef_out->pw[p])
+            HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[p] + ((size_t)r[1] * out->stride[p] + pw) * bps,
+                                     out->stride[p] * bps,
+                                     (const uint8_t *)cdef_out->plane[p] + ((size_t)r[1] * cdef_out->stride[p] + pw) * bps,
+                                     cdef_out->stride[p] * bps, (cdef_out->pw[p] - pw) * bps, r[3] - r[1],
+                                     hipMemcpyDeviceToDevice, st));
+        if (r[3] == ph && ph < cdef_out->ph[p])
+            HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[p] + ((size_t)ph * out->stride[p] + r[0]) * bps,
+                                     out->stride[p] * bps,
+                                     (const uint8_t *)cdef_out->plane[p] + ((size_t)ph * cdef_out->stride[p] + r[0]) * bps,
+                                     cdef_out->stride[p] * bps,
+                                     ((r[2] == pw ? cdef_out->pw[p] : r[2]) - r[0]) * bps, cdef_out->ph[p] - ph,
+                                     hipMemcpyDeviceToDevice, st));
         if (frame_type[p] == SVTGPU_RESTORE_NONE) {
             const size_t io = ((size_t)r[1] * cdef_out->stride[p] + r[0]) * bps, oo = ((size_t)r[1] * out->stride[p] + r[0]) * bps;
             HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[p] + oo, out->stride[p] * bps,
@@ -402,8 +418,8 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
         a.dlf_stride  = deblocked->stride[p];
         a.cdef_stride = cdef_out->stride[p];
         a.out_stride  = out->stride[p];
-        a.W           = cdef_out->pw[p];
-        a.H           = cdef_out->ph[p];
+        a.W           = pw;
+        a.H           = ph;
         a.ss          = p > 0;
         a.unit_size   = s->unit_size[p];
         a.hunits      = s->hunits[p];

@@ -38,6 +38,14 @@ struct SvtGpuLrState {
     SvtGpuComm          *comm;
 };
 void lr_profiler_destroy(void *prof);
+// The restored area of a plane: the frame's crop size (frm_size.frame_width / _height; chroma rounded up, the
+// reference's crop_widths / crop_heights, EbPictureBufferDesc.c) -- the device frames themselves are the 8-aligned
+// coded size the deblocking and CDEF stages cover (mi_cols x 4)
+inline int lr_plane_w(const SvtGpuLrState *s, int p) { return p ? (s->width + 1) >> 1 : s->width; }
+inline int lr_plane_h(const SvtGpuLrState *s, int p) { return p ? (s->height + 1) >> 1 : s->height; }
+inline bool lr_frame_fits(const SvtGpuLrState *s, const SvtGpuFrame *f) {
+    return f && f->width == ((s->width + 7) & ~7) && f->height == ((s->height + 7) & ~7);
+}
 
 namespace {
 

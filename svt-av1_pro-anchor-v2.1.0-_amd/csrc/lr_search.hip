@@ -138,17 +138,22 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
     const PlaneArgs &P = A.pl[t.plane];
     const T         *d = (const T *)P.dgd, *s = (const T *)P.src;
     uint32_t ps = 0, pe = 0; // <= 16 samples per lane: fits 32 bits
-    // 4-sample chunks (tile x offsets and widths are multiples of 4): chunk k of this lane is row
-    // (threadIdx.x >> 4) + 16 k, columns 4 (threadIdx.x & 15) .. + 3; all four chunks' loads are issued first
+    // 4-sample chunks (tile x offsets are multiples of 4): chunk k of this lane is row (threadIdx.x >> 4) + 16 k,
+    // columns 4 (threadIdx.x & 15) .. + 3; all four chunks' loads are issued first.  A plane whose crop width is not a
+    // multiple of 4 ends in a partial chunk: its samples past the crop are read one by one and left out
     int dv[4][4], sv[4][4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int r = (threadIdx.x >> 4) + 16 * k, c = 4 * (threadIdx.x & 15);
 #pragma unroll
         for (int j = 0; j < 4; j++) dv[k][j] = sv[k][j] = 0;
-        if (r < t.h && c < t.w) {
+        if (r < t.h && c + 4 <= t.w) {
             load4(d + (size_t)(t.y0 + r) * P.dstride + t.x0 + c, dv[k]);
             load4(s + (size_t)(t.y0 + r) * P.sstride + t.x0 + c, sv[k]);
+        } else if (r < t.h && c < t.w) {
+            for (int j = 0; j < t.w - c; j++)
+                dv[k][j] = d[(size_t)(t.y0 + r) * P.dstride + t.x0 + c + j],
+                sv[k][j] = s[(size_t)(t.y0 + r) * P.sstride + t.x0 + c + j];
         }
     }
 #pragma unroll
@@ -595,13 +600,22 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
         const int    y = t.y0 + r, x = t.x0 + c;
         const size_t o = (size_t)y * P.fstride + x;
         int          dv[4], sv[4], g0[4] = {0, 0, 0, 0}, g1[4] = {0, 0, 0, 0};
-        load4(d + (size_t)y * P.dstride + x, dv);
-        load4(s + (size_t)y * P.sstride + x, sv);
-        if (r0 > 0) load4s(f0 + o, g0);
+        const int    nv = min(4, t.w - c); // a partial chunk at a crop width that is not a multiple of 4
+        if (nv == 4) {
+            load4(d + (size_t)y * P.dstride + x, dv);
+            load4(s + (size_t)y * P.sstride + x, sv);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                dv[j] = j < nv ? (int)d[(size_t)y * P.dstride + x + j] : 0,
+                sv[j] = j < nv ? (int)s[(size_t)y * P.sstride + x + j] : 0;
+        }
+        if (r0 > 0) load4s(f0 + o, g0); // the filter planes' rows are padded to 64 samples
         if (r1 > 0) load4s(f1 + o, g1);
         uint32_t e2 = 0; // 4 squared errors of at most 1023^2
 #pragma unroll
         for (int j = 0; j < 4; j++) {
+            if (j >= nv) break;
             const int u = dv[j] << 4;
             int       v = u << 7;
             if (r0 > 0) v += xq0 * (g0[j] - u);
@@ -1703,7 +1717,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
     const PlaneArgs &P  = A.pl[p];
     const int        ul = (it.pair - P.pair_base) / P.ne, k = it.pair - P.pair_base - ul * P.ne, ep = P.eps[k];
     const URect      ur = A.units[P.unit_base + ul];
-    const int        cw = (ur.h_end - ur.h_start) >> 2, nch = cw * (it.y1 - it.y0), K = (nch + SR_PL - 1) / SR_PL;
+    const int        uw = ur.h_end - ur.h_start, cw = (uw + 3) >> 2, nch = cw * (it.y1 - it.y0), K = (nch + SR_PL - 1) / SR_PL;
     if (K > SR_KMAX || nch <= 0) { // the host plans parts of <= SR_MAX_PX pixels; never index past the registers
         if (threadIdx.x == 0) atomicOr(status, 4);
         return;
@@ -1762,13 +1776,15 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                         if (kb + j < SR_KMAX) sr_dx[(kb + j) * SR_PL + pl] = make_uint2(0u, 0u);
                 continue;
             }
-            int2 dv2[LB2], sv2[LB2];
-            bool on[LB2];
+            int2     dv2[LB2], sv2[LB2];
+            uint64_t pm[LB2]; // 16 bits per pixel of the chunk inside the part: all four, fewer in the last column of a
+                              // crop width that is not a multiple of 4, none past the part
 #pragma unroll
             for (int j = 0; j < LB2; j++) { // the group's loads in flight together
                 int row, col;
                 chunk_at(kb + j, row, col);
-                on[j] = kb + j < SR_KMAX && pl + (kb + j) * SR_PL < nch;
+                const int nin = kb + j < SR_KMAX && pl + (kb + j) * SR_PL < nch ? min(4, uw - 4 * col) : 0;
+                pm[j]         = nin >= 4 ? ~0ull : (1ull << (16 * nin)) - 1;
                 const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
                 if constexpr (sizeof(T) == 2) {
                     dv2[j] = *(const int2 *)(d + (size_t)y * P.dstride + x);
@@ -1784,6 +1800,15 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 const int kk = kb + j;
                 if (kk >= SR_KMAX) break;
                 int       dv[4], sv[4];
+                // pixels outside the part read as zeros everywhere: g = 0 and (x - src) = 0 add nothing to any sum
+                const uint32_t mlo = (uint32_t)pm[j], mhi = (uint32_t)(pm[j] >> 32);
+                g[kk][0] &= mlo, g[kk][2] &= mlo, g[kk][1] &= mhi, g[kk][3] &= mhi;
+                if constexpr (sizeof(T) == 2) {
+                    dv2[j].x &= mlo, sv2[j].x &= mlo, dv2[j].y &= mhi, sv2[j].y &= mhi;
+                } else {
+                    const uint32_t m8 = __builtin_amdgcn_perm(mhi, mlo, 0x06040200u); // one byte per pixel
+                    dv2[j].x &= m8, sv2[j].x &= m8;
+                }
                 if constexpr (sizeof(T) == 2) {
                     dv[0] = dv2[j].x & 0xFFFF, dv[1] = (uint32_t)dv2[j].x >> 16, dv[2] = dv2[j].y & 0xFFFF, dv[3] = (uint32_t)dv2[j].y >> 16;
                     sv[0] = sv2[j].x & 0xFFFF, sv[1] = (uint32_t)sv2[j].x >> 16, sv[2] = sv2[j].y & 0xFFFF, sv[3] = (uint32_t)sv2[j].y >> 16;
@@ -1800,7 +1825,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     // g = (flt0 - u, flt1 - u) on packed 16-bit lanes (|g| < 2^15: the wrapped halves are exact)
-                    const uint32_t gq = on[j] ? pk_sub16(fw[q], __umul24((uint32_t)dv[q], 0x00100010u)) & gmask : 0u;
+                    const uint32_t gq = pk_sub16(fw[q], __umul24((uint32_t)dv[q], 0x00100010u)) & gmask;
                     const int      g1 = (int)(int16_t)(gq & 0xFFFF), g2 = (int)gq >> 16, ss = (sv[q] - dv[q]) << 4;
                     m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
                     m3 += g1 * ss, m4 += g2 * ss;
@@ -1808,8 +1833,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     g[kk][q] = gq;
                 }
                 M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
-                sr_dx[kk * SR_PL + pl] = on[j] ? make_uint2(pack2(dv[0] - sv[0], dv[1] - sv[1]), pack2(dv[2] - sv[2], dv[3] - sv[3]))
-                                               : make_uint2(0u, 0u);
+                sr_dx[kk * SR_PL + pl] = make_uint2(pack2(dv[0] - sv[0], dv[1] - sv[1]), pack2(dv[2] - sv[2], dv[3] - sv[3]));
             }
         }
         {
@@ -2424,7 +2448,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     size_t               flt_elems = 0, part_elems = 0, mh_elems = 0;
     for (int p = 0; p < nplanes; p++) {
         PlanePlan &q = pp[p];
-        const int  W = rec->pw[p], H = rec->ph[p], usz = s->unit_size[p], ext = usz * 3 / 2, off = 8 >> (p > 0);
+        const int  W = lr_plane_w(s, p), H = lr_plane_h(s, p), usz = s->unit_size[p], ext = usz * 3 / 2, off = 8 >> (p > 0);
         q.unit_base = (int)units.size(), q.tile_base = (int)tiles.size();
         int urow = 0, uidx = 0;
         for (int y0 = 0; y0 < H; urow++) {
@@ -2467,8 +2491,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
     }
     tile0.push_back((int)tiles.size());
-    for (const Tile &t : tiles) // the projection kernel reads 4-pixel chunks
-        if ((t.x0 & 3) || (t.w & 3)) return SVTGPU_ERR_UNSUPPORTED;
+    for (const Tile &t : tiles) // 4-pixel chunks start on tile x offsets (unit columns: multiples of 32)
+        if (t.x0 & 3) return SVTGPU_ERR_UNSUPPORTED;
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
     if (n_all == 0) return SVTGPU_OK; // an empty band
     // the resident Wiener kernel takes every unit whose rows fit its registers (all units of the 4K / 1080p frames);
@@ -2525,7 +2549,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             int p = 0;
             while (p + 1 < nplanes && u >= pp[p + 1].unit_base) p++;
             const PlanePlan &q = pp[p];
-            const int        cw = (units[u].h_end - units[u].h_start) >> 2, h = units[u].v_end - units[u].v_start;
+            const int        cw = (units[u].h_end - units[u].h_start + 3) >> 2, h = units[u].v_end - units[u].v_start;
             const int        maxrows = std::max(1, sr_part_px() / 4 / std::max(cw, 1)), np = (h + maxrows - 1) / maxrows;
             if (np > SR_MAX_PARTS) return SVTGPU_ERR_UNSUPPORTED; // a unit wider than 1024 x 4 samples per row part
             sr_parted |= np > 1;
@@ -2600,7 +2624,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     for (int p = 0; p < nplanes; p++) {
         PlaneArgs &P = A.pl[p];
         P.dgd = rec->plane[p], P.src = src->plane[p], P.dstride = rec->stride[p], P.sstride = src->stride[p];
-        P.W = rec->pw[p], P.H = rec->ph[p], P.bd = rec->bit_depth, P.fstride = (P.W + 63) & ~63;
+        P.W = lr_plane_w(s, p), P.H = lr_plane_h(s, p), P.bd = rec->bit_depth, P.fstride = (P.W + 63) & ~63;
         P.flt       = s->d_flt + flt_off;
         P.unit_base = pp[p].unit_base, P.pair_base = pp[p].pair_base, P.ne = pp[p].ne;
         for (int k = 0; k < pp[p].ne; k++) {
@@ -2959,8 +2983,8 @@ extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfi
 namespace {
 int check_search_args(const SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                       const SvtGpuLrSearchControls *ctrls) {
-    if (!s || !recon || !source || !ctrls || recon->width != s->width || recon->height != s->height ||
-        source->width != s->width || source->height != s->height || recon->bit_depth != source->bit_depth)
+    if (!s || !recon || !source || !ctrls || !lr_frame_fits(s, recon) || !lr_frame_fits(s, source) ||
+        recon->bit_depth != source->bit_depth)
         return SVTGPU_ERR_INVALID_ARG;
     if (recon->bit_depth != 8 && recon->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
     for (int q = 0; q < 2; q++)
@@ -3022,7 +3046,7 @@ extern "C" int svtgpu_lr_set_tile(SvtGpuLrState *s, const int32_t units[3][4], c
                                   SvtGpuComm *comm) {
     if (!s) return SVTGPU_ERR_INVALID_ARG;
     for (int p = 0; p < 3; p++) {
-        const int pw = p ? s->width / 2 : s->width, ph = p ? s->height / 2 : s->height;
+        const int pw = lr_plane_w(s, p), ph = lr_plane_h(s, p);
         const int32_t all_u[4] = {0, 0, s->hunits[p], s->vunits[p]}, all_o[4] = {0, 0, pw, ph};
         const int32_t *u = units ? units[p] : all_u, *o = out ? out[p] : all_o;
         if (u[0] < 0 || u[1] < 0 || u[2] > s->hunits[p] || u[3] > s->vunits[p] || u[0] > u[2] || u[1] > u[3])

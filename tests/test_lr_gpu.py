@@ -71,39 +71,74 @@ def test_sgr_shims_golden(ctx):
         assert np.array_equal(out.astype(np.uint16), g["out%d" % n]), (n, eps)
 
 
+def _coded(planes, seed):
+    """Crop-size planes (the restored area) inside the 8-aligned coded frame the device stages work on: the samples
+    past the crop are random, so a read of them would show in the results."""
+    h, w = planes[0].shape
+    w8, h8 = (w + 7) & ~7, (h + 7) & ~7
+    if (w8, h8) == (w, h):
+        return planes
+    r = np.random.default_rng(seed)
+    out = []
+    for p, a in enumerate(planes):
+        pw, ph = (w8, h8) if p == 0 else (w8 // 2, h8 // 2)
+        b = r.integers(0, int(a.max()) + 1, (ph, pw)).astype(a.dtype)
+        b[:a.shape[0], :a.shape[1]] = a
+        out.append(b)
+    return out
+
+
 def _gpu_apply(ctx, dlf, cdef, bd, frame_type, unit_size, units):
-    h, w = cdef[0].shape
-    D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(3))
-    D.upload(dlf)
-    C.upload(cdef)
+    h, w = cdef[0].shape  # the crop size; the frames are the coded size
+    dlf8, cdef8 = _coded(dlf, 1), _coded(cdef, 2)
+    D, C, O = (svtgpu.Frame(ctx, cdef8[0].shape[1], cdef8[0].shape[0], bd) for _ in range(3))
+    D.upload(dlf8)
+    C.upload(cdef8)
     st = svtgpu.LrState(ctx, w, h, unit_size)
     for p in range(3):
         st.set_units(p, units[p])
     st.apply(D, C, O, frame_type)
-    return O.download()
+    got = O.download()
+    for p in range(3):  # past the crop the output keeps the CDEF samples
+        ph, pw = cdef[p].shape
+        m = np.ones(got[p].shape, bool)
+        m[:ph, :pw] = False
+        assert np.array_equal(got[p][m], cdef8[p][m]), p
+    return [got[p][:cdef[p].shape[0], :cdef[p].shape[1]] for p in range(3)]
 
 
-@pytest.mark.parametrize("case", list(range(6)))
+@pytest.mark.parametrize("case", list(range(9)))
 def test_lr_frame_golden(ctx, case):
+    """The reference's svt_av1_loop_restoration_filter_frame outputs (gen_golden_lr.c), cases 6-8 at crop sizes that
+    are not multiples of 8 (odd chroma widths / heights)."""
     c = list(lc.frame_cases())[case]
     got = _gpu_apply(ctx, c["dlf"], c["cdef"], c["bd"], c["frame_type"], c["unit_size"], c["units"])
     for p in range(3):
         assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
 
 
-LR_CASES = [(640, 360, 10, 64, 1), (1920, 1080, 8, 128, 2), (392, 232, 8, 256, 3), (3840, 2160, 10, 256, 4)]
+def _crop_pair(w, h, bd, seed):
+    """A synthetic (source, recon) pair at a crop size: generated at the coded size and cut to the crop."""
+    src, rec = synth.frame_pair((w + 7) & ~7, (h + 7) & ~7, bd, seed=seed)
+    cut = lambda planes: [a[:(h if p == 0 else (h + 1) // 2), :(w if p == 0 else (w + 1) // 2)] for p, a in enumerate(planes)]
+    return cut(src), cut(rec)
+
+
+# the last two: crop sizes of a 1366 x 766 picture (683 x 383 chroma) and 330 x 182 (165 x 91)
+LR_CASES = [(640, 360, 10, 64, 1), (1920, 1080, 8, 128, 2), (392, 232, 8, 256, 3), (3840, 2160, 10, 256, 4),
+            (1366, 766, 10, 64, 5), (330, 182, 8, 128, 6)]
 
 
 @pytest.mark.parametrize("w,h,bd,usize,seed", LR_CASES)
 def test_lr_frame_vs_oracle(ctx, w, h, bd, usize, seed):
-    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0700 + seed)
+    src, rec = _crop_pair(w, h, bd, seed=0x5EED0700 + seed)
     dlf = rec
     cdef = [np.clip(p.astype(np.int32) + ((src[i].astype(np.int32) - p) >> 2), 0, (1 << bd) - 1).astype(p.dtype)
             for i, p in enumerate(rec)]
     unit_size = [usize, usize >> 1, usize >> 1]
     units = []
     for p in range(3):
-        pw, ph = (w, h) if p == 0 else (w // 2, h // 2)
+        pw, ph = (w, h) if p == 0 else ((w + 1) // 2, (h + 1) // 2)
         n = oracle.lr_units(unit_size[p], pw) * oracle.lr_units(unit_size[p], ph)
         units.append(lc.random_units(n, seed * 10 + p, chroma=p > 0))
     ft = [1, 1, 1]
@@ -115,38 +150,43 @@ def test_lr_frame_vs_oracle(ctx, w, h, bd, usize, seed):
 
 # ------------------------------------------------------------------ search
 def _gpu_search(ctx, rec, src, bd, unit_size, ctrls):
-    h, w = rec[0].shape
-    R, S = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
-    R.upload(rec)
-    S.upload(src)
+    h, w = rec[0].shape  # the crop size; the frames are the coded size
+    rec8, src8 = _coded(rec, 3), _coded(src, 4)
+    R, S = (svtgpu.Frame(ctx, rec8[0].shape[1], rec8[0].shape[0], bd) for _ in range(2))
+    R.upload(rec8)
+    S.upload(src8)
     st = svtgpu.LrState(ctx, w, h, unit_size)
     ft, recs = st.search(R, S, ctrls, records=True)
     return st, R, ft, recs
 
 
-@pytest.mark.parametrize("case", list(range(6)))
+@pytest.mark.parametrize("case", list(range(10)))
 def test_lr_search_golden(ctx, case):
+    """The reference's restoration_seg_search + rest_finish_search records (gen_golden_lr.c), cases 6-9 at crop sizes
+    that are not multiples of 8."""
     c = list(lc.search_cases())[case]
     st, R, ft, recs = _gpu_search(ctx, c["rec"], c["src"], c["bd"], c["unit_size"], c["ctrls"])
     lc.compare_search(ft, c["units"], recs, c)  # frame types + per-unit records vs the reference
     # the picked units stay in the state: applying them must equal applying the reference's picked units
-    h, w = c["rec"][0].shape
+    h, w = R.height, R.width
+    rec8 = _coded(c["rec"], 3)
     D, O = svtgpu.Frame(ctx, w, h, c["bd"]), svtgpu.Frame(ctx, w, h, c["bd"])
-    D.upload(c["rec"])
+    D.upload(rec8)
     st.apply(D, R, O, ft)
     want = oracle.lr_apply_frame(c["rec"], c["rec"], c["bd"], ft, c["unit_size"], c["units"])
     got = O.download()
     for p in range(3):
-        assert np.array_equal(got[p], want[p]), (c["name"], p)
+        assert np.array_equal(got[p][:want[p].shape[0], :want[p].shape[1]], want[p]), (c["name"], p)
 
 
 LR_SEARCH_CASES = [(320, 192, 10, 64, 1, 1, 5), (640, 360, 8, 128, 1, 1, 6), (1920, 1080, 10, 256, 1, 1, 7),
-                   (512, 288, 10, 128, 3, 2, 8), (328, 184, 10, 64, 1, 1, 9), (264, 152, 8, 64, 2, 3, 10)]
+                   (512, 288, 10, 128, 3, 2, 8), (328, 184, 10, 64, 1, 1, 9), (264, 152, 8, 64, 2, 3, 10),
+                   (1366, 766, 10, 64, 1, 1, 11), (330, 182, 8, 64, 2, 3, 12), (1918, 1078, 10, 256, 1, 1, 13)]
 
 
 @pytest.mark.parametrize("w,h,bd,usize,wn,sg,seed", LR_SEARCH_CASES)
 def test_lr_search_vs_oracle(ctx, w, h, bd, usize, wn, sg, seed):
-    src, rec = synth.frame_pair(w, h, bd, seed=0x5EED0800 + seed)
+    src, rec = _crop_pair(w, h, bd, seed=0x5EED0800 + seed)
     ctrls = oracle.lr_controls(wn, sg, rdmult=6000 + seed * 1000, switchable=(300, 700, 900), wiener=(250, 800),
                                sgrproj=(250, 900))
     unit_size = [usize, usize >> 1, usize >> 1]
@@ -160,13 +200,13 @@ def test_lr_search_vs_oracle(ctx, w, h, bd, usize, wn, sg, seed):
         ok = recs[p]["sse"][:, 1] != np.iinfo(np.int64).max
         np.testing.assert_array_equal(recs[p]["wiener"][ok], want_recs[p]["wiener"][ok])
     # the searched units drive the apply: compare the restored frame with the oracle apply of the oracle's units
-    D, O = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
-    D.upload(rec)
+    D, O = svtgpu.Frame(ctx, R.width, R.height, bd), svtgpu.Frame(ctx, R.width, R.height, bd)
+    D.upload(_coded(rec, 3))
     st.apply(D, R, O, ft)
     want = oracle.lr_apply_frame(rec, rec, bd, ft, unit_size, want_units)
     got = O.download()
     for p in range(3):
-        assert np.array_equal(got[p], want[p]), p
+        assert np.array_equal(got[p][:want[p].shape[0], :want[p].shape[1]], want[p]), p
 
 
 @pytest.mark.parametrize("nb", [2, 3])
