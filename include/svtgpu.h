@@ -436,6 +436,12 @@ int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stre
  * SVTGPU_ERR_INVALID_ARG by the next svtgpu_dlf_pick, or by the next svtgpu_dlf_frame(_to) when no pick ran (the
  * FROM_Q levels); each upload is judged on its own. */
 int svtgpu_dlf_set_mode_info_device(SvtGpuDlfState *s, const SvtGpuLfMi *d_mi, void *stream);
+/* The picture's unpadded size when it is off the 8-sample grid (scs->max_input_luma_width - max_input_pad_right,
+ * _height - _pad_bottom; EbDeblockingFilter.c:99-129): set_lpf_parameters filters no edge at or past it in a plane
+ * (luma crop_width x crop_height, chroma both >> 1; :173-178), while the frames and the mode-info grid stay the
+ * 8-aligned coded size the state was created with.  Default: the coded size.  Takes effect at the next
+ * svtgpu_dlf_set_mode_info(_device). */
+int svtgpu_dlf_set_crop(SvtGpuDlfState *s, int32_t crop_width, int32_t crop_height);
 /* ≙ svt_av1_loop_filter_frame(frame, pcs, plane_start, plane_end) (EbDeblockingFilter.c:624-653):
  * all vertical edges of each plane, then all horizontal edges (equivalent to the reference's
  * SB-lagged order with combine_vert_horz_lf = 1, :41, :580-605), in place on `frame`. */

@@ -293,13 +293,16 @@ static void filter_sb_plane(const DlfCtx *C, int plane, int vert, int mi_row, in
     }
 }
 
-int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end) {
+/* crop_w / crop_h: the unpadded size set_lpf_parameters stops at (scs->max_input_luma_width - max_input_pad_right,
+ * EbDeblockingFilter.c:99-129); the frame is the coded size */
+int oracle_dlf_frame_crop(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end,
+                          int crop_w, int crop_h) {
     DlfCtx C;
     C.mi      = mi;
     C.mi_cols = ((f->width + 7) & ~7) >> 2;
     C.mi_rows = ((f->height + 7) & ~7) >> 2;
-    C.width   = f->width;
-    C.height  = f->height;
+    C.width   = crop_w;
+    C.height  = crop_h;
     C.f       = f;
     lf_info_init(&C.L, p, plane_start, plane_end);
     const int nsb_c = (f->width + 63) / 64, nsb_r = (f->height + 63) / 64;
@@ -319,6 +322,9 @@ int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams 
                     filter_sb_plane(&C, plane, 0, 16 * r, 16 * c);
             }
     return SVTGPU_OK;
+}
+int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end) {
+    return oracle_dlf_frame_crop(f, mi, p, plane_start, plane_end, f->width, f->height);
 }
 
 /* ------------------------------------------------------------------------------------------- */

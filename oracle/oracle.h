@@ -67,6 +67,9 @@ void oracle_highbd_lpf(uint16_t *s, int32_t pitch, int vertical, int len, const 
                        const uint8_t *limit, const uint8_t *thresh, int32_t bd);
 /* mi: [mi_rows][mi_cols] with mi_cols = ((w+7)&~7)/4; filters planes [plane_start, plane_end) in place */
 int oracle_dlf_frame(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end);
+/* the same on a coded-size frame whose unpadded size is crop_w x crop_h (edges at or past it are not filtered) */
+int oracle_dlf_frame_crop(OracleFrame *f, const SvtGpuLfMi *mi, const SvtGpuLfParams *p, int plane_start, int plane_end,
+                          int crop_w, int crop_h);
 /* level search; p in = last-frame levels (already averaged when dlf_avg), out = picked levels */
 int oracle_dlf_pick(OracleFrame *recon, const OracleFrame *src, const SvtGpuLfMi *mi, SvtGpuLfParams *p, int dlf_avg,
                     int dlf_avg_uv, int temporal_layer_index, int early_exit, int only4x4);

@@ -77,6 +77,8 @@ _SIGS = {
                                     _P]),
     "oracle_dlf_frame": (ctypes.c_int, [ctypes.POINTER(OracleFrame), _P, ctypes.POINTER(LfParams), ctypes.c_int,
                                         ctypes.c_int]),
+    "oracle_dlf_frame_crop": (ctypes.c_int, [ctypes.POINTER(OracleFrame), _P, ctypes.POINTER(LfParams), ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "oracle_dlf_pick": (ctypes.c_int, [ctypes.POINTER(OracleFrame), ctypes.POINTER(OracleFrame), _P,
                                        ctypes.POINTER(LfParams), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_int, ctypes.c_int]),
@@ -203,13 +205,15 @@ def lpf_lines(lines, bd, fn, blimit, limit, thresh, lowbd=False):
     return np.stack([win[8 + i, :] if vertical else win[:, 8 + i] for i in range(4)]).astype(np.uint16)
 
 
-def dlf_frame(planes, bd, mi, params, plane_start=0, plane_end=3):
-    """svt_av1_loop_filter_frame restatement; returns filtered copies of the planes."""
+def dlf_frame(planes, bd, mi, params, plane_start=0, plane_end=3, crop=None):
+    """svt_av1_loop_filter_frame restatement; returns filtered copies of the planes.  crop = (w, h): the unpadded size
+    of a coded-size picture (no edge at or past it is filtered)."""
     keep = []
     out = [np.array(p, copy=True) for p in planes]
     F = _frame(out, bd, keep)
     m = _mi(mi, *planes[0].shape)
-    rc = lib().oracle_dlf_frame(ctypes.byref(F), ptr(m), ctypes.byref(params), plane_start, plane_end)
+    cw, ch = crop if crop else (planes[0].shape[1], planes[0].shape[0])
+    rc = lib().oracle_dlf_frame_crop(ctypes.byref(F), ptr(m), ctypes.byref(params), plane_start, plane_end, cw, ch)
     assert rc == 0
     return out
 

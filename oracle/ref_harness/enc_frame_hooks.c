@@ -17,8 +17,10 @@
  * Each hook moves the encoder's picture buffers to the device (svtgpu_frame_upload) and its results back into the
  * encoder's own structures exactly where the reference function writes them (frame header fields, mode-info grid,
  * restoration units, the recon samples).  Configurations the library does not cover (DLF methods other than
- * FULL_IMAGE, delta LF, superres / resize, the previous-frame Wiener coefficients, the reference-based SGR ep range,
- * frame sizes off the 8-sample grid) call the encoder's own function (dlsym RTLD_NEXT) and count a fallback.
+ * FULL_IMAGE, delta LF, superres / resize, the previous-frame Wiener coefficients, the reference-based SGR ep range)
+ * call the encoder's own function (dlsym RTLD_NEXT) and count a fallback.  A picture whose size is off the 8-sample
+ * grid runs on the device too: the deblocking / CDEF frames are the encoder's padded (8-aligned) pictures, the loop
+ * restoration state the crop size frm_size.frame_width x frame_height (EbPictureControlSet.c:1207).
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -53,6 +55,15 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static SvtGpuContext  *g_ctx;
 
 void enc_frame_hooks_enable(int on) { g_on = on; }
+/* ENC_HOOK_STAGES (diagnostics): the stages whose hooks are active, bits 1 DLF, 2 CDEF, 4 LR (default all) */
+static int stage_on(int bit) {
+    static int m = -1;
+    if (m < 0) {
+        const char *e = getenv("ENC_HOOK_STAGES");
+        m             = e ? atoi(e) : 7;
+    }
+    return g_on && (m & bit);
+}
 uint64_t enc_frame_hook_calls(void) { return g_calls; }
 uint64_t enc_frame_hook_fallbacks(void) { return g_fallbacks; }
 void enc_frame_hook_kinds(uint64_t out[7]) { memcpy(out, g_kind, sizeof g_kind); }
@@ -78,7 +89,8 @@ static void count_kind(int fallback, int kind) {
 /* ---- per-picture device state (the encoder runs several pictures through the stages at once) ---- */
 typedef struct Ctx {
     PictureControlSet    *pcs;
-    int                   w, h, bd;
+    int                   w, h, bd; /* the coded (8-aligned) picture the frames hold */
+    int                   cw, ch;   /* the crop size loop restoration covers */
     SvtGpuFrame          *R, *S, *D, *O, *L; /* recon in, source, deblocked (pre-CDEF), CDEF output, LR output */
     SvtGpuDlfState       *dlf;
     SvtGpuCdefFrameState *cdef;
@@ -101,13 +113,17 @@ static Ctx *ctx_of(PictureControlSet *pcs) {
     if (!c) die("ctx_of: more than 64 pictures in flight", -1);
     SequenceControlSet *scs = pcs->scs;
     Av1Common          *cm  = pcs->ppcs->av1_cm;
-    const int w = cm->frm_size.frame_width, h = cm->frm_size.frame_height, bd = (int)scs->static_config.encoder_bit_depth;
-    if (c->R && (c->w != w || c->h != h || c->bd != bd)) die("picture geometry changed", -1);
+    const int cw = cm->frm_size.frame_width, ch = cm->frm_size.frame_height;
+    const int w = (cw + 7) & ~7, h = (ch + 7) & ~7, bd = (int)scs->static_config.encoder_bit_depth;
+    if (c->R && (c->cw != cw || c->ch != ch || c->bd != bd)) die("picture geometry changed", -1);
     if (!c->R) {
-        c->w = w, c->h = h, c->bd = bd;
+        c->w = w, c->h = h, c->cw = cw, c->ch = ch, c->bd = bd;
         SvtGpuFrame **f[5] = {&c->R, &c->S, &c->D, &c->O, &c->L};
         for (int i = 0; i < 5; i++) GPU(svtgpu_frame_create(g_ctx, w, h, bd, f[i]));
         GPU(svtgpu_dlf_state_create(g_ctx, w, h, &c->dlf));
+        /* the unpadded size set_lpf_parameters stops at (EbDeblockingFilter.c:99-129, :173-178) */
+        GPU(svtgpu_dlf_set_crop(c->dlf, scs->max_input_luma_width - scs->max_input_pad_right,
+                                scs->max_input_luma_height - scs->max_input_pad_bottom));
         GPU(svtgpu_cdef_state_create(g_ctx, w, h, &c->cdef));
     }
     return c;
@@ -141,12 +157,14 @@ static void yv12_planes(const Yv12BufferConfig *y, int hbd, void *pl[3], int32_t
     st[0] = y->y_stride, st[1] = st[2] = y->uv_stride;
 }
 
-/* the library covers 4:2:0 pictures on the 8-sample grid, 8/10-bit, without superres / resize */
+/* the library covers 4:2:0 pictures, 8/10-bit, without superres / resize; the encoder pads its pictures to the
+ * 8-sample grid (aligned_width / _height) and the frame-level stages work on that padded size */
 static int frame_supported(PictureControlSet *pcs) {
     SequenceControlSet *scs = pcs->scs;
     Av1Common          *cm  = pcs->ppcs->av1_cm;
     const int w = cm->frm_size.frame_width, h = cm->frm_size.frame_height, bd = (int)scs->static_config.encoder_bit_depth;
-    return g_on && (w & 7) == 0 && (h & 7) == 0 && (bd == 8 || bd == 10) &&
+    return g_on && pcs->ppcs->aligned_width == ((w + 7) & ~7) && pcs->ppcs->aligned_height == ((h + 7) & ~7) &&
+           (bd == 8 || bd == 10) &&
            scs->static_config.encoder_color_format == EB_YUV420 && scs->static_config.superres_mode == SUPERRES_NONE &&
            scs->static_config.resize_mode == RESIZE_NONE && cm->frm_size.superres_upscaled_width == w &&
            (scs->seq_header.sb_size == BLOCK_64X64 || scs->seq_header.sb_size == BLOCK_128X128);
@@ -158,7 +176,7 @@ typedef void (*SaveLinesFn)(const Yv12BufferConfig *, Av1Common *, int32_t);
 void svt_av1_loop_restoration_save_boundary_lines(const Yv12BufferConfig *frame, Av1Common *cm, int32_t after_cdef) {
     static SaveLinesFn orig;
     if (!orig) orig = (SaveLinesFn)dlsym(RTLD_NEXT, "svt_av1_loop_restoration_save_boundary_lines");
-    if (g_on && !after_cdef && frame_supported(cm->child_pcs)) {
+    if (stage_on(4) && !after_cdef && frame_supported(cm->child_pcs)) {
         Ctx    *c = ctx_of(cm->child_pcs);
         void   *pl[3];
         int32_t st[3];
@@ -213,7 +231,7 @@ typedef EbErrorType (*PickFn)(EbPictureBufferDesc *, PictureControlSet *, LpfPic
 EbErrorType svt_av1_pick_filter_level(EbPictureBufferDesc *srcBuffer, PictureControlSet *pcs, LpfPickMethod method) {
     static PickFn orig;
     if (!orig) orig = (PickFn)dlsym(RTLD_NEXT, "svt_av1_pick_filter_level");
-    if (!g_on) return orig(srcBuffer, pcs, method);
+    if (!stage_on(1)) return orig(srcBuffer, pcs, method);
     if (method != LPF_PICK_FROM_FULL_IMAGE || !dlf_supported(pcs)) {
         count(1);
         return orig(srcBuffer, pcs, method);
@@ -262,7 +280,7 @@ void svt_av1_loop_filter_frame(EbPictureBufferDesc *frame_buffer, PictureControl
                                int32_t plane_end) {
     static LfFrameFn orig;
     if (!orig) orig = (LfFrameFn)dlsym(RTLD_NEXT, "svt_av1_loop_filter_frame");
-    if (!g_on) return orig(frame_buffer, pcs, plane_start, plane_end);
+    if (!stage_on(1)) return orig(frame_buffer, pcs, plane_start, plane_end);
     if (!dlf_supported(pcs)) {
         count(1);
         return orig(frame_buffer, pcs, plane_start, plane_end);
@@ -300,7 +318,7 @@ typedef void (*FinishFn)(PictureControlSet *);
 void finish_cdef_search(PictureControlSet *pcs) {
     static FinishFn orig;
     if (!orig) orig = (FinishFn)dlsym(RTLD_NEXT, "finish_cdef_search");
-    if (!g_on) return orig(pcs);
+    if (!stage_on(2)) return orig(pcs);
     if (!frame_supported(pcs)) {
         count(1);
         return orig(pcs);
@@ -377,7 +395,7 @@ typedef void (*CdefFrameFn)(SequenceControlSet *, PictureControlSet *);
 void svt_av1_cdef_frame(SequenceControlSet *scs, PictureControlSet *pcs) {
     static CdefFrameFn orig;
     if (!orig) orig = (CdefFrameFn)dlsym(RTLD_NEXT, "svt_av1_cdef_frame");
-    Ctx *c = g_on && frame_supported(pcs) ? ctx_of(pcs) : NULL;
+    Ctx *c = stage_on(2) && frame_supported(pcs) ? ctx_of(pcs) : NULL;
     if (!c || !c->cdef_searched) {
         if (g_on) count(1);
         return orig(scs, pcs);
@@ -404,8 +422,7 @@ static int lr_supported(PictureControlSet *pcs) {
     if (!frame_supported(pcs)) return 0;
     if (cm->wn_filter_ctrls.enabled && cm->wn_filter_ctrls.use_prev_frame_coeffs) return 0;
     if (cm->sg_filter_ctrls.enabled && cm->sg_filter_ctrls.step_range < 16) return 0; /* reference-based ep range */
-    if (cm->use_boundaries_in_rest_search) return 0; /* the device search runs without stripe boundaries */
-    return ((cm->frm_size.frame_width >> 1) & 3) == 0;                               /* 4-sample chunks per plane */
+    return !cm->use_boundaries_in_rest_search; /* the device search runs without stripe boundaries */
 }
 static void lr_controls(PictureControlSet *pcs, SvtGpuLrSearchControls *lc) {
     Av1Common        *cm = pcs->ppcs->av1_cm;
@@ -434,7 +451,26 @@ void restoration_seg_search(int32_t *rst_tmpbuf, Yv12BufferConfig *org_fts, cons
                             Yv12BufferConfig *trial_frame_rst, PictureControlSet *pcs, uint32_t segment_index) {
     static SegSearchFn orig;
     if (!orig) orig = (SegSearchFn)dlsym(RTLD_NEXT, "restoration_seg_search");
-    if (g_on && lr_supported(pcs)) return; /* the device searches the whole frame in rest_finish_search */
+    if (stage_on(4) && lr_supported(pcs)) {
+        /* the device searches the whole frame in rest_finish_search; the one side effect the reference search has on
+         * the encoder's picture is kept: it extends the CDEF output's borders in place from the crop size
+         * (EbRestorationPick.c:1497-1519), which for a picture off the 8-sample grid rewrites the columns / rows
+         * between the crop and the padded size that the reference picture keeps */
+        Av1Common *cm  = pcs->ppcs->av1_cm;
+        const int  pe  = ((cm->wn_filter_ctrls.enabled && cm->wn_filter_ctrls.use_chroma) ||
+                        (cm->sg_filter_ctrls.enabled && cm->sg_filter_ctrls.use_chroma)) ? 2 : 0;
+        svt_block_on_mutex(pcs->rest_search_mutex);
+        for (int plane = 0; plane <= pe; plane++) {
+            if (pcs->rest_extend_flag[plane]) continue;
+            const int is_uv = plane > 0, pw = org_fts->crop_widths[is_uv], ph = org_fts->crop_heights[is_uv];
+            const int pad16 = (pw % 16) ? 16 - (pw % 16) : 0;
+            svt_extend_frame(org_fts->buffers[plane], pw, ph, org_fts->strides[is_uv], RESTORATION_BORDER + 1 + pad16,
+                             RESTORATION_BORDER, cm->use_highbitdepth);
+            pcs->rest_extend_flag[plane] = TRUE;
+        }
+        svt_release_mutex(pcs->rest_search_mutex);
+        return;
+    }
     orig(rst_tmpbuf, org_fts, src, trial_frame_rst, pcs, segment_index);
 }
 
@@ -443,8 +479,8 @@ void restoration_seg_search(int32_t *rst_tmpbuf, Yv12BufferConfig *org_fts, cons
 void rest_finish_search(PictureControlSet *pcs) {
     static FinishFn orig;
     if (!orig) orig = (FinishFn)dlsym(RTLD_NEXT, "rest_finish_search");
-    if (!g_on || !lr_supported(pcs)) {
-        if (g_on) count(1);
+    if (!stage_on(4) || !lr_supported(pcs)) {
+        if (stage_on(4)) count(1);
         return orig(pcs);
     }
     count(0);
@@ -456,7 +492,7 @@ void rest_finish_search(PictureControlSet *pcs) {
     for (int p = 0; p < 3; p++) us[p] = pcs->rst_info[p].restoration_unit_size;
     if (!c->lr || memcmp(us, c->lr_units, sizeof us)) {
         if (c->lr) svtgpu_lr_state_destroy(c->lr);
-        GPU(svtgpu_lr_state_create(g_ctx, c->w, c->h, us, &c->lr));
+        GPU(svtgpu_lr_state_create(g_ctx, c->cw, c->ch, us, &c->lr)); /* the crop size */
         memcpy(c->lr_units, us, sizeof us);
     }
     /* the CDEF output the search reads (EbRestProcess.c:562) and the source (:563) */
@@ -517,7 +553,7 @@ void svt_av1_loop_restoration_filter_frame(int32_t *rst_tmpbuf, Yv12BufferConfig
     static LrFrameFn orig;
     if (!orig) orig = (LrFrameFn)dlsym(RTLD_NEXT, "svt_av1_loop_restoration_filter_frame");
     PictureControlSet *pcs = cm->child_pcs;
-    Ctx               *c   = g_on && frame_supported(pcs) ? ctx_of(pcs) : NULL;
+    Ctx               *c   = stage_on(4) && frame_supported(pcs) ? ctx_of(pcs) : NULL;
     if (!c || !c->lr_searched) {
         if (g_on) count(1);
         return orig(rst_tmpbuf, frame, cm, optimized_lr);

@@ -246,7 +246,14 @@ static void gen_frames(const char *dir) {
         {72, 40, 10, 1, 0, 3, 0, 0, 20, 20, 0, 0, 0},  /* luma off: the reference skips chroma too */
         {160, 96, 10, 1, 1, 3, 30, 30, 25, 0, 0, 1, 0}, /* chroma-only pass (level search trial) */
         {120, 64, 8, 0, 0, 1, 5, 50, 0, 0, 1, 0, 1},
+        /* pictures off the 8-sample grid (coded size w x h, unpadded w - pad_right x h - pad_bottom, kPad): edges at
+         * or past the unpadded size are not filtered (set_lpf_parameters, EbDeblockingFilter.c:173-178) */
+        {200, 136, 10, 1, 0, 3, 40, 24, 20, 30, 0, 1, 0},
+        {136, 72, 8, 0, 0, 3, 30, 36, 16, 12, 2, 0, 1},
+        {96, 80, 10, 1, 0, 3, 63, 50, 40, 40, 0, 0, 0},
     };
+    /* {pad_right, pad_bottom} of the cases above (0 before the crop cases) */
+    static const int kPad[][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}, {6, 2}, {2, 6}, {4, 4}};
     const int ncase = (int)(sizeof(cases) / sizeof(cases[0]));
     char      path[512];
     snprintf(path, sizeof path, "%s/dlf_frame.bin", dir);
@@ -269,6 +276,8 @@ static void gen_frames(const char *dir) {
         scs->static_config.encoder_bit_depth = (uint32_t)c->bd;
         scs->max_input_luma_width      = (uint16_t)W;
         scs->max_input_luma_height     = (uint16_t)H;
+        scs->max_input_pad_right       = (uint16_t)kPad[ci][0];
+        scs->max_input_pad_bottom      = (uint16_t)kPad[ci][1];
         ppcs->aligned_width            = (uint16_t)W;
         ppcs->aligned_height           = (uint16_t)H;
         FrameHeader       *fh          = &ppcs->frm_hdr;
@@ -357,6 +366,11 @@ static void gen_frames(const char *dir) {
             }
         snprintf(nm, sizeof nm, "c%d_params", ci);
         golden_put1(&g, nm, 'i', (uint32_t)(sizeof(prm) / 4), prm);
+        if (kPad[ci][0] || kPad[ci][1]) {
+            const int32_t pad[2] = {kPad[ci][0], kPad[ci][1]};
+            snprintf(nm, sizeof nm, "c%d_pad", ci);
+            golden_put1(&g, nm, 'i', 2, pad);
+        }
         /* mi grid as SvtGpuLfMi records {bsize, tx_depth, skip, ref_frame0, mode, segment_id, 0, 0} */
         uint8_t *mi = calloc((size_t)G.cap, 8);
         for (int k = 0; k < G.cap; k++) {

@@ -87,7 +87,8 @@ __device__ __forceinline__ SvtGpuLfMi checked_mi(SvtGpuLfMi m, unsigned long lon
 }
 
 __global__ void dlf_edge_records_kernel(const SvtGpuLfMi *__restrict__ mi, int mi_cols, int units_w, int units_h,
-                                        int chroma, int vert, uint32_t *__restrict__ rec, unsigned long long *bad) {
+                                        int chroma, int vert, int crop_w, int crop_h, uint32_t *__restrict__ rec,
+                                        unsigned long long *bad) {
     const int ux = blockIdx.x * blockDim.x + threadIdx.x;
     const int uy = blockIdx.y;
     if (ux >= units_w || uy >= units_h) return;
@@ -98,7 +99,8 @@ __global__ void dlf_edge_records_kernel(const SvtGpuLfMi *__restrict__ mi, int m
     const int coord    = vert ? x : y;
     uint32_t  r        = 0;
     const int lt       = tx_log2(m, vert, chroma);
-    if (coord && !(coord & ((1 << lt) - 1))) { // a transform edge with a block on the other side
+    // an edge at or past the plane's unpadded size is not filtered (set_lpf_parameters, EbDeblockingFilter.c:173-178)
+    if (coord && !(coord & ((1 << lt) - 1)) && x < crop_w && y < crop_h) { // a transform edge with a block beyond it
         const SvtGpuLfMi p = checked_mi(vert ? mi[mi_row * mi_cols + mi_col - (1 << ss)]
                                              : mi[(mi_row - (1 << ss)) * mi_cols + mi_col], bad);
         const int cur_skip = m.skip && m.ref_frame0 > 0;
@@ -508,6 +510,7 @@ struct SvtGpuDlfState {
     SvtGpuLfMi    *d_mi;
     uint32_t      *d_rec[2][2]; // [chroma][dir]
     int32_t        uw[2], uh[2]; // record grid per plane type
+    int32_t        crop_w, crop_h; // the unpadded luma size (svtgpu_dlf_set_crop; default the coded size)
     void          *d_scratch;    // plane copy for in-place apply
     unsigned long long *d_sse;   // trial accumulators [MAX_JOBS][MAX_TRIALS], zero between launches
     unsigned int       *d_arrive; // trial workgroup arrivals, zero between launches
@@ -945,6 +948,7 @@ extern "C" int svtgpu_dlf_state_create(SvtGpuContext *ctx, int32_t width, int32_
     s->height  = height;
     s->mi_cols = width >> 2;
     s->mi_rows = height >> 2;
+    s->crop_w  = width, s->crop_h = height;
     s->uw[0]   = width / 4, s->uh[0] = height / 4;
     s->uw[1]   = width / 8, s->uh[1] = height / 8;
     s->sse_rect[2] = s->out_rect[2] = width, s->sse_rect[3] = s->out_rect[3] = height;
@@ -996,7 +1000,8 @@ int edge_records(SvtGpuDlfState *s, hipStream_t st, unsigned long long *bad) {
     for (int c = 0; c < 2; c++)
         for (int d = 0; d < 2; d++) {
             hipLaunchKernelGGL(dlf_edge_records_kernel, dim3((s->uw[c] + 127) / 128, s->uh[c]), dim3(128), 0, st,
-                               s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->d_rec[c][d], bad);
+                               s->d_mi, s->mi_cols, s->uw[c], s->uh[c], c, d == 0, s->crop_w >> c, s->crop_h >> c,
+                               s->d_rec[c][d], bad);
             HIP_TRY(hipGetLastError());
         }
     s->have_mi = 1;
@@ -1011,6 +1016,14 @@ bool take_bad_mi(SvtGpuDlfState *s) {
     return true;
 }
 } // namespace
+
+extern "C" int svtgpu_dlf_set_crop(SvtGpuDlfState *s, int32_t crop_width, int32_t crop_height) {
+    if (!s || crop_width <= s->width - 8 || crop_width > s->width || crop_height <= s->height - 8 ||
+        crop_height > s->height)
+        return SVTGPU_ERR_INVALID_ARG; // the coded size is the crop rounded up to 8
+    s->crop_w = crop_width, s->crop_h = crop_height;
+    return SVTGPU_OK;
+}
 
 extern "C" int svtgpu_dlf_set_mode_info(SvtGpuDlfState *s, const SvtGpuLfMi *mi, void *stream) {
     if (!s || !mi) return SVTGPU_ERR_INVALID_ARG;

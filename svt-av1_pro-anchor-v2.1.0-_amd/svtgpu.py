@@ -364,6 +364,7 @@ _SIGS = {
     "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
     "svtgpu_tile_plan_sb": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
+    "svtgpu_dlf_set_crop": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_lr_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
 }
@@ -738,6 +739,10 @@ class DlfState:
 
     def filter_to(self, src, out, params, plane_start=0, plane_end=3, stream=None):
         check(lib().svtgpu_dlf_frame_to(self.h, src.h, out.h, ctypes.byref(params), plane_start, plane_end, stream))
+
+    def set_crop(self, crop_width, crop_height):
+        """svtgpu_dlf_set_crop: no edge at or past the unpadded size is filtered (next set_mode_info on)."""
+        check(lib().svtgpu_dlf_set_crop(self.h, crop_width, crop_height))
 
     def set_tile(self, sse_rect=None, out_rect=None, comm=None):
         """svtgpu_dlf_set_tile: trial SSEs over sse_rect summed over `comm`; the filter writes out_rect."""

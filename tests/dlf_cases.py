@@ -20,9 +20,12 @@ def frame_cases():
                           ref_deltas=prm[13:21] if mrd else None, mode_deltas=prm[21:23] if mrd else None,
                           seg_enabled=en if seg else None, seg_data=data if seg else None)
         dt = np.uint16 if bd > 8 else np.uint8
+        pad = [int(x) for x in g["c%d_pad" % ci]] if ("c%d_pad" % ci) in g else [0, 0]
         yield {
-            "name": "c%d_%dx%d_bd%d%s" % (ci, w, h, bd, "_p16" if pipe16 else ""),
+            "name": "c%d_%dx%d_bd%d%s%s" % (ci, w, h, bd, "_p16" if pipe16 else "",
+                                           "_crop%dx%d" % (w - pad[0], h - pad[1]) if any(pad) else ""),
             "w": int(w), "h": int(h), "bd": int(bd), "plane_start": int(ps), "plane_end": int(pe),
+            "crop": (int(w - pad[0]), int(h - pad[1])),
             "params": p,
             "mi": np.ascontiguousarray(g["c%d_mi" % ci]).view(LF_MI_DTYPE).reshape(g["c%d_mi" % ci].shape[:2]),
             "inp": [g["c%d_in%d" % (ci, k)].astype(dt) for k in range(3)],

@@ -59,11 +59,13 @@ def test_encoder_bitstream_identical_with_filter_rtcd(tmp_path, geom):
 @needs_exe
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("geom", [(320, 192, 5, 2, 40), (256, 144, 3, 2, 20), (384, 256, 4, 1, 32)])
+@pytest.mark.parametrize("geom", [(320, 192, 5, 2, 40), (256, 144, 3, 2, 20), (384, 256, 4, 1, 32),
+                                  (250, 138, 3, 2, 40)])
 def test_encoder_bitstream_identical_with_frame_hooks(tmp_path, geom):
     """The encoder's DLF / CDEF / LR process bodies calling libsvtgpu's frame-level API (level searches, strength
     pick, restoration search + RD finish, the three frame filters on the device) write the same bitstream as the
-    encoder as built; every hooked call was served by the device path (no fallback)."""
+    encoder as built; every hooked call was served by the device path (no fallback).  250 x 138: a picture off the
+    8-sample grid (the encoder pads it to 256 x 144; loop restoration covers the 250 x 138 crop, chroma 125 x 69)."""
     cpu, gpu = str(tmp_path / "cpu.obu"), str(tmp_path / "frame.obu")
     ic = _encode("cpu", cpu, *geom)
     ig = _encode("frame", gpu, *geom)

@@ -84,11 +84,11 @@ def test_dlf_frame_golden():
     import dlf_cases as dc
     n = 0
     for c in dc.frame_cases():
-        got = oracle.dlf_frame(c["inp"], c["bd"], c["mi"], c["params"], c["plane_start"], c["plane_end"])
+        got = oracle.dlf_frame(c["inp"], c["bd"], c["mi"], c["params"], c["plane_start"], c["plane_end"], c["crop"])
         for p in range(3):
             assert np.array_equal(got[p], c["out"][p]), (c["name"], p)
         n += 1
-    assert n >= 8
+    assert n >= 11
 
 
 # ---------------------------------------------------------------- MD distortion (gen_golden_md.c)
