@@ -376,7 +376,8 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 // pairs.  Fixed lane mappings (no runtime divisions): staging in 18 groups of 4 pixels per row, the horizontal
 // pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
 // ---------------------------------------------------------------------------------------------
-__device__ inline uint32_t pack2(int lo, int hi) { return (uint32_t)(lo & 0xFFFF) | ((uint32_t)hi << 16); }
+// the low halves of lo and hi as one packed int16 pair: one v_perm_b32 (the and + shift-or form took two VALU ops)
+__device__ inline uint32_t pack2(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
 
 // ---------------------------------------------------------------------------------------------
 // self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
@@ -1757,7 +1758,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 int row, col;
                 chunk_at(kk, row, col);
                 const size_t fo = (size_t)(ur.v_start + it.y0 + row) * P.fstride + ur.h_start + 4 * col;
-                const uint2  a0 = *(const uint2 *)(f0 + fo), a1 = *(const uint2 *)(f1 + fo);
+                // an ep without one of the filters (eps 10-15) reads only the other plane (r0 / r1 uniform)
+                const uint2  a0 = r0 ? *(const uint2 *)(f0 + fo) : make_uint2(0u, 0u);
+                const uint2  a1 = r1 ? *(const uint2 *)(f1 + fo) : make_uint2(0u, 0u);
                 g[kk][0] = a0.x, g[kk][1] = a0.y, g[kk][2] = a1.x, g[kk][3] = a1.y;
                 advance();
             }
