@@ -158,6 +158,10 @@ def parse():
                     help="pinned: the reference-pinned pipeline case of this size when there is one (else synth); "
                          "synth: the float generator (synth.frame_pair)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
+    ap.add_argument("--lr-serial", action="store_true",
+                    help="measurement: every LR search runs its Wiener chain after its self-guided chain on one stream, "
+                         "so each search kernel has the device to itself (the condition of the roofline's isolated "
+                         "phase; rocprofv3 of a --frames-in-flight 1 --lr-serial run reproduces its durations)")
     ap.add_argument("--lr-levels", default="1,1", metavar="WN,SG",
                     help="diagnostic only (sensitivity runs; the headline is 1,1): the Wiener / self-guided search levels")
     ap.add_argument("--stages", default="all", choices=("all", "cdef", "md"),
@@ -849,11 +853,14 @@ def main():
         if errors:
             raise errors[0]
 
+    if a.lr_serial:
+        for s_ in slots:
+            s_.lr.profile([], serial=True)
     run_all(a.warmup, False)
     svtgpu.transfer_bytes(reset=True)
     # LR search kernel classes timed on the device clock over the timed steps (first WG start -> last WG end
     # of every launch, accumulated on the device and read once after the timed region) -- slot 0's searches
-    lr.profile(not a.no_kernel_timing)
+    lr.profile(not a.no_kernel_timing, serial=a.lr_serial)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -925,7 +932,10 @@ def main():
     if F > 1:
         s0 = slots[0]
         s0.ev = []
-        lr.profile(not a.no_kernel_timing, events=True)  # the roofline's launch spans: HIP events (rocprofv3's span)
+        # the roofline's launch spans: HIP events around each launch (rocprofv3's span), the two LR chains one after
+        # the other so that each kernel's duration is its own (beside the other chain, a resident descent's duration
+        # is mostly its wait for the CUs the other chain's descent holds)
+        lr.profile(not a.no_kernel_timing, events=True, serial=True)
         iso_steps = max(10, min(a.steps, 40))
         torch.cuda.synchronize()
         for _ in range(iso_steps):
@@ -937,8 +947,9 @@ def main():
         iso = dict(steps=iso_steps, frame_ms=float(np.mean([es[0].elapsed_time(es[5]) for es in s0.ev])),
                    kernels=kernel_table(float(iso_ms[1]), float(iso_ms[4]), lr_classes(iso_tot), bool(iso_tot)))
     roof = roofline_of(iso["kernels"] if iso else kernels_f, bd, a.pmc_json)
-    roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run; the PMC counters' "
-                         "condition)" % iso["steps"]) if iso else "one frame in flight (the main run)"
+    roof["condition"] = ("one frame in flight (slot 0 alone, %d timed steps after the main run, the LR search's two "
+                         "chains one after the other; the PMC counters' condition)" % iso["steps"]) if iso else \
+        "one frame in flight (the main run%s)" % (", LR chains serial" if a.lr_serial else "")
     if iso:
         cont = roofline_of(kernels_f, bd, a.pmc_json)
         roof["contended"] = {"frames_in_flight": F, "kernel": cont["kernel"], "avg_launch_ms": cont["avg_launch_ms"],

@@ -896,7 +896,9 @@ typedef struct SvtGpuLrProfile {
 } SvtGpuLrProfile;
 /* enable != 0 turns timing of the following searches on (0 off): a bit mask of the classes to time (bit c =
  * class c; -1 = all); bit 6 also brackets each timed launch with HIP events (ms_events: the span rocprofv3 reports;
- * events between launches can change how the two LR chains interleave, so they are a separate, opt-in bit).  `totals` (nullable) first receives the sums over the searches timed since the previous read
+ * events between launches can change how the two LR chains interleave, so they are a separate, opt-in bit); bit 7 runs
+ * the Wiener chain on the caller's stream after the self-guided one instead of beside it, so every search kernel has the
+ * device to itself and its duration is its own (measurement only: slower searches).  `totals` (nullable) first receives the sums over the searches timed since the previous read
  * (untimed classes read 0), which are then reset; reading synchronizes the device.  The timings accumulate on the
  * device: a timed search adds one small launch and no copies or host synchronization. */
 int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *totals);

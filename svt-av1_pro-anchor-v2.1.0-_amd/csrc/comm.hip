@@ -203,7 +203,11 @@ extern "C" int32_t svtgpu_comm_failed(const SvtGpuComm *c) { return c && c->fail
 // (any stream: the caller's waits reach the collective through stream order or events).  No communicator, a host
 // transport (its sums are synchronous) or nothing outstanding: the runtime's own wait.
 int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
-    if (!c || c->is_host || !prune(c)) {
+    static const bool plain = [] { // SVTGPU_COMM_WAIT=sync (diagnostic A/B): an unbounded stream synchronize
+        const char *e = std::getenv("SVTGPU_COMM_WAIT");
+        return e && !std::strcmp(e, "sync");
+    }();
+    if (!c || c->is_host || plain || !prune(c)) {
         HIP_TRY(hipStreamSynchronize(st));
         return SVTGPU_OK;
     }

@@ -2142,6 +2142,7 @@ struct LrProfiler {
     bool                ok   = false;
     int32_t             mask = 63; // classes timed (bit c)
     bool                events = false; // bit 6 of the enable mask: HIP events around the timed launches too
+    bool                serial = false; // bit 7: the Wiener chain on the caller's stream -- every kernel runs alone
     LrProfiler() {
         ok = hipMalloc(&d_clk, 16 * PROF_NL * PROF_SP) == hipSuccess && hipMalloc(&d_px, 24 * PROF_SP) == hipSuccess &&
              hipMalloc(&d_acc, 8 * NCLS) == hipSuccess && hipMemset(d_clk, 0xFF, 8 * PROF_NL * PROF_SP) == hipSuccess &&
@@ -2746,9 +2747,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
     }
-    hipStream_t sw = s->wst;
-    HIP_TRY(hipEventRecord(s->ev_fork, st));
-    HIP_TRY(hipStreamWaitEvent(sw, s->ev_fork, 0));
+    // measurement (svtgpu_lr_profile bit 7): both chains on the caller's stream, so a kernel's duration is its own,
+    // not its share of the CUs beside the other chain's kernels
+    const bool  serial = prof && prof->serial;
+    hipStream_t sw     = serial ? st : s->wst;
+    if (!serial) {
+        HIP_TRY(hipEventRecord(s->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(sw, s->ev_fork, 0));
+    }
     for (int p = 0; p < nplanes; p++) {
         const PlanePlan &q = pp[p];
         if (!q.wn) continue;
@@ -2813,8 +2819,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         });
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipEventRecord(s->ev_join, sw)); // the Wiener chain joins the caller's stream
-    HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
+    if (!serial) {
+        HIP_TRY(hipEventRecord(s->ev_join, sw)); // the Wiener chain joins the caller's stream
+        HIP_TRY(hipStreamWaitEvent(st, s->ev_join, 0));
+    }
     if (prof)
         if (int rc = prof->finish(st)) return rc; // fold the launch timings on the device, no read-back
     Descent        *hw = (Descent *)hp(h_wds);
@@ -2976,6 +2984,7 @@ extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfi
     if (enable) {
         pr->mask   = enable < 0 ? 63 : enable & 63;
         pr->events = enable > 0 && (enable & 64);
+        pr->serial = enable > 0 && (enable & 128);
     } else if (pr) {
         delete pr;
         s->prof = nullptr;

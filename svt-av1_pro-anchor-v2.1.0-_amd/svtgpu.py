@@ -902,7 +902,7 @@ class LrState:
 
     PROFILE_CLASSES = ("stats", "sgr_filters", "wiener_trials", "projection", "other", "sgr_moments")
 
-    def profile(self, enable=True, events=False):
+    def profile(self, enable=True, events=False, serial=False):
         """svtgpu_lr_profile: device-clock timing of the searches (enable: True = every class, a class name or a
         list of names = those classes, False = off).  Returns the per-class {launches, ms (device clock), ms_events
         (HIP events around each launch), bytes} totals of the
@@ -917,6 +917,8 @@ class LrState:
             mask = sum(1 << self.PROFILE_CLASSES.index(c) for c in names)
         if mask and events:
             mask = (63 if mask < 0 else mask) | 64
+        if serial:  # both LR chains on one stream: each kernel's duration is its own (measurement)
+            mask = (63 if mask < 0 else mask) | 128
         raw = np.zeros(1, LR_PROFILE_DTYPE)
         check(lib().svtgpu_lr_profile(self.h, mask, ptr(raw)))
         out = {c: {"launches": int(raw["launches"][0][i]), "ms": float(raw["ms"][0][i]),

@@ -267,3 +267,24 @@ def test_wiener_stats_mfma_vs_reference(ctx, case):
     else:
         np.testing.assert_array_equal(M, g["wn_stats_M"], err_msg=case)
         np.testing.assert_array_equal(H, g["wn_stats_H"], err_msg=case)
+
+
+def test_lr_search_serial_measurement_mode_same_records(ctx):
+    """svtgpu_lr_profile bit 7 (the roofline's isolated measurement: both LR chains on the caller's stream) changes
+    only where the Wiener chain runs, never a result: records, frame types and picked units equal the default search."""
+    w, h, bd, usize = 640, 360, 10, 64
+    src, rec = _crop_pair(w, h, bd, seed=0x5EED0900)
+    ctrls = oracle.lr_controls(1, 1, rdmult=7000, switchable=(300, 700, 900), wiener=(250, 800), sgrproj=(250, 900))
+    unit_size = [usize, usize >> 1, usize >> 1]
+    _, _, ft0, recs0 = _gpu_search(ctx, rec, src, bd, unit_size, ctrls)
+    R, S = svtgpu.Frame(ctx, w, h, bd), svtgpu.Frame(ctx, w, h, bd)
+    R.upload(rec)
+    S.upload(src)
+    st = svtgpu.LrState(ctx, w, h, unit_size)
+    st.profile(True, events=True, serial=True)
+    ft1, recs1 = st.search(R, S, ctrls, records=True)
+    prof = st.profile(False)
+    assert prof["searches"] == 1 and prof["projection"]["launches"] > 0 and prof["projection"]["ms_events"] > 0
+    assert ft1 == ft0
+    for p in range(3):
+        np.testing.assert_array_equal(recs1[p], recs0[p])
