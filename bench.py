@@ -131,7 +131,7 @@ def parse():
     ap.add_argument("--cdef-level", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no device-clock timing inside the LR search")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04", "pmc", "kernels.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05", "pmc", "kernels.json"),
                     help="per-launch traffic / VALU counters from scripts/pmc_traffic.sh (PMC passes cannot run inside "
                          "the bench)")
     ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
@@ -926,7 +926,7 @@ def main():
         return kernels
     kernels_f = kernel_table(search_ms, md_ms, lr_cls, bool(lr_tot))
     # The roofline's durations come from the condition its PMC counters were collected in: one frame in flight
-    # (scripts/pmc_r04.sh runs the bench at F = 1).  With F > 1 slot 0 runs alone for a short timed phase after the
+    # (scripts/r5/pmc_r05.sh runs the bench at F = 1 with the LR chains serial).  With F > 1 slot 0 runs alone for a short timed phase after the
     # main one; the contended figures of the F-frame run are reported beside it.
     iso = None
     if F > 1:
