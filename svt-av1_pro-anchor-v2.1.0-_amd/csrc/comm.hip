@@ -17,11 +17,12 @@
 //
 // Every exchange is bounded (round 5): a rank whose peer never arrives (a skipped exchange, a peer that failed before
 // its all-reduce) must not hang the node.  The device-side collectives are enqueued without a host wait (the CDEF
-// tables before the pick, the DLF trial SSEs between a trial and its step kernel), so each one records an event in a
-// small ring, and every host wait of a frame-level call that may sit behind a collective goes through
-// svtgpu_comm_wait: it polls against the communicator's deadline and, when it expires while a collective is still
-// outstanding, names that exchange (what, frame slot, sequence number), aborts the RCCL communicator (ncclCommAbort
-// ends the pending collectives on this rank) and returns SVTGPU_ERR_HIP; the communicator then fails every later call.
+// tables before the pick, the DLF trial SSEs between a trial and its step kernel), so each one is noted in a small ring
+// (what, sequence number, stream -- no event: a marker packet per exchange lengthened the tiled rank's latency chains),
+// and every host wait of a frame-level call that may sit behind a collective goes through svtgpu_comm_wait: one event
+// on the waited stream, polled against the communicator's deadline; when it expires with exchanges of that stream
+// outstanding it names the oldest (what, frame slot, sequence number), aborts the RCCL communicator (ncclCommAbort ends
+// the pending collectives on this rank) and returns SVTGPU_ERR_HIP; the communicator then fails every later call.
 // A host transport gets the deadline from svtgpu_comm_timeout_ms and reports an expired wait by returning non-zero.
 #include <rccl/rccl.h>
 
@@ -35,7 +36,7 @@
 namespace {
 constexpr int XCH_RING = 32;
 struct XchRecord {
-    hipEvent_t  ev   = nullptr;
+    hipStream_t st   = nullptr; // the stream the collective was enqueued on
     const char *what = nullptr;
     uint64_t    seq  = 0;
     size_t      words = 0;
@@ -108,17 +109,11 @@ int comm_timeout(SvtGpuComm *c, const XchRecord &r, long long waited_ms) {
     c->nccl = nullptr;
     return comm_failed(c);
 }
-// drop the ring's completed collectives; the oldest outstanding one, or null
-const XchRecord *prune(SvtGpuComm *c) {
+// the oldest exchange enqueued on `st` not yet seen complete, or null
+const XchRecord *outstanding(SvtGpuComm *c, hipStream_t st) {
     const XchRecord *oldest = nullptr;
-    for (auto &r : c->ring) {
-        if (!r.live) continue;
-        if (hipEventQuery(r.ev) == hipSuccess) {
-            r.live = false;
-            continue;
-        }
-        if (!oldest || r.seq < oldest->seq) oldest = &r;
-    }
+    for (auto &r : c->ring)
+        if (r.live && r.st == st && (!oldest || r.seq < oldest->seq)) oldest = &r;
     return oldest;
 }
 int grow_dev(SvtGpuComm *c, size_t n) {
@@ -151,13 +146,11 @@ extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t ra
     auto *c   = new SvtGpuComm();
     c->nranks = nranks, c->rank = rank, c->nccl = comm, c->device = ctx->device;
     c->timeout_ms = default_timeout_ms();
-    for (auto &r : c->ring)
-        if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
-            svtgpu_comm_destroy(c);
-            svtgpu_set_last_hip_error(hipErrorOutOfMemory, "comm events", __FILE__, __LINE__);
-            return SVTGPU_ERR_HIP;
-        }
-    HIP_TRY(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming));
+    if (hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess) {
+        svtgpu_comm_destroy(c);
+        svtgpu_set_last_hip_error(hipErrorOutOfMemory, "comm event", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
     *out      = c;
     return SVTGPU_OK;
 }
@@ -174,8 +167,6 @@ extern "C" int svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGp
 extern "C" void svtgpu_comm_destroy(SvtGpuComm *c) {
     if (!c) return;
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
-    for (auto &r : c->ring)
-        if (r.ev) (void)hipEventDestroy(r.ev);
     if (c->wait_ev) (void)hipEventDestroy(c->wait_ev);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->dev) (void)hipFree(c->dev);
@@ -207,7 +198,8 @@ int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
         const char *e = std::getenv("SVTGPU_COMM_WAIT");
         return e && !std::strcmp(e, "sync");
     }();
-    if (!c || c->is_host || plain || !prune(c)) {
+    const XchRecord *r = c && !c->is_host && !plain ? outstanding(c, st) : nullptr;
+    if (!r) {
         HIP_TRY(hipStreamSynchronize(st));
         return SVTGPU_OK;
     }
@@ -219,15 +211,12 @@ int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
         if (q != hipErrorNotReady) HIP_TRY(q);
         if ((it & 63) != 63) continue;
         const auto waited = std::chrono::steady_clock::now() - t0;
-        if (waited > std::chrono::milliseconds(c->timeout_ms)) {
-            if (const XchRecord *r = prune(c))
-                return comm_timeout(c, *r, std::chrono::duration_cast<std::chrono::milliseconds>(waited).count());
-            HIP_TRY(hipEventSynchronize(c->wait_ev)); // every exchange done: an ordinary (long) wait
-            break;
-        }
+        if (waited > std::chrono::milliseconds(c->timeout_ms))
+            return comm_timeout(c, *r, std::chrono::duration_cast<std::chrono::milliseconds>(waited).count());
         std::this_thread::yield();
     }
-    (void)prune(c);
+    for (auto &x : c->ring) // everything enqueued on `st` before the event has completed
+        if (x.live && x.st == st) x.live = false;
     return SVTGPU_OK;
 }
 
@@ -282,12 +271,11 @@ int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStrea
         c->failed = true;
         return comm_failed(c);
     }
-    // the ring slot of this exchange: an outstanding collective 32 exchanges back is waited for (bounded) first
+    // the ring slot of this exchange: an exchange 32 back not yet seen complete is waited for (bounded) first
     XchRecord *slot = &c->ring[seq % XCH_RING];
-    if (slot->live && hipEventQuery(slot->ev) != hipSuccess)
-        if (int rc = svtgpu_comm_wait(c, st)) return rc;
-    HIP_TRY(hipEventRecord(slot->ev, st));
-    slot->what = what, slot->seq = seq, slot->words = n, slot->live = true;
+    if (slot->live)
+        if (int rc = svtgpu_comm_wait(c, slot->st)) return rc;
+    slot->st = st, slot->what = what, slot->seq = seq, slot->words = n, slot->live = true;
     if (!on_device) {
         HIP_TRY(hipMemcpyAsync(buf, c->dev, n * 8, hipMemcpyDeviceToHost, st));
         return svtgpu_comm_wait(c, st);
