@@ -170,8 +170,10 @@ int     svtgpu_comm_set_timeout(SvtGpuComm *c, int32_t timeout_ms);
 int32_t svtgpu_comm_timeout_ms(const SvtGpuComm *c);
 int     svtgpu_comm_set_slot(SvtGpuComm *c, int32_t frame_slot); /* the frame slot named in a timeout's message */
 int32_t svtgpu_comm_failed(const SvtGpuComm *c);
-/* host wait for `stream`, bounded by the deadline while one of the communicator's device-side exchanges (enqueued
- * without a host wait: svtgpu_comm_allreduce_u64 on device memory) is outstanding */
+/* host wait for `stream`, bounded by the deadline when one of the communicator's device-side exchanges (enqueued
+ * without a host wait: svtgpu_comm_allreduce_u64 on device memory) was enqueued on `stream` since its last completed
+ * wait -- the whole wait is then bounded (per-exchange completion markers lengthened a tiled rank's latency chains
+ * by 7 %), so work queued behind an exchange counts against the deadline too */
 int     svtgpu_comm_sync(SvtGpuComm *c, void *stream);
 /* the number of per-block RTCD shim calls this process made (each runs on the process-wide default context): evidence
  * that an encoder with the shims installed really ran its kernels on the device */

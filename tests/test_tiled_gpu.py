@@ -199,7 +199,7 @@ def test_rccl_exchange_deadline_aborts():
     """The RCCL branch of the exchange deadline (one rank): a collective held behind a stalled stream is still
     outstanding when the deadline expires, so the bounded wait names it, aborts the communicator (ncclCommAbort) and
     fails every later call; the stream itself drains (the stall ends on its own clock).  A deadline that expires with
-    no collective outstanding is an ordinary wait (no false timeout)."""
+    no exchange enqueued on the stream since its last completed wait is an ordinary wait (no false timeout)."""
     import time
     import torch
     import svtgpu
@@ -210,8 +210,10 @@ def test_rccl_exchange_deadline_aborts():
     s = torch.cuda.Stream()
     t = torch.arange(64, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
-    # no collective outstanding: a stall longer than the deadline is waited for, not reported
+    # no exchange outstanding (the last one completed at a wait): a stall longer than the deadline is waited for,
+    # not reported
     comm.allreduce_device(t.data_ptr(), t.numel(), stream=s.cuda_stream)
+    comm.sync(s.cuda_stream)
     ctx.debug_stall(900, s.cuda_stream)
     time.sleep(0.05)
     comm.sync(s.cuda_stream)
