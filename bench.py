@@ -158,6 +158,9 @@ def parse():
                     help="pinned: the reference-pinned pipeline case of this size when there is one (else synth); "
                          "synth: the float generator (synth.frame_pair)")
     ap.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py spawns its ranks")
+    ap.add_argument("--md-main", action="store_true", default=None,
+                    help="run the MD batch on the frame's main stream (after the CDEF stage) instead of its own: one "
+                         "hardware queue less per frame in flight")
     ap.add_argument("--lr-serial", action="store_true",
                     help="measurement: every LR search runs its Wiener chain after its self-guided chain on one stream, "
                          "so each search kernel has the device to itself (the condition of the roofline's isolated "
@@ -702,7 +705,9 @@ def main():
             md_range: the MD batch's superblock range (default: all)."""
             self.k = k
             self.stream = torch.cuda.Stream()     # the library launches on it, torch events time it
-            self.md_stream = torch.cuda.Stream()  # the MD batch (memory-bound) runs beside the VALU-bound LR search
+            # the MD batch (memory-bound) runs beside the VALU-bound LR search on its own stream, or (--md-main) on the
+            # main stream: one hardware queue less per frame in flight
+            self.md_stream = self.stream if a.md_main else torch.cuda.Stream()
             sp = self.stream.cuda_stream
             self.src, self.rec = frame_inputs(k)
             self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
