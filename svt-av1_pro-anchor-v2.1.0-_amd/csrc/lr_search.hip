@@ -54,7 +54,8 @@ const int     kHostSgrS1[16] = {3236, 2158, 1618, 1438, 1295, 1177, 1079, 996, 9
 
 struct PlaneArgs {
     const void *dgd, *src;
-    int16_t    *flt; // [ne][2][H][fstride] self-guided outputs
+    int16_t    *flt; // [ne][2][H][fstride] self-guided outputs minus the scaled source, g = flt - (dgd << 4) (int16)
+    int16_t    *dxp; // [H][fstride] dgd - src (int16; planes with a self-guided search, else null)
     int32_t     dstride, sstride, W, H, bd, fstride;
     int32_t     unit_base, pair_base, ne; // SGR pair of (unit, k) = pair_base + (unit - unit_base) * ne + k
     int32_t     eps[16];
@@ -129,6 +130,9 @@ __device__ inline void load4s(const int16_t *p, int *v) {
     v[0] = (int)(int16_t)(w.x & 0xFFFF), v[1] = w.x >> 16, v[2] = (int)(int16_t)(w.y & 0xFFFF), v[3] = w.y >> 16;
 }
 
+// the low halves of lo and hi as one packed int16 pair: one v_perm_b32 (the and + shift-or form took two VALU ops)
+__device__ inline uint32_t pack2(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
+
 // ---------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsigned long long *sum,
@@ -163,6 +167,14 @@ __global__ __launch_bounds__(256) void unit_sums_kernel(const SearchArgs A, unsi
             const int e = dv[k][j] - sv[k][j];
             ps += (uint32_t)dv[k][j];
             pe += (uint32_t)(e * e);
+        }
+    if (P.dxp) // the dx plane the resident self-guided search reads (one 8-B store per chunk; rows padded to 64)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int r = (threadIdx.x >> 4) + 16 * k, c = 4 * (threadIdx.x & 15);
+            if (r < t.h && c < t.w)
+                *(uint2 *)(P.dxp + (size_t)(t.y0 + r) * P.fstride + t.x0 + c) =
+                    make_uint2(pack2(dv[k][0] - sv[k][0], dv[k][1] - sv[k][1]), pack2(dv[k][2] - sv[k][2], dv[k][3] - sv[k][3]));
         }
     const unsigned long long tsum = wave_sum_u32_wide(ps), tsse = wave_sum_u32_wide(pe);
     if ((threadIdx.x & 63) == WAVE_LAST) {
@@ -376,13 +388,11 @@ __global__ void reduce_parts_kernel(const long long *part, const int32_t *unit_t
 // pairs.  Fixed lane mappings (no runtime divisions): staging in 18 groups of 4 pixels per row, the horizontal
 // pass as 32 column pairs x 8 rows per step, the vertical pass as 64 columns x 4 row pairs per step.
 // ---------------------------------------------------------------------------------------------
-// the low halves of lo and hi as one packed int16 pair: one v_perm_b32 (the and + shift-or form took two VALU ops)
-__device__ inline uint32_t pack2(int lo, int hi) { return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u); }
 
 // ---------------------------------------------------------------------------------------------
 // self-guided filters of every searched ep of a tile.  The 3x3 and 5x5 box sums do not depend on ep and stay in
-// registers; per ep the A/B maps (packed B << 9 | A) go to LDS and the filters to HBM (the projection moments are
-// the resident search, sgr_res_kernel).
+// registers; per ep the A/B maps (packed B << 9 | A) go to LDS and the filters to HBM as g = flt - (dgd << 4), the
+// projection's operand (int16: |g| < 2^15), so the resident search (sgr_res_kernel) needs no dgd to form it.
 // ---------------------------------------------------------------------------------------------
 constexpr int SG_V = 70, SG_B = 66, SG_NT = 1024, SG_NQ = (SG_B * SG_B + SG_NT - 1) / SG_NT;
 constexpr int SG_NQ2 = ((SG_B + 1) / 2 * SG_B + SG_NT - 1) / SG_NT; // r = 2 map positions per lane (odd rows only)
@@ -541,13 +551,14 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                         const int c5 = up.s - up.c + dn.s - dn.c, a5 = up.sa - up.ca + dn.sa - dn.ca;
                         const int aa = a6 * 6 + a5 * 5, bb = ((c6 - a6) >> 9) * 6 + ((c5 - a5) >> 9) * 5;
                         f0g[fo + (size_t)k * P.fstride] =
-                            (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9);
+                            (int16_t)((((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9) - (pix[k] << 4));
                     }
                     if (k + 1 < nk) { // odd row fy0 + k + 1: its own row, weights 6 (centre) and 5 (sides)
                         const int a6 = dn.ca, a5 = dn.sa - dn.ca;
                         const int aa = a6 * 6 + a5 * 5, bb = ((dn.c - a6) >> 9) * 6 + ((dn.s - dn.c - a5) >> 9) * 5;
                         f0g[fo + (size_t)(k + 1) * P.fstride] =
-                            (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k + 1]) + bb + (1 << 7)) >> 8);
+                            (int16_t)((((int)__umul24((uint32_t)aa, (uint32_t)pix[k + 1]) + bb + (1 << 7)) >> 8) -
+                                      (pix[k + 1] << 4));
                     }
                     up = dn;
                 }
@@ -563,7 +574,7 @@ __global__ __launch_bounds__(SG_NT) void sgr_flt_kernel(const SearchArgs A, unsi
                     const int c3 = pv.s - pv.c + nx.s - nx.c, a3 = pv.sa - pv.ca + nx.sa - nx.ca;
                     const int aa = a4 * 4 + a3 * 3, bb = ((c4 - a4) >> 9) * 4 + ((c3 - a3) >> 9) * 3;
                     f1g[fo + (size_t)k * P.fstride] =
-                        (int16_t)(((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9);
+                        (int16_t)((((int)__umul24((uint32_t)aa, (uint32_t)pix[k]) + bb + (1 << 8)) >> 9) - (pix[k] << 4));
                     pv = cu, cu = nx;
                 }
             }
@@ -611,7 +622,7 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
                 dv[j] = j < nv ? (int)d[(size_t)y * P.dstride + x + j] : 0,
                 sv[j] = j < nv ? (int)s[(size_t)y * P.sstride + x + j] : 0;
         }
-        if (r0 > 0) load4s(f0 + o, g0); // the filter planes' rows are padded to 64 samples
+        if (r0 > 0) load4s(f0 + o, g0); // g = flt - u planes; rows padded to 64 samples
         if (r1 > 0) load4s(f1 + o, g1);
         uint32_t e2 = 0; // 4 squared errors of at most 1023^2
 #pragma unroll
@@ -619,8 +630,8 @@ __global__ __launch_bounds__(256) void sgr_sse_kernel(const SearchArgs A, const 
             if (j >= nv) break;
             const int u = dv[j] << 4;
             int       v = u << 7;
-            if (r0 > 0) v += xq0 * (g0[j] - u);
-            if (r1 > 0) v += xq1 * (g1[j] - u);
+            if (r0 > 0) v += xq0 * g0[j];
+            if (r1 > 0) v += xq1 * g1[j];
             const int16_t w  = (int16_t)((v + (1 << 10)) >> 11);
             const int     ov = min(max((int)w, 0), maxv);
             e2 += (uint32_t)((ov - sv[j]) * (ov - sv[j]));
@@ -1765,11 +1776,12 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 advance();
             }
         }
-        // 2. the CDEF output and the source in groups of SR_LB chunks (the eps of a unit read them through one L2):
-        //    g formed in place, (x - src) to LDS, the moments
+        // 2. dx = dgd - src (the plane unit_sums_kernel writes; the eps of a unit read it through one L2) in groups of
+        //    SR_LB chunks: the moments, and the (x - src) pairs to LDS.  g (1.) already holds flt - (dgd << 4), so a
+        //    chunk needs two registers here instead of four for the CDEF output and the source: half the round trips
         crow = pl / cw, ccol = pl - crow * cw;
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
-        constexpr int LB2 = 2; // chunks per group here: g holds every chunk already
+        constexpr int LB2 = SR_LB;
 #pragma unroll
         for (int kb = 0; kb < SR_KMAX; kb += LB2) {
             if (kb >= K) { // uniform: zeros up to the next multiple of SR_LB (sr_pass reads whole groups)
@@ -1779,46 +1791,31 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                         if (kb + j < SR_KMAX) sr_dx[(kb + j) * SR_PL + pl] = make_uint2(0u, 0u);
                 continue;
             }
-            int2     dv2[LB2], sv2[LB2];
-            uint64_t pm[LB2]; // 16 bits per pixel of the chunk inside the part: all four, fewer in the last column of a
-                              // crop width that is not a multiple of 4, none past the part
+            uint2 xv[LB2];
+            int   nin[LB2]; // the chunk's pixels inside the part: 4, fewer in the last column of a crop width that is
+                            // not a multiple of 4, none past the part
 #pragma unroll
             for (int j = 0; j < LB2; j++) { // the group's loads in flight together
+                xv[j] = make_uint2(0u, 0u), nin[j] = 0;
+                if (kb + j >= SR_KMAX) continue;
                 int row, col;
                 chunk_at(kb + j, row, col);
-                const int nin = kb + j < SR_KMAX && pl + (kb + j) * SR_PL < nch ? min(4, uw - 4 * col) : 0;
-                pm[j]         = nin >= 4 ? ~0ull : (1ull << (16 * nin)) - 1;
+                nin[j]      = pl + (kb + j) * SR_PL < nch ? min(4, uw - 4 * col) : 0;
                 const int y = ur.v_start + it.y0 + row, x = ur.h_start + 4 * col;
-                if constexpr (sizeof(T) == 2) {
-                    dv2[j] = *(const int2 *)(d + (size_t)y * P.dstride + x);
-                    sv2[j] = *(const int2 *)(s + (size_t)y * P.sstride + x);
-                } else {
-                    dv2[j].x = *(const int *)(d + (size_t)y * P.dstride + x), dv2[j].y = 0;
-                    sv2[j].x = *(const int *)(s + (size_t)y * P.sstride + x), sv2[j].y = 0;
-                }
+                xv[j]       = *(const uint2 *)(P.dxp + (size_t)y * P.fstride + x);
                 advance();
             }
 #pragma unroll
             for (int j = 0; j < LB2; j++) {
                 const int kk = kb + j;
                 if (kk >= SR_KMAX) break;
-                int       dv[4], sv[4];
                 // pixels outside the part read as zeros everywhere: g = 0 and (x - src) = 0 add nothing to any sum
-                const uint32_t mlo = (uint32_t)pm[j], mhi = (uint32_t)(pm[j] >> 32);
+                const uint32_t mlo = nin[j] >= 2 ? ~0u : nin[j] == 1 ? 0xFFFFu : 0u;
+                const uint32_t mhi = nin[j] >= 4 ? ~0u : nin[j] == 3 ? 0xFFFFu : 0u;
                 g[kk][0] &= mlo, g[kk][2] &= mlo, g[kk][1] &= mhi, g[kk][3] &= mhi;
-                if constexpr (sizeof(T) == 2) {
-                    dv2[j].x &= mlo, sv2[j].x &= mlo, dv2[j].y &= mhi, sv2[j].y &= mhi;
-                } else {
-                    const uint32_t m8 = __builtin_amdgcn_perm(mhi, mlo, 0x06040200u); // one byte per pixel
-                    dv2[j].x &= m8, sv2[j].x &= m8;
-                }
-                if constexpr (sizeof(T) == 2) {
-                    dv[0] = dv2[j].x & 0xFFFF, dv[1] = (uint32_t)dv2[j].x >> 16, dv[2] = dv2[j].y & 0xFFFF, dv[3] = (uint32_t)dv2[j].y >> 16;
-                    sv[0] = sv2[j].x & 0xFFFF, sv[1] = (uint32_t)sv2[j].x >> 16, sv[2] = sv2[j].y & 0xFFFF, sv[3] = (uint32_t)sv2[j].y >> 16;
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) dv[q] = ((uint32_t)dv2[j].x >> (8 * q)) & 0xFF, sv[q] = ((uint32_t)sv2[j].x >> (8 * q)) & 0xFF;
-                }
+                const uint2    x2 = make_uint2(xv[j].x & mlo, xv[j].y & mhi);
+                const int      dxq[4] = {(int)(int16_t)(x2.x & 0xFFFF), (int)x2.x >> 16, (int)(int16_t)(x2.y & 0xFFFF),
+                                         (int)x2.y >> 16};
                 const uint32_t fw[4] = {__builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x05040100u),
                                         __builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x07060302u),
                                         __builtin_amdgcn_perm(g[kk][3], g[kk][1], 0x05040100u),
@@ -1827,16 +1824,15 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 int      m3 = 0, m4 = 0; // |4 g s| < 2^31
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    // g = (flt0 - u, flt1 - u) on packed 16-bit lanes (|g| < 2^15: the wrapped halves are exact)
-                    const uint32_t gq = pk_sub16(fw[q], __umul24((uint32_t)dv[q], 0x00100010u)) & gmask;
-                    const int      g1 = (int)(int16_t)(gq & 0xFFFF), g2 = (int)gq >> 16, ss = (sv[q] - dv[q]) << 4;
+                    const uint32_t gq = fw[q] & gmask; // (flt0 - u, flt1 - u); an ep's absent filter reads as 0
+                    const int      g1 = (int)(int16_t)(gq & 0xFFFF), g2 = (int)gq >> 16, ss = -(dxq[q] << 4);
                     m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
                     m3 += g1 * ss, m4 += g2 * ss;
                     M2 += (unsigned long long)(long long)(g1 * g2);
                     g[kk][q] = gq;
                 }
                 M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
-                sr_dx[kk * SR_PL + pl] = make_uint2(pack2(dv[0] - sv[0], dv[1] - sv[1]), pack2(dv[2] - sv[2], dv[3] - sv[3]));
+                sr_dx[kk * SR_PL + pl] = x2;
             }
         }
         {
@@ -2491,7 +2487,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         }
         if (q.sg) {
             n_sg += q.n, nt_sg += q.nt, sg_planes++;
-            flt_elems += (size_t)q.ne * 2 * ((W + 63) & ~63) * H;
+            flt_elems += (size_t)(q.ne * 2 + 1) * ((W + 63) & ~63) * H; // the eps' g planes and the dx plane
         }
     }
     tile0.push_back((int)tiles.size());
@@ -2640,7 +2636,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
                 }
         }
         P.win = pp[p].win, P.nval = pp[p].nval, P.mh_off = (int64_t)pp[p].mh_off;
-        if (pp[p].sg) flt_off += (size_t)pp[p].ne * 2 * P.fstride * P.H;
+        P.dxp = pp[p].sg ? P.flt + (size_t)pp[p].ne * 2 * P.fstride * P.H : nullptr;
+        if (pp[p].sg) flt_off += (size_t)(pp[p].ne * 2 + 1) * P.fstride * P.H;
     }
     A.tiles = (const Tile *)dp(o_tiles), A.units = (const URect *)dp(o_units), A.tile0 = (const int32_t *)dp(o_t0);
     auto *d_t0 = (int32_t *)dp(o_t0);
