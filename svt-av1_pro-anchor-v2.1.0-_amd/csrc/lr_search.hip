@@ -1521,6 +1521,9 @@ __global__ void sgr_best_kernel(const Descent *ds, const SearchArgs A, int nplan
 // Two 512-lane workgroups per CU (7 pixel waves + 1 control wave each, 68 KB of LDS): one workgroup's loads, control
 // steps and barriers overlap the other's passes (1024-lane workgroups, one per CU: 2204 vs 2366 Mpx/s at three frames
 // in flight, 1656 vs 1740 at one, same box, profiles/r03/srvar)
+#ifndef SVTGPU_SR_GLDS
+#define SVTGPU_SR_GLDS 0 // 1: the load phase's dx chunks by direct global -> LDS loads (A/B)
+#endif
 #ifndef SVTGPU_SR_NT
 #define SVTGPU_SR_NT 512
 #endif
@@ -1654,7 +1657,7 @@ __device__ __forceinline__ void sr_tree_publish(const Descent &d, bool live, int
 // one per chunk (the load phase leaves zeros in the chunks from K up to the next multiple of four, so a group never
 // needs a per-chunk guard).  Issuing the next group's reads before the current group spills the load phase's registers.
 template <int NV>
-__device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const uint2 *dx, int pl, int K, int nv,
+__device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const uint32_t *dx, int pl, int K, int nv,
                                         const uint32_t *s_xq, unsigned long long (*s_red)[SG_NC]) {
     static_assert(SR_LB == 4, "the load phase zero-fills whole groups of four chunks");
     constexpr int GS = NV == 1 ? 4 : 1, NG = (SR_KMAX + GS - 1) / GS;
@@ -1670,7 +1673,7 @@ __device__ __forceinline__ void sr_pass(const uint32_t (&g)[SR_KMAX][4], const u
             uint2 cur[GS];
 #pragma unroll
             for (int j = 0; j < GS; j++)
-                if (kb + j < SR_KMAX) cur[j] = dx[(kb + j) * SR_PL + pl];
+                if (kb + j < SR_KMAX) cur[j] = make_uint2(dx[(kb + j) * SR_PL + pl], dx[(SR_KMAX + kb + j) * SR_PL + pl]);
 #pragma unroll
             for (int j = 0; j < GS; j++) {
                 const int kk = kb + j;
@@ -1709,7 +1712,9 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
     // one node per pass in the default kernel: a compile-time constant there, so the per-lane tree builder (a
     // divergent Descent copy per lane) is not compiled in and the descent keeps to registers
     const int nodes = TREE ? nodes_arg : 1;
-    extern __shared__ uint2 sr_dx[];                   // [chunk k][pixel lane]: (x - src) of pixels 0, 1 | 2, 3 (int16)
+    // [half][chunk k][pixel lane]: (x - src) of pixels 0, 1 (half 0) and 2, 3 (half 1), int16 pairs -- two planes of
+    // lane-linear words, the layout the direct global -> LDS loads (SVTGPU_SR_GLDS) write
+    extern __shared__ uint32_t sr_dx[];
     // wave partials: the moments, then each pass's errors; two buffers by pass parity (the one-barrier path of
     // one-part items reads a pass's partials while the next pass writes the other buffer)
     __shared__ unsigned long long s_red2[2][SR_PW][SG_NC];
@@ -1781,6 +1786,62 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
         //    chunk needs two registers here instead of four for the CDEF output and the source: half the round trips
         crow = pl / cw, ccol = pl - crow * cw;
         unsigned long long M0 = 0, M1 = 0, M2 = 0, M3 = 0, M4 = 0; // M2..M4 hold signed sums mod 2^64
+#if SVTGPU_SR_GLDS
+        // every chunk's dx straight into its LDS words with direct global -> LDS loads (no registers: one round trip
+        // for the part), then each lane reads its own words back, masks them and forms the moments
+        {
+            uint32_t *lw = sr_dx + (pl & ~63); // the wave's lane-linear base: lane l of the wave lands at lw[l + ...]
+#pragma unroll
+            for (int kk = 0; kk < SR_KMAX; kk++) {
+                if (kk >= K) break; // uniform
+                int row, col;
+                chunk_at(kk, row, col);
+                const int16_t *src = P.dxp + (size_t)(ur.v_start + it.y0 + row) * P.fstride + ur.h_start + 4 * col;
+                __builtin_amdgcn_global_load_lds((const void *)src,
+                                                 (__attribute__((address_space(3))) void *)(lw + kk * SR_PL), 4, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void *)(src + 2),
+                                                 (__attribute__((address_space(3))) void *)(lw + (SR_KMAX + kk) * SR_PL),
+                                                 4, 0, 0);
+                advance();
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        crow = pl / cw, ccol = pl - crow * cw;
+#pragma unroll
+        for (int kk = 0; kk < SR_KMAX; kk++) {
+            if (kk >= K) { // uniform: zeros up to the next multiple of SR_LB (sr_pass reads whole groups)
+                if (kk < ((K + SR_LB - 1) & ~(SR_LB - 1))) sr_dx[kk * SR_PL + pl] = sr_dx[(SR_KMAX + kk) * SR_PL + pl] = 0u;
+                continue;
+            }
+            int row, col;
+            chunk_at(kk, row, col);
+            const int nin = pl + kk * SR_PL < nch ? min(4, uw - 4 * col) : 0;
+            advance();
+            const uint32_t mlo = nin >= 2 ? ~0u : nin == 1 ? 0xFFFFu : 0u;
+            const uint32_t mhi = nin >= 4 ? ~0u : nin == 3 ? 0xFFFFu : 0u;
+            g[kk][0] &= mlo, g[kk][2] &= mlo, g[kk][1] &= mhi, g[kk][3] &= mhi;
+            const uint2 x2 = make_uint2(sr_dx[kk * SR_PL + pl] & mlo, sr_dx[(SR_KMAX + kk) * SR_PL + pl] & mhi);
+            if (nin < 4) sr_dx[kk * SR_PL + pl] = x2.x, sr_dx[(SR_KMAX + kk) * SR_PL + pl] = x2.y;
+            const int      dxq[4] = {(int)(int16_t)(x2.x & 0xFFFF), (int)x2.x >> 16, (int)(int16_t)(x2.y & 0xFFFF),
+                                     (int)x2.y >> 16};
+            const uint32_t fw[4] = {__builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x05040100u),
+                                    __builtin_amdgcn_perm(g[kk][2], g[kk][0], 0x07060302u),
+                                    __builtin_amdgcn_perm(g[kk][3], g[kk][1], 0x05040100u),
+                                    __builtin_amdgcn_perm(g[kk][3], g[kk][1], 0x07060302u)};
+            uint32_t m0 = 0, m1 = 0;
+            int      m3 = 0, m4 = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t gq = fw[q] & gmask;
+                const int      g1 = (int)(int16_t)(gq & 0xFFFF), g2 = (int)gq >> 16, ss = -(dxq[q] << 4);
+                m0 += (uint32_t)(g1 * g1), m1 += (uint32_t)(g2 * g2);
+                m3 += g1 * ss, m4 += g2 * ss;
+                M2 += (unsigned long long)(long long)(g1 * g2);
+                g[kk][q] = gq;
+            }
+            M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
+        }
+#else
         constexpr int LB2 = SR_LB;
 #pragma unroll
         for (int kb = 0; kb < SR_KMAX; kb += LB2) {
@@ -1788,7 +1849,7 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                 if (kb < ((K + SR_LB - 1) & ~(SR_LB - 1)))
 #pragma unroll
                     for (int j = 0; j < LB2; j++)
-                        if (kb + j < SR_KMAX) sr_dx[(kb + j) * SR_PL + pl] = make_uint2(0u, 0u);
+                        if (kb + j < SR_KMAX) sr_dx[(kb + j) * SR_PL + pl] = sr_dx[(SR_KMAX + kb + j) * SR_PL + pl] = 0u;
                 continue;
             }
             uint2 xv[LB2];
@@ -1832,9 +1893,10 @@ __global__ __launch_bounds__(SR_NT, 4) void sgr_res_kernel(const SearchArgs A, i
                     g[kk][q] = gq;
                 }
                 M0 += m0, M1 += m1, M3 += (unsigned long long)(long long)m3, M4 += (unsigned long long)(long long)m4;
-                sr_dx[kk * SR_PL + pl] = x2;
+                sr_dx[kk * SR_PL + pl] = x2.x, sr_dx[(SR_KMAX + kk) * SR_PL + pl] = x2.y;
             }
         }
+#endif
         {
             const unsigned long long t[5] = {wave_sum_u64_limbs(M0), wave_sum_u64_limbs(M1), wave_sum_u64_limbs(M2),
                                              wave_sum_u64_limbs(M3), wave_sum_u64_limbs(M4)};
