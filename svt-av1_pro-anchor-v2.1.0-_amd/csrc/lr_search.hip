@@ -1072,6 +1072,10 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
     // one candidate over the lane's rows: its error sum.  Taps uniform (scalar registers), the add-source 128 folded
     // into the centre taps
     auto eval = [&](const int *tap_h, const int *tap_v) -> int {
+        // the row bounds made opaque per candidate: the unrolled steps' conditions then stay scalar compares, where
+        // the compiler otherwise hoisted all of them out of the candidate loop as 64-bit lane masks and spilled them
+        int je = jend, nr = nrows;
+        asm volatile("" : "+s"(je), "+s"(nr));
         int hf[8], vf[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) hf[k] = tap_h[k], vf[k] = tap_v[k];
@@ -1102,7 +1106,7 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
                 const uint32_t d0 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(o0, o1)) -
                                                                           __builtin_bit_cast(v2i16, sa)) & dmask;
                 e = dot2(d0, d0, e);
-                if (2 * i + 1 < nrows) {
+                if (2 * i + 1 < nr) {
                     const int q0 = vclip(dot2(hq0[3], Vo3, dot2(hq0[2], Vo2, dot2(hq0[1], Vo1, dot2_s(hq0[0], Vo0, vb)))));
                     const int q1 = vclip(dot2(hq1[3], Vo3, dot2(hq1[2], Vo2, dot2(hq1[1], Vo1, dot2_s(hq1[0], Vo0, vb)))));
                     const uint32_t d1 = (uint32_t)__builtin_bit_cast(int, __builtin_bit_cast(v2i16, pack2(q0, q1)) -
@@ -1111,17 +1115,17 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
                 }
             }
         };
-        if (nrows) {
+        if (nr) {
             wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0, na);
             wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 1, nb);
         }
         if constexpr (LDSW) { // unrolled: the source pairs are addressed by constants
 #pragma unroll
             for (int j = 0; j < WR_RMAX / 2 + 3; j++) {
-                if (j < jend) { // uniform per wave (one segment per wave)
+                if (j < je) { // uniform per wave (one segment per wave)
 #pragma unroll
                     for (int k = 0; k < 5; k++) pa[k] = na[k], pb[k] = nb[k];
-                    if (j + 1 < jend) { // the next pair of window rows is in flight during this step
+                    if (j + 1 < je) { // the next pair of window rows is in flight during this step
                         wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 2, na);
                         wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 3, nb);
                     }
@@ -1131,16 +1135,16 @@ __device__ void wr_run(const SearchArgs &A, const PlaneArgs &P, Descent &D, cons
         } else { // window and source rows from global memory, one step ahead
             uint32_t sa = 0, sb = 0;
 #pragma unroll 1
-            for (int j = 0; j < jend; j++) {
+            for (int j = 0; j < je; j++) {
 #pragma unroll
                 for (int k = 0; k < 5; k++) pa[k] = na[k], pb[k] = nb[k];
                 const uint32_t ca = sa, cb = sb;
-                if (j + 1 < jend) {
+                if (j + 1 < je) {
                     wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 2, na);
                     wr_fetch<T, LDSW>(win, ws, P, ux, uy, hw, xc, seg0 + 2 * j + 3, nb);
                 }
                 const int in = j - 2; // the output pair of the next step
-                if (in >= 0 && 2 * in < nrows) sa = load_src(2 * in), sb = 2 * in + 1 < nrows ? load_src(2 * in + 1) : 0u;
+                if (in >= 0 && 2 * in < nr) sa = load_src(2 * in), sb = 2 * in + 1 < nr ? load_src(2 * in + 1) : 0u;
                 step(j, ca, cb);
             }
         }
