@@ -20,37 +20,80 @@
 
 namespace {
 
-// self-guided filter + projection (svt_apply_selfguided_restoration_c) of a w x h tile; AB holds 2 int arrays of
-// (h+2) x (w+2); flt0 is kept per thread between the passes (px k of thread = threadIdx.x + k * NTHR)
+// A, B of one self-guided pass at the centres (ys + YS m, x), m < ncent, x = -1 .. w (box radius R): an item slides a
+// window of per-row sums down one column segment -- 2R + 1 row sums to start, YS more per further centre -- instead
+// of reading the (2R + 1)^2 box at every centre (r = 2: 125 LDS reads per 11 centres instead of 275).  A and B land
+// packed in one word, A | B << 9 (A <= 256; B < 2^20 up to 12 bits): one LDS array, so a tile takes 29 KB instead of
+// 46 and five workgroups fit a CU instead of three
+template <int R, int YS>
+__device__ __forceinline__ void sgr_ab_slide(const uint16_t *v, int vs, int bw, int ys, int ncent, int s, int bd,
+                                             uint32_t *P) {
+    constexpr int N = 2 * R + 1;
+    const int     G = max(1, NTHR / bw), per = (ncent + G - 1) / G; // column segments of `per` centres
+    for (int it = threadIdx.x; it < bw * G; it += NTHR) {
+        const int g = it / bw, x = it - g * bw - 1, m0 = g * per, m1 = min(ncent, m0 + per);
+        if (m0 >= m1) continue;
+        int  ws[N], wq[N];
+        auto row = [&](int y, int &sum, int &sq) {
+            const uint16_t *p = v + y * vs + x - R;
+            sum = 0, sq = 0;
+#pragma unroll
+            for (int k = 0; k < N; k++) {
+                const int q = p[k];
+                sum += q, sq += q * q;
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < N; k++) row(ys + YS * m0 - R + k, ws[k], wq[k]);
+        for (int m = m0; m < m1; m++) {
+            const int y = ys + YS * m;
+            if (m > m0) {
+#pragma unroll
+                for (int k = 0; k + YS < N; k++) ws[k] = ws[k + YS], wq[k] = wq[k + YS];
+#pragma unroll
+                for (int k = N - YS; k < N; k++) row(y - R + k, ws[k], wq[k]);
+            }
+            int sum = 0, sq = 0;
+#pragma unroll
+            for (int k = 0; k < N; k++) sum += ws[k], sq += wq[k];
+            int a, b;
+            sgr_ab_from_sums(sum, sq, N * N, s, bd, c_x_by_xplus1, &a, &b);
+            P[(y + 1) * bw + x + 1] = (uint32_t)a | ((uint32_t)b << 9);
+        }
+    }
+}
+
+// self-guided filter + projection (svt_apply_selfguided_restoration_c) of a w x h tile; P holds the packed A, B of
+// (h+2) x (w+2) positions; flt0 is kept per thread between the passes (px k of thread = threadIdx.x + k * NTHR)
 constexpr int SGR_MAXPX = 64 * 64 / NTHR;
 template <typename T>
-__device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h, int eps, const int32_t *xqd,
-                         int bd, T *out, size_t os) {
+__device__ void sgr_tile(const uint16_t *v, int vs, uint32_t *P, int w, int h, int eps, const int32_t *xqd, int bd,
+                         T *out, size_t os) {
     const int     bw = w + 2;
-    const FastDiv dbw(bw), dw(w);
+    const FastDiv dw(w);
+    auto          pa = [](uint32_t p) { return (int)(p & 511u); };
+    auto          pb = [](uint32_t p) { return (int)(p >> 9); };
     int           f0[SGR_MAXPX];
     const int     r0 = c_sgr_r[eps][0], r1 = c_sgr_r[eps][1];
     if (r0 > 0) { // r = 2 on odd rows -1, 1, 3, ...
-        const int nrow = (h + 3) / 2;
-        for (int i = threadIdx.x; i < nrow * bw; i += NTHR) {
-            const int q = dbw(i), y = 2 * q - 1, x = i - q * bw - 1;
-            sgr_ab(v, vs, y, x, 2, c_sgr_s[eps][0], bd, &A[(y + 1) * bw + x + 1], &B[(y + 1) * bw + x + 1]);
-        }
+        sgr_ab_slide<2, 2>(v, vs, bw, -1, (h + 3) / 2, c_sgr_s[eps][0], bd, P);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SGR_MAXPX; k++) {
             const int i = threadIdx.x + k * NTHR;
             if (i >= w * h) break;
             const int y = dw(i), x = i - y * w;
-            const int *a = A + (y + 1) * bw + x + 1, *b = B + (y + 1) * bw + x + 1;
-            int        aa, bb, nb;
+            const uint32_t *q = P + (y + 1) * bw + x + 1;
+            int             aa, bb, nb;
             if (!(y & 1)) {
-                aa = (a[-bw] + a[bw]) * 6 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 5;
-                bb = (b[-bw] + b[bw]) * 6 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 5;
+                const uint32_t n0 = q[-bw], n1 = q[bw], c0 = q[-bw - 1], c1 = q[bw - 1], c2 = q[-bw + 1], c3 = q[bw + 1];
+                aa = (pa(n0) + pa(n1)) * 6 + (pa(c0) + pa(c1) + pa(c2) + pa(c3)) * 5;
+                bb = (pb(n0) + pb(n1)) * 6 + (pb(c0) + pb(c1) + pb(c2) + pb(c3)) * 5;
                 nb = 5;
             } else {
-                aa = a[0] * 6 + (a[-1] + a[1]) * 5;
-                bb = b[0] * 6 + (b[-1] + b[1]) * 5;
+                const uint32_t m = q[0], l = q[-1], r = q[1];
+                aa = pa(m) * 6 + (pa(l) + pa(r)) * 5;
+                bb = pb(m) * 6 + (pb(l) + pb(r)) * 5;
                 nb = 4;
             }
             const int sh = 8 + nb - 4;
@@ -59,10 +102,7 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
         __syncthreads();
     }
     if (r1 > 0) {
-        for (int i = threadIdx.x; i < (h + 2) * bw; i += NTHR) {
-            const int q = dbw(i), y = q - 1, x = i - q * bw - 1;
-            sgr_ab(v, vs, y, x, 1, c_sgr_s[eps][1], bd, &A[i], &B[i]);
-        }
+        sgr_ab_slide<1, 1>(v, vs, bw, -1, h + 2, c_sgr_s[eps][1], bd, P);
         __syncthreads();
     }
     // projection: xq from xqd (svt_decode_xq, EbRestoration.c:634-646)
@@ -83,9 +123,11 @@ __device__ void sgr_tile(const uint16_t *v, int vs, int *A, int *B, int w, int h
         int       val = u << 7;
         if (r0 > 0) val += xq0 * (f0[k] - u);
         if (r1 > 0) {
-            const int *a = A + (y + 1) * bw + x + 1, *b = B + (y + 1) * bw + x + 1;
-            const int  aa = (a[0] + a[-1] + a[1] + a[-bw] + a[bw]) * 4 + (a[-bw - 1] + a[bw - 1] + a[-bw + 1] + a[bw + 1]) * 3;
-            const int  bb = (b[0] + b[-1] + b[1] + b[-bw] + b[bw]) * 4 + (b[-bw - 1] + b[bw - 1] + b[-bw + 1] + b[bw + 1]) * 3;
+            const uint32_t *q = P + (y + 1) * bw + x + 1;
+            const uint32_t  e0 = q[0], e1 = q[-1], e2 = q[1], e3 = q[-bw], e4 = q[bw];
+            const uint32_t  c0 = q[-bw - 1], c1 = q[bw - 1], c2 = q[-bw + 1], c3 = q[bw + 1];
+            const int aa = (pa(e0) + pa(e1) + pa(e2) + pa(e3) + pa(e4)) * 4 + (pa(c0) + pa(c1) + pa(c2) + pa(c3)) * 3;
+            const int bb = (pb(e0) + pb(e1) + pb(e2) + pb(e3) + pb(e4)) * 4 + (pb(c0) + pb(c1) + pb(c2) + pb(c3)) * 3;
             const int  f1 = (aa * (int)v[y * vs + x] + bb + (1 << 8)) >> 9;
             val += xq1 * (f1 - u);
         }
@@ -107,6 +149,7 @@ struct LrPlaneArgs {
     int32_t               dlf_stride, cdef_stride, out_stride;
     int32_t               W, H, ss, unit_size, hunits, vunits, nchunks, bd;
     int32_t               k0, c0, nc; // the (stripe, column chunk) tiles written: k0 + i / nc, c0 + i % nc
+    int32_t               count;      // nk x nc tiles (the plane's block range is padded to a multiple of 8)
     const SvtGpuRestUnit *units;
 };
 
@@ -114,20 +157,25 @@ struct LrPlaneArgs {
 // one tail instead of three for a kernel of ~20 us per plane)
 struct LrApplyArgs {
     LrPlaneArgs pl[3];
-    int32_t     nplanes, end[3]; // end[i]: first block past plane i of the launch
+    int32_t     nplanes, end[3]; // end[i]: first block past plane i of the launch (each range a multiple of 8)
 };
 
 template <typename T>
 __global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrApplyArgs args) {
     int pi = 0;
     while (pi + 1 < args.nplanes && (int)blockIdx.x >= args.end[pi]) pi++;
-    const LrPlaneArgs &a   = args.pl[pi];
-    const int          blk = (int)blockIdx.x - (pi ? args.end[pi - 1] : 0);
+    const LrPlaneArgs &a = args.pl[pi];
+    // XCD-aware order within each plane (its block range starts on a multiple of 8): every XCD takes a contiguous
+    // eighth of each plane -- a few stripes, so the apron lines a tile shares with its neighbours (3 + 5 columns,
+    // 7 rows) are fetched into one L2 instead of up to three, and the luma / chroma work stays spread over all XCDs
+    const int b0  = pi ? args.end[pi - 1] : 0;
+    const int blk = xcd_swizzle((int)blockIdx.x - b0, args.end[pi] - b0);
+    if (blk >= a.count) return; // the padding to a multiple of 8
     __shared__ __attribute__((aligned(16))) uint16_t v[VR * VS];
     // a unit is Wiener or self-guided: the Wiener intermediate (VR x TW u16) shares the A/B arrays' LDS
-    __shared__ int      AB[2][(TH + 2) * (TW + 2)];
-    static_assert(VR * TW * 2 <= sizeof(int) * (TH + 2) * (TW + 2), "Wiener intermediate in AB[0]");
-    uint16_t *t = (uint16_t *)AB[0];
+    __shared__ uint32_t AB[(TH + 2) * (TW + 2)];
+    static_assert(VR * TW * 2 <= sizeof(uint32_t) * (TH + 2) * (TW + 2), "Wiener intermediate in AB");
+    uint16_t *t = (uint16_t *)AB;
     const int S = 64 >> a.ss, off = 8 >> a.ss, cwmax = 64 >> a.ss;
     const int k = a.k0 + blk / a.nc, c = a.c0 + blk % a.nc;
     const int y0 = max(0, k * S - off), y1 = min((k + 1) * S - off, a.H);
@@ -209,7 +257,7 @@ __global__ __launch_bounds__(NTHR) void lr_apply_kernel(const LrApplyArgs args) 
     if (u.type == SVTGPU_RESTORE_WIENER)
         wiener_tile(v0, VS, t, TW, w, h, u.hfilter, u.vfilter, a.bd, o0, (size_t)a.out_stride);
     else
-        sgr_tile(v0, VS, AB[0], AB[1], w, h, u.ep, u.xqd, a.bd, o0, (size_t)a.out_stride);
+        sgr_tile(v0, VS, AB, w, h, u.ep, u.xqd, a.bd, o0, (size_t)a.out_stride);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -283,7 +331,7 @@ __global__ __launch_bounds__(NTHR) void sgr_shim_kernel(const uint16_t *in, int 
         }
     } else {
         const int32_t xqd[2] = {x0q, x1q};
-        sgr_tile(v0, 70, AB[0], AB[1], w, h, eps, xqd, bd, out, (size_t)w);
+        sgr_tile(v0, 70, (uint32_t *)AB[0], w, h, eps, xqd, bd, out, (size_t)w);
     }
 }
 
@@ -431,7 +479,8 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
         // the rect is a union of whole (stripe, chunk) tiles (svtgpu_lr_set_tile checks)
         a.k0 = (r[1] + off) / S, a.c0 = r[0] / cw, a.nc = (r[2] + cw - 1) / cw - a.c0;
         const int nk = (r[3] + off + S - 1) / S - a.k0;
-        nblk += nk * a.nc;
+        a.count = nk * a.nc;
+        nblk += (a.count + 7) & ~7;
         L.end[L.nplanes++] = nblk;
     }
     if (!nblk) return SVTGPU_OK;
