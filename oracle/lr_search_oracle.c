@@ -707,3 +707,65 @@ void oracle_lr_debug_decompose(int win, const int64_t *M, const int64_t *H, int3
 void oracle_lr_debug_update(int which, int win, const int64_t *M, const int64_t *H, int32_t *a, int32_t *b) {
     update_sep_sym(which, win, M, H, a, b);
 }
+
+/* ------------------------------------------------------------------------------------------- */
+/* measurement probe (not part of the restatement): for every unit of one plane and every ep of the search, the
+ * exact error search_sgr finds (proj_subspace + finer_proj, EbRestorationPick.c:550-652) and a lower bound valid for
+ * any xq: err >= (max(0, sqrt(Qmin) - sqrt(N) / 2))^2, Qmin the real least-squares minimum of the projection
+ * residual over the unit (proj_err's per-pixel rounding moves each residual by at most 1/2).  Used to estimate how
+ * many eps a bound-ordered search could skip (scripts/r5/sgr_prune_probe.py).  err/bound: [units][eps] */
+int oracle_lr_sgr_probe(const uint16_t *dgd_p, int dgd_stride, const uint16_t *src_p, int src_stride, int W, int H,
+                        int bd, int usz, int start, int end, int inc, int refine, int64_t *err_out, double *bound_out) {
+    const Pl  dgd = {dgd_p, dgd_stride, W, H, 1}, src = {src_p, src_stride, W, H, 1};
+    const int ext = usz * 3 / 2, off = 8;
+    int       ui = 0, neps = 0;
+    for (int ep = start; ep < end; ep += inc) neps++;
+    for (int y0 = 0; y0 < H;) {
+        const int uh = (H - y0 < ext) ? H - y0 : usz;
+        int       vs = MAX_(0, y0 - off), ve = y0 + uh;
+        if (ve < H) ve -= off;
+        for (int x0 = 0; x0 < W;) {
+            const int uw = (W - x0 < ext) ? W - x0 : usz;
+            const Lim l  = {x0, x0 + uw, vs, ve};
+            const int w = uw, h = ve - vs, es = w + 6;
+            int32_t  *d  = malloc(sizeof(int32_t) * (size_t)es * (h + 6));
+            int32_t  *f0 = malloc(sizeof(int32_t) * (size_t)w * h), *f1 = malloc(sizeof(int32_t) * (size_t)w * h);
+            for (int i = -3; i < h + 3; i++)
+                for (int j = -3; j < w + 3; j++) d[(i + 3) * es + j + 3] = at(&dgd, l.v_start + i, l.h_start + j);
+            int k = 0;
+            for (int ep = start; ep < end; ep += inc, k++) {
+                for (int i = 0; i < h; i += 64)
+                    for (int j = 0; j < w; j += 64)
+                        oracle_sgr_filter(d + (3 + i) * es + 3 + j, es, MIN_(64, w - j), MIN_(64, h - i), ep, bd,
+                                          f0 + i * w + j, f1 + i * w + j, w);
+                int32_t xqd[2];
+                proj_subspace(&src, &dgd, &l, f0, f1, w, ep, xqd);
+                err_out[(size_t)ui * neps + k] = finer_proj(&src, &dgd, &l, f0, f1, w, xqd, refine, ep);
+                double G00 = 0, G01 = 0, G11 = 0, c0 = 0, c1 = 0, yy = 0;
+                for (int i = 0; i < h; i++)
+                    for (int j = 0; j < w; j++) {
+                        const int    dv = at(&dgd, vs + i, x0 + j), sv = at(&src, vs + i, x0 + j), u = dv << 4;
+                        const double y  = (double)(sv - dv);
+                        const double g0 = kSgrR[ep][0] > 0 ? (double)(f0[i * w + j] - u) : 0;
+                        const double g1 = kSgrR[ep][1] > 0 ? (double)(f1[i * w + j] - u) : 0;
+                        G00 += g0 * g0, G01 += g0 * g1, G11 += g1 * g1, c0 += g0 * y, c1 += g1 * y, yy += y * y;
+                    }
+                double       q   = yy;
+                const double det = G00 * G11 - G01 * G01;
+                if (det > 1e-9 * (G00 * G11 + 1))
+                    q = yy - (G11 * c0 * c0 - 2 * G01 * c0 * c1 + G00 * c1 * c1) / det;
+                else if (G00 > 0)
+                    q = yy - c0 * c0 / G00;
+                else if (G11 > 0)
+                    q = yy - c1 * c1 / G11;
+                const double r = sqrt(q > 0 ? q : 0) - sqrt((double)(w * h)) / 2;
+                bound_out[(size_t)ui * neps + k] = r > 0 ? r * r : 0;
+            }
+            free(d), free(f0), free(f1);
+            ui++;
+            x0 += uw;
+        }
+        y0 += uh;
+    }
+    return ui;
+}
