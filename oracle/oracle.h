@@ -105,6 +105,10 @@ int oracle_lr_controls_for_level(int wn, int sg, SvtGpuLrSearchControls *c);
 int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, const int *unit_size,
                            const SvtGpuLrSearchControls *c, int *frame_type_out, SvtGpuRestUnit *const *units_out,
                            SvtGpuLrUnitSearch *const *search_out);
+/* measurement probe (scripts/r5/sgr_prune_probe.py): per luma unit and ep, search_sgr's exact error and the
+ * rounding lower bound; returns the number of units */
+int oracle_lr_sgr_probe(const uint16_t *dgd, int dgd_stride, const uint16_t *src, int src_stride, int W, int H, int bd,
+                        int usz, int start, int end, int inc, int refine, int64_t *err_out, double *bound_out);
 
 #ifdef __cplusplus
 }
