@@ -127,7 +127,7 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
               hipMalloc(&s->d_mse, nfb * 2 * 64 * 8) == hipSuccess && hipMalloc(&s->d_skip, (nfb + 7) & ~(size_t)7) == hipSuccess &&
               hipMalloc(&s->d_dir, nfb * 64) == hipSuccess && hipMalloc(&s->d_var, nfb * 64 * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_strength, nfb) == hipSuccess &&
-              hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096 + 41 * 4) * 8) == hipSuccess &&
+              hipMalloc(&s->d_pick_part, (nfb * 128 + (size_t)3 * 4 * 4096 + 41 * 4 + (size_t)nfb * 64) * 8) == hipSuccess &&
               hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, (size_t)(41 * 4 * 32 + 4 * 32 + 64) * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_list, (2 * nfb + 1) * 4) == hipSuccess &&
               hipMalloc(&s->d_pick_xch, SVTGPU_PICK_XCH_BYTES) == hipSuccess &&

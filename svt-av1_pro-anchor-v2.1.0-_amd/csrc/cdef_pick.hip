@@ -34,6 +34,7 @@ struct StepChain {
 };
 struct StepArgs {
     const uint64_t *wmse;   // [sb_count][2][64] compacted, bias applied
+    const uint32_t *wmse32; // the same entries' low words (what a step stages; the 64-bit path reads wmse)
     const int32_t  *count;  // sb_count, the number of non-skipped FBs (device)
     const int32_t  *wide;   // nonzero when some wmse entry is >= 2^31 (the 32-bit path would not be exact)
     int32_t         chunk, start_gi, end_gi, step, na; // na: chains in this launch
@@ -74,7 +75,7 @@ __global__ void pick_compact_kernel(const uint8_t *skip, int nfb, int32_t *fb_li
 }
 
 __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *fb_list, const int32_t *count,
-                                   int bias, uint64_t *wmse, int32_t *wide, uint64_t *tot0) {
+                                   int bias, uint64_t *wmse, uint32_t *wmse32, int32_t *wide, uint64_t *tot0) {
     const int i = blockIdx.x;
     if (tot0) // the first step's accumulators (launch path), spread over the grid
         for (int e = i * 128 + threadIdx.x; e < MAX_CHAINS * 4096; e += gridDim.x * 128) tot0[e] = 0;
@@ -83,7 +84,8 @@ __global__ void pick_gather_kernel(const uint64_t *mse, int nfb, const int32_t *
     const int p = threadIdx.x >> 6, g = threadIdx.x & 63; // 128 threads
     uint64_t  v = mse[((size_t)p * nfb + fb) * 64 + g];
     if (bias && g == 0) v = ((uint64_t)bias * v) >> 6;
-    wmse[((size_t)i * 2 + p) * 64 + g] = v;
+    wmse[((size_t)i * 2 + p) * 64 + g]   = v;
+    wmse32[((size_t)i * 2 + p) * 64 + g] = (uint32_t)v;
     if (__any(v >> 31)) // m0 + m1 may leave 32 bits: the step kernels keep the 64-bit arithmetic
         if ((threadIdx.x & 63) == 0) atomicOr(wide, 1);
 }
@@ -162,19 +164,19 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     }
     // 0. then every other global load of the step, issued before anything waits on one: the previous call's totals, this
     // workgroup's FB chunk (clamped into the allocated table, not the live count, so no load waits for the count)
-    // and the live count and width flag.  The chunk stays in named registers (not an array: VGPRs, not scratch)
-    // through the argmin and lands in LDS after it (<= PICK_CHUNK * 64 / NT each)
+    // and the live count and width flag.  The chunk (its low words: half the bytes of the 64-bit rows) stays in named
+    // registers (not an array: VGPRs, not scratch) through the argmin and lands in LDS after it
     uint64_t tv[4096 / NT];
     {
         const uint64_t *tot = A.tot + ((size_t)((A.step + 2) % 3) * MAX_CHAINS + c) * 4096;
 #pragma unroll
         for (int u = 0; u < 4096 / NT; u++) tv[u] = C.prev_nb_sel >= 0 ? tot[u * NT + t] : 0;
     }
-    static_assert(PICK_CHUNK * 64 / NT == 12, "twelve staging registers per lane");
-    const uint4 *src = (const uint4 *)(A.wmse + (size_t)f0 * 128);
-    const int    lim = min(A.chunk, A.fb_alloc - f0) * 64 - 1; // f0 < fb_alloc: the grid covers the table
+    static_assert(PICK_CHUNK * 32 / NT == 6, "six staging registers per lane");
+    const uint4 *src = (const uint4 *)(A.wmse32 + (size_t)f0 * 128);
+    const int    lim = min(A.chunk, A.fb_alloc - f0) * 32 - 1; // f0 < fb_alloc: the grid covers the table
 #define LD(u) const uint4 v##u = src[min(t + (u) * NT, lim)];
-    LD(0) LD(1) LD(2) LD(3) LD(4) LD(5) LD(6) LD(7) LD(8) LD(9) LD(10) LD(11)
+    LD(0) LD(1) LD(2) LD(3) LD(4) LD(5)
 #undef LD
     const int  nfb  = C.nb_sel < 0 ? 0 : min(*A.count - f0, A.chunk);
     const int  wide = *A.wide;
@@ -209,10 +211,10 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
         }
     }
     if (nfb > 0) {
-        uint2 *dst = (uint2 *)dyn; // the low words (the 64-bit path reads the table itself), rows MROW dwords apart
+        uint4 *dst = (uint4 *)dyn; // the low words (the 64-bit path reads the table itself), rows MROW dwords apart
 #define ST(u) \
-    if (t + (u) * NT < nfb * 64) dst[((t + (u) * NT) >> 6) * (MROW / 2) + ((t + (u) * NT) & 63)] = make_uint2(v##u.x, v##u.z);
-        ST(0) ST(1) ST(2) ST(3) ST(4) ST(5) ST(6) ST(7) ST(8) ST(9) ST(10) ST(11)
+    if (t + (u) * NT < nfb * 32) dst[((t + (u) * NT) >> 5) * (MROW / 4) + ((t + (u) * NT) & 31)] = v##u;
+        ST(0) ST(1) ST(2) ST(3) ST(4) ST(5)
 #undef ST
     }
     __syncthreads();
@@ -660,6 +662,8 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     int32_t    *d_inv   = s->d_fb_list + nfb + 1;
     A.tot               = wmse + wmse_elems;                          // [3][4][4096]
     A.val               = A.tot + (size_t)3 * MAX_CHAINS * 4096;      // [NSTEPS+1][4]
+    uint32_t *wmse32    = (uint32_t *)(A.val + (NSTEPS + 1) * MAX_CHAINS); // [nfb][128] low words
+    A.wmse32            = wmse32;
     hipLaunchKernelGGL(pick_compact_kernel, dim3(1), dim3(NT), 0, st, s->d_skip, nfb, s->d_fb_list, d_count,
                        (int32_t *)A.wide, d_inv);
     const int sb_max = nfb; // launch shapes for every FB; the kernels read the non-skipped count on the device
@@ -671,7 +675,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     A.end_gi   = end;
     A.best     = s->d_pick_out;
     hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
-                       (int)ctrls->zero_fs_cost_bias, wmse, (int32_t *)A.wide, persist ? nullptr : A.tot);
+                       (int)ctrls->zero_fs_cost_bias, wmse, wmse32, (int32_t *)A.wide, persist ? nullptr : A.tot);
     unsigned long long *xch = (unsigned long long *)s->d_pick_xch, *stat = nullptr;
     int32_t            *d_status = (int32_t *)(xch + PS_NCH * 4 * 4096 + 4 * 64 * 2);
     if (persist) {
