@@ -22,7 +22,7 @@ for VE in $VARS; do
   fi
   for F in 1 4; do
     env $E timeout -k 10 300 $B --frames-in-flight $F > $O/${V}_f${F}_$rep.log 2>&1 || { echo "$V F=$F failed"; tail -20 $O/${V}_f${F}_$rep.log; exit 1; }
-    echo "$V F=$F: $(grep '^{' $O/${V}_f${F}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["config"]["stage_ms"]["lr_search_apply"], r["all_kernels_ms_per_frame"])')"
+    echo "$V F=$F: $(grep '^{' $O/${V}_f${F}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["config"]["stage_ms"]["'"${STAGE:-lr_search_apply}"'"], r["all_kernels_ms_per_frame"])')"
   done
 done
 done
