@@ -161,6 +161,9 @@ def parse():
     ap.add_argument("--md-main", action="store_true", default=None,
                     help="run the MD batch on the frame's main stream (after the CDEF stage) instead of its own: one "
                          "hardware queue less per frame in flight")
+    ap.add_argument("--lr-sync", action="store_true",
+                    help="A/B: the synchronous LR search (svtgpu_lr_search_frame: one host wait, frame types back before "
+                         "the apply) instead of the asynchronous one (search + device RD finish + apply in stream order)")
     ap.add_argument("--lr-serial", action="store_true",
                     help="measurement: every LR search runs its Wiener chain after its self-guided chain on one stream, "
                          "so each search kernel has the device to itself (the condition of the roofline's isolated "
@@ -183,6 +186,13 @@ def parse():
     a.explicit_frames = a.frames_in_flight is not None
     if a.frames_in_flight is None:
         a.frames_in_flight = _frames_in_flight(sys.argv[1:])
+    # one hardware queue per stream: per frame in flight the main stream, the MD stream and the LR search's Wiener
+    # stream, plus the library context's and torch's null stream.  Streams beyond GPU_MAX_HW_QUEUES share queues, and
+    # a shared in-order queue serializes two frames' chains (round 5's six-frames collapse, 2903 -> 1360 Mpx/s with the
+    # same frame latency: the lazily created Wiener streams landed on queues in thread order).  The MD batch moves onto
+    # the main stream when its own stream would not get a queue of its own.
+    if a.md_main is None:
+        a.md_main = 3 * a.frames_in_flight + 2 > _want_queues
     return a
 
 
@@ -583,6 +593,11 @@ def bench_md(a, torch, dist, n, rank, local):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1e3 / a.steps
+    concurrency = sum(slot_lat) / ms_per_step if slot_lat else None
+    if concurrency is not None and F > 1 and concurrency < F / 2:
+        print("bench: WARNING: frames in flight overlap poorly: concurrency %.2f of %d (slot latencies %s ms, step %.2f "
+              "ms) -- frames are serializing (shared hardware queues?)" % (concurrency, F,
+              [round(x, 2) for x in slot_lat], ms_per_step), file=sys.stderr)
     nsb_mine = sb1 - sb0
     alg_in = nsb_mine * (1 + NREF) * 64 * 64 * B
     alg_out = nsb_mine * NREF * 3 * svtgpu.MD_BLOCKS * 4
@@ -684,7 +699,8 @@ def main():
         if a.dist_backend == "nccl":
             uid = [svtgpu.Comm.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
-            c = svtgpu.Comm.rccl(ctx, n, rank, uid[0])
+            # bounded init: a rank that died after the broadcast makes the others fail with the slot named
+            c = svtgpu.Comm.rccl(ctx, n, rank, uid[0], timeout_ms=a.comm_timeout_ms, slot=k)
         else:
             grp = dist.new_group(backend="gloo")
 
@@ -796,9 +812,14 @@ def main():
             # LR search + apply on the CDEF output (tiles: this rank's units; the records are summed before the
             # finish) with the boundary lines from the DLF output
             self.at_lr.set()
-            lr_ft = lr.search(O, S, lr_ctrls, sp)
-            hc("lr_search")
-            lr.apply(D, O, L, lr_ft, sp)
+            if a.lr_sync:
+                lr_ft = lr.search(O, S, lr_ctrls, sp)
+                hc("lr_search")
+                lr.apply(D, O, L, lr_ft, sp)
+            else:  # search, device RD finish and apply in stream order: no host wait in the LR stage
+                lr.search_async(O, S, lr_ctrls, sp)
+                hc("lr_search")
+                lr.apply(D, O, L, None, sp)
             hc("lr_apply")
             if hc.on:
                 self.ht.append(hc.t)
@@ -833,6 +854,7 @@ def main():
     errors = []
 
     def run(slot, steps, timed, slots=slots):
+        t_start = time.perf_counter()
         try:
             # frame k starts when frame k - 1 reaches its LR stage: the frames stay offset by part of a frame, so one's
             # VALU-bound search overlaps the other's latency-bound stages (started together they run in lockstep and
@@ -841,6 +863,7 @@ def main():
                 slots[slot.k - 1].at_lr.wait(60)  # bounded: a failed slot must not hang the next
             for _ in range(steps):
                 slot.step(timed)
+            slot.wall_ms = (time.perf_counter() - t_start) * 1e3  # the thread's enqueue span (its last waits included)
         except BaseException as e:  # re-raised on the main thread
             errors.append(e)
 
@@ -877,6 +900,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if a.stages == "all" and not a.lr_sync:  # the asynchronous searches' results: a device-side failure raises here
+        for sl in slots:
+            sl.lr.read_result(sl.stream.cuda_stream)
     lr_tot = lr.profile(False) if not a.no_kernel_timing else None
     h2d, d2h = svtgpu.transfer_bytes(reset=True)
     if n > 1:
@@ -886,6 +912,9 @@ def main():
     stage_ms = np.mean([[es[i].elapsed_time(es[i + 1]) for i in range(4)] + [es[6].elapsed_time(es[7])]
                         for es in slots[0].ev], axis=0)
     frame_ms = float(np.mean([es[0].elapsed_time(es[5]) for es in slots[0].ev]))
+    # frames really in flight: the sum over the slots of their mean frame latency over the step time (F when every
+    # frame overlaps the others for the whole step); round 5's collapse read 2.3 of 6 with unchanged latencies
+    slot_lat = [float(np.mean([es[0].elapsed_time(es[5]) for es in sl.ev])) for sl in slots if sl.ev]
     ht_main = list(slots[0].ht)  # --host-timing: the main run's (the iso phase below appends its own)
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
@@ -1018,6 +1047,14 @@ def main():
                              "synthetic, unpinned (%s generator)" % ("integer" if a.inputs == "pinned" else "float"),
                    "width": W, "height": H, "bit_depth": bd, "frames_per_step": frames_per_step,
                    "frames_in_flight": F, "frame_latency_ms": round(frame_ms, 4), "ranks_requested": a.gpus,
+                   "concurrency": {"value": round(concurrency, 3) if concurrency is not None else None,
+                                   "slot_latency_ms": [round(x, 3) for x in slot_lat],
+                                   "slot_wall_ms": [round(getattr(sl, "wall_ms", 0.0), 2) for sl in slots],
+                                   "streams_per_frame": 2 if a.md_main else 3,
+                                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                                   "low": bool(concurrency is not None and F > 1 and concurrency < F / 2),
+                                   "note": "sum over the frame slots of their mean frame latency / step time"},
+                   "lr_search_mode": "sync (host wait)" if a.lr_sync else "async (device RD finish, no host wait)",
                    "ranks": n,
                    "parallelism": ("tiles%dx%d (each frame tiled over the ranks: DLF trials/filter, CDEF search/apply, "
                                    "LR search/apply per tile; RCCL sums of the DLF trial SSEs, CDEF tables, LR records "

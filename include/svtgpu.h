@@ -100,6 +100,12 @@ typedef struct SvtGpuConvolveParams {
 /* 1 when a gfx950 device is visible and the kernels are loadable, else 0. Never aborts. */
 int         svtgpu_device_available(void);
 const char *svtgpu_version(void);
+/* ABI revision of this header: bumped whenever a struct passed across the boundary changes layout or an entry
+ * point changes meaning (6: SvtGpuLrProfile::ms_events, svtgpu_comm_create_bounded, the asynchronous LR search
+ * svtgpu_lr_search_frame_async).  A caller built against another header checks svtgpu_abi_version() ==
+ * SVTGPU_ABI_VERSION once at start-up and refuses to run on a mismatch. */
+#define SVTGPU_ABI_VERSION 6
+int32_t     svtgpu_abi_version(void);
 const char *svtgpu_error_string(int code);
 
 typedef struct SvtGpuContext SvtGpuContext;
@@ -146,6 +152,14 @@ typedef struct SvtGpuComm SvtGpuComm;
 int svtgpu_comm_unique_id(uint8_t id[SVTGPU_COMM_ID_BYTES]);
 int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t rank, const uint8_t id[SVTGPU_COMM_ID_BYTES],
                        SvtGpuComm **out);
+/* svtgpu_comm_create with a bounded init: the communicator is created non-blocking (ncclCommInitRankConfig, blocking
+ * = 0) and polled against timeout_ms (0: the default deadline, SVTGPU_COMM_TIMEOUT_MS or 60000 ms).  A peer that never
+ * joins (it died between the id broadcast and its init) returns SVTGPU_ERR_HIP within the deadline with
+ * svtgpu_error_string naming "communicator init", the frame slot `slot`, this rank and the rank count; the partial
+ * communicator is aborted.  svtgpu_comm_create = this with timeout_ms 0 and slot -1.  SVTGPU_COMM_INIT=blocking
+ * restores the blocking ncclCommInitRank. */
+int svtgpu_comm_create_bounded(SvtGpuContext *ctx, int32_t nranks, int32_t rank, const uint8_t id[SVTGPU_COMM_ID_BYTES],
+                               int32_t timeout_ms, int32_t slot, SvtGpuComm **out);
 /* A caller-supplied host transport (e.g. MPI or gloo): allreduce_u64 sums n uint64 element-wise over the ranks in
  * place (every rank receives the sums) and returns 0.  Device buffers are staged through pinned host memory.  For
  * rehearsals on CPUs and for several ranks on one GPU (RCCL needs one rank per device). */
@@ -838,7 +852,9 @@ int  svtgpu_lr_set_units(SvtGpuLrState *s, int32_t plane, const SvtGpuRestUnit *
  * stripe boundary lines of svt_av1_loop_restoration_save_boundary_lines (EbRestoration.c:1682): rows above /
  * below each 64-row processing stripe come from `deblocked` (the DLF output) inside the frame and from
  * `cdef_out` at the frame top/bottom.  Writes every sample of `out` (planes whose frame_type is NONE are
- * copied).  frame_type[plane]: SVTGPU_RESTORE_NONE or any other value (= per-unit types apply). */
+ * copied).  frame_type[plane]: SVTGPU_RESTORE_NONE or any other value (= per-unit types apply); frame_type == NULL:
+ * every plane unit by unit with the units the last search left on the device (svtgpu_lr_search_frame_async: a plane
+ * whose frame type came out NONE holds NONE units, which are copied) -- no host round trip between search and apply. */
 int  svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *deblocked, const SvtGpuFrame *cdef_out,
                            SvtGpuFrame *out, const int32_t frame_type[3], void *stream);
 
@@ -863,6 +879,19 @@ typedef struct SvtGpuLrUnitSearch {
 int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
                            const SvtGpuLrSearchControls *ctrls, int32_t frame_type_out[3],
                            SvtGpuLrUnitSearch *const search_out[3], void *stream);
+/* The asynchronous form of svtgpu_lr_search_frame (≙ restoration_seg_search + rest_finish_search with no host wait):
+ * the search, the per-unit records and the RD finish (rest_finish_search, EbRestorationPick.c:1555-1634) are enqueued
+ * on `stream` and set the state's units in stream order; a picture tiled over GPUs sums the records over its
+ * communicator on the device first.  Returns without waiting.  svtgpu_lr_apply_frame(..., frame_type = NULL, ...)
+ * applies the result in stream order; svtgpu_lr_read_result waits for it and returns the frame types (and a failure
+ * of the device search, e.g. a descent's bound, which this call cannot see).  SVTGPU_LR_FINISH=host: the round-5 form
+ * (the records read back, the finish on the host, one wait inside this call). */
+int svtgpu_lr_search_frame_async(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                 const SvtGpuLrSearchControls *ctrls, void *stream);
+/* Waits for the last asynchronous search of `s` queued on `stream` and returns its frame types (SVTGPU_RESTORE_*);
+ * after a synchronous search, or a second call, the last frame types collected.  SVTGPU_ERR_HIP: the device search
+ * failed (svtgpu_error_string names it). */
+int svtgpu_lr_read_result(SvtGpuLrState *s, int32_t frame_type_out[3], void *stream);
 /* Per-unit part of the search for a band of unit rows: the units of unit rows [row_begin[p], row_end[p]) of each
  * searched plane (restoration_seg_search restricted to those units; every unit's search is independent of the
  * others).  Writes those units' records into search_out[p] (arrays of all units of the plane, row-major; other
@@ -877,6 +906,14 @@ int svtgpu_lr_search_units(SvtGpuLrState *s, const SvtGpuFrame *recon, const Svt
  * work, usable without a GPU); returns SVTGPU_OK with *frame_type_out = NONE for a plane that is not searched. */
 int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32_t plane, int32_t nunits,
                            const SvtGpuLrUnitSearch *records, int32_t *frame_type_out, SvtGpuRestUnit *units_out);
+/* ≙ rest_finish_search of the whole frame (EbRestorationPick.c:1555-1634): the planes in order over one
+ * RestUnitSearchInfo array shared by the planes, as the reference allocates it -- a chroma plane's switchable pass reads
+ * luma's entries for a filter type chroma does not search (Wiener level 5 beside self-guided level 1-3: presets 3-9),
+ * which svtgpu_lr_finish_plane on one plane alone cannot.  nunits[p] / records[p] / units_out[p] for the searched
+ * planes (units_out of the others zeroed when non-NULL).  Host only. */
+int svtgpu_lr_finish_frame(const SvtGpuLrSearchControls *ctrls, const int32_t nunits[3],
+                           const SvtGpuLrUnitSearch *const records[3], int32_t frame_type_out[3],
+                           SvtGpuRestUnit *const units_out[3]);
 /* A picture tiled over GPUs (svtgpu_tile_plan): svtgpu_lr_search_frame searches only the units of units[p] = {col0,
  * row0, col1, row1} of each plane, sums the zero-padded per-unit records over `comm` (the gather), and runs the RD
  * finish of every plane on every rank (the same frame types and units everywhere); svtgpu_lr_apply_frame writes only

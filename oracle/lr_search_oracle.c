@@ -544,12 +544,20 @@ static int64_t finer_wiener(const Pl *dgd, const Pl *src, const Lim *l, SvtGpuRe
 /* ------------------------------------------------------------------------------------------- */
 /* frame                                                                                         */
 /* ------------------------------------------------------------------------------------------- */
+/* RestUnitSearchInfo (EbRestoration.h:349-360) as rest_finish_search uses it */
+typedef struct Rusi {
+    int64_t        sse[3];
+    SvtGpuRestUnit wiener, sgrproj;
+    int            best[3]; /* best_rtype[RESTORE_WIENER - 1 .. RESTORE_SWITCHABLE - 1] */
+} Rusi;
+
 int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, const int *unit_size,
                            const SvtGpuLrSearchControls *c, int *frame_type_out, SvtGpuRestUnit *const *units_out,
                            SvtGpuLrUnitSearch *const *search_out) {
     const int bd = recon->bit_depth, hb = bd > 8;
     const int plane_end = ((c->wn_enabled && c->wn_use_chroma) || (c->sg_enabled && c->sg_use_chroma)) ? 2 : 0;
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
+    Rusi *rusi = NULL; /* rest_finish_search's per-unit array, shared by the planes (luma's unit count) */
     for (int p = 0; p <= plane_end; p++) {
         const int W = p ? (recon->width + 1) >> 1 : recon->width, H = p ? (recon->height + 1) >> 1 : recon->height;
         const Pl  dgd = {recon->plane[p], recon->stride[p], W, H, hb}, src = {source->plane[p], source->stride[p], W, H, hb};
@@ -600,14 +608,17 @@ int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, 
                 r->sse[2] = try_unit(&dgd, &src, &lim[u], &r->sgrproj, bd);
             }
         }
-        /* rest_finish_search */
+        /* rest_finish_search (EbRestorationPick.c:1555-1634).  Its RestUnitSearchInfo array is allocated once for
+         * the frame (luma's unit count) and shared by the planes: each finish pass overwrites only what it computes,
+         * so a chroma plane's switchable pass reads the luma plane's best_rtype / sse / wiener (or sgrproj) entries
+         * for a restoration type that chroma does not search (search_switchable :1148-1200 reads rusi->best_rtype,
+         * rusi->sse, rusi->wiener, rusi->sgrproj; copy_unit_info :1202-1209 copies them) */
+        if (p == 0) rusi = calloc((size_t)n, sizeof *rusi);
         const int force_all = c->wn_enabled && c->sg_enabled;
         const int force     = c->wn_enabled ? (c->sg_enabled ? 4 : 1) : (c->sg_enabled ? 2 : 0);
         const int nrt       = n > 1 ? 4 : 3;
-        int      *best_rt = (int *)calloc((size_t)3 * n, sizeof(int));
-        SvtGpuRestUnit *uw_ = calloc((size_t)n, sizeof(SvtGpuRestUnit)), *us_ = calloc((size_t)n, sizeof(SvtGpuRestUnit));
-        double best_cost = 0;
-        int    best_type = 0;
+        double    best_cost = 0;
+        int       best_type = 0;
         for (int r = 0; r < nrt; r++) {
             if (!force_all && r != 0 && r != force) continue;
             if (p && ((r == 1 && !c->wn_use_chroma) || (r == 2 && !c->sg_use_chroma))) continue;
@@ -622,54 +633,58 @@ int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, 
             int64_t sse = 0, bits = 0;
             for (int u = 0; u < n; u++) {
                 const SvtGpuLrUnitSearch *R = &rs[u];
-                if (r == 0) {
-                    sse += R->sse[0];
-                } else if (r == 1) {
+                Rusi                     *Q = &rusi[u];
+                if (r == 0) { /* search_norestore_finish */
+                    Q->sse[0] = R->sse[0];
+                    sse += Q->sse[0];
+                } else if (r == 1) { /* search_wiener_finish */
                     const int64_t bn = c->wiener_restore_cost[0];
-                    if (R->sse[1] == INT64_MAX) {
+                    Q->sse[1]        = R->sse[1];
+                    if (Q->sse[1] == INT64_MAX) {
                         bits += bn;
-                        sse += R->sse[0];
-                        best_rt[3 * u] = 0;
+                        sse += Q->sse[0];
+                        Q->best[0] = 0;
                         continue;
                     }
-                    uw_[u]          = R->wiener;
-                    const int64_t bw = c->wiener_restore_cost[1] + ((int64_t)count_wiener_bits(win, &R->wiener, &refw) << 9);
-                    const double  cn = rdcost(c->rdmult, bn >> 4, R->sse[0]), cw = rdcost(c->rdmult, bw >> 4, R->sse[1]);
+                    Q->wiener        = R->wiener;
+                    const int64_t bw = c->wiener_restore_cost[1] + ((int64_t)count_wiener_bits(win, &Q->wiener, &refw) << 9);
+                    const double  cn = rdcost(c->rdmult, bn >> 4, Q->sse[0]), cw = rdcost(c->rdmult, bw >> 4, Q->sse[1]);
                     const int     t  = cw < cn;
-                    best_rt[3 * u]   = t ? 1 : 0;
-                    sse += R->sse[t ? 1 : 0];
+                    Q->best[0]       = t ? 1 : 0;
+                    sse += Q->sse[t ? 1 : 0];
                     bits += t ? bw : bn;
-                    if (t) refw = R->wiener;
-                } else if (r == 2) {
-                    us_[u]          = R->sgrproj;
+                    if (t) refw = Q->wiener;
+                } else if (r == 2) { /* search_sgrproj_finish */
+                    Q->sse[2]        = R->sse[2];
+                    Q->sgrproj       = R->sgrproj;
                     const int64_t bn = c->sgrproj_restore_cost[0];
-                    const int64_t bs = c->sgrproj_restore_cost[1] + ((int64_t)count_sgrproj_bits(&R->sgrproj, &refs) << 9);
-                    const double  cn = rdcost(c->rdmult, bn >> 4, R->sse[0]), cs = rdcost(c->rdmult, bs >> 4, R->sse[2]);
+                    const int64_t bs = c->sgrproj_restore_cost[1] + ((int64_t)count_sgrproj_bits(&Q->sgrproj, &refs) << 9);
+                    const double  cn = rdcost(c->rdmult, bn >> 4, Q->sse[0]), cs = rdcost(c->rdmult, bs >> 4, Q->sse[2]);
                     const int     t  = cs < cn;
-                    best_rt[3 * u + 1] = t ? 2 : 0;
-                    sse += R->sse[t ? 2 : 0];
+                    Q->best[1]       = t ? 2 : 0;
+                    sse += Q->sse[t ? 2 : 0];
                     bits += t ? bs : bn;
-                    if (t) refs = R->sgrproj;
+                    if (t) refs = Q->sgrproj;
                 } else { /* search_switchable */
                     double  bc = 0;
                     int64_t bb = 0;
                     int     bt = 0;
                     for (int t = 0; t < 3; t++) {
-                        if (t > 0 && best_rt[3 * u + t - 1] == 0) continue;
+                        if (t > 0 && Q->best[t - 1] == 0) continue;
                         /* search_switchable sizes the Wiener rate by plane only (7 luma / 5 chroma taps) */
                         const int win_sw = p == 0 ? 7 : 5;
-                        int64_t   cp     = t == 1 ? count_wiener_bits(win_sw, &uw_[u], &refw)
-                                         : t == 2 ? count_sgrproj_bits(&us_[u], &refs)
+                        int64_t   cp     = t == 1 ? count_wiener_bits(win_sw, &Q->wiener, &refw)
+                                         : t == 2 ? count_sgrproj_bits(&Q->sgrproj, &refs)
                                                   : 0;
                         const int64_t b = c->switchable_restore_cost[t] + (cp << 9);
-                        const double  cost = rdcost(c->rdmult, b >> 4, R->sse[t]);
+                        const double  cost = rdcost(c->rdmult, b >> 4, Q->sse[t]);
                         if (t == 0 || cost < bc) bc = cost, bb = b, bt = t;
                     }
-                    best_rt[3 * u + 2] = bt;
-                    sse += R->sse[bt];
+                    Q->best[2] = bt;
+                    sse += Q->sse[bt];
                     bits += bb;
-                    if (bt == 1) refw = uw_[u];
-                    if (bt == 2) refs = us_[u];
+                    if (bt == 1) refw = Q->wiener;
+                    if (bt == 2) refs = Q->sgrproj;
                 }
             }
             const double cost = rdcost(c->rdmult, bits >> 4, sse);
@@ -680,19 +695,17 @@ int oracle_lr_search_frame(const OracleFrame *recon, const OracleFrame *source, 
             SvtGpuRestUnit o;
             memset(&o, 0, sizeof o);
             if (best_type != 0) {
-                const int t = best_rt[3 * u + best_type - 1];
-                o           = t == 1 ? uw_[u] : us_[u];
+                const int t = rusi[u].best[best_type - 1];
+                o           = t == 1 ? rusi[u].wiener : rusi[u].sgrproj;
                 o.type      = t;
             }
             if (units_out && units_out[p]) units_out[p][u] = o;
             if (search_out && search_out[p]) search_out[p][u] = rs[u];
         }
-        free(best_rt);
-        free(uw_);
-        free(us_);
         free(rs);
         free(lim);
     }
+    free(rusi);
     return SVTGPU_OK;
 }
 

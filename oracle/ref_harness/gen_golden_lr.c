@@ -342,6 +342,10 @@ static void gen_search(const char *dir) {
         {160, 96, 8, 64, 3, 3}, {128, 128, 10, 64, 4, 4}, {96, 64, 8, 128, 1, 0},
         /* crop sizes that are not multiples of 8 (see gen_frames) */
         {202, 138, 10, 64, 1, 1}, {134, 74, 8, 64, 2, 2}, {250, 90, 10, 128, 1, 1}, {198, 102, 8, 64, 3, 3},
+        /* one restoration type searched for luma only (Wiener level 5 of presets 3-9 beside self-guided level 3 / 1,
+         * self-guided level 4 beside Wiener level 1): rest_finish_search's switchable pass over a chroma plane then
+         * reads the luma plane's entries of the shared rusi array for the type chroma did not search */
+        {264, 200, 10, 64, 5, 3}, {200, 136, 8, 64, 5, 1}, {192, 128, 10, 64, 1, 4}, {328, 184, 10, 64, 5, 3},
     };
     const int ncase = (int)(sizeof(cases) / sizeof(cases[0]));
     char      path[512];

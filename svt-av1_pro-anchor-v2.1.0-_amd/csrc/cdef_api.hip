@@ -340,6 +340,8 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
         params_out->cdef_uv_strength[0] = (uint8_t)ctrls->pred_uv_f;
         HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, s->nfb, st));
         if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
+        // tiled: the dir / var exchanges above are bounded here, not by some later unbounded wait
+        if (svtgpu_comm_tiled(s->comm)) return svtgpu_comm_wait(s->comm, st);
         return SVTGPU_OK;
     }
     hipStream_t hs;
@@ -392,7 +394,7 @@ extern "C" int svtgpu_cdef_read_state(SvtGpuCdefFrameState *s, uint64_t *mse, ui
     if (skip) HIP_TRY(hipMemcpyAsync(skip, s->d_skip, nfb, hipMemcpyDeviceToHost, st));
     if (dir) HIP_TRY(hipMemcpyAsync(dir, s->d_dir, nfb * 64, hipMemcpyDeviceToHost, st));
     if (var) HIP_TRY(hipMemcpyAsync(var, s->d_var, nfb * 64 * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    return svtgpu_comm_wait(s->comm, st); // bounded when the tables' exchange sits before the copies
     return SVTGPU_OK;
 }
 

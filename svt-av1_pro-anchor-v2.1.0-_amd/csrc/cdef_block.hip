@@ -77,7 +77,7 @@ __global__ void cdef_find_dir_kernel(const uint16_t *img, int n, int cs, uint8_t
 }
 
 static void find_dir_batch(const uint16_t *const *imgs, int stride, int n, int cs, uint8_t *dirs, int32_t *vars) {
-    hipStream_t           st = svtgpu_default_stream();
+    hipStream_t           st = svtgpu_shim_stream();
     std::vector<uint16_t> h((size_t)n * 64);
     for (int b = 0; b < n; b++)
         for (int i = 0; i < 8; i++) memcpy(&h[(size_t)b * 64 + i * 8], imgs[b] + (size_t)i * stride, 16);
@@ -132,7 +132,7 @@ extern "C" void svtgpu_cdef_filter_block(uint8_t *dst8, uint16_t *dst16, int32_t
     std::vector<uint16_t> win((size_t)ws * wh);
     for (int r = 0; r < wh; r++) // exactly the samples the reference reads (rows/cols -2..+1 past the block)
         memcpy(&win[(size_t)r * ws], in + (long)(r - CDEF_BORDER) * 144 - CDEF_BORDER, (size_t)ws * 2);
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     char       *d  = (char *)g_scratch.get(win.size() * 2 + 256);
     uint16_t   *dout = (uint16_t *)(d + ((win.size() * 2 + 15) & ~(size_t)15));
     HIP_OR_DIE(hipMemcpyAsync(d, win.data(), win.size() * 2, hipMemcpyHostToDevice, st));
@@ -205,7 +205,7 @@ static uint64_t cdef_dist_host(const T *dst, int32_t dstride, const T *src, cons
     const size_t o2 = o1 + ((fbytes + 255) & ~(size_t)255);
     const size_t o3 = o2 + (((size_t)n * 2 + 255) & ~(size_t)255);
     char        *d  = (char *)g_scratch.get(o3 + 64);
-    hipStream_t  st = svtgpu_default_stream();
+    hipStream_t  st = svtgpu_shim_stream();
     HIP_OR_DIE(hipMemcpyAsync(d, org.data(), org.size() * sizeof(T), hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemcpyAsync(d + o1, src, fbytes, hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemcpyAsync(d + o2, dlist, (size_t)n * 2, hipMemcpyHostToDevice, st));
@@ -245,7 +245,7 @@ extern "C" void svtgpu_cdef_filter_block_8xn_16(const uint16_t *const in, const 
     std::vector<uint16_t> win((size_t)ws * wh);
     for (int r = 0; r < wh; r++)
         memcpy(&win[(size_t)r * ws], in + (long)(r - CDEF_BORDER) * 144 - CDEF_BORDER, (size_t)ws * 2);
-    hipStream_t st   = svtgpu_default_stream();
+    hipStream_t st   = svtgpu_shim_stream();
     char       *d    = (char *)g_scratch.get(win.size() * 2 + 2 * 1024 + 256);
     uint16_t   *dout = (uint16_t *)(d + ((win.size() * 2 + 15) & ~(size_t)15));
     HIP_OR_DIE(hipMemcpyAsync(d, win.data(), win.size() * 2, hipMemcpyHostToDevice, st));
@@ -268,7 +268,7 @@ extern "C" void svtgpu_aom_copy_rect8_8bit_to_16bit(uint16_t *dst, int32_t dstri
     if (v <= 0 || h <= 0) return;
     std::vector<uint8_t> hs((size_t)v * h);
     for (int r = 0; r < v; r++) memcpy(&hs[(size_t)r * h], src + (long)r * sstride, (size_t)h);
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     char       *d  = (char *)g_scratch.get(hs.size() * 3 + 64);
     uint16_t   *d16 = (uint16_t *)(d + ((hs.size() + 15) & ~(size_t)15));
     HIP_OR_DIE(hipMemcpyAsync(d, hs.data(), hs.size(), hipMemcpyHostToDevice, st));
@@ -331,7 +331,7 @@ __global__ void sod_argmin_kernel(const uint64_t *tot, int start, int end, uint6
 
 extern "C" uint64_t svtgpu_search_one_dual(int *lev0, int *lev1, int nb_strengths, uint64_t **mse[2], int sb_count,
                                            int start_gi, int end_gi) {
-    hipStream_t           st = svtgpu_default_stream();
+    hipStream_t           st = svtgpu_shim_stream();
     std::vector<uint64_t> h((size_t)std::max(sb_count, 1) * 128);
     for (int fb = 0; fb < sb_count; fb++) {
         memcpy(&h[(size_t)fb * 128], mse[0][fb], 64 * 8);

@@ -66,6 +66,7 @@ struct SvtGpuComm {
     int32_t             slot       = -1; // the frame slot it serves (error messages only)
     uint64_t            seq        = 0;  // exchanges issued
     bool                failed     = false;
+    bool                nonblocking = false; // created with ncclConfig_t::blocking = 0: calls may return ncclInProgress
     char                fail_msg[320] = {0};
     XchRecord           ring[XCH_RING]; // the device-side collectives not yet seen complete
     hipEvent_t          wait_ev = nullptr;
@@ -109,12 +110,33 @@ int comm_timeout(SvtGpuComm *c, const XchRecord &r, long long waited_ms) {
     c->nccl = nullptr;
     return comm_failed(c);
 }
-// the oldest exchange enqueued on `st` not yet seen complete, or null
+// the oldest exchange enqueued on `st` not yet seen complete; else the oldest one enqueued on any other stream (a wait
+// on another stream can reach it through events: the CDEF pick's priority lane waits behind the caller's stream,
+// ADVICE r5), or null
 const XchRecord *outstanding(SvtGpuComm *c, hipStream_t st) {
-    const XchRecord *oldest = nullptr;
-    for (auto &r : c->ring)
-        if (r.live && r.st == st && (!oldest || r.seq < oldest->seq)) oldest = &r;
-    return oldest;
+    const XchRecord *oldest = nullptr, *other = nullptr;
+    for (auto &r : c->ring) {
+        if (!r.live) continue;
+        if (r.st == st) {
+            if (!oldest || r.seq < oldest->seq) oldest = &r;
+        } else if (!other || r.seq < other->seq) {
+            other = &r;
+        }
+    }
+    return oldest ? oldest : other;
+}
+// RCCL calls of a non-blocking communicator may return ncclInProgress: poll its state against the deadline
+ncclResult_t nccl_settle(ncclComm_t comm, ncclResult_t r, int timeout_ms, long long *waited_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    *waited_ms    = 0;
+    while (r == ncclInProgress) {
+        const auto w = std::chrono::steady_clock::now() - t0;
+        *waited_ms   = std::chrono::duration_cast<std::chrono::milliseconds>(w).count();
+        if (*waited_ms > timeout_ms) return ncclInProgress;
+        std::this_thread::yield();
+        if (ncclResult_t q = ncclCommGetAsyncError(comm, &r)) return q;
+    }
+    return r;
 }
 int grow_dev(SvtGpuComm *c, size_t n) {
     if (n <= c->dev_words) return SVTGPU_OK;
@@ -135,17 +157,50 @@ extern "C" int svtgpu_comm_unique_id(uint8_t id[SVTGPU_COMM_ID_BYTES]) {
     return SVTGPU_OK;
 }
 
-extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t rank,
-                                  const uint8_t id[SVTGPU_COMM_ID_BYTES], SvtGpuComm **out) {
-    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return SVTGPU_ERR_INVALID_ARG;
+// Communicator creation is bounded like the exchanges: a non-blocking ncclCommInitRankConfig polled with
+// ncclCommGetAsyncError against the deadline, so a rank whose peer died between the id broadcast and its init returns
+// a named error instead of blocking in the bootstrap until the job is killed.  SVTGPU_COMM_INIT=blocking: the plain
+// blocking ncclCommInitRank (A/B).
+extern "C" int svtgpu_comm_create_bounded(SvtGpuContext *ctx, int32_t nranks, int32_t rank,
+                                          const uint8_t id[SVTGPU_COMM_ID_BYTES], int32_t timeout_ms, int32_t slot,
+                                          SvtGpuComm **out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks || timeout_ms < 0) return SVTGPU_ERR_INVALID_ARG;
+    static const bool blocking = [] {
+        const char *e = std::getenv("SVTGPU_COMM_INIT");
+        return e && !std::strcmp(e, "blocking");
+    }();
+    const int tmo = timeout_ms > 0 ? timeout_ms : default_timeout_ms();
     HIP_TRY(hipSetDevice(ctx->device));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclComm_t comm = nullptr;
-    if (ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank)) return nccl_fail(r, "ncclCommInitRank");
+    if (blocking) {
+        if (ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank)) return nccl_fail(r, "ncclCommInitRank");
+    } else {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking     = 0;
+        ncclResult_t r   = ncclCommInitRankConfig(&comm, nranks, u, rank, &cfg);
+        long long    waited = 0;
+        if (r == ncclInProgress && comm) r = nccl_settle(comm, r, tmo, &waited);
+        if (r != ncclSuccess) {
+            char msg[320];
+            if (r == ncclInProgress)
+                std::snprintf(msg, sizeof msg,
+                              "communicator init timed out: frame slot %d, rank %d of %d did not complete "
+                              "ncclCommInitRankConfig within %d ms (waited %lld ms) -- a peer rank never joined; "
+                              "RCCL communicator aborted", slot, rank, nranks, tmo, waited);
+            else
+                std::snprintf(msg, sizeof msg, "communicator init failed: frame slot %d, rank %d of %d: %s", slot, rank,
+                              nranks, ncclGetErrorString(r));
+            if (comm) (void)ncclCommAbort(comm);
+            svtgpu_set_last_hip_error(hipErrorUnknown, msg, __FILE__, __LINE__);
+            return SVTGPU_ERR_HIP;
+        }
+    }
     auto *c   = new SvtGpuComm();
     c->nranks = nranks, c->rank = rank, c->nccl = comm, c->device = ctx->device;
-    c->timeout_ms = default_timeout_ms();
+    c->timeout_ms = tmo, c->slot = slot;
+    c->nonblocking = !blocking;
     if (hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming) != hipSuccess) {
         svtgpu_comm_destroy(c);
         svtgpu_set_last_hip_error(hipErrorOutOfMemory, "comm event", __FILE__, __LINE__);
@@ -153,6 +208,11 @@ extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t ra
     }
     *out      = c;
     return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_comm_create(SvtGpuContext *ctx, int32_t nranks, int32_t rank,
+                                  const uint8_t id[SVTGPU_COMM_ID_BYTES], SvtGpuComm **out) {
+    return svtgpu_comm_create_bounded(ctx, nranks, rank, id, 0, -1, out);
 }
 
 extern "C" int svtgpu_comm_create_host(int32_t nranks, int32_t rank, const SvtGpuHostTransport *t, SvtGpuComm **out) {
@@ -220,6 +280,7 @@ int svtgpu_comm_wait(SvtGpuComm *c, hipStream_t st) {
     return SVTGPU_OK;
 }
 
+
 extern "C" int svtgpu_comm_sync(SvtGpuComm *c, void *stream) {
     if (!c) return SVTGPU_ERR_INVALID_ARG;
     if (c->failed) return comm_failed(c);
@@ -259,22 +320,30 @@ int svtgpu_comm_sum(SvtGpuComm *c, void *buf, size_t n, bool on_device, hipStrea
         }
         return SVTGPU_OK;
     }
+    // the ring slot of this exchange: an exchange 32 back not yet seen complete is waited for (bounded) first, before
+    // this one is enqueued (so the wait, and a timeout's message, concern the older exchange only)
+    XchRecord *slot = &c->ring[seq % XCH_RING];
+    if (slot->live)
+        if (int rc = svtgpu_comm_wait(c, slot->st)) return rc;
+    slot->live = false;
     void *d = buf;
     if (!on_device) {
         if (int rc = grow_dev(c, n)) return rc;
         HIP_TRY(hipMemcpyAsync(c->dev, buf, n * 8, hipMemcpyHostToDevice, st));
         d = c->dev;
     }
-    if (ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, st)) {
+    ncclResult_t r = ncclAllReduce(d, d, n, ncclUint64, ncclSum, c->nccl, st);
+    long long    waited = 0;
+    if (r == ncclInProgress && c->nonblocking) r = nccl_settle(c->nccl, r, c->timeout_ms, &waited);
+    if (r != ncclSuccess) {
+        XchRecord me;
+        me.what = what, me.seq = seq, me.words = n, me.st = st;
+        if (r == ncclInProgress) return comm_timeout(c, me, waited); // never enqueued within the deadline
         std::snprintf(c->fail_msg, sizeof c->fail_msg, "ncclAllReduce of the %s (exchange #%llu): %s", what,
                       (unsigned long long)seq, ncclGetErrorString(r));
         c->failed = true;
         return comm_failed(c);
     }
-    // the ring slot of this exchange: an exchange 32 back not yet seen complete is waited for (bounded) first
-    XchRecord *slot = &c->ring[seq % XCH_RING];
-    if (slot->live)
-        if (int rc = svtgpu_comm_wait(c, slot->st)) return rc;
     slot->st = st, slot->what = what, slot->seq = seq, slot->words = n, slot->live = true;
     if (!on_device) {
         HIP_TRY(hipMemcpyAsync(buf, c->dev, n * 8, hipMemcpyDeviceToHost, st));

@@ -1021,6 +1021,9 @@ extern "C" int svtgpu_dlf_set_crop(SvtGpuDlfState *s, int32_t crop_width, int32_
     if (!s || crop_width <= s->width - 8 || crop_width > s->width || crop_height <= s->height - 8 ||
         crop_height > s->height)
         return SVTGPU_ERR_INVALID_ARG; // the coded size is the crop rounded up to 8
+    // the edge records stop at the crop: records built for another crop are stale, so filter / pick refuse until the
+    // next svtgpu_dlf_set_mode_info(_device) rebuilds them
+    if (crop_width != s->crop_w || crop_height != s->crop_h) s->have_mi = 0;
     s->crop_w = crop_width, s->crop_h = crop_height;
     return SVTGPU_OK;
 }
@@ -1086,7 +1089,7 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
                    int32_t ps, int32_t pe, hipStream_t st) {
     if (s->mi_on_device) { // a device grid no pick has reported on (the FROM_Q levels): its verdict first
         s->mi_on_device = 0;
-        HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded when an exchange may sit before it
         if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
     }
     LevelTables L;
@@ -1179,7 +1182,7 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     if (rc) return rc;
     if (s->mi_on_device) { // the grid was checked by the records kernel: its verdict, once the stream has passed it
         s->mi_on_device = 0;
-        HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = svtgpu_comm_wait(s->comm, st)) return rc;
         if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
     }
     p.filter_level[0] = p.filter_level[1] = ys.best;
@@ -1225,7 +1228,7 @@ void lpf_shim(T *s, int32_t pitch, int vertical, int len, const uint8_t *blimit,
     uint16_t   lines[4 * 16] = {0};
     for (int l = 0; l < 4; l++) // only the samples the reference function touches
         for (int k = -h; k < h; k++) lines[l * 16 + 8 + k] = s[l * adv + k * step];
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     static thread_local uint16_t *d = nullptr;
     if (!d) HIP_OR_DIE(hipMalloc(&d, sizeof lines));
     HIP_OR_DIE(hipMemcpyAsync(d, lines, sizeof lines, hipMemcpyHostToDevice, st));

@@ -184,7 +184,7 @@ void stage_out(hipStream_t st, T *h, size_t first, const HostSpan &sp, size_t n_
 extern "C" void svtgpu_convert_8bit_to_16bit(uint8_t *src, uint32_t src_stride, uint16_t *dst, uint32_t dst_stride,
                                              uint32_t width, uint32_t height) {
     if (!width || !height) return;
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     HostSpan    a, b;
     const size_t ns = (size_t)(height - 1) * src_stride + width, nd = (size_t)(height - 1) * dst_stride + width;
     uint8_t     *ds = stage_in(st, a, src, 0, ns);
@@ -198,7 +198,7 @@ extern "C" void svtgpu_convert_8bit_to_16bit(uint8_t *src, uint32_t src_stride, 
 extern "C" void svtgpu_convert_16bit_to_8bit(uint16_t *src, uint32_t src_stride, uint8_t *dst, uint32_t dst_stride,
                                              uint32_t width, uint32_t height) {
     if (!width || !height) return;
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     HostSpan    a, b;
     const size_t ns = (size_t)(height - 1) * src_stride + width, nd = (size_t)(height - 1) * dst_stride + width;
     uint16_t    *ds = stage_in(st, a, src, 0, ns);
@@ -213,7 +213,7 @@ extern "C" void svtgpu_aom_generate_padding(uint8_t *src_pic, uint32_t src_strid
                                             uint32_t original_src_height, uint32_t padding_width,
                                             uint32_t padding_height) {
     if (!src_pic) return;
-    hipStream_t  st = svtgpu_default_stream();
+    hipStream_t  st = svtgpu_shim_stream();
     HostSpan     a;
     const size_t n  = (size_t)(original_src_height + 2 * padding_height) * src_stride;
     uint8_t     *d  = stage_in(st, a, src_pic, 0, n);
@@ -228,7 +228,7 @@ extern "C" void svtgpu_aom_generate_padding(uint8_t *src_pic, uint32_t src_strid
 extern "C" void svtgpu_aom_generate_padding16_bit(uint16_t *src_pic, uint32_t src_stride, uint32_t original_src_width,
                                                   uint32_t original_src_height, uint32_t padding_width,
                                                   uint32_t padding_height) {
-    hipStream_t  st = svtgpu_default_stream();
+    hipStream_t  st = svtgpu_shim_stream();
     HostSpan     a;
     const size_t n  = (size_t)(original_src_height + 2 * padding_height) * src_stride;
     uint16_t    *d  = stage_in(st, a, src_pic, 0, n);
@@ -242,7 +242,7 @@ extern "C" void svtgpu_aom_generate_padding16_bit(uint16_t *src_pic, uint32_t sr
 // svt_extend_frame (EbRestoration.c:197; highbd data is a CONVERT_TO_BYTEPTR pointer)
 extern "C" void svtgpu_extend_frame(uint8_t *data, int32_t width, int32_t height, int32_t stride, int32_t border_horz,
                                     int32_t border_vert, int32_t highbd) {
-    hipStream_t st    = svtgpu_default_stream();
+    hipStream_t st    = svtgpu_shim_stream();
     const size_t rows = (size_t)height + 2 * border_vert;
     // the touched span: from (-bv, -bh) to (h + bv - 1, w + bh - 1)
     const ptrdiff_t first = -(ptrdiff_t)border_vert * stride - border_horz;

@@ -373,6 +373,7 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) s->d_units[0] = nullptr;
     for (int p = 1; p < 3 && s->d_units[0]; p++) s->d_units[p] = s->d_units[p - 1] + s->hunits[p - 1] * s->vunits[p - 1];
+    if (e == hipSuccess && lr_make_wiener_stream(s) != SVTGPU_OK) e = hipErrorOutOfMemory;
     if (e != hipSuccess) {
         svtgpu_lr_state_destroy(s);
         svtgpu_set_last_hip_error(e, "lr state alloc", __FILE__, __LINE__);
@@ -394,6 +395,7 @@ extern "C" void svtgpu_lr_state_destroy(SvtGpuLrState *s) {
     if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
     if (s->ev_join) (void)hipEventDestroy(s->ev_join);
     if (s->h_pin) (void)hipHostFree(s->h_pin);
+    if (s->h_fout) (void)hipHostFree(s->h_fout);
     lr_profiler_destroy(s->prof);
     delete s;
 }
@@ -425,8 +427,7 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
     auto ok = [&](const SvtGpuFrame *f) {
         return lr_frame_fits(s, f) && f->bit_depth == cdef_out->bit_depth;
     };
-    if (!s || !cdef_out || !ok(cdef_out) || !ok(deblocked) || !ok(out) || !frame_type || out == cdef_out ||
-        out == deblocked)
+    if (!s || !cdef_out || !ok(cdef_out) || !ok(deblocked) || !ok(out) || out == cdef_out || out == deblocked)
         return SVTGPU_ERR_INVALID_ARG;
     if (cdef_out->bit_depth != 8 && cdef_out->bit_depth != 10) return SVTGPU_ERR_UNSUPPORTED;
     hipStream_t  st  = pick_stream(s->ctx, stream);
@@ -452,7 +453,9 @@ extern "C" int svtgpu_lr_apply_frame(SvtGpuLrState *s, const SvtGpuFrame *debloc
                                      cdef_out->stride[p] * bps,
                                      ((r[2] == pw ? cdef_out->pw[p] : r[2]) - r[0]) * bps, cdef_out->ph[p] - ph,
                                      hipMemcpyDeviceToDevice, st));
-        if (frame_type[p] == SVTGPU_RESTORE_NONE) {
+        // frame_type == nullptr: the units the last search left on the device (an asynchronous search's device finish:
+        // a plane whose frame type is NONE holds NONE units, which the kernel copies)
+        if (frame_type && frame_type[p] == SVTGPU_RESTORE_NONE) {
             const size_t io = ((size_t)r[1] * cdef_out->stride[p] + r[0]) * bps, oo = ((size_t)r[1] * out->stride[p] + r[0]) * bps;
             HIP_TRY(hipMemcpy2DAsync((uint8_t *)out->plane[p] + oo, out->stride[p] * bps,
                                      (const uint8_t *)cdef_out->plane[p] + io, cdef_out->stride[p] * bps,
@@ -529,7 +532,7 @@ void wiener_shim(const T *src, ptrdiff_t ss, T *dst, ptrdiff_t ds, const int16_t
     uint8_t  *d    = (uint8_t *)g_lr_buf.get(in.size() * 2 + (size_t)w * h * 2 + 64);
     uint16_t *di   = (uint16_t *)d, *dout = (uint16_t *)(d + in.size() * 2);
     int16_t  *dt   = (int16_t *)(d + in.size() * 2 + (size_t)w * h * 2);
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     HIP_OR_DIE(hipMemcpyAsync(di, in.data(), in.size() * 2, hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemcpyAsync(dt, taps, 32, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(wiener_shim_kernel, dim3(1), dim3(NTHR), 0, st, di, is, dout, w, h, dt, bd, r0, r1);
@@ -554,7 +557,7 @@ void sgr_shim(const T *src, int stride, int w, int h, int eps, const int32_t *xq
     uint16_t    *di = (uint16_t *)d;
     int32_t     *f0 = (int32_t *)(d + ((nb + 15) & ~15)), *f1 = f0 + no;
     uint16_t    *dout = (uint16_t *)(f1 + no);
-    hipStream_t  st   = svtgpu_default_stream();
+    hipStream_t  st   = svtgpu_shim_stream();
     HIP_OR_DIE(hipMemcpyAsync(di, in.data(), nb, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(sgr_shim_kernel, dim3(1), dim3(NTHR), 0, st, di, is, w, h, eps, bd, xqd ? xqd[0] : 0,
                        xqd ? xqd[1] : 0, mode, f0, f1, dout);

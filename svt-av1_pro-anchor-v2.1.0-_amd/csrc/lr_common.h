@@ -36,8 +36,14 @@ struct SvtGpuLrState {
     // written {x0, y0, x1, y1} per plane, the exchange of the search records (null: one rank)
     int32_t              tile_units[3][4], tile_out[3][4];
     SvtGpuComm          *comm;
+    // the device RD finish (round 6): its result words in mapped pinned memory, the sequence number of the last finish
+    // queued, whether its result has not been collected yet (svtgpu_lr_read_result), the last frame types collected
+    int32_t             *h_fout, *h_fout_dev;
+    int32_t              fin_seq, fin_pending;
+    int32_t              last_ft[3];
 };
 void lr_profiler_destroy(void *prof);
+int  lr_make_wiener_stream(SvtGpuLrState *s); // the search's Wiener-chain stream and its fork / join events
 // The restored area of a plane: the frame's crop size (frm_size.frame_width / _height; chroma rounded up, the
 // reference's crop_widths / crop_heights, EbPictureBufferDesc.c) -- the device frames themselves are the 8-aligned
 // coded size the deblocking and CDEF stages cover (mi_cols x 4)

@@ -46,7 +46,6 @@ struct URect {
     int32_t h_start, h_end, v_start, v_end;
 };
 constexpr int PRJ_MIN0 = -96, PRJ_MAX0 = 31, PRJ_MIN1 = -32, PRJ_MAX1 = 95;
-const int     kTapMin[3] = {-5, -23, -17}, kTapMax[3] = {10, 8, 46};
 const int     kHostSgrR[16][2] = {{2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1}, {2, 1},
                               {2, 1}, {2, 1}, {0, 1}, {0, 1}, {0, 1}, {0, 1}, {2, 0}, {2, 0}};
 // r = 1 s values of the sets (c_sgr_s[.][1]): eps 2/11, 5/12 and 8/13 share theirs, so their r = 1 filters are equal
@@ -783,13 +782,14 @@ __device__ int64_t compute_score(int win, WienerSolveLds &L, const int16_t *vf, 
     return (L.accQ - 2 * L.accP) - (L.H[(win2 >> 1) * win2 + (win2 >> 1)] - 2 * L.M[win2 >> 1]);
 }
 
-// rates (EbEntropyCoding.c:2876-3022, EbRestorationPick.c:655-668, 1008-1040)
-int count_quniform(int n, int v) {
+// rates (EbEntropyCoding.c:2876-3022, EbRestorationPick.c:655-668, 1008-1040); host and device (the RD finish runs
+// on either)
+__host__ __device__ inline int count_quniform(int n, int v) {
     if (n <= 1) return 0;
     const int l = 32 - __builtin_clz((unsigned)(n - 1)), m = (1 << l) - n;
     return v < m ? l - 1 : l;
 }
-int count_subexpfin(int n, int k, int v) {
+__host__ __device__ inline int count_subexpfin(int n, int k, int v) {
     int count = 0, i = 0, mk = 0;
     for (;;) {
         const int b = i ? k + i - 1 : k, a = 1 << b;
@@ -802,30 +802,47 @@ int count_subexpfin(int n, int k, int v) {
             return count + b;
     }
 }
-int refsubexpfin(int n, int k, int ref, int v) {
+__host__ __device__ inline int refsubexpfin(int n, int k, int ref, int v) {
     n &= 0xFFFF, ref &= 0xFFFF, v &= 0xFFFF;
-    auto recenter = [](int r, int x) { return x > (r << 1) ? x : x >= r ? (x - r) << 1 : ((r - x) << 1) - 1; };
-    const int rv = (ref << 1) <= n ? recenter(ref, v) : recenter(n - 1 - ref, n - 1 - v);
+    const int r = (ref << 1) <= n ? ref : n - 1 - ref, x = (ref << 1) <= n ? v : n - 1 - v; // recentering
+    const int rv = x > (r << 1) ? x : x >= r ? (x - r) << 1 : ((r - x) << 1) - 1;
     return count_subexpfin(n, k, rv & 0xFFFF);
 }
-int wiener_bits(int win, const SvtGpuRestUnit &w, const SvtGpuRestUnit &ref) {
-    static const int K[3] = {1, 2, 3};
-    int              bits = 0;
+// WIENER_FILT_TAP{0,1,2}_{MINV,MAXV} (EbDefinitions.h) and the self-guided sets with an r = 0 / r = 1 pass
+__host__ __device__ inline int tap_min(int t) { return t == 0 ? -5 : t == 1 ? -23 : -17; }
+__host__ __device__ inline int tap_max(int t) { return t == 0 ? 10 : t == 1 ? 8 : 46; }
+__host__ __device__ inline bool sgr_r0(int ep) { return ep < 10 || ep > 13; } // c_sgr_r[ep][0] > 0
+__host__ __device__ inline bool sgr_r1(int ep) { return ep < 14; }            // c_sgr_r[ep][1] > 0
+__host__ __device__ inline int wiener_bits(int win, const SvtGpuRestUnit &w, const SvtGpuRestUnit &ref) {
+    int bits = 0;
     for (int f = 0; f < 2; f++) {
         const int16_t *a = f ? w.hfilter : w.vfilter, *r = f ? ref.hfilter : ref.vfilter;
         for (int t = win == 7 ? 0 : 1; t < 3; t++)
-            bits += refsubexpfin(kTapMax[t] - kTapMin[t] + 1, K[t], r[t] - kTapMin[t], a[t] - kTapMin[t]);
+            bits += refsubexpfin(tap_max(t) - tap_min(t) + 1, t + 1, r[t] - tap_min(t), a[t] - tap_min(t));
     }
     return bits;
 }
-int sgrproj_bits(const SvtGpuRestUnit &s, const SvtGpuRestUnit &ref) {
+__host__ __device__ inline int sgrproj_bits(const SvtGpuRestUnit &s, const SvtGpuRestUnit &ref) {
     int bits = 4;
-    if (kHostSgrR[s.ep][0] > 0) bits += refsubexpfin(PRJ_MAX0 - PRJ_MIN0 + 1, 4, ref.xqd[0] - PRJ_MIN0, s.xqd[0] - PRJ_MIN0);
-    if (kHostSgrR[s.ep][1] > 0) bits += refsubexpfin(PRJ_MAX1 - PRJ_MIN1 + 1, 4, ref.xqd[1] - PRJ_MIN1, s.xqd[1] - PRJ_MIN1);
+    if (sgr_r0(s.ep)) bits += refsubexpfin(PRJ_MAX0 - PRJ_MIN0 + 1, 4, ref.xqd[0] - PRJ_MIN0, s.xqd[0] - PRJ_MIN0);
+    if (sgr_r1(s.ep)) bits += refsubexpfin(PRJ_MAX1 - PRJ_MIN1 + 1, 4, ref.xqd[1] - PRJ_MIN1, s.xqd[1] - PRJ_MIN1);
     return bits;
 }
-double rdcost(int rdmult, int64_t bits, int64_t sse) { // RDCOST_DBL (EbRestoration.h:346-347)
+// RDCOST_DBL (EbRestoration.h:346-347); the library is built with -ffp-contract=off, so host and device round alike
+__host__ __device__ inline double rdcost(int rdmult, int64_t bits, int64_t sse) {
     return ((double)bits * rdmult) / (double)(1 << 9) + (double)sse * (1 << 7);
+}
+// set_default_wiener / set_default_sgrproj (EbRestorationPick.c rsc_on_tile): the first unit's reference
+__host__ __device__ inline SvtGpuRestUnit default_wiener() {
+    SvtGpuRestUnit r{};
+    const int16_t  mid[7] = {3, -7, 15, -22, 15, -7, 3};
+    for (int k = 0; k < 7; k++) r.vfilter[k] = r.hfilter[k] = mid[k];
+    return r;
+}
+__host__ __device__ inline SvtGpuRestUnit default_sgrproj() {
+    SvtGpuRestUnit r{};
+    r.xqd[0] = (PRJ_MIN0 + PRJ_MAX0) / 2, r.xqd[1] = (PRJ_MIN1 + PRJ_MAX1) / 2;
+    return r;
 }
 
 // Resumable coordinate descent shared by finer_tile_search_wiener_seg (EbRestorationPick.c:1042-1146) and
@@ -2291,67 +2308,86 @@ struct PlanePlan {
     std::vector<int32_t> eps;
 };
 
-// rest_finish_search (EbRestorationPick.c:1555-1634) of one plane over its per-unit search results
-void finish_plane(const SvtGpuLrSearchControls *c, int p, int win, const SvtGpuLrUnitSearch *rs, int n,
-                  int32_t *frame_type, SvtGpuRestUnit *out) {
+int plane_win(const SvtGpuLrSearchControls *c, int p) {
+    const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
+    return p == 0 ? win_l : std::min(win_l, 5);
+}
+
+// RestUnitSearchInfo as rest_finish_search uses it (EbRestoration.h:349-360): best[] = best_rtype[WIENER - 1 ..
+// SWITCHABLE - 1]
+struct FinRusi {
+    int64_t        sse[3];
+    SvtGpuRestUnit wiener, sgrproj;
+    int32_t        best[3];
+};
+// which finish passes of rest_finish_search run for plane p (force_restore_type_d and the per-plane skips,
+// EbRestorationPick.c:1558-1560, 1597-1610): r 0 always; num_rtypes = 4 only with more than one unit
+inline bool finish_runs(const SvtGpuLrSearchControls *c, int p, int n, int r) {
     const int force = c->wn_enabled ? (c->sg_enabled ? 4 : 1) : (c->sg_enabled ? 2 : 0);
-    const int nrt   = n > 1 ? 4 : 3;
-    std::vector<int>            brt((size_t)3 * n, 0);
-    std::vector<SvtGpuRestUnit> uw(n), us(n);
-    double                      best_cost = 0;
-    int                         best_type = 0;
-    static const int16_t        kMid[7]   = {3, -7, 15, -22, 15, -7, 3}; // set_default_wiener
-    for (int r = 0; r < nrt; r++) {
-        if (force != 4 && r != 0 && r != force) continue;
-        if (p && ((r == 1 && !c->wn_use_chroma) || (r == 2 && !c->sg_use_chroma))) continue;
-        SvtGpuRestUnit refw, refs;
-        std::memset(&refw, 0, sizeof refw);
-        std::memset(&refs, 0, sizeof refs);
-        for (int k = 0; k < 7; k++) refw.vfilter[k] = refw.hfilter[k] = kMid[k];
-        refs.xqd[0] = (PRJ_MIN0 + PRJ_MAX0) / 2, refs.xqd[1] = (PRJ_MIN1 + PRJ_MAX1) / 2;
-        int64_t sse = 0, bits = 0;
+    if (r == 3 && n <= 1) return false;
+    if (force != 4 && r != 0 && r != force) return false;
+    if (p && ((r == 1 && !c->wn_use_chroma) || (r == 2 && !c->sg_use_chroma))) return false;
+    return true;
+}
+
+// rest_finish_search (EbRestorationPick.c:1555-1634) of plane p over its per-unit search records, on the host.  `rusi`
+// is the reference's per-unit array, allocated once per frame (luma's unit count) and shared by the planes: each pass
+// overwrites only what it computes, so a chroma plane's switchable pass reads luma's best_rtype / sse / wiener (or
+// sgrproj) entries for a type that chroma does not search (search_switchable :1148-1200, copy_unit_info :1202-1209).
+// Planes run in order 0, 1, 2 over the same array.
+void finish_plane_shared(const SvtGpuLrSearchControls *c, int p, int win, const SvtGpuLrUnitSearch *rs, int n,
+                         FinRusi *rusi, int32_t *frame_type, SvtGpuRestUnit *out) {
+    double best_cost = 0;
+    int    best_type = 0;
+    for (int r = 0; r < 4; r++) {
+        if (!finish_runs(c, p, n, r)) continue;
+        SvtGpuRestUnit refw = default_wiener(), refs = default_sgrproj(); // rsc_on_tile
+        int64_t        sse = 0, bits = 0;
         for (int u = 0; u < n; u++) {
             const SvtGpuLrUnitSearch &R = rs[u];
-            if (r == 0) {
-                sse += R.sse[0];
+            FinRusi                  &Q = rusi[u];
+            if (r == 0) { // search_norestore_finish
+                Q.sse[0] = R.sse[0];
+                sse += Q.sse[0];
             } else if (r == 1) { // search_wiener_finish
                 const int64_t bn = c->wiener_restore_cost[0];
-                if (R.sse[1] == INT64_MAX) {
-                    bits += bn, sse += R.sse[0], brt[3 * u] = 0;
+                Q.sse[1]         = R.sse[1];
+                if (Q.sse[1] == INT64_MAX) {
+                    bits += bn, sse += Q.sse[0], Q.best[0] = 0;
                     continue;
                 }
-                uw[u]            = R.wiener;
-                const int64_t bw = c->wiener_restore_cost[1] + ((int64_t)wiener_bits(win, R.wiener, refw) << 9);
-                const bool    t  = rdcost(c->rdmult, bw >> 4, R.sse[1]) < rdcost(c->rdmult, bn >> 4, R.sse[0]);
-                brt[3 * u]       = t ? 1 : 0;
-                sse += R.sse[t ? 1 : 0];
+                Q.wiener         = R.wiener;
+                const int64_t bw = c->wiener_restore_cost[1] + ((int64_t)wiener_bits(win, Q.wiener, refw) << 9);
+                const bool    t  = rdcost(c->rdmult, bw >> 4, Q.sse[1]) < rdcost(c->rdmult, bn >> 4, Q.sse[0]);
+                Q.best[0]        = t ? 1 : 0;
+                sse += Q.sse[t ? 1 : 0];
                 bits += t ? bw : bn;
-                if (t) refw = R.wiener;
+                if (t) refw = Q.wiener;
             } else if (r == 2) { // search_sgrproj_finish
-                us[u]            = R.sgrproj;
+                Q.sse[2] = R.sse[2], Q.sgrproj = R.sgrproj;
                 const int64_t bn = c->sgrproj_restore_cost[0];
-                const int64_t bs = c->sgrproj_restore_cost[1] + ((int64_t)sgrproj_bits(R.sgrproj, refs) << 9);
-                const bool    t  = rdcost(c->rdmult, bs >> 4, R.sse[2]) < rdcost(c->rdmult, bn >> 4, R.sse[0]);
-                brt[3 * u + 1]   = t ? 2 : 0;
-                sse += R.sse[t ? 2 : 0];
+                const int64_t bs = c->sgrproj_restore_cost[1] + ((int64_t)sgrproj_bits(Q.sgrproj, refs) << 9);
+                const bool    t  = rdcost(c->rdmult, bs >> 4, Q.sse[2]) < rdcost(c->rdmult, bn >> 4, Q.sse[0]);
+                Q.best[1]        = t ? 2 : 0;
+                sse += Q.sse[t ? 2 : 0];
                 bits += t ? bs : bn;
-                if (t) refs = R.sgrproj;
+                if (t) refs = Q.sgrproj;
             } else { // search_switchable (7 / 5 Wiener taps by plane)
                 double  bc = 0;
                 int64_t bb = 0;
                 int     bt = 0;
                 for (int t = 0; t < 3; t++) {
-                    if (t > 0 && brt[3 * u + t - 1] == 0) continue;
-                    const int64_t cp = t == 1 ? wiener_bits(p == 0 ? 7 : 5, uw[u], refw) : t == 2 ? sgrproj_bits(us[u], refs) : 0;
+                    if (t > 0 && Q.best[t - 1] == 0) continue;
+                    const int64_t cp = t == 1 ? wiener_bits(p == 0 ? 7 : 5, Q.wiener, refw) : t == 2 ? sgrproj_bits(Q.sgrproj, refs) : 0;
                     const int64_t b  = c->switchable_restore_cost[t] + (cp << 9);
-                    const double  cost = rdcost(c->rdmult, b >> 4, R.sse[t]);
+                    const double  cost = rdcost(c->rdmult, b >> 4, Q.sse[t]);
                     if (t == 0 || cost < bc) bc = cost, bb = b, bt = t;
                 }
-                brt[3 * u + 2] = bt;
-                sse += R.sse[bt];
+                Q.best[2] = bt;
+                sse += Q.sse[bt];
                 bits += bb;
-                if (bt == 1) refw = uw[u];
-                if (bt == 2) refs = us[u];
+                if (bt == 1) refw = Q.wiener;
+                if (bt == 2) refs = Q.sgrproj;
             }
         }
         const double cost = rdcost(c->rdmult, bits >> 4, sse);
@@ -2361,10 +2397,343 @@ void finish_plane(const SvtGpuLrSearchControls *c, int p, int win, const SvtGpuL
     for (int u = 0; u < n; u++) { // copy_unit_info
         std::memset(&out[u], 0, sizeof out[u]);
         if (best_type) {
-            const int t = brt[3 * u + best_type - 1];
-            out[u]      = t == 1 ? uw[u] : us[u];
+            const int t = rusi[u].best[best_type - 1];
+            out[u]      = t == 1 ? rusi[u].wiener : rusi[u].sgrproj;
             out[u].type = t;
         }
+    }
+}
+
+// the whole frame's finish on the host: planes [0, nplanes) in order over one shared array
+void finish_frame_host(const SvtGpuLrSearchControls *c, int nplanes, const int32_t *n, const SvtGpuLrUnitSearch *const *rs,
+                       int32_t *frame_type, SvtGpuRestUnit *const *out) {
+    std::vector<FinRusi> rusi((size_t)std::max(1, n[0]));
+    std::memset(rusi.data(), 0, sizeof(FinRusi) * rusi.size());
+    for (int p = 0; p < nplanes; p++)
+        finish_plane_shared(c, p, plane_win(c, p), rs[p], n[p], rusi.data(), &frame_type[p], out[p]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rest_finish_search on the device (round 6; the host form above stays behind SVTGPU_LR_FINISH=host).
+// The reference's finish is sequential over a plane's units because every unit's Wiener / self-guided rate is coded
+// against the last unit that took that filter (rsc->wiener / rsc->sgrproj).  A lane stepping that chain with the
+// rate arithmetic inside would be slower than the host; instead
+//   lr_records_kernel      the per-unit records (SvtGpuLrUnitSearch) from the search's device results -- what the host
+//                          read-back assembled -- into one array of all planes' units (the gather a tiled picture
+//                          all-reduces);
+//   lr_fin_tables_kernel   one wave per unit evaluates, for every reference the chain can hold at that unit (the 63
+//                          units before it and the default), the pass's decision: search_wiener_finish /
+//                          search_sgrproj_finish as bits of a 64-bit mask, search_switchable as a 2-bit choice for
+//                          each of 16 x 16 (Wiener reference, self-guided reference) pairs (15 units back + default);
+//   lr_fin_walk_kernel     one workgroup walks the chains -- per unit a mask bit (a table entry) selected by how far
+//                          back the reference is, a few scalar instructions -- evaluating a decision directly only when
+//                          the reference lies outside the tabulated window; then the per-unit rates of the taken path
+//                          in parallel, each pass's frame cost, the frame types and copy_unit_info into the state's
+//                          units.  The decisions are the reference's own comparisons (RDCOST_DBL in double,
+//                          -ffp-contract=off), so the walk takes exactly the reference's path.
+// The shared RestUnitSearchInfo array (finish_plane_shared) is modelled by reading luma's entries for a type a chroma
+// plane does not search.
+// ---------------------------------------------------------------------------------------------
+constexpr int FIN_K1 = 63; // r = 1 / 2 masks: bit k < 63 = the unit k + 1 back as the reference, bit 63 = the default
+constexpr int FIN_K3 = 15; // switchable tables: kw, ks < 15 = that many + 1 back, 15 = the default
+constexpr int FIN_T3 = 17; // words per unit: 16 x 16 two-bit choices (word kw, bits 2 ks), then T10 | T01 << 16
+constexpr int FIN_OUT = 8; // device result words: frame types [3], search status, sequence
+
+struct RecArgs {
+    int32_t                   nplanes, n_all, wn[3], sg[3];
+    const unsigned long long *sse0, *sse2;
+    const SvtGpuRestUnit     *wu;
+    const Descent            *wds;
+    const int32_t            *best, *raw;
+    const int32_t            *dst; // record index of every searched unit
+    SvtGpuLrUnitSearch       *rec;
+};
+__global__ __launch_bounds__(256) void lr_records_kernel(const SearchArgs A, const RecArgs R) {
+    const int gu = blockIdx.x * 256 + threadIdx.x;
+    if (gu >= R.n_all) return;
+    int p = 0;
+    while (p + 1 < R.nplanes && gu >= A.pl[p + 1].unit_base) p++;
+    SvtGpuLrUnitSearch o;
+    memset(&o, 0, sizeof o);
+    o.sse[0] = (int64_t)R.sse0[gu];
+    o.sse[1] = INT64_MAX;
+    if (R.wn[p] && R.wu[gu].type) {
+        const Descent &d = R.wds[gu];
+        o.sse[1]         = d.err;
+        o.wiener         = R.wu[gu];
+        int v[3];
+        d.taps(0, v), set_wiener_taps(o.wiener.hfilter, v);
+        d.taps(1, v), set_wiener_taps(o.wiener.vfilter, v);
+    }
+    if (R.sg[p]) { // sgr_best_kernel: the first ep of least error and its descent's two values
+        o.sgrproj.type   = SVTGPU_RESTORE_SGRPROJ;
+        o.sgrproj.ep     = A.pl[p].eps[R.best[4 * gu]];
+        o.sgrproj.xqd[0] = R.raw[2 * gu], o.sgrproj.xqd[1] = R.raw[2 * gu + 1];
+        o.sse[2]         = (int64_t)R.sse2[gu];
+    }
+    R.rec[R.dst[gu]] = o;
+}
+
+struct FinPlane {
+    int32_t n, base;   // units of the plane; its first record (and table entry)
+    int32_t run[4];    // the finish passes that run (finish_runs)
+    int32_t win1;      // search_wiener_finish's window (plane_win); search_switchable uses 7 luma / 5 chroma
+    int32_t own1, own2; // the shared rusi's Wiener / self-guided entries are this plane's own (else luma's)
+};
+struct FinArgs {
+    FinPlane                  pl[3];
+    int32_t                   nplanes, nrec, rdmult, sw[3], wn[2], sg[2];
+    const SvtGpuLrUnitSearch *rec;
+    unsigned long long       *m1, *m2;
+    uint32_t                 *t3;
+    int32_t                  *path;   // [4][nrec]: r 1, r 2, r 3 (Wiener ref), r 3 (self-guided ref): choice | (ref + 1) << 2
+    SvtGpuRestUnit           *units;  // the state's units (d_units[0]: the planes back to back, the records' layout)
+    int32_t                  *out;    // [FIN_OUT] device results
+    int32_t                  *out_host; // mapped pinned copy
+    const int32_t            *wstat, *sstat; // the descents' status words (wiener_res / sgr_res) or null
+    int32_t                   seq;
+};
+
+// the shared rusi entries of unit u of plane p a switchable pass and copy_unit_info read
+__device__ inline const SvtGpuLrUnitSearch &fin_rec(const FinArgs &F, int p, int u) { return F.rec[F.pl[p].base + u]; }
+__device__ inline const SvtGpuLrUnitSearch &fin_w(const FinArgs &F, int p, int u) { return fin_rec(F, F.pl[p].own1 ? p : 0, u); }
+__device__ inline const SvtGpuLrUnitSearch &fin_s(const FinArgs &F, int p, int u) { return fin_rec(F, F.pl[p].own2 ? p : 0, u); }
+
+// search_wiener_finish's decision at unit u with the reference unit `ref` (-1: the default)
+__device__ bool fin_accept1(const FinArgs &F, int p, int u, int ref) {
+    const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
+    if (R.sse[1] == INT64_MAX) return false;
+    const SvtGpuRestUnit rw = ref < 0 ? default_wiener() : fin_rec(F, p, ref).wiener;
+    const int64_t        bw = F.wn[1] + ((int64_t)wiener_bits(F.pl[p].win1, R.wiener, rw) << 9);
+    return rdcost(F.rdmult, bw >> 4, R.sse[1]) < rdcost(F.rdmult, (int64_t)F.wn[0] >> 4, R.sse[0]);
+}
+// search_sgrproj_finish's decision
+__device__ bool fin_accept2(const FinArgs &F, int p, int u, int ref) {
+    const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
+    const SvtGpuRestUnit      rs = ref < 0 ? default_sgrproj() : fin_rec(F, p, ref).sgrproj;
+    const int64_t             bs = F.sg[1] + ((int64_t)sgrproj_bits(R.sgrproj, rs) << 9);
+    return rdcost(F.rdmult, bs >> 4, R.sse[2]) < rdcost(F.rdmult, (int64_t)F.sg[0] >> 4, R.sse[0]);
+}
+// search_switchable's costs of types 1 and 2 against the references rw / rs
+__device__ double fin_c1(const FinArgs &F, int p, int u, int rw) {
+    const SvtGpuRestUnit r = rw < 0 ? default_wiener() : fin_w(F, p, rw).wiener;
+    const int64_t        b = F.sw[1] + ((int64_t)wiener_bits(p == 0 ? 7 : 5, fin_w(F, p, u).wiener, r) << 9);
+    return rdcost(F.rdmult, b >> 4, fin_w(F, p, u).sse[1]);
+}
+__device__ double fin_c2(const FinArgs &F, int p, int u, int rs) {
+    const SvtGpuRestUnit r = rs < 0 ? default_sgrproj() : fin_s(F, p, rs).sgrproj;
+    const int64_t        b = F.sw[2] + ((int64_t)sgrproj_bits(fin_s(F, p, u).sgrproj, r) << 9);
+    return rdcost(F.rdmult, b >> 4, fin_s(F, p, u).sse[2]);
+}
+__device__ inline double fin_c0(const FinArgs &F, int p, int u) {
+    return rdcost(F.rdmult, (int64_t)F.sw[0] >> 4, fin_rec(F, p, u).sse[0]);
+}
+// the choice (t == 0 || cost < best, in type order) with types 1 / 2 allowed by a1 / a2
+__device__ inline int fin_pick(double c0, double c1, double c2, bool a1, bool a2) {
+    int    bt = 0;
+    double bc = c0;
+    if (a1 && c1 < bc) bt = 1, bc = c1;
+    if (a2 && c2 < bc) bt = 2;
+    return bt;
+}
+
+__global__ __launch_bounds__(64) void lr_fin_tables_kernel(const FinArgs F) {
+    __shared__ double c1s[FIN_K3 + 1], c2s[FIN_K3 + 1];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    int       p = 0;
+    while (p + 1 < F.nplanes && b >= F.pl[p + 1].base) p++;
+    const FinPlane &P = F.pl[p];
+    const int       u = b - P.base;
+    if (u >= P.n) return;
+    for (int r = 1; r <= 2; r++) {
+        if (!P.run[r]) continue;
+        const int  ref = lane < FIN_K1 ? u - 1 - lane : -1;
+        const bool a   = (lane == FIN_K1 || ref >= 0) && (r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref));
+        const unsigned long long m = __ballot(a);
+        if (lane == 0) (r == 1 ? F.m1 : F.m2)[b] = m;
+    }
+    if (!P.run[3]) return;
+    if (lane <= FIN_K3) {
+        const int rw = lane < FIN_K3 ? u - 1 - lane : -1;
+        c1s[lane]    = (lane == FIN_K3 || rw >= 0) ? fin_c1(F, p, u, rw) : 0.0;
+    } else if (lane >= 32 && lane <= 32 + FIN_K3) {
+        const int k = lane - 32, rs = k < FIN_K3 ? u - 1 - k : -1;
+        c2s[k]      = (k == FIN_K3 || rs >= 0) ? fin_c2(F, p, u, rs) : 0.0;
+    }
+    __syncthreads();
+    const double c0 = fin_c0(F, p, u);
+    uint32_t    *T  = F.t3 + (size_t)b * FIN_T3;
+    if (lane <= FIN_K3) { // word kw = lane: the choices with both types allowed, ks = 0..15
+        uint32_t w = 0;
+        for (int ks = 0; ks <= FIN_K3; ks++) w |= (uint32_t)fin_pick(c0, c1s[lane], c2s[ks], true, true) << (2 * ks);
+        T[lane] = w;
+    } else if (lane == FIN_K3 + 1) { // one type allowed: bit kw of T10 (type 1), bit ks of T01 (type 2)
+        uint32_t w = 0;
+        for (int k = 0; k <= FIN_K3; k++) {
+            w |= (uint32_t)(fin_pick(c0, c1s[k], 0.0, true, false) == 1) << k;
+            w |= (uint32_t)(fin_pick(c0, 0.0, c2s[k], false, true) == 2) << (16 + k);
+        }
+        T[FIN_T3 - 1] = w;
+    }
+}
+
+// a wave-uniform 64-bit value held by lane i of v
+__device__ inline unsigned long long lane_u64(unsigned long long v, int i) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, i);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), i);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// the r = 1 / r = 2 chain of plane p (one wave): path[u] = decision | (reference + 1) << 2
+__device__ void fin_walk12(const FinArgs &F, int p, int r, int lane) {
+    const FinPlane           &P    = F.pl[p];
+    const unsigned long long *M    = (r == 1 ? F.m1 : F.m2) + P.base;
+    int32_t                  *path = F.path + (size_t)(r - 1) * F.nrec + P.base;
+    int                       ref  = -1;
+    for (int u0 = 0; u0 < P.n; u0 += 64) {
+        const unsigned long long mv = u0 + lane < P.n ? M[u0 + lane] : 0ull;
+        const int                nl = min(64, P.n - u0);
+        for (int i = 0; i < nl; i++) {
+            const int u = u0 + i;
+            bool      a;
+            if (ref < 0 || u - 1 - ref < FIN_K1) {
+                const int k = ref < 0 ? FIN_K1 : u - 1 - ref;
+                a           = (lane_u64(mv, i) >> k) & 1;
+            } else { // the reference lies outside the tabulated window: the decision itself
+                a = r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref);
+            }
+            if (lane == 0) path[u] = (int32_t)a | ((ref + 1) << 2);
+            if (a) ref = u;
+        }
+    }
+}
+
+// the switchable chain of plane p (one wave): path[2][u] / path[3][u] = choice | (Wiener / self-guided ref + 1) << 2
+__device__ void fin_walk3(const FinArgs &F, int p, int lane) {
+    const FinPlane &P  = F.pl[p];
+    const uint32_t *T  = F.t3 + (size_t)P.base * FIN_T3;
+    const int32_t  *d1 = F.path + F.pl[P.own1 ? p : 0].base, *d2 = F.path + F.nrec + F.pl[P.own2 ? p : 0].base;
+    int32_t        *pw = F.path + 2 * (size_t)F.nrec + P.base, *ps = F.path + 3 * (size_t)F.nrec + P.base;
+    int             rw = -1, rs = -1;
+    for (int u0 = 0; u0 < P.n; u0 += 64) {
+        const int nl = min(64, P.n - u0);
+        const int a1v = lane < nl ? d1[u0 + lane] & 1 : 0, a2v = lane < nl ? d2[u0 + lane] & 1 : 0;
+        uint32_t  row = lane < FIN_T3 ? T[(size_t)u0 * FIN_T3 + lane] : 0u;
+        for (int i = 0; i < nl; i++) {
+            const int      u   = u0 + i;
+            const uint32_t cur = row;
+            if (i + 1 < nl) row = lane < FIN_T3 ? T[(size_t)(u + 1) * FIN_T3 + lane] : 0u; // the next unit's row
+            const bool a1 = __builtin_amdgcn_readlane(a1v, i) != 0, a2 = __builtin_amdgcn_readlane(a2v, i) != 0;
+            const int  kw = rw < 0 ? FIN_K3 : u - 1 - rw, ks = rs < 0 ? FIN_K3 : u - 1 - rs;
+            int        bt;
+            if (kw <= FIN_K3 && ks <= FIN_K3 && (rw < 0 || kw < FIN_K3) && (rs < 0 || ks < FIN_K3)) {
+                if (a1 && a2)
+                    bt = ((uint32_t)__builtin_amdgcn_readlane((int)cur, kw) >> (2 * ks)) & 3;
+                else if (a1 || a2) {
+                    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cur, FIN_T3 - 1);
+                    bt               = a1 ? ((w >> kw) & 1) : ((w >> (16 + ks)) & 1) ? 2 : 0;
+                } else
+                    bt = 0;
+            } else { // a reference outside the window: the costs themselves
+                bt = fin_pick(fin_c0(F, p, u), a1 ? fin_c1(F, p, u, rw) : 0.0, a2 ? fin_c2(F, p, u, rs) : 0.0, a1, a2);
+            }
+            if (lane == 0) pw[u] = bt | ((rw + 1) << 2), ps[u] = bt | ((rs + 1) << 2);
+            if (bt == 1) rw = u;
+            if (bt == 2) rs = u;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void lr_fin_walk_kernel(const FinArgs F) {
+    __shared__ unsigned long long acc[3][4][2]; // per plane and pass: sse, bits
+    __shared__ int32_t            ft[3];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    if (tid < 24) (&acc[0][0][0])[tid] = 0;
+    // the r = 1 / 2 chains (wave w: plane w; independent of each other), then the switchable chains (which read the
+    // r = 1 / 2 outcomes, luma's for a type chroma does not search)
+    if (wv < F.nplanes)
+        for (int r = 1; r <= 2; r++)
+            if (F.pl[wv].run[r]) fin_walk12(F, wv, r, lane);
+    __syncthreads();
+    if (wv < F.nplanes && F.pl[wv].run[3]) fin_walk3(F, wv, lane);
+    __syncthreads();
+    // the rate and distortion of every unit on each pass's path, summed per (plane, pass)
+    for (int p = 0; p < F.nplanes; p++) {
+        const FinPlane &P = F.pl[p];
+        for (int i = tid; i < 4 * P.n; i += 256) {
+            const int r = i / P.n, u = i - r * P.n;
+            if (!P.run[r]) continue;
+            const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
+            int64_t                   sse = 0, bits = 0;
+            if (r == 0) {
+                sse = R.sse[0];
+            } else if (r <= 2) {
+                const int32_t q = F.path[(size_t)(r - 1) * F.nrec + P.base + u];
+                const int     ref = (q >> 2) - 1;
+                if (!(q & 1)) {
+                    sse = R.sse[0], bits = r == 1 ? F.wn[0] : F.sg[0];
+                } else if (r == 1) {
+                    const SvtGpuRestUnit rw = ref < 0 ? default_wiener() : fin_rec(F, p, ref).wiener;
+                    sse = R.sse[1], bits = F.wn[1] + ((int64_t)wiener_bits(P.win1, R.wiener, rw) << 9);
+                } else {
+                    const SvtGpuRestUnit rs = ref < 0 ? default_sgrproj() : fin_rec(F, p, ref).sgrproj;
+                    sse = R.sse[2], bits = F.sg[1] + ((int64_t)sgrproj_bits(R.sgrproj, rs) << 9);
+                }
+            } else {
+                const int32_t qw = F.path[2 * (size_t)F.nrec + P.base + u], qs = F.path[3 * (size_t)F.nrec + P.base + u];
+                const int     bt = qw & 3, rw = (qw >> 2) - 1, rs = (qs >> 2) - 1;
+                int64_t       cp = 0;
+                if (bt == 1) {
+                    const SvtGpuRestUnit r0 = rw < 0 ? default_wiener() : fin_w(F, p, rw).wiener;
+                    cp = wiener_bits(p == 0 ? 7 : 5, fin_w(F, p, u).wiener, r0), sse = fin_w(F, p, u).sse[1];
+                } else if (bt == 2) {
+                    const SvtGpuRestUnit r0 = rs < 0 ? default_sgrproj() : fin_s(F, p, rs).sgrproj;
+                    cp = sgrproj_bits(fin_s(F, p, u).sgrproj, r0), sse = fin_s(F, p, u).sse[2];
+                } else {
+                    sse = R.sse[0];
+                }
+                bits = F.sw[bt] + (cp << 9);
+            }
+            atomicAdd(&acc[p][r][0], (unsigned long long)sse);
+            atomicAdd(&acc[p][r][1], (unsigned long long)bits);
+        }
+    }
+    __syncthreads();
+    if (tid < 3) { // each pass's frame cost; the first of least cost (r == 0 || cost < best)
+        int best = 0;
+        if (tid < F.nplanes) {
+            double bc = 0;
+            for (int r = 0; r < 4; r++) {
+                if (!F.pl[tid].run[r]) continue;
+                const double c = rdcost(F.rdmult, (int64_t)acc[tid][r][1] >> 4, (int64_t)acc[tid][r][0]);
+                if (r == 0 || c < bc) bc = c, best = r;
+            }
+        }
+        ft[tid] = best;
+    }
+    __syncthreads();
+    // copy_unit_info into the state's units (every plane; zero where the frame type is NONE)
+    for (int p = 0; p < 3; p++) {
+        const FinPlane &P = F.pl[p];
+        for (int u = tid; u < P.n; u += 256) {
+            SvtGpuRestUnit o;
+            memset(&o, 0, sizeof o);
+            if (p < F.nplanes && ft[p]) {
+                const int32_t q = F.path[(size_t)(ft[p] - 1) * F.nrec + P.base + u];
+                const int     t = ft[p] == 3 ? (q & 3) : (q & 1) ? ft[p] : 0;
+                o               = t == 1 ? fin_w(F, p, u).wiener : fin_s(F, p, u).sgrproj;
+                o.type          = t;
+            }
+            F.units[P.base + u] = o;
+        }
+    }
+    if (tid < FIN_OUT) {
+        const int32_t v = tid < 3   ? ft[tid]
+                        : tid == 3 ? (F.wstat && *F.wstat ? 1 : 0) | (F.sstat && *F.sstat ? 2 : 0)
+                        : tid == 4 ? F.seq
+                                   : 0;
+        F.out[tid] = v;
+        if (F.out_host) __hip_atomic_store(&F.out_host[tid], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2448,7 +2817,7 @@ int stats_unit_mfma(int win, const T *dgd, const T *src, int h_start, int h_end,
         cap = c.off;
     }
     uint8_t    *d  = (uint8_t *)buf;
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     const int32_t t0[2] = {0, nt};
     HIP_TRY(hipMemcpyAsync(d + o_d, fd.data(), sizeof(T) * fd.size(), hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d + o_s, fs.data(), sizeof(T) * fs.size(), hipMemcpyHostToDevice, st));
@@ -2484,17 +2853,50 @@ int stats_unit_mfma(int win, const T *dgd, const T *src, int h_start, int h_end,
 }
 
 // plane p's Wiener window for the controls
-int plane_win(const SvtGpuLrSearchControls *c, int p) {
-    const int win_l = c->wn_filter_tap_lvl == 1 ? 7 : c->wn_filter_tap_lvl == 2 ? 5 : 3;
-    return p == 0 ? win_l : std::min(win_l, 5);
-}
 
 // The search of the units in unit rows [rb[p], re[p]) of planes 0..nplanes-1.  frame_type != nullptr: the band
 // is the whole frame and the RD finish runs and sets the state's units.
+// waits for the last device finish queued on `st` (bounded when an exchange sits before it) and returns its frame
+// types, or the failure a resident descent reported (status words copied by lr_fin_walk_kernel)
+int lr_collect(SvtGpuLrState *s, hipStream_t st, int32_t *frame_type) {
+    if (int rc = svtgpu_comm_wait(s->comm, st)) return rc;
+    s->fin_pending            = 0;
+    const volatile int32_t *o = s->h_fout;
+    if (o[4] != s->fin_seq) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "LR device finish: result word missing after the stream wait",
+                                  __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    if (o[3]) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, (o[3] & 1) ? "LR Wiener descent: round bound or part exchange timed out"
+                                                              : "LR self-guided descent: pass bound, part plan or exchange failed",
+                                  __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    for (int p = 0; p < 3; p++) s->last_ft[p] = o[p];
+    if (frame_type)
+        for (int p = 0; p < 3; p++) frame_type[p] = o[p];
+    return SVTGPU_OK;
+}
+
+// SVTGPU_LR_FINISH=host: rest_finish_search on the host after a read-back of the records (the round-5 form; A/B)
+bool lr_finish_on_host() {
+    static const bool h = [] {
+        const char *e = std::getenv("SVTGPU_LR_FINISH");
+        return e && !std::strcmp(e, "host");
+    }();
+    return h;
+}
+
+// fin == 0: the records come back to the host (search_out) and, for the whole frame (frame_type != nullptr), the RD
+// finish runs there.  fin == 1: the records and the RD finish stay on the device (a tiled picture all-reduces the
+// records on the device first), the state's units are written in stream order; frame_type != nullptr then waits for
+// the result and reads the frame types (and the records into search_out), nullptr returns at once (the asynchronous
+// search: svtgpu_lr_read_result collects it).
 template <typename T>
 int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *src, const SvtGpuLrSearchControls *c,
                  int nplanes, const int32_t *rb, const int32_t *re, const int32_t *cb, const int32_t *ce,
-                 int32_t *frame_type, SvtGpuLrUnitSearch *const *search_out, hipStream_t st) {
+                 int32_t *frame_type, SvtGpuLrUnitSearch *const *search_out, hipStream_t st, int fin = 0) {
     // SVTGPU_LR_TIMING=1 prints the host-side phase times (wall clock, including the waits) to stderr
     static const bool timing = std::getenv("SVTGPU_LR_TIMING") != nullptr;
     auto              clk    = [] { return std::chrono::steady_clock::now(); };
@@ -2561,6 +2963,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         if (t.x0 & 3) return SVTGPU_ERR_UNSUPPORTED;
     const int n_all = (int)units.size(), nt_all = (int)tiles.size();
     if (n_all == 0) return SVTGPU_OK; // an empty band
+    // the records' layout: every plane's units back to back (the state's units, d_units[0]); dst[gu]: the record of
+    // searched unit gu
+    int32_t nrec = 0, rbase[3];
+    for (int p = 0; p < 3; p++) rbase[p] = nrec, nrec += s->hunits[p] * s->vunits[p];
+    std::vector<int32_t> dst(n_all);
+    for (int p = 0, gu = 0; p < nplanes; p++)
+        for (int u = 0; u < pp[p].n; u++, gu++) dst[gu] = rbase[p] + uloc[gu];
     // the resident Wiener kernel takes every unit whose rows fit its registers (all units of the 4K / 1080p frames);
     // its workgroups start with the largest units (the longest chains); windows up to WR_LDS_CAP live in LDS
     // The resident Wiener kernel takes every unit up to 384 columns wide (unit sizes <= 256): a unit is cut into the
@@ -2644,9 +3053,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // accumulators zeroed per search, the results read back (o_sse is the last zeroed and the first read)
     Carver       dc;
     const size_t o_tiles = dc(sizeof(Tile) * nt_all), o_units = dc(sizeof(URect) * n_all), o_t0 = dc(4 * (n_all + 1)),
-                 o_witem = dc(sizeof(WrItem) * (size_t)n_wr), o_sritem = dc(sizeof(SrItem) * (size_t)n_sr);
+                 o_witem = dc(sizeof(WrItem) * (size_t)n_wr), o_sritem = dc(sizeof(SrItem) * (size_t)n_sr),
+                 o_dst = dc(4 * (size_t)n_all);
     const size_t plan_span = dc.off;
-    const size_t o_sum = dc(8 * n_all), o_sse = dc(8 * n_all), o_sse2 = dc(8 * (size_t)n_sg), o_wstat = dc(8),
+    // zeroed per search: the accumulators, the device finish's records (zero-padded: a tiled picture sums them) and
+    // paths (a pass that does not run reads as "none taken")
+    const size_t o_sum = dc(8 * n_all), o_rec = dc(sizeof(SvtGpuLrUnitSearch) * (size_t)nrec),
+                 o_path = dc(16 * (size_t)nrec), o_sse = dc(8 * n_all), o_sse2 = dc(8 * (size_t)n_sg), o_wstat = dc(8),
                  o_sstat = dc(8);
     const size_t zero_span = dc.off - o_sum;
     const size_t o_wu = dc(sizeof(SvtGpuRestUnit) * n_wn), o_wds = dc(sizeof(Descent) * n_wn),
@@ -2654,11 +3067,14 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t res_span = dc.off - o_sse; // the (unit, ep) descents stay on the device: the best ep's come back
     const size_t o_sds = dc(sizeof(Descent) * npairs);
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
+    const size_t o_m1 = dc(8 * (size_t)nrec), o_m2 = dc(8 * (size_t)nrec), o_t3 = dc(4 * FIN_T3 * (size_t)nrec),
+                 o_fout = dc(4 * FIN_OUT);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
     const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
     Carver       hc; // host mirrors of the plan and result spans keep the device layout
-    const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all);
+    const size_t h_plan = hc(plan_span), h_res = hc(res_span), h_cnt = hc(32), h_out = hc(sizeof(SvtGpuRestUnit) * n_all),
+                 h_rec = hc(sizeof(SvtGpuLrUnitSearch) * (size_t)nrec);
     const size_t h_sse = h_res, h_sse2 = h_res + (o_sse2 - o_sse), h_wu = h_res + (o_wu - o_sse),
                  h_wds = h_res + (o_wds - o_sse), h_best = h_res + (o_best - o_sse), h_braw = h_res + (o_braw - o_sse);
     if (dc.off > s->work_bytes) {
@@ -2724,6 +3140,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         std::memcpy(pl + o_t0, tile0.data(), 4 * (n_all + 1));
         std::memcpy(pl + o_witem, wr_items.data(), sizeof(WrItem) * (size_t)n_wr);
         std::memcpy(pl + o_sritem, sr_items.data(), sizeof(SrItem) * (size_t)n_sr);
+        std::memcpy(pl + o_dst, dst.data(), 4 * (size_t)n_all);
         if (s->plan_work != s->d_work || s->plan_bytes.size() != plan_span ||
             std::memcmp(s->plan_bytes.data(), pl, plan_span)) { // a new plan: one upload
             HIP_TRY(hipMemcpyAsync(dp(0), pl, plan_span, hipMemcpyHostToDevice, st));
@@ -2797,19 +3214,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // The Wiener chain (statistics, decomposition, trial rounds) and the self-guided chain (filters, seeds,
     // projection rounds) are independent until the RD finish: the Wiener chain runs on a second stream, so its
     // latency-bound rounds fill the gaps of the self-guided work and the other way round.
-    if (!s->wst) {
-        // the Wiener chain (statistics, solve, ~48 trial rounds) is the search's critical path: its stream gets the
-        // highest priority so its workgroups are dispatched first while the self-guided filters fill the CUs
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        static const int wprio = [] { // SVTGPU_WN_PRIO=0: the Wiener chain at normal priority (A/B)
-            const char *e = std::getenv("SVTGPU_WN_PRIO");
-            return e ? std::atoi(e) : 1;
-        }();
-        HIP_TRY(hipStreamCreateWithPriority(&s->wst, hipStreamNonBlocking, wprio ? greatest : least));
-        HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
-    }
+    if (!s->wst)
+        if (int rc = lr_make_wiener_stream(s)) return rc;
     // measurement (svtgpu_lr_profile bit 7): both chains on the caller's stream, so a kernel's duration is its own,
     // not its share of the CUs beside the other chain's kernels
     const bool  serial = prof && prof->serial;
@@ -2888,12 +3294,84 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     }
     if (prof)
         if (int rc = prof->finish(st)) return rc; // fold the launch timings on the device, no read-back
+    if (fin) { // ---- phase 5 on the device: the records, [the gather,] rest_finish_search ----
+        if (!s->h_fout) {
+            HIP_TRY(hipHostMalloc((void **)&s->h_fout, 4 * FIN_OUT, hipHostMallocMapped | hipHostMallocCoherent));
+            std::memset(s->h_fout, 0, 4 * FIN_OUT);
+            HIP_TRY(hipHostGetDevicePointer((void **)&s->h_fout_dev, s->h_fout, 0));
+        }
+        RecArgs R;
+        std::memset(&R, 0, sizeof R);
+        R.nplanes = nplanes, R.n_all = n_all;
+        for (int p = 0; p < nplanes; p++) R.wn[p] = pp[p].wn, R.sg[p] = pp[p].sg;
+        R.sse0 = (const unsigned long long *)dp(o_sse), R.sse2 = (const unsigned long long *)dp(o_sse2);
+        R.wu = (const SvtGpuRestUnit *)dp(o_wu), R.wds = (const Descent *)dp(o_wds);
+        R.best = (const int32_t *)dp(o_best), R.raw = (const int32_t *)dp(o_braw);
+        R.dst = (const int32_t *)dp(o_dst), R.rec = (SvtGpuLrUnitSearch *)dp(o_rec);
+        hipLaunchKernelGGL(lr_records_kernel, dim3((n_all + 255) / 256), dim3(256), 0, st, A, R);
+        HIP_TRY(hipGetLastError());
+        // a picture tiled over GPUs: the zero-padded records summed over the ranks = the gather rest_finish_search reads
+        // (one contributor per unit), on the device: no host wait
+        static_assert(sizeof(SvtGpuLrUnitSearch) % 8 == 0, "records travel as uint64 words");
+        if (svtgpu_comm_tiled(s->comm))
+            if (int rc = svtgpu_comm_sum(s->comm, dp(o_rec), (size_t)nrec * sizeof(SvtGpuLrUnitSearch) / 8, true, st,
+                                         SVTGPU_XCH_LR))
+                return rc;
+        FinArgs F;
+        std::memset(&F, 0, sizeof F);
+        bool tables = false;
+        for (int p = 0; p < 3; p++) {
+            FinPlane &P = F.pl[p];
+            P.n = s->hunits[p] * s->vunits[p], P.base = rbase[p];
+            for (int r = 0; r < 4; r++) P.run[r] = p < nplanes && finish_runs(c, p, P.n, r);
+            P.win1 = plane_win(c, p);
+            P.own1 = p == 0 || P.run[1], P.own2 = p == 0 || P.run[2];
+            tables |= P.run[1] || P.run[2] || P.run[3];
+        }
+        F.nplanes = nplanes, F.nrec = nrec, F.rdmult = c->rdmult;
+        for (int k = 0; k < 3; k++) F.sw[k] = c->switchable_restore_cost[k];
+        for (int k = 0; k < 2; k++) F.wn[k] = c->wiener_restore_cost[k], F.sg[k] = c->sgrproj_restore_cost[k];
+        F.rec = (const SvtGpuLrUnitSearch *)dp(o_rec);
+        F.m1 = (unsigned long long *)dp(o_m1), F.m2 = (unsigned long long *)dp(o_m2), F.t3 = (uint32_t *)dp(o_t3);
+        F.path = (int32_t *)dp(o_path), F.units = s->d_units[0];
+        F.out = (int32_t *)dp(o_fout), F.out_host = s->h_fout_dev;
+        F.wstat = n_wn ? (const int32_t *)dp(o_wstat) : nullptr, F.sstat = n_sr ? (const int32_t *)dp(o_sstat) : nullptr;
+        F.seq = ++s->fin_seq;
+        if (tables) {
+            hipLaunchKernelGGL(lr_fin_tables_kernel, dim3(F.pl[nplanes - 1].base + F.pl[nplanes - 1].n), dim3(64), 0,
+                               st, F);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(lr_fin_walk_kernel, dim3(1), dim3(256), 0, st, F);
+        HIP_TRY(hipGetLastError());
+        if (search_out) { // the records, all planes' units
+            HIP_TRY(hipMemcpyAsync(hp(h_rec), dp(o_rec), sizeof(SvtGpuLrUnitSearch) * (size_t)nrec,
+                                   hipMemcpyDeviceToHost, st));
+            svtgpu_count_xfer(1, sizeof(SvtGpuLrUnitSearch) * (size_t)nrec);
+        }
+        if (!s->pin_free) HIP_TRY(hipEventCreateWithFlags(&s->pin_free, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->pin_free, st));
+        s->fin_pending = 1;
+        mark(3);
+        if (!frame_type) return SVTGPU_OK; // asynchronous: svtgpu_lr_read_result collects the frame types
+        if (int rc = lr_collect(s, st, frame_type)) return rc;
+        if (search_out) {
+            const SvtGpuLrUnitSearch *hr = (const SvtGpuLrUnitSearch *)hp(h_rec);
+            for (int p = 0; p < 3; p++)
+                if (search_out[p]) std::memcpy(search_out[p], hr + rbase[p], sizeof(SvtGpuLrUnitSearch) * F.pl[p].n);
+        }
+        mark(4);
+        if (timing)
+            std::fprintf(stderr, "lr_search ms: stats+flt %.3f  seeds %.3f  descents %.3f  device finish + wait %.3f\n",
+                         t_ph[0], t_ph[1], t_ph[2], t_ph[3] + t_ph[4]);
+        return SVTGPU_OK;
+    }
     Descent        *hw = (Descent *)hp(h_wds);
     const int32_t  *hbest = (const int32_t *)hp(h_best), *hraw = (const int32_t *)hp(h_braw);
     SvtGpuRestUnit *wu = (SvtGpuRestUnit *)hp(h_wu);
     HIP_TRY(hipMemcpyAsync(hp(h_res), dp(o_sse), res_span, hipMemcpyDeviceToHost, st)); // every result, one copy
     svtgpu_count_xfer(1, res_span);
-    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded when an exchange sits before it
     if (n_wn && *(const int32_t *)hp(h_res + (o_wstat - o_sse))) { // status bits of wiener_res_kernel
         svtgpu_set_last_hip_error(hipErrorUnknown, "LR Wiener descent: round bound or part exchange timed out",
                                   __FILE__, __LINE__);
@@ -2956,9 +3434,13 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
             }
             if (search_out && search_out[p]) search_out[p][uloc[gu]] = R;
         }
-        if (frame_type) { // whole frame: units are in plane order, uloc[gu] == u
-            finish_plane(c, p, q.win, rs.data() + q.unit_base, q.n, &frame_type[p], out + q.unit_base);
-        }
+    }
+    if (frame_type) { // whole frame: units are in plane order, uloc[gu] == u
+        std::vector<FinRusi> rusi((size_t)std::max(1, pp[0].n));
+        std::memset(rusi.data(), 0, sizeof(FinRusi) * rusi.size());
+        for (int p = 0; p < nplanes; p++)
+            finish_plane_shared(c, p, pp[p].win, rs.data() + pp[p].unit_base, pp[p].n, rusi.data(), &frame_type[p],
+                                out + pp[p].unit_base);
     }
     if (frame_type) // d_units holds the planes back to back in the same order: one upload
         HIP_TRY(hipMemcpyAsync(s->d_units[0], out, sizeof(SvtGpuRestUnit) * n_all, hipMemcpyHostToDevice, st));
@@ -3026,6 +3508,24 @@ extern "C" int svtgpu_lr_controls_for_level(int32_t wn, int32_t sg, SvtGpuLrSear
 
 void lr_profiler_destroy(void *prof) { delete (LrProfiler *)prof; }
 
+// the search's Wiener-chain stream (statistics, solve, ~48 trial rounds: the search's critical path) at the highest
+// priority, so its workgroups are dispatched first while the self-guided filters fill the CUs.  Created with the
+// state (svtgpu_lr_state_create), in the caller's order: a stream created lazily by the first search of each of
+// several host threads landed on the hardware queues in thread order, and a queue shared with another frame's chain
+// serializes the two (round 5's six-frames collapse)
+int lr_make_wiener_stream(SvtGpuLrState *s) {
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    static const int wprio = [] { // SVTGPU_WN_PRIO=0: the Wiener chain at normal priority (A/B)
+        const char *e = std::getenv("SVTGPU_WN_PRIO");
+        return e ? std::atoi(e) : 1;
+    }();
+    HIP_TRY(hipStreamCreateWithPriority(&s->wst, hipStreamNonBlocking, wprio ? greatest : least));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *last) {
     if (!s) return SVTGPU_ERR_INVALID_ARG;
     LrProfiler *pr = (LrProfiler *)s->prof;
@@ -3080,6 +3580,16 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
     hipStream_t st      = pick_stream(s->ctx, stream);
     const int   nplanes = searched_planes(ctrls);
     for (int p = 0; p < 3; p++) frame_type_out[p] = SVTGPU_RESTORE_NONE;
+    if (!lr_finish_on_host()) { // the records and the RD finish on the device; one wait at the end
+        int32_t rb[3], re[3], cb[3], ce[3];
+        for (int p = 0; p < 3; p++)
+            cb[p] = s->tile_units[p][0], rb[p] = s->tile_units[p][1], ce[p] = s->tile_units[p][2], re[p] = s->tile_units[p][3];
+        if (!svtgpu_comm_tiled(s->comm))
+            for (int p = 0; p < 3; p++) rb[p] = cb[p] = 0, re[p] = s->vunits[p], ce[p] = s->hunits[p];
+        return recon->bytes_per_sample == 2
+            ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, frame_type_out, search_out, st, 1)
+            : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, frame_type_out, search_out, st, 1);
+    }
     if (!svtgpu_comm_tiled(s->comm)) {
         int32_t rb[3] = {0, 0, 0}, re[3] = {s->vunits[0], s->vunits[1], s->vunits[2]};
         int32_t cb[3] = {0, 0, 0}, ce[3] = {s->hunits[0], s->hunits[1], s->hunits[2]};
@@ -3106,14 +3616,15 @@ extern "C" int svtgpu_lr_search_frame(SvtGpuLrState *s, const SvtGpuFrame *recon
     if ((rc = svtgpu_comm_sum(s->comm, rec.data(), nrec * sizeof(SvtGpuLrUnitSearch) / 8, false, st, SVTGPU_XCH_LR))) return rc;
     std::vector<SvtGpuRestUnit> units(nrec);
     std::memset(units.data(), 0, sizeof(SvtGpuRestUnit) * nrec);
-    for (int p = 0; p < nplanes; p++) {
-        const int n = s->hunits[p] * s->vunits[p];
-        finish_plane(ctrls, p, plane_win(ctrls, p), outs[p], n, &frame_type_out[p], units.data() + base[p]);
-        if (search_out && search_out[p]) std::memcpy(search_out[p], outs[p], sizeof(SvtGpuLrUnitSearch) * n);
-    }
+    int32_t         nu[3];
+    SvtGpuRestUnit *uo[3];
+    for (int p = 0; p < 3; p++) nu[p] = s->hunits[p] * s->vunits[p], uo[p] = units.data() + base[p];
+    finish_frame_host(ctrls, nplanes, nu, outs, frame_type_out, uo);
+    for (int p = 0; p < nplanes; p++)
+        if (search_out && search_out[p]) std::memcpy(search_out[p], outs[p], sizeof(SvtGpuLrUnitSearch) * nu[p]);
     HIP_TRY(hipMemcpyAsync(s->d_units[0], units.data(), sizeof(SvtGpuRestUnit) * nrec, hipMemcpyHostToDevice, st));
     svtgpu_count_xfer(0, sizeof(SvtGpuRestUnit) * nrec);
-    HIP_TRY(hipStreamSynchronize(st)); // the host staging of the units goes out of scope
+    if ((rc = svtgpu_comm_wait(s->comm, st))) return rc; // the host staging of the units goes out of scope
     return SVTGPU_OK;
 }
 
@@ -3171,6 +3682,58 @@ extern "C" int svtgpu_lr_finish_plane(const SvtGpuLrSearchControls *ctrls, int32
         std::memset(units_out, 0, sizeof(SvtGpuRestUnit) * nunits);
         return SVTGPU_OK;
     }
-    finish_plane(ctrls, plane, plane_win(ctrls, plane), records, nunits, frame_type_out, units_out);
+    // one plane alone: the shared array starts zeroed (a chroma plane's switchable pass sees no luma entries; the whole
+    // frame's finish is svtgpu_lr_finish_frame)
+    std::vector<FinRusi> rusi((size_t)nunits);
+    std::memset(rusi.data(), 0, sizeof(FinRusi) * rusi.size());
+    finish_plane_shared(ctrls, plane, plane_win(ctrls, plane), records, nunits, rusi.data(), frame_type_out, units_out);
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_lr_finish_frame(const SvtGpuLrSearchControls *ctrls, const int32_t nunits[3],
+                                      const SvtGpuLrUnitSearch *const records[3], int32_t frame_type_out[3],
+                                      SvtGpuRestUnit *const units_out[3]) {
+    if (!ctrls || !nunits || !records || !frame_type_out || !units_out) return SVTGPU_ERR_INVALID_ARG;
+    const int nplanes = searched_planes(ctrls);
+    for (int p = 0; p < 3; p++) {
+        if (p >= nplanes) continue;
+        if (nunits[p] <= 0 || !records[p] || !units_out[p] || (p && nunits[p] > nunits[0])) return SVTGPU_ERR_INVALID_ARG;
+        for (int u = 0; u < nunits[p]; u++)
+            if (records[p][u].sgrproj.ep < 0 || records[p][u].sgrproj.ep > 15) return SVTGPU_ERR_INVALID_ARG;
+    }
+    for (int p = 0; p < 3; p++) {
+        frame_type_out[p] = SVTGPU_RESTORE_NONE;
+        if (p >= nplanes && units_out[p] && nunits[p] > 0) std::memset(units_out[p], 0, sizeof(SvtGpuRestUnit) * nunits[p]);
+    }
+    finish_frame_host(ctrls, nplanes, nunits, records, frame_type_out, units_out);
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_lr_search_frame_async(SvtGpuLrState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                            const SvtGpuLrSearchControls *ctrls, void *stream) {
+    if (int rc = check_search_args(s, recon, source, ctrls)) return rc;
+    hipStream_t st      = pick_stream(s->ctx, stream);
+    const int   nplanes = searched_planes(ctrls);
+    if (lr_finish_on_host()) { // the host finish waits anyway: the synchronous search, its frame types kept
+        int32_t ft[3];
+        if (int rc = svtgpu_lr_search_frame(s, recon, source, ctrls, ft, nullptr, stream)) return rc;
+        for (int p = 0; p < 3; p++) s->last_ft[p] = ft[p];
+        s->fin_pending = 0;
+        return SVTGPU_OK;
+    }
+    int32_t rb[3], re[3], cb[3], ce[3];
+    for (int p = 0; p < 3; p++)
+        cb[p] = s->tile_units[p][0], rb[p] = s->tile_units[p][1], ce[p] = s->tile_units[p][2], re[p] = s->tile_units[p][3];
+    if (!svtgpu_comm_tiled(s->comm))
+        for (int p = 0; p < 3; p++) rb[p] = cb[p] = 0, re[p] = s->vunits[p], ce[p] = s->hunits[p];
+    return recon->bytes_per_sample == 2
+        ? search_frame<uint16_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, nullptr, st, 1)
+        : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, nullptr, st, 1);
+}
+
+extern "C" int svtgpu_lr_read_result(SvtGpuLrState *s, int32_t frame_type_out[3], void *stream) {
+    if (!s || !frame_type_out) return SVTGPU_ERR_INVALID_ARG;
+    if (s->fin_pending) return lr_collect(s, pick_stream(s->ctx, stream), frame_type_out);
+    for (int p = 0; p < 3; p++) frame_type_out[p] = s->last_ft[p];
     return SVTGPU_OK;
 }

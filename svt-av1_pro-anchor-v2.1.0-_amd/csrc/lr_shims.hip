@@ -80,7 +80,7 @@ void compute_stats(int32_t win, const T *dgd, const T *src, int32_t h_start, int
     const size_t od = 0, os = (hd.size() * sizeof(T) + 255) & ~(size_t)255, osum = os + ((hs.size() * sizeof(T) + 255) & ~(size_t)255);
     const size_t om = osum + 256, oh = om + 8 * 64;
     char        *d = (char *)g_lr_scratch.get(oh + (size_t)8 * win2 * win2);
-    hipStream_t  st = svtgpu_default_stream();
+    hipStream_t  st = svtgpu_shim_stream();
     HIP_OR_DIE(hipMemcpyAsync(d + od, hd.data(), hd.size() * sizeof(T), hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemcpyAsync(d + os, hs.data(), hs.size() * sizeof(T), hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemsetAsync(d + osum, 0, 8, st));
@@ -175,7 +175,7 @@ int64_t pixel_proj_error(const T *src, int32_t width, int32_t height, int32_t sr
                          int32_t flt1_stride, const int32_t xq[2], const SVTGPU_SGR_PARAMS_T *params) {
     const bool  use0 = params->r[0] > 0, use1 = params->r[1] > 0;
     const int   mode = use0 && use1 ? 0 : use0 ? 1 : use1 ? 2 : 3;
-    hipStream_t st   = svtgpu_default_stream();
+    hipStream_t st   = svtgpu_shim_stream();
     auto        S    = stage_proj<T>(src, src_stride, dat, dat_stride, flt0, flt0_stride, flt1, flt1_stride, width,
                                      height, use0, use1, st);
     hipLaunchKernelGGL((proj_err_shim_kernel<T, HBD>), dim3(32), dim3(256), 0, st, S.src, S.dat, S.f0, S.f1, width,
@@ -235,7 +235,7 @@ extern "C" void svtgpu_get_proj_subspace(const uint8_t *src8, int width, int hei
                                          int flt0_stride, int32_t *flt1, int flt1_stride, int *xq,
                                          const SVTGPU_SGR_PARAMS_T *params) {
     const bool         use0 = params->r[0] > 0, use1 = params->r[1] > 0;
-    hipStream_t        st   = svtgpu_default_stream();
+    hipStream_t        st   = svtgpu_shim_stream();
     unsigned long long r[5];
     if (use_highbitdepth) {
         auto S = stage_proj<uint16_t>(short_ptr(src8), src_stride, short_ptr(dat8), dat_stride, flt0, flt0_stride, flt1,

@@ -246,7 +246,7 @@ void block_stats(const T *a, int as, const T *const *b, int bs, int nblk, int w,
         cap = need;
     }
     if (!dr) HIP_OR_DIE(hipMalloc(&dr, sizeof(unsigned long long) * 3 * 4));
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     HIP_OR_DIE(hipMemcpyAsync(d, ha.data(), need / 2, hipMemcpyHostToDevice, st));
     HIP_OR_DIE(hipMemcpyAsync(d + (size_t)n * nblk, hb.data(), need / 2, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(block_stats_kernel, dim3(nblk), dim3(256), 0, st, d, d + (size_t)n * nblk, n, dr);
@@ -436,7 +436,7 @@ uint32_t subpel_var(const uint8_t *a, int a_stride, int xoff, int yoff, const ui
     std::vector<uint8_t> ha((size_t)(h + 1) * (w + 1)), hb((size_t)h * w);
     for (int r = 0; r <= h; r++) memcpy(&ha[(size_t)r * (w + 1)], a + (long)r * a_stride, (size_t)w + 1);
     for (int r = 0; r < h; r++) memcpy(&hb[(size_t)r * w], b + (long)r * b_stride, (size_t)w);
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     static thread_local uint8_t *d = nullptr;
     if (!d) HIP_OR_DIE(hipMalloc(&d, 129 * 129 + 128 * 128 + 64));
     unsigned long long *dr = (unsigned long long *)(d + 129 * 129 + 128 * 128 + 16);

@@ -362,7 +362,7 @@ extern "C" void svtgpu_ext_all_sad_calculation_8x8_16x16(uint8_t *src, uint32_t 
                                                          uint32_t *p_best_mv16x16, uint32_t p_eight_sad16x16[16][8],
                                                          uint32_t p_eight_sad8x8[64][8], Bool sub_sad) {
     (void)p_eight_sad8x8; // not written by the reference's C either (EbMotionEstimation.c:223)
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     Span        s, r, b8, b16, m8, m16, e16;
     upload_span(st, s, src, (size_t)63 * src_stride + 64);
     upload_span(st, r, ref, (size_t)63 * ref_stride + 64 + 7);
@@ -380,7 +380,7 @@ extern "C" void svtgpu_ext_all_sad_calculation_8x8_16x16(uint8_t *src, uint32_t 
 
 static void sad_32_64(const uint32_t *sad16, int npos, uint32_t *best32, uint32_t *best64, uint32_t *mv32,
                       uint32_t *mv64, uint32_t mv, uint32_t *sad32) {
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     Span        a, b32, b64, m32, m64, s32;
     uint32_t   *da = upload_words(st, a, sad16, 16 * (size_t)npos);
     uint32_t   *d32 = upload_words(st, b32, best32, 4), *d64 = upload_words(st, b64, best64, 1);
@@ -413,7 +413,7 @@ extern "C" void svtgpu_ext_sad_calculation_8x8_16x16(uint8_t *src, uint32_t src_
                                                      uint32_t *p_best_sad_16x16, uint32_t *p_best_mv8x8,
                                                      uint32_t *p_best_mv16x16, uint32_t mv, uint32_t *p_sad16x16,
                                                      uint32_t *p_sad8x8, Bool sub_sad) {
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     Span        s, r, b8, b16, m8, m16, s16, s8;
     upload_span(st, s, src, (size_t)15 * src_stride + 16);
     upload_span(st, r, ref, (size_t)15 * ref_stride + 16);
@@ -436,7 +436,7 @@ extern "C" void svtgpu_sad_loop_kernel(uint8_t *src, uint32_t src_stride, uint8_
                                        int16_t search_area_height) {
     *best_sad = 0xffffff;
     if (search_area_width <= 0 || search_area_height <= 0 || !block_width || !block_height) return;
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     Span        s, r, o;
     upload_span(st, s, src, (size_t)(block_height - 1) * src_stride + block_width);
     upload_span(st, r, ref,
@@ -545,7 +545,7 @@ extern "C" void svtgpu_pme_sad_loop_kernel(const struct svt_mv_cost_param *mv_co
         }
     }
     if (pos.empty()) return;
-    hipStream_t st = svtgpu_default_stream();
+    hipStream_t st = svtgpu_shim_stream();
     PmeArgs     a;
     std::memset(&a, 0, sizeof a);
     a.ss = (int)src_stride, a.rs = (int)ref_stride, a.bh = (int)block_height, a.bw = (int)block_width;

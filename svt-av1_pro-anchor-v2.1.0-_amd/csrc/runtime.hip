@@ -21,6 +21,7 @@ void svtgpu_fatal(const char *what) {
 }
 
 extern "C" const char *svtgpu_version(void) { return SVTGPU_VERSION_STR; }
+extern "C" int32_t svtgpu_abi_version(void) { return SVTGPU_ABI_VERSION; }
 
 extern "C" const char *svtgpu_error_string(int code) {
     switch (code) {
@@ -110,9 +111,12 @@ SvtGpuContext        *svtgpu_default_context() {
         svtgpu_fatal("svtgpu per-block shim called without a usable gfx950 device");
     return g_default_ctx;
 }
-// every per-block shim launches on the default context's stream: its uses count the shim calls (svtgpu_shim_calls)
+// every per-block shim launches on the default context's stream; each shim entry point takes it once through
+// svtgpu_shim_stream, which counts the shim calls (svtgpu_shim_calls) -- frame-level calls with a null stream and the
+// communicator's waits use svtgpu_default_stream and are not counted
 static std::atomic<unsigned long long> g_shim_calls{0};
-hipStream_t svtgpu_default_stream() {
+hipStream_t svtgpu_default_stream() { return svtgpu_default_context()->stream; }
+hipStream_t svtgpu_shim_stream() {
     g_shim_calls.fetch_add(1, std::memory_order_relaxed);
     return svtgpu_default_context()->stream;
 }

@@ -155,7 +155,10 @@ void svtgpu_cdef_sb128_dup_host(const SvtGpuCdefFrameState *s, int8_t *fbs);
 int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                              const SvtGpuCdefParams *p, hipStream_t st);
 
+// the default context's stream (per-block shims and stream-less frame-level calls)
 hipStream_t svtgpu_default_stream();
+// the same stream, counted as one per-block shim call (svtgpu_shim_calls): used once per RTCD shim entry point only
+hipStream_t svtgpu_shim_stream();
 // svt_av1_compute_stats(_highbd) of one unit on the matrix cores (lr_search.hip; 8- and 10-bit samples)
 int svtgpu_stats_unit_mfma8(int win, const uint8_t *dgd, const uint8_t *src, int h_start, int h_end, int v_start,
                             int v_end, int dgd_stride, int src_stride, int64_t *M, int64_t *H);

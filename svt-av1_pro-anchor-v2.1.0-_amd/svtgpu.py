@@ -208,6 +208,7 @@ _LPF16 = (None, [_P, _I32, _P, _P, _P, _I32])
 _SIGS = {
     "svtgpu_device_available": (ctypes.c_int, []),
     "svtgpu_version": (ctypes.c_char_p, []),
+    "svtgpu_abi_version": (_I32, []),
     "svtgpu_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "svtgpu_context_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
     "svtgpu_context_destroy": (None, [_P]),
@@ -345,10 +346,14 @@ _SIGS = {
     "svtgpu_lr_controls_for_level": (ctypes.c_int, [_I32, _I32, ctypes.POINTER(LrSearchControls)]),
     "svtgpu_lr_search_units": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P, _P, _P, _P]),
     "svtgpu_lr_finish_plane": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _I32, _I32, _P, _P, _P]),
+    "svtgpu_lr_finish_frame": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _P, _P, _P, _P]),
+    "svtgpu_lr_search_frame_async": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P]),
+    "svtgpu_lr_read_result": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_lr_profile": (ctypes.c_int, [_P, _I32, _P]),
     "svtgpu_transfer_bytes": (ctypes.c_int, [_P, _P, _I32]),
     "svtgpu_comm_unique_id": (ctypes.c_int, [_P]),
     "svtgpu_comm_create": (ctypes.c_int, [_P, _I32, _I32, _P, ctypes.POINTER(_P)]),
+    "svtgpu_comm_create_bounded": (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _I32, ctypes.POINTER(_P)]),
     "svtgpu_comm_create_host": (ctypes.c_int, [_I32, _I32, _P, ctypes.POINTER(_P)]),
     "svtgpu_comm_destroy": (None, [_P]),
     "svtgpu_comm_nranks": (_I32, [_P]),
@@ -542,10 +547,12 @@ class Comm:
         return bytes(b)
 
     @classmethod
-    def rccl(cls, ctx, nranks, rank, uid):
+    def rccl(cls, ctx, nranks, rank, uid, timeout_ms=0, slot=-1):
+        """svtgpu_comm_create_bounded: the RCCL communicator, its init bounded by timeout_ms (0: the default
+        deadline); a peer that never joins raises SvtGpuError naming "communicator init", the slot and the rank."""
         b = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         h = _P()
-        check(lib().svtgpu_comm_create(ctx.h, nranks, rank, b, ctypes.byref(h)))
+        check(lib().svtgpu_comm_create_bounded(ctx.h, nranks, rank, b, int(timeout_ms), int(slot), ctypes.byref(h)))
         return cls(h)
 
     @classmethod
@@ -888,6 +895,17 @@ class LrState:
         check(lib().svtgpu_lr_search_frame(self.h, recon.h, source.h, ctypes.byref(ctrls), ptr(ft), rp, stream))
         return ([int(x) for x in ft], recs) if records else [int(x) for x in ft]
 
+    def search_async(self, recon, source, ctrls, stream=None):
+        """svtgpu_lr_search_frame_async: search + device RD finish enqueued on `stream`, no host wait; apply(...,
+        frame_type=None) applies the result in stream order, read_result() collects the frame types."""
+        check(lib().svtgpu_lr_search_frame_async(self.h, recon.h, source.h, ctypes.byref(ctrls), stream))
+
+    def read_result(self, stream=None):
+        """svtgpu_lr_read_result: waits for the last asynchronous search and returns its frame types."""
+        ft = np.zeros(3, np.int32)
+        check(lib().svtgpu_lr_read_result(self.h, ptr(ft), stream))
+        return [int(x) for x in ft]
+
     def search_units(self, recon, source, ctrls, row_begin, row_end, records=None, stream=None):
         """svtgpu_lr_search_units: per-unit records of the unit rows [row_begin[p], row_end[p]) of every plane,
         written into `records` (per-plane arrays of all units; allocated zeroed when None).  No RD finish."""
@@ -932,8 +950,10 @@ class LrState:
         check(lib().svtgpu_lr_set_tile(self.h, _rects3(units), _rects3(out), comm.h if comm else None))
 
     def apply(self, deblocked, cdef_out, out, frame_type, stream=None):
-        ft = np.ascontiguousarray(frame_type, np.int32)
-        check(lib().svtgpu_lr_apply_frame(self.h, deblocked.h, cdef_out.h, out.h, ptr(ft), stream))
+        """svtgpu_lr_apply_frame; frame_type None: the units the last (asynchronous) search left on the device."""
+        ft = None if frame_type is None else np.ascontiguousarray(frame_type, np.int32)
+        check(lib().svtgpu_lr_apply_frame(self.h, deblocked.h, cdef_out.h, out.h, None if ft is None else ptr(ft),
+                                          stream))
 
     def close(self):
         if self.h:
@@ -968,6 +988,19 @@ def lr_finish_plane(ctrls, plane, records):
     ft = _I32()
     check(lib().svtgpu_lr_finish_plane(ctypes.byref(ctrls), plane, len(r), ptr(r), ctypes.byref(ft), ptr(units)))
     return ft.value, units
+
+
+def lr_finish_frame(ctrls, records):
+    """svtgpu_lr_finish_frame (host only): rest_finish_search of the whole frame over one RestUnitSearchInfo array
+    shared by the planes.  records: per-plane arrays of all units.  Returns (frame types [3], units [3])."""
+    rs = [np.ascontiguousarray(r, LR_UNIT_SEARCH_DTYPE) for r in records]
+    units = [np.zeros(len(r), REST_UNIT_DTYPE) for r in rs]
+    n = np.array([len(r) for r in rs], np.int32)
+    ft = np.zeros(3, np.int32)
+    rp = (ctypes.c_void_p * 3)(*[r.ctypes.data for r in rs])
+    up = (ctypes.c_void_p * 3)(*[u.ctypes.data for u in units])
+    check(lib().svtgpu_lr_finish_frame(ctypes.byref(ctrls), ptr(n), rp, ptr(ft), up))
+    return [int(x) for x in ft], units
 
 
 # ---------------------------------------------------------------------------------------------

@@ -160,10 +160,12 @@ def _gpu_search(ctx, rec, src, bd, unit_size, ctrls):
     return st, R, ft, recs
 
 
-@pytest.mark.parametrize("case", list(range(10)))
+@pytest.mark.parametrize("case", list(range(len(list(lc.search_cases())))))
 def test_lr_search_golden(ctx, case):
     """The reference's restoration_seg_search + rest_finish_search records (gen_golden_lr.c), cases 6-9 at crop sizes
-    that are not multiples of 8."""
+    that are not multiples of 8, cases 10-13 with one filter type searched for luma only (the finish's shared
+    RestUnitSearchInfo array: c13's chroma takes a Wiener unit from luma's entry).  The RD finish runs on the device
+    (lr_fin_*_kernel) unless SVTGPU_LR_FINISH=host."""
     c = list(lc.search_cases())[case]
     st, R, ft, recs = _gpu_search(ctx, c["rec"], c["src"], c["bd"], c["unit_size"], c["ctrls"])
     lc.compare_search(ft, c["units"], recs, c)  # frame types + per-unit records vs the reference
@@ -288,3 +290,24 @@ def test_lr_search_serial_measurement_mode_same_records(ctx):
     assert ft1 == ft0
     for p in range(3):
         np.testing.assert_array_equal(recs1[p], recs0[p])
+
+
+@pytest.mark.parametrize("case", [1, 4, 10, 13])
+def test_lr_search_async_equals_sync(ctx, case):
+    """svtgpu_lr_search_frame_async + svtgpu_lr_apply_frame(frame_type = NULL) -- the search, the device RD finish and
+    the apply in stream order with no host wait -- writes the same restored frame as the synchronous search + apply,
+    and svtgpu_lr_read_result returns the reference's frame types."""
+    c = list(lc.search_cases())[case]
+    st, R, ft, recs = _gpu_search(ctx, c["rec"], c["src"], c["bd"], c["unit_size"], c["ctrls"])
+    h, w = R.height, R.width
+    D, O1, O2, S = (svtgpu.Frame(ctx, w, h, c["bd"]) for _ in range(4))
+    D.upload(_coded(c["rec"], 3))
+    S.upload(_coded(c["src"], 4))  # as _gpu_search
+    st.apply(D, R, O1, ft)
+    st2 = svtgpu.LrState(ctx, c["w"], c["h"], c["unit_size"])
+    st2.search_async(R, S, c["ctrls"])
+    st2.apply(D, R, O2, None)
+    assert st2.read_result() == ft == c["ftype"]
+    a, b = O1.download(), O2.download()
+    for p in range(3):
+        assert np.array_equal(a[p], b[p]), (c["name"], p)

@@ -242,6 +242,34 @@ def test_rccl_exchange_deadline_aborts():
     ctx.close()
 
 
+@pytest.mark.gpu
+def test_rccl_comm_init_bounded_peer_never_joins():
+    """communicator creation is bounded like the exchanges.  Rank 0 of a two-rank RCCL communicator whose
+    rank 1 never joins (it died between the id broadcast and its init) returns SVTGPU_ERR_HIP within the deadline,
+    with "communicator init", the frame slot, the rank and the rank count in the message; the partial communicator is
+    aborted and the device stays usable (a one-rank communicator afterwards works)."""
+    import time
+    import torch
+    import svtgpu
+    ctx = svtgpu.Context(0)
+    uid = svtgpu.Comm.unique_id()
+    t0 = time.monotonic()
+    with pytest.raises(svtgpu.SvtGpuError) as ei:
+        svtgpu.Comm.rccl(ctx, 2, 0, uid, timeout_ms=1500, slot=3)
+    dt = time.monotonic() - t0
+    msg = str(ei.value)
+    assert "communicator init" in msg and "frame slot 3" in msg and "rank 0 of 2" in msg, msg
+    assert 1.4 <= dt < 1.5 + 8.0, dt  # detected at the deadline (the abort of the bootstrap may take a moment)
+    c = svtgpu.Comm.rccl(ctx, 1, 0, svtgpu.Comm.unique_id(), timeout_ms=5000, slot=0)
+    t = torch.arange(16, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    c.allreduce_device(t.data_ptr(), t.numel(), stream=torch.cuda.current_stream().cuda_stream)
+    c.sync(torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(t.cpu(), torch.arange(16, dtype=torch.int64))
+    c.close()
+    ctx.close()
+
+
 def _skip_pick_worker(rank, world, port, q):
     import datetime
     import time
