@@ -161,6 +161,9 @@ def parse():
     ap.add_argument("--md-main", action="store_true", default=None,
                     help="run the MD batch on the frame's main stream (after the CDEF stage) instead of its own: one "
                          "hardware queue less per frame in flight")
+    ap.add_argument("--dlf-sync", action="store_true",
+                    help="A/B: the synchronous DLF level search (svtgpu_dlf_pick: host-driven bisection, levels back "
+                         "before the filter) instead of the asynchronous one (device bisection + filter in stream order)")
     ap.add_argument("--lr-sync", action="store_true",
                     help="A/B: the synchronous LR search (svtgpu_lr_search_frame: one host wait, frame types back before "
                          "the apply) instead of the asynchronous one (search + device RD finish + apply in stream order)")
@@ -780,13 +783,19 @@ def main():
             hc = HostClock(timed and a.host_timing)
             dl.set_mode_info_device(mi_dev, sp)
             hc("mode_info")
-            lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
-            hc("dlf_pick")
-            dl.filter_to(R, D, lfp, 0, 3, sp)
+            if a.dlf_sync:
+                lfp = dl.pick(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
+                hc("dlf_pick")
+                dl.filter_to(R, D, lfp, 0, 3, sp)
+            else:  # the bisection on the device, the filter with its levels: no host wait in the DLF stage
+                dl.pick_async(R, S, lf_start, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=0, stream=sp)
+                hc("dlf_pick")
+                dl.filter_to(R, D, None, 0, 3, sp)
             hc("dlf_filter")
             if timed:
                 es[1].record(stream)
-                self.lf_levels.append(lfp.levels())
+                if a.dlf_sync:
+                    self.lf_levels.append(lfp.levels())
             # CDEF stage on the deblocked frame (tiles: this rank's filter blocks; the pick sums the tables)
             st.search(D, S, ctrls, q, sp)
             hc("cdef_search")
@@ -903,6 +912,9 @@ def main():
     if a.stages == "all" and not a.lr_sync:  # the asynchronous searches' results: a device-side failure raises here
         for sl in slots:
             sl.lr.read_result(sl.stream.cuda_stream)
+    if a.stages == "all" and not a.dlf_sync:  # the last asynchronous level search of every slot
+        for sl in slots:
+            sl.lf_levels.append(sl.dl.read_levels(sl.stream.cuda_stream).levels())
     lr_tot = lr.profile(False) if not a.no_kernel_timing else None
     h2d, d2h = svtgpu.transfer_bytes(reset=True)
     if n > 1:
@@ -1055,6 +1067,8 @@ def main():
                                    "low": bool(concurrency is not None and F > 1 and concurrency < F / 2),
                                    "note": "sum over the frame slots of their mean frame latency / step time"},
                    "lr_search_mode": "sync (host wait)" if a.lr_sync else "async (device RD finish, no host wait)",
+                   "dlf_search_mode": "sync (host-driven bisection)" if a.dlf_sync
+                   else "async (device bisection, no host wait)",
                    "ranks": n,
                    "parallelism": ("tiles%dx%d (each frame tiled over the ranks: DLF trials/filter, CDEF search/apply, "
                                    "LR search/apply per tile; RCCL sums of the DLF trial SSEs, CDEF tables, LR records "

@@ -475,6 +475,21 @@ int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *o
 int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtGpuFrame *source, SvtGpuLfParams *params,
                     int32_t dlf_avg, int32_t dlf_avg_uv, int32_t temporal_layer_index,
                     int32_t early_exit_convergence, int32_t tx_mode_only_4x4, void *stream);
+/* The same level search with no host wait (≙ svt_av1_pick_filter_level, LPF_PICK_FROM_FULL_IMAGE): the bisection of
+ * search_filter_level (EbDeblockingFilter.c:886-991) runs on the device -- every trial round's last workgroup takes the
+ * step, a final one-workgroup kernel completes a search still open after the rounds enqueued (sized from the previous
+ * search) -- and the picked levels stay there.  `params` carries the previous levels in (read at the call).
+ * svtgpu_dlf_frame(_to)(..., params = NULL, ...) then filters with the picked levels in stream order, and
+ * svtgpu_dlf_read_levels waits for them (the frame header's levels).  A picture tiled over GPUs runs the synchronous
+ * search here and keeps its levels. */
+int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                          const SvtGpuLfParams *params, int32_t dlf_avg, int32_t dlf_avg_uv,
+                          int32_t temporal_layer_index, int32_t early_exit_convergence, int32_t tx_mode_only_4x4,
+                          void *stream);
+/* Waits for the last svtgpu_dlf_pick_async of `s` on `stream` and returns its parameters (the input parameters with
+ * the picked levels; sharpness 0).  SVTGPU_ERR_INVALID_ARG: no asynchronous pick ran, or the device mode-info grid it
+ * used had records out of range. */
+int svtgpu_dlf_read_levels(SvtGpuDlfState *s, SvtGpuLfParams *params_out, void *stream);
 /* A picture tiled over GPUs (svtgpu_tile_plan): the level search measures each trial's SSE over the luma
  * rectangle sse_rect = {x0, y0, x1, y1} (the rank's tile; chroma halved) and sums it over `comm` before every
  * bisection step, so every rank takes the same steps; svtgpu_dlf_frame(_to) writes only out_rect (chroma halved,
@@ -892,6 +907,9 @@ int svtgpu_lr_search_frame_async(SvtGpuLrState *s, const SvtGpuFrame *recon, con
  * after a synchronous search, or a second call, the last frame types collected.  SVTGPU_ERR_HIP: the device search
  * failed (svtgpu_error_string names it). */
 int svtgpu_lr_read_result(SvtGpuLrState *s, int32_t frame_type_out[3], void *stream);
+/* The state's units of one plane (the RestorationUnitInfo the frame header / tile coding writes: the last search's
+ * picks, NONE units for a plane whose frame type is NONE); waits for an asynchronous search first. */
+int svtgpu_lr_read_units(SvtGpuLrState *s, int32_t plane, SvtGpuRestUnit *units_out, void *stream);
 /* Per-unit part of the search for a band of unit rows: the units of unit rows [row_begin[p], row_end[p]) of each
  * searched plane (restoration_seg_search restricted to those units; every unit's search is independent of the
  * others).  Writes those units' records into search_out[p] (arrays of all units of the plane, row-major; other

@@ -205,6 +205,7 @@ constexpr int MAX_JOBS   = 3; // planes per launch: the Y, U and V level searche
 
 // one plane of a launch
 struct DlfPlaneJob {
+    int32_t         plane;    // 0 Y, 1 U, 2 V (the device level tables' index)
     const void     *src;      // recon plane (apply: a copy of it)
     void           *dst;      // apply output
     const void     *ref;      // source picture plane (trial)
@@ -238,6 +239,31 @@ struct DlfTileArgs {
     unsigned long long  seq;
     unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
     const DlfDevPlan   *plan;  // trial mode: levels from the device plan (the grid covers MAX_TRIALS per job) or null
+    int32_t             dyn;   // with plan: the items are the plan's levels only, Σ tiles x plan->ntrial (persistent grid)
+    const uint8_t      *dev_lvl; // apply: the level tables [plane][dir][128] the device search left (null: job lvl[0])
+};
+
+// The launch arguments as the kernels' items read them: in the kernarg segment (constant address space, scalar
+// loads).  A reference to the by-value kernel parameter passed into the item function made the compiler copy the
+// 2 KB argument block to scratch (private segment 2168 B, 13 VGPRs spilled); the kernarg pointer keeps it in place
+// (the argument block is every launch's first parameter, at offset 0).
+typedef const __attribute__((address_space(4))) DlfTileArgs KArgs;
+typedef const __attribute__((address_space(4))) DlfPlaneJob KJob;
+__device__ __forceinline__ KArgs &kargs() { return *(KArgs *)__builtin_amdgcn_kernarg_segment_ptr(); }
+
+// the LDS of one tile item (dlf_tile_item); the persistent trial kernel's last workgroup reuses `t` for the step
+struct DlfTileLds {
+    uint16_t t[LW * LW];
+    uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
+    uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
+    unsigned long long red[NTHR / 64];
+    // this workgroup's level table (per direction and level class) and the per-level thresholds (mblim | lim << 8 |
+    // hev << 16), looked up per edge with lane-varying indices: from LDS, not from the kernel arguments (a lane-varying
+    // index into the argument block is a memory load per lookup)
+    uint8_t  s_lvl[2][128];
+    uint32_t s_thr[64];
+    uint16_t s_list[(LW / 4) * (TILE / 4 + 3)]; // list_edges (>= the horizontal count, 19 x 16)
+    int      s_cnt[8];
 };
 
 // The edges of one direction that filter anything (a length and a nonzero level on either side), listed in LDS
@@ -288,36 +314,39 @@ __device__ __forceinline__ int list_edges(const uint32_t *rec, int n, const uint
     return s_cnt[3]; // the last group's cursor ends at the total
 }
 
+// one (plane job, tile, trial) item -- item `bi` of `nbi` -- of a trial or apply launch (uniform per workgroup)
 template <typename T, bool TRIAL>
-__global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a) {
-    __shared__ __align__(16) uint16_t t[LW * LW];
-    __shared__ uint32_t rv[(LW / 4) * (TILE / 4 + 3)]; // vertical-edge records: 22 rows x 19 edges
-    __shared__ uint32_t rh[(TILE / 4 + 3) * (TILE / 4)]; // horizontal-edge records: 19 edges x 16 cols
-    __shared__ unsigned long long red[NTHR / 64];
-    // this workgroup's level table (per direction and level class) and the per-level thresholds (mblim | lim << 8 |
-    // hev << 16), looked up per edge with lane-varying indices: from LDS, not from the kernel arguments (a
-    // lane-varying index into the argument block is a memory load per lookup)
-    __shared__ uint8_t  s_lvl[2][128];
-    __shared__ uint32_t s_thr[64];
-    __shared__ uint16_t s_list[(LW / 4) * (TILE / 4 + 3)]; // list_edges (>= the horizontal count, 19 x 16)
-    __shared__ int      s_cnt[8];
-    const int tid = threadIdx.x;
+__device__ __forceinline__ void dlf_tile_item(KArgs &a, int bi, int nbi, DlfTileLds &L) {
+    uint16_t           *t = L.t;
+    uint32_t           *rv = L.rv, *rh = L.rh;
+    unsigned long long *red = L.red;
+    uint8_t(*s_lvl)[128]   = L.s_lvl;
+    uint32_t           *s_thr = L.s_thr;
+    uint16_t           *s_list = L.s_list;
+    int                *s_cnt = L.s_cnt;
+    const int           tid = threadIdx.x;
     wgclk_mark(a.wgclk, 0);
-    // one (plane job, tile, trial) per workgroup: the trials of a tile are neighbours after the XCD swizzle, so
-    // the second staging of a tile hits the L2; one working image in LDS (18 KB) keeps 8 waves per SIMD
-    const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+    // one (plane job, tile, trial) per item: the trials of a tile are neighbours after the XCD swizzle, so the second
+    // staging of a tile hits the L2; one working image in LDS (18 KB) keeps 8 waves per SIMD.  a.dyn: the items are the
+    // device plan's levels only (its trial count per job), no item for an untried level
+    const int b = xcd_swizzle(bi, nbi);
+#define DLF_NTR(j) (TRIAL ? (a.dyn ? a.plan->ntrial[j] : a.job[j].ntrial) : 1)
     int       jb = 0, tb = b;
-    while (jb + 1 < a.njob && tb >= a.job[jb].tiles * (TRIAL ? a.job[jb].ntrial : 1))
-        tb -= a.job[jb].tiles * (TRIAL ? a.job[jb].ntrial : 1), jb++;
-    const DlfPlaneJob &J = a.job[jb];
-    const int tr = TRIAL ? tb % J.ntrial : 0;
-    if (TRIAL) tb /= J.ntrial;
+    while (jb + 1 < a.njob && tb >= a.job[jb].tiles * DLF_NTR(jb)) tb -= a.job[jb].tiles * DLF_NTR(jb), jb++;
+    KJob     &J  = a.job[jb];
+    const int nt = DLF_NTR(jb);
+#undef DLF_NTR
+    if (TRIAL && nt == 0) return;
+    const int tr = TRIAL ? tb % nt : 0;
+    if (TRIAL) tb /= nt;
     if (TRIAL && a.plan && tr >= a.plan->ntrial[jb]) return; // a level the device plan does not try this launch
     const int x0 = J.ox + (tb % J.tiles_x) * TILE, y0 = J.oy + (tb / J.tiles_x) * TILE;
     const int gx = x0 - APRON, gy = y0 - APRON;
     const T  *src = (const T *)J.src;
+    __syncthreads(); // this workgroup's previous item is done with the LDS
     s_lvl[tid >> 7][tid & 127] = (TRIAL && a.plan) ? a.plan->lvl[jb][tr][tid >> 7][tid & 127]
-                                                   : J.lvl[tr][tid >> 7][tid & 127]; // NTHR == 256 entries
+                               : (!TRIAL && a.dev_lvl) ? a.dev_lvl[(J.plane * 2 + (tid >> 7)) * 128 + (tid & 127)]
+                                                       : J.lvl[tr][tid >> 7][tid & 127]; // NTHR == 256 entries
     if (tid < 64) s_thr[tid] = (uint32_t)a.mblim[tid] | ((uint32_t)a.lim[tid] << 8) | ((uint32_t)a.hev[tid] << 16);
 
     // edge records reaching the tile (no records outside the plane: length 0) and the tile + apron (samples outside
@@ -455,6 +484,14 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a) 
         }
     }
     wgclk_mark(a.wgclk, 5);
+}
+
+template <typename T, bool TRIAL>
+__global__ __launch_bounds__(NTHR, 8) void dlf_tile_kernel(const DlfTileArgs a0) {
+    __shared__ __align__(16) DlfTileLds L;
+    KArgs    &a   = kargs();
+    const int tid = threadIdx.x;
+    dlf_tile_item<T, TRIAL>(a, blockIdx.x, gridDim.x, L);
     // trial: the last workgroup to finish reads the sums (8-B agent atomics on both sides; this lane's SSE adds have
     // completed before its arrival is counted) and re-arms the accumulators for the next launch
     if (TRIAL && tid == 0 && !a.plan) { // (device plan: dlf_search_step_kernel reads the sums in stream order)
@@ -528,6 +565,11 @@ struct SvtGpuDlfState {
     SvtGpuLfMi    *h_mi = nullptr;      // pinned staging of the mode info (one upload per frame, asynchronous)
     SvtGpuPrioLane prio;                // the level search's trial launches
     hipEvent_t     mi_free = nullptr;   // the previous upload has read h_mi
+    // svtgpu_dlf_pick_async: the result the device search leaves (device: the apply's tables; mapped: the caller's
+    // levels), the picks enqueued / collected, the parameters it started from, the rounds to enqueue next time
+    void          *d_res = nullptr, *h_res = nullptr, *h_res_dev = nullptr;
+    int32_t        dev_seq = 0, dev_pending = 0, dev_ready = 0, dev_rounds = 6;
+    SvtGpuLfParams dev_params{};
 };
 
 namespace {
@@ -589,6 +631,7 @@ __host__ __device__ bool plane_active(const SvtGpuLfParams &p, int plane) {
 DlfPlaneJob plane_job(SvtGpuDlfState *s, const SvtGpuFrame *f, int plane, bool trial) {
     DlfPlaneJob j;
     std::memset(&j, 0, sizeof j);
+    j.plane   = plane;
     const int ch = plane > 0;
     j.rec_v   = s->d_rec[ch][0];
     j.rec_h   = s->d_rec[ch][1];
@@ -734,6 +777,13 @@ struct DlfDevSearch {
     int32_t        ns;
     SvtGpuLfParams p;
     DlfDevPlan     plan;
+    int32_t        rounds; // trial rounds taken (svtgpu_dlf_pick_async)
+};
+// what an asynchronous search leaves for the apply (device) and the caller (mapped host memory)
+struct DlfDevResult {
+    int32_t levels[4]; // filter_level[0], [1], _u, _v
+    int32_t rounds, seq, pad[2];
+    uint8_t lvl[3][2][128]; // the apply's level tables of the picked levels (zero for a plane that is not filtered)
 };
 
 // the next launch's levels per search (the bisection steps), then each (search, level)'s tables: that plane's only, as
@@ -769,30 +819,135 @@ void plan_next(DlfDevSearch &S) { // host
     for (int e = 0; e < PLAN_ENTRIES; e++) plan_table_entry(S, e);
 }
 
-// one bisection decision per search from the last trial launch's sums (which it re-zeroes), then the next plan.  The
-// state is copied into LDS by the wave and walked there by one lane (the search is a chain of dependent reads: from
-// global memory each would wait a full memory latency), then written back
+// one bisection decision per search from the last trial launch's sums (re-zeroed), then the next plan.  The state is
+// copied into the LDS words `w` (>= sizeof(DlfDevSearch) / 4) by the workgroup and walked there by one lane (the
+// search is a chain of dependent reads: from global memory each would wait a full memory latency), then written back.
+// atomic_sums: the sums are exchanged to zero with device-scope atomics (a workgroup of the trial launch itself runs
+// the step), else read and zeroed in stream order
 static_assert(sizeof(DlfDevSearch) % 4 == 0, "word copies of the search state");
-__global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
+static_assert(sizeof(DlfDevSearch) <= sizeof(DlfTileLds::t), "the step's LDS copy fits the tile image it reuses");
+__device__ void dlf_step(DlfDevSearch *S, unsigned long long *sse, uint32_t *w, bool atomic_sums) {
     constexpr int NW = (int)(sizeof(DlfDevSearch) / 4);
-    __shared__ __align__(16) uint32_t w[NW];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < NW; i += 64) w[i] = ((const uint32_t *)S)[i];
+    const int     tid = threadIdx.x, nt = blockDim.x;
+    for (int i = tid; i < NW; i += nt) w[i] = ((const uint32_t *)S)[i];
     __syncthreads();
     DlfDevSearch &D = *(DlfDevSearch *)w;
     if (D.plan.done) return; // uniform: every lane read the same word
     if (tid == 0) {
         unsigned long long v[MAX_JOBS * MAX_TRIALS];
-        for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) v[q] = sse[q];
+        for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) v[q] = atomic_sums ? atomicExch(&sse[q], 0ull) : sse[q];
         for (int i = 0; i < D.ns; i++)
             if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], v + i * MAX_TRIALS);
         plan_levels(D);
+        D.rounds++;
     }
     __syncthreads();
-    for (int e = tid; e < PLAN_ENTRIES; e += 64) plan_table_entry(D, e); // the tables: one entry per lane and pass
+    for (int e = tid; e < PLAN_ENTRIES; e += nt) plan_table_entry(D, e); // the tables: one entry per lane and pass
     __syncthreads();
-    if (tid < MAX_JOBS * MAX_TRIALS) sse[tid] = 0;
+    if (!atomic_sums && tid < MAX_JOBS * MAX_TRIALS) sse[tid] = 0;
+    for (int i = tid; i < NW; i += nt) ((uint32_t *)S)[i] = w[i];
+}
+__global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
+    __shared__ __align__(16) uint32_t w[sizeof(DlfDevSearch) / 4];
+    dlf_step(S, sse, w, false);
+}
+
+// svtgpu_dlf_pick_async, 1: the searches' start (LevelSearch's constructor: the start level) and the first plan,
+// from the caller's parameters -- no host staging
+__global__ __launch_bounds__(64) void dlf_search_init_kernel(DlfDevSearch *S, SvtGpuLfParams p, int ns, int dlf_avg,
+                                                            int early_exit, int only4x4) {
+    __shared__ __align__(16) uint32_t w[sizeof(DlfDevSearch) / 4];
+    constexpr int NW = (int)(sizeof(DlfDevSearch) / 4);
+    DlfDevSearch &D  = *(DlfDevSearch *)w;
+    const int     tid = threadIdx.x;
+    if (tid == 0) {
+        const int last[4] = {p.filter_level[0], p.filter_level[1], p.filter_level_u, p.filter_level_v};
+        const int dirs[3] = {2, 0, 0};
+        for (int i = 0; i < MAX_JOBS; i++) D.srch[i] = LevelSearch(last, dlf_avg, early_exit, only4x4, i, dirs[i]);
+        D.ns = ns, D.p = p, D.rounds = 0;
+        plan_levels(D);
+    }
+    __syncthreads();
+    for (int e = tid; e < PLAN_ENTRIES; e += 64) plan_table_entry(D, e);
+    __syncthreads();
     for (int i = tid; i < NW; i += 64) ((uint32_t *)S)[i] = w[i];
+}
+
+// svtgpu_dlf_pick_async, 2: one trial round of the device plan (items = the plan's levels only);
+// the last workgroup to finish takes the bisection step (fuse; a tiled rank steps after the SSE all-reduce instead)
+template <typename T>
+__global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArgs a0, DlfDevSearch *S, int fuse) {
+    __shared__ __align__(16) DlfTileLds L;
+    KArgs    &a = kargs();
+    __shared__ int last;
+    const int tid    = threadIdx.x;
+    int       nitems = 0;
+    for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
+    // one item per workgroup over a grid sized for the most levels a round can try; the workgroups past this round's
+    // items go straight to the arrival count (a persistent loop over the items spilled 60 VGPRs: the item's registers
+    // live across the loop)
+    if ((int)blockIdx.x < nitems) dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
+    if (!fuse) return;
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence(); // this workgroup's SSE atomics before its arrival
+        last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    dlf_step(S, a.sse, (uint32_t *)L.t, true);
+    if (tid == 0) atomicExch(a.arrive, 0u);
+}
+
+// svtgpu_dlf_pick_async, 3: one workgroup.  A search still unfinished after the enqueued rounds (they are sized from the
+// previous frame's count) continues here, exactly, each round's items looped by this workgroup alone -- slow, but no
+// host decision; then the apply's level tables of the picked levels and the caller's result (mapped memory)
+template <typename T>
+__global__ __launch_bounds__(NTHR) void dlf_finish_kernel(const DlfTileArgs a0, DlfDevSearch *S, DlfDevResult *res,
+                                                          DlfDevResult *host, int seq) {
+    __shared__ __align__(16) DlfTileLds L;
+    KArgs    &a = kargs();
+    __shared__ int done;
+    const int tid = threadIdx.x;
+    for (int guard = 0; guard < 4096; guard++) { // a search ends after at most ~64 rounds
+        if (tid == 0) done = __hip_atomic_load(&S->plan.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (done) break;
+        int nitems = 0;
+        for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
+        for (int i = 0; i < nitems; i++) dlf_tile_item<T, true>(a, i, nitems, L);
+        __syncthreads();
+        __threadfence();
+        dlf_step(S, a.sse, (uint32_t *)L.t, true);
+        __syncthreads();
+    }
+    // the picked levels (svt_av1_pick_filter_level: luma both directions from the dir-2 search; chroma searched, or the
+    // start levels when dlf_avg_uv skips it) and their tables (build_level_tables / plane_active / luma_off)
+    __shared__ int lv[4];
+    if (tid == 0) {
+        const DlfDevSearch &D = *S;
+        lv[0] = lv[1] = D.srch[0].best;
+        lv[2] = D.ns == 3 ? D.srch[1].best : D.p.filter_level_u;
+        lv[3] = D.ns == 3 ? D.srch[2].best : D.p.filter_level_v;
+    }
+    __syncthreads();
+    SvtGpuLfParams q = S->p;
+    q.filter_level[0] = lv[0], q.filter_level[1] = lv[1], q.filter_level_u = lv[2], q.filter_level_v = lv[3];
+    const bool luma_off = !plane_active(q, 0);
+    for (int e = tid; e < 3 * 2 * 128; e += NTHR) {
+        const int pl = e >> 8, d = (e >> 7) & 1, cls = e & 127;
+        const int base = pl == 0 ? q.filter_level[d] : pl == 1 ? q.filter_level_u : q.filter_level_v;
+        res->lvl[pl][d][cls] = (!luma_off && plane_active(q, pl)) ? level_entry(q, pl, d, base, cls) : 0;
+    }
+    if (tid < 4) res->levels[tid] = lv[tid];
+    if (tid == 0) {
+        res->rounds = S->rounds, res->seq = seq;
+        for (int k = 0; k < 4; k++) __hip_atomic_store(&host->levels[k], lv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host->rounds, S->rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(&host->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // (trial, step) pairs per host read-back; 0: the host-driven search.  Default: the device search for a tile of a
@@ -989,6 +1144,8 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     (void)hipFree(s->d_arrive);
     if (s->h_sse) (void)hipHostFree(s->h_sse);
     (void)hipFree(s->d_search);
+    (void)hipFree(s->d_res);
+    if (s->h_res) (void)hipHostFree(s->h_res);
     svtgpu_prio_destroy(&s->prio);
     if (s->h_search) (void)hipHostFree(s->h_search);
     delete s;
@@ -1087,7 +1244,11 @@ namespace {
 // allowed (the planes are staged in scratch)
 int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, const SvtGpuLfParams *params,
                    int32_t ps, int32_t pe, hipStream_t st) {
-    if (s->mi_on_device) { // a device grid no pick has reported on (the FROM_Q levels): its verdict first
+    // params == nullptr: the levels of the last svtgpu_dlf_pick_async, as level tables on the device (every plane goes
+    // through the tile kernel: a plane that is not filtered has all-zero tables, lists no edge and is copied)
+    const bool dev = params == nullptr;
+    if (dev) params = &s->dev_params;
+    if (s->mi_on_device && !dev) { // a device grid no pick has reported on (the FROM_Q levels): its verdict first
         s->mi_on_device = 0;
         if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded when an exchange may sit before it
         if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
@@ -1100,7 +1261,7 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
     for (int pl = ps; pl < pe; pl++) {
         if (pl == 0 && !plane_active(*params, 0)) luma_off = true; // no plane is filtered (:575-577)
         const size_t bps = in->bytes_per_sample;
-        const bool   on  = !luma_off && plane_active(*params, pl);
+        const bool   on  = dev || (!luma_off && plane_active(*params, pl));
         if (!on) { // the output rectangle of the plane passes through
             const DlfPlaneJob R = plane_job(s, in, pl, false);
             if (in != out && R.ow > 0 && R.oh > 0) {
@@ -1131,6 +1292,7 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
         J.ntrial     = 1;
         for (int dir = 0; dir < 2; dir++) std::memcpy(J.lvl[0][dir], L.lvl[pl][dir], 128);
     }
+    if (dev) a.dev_lvl = ((const DlfDevResult *)s->d_res)->lvl[0][0];
     if (a.njob) return launch_tile(a, (int)in->bytes_per_sample, false, st);
     return SVTGPU_OK;
 }
@@ -1138,7 +1300,7 @@ int dlf_frame_impl(SvtGpuDlfState *s, const SvtGpuFrame *in, SvtGpuFrame *out, c
 
 extern "C" int svtgpu_dlf_frame(SvtGpuDlfState *s, SvtGpuFrame *frame, const SvtGpuLfParams *params,
                                 int32_t plane_start, int32_t plane_end, void *stream) {
-    if (!s || !frame_matches(s, frame) || !valid_params(params) || plane_start < 0 || plane_end > 3 ||
+    if (!s || !frame_matches(s, frame) || (params ? !valid_params(params) : !s->dev_ready) || plane_start < 0 || plane_end > 3 ||
         plane_start > plane_end || !s->have_mi)
         return SVTGPU_ERR_INVALID_ARG;
     return dlf_frame_impl(s, frame, frame, params, plane_start, plane_end, pick_stream(s->ctx, stream));
@@ -1148,7 +1310,8 @@ extern "C" int svtgpu_dlf_frame_to(SvtGpuDlfState *s, const SvtGpuFrame *in, Svt
                                    const SvtGpuLfParams *params, int32_t plane_start, int32_t plane_end,
                                    void *stream) {
     if (!s || !frame_matches(s, in) || !frame_matches(s, out) || in->bit_depth != out->bit_depth ||
-        !valid_params(params) || plane_start < 0 || plane_end > 3 || plane_start > plane_end || !s->have_mi)
+        (params ? !valid_params(params) : !s->dev_ready) || plane_start < 0 || plane_end > 3 || plane_start > plane_end ||
+        !s->have_mi)
         return SVTGPU_ERR_INVALID_ARG;
     return dlf_frame_impl(s, in, out, params, plane_start, plane_end, pick_stream(s->ctx, stream));
 }
@@ -1189,6 +1352,120 @@ extern "C" int svtgpu_dlf_pick(SvtGpuDlfState *s, SvtGpuFrame *recon, const SvtG
     p.filter_level_u = search_uv ? us.best : last[2];
     p.filter_level_v = search_uv ? vs.best : last[3];
     *params          = p;
+    return SVTGPU_OK;
+}
+
+// The level search with no host wait: the start (dlf_search_init_kernel), a number of device trial rounds sized from the
+// previous search's count, each stepping itself (dlf_trial_dev_kernel), then dlf_finish_kernel, which completes a search
+// still open and writes the apply's tables and the caller's levels -- all in stream order.  A picture tiled over GPUs
+// (an all-reduce between a trial round and its step) runs the synchronous search here and keeps its levels.
+extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon, const SvtGpuFrame *source,
+                                     const SvtGpuLfParams *params, int32_t dlf_avg, int32_t dlf_avg_uv,
+                                     int32_t temporal_layer_index, int32_t early_exit_convergence,
+                                     int32_t tx_mode_only_4x4, void *stream) {
+    if (!s || !frame_matches(s, recon) || !frame_matches(s, source) || source->bit_depth != recon->bit_depth ||
+        !valid_params(params) || !s->have_mi)
+        return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    if (!s->d_res) {
+        HIP_TRY(hipMalloc(&s->d_res, sizeof(DlfDevResult)));
+        HIP_TRY(hipHostMalloc(&s->h_res, sizeof(DlfDevResult), hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(s->h_res, 0, sizeof(DlfDevResult));
+        HIP_TRY(hipHostGetDevicePointer(&s->h_res_dev, s->h_res, 0));
+    }
+    if (svtgpu_comm_tiled(s->comm)) { // the tiled search (host read-backs per chunk); its levels become the result
+        SvtGpuLfParams p = *params;
+        if (int rc = svtgpu_dlf_pick(s, const_cast<SvtGpuFrame *>(recon), source, &p, dlf_avg, dlf_avg_uv, temporal_layer_index,
+                                     early_exit_convergence, tx_mode_only_4x4, stream))
+            return rc;
+        DlfDevResult r;
+        std::memset(&r, 0, sizeof r);
+        LevelTables L;
+        build_level_tables(p, L);
+        const bool luma_off = !plane_active(p, 0);
+        for (int pl = 0; pl < 3; pl++)
+            if (!luma_off && plane_active(p, pl)) std::memcpy(r.lvl[pl], L.lvl[pl], sizeof r.lvl[pl]);
+        r.levels[0] = p.filter_level[0], r.levels[1] = p.filter_level[1], r.levels[2] = p.filter_level_u;
+        r.levels[3] = p.filter_level_v, r.seq = ++s->dev_seq;
+        std::memcpy(s->h_res, &r, sizeof r);
+        HIP_TRY(hipMemcpyAsync(s->d_res, s->h_res, sizeof r, hipMemcpyHostToDevice, st));
+        s->dev_params = p, s->dev_ready = 1, s->dev_pending = 1;
+        return SVTGPU_OK;
+    }
+    if (!s->d_search) {
+        HIP_TRY(hipMalloc(&s->d_search, sizeof(DlfDevSearch)));
+        HIP_TRY(hipHostMalloc(&s->h_search, sizeof(DlfDevSearch), hipHostMallocDefault));
+    }
+    // the rounds to enqueue: one more than the previous search took (read from mapped memory without waiting: the
+    // previous result when it is already there, else the last hint); SVTGPU_DLF_ROUNDS=k fixes it (tests: 1 makes the
+    // finish kernel complete the search)
+    static const int fixed = [] {
+        const char *e = std::getenv("SVTGPU_DLF_ROUNDS");
+        return e ? std::max(1, std::min(64, std::atoi(e))) : 0;
+    }();
+    const volatile DlfDevResult *hr = (const volatile DlfDevResult *)s->h_res;
+    if (hr->seq == s->dev_seq && s->dev_seq) s->dev_rounds = std::max(2, std::min(16, hr->rounds + 1));
+    const int rounds = fixed ? fixed : s->dev_rounds;
+    SvtGpuLfParams p  = *params;
+    p.sharpness_level = 0;
+    const int ns      = (dlf_avg_uv && temporal_layer_index > 0) ? 1 : 3;
+    DlfDevSearch *D   = (DlfDevSearch *)s->d_search;
+    hipLaunchKernelGGL(dlf_search_init_kernel, dim3(1), dim3(64), 0, st, D, p, ns, dlf_avg, early_exit_convergence,
+                       tx_mode_only_4x4);
+    HIP_TRY(hipGetLastError());
+    LevelTables L;
+    build_level_tables(p, L); // the thresholds (sharpness 0); the levels come from the plan
+    DlfTileArgs a = base_args(recon, L);
+    int         max_items = 0;
+    for (int i = 0; i < ns; i++) {
+        DlfPlaneJob &J = a.job[i];
+        J              = plane_job(s, recon, i, true);
+        J.src = recon->plane[i], J.src_stride = recon->stride[i];
+        J.ref = source->plane[i], J.ref_stride = source->stride[i];
+        J.ntrial = MAX_TRIALS;
+        max_items += J.tiles * MAX_TRIALS;
+    }
+    a.njob = ns, a.sse = s->d_sse, a.arrive = s->d_arrive, a.plan = &D->plan, a.dyn = 1;
+    const int grid = std::max(1, max_items);
+    for (int k = 0; k < rounds; k++) {
+        if (recon->bytes_per_sample == 2)
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint16_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
+        else
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint8_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
+        HIP_TRY(hipGetLastError());
+    }
+    const int seq = ++s->dev_seq;
+    if (recon->bytes_per_sample == 2)
+        hipLaunchKernelGGL(dlf_finish_kernel<uint16_t>, dim3(1), dim3(NTHR), 0, st, a, D, (DlfDevResult *)s->d_res,
+                           (DlfDevResult *)s->h_res_dev, seq);
+    else
+        hipLaunchKernelGGL(dlf_finish_kernel<uint8_t>, dim3(1), dim3(NTHR), 0, st, a, D, (DlfDevResult *)s->d_res,
+                           (DlfDevResult *)s->h_res_dev, seq);
+    HIP_TRY(hipGetLastError());
+    s->dev_params = p, s->dev_ready = 1, s->dev_pending = 1;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_dlf_read_levels(SvtGpuDlfState *s, SvtGpuLfParams *params_out, void *stream) {
+    if (!s || !params_out || !s->dev_ready) return SVTGPU_ERR_INVALID_ARG;
+    if (s->dev_pending) {
+        if (int rc = svtgpu_comm_wait(s->comm, pick_stream(s->ctx, stream))) return rc;
+        s->dev_pending = 0;
+        if (((const volatile DlfDevResult *)s->h_res)->seq != s->dev_seq) {
+            svtgpu_set_last_hip_error(hipErrorUnknown, "dlf asynchronous level search: result word missing after the "
+                                      "stream wait", __FILE__, __LINE__);
+            return SVTGPU_ERR_HIP;
+        }
+        if (s->mi_on_device) { // the device grid's verdict (its records kernel ran before the search)
+            s->mi_on_device = 0;
+            if (take_bad_mi(s)) return SVTGPU_ERR_INVALID_ARG;
+        }
+    }
+    const volatile DlfDevResult *r = (const volatile DlfDevResult *)s->h_res;
+    SvtGpuLfParams               p = s->dev_params;
+    p.filter_level[0] = r->levels[0], p.filter_level[1] = r->levels[1];
+    p.filter_level_u = r->levels[2], p.filter_level_v = r->levels[3];
+    *params_out = p;
     return SVTGPU_OK;
 }
 

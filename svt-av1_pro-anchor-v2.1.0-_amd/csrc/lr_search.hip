@@ -3731,6 +3731,18 @@ extern "C" int svtgpu_lr_search_frame_async(SvtGpuLrState *s, const SvtGpuFrame 
         : search_frame<uint8_t>(s, recon, source, ctrls, nplanes, rb, re, cb, ce, nullptr, nullptr, st, 1);
 }
 
+extern "C" int svtgpu_lr_read_units(SvtGpuLrState *s, int32_t plane, SvtGpuRestUnit *units_out, void *stream) {
+    if (!s || plane < 0 || plane > 2 || !units_out) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    if (s->fin_pending)
+        if (int rc = lr_collect(s, st, nullptr)) return rc;
+    const size_t n = (size_t)s->hunits[plane] * s->vunits[plane];
+    HIP_TRY(hipMemcpyAsync(units_out, s->d_units[plane], sizeof(SvtGpuRestUnit) * n, hipMemcpyDeviceToHost, st));
+    svtgpu_count_xfer(1, sizeof(SvtGpuRestUnit) * n);
+    HIP_TRY(hipStreamSynchronize(st));
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_lr_read_result(SvtGpuLrState *s, int32_t frame_type_out[3], void *stream) {
     if (!s || !frame_type_out) return SVTGPU_ERR_INVALID_ARG;
     if (s->fin_pending) return lr_collect(s, pick_stream(s->ctx, stream), frame_type_out);

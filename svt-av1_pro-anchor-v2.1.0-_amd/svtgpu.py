@@ -257,6 +257,8 @@ _SIGS = {
     "svtgpu_dlf_frame": (ctypes.c_int, [_P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_frame_to": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _P]),
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_dlf_pick_async": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_dlf_read_levels": (ctypes.c_int, [_P, ctypes.POINTER(LfParams), _P]),
     "svtgpu_dlf_pick_by_q": (ctypes.c_int, [_P, _P]),
     "svtgpu_dlf_qp_based_param": (ctypes.c_int, [_I32, _I32, _I32, _P, _P]),
     "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
@@ -349,6 +351,7 @@ _SIGS = {
     "svtgpu_lr_finish_frame": (ctypes.c_int, [ctypes.POINTER(LrSearchControls), _P, _P, _P, _P]),
     "svtgpu_lr_search_frame_async": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LrSearchControls), _P]),
     "svtgpu_lr_read_result": (ctypes.c_int, [_P, _P, _P]),
+    "svtgpu_lr_read_units": (ctypes.c_int, [_P, _I32, _P, _P]),
     "svtgpu_lr_profile": (ctypes.c_int, [_P, _I32, _P]),
     "svtgpu_transfer_bytes": (ctypes.c_int, [_P, _P, _I32]),
     "svtgpu_comm_unique_id": (ctypes.c_int, [_P]),
@@ -742,10 +745,29 @@ class DlfState:
         check(lib().svtgpu_dlf_set_mode_info_device(self.h, _P(d_mi), stream))
 
     def filter(self, frame, params, plane_start=0, plane_end=3, stream=None):
-        check(lib().svtgpu_dlf_frame(self.h, frame.h, ctypes.byref(params), plane_start, plane_end, stream))
+        """svtgpu_dlf_frame; params None: the levels of the last pick_async (on the device, in stream order)."""
+        check(lib().svtgpu_dlf_frame(self.h, frame.h, None if params is None else ctypes.byref(params), plane_start,
+                                     plane_end, stream))
 
     def filter_to(self, src, out, params, plane_start=0, plane_end=3, stream=None):
-        check(lib().svtgpu_dlf_frame_to(self.h, src.h, out.h, ctypes.byref(params), plane_start, plane_end, stream))
+        """svtgpu_dlf_frame_to; params None: the levels of the last pick_async (on the device, in stream order)."""
+        check(lib().svtgpu_dlf_frame_to(self.h, src.h, out.h, None if params is None else ctypes.byref(params),
+                                        plane_start, plane_end, stream))
+
+    def pick_async(self, recon, source, params, dlf_avg=0, dlf_avg_uv=0, temporal_layer_index=0, early_exit=2,
+                   only_4x4=0, stream=None):
+        """svtgpu_dlf_pick_async: the level search on the device, no host wait; filter(_to)(..., None) applies the
+        picked levels, read_levels() returns them."""
+        p = LfParams()
+        ctypes.pointer(p)[0] = params
+        check(lib().svtgpu_dlf_pick_async(self.h, recon.h, source.h, ctypes.byref(p), dlf_avg, dlf_avg_uv,
+                                          temporal_layer_index, early_exit, only_4x4, stream))
+
+    def read_levels(self, stream=None):
+        """svtgpu_dlf_read_levels: waits for the last pick_async and returns its LfParams."""
+        p = LfParams()
+        check(lib().svtgpu_dlf_read_levels(self.h, ctypes.byref(p), stream))
+        return p
 
     def set_crop(self, crop_width, crop_height):
         """svtgpu_dlf_set_crop: no edge at or past the unpadded size is filtered (next set_mode_info on)."""
@@ -899,6 +921,12 @@ class LrState:
         """svtgpu_lr_search_frame_async: search + device RD finish enqueued on `stream`, no host wait; apply(...,
         frame_type=None) applies the result in stream order, read_result() collects the frame types."""
         check(lib().svtgpu_lr_search_frame_async(self.h, recon.h, source.h, ctypes.byref(ctrls), stream))
+
+    def read_units(self, plane, stream=None):
+        """svtgpu_lr_read_units: the state's units of `plane` (waits for an asynchronous search)."""
+        u = np.zeros(self.units[plane][0] * self.units[plane][1], REST_UNIT_DTYPE)
+        check(lib().svtgpu_lr_read_units(self.h, plane, ptr(u), stream))
+        return u
 
     def read_result(self, stream=None):
         """svtgpu_lr_read_result: waits for the last asynchronous search and returns its frame types."""

@@ -182,8 +182,14 @@ def run_oracle(case):
                 fbs=fbs, applied=applied, cdef=cdef, ft=ft, units=units, recs=recs, lrc=lrc, lr=lr)
 
 
-def run_gpu(case, ctx=None):
-    """The MI355X library (libsvtgpu) on the whole path, one stream, frames resident on the device."""
+def run_gpu(case, ctx=None, async_=None):
+    """The MI355X library (libsvtgpu) on the whole path, one stream, frames resident on the device.  async_ (default:
+    SVTGPU_TEST_ASYNC=1 in the environment): the DLF level search and the LR search + RD finish in their asynchronous
+    forms (svtgpu_dlf_pick_async + filter with the device levels, svtgpu_lr_search_frame_async + apply with the device
+    units), the levels / frame types / units read back at the end."""
+    import os
+    if async_ is None:
+        async_ = os.environ.get("SVTGPU_TEST_ASYNC") == "1"
     import svtgpu
     c = pc.CASES[case]
     g = pc.load(case)
@@ -195,8 +201,14 @@ def run_gpu(case, ctx=None):
     R.upload(rec)
     dl = svtgpu.DlfState(ctx, w, h)
     dl.set_mode_info(mi)
-    lfp = gpu_dlf_pick(dl, R, S, c)
-    dl.filter_to(R, D, lfp)
+    if async_ and not dlf_ctrls(c["dlf_level"])["sb_based"]:
+        dc = dlf_ctrls(c["dlf_level"])
+        dl.pick_async(R, S, pc.lf_params(c), dc["avg"], dc["avg_uv"], c["tl"], dc["early_exit"], c["only4x4"])
+        dl.filter_to(R, D, None)
+        lfp = dl.read_levels()
+    else:
+        lfp = gpu_dlf_pick(dl, R, S, c)
+        dl.filter_to(R, D, lfp)
     st = svtgpu.CdefState(ctx, w, h)
     st.set_block_mask(pc.cdef_mask(mi))
     if c["sb"] == 128:
@@ -215,12 +227,18 @@ def run_gpu(case, ctx=None):
     us = [c["us"][0], c["us"][1], c["us"][1]]
     lr = svtgpu.LrState(ctx, w, h, us)
     lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
-    ft, recs = lr.search(C, S, lrc, records=True)
-    units = [svtgpu.lr_finish_plane(lrc, p, recs[p])[1] for p in range(3)]
-    if any(ft):
-        lr.apply(D, C, O, ft)
+    if async_:
+        lr.search_async(C, S, lrc)
+        lr.apply(D, C, O, None)
+        ft, recs = lr.read_result(), None
+        units = [lr.read_units(p) for p in range(3)]
     else:
-        svtgpu.check(svtgpu.lib().svtgpu_frame_copy(O.h, C.h, None))
+        ft, recs = lr.search(C, S, lrc, records=True)
+        units = svtgpu.lr_finish_frame(lrc, recs)[1]
+        if any(ft):
+            lr.apply(D, C, O, ft)
+        else:
+            svtgpu.check(svtgpu.lib().svtgpu_frame_copy(O.h, C.h, None))
     ctx.synchronize()
     out = dict(src=src, rec=rec, mi=mi, lf=lfp.levels(), dlf=D.download(), tables=tables, prm=prm, nb=nb, fbs=fbs,
                applied=applied, cdef=C.download(), ft=ft, units=units, recs=recs, lrc=lrc, lr=O.download())
@@ -335,7 +353,7 @@ def run_gpu_tiled(case, rank, world, comm, ctx=None):
     lr.set_tile(plan["lr_units"], plan["lr_out"], comm)
     lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
     ft, recs = lr.search(C, S, lrc, records=True)
-    units = [svtgpu.lr_finish_plane(lrc, p, recs[p])[1] for p in range(3)]
+    units = svtgpu.lr_finish_frame(lrc, recs)[1]
     if any(ft):
         lr.apply(D, C, O, ft)
     else:
