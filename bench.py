@@ -591,19 +591,23 @@ def bench_md(a, torch, dist, n, rank, local):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     gpu_ms = e0.elapsed_time(e1) / a.steps  # this rank's device time per step
+    # the on-demand expansion of the moments into every shape's values (svtgpu_md_expand), timed apart: a consumer
+    # that wants the per-shape table pays it once per frame
+    e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e2.record(stream)
+    for _ in range(5):
+        md.expand(sb0, sb1, sp)
+    e3.record(stream)
+    torch.cuda.synchronize()
+    expand_ms = e2.elapsed_time(e3) / 5
     if n > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1e3 / a.steps
-    concurrency = sum(slot_lat) / ms_per_step if slot_lat else None
-    if concurrency is not None and F > 1 and concurrency < F / 2:
-        print("bench: WARNING: frames in flight overlap poorly: concurrency %.2f of %d (slot latencies %s ms, step %.2f "
-              "ms) -- frames are serializing (shared hardware queues?)" % (concurrency, F,
-              [round(x, 2) for x in slot_lat], ms_per_step), file=sys.stderr)
     nsb_mine = sb1 - sb0
     alg_in = nsb_mine * (1 + NREF) * 64 * 64 * B
-    alg_out = nsb_mine * NREF * 3 * svtgpu.MD_BLOCKS * 4
+    alg_out = nsb_mine * NREF * 256 * 8  # the cell moments
     gbs = (alg_in + alg_out) / (gpu_ms * 1e-3) / 1e9
     out = {"metric": "MD SAD/SSE/variance Mpixels/s on 8K10b; per-GPU HBM GB/s vs roofline", "value": round(W * H / (ms_per_step * 1e-3) / 1e6, 3),
            "unit": "Mpixels/s", "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -617,9 +621,12 @@ def bench_md(a, torch, dist, n, rank, local):
                       "md_roofline": {"alg_in_MB_per_gpu": round(alg_in / 1e6, 2), "out_MB_per_gpu": round(alg_out / 1e6, 2),
                                       "gpu_ms_per_frame": round(gpu_ms, 4), "achieved_GBs_per_gpu": round(gbs, 1),
                                       "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                      "expand_ms_per_frame": round(expand_ms, 4),
                                       "note": "rank 0's HIP-event time per step; bytes = the SB samples of the source and "
-                                              "every reference read once (SURVEY §8(d)) + the u32 [SB][ref][3][%d] "
-                                              "outputs written once" % svtgpu.MD_BLOCKS}}}
+                                              "every reference read once (SURVEY §8(d)) + the 8-byte moments of every "
+                                              "4x4 cell x ref written once (every shape's SAD / SSE / variance are exact "
+                                              "sums of them; svtgpu_md_expand derives the u32 [SB][ref][3][%d] table "
+                                              "on demand: expand_ms_per_frame)" % svtgpu.MD_BLOCKS}}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     md.close()
@@ -931,6 +938,11 @@ def main():
     dlf_ms, search_ms, cdef_rest_ms, lr_ms, md_ms = (float(x) for x in stage_ms)
 
     ms_per_step = dt * 1e3 / a.steps
+    concurrency = sum(slot_lat) / ms_per_step if slot_lat else None
+    if concurrency is not None and F > 1 and concurrency < F / 2:
+        print("bench: WARNING: frames in flight overlap poorly: concurrency %.2f of %d (slot latencies %s ms, step %.2f "
+              "ms) -- frames are serializing (shared hardware queues?)" % (concurrency, F,
+              [round(x, 2) for x in slot_lat], ms_per_step), file=sys.stderr)
     frames_per_step = F * (1 if tiled else n)  # frames split: every rank filters F frames per step
     value = frames_per_step * W * H / (ms_per_step * 1e-3) / 1e6  # the whole job's luma pixels per second
     def lr_classes(tot):

@@ -682,11 +682,16 @@ uint32_t svtgpu_aom_sub_pixel_variance64x16(const uint8_t *src_ptr, int source_s
 /* Batched MD distortion (the frame-level GPU boundary; no single reference equivalent: it evaluates what
  * the MD candidate loops evaluate block by block through svt_aom_mefn_ptr, av1me.c:29-174).
  * For every 64x64 SB of `source` and every reference frame r at the SB's full-pel motion vector
- * mv[sb][r] = {x, y}, it computes for every block of every AV1 shape <= 64x64 tiling the SB:
+ * mv[sb][r] = {x, y}, svtgpu_md_dist_batch computes the raw moments of every 4x4 cell of the SB (moments[sb][r][256],
+ * cells in raster order, 8 bytes each: x = SAD | (uint16_t)(signed sum) << 16, y = SSE of the differences): every
+ * block of every AV1 shape <= 64x64 tiling the SB has exact sums of its cells' moments.  svtgpu_md_expand derives,
+ * for an SB range, every block's
  *   q = 0: SAD (sad{W}x{H} / sad_16b_kernel), q = 1: the *sse the variance function reports,
- *   q = 2: the variance (8-bit: svt_aom_variance{W}x{H}; 10-bit: svt_aom_highbd_10_variance{W}x{H}).
+ *   q = 2: the variance (8-bit: svt_aom_variance{W}x{H}; 10-bit: svt_aom_highbd_10_variance{W}x{H}, which round only
+ *          the block totals, EbPsnr.c:183-214);
+ * svtgpu_md_read expands and reads an SB range.
  * Samples outside the frame read the nearest edge sample (the encoder's padded pictures).
- * Output layout: out[sb][r][q][SVTGPU_MD_BLOCKS]; shapes in BlockSize order without the 128 shapes,
+ * Expanded layout: out[sb][r][q][SVTGPU_MD_BLOCKS]; shapes in BlockSize order without the 128 shapes,
  * blocks of one shape in raster order (svtgpu_md_layout). */
 #define SVTGPU_MD_SHAPES 19
 #define SVTGPU_MD_BLOCKS 849
@@ -697,8 +702,13 @@ int32_t svtgpu_md_batch_nsb(const SvtGpuMdBatch *b);
 int     svtgpu_md_set_mvs(SvtGpuMdBatch *b, const int16_t *mv, void *stream); /* host [nsb][nref][2] */
 int     svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source, const SvtGpuFrame *const *refs,
                              int32_t sb_begin, int32_t sb_end, void *stream);
+/* every block's values of SBs [sb_begin, sb_end) from the last batch's moments, into the expanded table (in stream
+ * order; svtgpu_md_out_device_ptr) -- for a consumer that wants per-shape values rather than the moments */
+int     svtgpu_md_expand(SvtGpuMdBatch *b, int32_t sb_begin, int32_t sb_end, void *stream);
+/* expands SBs [sb_begin, sb_end) and copies their rows [sb][r][3][SVTGPU_MD_BLOCKS] to `out` (synchronous) */
 int     svtgpu_md_read(SvtGpuMdBatch *b, uint32_t *out, int32_t sb_begin, int32_t sb_end, void *stream);
-void   *svtgpu_md_out_device_ptr(SvtGpuMdBatch *b);
+void   *svtgpu_md_out_device_ptr(SvtGpuMdBatch *b);     /* the expanded table [nsb][nref][3][SVTGPU_MD_BLOCKS] */
+void   *svtgpu_md_moments_device_ptr(SvtGpuMdBatch *b); /* the cell moments [nsb][nref][256] (uint32 pairs) */
 /* shape_w/shape_h/shape_offset: [SVTGPU_MD_SHAPES] block dims and first output index of each shape */
 void    svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offset);
 

@@ -5,12 +5,16 @@
 // (highbd_10_variance{W}x{H}), Encoder/Codec/EbEncInterPrediction.c:562-590 (sse / highbd_sse),
 // Common/C_DEFAULT/EbPictureOperators_C.c:62 and Common/Codec/EbPictureOperators.c:174 (full distortion).
 //
-// Batch design (svtgpu_md_dist_batch): one 256-lane workgroup per 64x64 SB stages the source SB in LDS
-// once and loops over the reference frames.  Each lane owns one 4x4 cell (lanes 0-15 of a cell row read
-// 64 consecutive samples of a picture row, so each load instruction covers 4 rows x 128 B); the cell's
-// SAD, SSE and signed sum are additive, so every larger shape is reduced from two halves of a smaller
-// one in 8 LDS passes (no sample is read twice), and the per-bit-depth variance formula of the
-// reference is applied per block at the end.  Output rows [q][849] per (SB, ref) are written coalesced.
+// Batch design (svtgpu_md_dist_batch, round 6): the raw moments of every 4x4 cell -- SAD, signed sum and SSE of the
+// differences, additive over cells -- per (SB, reference): one 256-lane workgroup per 64x64 SB, each lane owning one
+// 4x4 cell, its 16 source samples in registers across the references (lanes 0-15 of a cell row read 64 consecutive
+// samples of a picture row, so each load instruction covers 4 rows x 128 B), one 8-byte store per cell and reference:
+// 2 KB per (SB, reference) instead of the 849 x 3 words (10.2 KB) of every shape's values, which wrote more than the
+// kernel read (146 MB of outputs against 137 MB of reads per 4K frame, 7 references).  Every shape's SAD, SSE and sum
+// are exact sums of its cells' moments, and the reference's variance rounds only the block totals
+// (svt_aom_highbd_10_variance*, EbPsnr.c:183-214; variance.c:256-345), so md_expand_kernel derives the [q][849] table of
+// an SB range on demand (svtgpu_md_expand / svtgpu_md_read) -- 8 LDS passes, each shape from two halves of a smaller
+// one, then the per-bit-depth variance formula.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -80,39 +84,36 @@ struct MdArgs {
     int32_t        src_stride;
     const void    *ref[8];
     int32_t        ref_stride[8];
-    const int16_t *mv; // [nsb][nref][2]
-    uint32_t      *out; // [nsb][nref][3][849]
+    const int16_t *mv;  // [nsb][nref][2]
+    uint2         *mom; // [nsb][nref][256] cell moments
     int32_t        nref, width, height, nsbx, sb_begin, highbd;
 };
 
+// cell moments: SAD (<= 16 x 1023, 14 bits) | signed sum (16 bits) << 16, and the SSE (<= 16 x 1023^2 < 2^24)
 template <typename T>
 __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
-    __shared__ uint16_t s_src[64 * 64];
-    __shared__ uint32_t s_sad[kBlocks], s_sse[kBlocks];
-    __shared__ int32_t  s_sum[kBlocks];
     const int tid = threadIdx.x;
     const int sb  = a.sb_begin + xcd_swizzle(blockIdx.x, gridDim.x);
     const int ox = (sb % a.nsbx) * 64, oy = (sb / a.nsbx) * 64;
     const int W = a.width, H = a.height;
     const T  *src = (const T *)a.src;
     const bool inside = ox + 64 <= W && oy + 64 <= H;
-    for (int i = tid; i < 64 * 64; i += 256) {
-        int y = oy + i / 64, x = ox + i % 64;
-        if (!inside) y = min(y, H - 1), x = min(x, W - 1);
-        s_src[i] = src[(size_t)y * a.src_stride + x];
-    }
-    const int cy = tid >> 4, cx = tid & 15;
-    // the shape (pixel count) of each output block this lane writes, looked up once (the shape table is indexed per
-    // lane: every lookup is a memory load, so not once per reference)
-    constexpr int KO = (kBlocks + 255) / 256;
-    int           npx[KO];
+    const int  cy = tid >> 4, cx = tid & 15;
+    int        sv[16]; // the lane's 4x4 source cell, kept for every reference
 #pragma unroll
-    for (int j = 0; j < KO; j++) {
-        const int k = tid + 256 * j;
-        int       sh = 0;
-        if (k < kBlocks)
-            while (k >= c_off[sh + 1]) sh++;
-        npx[j] = c_w[sh] * c_h[sh];
+    for (int i = 0; i < 4; i++) {
+        int y = oy + cy * 4 + i;
+        if (!inside) y = min(y, H - 1);
+        const T *row = src + (size_t)y * a.src_stride;
+        if (inside) {
+            int v[4];
+            row4<T>(row, ox + cx * 4, v);
+#pragma unroll
+            for (int j = 0; j < 4; j++) sv[4 * i + j] = v[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) sv[4 * i + j] = (int)row[min(ox + cx * 4 + j, W - 1)];
+        }
     }
     for (int r = 0; r < a.nref; r++) {
         const int mx = a.mv[((size_t)sb * a.nref + r) * 2], my = a.mv[((size_t)sb * a.nref + r) * 2 + 1];
@@ -120,9 +121,8 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
         const int rs  = a.ref_stride[r];
         const int rx = ox + mx, ry = oy + my;
         const bool rin = rx >= 0 && ry >= 0 && rx + 64 <= W && ry + 64 <= H;
-        __syncthreads(); // s_src staged / previous reference's outputs written
-        uint32_t sad = 0, sse = 0;
-        int32_t  sum = 0;
+        uint32_t   sad = 0, sse = 0;
+        int32_t    sum = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             int y = ry + cy * 4 + i;
@@ -135,56 +135,76 @@ __global__ __launch_bounds__(256) void md_dist_kernel(const MdArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) rv[j] = (int)row[min(max(rx + cx * 4 + j, 0), W - 1)];
             }
-            const uint2 sw = *(const uint2 *)&s_src[(cy * 4 + i) * 64 + cx * 4]; // four source samples
-            const int   sv[4] = {(int)(sw.x & 0xFFFF), (int)(sw.x >> 16), (int)(sw.y & 0xFFFF), (int)(sw.y >> 16)};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const int d = sv[j] - rv[j];
+                const int d = sv[4 * i + j] - rv[j];
                 sad += (uint32_t)abs(d);
                 sse += (uint32_t)(d * d);
                 sum += d;
             }
         }
-        s_sad[tid] = sad, s_sse[tid] = sse, s_sum[tid] = sum;
-        // hierarchical reduction: 8 passes, each shape from two halves of an already reduced shape
-        int st = 0;
-        for (int p = 0; p < 8; p++) {
-            __syncthreads();
-            for (; st < c_pass_end[p]; st++) {
-                const StepX q = c_steps[st];
-                const int   n = 1 << q.lg_n, mcol = (1 << q.lg_ncol) - 1, ccol = 1 << q.lg_ccol;
-                for (int b = tid; b < n; b += 256) {
-                    const int bi = b >> q.lg_ncol, bj = b & mcol;
-                    const int c0 = q.horiz ? (bi << q.lg_ccol) + 2 * bj : ((2 * bi) << q.lg_ccol) + bj;
-                    const int c1 = q.horiz ? c0 + 1 : c0 + ccol;
-                    const int dst = q.off_s + b, x0 = q.off_c + c0, x1 = q.off_c + c1;
-                    s_sad[dst] = s_sad[x0] + s_sad[x1];
-                    s_sse[dst] = s_sse[x0] + s_sse[x1];
-                    s_sum[dst] = s_sum[x0] + s_sum[x1];
-                }
-            }
-        }
-        __syncthreads();
-        uint32_t *out = a.out + ((size_t)sb * a.nref + r) * 3 * kBlocks;
+        a.mom[((size_t)sb * a.nref + r) * 256 + tid] = make_uint2(sad | ((uint32_t)(uint16_t)sum << 16), sse);
+    }
+}
+
+// every shape's SAD, SSE and variance of (SB, reference) pairs [p0, p0 + grid) from the cell moments
+__global__ __launch_bounds__(256) void md_expand_kernel(const uint2 *__restrict__ mom, uint32_t *__restrict__ out,
+                                                        size_t p0, int highbd) {
+    __shared__ uint32_t s_sad[kBlocks], s_sse[kBlocks];
+    __shared__ int32_t  s_sum[kBlocks];
+    const int    tid = threadIdx.x;
+    const size_t pr  = p0 + blockIdx.x;
+    const uint2  m   = mom[pr * 256 + tid];
+    s_sad[tid] = m.x & 0xFFFF, s_sse[tid] = m.y, s_sum[tid] = (int32_t)(int16_t)(m.x >> 16);
+    // the shape (pixel count) of each output block this lane writes
+    constexpr int KO = (kBlocks + 255) / 256;
+    int           npx[KO];
 #pragma unroll
-        for (int j = 0; j < KO; j++) {
-            const int k = tid + 256 * j;
-            if (k >= kBlocks) break;
-            const int n = npx[j];
-            uint32_t  e, v;
-            if (a.highbd) { // highbd_10_variance: sse rounded >> 4, sum rounded >> 2, clamped at 0
-                e                = (s_sse[k] + 8u) >> 4;
-                const int64_t rs2 = ((int64_t)s_sum[k] + 2) >> 2;
-                const int64_t var = (int64_t)e - (rs2 * rs2) / n;
-                v                = var >= 0 ? (uint32_t)var : 0u;
-            } else {
-                e = s_sse[k];
-                v = e - (uint32_t)(((int64_t)s_sum[k] * s_sum[k]) / n);
+    for (int j = 0; j < KO; j++) {
+        const int k = tid + 256 * j;
+        int       sh = 0;
+        if (k < kBlocks)
+            while (k >= c_off[sh + 1]) sh++;
+        npx[j] = c_w[sh] * c_h[sh];
+    }
+    // hierarchical reduction: 8 passes, each shape from two halves of an already reduced shape
+    int st = 0;
+    for (int p = 0; p < 8; p++) {
+        __syncthreads();
+        for (; st < c_pass_end[p]; st++) {
+            const StepX q = c_steps[st];
+            const int   n = 1 << q.lg_n, mcol = (1 << q.lg_ncol) - 1, ccol = 1 << q.lg_ccol;
+            for (int b = tid; b < n; b += 256) {
+                const int bi = b >> q.lg_ncol, bj = b & mcol;
+                const int c0 = q.horiz ? (bi << q.lg_ccol) + 2 * bj : ((2 * bi) << q.lg_ccol) + bj;
+                const int c1 = q.horiz ? c0 + 1 : c0 + ccol;
+                const int dst = q.off_s + b, x0 = q.off_c + c0, x1 = q.off_c + c1;
+                s_sad[dst] = s_sad[x0] + s_sad[x1];
+                s_sse[dst] = s_sse[x0] + s_sse[x1];
+                s_sum[dst] = s_sum[x0] + s_sum[x1];
             }
-            out[k]               = s_sad[k];
-            out[kBlocks + k]     = e;
-            out[2 * kBlocks + k] = v;
         }
+    }
+    __syncthreads();
+    uint32_t *o = out + pr * 3 * kBlocks;
+#pragma unroll
+    for (int j = 0; j < KO; j++) {
+        const int k = tid + 256 * j;
+        if (k >= kBlocks) break;
+        const int n = npx[j];
+        uint32_t  e, v;
+        if (highbd) { // highbd_10_variance: sse rounded >> 4, sum rounded >> 2, clamped at 0
+            e                 = (s_sse[k] + 8u) >> 4;
+            const int64_t rs2 = ((int64_t)s_sum[k] + 2) >> 2;
+            const int64_t var = (int64_t)e - (rs2 * rs2) / n;
+            v                 = var >= 0 ? (uint32_t)var : 0u;
+        } else {
+            e = s_sse[k];
+            v = e - (uint32_t)(((int64_t)s_sum[k] * s_sum[k]) / n);
+        }
+        o[k]               = s_sad[k];
+        o[kBlocks + k]     = e;
+        o[2 * kBlocks + k] = v;
     }
 }
 
@@ -488,7 +508,9 @@ struct SvtGpuMdBatch {
     SvtGpuContext *ctx;
     int32_t        width, height, nref, nsbx, nsby;
     int16_t       *d_mv;
-    uint32_t      *d_out;
+    uint2         *d_mom;  // [nsb][nref][256] cell moments (svtgpu_md_dist_batch)
+    uint32_t      *d_out;  // [nsb][nref][3][849] every shape's values (svtgpu_md_expand)
+    int32_t        highbd; // the bit depth of the last batch (the expansion's variance formula)
 };
 
 extern "C" void svtgpu_md_layout(int32_t *shape_w, int32_t *shape_h, int32_t *shape_offset) {
@@ -513,6 +535,7 @@ extern "C" int svtgpu_md_batch_create(SvtGpuContext *ctx, int32_t width, int32_t
     const size_t nsb = (size_t)b->nsbx * b->nsby;
     hipError_t   e   = hipMalloc(&b->d_mv, nsb * nref * 2 * sizeof(int16_t));
     if (e == hipSuccess) e = hipMalloc(&b->d_out, nsb * nref * 3 * kBlocks * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&b->d_mom, nsb * nref * 256 * sizeof(uint2));
     if (e == hipSuccess) e = hipMemset(b->d_mv, 0, nsb * nref * 2 * sizeof(int16_t));
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) {
@@ -528,6 +551,7 @@ extern "C" void svtgpu_md_batch_destroy(SvtGpuMdBatch *b) {
     if (!b) return;
     (void)hipFree(b->d_mv);
     (void)hipFree(b->d_out);
+    (void)hipFree(b->d_mom);
     delete b;
 }
 
@@ -564,13 +588,14 @@ extern "C" int svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source,
         a.ref_stride[r] = f->stride[0];
     }
     a.mv       = b->d_mv;
-    a.out      = b->d_out;
+    a.mom      = b->d_mom;
     a.nref     = b->nref;
     a.width    = b->width;
     a.height   = b->height;
     a.nsbx     = b->nsbx;
     a.sb_begin = sb_begin;
     a.highbd   = source->bit_depth > 8;
+    b->highbd  = a.highbd;
     if (sb_end == sb_begin) return SVTGPU_OK;
     hipStream_t st = pick_stream(b->ctx, stream);
     if (a.highbd)
@@ -581,10 +606,23 @@ extern "C" int svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source,
     return SVTGPU_OK;
 }
 
+extern "C" int svtgpu_md_expand(SvtGpuMdBatch *b, int32_t sb_begin, int32_t sb_end, void *stream) {
+    const int nsb = b ? b->nsbx * b->nsby : 0;
+    if (!b || sb_begin < 0 || sb_end > nsb || sb_begin > sb_end) return SVTGPU_ERR_INVALID_ARG;
+    if (sb_end == sb_begin) return SVTGPU_OK;
+    hipLaunchKernelGGL(md_expand_kernel, dim3((sb_end - sb_begin) * b->nref), dim3(256), 0, pick_stream(b->ctx, stream),
+                       (const uint2 *)b->d_mom, b->d_out, (size_t)sb_begin * b->nref, (int)b->highbd);
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
+extern "C" void *svtgpu_md_moments_device_ptr(SvtGpuMdBatch *b) { return b ? (void *)b->d_mom : nullptr; }
+
 extern "C" int svtgpu_md_read(SvtGpuMdBatch *b, uint32_t *out, int32_t sb_begin, int32_t sb_end, void *stream) {
     const int nsb = b ? b->nsbx * b->nsby : 0;
     if (!b || !out || sb_begin < 0 || sb_end > nsb || sb_begin > sb_end) return SVTGPU_ERR_INVALID_ARG;
     hipStream_t  st  = pick_stream(b->ctx, stream);
+    if (int rc = svtgpu_md_expand(b, sb_begin, sb_end, st)) return rc; // the rows read, from the moments
     const size_t row = (size_t)b->nref * 3 * kBlocks;
     svtgpu_count_xfer(1, (size_t)(sb_end - sb_begin) * row * sizeof(uint32_t));
     HIP_TRY(hipMemcpyAsync(out, b->d_out + sb_begin * row, (sb_end - sb_begin) * row * sizeof(uint32_t),

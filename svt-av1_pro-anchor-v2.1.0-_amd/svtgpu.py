@@ -332,6 +332,8 @@ _SIGS = {
     "svtgpu_md_dist_batch": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _P]),
     "svtgpu_md_read": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     "svtgpu_md_out_device_ptr": (_P, [_P]),
+    "svtgpu_md_moments_device_ptr": (_P, [_P]),
+    "svtgpu_md_expand": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "svtgpu_md_layout": (None, [_P, _P, _P]),
     "svtgpu_av1_wiener_convolve_add_src": (None, [_P, ctypes.c_ssize_t, _P, ctypes.c_ssize_t, _P, _P, _I32, _I32,
                                                   ctypes.POINTER(ConvolveParams)]),
@@ -865,6 +867,11 @@ class MdBatch:
         out = np.empty((end - sb_begin, self.nref, 3, MD_BLOCKS), np.uint32)
         check(lib().svtgpu_md_read(self.h, ptr(out), sb_begin, end, stream))
         return out
+
+    def expand(self, sb_begin=0, sb_end=None, stream=None):
+        """svtgpu_md_expand: every shape's values of the SB range from the cell moments (in stream order)."""
+        end = self.nsb if sb_end is None else sb_end
+        check(lib().svtgpu_md_expand(self.h, sb_begin, end, stream))
 
     def out_device_ptr(self):
         return lib().svtgpu_md_out_device_ptr(self.h)
