@@ -919,9 +919,11 @@ def main():
     if a.stages == "all" and not a.lr_sync:  # the asynchronous searches' results: a device-side failure raises here
         for sl in slots:
             sl.lr.read_result(sl.stream.cuda_stream)
+    dlf_rounds = None
     if a.stages == "all" and not a.dlf_sync:  # the last asynchronous level search of every slot
         for sl in slots:
             sl.lf_levels.append(sl.dl.read_levels(sl.stream.cuda_stream).levels())
+        dlf_rounds = slots[0].dl.async_rounds()
     lr_tot = lr.profile(False) if not a.no_kernel_timing else None
     h2d, d2h = svtgpu.transfer_bytes(reset=True)
     if n > 1:
@@ -1080,7 +1082,7 @@ def main():
                                    "note": "sum over the frame slots of their mean frame latency / step time"},
                    "lr_search_mode": "sync (host wait)" if a.lr_sync else "async (device RD finish, no host wait)",
                    "dlf_search_mode": "sync (host-driven bisection)" if a.dlf_sync
-                   else "async (device bisection, no host wait)",
+                   else "async (device bisection, no host wait; trial rounds taken / enqueued %s)" % (dlf_rounds,),
                    "ranks": n,
                    "parallelism": ("tiles%dx%d (each frame tiled over the ranks: DLF trials/filter, CDEF search/apply, "
                                    "LR search/apply per tile; RCCL sums of the DLF trial SSEs, CDEF tables, LR records "

@@ -490,6 +490,9 @@ int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon, const Svt
  * the picked levels; sharpness 0).  SVTGPU_ERR_INVALID_ARG: no asynchronous pick ran, or the device mode-info grid it
  * used had records out of range. */
 int svtgpu_dlf_read_levels(SvtGpuDlfState *s, SvtGpuLfParams *params_out, void *stream);
+/* measurement: the trial rounds the last collected asynchronous search took, and the rounds the last one enqueued
+ * (a search needing more is completed by the finish kernel, one workgroup: far slower) */
+int svtgpu_dlf_async_rounds(const SvtGpuDlfState *s, int32_t *taken, int32_t *enqueued);
 /* A picture tiled over GPUs (svtgpu_tile_plan): the level search measures each trial's SSE over the luma
  * rectangle sse_rect = {x0, y0, x1, y1} (the rank's tile; chroma halved) and sums it over `comm` before every
  * bisection step, so every rank takes the same steps; svtgpu_dlf_frame(_to) writes only out_rect (chroma halved,

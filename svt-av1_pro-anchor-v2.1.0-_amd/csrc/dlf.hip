@@ -568,7 +568,7 @@ struct SvtGpuDlfState {
     // svtgpu_dlf_pick_async: the result the device search leaves (device: the apply's tables; mapped: the caller's
     // levels), the picks enqueued / collected, the parameters it started from, the rounds to enqueue next time
     void          *d_res = nullptr, *h_res = nullptr, *h_res_dev = nullptr;
-    int32_t        dev_seq = 0, dev_pending = 0, dev_ready = 0, dev_rounds = 6;
+    int32_t        dev_seq = 0, dev_pending = 0, dev_ready = 0, dev_rounds = 8, dev_rounds_last = 0, dev_seen = 0;
     SvtGpuLfParams dev_params{};
 };
 
@@ -833,9 +833,10 @@ __device__ void dlf_step(DlfDevSearch *S, unsigned long long *sse, uint32_t *w, 
     __syncthreads();
     DlfDevSearch &D = *(DlfDevSearch *)w;
     if (D.plan.done) return; // uniform: every lane read the same word
+    __shared__ unsigned long long v[MAX_JOBS * MAX_TRIALS]; // the sums, one lane each (not a chain of atomics)
+    if (tid < MAX_JOBS * MAX_TRIALS) v[tid] = atomic_sums ? atomicExch(&sse[tid], 0ull) : sse[tid];
+    __syncthreads();
     if (tid == 0) {
-        unsigned long long v[MAX_JOBS * MAX_TRIALS];
-        for (int q = 0; q < MAX_JOBS * MAX_TRIALS; q++) v[q] = atomic_sums ? atomicExch(&sse[q], 0ull) : sse[q];
         for (int i = 0; i < D.ns; i++)
             if (D.plan.ntrial[i]) D.srch[i].feed(D.plan.lv[i], D.plan.ntrial[i], v + i * MAX_TRIALS);
         plan_levels(D);
@@ -886,16 +887,21 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArg
     // one item per workgroup over a grid sized for the most levels a round can try; the workgroups past this round's
     // items go straight to the arrival count (a persistent loop over the items spilled 60 VGPRs: the item's registers
     // live across the loop)
-    if ((int)blockIdx.x < nitems) dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
+    // (nitems == 0: every search has finished, nothing to step)
+    if ((int)blockIdx.x >= nitems) return;
+    dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
     if (!fuse) return;
     __syncthreads();
+    // Only the workgroups with an item count (the others left without touching the counter).  No __threadfence: an
+    // agent-scope fence writes back and invalidates this XCD's L2 (the L2s of the 8 XCDs are not coherent), which
+    // doubled every round (the trials of a tile share their staging through the L2); the sums are device-scope atomics,
+    // so waiting for this lane's to complete before its arrival is enough
     if (tid == 0) {
-        __threadfence(); // this workgroup's SSE atomics before its arrival
-        last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(a.arrive, 1u) == (unsigned)nitems - 1;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
     dlf_step(S, a.sse, (uint32_t *)L.t, true);
     if (tid == 0) atomicExch(a.arrive, 0u);
 }
@@ -918,7 +924,8 @@ __global__ __launch_bounds__(NTHR) void dlf_finish_kernel(const DlfTileArgs a0, 
         for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
         for (int i = 0; i < nitems; i++) dlf_tile_item<T, true>(a, i, nitems, L);
         __syncthreads();
-        __threadfence();
+        if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // the last item's SSE atomic
+        __syncthreads();
         dlf_step(S, a.sse, (uint32_t *)L.t, true);
         __syncthreads();
     }
@@ -1403,9 +1410,12 @@ extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon
         const char *e = std::getenv("SVTGPU_DLF_ROUNDS");
         return e ? std::max(1, std::min(64, std::atoi(e))) : 0;
     }();
+    // the latest search that has completed (whichever: the caller's thread may run ahead of the device) sizes the next
+    // one's rounds with a margin of two
     const volatile DlfDevResult *hr = (const volatile DlfDevResult *)s->h_res;
-    if (hr->seq == s->dev_seq && s->dev_seq) s->dev_rounds = std::max(2, std::min(16, hr->rounds + 1));
+    if (hr->seq != s->dev_seen) s->dev_seen = hr->seq, s->dev_rounds = std::max(4, std::min(16, hr->rounds + 2));
     const int rounds = fixed ? fixed : s->dev_rounds;
+    s->dev_rounds_last = rounds;
     SvtGpuLfParams p  = *params;
     p.sharpness_level = 0;
     const int ns      = (dlf_avg_uv && temporal_layer_index > 0) ? 1 : 3;
@@ -1466,6 +1476,13 @@ extern "C" int svtgpu_dlf_read_levels(SvtGpuDlfState *s, SvtGpuLfParams *params_
     p.filter_level[0] = r->levels[0], p.filter_level[1] = r->levels[1];
     p.filter_level_u = r->levels[2], p.filter_level_v = r->levels[3];
     *params_out = p;
+    return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_dlf_async_rounds(const SvtGpuDlfState *s, int32_t *taken, int32_t *enqueued) {
+    if (!s || !s->h_res) return SVTGPU_ERR_INVALID_ARG;
+    if (taken) *taken = ((const volatile DlfDevResult *)s->h_res)->rounds;
+    if (enqueued) *enqueued = s->dev_rounds_last;
     return SVTGPU_OK;
 }
 

@@ -2423,11 +2423,13 @@ void finish_frame_host(const SvtGpuLrSearchControls *c, int nplanes, const int32
 //                          all-reduces);
 //   lr_fin_tables_kernel   one wave per unit evaluates, for every reference the chain can hold at that unit (the 63
 //                          units before it and the default), the pass's decision: search_wiener_finish /
-//                          search_sgrproj_finish as bits of a 64-bit mask, search_switchable as a 2-bit choice for
-//                          each of 16 x 16 (Wiener reference, self-guided reference) pairs (15 units back + default);
-//   lr_fin_walk_kernel     one workgroup walks the chains -- per unit a mask bit (a table entry) selected by how far
-//                          back the reference is, a few scalar instructions -- evaluating a decision directly only when
-//                          the reference lies outside the tabulated window; then the per-unit rates of the taken path
+//                          search_sgrproj_finish as bits of a 64-bit mask; for search_switchable the costs of the
+//                          Wiener and the self-guided choice against each of those references (the choice needs one
+//                          of each: two tables of 64 doubles instead of a 64 x 64 table);
+//   lr_fin_walk_kernel     one workgroup walks the chains -- per unit a mask bit (two table entries and two compares)
+//                          selected by how far back the reference is, the tables staged in LDS a chunk of units at a
+//                          time -- evaluating a decision directly only when the reference lies outside the tabulated
+//                          window; then the per-unit rates of the taken path
 //                          in parallel, each pass's frame cost, the frame types and copy_unit_info into the state's
 //                          units.  The decisions are the reference's own comparisons (RDCOST_DBL in double,
 //                          -ffp-contract=off), so the walk takes exactly the reference's path.
@@ -2435,8 +2437,7 @@ void finish_frame_host(const SvtGpuLrSearchControls *c, int nplanes, const int32
 // plane does not search.
 // ---------------------------------------------------------------------------------------------
 constexpr int FIN_K1 = 63; // r = 1 / 2 masks: bit k < 63 = the unit k + 1 back as the reference, bit 63 = the default
-constexpr int FIN_K3 = 15; // switchable tables: kw, ks < 15 = that many + 1 back, 15 = the default
-constexpr int FIN_T3 = 17; // words per unit: 16 x 16 two-bit choices (word kw, bits 2 ks), then T10 | T01 << 16
+constexpr int FIN_CH = 16; // switchable walk: units of cost tables staged in LDS at a time (per wave)
 constexpr int FIN_OUT = 8; // device result words: frame types [3], search status, sequence
 
 struct RecArgs {
@@ -2485,13 +2486,14 @@ struct FinArgs {
     int32_t                   nplanes, nrec, rdmult, sw[3], wn[2], sg[2];
     const SvtGpuLrUnitSearch *rec;
     unsigned long long       *m1, *m2;
-    uint32_t                 *t3;
+    double                   *c0, *c1, *c2; // switchable: the NONE cost; the Wiener / self-guided costs [unit][64]
     int32_t                  *path;   // [4][nrec]: r 1, r 2, r 3 (Wiener ref), r 3 (self-guided ref): choice | (ref + 1) << 2
     SvtGpuRestUnit           *units;  // the state's units (d_units[0]: the planes back to back, the records' layout)
     int32_t                  *out;    // [FIN_OUT] device results
     int32_t                  *out_host; // mapped pinned copy
     const int32_t            *wstat, *sstat; // the descents' status words (wiener_res / sgr_res) or null
     int32_t                   seq;
+    unsigned long long       *clk; // diagnostics (SVTGPU_LR_FIN_CLK): the walk's phase ends on s_memrealtime, or null
 };
 
 // the shared rusi entries of unit u of plane p a switchable pass and copy_unit_info read
@@ -2538,43 +2540,24 @@ __device__ inline int fin_pick(double c0, double c1, double c2, bool a1, bool a2
 }
 
 __global__ __launch_bounds__(64) void lr_fin_tables_kernel(const FinArgs F) {
-    __shared__ double c1s[FIN_K3 + 1], c2s[FIN_K3 + 1];
     const int b = blockIdx.x, lane = threadIdx.x;
     int       p = 0;
     while (p + 1 < F.nplanes && b >= F.pl[p + 1].base) p++;
     const FinPlane &P = F.pl[p];
     const int       u = b - P.base;
     if (u >= P.n) return;
+    const int ref = lane < FIN_K1 ? u - 1 - lane : -1; // lane k: the unit k + 1 back; lane 63: the default
+    const bool ok = lane == FIN_K1 || ref >= 0;
     for (int r = 1; r <= 2; r++) {
         if (!P.run[r]) continue;
-        const int  ref = lane < FIN_K1 ? u - 1 - lane : -1;
-        const bool a   = (lane == FIN_K1 || ref >= 0) && (r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref));
+        const bool a = ok && (r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref));
         const unsigned long long m = __ballot(a);
         if (lane == 0) (r == 1 ? F.m1 : F.m2)[b] = m;
     }
     if (!P.run[3]) return;
-    if (lane <= FIN_K3) {
-        const int rw = lane < FIN_K3 ? u - 1 - lane : -1;
-        c1s[lane]    = (lane == FIN_K3 || rw >= 0) ? fin_c1(F, p, u, rw) : 0.0;
-    } else if (lane >= 32 && lane <= 32 + FIN_K3) {
-        const int k = lane - 32, rs = k < FIN_K3 ? u - 1 - k : -1;
-        c2s[k]      = (k == FIN_K3 || rs >= 0) ? fin_c2(F, p, u, rs) : 0.0;
-    }
-    __syncthreads();
-    const double c0 = fin_c0(F, p, u);
-    uint32_t    *T  = F.t3 + (size_t)b * FIN_T3;
-    if (lane <= FIN_K3) { // word kw = lane: the choices with both types allowed, ks = 0..15
-        uint32_t w = 0;
-        for (int ks = 0; ks <= FIN_K3; ks++) w |= (uint32_t)fin_pick(c0, c1s[lane], c2s[ks], true, true) << (2 * ks);
-        T[lane] = w;
-    } else if (lane == FIN_K3 + 1) { // one type allowed: bit kw of T10 (type 1), bit ks of T01 (type 2)
-        uint32_t w = 0;
-        for (int k = 0; k <= FIN_K3; k++) {
-            w |= (uint32_t)(fin_pick(c0, c1s[k], 0.0, true, false) == 1) << k;
-            w |= (uint32_t)(fin_pick(c0, 0.0, c2s[k], false, true) == 2) << (16 + k);
-        }
-        T[FIN_T3 - 1] = w;
-    }
+    F.c1[(size_t)b * 64 + lane] = ok ? fin_c1(F, p, u, ref) : 0.0;
+    F.c2[(size_t)b * 64 + lane] = ok ? fin_c2(F, p, u, ref) : 0.0;
+    if (lane == 0) F.c0[b] = fin_c0(F, p, u);
 }
 
 // a wave-uniform 64-bit value held by lane i of v
@@ -2584,7 +2567,13 @@ __device__ inline unsigned long long lane_u64(unsigned long long v, int i) {
     return ((unsigned long long)hi << 32) | lo;
 }
 
-// the r = 1 / r = 2 chain of plane p (one wave): path[u] = decision | (reference + 1) << 2
+// The chains are walked a chunk of units at a time by one wave.  At a chunk's start the wave evaluates, lane-parallel,
+// every unit of the chunk against the reference the chain holds then (the decision or the costs themselves, exactly as
+// the tables do): while the chain keeps that reference -- however far back it lies -- a unit's step reads that; once a
+// unit of the chunk has taken the filter, the reference lies inside the chunk, within the tabulated window.  No unit
+// waits on a serial evaluation or on a global load that depends on the chain.
+
+// the r = 1 / r = 2 chain of plane p: path[u] = decision | (reference + 1) << 2
 __device__ void fin_walk12(const FinArgs &F, int p, int r, int lane) {
     const FinPlane           &P    = F.pl[p];
     const unsigned long long *M    = (r == 1 ? F.m1 : F.m2) + P.base;
@@ -2592,75 +2581,75 @@ __device__ void fin_walk12(const FinArgs &F, int p, int r, int lane) {
     int                       ref  = -1;
     for (int u0 = 0; u0 < P.n; u0 += 64) {
         const unsigned long long mv = u0 + lane < P.n ? M[u0 + lane] : 0ull;
-        const int                nl = min(64, P.n - u0);
+        const int                nl = min(64, P.n - u0), ref0 = ref;
+        const bool               sa = lane < nl && (r == 1 ? fin_accept1(F, p, u0 + lane, ref0) : fin_accept2(F, p, u0 + lane, ref0));
+        const unsigned long long spec = __ballot(sa); // bit i: unit u0 + i against the chunk's starting reference
         for (int i = 0; i < nl; i++) {
-            const int u = u0 + i;
-            bool      a;
-            if (ref < 0 || u - 1 - ref < FIN_K1) {
-                const int k = ref < 0 ? FIN_K1 : u - 1 - ref;
-                a           = (lane_u64(mv, i) >> k) & 1;
-            } else { // the reference lies outside the tabulated window: the decision itself
-                a = r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref);
-            }
+            const int  u = u0 + i;
+            const bool a = ref == ref0 ? (spec >> i) & 1 : (lane_u64(mv, i) >> (u - 1 - ref)) & 1; // u - 1 - ref < 63
             if (lane == 0) path[u] = (int32_t)a | ((ref + 1) << 2);
             if (a) ref = u;
         }
     }
 }
 
-// the switchable chain of plane p (one wave): path[2][u] / path[3][u] = choice | (Wiener / self-guided ref + 1) << 2
-__device__ void fin_walk3(const FinArgs &F, int p, int lane) {
+// the switchable chain of plane p: path[2][u] / path[3][u] = choice | (Wiener / self-guided ref + 1) << 2.  The cost
+// tables of FIN_CH units are staged in the wave's LDS (lc1 / lc2: [FIN_CH][64], lc0 / s1 / s2: [FIN_CH])
+__device__ void fin_walk3(const FinArgs &F, int p, int lane, double *lc0, double *lc1, double *lc2, double *s1, double *s2) {
     const FinPlane &P  = F.pl[p];
-    const uint32_t *T  = F.t3 + (size_t)P.base * FIN_T3;
     const int32_t  *d1 = F.path + F.pl[P.own1 ? p : 0].base, *d2 = F.path + F.nrec + F.pl[P.own2 ? p : 0].base;
     int32_t        *pw = F.path + 2 * (size_t)F.nrec + P.base, *ps = F.path + 3 * (size_t)F.nrec + P.base;
     int             rw = -1, rs = -1;
-    for (int u0 = 0; u0 < P.n; u0 += 64) {
-        const int nl = min(64, P.n - u0);
-        const int a1v = lane < nl ? d1[u0 + lane] & 1 : 0, a2v = lane < nl ? d2[u0 + lane] & 1 : 0;
-        uint32_t  row = lane < FIN_T3 ? T[(size_t)u0 * FIN_T3 + lane] : 0u;
+    for (int u0 = 0; u0 < P.n; u0 += FIN_CH) {
+        const int nl = min(FIN_CH, P.n - u0), rw0 = rw, rs0 = rs;
         for (int i = 0; i < nl; i++) {
-            const int      u   = u0 + i;
-            const uint32_t cur = row;
-            if (i + 1 < nl) row = lane < FIN_T3 ? T[(size_t)(u + 1) * FIN_T3 + lane] : 0u; // the next unit's row
-            const bool a1 = __builtin_amdgcn_readlane(a1v, i) != 0, a2 = __builtin_amdgcn_readlane(a2v, i) != 0;
-            const int  kw = rw < 0 ? FIN_K3 : u - 1 - rw, ks = rs < 0 ? FIN_K3 : u - 1 - rs;
-            int        bt;
-            if (kw <= FIN_K3 && ks <= FIN_K3 && (rw < 0 || kw < FIN_K3) && (rs < 0 || ks < FIN_K3)) {
-                if (a1 && a2)
-                    bt = ((uint32_t)__builtin_amdgcn_readlane((int)cur, kw) >> (2 * ks)) & 3;
-                else if (a1 || a2) {
-                    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cur, FIN_T3 - 1);
-                    bt               = a1 ? ((w >> kw) & 1) : ((w >> (16 + ks)) & 1) ? 2 : 0;
-                } else
-                    bt = 0;
-            } else { // a reference outside the window: the costs themselves
-                bt = fin_pick(fin_c0(F, p, u), a1 ? fin_c1(F, p, u, rw) : 0.0, a2 ? fin_c2(F, p, u, rs) : 0.0, a1, a2);
-            }
+            const size_t row = (size_t)(P.base + u0 + i) * 64 + lane;
+            lc1[i * 64 + lane] = F.c1[row], lc2[i * 64 + lane] = F.c2[row];
+        }
+        if (lane < nl) lc0[lane] = F.c0[P.base + u0 + lane];
+        // the chunk's units against the chain's starting references (lanes 0..15 Wiener, 32..47 self-guided)
+        if (lane < nl) s1[lane] = fin_c1(F, p, u0 + lane, rw0);
+        else if (lane >= 32 && lane - 32 < nl) s2[lane - 32] = fin_c2(F, p, u0 + lane - 32, rs0);
+        const int a1v = lane < nl ? d1[u0 + lane] & 1 : 0, a2v = lane < nl ? d2[u0 + lane] & 1 : 0;
+        __builtin_amdgcn_wave_barrier(); // the wave's LDS stores before its loads (in order within a wave)
+        for (int i = 0; i < nl; i++) {
+            const int    u  = u0 + i;
+            const bool   a1 = __builtin_amdgcn_readlane(a1v, i) != 0, a2 = __builtin_amdgcn_readlane(a2v, i) != 0;
+            const double c1 = rw == rw0 ? s1[i] : lc1[i * 64 + (u - 1 - rw)]; // a reference inside the chunk
+            const double c2 = rs == rs0 ? s2[i] : lc2[i * 64 + (u - 1 - rs)];
+            const int    bt = fin_pick(lc0[i], c1, c2, a1, a2);
             if (lane == 0) pw[u] = bt | ((rw + 1) << 2), ps[u] = bt | ((rs + 1) << 2);
             if (bt == 1) rw = u;
             if (bt == 2) rs = u;
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-__global__ __launch_bounds__(256) void lr_fin_walk_kernel(const FinArgs F) {
+constexpr int FIN_NT = 1024; // the walk kernel's lanes: three walking waves, then all of them for the per-unit sums
+__global__ __launch_bounds__(FIN_NT) void lr_fin_walk_kernel(const FinArgs F) {
     __shared__ unsigned long long acc[3][4][2]; // per plane and pass: sse, bits
     __shared__ int32_t            ft[3];
+    __shared__ double             lc[3][FIN_CH * (2 * 64 + 3)]; // fin_walk3's staging, per wave
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     if (tid < 24) (&acc[0][0][0])[tid] = 0;
+    if (F.clk && tid == 0) F.clk[0] = __builtin_amdgcn_s_memrealtime();
     // the r = 1 / 2 chains (wave w: plane w; independent of each other), then the switchable chains (which read the
     // r = 1 / 2 outcomes, luma's for a type chroma does not search)
     if (wv < F.nplanes)
         for (int r = 1; r <= 2; r++)
             if (F.pl[wv].run[r]) fin_walk12(F, wv, r, lane);
     __syncthreads();
-    if (wv < F.nplanes && F.pl[wv].run[3]) fin_walk3(F, wv, lane);
+    if (F.clk && tid == 0) F.clk[1] = __builtin_amdgcn_s_memrealtime();
+    if (wv < F.nplanes && F.pl[wv].run[3])
+        fin_walk3(F, wv, lane, lc[wv], lc[wv] + FIN_CH, lc[wv] + FIN_CH + FIN_CH * 64, lc[wv] + FIN_CH + 2 * FIN_CH * 64,
+                  lc[wv] + 2 * FIN_CH + 2 * FIN_CH * 64);
     __syncthreads();
+    if (F.clk && tid == 0) F.clk[2] = __builtin_amdgcn_s_memrealtime();
     // the rate and distortion of every unit on each pass's path, summed per (plane, pass)
     for (int p = 0; p < F.nplanes; p++) {
         const FinPlane &P = F.pl[p];
-        for (int i = tid; i < 4 * P.n; i += 256) {
+        for (int i = tid; i < 4 * P.n; i += FIN_NT) {
             const int r = i / P.n, u = i - r * P.n;
             if (!P.run[r]) continue;
             const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
@@ -2699,6 +2688,7 @@ __global__ __launch_bounds__(256) void lr_fin_walk_kernel(const FinArgs F) {
         }
     }
     __syncthreads();
+    if (F.clk && tid == 0) F.clk[3] = __builtin_amdgcn_s_memrealtime();
     if (tid < 3) { // each pass's frame cost; the first of least cost (r == 0 || cost < best)
         int best = 0;
         if (tid < F.nplanes) {
@@ -2712,10 +2702,11 @@ __global__ __launch_bounds__(256) void lr_fin_walk_kernel(const FinArgs F) {
         ft[tid] = best;
     }
     __syncthreads();
+    if (F.clk && tid == 0) F.clk[4] = __builtin_amdgcn_s_memrealtime();
     // copy_unit_info into the state's units (every plane; zero where the frame type is NONE)
     for (int p = 0; p < 3; p++) {
         const FinPlane &P = F.pl[p];
-        for (int u = tid; u < P.n; u += 256) {
+        for (int u = tid; u < P.n; u += FIN_NT) {
             SvtGpuRestUnit o;
             memset(&o, 0, sizeof o);
             if (p < F.nplanes && ft[p]) {
@@ -3067,8 +3058,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t res_span = dc.off - o_sse; // the (unit, ep) descents stay on the device: the best ep's come back
     const size_t o_sds = dc(sizeof(Descent) * npairs);
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_m1 = dc(8 * (size_t)nrec), o_m2 = dc(8 * (size_t)nrec), o_t3 = dc(4 * FIN_T3 * (size_t)nrec),
-                 o_fout = dc(4 * FIN_OUT);
+    const size_t o_m1 = dc(8 * (size_t)nrec), o_m2 = dc(8 * (size_t)nrec), o_c0 = dc(8 * (size_t)nrec),
+                 o_c1 = dc(8 * 64 * (size_t)nrec), o_c2 = dc(8 * 64 * (size_t)nrec), o_fout = dc(4 * FIN_OUT);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
     const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
@@ -3332,17 +3323,22 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         for (int k = 0; k < 3; k++) F.sw[k] = c->switchable_restore_cost[k];
         for (int k = 0; k < 2; k++) F.wn[k] = c->wiener_restore_cost[k], F.sg[k] = c->sgrproj_restore_cost[k];
         F.rec = (const SvtGpuLrUnitSearch *)dp(o_rec);
-        F.m1 = (unsigned long long *)dp(o_m1), F.m2 = (unsigned long long *)dp(o_m2), F.t3 = (uint32_t *)dp(o_t3);
+        F.m1 = (unsigned long long *)dp(o_m1), F.m2 = (unsigned long long *)dp(o_m2);
+        F.c0 = (double *)dp(o_c0), F.c1 = (double *)dp(o_c1), F.c2 = (double *)dp(o_c2);
         F.path = (int32_t *)dp(o_path), F.units = s->d_units[0];
         F.out = (int32_t *)dp(o_fout), F.out_host = s->h_fout_dev;
         F.wstat = n_wn ? (const int32_t *)dp(o_wstat) : nullptr, F.sstat = n_sr ? (const int32_t *)dp(o_sstat) : nullptr;
         F.seq = ++s->fin_seq;
+        static const bool fin_clk = std::getenv("SVTGPU_LR_FIN_CLK") != nullptr;
+        static unsigned long long *d_clk = nullptr;
+        if (fin_clk && !d_clk) HIP_TRY(hipMalloc(&d_clk, 64));
+        F.clk = fin_clk ? d_clk : nullptr;
         if (tables) {
             hipLaunchKernelGGL(lr_fin_tables_kernel, dim3(F.pl[nplanes - 1].base + F.pl[nplanes - 1].n), dim3(64), 0,
                                st, F);
             HIP_TRY(hipGetLastError());
         }
-        hipLaunchKernelGGL(lr_fin_walk_kernel, dim3(1), dim3(256), 0, st, F);
+        hipLaunchKernelGGL(lr_fin_walk_kernel, dim3(1), dim3(FIN_NT), 0, st, F);
         HIP_TRY(hipGetLastError());
         if (search_out) { // the records, all planes' units
             HIP_TRY(hipMemcpyAsync(hp(h_rec), dp(o_rec), sizeof(SvtGpuLrUnitSearch) * (size_t)nrec,
@@ -3355,6 +3351,12 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         mark(3);
         if (!frame_type) return SVTGPU_OK; // asynchronous: svtgpu_lr_read_result collects the frame types
         if (int rc = lr_collect(s, st, frame_type)) return rc;
+        if (F.clk) {
+            unsigned long long v[8];
+            HIP_TRY(hipMemcpy(v, F.clk, 64, hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "lr_fin_walk us: r1/r2 walks %.1f, switchable walks %.1f, sums %.1f, types %.1f\n",
+                         (v[1] - v[0]) * 0.01, (v[2] - v[1]) * 0.01, (v[3] - v[2]) * 0.01, (v[4] - v[3]) * 0.01);
+        }
         if (search_out) {
             const SvtGpuLrUnitSearch *hr = (const SvtGpuLrUnitSearch *)hp(h_rec);
             for (int p = 0; p < 3; p++)

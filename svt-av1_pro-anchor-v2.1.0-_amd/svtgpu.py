@@ -259,6 +259,7 @@ _SIGS = {
     "svtgpu_dlf_pick": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_pick_async": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(LfParams), _I32, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_read_levels": (ctypes.c_int, [_P, ctypes.POINTER(LfParams), _P]),
+    "svtgpu_dlf_async_rounds": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_dlf_pick_by_q": (ctypes.c_int, [_P, _P]),
     "svtgpu_dlf_qp_based_param": (ctypes.c_int, [_I32, _I32, _I32, _P, _P]),
     "svtgpu_plane_sse": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_U64), _P]),
@@ -764,6 +765,12 @@ class DlfState:
         ctypes.pointer(p)[0] = params
         check(lib().svtgpu_dlf_pick_async(self.h, recon.h, source.h, ctypes.byref(p), dlf_avg, dlf_avg_uv,
                                           temporal_layer_index, early_exit, only_4x4, stream))
+
+    def async_rounds(self):
+        """svtgpu_dlf_async_rounds: (rounds the last collected asynchronous search took, rounds enqueued)."""
+        t, e = _I32(), _I32()
+        check(lib().svtgpu_dlf_async_rounds(self.h, ctypes.byref(t), ctypes.byref(e)))
+        return t.value, e.value
 
     def read_levels(self, stream=None):
         """svtgpu_dlf_read_levels: waits for the last pick_async and returns its LfParams."""
