@@ -16,7 +16,9 @@
  *          so the reference sources are compiled unmodified and the process bodies call libsvtgpu's frame-level API.
  * tests/test_encoder_drop_in.py compares the three bitstreams byte for byte.
  *
- *   enc_drop_in <cpu|rtcd|frame> <out.obu> [width height frames preset qp]
+ *   enc_drop_in <cpu|rtcd|frame> <out.obu> [width height frames preset qp bit_depth logical_processors]
+ * (bit_depth 8 or 10, default 10: an 8-bit clip runs the encoder's 8-bit pipeline; logical_processors > 1: several
+ * pictures through the encoder's DLF / CDEF / REST processes at once)
  * Prints one line: "<mode> bytes <n> packets <n> shim_calls <n> frame_calls <n> frame_fallbacks <n>".
  */
 #define _GNU_SOURCE
@@ -74,7 +76,7 @@ static int in_libsvtgpu(const void *f) {
 
 int main(int argc, char **argv) {
     if (argc < 3) {
-        fprintf(stderr, "usage: enc_drop_in <cpu|rtcd|frame> <out.obu> [width height frames preset qp]\n");
+        fprintf(stderr, "usage: enc_drop_in <cpu|rtcd|frame> <out.obu> [width height frames preset qp bit_depth lp]\n");
         return 2;
     }
     const char *mode   = argv[1];
@@ -85,6 +87,9 @@ int main(int argc, char **argv) {
     const int   nfr    = argc > 5 ? atoi(argv[5]) : 5;
     const int   preset = argc > 6 ? atoi(argv[6]) : 2;
     const int   qp     = argc > 7 ? atoi(argv[7]) : 40;
+    const int   bd     = argc > 8 ? atoi(argv[8]) : 10;
+    const int   lp     = argc > 9 ? atoi(argv[9]) : 1;
+    if (bd != 8 && bd != 10) return 2;
     if (!rtcd && !frame && strcmp(mode, "cpu")) return 2;
     if ((rtcd || frame) && !svtgpu_device_available()) {
         fprintf(stderr, "enc_drop_in: no gfx950 device\n");
@@ -99,7 +104,7 @@ int main(int argc, char **argv) {
     cfg.enc_mode                     = (int8_t)preset;
     cfg.source_width                 = (uint32_t)w;
     cfg.source_height                = (uint32_t)h;
-    cfg.encoder_bit_depth            = 10;
+    cfg.encoder_bit_depth            = (uint32_t)bd;
     cfg.encoder_color_format         = EB_YUV420;
     cfg.frame_rate_numerator         = 30;
     cfg.frame_rate_denominator       = 1;
@@ -110,7 +115,7 @@ int main(int argc, char **argv) {
     cfg.enable_dlf_flag              = TRUE;
     cfg.cdef_level                   = DEFAULT;
     cfg.enable_restoration_filtering = 1;
-    cfg.logical_processors           = 1;
+    cfg.logical_processors           = (uint32_t)lp;
     check(svt_av1_enc_set_parameter(enc, &cfg), "svt_av1_enc_set_parameter");
     check(svt_av1_enc_init(enc), "svt_av1_enc_init");
     /* the RTCD setup ran inside svt_av1_enc_init (EbEncHandle.c:1530-1531); no picture has been sent yet, and the
@@ -136,6 +141,8 @@ int main(int argc, char **argv) {
     svt_av1_enc_stream_header_release(hdr);
 
     uint16_t *y = malloc((size_t)w * h * 2), *u = malloc((size_t)w * h / 2), *v = malloc((size_t)w * h / 2);
+    /* the 8-bit clip: the same pictures >> 2 */
+    uint8_t *y8 = malloc((size_t)w * h), *u8 = malloc((size_t)w * h / 4), *v8 = malloc((size_t)w * h / 4);
     int       got = 0, done = 0;
     for (int k = 0; k <= nfr && !done; k++) {
         EbBufferHeaderType in;
@@ -145,12 +152,18 @@ int main(int argc, char **argv) {
         in.size = sizeof in;
         if (k < nfr) {
             fill_frame(y, u, v, w, h, k);
-            pic.luma = (uint8_t *)y, pic.cb = (uint8_t *)u, pic.cr = (uint8_t *)v;
+            if (bd == 8) {
+                for (size_t i = 0; i < (size_t)w * h; i++) y8[i] = (uint8_t)(y[i] >> 2);
+                for (size_t i = 0; i < (size_t)w * h / 4; i++) u8[i] = (uint8_t)(u[i] >> 2), v8[i] = (uint8_t)(v[i] >> 2);
+                pic.luma = y8, pic.cb = u8, pic.cr = v8;
+            } else {
+                pic.luma = (uint8_t *)y, pic.cb = (uint8_t *)u, pic.cr = (uint8_t *)v;
+            }
             pic.y_stride = (uint32_t)w, pic.cb_stride = pic.cr_stride = (uint32_t)(w / 2);
             pic.width = (uint32_t)w, pic.height = (uint32_t)h;
-            pic.color_fmt = EB_YUV420, pic.bit_depth = EB_TEN_BIT;
+            pic.color_fmt = EB_YUV420, pic.bit_depth = bd == 8 ? EB_EIGHT_BIT : EB_TEN_BIT;
             in.p_buffer     = (uint8_t *)&pic;
-            in.n_filled_len = (uint32_t)((size_t)w * h * 3);
+            in.n_filled_len = (uint32_t)((size_t)w * h * 3 / (bd == 8 ? 2 : 1));
             in.n_alloc_len  = in.n_filled_len;
             in.pts          = k;
             in.pic_type     = EB_AV1_INVALID_PICTURE;
@@ -187,6 +200,6 @@ int main(int argc, char **argv) {
                "lr_on %llu\n", (unsigned long long)k[0], (unsigned long long)k[1], (unsigned long long)k[2],
                (unsigned long long)k[3], (unsigned long long)k[4], (unsigned long long)k[5], (unsigned long long)k[6]);
     }
-    free(y), free(u), free(v);
+    free(y), free(u), free(v), free(y8), free(u8), free(v8);
     return 0;
 }

@@ -12,7 +12,7 @@
  *                                                  cdef_seg_search is static and still runs, its tables unused),
  *                                                  svt_av1_cdef_frame -> svtgpu_cdef_apply_frame;
  *   svt_aom_rest_kernel  (EbRestProcess.c:580-626): restoration_seg_search -> nothing (the device searches the frame),
- *                                                  rest_finish_search -> svtgpu_lr_search_frame + svtgpu_lr_finish_plane,
+ *                                                  rest_finish_search -> svtgpu_lr_search_frame + svtgpu_lr_finish_frame,
  *                                                  svt_av1_loop_restoration_filter_frame -> svtgpu_lr_apply_frame.
  * Each hook moves the encoder's picture buffers to the device (svtgpu_frame_upload) and its results back into the
  * encoder's own structures exactly where the reference function writes them (frame header fields, mode-info grid,
@@ -513,32 +513,45 @@ void rest_finish_search(PictureControlSet *pcs) {
     int32_t ft[3];
     GPU(svtgpu_lr_search_frame(c->lr, c->O, c->S, &lc, ft, rec, NULL));
     const int nplanes = ((lc.wn_enabled && lc.wn_use_chroma) || (lc.sg_enabled && lc.sg_use_chroma)) ? 3 : 1;
+    /* the units for the encoder's rst_info: the whole frame's host finish over the records (its RestUnitSearchInfo
+     * shared by the planes, as rest_finish_search's: a chroma plane's switchable pass reads luma's entries for a type
+     * chroma does not search -- presets 3-9 with Wiener level 5), which must agree with the device finish's types */
+    SvtGpuRestUnit *units[3];
+    int32_t         t[3];
+    for (int p = 0; p < 3; p++) units[p] = calloc((size_t)n[p], sizeof **units);
+    GPU(svtgpu_lr_finish_frame(&lc, n, (const SvtGpuLrUnitSearch *const *)rec, t, units));
     for (int p = 0; p < 3; p++) {
         RestorationInfo *ri = &pcs->rst_info[p];
         if (p >= nplanes) { /* luma-only search: chroma off (EbRestorationPick.c:1626-1629) */
             ri->frame_restoration_type = RESTORE_NONE;
+            free(units[p]);
             continue;
         }
-        SvtGpuRestUnit *units = calloc((size_t)n[p], sizeof *units);
-        int32_t         t;
-        GPU(svtgpu_lr_finish_plane(&lc, p, n[p], rec[p], &t, units));
-        if (t != ft[p]) die("lr finish: frame type differs from the search's", t);
-        ri->frame_restoration_type = (RestorationType)t;
-        if (t != RESTORE_NONE)
+        if (t[p] != ft[p]) die("lr finish: the host finish's frame type differs from the device's", t[p]);
+        ri->frame_restoration_type = (RestorationType)t[p];
+        if (t[p] != RESTORE_NONE)
             for (int u = 0; u < n[p]; u++) { /* copy_unit_info (EbRestorationPick.c:1202-1209) */
-                RestorationUnitInfo *ui = &ri->unit_info[u];
-                ui->restoration_type    = (RestorationType)units[u].type;
-                if (units[u].type == RESTORE_WIENER)
-                    for (int k = 0; k < 8; k++)
-                        ui->wiener_info.vfilter[k] = units[u].vfilter[k], ui->wiener_info.hfilter[k] = units[u].hfilter[k];
-                else if (units[u].type == RESTORE_SGRPROJ)
-                    ui->sgrproj_info.ep = units[u].ep, ui->sgrproj_info.xqd[0] = units[u].xqd[0],
-                    ui->sgrproj_info.xqd[1] = units[u].xqd[1];
+                RestorationUnitInfo  *ui = &ri->unit_info[u];
+                const SvtGpuRestUnit *g  = &units[p][u];
+                ui->restoration_type     = (RestorationType)g->type;
+                if (g->type == RESTORE_WIENER)
+                    for (int k = 0; k < 8; k++) ui->wiener_info.vfilter[k] = g->vfilter[k], ui->wiener_info.hfilter[k] = g->hfilter[k];
+                else if (g->type == RESTORE_SGRPROJ)
+                    ui->sgrproj_info.ep = g->ep, ui->sgrproj_info.xqd[0] = g->xqd[0], ui->sgrproj_info.xqd[1] = g->xqd[1];
             }
+        /* the device finish's units (svtgpu_lr_read_units) must be the same picks */
+        SvtGpuRestUnit *dev = calloc((size_t)n[p], sizeof *dev);
+        GPU(svtgpu_lr_read_units(c->lr, p, dev, NULL));
+        for (int u = 0; u < n[p] && t[p] != RESTORE_NONE; u++)
+            if (dev[u].type != units[p][u].type || (dev[u].type == RESTORE_WIENER && memcmp(dev[u].vfilter, units[p][u].vfilter, 32)) ||
+                (dev[u].type == RESTORE_SGRPROJ && (dev[u].ep != units[p][u].ep || dev[u].xqd[0] != units[p][u].xqd[0] ||
+                                                    dev[u].xqd[1] != units[p][u].xqd[1])))
+                die("lr finish: the device finish's unit differs from the host finish's", u);
+        free(dev);
         /* search_sgrproj_seg counts each unit's best ep (EbRestorationPick.c:1256; the frame's ep for later frames) */
         if (lc.sg_enabled && (p == 0 || lc.sg_use_chroma))
             for (int u = 0; u < n[p]; u++) cm->sg_frame_ep_cnt[rec[p][u].sgrproj.ep]++;
-        free(units);
+        free(units[p]);
     }
     for (int p = 0; p < 3; p++) c->lr_ft[p] = pcs->rst_info[p].frame_restoration_type, free(rec[p]);
     if (c->lr_ft[0] || c->lr_ft[1] || c->lr_ft[2]) count_kind(0, K_LR_ON), g_calls--;

@@ -75,3 +75,39 @@ def test_encoder_bitstream_identical_with_frame_hooks(tmp_path, geom):
         assert ig[k] >= geom[2], (k, ig)
     assert ig["cdef_apply"] >= 1 and ig["lr_apply"] >= 1 and ig["lr_on"] >= 1, ig
     assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(gpu, "rb").read(), (ic, ig)
+
+
+# Round 6: the configurations an encoder actually runs.  args: width height frames preset qp
+# bit_depth logical_processors.  Presets 3 and 4 run Wiener level 5 (luma only, non-last layers) beside self-guided
+# level 3 (luma and chroma, ep_inc 8): rest_finish_search's switchable pass over a chroma plane then reads luma's entries
+# of the shared RestUnitSearchInfo array (svtgpu_lr_finish_frame; the device finish models the same).  8-bit: the
+# encoder's 8-bit pipeline (is_16bit_pipeline = 0, EbEncHandle.c:4534) through the hooks' 8-bit branch.  Four logical
+# processors: several pictures through the DLF / CDEF / REST processes -- and the hooks' per-picture device state -- at
+# once.  640 x 360: a larger picture (more units per plane, SB rows of every kind).
+WIDE = [
+    ("preset3", (320, 192, 5, 3, 40, 10, 1)),
+    ("preset4", (320, 192, 5, 4, 44, 10, 1)),
+    ("8bit_p2", (320, 192, 4, 2, 40, 8, 1)),
+    ("8bit_p3", (256, 144, 4, 3, 36, 8, 1)),
+    ("lp4_p2", (320, 192, 6, 2, 40, 10, 4)),
+    ("640x360_p3", (640, 360, 3, 3, 40, 10, 2)),
+]
+
+
+@needs_exe
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("name,geom", WIDE)
+def test_encoder_bitstream_identical_wide(tmp_path, name, geom):
+    """Frame-level hooks and the filter RTCD shims, each against the encoder as built, byte for byte, with every hooked
+    call served by the device."""
+    cpu, frm, rt = str(tmp_path / "cpu.obu"), str(tmp_path / "frame.obu"), str(tmp_path / "rtcd.obu")
+    ic = _encode("cpu", cpu, *geom, timeout=1100)
+    ig = _encode("frame", frm, *geom, timeout=1100)
+    assert ig["frame_fallbacks"] == 0 and ig["frame_calls"] >= 3 * geom[2], (name, ig)
+    for k in ("dlf_pick", "dlf_frame", "cdef_pick", "lr_search"):
+        assert ig[k] >= geom[2], (name, k, ig)
+    assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(frm, "rb").read(), (name, ic, ig)
+    ir = _encode("rtcd", rt, *geom, timeout=1100)
+    assert ir["shim_calls"] > 1000, (name, ir)
+    assert open(cpu, "rb").read() == open(rt, "rb").read(), (name, ic, ir)
