@@ -105,9 +105,15 @@ def test_encoder_bitstream_identical_wide(tmp_path, name, geom):
     ic = _encode("cpu", cpu, *geom, timeout=1100)
     ig = _encode("frame", frm, *geom, timeout=1100)
     assert ig["frame_fallbacks"] == 0 and ig["frame_calls"] >= 3 * geom[2], (name, ig)
-    for k in ("dlf_pick", "dlf_frame", "cdef_pick", "lr_search"):
+    for k in ("dlf_pick", "dlf_frame", "cdef_pick"):
         assert ig[k] >= geom[2], (name, k, ig)
     assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(frm, "rb").read(), (name, ic, ig)
+    # restoration is per picture (EncModeConfig.c:1884-1903: the Wiener level depends on is_not_last_layer), and at
+    # preset 4 some pictures have it off, so the search runs on a subset of the frames -- at least one.  Preset 4's
+    # luma-only Wiener level 5 picks RESTORE_NONE for every unit of this clip (the RD finish still runs on the device
+    # and must agree); the other cases really filter
+    assert ig["lr_search"] >= 1, (name, ig)
+    assert name == "preset4" or ig["lr_on"] >= 1, (name, ig)
     ir = _encode("rtcd", rt, *geom, timeout=1100)
     assert ir["shim_calls"] > 1000, (name, ir)
     assert open(cpu, "rb").read() == open(rt, "rb").read(), (name, ic, ir)
