@@ -167,6 +167,9 @@ def parse():
     ap.add_argument("--lr-sync", action="store_true",
                     help="A/B: the synchronous LR search (svtgpu_lr_search_frame: one host wait, frame types back before "
                          "the apply) instead of the asynchronous one (search + device RD finish + apply in stream order)")
+    ap.add_argument("--torch-streams", action="store_true",
+                    help="A/B: the frame slots' streams from torch.cuda.Stream() (torch's stream pool) instead of "
+                         "svtgpu_stream_create")
     ap.add_argument("--lr-serial", action="store_true",
                     help="measurement: every LR search runs its Wiener chain after its self-guided chain on one stream, "
                          "so each search kernel has the device to itself (the condition of the roofline's isolated "
@@ -723,6 +726,19 @@ def main():
         c.set_slot(k)
         return c
 
+    lib_streams = []
+
+    def frame_stream():
+        """A frame slot's stream: made by the library (svtgpu_stream_create), one hardware queue each, wrapped for
+        torch's events; --torch-streams: torch.cuda.Stream() (its pool of 32 streams per priority puts the process
+        past GPU_MAX_HW_QUEUES, and the queues later streams share then depend on creation order: 1080p 10-bit F = 4
+        1870 vs 2440 Mpx/s)."""
+        if a.torch_streams:
+            return torch.cuda.Stream()
+        p = ctx.stream_create(0)
+        lib_streams.append(p)
+        return torch.cuda.ExternalStream(p)
+
     class Slot:
         """One frame in flight: its own input frames, stage states, streams and (tiles) communicator."""
 
@@ -730,10 +746,10 @@ def main():
             """tplan: this rank's SvtGpuTilePlan rects (a tiled picture; comm its communicator), None: the whole frame.
             md_range: the MD batch's superblock range (default: all)."""
             self.k = k
-            self.stream = torch.cuda.Stream()     # the library launches on it, torch events time it
+            self.stream = frame_stream()     # the library launches on it, torch events time it
             # the MD batch (memory-bound) runs beside the VALU-bound LR search on its own stream, or (--md-main) on the
             # main stream: one hardware queue less per frame in flight
-            self.md_stream = self.stream if a.md_main else torch.cuda.Stream()
+            self.md_stream = self.stream if a.md_main else frame_stream()
             sp = self.stream.cuda_stream
             self.src, self.rec = frame_inputs(k)
             self.R, self.S, self.D, self.O, self.L = (svtgpu.Frame(ctx, W, H, bd) for _ in range(5))
@@ -1077,6 +1093,8 @@ def main():
                                    "slot_latency_ms": [round(x, 3) for x in slot_lat],
                                    "slot_wall_ms": [round(getattr(sl, "wall_ms", 0.0), 2) for sl in slots],
                                    "streams_per_frame": 2 if a.md_main else 3,
+                                   "stream_source": "torch.cuda.Stream (pool)" if a.torch_streams
+                                   else "svtgpu_stream_create",
                                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                                    "low": bool(concurrency is not None and F > 1 and concurrency < F / 2),
                                    "note": "sum over the frame slots of their mean frame latency / step time"},
@@ -1145,6 +1163,9 @@ def main():
     for sl in slots:
         if sl.comm is not None:
             sl.comm.close()
+    torch.cuda.synchronize()
+    for p in lib_streams:
+        svtgpu.Context.stream_destroy(p)
     if n > 1:
         dist.destroy_process_group()
 

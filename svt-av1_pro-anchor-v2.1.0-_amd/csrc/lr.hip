@@ -13,6 +13,7 @@
 // workgroup each: the virtual tile is staged in LDS straight from the resident DLF and CDEF frames (no line
 // buffers, no frame extension pass), then the unit's filter runs from LDS and the tile is written once.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -373,7 +374,11 @@ extern "C" int svtgpu_lr_state_create(SvtGpuContext *ctx, int32_t width, int32_t
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr); // null-stream memset done before the caller's streams run
     if (e != hipSuccess) s->d_units[0] = nullptr;
     for (int p = 1; p < 3 && s->d_units[0]; p++) s->d_units[p] = s->d_units[p - 1] + s->hunits[p - 1] * s->vunits[p - 1];
-    if (e == hipSuccess && lr_make_wiener_stream(s) != SVTGPU_OK) e = hipErrorOutOfMemory;
+    static const bool lazy_wst = [] { // SVTGPU_LR_WST_LAZY=1: the Wiener stream made by the first search (A/B)
+        const char *v = std::getenv("SVTGPU_LR_WST_LAZY");
+        return v && v[0] == '1';
+    }();
+    if (e == hipSuccess && !lazy_wst && lr_make_wiener_stream(s) != SVTGPU_OK) e = hipErrorOutOfMemory;
     if (e != hipSuccess) {
         svtgpu_lr_state_destroy(s);
         svtgpu_set_last_hip_error(e, "lr state alloc", __FILE__, __LINE__);

@@ -16,6 +16,7 @@
 // an SB range on demand (svtgpu_md_expand / svtgpu_md_read) -- 8 LDS passes, each shape from two halves of a smaller
 // one, then the per-bit-depth variance formula.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -598,10 +599,16 @@ extern "C" int svtgpu_md_dist_batch(SvtGpuMdBatch *b, const SvtGpuFrame *source,
     b->highbd  = a.highbd;
     if (sb_end == sb_begin) return SVTGPU_OK;
     hipStream_t st = pick_stream(b->ctx, stream);
+    // SVTGPU_MD_LDS=<bytes>: unused dynamic LDS per workgroup, capping how many workgroups share a CU (A/B of the
+    // batch's occupancy beside the frames' latency chains)
+    static const unsigned lds_pad = [] {
+        const char *v = std::getenv("SVTGPU_MD_LDS");
+        return v ? (unsigned)std::atoi(v) : 0u;
+    }();
     if (a.highbd)
-        hipLaunchKernelGGL(md_dist_kernel<uint16_t>, dim3(sb_end - sb_begin), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(md_dist_kernel<uint16_t>, dim3(sb_end - sb_begin), dim3(256), lds_pad, st, a);
     else
-        hipLaunchKernelGGL(md_dist_kernel<uint8_t>, dim3(sb_end - sb_begin), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(md_dist_kernel<uint8_t>, dim3(sb_end - sb_begin), dim3(256), lds_pad, st, a);
     HIP_TRY(hipGetLastError());
     return SVTGPU_OK;
 }

@@ -73,6 +73,35 @@ extern "C" void svtgpu_context_destroy(SvtGpuContext *ctx) {
 
 extern "C" void *svtgpu_context_stream(SvtGpuContext *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+// A caller's stream for the frame-level calls, created here in the caller's order (priority > 0: the device's
+// highest, < 0: its lowest, 0: normal).  Every stream is one hardware queue while there are no more streams than
+// GPU_MAX_HW_QUEUES, and beyond that streams share queues in order -- a frame's chain then waits behind another frame's
+// on the shared queue.  A framework's stream pool (torch.cuda.Stream() draws from 32 streams per priority created at
+// once) puts the process past that count before the first frame runs, which made the queue that each later stream
+// got depend on when it was created (round 6: 1080p 10-bit at four frames in flight 1870 vs 2440 Mpx/s for the same
+// streams created at state creation or at the first search).  A caller that creates exactly the streams it runs
+// frames on gets one queue each.
+extern "C" int svtgpu_stream_create(SvtGpuContext *ctx, int32_t priority, void **out) {
+    if (!ctx || !out) return SVTGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t s = nullptr;
+    if (priority == 0)
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    else
+        HIP_TRY(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority > 0 ? greatest : least));
+    *out = (void *)s;
+    return SVTGPU_OK;
+}
+
+extern "C" void svtgpu_stream_destroy(void *stream) {
+    if (!stream) return;
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    (void)hipStreamDestroy((hipStream_t)stream);
+}
+
 // Test support (the exchange deadline's abort path): one wave that spins on the 100 MHz s_memrealtime clock for `ms`
 // milliseconds (at most 10 s; every lane leaves at the same bound), holding `stream` busy.
 __global__ void stall_kernel(unsigned long long ticks) {

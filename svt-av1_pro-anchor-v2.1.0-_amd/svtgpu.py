@@ -214,6 +214,8 @@ _SIGS = {
     "svtgpu_context_destroy": (None, [_P]),
     "svtgpu_context_stream": (_P, [_P]),
     "svtgpu_synchronize": (ctypes.c_int, [_P, _P]),
+    "svtgpu_stream_create": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_stream_destroy": (None, [_P]),
     "svtgpu_frame_create": (ctypes.c_int, [_P, _I32, _I32, _I32, ctypes.POINTER(_P)]),
     "svtgpu_frame_destroy": (None, [_P]),
     "svtgpu_frame_stride": (_I32, [_P, ctypes.c_int]),
@@ -430,6 +432,18 @@ class Context:
 
     def synchronize(self, stream=None):
         check(lib().svtgpu_synchronize(self.h, stream))
+
+    def stream_create(self, priority=0):
+        """A new hipStream_t (as an int) for the frame-level calls: one hardware queue each while the process has no
+        more streams than GPU_MAX_HW_QUEUES (svtgpu_stream_create).  Wrap it with torch.cuda.ExternalStream to time
+        it with torch events; destroy it with stream_destroy."""
+        h = _P()
+        check(lib().svtgpu_stream_create(self.h, int(priority), ctypes.byref(h)))
+        return h.value
+
+    @staticmethod
+    def stream_destroy(stream):
+        lib().svtgpu_stream_destroy(stream)
 
     def debug_stall(self, ms, stream=None):
         """Test support: hold `stream` busy for `ms` milliseconds (one spinning wave)."""
