@@ -164,6 +164,13 @@ def parse():
     ap.add_argument("--dlf-sync", action="store_true",
                     help="A/B: the synchronous DLF level search (svtgpu_dlf_pick: host-driven bisection, levels back "
                          "before the filter) instead of the asynchronous one (device bisection + filter in stream order)")
+    ap.add_argument("--run-ahead", type=int, default=2, metavar="K",
+                    help="steps a slot's thread may enqueue ahead of its stream's completed ones (the asynchronous "
+                         "searches leave no host wait inside a step)")
+    ap.add_argument("--cdef-async", dest="cdef_sync", action="store_false",
+                    help="A/B: the asynchronous CDEF pick (svtgpu_cdef_pick_async + the apply from device memory, no "
+                         "host wait) instead of the synchronous one (svtgpu_cdef_pick: the host waits for the settle check "
+                         "and the strengths; the default: measured faster at four frames in flight, DESIGN §5)")
     ap.add_argument("--lr-sync", action="store_true",
                     help="A/B: the synchronous LR search (svtgpu_lr_search_frame: one host wait, frame types back before "
                          "the apply) instead of the asynchronous one (search + device RD finish + apply in stream order)")
@@ -773,6 +780,7 @@ def main():
             self.ev = []  # per timed step: events on the streams the kernels run on
             self.ht = []  # --host-timing: per timed step, {call: (wall ms, thread CPU ms)}
             self.lf_levels = []
+            self.inflight = []  # completion events of the steps this slot's thread has enqueued
             self.at_lr = threading.Event()  # this slot's step has reached its LR stage (staggers the next slot)
 
         def close(self):
@@ -793,7 +801,11 @@ def main():
                 st.search(R, S, ctrls, q, sp)
                 if timed:
                     es[2].record(stream)
-                prm, _ = st.pick(ctrls, q, lam, sp)
+                if a.cdef_sync:
+                    prm, _ = st.pick(ctrls, q, lam, sp)
+                else:
+                    st.pick_async(ctrls, q, lam, sp)
+                    prm = None
                 st.apply(R, O, prm, sp)
                 self.at_lr.set()
                 if timed:
@@ -824,7 +836,11 @@ def main():
             hc("cdef_search")
             if timed:
                 es[2].record(stream)
-            prm, _ = st.pick(ctrls, q, lam, sp)
+            if a.cdef_sync:
+                prm, _ = st.pick(ctrls, q, lam, sp)
+            else:  # the strength search and RD choice in stream order, the apply reading their result on the device
+                st.pick_async(ctrls, q, lam, sp)
+                prm = None
             hc("cdef_pick")
             if timed:
                 es[8].record(stream)
@@ -861,6 +877,12 @@ def main():
             if timed:
                 es[5].record(stream)
                 self.ev.append(es)
+            # with no host wait inside a step the thread runs ahead of its stream: at most two steps enqueued
+            done = torch.cuda.Event()
+            done.record(stream)
+            self.inflight.append(done)
+            if len(self.inflight) > a.run_ahead:
+                self.inflight.pop(0).synchronize()
 
     F = a.frames_in_flight
     if emu_rank is not None:
@@ -936,6 +958,9 @@ def main():
         for sl in slots:
             sl.lr.read_result(sl.stream.cuda_stream)
     dlf_rounds = None
+    if a.stages in ("all", "cdef") and not a.cdef_sync:  # every slot's last asynchronous pick (errors raise)
+        for sl in slots:
+            sl.cdef_last = sl.st.read_params(sl.stream.cuda_stream)[0]
     if a.stages == "all" and not a.dlf_sync:  # the last asynchronous level search of every slot
         for sl in slots:
             sl.lf_levels.append(sl.dl.read_levels(sl.stream.cuda_stream).levels())
@@ -1099,6 +1124,8 @@ def main():
                                    "low": bool(concurrency is not None and F > 1 and concurrency < F / 2),
                                    "note": "sum over the frame slots of their mean frame latency / step time"},
                    "lr_search_mode": "sync (host wait)" if a.lr_sync else "async (device RD finish, no host wait)",
+                   "cdef_pick_mode": "sync (host waits: settle check, strengths)" if a.cdef_sync
+                   else "async (device settle flag and parameters, no host wait)",
                    "dlf_search_mode": "sync (host-driven bisection)" if a.dlf_sync
                    else "async (device bisection, no host wait; trial rounds taken / enqueued %s)" % (dlf_rounds,),
                    "ranks": n,

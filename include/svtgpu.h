@@ -102,9 +102,10 @@ int         svtgpu_device_available(void);
 const char *svtgpu_version(void);
 /* ABI revision of this header: bumped whenever a struct passed across the boundary changes layout or an entry
  * point changes meaning (6: SvtGpuLrProfile::ms_events, svtgpu_comm_create_bounded, the asynchronous LR search
- * svtgpu_lr_search_frame_async).  A caller built against another header checks svtgpu_abi_version() ==
+ * svtgpu_lr_search_frame_async; 7: svtgpu_cdef_apply_frame accepts params == NULL, svtgpu_stream_create).
+ * A caller built against another header checks svtgpu_abi_version() ==
  * SVTGPU_ABI_VERSION once at start-up and refuses to run on a mismatch. */
-#define SVTGPU_ABI_VERSION 6
+#define SVTGPU_ABI_VERSION 7
 int32_t     svtgpu_abi_version(void);
 const char *svtgpu_error_string(int code);
 
@@ -335,12 +336,23 @@ int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
 int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                      uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream);
 
+/* The same pick with no host wait (round 6): the settle check's outcome reaches the later strength-search steps
+ * through device memory (they exit at once when every chain has settled), and the RD choice leaves the frame
+ * parameters and the per-FB indices in device memory, where svtgpu_cdef_apply_frame(params = NULL) reads them --
+ * everything in stream order.  svtgpu_cdef_read_params returns them (after a bounded wait for `stream`) once the
+ * caller needs them on the host, e.g. to write the frame header. */
+int svtgpu_cdef_pick_async(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                           uint64_t lambda, void *stream);
+int svtgpu_cdef_read_params(SvtGpuCdefFrameState *s, SvtGpuCdefParams *params_out, int8_t *fb_strength_out,
+                            void *stream);
+
 /* Optional override of the per-FB strength index used by apply (host array of nfb entries). */
 int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream);
 
 /* ≙ svt_av1_cdef_frame (EbEncCdef.c:284-610): apply params to `recon` (DLF output) and write the
  * filtered picture to `out` (out-of-place; the reference's in-place result with its saved
- * unfiltered line/column buffers is identical).  Uses dir/var of the last search. */
+ * unfiltered line/column buffers is identical).  Uses dir/var of the last search.  params == NULL: the parameters
+ * of the last svtgpu_cdef_pick_async, read from device memory in stream order. */
 int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                             const SvtGpuCdefParams *params, void *stream);
 

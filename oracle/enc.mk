@@ -23,7 +23,7 @@ ENC_SRC  := $(wildcard $(S)/Lib/Common/Codec/*.c $(S)/Lib/Common/C_DEFAULT/*.c $
                        $(S)/Lib/Encoder/C_DEFAULT/*.c $(S)/Lib/Encoder/Globals/*.c $(REF)/third_party/fastfeat/*.c)
 ENC_OBJ  := $(patsubst $(REF)/%.c,$(OUT)/obj/%.o,$(ENC_SRC))
 
-all: $(OUT)/libsvtenc.so $(OUT)/enc_drop_in
+all: $(OUT)/libsvtenc.so $(OUT)/enc_drop_in $(OUT)/nss/enc_drop_in
 
 $(OUT)/gen/EbVersion.h: $(S)/Lib/Common/Codec/EbVersion.h.in
 	@mkdir -p $(dir $@)
@@ -42,6 +42,28 @@ $(OUT)/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_fram
                     $(SVTGPU)/libsvtgpu.so
 	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
 	    -L$(OUT) -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../$(SVTGPU)' \
+	    -rdynamic -ldl -lm -lpthread
+
+# The same encoder with the CDEF process body's per-segment CPU search removed (INTEGRATION.md §2 applied): a /tmp copy
+# of EbCdefProcess.c edited by oracle/ref_harness/no_seg_search.py (one call statement), compiled into
+# $(OUT)/nss/libsvtenc.so beside the unchanged objects, and the harness linked against it (frame mode only: the hooked
+# finish_cdef_search searches the frame on the device; the encoder's own finish_cdef_search would find no tables).
+NSS_TMP  ?= /tmp/svtgpu_enc_nss
+$(NSS_TMP)/EbCdefProcess.c: $(S)/Lib/Encoder/Codec/EbCdefProcess.c oracle/ref_harness/no_seg_search.py
+	@mkdir -p $(dir $@)
+	python3 oracle/ref_harness/no_seg_search.py $< $@
+
+$(OUT)/nss/EbCdefProcess.o: $(NSS_TMP)/EbCdefProcess.c $(OUT)/gen/EbVersion.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/nss/libsvtenc.so: $(filter-out %/EbCdefProcess.o,$(ENC_OBJ)) $(OUT)/nss/EbCdefProcess.o
+	$(CC) -shared -o $@ $^ -lm -lpthread
+
+$(OUT)/nss/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_frame_hooks.c $(OUT)/nss/libsvtenc.so \
+                        $(SVTGPU)/libsvtgpu.so
+	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
+	    -L$(OUT)/nss -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../../$(SVTGPU)' \
 	    -rdynamic -ldl -lm -lpthread
 
 clean:

@@ -5,6 +5,7 @@
 
 #include "svtgpu_internal.h"
 
+int svtgpu_cdef_pick_read(SvtGpuCdefFrameState *s, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st);
 int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                           uint64_t lambda, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st);
 
@@ -131,6 +132,7 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
               hipMalloc(&s->d_pick_out, 8 * 8) == hipSuccess && hipMalloc(&s->d_pick_lev, (size_t)(41 * 4 * 32 + 4 * 32 + 64) * 4) == hipSuccess &&
               hipMalloc(&s->d_fb_list, (2 * nfb + 1) * 4) == hipSuccess &&
               hipMalloc(&s->d_pick_xch, SVTGPU_PICK_XCH_BYTES) == hipSuccess &&
+              hipMalloc(&s->d_apick, 64) == hipSuccess &&
               hipHostMalloc((void **)&s->h_pick, 512 + nfb, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
               hipHostGetDevicePointer((void **)&s->h_pick_dev, s->h_pick, 0) == hipSuccess;
     if (!ok) {
@@ -138,6 +140,8 @@ extern "C" int svtgpu_cdef_state_create(SvtGpuContext *ctx, int32_t width, int32
         return SVTGPU_ERR_OOM;
     }
     HIP_TRY(hipMemset(s->d_fb_strength, 0, nfb));
+    HIP_TRY(hipMemset(s->d_apick, 0, 64));
+    std::memset(s->h_pick, 0, 512 + nfb); // no record carries a sequence number yet
     HIP_TRY(hipMemset(s->d_pick_xch, 0, SVTGPU_PICK_XCH_BYTES)); // no word carries a valid tag
     HIP_TRY(hipMemset(s->d_skip, 0, (nfb + 7) & ~(size_t)7)); // the padding stays 0 (the tables' word sums)
     HIP_TRY(hipMemset(s->d_skip, 1, nfb));
@@ -160,7 +164,7 @@ extern "C" void svtgpu_cdef_state_destroy(SvtGpuCdefFrameState *s) {
     delete[] s->h_fb_kind;
     void *bufs[] = {s->d_fb_kind, s->d_mse_rem, s->d_mask, s->own_mse ? s->own_mse : s->d_mse, s->own_skip ? s->own_skip : s->d_skip,
                     s->own_dir ? s->own_dir : s->d_dir, s->own_var ? (void *)s->own_var : (void *)s->d_var, s->d_fb_strength, s->d_pick_part,
-                    s->d_pick_out, s->d_pick_lev, s->d_fb_list, s->d_pick_xch};
+                    s->d_pick_out, s->d_pick_lev, s->d_fb_list, s->d_pick_xch, s->d_apick};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (s->h_pick) (void)hipHostFree(s->h_pick);
@@ -311,11 +315,10 @@ extern "C" int svtgpu_cdef_search_frame(SvtGpuCdefFrameState *s, const SvtGpuFra
     return svtgpu_launch_cdef_sb128_fold(s, uv_on, recon->bit_depth - 8, ctrls->subsampling_factor, st);
 }
 
-extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
-                                uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream) {
-    if (!s || !ctrls || !params_out || !valid_controls(ctrls))
-        return SVTGPU_ERR_INVALID_ARG;
-    hipStream_t st = pick_stream(s->ctx, stream);
+// the pick of svtgpu_cdef_pick (params_out) and svtgpu_cdef_pick_async (params_out == nullptr: no host wait)
+static int cdef_pick_common(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                            uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, hipStream_t st) {
+    const bool async_ = params_out == nullptr;
     // the ranks' search tables (zero elsewhere) summed = gathered; once per search, so a second pick on the same
     // search (another level, another lambda) reads the gathered tables instead of summing them again
     if (svtgpu_comm_tiled(s->comm) && !s->gathered) {
@@ -332,13 +335,20 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
         }
         s->gathered = 1;
     }
+    if (async_) s->apick_ref = ctrls->use_reference_cdef_fs != 0, s->apick_pending = 1, s->apick_ready = 1;
     if (ctrls->use_reference_cdef_fs) { // EbEncCdef.c:744-789: index 0 for every filter block, one pair
-        memset(params_out, 0, sizeof(*params_out));
-        params_out->cdef_damping        = (uint8_t)(3 + (base_q_idx >> 6));
-        params_out->cdef_bits           = 0;
-        params_out->cdef_y_strength[0]  = (uint8_t)ctrls->pred_y_f;
-        params_out->cdef_uv_strength[0] = (uint8_t)ctrls->pred_uv_f;
+        SvtGpuCdefParams q;
+        memset(&q, 0, sizeof(q));
+        q.cdef_damping        = (uint8_t)(3 + (base_q_idx >> 6));
+        q.cdef_bits           = 0;
+        q.cdef_y_strength[0]  = (uint8_t)ctrls->pred_y_f;
+        q.cdef_uv_strength[0] = (uint8_t)ctrls->pred_uv_f;
         HIP_TRY(hipMemsetAsync(s->d_fb_strength, 0, s->nfb, st));
+        if (async_) { // the apply's device copy, in stream order
+            s->apick_params = q;
+            return svtgpu_launch_cdef_set_params(s, &q, st);
+        }
+        *params_out = q;
         if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
         // tiled: the dir / var exchanges above are bounded here, not by some later unbounded wait
         if (svtgpu_comm_tiled(s->comm)) return svtgpu_comm_wait(s->comm, st);
@@ -360,6 +370,31 @@ extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControl
     return svtgpu_prio_leave(&s->prio, hs, st);
 }
 
+extern "C" int svtgpu_cdef_pick(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                                uint64_t lambda, SvtGpuCdefParams *params_out, int8_t *fb_strength_out, void *stream) {
+    if (!s || !ctrls || !params_out || !valid_controls(ctrls))
+        return SVTGPU_ERR_INVALID_ARG;
+    return cdef_pick_common(s, ctrls, base_q_idx, lambda, params_out, fb_strength_out, pick_stream(s->ctx, stream));
+}
+
+// The pick with no host wait: everything in stream order, the frame parameters left in device memory for
+// svtgpu_cdef_apply_frame(params = NULL); svtgpu_cdef_read_params returns them (and the per-FB strengths) later.
+extern "C" int svtgpu_cdef_pick_async(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
+                                      uint64_t lambda, void *stream) {
+    if (!s || !ctrls || !valid_controls(ctrls))
+        return SVTGPU_ERR_INVALID_ARG;
+    return cdef_pick_common(s, ctrls, base_q_idx, lambda, nullptr, nullptr, pick_stream(s->ctx, stream));
+}
+
+extern "C" int svtgpu_cdef_read_params(SvtGpuCdefFrameState *s, SvtGpuCdefParams *params_out, int8_t *fb_strength_out,
+                                       void *stream) {
+    if (!s || !params_out || !s->apick_ready)
+        return SVTGPU_ERR_INVALID_ARG;
+    if (int rc = svtgpu_cdef_pick_read(s, params_out, fb_strength_out, pick_stream(s->ctx, stream))) return rc;
+    if (fb_strength_out && s->d_fb_kind && !s->apick_ref) svtgpu_cdef_sb128_dup_host(s, fb_strength_out);
+    return SVTGPU_OK;
+}
+
 extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t *fb_strength, void *stream) {
     if (!s || !fb_strength)
         return SVTGPU_ERR_INVALID_ARG;
@@ -370,14 +405,14 @@ extern "C" int svtgpu_cdef_set_fb_strength(SvtGpuCdefFrameState *s, const int8_t
 
 extern "C" int svtgpu_cdef_apply_frame(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                                        const SvtGpuCdefParams *params, void *stream) {
-    if (!s || !recon || !out || !params || recon == out)
-        return SVTGPU_ERR_INVALID_ARG;
+    if (!s || !recon || !out || recon == out || (!params && !s->apick_ready))
+        return SVTGPU_ERR_INVALID_ARG; // params == NULL: the last svtgpu_cdef_pick_async's, from device memory
     if (recon->width != s->width || recon->height != s->height || out->width != s->width ||
         out->height != s->height || out->bit_depth != recon->bit_depth)
         return SVTGPU_ERR_INVALID_ARG;
-    if (params->cdef_bits > 3)
+    if (params && params->cdef_bits > 3)
         return SVTGPU_ERR_INVALID_ARG;
-    for (int i = 0; i < (1 << params->cdef_bits); i++)
+    for (int i = 0; params && i < (1 << params->cdef_bits); i++)
         if (params->cdef_y_strength[i] > 63 || params->cdef_uv_strength[i] > 63)
             return SVTGPU_ERR_INVALID_ARG;
     return svtgpu_launch_cdef_apply(s, recon, out, params, pick_stream(s->ctx, stream));

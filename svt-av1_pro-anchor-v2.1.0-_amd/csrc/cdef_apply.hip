@@ -7,6 +7,8 @@
 // LDS once and writes every output sample of the FB exactly once (filtered, or copied when the FB /
 // block / plane is not filtered).  1 read + 1 write per sample (+ the 2-px apron); ~130 integer ops per filtered
 // sample, done two samples per lane on packed int16.
+#include <cstring>
+
 #include "cdef_common.h"
 
 #define NT 256
@@ -29,6 +31,7 @@ struct ApplyArgs {
     const int32_t *var;
     const int8_t  *fb_strength;
     SvtGpuCdefParams prm;
+    const SvtGpuCdefParams *dprm; // the asynchronous pick's parameters in device memory (read instead of prm), or null
     unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
 };
 
@@ -166,8 +169,11 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     const int fbr = fb / A.nhfb, fbc = fb - fbr * A.nhfb, tid = threadIdx.x;
     const int cs = A.cs;
     const int si = A.fb_strength[fb];
-    int level = A.prm.cdef_y_strength[si] >> 2, sec = A.prm.cdef_y_strength[si] & 3;
-    int uvl = A.prm.cdef_uv_strength[si] >> 2, uvs = A.prm.cdef_uv_strength[si] & 3;
+    const int ycode = A.dprm ? A.dprm->cdef_y_strength[si] : A.prm.cdef_y_strength[si];
+    const int uvcode = A.dprm ? A.dprm->cdef_uv_strength[si] : A.prm.cdef_uv_strength[si];
+    const int damping = A.dprm ? A.dprm->cdef_damping : A.prm.cdef_damping;
+    int level = ycode >> 2, sec = ycode & 3;
+    int uvl = uvcode >> 2, uvs = uvcode & 3;
     sec += sec == 3; // EbEncCdef.c:390-396
     uvs += uvs == 3;
     if (tid == 0) nlisted = 0;
@@ -178,7 +184,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
         slisted[tid]  = (uint8_t)l;
         const int dir = l ? A.dir[(size_t)fb * 64 + tid] : 0; // pri_strength ? dir : 0 (EbCdef.c:404)
         const int t   = l ? cdef_adjust_strength(level << cs, A.var[(size_t)fb * 64 + tid]) : 0;
-        sadj[tid]     = (uint32_t)t | ((uint32_t)max(0, A.prm.cdef_damping + cs - msb32_dev((uint32_t)t)) << 16);
+        sadj[tid]     = (uint32_t)t | ((uint32_t)max(0, damping + cs - msb32_dev((uint32_t)t)) << 16);
         sofs[0][tid]  = cdef_tap_offsets(level ? dir : 0, LT);
         sofs[1][tid]  = cdef_tap_offsets(uvl ? dir : 0, CT);
         if (l) atomicAdd(&nlisted, 1);
@@ -235,7 +241,7 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
                   yhi = min(ph[pli], (A.rect[3] + sh) >> sh);
         const uint16_t *tile = pli ? ctile[pli - 1] : ltile;
         // plane-uniform strengths: the chroma primary (no variance adjustment, EbCdef.c:401) and the secondary
-        const int   damp = A.prm.cdef_damping + cs - (pli != 0);
+        const int   damp = damping + cs - (pli != 0);
         const int   cpri = uvl << cs, secs = (pli ? uvs : sec) << cs, podd_c = (cpri >> cs) & 1;
         const s16x2 sthr = {(short)secs, (short)secs};
         const unsigned short ss = (unsigned short)max(0, damp - msb32_dev((uint32_t)secs)),
@@ -278,6 +284,15 @@ __global__ void __launch_bounds__(NT) cdef_apply_kernel(const ApplyArgs A) {
     }
 }
 
+__global__ void cdef_set_params_kernel(SvtGpuCdefParams *d, const SvtGpuCdefParams p) {
+    if (threadIdx.x == 0) *d = p;
+}
+int svtgpu_launch_cdef_set_params(SvtGpuCdefFrameState *s, const SvtGpuCdefParams *p, hipStream_t st) {
+    hipLaunchKernelGGL(cdef_set_params_kernel, dim3(1), dim3(64), 0, st, (SvtGpuCdefParams *)((uint8_t *)s->d_apick + 16), *p);
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
 int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                              const SvtGpuCdefParams *p, hipStream_t st) {
     ApplyArgs A;
@@ -302,7 +317,9 @@ int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, 
     A.dir         = s->d_dir;
     A.var         = s->d_var;
     A.fb_strength = s->d_fb_strength;
-    A.prm         = *p;
+    if (p) A.prm = *p;
+    else std::memset(&A.prm, 0, sizeof A.prm);
+    A.dprm        = p ? nullptr : (const SvtGpuCdefParams *)((const uint8_t *)s->d_apick + 16);
     const dim3 grid((r1 - r0) * A.fbw);
     A.wgclk = svtgpu_wgclk_begin((int)grid.x);
     if (recon->bit_depth > 8)

@@ -46,6 +46,7 @@ struct StepArgs {
     uint64_t       *val;    // [NSTEPS+1][4] value of the call before each step (the period shortcut's copy source)
     StepChain       ch[MAX_CHAINS];
     unsigned long long *wgclk; // diagnostics or null
+    const int32_t  *skip;   // asynchronous pick, the steps after the settle check: nonzero = every chain settled, exit
 };
 
 // ---- compaction: non-skipped FBs in raster order, zero-strength bias (EbEncCdef.c:820-851) ----
@@ -136,6 +137,7 @@ __global__ void __launch_bounds__(NT) sod_step_kernel(const StepArgs A) {
     __shared__ int32_t  sl[32];
     // 1-D grid of 4 row tiles x parts x chains, ordered part-major on the logical index and placed so that
     // consecutive logical indices share an XCD: the 4 * na workgroups staging one FB chunk read it through one L2
+    if (A.skip && *A.skip) return; // uniform: the settle check wrote the final lists (svtgpu_cdef_pick_async)
     wgclk_mark(A.wgclk, 0);
     const int li = xcd_swizzle(blockIdx.x, gridDim.x), tx = li & 3, tz = (li >> 2) % A.na, ty = (li >> 2) / A.na;
     const int nparts = gridDim.x / (4 * A.na);
@@ -530,10 +532,11 @@ __global__ void __launch_bounds__(NT, 4) sod_persist_kernel(const PersistArgs A)
 // steps T + 1 .. L would produce.  One lane per chain; out[0] = 1 when every unfinished chain settled (their fin / best
 // written), out[1] = the latest step at which a chain that needs one settled (or finished): the host's next T.
 struct SettleOut {
-    int32_t settled, step;
+    int32_t settled, step, seq; // seq: the asynchronous pick that wrote it (its next T is read without a wait)
 };
+// flag (device memory, asynchronous pick): the settled word the later steps read
 __global__ void pick_settle_kernel(const int32_t *lev, const uint64_t *val, int32_t *fin, uint64_t *best, int T,
-                                   SettleOut *out) {
+                                   SettleOut *out, int32_t *flag, int seq) {
     __shared__ int s_ok[MAX_CHAINS], s_at[MAX_CHAINS];
     const int c = threadIdx.x;
     if (c < MAX_CHAINS) {
@@ -562,20 +565,33 @@ __global__ void pick_settle_kernel(const int32_t *lev, const uint64_t *val, int3
     }
     __syncthreads();
     if (c == 0) {
-        out->settled = s_ok[0] && s_ok[1] && s_ok[2] && s_ok[3];
+        const int ok = s_ok[0] && s_ok[1] && s_ok[2] && s_ok[3];
+        if (flag) *flag = ok;
+        out->settled = ok;
         out->step    = max(max(s_at[0], s_at[1]), max(s_at[2], s_at[3]));
+        if (seq) {
+            __threadfence_system();
+            __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
 // ---- RD choice over the number of signalled strengths (EbEncCdef.c:853-872) ----
 struct PickOut {
-    int32_t  sb_count, nbits, status, pad;
+    int32_t  sb_count, nbits, status, seq; // seq: the asynchronous pick that wrote it (0: a synchronous one)
     int32_t  gi[32]; // [0, 16) luma, [16, 32) chroma strength indices of the chosen list (zero past nb)
     uint64_t best[MAX_CHAINS];
 };
+// the asynchronous pick's conversion of the chosen list into the frame parameters: strength index gi -> its code
+// (filter_map, EbEncCdef.c:911-919), the damping (:921)
+struct PickMap {
+    uint8_t code[64];
+    uint8_t damping;
+};
 __global__ void pick_final_kernel(const uint64_t *best, const int32_t *fin, const int32_t *count, uint64_t lambda,
                                   PickOut *out, int32_t *status, const uint64_t *wmse, const int32_t *fb_inv, int nfb,
-                                  int8_t *fb_strength, int8_t *host_fbs) {
+                                  int8_t *fb_strength, int8_t *host_fbs, SvtGpuCdefParams *dprm, const PickMap map,
+                                  int seq) {
     __shared__ int32_t gi[32];
     __shared__ int32_t s_nb;
     const int t = threadIdx.x;
@@ -603,6 +619,17 @@ __global__ void pick_final_kernel(const uint64_t *best, const int32_t *fin, cons
             for (int c = 0; c < MAX_CHAINS; c++) out->best[c] = best[c];
             out->status = *status; // the persistent kernel's (0 on the launch path), re-armed for the next pick
             *status     = 0;
+            if (dprm) { // the parameters the apply reads (svtgpu_cdef_apply_frame with params == NULL)
+                SvtGpuCdefParams q;
+                memset(&q, 0, sizeof q);
+                q.cdef_damping = map.damping, q.cdef_bits = (uint8_t)nbits;
+                for (int j = 0; j < nb; j++) q.cdef_y_strength[j] = map.code[gi[j]], q.cdef_uv_strength[j] = map.code[gi[16 + j]];
+                *dprm = q;
+            }
+            if (seq) {
+                __threadfence_system();
+                __hip_atomic_store(&out->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
     __syncthreads();
@@ -643,8 +670,15 @@ static int pick_chunk() {
     return v;
 }
 
+void cdef_pick_host_result(SvtGpuCdefFrameState *s, const PickMap &map, SvtGpuCdefParams *params,
+                           int8_t *fb_strength_out);
+
+// params == nullptr: the asynchronous pick (svtgpu_cdef_pick_async) -- no host wait: the settle check's outcome reaches
+// the later steps through a device flag (they exit at once when every chain has settled), the final kernel writes the
+// frame parameters to device memory for the apply, and the host reads the result later (svtgpu_cdef_read_params)
 int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctrls, int32_t base_q_idx,
                           uint64_t lambda, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st) {
+    const bool async_ = params == nullptr;
     const int nfb = s->nfb;
     const int end = ctrls->first_pass_fs_num + ctrls->default_second_pass_fs_num;
     if (end <= 0 || end > 64)
@@ -674,6 +708,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     A.start_gi = 0;
     A.end_gi   = end;
     A.best     = s->d_pick_out;
+    A.skip     = nullptr;
     hipLaunchKernelGGL(pick_gather_kernel, dim3(nfb), dim3(128), 0, st, s->d_mse, nfb, s->d_fb_list, d_count,
                        (int)ctrls->zero_fs_cost_bias, wmse, wmse32, (int32_t *)A.wide, persist ? nullptr : A.tot);
     unsigned long long *xch = (unsigned long long *)s->d_pick_xch, *stat = nullptr;
@@ -711,6 +746,21 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     }();
     SettleOut *h_settle = (SettleOut *)(s->h_pick + 448), *d_settle = (SettleOut *)(s->h_pick_dev + 448);
     static_assert(sizeof(PickOut) <= 448, "pick output slot below the settle record");
+    int32_t *d_flag = (int32_t *)s->d_apick; // asynchronous: the settled word (device memory)
+    if (async_) {
+        // the last asynchronous check whose record has landed (read without a wait: the host may run ahead of the
+        // device) moves T as the synchronous path does right after its check
+        const volatile SettleOut *hs = (const volatile SettleOut *)h_settle;
+        if (hs->seq != 0 && hs->seq != s->settle_seen) {
+            s->settle_seen = hs->seq;
+            if (hs->settled) {
+                s->pick_settle = hs->step, s->pick_miss = 0;
+            } else {
+                s->pick_settle = std::min(s->pick_settle + 4, NSTEPS - 4);
+                if (++s->pick_miss >= 2) s->pick_skip = 8, s->pick_miss = 0;
+            }
+        }
+    }
     // after two consecutive checks that found a chain unsettled the next 8 picks skip the check (its host wait saves
     // nothing on a sequence that does not settle), then it is tried again from step 24
     const bool check = settle_on && s->pick_skip == 0;
@@ -729,6 +779,7 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
             C.prev_shift   = step >= 1 && step < len && step >= nb; // shift before calls nb.. (refinements)
         }
         A.step = step;
+        A.skip = async_ && step > T ? d_flag : nullptr;
         // ~256 workgroups per step whatever the number of live chains (64 parts x 4 row tiles: 256 parts spent
         // more on the u64 atomics than they gained, 0.66 -> 0.59 ms per pick + apply); chunk <= PICK_CHUNK FBs
         const int want  = std::max(1, pick_parts() / std::max(na, 1));
@@ -739,9 +790,13 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         A.wgclk = svtgpu_wgclk_begin(4 * parts * na);
         hipLaunchKernelGGL(sod_step_kernel, dim3(4 * parts * na), dim3(NT), lds, st, A);
         svtgpu_wgclk_end("sod_step", 4 * parts * na, st);
-        if (step == T && T < NSTEPS) {
+        if (step == T && T < NSTEPS && async_) { // the check in stream order; the later steps read its flag
             hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
-                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle);
+                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, d_flag, ++s->settle_seq);
+            HIP_TRY(hipGetLastError());
+        } else if (step == T && T < NSTEPS) {
+            hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
+                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, (int32_t *)nullptr, 0);
             HIP_TRY(hipGetLastError());
             if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded behind the tables' exchange
             svtgpu_count_xfer(1, sizeof(SettleOut));
@@ -756,13 +811,25 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     }
     HIP_TRY(hipGetLastError());
     PickOut *h_out = (PickOut *)s->h_pick;
-    int8_t  *h_fbs = (int8_t *)(s->h_pick + 512);
     static_assert(sizeof(PickOut) <= 512, "pick output slot");
-    int8_t *host_fbs = fb_strength_out ? (int8_t *)(s->h_pick_dev + 512) : nullptr;
+    int8_t *host_fbs = fb_strength_out || async_ ? (int8_t *)(s->h_pick_dev + 512) : nullptr;
+    PickMap map;
+    std::memset(&map, 0, sizeof map);
+    const int nf = ctrls->first_pass_fs_num;
+    for (int g = 0; g < end; g++) // gi -> strength code (filter_map, EbEncCdef.c:911-919)
+        map.code[g] = g < nf ? ctrls->default_first_pass_fs[g] : ctrls->default_second_pass_fs[g - nf];
+    map.damping = (uint8_t)(3 + (base_q_idx >> 6)); // :921
+    const int seq = async_ ? ++s->apick_seq : 0;
     hipLaunchKernelGGL(pick_final_kernel, dim3((nfb + NT - 1) / NT), dim3(NT), 0, st, (const uint64_t *)s->d_pick_out,
                        (const int32_t *)A.fin, (const int32_t *)d_count, (uint64_t)lambda, (PickOut *)s->h_pick_dev,
-                       d_status, (const uint64_t *)wmse, (const int32_t *)d_inv, nfb, s->d_fb_strength, host_fbs);
+                       d_status, (const uint64_t *)wmse, (const int32_t *)d_inv, nfb, s->d_fb_strength, host_fbs,
+                       async_ ? (SvtGpuCdefParams *)((uint8_t *)s->d_apick + 16) : (SvtGpuCdefParams *)nullptr, map, seq);
     HIP_TRY(hipGetLastError());
+    if (async_) {
+        std::memcpy(s->apick_map, map.code, 64);
+        s->apick_damping = map.damping;
+        return SVTGPU_OK;
+    }
     if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // the only wait of the pick (bounded when tiled)
     if (h_out->status) {
         svtgpu_set_last_hip_error(hipErrorUnknown, "CDEF pick: the persistent step exchange timed out", __FILE__, __LINE__);
@@ -775,22 +842,49 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         std::fprintf(stderr, "sod_persist (workgroup 0): compute+store %.1f us, reduce %.1f us, minima %.1f us\n",
                      v[0] * 0.01, v[1] * 0.01, v[2] * 0.01);
     }
+    cdef_pick_host_result(s, map, params, fb_strength_out);
+    return SVTGPU_OK;
+}
+
+// the pick's result from the mapped record (after the stream wait): the parameters through the strength map, the
+// per-FB strengths
+void cdef_pick_host_result(SvtGpuCdefFrameState *s, const PickMap &map, SvtGpuCdefParams *params,
+                           int8_t *fb_strength_out) {
+    const PickOut *h_out = (const PickOut *)s->h_pick;
     memset(params, 0, sizeof(*params));
     const int nbits = h_out->nbits, nb = 1 << nbits;
-    params->cdef_bits = (uint8_t)nbits;
+    params->cdef_bits    = (uint8_t)nbits;
+    params->cdef_damping = map.damping;
     for (int j = 0; j < nb; j++) {
-        params->cdef_y_strength[j]  = (uint8_t)h_out->gi[j];
-        params->cdef_uv_strength[j] = (uint8_t)h_out->gi[16 + j];
+        params->cdef_y_strength[j]  = map.code[h_out->gi[j]];
+        params->cdef_uv_strength[j] = map.code[h_out->gi[16 + j]];
     }
-    if (fb_strength_out) memcpy(fb_strength_out, h_fbs, nfb);
-    svtgpu_count_xfer(1, sizeof(PickOut) + (fb_strength_out ? nfb : 0)); // mapped memory
-    // gi -> strength code (filter_map, EbEncCdef.c:911-919); damping (:921)
-    const int nf = ctrls->first_pass_fs_num;
-    for (int i = 0; i < nb; i++) {
-        const int y = params->cdef_y_strength[i], uv = params->cdef_uv_strength[i];
-        params->cdef_y_strength[i]  = y < nf ? ctrls->default_first_pass_fs[y] : ctrls->default_second_pass_fs[y - nf];
-        params->cdef_uv_strength[i] = uv < nf ? ctrls->default_first_pass_fs[uv] : ctrls->default_second_pass_fs[uv - nf];
+    if (fb_strength_out) memcpy(fb_strength_out, s->h_pick + 512, s->nfb);
+    svtgpu_count_xfer(1, sizeof(PickOut) + (fb_strength_out ? s->nfb : 0)); // mapped memory
+}
+
+// svtgpu_cdef_read_params: the last asynchronous pick's result, after a (bounded) wait for the stream
+int svtgpu_cdef_pick_read(SvtGpuCdefFrameState *s, SvtGpuCdefParams *params, int8_t *fb_strength_out, hipStream_t st) {
+    if (int rc = svtgpu_comm_wait(s->comm, st)) return rc;
+    s->apick_pending = 0;
+    if (s->apick_ref) { // the reference-fs parameters (no search): known when the pick was enqueued
+        *params = s->apick_params;
+        if (fb_strength_out) memset(fb_strength_out, 0, s->nfb);
+        return SVTGPU_OK;
     }
-    params->cdef_damping = (uint8_t)(3 + (base_q_idx >> 6));
+    const volatile PickOut *h_out = (const volatile PickOut *)s->h_pick;
+    if (h_out->seq != s->apick_seq) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "CDEF asynchronous pick: result record missing after the stream wait",
+                                  __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    if (h_out->status) {
+        svtgpu_set_last_hip_error(hipErrorUnknown, "CDEF pick: the persistent step exchange timed out", __FILE__, __LINE__);
+        return SVTGPU_ERR_HIP;
+    }
+    PickMap map;
+    std::memcpy(map.code, s->apick_map, 64);
+    map.damping = s->apick_damping;
+    cdef_pick_host_result(s, map, params, fb_strength_out);
     return SVTGPU_OK;
 }

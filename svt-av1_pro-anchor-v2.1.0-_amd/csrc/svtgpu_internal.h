@@ -123,6 +123,13 @@ struct SvtGpuCdefFrameState {
     int8_t        *h_fb_kind;     // host copy
     uint8_t       *d_mse_rem;     // [3][nfb][64] remainders of the per-FB distortion shift (SB128 only)
     SvtGpuPrioLane prio;          // the pick's launch chain
+    // svtgpu_cdef_pick_async: [0] the settle check's flag for the later steps, [16..] the parameters the apply reads
+    void          *d_apick;
+    int32_t        settle_seq, settle_seen; // settle checks enqueued / the last one whose record the host has taken
+    int32_t        apick_seq;               // asynchronous picks enqueued (the record's seq)
+    int32_t        apick_pending, apick_ready, apick_ref; // a result not yet read; device parameters exist; ref-fs
+    SvtGpuCdefParams apick_params;          // ref-fs: the parameters (known at enqueue)
+    uint8_t        apick_map[64], apick_damping; // the strength map of the pending pick (its read-back)
 };
 
 // Device-side view of the searched strengths (built on the host from SvtGpuCdefControls).
@@ -152,8 +159,11 @@ int svtgpu_launch_cdef_search(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon,
 int  svtgpu_launch_cdef_sb128_fold(SvtGpuCdefFrameState *s, unsigned long long uv_on, int cs, int ss, hipStream_t st);
 int  svtgpu_launch_cdef_sb128_dup(SvtGpuCdefFrameState *s, hipStream_t st);
 void svtgpu_cdef_sb128_dup_host(const SvtGpuCdefFrameState *s, int8_t *fbs);
+// p == nullptr: the parameters the last asynchronous pick left in device memory
 int svtgpu_launch_cdef_apply(SvtGpuCdefFrameState *s, const SvtGpuFrame *recon, SvtGpuFrame *out,
                              const SvtGpuCdefParams *p, hipStream_t st);
+// the asynchronous pick's device parameters set to `p` in stream order (the reference-fs case: no search)
+int svtgpu_launch_cdef_set_params(SvtGpuCdefFrameState *s, const SvtGpuCdefParams *p, hipStream_t st);
 
 // the default context's stream (per-block shims and stream-less frame-level calls)
 hipStream_t svtgpu_default_stream();

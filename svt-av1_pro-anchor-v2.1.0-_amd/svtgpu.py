@@ -244,6 +244,8 @@ _SIGS = {
                                         _P, _P]),
     "svtgpu_cdef_set_fb_strength": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_cdef_apply_frame": (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(CdefParams), _P]),
+    "svtgpu_cdef_pick_async": (ctypes.c_int, [_P, ctypes.POINTER(CdefControls), _I32, _U64, _P]),
+    "svtgpu_cdef_read_params": (ctypes.c_int, [_P, ctypes.POINTER(CdefParams), _P, _P]),
     "svtgpu_cdef_set_fb_rows": (ctypes.c_int, [_P, _I32, _I32]),
     "svtgpu_cdef_bind_tables": (ctypes.c_int, [_P, _P, _P]),
     "svtgpu_cdef_bind_dir_tables": (ctypes.c_int, [_P, _P, _P]),
@@ -689,12 +691,25 @@ class CdefState:
         check(lib().svtgpu_cdef_pick(self.h, ctypes.byref(ctrls), base_q_idx, lam, ctypes.byref(prm), ptr(fbs), stream))
         return prm, fbs
 
+    def pick_async(self, ctrls, base_q_idx, lam, stream=None):
+        """svtgpu_cdef_pick_async: the pick in stream order, no host wait; apply(params=None) uses its result."""
+        check(lib().svtgpu_cdef_pick_async(self.h, ctypes.byref(ctrls), base_q_idx, lam, stream))
+
+    def read_params(self, stream=None):
+        """The last pick_async's parameters and per-FB strength indices (waits for `stream`)."""
+        prm = CdefParams()
+        fbs = np.zeros(self.nfb, dtype=np.int8)
+        check(lib().svtgpu_cdef_read_params(self.h, ctypes.byref(prm), ptr(fbs), stream))
+        return prm, fbs
+
     def set_fb_strength(self, fbs, stream=None):
         self._fbs = np.ascontiguousarray(fbs, dtype=np.int8)
         check(lib().svtgpu_cdef_set_fb_strength(self.h, ptr(self._fbs), stream))
 
     def apply(self, recon, out, params, stream=None):
-        check(lib().svtgpu_cdef_apply_frame(self.h, recon.h, out.h, ctypes.byref(params), stream))
+        """params None: the last pick_async's parameters, from device memory."""
+        check(lib().svtgpu_cdef_apply_frame(self.h, recon.h, out.h, ctypes.byref(params) if params is not None else None,
+                                            stream))
 
     def read(self, stream=None):
         mse = np.empty((2, self.nfb, 64), dtype=np.uint64)

@@ -217,13 +217,17 @@ def run_gpu(case, ctx=None, async_=None):
     ctrls.pred_y_f, ctrls.pred_uv_f = c["pred"]
     st.search(D, S, ctrls, c["q"])
     tables = st.read()
-    prm, fbs = st.pick(ctrls, c["q"], int(g["cdef_lambda"][0]))
-    nb = 1 << prm.cdef_bits
-    applied = int(prm.cdef_y_strength[0] != 0 or prm.cdef_uv_strength[0] != 0 or nb != 1)
-    if applied:
-        st.apply(D, C, prm)
+    if async_:  # the pick in stream order; the apply reads its parameters on the device (zero strengths: a copy)
+        st.pick_async(ctrls, c["q"], int(g["cdef_lambda"][0]))
+        st.apply(D, C, None)
     else:
-        svtgpu.check(svtgpu.lib().svtgpu_frame_copy(C.h, D.h, None))
+        prm, fbs = st.pick(ctrls, c["q"], int(g["cdef_lambda"][0]))
+        nb = 1 << prm.cdef_bits
+        applied = int(prm.cdef_y_strength[0] != 0 or prm.cdef_uv_strength[0] != 0 or nb != 1)
+        if applied:
+            st.apply(D, C, prm)
+        else:
+            svtgpu.check(svtgpu.lib().svtgpu_frame_copy(C.h, D.h, None))
     us = [c["us"][0], c["us"][1], c["us"][1]]
     lr = svtgpu.LrState(ctx, w, h, us)
     lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
@@ -240,6 +244,10 @@ def run_gpu(case, ctx=None, async_=None):
         else:
             svtgpu.check(svtgpu.lib().svtgpu_frame_copy(O.h, C.h, None))
     ctx.synchronize()
+    if async_:
+        prm, fbs = st.read_params()
+        nb = 1 << prm.cdef_bits
+        applied = int(prm.cdef_y_strength[0] != 0 or prm.cdef_uv_strength[0] != 0 or nb != 1)
     out = dict(src=src, rec=rec, mi=mi, lf=lfp.levels(), dlf=D.download(), tables=tables, prm=prm, nb=nb, fbs=fbs,
                applied=applied, cdef=C.download(), ft=ft, units=units, recs=recs, lrc=lrc, lr=O.download())
     for x in (S, R, D, C, O, dl, st, lr):

@@ -351,3 +351,51 @@ def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch, scale_hi):
             prm, fbs = st.pick(ctrls, q, lam)
             assert prm.as_tuple() == oprm.as_tuple() and np.array_equal(fbs, ofbs), seed
     assert seen == {True, False}  # settled and unsettled chains both covered
+
+
+@pytest.mark.parametrize("persist", ["0", "1"])
+def test_cdef_pick_async_vs_oracle(ctx, monkeypatch, persist):
+    """svtgpu_cdef_pick_async (no host wait: the settle check's outcome reaches the later steps through a device flag,
+    the parameters stay on the device) on the settled / unsettled tables of the test above: svtgpu_cdef_read_params
+    equals the oracle's pick on every seed, three picks in a row on one state (the checkpoint T then moves from the
+    records the earlier picks left, read without a wait), and the apply from device parameters writes the same planes
+    as the apply with the host parameters."""
+    import torch
+    monkeypatch.setenv("SVTGPU_PICK_PERSIST", persist)
+    w, h, q, lam = 1920, 1080, 128, 60000
+    ctrls = svtgpu.cdef_controls(1)
+    st = svtgpu.CdefState(ctx, w, h)
+    seen = set()
+    for seed in range(6):
+        rng = np.random.default_rng(seed)
+        j = np.arange(64)
+        opt = rng.integers(0, 64, size=(2, st.nfb, 1))
+        scale = rng.integers(1 << 10, 1 << 14, size=(2, st.nfb, 1))
+        mse = (scale * (64 + (j - opt) ** 2) + rng.integers(0, 1 << 12, size=(2, st.nfb, 64))).astype(np.uint64)
+        skip = (rng.random(st.nfb) < 0.1).astype(np.uint8)
+        seen.update(x is None for x in _settle_calls(mse, skip)[1:])
+        mse_t = torch.from_numpy(mse.view(np.int64)).cuda()
+        skip_t = torch.from_numpy(skip).cuda()
+        st.bind_tables(mse_t.data_ptr(), skip_t.data_ptr())
+        torch.cuda.synchronize()
+        oprm, ofbs = oracle.cdef_pick(w, h, mse, skip, ctrls, q, lam)
+        for _ in range(3):
+            st.pick_async(ctrls, q, lam)
+            prm, fbs = st.read_params()
+            assert prm.as_tuple() == oprm.as_tuple() and np.array_equal(fbs, ofbs), seed
+    assert seen == {True, False}
+    # the apply from device parameters: a real frame, search + async pick + apply(None) vs the synchronous pick
+    w2, h2 = 640, 384
+    src, rec = synth.frame_pair(w2, h2, 10, seed=0x5EED0177)
+    S, R, O1, O2 = (svtgpu.Frame(ctx, w2, h2, 10) for _ in range(4))
+    S.upload(src), R.upload(rec)
+    st2 = svtgpu.CdefState(ctx, w2, h2)
+    st2.search(R, S, ctrls, q)
+    prm1, fbs1 = st2.pick(ctrls, q, lam)
+    st2.apply(R, O1, prm1)
+    st2.pick_async(ctrls, q, lam)
+    st2.apply(R, O2, None)
+    prm2, fbs2 = st2.read_params()
+    assert prm1.as_tuple() == prm2.as_tuple() and np.array_equal(fbs1, fbs2)
+    for a, b in zip(O1.download(), O2.download()):
+        assert np.array_equal(a, b)

@@ -21,8 +21,15 @@ EXE = os.path.join(ROOT, "oracle", "_ref", "enc", "enc_drop_in")
 needs_exe = pytest.mark.skipif(not os.path.exists(EXE), reason="oracle/_ref/enc not built (needs /root/reference)")
 
 
-def _encode(mode, path, *args, timeout=600):
-    r = subprocess.run([EXE, mode, path] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout)
+# the encoder with the CDEF process body's per-segment CPU search removed (oracle/ref_harness/no_seg_search.py: a /tmp
+# copy of EbCdefProcess.c with its one cdef_seg_search call taken out; INTEGRATION.md §2 applied)
+EXE_NSS = os.path.join(ROOT, "oracle", "_ref", "enc", "nss", "enc_drop_in")
+OBJ = os.path.join(ROOT, "oracle", "_ref", "enc", "obj", "Source", "Lib", "Encoder", "Codec", "EbCdefProcess.o")
+OBJ_NSS = os.path.join(ROOT, "oracle", "_ref", "enc", "nss", "EbCdefProcess.o")
+
+
+def _encode(mode, path, *args, timeout=600, exe=EXE):
+    r = subprocess.run([exe, mode, path] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, (mode, r.returncode, r.stderr[-2000:])
     out = {}
     for l in r.stdout.splitlines():  # "<mode> bytes <n> packets <n> ..." and (frame mode) "frame kinds <k> <n> ..."
@@ -117,3 +124,32 @@ def test_encoder_bitstream_identical_wide(tmp_path, name, geom):
     ir = _encode("rtcd", rt, *geom, timeout=1100)
     assert ir["shim_calls"] > 1000, (name, ir)
     assert open(cpu, "rb").read() == open(rt, "rb").read(), (name, ic, ir)
+
+
+@pytest.mark.skipif(not os.path.exists(OBJ_NSS), reason="oracle/_ref/enc/nss not built (needs /root/reference)")
+def test_no_seg_search_build_drops_the_cpu_search():
+    """The edited CDEF process body no longer contains the per-segment search: the static cdef_seg_search is defined
+    in the encoder's own object and absent from the edited one (unreferenced after the edit, the compiler drops it),
+    and the edited object references no other symbol than the original does."""
+    def syms(path):
+        r = subprocess.run(["nm", path], capture_output=True, text=True, check=True)
+        return {l.split()[-1]: l.split()[-2] for l in r.stdout.splitlines() if l.strip()}
+    a, b = syms(OBJ), syms(OBJ_NSS)
+    assert "cdef_seg_search" in a and "cdef_seg_search" not in b
+    assert {k for k, t in b.items() if t == "U"} <= {k for k, t in a.items() if t == "U"} | {"svt_aom_assert_err"}
+
+
+@pytest.mark.skipif(not os.path.exists(EXE_NSS), reason="oracle/_ref/enc/nss not built (needs /root/reference)")
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("name,geom", [("p2_10bit", (320, 192, 5, 2, 40, 10, 1)), ("8bit_p3", (256, 144, 4, 3, 36, 8, 1)),
+                                       ("640x360_p3_lp2", (640, 360, 3, 3, 40, 10, 2))])
+def test_encoder_without_cpu_cdef_search(tmp_path, name, geom):
+    """The encoder with the per-segment CPU search removed from its CDEF process body and finish_cdef_search /
+    svt_av1_cdef_frame (and the DLF / LR frame functions) served by the device writes the bitstream of the encoder as
+    built, byte for byte, every hooked call on the device: nothing of the CPU search's output was needed."""
+    cpu, frm = str(tmp_path / "cpu.obu"), str(tmp_path / "frame_nss.obu")
+    ic = _encode("cpu", cpu, *geom, timeout=1100)
+    ig = _encode("frame", frm, *geom, timeout=1100, exe=EXE_NSS)
+    assert ig["frame_fallbacks"] == 0 and ig["cdef_pick"] >= geom[2], (name, ig)
+    assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(frm, "rb").read(), (name, ic, ig)
