@@ -813,13 +813,18 @@ __host__ __device__ inline int tap_min(int t) { return t == 0 ? -5 : t == 1 ? -2
 __host__ __device__ inline int tap_max(int t) { return t == 0 ? 10 : t == 1 ? 8 : 46; }
 __host__ __device__ inline bool sgr_r0(int ep) { return ep < 10 || ep > 13; } // c_sgr_r[ep][0] > 0
 __host__ __device__ inline bool sgr_r1(int ep) { return ep < 14; }            // c_sgr_r[ep][1] > 0
+// unrolled over constant tap indices: on the device the taps stay in registers (a pointer to either filter array,
+// indexed in a loop, put the unit on the stack: every evaluation a chain of scratch round trips)
 __host__ __device__ inline int wiener_bits(int win, const SvtGpuRestUnit &w, const SvtGpuRestUnit &ref) {
     int bits = 0;
-    for (int f = 0; f < 2; f++) {
-        const int16_t *a = f ? w.hfilter : w.vfilter, *r = f ? ref.hfilter : ref.vfilter;
-        for (int t = win == 7 ? 0 : 1; t < 3; t++)
-            bits += refsubexpfin(tap_max(t) - tap_min(t) + 1, t + 1, r[t] - tap_min(t), a[t] - tap_min(t));
-    }
+#pragma unroll
+    for (int f = 0; f < 2; f++)
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+            if (t == 0 && win != 7) continue;
+            const int a = f ? w.hfilter[t] : w.vfilter[t], r = f ? ref.hfilter[t] : ref.vfilter[t];
+            bits += refsubexpfin(tap_max(t) - tap_min(t) + 1, t + 1, r - tap_min(t), a - tap_min(t));
+        }
     return bits;
 }
 __host__ __device__ inline int sgrproj_bits(const SvtGpuRestUnit &s, const SvtGpuRestUnit &ref) {
@@ -2437,7 +2442,7 @@ void finish_frame_host(const SvtGpuLrSearchControls *c, int nplanes, const int32
 // plane does not search.
 // ---------------------------------------------------------------------------------------------
 constexpr int FIN_K1 = 63; // r = 1 / 2 masks: bit k < 63 = the unit k + 1 back as the reference, bit 63 = the default
-constexpr int FIN_CH = 16; // switchable walk: units of cost tables staged in LDS at a time (per wave)
+constexpr int FIN_CH = 64; // the walks: units per chunk (a lane per unit; the switchable tables staged in LDS)
 constexpr int FIN_OUT = 8; // device result words: frame types [3], search status, sequence
 
 struct RecArgs {
@@ -2486,7 +2491,7 @@ struct FinArgs {
     int32_t                   nplanes, nrec, rdmult, sw[3], wn[2], sg[2];
     const SvtGpuLrUnitSearch *rec;
     unsigned long long       *m1, *m2;
-    double                   *c0, *c1, *c2; // switchable: the NONE cost; the Wiener / self-guided costs [unit][64]
+    uint8_t                  *b1, *b2; // switchable: the Wiener / self-guided coefficient bits [unit][64] (< 2^8)
     int32_t                  *path;   // [4][nrec]: r 1, r 2, r 3 (Wiener ref), r 3 (self-guided ref): choice | (ref + 1) << 2
     SvtGpuRestUnit           *units;  // the state's units (d_units[0]: the planes back to back, the records' layout)
     int32_t                  *out;    // [FIN_OUT] device results
@@ -2494,6 +2499,8 @@ struct FinArgs {
     const int32_t            *wstat, *sstat; // the descents' status words (wiener_res / sgr_res) or null
     int32_t                   seq;
     unsigned long long       *clk; // diagnostics (SVTGPU_LR_FIN_CLK): the walk's phase ends on s_memrealtime, or null
+    int32_t                   wtab; // the walks read the tables for references up to wtab units back (FIN_K1; tests:
+                                    // SVTGPU_LR_FIN_WIN = 1 sends nearly every step to the evaluation at the step)
 };
 
 // the shared rusi entries of unit u of plane p a switchable pass and copy_unit_info read
@@ -2530,6 +2537,11 @@ __device__ double fin_c2(const FinArgs &F, int p, int u, int rs) {
 __device__ inline double fin_c0(const FinArgs &F, int p, int u) {
     return rdcost(F.rdmult, (int64_t)F.sw[0] >> 4, fin_rec(F, p, u).sse[0]);
 }
+// the rate term of RDCOST_DBL for the bits sw + (coef << 9) (rdcost's first addend, the same operations)
+__device__ inline double fin_rate(int rdmult, int sw, int coef) {
+    const int64_t b = sw + ((int64_t)coef << 9);
+    return ((double)(b >> 4) * rdmult) / (double)(1 << 9);
+}
 // the choice (t == 0 || cost < best, in type order) with types 1 / 2 allowed by a1 / a2
 __device__ inline int fin_pick(double c0, double c1, double c2, bool a1, bool a2) {
     int    bt = 0;
@@ -2555,9 +2567,16 @@ __global__ __launch_bounds__(64) void lr_fin_tables_kernel(const FinArgs F) {
         if (lane == 0) (r == 1 ? F.m1 : F.m2)[b] = m;
     }
     if (!P.run[3]) return;
-    F.c1[(size_t)b * 64 + lane] = ok ? fin_c1(F, p, u, ref) : 0.0;
-    F.c2[(size_t)b * 64 + lane] = ok ? fin_c2(F, p, u, ref) : 0.0;
-    if (lane == 0) F.c0[b] = fin_c0(F, p, u);
+    // the switchable pass's coefficient bits against each candidate reference (its costs are formed in the walk)
+    int c1 = 0, c2 = 0;
+    if (ok) {
+        const SvtGpuRestUnit rw = ref < 0 ? default_wiener() : fin_w(F, p, ref).wiener;
+        const SvtGpuRestUnit rs = ref < 0 ? default_sgrproj() : fin_s(F, p, ref).sgrproj;
+        c1 = wiener_bits(p == 0 ? 7 : 5, fin_w(F, p, u).wiener, rw);
+        c2 = sgrproj_bits(fin_s(F, p, u).sgrproj, rs);
+    }
+    F.b1[(size_t)b * 64 + lane] = (uint8_t)c1;
+    F.b2[(size_t)b * 64 + lane] = (uint8_t)c2;
 }
 
 // a wave-uniform 64-bit value held by lane i of v
@@ -2567,11 +2586,15 @@ __device__ inline unsigned long long lane_u64(unsigned long long v, int i) {
     return ((unsigned long long)hi << 32) | lo;
 }
 
-// The chains are walked a chunk of units at a time by one wave.  At a chunk's start the wave evaluates, lane-parallel,
-// every unit of the chunk against the reference the chain holds then (the decision or the costs themselves, exactly as
-// the tables do): while the chain keeps that reference -- however far back it lies -- a unit's step reads that; once a
-// unit of the chunk has taken the filter, the reference lies inside the chunk, within the tabulated window.  No unit
-// waits on a serial evaluation or on a global load that depends on the chain.
+// a wave-uniform double held by lane i of v
+__device__ inline double lane_f64(double v, int i) { return __builtin_bit_cast(double, lane_u64(__builtin_bit_cast(unsigned long long, v), i)); }
+
+// The chains are walked by one wave each, a chunk of FIN_CH units at a time, a lane per unit of the chunk.  A unit's
+// decision against its reference comes from the tables when the reference is one of the 63 units before it or the
+// default (a bit of the unit's mask, or its coefficient bits in LDS); a reference further back can only be the one the
+// chain held when the chunk began (a reference taken inside the chunk is at most 62 units back), so every unit of the
+// chunk is evaluated against that one at the chunk's start, lane-parallel.  A step reads no global memory and waits
+// on no evaluation (only the test window SVTGPU_LR_FIN_WIN < 63 reaches the evaluation at the step).
 
 // the r = 1 / r = 2 chain of plane p: path[u] = decision | (reference + 1) << 2
 __device__ void fin_walk12(const FinArgs &F, int p, int r, int lane) {
@@ -2579,113 +2602,150 @@ __device__ void fin_walk12(const FinArgs &F, int p, int r, int lane) {
     const unsigned long long *M    = (r == 1 ? F.m1 : F.m2) + P.base;
     int32_t                  *path = F.path + (size_t)(r - 1) * F.nrec + P.base;
     int                       ref  = -1;
-    for (int u0 = 0; u0 < P.n; u0 += 64) {
-        const unsigned long long mv = u0 + lane < P.n ? M[u0 + lane] : 0ull;
-        const int                nl = min(64, P.n - u0), ref0 = ref;
-        const bool               sa = lane < nl && (r == 1 ? fin_accept1(F, p, u0 + lane, ref0) : fin_accept2(F, p, u0 + lane, ref0));
-        const unsigned long long spec = __ballot(sa); // bit i: unit u0 + i against the chunk's starting reference
+    for (int u0 = 0; u0 < P.n; u0 += FIN_CH) {
+        const int                nl = min(FIN_CH, P.n - u0);
+        const unsigned long long mv = lane < nl ? M[u0 + lane] : 0ull;
+        const int                ref0 = ref; // the chunk's units against the chain's reference at its start
+        const bool sa = ref0 >= 0 && lane < nl && (r == 1 ? fin_accept1(F, p, u0 + lane, ref0) : fin_accept2(F, p, u0 + lane, ref0));
+        const unsigned long long spec = __ballot(sa);
+        int                      pv = 0;
         for (int i = 0; i < nl; i++) {
-            const int  u = u0 + i;
-            const bool a = ref == ref0 ? (spec >> i) & 1 : (lane_u64(mv, i) >> (u - 1 - ref)) & 1; // u - 1 - ref < 63
-            if (lane == 0) path[u] = (int32_t)a | ((ref + 1) << 2);
+            const int u = u0 + i, k = ref < 0 ? FIN_K1 : u - 1 - ref;
+            bool      a;
+            if (ref < 0 || k < F.wtab) a = (lane_u64(mv, i) >> k) & 1; // bit FIN_K1: the default
+            else if (ref == ref0) a = (spec >> i) & 1;
+            else a = r == 1 ? fin_accept1(F, p, u, ref) : fin_accept2(F, p, u, ref);
+            // uniform (every lane takes the same decision): a scalar, so the chain's branches are scalar branches
+            a = __builtin_amdgcn_readfirstlane((int)a) != 0;
+            if (lane == i) pv = (int)a | ((ref + 1) << 2);
             if (a) ref = u;
         }
+        if (lane < nl) path[u0 + lane] = pv;
     }
 }
 
-// the switchable chain of plane p: path[2][u] / path[3][u] = choice | (Wiener / self-guided ref + 1) << 2.  The cost
-// tables of FIN_CH units are staged in the wave's LDS (lc1 / lc2: [FIN_CH][64], lc0 / s1 / s2: [FIN_CH])
-__device__ void fin_walk3(const FinArgs &F, int p, int lane, double *lc0, double *lc1, double *lc2, double *s1, double *s2) {
+// the switchable chain of plane p: path[2][u] / path[3][u] = choice | (Wiener / self-guided ref + 1) << 2.  lb1 / lb2:
+// the wave's LDS for the chunk's coefficient bits [FIN_CH][64]
+__device__ void fin_walk3(const FinArgs &F, int p, int lane, uint8_t *lb1, uint8_t *lb2, const double *rate1,
+                          const double *rate2) {
     const FinPlane &P  = F.pl[p];
     const int32_t  *d1 = F.path + F.pl[P.own1 ? p : 0].base, *d2 = F.path + F.nrec + F.pl[P.own2 ? p : 0].base;
     int32_t        *pw = F.path + 2 * (size_t)F.nrec + P.base, *ps = F.path + 3 * (size_t)F.nrec + P.base;
     int             rw = -1, rs = -1;
     for (int u0 = 0; u0 < P.n; u0 += FIN_CH) {
-        const int nl = min(FIN_CH, P.n - u0), rw0 = rw, rs0 = rs;
-        for (int i = 0; i < nl; i++) {
-            const size_t row = (size_t)(P.base + u0 + i) * 64 + lane;
-            lc1[i * 64 + lane] = F.c1[row], lc2[i * 64 + lane] = F.c2[row];
+        const int nl = min(FIN_CH, P.n - u0);
+        const unsigned long long tc0 = F.clk && p == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+        // the chunk's bit rows (64 B per unit and table), 16-B pieces; then per lane its unit's cost terms
+        for (int q = lane; q < nl * 4; q += 64) {
+            const size_t row = (size_t)(P.base + u0 + (q >> 2)) * 64;
+            ((uint4 *)lb1)[q] = ((const uint4 *)(F.b1 + row))[q & 3];
+            ((uint4 *)lb2)[q] = ((const uint4 *)(F.b2 + row))[q & 3];
         }
-        if (lane < nl) lc0[lane] = F.c0[P.base + u0 + lane];
-        // the chunk's units against the chain's starting references (lanes 0..15 Wiener, 32..47 self-guided)
-        if (lane < nl) s1[lane] = fin_c1(F, p, u0 + lane, rw0);
-        else if (lane >= 32 && lane - 32 < nl) s2[lane - 32] = fin_c2(F, p, u0 + lane - 32, rs0);
-        const int a1v = lane < nl ? d1[u0 + lane] & 1 : 0, a2v = lane < nl ? d2[u0 + lane] & 1 : 0;
+        const int rw0 = rw, rs0 = rs; // the chunk's units against the chain's references at its start (far ones)
+        double    c0v = 0, s1v = 0, s2v = 0, f1v = 0, f2v = 0;
+        int       a1v = 0, a2v = 0;
+        if (lane < nl) {
+            const int u = u0 + lane;
+            c0v = fin_c0(F, p, u);
+            s1v = (double)fin_w(F, p, u).sse[1] * (1 << 7); // rdcost's second addend
+            s2v = (double)fin_s(F, p, u).sse[2] * (1 << 7);
+            a1v = d1[u] & 1, a2v = d2[u] & 1;
+            if (rw0 >= 0) f1v = fin_c1(F, p, u, rw0);
+            if (rs0 >= 0) f2v = fin_c2(F, p, u, rs0);
+        }
         __builtin_amdgcn_wave_barrier(); // the wave's LDS stores before its loads (in order within a wave)
+        unsigned long long tc1 = 0;
+        if (F.clk && p == 0) { // diagnostics: luma's chunk preparation / step loop
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            tc1 = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) F.clk[5] += tc1 - tc0, F.clk[7] += 1;
+        }
+        int qw = 0, qs = 0;
         for (int i = 0; i < nl; i++) {
-            const int    u  = u0 + i;
-            const bool   a1 = __builtin_amdgcn_readlane(a1v, i) != 0, a2 = __builtin_amdgcn_readlane(a2v, i) != 0;
-            const double c1 = rw == rw0 ? s1[i] : lc1[i * 64 + (u - 1 - rw)]; // a reference inside the chunk
-            const double c2 = rs == rs0 ? s2[i] : lc2[i * 64 + (u - 1 - rs)];
-            const int    bt = fin_pick(lc0[i], c1, c2, a1, a2);
-            if (lane == 0) pw[u] = bt | ((rw + 1) << 2), ps[u] = bt | ((rs + 1) << 2);
+            const int  u  = u0 + i;
+            const bool a1 = __builtin_amdgcn_readlane(a1v, i) != 0, a2 = __builtin_amdgcn_readlane(a2v, i) != 0;
+            const int  kw = rw < 0 ? FIN_K1 : u - 1 - rw, ks = rs < 0 ? FIN_K1 : u - 1 - rs;
+            // the rate terms of all 256 coefficient-bit counts are tabulated (rate1 / rate2): two dependent LDS reads
+            const double c1 = rw < 0 || kw < F.wtab ? rate1[lb1[i * 64 + kw]] + lane_f64(s1v, i)
+                            : rw == rw0             ? lane_f64(f1v, i)
+                                                    : fin_c1(F, p, u, rw);
+            const double c2 = rs < 0 || ks < F.wtab ? rate2[lb2[i * 64 + ks]] + lane_f64(s2v, i)
+                            : rs == rs0             ? lane_f64(f2v, i)
+                                                    : fin_c2(F, p, u, rs);
+            // uniform: a scalar (otherwise the chain's references live in VGPRs and every branch on them is exec-masked)
+            const int    bt = __builtin_amdgcn_readfirstlane(fin_pick(lane_f64(c0v, i), c1, c2, a1, a2));
+            if (lane == i) qw = bt | ((rw + 1) << 2), qs = bt | ((rs + 1) << 2);
             if (bt == 1) rw = u;
             if (bt == 2) rs = u;
         }
-        __builtin_amdgcn_wave_barrier();
+        if (F.clk && p == 0 && lane == 0) F.clk[6] += __builtin_amdgcn_s_memrealtime() - tc1;
+        if (lane < nl) pw[u0 + lane] = qw, ps[u0 + lane] = qs;
+        __builtin_amdgcn_wave_barrier(); // this chunk's LDS reads before the next chunk's stores
     }
 }
 
-constexpr int FIN_NT = 1024; // the walk kernel's lanes: three walking waves, then all of them for the per-unit sums
+constexpr int FIN_NT = 1024; // the walk kernel's lanes: six / three walking waves, then all of them for the sums
 __global__ __launch_bounds__(FIN_NT) void lr_fin_walk_kernel(const FinArgs F) {
     __shared__ unsigned long long acc[3][4][2]; // per plane and pass: sse, bits
     __shared__ int32_t            ft[3];
-    __shared__ double             lc[3][FIN_CH * (2 * 64 + 3)]; // fin_walk3's staging, per wave
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    __shared__ __attribute__((aligned(16))) uint8_t lb[3][2][FIN_CH * 64]; // fin_walk3's staging, per wave
+    __shared__ double rate[2][256]; // fin_rate of the switchable Wiener / self-guided costs for every bit count < 2^8
+    // the wave index through readfirstlane: the compiler then knows each walk's plane, unit count and loop bounds are
+    // wave-uniform, and keeps the chains' references in SGPRs with scalar branches (from threadIdx.x >> 6 it treated
+    // the loops as divergent and every step as exec-masked vector code)
+    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     if (tid < 24) (&acc[0][0][0])[tid] = 0;
-    if (F.clk && tid == 0) F.clk[0] = __builtin_amdgcn_s_memrealtime();
-    // the r = 1 / 2 chains (wave w: plane w; independent of each other), then the switchable chains (which read the
+    if (F.clk && tid == 0) F.clk[0] = __builtin_amdgcn_s_memrealtime(), F.clk[5] = F.clk[6] = F.clk[7] = 0;
+    if (tid < 512) rate[tid >> 8][tid & 255] = fin_rate(F.rdmult, F.sw[1 + (tid >> 8)], tid & 255); // read after the barrier
+    // the r = 1 / 2 chains (wave 2 p + r - 1: independent of each other), then the switchable chains (which read the
     // r = 1 / 2 outcomes, luma's for a type chroma does not search)
-    if (wv < F.nplanes)
-        for (int r = 1; r <= 2; r++)
-            if (F.pl[wv].run[r]) fin_walk12(F, wv, r, lane);
+    if (wv < 2 * F.nplanes && F.pl[wv >> 1].run[1 + (wv & 1)]) fin_walk12(F, wv >> 1, 1 + (wv & 1), lane);
     __syncthreads();
     if (F.clk && tid == 0) F.clk[1] = __builtin_amdgcn_s_memrealtime();
-    if (wv < F.nplanes && F.pl[wv].run[3])
-        fin_walk3(F, wv, lane, lc[wv], lc[wv] + FIN_CH, lc[wv] + FIN_CH + FIN_CH * 64, lc[wv] + FIN_CH + 2 * FIN_CH * 64,
-                  lc[wv] + 2 * FIN_CH + 2 * FIN_CH * 64);
+    if (wv < F.nplanes && F.pl[wv].run[3]) fin_walk3(F, wv, lane, lb[wv][0], lb[wv][1], rate[0], rate[1]);
     __syncthreads();
     if (F.clk && tid == 0) F.clk[2] = __builtin_amdgcn_s_memrealtime();
-    // the rate and distortion of every unit on each pass's path, summed per (plane, pass)
-    for (int p = 0; p < F.nplanes; p++) {
+    // the rate and distortion of every unit on each pass's path, summed per (plane, pass): one pass over the items of
+    // all planes (item i: plane p, pass r, unit u)
+    const int n0 = 4 * F.pl[0].n, n1 = n0 + 4 * F.pl[1].n, nall = F.nplanes > 2 ? n1 + 4 * F.pl[2].n : F.nplanes > 1 ? n1 : n0;
+    for (int i = tid; i < nall; i += FIN_NT) {
+        const int p = i < n0 ? 0 : i < n1 ? 1 : 2, j = i - (p == 0 ? 0 : p == 1 ? n0 : n1);
         const FinPlane &P = F.pl[p];
-        for (int i = tid; i < 4 * P.n; i += FIN_NT) {
-            const int r = i / P.n, u = i - r * P.n;
-            if (!P.run[r]) continue;
-            const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
-            int64_t                   sse = 0, bits = 0;
-            if (r == 0) {
-                sse = R.sse[0];
-            } else if (r <= 2) {
-                const int32_t q = F.path[(size_t)(r - 1) * F.nrec + P.base + u];
-                const int     ref = (q >> 2) - 1;
-                if (!(q & 1)) {
-                    sse = R.sse[0], bits = r == 1 ? F.wn[0] : F.sg[0];
-                } else if (r == 1) {
-                    const SvtGpuRestUnit rw = ref < 0 ? default_wiener() : fin_rec(F, p, ref).wiener;
-                    sse = R.sse[1], bits = F.wn[1] + ((int64_t)wiener_bits(P.win1, R.wiener, rw) << 9);
-                } else {
-                    const SvtGpuRestUnit rs = ref < 0 ? default_sgrproj() : fin_rec(F, p, ref).sgrproj;
-                    sse = R.sse[2], bits = F.sg[1] + ((int64_t)sgrproj_bits(R.sgrproj, rs) << 9);
-                }
+        const int r = j / P.n, u = j - r * P.n;
+        if (!P.run[r]) continue;
+        const SvtGpuLrUnitSearch &R = fin_rec(F, p, u);
+        int64_t                   sse = 0, bits = 0;
+        if (r == 0) {
+            sse = R.sse[0];
+        } else if (r <= 2) {
+            const int32_t q = F.path[(size_t)(r - 1) * F.nrec + P.base + u];
+            const int     ref = (q >> 2) - 1;
+            if (!(q & 1)) {
+                sse = R.sse[0], bits = r == 1 ? F.wn[0] : F.sg[0];
+            } else if (r == 1) {
+                const SvtGpuRestUnit rw = ref < 0 ? default_wiener() : fin_rec(F, p, ref).wiener;
+                sse = R.sse[1], bits = F.wn[1] + ((int64_t)wiener_bits(P.win1, R.wiener, rw) << 9);
             } else {
-                const int32_t qw = F.path[2 * (size_t)F.nrec + P.base + u], qs = F.path[3 * (size_t)F.nrec + P.base + u];
-                const int     bt = qw & 3, rw = (qw >> 2) - 1, rs = (qs >> 2) - 1;
-                int64_t       cp = 0;
-                if (bt == 1) {
-                    const SvtGpuRestUnit r0 = rw < 0 ? default_wiener() : fin_w(F, p, rw).wiener;
-                    cp = wiener_bits(p == 0 ? 7 : 5, fin_w(F, p, u).wiener, r0), sse = fin_w(F, p, u).sse[1];
-                } else if (bt == 2) {
-                    const SvtGpuRestUnit r0 = rs < 0 ? default_sgrproj() : fin_s(F, p, rs).sgrproj;
-                    cp = sgrproj_bits(fin_s(F, p, u).sgrproj, r0), sse = fin_s(F, p, u).sse[2];
-                } else {
-                    sse = R.sse[0];
-                }
-                bits = F.sw[bt] + (cp << 9);
+                const SvtGpuRestUnit rs = ref < 0 ? default_sgrproj() : fin_rec(F, p, ref).sgrproj;
+                sse = R.sse[2], bits = F.sg[1] + ((int64_t)sgrproj_bits(R.sgrproj, rs) << 9);
             }
-            atomicAdd(&acc[p][r][0], (unsigned long long)sse);
-            atomicAdd(&acc[p][r][1], (unsigned long long)bits);
+        } else {
+            const int32_t qw = F.path[2 * (size_t)F.nrec + P.base + u], qs = F.path[3 * (size_t)F.nrec + P.base + u];
+            const int     bt = qw & 3, rw = (qw >> 2) - 1, rs = (qs >> 2) - 1;
+            int64_t       cp = 0;
+            if (bt == 1) {
+                const SvtGpuRestUnit r0 = rw < 0 ? default_wiener() : fin_w(F, p, rw).wiener;
+                cp = wiener_bits(p == 0 ? 7 : 5, fin_w(F, p, u).wiener, r0), sse = fin_w(F, p, u).sse[1];
+            } else if (bt == 2) {
+                const SvtGpuRestUnit r0 = rs < 0 ? default_sgrproj() : fin_s(F, p, rs).sgrproj;
+                cp = sgrproj_bits(fin_s(F, p, u).sgrproj, r0), sse = fin_s(F, p, u).sse[2];
+            } else {
+                sse = R.sse[0];
+            }
+            bits = F.sw[bt] + (cp << 9);
         }
+        atomicAdd(&acc[p][r][0], (unsigned long long)sse);
+        atomicAdd(&acc[p][r][1], (unsigned long long)bits);
     }
     __syncthreads();
     if (F.clk && tid == 0) F.clk[3] = __builtin_amdgcn_s_memrealtime();
@@ -2703,20 +2763,20 @@ __global__ __launch_bounds__(FIN_NT) void lr_fin_walk_kernel(const FinArgs F) {
     }
     __syncthreads();
     if (F.clk && tid == 0) F.clk[4] = __builtin_amdgcn_s_memrealtime();
-    // copy_unit_info into the state's units (every plane; zero where the frame type is NONE)
-    for (int p = 0; p < 3; p++) {
+    // copy_unit_info into the state's units (every plane; zero where the frame type is NONE): one pass over all units
+    const int m0 = F.pl[0].n, m1 = m0 + F.pl[1].n, mall = m1 + F.pl[2].n;
+    for (int i = tid; i < mall; i += FIN_NT) {
+        const int       p = i < m0 ? 0 : i < m1 ? 1 : 2, u = i - (p == 0 ? 0 : p == 1 ? m0 : m1);
         const FinPlane &P = F.pl[p];
-        for (int u = tid; u < P.n; u += FIN_NT) {
-            SvtGpuRestUnit o;
-            memset(&o, 0, sizeof o);
-            if (p < F.nplanes && ft[p]) {
-                const int32_t q = F.path[(size_t)(ft[p] - 1) * F.nrec + P.base + u];
-                const int     t = ft[p] == 3 ? (q & 3) : (q & 1) ? ft[p] : 0;
-                o               = t == 1 ? fin_w(F, p, u).wiener : fin_s(F, p, u).sgrproj;
-                o.type          = t;
-            }
-            F.units[P.base + u] = o;
+        SvtGpuRestUnit  o;
+        memset(&o, 0, sizeof o);
+        if (p < F.nplanes && ft[p]) {
+            const int32_t q = F.path[(size_t)(ft[p] - 1) * F.nrec + P.base + u];
+            const int     t = ft[p] == 3 ? (q & 3) : (q & 1) ? ft[p] : 0;
+            o               = t == 1 ? fin_w(F, p, u).wiener : fin_s(F, p, u).sgrproj;
+            o.type          = t;
         }
+        F.units[P.base + u] = o;
     }
     if (tid < FIN_OUT) {
         const int32_t v = tid < 3   ? ft[tid]
@@ -3058,8 +3118,8 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     const size_t res_span = dc.off - o_sse; // the (unit, ep) descents stay on the device: the best ep's come back
     const size_t o_sds = dc(sizeof(Descent) * npairs);
     const size_t o_part = dc(8 * part_elems), o_mh = dc(8 * mh_elems);
-    const size_t o_m1 = dc(8 * (size_t)nrec), o_m2 = dc(8 * (size_t)nrec), o_c0 = dc(8 * (size_t)nrec),
-                 o_c1 = dc(8 * 64 * (size_t)nrec), o_c2 = dc(8 * 64 * (size_t)nrec), o_fout = dc(4 * FIN_OUT);
+    const size_t o_m1 = dc(8 * (size_t)nrec), o_m2 = dc(8 * (size_t)nrec), o_b1 = dc(64 * (size_t)nrec),
+                 o_b2 = dc(64 * (size_t)nrec), o_fout = dc(4 * FIN_OUT);
     // the uncached arena: the SSE exchange words of the Wiener units cut into row parts (wiener_res_kernel)
     Carver       qc;
     const size_t q_wrx = qc(16 * (size_t)n_wr), q_srx = qc(128 * (size_t)n_sr);
@@ -3324,7 +3384,7 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         for (int k = 0; k < 2; k++) F.wn[k] = c->wiener_restore_cost[k], F.sg[k] = c->sgrproj_restore_cost[k];
         F.rec = (const SvtGpuLrUnitSearch *)dp(o_rec);
         F.m1 = (unsigned long long *)dp(o_m1), F.m2 = (unsigned long long *)dp(o_m2);
-        F.c0 = (double *)dp(o_c0), F.c1 = (double *)dp(o_c1), F.c2 = (double *)dp(o_c2);
+        F.b1 = (uint8_t *)dp(o_b1), F.b2 = (uint8_t *)dp(o_b2);
         F.path = (int32_t *)dp(o_path), F.units = s->d_units[0];
         F.out = (int32_t *)dp(o_fout), F.out_host = s->h_fout_dev;
         F.wstat = n_wn ? (const int32_t *)dp(o_wstat) : nullptr, F.sstat = n_sr ? (const int32_t *)dp(o_sstat) : nullptr;
@@ -3333,6 +3393,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         static unsigned long long *d_clk = nullptr;
         if (fin_clk && !d_clk) HIP_TRY(hipMalloc(&d_clk, 64));
         F.clk = fin_clk ? d_clk : nullptr;
+        static const int fin_win = [] {
+            const char *e = std::getenv("SVTGPU_LR_FIN_WIN");
+            return e ? std::max(1, std::min(FIN_K1, std::atoi(e))) : FIN_K1;
+        }();
+        F.wtab = fin_win;
         if (tables) {
             hipLaunchKernelGGL(lr_fin_tables_kernel, dim3(F.pl[nplanes - 1].base + F.pl[nplanes - 1].n), dim3(64), 0,
                                st, F);
@@ -3354,8 +3419,10 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
         if (F.clk) {
             unsigned long long v[8];
             HIP_TRY(hipMemcpy(v, F.clk, 64, hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "lr_fin_walk us: r1/r2 walks %.1f, switchable walks %.1f, sums %.1f, types %.1f\n",
-                         (v[1] - v[0]) * 0.01, (v[2] - v[1]) * 0.01, (v[3] - v[2]) * 0.01, (v[4] - v[3]) * 0.01);
+            std::fprintf(stderr, "lr_fin_walk us: r1/r2 walks %.1f, switchable walks %.1f (luma: %llu chunks, preparation "
+                                 "%.1f, steps %.1f), sums %.1f, types %.1f\n",
+                         (v[1] - v[0]) * 0.01, (v[2] - v[1]) * 0.01, v[7], v[5] * 0.01, v[6] * 0.01, (v[3] - v[2]) * 0.01,
+                         (v[4] - v[3]) * 0.01);
         }
         if (search_out) {
             const SvtGpuLrUnitSearch *hr = (const SvtGpuLrUnitSearch *)hp(h_rec);

@@ -311,3 +311,48 @@ def test_lr_search_async_equals_sync(ctx, case):
     a, b = O1.download(), O2.download()
     for p in range(3):
         assert np.array_equal(a[p], b[p]), (c["name"], p)
+
+
+FIN_WIN_CHILD = r"""
+import sys
+sys.path[:0] = [%r, %r, %r, %r]
+import torch
+if torch.cuda.is_available():
+    torch.cuda.init()
+import numpy as np
+import svtgpu
+import lr_cases as lc
+import pipeline_run as prun
+ctx = svtgpu.Context(0)
+for c in lc.search_cases():
+    h, w = c["rec"][0].shape
+    pad = lambda planes, n: [np.pad(p, ((0, (-p.shape[0]) %% (8 if i == 0 else 4)),
+                                        (0, (-p.shape[1]) %% (8 if i == 0 else 4))), mode="edge")
+                             for i, p in enumerate(planes)]
+    rec8, src8 = pad(c["rec"], 3), pad(c["src"], 4)
+    R, S = (svtgpu.Frame(ctx, rec8[0].shape[1], rec8[0].shape[0], c["bd"]) for _ in range(2))
+    R.upload(rec8), S.upload(src8)
+    st = svtgpu.LrState(ctx, w, h, c["unit_size"])
+    ft, recs = st.search(R, S, c["ctrls"], records=True)
+    lc.compare_search(ft, c["units"], recs, c)
+for case in %r:
+    prun.check(case, prun.run_gpu(case, ctx, async_=True), "fin window")
+print("ok")
+"""
+
+
+@pytest.mark.timeout(600)
+def test_lr_finish_walk_evaluates_far_references():
+    """The device RD finish's walks read a unit's decision / coefficient bits from the tables for references up to 63
+    units back and evaluate the others at the step.  With the window cut to one unit (SVTGPU_LR_FIN_WIN=1, in a child
+    process: the switch is read once) nearly every step takes the evaluation path; the reference's records, frame types
+    and restored planes must not change (every LR golden case, the 1080p 8-bit and 4K 10-bit pipeline goldens)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = FIN_WIN_CHILD % (root, os.path.join(root, "svt-av1_pro-anchor-v2.1.0-_amd"), os.path.join(root, "oracle"),
+                            os.path.join(root, "tests"), ("mini10", "c1_1080p8", "c3_4k10"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=550,
+                       env=dict(os.environ, SVTGPU_LR_FIN_WIN="1"))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
