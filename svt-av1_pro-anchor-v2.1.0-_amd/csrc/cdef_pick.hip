@@ -321,6 +321,8 @@ struct PersistArgs {
     uint64_t           *best;   // [4]
     int32_t            *status; // bit 0: a poll gave up
     unsigned long long *stat;   // diagnostics (SVTGPU_PICK_STATS) or null: ticks of compute, exchange 1, exchange 2
+    const int32_t      *skip;   // the asynchronous pick's fallback: nonzero = every chain settled at the check, exit
+    const uint32_t     *dep;    // ... its epoch, counted on the device (the check raises it when this launch will run)
 };
 
 // chain c's call at step s (the host schedule of the launch path): nb_sel = selection size of this call (-1: the
@@ -392,7 +394,8 @@ __global__ void __launch_bounds__(NT, 4) sod_persist_kernel(const PersistArgs A)
     const int f0 = ci * A.chunk, end = A.end_gi;
     const int nfb  = max(0, min(*A.count - f0, A.chunk));
     const int wide = *A.wide;
-    const unsigned long long ep = (unsigned long long)(A.epoch & 3) << 62;
+    if (A.skip && *A.skip) return; // uniform: the settle check finished the pick (svtgpu_cdef_pick_async)
+    const unsigned long long ep = (unsigned long long)((A.dep ? *A.dep : A.epoch) & 3) << 62;
     unsigned long long       tk[3] = {0, 0, 0}, t0 = 0;
     if (t == 0) s_fail = 0;
     // the chunk into LDS, once (narrow: the low words, entry e of FB f at m32[f * 128 + e])
@@ -535,8 +538,10 @@ struct SettleOut {
     int32_t settled, step, seq; // seq: the asynchronous pick that wrote it (its next T is read without a wait)
 };
 // flag (device memory, asynchronous pick): the settled word the later steps read
+// dep: the persistent fallback's epoch (asynchronous pick), raised when the check finds a chain unsettled -- only then
+// does the fallback launch run, so its exchange words' epochs differ from those of its last four real runs
 __global__ void pick_settle_kernel(const int32_t *lev, const uint64_t *val, int32_t *fin, uint64_t *best, int T,
-                                   SettleOut *out, int32_t *flag, int seq) {
+                                   SettleOut *out, int32_t *flag, int seq, uint32_t *dep) {
     __shared__ int s_ok[MAX_CHAINS], s_at[MAX_CHAINS];
     const int c = threadIdx.x;
     if (c < MAX_CHAINS) {
@@ -567,6 +572,7 @@ __global__ void pick_settle_kernel(const int32_t *lev, const uint64_t *val, int3
     if (c == 0) {
         const int ok = s_ok[0] && s_ok[1] && s_ok[2] && s_ok[3];
         if (flag) *flag = ok;
+        if (dep && !ok) *dep += 1;
         out->settled = ok;
         out->step    = max(max(s_at[0], s_at[1]), max(s_at[2], s_at[3]));
         if (seq) {
@@ -734,6 +740,8 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         P.best     = A.best;
         P.status   = d_status;
         P.stat     = stat;
+        P.skip     = nullptr;
+        P.dep      = nullptr;
         hipLaunchKernelGGL(sod_persist_kernel, dim3(PS_GRID), dim3(NT), 0, st, P);
     }
     // the settle checkpoint (SVTGPU_PICK_SETTLE=0: off): after step T one small kernel checks whether every chain has
@@ -766,7 +774,18 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
     const bool check = settle_on && s->pick_skip == 0;
     if (s->pick_skip > 0 && --s->pick_skip == 0) s->pick_settle = 24;
     const int T = check ? std::min(std::max(s->pick_settle, 16), NSTEPS) : NSTEPS;
-    for (int step = 0; step <= NSTEPS && !persist; step++) {
+    // asynchronous: after the check no further step is launched -- when a chain has not settled, one persistent launch
+    // (sod_persist_kernel, which returns at once when the check's flag says settled) recomputes the whole pick.  The
+    // flag-only step launches it replaces each needed 256 workgroup slots, which at four frames in flight waited for
+    // CUs held by other frames' kernels.  Frames with more FBs than its chunks hold keep the flagged launches.
+    const char *afb         = std::getenv("SVTGPU_PICK_ASYNC_FALLBACK"); // =steps: the flagged step launches (A/B)
+    const bool  async_steps = afb && !std::strcmp(afb, "steps");
+    const bool pfb = async_ && !persist && !async_steps && T < NSTEPS && nfb <= PS_NCH * PS_CH;
+    if (pfb && s->pick_xch_end != end) { // words of a different strength count could carry a current tag
+        HIP_TRY(hipMemsetAsync(s->d_pick_xch, 0, SVTGPU_PICK_XCH_BYTES, st));
+        s->pick_xch_end = end;
+    }
+    for (int step = 0; step <= NSTEPS && !persist && !(pfb && step > T); step++) {
         int na = 0;
         for (int c = 0; c < MAX_CHAINS; c++) {
             const int nb = 1 << c, len = 5 * nb; // nb calls + 4*nb refinements
@@ -792,11 +811,13 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         svtgpu_wgclk_end("sod_step", 4 * parts * na, st);
         if (step == T && T < NSTEPS && async_) { // the check in stream order; the later steps read its flag
             hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
-                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, d_flag, ++s->settle_seq);
+                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, d_flag, ++s->settle_seq,
+                               pfb ? (uint32_t *)((uint8_t *)s->d_apick + 8) : (uint32_t *)nullptr);
             HIP_TRY(hipGetLastError());
         } else if (step == T && T < NSTEPS) {
             hipLaunchKernelGGL(pick_settle_kernel, dim3(1), dim3(64), 0, st, (const int32_t *)A.lev,
-                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, (int32_t *)nullptr, 0);
+                               (const uint64_t *)A.val, A.fin, A.best, T, d_settle, (int32_t *)nullptr, 0,
+                               (uint32_t *)nullptr);
             HIP_TRY(hipGetLastError());
             if (int rc = svtgpu_comm_wait(s->comm, st)) return rc; // bounded behind the tables' exchange
             svtgpu_count_xfer(1, sizeof(SettleOut));
@@ -810,6 +831,26 @@ int svtgpu_cdef_pick_impl(SvtGpuCdefFrameState *s, const SvtGpuCdefControls *ctr
         }
     }
     HIP_TRY(hipGetLastError());
+    if (pfb) { // the fallback: the whole pick again, only when the check found a chain unsettled
+        PersistArgs P;
+        P.wmse     = wmse;
+        P.count    = d_count;
+        P.wide     = A.wide;
+        P.chunk    = std::max(1, (nfb + PS_NCH - 1) / PS_NCH);
+        P.fb_alloc = nfb;
+        P.end_gi   = end;
+        P.epoch    = 0;
+        P.part     = (unsigned long long *)s->d_pick_xch;
+        P.amin     = P.part + PS_NCH * 4 * 4096;
+        P.fin      = A.fin;
+        P.best     = A.best;
+        P.status   = d_status;
+        P.stat     = nullptr;
+        P.skip     = d_flag;
+        P.dep      = (const uint32_t *)((const uint8_t *)s->d_apick + 8);
+        hipLaunchKernelGGL(sod_persist_kernel, dim3(PS_GRID), dim3(NT), 0, st, P);
+        HIP_TRY(hipGetLastError());
+    }
     PickOut *h_out = (PickOut *)s->h_pick;
     static_assert(sizeof(PickOut) <= 512, "pick output slot");
     int8_t *host_fbs = fb_strength_out || async_ ? (int8_t *)(s->h_pick_dev + 512) : nullptr;

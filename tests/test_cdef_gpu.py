@@ -353,15 +353,18 @@ def test_cdef_pick_settled_chains_vs_oracle(ctx, monkeypatch, scale_hi):
     assert seen == {True, False}  # settled and unsettled chains both covered
 
 
-@pytest.mark.parametrize("persist", ["0", "1"])
-def test_cdef_pick_async_vs_oracle(ctx, monkeypatch, persist):
+@pytest.mark.parametrize("persist,fallback", [("0", "persist"), ("0", "steps"), ("1", "persist")])
+def test_cdef_pick_async_vs_oracle(ctx, monkeypatch, persist, fallback):
     """svtgpu_cdef_pick_async (no host wait: the settle check's outcome reaches the later steps through a device flag,
     the parameters stay on the device) on the settled / unsettled tables of the test above: svtgpu_cdef_read_params
     equals the oracle's pick on every seed, three picks in a row on one state (the checkpoint T then moves from the
     records the earlier picks left, read without a wait), and the apply from device parameters writes the same planes
-    as the apply with the host parameters."""
+    as the apply with the host parameters.  After the check the asynchronous pick launches either one persistent
+    launch that recomputes the pick when a chain has not settled (default) or the remaining steps, each returning at
+    once when every chain has (SVTGPU_PICK_ASYNC_FALLBACK=steps); the unsettled seeds exercise both."""
     import torch
     monkeypatch.setenv("SVTGPU_PICK_PERSIST", persist)
+    monkeypatch.setenv("SVTGPU_PICK_ASYNC_FALLBACK", fallback)
     w, h, q, lam = 1920, 1080, 128, 60000
     ctrls = svtgpu.cdef_controls(1)
     st = svtgpu.CdefState(ctx, w, h)
