@@ -131,7 +131,7 @@ def parse():
     ap.add_argument("--cdef-level", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no device-clock timing inside the LR search")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r05", "pmc", "kernels.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r06", "pmc", "kernels.json"),
                     help="per-launch traffic / VALU counters from scripts/pmc_traffic.sh (PMC passes cannot run inside "
                          "the bench)")
     ap.add_argument("--cpu-grid", default="4x4", help="crops of the frame timed on the host CPU (one per thread)")
