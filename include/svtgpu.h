@@ -226,6 +226,13 @@ int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], 
  * 128x128 CDEF area is cut (svtgpu_tile_plan = sb_size 64). */
 int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t unit_size[3], int32_t sb_size, int32_t gx,
                         int32_t gy, int32_t rank, SvtGpuTilePlan *out);
+/* A picture whose crop size (frm_size.frame_width x frame_height, the area loop restoration covers) is below its
+ * 8-aligned coded size (width x height: the deblocking / CDEF frames, coded - crop < 8 each way): the restoration
+ * units tile the crop (chroma rounded up), the tiles keep their edges on the luma unit grid and the last tile runs to
+ * the coded edge.  Each rank's LR state is created with the crop size and its DLF state told the crop
+ * (svtgpu_dlf_set_crop), as on one GPU.  svtgpu_tile_plan_sb = crop equal to the coded size. */
+int svtgpu_tile_plan_crop(int32_t width, int32_t height, int32_t crop_w, int32_t crop_h, const int32_t unit_size[3],
+                          int32_t sb_size, int32_t gx, int32_t gy, int32_t rank, SvtGpuTilePlan *out);
 
 /* ---------------------------------------------------------------------------------------------
  * CDEF — per-block RTCD shims (host pointers, synchronous)

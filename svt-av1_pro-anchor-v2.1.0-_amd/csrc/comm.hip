@@ -371,10 +371,16 @@ void grow(int32_t *r, int a, int w, int h) {
 }
 } // namespace
 
-extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t unit_size[3], int32_t sb_size,
-                                   int32_t gx, int32_t gy, int32_t rank, SvtGpuTilePlan *out) {
+// A picture whose crop size (the restored area, frm_size.frame_width x frame_height) is smaller than its 8-aligned coded
+// size: the deblocking and CDEF frames are the coded size, the restoration units tile the crop (chroma rounded up, the
+// reference's crop_widths).  The tiles' edges stay on the luma unit grid; the last tile column / row runs to the coded
+// edge, the last unit to the crop edge.
+extern "C" int svtgpu_tile_plan_crop(int32_t width, int32_t height, int32_t crop_w, int32_t crop_h,
+                                     const int32_t unit_size[3], int32_t sb_size, int32_t gx, int32_t gy, int32_t rank,
+                                     SvtGpuTilePlan *out) {
     if (!unit_size || !out || width <= 0 || height <= 0 || (width & 7) || (height & 7) || gx < 1 || gy < 1 ||
-        rank < 0 || rank >= gx * gy || (sb_size != 64 && sb_size != 128))
+        rank < 0 || rank >= gx * gy || (sb_size != 64 && sb_size != 128) || crop_w <= 0 || crop_h <= 0 ||
+        crop_w > width || crop_h > height || width - crop_w >= 8 || height - crop_h >= 8)
         return SVTGPU_ERR_INVALID_ARG;
     for (int p = 0; p < 3; p++)
         if (unit_size[p] < (p ? 32 : 64) || unit_size[p] > 256 || (unit_size[p] & (unit_size[p] - 1)))
@@ -382,7 +388,7 @@ extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t 
     SvtGpuTilePlan o;
     std::memset(&o, 0, sizeof o);
     const int tx = rank % gx, ty = rank / gx, U = unit_size[0];
-    const int nux = units_of(U, width), nuy = units_of(U, height);
+    const int nux = units_of(U, crop_w), nuy = units_of(U, crop_h);
     // tile edges on the unit grid and on the superblock grid: with 64-sample units in a SB128 picture the units go in
     // pairs, so no 128x128 CDEF area (searched as one, EbCdefProcess.c:193-196) is cut
     const int k = std::max(1, sb_size / U), gux = (nux + k - 1) / k, guy = (nuy + k - 1) / k;
@@ -395,7 +401,7 @@ extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t 
     o.fb_rect[0] = o.tile[0] / 64, o.fb_rect[1] = o.tile[1] / 64;
     o.fb_rect[2] = (o.tile[2] + 63) / 64, o.fb_rect[3] = (o.tile[3] + 63) / 64;
     for (int p = 0; p < 3; p++) {
-        const int pw = p ? width / 2 : width, ph = p ? height / 2 : height, up = unit_size[p], off = p ? 4 : 8;
+        const int pw = p ? (crop_w + 1) / 2 : crop_w, ph = p ? (crop_h + 1) / 2 : crop_h, up = unit_size[p], off = p ? 4 : 8;
         const int hx = units_of(up, pw), hy = units_of(up, ph);
         // the luma unit columns / rows when the plane's unit grid matches luma's (chroma units of half the luma size),
         // else an even split of the plane's own grid
@@ -428,6 +434,11 @@ extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t 
     std::memcpy(o.in_rect, d, sizeof d);
     *out = o;
     return SVTGPU_OK;
+}
+
+extern "C" int svtgpu_tile_plan_sb(int32_t width, int32_t height, const int32_t unit_size[3], int32_t sb_size,
+                                   int32_t gx, int32_t gy, int32_t rank, SvtGpuTilePlan *out) {
+    return svtgpu_tile_plan_crop(width, height, width, height, unit_size, sb_size, gx, gy, rank, out);
 }
 
 extern "C" int svtgpu_tile_plan(int32_t width, int32_t height, const int32_t unit_size[3], int32_t gx, int32_t gy,

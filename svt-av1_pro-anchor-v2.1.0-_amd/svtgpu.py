@@ -378,6 +378,7 @@ _SIGS = {
     "svtgpu_shim_calls": (ctypes.c_uint64, []),
     "svtgpu_tile_plan": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P]),
     "svtgpu_tile_plan_sb": (ctypes.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
+    "svtgpu_tile_plan_crop": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _I32, _I32, _I32, _I32, _P]),
     "svtgpu_dlf_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_dlf_set_crop": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
@@ -537,10 +538,16 @@ def tile_grid(n):
     return gx, n // gx
 
 
-def tile_plan(width, height, unit_size, gx, gy, rank, sb=64):
+def tile_plan(width, height, unit_size, gx, gy, rank, sb=64, crop=None):
+    """svtgpu_tile_plan_sb; crop=(w, h): a picture whose crop size is below the 8-aligned coded size width x height
+    (svtgpu_tile_plan_crop)."""
     us = np.ascontiguousarray(unit_size, np.int32)
     t = TilePlan()
-    check(lib().svtgpu_tile_plan_sb(width, height, ptr(us), sb, gx, gy, rank, ctypes.byref(t)))
+    if crop is None:
+        check(lib().svtgpu_tile_plan_sb(width, height, ptr(us), sb, gx, gy, rank, ctypes.byref(t)))
+    else:
+        check(lib().svtgpu_tile_plan_crop(width, height, int(crop[0]), int(crop[1]), ptr(us), sb, gx, gy, rank,
+                                          ctypes.byref(t)))
     return t
 
 

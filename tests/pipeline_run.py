@@ -408,3 +408,74 @@ def assemble_tiled(case, parts):
     return dict(src=src, rec=rec, mi=mi, lf=p0["lf"], dlf=full["dlf"], tables=p0["tables"], prm=prm, nb=p0["nb"],
                 fbs=p0["fbs"], applied=p0["applied"], cdef=full["cdef"], ft=p0["ft"], units=p0["units"],
                 recs=p0["recs"], lrc=lrc, lr=full["lr"])
+
+
+# --------------------------------------------------------------------------- a picture off the 8-sample grid, tiled
+def run_crop(c, crop, rank=0, world=1, comm=None, ctx=None, lam=60000):
+    """The whole path on a synthetic case dict `c` (pipeline_cases._case: w x h the 8-aligned coded size) whose crop
+    size `crop` = (w, h) is below it: the DLF state told the crop (svtgpu_dlf_set_crop), the CDEF on the coded frames,
+    the LR state at the crop size.  world > 1: this rank's part of the picture tiled with svtgpu_tile_plan_crop (the
+    rest of its input pictures poisoned).  Returns the decisions and the output planes (whole frames; a rank's are
+    valid inside its plan's rects)."""
+    import svtgpu
+    bd, w, h = c["bd"], c["w"], c["h"]
+    src, rec = pc.frame_pair(w, h, bd, c["seed"])
+    mi = pc.mode_info(c)
+    us = [c["us"][0], c["us"][1], c["us"][1]]
+    ctx = ctx or svtgpu.Context()
+    S, R, D, C, O = (svtgpu.Frame(ctx, w, h, bd) for _ in range(5))
+    plan = None
+    if world > 1:
+        plan = svtgpu.tile_plan(w, h, us, *svtgpu.tile_grid(world), rank, sb=c["sb"], crop=crop).rects()
+        rng = np.random.default_rng(17 + rank)
+        for F in (S, R):
+            F.upload([rng.integers(0, 1 << bd, size=F.plane_shape(p), dtype=np.uint16) for p in range(3)])
+        S.upload(src, rect=plan["in_rect"])
+        R.upload(rec, rect=plan["in_rect"])
+    else:
+        S.upload(src)
+        R.upload(rec)
+    dl = svtgpu.DlfState(ctx, w, h)
+    dl.set_crop(*crop)
+    dl.set_mode_info(mi)
+    if plan:
+        dl.set_tile(plan["tile"], plan["dlf_out"], comm)
+    lfp = gpu_dlf_pick(dl, R, S, c)
+    dl.filter_to(R, D, lfp)
+    st = svtgpu.CdefState(ctx, w, h)
+    st.set_block_mask(pc.cdef_mask(mi))
+    if plan:
+        st.set_tile(plan["fb_rect"], plan["cdef_out"], comm)
+    ctrls = svtgpu.cdef_controls(c["cdef_level"])
+    st.search(D, S, ctrls, c["q"])
+    prm, fbs = st.pick(ctrls, c["q"], lam)
+    st.apply(D, C, prm)
+    lr = svtgpu.LrState(ctx, crop[0], crop[1], us)
+    if plan:
+        lr.set_tile(plan["lr_units"], plan["lr_out"], comm)
+    lrc = svtgpu.lr_controls(c["wn_level"], c["sg_level"], c["rdmult"], c["sw"], c["wc"], c["sc"])
+    ft, recs = lr.search(C, S, lrc, records=True)
+    lr.apply(D, C, O, ft)
+    ctx.synchronize()
+    out = dict(plan=plan, lf=tuple(lfp.levels()), prm=prm.as_tuple(), fbs=fbs, ft=list(ft), recs=recs,
+               dlf=D.download(), cdef=C.download(), lr=O.download())
+    for x in (S, R, D, C, O, dl, st, lr):
+        x.close()
+    return out
+
+
+def compare_crop_parts(single, parts):
+    """Every rank's decisions equal the single-GPU run's, and its outputs inside its plan's rects (the DLF output over
+    its tile, the CDEF and LR outputs over its LR units' samples) equal the single-GPU planes."""
+    for q in parts:
+        assert q["lf"] == single["lf"] and q["prm"] == single["prm"] and q["ft"] == single["ft"], (q["lf"], single["lf"])
+        assert np.array_equal(q["fbs"], single["fbs"])
+        for p in range(3):
+            assert q["recs"][p].tobytes() == single["recs"][p].tobytes(), p
+        t = q["plan"]["tile"]
+        tile3 = [t] + [[t[0] // 2, t[1] // 2, (t[2] + 1) // 2, (t[3] + 1) // 2]] * 2
+        for key, rects in (("dlf", tile3), ("cdef", q["plan"]["lr_out"]), ("lr", q["plan"]["lr_out"])):
+            for p, r in enumerate(rects):
+                a = q[key][p][r[1]:r[3], r[0]:r[2]]
+                b = single[key][p][r[1]:r[3], r[0]:r[2]]
+                assert np.array_equal(a, b), (key, p, r)

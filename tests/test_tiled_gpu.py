@@ -382,3 +382,98 @@ def test_cdef_rebind_tables_between_picks_sums_again():
         del mse_t, skip_t
     for x in (st, ref, comm, ctx):
         x.close()
+
+
+# a picture off the 8-sample grid tiled over the ranks (svtgpu_tile_plan_crop): coded size 8-aligned, crop below it
+CROP_CASES = {
+    2: [(dict(w=336, h=184, bd=10, q=150, us=(64, 32), mi=("random", 31, 0.3), seed=131), (330, 182))],
+    4: [(dict(w=1368, h=768, bd=10, q=170, us=(64, 32), mi=("random", 32, 0.3), seed=132), (1366, 766)),
+        (dict(w=640, h=368, bd=8, q=90, us=(64, 32), cdef_level=3, mi=("random", 33, 0.4), seed=133), (634, 362))],
+}
+
+
+def _crop_worker(rank, world, port, cases, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if torch.cuda.is_available():
+        torch.cuda.init()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pipeline_cases as pcs
+        import svtgpu
+
+        def allreduce(words):
+            dist.all_reduce(torch.from_numpy(words.view(np.int64)))
+
+        comm = svtgpu.Comm.host(world, rank, allreduce)
+        ctx = svtgpu.Context(0)
+        for i, (kw, crop) in enumerate(cases):
+            c = pcs._case(**kw)
+            part = prun.run_crop(c, crop, rank, world, comm, ctx)
+            parts = [None] * world
+            dist.all_gather_object(parts, part)
+            if rank == 0:
+                try:
+                    prun.compare_crop_parts(prun.run_crop(c, crop, ctx=ctx), parts)
+                    q.put((i, "ok"))
+                except AssertionError as e:
+                    q.put((i, "FAIL: %s" % str(e)[:2000]))
+        comm.close()
+    except BaseException as e:
+        q.put(("rank %d" % rank, "ERROR: %r" % e))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_ranks_one_gpu_crop_size(world):
+    """A picture whose crop size is off the 8-sample grid (1366 x 766 in a 1368 x 768 coded frame, 330 x 182, 634 x 362),
+    tiled over 2 / 4 ranks on one GPU with svtgpu_tile_plan_crop: every rank's decisions (DLF levels, CDEF strengths,
+    LR frame types and the summed unit records) and its outputs over its rects equal the single-GPU run, whose crop
+    handling the reference fixtures pin (DLF: gen_golden_dlf.c cases 8-10; LR: the crop-size search / frame goldens)."""
+    cases = CROP_CASES[world]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_crop_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        while len(res) < len(cases):
+            item = q.get(timeout=300)
+            res.append(item)
+            assert not str(item[1]).startswith("ERROR"), item
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.exitcode is None:
+                p.kill()
+    for case, status in res:
+        assert status == "ok", (case, status)
+    assert all(p.exitcode == 0 for p in procs)
+
+
+def test_tile_plan_crop_units_cover_the_crop():
+    """CPU check of svtgpu_tile_plan_crop: the ranks' LR units partition each plane's unit grid of the crop size, their
+    sample rects reach the crop edge (not the coded edge), the tiles reach the coded edge; invalid crops are refused."""
+    import svtgpu
+    for (w, h), (cw, ch) in (((1368, 768), (1366, 766)), ((336, 184), (330, 182))):
+        us = [64, 32, 32]
+        for world in (2, 4):
+            gx, gy = svtgpu.tile_grid(world)
+            plans = [svtgpu.tile_plan(w, h, us, gx, gy, r, crop=(cw, ch)).rects() for r in range(world)]
+            assert max(p["tile"][2] for p in plans) == w and max(p["tile"][3] for p in plans) == h
+            for p, (pw, ph) in enumerate(((cw, ch), ((cw + 1) // 2, (ch + 1) // 2), ((cw + 1) // 2, (ch + 1) // 2))):
+                assert max(q["lr_out"][p][2] for q in plans) == pw and max(q["lr_out"][p][3] for q in plans) == ph
+                covered = sum((q["lr_units"][p][2] - q["lr_units"][p][0]) * (q["lr_units"][p][3] - q["lr_units"][p][1])
+                              for q in plans)
+                nx = max(q["lr_units"][p][2] for q in plans)
+                ny = max(q["lr_units"][p][3] for q in plans)
+                assert covered == nx * ny
+    with pytest.raises(svtgpu.SvtGpuError):
+        svtgpu.tile_plan(1368, 768, [64, 32, 32], 2, 2, 0, crop=(1360, 766))  # the coded size is not the crop's alignment
