@@ -24,6 +24,7 @@
 #ifndef SVTGPU_H
 #define SVTGPU_H
 
+#include <stdbool.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -102,10 +103,11 @@ int         svtgpu_device_available(void);
 const char *svtgpu_version(void);
 /* ABI revision of this header: bumped whenever a struct passed across the boundary changes layout or an entry
  * point changes meaning (6: SvtGpuLrProfile::ms_events, svtgpu_comm_create_bounded, the asynchronous LR search
- * svtgpu_lr_search_frame_async; 7: svtgpu_cdef_apply_frame accepts params == NULL, svtgpu_stream_create).
+ * svtgpu_lr_search_frame_async; 7: svtgpu_cdef_apply_frame accepts params == NULL, svtgpu_stream_create; 8: the CCSO entry points,
+ * SvtGpuCcsoParams).
  * A caller built against another header checks svtgpu_abi_version() ==
  * SVTGPU_ABI_VERSION once at start-up and refuses to run on a mismatch. */
-#define SVTGPU_ABI_VERSION 7
+#define SVTGPU_ABI_VERSION 8
 int32_t     svtgpu_abi_version(void);
 const char *svtgpu_error_string(int code);
 
@@ -1003,6 +1005,79 @@ int svtgpu_lr_profile(SvtGpuLrState *s, int32_t enable, SvtGpuLrProfile *totals)
 int svtgpu_transfer_bytes(uint64_t *h2d, uint64_t *d2h, int32_t reset);
 /* controls of wn_filter_lvl / sg_filter_lvl (EncModeConfig.c:1329-1445); rate fields are left zero */
 int svtgpu_lr_controls_for_level(int32_t wn_level, int32_t sg_level, SvtGpuLrSearchControls *c);
+
+/* ---------------------------------------------------------------------------------------------
+ * CCSO, cross-component sample offset: the fork's AVM experiment, EbCcso.c / EbPickccso.c.
+ * The fork's encoder never calls it (EbCdefProcess.c:621-623 comment the search and the apply out); these entry points
+ * are what an encoder that re-enables it binds.  Geometry as the reference's: every plane's samples are addressed with
+ * the luma width as stride (ccso_stride, EbPickccso.c:800), chroma planes are (width >> 1) x (height >> 1) (the
+ * unpadded size >> 1, svt_av1_setup_dst_planes, EbDeblockingFilter.c:114-116), the classifier reads the luma plane
+ * padded by SVTGPU_CCSO_PAD samples (ext_rec_y, stride width + 2 * SVTGPU_CCSO_PAD), and the filter blocks are
+ * 256 x 256 luma / 128 x 128 chroma samples (CCSO_BLK_SIZE 7, EbDefinitions.h:1409), counted on the 8-aligned mode-info
+ * grid: nvfb x nhfb (derive_ccso_filter, EbPickccso.c:473-476).
+ * --------------------------------------------------------------------------------------------- */
+#define SVTGPU_CCSO_PAD 5     /* CCSO_PADDING_SIZE (EbDefinitions.h:1410) */
+#define SVTGPU_CCSO_LUT 2048  /* CCSO_BAND_NUM * 16 (EbDefinitions.h:1411) */
+/* one plane of FrameHeader.ccso_info (EbAv1Structs.h:407-427); filter_offset index (band << 4) + (cls0 << 2) + cls1 */
+typedef struct SvtGpuCcsoParams {
+    uint8_t enable, bo_only, quant_idx, ext_filter_support, max_band_log2, edge_clf, reserved[2];
+    int8_t  filter_offset[SVTGPU_CCSO_LUT];
+} SvtGpuCcsoParams;
+/* the filter-block grid of a plane (nvfb rows x nhfb columns; the block flags arrays are nvfb * nhfb bytes, row-major) */
+int svtgpu_ccso_grid(int32_t width, int32_t height, int32_t plane, int32_t *nvfb, int32_t *nhfb);
+/* ≙ the ext_rec_y construction (the copy of EbPickccso.c:907-918 + extend_ccso_border, EbCcso.c:185-201): the luma
+ * plane (8- or 16-bit samples, device) into `ext` (device, (height + 10) rows of width + 10 uint16), replicated
+ * SVTGPU_CCSO_PAD samples on every side. */
+int svtgpu_ccso_extend_luma(const void *luma, int32_t bits, int32_t stride, int32_t width, int32_t height,
+                            uint16_t *ext, void *stream);
+typedef struct SvtGpuCcsoState SvtGpuCcsoState;
+int  svtgpu_ccso_state_create(SvtGpuContext *ctx, int32_t width, int32_t height, SvtGpuCcsoState **out);
+void svtgpu_ccso_state_destroy(SvtGpuCcsoState *s);
+/* ≙ derive_ccso_filter (EbPickccso.c:464-779) of one plane: every (band-offset-only, filter support, quantization step,
+ * edge classifier, band count) configuration trained as the reference trains it, the cheapest kept, then weighed
+ * against the unfiltered plane.  ext (device, svtgpu_ccso_extend_luma of the pre-filter luma), org / rec (device,
+ * uint16, stride = width).  rdmult as derive_ccso_filter receives it (ccso_search's weighting applied).  Results stay
+ * in the state for svtgpu_ccso_apply_plane(..., params = NULL); params_out / flags_out (host, nullable) also receive
+ * them (one wait).  A disabled plane reads enable = 0 and zero fields / flags. */
+int svtgpu_ccso_search_plane(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *org, const uint16_t *rec,
+                             int32_t plane, int32_t bit_depth, int32_t rdmult, SvtGpuCcsoParams *params_out,
+                             uint8_t *flags_out, void *stream);
+/* ≙ ccso_search (EbPickccso.c:785-815): rdmult weighted by clamp(base_q_idx, 1, 63), the three planes searched.
+ * Returns 1 and searches nothing when the weighted rdmult reaches INT_MAX (the reference returns early);
+ * *frame_flag = ccso_frame_flag (any plane enabled). */
+int svtgpu_ccso_search_frame(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const org[3],
+                             const uint16_t *const rec[3], int32_t bit_depth, int32_t rdmult, int32_t base_q_idx,
+                             SvtGpuCcsoParams params_out[3], uint8_t *const flags_out[3], int32_t *frame_flag,
+                             void *stream);
+/* ≙ ccso_frame's body for one plane (EbCcso.c:637-677 with ccso_apply_{luma,chroma}_{mb,sb}_filter, :297-622): the
+ * plane at `dst` (device, 8- or 16-bit samples, dst_stride samples) offset in place where the block flag is set,
+ * classified on `ext`.  params (host) + flags (host, nvfb * nhfb): those; params = NULL: the state's last search of
+ * this plane (stream order, no host wait).  A plane with enable = 0 is left as it is. */
+int svtgpu_ccso_apply_plane(SvtGpuCcsoState *s, const uint16_t *ext, int32_t plane, int32_t bit_depth, void *dst,
+                            int32_t dst_bits, int32_t dst_stride, const SvtGpuCcsoParams *params,
+                            const uint8_t *flags, void *stream);
+/* per-block RTCD shims (common_dsp_rtcd.h:1025-1090; host pointers, synchronous) */
+uint64_t svtgpu_compute_distortion_block(const uint16_t *org, const int org_stride, const uint16_t *rec16,
+                                         const int rec_stride, const int x, const int y,
+                                         const int log2_filter_unit_size, const int height, const int width);
+void svtgpu_ccso_derive_src_block(const uint16_t *src_y, uint8_t *const src_cls0, uint8_t *const src_cls1,
+                                  const int src_y_stride, const int ccso_stride, const int x, const int y,
+                                  const int pic_width, const int pic_height, const int y_uv_hscale,
+                                  const int y_uv_vscale, const int qstep, const int neg_qstep, const int *src_loc,
+                                  const int blk_size, const int edge_clf);
+void svtgpu_ccso_filter_block_hbd_with_buf(const uint16_t *src_y, uint16_t *dst_yuv, const uint8_t *src_cls0,
+                                           const uint8_t *src_cls1, const int src_y_stride, const int dst_stride,
+                                           const int ccso_stride, const int x, const int y, const int pic_width,
+                                           const int pic_height, const int8_t *filter_offset, const int blk_size,
+                                           const int y_uv_hscale, const int y_uv_vscale, const int max_val,
+                                           const uint8_t shift_bits, const uint8_t ccso_bo_only);
+void svtgpu_ccso_filter_block_hbd_wo_buf(const uint16_t *src_y, uint16_t *dst_yuv, const int x, const int y,
+                                         const int pic_width, const int pic_height, int *src_cls,
+                                         const int8_t *offset_buf, const int src_y_stride, const int dst_stride,
+                                         const int y_uv_hscale, const int y_uv_vscale, const int thr,
+                                         const int neg_thr, const int *src_loc, const int max_val, const int blk_size,
+                                         const bool isSingleBand, const uint8_t shift_bits, const int edge_clf,
+                                         const uint8_t ccso_bo_only);
 
 #ifdef __cplusplus
 }

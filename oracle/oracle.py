@@ -17,7 +17,7 @@ ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 sys.path.insert(0, os.path.join(ROOT, "svt-av1_pro-anchor-v2.1.0-_amd"))
 from svtgpu import (CdefControls, CdefParams, CdefList, LfParams, LF_MI_DTYPE, REST_UNIT_DTYPE,  # noqa: E402
-                    LrSearchControls, LR_UNIT_SEARCH_DTYPE)  # (shared C struct layouts)
+                    LrSearchControls, LR_UNIT_SEARCH_DTYPE, CcsoParams)  # (shared C struct layouts)
 
 
 class OracleFrame(ctypes.Structure):
@@ -93,6 +93,13 @@ _SIGS = {
     "oracle_pme_sad_loop": (None, [_P, _P, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                    _P, _P, _P, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16, ctypes.c_int16,
                                    ctypes.c_int16, ctypes.c_int16, ctypes.c_int16]),
+    "oracle_ccso_grid": (ctypes.c_int, [_I32, _I32, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "oracle_ccso_extend": (None, [_P, _I32, _I32, _I32, _I32, _P]),
+    "oracle_ccso_apply_plane": (None, [_P, _I32, _I32, _I32, _I32, _P, _I32, _I32, ctypes.POINTER(CcsoParams), _P]),
+    "oracle_ccso_search_plane": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, ctypes.POINTER(CcsoParams),
+                                                _P]),
+    "oracle_ccso_search_frame": (ctypes.c_int, [_P, _P * 3, _P * 3, _I32, _I32, _I32, _I32, _I32,
+                                                ctypes.POINTER(CcsoParams), _P * 3, ctypes.POINTER(_I32)]),
 }
 _lib = None
 
@@ -434,3 +441,53 @@ def extend(buf, offset, stride, w, h, bh, bv):
     """svt_extend_frame restated, in place; offset = index of the first visible sample in the flat buffer."""
     lib().oracle_extend(ctypes.c_void_p(buf.ctypes.data + offset * buf.dtype.itemsize), buf.dtype.itemsize * 8,
                         stride, w, h, bh, bv)
+
+
+# ---- CCSO (ccso_oracle.c; SURVEY §8(f)4) ----
+def ccso_grid(w, h, plane):
+    a, b = _I32(), _I32()
+    lib().oracle_ccso_grid(w, h, plane, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def ccso_extend(luma):
+    """ext_rec_y of a (H, W) luma plane (uint8 or uint16): (H + 10, W + 10) uint16."""
+    luma = np.ascontiguousarray(luma)
+    h, w = luma.shape
+    ext = np.zeros((h + 10, w + 10), np.uint16)
+    lib().oracle_ccso_extend(ptr(luma), 8 if luma.dtype == np.uint8 else 16, w, w, h, ptr(ext))
+    return ext
+
+
+def ccso_apply_plane(ext, bd, plane, dst, params, flags):
+    """ccso_frame's body for one plane: returns the filtered copy of dst (uint8 / uint16 (ph, pw) array)."""
+    out = np.ascontiguousarray(dst).copy()
+    h, w = ext.shape[0] - 10, ext.shape[1] - 10
+    f = np.ascontiguousarray(flags, dtype=np.uint8)
+    lib().oracle_ccso_apply_plane(ptr(np.ascontiguousarray(ext)), w, h, bd, plane, ptr(out),
+                                  8 if out.dtype == np.uint8 else 16, out.shape[1], ctypes.byref(params), ptr(f))
+    return out
+
+
+def ccso_search_plane(ext, org, rec, plane, bd, rdmult):
+    """derive_ccso_filter of one plane: org / rec (H, W) uint16 (chroma in the top-left quarter).  (params, flags)."""
+    h, w = org.shape
+    nv, nh = ccso_grid(w, h, plane)
+    prm, flags = CcsoParams(), np.zeros((nv, nh), np.uint8)
+    lib().oracle_ccso_search_plane(ptr(np.ascontiguousarray(ext)), ptr(np.ascontiguousarray(org)),
+                                   ptr(np.ascontiguousarray(rec)), w, h, plane, bd, rdmult, ctypes.byref(prm),
+                                   ptr(flags))
+    return prm, flags
+
+
+def ccso_search_frame(ext, org, rec, bd, rdmult, base_q_idx):
+    """ccso_search: (rc, [params] * 3, [flags] * 3, frame_flag); rc 1 = nothing searched (rdmult overflow)."""
+    h, w = org[0].shape
+    keep = [np.ascontiguousarray(a) for a in list(org) + list(rec)]
+    prms = (CcsoParams * 3)()
+    flags = [np.zeros(ccso_grid(w, h, p), np.uint8) for p in range(3)]
+    ff = _I32(0)
+    rc = lib().oracle_ccso_search_frame(ptr(np.ascontiguousarray(ext)), (_P * 3)(*[a.ctypes.data for a in keep[:3]]),
+                                        (_P * 3)(*[a.ctypes.data for a in keep[3:]]), w, h, bd, rdmult, base_q_idx,
+                                        prms, (_P * 3)(*[f.ctypes.data for f in flags]), ctypes.byref(ff))
+    return rc, list(prms), flags, ff.value

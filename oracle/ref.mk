@@ -50,7 +50,7 @@ PIPE_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(PIPE_C))
 
 all: $(OUT)/gen_golden_cdef $(OUT)/gen_golden_dlf $(OUT)/gen_golden_md $(OUT)/gen_golden_lr $(OUT)/gen_golden_pipe \
      $(OUT)/gen_golden_shims $(OUT)/rtcd_pipe $(OUT)/ref_bench $(OUT)/gen_golden_me $(OUT)/gen_golden_frame \
-     $(OUT)/rtcd_install
+     $(OUT)/rtcd_install $(OUT)/gen_golden_ccso
 
 $(OUT)/obj/Lib/Common/ASM_AVX2/%.o $(OUT)/obj/Lib/Encoder/ASM_AVX2/%.o: CFLAGS += -mavx2
 $(OUT)/obj/Lib/Common/ASM_SSE2/%.o: CFLAGS += -msse2
@@ -128,3 +128,10 @@ FRAME_C  := Lib/Common/C_DEFAULT/EbPackUnPack_C.c Lib/Common/Codec/EbMcp.c
 FRAME_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(FRAME_C))
 $(OUT)/gen_golden_frame: oracle/ref_harness/gen_golden_frame.c $(sort $(FRAME_OBJ) $(LR_OBJ) $(MD_OBJ) $(C_OBJ))
 	$(CC) $(CFLAGS) $^ -o $@ -Wl,--gc-sections -lm -lpthread
+
+# CCSO: the fork's EbCcso.c / EbPickccso.c; ccso_search reaches svt_aom_get_recon_pic (EbRestProcess.c),
+# svt_av1_setup_dst_planes (EbDeblockingFilter.c) and svt_aom_get_syntax_rate_from_cdf (EbMdRateEstimation.c)
+CCSO_C   := Lib/Common/Codec/EbCcso.c Lib/Encoder/Codec/EbPickccso.c Lib/Encoder/Codec/EbMdRateEstimation.c
+CCSO_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(CCSO_C))
+$(OUT)/gen_golden_ccso: oracle/ref_harness/gen_golden_ccso.c $(sort $(CCSO_OBJ) $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ))
+	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread

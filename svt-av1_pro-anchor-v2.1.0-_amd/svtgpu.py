@@ -180,6 +180,29 @@ LR_UNIT_SEARCH_DTYPE = np.dtype([("sse", np.int64, 3), ("wiener", REST_UNIT_DTYP
                                 align=True)
 
 
+class CcsoParams(ctypes.Structure):
+    """SvtGpuCcsoParams: one plane of FrameHeader.ccso_info (EbAv1Structs.h:407-427)."""
+    _fields_ = [("enable", ctypes.c_uint8), ("bo_only", ctypes.c_uint8), ("quant_idx", ctypes.c_uint8),
+                ("ext_filter_support", ctypes.c_uint8), ("max_band_log2", ctypes.c_uint8), ("edge_clf", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8 * 2), ("filter_offset", ctypes.c_int8 * 2048)]
+
+    FIELDS = ("enable", "bo_only", "quant_idx", "ext_filter_support", "max_band_log2", "edge_clf")
+
+    @classmethod
+    def make(cls, fields, lut):
+        p = cls()
+        for n, v in zip(cls.FIELDS, fields):
+            setattr(p, n, int(v))
+        ctypes.memmove(p.filter_offset, np.ascontiguousarray(lut, dtype=np.int8).ctypes.data, 2048)
+        return p
+
+    def fields(self):
+        return tuple(int(getattr(self, n)) for n in self.FIELDS)
+
+    def lut(self):
+        return np.frombuffer(bytes(self.filter_offset), dtype=np.int8).copy()
+
+
 class ConvolveParams(ctypes.Structure):
     """SvtGpuConvolveParams: the reference's ConvolveParams layout (EbDefinitions.h:577-590)."""
     _fields_ = [("ref", ctypes.c_int32), ("do_average", ctypes.c_int32), ("dst", ctypes.c_void_p),
@@ -383,6 +406,24 @@ _SIGS = {
     "svtgpu_dlf_set_crop": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_lr_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
+    "svtgpu_ccso_grid": (ctypes.c_int, [_I32, _I32, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "svtgpu_ccso_extend_luma": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P]),
+    "svtgpu_ccso_state_create": (ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(_P)]),
+    "svtgpu_ccso_state_destroy": (None, [_P]),
+    "svtgpu_ccso_search_plane": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(CcsoParams), _P,
+                                                _P]),
+    "svtgpu_ccso_search_frame": (ctypes.c_int, [_P, _P, _P * 3, _P * 3, _I32, _I32, _I32, ctypes.POINTER(CcsoParams),
+                                                _P * 3, ctypes.POINTER(_I32), _P]),
+    "svtgpu_ccso_apply_plane": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _I32, ctypes.POINTER(CcsoParams), _P,
+                                               _P]),
+    "svtgpu_compute_distortion_block": (ctypes.c_uint64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "svtgpu_ccso_derive_src_block": (None, [_P, _P, _P] + [ctypes.c_int] * 10 + [_P, ctypes.c_int, ctypes.c_int]),
+    "svtgpu_ccso_filter_block_hbd_with_buf": (None, [_P, _P, _P, _P] + [ctypes.c_int] * 7 + [_P] +
+                                              [ctypes.c_int] * 4 + [ctypes.c_uint8, ctypes.c_uint8]),
+    "svtgpu_ccso_filter_block_hbd_wo_buf": (None, [_P, _P] + [ctypes.c_int] * 4 + [_P, _P] + [ctypes.c_int] * 6 +
+                                            [_P, ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_uint8,
+                                             ctypes.c_int, ctypes.c_uint8]),
 }
 
 _lib = None
@@ -1117,6 +1158,67 @@ def gather_lr_records(records, units, n, rank, group=None, device=None):
             out[b * hu:e * hu] = got[b * hu:e * hu]
         merged.append(out)
     return merged
+
+
+class CcsoState:
+    """CCSO on the device: the reference's ccso_search / derive_ccso_filter and ccso_frame
+    (EbPickccso.c:464-815, EbCcso.c:626-678) over device buffers given as integer addresses (e.g. a torch tensor's
+    data_ptr()).  org / rec / the planes' samples use the luma width as stride (ccso_stride)."""
+
+    def __init__(self, ctx, width, height):
+        self.ctx, self.width, self.height = ctx, width, height
+        h = _P()
+        check(lib().svtgpu_ccso_state_create(ctx.h, width, height, ctypes.byref(h)))
+        self.h = h
+
+    def grid(self, plane):
+        a, b = _I32(), _I32()
+        check(lib().svtgpu_ccso_grid(self.width, self.height, plane, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def extend(self, luma, bits, stride, ext, stream=None):
+        """ext_rec_y (EbPickccso.c:907-918 + extend_ccso_border) from a device luma plane into `ext`."""
+        check(lib().svtgpu_ccso_extend_luma(luma, bits, stride, self.width, self.height, ext, stream))
+
+    def search_plane(self, ext, org, rec, plane, bit_depth, rdmult, stream=None, read=True):
+        """derive_ccso_filter of one plane; (CcsoParams, flags (nvfb, nhfb) uint8) when read, else None (the result
+        stays on the device for apply(params=None))."""
+        if not read:
+            check(lib().svtgpu_ccso_search_plane(self.h, ext, org, rec, plane, bit_depth, rdmult, None, None, stream))
+            return None
+        prm, flags = CcsoParams(), np.zeros(self.grid(plane), np.uint8)
+        check(lib().svtgpu_ccso_search_plane(self.h, ext, org, rec, plane, bit_depth, rdmult, ctypes.byref(prm),
+                                             ptr(flags), stream))
+        return prm, flags
+
+    def search_frame(self, ext, org, rec, bit_depth, rdmult, base_q_idx, stream=None):
+        """ccso_search: (rc, [CcsoParams] * 3, [flags] * 3, frame_flag); rc 1 = rdmult overflow, nothing searched."""
+        prms = (CcsoParams * 3)()
+        flags = [np.zeros(self.grid(p), np.uint8) for p in range(3)]
+        ff = _I32(0)
+        rc = lib().svtgpu_ccso_search_frame(self.h, ext, (_P * 3)(*org), (_P * 3)(*rec), bit_depth, rdmult,
+                                            base_q_idx, prms, (_P * 3)(*[f.ctypes.data for f in flags]),
+                                            ctypes.byref(ff), stream)
+        if rc not in (0, 1):
+            check(rc)
+        return rc, list(prms), flags, ff.value
+
+    def apply(self, ext, plane, bit_depth, dst, dst_bits, dst_stride, params=None, flags=None, stream=None):
+        """ccso_frame's body for one plane, in place on the device plane `dst`; params None: the last search's."""
+        f = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        check(lib().svtgpu_ccso_apply_plane(self.h, ext, plane, bit_depth, dst, dst_bits, dst_stride,
+                                            None if params is None else ctypes.byref(params), ptr(f), stream))
+
+    def close(self):
+        if self.h:
+            lib().svtgpu_ccso_state_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def plane_sse(a, b, plane, stream=None):

@@ -1,0 +1,187 @@
+"""CCSO on the MI355X: the per-block RTCD shims, ccso_frame and ccso_search through the C ABI against
+the fork's own EbCcso.c / EbPickccso.c (tests/golden/ccso.bin, oracle/ref_harness/gen_golden_ccso.c) and, at 720p /
+10-bit sizes the goldens do not reach, against the CPU oracle (oracle/ccso_oracle.c, pinned by the same goldens on
+CPU in test_oracle_golden.py).  Bit-exact: header fields, the 2048-entry table, the block flags, filtered samples."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import ccso_cases as xc
+import oracle
+import svtgpu
+
+pytestmark = pytest.mark.gpu
+P = lambda a: ctypes.c_void_p(a.ctypes.data)
+
+
+@pytest.fixture(scope="module")
+def g():
+    return xc.golden()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return svtgpu.Context(0)
+
+
+def dev(a):
+    """a numpy array on the device (uint16 through int16, uint8 as is); the tensor and its address"""
+    import torch
+    a = np.ascontiguousarray(a)
+    t = torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).cuda()
+    torch.cuda.synchronize()
+    return t
+
+
+def host(t, dtype):
+    import torch
+    torch.cuda.synchronize()
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if dtype == np.uint16 else a
+
+
+def ext_dev(st, pre):
+    """svtgpu_ccso_extend_luma of a host luma plane -> (device ext, its host copy)"""
+    import torch
+    h, w = pre.shape
+    d_pre = dev(pre)
+    ext = torch.zeros(((h + 10) * (w + 10),), dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    st.extend(d_pre.data_ptr(), 8 if pre.dtype == np.uint8 else 16, w, ext.data_ptr())
+    return ext, host(ext, np.uint16).reshape(h + 10, w + 10)
+
+
+def test_block_shims_golden(g):
+    """ccso_derive_src_block / ccso_filter_block_hbd_with_buf / ccso_filter_block_hbd_wo_buf / compute_distortion_block
+    (common_dsp_rtcd.h:1025-1090) on host buffers: ragged blocks, luma and 4:2:0 chroma, 8 and 10 bits, every support,
+    band-offset-only."""
+    L = svtgpu.lib()
+    for c in xc.block_cases(g):
+        msg = "block case %d" % c["n"]
+        ext, es, cs = c["ext"], c["es"], c["cs"]
+        src = ctypes.c_void_p(ext.ctypes.data + 2 * (5 * es + 5))
+        loc = np.array(xc.sample_pos(es, c["sup"]), np.int32)
+        assert loc[0] == c["loc0"]
+        c0, c1 = np.zeros_like(c["cls0"]), np.zeros_like(c["cls1"])
+        L.svtgpu_ccso_derive_src_block(src, P(c0), P(c1), es, cs, c["x"], c["y"], c["pw"], c["ph"], c["hs"], c["vs"],
+                                       c["qs"], -c["qs"], P(loc), c["blk"], c["clf"])
+        np.testing.assert_array_equal(c0, c["cls0"], err_msg=msg)
+        np.testing.assert_array_equal(c1, c["cls1"], err_msg=msg)
+        maxv, shift = (1 << c["bd"]) - 1, c["bd"] - c["band_log2"]
+        d = c["dst0"].copy()
+        L.svtgpu_ccso_filter_block_hbd_with_buf(src, P(d), P(c0), P(c1), es, cs, cs, c["x"], c["y"], c["pw"], c["ph"],
+                                                P(c["lut"]), c["blk"], c["hs"], c["vs"], maxv, shift, c["bo"])
+        np.testing.assert_array_equal(d, c["with_buf"], err_msg=msg)
+        d2, cls = c["dst0"].copy(), np.zeros(2, np.int32)
+        L.svtgpu_ccso_filter_block_hbd_wo_buf(src, P(d2), c["x"], c["y"], c["pw"], c["ph"], P(cls), P(c["lut"]), es, cs,
+                                              c["hs"], c["vs"], c["qs"], -c["qs"], P(loc), maxv, c["blk"],
+                                              c["band_log2"] == 0, shift, c["clf"], c["bo"])
+        np.testing.assert_array_equal(d2, c["wo_buf"], err_msg=msg)
+        log2 = 7 if c["hs"] else 8
+        ssd = L.svtgpu_compute_distortion_block(P(c["dst0"]), cs, P(d), cs, c["x"], c["y"], log2, c["ph"], c["pw"])
+        assert ssd == c["ssd"], msg
+
+
+def test_apply_golden(g, ctx):
+    """ccso_frame with random ccso_info / block flags (every support, band-offset-only, 1-128 bands): the padded luma
+    built on the device, each plane filtered in place."""
+    for c in xc.apply_cases(g):
+        st = svtgpu.CcsoState(ctx, c["w"], c["h"])
+        ext, ext_h = ext_dev(st, c["pre"])
+        np.testing.assert_array_equal(ext_h, oracle.ccso_extend(c["pre"]))
+        for p in range(3):
+            d = dev(c["inp"][p])
+            st.apply(ext.data_ptr(), p, 8, d.data_ptr(), 8, d.shape[1], c["params"][p], c["flags"][p])
+            np.testing.assert_array_equal(host(d, np.uint8), c["out"][p], err_msg="case %d plane %d" % (c["n"], p))
+        st.close()
+
+
+def _search(ctx, w, h, bd, pre, org, rec, rdmult, q):
+    import torch
+    st = svtgpu.CcsoState(ctx, w, h)
+    ext, _ = ext_dev(st, pre)
+    d_org, d_rec = [dev(a) for a in org], [dev(a) for a in rec]
+    rc, prms, flags, ff = st.search_frame(ext.data_ptr(), [t.data_ptr() for t in d_org],
+                                          [t.data_ptr() for t in d_rec], bd, rdmult, q)
+    torch.cuda.synchronize()
+    return st, ext, d_rec, rc, prms, flags, ff
+
+
+def test_search_golden(g, ctx):
+    """ccso_search on the device equals the reference's (header fields, table, block flags, frame flag), including
+    planes that stay off, the rdmult overflow that searches nothing, an odd width whose chroma block grid is wider than
+    the plane; at 8 bits the search's own device result (apply with params = NULL) filters like the reference's
+    ccso_frame."""
+    for c in xc.search_cases(g):
+        msg = "case %d (%dx%d %d-bit)" % (c["n"], c["w"], c["h"], c["bd"])
+        st, ext, d_rec, rc, prms, flags, ff = _search(ctx, c["w"], c["h"], c["bd"], c["pre"], c["org"], c["rec"],
+                                                      c["rdmult"], c["q"])
+        assert ff == c["frame_flag"], msg
+        if rc == 1:
+            assert not any(p.enable for p in c["params"]), msg
+            continue
+        for p in range(3):
+            want = c["params"][p]
+            assert prms[p].fields() == want.fields(), "%s plane %d" % (msg, p)
+            if want.enable:
+                np.testing.assert_array_equal(prms[p].lut(), want.lut(), err_msg="%s plane %d" % (msg, p))
+                np.testing.assert_array_equal(flags[p], c["flags"][p], err_msg="%s plane %d" % (msg, p))
+            if c["out"] is not None:
+                ph, pw = c["out"][p].shape
+                d8 = dev(c["rec"][p][:ph, :pw].astype(np.uint8))
+                st.apply(ext.data_ptr(), p, 8, d8.data_ptr(), 8, pw)  # the state's result of this plane
+                np.testing.assert_array_equal(host(d8, np.uint8), c["out"][p], err_msg="%s plane %d" % (msg, p))
+        st.close()
+
+
+def _content(w, h, bd, seed):
+    """smooth org, rec = org + a band / edge biased error (the golden generator's model, numpy)"""
+    rng = np.random.default_rng(seed)
+    maxv, sh = (1 << bd) - 1, bd - 8
+    org, rec = [], []
+    for p in range(3):
+        pw, ph = (w >> 1, h >> 1) if p else (w, h)
+        kn = rng.integers(0, 256, size=(ph // 16 + 2, pw // 16 + 2)).astype(np.float64)
+        ys, xs = np.arange(ph) / 16.0, np.arange(pw) / 16.0
+        gy, gx = np.floor(ys).astype(int), np.floor(xs).astype(int)
+        fy, fx = (ys - gy)[:, None], (xs - gx)[None, :]
+        v = (kn[gy][:, gx] * (1 - fx) * (1 - fy) + kn[gy][:, gx + 1] * fx * (1 - fy) +
+             kn[gy + 1][:, gx] * (1 - fx) * fy + kn[gy + 1][:, gx + 1] * fx * fy)
+        v[:, : pw // 8] /= 16
+        v[:, pw - pw // 8:] = 255 - (255 - v[:, pw - pw // 8:]) / 16
+        o = np.clip((v.astype(np.int64) << sh) + rng.integers(-2 << sh, 3 << sh, size=v.shape), 0, maxv)
+        gxd = np.zeros_like(o)
+        gxd[:, :-1] = o[:, 1:] - o[:, :-1]
+        e = rng.integers(-3, 4, size=o.shape) - 2 * (o > maxv * 3 // 4) + 2 * (gxd > (8 << sh)) - 2 * (gxd < -(8 << sh))
+        r = np.clip(o + (e << sh), 0, maxv)
+        org.append(xc.full(o.astype(np.uint16), w, h))
+        rec.append(xc.full(r.astype(np.uint16), w, h))
+    pre = np.clip(rec[0].astype(np.int64) + rng.integers(-1, 2, size=(h, w)), 0, maxv).astype(np.uint16)
+    return org, rec, pre
+
+
+@pytest.mark.parametrize("w,h,bd,rdmult,q", [(1280, 720, 8, 1500, 80), (640, 360, 10, 900, 120),
+                                             (1000, 504, 8, 50000, 40)])
+def test_search_and_apply_vs_oracle(ctx, w, h, bd, rdmult, q):
+    """Frame sizes past the goldens (several block rows and columns per plane, 10-bit, a high rdmult): the device
+    search and the device apply of its result against the oracle's search and apply (16-bit planes for 10 bits: the
+    reference's ccso_frame reads only 8-bit buffers, so the high-bit-depth apply is pinned through the oracle's
+    ccso_filter_block_hbd_wo_buf_c restatement)."""
+    org, rec, pre = _content(w, h, bd, seed=w + h + bd)
+    st, ext, d_rec, rc, prms, flags, ff = _search(ctx, w, h, bd, pre, org, rec, rdmult, q)
+    ext_h = oracle.ccso_extend(pre)
+    orc, oprms, oflags, off = oracle.ccso_search_frame(ext_h, org, rec, bd, rdmult, q)
+    assert (rc, ff) == (orc, off)
+    assert any(p.enable for p in oprms) or rdmult == 50000
+    for p in range(3):
+        assert prms[p].fields() == oprms[p].fields(), p
+        np.testing.assert_array_equal(prms[p].lut(), oprms[p].lut())
+        np.testing.assert_array_equal(flags[p], oflags[p])
+        ph, pw = (h >> 1, w >> 1) if p else (h, w)
+        plane = rec[p][:ph, :pw] if bd > 8 else rec[p][:ph, :pw].astype(np.uint8)
+        d = dev(plane)
+        st.apply(ext.data_ptr(), p, bd, d.data_ptr(), 16 if bd > 8 else 8, pw)
+        want = oracle.ccso_apply_plane(ext_h, bd, p, plane, oprms[p], oflags[p])
+        np.testing.assert_array_equal(host(d, plane.dtype.type), want, err_msg="plane %d" % p)
+    st.close()

@@ -276,3 +276,49 @@ def test_oracle_md_batch_sb_range():
     whole = oracle.md_dist_batch(src[0], refs, bd, mv)
     for b, e in ((0, 3), (5, 12), (9, 12)):
         assert np.array_equal(oracle.md_dist_batch(src[0], refs, bd, mv, sb_range=(b, e)), whole[b:e])
+
+
+# ---- CCSO (ccso_oracle.c vs the fork's EbCcso.c / EbPickccso.c, tests/golden/ccso.bin) ----
+def test_oracle_ccso_extend_vs_reference():
+    import ccso_cases as xc
+    cases = [c for c in xc.search_cases(xc.golden()) if c["ext"] is not None]
+    assert cases
+    for c in cases:
+        np.testing.assert_array_equal(oracle.ccso_extend(c["pre"]), c["ext"], err_msg="case %d" % c["n"])
+
+
+def test_oracle_ccso_apply_vs_reference():
+    """ccso_frame with random ccso_info and block flags (every filter support, band-offset-only, 1-128 bands)."""
+    import ccso_cases as xc
+    for c in xc.apply_cases(xc.golden()):
+        ext = oracle.ccso_extend(c["pre"])
+        for p in range(3):
+            got = oracle.ccso_apply_plane(ext, 8, p, c["inp"][p], c["params"][p], c["flags"][p])
+            np.testing.assert_array_equal(got, c["out"][p], err_msg="case %d plane %d" % (c["n"], p))
+
+
+def test_oracle_ccso_search_vs_reference():
+    """ccso_search (every plane's derive_ccso_filter) and, at 8 bits, ccso_frame applying its result: the frame header
+    fields, the LUT, the block flags and the filtered planes equal the reference's; the cases include planes that
+    stay off (no coding-error bias at a high rdmult) and the rdmult overflow that returns before any search."""
+    import ccso_cases as xc
+    cases = xc.search_cases(xc.golden())
+    assert any(c["params"][0].enable for c in cases) and any(not c["params"][0].enable for c in cases)
+    for c in cases:
+        ext = oracle.ccso_extend(c["pre"])
+        rc, prms, flags, ff = oracle.ccso_search_frame(ext, c["org"], c["rec"], c["bd"], c["rdmult"], c["q"])
+        msg = "case %d (%dx%d %d-bit)" % (c["n"], c["w"], c["h"], c["bd"])
+        assert ff == c["frame_flag"], msg
+        for p in range(3):
+            want = c["params"][p]
+            if rc == 1:  # nothing searched: the header keeps its (zeroed) fields
+                assert not want.enable, msg
+                continue
+            assert prms[p].fields() == want.fields(), "%s plane %d" % (msg, p)
+            if want.enable:
+                np.testing.assert_array_equal(prms[p].lut(), want.lut(), err_msg="%s plane %d" % (msg, p))
+                np.testing.assert_array_equal(flags[p], c["flags"][p], err_msg="%s plane %d" % (msg, p))
+            if c["out"] is not None:
+                inp = c["rec"][p][:c["out"][p].shape[0], :c["out"][p].shape[1]].astype(np.uint8)
+                got = oracle.ccso_apply_plane(ext, 8, p, inp, prms[p], flags[p])
+                np.testing.assert_array_equal(got, c["out"][p], err_msg="%s plane %d" % (msg, p))
