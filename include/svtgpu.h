@@ -1042,9 +1042,10 @@ void svtgpu_ccso_state_destroy(SvtGpuCcsoState *s);
 int svtgpu_ccso_search_plane(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *org, const uint16_t *rec,
                              int32_t plane, int32_t bit_depth, int32_t rdmult, SvtGpuCcsoParams *params_out,
                              uint8_t *flags_out, void *stream);
-/* ≙ ccso_search (EbPickccso.c:785-815): rdmult weighted by clamp(base_q_idx, 1, 63), the three planes searched.
- * Returns 1 and searches nothing when the weighted rdmult reaches INT_MAX (the reference returns early);
- * *frame_flag = ccso_frame_flag (any plane enabled). */
+/* ≙ ccso_search (EbPickccso.c:785-815): rdmult weighted by clamp(base_q_idx, 1, 63), the three planes searched side by
+ * side (one launch per pass).  Returns 1 and searches nothing when the weighted rdmult reaches INT_MAX (the reference
+ * returns early); *frame_flag = ccso_frame_flag (any plane enabled).  params_out = NULL: nothing is read back and
+ * nothing waited for (*frame_flag = 0); the results stay in the state for svtgpu_ccso_apply_plane(..., NULL, ...). */
 int svtgpu_ccso_search_frame(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const org[3],
                              const uint16_t *const rec[3], int32_t bit_depth, int32_t rdmult, int32_t base_q_idx,
                              SvtGpuCcsoParams params_out[3], uint8_t *const flags_out[3], int32_t *frame_flag,

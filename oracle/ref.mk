@@ -132,6 +132,6 @@ $(OUT)/gen_golden_frame: oracle/ref_harness/gen_golden_frame.c $(sort $(FRAME_OB
 # CCSO: the fork's EbCcso.c / EbPickccso.c; ccso_search reaches svt_aom_get_recon_pic (EbRestProcess.c),
 # svt_av1_setup_dst_planes (EbDeblockingFilter.c) and svt_aom_get_syntax_rate_from_cdf (EbMdRateEstimation.c)
 CCSO_C   := Lib/Common/Codec/EbCcso.c Lib/Encoder/Codec/EbPickccso.c Lib/Encoder/Codec/EbMdRateEstimation.c
-CCSO_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(CCSO_C))
+CCSO_OBJ := $(patsubst %.c,$(OUT)/obj/%.o,$(CCSO_C)) $(OUT)/obj/Lib/Common/ASM_AVX2/ccso_avx2.o
 $(OUT)/gen_golden_ccso: oracle/ref_harness/gen_golden_ccso.c $(sort $(CCSO_OBJ) $(LR_OBJ) $(MD_OBJ) $(DLF_OBJ) $(C_OBJ) $(PIPE_OBJ))
 	$(CC) $(CFLAGS) $(filter %.c,$^) $(filter %.o,$^) -o $@ -Wl,--gc-sections -lm -lpthread

@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "EbDefinitions.h"
 #include "EbPictureControlSet.h"
@@ -380,7 +381,75 @@ static void apply_cases(GoldenFile *g, Rng *r) {
     golden_put(g, "app_meta", 'i', 2, dims, meta);
 }
 
+/* the reference's CPU cost of one frame's ccso_search (+ ccso_frame at 8 bits) on the golden content model: the
+ * cpu_baseline of scripts/r6/ccso_perf.py (kind "reference", one thread) */
+void     ccso_filter_block_hbd_wo_buf_avx2(const uint16_t *src_y, uint16_t *dst_yuv, const int x, const int y,
+                                           const int pic_width, const int pic_height, int *src_cls,
+                                           const int8_t *offset_buf, const int src_y_stride, const int dst_stride,
+                                           const int y_uv_hscale, const int y_uv_vscale, const int thr,
+                                           const int neg_thr, const int *src_loc, const int max_val, const int blk_size,
+                                           const bool isSingleBand, const uint8_t shift_bits, const int edge_clf,
+                                           const uint8_t ccso_bo_only);
+void     ccso_derive_src_block_avx2(const uint16_t *src_y, uint8_t *const src_cls0, uint8_t *const src_cls1,
+                                    const int src_y_stride, const int ccso_stride, const int x, const int y,
+                                    const int pic_width, const int pic_height, const int y_uv_hscale,
+                                    const int y_uv_vscale, const int qstep, const int neg_qstep, const int *src_loc,
+                                    const int blk_size, const int edge_clf);
+void     ccso_filter_block_hbd_with_buf_avx2(const uint16_t *src_y, uint16_t *dst_yuv, const uint8_t *src_cls0,
+                                             const uint8_t *src_cls1, const int src_y_stride, const int dst_stride,
+                                             const int ccso_stride, const int x, const int y, const int pic_width,
+                                             const int pic_height, const int8_t *filter_offset, const int blk_size,
+                                             const int y_uv_hscale, const int y_uv_vscale, const int max_val,
+                                             const uint8_t shift_bits, const uint8_t ccso_bo_only);
+uint64_t compute_distortion_block_avx2(const uint16_t *org, const int org_stride, const uint16_t *rec16,
+                                       const int rec_stride, const int x, const int y, const int log2_filter_unit_size,
+                                       const int height, const int width);
+
+static int bench(int W, int H, int bd, int reps, int avx2) {
+    bind_c_kernels();
+    if (avx2) { /* the bindings setup_common_rtcd_internal makes on an AVX2 host (common_dsp_rtcd.c:637-639) */
+        ccso_filter_block_hbd_wo_buf   = ccso_filter_block_hbd_wo_buf_avx2;
+        ccso_filter_block_hbd_with_buf = ccso_filter_block_hbd_with_buf_avx2;
+        ccso_derive_src_block          = ccso_derive_src_block_avx2;
+        compute_distortion_block       = compute_distortion_block_avx2;
+    }
+    Rng       r = {0x4343534F0000BE01ull};
+    uint16_t *org[3], *rec[3], *pre = malloc(2 * (size_t)W * H);
+    for (int p = 0; p < 3; p++) org[p] = calloc((size_t)W * H, 2), rec[p] = calloc((size_t)W * H, 2);
+    content(&r, W, H, bd, org, rec, pre, 2);
+    uint16_t *ext = make_ext(pre, W, H);
+    double    best = 1e30, best_apply = 1e30;
+    for (int k = 0; k < reps; k++) {
+        Pic P;
+        pic_init(&P, W, H, bd, 100);
+        MacroblockdPlane pd[3];
+        pd_init(pd);
+        struct timespec t0, t1, t2;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        ccso_search(P.pcs, pd, 1500, ext, rec, org);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        const double ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;
+        best            = ms < best ? ms : best;
+        if (bd == 8) {
+            load_recon8(&P, rec, W, H);
+            pd_init(pd);
+            ccso_frame(P.recon, P.pcs, pd, ext);
+            clock_gettime(CLOCK_MONOTONIC, &t2);
+            const double ma = (t2.tv_sec - t1.tv_sec) * 1e3 + (t2.tv_nsec - t1.tv_nsec) * 1e-6;
+            best_apply      = ma < best_apply ? ma : best_apply;
+        }
+        printf("rep %d: search %.1f ms enable %d %d %d\n", k, ms, P.ppcs->frm_hdr.ccso_info.ccso_enable[0],
+               P.ppcs->frm_hdr.ccso_info.ccso_enable[1], P.ppcs->frm_hdr.ccso_info.ccso_enable[2]);
+    }
+    printf("{\"w\": %d, \"h\": %d, \"bd\": %d, \"search_ms\": %.3f, \"apply_ms\": %.3f, \"threads\": 1, "
+           "\"kernels\": \"%s\"}\n", W, H, bd, best, bd == 8 ? best_apply : -1.0, avx2 ? "avx2" : "c");
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "bench"))
+        return bench(argc > 2 ? atoi(argv[2]) : 1920, argc > 3 ? atoi(argv[3]) : 1080, argc > 4 ? atoi(argv[4]) : 8,
+                     argc > 5 ? atoi(argv[5]) : 1, argc > 6 && !strcmp(argv[6], "avx2"));
     const char *dir = argc > 1 ? argv[1] : "tests/golden";
     char        path[512];
     snprintf(path, sizeof path, "%s/ccso.bin", dir);

@@ -94,75 +94,118 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // ---------------------------------------------------------------------------------------------
 // pass 1: histograms (grid: nbp * strips, NKIND)
 // ---------------------------------------------------------------------------------------------
-struct BinsArgs {
-    const uint16_t *ext, *org, *rec;
-    Bin            *bins; // [NKIND][nbp][NBIN]
-    Geo             g;
-    int32_t         bd, strips;
+struct Planes { // the planes of one search launch: plane = plane0 + blockIdx.z (final: + blockIdx.x)
+    Geo               g[3];
+    const uint16_t   *ext, *org[3], *rec[3];
+    Bin              *bins[3];  // [NKIND][nbp][NBIN]
+    Mom              *mom[3];   // [NCOMBO + 1][nbp][NFINE]
+    double           *cost[3];  // [NCFG]
+    int8_t           *lut[3];   // [NCFG][NFINE] offset of each merged class
+    uint8_t          *ctrl[3];  // [NCFG][nb]
+    SvtGpuCcsoParams *params[3];
+    uint8_t          *flags[3];
+    int32_t           bd, rdmult, plane0;
 };
 
-__global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(BinsArgs a) {
-    __shared__ uint32_t s_n[NBIN], s_s1[NBIN];
-    __shared__ unsigned long long s_s2[NBIN], s_corr[8][NBIN];
-    const int  tid = threadIdx.x, kind = blockIdx.y;
-    const Geo &g = a.g;
-    const int  pb = blockIdx.x / a.strips, strip = blockIdx.x % a.strips;
+// LDS cells: the count and the squared-error sum share one 64-bit word (count << 50 | sum of squares: a workgroup sees
+// at most 32 x 256 samples and 12-bit errors, so neither field overflows) and the error sum is kept biased by +4096 per
+// sample (non-negative, < 2^26); every sample costs two LDS atomics, fewer where neighbours share a bin (RUN below)
+constexpr int      NQ_SHIFT = 50;
+constexpr uint32_t S1_BIAS  = 4096;
+constexpr int      RUN      = 8; // consecutive samples per thread: runs of one bin are summed in registers first
+
+__global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(Planes a) {
+    __shared__ unsigned long long s_nq[NBIN], s_corr[8][NBIN];
+    __shared__ uint32_t           s_s1[NBIN];
+    const int  tid = threadIdx.x, kind = blockIdx.y, pl = a.plane0 + blockIdx.z;
+    const Geo &g = a.g[pl];
+    const int  strips = g.bs / STRIP;
+    if ((int)blockIdx.x >= g.nbp * strips) return;
+    const int  pb = blockIdx.x / strips, strip = blockIdx.x % strips;
+    const uint16_t *org = a.org[pl], *rec = a.rec[pl];
     const int  bx = pb % g.nbx, by = pb / g.nbx;
     const int  x0 = bx * g.bs, y0 = by * g.bs + strip * STRIP;
     const int  nbins = kind < NSUP ? NBIN : 128;
     for (int i = tid; i < nbins; i += BTHREADS) {
-        s_n[i] = 0, s_s1[i] = 0, s_s2[i] = 0;
+        s_nq[i] = 0, s_s1[i] = 0;
         for (int o = 0; o < 8; o++) s_corr[o][i] = 0;
     }
     __syncthreads();
     const int rows = min(STRIP, min(g.bs - strip * STRIP, g.ph - y0)), cols = min(g.bs, g.pw - x0);
     if (rows > 0 && cols > 0) {
-        const int es = g.w + 2 * PAD, maxv = (1 << a.bd) - 1;
+        const int es = g.w + 2 * PAD, maxv = (1 << a.bd) - 1, n_px = rows * cols;
         int       loc[2];
         sample_pos(loc, es, kind < NSUP ? kind : 0);
         const int sh = kind < NSUP ? a.bd - 3 : a.bd - 7;
-        for (int i = tid; i < rows * cols; i += BTHREADS) {
-            const int       yy = y0 + i / cols, xx = x0 + i % cols;
-            const uint16_t *c  = a.ext + (size_t)(PAD + (yy << g.ss)) * es + PAD + (xx << g.ss);
-            const int       cv = c[0];
-            const int       o  = a.org[(size_t)yy * g.w + xx], r = a.rec[(size_t)yy * g.w + xx], e = o - r;
-            int             bin = cv >> sh;
-            if (kind < NSUP) bin = (bin * 9 + bucket(c[loc[0]] - cv)) * 9 + bucket(c[loc[1]] - cv);
-            atomicAdd(&s_n[bin], 1u);
-            atomicAdd(&s_s1[bin], (uint32_t)e);
-            atomicAdd(&s_s2[bin], (unsigned long long)(e * e));
-            if (r < 10 || r > maxv - 7)
-                for (int k = 0; k < 8; k++) {
-                    const int f = clampi(r + kOff[k], 0, maxv), d = o - f, u = e - kOff[k];
-                    if (d * d != u * u) atomicAdd(&s_corr[k][bin], (unsigned long long)(long long)(d * d - u * u));
+        for (int i0 = tid * RUN; i0 < n_px; i0 += BTHREADS * RUN) {
+            int                cur = -1;
+            unsigned long long nq  = 0;
+            uint32_t           s1  = 0;
+            for (int j = 0; j < RUN && i0 + j < n_px; j++) {
+                const int       yy = y0 + (i0 + j) / cols, xx = x0 + (i0 + j) % cols;
+                const uint16_t *c  = a.ext + (size_t)(PAD + (yy << g.ss)) * es + PAD + (xx << g.ss);
+                const int       cv = c[0];
+                const int       o = org[(size_t)yy * g.w + xx], r = rec[(size_t)yy * g.w + xx], e = o - r;
+                int             bin = cv >> sh;
+                if (kind < NSUP) bin = (bin * 9 + bucket(c[loc[0]] - cv)) * 9 + bucket(c[loc[1]] - cv);
+                if (bin != cur) {
+                    if (cur >= 0) atomicAdd(&s_nq[cur], nq), atomicAdd(&s_s1[cur], s1);
+                    cur = bin, nq = 0, s1 = 0;
                 }
+                nq += (1ull << NQ_SHIFT) + (unsigned long long)(e * e);
+                s1 += (uint32_t)(e + (int)S1_BIAS);
+                if (r < 10 || r > maxv - 7)
+                    for (int k = 0; k < 8; k++) {
+                        const int f = clampi(r + kOff[k], 0, maxv), d = o - f, u = e - kOff[k];
+                        if (d * d != u * u) atomicAdd(&s_corr[k][bin], (unsigned long long)(long long)(d * d - u * u));
+                    }
+            }
+            if (cur >= 0) atomicAdd(&s_nq[cur], nq), atomicAdd(&s_s1[cur], s1);
         }
     }
     __syncthreads();
-    Bin *out = a.bins + ((size_t)kind * g.nbp + pb) * NBIN;
+    Bin *out = a.bins[pl] + ((size_t)kind * g.nbp + pb) * NBIN;
     for (int i = tid; i < nbins; i += BTHREADS) {
-        if (!s_n[i]) continue;
-        atomicAdd(&out[i].n, s_n[i]);
-        atomicAdd(&out[i].s1, s_s1[i]);
-        atomicAdd((unsigned long long *)&out[i].s2, s_s2[i]);
+        const unsigned long long nq = s_nq[i];
+        const uint32_t           n  = (uint32_t)(nq >> NQ_SHIFT);
+        if (!n) continue;
+        atomicAdd(&out[i].n, n);
+        atomicAdd(&out[i].s1, s_s1[i] - S1_BIAS * n);
+        atomicAdd((unsigned long long *)&out[i].s2, nq & ((1ull << NQ_SHIFT) - 1));
         for (int k = 0; k < 8; k++)
             if (s_corr[k][i]) atomicAdd((unsigned long long *)&out[i].corr[k], s_corr[k][i]);
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// pass 2: moments per combination (grid: nbp, NCOMBO + 1; block NFINE)
+// pass 2: moments per combination (grid: nbp, NKIND; the support's 648 bins of one block staged in LDS once, its 8
+// (quantization step, classifier) combinations x 72 fine classes summed from there)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NFINE) void ccso_merge_kernel(const Bin *bins, Mom *mom, int nbp) {
-    const int f = threadIdx.x, pb = blockIdx.x, combo = blockIdx.y;
-    uint32_t  n = 0, s1 = 0;
-    uint64_t  s2 = 0, corr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (combo < NCOMBO) {
-        const int sup = combo >> 3, qi = (combo >> 1) & 3, clf = combo & 1;
-        const int L   = qi == 0 ? 2 : qi == 1 ? 1 : qi == 2 ? 3 : 4; // quant_sz {16, 8, 32, 64}
-        if (f < 72) {
+__global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
+    __shared__ Bin s_bin[NBIN];
+    const int tid = threadIdx.x, pb = blockIdx.x, kind = blockIdx.y, pl = a.plane0 + blockIdx.z, nbp = a.g[pl].nbp;
+    if (pb >= nbp) return;
+    const Bin *bins = a.bins[pl];
+    Mom       *mom  = a.mom[pl];
+    const int  nbins = kind < NSUP ? NBIN : 128;
+    const Bin *src   = bins + ((size_t)kind * nbp + pb) * NBIN;
+    {
+        const uint64_t *s = (const uint64_t *)src;
+        uint64_t       *d = (uint64_t *)s_bin;
+        for (int i = tid; i < nbins * (int)(sizeof(Bin) / 8); i += 256) d[i] = s[i];
+    }
+    __syncthreads();
+    const int nout = kind < NSUP ? 8 * 72 : 128;
+    for (int o = tid; o < nout; o += 256) {
+        uint32_t n = 0, s1 = 0;
+        uint64_t s2 = 0, corr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int      combo, f;
+        if (kind < NSUP) {
+            const int qc = o / 72, qi = qc >> 1, clf = qc & 1;
+            const int L  = qi == 0 ? 2 : qi == 1 ? 1 : qi == 2 ? 3 : 4; // quant_sz {16, 8, 32, 64}
+            f = o % 72, combo = (kind * 4 + qi) * 2 + clf;
             const int  band = f / 9, c0 = (f / 3) % 3, c1 = f % 3;
-            const Bin *b    = bins + ((size_t)sup * nbp + pb) * NBIN + band * 81;
+            const Bin *b    = s_bin + band * 81;
             for (int b0 = 0; b0 < 9; b0++) {
                 if (bucket_class(b0, L, clf) != c0) continue;
                 for (int b1 = 0; b1 < 9; b1++) {
@@ -173,30 +216,23 @@ __global__ __launch_bounds__(NFINE) void ccso_merge_kernel(const Bin *bins, Mom 
                     for (int k = 0; k < 8; k++) corr[k] += x.corr[k];
                 }
             }
+        } else {
+            f = o, combo = NCOMBO;
+            const Bin &x = s_bin[f];
+            n = x.n, s1 = x.s1, s2 = x.s2;
+            for (int k = 0; k < 8; k++) corr[k] = x.corr[k];
         }
-    } else {
-        const Bin &x = bins[((size_t)NSUP * nbp + pb) * NBIN + f];
-        n = x.n, s1 = x.s1, s2 = x.s2;
-        for (int k = 0; k < 8; k++) corr[k] = x.corr[k];
+        Mom          &m  = mom[((size_t)combo * nbp + pb) * NFINE + f];
+        const int64_t S1 = (int32_t)s1;
+        m.n = n, m.s1 = s1;
+        for (int k = 0; k < 8; k++)
+            m.ssd[k] = s2 - (uint64_t)(2 * kOff[k] * S1) + (uint64_t)(kOff[k] * kOff[k]) * n + corr[k];
     }
-    Mom      &m  = mom[((size_t)combo * nbp + pb) * NFINE + f];
-    const int64_t S1 = (int32_t)s1;
-    m.n = n, m.s1 = s1;
-    for (int k = 0; k < 8; k++)
-        m.ssd[k] = s2 - (uint64_t)(2 * kOff[k] * S1) + (uint64_t)(kOff[k] * kOff[k]) * n + corr[k];
 }
 
 // ---------------------------------------------------------------------------------------------
 // pass 3: the training loop of every configuration (grid NCFG; one wave each)
 // ---------------------------------------------------------------------------------------------
-struct TrainArgs {
-    const Mom *mom;
-    double    *cost;  // [NCFG]
-    int8_t    *lut;   // [NCFG][128] offset of each merged class
-    uint8_t   *ctrl;  // [NCFG][nb]
-    Geo        g;
-    int32_t    bd, rdmult;
-};
 
 // RDCOST_DBL_WITH_NATIVE_BD_DIST1 (EbPickccso.h:9) over RDCOST_DBL (EbRestoration.h:346); -ffp-contract=off
 __device__ __host__ inline double rdcost(int rdmult, int bits, uint64_t dist, int bd) {
@@ -224,29 +260,30 @@ __device__ __forceinline__ int lut_bits_of(int k) {
     return pos[k];
 }
 
-__global__ __launch_bounds__(64) void ccso_train_kernel(TrainArgs a) {
+constexpr int TT = 512; // threads per configuration: the moment loads of a training pass spread over 8 waves
+
+__global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
     __shared__ uint8_t            s_ctrl[MAXNB], s_best[MAXNB];
     __shared__ unsigned long long s_unf[MAXNB], s_trn[MAXNB];
     __shared__ uint32_t           s_err[NFINE], s_cnt[NFINE];
     __shared__ uint8_t            s_off[NFINE], s_boff[NFINE];
     __shared__ unsigned long long s_dist;
     __shared__ int                s_any, s_bits;
-    const int  lane = threadIdx.x, cfg = blockIdx.x;
-    const Geo &g    = a.g;
+    const int  tid = threadIdx.x, cfg = blockIdx.x, pl = a.plane0 + blockIdx.z;
+    const Geo &g   = a.g[pl];
     const int  bo = cfg >= NCOMBO * 4, k = bo ? cfg - NCOMBO * 4 : cfg & 3, combo = bo ? NCOMBO : cfg >> 2;
     const int  clf = bo ? 0 : combo & 1, edges = bo ? 1 : (clf ? 2 : 3), F = bo ? 128 : 72;
     const int  nb = g.nb, nbp = g.nbp, nbands = 1 << k;
-    const Mom *mom = a.mom + (size_t)combo * nbp * NFINE;
+    const Mom *mom = a.mom[pl] + (size_t)combo * nbp * NFINE;
     // the merged class of a fine class at this band count
     auto merged = [&](int f) { return bo ? f >> (7 - k) : ((f / 9) >> (3 - k)) * 9 + f % 9; };
     auto blk2d  = [&](int p) { return (p / g.nbx) * g.nhfb + p % g.nbx; };
-    for (int i = lane; i < nb; i += 64) s_unf[i] = 0, s_ctrl[i] = 1, s_best[i] = 0;
-    if (lane < NFINE / 2) s_boff[lane] = 4, s_boff[lane + 64] = 4;
+    for (int i = tid; i < nb; i += TT) s_unf[i] = 0, s_ctrl[i] = 1, s_best[i] = 0;
+    if (tid < NFINE) s_boff[tid] = 4;
     __syncthreads();
-    for (int p = lane; p < nbp; p += 64) { // compute_distortion of the unfiltered plane
-        unsigned long long u = 0;
-        for (int f = 0; f < F; f++) u += mom[(size_t)p * NFINE + f].ssd[4];
-        s_unf[blk2d(p)] = u;
+    for (int i = tid; i < nbp * F; i += TT) { // compute_distortion of the unfiltered plane
+        const unsigned long long u = mom[(size_t)(i / F) * NFINE + i % F].ssd[4];
+        if (u) atomicAdd(&s_unf[blk2d(i / F)], u);
     }
     __syncthreads();
     double best = DBL_MAX, prev = DBL_MAX;
@@ -254,45 +291,44 @@ __global__ __launch_bounds__(64) void ccso_train_kernel(TrainArgs a) {
     for (int iter = 0;; iter++) {
         int improvement = 0;
         if (enable) { // ccso_compute_class_err + derive_lut_offset
-            if (lane < NFINE / 2) s_err[lane] = s_err[lane + 64] = 0, s_cnt[lane] = s_cnt[lane + 64] = 0;
+            if (tid < NFINE) s_err[tid] = 0, s_cnt[tid] = 0;
             __syncthreads();
-            for (int i = lane; i < nbp * F; i += 64) {
+            for (int i = tid; i < nbp * F; i += TT) {
                 const int p = i / F, f = i % F;
                 if (!s_ctrl[p]) continue; // the class errors of block p pair with the flag of index p (:211-233)
                 const Mom &m = mom[(size_t)p * NFINE + f];
-                if (!m.n) continue;
+                const uint32_t n = m.n;
+                if (!n) continue;
                 atomicAdd(&s_err[merged(f)], m.s1);
-                atomicAdd(&s_cnt[merged(f)], m.n);
+                atomicAdd(&s_cnt[merged(f)], n);
             }
             __syncthreads();
-            for (int c = lane; c < NFINE; c += 64) s_off[c] = (uint8_t)lut_offset_index((int32_t)s_err[c], (int32_t)s_cnt[c]);
-            __syncthreads();
+            if (tid < NFINE) s_off[tid] = (uint8_t)lut_offset_index((int32_t)s_err[tid], (int32_t)s_cnt[tid]);
         }
-        for (int i = lane; i < nb; i += 64) s_trn[i] = 0;
-        if (lane == 0) s_dist = 0, s_any = 0, s_bits = 0;
+        for (int i = tid; i < nb; i += TT) s_trn[i] = 0;
+        if (tid == 0) s_dist = 0, s_any = 0, s_bits = 0;
         __syncthreads();
-        for (int i = lane; i < nbp * F; i += 64) { // the filtered plane's block SSDs
-            const int p = i / F, f = i % F;
-            atomicAdd(&s_trn[blk2d(p)], mom[(size_t)p * NFINE + f].ssd[s_off[merged(f)]]);
+        for (int i = tid; i < nbp * F; i += TT) { // the filtered plane's block SSDs
+            const int                p = i / F, f = i % F;
+            const unsigned long long v = mom[(size_t)p * NFINE + f].ssd[s_off[merged(f)]];
+            if (v) atomicAdd(&s_trn[blk2d(p)], v);
         }
         __syncthreads();
         if (enable) { // derive_blk_md: the rate it sums is never read (EbPickccso.c:666-687)
             unsigned long long d = 0;
             int                any = 0;
-            for (int i = lane; i < nb; i += 64) {
+            for (int i = tid; i < nb; i += TT) {
                 const int on = s_trn[i] < s_unf[i];
                 s_ctrl[i]    = (uint8_t)on;
                 d += on ? s_trn[i] : s_unf[i];
                 any |= on;
             }
-            atomicAdd(&s_dist, d);
+            if (d) atomicAdd(&s_dist, d);
             if (any) atomicOr(&s_any, 1);
-            int bits = 0;
-            for (int c = lane; c < NFINE; c += 64) {
-                const int band = bo ? c : c / 9, d0 = bo ? 0 : (c / 3) % 3, d1 = bo ? 0 : c % 3;
-                if (band < nbands && d0 < edges && d1 < edges) bits += lut_bits_of(s_off[c]);
+            if (tid < NFINE) {
+                const int c = tid, band = bo ? c : c / 9, d0 = bo ? 0 : (c / 3) % 3, d1 = bo ? 0 : c % 3;
+                if (band < nbands && d0 < edges && d1 < edges) atomicAdd(&s_bits, lut_bits_of(s_off[c]));
             }
-            atomicAdd(&s_bits, bits);
         }
         __syncthreads();
         enable = enable && s_any;
@@ -302,73 +338,78 @@ __global__ __launch_bounds__(64) void ccso_train_kernel(TrainArgs a) {
             if (cost < prev) prev = cost, improvement = 1;
             if (cost < best) {
                 best = cost;
-                for (int c = lane; c < NFINE; c += 64) s_boff[c] = s_off[c];
-                for (int i = lane; i < nb; i += 64) s_best[i] = s_ctrl[i];
+                if (tid < NFINE) s_boff[tid] = s_off[tid];
+                for (int i = tid; i < nb; i += TT) s_best[i] = s_ctrl[i];
             }
         }
         __syncthreads();
         if (!improvement || iter + 1 > 15) break; // CCSO_MAX_ITERATIONS (EbPickccso.h:7)
     }
-    if (lane == 0) a.cost[cfg] = best;
-    for (int c = lane; c < NFINE; c += 64) a.lut[(size_t)cfg * NFINE + c] = (int8_t)kOff[s_boff[c]];
-    for (int i = lane; i < nb; i += 64) a.ctrl[(size_t)cfg * nb + i] = s_best[i];
+    if (tid == 0) a.cost[pl][cfg] = best;
+    if (tid < NFINE) a.lut[pl][(size_t)cfg * NFINE + tid] = (int8_t)kOff[s_boff[tid]];
+    for (int i = tid; i < nb; i += TT) a.ctrl[pl][(size_t)cfg * nb + i] = s_best[i];
 }
 
 // ---------------------------------------------------------------------------------------------
 // pass 4: the plane's choice (one workgroup)
 // ---------------------------------------------------------------------------------------------
-struct FinalArgs {
-    const Mom        *mom;
-    const double     *cost;
-    const int8_t     *lut;
-    const uint8_t    *ctrl;
-    SvtGpuCcsoParams *params;
-    uint8_t          *flags;
-    Geo               g;
-    int32_t           bd, rdmult;
-};
 
-__global__ __launch_bounds__(64) void ccso_final_kernel(FinalArgs a) {
+__global__ __launch_bounds__(256) void ccso_final_kernel(Planes a) {
     __shared__ int                s_win;
     __shared__ unsigned long long s_unf;
-    const int lane = threadIdx.x, nb = a.g.nb;
+    __shared__ double             s_c[256];
+    __shared__ int                s_i[256];
+    const int         lane = threadIdx.x, pl = a.plane0 + blockIdx.x, nb = a.g[pl].nb;
+    const Mom        *mom  = a.mom[pl];
+    const double     *cost = a.cost[pl];
+    SvtGpuCcsoParams *prm  = a.params[pl];
+    uint8_t          *flg  = a.flags[pl];
     if (lane == 0) s_unf = 0;
     __syncthreads();
     unsigned long long u = 0;
-    for (int i = lane; i < a.g.nbp * 72; i += 64) u += a.mom[(size_t)(i / 72) * NFINE + i % 72].ssd[4];
+    for (int i = lane; i < a.g[pl].nbp * 72; i += 256) u += mom[(size_t)(i / 72) * NFINE + i % 72].ssd[4];
     atomicAdd(&s_unf, u);
+    // the reference's loop order (EbPickccso.c:550-578) keeps the first strict minimum: the smallest cost, earliest
+    // configuration among equals
+    double c_min = DBL_MAX;
+    int    i_min = -1;
+    for (int c = lane; c < NCFG; c += 256)
+        if (cost[c] < c_min) c_min = cost[c], i_min = c;
+    s_c[lane] = c_min, s_i[lane] = i_min;
     __syncthreads();
-    if (lane == 0) {
-        double fin = DBL_MAX;
-        int    win = -1;
-        for (int c = 0; c < NCFG; c++)
-            if (a.cost[c] < fin) fin = a.cost[c], win = c; // the loop order of EbPickccso.c:550-578
-        if (rdcost(a.rdmult, 1, s_unf, a.bd) < fin) win = -1;
-        s_win = win;
+    for (int w = 128; w > 0; w >>= 1) {
+        if (lane < w) {
+            const double c2 = s_c[lane + w];
+            const int    i2 = s_i[lane + w];
+            if (i2 >= 0 && (s_i[lane] < 0 || c2 < s_c[lane] || (c2 == s_c[lane] && i2 < s_i[lane])))
+                s_c[lane] = c2, s_i[lane] = i2;
+        }
+        __syncthreads();
     }
+    if (lane == 0) s_win = (s_i[0] >= 0 && !(rdcost(a.rdmult, 1, s_unf, a.bd) < s_c[0])) ? s_i[0] : -1;
     __syncthreads();
     const int win = s_win;
-    uint8_t  *P   = (uint8_t *)a.params;
-    for (int i = lane; i < (int)sizeof(SvtGpuCcsoParams); i += 64) P[i] = 0;
+    uint8_t  *P   = (uint8_t *)prm;
+    for (int i = lane; i < (int)sizeof(SvtGpuCcsoParams); i += 256) P[i] = 0;
     __syncthreads();
     if (win < 0) {
-        for (int i = lane; i < nb; i += 64) a.flags[i] = 0;
+        for (int i = lane; i < nb; i += 256) flg[i] = 0;
         return;
     }
     const int bo = win >= NCOMBO * 4, k = bo ? win - NCOMBO * 4 : win & 3, combo = win >> 2;
     if (lane == 0) {
-        a.params->enable = 1, a.params->bo_only = (uint8_t)bo, a.params->max_band_log2 = (uint8_t)k;
-        a.params->quant_idx          = (uint8_t)(bo ? 0 : (combo >> 1) & 3);
-        a.params->ext_filter_support = (uint8_t)(bo ? 0 : combo >> 3);
-        a.params->edge_clf           = (uint8_t)(bo ? 0 : combo & 1);
+        prm->enable = 1, prm->bo_only = (uint8_t)bo, prm->max_band_log2 = (uint8_t)k;
+        prm->quant_idx          = (uint8_t)(bo ? 0 : (combo >> 1) & 3);
+        prm->ext_filter_support = (uint8_t)(bo ? 0 : combo >> 3);
+        prm->edge_clf           = (uint8_t)(bo ? 0 : combo & 1);
     }
     const int edges = bo ? 1 : ((combo & 1) ? 2 : 3);
-    for (int c = lane; c < NFINE; c += 64) {
+    for (int c = lane; c < NFINE; c += 256) {
         const int band = bo ? c : c / 9, d0 = bo ? 0 : (c / 3) % 3, d1 = bo ? 0 : c % 3;
         if (band < (1 << k) && d0 < edges && d1 < edges)
-            a.params->filter_offset[(band << 4) + (d0 << 2) + d1] = a.lut[(size_t)win * NFINE + c];
+            prm->filter_offset[(band << 4) + (d0 << 2) + d1] = a.lut[pl][(size_t)win * NFINE + c];
     }
-    for (int i = lane; i < nb; i += 64) a.flags[i] = a.ctrl[(size_t)win * nb + i];
+    for (int i = lane; i < nb; i += 256) flg[i] = a.ctrl[pl][(size_t)win * nb + i];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -409,11 +450,11 @@ __global__ __launch_bounds__(256) void ccso_extend_kernel(const T *luma, int str
 struct SvtGpuCcsoState {
     SvtGpuContext    *ctx;
     int32_t           width, height, nbp_max, nb_max;
-    Bin              *bins;
-    Mom              *mom;
-    double           *cost;
-    int8_t           *lut;
-    uint8_t          *ctrl;
+    Bin              *bins; // per plane: [3][NKIND][nbp_max][NBIN] (the three planes' searches run in one launch)
+    Mom              *mom;  // [3][NCOMBO + 1][nbp_max][NFINE]
+    double           *cost; // [3][NCFG]
+    int8_t           *lut;  // [3][NCFG][NFINE]
+    uint8_t          *ctrl; // [3][NCFG][nb_max]
     SvtGpuCcsoParams *params; // [3] the planes' current parameters (device)
     uint8_t          *flags;  // [3][nb_max]
 };
@@ -448,10 +489,11 @@ extern "C" int svtgpu_ccso_state_create(SvtGpuContext *ctx, int32_t width, int32
     if (nb > MAXNB) return SVTGPU_ERR_UNSUPPORTED;
     SvtGpuCcsoState *s = new SvtGpuCcsoState();
     s->ctx = ctx, s->width = width, s->height = height, s->nbp_max = nbp, s->nb_max = nb;
-    const size_t nbins = (size_t)NKIND * nbp * NBIN, nmom = (size_t)(NCOMBO + 1) * nbp * NFINE;
+    const size_t nbins = (size_t)3 * NKIND * nbp * NBIN, nmom = (size_t)3 * (NCOMBO + 1) * nbp * NFINE;
     if (hipMalloc(&s->bins, nbins * sizeof(Bin)) != hipSuccess || hipMalloc(&s->mom, nmom * sizeof(Mom)) != hipSuccess ||
-        hipMalloc(&s->cost, NCFG * sizeof(double)) != hipSuccess || hipMalloc(&s->lut, NCFG * NFINE) != hipSuccess ||
-        hipMalloc(&s->ctrl, (size_t)NCFG * nb) != hipSuccess ||
+        hipMalloc(&s->cost, 3 * NCFG * sizeof(double)) != hipSuccess ||
+        hipMalloc(&s->lut, (size_t)3 * NCFG * NFINE) != hipSuccess ||
+        hipMalloc(&s->ctrl, (size_t)3 * NCFG * nb) != hipSuccess ||
         hipMalloc(&s->params, 3 * sizeof(SvtGpuCcsoParams)) != hipSuccess ||
         hipMalloc(&s->flags, (size_t)3 * nb) != hipSuccess) {
         svtgpu_ccso_state_destroy(s);
@@ -473,34 +515,60 @@ extern "C" void svtgpu_ccso_state_destroy(SvtGpuCcsoState *s) {
     delete s;
 }
 
+namespace {
+// the searches of planes [p0, p0 + n) in one launch per pass (their kernels are latency-bound: side by side they share
+// the device instead of running one after another)
+int launch_search(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const *org, const uint16_t *const *rec,
+                  int p0, int n, int32_t bd, int32_t rdmult, hipStream_t st) {
+    Planes a{};
+    a.ext = ext, a.bd = bd, a.rdmult = rdmult, a.plane0 = p0;
+    int gx = 0, gm = 0;
+    for (int p = 0; p < 3; p++) {
+        a.g[p]      = geo_of(s->width, s->height, p);
+        a.org[p]    = p >= p0 && p < p0 + n ? org[p - p0] : nullptr;
+        a.rec[p]    = p >= p0 && p < p0 + n ? rec[p - p0] : nullptr;
+        a.bins[p]   = s->bins + (size_t)p * NKIND * s->nbp_max * NBIN;
+        a.mom[p]    = s->mom + (size_t)p * (NCOMBO + 1) * s->nbp_max * NFINE;
+        a.cost[p]   = s->cost + (size_t)p * NCFG;
+        a.lut[p]    = s->lut + (size_t)p * NCFG * NFINE;
+        a.ctrl[p]   = s->ctrl + (size_t)p * NCFG * s->nb_max;
+        a.params[p] = s->params + p;
+        a.flags[p]  = s->flags + (size_t)p * s->nb_max;
+        if (p >= p0 && p < p0 + n) gx = std::max(gx, a.g[p].nbp * (a.g[p].bs / STRIP)), gm = std::max(gm, a.g[p].nbp);
+    }
+    HIP_TRY(hipMemsetAsync(a.bins[p0], 0, (size_t)n * NKIND * s->nbp_max * NBIN * sizeof(Bin), st));
+    ccso_bins_kernel<<<dim3(gx, NKIND, n), BTHREADS, 0, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    ccso_merge_kernel<<<dim3(gm, NKIND, n), 256, 0, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    ccso_train_kernel<<<dim3(NCFG, 1, n), TT, 0, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    ccso_final_kernel<<<n, 256, 0, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    return SVTGPU_OK;
+}
+
+int read_result(SvtGpuCcsoState *s, int plane, SvtGpuCcsoParams *params_out, uint8_t *flags_out, hipStream_t st) {
+    const Geo g = geo_of(s->width, s->height, plane);
+    if (params_out)
+        HIP_TRY(hipMemcpyAsync(params_out, s->params + plane, sizeof(SvtGpuCcsoParams), hipMemcpyDeviceToHost, st));
+    if (flags_out)
+        HIP_TRY(hipMemcpyAsync(flags_out, s->flags + (size_t)plane * s->nb_max, g.nb, hipMemcpyDeviceToHost, st));
+    svtgpu_count_xfer(1, (params_out ? sizeof(SvtGpuCcsoParams) : 0) + (flags_out ? g.nb : 0));
+    return SVTGPU_OK;
+}
+} // namespace
+
 extern "C" int svtgpu_ccso_search_plane(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *org,
                                         const uint16_t *rec, int32_t plane, int32_t bit_depth, int32_t rdmult,
                                         SvtGpuCcsoParams *params_out, uint8_t *flags_out, void *stream) {
     if (!s || !ext || !org || !rec || plane < 0 || plane > 2 || bit_depth < 8 || bit_depth > 12 || rdmult < 0)
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = pick_stream(s->ctx, stream);
-    const Geo   g  = geo_of(s->width, s->height, plane);
-    const int   strips = g.bs / STRIP;
-    HIP_TRY(hipMemsetAsync(s->bins, 0, (size_t)NKIND * g.nbp * NBIN * sizeof(Bin), st));
-    BinsArgs ba{ext, org, rec, s->bins, g, bit_depth, strips};
-    ccso_bins_kernel<<<dim3(g.nbp * strips, NKIND), BTHREADS, 0, st>>>(ba);
-    HIP_TRY(hipGetLastError());
-    ccso_merge_kernel<<<dim3(g.nbp, NCOMBO + 1), NFINE, 0, st>>>(s->bins, s->mom, g.nbp);
-    HIP_TRY(hipGetLastError());
-    TrainArgs ta{s->mom, s->cost, s->lut, s->ctrl, g, bit_depth, rdmult};
-    ccso_train_kernel<<<NCFG, 64, 0, st>>>(ta);
-    HIP_TRY(hipGetLastError());
-    FinalArgs fa{s->mom, s->cost, s->lut, s->ctrl, s->params + plane, s->flags + (size_t)plane * s->nb_max, g,
-                 bit_depth, rdmult};
-    ccso_final_kernel<<<1, 64, 0, st>>>(fa);
-    HIP_TRY(hipGetLastError());
+    if (int rc = launch_search(s, ext, &org, &rec, plane, 1, bit_depth, rdmult, st)) return rc;
     if (params_out || flags_out) {
-        if (params_out)
-            HIP_TRY(hipMemcpyAsync(params_out, s->params + plane, sizeof(SvtGpuCcsoParams), hipMemcpyDeviceToHost, st));
-        if (flags_out)
-            HIP_TRY(hipMemcpyAsync(flags_out, s->flags + (size_t)plane * s->nb_max, g.nb, hipMemcpyDeviceToHost, st));
+        if (int rc = read_result(s, plane, params_out, flags_out, st)) return rc;
         HIP_TRY(hipStreamSynchronize(st));
-        svtgpu_count_xfer(1, (params_out ? sizeof(SvtGpuCcsoParams) : 0) + (flags_out ? g.nb : 0));
     }
     return SVTGPU_OK;
 }
@@ -509,16 +577,20 @@ extern "C" int svtgpu_ccso_search_frame(SvtGpuCcsoState *s, const uint16_t *ext,
                                         const uint16_t *const rec[3], int32_t bit_depth, int32_t rdmult,
                                         int32_t base_q_idx, SvtGpuCcsoParams params_out[3],
                                         uint8_t *const flags_out[3], int32_t *frame_flag, void *stream) {
-    if (!s || !org || !rec || !params_out || !frame_flag) return SVTGPU_ERR_INVALID_ARG;
+    if (!s || !ext || !org || !rec || !frame_flag || bit_depth < 8 || bit_depth > 12 || rdmult < 0)
+        return SVTGPU_ERR_INVALID_ARG;
+    for (int p = 0; p < 3; p++)
+        if (!org[p] || !rec[p]) return SVTGPU_ERR_INVALID_ARG;
     const int64_t r = (int64_t)rdmult * std::min(std::max(base_q_idx, 1), 63); // EbPickccso.c:788-793
     if (r >= INT_MAX) return 1;
+    hipStream_t st = pick_stream(s->ctx, stream);
+    if (int rc = launch_search(s, ext, org, rec, 0, 3, bit_depth, (int32_t)r, st)) return rc;
     *frame_flag = 0;
-    for (int p = 0; p < 3; p++) {
-        const int rc = svtgpu_ccso_search_plane(s, ext, org[p], rec[p], p, bit_depth, (int32_t)r, &params_out[p],
-                                                flags_out ? flags_out[p] : nullptr, stream);
-        if (rc) return rc;
-        *frame_flag |= params_out[p].enable;
-    }
+    if (!params_out) return SVTGPU_OK; // the result stays on the device (apply with params = NULL)
+    for (int p = 0; p < 3; p++)
+        if (int rc = read_result(s, p, &params_out[p], flags_out ? flags_out[p] : nullptr, st)) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int p = 0; p < 3; p++) *frame_flag |= params_out[p].enable;
     return SVTGPU_OK;
 }
 

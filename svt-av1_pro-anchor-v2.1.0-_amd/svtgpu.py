@@ -1191,8 +1191,15 @@ class CcsoState:
                                              ptr(flags), stream))
         return prm, flags
 
-    def search_frame(self, ext, org, rec, bit_depth, rdmult, base_q_idx, stream=None):
-        """ccso_search: (rc, [CcsoParams] * 3, [flags] * 3, frame_flag); rc 1 = rdmult overflow, nothing searched."""
+    def search_frame(self, ext, org, rec, bit_depth, rdmult, base_q_idx, stream=None, read=True):
+        """ccso_search: (rc, [CcsoParams] * 3, [flags] * 3, frame_flag); rc 1 = rdmult overflow, nothing searched.
+        read=False: no read-back and no host wait (rc only); the results stay on the device for apply()."""
+        if not read:
+            rc = lib().svtgpu_ccso_search_frame(self.h, ext, (_P * 3)(*org), (_P * 3)(*rec), bit_depth, rdmult,
+                                                base_q_idx, None, None, ctypes.byref(_I32(0)), stream)
+            if rc not in (0, 1):
+                check(rc)
+            return rc
         prms = (CcsoParams * 3)()
         flags = [np.zeros(self.grid(p), np.uint8) for p in range(3)]
         ff = _I32(0)

@@ -69,3 +69,29 @@ def block_cases(g):
 def sample_pos(stride, sup):
     """derive_ccso_sample_pos (EbCcso.c:204-234)"""
     return [(-stride, stride), (-stride - 1, stride + 1), (-1, 1), (stride - 1, -stride + 1), (-3, 3), (-5, 5)][sup]
+
+
+def content(w, h, bd, seed):
+    """smooth org, rec = org + a band / edge biased error (the golden generator's model, numpy)"""
+    rng = np.random.default_rng(seed)
+    maxv, sh = (1 << bd) - 1, bd - 8
+    org, rec = [], []
+    for p in range(3):
+        pw, ph = (w >> 1, h >> 1) if p else (w, h)
+        kn = rng.integers(0, 256, size=(ph // 16 + 2, pw // 16 + 2)).astype(np.float64)
+        ys, xs = np.arange(ph) / 16.0, np.arange(pw) / 16.0
+        gy, gx = np.floor(ys).astype(int), np.floor(xs).astype(int)
+        fy, fx = (ys - gy)[:, None], (xs - gx)[None, :]
+        v = (kn[gy][:, gx] * (1 - fx) * (1 - fy) + kn[gy][:, gx + 1] * fx * (1 - fy) +
+             kn[gy + 1][:, gx] * (1 - fx) * fy + kn[gy + 1][:, gx + 1] * fx * fy)
+        v[:, : pw // 8] /= 16
+        v[:, pw - pw // 8:] = 255 - (255 - v[:, pw - pw // 8:]) / 16
+        o = np.clip((v.astype(np.int64) << sh) + rng.integers(-2 << sh, 3 << sh, size=v.shape), 0, maxv)
+        gxd = np.zeros_like(o)
+        gxd[:, :-1] = o[:, 1:] - o[:, :-1]
+        e = rng.integers(-3, 4, size=o.shape) - 2 * (o > maxv * 3 // 4) + 2 * (gxd > (8 << sh)) - 2 * (gxd < -(8 << sh))
+        r = np.clip(o + (e << sh), 0, maxv)
+        org.append(full(o.astype(np.uint16), w, h))
+        rec.append(full(r.astype(np.uint16), w, h))
+    pre = np.clip(rec[0].astype(np.int64) + rng.integers(-1, 2, size=(h, w)), 0, maxv).astype(np.uint16)
+    return org, rec, pre

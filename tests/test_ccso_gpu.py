@@ -135,32 +135,6 @@ def test_search_golden(g, ctx):
         st.close()
 
 
-def _content(w, h, bd, seed):
-    """smooth org, rec = org + a band / edge biased error (the golden generator's model, numpy)"""
-    rng = np.random.default_rng(seed)
-    maxv, sh = (1 << bd) - 1, bd - 8
-    org, rec = [], []
-    for p in range(3):
-        pw, ph = (w >> 1, h >> 1) if p else (w, h)
-        kn = rng.integers(0, 256, size=(ph // 16 + 2, pw // 16 + 2)).astype(np.float64)
-        ys, xs = np.arange(ph) / 16.0, np.arange(pw) / 16.0
-        gy, gx = np.floor(ys).astype(int), np.floor(xs).astype(int)
-        fy, fx = (ys - gy)[:, None], (xs - gx)[None, :]
-        v = (kn[gy][:, gx] * (1 - fx) * (1 - fy) + kn[gy][:, gx + 1] * fx * (1 - fy) +
-             kn[gy + 1][:, gx] * (1 - fx) * fy + kn[gy + 1][:, gx + 1] * fx * fy)
-        v[:, : pw // 8] /= 16
-        v[:, pw - pw // 8:] = 255 - (255 - v[:, pw - pw // 8:]) / 16
-        o = np.clip((v.astype(np.int64) << sh) + rng.integers(-2 << sh, 3 << sh, size=v.shape), 0, maxv)
-        gxd = np.zeros_like(o)
-        gxd[:, :-1] = o[:, 1:] - o[:, :-1]
-        e = rng.integers(-3, 4, size=o.shape) - 2 * (o > maxv * 3 // 4) + 2 * (gxd > (8 << sh)) - 2 * (gxd < -(8 << sh))
-        r = np.clip(o + (e << sh), 0, maxv)
-        org.append(xc.full(o.astype(np.uint16), w, h))
-        rec.append(xc.full(r.astype(np.uint16), w, h))
-    pre = np.clip(rec[0].astype(np.int64) + rng.integers(-1, 2, size=(h, w)), 0, maxv).astype(np.uint16)
-    return org, rec, pre
-
-
 @pytest.mark.parametrize("w,h,bd,rdmult,q", [(1280, 720, 8, 1500, 80), (640, 360, 10, 900, 120),
                                              (1000, 504, 8, 50000, 40)])
 def test_search_and_apply_vs_oracle(ctx, w, h, bd, rdmult, q):
@@ -168,7 +142,7 @@ def test_search_and_apply_vs_oracle(ctx, w, h, bd, rdmult, q):
     search and the device apply of its result against the oracle's search and apply (16-bit planes for 10 bits: the
     reference's ccso_frame reads only 8-bit buffers, so the high-bit-depth apply is pinned through the oracle's
     ccso_filter_block_hbd_wo_buf_c restatement)."""
-    org, rec, pre = _content(w, h, bd, seed=w + h + bd)
+    org, rec, pre = xc.content(w, h, bd, seed=w + h + bd)
     st, ext, d_rec, rc, prms, flags, ff = _search(ctx, w, h, bd, pre, org, rec, rdmult, q)
     ext_h = oracle.ccso_extend(pre)
     orc, oprms, oflags, off = oracle.ccso_search_frame(ext_h, org, rec, bd, rdmult, q)
