@@ -109,14 +109,16 @@ struct Planes { // the planes of one search launch: plane = plane0 + blockIdx.z 
 
 // LDS cells: the count and the squared-error sum share one 64-bit word (count << 50 | sum of squares: a workgroup sees
 // at most 32 x 256 samples and 12-bit errors, so neither field overflows) and the error sum is kept biased by +4096 per
-// sample (non-negative, < 2^26); every sample costs two LDS atomics, fewer where neighbours share a bin (RUN below)
+// sample (non-negative, < 2^26); every sample costs at most two LDS atomics, fewer where lanes share a bin
 constexpr int      NQ_SHIFT = 50;
 constexpr uint32_t S1_BIAS  = 4096;
-constexpr int      RUN      = 8; // consecutive samples per thread: runs of one bin are summed in registers first
+constexpr int      RUN      = 4; // wave-wide bin groups summed per step before the per-lane atomics
+constexpr int      U        = 8; // steps whose samples are loaded together
 
 __global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(Planes a) {
-    __shared__ unsigned long long s_nq[NBIN], s_corr[8][NBIN];
+    __shared__ unsigned long long s_nq[NBIN];
     __shared__ uint32_t           s_s1[NBIN];
+    __shared__ int32_t            s_corr[8][NBIN]; // |clamped - unclamped| <= 10 * 2 * 4105 per sample: int32 per tile
     const int  tid = threadIdx.x, kind = blockIdx.y, pl = a.plane0 + blockIdx.z;
     const Geo &g = a.g[pl];
     const int  strips = g.bs / STRIP;
@@ -133,34 +135,60 @@ __global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(Planes a) {
     __syncthreads();
     const int rows = min(STRIP, min(g.bs - strip * STRIP, g.ph - y0)), cols = min(g.bs, g.pw - x0);
     if (rows > 0 && cols > 0) {
-        const int es = g.w + 2 * PAD, maxv = (1 << a.bd) - 1, n_px = rows * cols;
+        const int es = g.w + 2 * PAD, maxv = (1 << a.bd) - 1;
         int       loc[2];
         sample_pos(loc, es, kind < NSUP ? kind : 0);
         const int sh = kind < NSUP ? a.bd - 3 : a.bd - 7;
-        for (int i0 = tid * RUN; i0 < n_px; i0 += BTHREADS * RUN) {
-            int                cur = -1;
-            unsigned long long nq  = 0;
-            uint32_t           s1  = 0;
-            for (int j = 0; j < RUN && i0 + j < n_px; j++) {
-                const int       yy = y0 + (i0 + j) / cols, xx = x0 + (i0 + j) % cols;
-                const uint16_t *c  = a.ext + (size_t)(PAD + (yy << g.ss)) * es + PAD + (xx << g.ss);
-                const int       cv = c[0];
-                const int       o = org[(size_t)yy * g.w + xx], r = rec[(size_t)yy * g.w + xx], e = o - r;
-                int             bin = cv >> sh;
-                if (kind < NSUP) bin = (bin * 9 + bucket(c[loc[0]] - cv)) * 9 + bucket(c[loc[1]] - cv);
-                if (bin != cur) {
-                    if (cur >= 0) atomicAdd(&s_nq[cur], nq), atomicAdd(&s_s1[cur], s1);
-                    cur = bin, nq = 0, s1 = 0;
+        // lane-contiguous columns (coalesced loads of org / rec / the luma row), rps rows per step; the samples of U
+        // steps are loaded before any is binned, so a wave keeps 5 U loads in flight instead of waiting on each row
+        const int rps = BTHREADS / cols, col = tid % cols, row0 = tid / cols, xx = x0 + col;
+        const bool nb2 = kind < NSUP;
+        for (int rb = 0; rb < rows; rb += rps * U) { // uniform trip count: the flushes below are convergent
+            int vc[U], v0[U], v1[U], vo[U], vr[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int ry = rb + row0 + u * rps;
+                vc[u] = -1;
+                if (row0 < rps && ry < rows) {
+                    const int       yy = y0 + ry;
+                    const uint16_t *c  = a.ext + (size_t)(PAD + (yy << g.ss)) * es + PAD + (xx << g.ss);
+                    vc[u] = c[0], vo[u] = org[(size_t)yy * g.w + xx], vr[u] = rec[(size_t)yy * g.w + xx];
+                    if (nb2) v0[u] = c[loc[0]], v1[u] = c[loc[1]];
                 }
-                nq += (1ull << NQ_SHIFT) + (unsigned long long)(e * e);
-                s1 += (uint32_t)(e + (int)S1_BIAS);
-                if (r < 10 || r > maxv - 7)
-                    for (int k = 0; k < 8; k++) {
-                        const int f = clampi(r + kOff[k], 0, maxv), d = o - f, u = e - kOff[k];
-                        if (d * d != u * u) atomicAdd(&s_corr[k][bin], (unsigned long long)(long long)(d * d - u * u));
-                    }
             }
-            if (cur >= 0) atomicAdd(&s_nq[cur], nq), atomicAdd(&s_s1[cur], s1);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                int                cur = -1;
+                unsigned long long nq  = 0;
+                uint32_t           s1  = 0;
+                if (vc[u] >= 0) {
+                    const int cv = vc[u], o = vo[u], r = vr[u], e = o - r;
+                    cur = cv >> sh;
+                    if (nb2) cur = (cur * 9 + bucket(v0[u] - cv)) * 9 + bucket(v1[u] - cv);
+                    nq = (1ull << NQ_SHIFT) + (unsigned long long)(e * e);
+                    s1 = (uint32_t)(e + (int)S1_BIAS);
+                    if (r < 10 || r > maxv - 7)
+                        for (int k = 0; k < 8; k++) {
+                            const int f = clampi(r + kOff[k], 0, maxv), d = o - f, w = e - kOff[k];
+                            if (d * d != w * w) atomicAdd(&s_corr[k][cur], d * d - w * w);
+                        }
+                }
+                // lanes in one bin are summed across the wave first (smooth content puts most of a wave in a few
+                // bins: one LDS atomic per bin instead of one per lane); small groups add directly
+                unsigned long long rem = __ballot(cur >= 0);
+                for (int t = 0; t < RUN && rem; t++) {
+                    const int                b    = __builtin_amdgcn_readlane(cur, __ffsll((long long)rem) - 1);
+                    const bool               mine = cur == b;
+                    const unsigned long long m    = __ballot(mine);
+                    if (__popcll(m) < 4) break;
+                    const unsigned long long v = wave_sum_lane63(mine ? nq : 0ull);
+                    const uint32_t           w = wave_sum_u32_lane63(mine ? s1 : 0u);
+                    if ((tid & 63) == 63) atomicAdd(&s_nq[b], v), atomicAdd(&s_s1[b], w);
+                    if (mine) cur = -1;
+                    rem &= ~m;
+                }
+                if (cur >= 0) atomicAdd(&s_nq[cur], nq), atomicAdd(&s_s1[cur], s1);
+            }
         }
     }
     __syncthreads();
@@ -173,7 +201,7 @@ __global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(Planes a) {
         atomicAdd(&out[i].s1, s_s1[i] - S1_BIAS * n);
         atomicAdd((unsigned long long *)&out[i].s2, nq & ((1ull << NQ_SHIFT) - 1));
         for (int k = 0; k < 8; k++)
-            if (s_corr[k][i]) atomicAdd((unsigned long long *)&out[i].corr[k], s_corr[k][i]);
+            if (s_corr[k][i]) atomicAdd((unsigned long long *)&out[i].corr[k], (unsigned long long)(long long)s_corr[k][i]);
     }
 }
 
@@ -192,6 +220,7 @@ __global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
     {
         const uint64_t *s = (const uint64_t *)src;
         uint64_t       *d = (uint64_t *)s_bin;
+#pragma unroll 8
         for (int i = tid; i < nbins * (int)(sizeof(Bin) / 8); i += 256) d[i] = s[i];
     }
     __syncthreads();
@@ -261,6 +290,7 @@ __device__ __forceinline__ int lut_bits_of(int k) {
 }
 
 constexpr int TT = 512; // threads per configuration: the moment loads of a training pass spread over 8 waves
+constexpr int LU = 4;   // moments loaded per thread before they are accumulated
 
 __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
     __shared__ uint8_t            s_ctrl[MAXNB], s_best[MAXNB];
@@ -281,9 +311,16 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
     for (int i = tid; i < nb; i += TT) s_unf[i] = 0, s_ctrl[i] = 1, s_best[i] = 0;
     if (tid < NFINE) s_boff[tid] = 4;
     __syncthreads();
-    for (int i = tid; i < nbp * F; i += TT) { // compute_distortion of the unfiltered plane
-        const unsigned long long u = mom[(size_t)(i / F) * NFINE + i % F].ssd[4];
-        if (u) atomicAdd(&s_unf[blk2d(i / F)], u);
+    for (int i0 = tid; i0 < nbp * F; i0 += TT * LU) { // compute_distortion of the unfiltered plane
+        unsigned long long v[LU];
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const int i = i0 + u * TT;
+            v[u]        = i < nbp * F ? mom[(size_t)(i / F) * NFINE + i % F].ssd[4] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < LU; u++)
+            if (v[u]) atomicAdd(&s_unf[blk2d((i0 + u * TT) / F)], v[u]);
     }
     __syncthreads();
     double best = DBL_MAX, prev = DBL_MAX;
@@ -293,14 +330,24 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
         if (enable) { // ccso_compute_class_err + derive_lut_offset
             if (tid < NFINE) s_err[tid] = 0, s_cnt[tid] = 0;
             __syncthreads();
-            for (int i = tid; i < nbp * F; i += TT) {
-                const int p = i / F, f = i % F;
-                if (!s_ctrl[p]) continue; // the class errors of block p pair with the flag of index p (:211-233)
-                const Mom &m = mom[(size_t)p * NFINE + f];
-                const uint32_t n = m.n;
-                if (!n) continue;
-                atomicAdd(&s_err[merged(f)], m.s1);
-                atomicAdd(&s_cnt[merged(f)], n);
+            // the class errors of block p pair with the flag of index p (:211-233); LU moments loaded per round
+            for (int i0 = tid; i0 < nbp * F; i0 += TT * LU) {
+                uint32_t n[LU], e[LU];
+#pragma unroll
+                for (int u = 0; u < LU; u++) {
+                    const int i = i0 + u * TT;
+                    n[u]        = 0;
+                    if (i < nbp * F && s_ctrl[i / F]) {
+                        const Mom &m = mom[(size_t)(i / F) * NFINE + i % F];
+                        n[u] = m.n, e[u] = m.s1;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < LU; u++)
+                    if (n[u]) {
+                        const int c = merged((i0 + u * TT) % F);
+                        atomicAdd(&s_err[c], e[u]), atomicAdd(&s_cnt[c], n[u]);
+                    }
             }
             __syncthreads();
             if (tid < NFINE) s_off[tid] = (uint8_t)lut_offset_index((int32_t)s_err[tid], (int32_t)s_cnt[tid]);
@@ -308,10 +355,16 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
         for (int i = tid; i < nb; i += TT) s_trn[i] = 0;
         if (tid == 0) s_dist = 0, s_any = 0, s_bits = 0;
         __syncthreads();
-        for (int i = tid; i < nbp * F; i += TT) { // the filtered plane's block SSDs
-            const int                p = i / F, f = i % F;
-            const unsigned long long v = mom[(size_t)p * NFINE + f].ssd[s_off[merged(f)]];
-            if (v) atomicAdd(&s_trn[blk2d(p)], v);
+        for (int i0 = tid; i0 < nbp * F; i0 += TT * LU) { // the filtered plane's block SSDs
+            unsigned long long v[LU];
+#pragma unroll
+            for (int u = 0; u < LU; u++) {
+                const int i = i0 + u * TT;
+                v[u]        = i < nbp * F ? mom[(size_t)(i / F) * NFINE + i % F].ssd[s_off[merged(i % F)]] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < LU; u++)
+                if (v[u]) atomicAdd(&s_trn[blk2d((i0 + u * TT) / F)], v[u]);
         }
         __syncthreads();
         if (enable) { // derive_blk_md: the rate it sums is never read (EbPickccso.c:666-687)

@@ -413,7 +413,7 @@ _SIGS = {
     "svtgpu_ccso_search_plane": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, ctypes.POINTER(CcsoParams), _P,
                                                 _P]),
     "svtgpu_ccso_search_frame": (ctypes.c_int, [_P, _P, _P * 3, _P * 3, _I32, _I32, _I32, ctypes.POINTER(CcsoParams),
-                                                _P * 3, ctypes.POINTER(_I32), _P]),
+                                                _P, ctypes.POINTER(_I32), _P]),
     "svtgpu_ccso_apply_plane": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _I32, ctypes.POINTER(CcsoParams), _P,
                                                _P]),
     "svtgpu_compute_distortion_block": (ctypes.c_uint64, [_P, ctypes.c_int, _P, ctypes.c_int, ctypes.c_int,
