@@ -10,6 +10,7 @@
  *     if (getenv("SVT_GPU") && svtgpu_device_available()) {
  *         svtgpu_install_filter_rtcd();                   // the in-loop filter path (DLF / CDEF / LR)
  *         svtgpu_install_me_md_rtcd();                    // ME / MD distortion + frame buffers
+ *         svtgpu_install_ccso_rtcd();                     // CCSO's block kernels (an encoder that re-enables it)
  *     }
  *     ...
  *     init_fn_ptr();                                      // EbEncHandle.c:1546: av1me.c:31 COPIES the sad / variance /
@@ -83,6 +84,15 @@ static inline void svtgpu_install_filter_rtcd(void) {
     svt_av1_highbd_pixel_proj_error        = svtgpu_av1_highbd_pixel_proj_error;
     svt_aom_mse16x16                       = svtgpu_aom_mse16x16;
     svt_aom_highbd_8_mse16x16              = svtgpu_aom_highbd_8_mse16x16;
+}
+
+/* CCSO's per-block kernels (common_dsp_rtcd.h:1025-1090), for an encoder that re-enables the fork's CCSO search /
+ * apply (EbCdefProcess.c:621-623); the frame-level path is svtgpu_ccso_search_frame + svtgpu_ccso_apply_plane */
+static inline void svtgpu_install_ccso_rtcd(void) {
+    ccso_filter_block_hbd_wo_buf   = svtgpu_ccso_filter_block_hbd_wo_buf;
+    ccso_filter_block_hbd_with_buf = svtgpu_ccso_filter_block_hbd_with_buf;
+    ccso_derive_src_block          = svtgpu_ccso_derive_src_block;
+    compute_distortion_block       = svtgpu_compute_distortion_block;
 }
 
 /* ME and MD distortion (every SAD / x4d / variance / highbd variance / sub-pixel variance size, sse, the open-loop ME

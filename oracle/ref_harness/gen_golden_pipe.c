@@ -109,6 +109,7 @@ static void bind_c_kernels(void) {
 static void bind_device_kernels(void) {
     svtgpu_install_filter_rtcd();
     svtgpu_install_me_md_rtcd(); /* compiled and installed; the frame code here calls none of them */
+    svtgpu_install_ccso_rtcd();  /* likewise (CCSO is dead in this encoder) */
 }
 /* the frame-buffer functions the reference calls directly (not through RTCD): a pointer of each one's type */
 void bind_check_frame(void);

@@ -491,11 +491,18 @@ __global__ __launch_bounds__(256) void ccso_apply_kernel(const uint16_t *ext, T 
     *d             = (T)clampi(prm->filter_offset[(band << 4) + (c0 << 2) + c1] + (int)*d, 0, maxv);
 }
 
+// one wave per padded row segment of 512 samples (8 per lane, lane-contiguous)
 template <typename T>
 __global__ __launch_bounds__(256) void ccso_extend_kernel(const T *luma, int stride, int w, int h, uint16_t *ext) {
-    const int es = w + 2 * PAD, x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (x >= es || y >= h + 2 * PAD) return;
-    ext[(size_t)y * es + x] = luma[(size_t)clampi(y - PAD, 0, h - 1) * stride + clampi(x - PAD, 0, w - 1)];
+    const int es = w + 2 * PAD, y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (y >= h + 2 * PAD) return;
+    const T  *src = luma + (size_t)clampi(y - PAD, 0, h - 1) * stride;
+    uint16_t *dst = ext + (size_t)y * es;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int x = blockIdx.x * 512 + k * 64 + (threadIdx.x & 63);
+        if (x < es) dst[x] = src[clampi(x - PAD, 0, w - 1)];
+    }
 }
 
 } // namespace
@@ -524,7 +531,7 @@ extern "C" int svtgpu_ccso_extend_luma(const void *luma, int32_t bits, int32_t s
     if (!luma || !ext || width <= 0 || height <= 0 || stride < width || (bits != 8 && bits != 16))
         return SVTGPU_ERR_INVALID_ARG;
     hipStream_t st = stream ? (hipStream_t)stream : svtgpu_default_stream();
-    dim3        grid((width + 2 * PAD + 63) / 64, (height + 2 * PAD + 3) / 4);
+    dim3        grid((width + 2 * PAD + 511) / 512, (height + 2 * PAD + 3) / 4);
     if (bits == 8) ccso_extend_kernel<uint8_t><<<grid, 256, 0, st>>>((const uint8_t *)luma, stride, width, height, ext);
     else ccso_extend_kernel<uint16_t><<<grid, 256, 0, st>>>((const uint16_t *)luma, stride, width, height, ext);
     HIP_TRY(hipGetLastError());
