@@ -124,6 +124,12 @@ int   svtgpu_synchronize(SvtGpuContext *ctx, void *stream);
  * torch.cuda.Stream()'s pool of 32 streams per priority cost 1080p 10-bit at four frames in flight 23%). */
 int  svtgpu_stream_create(SvtGpuContext *ctx, int32_t priority, void **out_stream);
 void svtgpu_stream_destroy(void *stream);
+/* Plain device buffers for the pointer-level entry points (CCSO, svtgpu_convert_plane, ...) when the caller has no
+ * allocator of its own; upload / download are complete when they return (the stream is synchronized). */
+int  svtgpu_buffer_alloc(SvtGpuContext *ctx, size_t bytes, void **dev_out);
+void svtgpu_buffer_free(void *dev);
+int  svtgpu_buffer_upload(void *dev, const void *host, size_t bytes, void *stream);
+int  svtgpu_buffer_download(void *host, const void *dev, size_t bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Device-resident 4:2:0 pictures

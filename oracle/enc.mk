@@ -23,7 +23,7 @@ ENC_SRC  := $(wildcard $(S)/Lib/Common/Codec/*.c $(S)/Lib/Common/C_DEFAULT/*.c $
                        $(S)/Lib/Encoder/C_DEFAULT/*.c $(S)/Lib/Encoder/Globals/*.c $(REF)/third_party/fastfeat/*.c)
 ENC_OBJ  := $(patsubst $(REF)/%.c,$(OUT)/obj/%.o,$(ENC_SRC))
 
-all: $(OUT)/libsvtenc.so $(OUT)/enc_drop_in $(OUT)/nss/enc_drop_in
+all: $(OUT)/libsvtenc.so $(OUT)/enc_drop_in $(OUT)/nss/enc_drop_in $(OUT)/ccso/enc_drop_in
 
 $(OUT)/gen/EbVersion.h: $(S)/Lib/Common/Codec/EbVersion.h.in
 	@mkdir -p $(dir $@)
@@ -64,6 +64,27 @@ $(OUT)/nss/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_
                         $(SVTGPU)/libsvtgpu.so
 	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
 	    -L$(OUT)/nss -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../../$(SVTGPU)' \
+	    -rdynamic -ldl -lm -lpthread
+
+# The encoder with the fork's CCSO switched back on: a /tmp copy of EbCdefProcess.c with the two
+# commented calls (ccso_search / ccso_frame, :621-623) uncommented by oracle/ref_harness/with_ccso.py, compiled into
+# $(OUT)/ccso/libsvtenc.so; its harness runs the CPU CCSO (cpu mode) or, through the hooks, the device's (frame mode).
+CCSO_TMP ?= /tmp/svtgpu_enc_ccso
+$(CCSO_TMP)/EbCdefProcess.c: $(S)/Lib/Encoder/Codec/EbCdefProcess.c oracle/ref_harness/with_ccso.py
+	@mkdir -p $(dir $@)
+	python3 oracle/ref_harness/with_ccso.py $< $@
+
+$(OUT)/ccso/EbCdefProcess.o: $(CCSO_TMP)/EbCdefProcess.c $(OUT)/gen/EbVersion.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/ccso/libsvtenc.so: $(filter-out %/EbCdefProcess.o,$(ENC_OBJ)) $(OUT)/ccso/EbCdefProcess.o
+	$(CC) -shared -o $@ $^ -lm -lpthread
+
+$(OUT)/ccso/enc_drop_in: oracle/ref_harness/enc_drop_in.c oracle/ref_harness/enc_frame_hooks.c $(OUT)/ccso/libsvtenc.so \
+                         $(SVTGPU)/libsvtgpu.so
+	$(CC) -O2 -w -std=gnu99 $(INC) -Iinclude -Werror=incompatible-pointer-types $(filter %.c,$^) -o $@ \
+	    -L$(OUT)/ccso -lsvtenc -L$(SVTGPU) -lsvtgpu -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../../$(SVTGPU)' \
 	    -rdynamic -ldl -lm -lpthread
 
 clean:

@@ -38,7 +38,7 @@
 uint64_t enc_frame_hook_calls(void); /* enc_frame_hooks.c: hooked frame-level calls served by libsvtgpu */
 uint64_t enc_frame_hook_fallbacks(void); /* ... and those left to the encoder's own function */
 void     enc_frame_hooks_enable(int on);
-void     enc_frame_hook_kinds(uint64_t out[7]);
+void     enc_frame_hook_kinds(uint64_t out[10]);
 
 /* a deterministic synthetic 10-bit picture: gradients, a moving disc, texture and noise (LCG) */
 static void fill_frame(uint16_t *y, uint16_t *u, uint16_t *v, int w, int h, int k) {
@@ -194,11 +194,13 @@ int main(int argc, char **argv) {
            (unsigned long long)(rtcd || frame ? svtgpu_shim_calls() : 0), (unsigned long long)enc_frame_hook_calls(),
            (unsigned long long)enc_frame_hook_fallbacks());
     if (frame) {
-        uint64_t k[7];
+        uint64_t k[10];
         enc_frame_hook_kinds(k);
         printf("frame kinds dlf_pick %llu dlf_frame %llu cdef_pick %llu cdef_apply %llu lr_search %llu lr_apply %llu "
-               "lr_on %llu\n", (unsigned long long)k[0], (unsigned long long)k[1], (unsigned long long)k[2],
-               (unsigned long long)k[3], (unsigned long long)k[4], (unsigned long long)k[5], (unsigned long long)k[6]);
+               "lr_on %llu ccso_search %llu ccso_apply %llu ccso_on %llu\n", (unsigned long long)k[0],
+               (unsigned long long)k[1], (unsigned long long)k[2], (unsigned long long)k[3], (unsigned long long)k[4],
+               (unsigned long long)k[5], (unsigned long long)k[6], (unsigned long long)k[7], (unsigned long long)k[8],
+               (unsigned long long)k[9]);
     }
     free(y), free(u), free(v), free(y8), free(u8), free(v8);
     return 0;

@@ -13,7 +13,9 @@
  *                                                  svt_av1_cdef_frame -> svtgpu_cdef_apply_frame;
  *   svt_aom_rest_kernel  (EbRestProcess.c:580-626): restoration_seg_search -> nothing (the device searches the frame),
  *                                                  rest_finish_search -> svtgpu_lr_search_frame + svtgpu_lr_finish_frame,
- *                                                  svt_av1_loop_restoration_filter_frame -> svtgpu_lr_apply_frame.
+ *                                                  svt_av1_loop_restoration_filter_frame -> svtgpu_lr_apply_frame;
+ *   the CCSO calls of the CDEF process body (EbCdefProcess.c:621-623, live only in the ccso build of the encoder,
+ *   oracle/ref_harness/with_ccso.py): ccso_search -> svtgpu_ccso_search_frame, ccso_frame -> svtgpu_ccso_apply_plane.
  * Each hook moves the encoder's picture buffers to the device (svtgpu_frame_upload) and its results back into the
  * encoder's own structures exactly where the reference function writes them (frame header fields, mode-info grid,
  * restoration units, the recon samples).  Configurations the library does not cover (DLF methods other than
@@ -41,6 +43,7 @@
 #include "common_dsp_rtcd.h"
 #include "EbMcp.h"
 #include "svtgpu_rtcd.h"
+#include "EbCcso.h"
 
 void    svt_aom_get_recon_pic(PictureControlSet *pcs, EbPictureBufferDesc **recon_ptr, Bool is_highbd);
 int32_t svt_sb_all_skip(PictureControlSet *pcs, const Av1Common *const cm, int32_t mi_row, int32_t mi_col);
@@ -49,24 +52,25 @@ static int             g_on;
 static uint64_t        g_calls, g_fallbacks;
 /* device calls by kind: DLF pick, DLF filter, CDEF pick, CDEF apply, LR search, LR apply; and frames whose LR search
  * chose a filter for some plane (so the apply really filtered) */
-enum { K_DLF_PICK, K_DLF_FRAME, K_CDEF_PICK, K_CDEF_APPLY, K_LR_SEARCH, K_LR_APPLY, K_LR_ON, K_N };
+enum { K_DLF_PICK, K_DLF_FRAME, K_CDEF_PICK, K_CDEF_APPLY, K_LR_SEARCH, K_LR_APPLY, K_LR_ON, K_CCSO_SEARCH,
+       K_CCSO_APPLY, K_CCSO_ON, K_N };
 static uint64_t g_kind[K_N];
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static SvtGpuContext  *g_ctx;
 
 void enc_frame_hooks_enable(int on) { g_on = on; }
-/* ENC_HOOK_STAGES (diagnostics): the stages whose hooks are active, bits 1 DLF, 2 CDEF, 4 LR (default all) */
+/* ENC_HOOK_STAGES (diagnostics): the stages whose hooks are active, bits 1 DLF, 2 CDEF, 4 LR, 8 CCSO (default all) */
 static int stage_on(int bit) {
     static int m = -1;
     if (m < 0) {
         const char *e = getenv("ENC_HOOK_STAGES");
-        m             = e ? atoi(e) : 7;
+        m             = e ? atoi(e) : 15;
     }
     return g_on && (m & bit);
 }
 uint64_t enc_frame_hook_calls(void) { return g_calls; }
 uint64_t enc_frame_hook_fallbacks(void) { return g_fallbacks; }
-void enc_frame_hook_kinds(uint64_t out[7]) { memcpy(out, g_kind, sizeof g_kind); }
+void enc_frame_hook_kinds(uint64_t out[K_N]) { memcpy(out, g_kind, sizeof g_kind); }
 
 static void die(const char *what, int rc) {
     fprintf(stderr, "enc_frame_hooks: %s failed (%d): %s\n", what, rc, svtgpu_error_string(rc));
@@ -98,6 +102,9 @@ typedef struct Ctx {
     int32_t               lr_units[3];
     int                   d_valid, cdef_searched, lr_searched;
     int32_t               lr_ft[3];
+    SvtGpuCcsoState      *ccso; /* the CCSO search / apply (the ccso build of the encoder only) */
+    void                 *d_ext, *d_org[3], *d_rec[3], *d_pl[3];
+    size_t                pl_bytes[3];
 } Ctx;
 static Ctx g_ctxs[64];
 
@@ -585,4 +592,139 @@ void svt_av1_loop_restoration_filter_frame(int32_t *rst_tmpbuf, Yv12BufferConfig
     for (int q = 0; q < 3; q++) GPU(svtgpu_frame_download(c->L, q, pl[q], st[q], NULL));
     GPU(svtgpu_synchronize(g_ctx, NULL));
     c->lr_searched = 0, c->d_valid = 0;
+}
+
+/* ============================== CCSO (the ccso build only) ============================== */
+/* the process body passes host buffers: ext_rec_y ((H + 10) x (W + 10)) and the planes' org / rec (H x W each, the
+ * luma width as stride) of the unpadded size W x H (svt_av1_setup_dst_planes, EbDeblockingFilter.c:95-137) */
+static int ccso_supported(PictureControlSet *pcs) {
+    return frame_supported(pcs) && !pcs->scs->is_16bit_pipeline && pcs->scs->static_config.encoder_bit_depth == 8 &&
+           !pcs->scs->seq_header.color_config.mono_chrome;
+}
+static void ccso_dims(PictureControlSet *pcs, int *W, int *H) {
+    SequenceControlSet *scs = pcs->scs;
+    *W = scs->max_input_luma_width - scs->max_input_pad_right, *H = scs->max_input_luma_height - scs->max_input_pad_bottom;
+}
+static void ccso_buffers(Ctx *c, int W, int H) {
+    if (c->ccso) return;
+    GPU(svtgpu_ccso_state_create(g_ctx, W, H, &c->ccso));
+    GPU(svtgpu_buffer_alloc(g_ctx, sizeof(uint16_t) * (size_t)(W + 10) * (H + 10), &c->d_ext));
+    for (int p = 0; p < 3; p++) {
+        GPU(svtgpu_buffer_alloc(g_ctx, sizeof(uint16_t) * (size_t)W * H, &c->d_org[p]));
+        GPU(svtgpu_buffer_alloc(g_ctx, sizeof(uint16_t) * (size_t)W * H, &c->d_rec[p]));
+    }
+}
+/* the block flags of one plane in the mode-info grid: mbmi.ccso_blk_{y,u,v} at (64 y, 64 x) (EbPickccso.c:731-751) */
+static uint8_t *ccso_flag(PictureControlSet *pcs, int plane, int y, int x, uint8_t *v) {
+    MbModeInfo *m = &pcs->mi_grid_base[64 * y * pcs->mi_stride + 64 * x]->mbmi;
+    if (v) {
+        if (plane == 0) m->ccso_blk_y = *v;
+        else if (plane == 1) m->ccso_blk_u = *v;
+        else m->ccso_blk_v = *v;
+        return v;
+    }
+    static __thread uint8_t r;
+    r = plane == 0 ? m->ccso_blk_y : plane == 1 ? m->ccso_blk_u : m->ccso_blk_v;
+    return &r;
+}
+
+typedef void (*CcsoSearchFn)(PictureControlSet *, MacroblockdPlane *, int, const uint16_t *, uint16_t *[3],
+                             uint16_t *[3]);
+#undef KIND
+#define KIND K_CCSO_SEARCH
+void ccso_search(PictureControlSet *pcs, MacroblockdPlane *pd, int rdmult, const uint16_t *ext_rec_y,
+                 uint16_t *rec_uv[3], uint16_t *org_uv[3]) {
+    static CcsoSearchFn orig;
+    if (!orig) orig = (CcsoSearchFn)dlsym(RTLD_NEXT, "ccso_search");
+    if (!stage_on(8) || !ccso_supported(pcs)) {
+        if (g_on) count(1);
+        return orig(pcs, pd, rdmult, ext_rec_y, rec_uv, org_uv);
+    }
+    Ctx *c = ctx_of(pcs);
+    int  W, H;
+    ccso_dims(pcs, &W, &H);
+    ccso_buffers(c, W, H);
+    GPU(svtgpu_buffer_upload(c->d_ext, ext_rec_y, sizeof(uint16_t) * (size_t)(W + 10) * (H + 10), NULL));
+    for (int p = 0; p < 3; p++) {
+        GPU(svtgpu_buffer_upload(c->d_org[p], org_uv[p], sizeof(uint16_t) * (size_t)W * H, NULL));
+        GPU(svtgpu_buffer_upload(c->d_rec[p], rec_uv[p], sizeof(uint16_t) * (size_t)W * H, NULL));
+    }
+    const uint16_t *org[3] = {c->d_org[0], c->d_org[1], c->d_org[2]}, *rec[3] = {c->d_rec[0], c->d_rec[1], c->d_rec[2]};
+    SvtGpuCcsoParams prm[3];
+    uint8_t         *flags[3];
+    int32_t          nv[3], nh[3], ff = 0;
+    for (int p = 0; p < 3; p++) {
+        GPU(svtgpu_ccso_grid(W, H, p, &nv[p], &nh[p]));
+        flags[p] = malloc((size_t)nv[p] * nh[p]);
+    }
+    FrameHeader *fh = &pcs->ppcs->frm_hdr;
+    const int    rc = svtgpu_ccso_search_frame(c->ccso, c->d_ext, org, rec, 8, rdmult,
+                                               fh->quantization_params.base_q_idx, prm, flags, &ff, NULL);
+    if (rc != 1) { /* 1: the weighted rdmult overflows and the reference returns before searching (EbPickccso.c:790) */
+        GPU(rc);
+        for (int p = 0; p < 3; p++) { /* the header fields and grid flags derive_ccso_filter writes (:725-757) */
+            fh->ccso_info.ccso_enable[p] = prm[p].enable;
+            if (!prm[p].enable) continue;
+            for (int y = 0; y < nv[p]; y++)
+                for (int x = 0; x < nh[p]; x++) ccso_flag(pcs, p, y, x, &flags[p][y * nh[p] + x]);
+            memcpy(fh->ccso_info.filter_offset[p], prm[p].filter_offset, sizeof prm[p].filter_offset);
+            fh->ccso_info.quant_idx[p]          = prm[p].quant_idx;
+            fh->ccso_info.ext_filter_support[p] = prm[p].ext_filter_support;
+            fh->ccso_info.ccso_bo_only[p]       = prm[p].bo_only;
+            fh->ccso_info.max_band_log2[p]      = prm[p].max_band_log2;
+            fh->ccso_info.edge_clf[p]           = prm[p].edge_clf;
+            pthread_mutex_lock(&g_mu), g_kind[K_CCSO_ON]++, pthread_mutex_unlock(&g_mu);
+        }
+        fh->ccso_info.ccso_frame_flag = ff != 0; /* CONFIG_D143_CCSO_FM_FLAG (:804-813) */
+    }
+    for (int p = 0; p < 3; p++) free(flags[p]);
+    count(0);
+}
+
+typedef void (*CcsoFrameFn)(EbPictureBufferDesc *, PictureControlSet *, MacroblockdPlane *, uint16_t *);
+#undef KIND
+#define KIND K_CCSO_APPLY
+void ccso_frame(EbPictureBufferDesc *frame, PictureControlSet *pcs, MacroblockdPlane *pd, uint16_t *ext_rec_y) {
+    static CcsoFrameFn orig;
+    if (!orig) orig = (CcsoFrameFn)dlsym(RTLD_NEXT, "ccso_frame");
+    if (!stage_on(8) || !ccso_supported(pcs) || frame->bit_depth != EB_EIGHT_BIT) {
+        if (g_on) count(1);
+        return orig(frame, pcs, pd, ext_rec_y);
+    }
+    Ctx *c = ctx_of(pcs);
+    int  W, H;
+    ccso_dims(pcs, &W, &H);
+    ccso_buffers(c, W, H);
+    GPU(svtgpu_buffer_upload(c->d_ext, ext_rec_y, sizeof(uint16_t) * (size_t)(W + 10) * (H + 10), NULL));
+    const FrameHeader *fh = &pcs->ppcs->frm_hdr;
+    for (int p = 0; p < 3; p++) {
+        if (!fh->ccso_info.ccso_enable[p]) continue;
+        /* the plane as svt_av1_setup_dst_planes1 points at it (EbCcso.c:121-183, 8-bit buffers) */
+        const int st = p == 0 ? frame->stride_y : p == 1 ? frame->stride_cb : frame->stride_cr;
+        uint8_t  *b  = p == 0 ? frame->buffer_y + frame->org_x + frame->org_y * frame->stride_y
+                     : (p == 1 ? frame->buffer_cb : frame->buffer_cr) + (frame->org_x + frame->org_y * st) / 2;
+        const int pw = p ? W >> 1 : W, ph = p ? H >> 1 : H;
+        const size_t n = (size_t)(ph - 1) * st + pw;
+        if (!c->d_pl[p] || c->pl_bytes[p] < n) {
+            if (c->d_pl[p]) svtgpu_buffer_free(c->d_pl[p]);
+            GPU(svtgpu_buffer_alloc(g_ctx, n, &c->d_pl[p]));
+            c->pl_bytes[p] = n;
+        }
+        SvtGpuCcsoParams prm;
+        memset(&prm, 0, sizeof prm);
+        prm.enable = 1, prm.bo_only = fh->ccso_info.ccso_bo_only[p], prm.quant_idx = fh->ccso_info.quant_idx[p];
+        prm.ext_filter_support = fh->ccso_info.ext_filter_support[p];
+        prm.max_band_log2 = (uint8_t)fh->ccso_info.max_band_log2[p], prm.edge_clf = fh->ccso_info.edge_clf[p];
+        memcpy(prm.filter_offset, fh->ccso_info.filter_offset[p], sizeof prm.filter_offset);
+        int32_t nv, nh;
+        GPU(svtgpu_ccso_grid(W, H, p, &nv, &nh));
+        uint8_t *flags = malloc((size_t)nv * nh);
+        for (int y = 0; y < nv; y++)
+            for (int x = 0; x < nh; x++) flags[y * nh + x] = *ccso_flag(pcs, p, y, x, NULL);
+        GPU(svtgpu_buffer_upload(c->d_pl[p], b, n, NULL));
+        GPU(svtgpu_ccso_apply_plane(c->ccso, c->d_ext, p, 8, c->d_pl[p], 8, st, &prm, flags, NULL));
+        GPU(svtgpu_buffer_download(b, c->d_pl[p], n, NULL));
+        free(flags);
+    }
+    count(0);
 }

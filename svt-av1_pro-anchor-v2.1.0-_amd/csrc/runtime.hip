@@ -102,6 +102,33 @@ extern "C" void svtgpu_stream_destroy(void *stream) {
     (void)hipStreamDestroy((hipStream_t)stream);
 }
 
+// Plain device buffers for the pointer-level entry points (CCSO, plane conversion) when the caller has no allocator of
+// its own: hipMalloc / hipFree and stream-ordered copies that are complete when they return.
+extern "C" int svtgpu_buffer_alloc(SvtGpuContext *ctx, size_t bytes, void **out) {
+    if (!ctx || !out || !bytes) return SVTGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (hipMalloc(out, bytes) != hipSuccess) return *out = nullptr, SVTGPU_ERR_OOM;
+    return SVTGPU_OK;
+}
+extern "C" void svtgpu_buffer_free(void *dev) { (void)hipFree(dev); }
+extern "C" int  svtgpu_buffer_upload(void *dev, const void *host, size_t bytes, void *stream) {
+    if (!dev || !host) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : svtgpu_default_stream();
+    HIP_TRY(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    svtgpu_count_xfer(0, bytes);
+    return SVTGPU_OK;
+}
+extern "C" int svtgpu_buffer_download(void *host, const void *dev, size_t bytes, void *stream) {
+    if (!dev || !host) return SVTGPU_ERR_INVALID_ARG;
+    hipStream_t st = stream ? (hipStream_t)stream : svtgpu_default_stream();
+    HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    svtgpu_count_xfer(1, bytes);
+    return SVTGPU_OK;
+}
+
 // Test support (the exchange deadline's abort path): one wave that spins on the 100 MHz s_memrealtime clock for `ms`
 // milliseconds (at most 10 s; every lane leaves at the same bound), holding `stream` busy.
 __global__ void stall_kernel(unsigned long long ticks) {

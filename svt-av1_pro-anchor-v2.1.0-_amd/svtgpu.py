@@ -406,6 +406,10 @@ _SIGS = {
     "svtgpu_dlf_set_crop": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32]),
     "svtgpu_cdef_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
     "svtgpu_lr_set_tile": (ctypes.c_int, [_P, _P, _P, _P]),
+    "svtgpu_buffer_alloc": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(_P)]),
+    "svtgpu_buffer_free": (None, [_P]),
+    "svtgpu_buffer_upload": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P]),
+    "svtgpu_buffer_download": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P]),
     "svtgpu_ccso_grid": (ctypes.c_int, [_I32, _I32, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "svtgpu_ccso_extend_luma": (ctypes.c_int, [_P, _I32, _I32, _I32, _I32, _P, _P]),
     "svtgpu_ccso_state_create": (ctypes.c_int, [_P, _I32, _I32, ctypes.POINTER(_P)]),

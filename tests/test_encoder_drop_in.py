@@ -26,6 +26,9 @@ needs_exe = pytest.mark.skipif(not os.path.exists(EXE), reason="oracle/_ref/enc 
 EXE_NSS = os.path.join(ROOT, "oracle", "_ref", "enc", "nss", "enc_drop_in")
 OBJ = os.path.join(ROOT, "oracle", "_ref", "enc", "obj", "Source", "Lib", "Encoder", "Codec", "EbCdefProcess.o")
 OBJ_NSS = os.path.join(ROOT, "oracle", "_ref", "enc", "nss", "EbCdefProcess.o")
+# the encoder with the fork's CCSO search / apply switched back on (oracle/ref_harness/with_ccso.py)
+EXE_CCSO = os.path.join(ROOT, "oracle", "_ref", "enc", "ccso", "enc_drop_in")
+needs_ccso = pytest.mark.skipif(not os.path.exists(EXE_CCSO), reason="oracle/_ref/enc/ccso not built (needs /root/reference)")
 
 
 def _encode(mode, path, *args, timeout=600, exe=EXE):
@@ -152,4 +155,36 @@ def test_encoder_without_cpu_cdef_search(tmp_path, name, geom):
     ic = _encode("cpu", cpu, *geom, timeout=1100)
     ig = _encode("frame", frm, *geom, timeout=1100, exe=EXE_NSS)
     assert ig["frame_fallbacks"] == 0 and ig["cdef_pick"] >= geom[2], (name, ig)
+    assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(frm, "rb").read(), (name, ic, ig)
+
+
+@needs_ccso
+def test_ccso_build_runs_ccso(tmp_path):
+    """The encoder with its CCSO calls switched back on (EbCdefProcess.c:621-623) encodes deterministically and writes a
+    different bitstream from the encoder as shipped: the CCSO frame header and block flags are coded and its filtering
+    feeds later pictures' prediction -- so an equal bitstream below is a check of the CCSO decisions and samples."""
+    a, b, c = str(tmp_path / "a.obu"), str(tmp_path / "b.obu"), str(tmp_path / "c.obu")
+    geom = (384, 256, 3, 2, 40, 8, 1)
+    ia, ib = _encode("cpu", a, *geom, exe=EXE_CCSO), _encode("cpu", b, *geom, exe=EXE_CCSO)
+    _encode("cpu", c, *geom)
+    assert ia["bytes"] > 0 and open(a, "rb").read() == open(b, "rb").read()
+    assert open(a, "rb").read() != open(c, "rb").read()
+
+
+@needs_ccso
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("name,geom", [("384x256_p2", (384, 256, 3, 2, 40, 8, 1)),
+                                       ("520x296_p3", (520, 296, 4, 3, 36, 8, 1))])
+def test_encoder_with_ccso_on_device(tmp_path, name, geom):
+    """The CCSO-enabled encoder with ccso_search / ccso_frame (and the DLF / CDEF / LR frame functions) served by the
+    device writes the bitstream of the same encoder on the CPU, byte for byte: the frame header's CCSO fields, the
+    per-block flags and the filtered recon all equal the fork's own C.  Every CCSO call on the device (no fallback)
+    and some plane enabled.  One logical processor: the fork's CPU search keeps its state in file-scope globals
+    (EbPickccso.c:18-41), so two pictures searching at once crash the reference itself (seen at lp 2)."""
+    cpu, frm = str(tmp_path / "cpu.obu"), str(tmp_path / "frame.obu")
+    ic = _encode("cpu", cpu, *geom, timeout=1100, exe=EXE_CCSO)
+    ig = _encode("frame", frm, *geom, timeout=1100, exe=EXE_CCSO)
+    assert ig["frame_fallbacks"] == 0, (name, ig)
+    assert ig["ccso_search"] >= geom[2] and ig["ccso_apply"] >= geom[2] and ig["ccso_on"] >= 1, (name, ig)
     assert ic["bytes"] == ig["bytes"] and open(cpu, "rb").read() == open(frm, "rb").read(), (name, ic, ig)
