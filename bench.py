@@ -45,8 +45,11 @@ import numpy as np
 FRAMES_IN_FLIGHT = 4  # default frames pipelined per GPU (round 3 final kernels: 2 -> 2672, 3 -> 2846, 4 -> 2914, 5 -> 2772 Mpx/s)
 # default when a rank filters a tile of the picture (N > 1, or an emulated rank): its stages are shorter but their
 # latency chains are not, so more frames overlap (round 4, emulated 8-GPU rank, 16 hardware queues: F = 4 5.9-6.0,
-# F = 5 7.1, F = 6 7.6-7.7 Gpx/s; profiles/r04/queues)
-TILED_FRAMES_IN_FLIGHT = 6
+# F = 5 7.1, F = 6 7.6-7.7 Gpx/s; profiles/r04/queues).  Round 6, library streams, the MD batch on the main stream
+# (2 streams per frame): F = 7 fills the 16 queues exactly (14 + the context's + the null stream) and beats F = 6 at
+# every rank count (emulated 8 / 4 / 2-GPU ranks 10.38-10.40 / 8.21-8.22 / 5.28-5.35 vs 9.48-9.52 / 7.59-7.69 /
+# 5.03-5.06 Gpx/s, two runs each, profiles/r06/fsweep_tiled.txt); F = 8 oversubscribes the queues (8.7)
+TILED_FRAMES_IN_FLIGHT = 7
 # hardware queues per process: HIP's default 4 would serialize the frames' streams, but past 16 the queues are
 # time-sliced and every frame's latency chain stretches (emulated 8-GPU rank: F = 6 with 16 queues 7.6 Gpx/s, with 18
 # 4.8; F = 8 with 32 queues 1.7); whole frames run the same with 8, 12 or 16 (3.03-3.06 Gpx/s at F = 4)
