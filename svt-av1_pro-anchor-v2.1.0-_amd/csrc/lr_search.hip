@@ -3265,11 +3265,11 @@ int search_frame(SvtGpuLrState *s, const SvtGpuFrame *rec, const SvtGpuFrame *sr
     // The Wiener chain (statistics, decomposition, trial rounds) and the self-guided chain (filters, seeds,
     // projection rounds) are independent until the RD finish: the Wiener chain runs on a second stream, so its
     // latency-bound rounds fill the gaps of the self-guided work and the other way round.
-    if (!s->wst)
-        if (int rc = lr_make_wiener_stream(s)) return rc;
     // measurement (svtgpu_lr_profile bit 7): both chains on the caller's stream, so a kernel's duration is its own,
     // not its share of the CUs beside the other chain's kernels
-    const bool  serial = prof && prof->serial;
+    const bool serial = prof && prof->serial;
+    if (!s->wst && !serial)
+        if (int rc = lr_make_wiener_stream(s)) return rc;
     hipStream_t sw     = serial ? st : s->wst;
     if (!serial) {
         HIP_TRY(hipEventRecord(s->ev_fork, st));
