@@ -50,10 +50,11 @@ struct Bin {            // one histogram cell (global); corr[o] = sum of clamped
     uint64_t s2;
     uint64_t corr[8];
 };
-struct Mom {            // one fine class of one block under one combination
-    uint32_t n, s1;
-    uint64_t ssd[8];    // block SSD contribution with table offset kOff[o]
-};
+// The moments of one (plane, combination): 9 arrays of nbp x NFINE words (block-major, fine class minor) -- count << 32
+// | error sum, then the block SSD under each of the 8 table offsets.  Structure of arrays: a wave's loads of one field
+// are contiguous.
+constexpr int MOM_WORDS = 9;
+__device__ __forceinline__ size_t mom_ssd(int k, size_t n) { return (size_t)(k + 1) * n; }
 struct Geo {
     int32_t w, h, pw, ph, ss, log2, bs, nvfb, nhfb, nb, nbx, nby, nbp;
 };
@@ -98,7 +99,7 @@ struct Planes { // the planes of one search launch: plane = plane0 + blockIdx.z 
     Geo               g[3];
     const uint16_t   *ext, *org[3], *rec[3];
     Bin              *bins[3];  // [NKIND][nbp][NBIN]
-    Mom              *mom[3];   // [NCOMBO + 1][nbp][NFINE]
+    uint64_t         *mom[3];   // [NCOMBO + 1][MOM_WORDS][nbp][NFINE]
     double           *cost[3];  // [NCFG]
     int8_t           *lut[3];   // [NCFG][NFINE] offset of each merged class
     uint8_t          *ctrl[3];  // [NCFG][nb]
@@ -214,7 +215,8 @@ __global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
     const int tid = threadIdx.x, pb = blockIdx.x, kind = blockIdx.y, pl = a.plane0 + blockIdx.z, nbp = a.g[pl].nbp;
     if (pb >= nbp) return;
     const Bin *bins = a.bins[pl];
-    Mom       *mom  = a.mom[pl];
+    uint64_t  *mom  = a.mom[pl];
+    const size_t N  = (size_t)nbp * NFINE;
     const int  nbins = kind < NSUP ? NBIN : 128;
     const Bin *src   = bins + ((size_t)kind * nbp + pb) * NBIN;
     {
@@ -251,11 +253,11 @@ __global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
             n = x.n, s1 = x.s1, s2 = x.s2;
             for (int k = 0; k < 8; k++) corr[k] = x.corr[k];
         }
-        Mom          &m  = mom[((size_t)combo * nbp + pb) * NFINE + f];
+        uint64_t     *m  = mom + (size_t)combo * MOM_WORDS * N + (size_t)pb * NFINE + f;
         const int64_t S1 = (int32_t)s1;
-        m.n = n, m.s1 = s1;
+        m[0]             = (uint64_t)n << 32 | s1;
         for (int k = 0; k < 8; k++)
-            m.ssd[k] = s2 - (uint64_t)(2 * kOff[k] * S1) + (uint64_t)(kOff[k] * kOff[k]) * n + corr[k];
+            m[mom_ssd(k, N)] = s2 - (uint64_t)(2 * kOff[k] * S1) + (uint64_t)(kOff[k] * kOff[k]) * n + corr[k];
     }
 }
 
@@ -304,7 +306,8 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
     const int  bo = cfg >= NCOMBO * 4, k = bo ? cfg - NCOMBO * 4 : cfg & 3, combo = bo ? NCOMBO : cfg >> 2;
     const int  clf = bo ? 0 : combo & 1, edges = bo ? 1 : (clf ? 2 : 3), F = bo ? 128 : 72;
     const int  nb = g.nb, nbp = g.nbp, nbands = 1 << k;
-    const Mom *mom = a.mom[pl] + (size_t)combo * nbp * NFINE;
+    const size_t    N   = (size_t)nbp * NFINE;
+    const uint64_t *mom = a.mom[pl] + (size_t)combo * MOM_WORDS * N;
     // the merged class of a fine class at this band count
     auto merged = [&](int f) { return bo ? f >> (7 - k) : ((f / 9) >> (3 - k)) * 9 + f % 9; };
     auto blk2d  = [&](int p) { return (p / g.nbx) * g.nhfb + p % g.nbx; };
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
 #pragma unroll
         for (int u = 0; u < LU; u++) {
             const int i = i0 + u * TT;
-            v[u]        = i < nbp * F ? mom[(size_t)(i / F) * NFINE + i % F].ssd[4] : 0;
+            v[u]        = i < nbp * F ? mom[mom_ssd(4, N) + (size_t)(i / F) * NFINE + i % F] : 0;
         }
 #pragma unroll
         for (int u = 0; u < LU; u++)
@@ -338,8 +341,8 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
                     const int i = i0 + u * TT;
                     n[u]        = 0;
                     if (i < nbp * F && s_ctrl[i / F]) {
-                        const Mom &m = mom[(size_t)(i / F) * NFINE + i % F];
-                        n[u] = m.n, e[u] = m.s1;
+                        const uint64_t m = mom[(size_t)(i / F) * NFINE + i % F];
+                        n[u] = (uint32_t)(m >> 32), e[u] = (uint32_t)m;
                     }
                 }
 #pragma unroll
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(TT) void ccso_train_kernel(Planes a) {
 #pragma unroll
             for (int u = 0; u < LU; u++) {
                 const int i = i0 + u * TT;
-                v[u]        = i < nbp * F ? mom[(size_t)(i / F) * NFINE + i % F].ssd[s_off[merged(i % F)]] : 0;
+                v[u] = i < nbp * F ? mom[mom_ssd(s_off[merged(i % F)], N) + (size_t)(i / F) * NFINE + i % F] : 0;
             }
 #pragma unroll
             for (int u = 0; u < LU; u++)
@@ -413,14 +416,15 @@ __global__ __launch_bounds__(256) void ccso_final_kernel(Planes a) {
     __shared__ double             s_c[256];
     __shared__ int                s_i[256];
     const int         lane = threadIdx.x, pl = a.plane0 + blockIdx.x, nb = a.g[pl].nb;
-    const Mom        *mom  = a.mom[pl];
+    const uint64_t   *mom  = a.mom[pl];
+    const size_t      N    = (size_t)a.g[pl].nbp * NFINE;
     const double     *cost = a.cost[pl];
     SvtGpuCcsoParams *prm  = a.params[pl];
     uint8_t          *flg  = a.flags[pl];
     if (lane == 0) s_unf = 0;
     __syncthreads();
     unsigned long long u = 0;
-    for (int i = lane; i < a.g[pl].nbp * 72; i += 256) u += mom[(size_t)(i / 72) * NFINE + i % 72].ssd[4];
+    for (int i = lane; i < a.g[pl].nbp * 72; i += 256) u += mom[mom_ssd(4, N) + (size_t)(i / 72) * NFINE + i % 72];
     atomicAdd(&s_unf, u);
     // the reference's loop order (EbPickccso.c:550-578) keeps the first strict minimum: the smallest cost, earliest
     // configuration among equals
@@ -511,7 +515,7 @@ struct SvtGpuCcsoState {
     SvtGpuContext    *ctx;
     int32_t           width, height, nbp_max, nb_max;
     Bin              *bins; // per plane: [3][NKIND][nbp_max][NBIN] (the three planes' searches run in one launch)
-    Mom              *mom;  // [3][NCOMBO + 1][nbp_max][NFINE]
+    uint64_t         *mom;  // [3][NCOMBO + 1][MOM_WORDS][nbp_max][NFINE] (a plane's combinations use its own nbp)
     double           *cost; // [3][NCFG]
     int8_t           *lut;  // [3][NCFG][NFINE]
     uint8_t          *ctrl; // [3][NCFG][nb_max]
@@ -549,8 +553,8 @@ extern "C" int svtgpu_ccso_state_create(SvtGpuContext *ctx, int32_t width, int32
     if (nb > MAXNB) return SVTGPU_ERR_UNSUPPORTED;
     SvtGpuCcsoState *s = new SvtGpuCcsoState();
     s->ctx = ctx, s->width = width, s->height = height, s->nbp_max = nbp, s->nb_max = nb;
-    const size_t nbins = (size_t)3 * NKIND * nbp * NBIN, nmom = (size_t)3 * (NCOMBO + 1) * nbp * NFINE;
-    if (hipMalloc(&s->bins, nbins * sizeof(Bin)) != hipSuccess || hipMalloc(&s->mom, nmom * sizeof(Mom)) != hipSuccess ||
+    const size_t nbins = (size_t)3 * NKIND * nbp * NBIN, nmom = (size_t)3 * (NCOMBO + 1) * MOM_WORDS * nbp * NFINE;
+    if (hipMalloc(&s->bins, nbins * sizeof(Bin)) != hipSuccess || hipMalloc(&s->mom, nmom * sizeof(uint64_t)) != hipSuccess ||
         hipMalloc(&s->cost, 3 * NCFG * sizeof(double)) != hipSuccess ||
         hipMalloc(&s->lut, (size_t)3 * NCFG * NFINE) != hipSuccess ||
         hipMalloc(&s->ctrl, (size_t)3 * NCFG * nb) != hipSuccess ||
@@ -588,7 +592,7 @@ int launch_search(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const
         a.org[p]    = p >= p0 && p < p0 + n ? org[p - p0] : nullptr;
         a.rec[p]    = p >= p0 && p < p0 + n ? rec[p - p0] : nullptr;
         a.bins[p]   = s->bins + (size_t)p * NKIND * s->nbp_max * NBIN;
-        a.mom[p]    = s->mom + (size_t)p * (NCOMBO + 1) * s->nbp_max * NFINE;
+        a.mom[p]    = s->mom + (size_t)p * (NCOMBO + 1) * MOM_WORDS * s->nbp_max * NFINE;
         a.cost[p]   = s->cost + (size_t)p * NCFG;
         a.lut[p]    = s->lut + (size_t)p * NCFG * NFINE;
         a.ctrl[p]   = s->ctrl + (size_t)p * NCFG * s->nb_max;
