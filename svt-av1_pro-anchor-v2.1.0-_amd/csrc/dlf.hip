@@ -885,20 +885,23 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArg
     int       nitems = 0;
     for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
     // one item per workgroup over a grid sized for the most levels a round can try; the workgroups past this round's
-    // items go straight to the arrival count (a persistent loop over the items spilled 60 VGPRs: the item's registers
-    // live across the loop)
-    // (nitems == 0: every search has finished, nothing to step)
-    if ((int)blockIdx.x >= nitems) return;
-    dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
+    // items have nothing to filter (a persistent loop over the items spilled 60 VGPRs: the item's registers live across
+    // the loop).  nitems == 0: every search has finished, nothing to step.
+    if ((int)blockIdx.x < nitems) dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
     if (!fuse) return;
     __syncthreads();
-    // Only the workgroups with an item count (the others left without touching the counter).  No __threadfence: an
-    // agent-scope fence writes back and invalidates this XCD's L2 (the L2s of the 8 XCDs are not coherent), which
-    // doubled every round (the trials of a tile share their staging through the L2); the sums are device-scope atomics,
-    // so waiting for this lane's to complete before its arrival is enough
+    // EVERY workgroup of the grid arrives, the spare ones too.  They read the plan at their start, and counting only the
+    // item workgroups let a spare one dispatched late (behind other frames' kernels) read the NEXT round's plan -- the
+    // step had already rewritten it --, take an item of that round and arrive at the freshly reset counter: the next
+    // round's step then fired one arrival early, on incomplete sums, and every later round of that state stayed off by
+    // one (round 6: one frame slot's DLF stage at 41 ms per frame, a search finished by the one-workgroup finisher).
+    // With every workgroup counted, the step runs after the last one has read this round's plan.
+    // No __threadfence: an agent-scope fence writes back and invalidates this XCD's L2 (the L2s of the 8 XCDs are not
+    // coherent), which doubled every round (the trials of a tile share their staging through the L2); the sums are
+    // device-scope atomics, so waiting for this lane's to complete before its arrival is enough
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = atomicAdd(a.arrive, 1u) == (unsigned)nitems - 1;
+        last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
