@@ -561,6 +561,7 @@ struct SvtGpuDlfState {
     int32_t        sse_rect[4] = {0, 0, 0, 0}, out_rect[4] = {0, 0, 0, 0};
     SvtGpuComm    *comm = nullptr;
     void          *d_search = nullptr;  // DlfDevSearch: the device-resident level search (SVTGPU_DLF_DEVICE)
+    void          *d_plans  = nullptr;  // DlfDevPlan[2]: the asynchronous search's trial launches read plan k & 1
     void          *h_search = nullptr;  // its pinned host copy
     SvtGpuLfMi    *h_mi = nullptr;      // pinned staging of the mode info (one upload per frame, asynchronous)
     SvtGpuPrioLane prio;                // the level search's trial launches
@@ -826,13 +827,22 @@ void plan_next(DlfDevSearch &S) { // host
 // the step), else read and zeroed in stream order
 static_assert(sizeof(DlfDevSearch) % 4 == 0, "word copies of the search state");
 static_assert(sizeof(DlfDevSearch) <= sizeof(DlfTileLds::t), "the step's LDS copy fits the tile image it reuses");
-__device__ void dlf_step(DlfDevSearch *S, unsigned long long *sse, uint32_t *w, bool atomic_sums) {
+// out_plan (nullable): the plan buffer the next trial launch reads (the asynchronous search's double-buffered plans)
+__device__ void copy_plan(DlfDevPlan *dst, const DlfDevPlan *src) {
+    constexpr int NP = (int)(sizeof(DlfDevPlan) / 4);
+    for (int i = threadIdx.x; i < NP; i += blockDim.x) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
+}
+__device__ void dlf_step(DlfDevSearch *S, unsigned long long *sse, uint32_t *w, bool atomic_sums,
+                         DlfDevPlan *out_plan = nullptr) {
     constexpr int NW = (int)(sizeof(DlfDevSearch) / 4);
     const int     tid = threadIdx.x, nt = blockDim.x;
     for (int i = tid; i < NW; i += nt) w[i] = ((const uint32_t *)S)[i];
     __syncthreads();
     DlfDevSearch &D = *(DlfDevSearch *)w;
-    if (D.plan.done) return; // uniform: every lane read the same word
+    if (D.plan.done) { // uniform: every lane read the same word
+        if (out_plan) copy_plan(out_plan, &D.plan);
+        return;
+    }
     __shared__ unsigned long long v[MAX_JOBS * MAX_TRIALS]; // the sums, one lane each (not a chain of atomics)
     if (tid < MAX_JOBS * MAX_TRIALS) v[tid] = atomic_sums ? atomicExch(&sse[tid], 0ull) : sse[tid];
     __syncthreads();
@@ -847,6 +857,7 @@ __device__ void dlf_step(DlfDevSearch *S, unsigned long long *sse, uint32_t *w, 
     __syncthreads();
     if (!atomic_sums && tid < MAX_JOBS * MAX_TRIALS) sse[tid] = 0;
     for (int i = tid; i < NW; i += nt) ((uint32_t *)S)[i] = w[i];
+    if (out_plan) copy_plan(out_plan, &D.plan);
 }
 __global__ __launch_bounds__(64) void dlf_search_step_kernel(DlfDevSearch *S, unsigned long long *sse) {
     __shared__ __align__(16) uint32_t w[sizeof(DlfDevSearch) / 4];
@@ -877,35 +888,41 @@ __global__ __launch_bounds__(64) void dlf_search_init_kernel(DlfDevSearch *S, Sv
 // svtgpu_dlf_pick_async, 2: one trial round of the device plan (items = the plan's levels only);
 // the last workgroup to finish takes the bisection step (fuse; a tiled rank steps after the SSE all-reduce instead)
 template <typename T>
-__global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArgs a0, DlfDevSearch *S, int fuse) {
+__global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArgs a0, DlfDevSearch *S, int fuse,
+                                                                DlfDevPlan *next_plan) {
     __shared__ __align__(16) DlfTileLds L;
     KArgs    &a = kargs();
     __shared__ int last;
     const int tid    = threadIdx.x;
     int       nitems = 0;
+    // This launch reads its own plan buffer (a.plan = plan k & 1), which nothing writes while it runs: the step of the
+    // round writes the NEXT launch's buffer (next_plan).  A spare workgroup dispatched late (behind other frames'
+    // kernels, after the step) therefore still reads this round's plan.  (With one plan rewritten in place, such a
+    // workgroup could read the next round's plan, take one of its items and arrive at the freshly reset counter: the
+    // next round's step fired one arrival early and every later round of that state stayed off by one -- round 6,
+    // one frame slot's DLF stage at 41 ms per frame under load.)
     for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
+    if (nitems == 0) { // every search has finished: carry the finished plan to the next launch's buffer
+        if (fuse && next_plan && blockIdx.x == 0) copy_plan(next_plan, a.plan);
+        return;
+    }
     // one item per workgroup over a grid sized for the most levels a round can try; the workgroups past this round's
-    // items have nothing to filter (a persistent loop over the items spilled 60 VGPRs: the item's registers live across
-    // the loop).  nitems == 0: every search has finished, nothing to step.
-    if ((int)blockIdx.x < nitems) dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
+    // items go straight out, uncounted (a persistent loop over the items spilled 60 VGPRs: the item's registers live
+    // across the loop)
+    if ((int)blockIdx.x >= nitems) return;
+    dlf_tile_item<T, true>(a, blockIdx.x, nitems, L);
     if (!fuse) return;
     __syncthreads();
-    // EVERY workgroup of the grid arrives, the spare ones too.  They read the plan at their start, and counting only the
-    // item workgroups let a spare one dispatched late (behind other frames' kernels) read the NEXT round's plan -- the
-    // step had already rewritten it --, take an item of that round and arrive at the freshly reset counter: the next
-    // round's step then fired one arrival early, on incomplete sums, and every later round of that state stayed off by
-    // one (round 6: one frame slot's DLF stage at 41 ms per frame, a search finished by the one-workgroup finisher).
-    // With every workgroup counted, the step runs after the last one has read this round's plan.
     // No __threadfence: an agent-scope fence writes back and invalidates this XCD's L2 (the L2s of the 8 XCDs are not
     // coherent), which doubled every round (the trials of a tile share their staging through the L2); the sums are
     // device-scope atomics, so waiting for this lane's to complete before its arrival is enough
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
+        last = atomicAdd(a.arrive, 1u) == (unsigned)nitems - 1;
     }
     __syncthreads();
     if (!last) return;
-    dlf_step(S, a.sse, (uint32_t *)L.t, true);
+    dlf_step(S, a.sse, (uint32_t *)L.t, true, next_plan);
     if (tid == 0) atomicExch(a.arrive, 0u);
 }
 
@@ -1154,6 +1171,7 @@ extern "C" void svtgpu_dlf_state_destroy(SvtGpuDlfState *s) {
     (void)hipFree(s->d_arrive);
     if (s->h_sse) (void)hipHostFree(s->h_sse);
     (void)hipFree(s->d_search);
+    (void)hipFree(s->d_plans);
     (void)hipFree(s->d_res);
     if (s->h_res) (void)hipHostFree(s->h_res);
     svtgpu_prio_destroy(&s->prio);
@@ -1406,6 +1424,7 @@ extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon
         HIP_TRY(hipMalloc(&s->d_search, sizeof(DlfDevSearch)));
         HIP_TRY(hipHostMalloc(&s->h_search, sizeof(DlfDevSearch), hipHostMallocDefault));
     }
+    if (!s->d_plans) HIP_TRY(hipMalloc(&s->d_plans, 2 * sizeof(DlfDevPlan)));
     // the rounds to enqueue: one more than the previous search took (read from mapped memory without waiting: the
     // previous result when it is already there, else the last hint); SVTGPU_DLF_ROUNDS=k fixes it (tests: 1 makes the
     // finish kernel complete the search)
@@ -1426,6 +1445,8 @@ extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon
     hipLaunchKernelGGL(dlf_search_init_kernel, dim3(1), dim3(64), 0, st, D, p, ns, dlf_avg, early_exit_convergence,
                        tx_mode_only_4x4);
     HIP_TRY(hipGetLastError());
+    DlfDevPlan *plans = (DlfDevPlan *)s->d_plans; // trial launch k reads plans[k & 1] and its step writes the other
+    HIP_TRY(hipMemcpyAsync(&plans[0], &D->plan, sizeof(DlfDevPlan), hipMemcpyDeviceToDevice, st));
     LevelTables L;
     build_level_tables(p, L); // the thresholds (sharpness 0); the levels come from the plan
     DlfTileArgs a = base_args(recon, L);
@@ -1441,12 +1462,14 @@ extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon
     a.njob = ns, a.sse = s->d_sse, a.arrive = s->d_arrive, a.plan = &D->plan, a.dyn = 1;
     const int grid = std::max(1, max_items);
     for (int k = 0; k < rounds; k++) {
+        a.plan = &plans[k & 1];
         if (recon->bytes_per_sample == 2)
-            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint16_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint16_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1, &plans[(k + 1) & 1]);
         else
-            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint8_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint8_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1, &plans[(k + 1) & 1]);
         HIP_TRY(hipGetLastError());
     }
+    a.plan = &D->plan; // the finisher: one workgroup stepping the search's own copy, nothing runs beside it
     const int seq = ++s->dev_seq;
     if (recon->bytes_per_sample == 2)
         hipLaunchKernelGGL(dlf_finish_kernel<uint16_t>, dim3(1), dim3(NTHR), 0, st, a, D, (DlfDevResult *)s->d_res,
