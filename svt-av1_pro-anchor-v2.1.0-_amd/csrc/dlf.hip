@@ -239,6 +239,7 @@ struct DlfTileArgs {
     unsigned long long  seq;
     unsigned long long *wgclk; // diagnostics (svtgpu_internal.h wgclk_mark) or null
     const DlfDevPlan   *plan;  // trial mode: levels from the device plan (the grid covers MAX_TRIALS per job) or null
+    DlfDevPlan         *next_plan = nullptr; // the asynchronous search: the plan buffer the next trial launch reads (or null)
     int32_t             dyn;   // with plan: the items are the plan's levels only, Σ tiles x plan->ntrial (persistent grid)
     const uint8_t      *dev_lvl; // apply: the level tables [plane][dir][128] the device search left (null: job lvl[0])
 };
@@ -888,8 +889,7 @@ __global__ __launch_bounds__(64) void dlf_search_init_kernel(DlfDevSearch *S, Sv
 // svtgpu_dlf_pick_async, 2: one trial round of the device plan (items = the plan's levels only);
 // the last workgroup to finish takes the bisection step (fuse; a tiled rank steps after the SSE all-reduce instead)
 template <typename T>
-__global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArgs a0, DlfDevSearch *S, int fuse,
-                                                                DlfDevPlan *next_plan) {
+__global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArgs a0, DlfDevSearch *S, int fuse) {
     __shared__ __align__(16) DlfTileLds L;
     KArgs    &a = kargs();
     __shared__ int last;
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArg
     // one frame slot's DLF stage at 41 ms per frame under load.)
     for (int j = 0; j < a.njob; j++) nitems += a.job[j].tiles * a.plan->ntrial[j];
     if (nitems == 0) { // every search has finished: carry the finished plan to the next launch's buffer
-        if (fuse && next_plan && blockIdx.x == 0) copy_plan(next_plan, a.plan);
+        if (fuse && a.next_plan && blockIdx.x == 0) copy_plan(a.next_plan, a.plan);
         return;
     }
     // one item per workgroup over a grid sized for the most levels a round can try; the workgroups past this round's
@@ -922,7 +922,7 @@ __global__ __launch_bounds__(NTHR, 8) void dlf_trial_dev_kernel(const DlfTileArg
     }
     __syncthreads();
     if (!last) return;
-    dlf_step(S, a.sse, (uint32_t *)L.t, true, next_plan);
+    dlf_step(S, a.sse, (uint32_t *)L.t, true, a.next_plan);
     if (tid == 0) atomicExch(a.arrive, 0u);
 }
 
@@ -1462,14 +1462,14 @@ extern "C" int svtgpu_dlf_pick_async(SvtGpuDlfState *s, const SvtGpuFrame *recon
     a.njob = ns, a.sse = s->d_sse, a.arrive = s->d_arrive, a.plan = &D->plan, a.dyn = 1;
     const int grid = std::max(1, max_items);
     for (int k = 0; k < rounds; k++) {
-        a.plan = &plans[k & 1];
+        a.plan = &plans[k & 1], a.next_plan = &plans[(k + 1) & 1];
         if (recon->bytes_per_sample == 2)
-            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint16_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1, &plans[(k + 1) & 1]);
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint16_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
         else
-            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint8_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1, &plans[(k + 1) & 1]);
+            hipLaunchKernelGGL(dlf_trial_dev_kernel<uint8_t>, dim3(grid), dim3(NTHR), 0, st, a, D, 1);
         HIP_TRY(hipGetLastError());
     }
-    a.plan = &D->plan; // the finisher: one workgroup stepping the search's own copy, nothing runs beside it
+    a.plan = &D->plan, a.next_plan = nullptr; // the finisher: one workgroup stepping the search's own copy
     const int seq = ++s->dev_seq;
     if (recon->bytes_per_sample == 2)
         hipLaunchKernelGGL(dlf_finish_kernel<uint16_t>, dim3(1), dim3(NTHR), 0, st, a, D, (DlfDevResult *)s->d_res,
