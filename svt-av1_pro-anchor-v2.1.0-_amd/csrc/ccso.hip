@@ -226,6 +226,24 @@ __global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
         for (int i = tid; i < nbins * (int)(sizeof(Bin) / 8); i += 256) d[i] = s[i];
     }
     __syncthreads();
+    constexpr int BW = (int)(sizeof(Bin) / 8); // words per cell: count | error sum (two u32), square sum, 8 corrections
+    if (kind < NSUP) { // running sums along the second bucket (every class is a range of buckets): in place, per word
+        for (int t = tid; t < 72 * BW; t += 256) {
+            const int row = t / BW, w = t % BW;
+            uint64_t *c   = (uint64_t *)(s_bin + row * 9) + w;
+            if (w == 0) { // the two u32 fields (n low, s1 high) add separately (the error sum wraps)
+                uint32_t an = 0, as = 0;
+                for (int j = 0; j < 9; j++) {
+                    an += (uint32_t)c[j * BW], as += (uint32_t)(c[j * BW] >> 32);
+                    c[j * BW] = (uint64_t)as << 32 | an;
+                }
+            } else {
+                uint64_t acc = 0;
+                for (int j = 0; j < 9; j++) acc += c[j * BW], c[j * BW] = acc;
+            }
+        }
+        __syncthreads();
+    }
     const int nout = kind < NSUP ? 8 * 72 : 128;
     for (int o = tid; o < nout; o += 256) {
         uint32_t n = 0, s1 = 0;
@@ -235,18 +253,21 @@ __global__ __launch_bounds__(256) void ccso_merge_kernel(Planes a) {
             const int qc = o / 72, qi = qc >> 1, clf = qc & 1;
             const int L  = qi == 0 ? 2 : qi == 1 ? 1 : qi == 2 ? 3 : 4; // quant_sz {16, 8, 32, 64}
             f = o % 72, combo = (kind * 4 + qi) * 2 + clf;
-            const int  band = f / 9, c0 = (f / 3) % 3, c1 = f % 3;
-            const Bin *b    = s_bin + band * 81;
-            for (int b0 = 0; b0 < 9; b0++) {
-                if (bucket_class(b0, L, clf) != c0) continue;
-                for (int b1 = 0; b1 < 9; b1++) {
-                    if (bucket_class(b1, L, clf) != c1) continue;
-                    const Bin &x = b[b0 * 9 + b1];
-                    if (!x.n) continue;
-                    n += x.n, s1 += x.s1, s2 += x.s2;
-                    for (int k = 0; k < 8; k++) corr[k] += x.corr[k];
+            const int band = f / 9, c0 = (f / 3) % 3, c1 = f % 3;
+            // the bucket range of a class (bucket_class): 0 [0, 4 - L]; 1 [5 - L, 3 + L] (clf 0) or [5 - L, 8];
+            // 2 [4 + L, 8] (clf 0 only)
+            auto lo = [&](int c) { return c == 0 ? 0 : c == 1 ? 5 - L : 4 + L; };
+            auto hi = [&](int c) { return c == 0 ? 4 - L : c == 1 ? (clf ? 8 : 3 + L) : (clf ? -1 : 8); };
+            const int l1 = lo(c1), h1 = hi(c1);
+            if (h1 >= l1)
+                for (int b0 = lo(c0); b0 <= hi(c0); b0++) {
+                    const uint64_t *r = (const uint64_t *)(s_bin + band * 81 + b0 * 9);
+                    const uint64_t *u = r + h1 * BW, *v = l1 ? r + (l1 - 1) * BW : nullptr;
+                    n += (uint32_t)u[0] - (v ? (uint32_t)v[0] : 0u);
+                    s1 += (uint32_t)(u[0] >> 32) - (v ? (uint32_t)(v[0] >> 32) : 0u);
+                    s2 += u[1] - (v ? v[1] : 0ull);
+                    for (int k = 0; k < 8; k++) corr[k] += u[2 + k] - (v ? v[2 + k] : 0ull);
                 }
-            }
         } else {
             f = o, combo = NCOMBO;
             const Bin &x = s_bin[f];
