@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include "svtgpu_internal.h"
@@ -40,7 +41,7 @@ constexpr int NFINE   = 128;          // fine classes per merged moment slot (72
 constexpr int NCOMBO  = NSUP * 4 * 2; // support x quantization step x edge classifier
 constexpr int NCFG    = NCOMBO * 4 + 8;
 constexpr int MAXNB   = 1024;         // filter blocks per plane (an 8192 x 8192 picture has 32 x 32)
-constexpr int STRIP   = 32;           // rows of a block per bins workgroup
+constexpr int STRIP   = 64;           // most rows of a block per bins workgroup (Planes::strip: 32 or 64)
 constexpr int BTHREADS = 256;
 
 __constant__ int kOff[8] = {-10, -7, -3, -1, 0, 1, 3, 7}; // ccso_offset (EbPickccso.c:43)
@@ -106,12 +107,13 @@ struct Planes { // the planes of one search launch: plane = plane0 + blockIdx.z 
     SvtGpuCcsoParams *params[3];
     uint8_t          *flags[3];
     int32_t           bd, rdmult, plane0;
+    int32_t           strip; // rows per bins workgroup: 64 for pictures of many blocks (fewer, longer workgroups), else 32
 };
 
 // LDS cells: the count and the squared-error sum share one 64-bit word (count << 50 | sum of squares: a workgroup sees
-// at most 32 x 256 samples and 12-bit errors, so neither field overflows) and the error sum is kept biased by +4096 per
+// at most 64 x 256 samples and 12-bit errors, so neither field overflows) and the error sum is kept biased by +4096 per
 // sample (non-negative, < 2^26); every sample costs at most two LDS atomics, fewer where lanes share a bin
-constexpr int      NQ_SHIFT = 50;
+constexpr int      NQ_SHIFT = 49;
 constexpr uint32_t S1_BIAS  = 4096;
 constexpr int      RUN      = 4; // wave-wide bin groups summed per step before the per-lane atomics
 constexpr int      U        = 8; // steps whose samples are loaded together
@@ -122,19 +124,19 @@ __global__ __launch_bounds__(BTHREADS) void ccso_bins_kernel(Planes a) {
     __shared__ int32_t            s_corr[8][NBIN]; // |clamped - unclamped| <= 10 * 2 * 4105 per sample: int32 per tile
     const int  tid = threadIdx.x, kind = blockIdx.y, pl = a.plane0 + blockIdx.z;
     const Geo &g = a.g[pl];
-    const int  strips = g.bs / STRIP;
+    const int  strips = g.bs / a.strip;
     if ((int)blockIdx.x >= g.nbp * strips) return;
     const int  pb = blockIdx.x / strips, strip = blockIdx.x % strips;
     const uint16_t *org = a.org[pl], *rec = a.rec[pl];
     const int  bx = pb % g.nbx, by = pb / g.nbx;
-    const int  x0 = bx * g.bs, y0 = by * g.bs + strip * STRIP;
+    const int  x0 = bx * g.bs, y0 = by * g.bs + strip * a.strip;
     const int  nbins = kind < NSUP ? NBIN : 128;
     for (int i = tid; i < nbins; i += BTHREADS) {
         s_nq[i] = 0, s_s1[i] = 0;
         for (int o = 0; o < 8; o++) s_corr[o][i] = 0;
     }
     __syncthreads();
-    const int rows = min(STRIP, min(g.bs - strip * STRIP, g.ph - y0)), cols = min(g.bs, g.pw - x0);
+    const int rows = min(a.strip, min(g.bs - strip * a.strip, g.ph - y0)), cols = min(g.bs, g.pw - x0);
     if (rows > 0 && cols > 0) {
         const int es = g.w + 2 * PAD, maxv = (1 << a.bd) - 1;
         int       loc[2];
@@ -607,6 +609,13 @@ int launch_search(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const
                   int p0, int n, int32_t bd, int32_t rdmult, hipStream_t st) {
     Planes a{};
     a.ext = ext, a.bd = bd, a.rdmult = rdmult, a.plane0 = p0;
+    // measured (scripts/r6/ccso_perf.py): 64-row workgroups 0.94 -> 0.75 ms at 4K (135 blocks a plane), slower at 1080p
+    // (40 blocks: too few workgroups)
+    static const int forced = [] { // SVTGPU_CCSO_STRIP=32|64 (tests: the 64-row path on small pictures)
+        const char *e = std::getenv("SVTGPU_CCSO_STRIP");
+        return e && (std::atoi(e) == 32 || std::atoi(e) == 64) ? std::atoi(e) : 0;
+    }();
+    a.strip = forced ? forced : s->nbp_max >= 96 ? 64 : 32;
     int gx = 0, gm = 0;
     for (int p = 0; p < 3; p++) {
         a.g[p]      = geo_of(s->width, s->height, p);
@@ -619,7 +628,7 @@ int launch_search(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const
         a.ctrl[p]   = s->ctrl + (size_t)p * NCFG * s->nb_max;
         a.params[p] = s->params + p;
         a.flags[p]  = s->flags + (size_t)p * s->nb_max;
-        if (p >= p0 && p < p0 + n) gx = std::max(gx, a.g[p].nbp * (a.g[p].bs / STRIP)), gm = std::max(gm, a.g[p].nbp);
+        if (p >= p0 && p < p0 + n) gx = std::max(gx, a.g[p].nbp * (a.g[p].bs / a.strip)), gm = std::max(gm, a.g[p].nbp);
     }
     HIP_TRY(hipMemsetAsync(a.bins[p0], 0, (size_t)n * NKIND * s->nbp_max * NBIN * sizeof(Bin), st));
     ccso_bins_kernel<<<dim3(gx, NKIND, n), BTHREADS, 0, st>>>(a);

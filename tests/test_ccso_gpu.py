@@ -159,3 +159,43 @@ def test_search_and_apply_vs_oracle(ctx, w, h, bd, rdmult, q):
         want = oracle.ccso_apply_plane(ext_h, bd, p, plane, oprms[p], oflags[p])
         np.testing.assert_array_equal(host(d, plane.dtype.type), want, err_msg="plane %d" % p)
     st.close()
+
+
+CHILD_STRIP = r"""
+import sys
+sys.path[:0] = %r
+import numpy as np, torch
+torch.cuda.init()
+import ccso_cases as xc, oracle, svtgpu
+ctx = svtgpu.Context(0)
+w, h, bd, rdmult, q = 1280, 720, 10, 900, 120
+org, rec, pre = xc.content(w, h, bd, seed=77)
+st = svtgpu.CcsoState(ctx, w, h)
+dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda()
+d_pre, d_org, d_rec = dev(pre), [dev(a) for a in org], [dev(a) for a in rec]
+ext = torch.zeros(((h + 10) * (w + 10),), dtype=torch.int16, device="cuda")
+torch.cuda.synchronize()
+st.extend(d_pre.data_ptr(), 16, w, ext.data_ptr())
+rc, prms, flags, ff = st.search_frame(ext.data_ptr(), [t.data_ptr() for t in d_org], [t.data_ptr() for t in d_rec], bd,
+                                      rdmult, q)
+orc, oprms, oflags, off = oracle.ccso_search_frame(oracle.ccso_extend(pre), org, rec, bd, rdmult, q)
+assert (rc, ff) == (orc, off)
+for p in range(3):
+    assert prms[p].fields() == oprms[p].fields(), p
+    assert np.array_equal(prms[p].lut(), oprms[p].lut()) and np.array_equal(flags[p], oflags[p]), p
+print("strip ok", [p.fields() for p in prms])
+"""
+
+
+def test_search_64_row_workgroups_vs_oracle():
+    """The binning pass with 64-row workgroups (the default for pictures of 96 blocks or more a plane, e.g. 4K) forced
+    on a 720p 10-bit picture (SVTGPU_CCSO_STRIP=64, read once per process: a child process) equals the oracle."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    paths = [here, os.path.join(root, "oracle"), os.path.join(root, "svt-av1_pro-anchor-v2.1.0-_amd")]
+    r = subprocess.run([sys.executable, "-c", CHILD_STRIP % (paths,)], capture_output=True, text=True, timeout=180,
+                       env=dict(os.environ, SVTGPU_CCSO_STRIP="64"))
+    assert r.returncode == 0 and "strip ok" in r.stdout, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
