@@ -609,13 +609,14 @@ int launch_search(SvtGpuCcsoState *s, const uint16_t *ext, const uint16_t *const
                   int p0, int n, int32_t bd, int32_t rdmult, hipStream_t st) {
     Planes a{};
     a.ext = ext, a.bd = bd, a.rdmult = rdmult, a.plane0 = p0;
-    // measured (scripts/r6/ccso_perf.py): 64-row workgroups 0.94 -> 0.75 ms at 4K (135 blocks a plane), slower at 1080p
-    // (40 blocks: too few workgroups)
+    // measured (scripts/r6/ccso_perf.py, profiles/r06/ccso/strip_threshold.txt): 64-row workgroups halve the flushes of
+    // the cell tile, which pays where the tiles are dense (10-bit: 0.94 -> 0.75 ms at 4K, 0.44 -> 0.37 at 1440p with 60
+    // blocks a plane) and is about even at 8 bits (4K 0.86 either way); at 1080p (40 blocks) too few workgroups
     static const int forced = [] { // SVTGPU_CCSO_STRIP=32|64 (tests: the 64-row path on small pictures)
         const char *e = std::getenv("SVTGPU_CCSO_STRIP");
         return e && (std::atoi(e) == 32 || std::atoi(e) == 64) ? std::atoi(e) : 0;
     }();
-    a.strip = forced ? forced : s->nbp_max >= 96 ? 64 : 32;
+    a.strip = forced ? forced : s->nbp_max >= (bd > 8 ? 56 : 96) ? 64 : 32;
     int gx = 0, gm = 0;
     for (int p = 0; p < 3; p++) {
         a.g[p]      = geo_of(s->width, s->height, p);
